@@ -1,0 +1,47 @@
+# Native build: host C++ (g++ -O3 -fopenmp) + HIP kernels (hipcc --offload-arch=gfx950)
+# linked into one shared library loaded by the Python package via ctypes, plus the CLI.
+#   make -j8            build lib + cli
+#   make clean
+ROCM ?= /opt/rocm
+HIPCC ?= $(ROCM)/bin/hipcc
+CXX ?= g++
+ARCH ?= gfx950
+BUILD := build
+LIBDIR := lightgbmv1_amd/lib
+LIB := $(LIBDIR)/lib_lightgbmv1_amd.so
+CLI := $(LIBDIR)/lightgbm
+
+CXXFLAGS ?= -O3 -std=c++17 -fPIC -fopenmp -Wall -Wno-unused-function -Wno-sign-compare -Iinclude -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -munsafe-fp-atomics -Wno-unused-result
+LDFLAGS := -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
+
+HOST_SRCS := $(filter-out src/cli/main.cpp,$(shell find src -name '*.cpp'))
+DEV_SRCS := $(shell find src -name '*.hip')
+HOST_OBJS := $(patsubst src/%.cpp,$(BUILD)/%.o,$(HOST_SRCS))
+DEV_OBJS := $(patsubst src/%.hip,$(BUILD)/%.hip.o,$(DEV_SRCS))
+HEADERS := $(shell find include src -name '*.h' -o -name '*.hpp' -o -name '*.inc' -o -name '*.cuh')
+
+all: $(LIB) $(CLI)
+
+include/lgbm_amd/config_fields.inc src/config/config_auto.cpp: tools/param_spec.py tools/gen_params.py
+	python3 tools/gen_params.py
+
+$(BUILD)/%.o: src/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(BUILD)/%.hip.o: src/%.hip $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HOST_OBJS) $(DEV_OBJS)
+	@mkdir -p $(LIBDIR)
+	$(CXX) -o $@ $^ $(LDFLAGS)
+
+$(CLI): src/cli/main.cpp $(LIB)
+	$(CXX) $(CXXFLAGS) -o $@ src/cli/main.cpp -L$(LIBDIR) -l_lightgbmv1_amd -Wl,-rpath,'$$ORIGIN' -fopenmp
+
+clean:
+	rm -rf $(BUILD) $(LIB) $(CLI)
+
+.PHONY: all clean

@@ -1,0 +1,150 @@
+// Host-side collective layer used by distributed training (control plane + CPU
+// learners) and the device-collective registry used by the HIP learners.
+//
+// Reference: include/LightGBM/network.h:89-313 (static Network facade, Allreduce /
+// Allgather / ReduceScatter, GlobalSyncUpBy{Min,Max,Sum,Mean}, external functions via
+// LGBM_NetworkInitWithFunctions).  Transport here is pluggable:
+//   * external functions (C API; the Python package plugs torch.distributed in),
+//   * built-in TCP full mesh for `machines=` / `machine_list_filename` configs,
+//   * in-process "fake" ranks (threads) for tests.
+// Device collectives (histogram all-reduce over xGMI) go through `DeviceComm`,
+// implemented with RCCL in src/network/rccl_comm.cpp.
+#pragma once
+
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "lgbm_amd/config.h"
+#include "lgbm_amd/meta.h"
+
+namespace lgbm_amd {
+
+// elementwise reducer: dst[i] = reduce(dst[i], src[i]) over `len` bytes of `type_size` items
+using ReduceFunction = std::function<void(const char* src, char* dst, int type_size, comm_size_t len)>;
+
+// C-ABI signatures of the reference's external collectives (c_api.h:1266-1288)
+typedef void (*ReduceFunctionPtr)(const char* input, char* output, int type_size, comm_size_t array_size);
+typedef void (*ReduceScatterFunctionPtr)(char* input, comm_size_t input_size, int type_size,
+                                         const comm_size_t* block_start, const comm_size_t* block_len,
+                                         int num_block, char* output, comm_size_t output_size,
+                                         const ReduceFunctionPtr& reducer);
+typedef void (*AllgatherFunctionPtr)(char* input, comm_size_t input_size, const comm_size_t* block_start,
+                                     const comm_size_t* block_len, int num_block, char* output,
+                                     comm_size_t output_size);
+
+class HostTransport {
+ public:
+  virtual ~HostTransport() = default;
+  virtual int rank() const = 0;
+  virtual int num_machines() const = 0;
+  // variable-size allgather: every rank contributes block_len[rank] bytes
+  virtual void Allgather(const char* input, comm_size_t input_size, const comm_size_t* block_start,
+                         const comm_size_t* block_len, char* output, comm_size_t output_size) = 0;
+  // optional native reduce-scatter; default implemented with Allgather + local reduce
+  virtual bool ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
+                             const comm_size_t* block_len, char* output, comm_size_t output_size,
+                             const ReduceFunction& reducer) {
+    (void)input; (void)input_size; (void)type_size; (void)block_start; (void)block_len; (void)output;
+    (void)output_size; (void)reducer;
+    return false;
+  }
+};
+
+// device collectives (all pointers are device pointers, stream-ordered)
+class DeviceComm {
+ public:
+  virtual ~DeviceComm() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual void AllreduceSumF64(double* buf, size_t count, void* stream) = 0;
+  virtual void AllreduceSumF32(float* buf, size_t count, void* stream) = 0;
+  virtual void Allgather(const void* send, void* recv, size_t bytes_per_rank, void* stream) = 0;
+  virtual void ReduceScatterSumF64(const double* send, double* recv, size_t recv_count, void* stream) = 0;
+  virtual void Broadcast(void* buf, size_t bytes, int root, void* stream) = 0;
+};
+
+class Network {
+ public:
+  // TCP mesh from config (num_machines > 1 with machines / machine_list_filename)
+  static void Init(const Config& cfg);
+  static void InitWithTransport(std::shared_ptr<HostTransport> t);
+  static void InitWithFunctions(int num_machines, int rank, ReduceScatterFunctionPtr rs, AllgatherFunctionPtr ag);
+  static void Dispose();
+  static int rank();
+  static int num_machines();
+  static bool IsDistributed() { return num_machines() > 1; }
+
+  static void SetDeviceComm(std::shared_ptr<DeviceComm> c);
+  static DeviceComm* device_comm();
+
+  static void Allreduce(char* input, comm_size_t input_size, int type_size, char* output,
+                        const ReduceFunction& reducer);
+  static void Allgather(char* input, comm_size_t send_size, char* output);
+  static void Allgather(char* input, const comm_size_t* block_start, const comm_size_t* block_len, char* output,
+                        comm_size_t all_size);
+  static void ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
+                            const comm_size_t* block_len, char* output, comm_size_t output_size,
+                            const ReduceFunction& reducer);
+
+  template <typename T>
+  static T GlobalSyncUpByMin(T v) {
+    return GlobalReduceScalar<T>(v, [](T a, T b) { return a < b ? a : b; });
+  }
+  template <typename T>
+  static T GlobalSyncUpByMax(T v) {
+    return GlobalReduceScalar<T>(v, [](T a, T b) { return a > b ? a : b; });
+  }
+  template <typename T>
+  static T GlobalSyncUpBySum(T v) {
+    return GlobalReduceScalar<T>(v, [](T a, T b) { return a + b; });
+  }
+  template <typename T>
+  static T GlobalSyncUpByMean(T v) {
+    return static_cast<T>(GlobalSyncUpBySum<double>(static_cast<double>(v)) / num_machines());
+  }
+  template <typename T>
+  static std::vector<T> GlobalSum(const std::vector<T>& v) {
+    std::vector<T> out(v.size());
+    if (num_machines() <= 1 || v.empty()) return v;
+    Allreduce(reinterpret_cast<char*>(const_cast<T*>(v.data())), static_cast<comm_size_t>(sizeof(T) * v.size()),
+              sizeof(T), reinterpret_cast<char*>(out.data()), [](const char* src, char* dst, int ts, comm_size_t len) {
+                for (comm_size_t i = 0; i < len; i += ts) {
+                  T a, b;
+                  std::memcpy(&a, src + i, sizeof(T));
+                  std::memcpy(&b, dst + i, sizeof(T));
+                  b += a;
+                  std::memcpy(dst + i, &b, sizeof(T));
+                }
+              });
+    return out;
+  }
+  // every rank's value, indexed by rank
+  template <typename T>
+  static std::vector<T> GlobalArray(T v) {
+    std::vector<T> out(num_machines());
+    if (num_machines() <= 1) {
+      out[0] = v;
+      return out;
+    }
+    Allgather(reinterpret_cast<char*>(&v), sizeof(T), reinterpret_cast<char*>(out.data()));
+    return out;
+  }
+
+ private:
+  template <typename T, typename F>
+  static T GlobalReduceScalar(T v, F f) {
+    if (num_machines() <= 1) return v;
+    auto all = GlobalArray<T>(v);
+    T r = all[0];
+    for (size_t i = 1; i < all.size(); ++i) r = f(r, all[i]);
+    return r;
+  }
+};
+
+// in-process multi-rank transport (ranks are threads sharing a rendezvous object)
+std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks);
+
+}  // namespace lgbm_amd

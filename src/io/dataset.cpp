@@ -1,0 +1,735 @@
+// Dataset construction (bin finding + Exclusive Feature Bundling), row pushing, CPU
+// histogram construction and binary persistence.
+// EFB follows reference src/io/dataset.cpp:97-313 (greedy conflict-bounded grouping
+// tried in two feature orders, smaller result kept, groups shuffled with an LCG seeded
+// by num_data) so that inner feature order -- which feature_fraction sampling depends
+// on -- matches the reference.  Multi-value (row-wise sparse) groups of the reference
+// are stored here as singleton dense groups: a storage choice that does not change
+// the model.
+#include "lgbm_amd/dataset.h"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+
+#include "lgbm_amd/common.h"
+#include "lgbm_amd/log.h"
+#include "lgbm_amd/network.h"
+#include "lgbm_amd/random.h"
+
+namespace lgbm_amd {
+
+namespace {
+
+int ConflictCount(const std::vector<bool>& mark, const int* idx, int n, data_size_t max_cnt) {
+  int c = 0;
+  for (int i = 0; i < n; ++i) {
+    if (mark[idx[i]]) ++c;
+    if (c > max_cnt) return -1;
+  }
+  return c;
+}
+
+void Mark(std::vector<bool>* mark, const int* idx, int n) {
+  for (int i = 0; i < n; ++i) (*mark)[idx[i]] = true;
+}
+
+// rows of the sample whose bin differs from the most frequent bin (only needed when
+// the zero bin is not the most frequent one)
+std::vector<int> NonMostFreqRows(const BinMapper* m, int total, int n, const int* idx, const double* vals) {
+  std::vector<int> out;
+  if (m->GetDefaultBin() == m->GetMostFreqBin()) return out;
+  int i = 0, j = 0;
+  while (i < total) {
+    if (j < n && idx[j] < i) {
+      ++j;
+    } else if (j < n && idx[j] == i) {
+      if (m->ValueToBin(vals[j]) != m->GetMostFreqBin()) out.push_back(i);
+      ++i;
+    } else {
+      out.push_back(i++);
+    }
+  }
+  return out;
+}
+
+std::vector<std::vector<int>> GreedyGroups(const std::vector<std::unique_ptr<BinMapper>>& mappers,
+                                           const std::vector<int>& order, int** sidx, const int* nper,
+                                           int num_sample_col, data_size_t total_sample, data_size_t num_data,
+                                           bool limit_256, bool is_sparse, std::vector<int8_t>* multi_val) {
+  const int kMaxSearch = 100;
+  const int kMaxBinPerGroup = 256;
+  const data_size_t max_conflict = static_cast<data_size_t>(total_sample / 10000);
+  multi_val->clear();
+  Random rnd(num_data);
+  std::vector<std::vector<int>> groups;
+  std::vector<std::vector<bool>> marks;
+  std::vector<data_size_t> used_rows, total_rows;
+  std::vector<int> group_bins;
+  auto extra_bins = [&](int f) { return mappers[f]->num_bin() + (mappers[f]->GetDefaultBin() == 0 ? -1 : 0); };
+
+  for (int f : order) {
+    const bool filtered = f >= num_sample_col;
+    const data_size_t nz = filtered ? 0 : nper[f];
+    std::vector<int> avail;
+    for (int g = 0; g < static_cast<int>(groups.size()); ++g) {
+      int nb = group_bins[g] + extra_bins(f);
+      if (total_rows[g] + nz <= total_sample + max_conflict) {
+        if (!limit_256 || nb <= kMaxBinPerGroup) avail.push_back(g);
+      }
+    }
+    std::vector<int> search;
+    if (!avail.empty()) {
+      int last = static_cast<int>(avail.size()) - 1;
+      auto picks = rnd.Sample(last, std::min(last, kMaxSearch - 1));
+      search.push_back(avail.back());
+      for (int p : picks) search.push_back(avail[p]);
+    }
+    int best = -1, best_conf = -1;
+    for (int g : search) {
+      const data_size_t rest = max_conflict - total_rows[g] + used_rows[g];
+      const data_size_t c = filtered ? 0 : ConflictCount(marks[g], sidx[f], nper[f], rest);
+      if (c >= 0 && c <= rest && c <= nz / 2) {
+        best = g;
+        best_conf = c;
+        break;
+      }
+    }
+    if (best >= 0) {
+      groups[best].push_back(f);
+      total_rows[best] += nz;
+      used_rows[best] += nz - best_conf;
+      if (!filtered) Mark(&marks[best], sidx[f], nper[f]);
+      group_bins[best] += extra_bins(f);
+    } else {
+      groups.emplace_back(1, f);
+      marks.emplace_back(total_sample, false);
+      if (!filtered) Mark(&marks.back(), sidx[f], nper[f]);
+      total_rows.push_back(nz);
+      used_rows.push_back(nz);
+      group_bins.push_back(1 + extra_bins(f));
+    }
+  }
+  if (!is_sparse) {
+    multi_val->assign(groups.size(), 0);
+    return groups;
+  }
+  // second round: sparse leftovers go into one (multi-value) group
+  std::vector<int> leftovers;
+  std::vector<std::vector<int>> groups2;
+  std::vector<std::vector<bool>> marks2;
+  const double kDense = 0.4;
+  for (int g = 0; g < static_cast<int>(groups.size()); ++g) {
+    if (static_cast<double>(used_rows[g]) / total_sample >= kDense) {
+      groups2.push_back(std::move(groups[g]));
+      marks2.push_back(std::move(marks[g]));
+    } else {
+      for (int f : groups[g]) leftovers.push_back(f);
+    }
+  }
+  groups = std::move(groups2);
+  multi_val->assign(groups.size(), 0);
+  if (!leftovers.empty()) {
+    groups.emplace_back();
+    std::vector<bool> m(total_sample, false);
+    bool is_multi = limit_256;
+    int conflicts = 0;
+    for (int f : leftovers) {
+      groups.back().push_back(f);
+      if (!is_multi) {
+        const int rest = max_conflict - conflicts;
+        const int c = ConflictCount(m, sidx[f], nper[f], rest);
+        conflicts += c;
+        if (c < 0 || conflicts > max_conflict) {
+          is_multi = true;
+          continue;
+        }
+        Mark(&m, sidx[f], nper[f]);
+      }
+    }
+    multi_val->push_back(is_multi ? 1 : 0);
+  }
+  return groups;
+}
+
+std::vector<std::vector<int>> BundleFeatures(const std::vector<std::unique_ptr<BinMapper>>& mappers,
+                                             std::vector<std::vector<int>>* sample_indices,
+                                             std::vector<std::vector<double>>* sample_values, int num_sample_col,
+                                             data_size_t total_sample, const std::vector<int>& used,
+                                             data_size_t num_data, bool limit_256, bool is_sparse,
+                                             std::vector<int8_t>* multi_val) {
+  std::vector<size_t> nz;
+  for (int f : used) nz.push_back(f < num_sample_col ? (*sample_indices)[f].size() : 0);
+  std::vector<int> by_cnt(used.size());
+  for (size_t i = 0; i < used.size(); ++i) by_cnt[i] = static_cast<int>(i);
+  std::stable_sort(by_cnt.begin(), by_cnt.end(), [&](int a, int b) { return nz[a] > nz[b]; });
+  std::vector<int> order2;
+  for (int i : by_cnt) order2.push_back(used[i]);
+
+  std::vector<std::vector<int>> fixed(num_sample_col);
+  std::vector<int*> sidx(num_sample_col, nullptr);
+  std::vector<int> nper(num_sample_col, 0);
+  for (int f = 0; f < num_sample_col; ++f) {
+    sidx[f] = (*sample_indices)[f].data();
+    nper[f] = static_cast<int>((*sample_indices)[f].size());
+  }
+  for (int f : used) {
+    if (f >= num_sample_col) continue;
+    auto r = NonMostFreqRows(mappers[f].get(), static_cast<int>(total_sample), nper[f], sidx[f],
+                             (*sample_values)[f].data());
+    if (!r.empty()) {
+      fixed[f] = std::move(r);
+      sidx[f] = fixed[f].data();
+      nper[f] = static_cast<int>(fixed[f].size());
+    }
+  }
+  std::vector<int8_t> mv1, mv2;
+  auto g1 = GreedyGroups(mappers, used, sidx.data(), nper.data(), num_sample_col, total_sample, num_data,
+                         limit_256, is_sparse, &mv1);
+  auto g2 = GreedyGroups(mappers, order2, sidx.data(), nper.data(), num_sample_col, total_sample, num_data,
+                         limit_256, is_sparse, &mv2);
+  if (g1.size() > g2.size()) {
+    g1 = g2;
+    mv1 = mv2;
+  }
+  const int ng = static_cast<int>(g1.size());
+  Random shuf(num_data);
+  for (int i = 0; i < ng - 1; ++i) {
+    int j = shuf.NextShort(i + 1, ng);
+    std::swap(g1[i], g1[j]);
+    std::swap(mv1[i], mv1[j]);
+  }
+  *multi_val = mv1;
+  return g1;
+}
+
+}  // namespace
+
+void Dataset::ConstructFromSample(std::vector<std::vector<double>>* sample_values,
+                                  std::vector<std::vector<int>>* sample_indices, int num_col,
+                                  size_t total_sample_cnt, data_size_t num_data, const Config& cfg,
+                                  const std::unordered_set<int>& categorical, const std::unordered_set<int>& ignored,
+                                  const std::vector<std::vector<double>>& forced_bins) {
+  num_data_ = num_data;
+  std::vector<std::unique_ptr<BinMapper>> mappers(num_col);
+  if (!cfg.max_bin_by_feature.empty()) {
+    LGBM_CHECK_EQ(static_cast<int>(cfg.max_bin_by_feature.size()), num_col);
+  }
+  const data_size_t filter_cnt =
+      static_cast<data_size_t>(static_cast<double>(cfg.min_data_in_leaf * total_sample_cnt) / num_data);
+  std::string err;
+  // distributed: each rank bins a contiguous block of columns from its local sample and
+  // the serialized mappers are allgathered, so every rank ends with identical bins
+  // (reference dataset_loader.cpp:680-760)
+  const int nm = Network::num_machines();
+  const int rank = Network::rank();
+  int col_begin = 0, col_end = num_col;
+  if (nm > 1) {
+    const int step = (num_col + nm - 1) / nm;
+    col_begin = std::min(num_col, step * rank);
+    col_end = std::min(num_col, col_begin + step);
+  }
+#pragma omp parallel for schedule(guided)
+  for (int i = col_begin; i < col_end; ++i) {
+    if (ignored.count(i)) continue;
+    BinType t = BinType::Numerical;
+    if (categorical.count(i)) {
+      t = BinType::Categorical;
+      if (!cfg.monotone_constraints.empty() && cfg.monotone_constraints[i] != 0) {
+#pragma omp critical
+        err = "The output cannot be monotone with respect to categorical features";
+        continue;
+      }
+    }
+    mappers[i].reset(new BinMapper());
+    int mb = cfg.max_bin_by_feature.empty() ? cfg.max_bin : cfg.max_bin_by_feature[i];
+    std::vector<double> vals = (*sample_values)[i];
+    static const std::vector<double> kNoForced;
+    const std::vector<double>& fb = i < static_cast<int>(forced_bins.size()) ? forced_bins[i] : kNoForced;
+    mappers[i]->FindBin(vals.data(), static_cast<int>(vals.size()), total_sample_cnt, mb, cfg.min_data_in_bin,
+                        filter_cnt, cfg.feature_pre_filter, t, cfg.use_missing, cfg.zero_as_missing, fb);
+  }
+  if (!err.empty()) Log::Fatal("%s", err.c_str());
+  if (nm > 1) {
+    // wire: per column [int8 present][mapper bytes]
+    std::string mine;
+    for (int i = col_begin; i < col_end; ++i) {
+      const char present = mappers[i] != nullptr ? 1 : 0;
+      mine.push_back(present);
+      if (present) {
+        std::string b(mappers[i]->SizesInByte(), '\0');
+        mappers[i]->CopyTo(&b[0]);
+        const uint64_t len = b.size();
+        mine.append(reinterpret_cast<const char*>(&len), sizeof(len));
+        mine += b;
+      }
+    }
+    auto sizes = Network::GlobalArray<comm_size_t>(static_cast<comm_size_t>(mine.size()));
+    std::vector<comm_size_t> starts(nm, 0);
+    for (int r = 1; r < nm; ++r) starts[r] = starts[r - 1] + sizes[r - 1];
+    std::string all(static_cast<size_t>(starts[nm - 1] + sizes[nm - 1]), '\0');
+    Network::Allgather(&mine[0], starts.data(), sizes.data(), &all[0], static_cast<comm_size_t>(all.size()));
+    const int step = (num_col + nm - 1) / nm;
+    for (int r = 0; r < nm; ++r) {
+      const char* p = all.data() + starts[r];
+      const int b = std::min(num_col, step * r), e = std::min(num_col, b + step);
+      for (int i = b; i < e; ++i) {
+        const char present = *p++;
+        if (!present) {
+          mappers[i].reset();
+          continue;
+        }
+        uint64_t len;
+        std::memcpy(&len, p, sizeof(len));
+        p += sizeof(len);
+        mappers[i].reset(new BinMapper());
+        mappers[i]->CopyFrom(p);
+        p += len;
+      }
+    }
+  }
+  forced_bin_bounds_ = forced_bins;
+  ConstructFromBinMappers(&mappers, num_data, cfg, sample_indices, sample_values, total_sample_cnt);
+}
+
+void Dataset::ConstructFromBinMappers(std::vector<std::unique_ptr<BinMapper>>* mappers, data_size_t num_data,
+                                      const Config& cfg, std::vector<std::vector<int>>* sample_indices,
+                                      std::vector<std::vector<double>>* sample_values, size_t total_sample_cnt) {
+  num_data_ = num_data;
+  max_bin_ = cfg.max_bin;
+  num_total_features_ = static_cast<int>(mappers->size());
+  std::vector<int> used;
+  for (int i = 0; i < num_total_features_; ++i) {
+    if ((*mappers)[i] != nullptr && !(*mappers)[i]->is_trivial()) used.push_back(i);
+  }
+  if (used.empty()) Log::Warning("There are no meaningful features, as all feature values are constant.");
+  std::vector<std::vector<int>> fig;
+  std::vector<int8_t> multi_val(used.size(), 0);
+  for (int f : used) fig.emplace_back(1, f);
+  const bool can_bundle = sample_indices != nullptr && sample_values != nullptr &&
+                          static_cast<int>(sample_indices->size()) > 0;
+  // bundling depends on the local sample; with several ranks it could differ per rank and
+  // break the shared feature layout, so distributed datasets keep one group per feature
+  if (cfg.enable_bundle && !used.empty() && can_bundle && Network::num_machines() <= 1) {
+    fig = BundleFeatures(*mappers, sample_indices, sample_values, static_cast<int>(sample_indices->size()),
+                         static_cast<data_size_t>(total_sample_cnt), used, num_data, cfg.device_type == "gpu",
+                         cfg.is_enable_sparse, &multi_val);
+    // multi-value groups are stored as singleton dense groups (same inner feature order)
+    std::vector<std::vector<int>> expanded;
+    for (size_t g = 0; g < fig.size(); ++g) {
+      if (multi_val[g]) {
+        for (int f : fig[g]) expanded.emplace_back(1, f);
+      } else {
+        expanded.push_back(fig[g]);
+      }
+    }
+    fig = std::move(expanded);
+  }
+  // inner feature numbering follows group order
+  used_feature_map_.assign(num_total_features_, -1);
+  real_feature_idx_.clear();
+  feature2group_.clear();
+  feature2subfeature_.clear();
+  bin_mappers_.clear();
+  for (size_t g = 0; g < fig.size(); ++g) {
+    for (size_t j = 0; j < fig[g].size(); ++j) {
+      int real = fig[g][j];
+      used_feature_map_[real] = static_cast<int>(real_feature_idx_.size());
+      real_feature_idx_.push_back(real);
+      feature2group_.push_back(static_cast<int>(g));
+      feature2subfeature_.push_back(static_cast<int>(j));
+      bin_mappers_.emplace_back((*mappers)[real].release());
+    }
+  }
+  num_features_ = static_cast<int>(real_feature_idx_.size());
+  std::vector<std::vector<int>> inner_groups;
+  int k = 0;
+  for (auto& g : fig) {
+    inner_groups.emplace_back();
+    for (size_t j = 0; j < g.size(); ++j) inner_groups.back().push_back(k++);
+  }
+  BuildGroups(inner_groups);
+  if (feature_names_.empty()) {
+    for (int i = 0; i < num_total_features_; ++i) feature_names_.push_back("Column_" + std::to_string(i));
+  }
+}
+
+void Dataset::BuildGroups(const std::vector<std::vector<int>>& features_in_group) {
+  groups_.clear();
+  need_push_zeros_.clear();
+  for (auto& fs : features_in_group) {
+    FeatureGroup g;
+    g.inner_features = fs;
+    g.bin_offsets.push_back(1);
+    int total = 1;
+    for (int f : fs) {
+      int nb = bin_mappers_[f]->num_bin();
+      if (bin_mappers_[f]->GetMostFreqBin() == 0) nb -= 1;
+      total += nb;
+      g.bin_offsets.push_back(static_cast<uint32_t>(total));
+      if (bin_mappers_[f]->GetDefaultBin() != bin_mappers_[f]->GetMostFreqBin()) need_push_zeros_.push_back(f);
+    }
+    g.num_total_bin = total;
+    g.bin_bytes = total <= 256 ? 1 : (total <= 65536 ? 2 : 4);
+    g.data.assign(static_cast<size_t>(num_data_) * g.bin_bytes, 0);
+    groups_.push_back(std::move(g));
+  }
+  group_bin_boundaries_.assign(1, 0);
+  for (auto& g : groups_) group_bin_boundaries_.push_back(group_bin_boundaries_.back() + g.num_total_bin);
+}
+
+void Dataset::CreateValid(const Dataset& ref, data_size_t num_data) {
+  num_data_ = num_data;
+  num_total_features_ = ref.num_total_features_;
+  num_features_ = ref.num_features_;
+  label_idx_ = ref.label_idx_;
+  used_feature_map_ = ref.used_feature_map_;
+  real_feature_idx_ = ref.real_feature_idx_;
+  feature2group_ = ref.feature2group_;
+  feature2subfeature_ = ref.feature2subfeature_;
+  feature_names_ = ref.feature_names_;
+  forced_bin_bounds_ = ref.forced_bin_bounds_;
+  max_bin_ = ref.max_bin_;
+  bin_mappers_.clear();
+  for (auto& m : ref.bin_mappers_) bin_mappers_.emplace_back(new BinMapper(*m));
+  std::vector<std::vector<int>> fig;
+  for (auto& g : ref.groups_) fig.push_back(g.inner_features);
+  BuildGroups(fig);
+}
+
+void Dataset::CopySubrow(const Dataset& full, const data_size_t* idx, data_size_t n) {
+  CreateValid(full, n);
+  for (size_t g = 0; g < groups_.size(); ++g) {
+    const auto& src = full.groups_[g];
+    auto& dst = groups_[g];
+#pragma omp parallel for schedule(static)
+    for (data_size_t i = 0; i < n; ++i) {
+      std::memcpy(dst.data.data() + static_cast<size_t>(i) * dst.bin_bytes,
+                  src.data.data() + static_cast<size_t>(idx[i]) * src.bin_bytes, dst.bin_bytes);
+    }
+  }
+  metadata_.Subset(full.metadata_, idx, n);
+  finished_ = true;
+}
+
+void Dataset::set_feature_names(const std::vector<std::string>& names) {
+  if (names.empty()) return;
+  if (static_cast<int>(names.size()) != num_total_features_ && num_total_features_ > 0) {
+    Log::Fatal("Size of feature_names error, should be %d, got %d", num_total_features_,
+               static_cast<int>(names.size()));
+  }
+  feature_names_.clear();
+  for (auto n : names) {
+    // the model format is whitespace-separated: replace blanks
+    for (auto& c : n) {
+      if (c == ' ' || c == '\t' || c == '\n' || c == '\r') c = '_';
+    }
+    feature_names_.push_back(n);
+  }
+}
+
+std::vector<std::string> Dataset::feature_infos() const {
+  std::vector<std::string> out;
+  for (int i = 0; i < num_total_features_; ++i) {
+    int inner = used_feature_map_[i];
+    out.push_back(inner < 0 ? std::string("none") : bin_mappers_[inner]->bin_info_string());
+  }
+  return out;
+}
+
+void Dataset::PushColumnValue(data_size_t row, int real_col, double value) {
+  if (real_col >= num_total_features_) return;
+  int inner = used_feature_map_[real_col];
+  if (inner < 0) return;
+  const BinMapper* m = bin_mappers_[inner].get();
+  uint32_t bin = m->ValueToBin(value);
+  if (bin == m->GetMostFreqBin()) return;
+  if (m->GetMostFreqBin() == 0) bin -= 1;
+  FeatureGroup& g = groups_[feature2group_[inner]];
+  g.Set(row, bin + g.bin_offsets[feature2subfeature_[inner]]);
+}
+
+void Dataset::PushDenseRow(data_size_t row, const double* values, int ncol) {
+  const int n = std::min(ncol, num_total_features_);
+  for (int i = 0; i < n; ++i) PushColumnValue(row, i, values[i]);
+}
+
+void Dataset::PushSparseRow(data_size_t row, const std::vector<std::pair<int, double>>& values) {
+  if (need_push_zeros_.empty()) {
+    for (auto& kv : values) PushColumnValue(row, kv.first, kv.second);
+    return;
+  }
+  std::vector<char> added(num_features_, 0);
+  for (auto& kv : values) {
+    if (kv.first >= num_total_features_) continue;
+    int inner = used_feature_map_[kv.first];
+    if (inner >= 0) added[inner] = 1;
+    PushColumnValue(row, kv.first, kv.second);
+  }
+  for (int inner : need_push_zeros_) {
+    if (!added[inner]) PushColumnValue(row, real_feature_idx_[inner], 0.0);
+  }
+}
+
+uint32_t Dataset::BinThreshold(int inner, double threshold_double) const {
+  const BinMapper* m = bin_mappers_[inner].get();
+  uint32_t b = m->ValueToBin(threshold_double);
+  // ValueToBin gives the bin containing the value; the split threshold is the bin whose
+  // upper bound is >= value
+  return b;
+}
+
+bool Dataset::CheckAlign(const Dataset& o) const {
+  if (num_features_ != o.num_features_ || num_total_features_ != o.num_total_features_ ||
+      label_idx_ != o.label_idx_) {
+    return false;
+  }
+  for (int i = 0; i < num_features_; ++i) {
+    if (!bin_mappers_[i]->CheckAlign(*o.bin_mappers_[i])) return false;
+  }
+  return true;
+}
+
+void Dataset::ConstructHistograms(const std::vector<int8_t>& group_used, const data_size_t* indices,
+                                  data_size_t n, const score_t* grad, const score_t* hess, hist_t* hist) const {
+  const int ng = num_groups();
+  // gather gradients once in leaf order (the reference's "ordered gradients")
+  std::vector<score_t> og, oh;
+  const score_t* pg = grad;
+  const score_t* ph = hess;
+  if (indices != nullptr) {
+    og.resize(n);
+    oh.resize(n);
+#pragma omp parallel for schedule(static) if (n >= 16384)
+    for (data_size_t i = 0; i < n; ++i) {
+      og[i] = grad[indices[i]];
+      oh[i] = hess[indices[i]];
+    }
+    pg = og.data();
+    ph = oh.data();
+  }
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int g = 0; g < ng; ++g) {
+    if (!group_used[g]) continue;
+    const FeatureGroup& grp = groups_[g];
+    hist_t* h = hist + 2 * group_bin_boundaries_[g];
+    std::fill(h, h + 2 * grp.num_total_bin, 0.0);
+    if (grp.bin_bytes == 1) {
+      const uint8_t* col = grp.data.data();
+      if (indices) {
+        for (data_size_t i = 0; i < n; ++i) {
+          const uint32_t b = col[indices[i]];
+          h[2 * b] += pg[i];
+          h[2 * b + 1] += ph[i];
+        }
+      } else {
+        for (data_size_t i = 0; i < n; ++i) {
+          const uint32_t b = col[i];
+          h[2 * b] += pg[i];
+          h[2 * b + 1] += ph[i];
+        }
+      }
+    } else {
+      for (data_size_t i = 0; i < n; ++i) {
+        const data_size_t r = indices ? indices[i] : i;
+        const uint32_t b = grp.Get(r);
+        h[2 * b] += pg[i];
+        h[2 * b + 1] += ph[i];
+      }
+    }
+  }
+}
+
+void Dataset::FixHistogram(int inner, double sum_grad, double sum_hess, hist_t* data) const {
+  const BinMapper* m = bin_mappers_[inner].get();
+  const int mfb = static_cast<int>(m->GetMostFreqBin());
+  if (mfb > 0) {
+    const int nb = m->num_bin();
+    data[2 * mfb] = sum_grad;
+    data[2 * mfb + 1] = sum_hess;
+    for (int i = 0; i < nb; ++i) {
+      if (i != mfb) {
+        data[2 * mfb] -= data[2 * i];
+        data[2 * mfb + 1] -= data[2 * i + 1];
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// binary persistence (own format; magic + versioned)
+namespace {
+const char kMagic[] = "LGBMAMD_DATASET_V1";
+template <typename T>
+void Put(std::string* s, const T& v) { s->append(reinterpret_cast<const char*>(&v), sizeof(T)); }
+template <typename T>
+void PutVec(std::string* s, const std::vector<T>& v) {
+  uint64_t n = v.size();
+  Put(s, n);
+  if (n) s->append(reinterpret_cast<const char*>(v.data()), n * sizeof(T));
+}
+void PutStr(std::string* s, const std::string& v) {
+  uint64_t n = v.size();
+  Put(s, n);
+  s->append(v);
+}
+template <typename T>
+const char* Get(const char* p, T* v) { std::memcpy(v, p, sizeof(T)); return p + sizeof(T); }
+template <typename T>
+const char* GetVec(const char* p, std::vector<T>* v) {
+  uint64_t n;
+  p = Get(p, &n);
+  v->resize(n);
+  if (n) std::memcpy(v->data(), p, n * sizeof(T));
+  return p + n * sizeof(T);
+}
+const char* GetStr(const char* p, std::string* v) {
+  uint64_t n;
+  p = Get(p, &n);
+  v->assign(p, n);
+  return p + n;
+}
+}  // namespace
+
+void Dataset::SaveBinaryFile(const std::string& path) const {
+  std::string s(kMagic, sizeof(kMagic));
+  Put(&s, num_data_);
+  Put(&s, num_total_features_);
+  Put(&s, label_idx_);
+  Put(&s, max_bin_);
+  uint64_t nn = feature_names_.size();
+  Put(&s, nn);
+  for (auto& n : feature_names_) PutStr(&s, n);
+  PutVec(&s, used_feature_map_);
+  PutVec(&s, real_feature_idx_);
+  PutVec(&s, feature2group_);
+  PutVec(&s, feature2subfeature_);
+  for (auto& m : bin_mappers_) {
+    std::string buf(m->SizesInByte(), '\0');
+    m->CopyTo(&buf[0]);
+    PutStr(&s, buf);
+  }
+  uint64_t ng = groups_.size();
+  Put(&s, ng);
+  for (auto& g : groups_) {
+    PutVec(&s, g.inner_features);
+    PutVec(&s, g.bin_offsets);
+    Put(&s, g.num_total_bin);
+    Put(&s, g.bin_bytes);
+    PutVec(&s, g.data);
+  }
+  uint64_t nf = forced_bin_bounds_.size();
+  Put(&s, nf);
+  for (auto& v : forced_bin_bounds_) PutVec(&s, v);
+  metadata_.SaveBinary(&s);
+  std::ofstream f(path, std::ios::binary);
+  if (!f) Log::Fatal("Cannot write binary data to %s", path.c_str());
+  f.write(s.data(), static_cast<std::streamsize>(s.size()));
+  Log::Info("Saving data to binary file %s", path.c_str());
+}
+
+bool Dataset::IsBinaryFile(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  char buf[sizeof(kMagic)];
+  f.read(buf, sizeof(buf));
+  return f.gcount() == static_cast<std::streamsize>(sizeof(buf)) && std::memcmp(buf, kMagic, sizeof(kMagic)) == 0;
+}
+
+std::unique_ptr<Dataset> Dataset::LoadBinaryFile(const std::string& path) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) Log::Fatal("Cannot open binary data file %s", path.c_str());
+  std::string s((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  if (s.size() < sizeof(kMagic) || std::memcmp(s.data(), kMagic, sizeof(kMagic)) != 0) {
+    Log::Fatal("%s is not a binary dataset file", path.c_str());
+  }
+  std::unique_ptr<Dataset> d(new Dataset());
+  const char* p = s.data() + sizeof(kMagic);
+  p = Get(p, &d->num_data_);
+  p = Get(p, &d->num_total_features_);
+  p = Get(p, &d->label_idx_);
+  p = Get(p, &d->max_bin_);
+  uint64_t nn;
+  p = Get(p, &nn);
+  d->feature_names_.resize(nn);
+  for (auto& n : d->feature_names_) p = GetStr(p, &n);
+  p = GetVec(p, &d->used_feature_map_);
+  p = GetVec(p, &d->real_feature_idx_);
+  p = GetVec(p, &d->feature2group_);
+  p = GetVec(p, &d->feature2subfeature_);
+  d->num_features_ = static_cast<int>(d->real_feature_idx_.size());
+  for (int i = 0; i < d->num_features_; ++i) {
+    std::string buf;
+    p = GetStr(p, &buf);
+    d->bin_mappers_.emplace_back(new BinMapper());
+    d->bin_mappers_.back()->CopyFrom(buf.data());
+  }
+  uint64_t ng;
+  p = Get(p, &ng);
+  d->groups_.resize(ng);
+  for (auto& g : d->groups_) {
+    p = GetVec(p, &g.inner_features);
+    p = GetVec(p, &g.bin_offsets);
+    p = Get(p, &g.num_total_bin);
+    p = Get(p, &g.bin_bytes);
+    p = GetVec(p, &g.data);
+    for (int f : g.inner_features) {
+      if (d->bin_mappers_[f]->GetDefaultBin() != d->bin_mappers_[f]->GetMostFreqBin()) d->need_push_zeros_.push_back(f);
+    }
+  }
+  d->group_bin_boundaries_.assign(1, 0);
+  for (auto& g : d->groups_) d->group_bin_boundaries_.push_back(d->group_bin_boundaries_.back() + g.num_total_bin);
+  uint64_t nf;
+  p = Get(p, &nf);
+  d->forced_bin_bounds_.resize(nf);
+  for (auto& v : d->forced_bin_bounds_) p = GetVec(p, &v);
+  d->metadata_.LoadBinary(p);
+  d->finished_ = true;
+  return d;
+}
+
+void Dataset::DumpText(const std::string& path) const {
+  std::ofstream f(path);
+  f << "num_features: " << num_features_ << "\n";
+  f << "num_total_features: " << num_total_features_ << "\n";
+  f << "num_groups: " << groups_.size() << "\n";
+  f << "num_data: " << num_data_ << "\n";
+  f << "feature_names: " << common::Join(feature_names_, ", ") << "\n";
+  for (data_size_t i = 0; i < num_data_; ++i) {
+    for (int j = 0; j < num_features_; ++j) f << (j ? " " : "") << FeatureBin(j, i);
+    f << "\n";
+  }
+}
+
+void Dataset::AddFeaturesFrom(const Dataset& other) {
+  if (other.num_data_ != num_data_) Log::Fatal("Cannot add features from other Dataset with a different number of rows");
+  const int old_total = num_total_features_;
+  const int old_inner = num_features_;
+  const int old_groups = num_groups();
+  for (int i = 0; i < other.num_total_features_; ++i) {
+    used_feature_map_.push_back(other.used_feature_map_[i] < 0 ? -1 : other.used_feature_map_[i] + old_inner);
+    feature_names_.push_back(i < static_cast<int>(other.feature_names_.size()) ? other.feature_names_[i]
+                                                                             : "Column_" + std::to_string(old_total + i));
+  }
+  for (int j = 0; j < other.num_features_; ++j) {
+    real_feature_idx_.push_back(other.real_feature_idx_[j] + old_total);
+    feature2group_.push_back(other.feature2group_[j] + old_groups);
+    feature2subfeature_.push_back(other.feature2subfeature_[j]);
+    bin_mappers_.emplace_back(new BinMapper(*other.bin_mappers_[j]));
+  }
+  for (auto g : other.groups_) {
+    for (auto& f : g.inner_features) f += old_inner;
+    groups_.push_back(std::move(g));
+  }
+  for (int f : other.need_push_zeros_) need_push_zeros_.push_back(f + old_inner);
+  num_total_features_ += other.num_total_features_;
+  num_features_ += other.num_features_;
+  group_bin_boundaries_.assign(1, 0);
+  for (auto& g : groups_) group_bin_boundaries_.push_back(group_bin_boundaries_.back() + g.num_total_bin);
+}
+
+}  // namespace lgbm_amd

@@ -1,0 +1,205 @@
+// Network facade: per-thread state (so tests can run several ranks as threads in one
+// process, like the reference's THREAD_LOCAL Network, src/network/network.cpp:17-27),
+// collectives built on a pluggable HostTransport.
+#include "lgbm_amd/network.h"
+
+#include <condition_variable>
+#include <mutex>
+
+#include "lgbm_amd/common.h"
+#include "lgbm_amd/log.h"
+
+namespace lgbm_amd {
+
+std::shared_ptr<HostTransport> MakeTcpTransport(const Config& cfg);  // tcp_transport.cpp
+
+namespace {
+
+struct NetState {
+  std::shared_ptr<HostTransport> transport;
+  std::shared_ptr<DeviceComm> device;
+};
+
+NetState& State() {
+  static thread_local NetState s;
+  return s;
+}
+
+// adapter for the reference's external function pair
+class ExternalFnTransport : public HostTransport {
+ public:
+  ExternalFnTransport(int n, int r, ReduceScatterFunctionPtr rs, AllgatherFunctionPtr ag)
+      : n_(n), r_(r), rs_(rs), ag_(ag) {}
+  int rank() const override { return r_; }
+  int num_machines() const override { return n_; }
+  void Allgather(const char* input, comm_size_t input_size, const comm_size_t* block_start,
+                 const comm_size_t* block_len, char* output, comm_size_t output_size) override {
+    ag_(const_cast<char*>(input), input_size, block_start, block_len, n_, output, output_size);
+  }
+  bool ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
+                     const comm_size_t* block_len, char* output, comm_size_t output_size,
+                     const ReduceFunction& reducer) override {
+    if (rs_ == nullptr) return false;
+    // the external ABI takes a plain function pointer: route through a thread-local trampoline
+    static thread_local const ReduceFunction* active = nullptr;
+    active = &reducer;
+    ReduceFunctionPtr tramp = [](const char* in, char* out, int ts, comm_size_t len) { (*active)(in, out, ts, len); };
+    rs_(input, input_size, type_size, block_start, block_len, n_, output, output_size, tramp);
+    active = nullptr;
+    return true;
+  }
+
+ private:
+  int n_, r_;
+  ReduceScatterFunctionPtr rs_;
+  AllgatherFunctionPtr ag_;
+};
+
+// threads-as-ranks rendezvous
+struct ThreadHub {
+  explicit ThreadHub(int n) : n(n), bufs(n), lens(n) {}
+  int n;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  int generation = 0;
+  int readers_done = 0;
+  std::vector<const char*> bufs;
+  std::vector<comm_size_t> lens;
+};
+
+class ThreadTransport : public HostTransport {
+ public:
+  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  int rank() const override { return rank_; }
+  int num_machines() const override { return hub_->n; }
+  void Allgather(const char* input, comm_size_t input_size, const comm_size_t* block_start,
+                 const comm_size_t* block_len, char* output, comm_size_t output_size) override {
+    (void)output_size;
+    std::unique_lock<std::mutex> lk(hub_->mu);
+    // wait until the previous round's readers are done
+    hub_->cv.wait(lk, [&] { return hub_->readers_done == 0 || hub_->readers_done == hub_->n; });
+    if (hub_->readers_done == hub_->n) hub_->readers_done = 0;
+    const int gen = hub_->generation;
+    hub_->bufs[rank_] = input;
+    hub_->lens[rank_] = input_size;
+    if (++hub_->arrived == hub_->n) {
+      hub_->arrived = 0;
+      hub_->generation++;
+      hub_->cv.notify_all();
+    } else {
+      hub_->cv.wait(lk, [&] { return hub_->generation != gen; });
+    }
+    lk.unlock();
+    for (int r = 0; r < hub_->n; ++r) std::memcpy(output + block_start[r], hub_->bufs[r], block_len[r]);
+    lk.lock();
+    hub_->readers_done++;
+    hub_->cv.notify_all();
+    // keep inputs alive until everyone has copied
+    hub_->cv.wait(lk, [&] { return hub_->readers_done == hub_->n || hub_->readers_done == 0; });
+  }
+
+ private:
+  std::shared_ptr<ThreadHub> hub_;
+  int rank_;
+};
+
+}  // namespace
+
+std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks) {
+  auto hub = std::make_shared<ThreadHub>(num_ranks);
+  std::vector<std::shared_ptr<HostTransport>> out;
+  for (int r = 0; r < num_ranks; ++r) out.push_back(std::make_shared<ThreadTransport>(hub, r));
+  return out;
+}
+
+void Network::Init(const Config& cfg) {
+  if (cfg.num_machines <= 1) return;
+  State().transport = MakeTcpTransport(cfg);
+  Log::Info("Local rank: %d, total number of machines: %d", rank(), num_machines());
+}
+
+void Network::InitWithTransport(std::shared_ptr<HostTransport> t) { State().transport = std::move(t); }
+
+void Network::InitWithFunctions(int num_machines, int rank, ReduceScatterFunctionPtr rs, AllgatherFunctionPtr ag) {
+  if (num_machines <= 1) {
+    State().transport.reset();
+    return;
+  }
+  if (ag == nullptr) Log::Fatal("An allgather function is required");
+  State().transport = std::make_shared<ExternalFnTransport>(num_machines, rank, rs, ag);
+}
+
+void Network::Dispose() {
+  State().transport.reset();
+  State().device.reset();
+}
+
+int Network::rank() { return State().transport ? State().transport->rank() : 0; }
+int Network::num_machines() { return State().transport ? State().transport->num_machines() : 1; }
+
+void Network::SetDeviceComm(std::shared_ptr<DeviceComm> c) { State().device = std::move(c); }
+DeviceComm* Network::device_comm() { return State().device.get(); }
+
+void Network::Allgather(char* input, comm_size_t send_size, char* output) {
+  const int n = num_machines();
+  if (n <= 1) {
+    std::memcpy(output, input, send_size);
+    return;
+  }
+  std::vector<comm_size_t> start(n), len(n, send_size);
+  for (int i = 0; i < n; ++i) start[i] = i * send_size;
+  Allgather(input, start.data(), len.data(), output, send_size * n);
+}
+
+void Network::Allgather(char* input, const comm_size_t* block_start, const comm_size_t* block_len, char* output,
+                        comm_size_t all_size) {
+  if (num_machines() <= 1) {
+    std::memcpy(output, input, block_len[0]);
+    return;
+  }
+  State().transport->Allgather(input, block_len[rank()], block_start, block_len, output, all_size);
+}
+
+void Network::ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
+                            const comm_size_t* block_len, char* output, comm_size_t output_size,
+                            const ReduceFunction& reducer) {
+  const int n = num_machines();
+  const int r = rank();
+  if (n <= 1) {
+    std::memcpy(output, input, input_size);
+    return;
+  }
+  if (State().transport->ReduceScatter(input, input_size, type_size, block_start, block_len, output, output_size,
+                                       reducer)) {
+    return;
+  }
+  // allgather every rank's full input, reduce own block locally
+  std::vector<comm_size_t> st(n), ln(n, input_size);
+  for (int i = 0; i < n; ++i) st[i] = i * input_size;
+  std::vector<char> all(static_cast<size_t>(input_size) * n);
+  State().transport->Allgather(input, input_size, st.data(), ln.data(), all.data(), input_size * n);
+  // fixed rank order (0, 1, ..., n-1) so the reduced block is independent of who reduces it
+  std::memcpy(output, all.data() + block_start[r], block_len[r]);
+  for (int i = 1; i < n; ++i) {
+    reducer(all.data() + static_cast<size_t>(i) * input_size + block_start[r], output, type_size, block_len[r]);
+  }
+}
+
+void Network::Allreduce(char* input, comm_size_t input_size, int type_size, char* output,
+                        const ReduceFunction& reducer) {
+  const int n = num_machines();
+  if (n <= 1) {
+    if (output != input) std::memcpy(output, input, input_size);
+    return;
+  }
+  // allgather + fixed-order local reduce: every rank gets bitwise identical results
+  std::vector<comm_size_t> st(n), ln(n, input_size);
+  for (int i = 0; i < n; ++i) st[i] = i * input_size;
+  std::vector<char> all(static_cast<size_t>(input_size) * n);
+  State().transport->Allgather(input, input_size, st.data(), ln.data(), all.data(), input_size * n);
+  std::memcpy(output, all.data(), input_size);
+  for (int i = 1; i < n; ++i) reducer(all.data() + static_cast<size_t>(i) * input_size, output, type_size, input_size);
+}
+
+}  // namespace lgbm_amd

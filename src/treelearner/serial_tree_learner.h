@@ -1,0 +1,123 @@
+// CPU leaf-wise (best-first) tree learner -- the host reference implementation used
+// for device_type=cpu, as the differential-testing oracle of the device learner, and as
+// the base of the CPU parallel learners.  Growth loop, histogram subtraction, the
+// smaller/larger leaf bookkeeping, forced splits, refit and output renewal follow
+// reference src/treelearner/serial_tree_learner.cpp:152-776.
+#pragma once
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "col_sampler.h"
+#include "lgbm_amd/json.h"
+#include "lgbm_amd/split_info.h"
+#include "lgbm_amd/tree_learner.h"
+#include "split_finder.h"
+
+namespace lgbm_amd {
+
+// per-leaf monotone bounds ("basic" method, reference monotone_constraints.hpp:98-145)
+struct LeafConstraints {
+  std::vector<ConstraintRange> entries;
+  void Init(int n) { entries.assign(n, ConstraintRange{-std::numeric_limits<double>::max(), std::numeric_limits<double>::max()}); }
+  void Update(bool is_numerical, int leaf, int new_leaf, int8_t mono, double right_out, double left_out) {
+    entries[new_leaf] = entries[leaf];
+    if (!is_numerical) return;
+    double mid = (left_out + right_out) / 2.0f;
+    if (mono < 0) {
+      entries[leaf].min = std::max(entries[leaf].min, mid);
+      entries[new_leaf].max = std::min(entries[new_leaf].max, mid);
+    } else if (mono > 0) {
+      entries[leaf].max = std::min(entries[leaf].max, mid);
+      entries[new_leaf].min = std::max(entries[new_leaf].min, mid);
+    }
+  }
+};
+
+double MonotoneSplitPenalty(int depth, double penalization);
+
+class SerialTreeLearner : public TreeLearner {
+ public:
+  explicit SerialTreeLearner(const Config* config);
+  void Init(const Dataset* train_data, bool is_constant_hessian) override;
+  void ResetTrainingData(const Dataset* train_data, bool is_constant_hessian) override;
+  void ResetConfig(const Config* config) override;
+  void SetForcedSplit(const std::string& json_text) override;
+  Tree* Train(const score_t* gradients, const score_t* hessians) override;
+  Tree* FitByExistingTree(const Tree* old_tree, const score_t* gradients, const score_t* hessians) const override;
+  Tree* FitByExistingTree(const Tree* old_tree, const std::vector<int>& leaf_pred, const score_t* gradients,
+                          const score_t* hessians) override;
+  void SetBaggingData(const Dataset* subset, const data_size_t* used_indices, data_size_t num_data) override;
+  void AddPredictionToScore(const Tree* tree, double* out_score) const override;
+  void RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
+                       const std::function<double(const label_t*, int)>& residual_getter,
+                       data_size_t total_num_data, const data_size_t* bag_indices, data_size_t bag_cnt) const override;
+
+ protected:
+  struct LeafState {
+    int leaf = -1;
+    data_size_t num_data = 0;
+    double sum_g = 0, sum_h = 0;
+    double output = 0;  // leaf output (parent output for smoothing)
+  };
+  // data partition
+  const data_size_t* LeafIndices(int leaf, data_size_t* cnt) const {
+    *cnt = leaf_count_[leaf];
+    return indices_.data() + leaf_begin_[leaf];
+  }
+  data_size_t PartitionLeaf(int leaf, int inner_feature, const SplitInfo& s, int new_leaf);
+
+  virtual void BeforeTrain();
+  virtual bool BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf);
+  virtual void FindBestSplits(const Tree* tree);
+  virtual void ConstructHistograms(const std::vector<int8_t>& feature_used, bool use_subtract);
+  virtual void FindBestSplitsFromHistograms(const std::vector<int8_t>& feature_used, bool use_subtract,
+                                            const Tree* tree);
+  virtual void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf);
+  virtual data_size_t GetGlobalDataCountInLeaf(int leaf) const { return leaf >= 0 ? leaf_count_[leaf] : 0; }
+  int ForceSplits(Tree* tree, int* left_leaf, int* right_leaf, int* cur_depth);
+  void ComputeBestSplitForFeature(int slot, int inner, const std::vector<int8_t>& node_used, const LeafState& ls,
+                                  int depth, SplitInfo* best);
+  // evaluate one feature histogram with explicit params; returns splittability
+  bool EvalFeature(hist_t* hist, int inner, const SplitParams& p, const LeafState& ls, int depth, SplitInfo* best);
+  void SplitInner(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf, bool update_cnt);
+  hist_t* FeatureHist(int slot, int inner) { return hist_pool_[slot].data() + 2 * data_->FeatureHistOffset(inner); }
+  void InitFeatureMeta();
+  std::vector<int8_t> GroupsUsed(const std::vector<int8_t>& feature_used) const;
+
+  const Config* config_;
+  const Dataset* data_ = nullptr;
+  data_size_t num_data_ = 0;
+  int num_features_ = 0;
+  SplitParams params_;
+  std::vector<FeatureMeta> meta_;
+  ColSampler col_sampler_;
+  LeafConstraints constraints_;
+  std::vector<SplitInfo> best_split_per_leaf_;
+
+  // histogram pool: one full histogram per slot, slot_of_leaf_ maps leaves to slots
+  std::vector<std::vector<hist_t>> hist_pool_;
+  std::vector<std::vector<char>> splittable_;  // per slot, per inner feature
+  std::vector<int> slot_of_leaf_;
+  int smaller_slot_ = -1, larger_slot_ = -1;
+  bool has_parent_hist_ = false;
+  LeafState smaller_, larger_;
+
+  // partition
+  std::vector<data_size_t> indices_;
+  std::vector<data_size_t> leaf_begin_, leaf_count_;
+  std::vector<data_size_t> tmp_left_, tmp_right_;
+  const data_size_t* bag_indices_ = nullptr;
+  data_size_t bag_cnt_ = 0;
+  bool use_bag_ = false;
+
+  const score_t* gradients_ = nullptr;
+  const score_t* hessians_ = nullptr;
+  Json forced_split_;
+  bool has_forced_split_ = false;
+  // features owned by this rank (feature-parallel); empty = all
+  std::vector<int8_t> feature_mask_;
+};
+
+}  // namespace lgbm_amd
