@@ -1,0 +1,153 @@
+"""Headline benchmark: sec/iteration of GBDT training on a Higgs-shaped 10M x 28 binary task.
+
+Config (BASELINE.json / docs GPU-Performance): objective=binary, max_bin=255,
+num_leaves=63, learning_rate=0.1, min_data_in_leaf=1, min_sum_hessian_in_leaf=100,
+device_type=gpu.  A "step" is one boosting iteration (gradients + one tree + score
+update).  Synthetic data: 10M rows x 28 float32 features with a non-linear label
+(21 "low-level" + 7 "high-level" derived features, Higgs-like layout); AUC on a
+held-out synthetic set is reported for parity checks.
+
+  python bench.py --gpus 1 --steps 50 --warmup 5
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+      --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 5
+
+With N>1 ranks the 10M rows are sharded row-wise (rank r owns rows r*10M/N ...), one
+process per GPU, tree_learner=data: per-split histograms are all-reduced with RCCL
+(strong scaling: the total work is fixed).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_SEC_PER_ITER = 0.232  # GTX 1080, Higgs 10.5M x 28, 255 bins
+
+
+def make_rows(start, count, num_features=28, seed=20240601):
+    """Deterministic synthetic Higgs-like rows [start, start+count)."""
+    block = 1 << 20
+    X = np.empty((count, num_features), dtype=np.float32)
+    y = np.empty(count, dtype=np.float32)
+    done = 0
+    while done < count:
+        gidx = start + done
+        b = gidx // block
+        off = gidx % block
+        n = min(count - done, block - off)
+        rng = np.random.default_rng(seed + b)
+        low = rng.standard_normal((block, 21), dtype=np.float32)[off:off + n]
+        low[:, 0::3] = np.abs(low[:, 0::3]) * 0.7 + 0.3          # momenta-like (positive, skewed)
+        low[:, 1::3] = np.clip(low[:, 1::3], -2.5, 2.5)          # pseudo-rapidities
+        low[:, 2::3] = np.tanh(low[:, 2::3]) * 1.74              # angles
+        m = np.empty((n, num_features - 21), dtype=np.float32)   # high-level invariant masses
+        for j in range(num_features - 21):
+            a, c = low[:, (3 * j) % 21], low[:, (3 * j + 3) % 21]
+            m[:, j] = np.sqrt(np.abs(a * c * (1.0 + np.cos(low[:, (3 * j + 2) % 21] - low[:, (3 * j + 5) % 21]))))
+        X[done:done + n, :21] = low
+        X[done:done + n, 21:] = m
+        noise = np.random.default_rng(seed + 7919 + b).standard_normal(block, dtype=np.float32)[off:off + n]
+        logit = (1.2 * m[:, 0] - 0.8 * m[:, 1] + 0.6 * m[:, 2] * low[:, 0] - 0.5 * low[:, 3] ** 2
+                 + 0.4 * np.sin(2.0 * low[:, 4]) + 0.3 * m[:, 3] * m[:, 4] - 0.9 + 0.8 * noise)
+        y[done:done + n] = (logit > 0).astype(np.float32)
+        done += n
+    return X, y
+
+
+def roc_auc(y, p):
+    from scipy.stats import rankdata
+    ranks = rankdata(p)
+    pos = y > 0.5
+    npos, nneg = int(pos.sum()), int((~pos).sum())
+    return float((ranks[pos].sum() - npos * (npos + 1) / 2.0) / max(1, npos * nneg))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rows", type=int, default=10_000_000)
+    ap.add_argument("--features", type=int, default=28)
+    ap.add_argument("--leaves", type=int, default=63)
+    ap.add_argument("--max-bin", type=int, default=255)
+    ap.add_argument("--device", default="gpu")
+    ap.add_argument("--test-rows", type=int, default=500_000)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    import lightgbmv1_amd as lgb
+    from lightgbmv1_amd.parallel import torch_dist
+
+    if world > 1:
+        torch_dist.init_network(use_rccl=args.device == "gpu")
+    n_total = args.rows
+    lo = n_total * rank // world
+    hi = n_total * (rank + 1) // world
+    t0 = time.time()
+    X, y = make_rows(lo, hi - lo, args.features)
+    params = {
+        "objective": "binary",
+        "metric": "auc",
+        "max_bin": args.max_bin,
+        "num_leaves": args.leaves,
+        "learning_rate": 0.1,
+        "min_data_in_leaf": 1,
+        "min_sum_hessian_in_leaf": 100,
+        "device_type": args.device,
+        "tree_learner": "data" if world > 1 else "serial",
+        "num_machines": world,
+        "pre_partition": True,
+        "verbose": -1,
+        "num_threads": min(16, os.cpu_count() or 8),
+    }
+    train = lgb.Dataset(X, y, params=params, free_raw_data=True)
+    booster = lgb.Booster(params=params, train_set=train)
+    del X
+    setup_s = time.time() - t0
+    for _ in range(args.warmup):
+        booster.update()
+    torch_dist.barrier()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        booster.update()
+    torch_dist.barrier()
+    elapsed = time.perf_counter() - t1
+    elapsed = torch_dist.allreduce_max(elapsed)
+    sec_per_iter = elapsed / max(1, args.steps)
+    auc = None
+    if rank == 0 and args.test_rows > 0:
+        Xt, yt = make_rows(n_total + 12345678, args.test_rows, args.features)
+        auc = roc_auc(yt, booster.predict(Xt))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "sec/iteration (500 trees, 255 bins, 63 leaves) on Higgs-shaped 10Mx28; AUC parity",
+            "value": round(sec_per_iter, 6),
+            "unit": "s/iter",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * sec_per_iter, 4),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": round(sec_per_iter / BASELINE_SEC_PER_ITER, 6),
+            "dtype": "fp32",
+            "data": "synthetic",
+            "config": {"model": "gbdt binary, num_leaves={}, max_bin={}".format(args.leaves, args.max_bin),
+                       "global_batch": n_total, "seq_len": args.features,
+                       "parallelism": "dp{}".format(world) if world > 1 else "single"},
+            "auc_heldout": auc,
+            "trees": booster.num_trees(),
+            "setup_s": round(setup_s, 2),
+        }), flush=True)
+    if world > 1:
+        torch_dist.shutdown()
+
+
+if __name__ == "__main__":
+    main()

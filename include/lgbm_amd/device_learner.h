@@ -2,16 +2,19 @@
 // src/treelearner/gpu_tree_learner.cpp).  Beyond tree growth, the device learner owns
 // the training score / gradient buffers in HBM so that one boosting iteration runs
 // without host<->device traffic except the finished tree (SURVEY.md §7.1 principle 1).
+// It is a mix-in next to TreeLearner; GBDT discovers it with dynamic_cast.
 #pragma once
+
+#include <vector>
 
 #include "lgbm_amd/objective.h"
 #include "lgbm_amd/tree_learner.h"
 
 namespace lgbm_amd {
 
-class DeviceTreeLearner : public TreeLearner {
+class DeviceTreeLearner {
  public:
-  bool IsDevice() const override { return true; }
+  virtual ~DeviceTreeLearner() = default;
   // allocate num_tree_per_iteration * num_data score/gradient buffers
   virtual void InitScores(int num_tree_per_iteration, const double* init_score) = 0;
   virtual void SyncScoreToHost(double* host, int tree_id) = 0;  // D2H of one class slice
@@ -28,9 +31,6 @@ class DeviceTreeLearner : public TreeLearner {
   virtual void DownloadGradients(score_t* g, score_t* h, int64_t n) = 0;
   virtual score_t* device_gradients() = 0;
   virtual score_t* device_hessians() = 0;
-  // host copy of the row indices of each leaf after Train() (for leaf renewal)
-  virtual void DownloadPartition(std::vector<data_size_t>* indices, std::vector<data_size_t>* begin,
-                                 std::vector<data_size_t>* count) = 0;
   virtual void Synchronize() = 0;
 };
 

@@ -1,0 +1,120 @@
+"""Distributed bootstrap over torch.distributed (one process per GPU).
+
+The native library needs two kinds of collectives:
+  * host collectives (bin-mapper exchange, split-info sync, metric sums): provided to
+    ``LGBM_NetworkInitWithFunctions`` as an allgather callback backed by a CPU (gloo)
+    process group -- the analogue of the reference's socket/MPI linkers
+    (reference src/network/linkers_socket.cpp, c_api.h LGBM_NetworkInitWithFunctions);
+  * device collectives (per-split histogram all-reduce, root statistics): an RCCL
+    communicator over xGMI created natively from an ncclUniqueId that rank 0 draws and
+    broadcasts through the same process group (src/network/rccl_comm.cpp).
+
+torch itself never touches the GPU here, so the HIP runtime is owned by the library.
+Rendezvous uses MASTER_ADDR / MASTER_PORT / RANK / WORLD_SIZE (torchrun); always use
+127.0.0.1 on a single node.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from ..basic import _load_lib, _safe_call
+
+_ALLGATHER_T = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                                ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
+
+_STATE = {"callbacks": None, "group": None, "rccl": False}
+
+
+def _make_allgather(dist, group):
+    import torch
+
+    def allgather(input_ptr, input_size, block_start, block_len, num_block, output_ptr, output_size):
+        lens = [block_len[i] for i in range(num_block)]
+        starts = [block_start[i] for i in range(num_block)]
+        max_len = max(lens) if lens else 0
+        mine = np.zeros(max(1, max_len), dtype=np.uint8)
+        if input_size > 0:
+            ctypes.memmove(mine.ctypes.data, input_ptr, input_size)
+        send = torch.from_numpy(mine)
+        recv = [torch.empty_like(send) for _ in range(num_block)]
+        dist.all_gather(recv, send, group=group)
+        for r in range(num_block):
+            if lens[r] > 0:
+                ctypes.memmove(output_ptr + starts[r], recv[r].numpy().ctypes.data, lens[r])
+    return _ALLGATHER_T(allgather)
+
+
+def init_network(use_rccl=True, backend="gloo", timeout_s=600):
+    """Initialise host (and optionally RCCL device) collectives for the current process group.
+
+    Returns (rank, world_size, local_rank).
+    """
+    import datetime
+
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world <= 1:
+        return rank, world, local_rank
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if not dist.is_initialized():
+        dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    group = dist.group.WORLD
+    lib = _load_lib()
+    cb = _make_allgather(dist, group)
+    _STATE["callbacks"] = cb
+    _STATE["group"] = group
+    _safe_call(lib.LGBM_NetworkInitWithFunctions(ctypes.c_int(world), ctypes.c_int(rank), None, cb))
+    if use_rccl:
+        ndev = ctypes.c_int(0)
+        _safe_call(lib.LGBM_AMD_DeviceCount(ctypes.byref(ndev)))
+        if ndev.value > 0:
+            import torch
+            size = ctypes.c_int(0)
+            _safe_call(lib.LGBM_AMD_RcclUniqueIdSize(ctypes.byref(size)))
+            uid = np.zeros(size.value, dtype=np.uint8)
+            if rank == 0:
+                _safe_call(lib.LGBM_AMD_RcclGetUniqueId(uid.ctypes.data_as(ctypes.c_char_p)))
+            t = torch.from_numpy(uid)
+            dist.broadcast(t, src=0, group=group)
+            uid = t.numpy()
+            _safe_call(lib.LGBM_AMD_RcclInit(ctypes.c_int(world), ctypes.c_int(rank),
+                                             ctypes.c_int(local_rank % ndev.value),
+                                             uid.ctypes.data_as(ctypes.c_char_p)))
+            _STATE["rccl"] = True
+    return rank, world, local_rank
+
+
+def barrier():
+    import torch.distributed as dist
+    if dist.is_initialized():
+        dist.barrier()
+
+
+def allreduce_max(value):
+    """Max of a float over ranks (host)."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return value
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown():
+    lib = _load_lib()
+    if _STATE["rccl"]:
+        lib.LGBM_AMD_RcclFree()
+        _STATE["rccl"] = False
+    lib.LGBM_NetworkFree()
+    try:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # pragma: no cover
+        pass

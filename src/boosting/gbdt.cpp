@@ -107,7 +107,7 @@ void GBDT::Init(const Config* cfg, const Dataset* train_data, const ObjectiveFun
   tree_learner_.reset(TreeLearner::CreateTreeLearner(config_->tree_learner, config_->device_type, config_.get()));
   tree_learner_->Init(train_data_, is_constant_hessian_);
   tree_learner_->SetForcedSplit(forced_splits_text_);
-  device_learner_ = tree_learner_->IsDevice() ? static_cast<DeviceTreeLearner*>(tree_learner_.get()) : nullptr;
+  device_learner_ = dynamic_cast<DeviceTreeLearner*>(tree_learner_.get());
   training_metrics_ = training_metrics;
   train_score_updater_.reset(new ScoreUpdater(train_data_, num_tree_per_iteration_));
   host_score_fresh_ = true;

@@ -1,0 +1,90 @@
+// POD records shared by the HIP kernels (src/device/*.hip) and the host orchestration
+// of the MI355X tree learner (src/treelearner/gpu_tree_learner.cpp).  All of them live
+// in HBM for the whole training run; the host only writes them at (re)initialisation and
+// reads the per-tree split records back once per tree.
+#pragma once
+
+#include <cstdint>
+
+#include "lgbm_amd/split_info.h"
+#include "lgbm_amd/split_math.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+constexpr int kMaxLeaves = 1024;  // device-mode tree size limit (num_leaves)
+
+// interleaved (gradient, hessian) of one row: one 8-byte gather per row
+struct alignas(8) GH {
+  float g;
+  float h;
+};
+
+// per inner feature, everything the split scan and the partition need
+struct Feature {
+  int32_t group;        // storage column (feature group)
+  int32_t hist_offset;  // first histogram bin of this feature (Dataset::FeatureHistOffset)
+  int32_t num_bin;      // BinMapper::num_bin
+  int32_t offset;       // 1 when the most frequent bin is 0 (bin 0 is not stored)
+  int32_t default_bin;
+  int32_t mfb;          // most frequent bin
+  int32_t missing_type;  // 0 none, 1 zero, 2 NaN
+  int32_t is_cat;
+  int32_t sub_lo, sub_hi;  // this feature's [lo, hi) range inside the group's bin space
+  int32_t real_index;
+  int32_t monotone;
+  double penalty;
+};
+
+// tree-growth parameters (uniform for the launch)
+struct Params {
+  SplitParams sp;
+  int32_t num_leaves;
+  int32_t max_depth;
+  int32_t num_features;
+  int32_t num_groups;
+  int32_t row_stride;  // bytes (or uint16 elements) per row in the bin matrix
+  int32_t total_bins;  // histogram length in bins
+  double monotone_penalty;
+  int32_t data_parallel;  // leaf sizes/decisions from global (split-estimated) counts
+  int32_t pad;
+};
+
+// per-leaf state
+struct Leaf {
+  int32_t begin;         // local index range in the partition array
+  int32_t count;         // local rows
+  int32_t global_count;  // rows over all ranks (== count without data-parallel)
+  int32_t depth;
+  int32_t slot;          // histogram slot
+  int32_t pad;
+  double sum_g, sum_h, output;
+  double cmin, cmax;  // monotone constraint range
+};
+
+// one split step: written by the select kernel, consumed by partition/hist/find
+struct Step {
+  int32_t done;       // tree finished: every later kernel of the tree exits
+  int32_t step;       // split index (0-based); new leaf id = step + 1
+  int32_t leaf;       // leaf being split (keeps its id as the left child)
+  int32_t new_leaf;   // right child id
+  int32_t smaller, larger;
+  int32_t skip_find;  // children can not be split further (depth / min_data)
+  int32_t total_left;  // local rows sent left (set by the scatter kernel)
+  int32_t num_blocks;  // partition blocks used
+  int32_t rows_per_block;
+  int32_t part_begin;  // range of the leaf being split, before the split
+  int32_t part_count;
+  DeviceSplit split;
+};
+
+// record of one applied split, read back by the host to rebuild the Tree
+struct SplitRecord {
+  int32_t leaf;
+  int32_t left_count, right_count;  // counts stored in the model (global)
+  int32_t pad;
+  DeviceSplit split;
+};
+
+}  // namespace dev
+}  // namespace lgbm_amd

@@ -1,0 +1,104 @@
+// Host-side launch interface of the MI355X tree-learner kernels (src/device/kernels.hip).
+// Every launcher is stream-ordered and performs no host synchronisation, so a whole tree
+// (root + num_leaves-1 split steps) can be enqueued back to back or captured into one
+// hipGraph.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+#include "device_types.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+// pointers and constants shared by the tree-growth kernels
+struct KArgs {
+  Params p;
+  const void* bins;          // row-major bin matrix, [rows][row_stride] of uint8 / uint16
+  const Feature* feat;       // [num_features]
+  const int32_t* group_off;  // [num_groups] first histogram bin of each storage column
+  const int8_t* tree_mask;   // [num_features] feature used by this tree
+  const GH* gh;              // interleaved (gradient, hessian) per row
+  int32_t* idx;              // partition indices
+  int32_t* tmp;              // partition scratch
+  Leaf* leaves;              // [num_leaves]
+  Step* st;
+  SplitRecord* rec;          // [num_leaves - 1]
+  DeviceSplit* best;         // [num_leaves]
+  float* hist;               // [num_leaves][total_bins][2]
+  float* scratch;            // [total_bins][2] (the histogram being built)
+  int32_t* blk;              // partition block counts [kMaxPartBlocks]
+  double* root;              // [sum_g, sum_h, count]
+  int32_t num_rows;          // local rows in the root
+  int32_t root_identity;     // root rows are 0..num_rows-1 (indices written by the root pass)
+  int32_t bin_bytes;         // 1 or 2
+  int32_t words_per_row;     // 32-bit words per row
+  int32_t hist_tiles;        // column tiles of the histogram kernel
+  int32_t tile_words;        // words per column tile
+  int32_t tile_bins;         // max histogram bins of one tile (LDS floats = 2 * tile_bins)
+  int32_t range_begin;       // explicit-range histogram (host-assisted mode)
+};
+
+constexpr int kMaxPartBlocks = 1024;
+constexpr int kHistBlockThreads = 256;
+
+int HistGridBlocks();  // blocks per column tile of a full-size histogram launch
+void SetNumCUs(int n);
+
+void PackGH(const float* g, const float* h, GH* gh, int64_t n, hipStream_t s);
+void TreeBegin(const KArgs& a, hipStream_t s);
+void RootSum(const KArgs& a, hipStream_t s);
+void HistRoot(const KArgs& a, hipStream_t s);
+void HistStep(const KArgs& a, hipStream_t s);
+// histogram of rows idx[range_begin, range_begin + num_rows) into scratch
+void HistRange(const KArgs& a, hipStream_t s);
+void FindRoot(const KArgs& a, hipStream_t s);
+void FindStep(const KArgs& a, hipStream_t s);
+void SelectSplit(const KArgs& a, hipStream_t s);
+void PartitionCount(const KArgs& a, hipStream_t s);
+void PartitionScatter(const KArgs& a, hipStream_t s);
+
+// score[k] += value[leaf(row)] for every partitioned row of the finished tree
+void AddLeafScore(const KArgs& a, const double* leaf_values, int num_leaves, double* score, hipStream_t s);
+
+// generic tree traversal over binned rows (out-of-bag rows, DART drops, refits)
+struct DevTree {
+  int32_t num_leaves;
+  const int32_t* split_feature_inner;
+  const uint32_t* threshold_in_bin;
+  const int8_t* decision_type;
+  const int32_t* left_child;
+  const int32_t* right_child;
+  const double* leaf_value;
+  const int32_t* cat_boundaries_inner;
+  const uint32_t* cat_threshold_inner;
+};
+void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
+                  hipStream_t s);
+
+void Iota(int32_t* p, int64_t n, hipStream_t s);
+
+// score scaling helpers
+void AddConst(double* score, int64_t n, double v, hipStream_t s);
+void MulConst(double* score, int64_t n, double v, hipStream_t s);
+
+// point-wise objective gradients: kind = DeviceGradKind
+struct GradArgs {
+  int32_t kind;
+  int32_t num_class;
+  int64_t num_data;
+  double p0, p1, p2;
+  double lw0, lw1;
+  const float* label;
+  const float* weights;      // may be null
+  const float* label_weight;  // MAPE per-row factor, may be null
+  const double* score;       // [num_class][num_data]
+  float* grad;
+  float* hess;
+};
+void Gradients(const GradArgs& g, hipStream_t s);
+
+}  // namespace dev
+}  // namespace lgbm_amd

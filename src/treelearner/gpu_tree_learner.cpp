@@ -1,0 +1,745 @@
+// MI355X tree learner host orchestration (see gpu_tree_learner.h).
+#include "gpu_tree_learner.h"
+
+#include <omp.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "lgbm_amd/common.h"
+#include "lgbm_amd/log.h"
+#include "lgbm_amd/network.h"
+
+#define HIPCHECK(x)                                                                               \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) Log::Fatal("HIP error %s at %s:%d: %s", #x, __FILE__, __LINE__, hipGetErrorString(e_)); \
+  } while (0)
+
+namespace lgbm_amd {
+
+namespace {
+
+int PickDevice(const Config* cfg) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    Log::Fatal("device_type=gpu requested but no HIP device is visible");
+  }
+  if (cfg->gpu_device_id >= 0) return cfg->gpu_device_id % count;
+  const char* lr = std::getenv("LOCAL_RANK");
+  if (lr != nullptr) return std::atoi(lr) % count;
+  return 0;
+}
+
+int PartBlocks(int count, int* rpb_out) {
+  int nb = (count + 4095) / 4096;
+  nb = std::max(1, std::min(dev::kMaxPartBlocks, nb));
+  int rpb = (count + nb - 1) / nb;
+  rpb = ((rpb + 255) / 256) * 256;
+  if (rpb == 0) rpb = 256;
+  nb = std::max(1, (count + rpb - 1) / rpb);
+  *rpb_out = rpb;
+  return nb;
+}
+
+}  // namespace
+
+TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Config* config) {
+  if (learner_type == "serial") return new GPUTreeLearner(config, false);
+  if (learner_type == "data") return new GPUTreeLearner(config, true);
+  if (learner_type == "feature") {
+    Log::Warning("feature-parallel learning on the device learner uses the serial device learner on every rank");
+    return new GPUTreeLearner(config, false);
+  }
+  if (learner_type == "voting") {
+    Log::Warning("voting-parallel on the device learner runs as data-parallel (full histogram all-reduce)");
+    return new GPUTreeLearner(config, true);
+  }
+  Log::Fatal("Unknown tree learner type %s", learner_type.c_str());
+  return nullptr;
+}
+
+GPUTreeLearner::GPUTreeLearner(const Config* config, bool data_parallel)
+    : SerialTreeLearner(config), data_parallel_(data_parallel) {}
+
+GPUTreeLearner::~GPUTreeLearner() { FreeAll(); }
+
+template <typename T>
+T* GPUTreeLearner::Alloc(size_t n) {
+  void* p = nullptr;
+  HIPCHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
+  allocs_.push_back(p);
+  return static_cast<T*>(p);
+}
+
+void GPUTreeLearner::FreeAll() {
+  for (void* p : allocs_) (void)hipFree(p);
+  allocs_.clear();
+  if (h_mask_) (void)hipHostFree(h_mask_);
+  if (h_rec_) (void)hipHostFree(h_rec_);
+  if (h_step_) (void)hipHostFree(h_step_);
+  if (h_root_) (void)hipHostFree(h_root_);
+  h_mask_ = nullptr;
+  h_rec_ = nullptr;
+  h_step_ = nullptr;
+  h_root_ = nullptr;
+  if (stream_) (void)hipStreamDestroy(stream_);
+  stream_ = nullptr;
+  d_score_ = nullptr;
+  d_grad_ = d_hess_ = nullptr;
+  d_label_ = d_weights_ = d_label_weight_ = nullptr;
+  uploaded_label_src_ = uploaded_weight_src_ = uploaded_lw_src_ = nullptr;
+  d_tree_i32_ = nullptr;
+  d_tree_u32_ = nullptr;
+  d_tree_i8_ = nullptr;
+  d_tree_f64_ = nullptr;
+  tree_cap_ = cat_cap_ = 0;
+}
+
+void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
+  SerialTreeLearner::Init(train_data, is_constant_hessian);
+  if (config_->num_leaves > dev::kMaxLeaves) {
+    Log::Fatal("device learner supports num_leaves <= %d", dev::kMaxLeaves);
+  }
+  device_id_ = PickDevice(config_);
+  HIPCHECK(hipSetDevice(device_id_));
+  int cus = 0;
+  HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
+  dev::SetNumCUs(cus);
+  HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  UploadData();
+  global_count_.assign(config_->num_leaves, 0);
+  Log::Info("MI355X learner on device %d (%d CUs): %d rows, %d groups, %d histogram bins, %s bins, %d hist tiles",
+            device_id_, cus, num_data_, num_groups_, total_bins_, args_.bin_bytes == 1 ? "8-bit" : "16-bit",
+            args_.hist_tiles);
+}
+
+void GPUTreeLearner::UploadData() {
+  num_groups_ = data_->num_groups();
+  total_bins_ = static_cast<int>(data_->num_total_bin());
+  int max_group_bins = 0;
+  for (int g = 0; g < num_groups_; ++g) max_group_bins = std::max(max_group_bins, data_->group(g).num_total_bin);
+  if (max_group_bins > 65536) Log::Fatal("device learner: a feature group has more than 65536 bins");
+  const int bin_bytes = max_group_bins <= 256 ? 1 : 2;
+  const int gpw = 4 / bin_bytes;
+  const int wpr = std::max(1, (num_groups_ + gpw - 1) / gpw);
+  const size_t row_bytes = static_cast<size_t>(wpr) * 4;
+  // row-major bin matrix (the dataset stores columns)
+  std::vector<uint8_t> host(static_cast<size_t>(num_data_) * row_bytes, 0);
+#pragma omp parallel for schedule(static)
+  for (data_size_t r = 0; r < num_data_; ++r) {
+    uint8_t* row = host.data() + static_cast<size_t>(r) * row_bytes;
+    for (int g = 0; g < num_groups_; ++g) {
+      const uint32_t v = data_->group(g).Get(r);
+      if (bin_bytes == 1) row[g] = static_cast<uint8_t>(v);
+      else reinterpret_cast<uint16_t*>(row)[g] = static_cast<uint16_t>(v);
+    }
+  }
+  d_bins_ = Alloc<uint8_t>(host.size());
+  HIPCHECK(hipMemcpy(d_bins_, host.data(), host.size(), hipMemcpyHostToDevice));
+  std::vector<uint8_t>().swap(host);
+  // features
+  std::vector<dev::Feature> feats(num_features_);
+  for (int f = 0; f < num_features_; ++f) {
+    const BinMapper* m = data_->FeatureBinMapper(f);
+    const int g = data_->Feature2Group(f), sub = data_->Feature2SubFeature(f);
+    dev::Feature& F = feats[f];
+    F.group = g;
+    F.hist_offset = static_cast<int32_t>(data_->FeatureHistOffset(f));
+    F.num_bin = m->num_bin();
+    F.offset = m->GetMostFreqBin() == 0 ? 1 : 0;
+    F.default_bin = static_cast<int32_t>(m->GetDefaultBin());
+    F.mfb = static_cast<int32_t>(m->GetMostFreqBin());
+    F.missing_type = m->missing_type() == MissingType::None ? 0 : (m->missing_type() == MissingType::Zero ? 1 : 2);
+    F.is_cat = m->bin_type() == BinType::Categorical ? 1 : 0;
+    F.sub_lo = static_cast<int32_t>(data_->group(g).bin_offsets[sub]);
+    F.sub_hi = static_cast<int32_t>(data_->group(g).bin_offsets[sub + 1]);
+    F.real_index = data_->RealFeatureIndex(f);
+    F.monotone = meta_[f].monotone_type;
+    F.penalty = meta_[f].penalty;
+  }
+  d_feat_ = Alloc<dev::Feature>(num_features_);
+  HIPCHECK(hipMemcpy(d_feat_, feats.data(), sizeof(dev::Feature) * num_features_, hipMemcpyHostToDevice));
+  std::vector<int32_t> goff(std::max(1, num_groups_), 0);
+  for (int g = 0; g < num_groups_; ++g) goff[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
+  d_group_off_ = Alloc<int32_t>(goff.size());
+  HIPCHECK(hipMemcpy(d_group_off_, goff.data(), sizeof(int32_t) * goff.size(), hipMemcpyHostToDevice));
+  // histogram column tiles: LDS per block <= 64 KiB (2 blocks / CU), else <= 128 KiB
+  auto tile_bins_for = [&](int tw) {
+    int mx = 0;
+    for (int w0 = 0; w0 < wpr; w0 += tw) {
+      const int g0 = w0 * gpw, g1 = std::min(num_groups_, (w0 + tw) * gpw);
+      if (g0 >= num_groups_) break;
+      const int lo = goff[g0], hi = g1 < num_groups_ ? goff[g1] : total_bins_;
+      mx = std::max(mx, hi - lo);
+    }
+    return mx;
+  };
+  int tile_words = 0;
+  for (int limit : {8192, 16384}) {
+    for (int tw = std::min(wpr, dev::kHistBlockThreads); tw >= 1; --tw) {
+      if (tile_bins_for(tw) <= limit) {
+        tile_words = tw;
+        break;
+      }
+    }
+    if (tile_words > 0) break;
+  }
+  if (tile_words == 0) Log::Fatal("device learner: feature groups too wide for LDS histograms; reduce max_bin");
+  const int n_leaves = config_->num_leaves;
+  d_tree_mask_ = Alloc<int8_t>(num_features_);
+  d_gh_ = Alloc<dev::GH>(num_data_);
+  d_idx_ = Alloc<int32_t>(num_data_);
+  d_tmp_ = Alloc<int32_t>(num_data_);
+  d_bag_ = Alloc<int32_t>(num_data_);
+  d_oob_ = Alloc<int32_t>(num_data_);
+  d_leaves_ = Alloc<dev::Leaf>(n_leaves);
+  d_step_ = Alloc<dev::Step>(1);
+  d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
+  d_best_ = Alloc<DeviceSplit>(n_leaves);
+  d_hist_ = Alloc<float>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
+  d_scratch_ = Alloc<float>(2 * static_cast<size_t>(total_bins_));
+  d_blk_ = Alloc<int32_t>(dev::kMaxPartBlocks);
+  d_root_ = Alloc<double>(4);
+  d_leaf_values_ = Alloc<double>(n_leaves);
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_mask_), std::max(1, num_features_), hipHostMallocDefault));
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_rec_), sizeof(dev::SplitRecord) * std::max(1, n_leaves - 1),
+                         hipHostMallocDefault));
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_step_), sizeof(dev::Step), hipHostMallocDefault));
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_root_), sizeof(double) * 4, hipHostMallocDefault));
+
+  dev::KArgs& a = args_;
+  a.p.sp = params_;
+  a.p.num_leaves = n_leaves;
+  a.p.max_depth = config_->max_depth;
+  a.p.num_features = num_features_;
+  a.p.num_groups = num_groups_;
+  a.p.row_stride = static_cast<int32_t>(row_bytes);
+  a.p.total_bins = total_bins_;
+  a.p.monotone_penalty = config_->monotone_penalty;
+  a.p.data_parallel = data_parallel_ ? 1 : 0;
+  a.bins = d_bins_;
+  a.feat = d_feat_;
+  a.group_off = d_group_off_;
+  a.tree_mask = d_tree_mask_;
+  a.gh = d_gh_;
+  a.idx = d_idx_;
+  a.tmp = d_tmp_;
+  a.leaves = d_leaves_;
+  a.st = d_step_;
+  a.rec = d_rec_;
+  a.best = d_best_;
+  a.hist = d_hist_;
+  a.scratch = d_scratch_;
+  a.blk = d_blk_;
+  a.root = d_root_;
+  a.num_rows = num_data_;
+  a.root_identity = 1;
+  a.bin_bytes = bin_bytes;
+  a.words_per_row = wpr;
+  a.tile_words = tile_words;
+  a.hist_tiles = (wpr + tile_words - 1) / tile_words;
+  a.tile_bins = tile_bins_for(tile_words);
+  a.range_begin = 0;
+}
+
+void GPUTreeLearner::ResetTrainingData(const Dataset* train_data, bool is_constant_hessian) {
+  SerialTreeLearner::ResetTrainingData(train_data, is_constant_hessian);
+  HIPCHECK(hipSetDevice(device_id_));
+  // rebuild the device data for the new rows (bin mappers are aligned)
+  for (void* p : allocs_) (void)hipFree(p);
+  allocs_.clear();
+  d_score_ = nullptr;
+  d_grad_ = d_hess_ = nullptr;
+  d_label_ = d_weights_ = d_label_weight_ = nullptr;
+  uploaded_label_src_ = uploaded_weight_src_ = uploaded_lw_src_ = nullptr;
+  d_tree_i32_ = nullptr;
+  d_tree_u32_ = nullptr;
+  d_tree_i8_ = nullptr;
+  d_tree_f64_ = nullptr;
+  tree_cap_ = cat_cap_ = 0;
+  if (h_mask_) (void)hipHostFree(h_mask_);
+  if (h_rec_) (void)hipHostFree(h_rec_);
+  if (h_step_) (void)hipHostFree(h_step_);
+  if (h_root_) (void)hipHostFree(h_root_);
+  h_mask_ = nullptr;
+  h_rec_ = nullptr;
+  h_step_ = nullptr;
+  h_root_ = nullptr;
+  UploadData();
+  oob_cnt_ = 0;
+}
+
+void GPUTreeLearner::ResetConfig(const Config* config) {
+  const int old_leaves = config_->num_leaves;
+  SerialTreeLearner::ResetConfig(config);
+  args_.p.sp = params_;
+  args_.p.max_depth = config_->max_depth;
+  args_.p.monotone_penalty = config_->monotone_penalty;
+  if (config_->num_leaves != old_leaves) {
+    if (config_->num_leaves > dev::kMaxLeaves) Log::Fatal("device learner supports num_leaves <= %d", dev::kMaxLeaves);
+    HIPCHECK(hipSetDevice(device_id_));
+    const int n_leaves = config_->num_leaves;
+    d_leaves_ = Alloc<dev::Leaf>(n_leaves);
+    d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
+    d_best_ = Alloc<DeviceSplit>(n_leaves);
+    d_hist_ = Alloc<float>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
+    d_leaf_values_ = Alloc<double>(n_leaves);
+    if (h_rec_) (void)hipHostFree(h_rec_);
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_rec_), sizeof(dev::SplitRecord) * std::max(1, n_leaves - 1),
+                           hipHostMallocDefault));
+    args_.p.num_leaves = n_leaves;
+    args_.leaves = d_leaves_;
+    args_.rec = d_rec_;
+    args_.best = d_best_;
+    args_.hist = d_hist_;
+    global_count_.assign(n_leaves, 0);
+  }
+  // monotone / penalty metadata may have changed
+  std::vector<dev::Feature> feats(num_features_);
+  HIPCHECK(hipMemcpy(feats.data(), d_feat_, sizeof(dev::Feature) * num_features_, hipMemcpyDeviceToHost));
+  for (int f = 0; f < num_features_; ++f) {
+    feats[f].monotone = meta_[f].monotone_type;
+    feats[f].penalty = meta_[f].penalty;
+  }
+  HIPCHECK(hipMemcpy(d_feat_, feats.data(), sizeof(dev::Feature) * num_features_, hipMemcpyHostToDevice));
+}
+
+void GPUTreeLearner::DecideMode() {
+  bool dm = true;
+  const char* force = std::getenv("LGBM_AMD_HOST_ASSIST");
+  if (force != nullptr && force[0] == '1') dm = false;
+  for (int f = 0; f < num_features_ && dm; ++f) {
+    if (data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) dm = false;
+  }
+  if (has_forced_split_ || !config_->interaction_constraints_vector.empty() || config_->extra_trees ||
+      config_->feature_fraction_bynode < 1.0 || config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
+      !config_->cegb_penalty_feature_lazy.empty() || !config_->cegb_penalty_feature_coupled.empty()) {
+    dm = false;
+  }
+  if (dm != device_mode_) {
+    Log::Debug("device learner: %s growth", dm ? "device-resident" : "host-assisted");
+  }
+  device_mode_ = dm;
+}
+
+void GPUTreeLearner::SetBaggingData(const Dataset* subset, const data_size_t* used_indices, data_size_t n) {
+  SerialTreeLearner::SetBaggingData(subset, used_indices, n);
+  HIPCHECK(hipSetDevice(device_id_));
+  oob_cnt_ = 0;
+  if (use_bag_) {
+    HIPCHECK(hipMemcpyAsync(d_bag_, used_indices, sizeof(int32_t) * n, hipMemcpyHostToDevice, stream_));
+    // GBDT keeps the out-of-bag rows after the in-bag ones (bag_data_indices_ has num_data entries)
+    oob_cnt_ = num_data_ - n;
+    if (oob_cnt_ > 0) {
+      HIPCHECK(hipMemcpyAsync(d_oob_, used_indices + n, sizeof(int32_t) * oob_cnt_, hipMemcpyHostToDevice, stream_));
+    }
+    HIPCHECK(hipStreamSynchronize(stream_));
+  }
+}
+
+// ---------------------------------------------------------------- tree growth
+Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
+  common::ScopedTimer timer("GPUTreeLearner::Train");
+  HIPCHECK(hipSetDevice(device_id_));
+  dev::PackGH(gradients, hessians, d_gh_, num_data_, stream_);
+  host_partition_fresh_ = false;
+  DecideMode();
+  if (device_mode_) return TrainDeviceMode();
+  return SerialTreeLearner::Train(gradients, hessians);
+}
+
+void GPUTreeLearner::AllreduceRoot() {
+  if (!data_parallel_ || Network::num_machines() <= 1) return;
+  DeviceComm* dc = Network::device_comm();
+  if (dc != nullptr) {
+    dc->AllreduceSumF64(d_root_, 3, stream_);
+    return;
+  }
+  HIPCHECK(hipMemcpyAsync(h_root_, d_root_, sizeof(double) * 3, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  auto v = Network::GlobalSum(std::vector<double>(h_root_, h_root_ + 3));
+  std::copy(v.begin(), v.end(), h_root_);
+  HIPCHECK(hipMemcpyAsync(d_root_, h_root_, sizeof(double) * 3, hipMemcpyHostToDevice, stream_));
+}
+
+void GPUTreeLearner::AllreduceScratch() {
+  if (!data_parallel_ || Network::num_machines() <= 1) return;
+  DeviceComm* dc = Network::device_comm();
+  const size_t n = 2 * static_cast<size_t>(total_bins_);
+  if (dc != nullptr) {
+    dc->AllreduceSumF32(d_scratch_, n, stream_);
+    return;
+  }
+  std::vector<float> h(n);
+  HIPCHECK(hipMemcpyAsync(h.data(), d_scratch_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  auto v = Network::GlobalSum(h);
+  HIPCHECK(hipMemcpyAsync(d_scratch_, v.data(), sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+Tree* GPUTreeLearner::TrainDeviceMode() {
+  col_sampler_.ResetByTree();
+  const auto& mask = col_sampler_.is_feature_used_bytree();
+  for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
+  HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
+  dev::KArgs a = args_;
+  if (use_bag_) {
+    HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * bag_cnt_, hipMemcpyDeviceToDevice, stream_));
+    a.num_rows = bag_cnt_;
+    a.root_identity = 0;
+  } else {
+    a.num_rows = num_data_;
+    a.root_identity = 1;
+  }
+  root_rows_ = a.num_rows;
+  const size_t scratch_bytes = sizeof(float) * 2 * static_cast<size_t>(total_bins_);
+  dev::TreeBegin(a, stream_);
+  dev::RootSum(a, stream_);
+  AllreduceRoot();
+  HIPCHECK(hipMemsetAsync(d_scratch_, 0, scratch_bytes, stream_));
+  dev::HistRoot(a, stream_);
+  AllreduceScratch();
+  dev::FindRoot(a, stream_);
+  for (int s = 0; s < config_->num_leaves - 1; ++s) {
+    dev::SelectSplit(a, stream_);
+    dev::PartitionCount(a, stream_);
+    dev::PartitionScatter(a, stream_);
+    HIPCHECK(hipMemsetAsync(d_scratch_, 0, scratch_bytes, stream_));
+    dev::HistStep(a, stream_);
+    AllreduceScratch();
+    dev::FindStep(a, stream_);
+  }
+  HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
+                          hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  const int num_splits = h_step_->step;
+  const bool track = !config_->interaction_constraints_vector.empty();
+  std::unique_ptr<Tree> tree(new Tree(config_->num_leaves, track));
+  for (int s = 0; s < num_splits; ++s) {
+    const dev::SplitRecord& r = h_rec_[s];
+    SplitInfo si;
+    si.FromDevice(r.split);
+    const int inner = si.inner_feature;
+    const BinMapper* m = data_->FeatureBinMapper(inner);
+    const float gain = static_cast<float>(si.gain + config_->min_gain_to_split);
+    tree->Split(r.leaf, inner, si.feature, si.threshold, data_->RealThreshold(inner, si.threshold), si.left_output,
+                si.right_output, r.left_count, r.right_count, si.left_sum_hessian, si.right_sum_hessian, gain,
+                m->missing_type(), si.default_left);
+  }
+  if (num_splits == 0) {
+    Log::Warning("No further splits with positive gain, best gain: %f", -std::numeric_limits<double>::infinity());
+  }
+  Log::Debug("Trained a tree with leaves = %d and max_depth = %d", tree->num_leaves(), tree->max_depth());
+  return tree.release();
+}
+
+// ---------------------------------------------------------------- host-assisted mode
+void GPUTreeLearner::BeforeTrain() {
+  col_sampler_.ResetByTree();
+  dev::KArgs a = args_;
+  if (use_bag_) {
+    HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * bag_cnt_, hipMemcpyDeviceToDevice, stream_));
+    a.num_rows = bag_cnt_;
+  } else {
+    dev::Iota(d_idx_, num_data_, stream_);
+    a.num_rows = num_data_;
+  }
+  a.root_identity = 0;
+  root_rows_ = a.num_rows;
+  dev::TreeBegin(a, stream_);
+  dev::RootSum(a, stream_);
+  HIPCHECK(hipMemcpyAsync(h_root_, d_root_, sizeof(double) * 3, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  double sg = h_root_[0], sh = h_root_[1], cnt = h_root_[2];
+  if (data_parallel_ && Network::num_machines() > 1) {
+    auto v = Network::GlobalSum(std::vector<double>{sg, sh, cnt});
+    sg = v[0];
+    sh = v[1];
+    cnt = v[2];
+  }
+  std::fill(leaf_begin_.begin(), leaf_begin_.end(), 0);
+  std::fill(leaf_count_.begin(), leaf_count_.end(), 0);
+  leaf_count_[0] = a.num_rows;
+  global_count_.assign(config_->num_leaves, 0);
+  global_count_[0] = static_cast<data_size_t>(cnt);
+  constraints_.Init(config_->num_leaves);
+  for (auto& s : best_split_per_leaf_) s.Reset();
+  smaller_ = LeafState{0, static_cast<data_size_t>(cnt), sg, sh, 0.0};
+  larger_ = LeafState{};
+  larger_.leaf = -1;
+}
+
+data_size_t GPUTreeLearner::GetGlobalDataCountInLeaf(int leaf) const {
+  if (leaf < 0) return 0;
+  return data_parallel_ ? global_count_[leaf] : leaf_count_[leaf];
+}
+
+void GPUTreeLearner::BuildRangeHistogram(int leaf, int slot) {
+  dev::KArgs a = args_;
+  a.range_begin = leaf_begin_[leaf];
+  a.num_rows = leaf_count_[leaf];
+  const size_t n = 2 * static_cast<size_t>(total_bins_);
+  HIPCHECK(hipMemsetAsync(d_scratch_, 0, sizeof(float) * n, stream_));
+  if (a.num_rows > 0) dev::HistRange(a, stream_);
+  std::vector<float> h(n);
+  HIPCHECK(hipMemcpyAsync(h.data(), d_scratch_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  std::vector<hist_t>& dst = hist_pool_[slot];
+  for (size_t i = 0; i < n; ++i) dst[i] = h[i];
+  if (data_parallel_ && Network::num_machines() > 1) dst = Network::GlobalSum(dst);
+}
+
+void GPUTreeLearner::ConstructHistograms(const std::vector<int8_t>&, bool use_subtract) {
+  common::ScopedTimer timer("GPUTreeLearner::ConstructHistograms");
+  BuildRangeHistogram(smaller_.leaf, smaller_slot_);
+  if (larger_slot_ >= 0 && !use_subtract) BuildRangeHistogram(larger_.leaf, larger_slot_);
+}
+
+data_size_t GPUTreeLearner::PartitionLeaf(int leaf, int inner, const SplitInfo& s, int new_leaf) {
+  const data_size_t begin = leaf_begin_[leaf];
+  const data_size_t cnt = leaf_count_[leaf];
+  dev::Step& st = *h_step_;
+  std::memset(&st, 0, sizeof(st));
+  st.leaf = leaf;
+  st.new_leaf = new_leaf;
+  st.part_begin = begin;
+  st.part_count = cnt;
+  int rpb = 0;
+  st.num_blocks = PartBlocks(cnt, &rpb);
+  st.rows_per_block = rpb;
+  SplitInfo si = s;
+  si.inner_feature = inner;
+  si.ToDevice(&st.split, data_->FeatureBinMapper(inner)->bin_type() == BinType::Categorical);
+  HIPCHECK(hipMemcpyAsync(d_step_, h_step_, sizeof(dev::Step), hipMemcpyHostToDevice, stream_));
+  dev::PartitionCount(args_, stream_);
+  dev::PartitionScatter(args_, stream_);
+  if (cnt > 0) {
+    HIPCHECK(hipMemcpyAsync(d_idx_ + begin, d_tmp_ + begin, sizeof(int32_t) * cnt, hipMemcpyDeviceToDevice, stream_));
+  }
+  HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  const data_size_t left = h_step_->total_left;
+  leaf_count_[leaf] = left;
+  leaf_begin_[new_leaf] = begin + left;
+  leaf_count_[new_leaf] = cnt - left;
+  return left;
+}
+
+void GPUTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) {
+  if (!data_parallel_) {
+    SplitInner(tree, best_leaf, left_leaf, right_leaf, true);
+    return;
+  }
+  SplitInner(tree, best_leaf, left_leaf, right_leaf, false);
+  const SplitInfo& s = best_split_per_leaf_[best_leaf];
+  global_count_[*left_leaf] = s.left_count;
+  global_count_[*right_leaf] = s.right_count;
+}
+
+// ---------------------------------------------------------------- partition mirror
+void GPUTreeLearner::DownloadPartitionToHost() const {
+  if (host_partition_fresh_) return;
+  auto* self = const_cast<GPUTreeLearner*>(this);
+  const int L = config_->num_leaves;
+  std::vector<dev::Leaf> leaves(L);
+  HIPCHECK(hipMemcpyAsync(leaves.data(), d_leaves_, sizeof(dev::Leaf) * L, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipMemcpyAsync(self->indices_.data(), d_idx_, sizeof(int32_t) * root_rows_, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  for (int l = 0; l < L; ++l) {
+    self->leaf_begin_[l] = leaves[l].begin;
+    self->leaf_count_[l] = leaves[l].count;
+  }
+  host_partition_fresh_ = true;
+}
+
+void GPUTreeLearner::AddPredictionToScore(const Tree* tree, double* out_score) const {
+  DownloadPartitionToHost();
+  SerialTreeLearner::AddPredictionToScore(tree, out_score);
+}
+
+void GPUTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
+                                     const std::function<double(const label_t*, int)>& residual,
+                                     data_size_t total_num_data, const data_size_t* bag_indices,
+                                     data_size_t bag_cnt) const {
+  if (obj == nullptr || !obj->IsRenewTreeOutput()) return;
+  DownloadPartitionToHost();
+  SerialTreeLearner::RenewTreeOutput(tree, obj, residual, total_num_data, bag_indices, bag_cnt);
+}
+
+// ---------------------------------------------------------------- scores & gradients
+void GPUTreeLearner::InitScores(int ntpi, const double* init_score) {
+  HIPCHECK(hipSetDevice(device_id_));
+  num_tree_per_iteration_ = ntpi;
+  const size_t n = static_cast<size_t>(num_data_) * ntpi;
+  if (d_score_ == nullptr) {
+    d_score_ = Alloc<double>(n);
+    d_grad_ = Alloc<float>(n);
+    d_hess_ = Alloc<float>(n);
+  }
+  if (init_score != nullptr) {
+    HIPCHECK(hipMemcpy(d_score_, init_score, sizeof(double) * n, hipMemcpyHostToDevice));
+  } else {
+    HIPCHECK(hipMemset(d_score_, 0, sizeof(double) * n));
+  }
+}
+
+void GPUTreeLearner::SyncScoreToHost(double* host, int k) {
+  HIPCHECK(hipMemcpyAsync(host, d_score_ + static_cast<size_t>(k) * num_data_, sizeof(double) * num_data_,
+                          hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+void GPUTreeLearner::SyncScoreFromHost(const double* host, int k) {
+  HIPCHECK(hipMemcpyAsync(d_score_ + static_cast<size_t>(k) * num_data_, host, sizeof(double) * num_data_,
+                          hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+void GPUTreeLearner::AddConstToScore(double v, int k) {
+  dev::AddConst(d_score_ + static_cast<size_t>(k) * num_data_, num_data_, v, stream_);
+}
+
+void GPUTreeLearner::MultiplyScore(double v, int k) {
+  dev::MulConst(d_score_ + static_cast<size_t>(k) * num_data_, num_data_, v, stream_);
+}
+
+void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
+  const int nl = tree->num_leaves();
+  double* score = d_score_ + static_cast<size_t>(k) * num_data_;
+  if (nl <= 1) {
+    AddConstToScore(tree->LeafOutput(0), k);
+    return;
+  }
+  std::vector<double> vals(nl);
+  for (int i = 0; i < nl; ++i) vals[i] = tree->LeafOutput(i);
+  HIPCHECK(hipMemcpyAsync(d_leaf_values_, vals.data(), sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
+  dev::KArgs a = args_;
+  a.num_rows = root_rows_;
+  dev::AddLeafScore(a, d_leaf_values_, nl, score, stream_);
+  if (oob_cnt_ > 0) {
+    in_trained_update_ = true;  // AddTreeToScore restricts the traversal to out-of-bag rows
+    AddTreeToScore(tree, k);
+    in_trained_update_ = false;
+  }
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
+  // NOTE: called from AddTrainedTreeToScore for out-of-bag rows only (oob_cnt_ > 0 and the
+  // tree just trained), otherwise for every row
+  const int nl = tree->num_leaves();
+  double* score = d_score_ + static_cast<size_t>(k) * num_data_;
+  if (nl <= 1) {
+    AddConstToScore(tree->LeafOutput(0), k);
+    return;
+  }
+  const int ni = nl - 1;
+  const auto& cb = tree->cat_boundaries_inner();
+  const auto& ct = tree->cat_threshold_inner();
+  const size_t need_i32 = 3 * static_cast<size_t>(ni) + cb.size() + 1;
+  const size_t need_u32 = static_cast<size_t>(ni) + ct.size() + 1;
+  if (tree_cap_ < need_i32 || cat_cap_ < need_u32) {
+    tree_cap_ = std::max(need_i32, 3 * static_cast<size_t>(config_->num_leaves) + 64);
+    cat_cap_ = std::max(need_u32, static_cast<size_t>(config_->num_leaves) + 1024);
+    d_tree_i32_ = Alloc<int32_t>(tree_cap_);
+    d_tree_u32_ = Alloc<uint32_t>(cat_cap_);
+    d_tree_i8_ = Alloc<int8_t>(std::max(cat_cap_, tree_cap_));
+    d_tree_f64_ = Alloc<double>(std::max(cat_cap_, tree_cap_));
+  }
+  std::vector<int32_t> i32(need_i32, 0);
+  std::vector<uint32_t> u32(need_u32, 0);
+  std::vector<int8_t> i8(ni);
+  std::vector<double> f64(nl);
+  for (int j = 0; j < ni; ++j) {
+    i32[j] = tree->split_feature_inner(j);
+    i32[ni + j] = tree->left_child(j);
+    i32[2 * ni + j] = tree->right_child(j);
+    u32[j] = tree->threshold_in_bin(j);
+    i8[j] = tree->decision_type(j);
+  }
+  for (size_t j = 0; j < cb.size(); ++j) i32[3 * ni + j] = cb[j];
+  for (size_t j = 0; j < ct.size(); ++j) u32[ni + j] = ct[j];
+  for (int j = 0; j < nl; ++j) f64[j] = tree->LeafOutput(j);
+  HIPCHECK(hipMemcpyAsync(d_tree_i32_, i32.data(), sizeof(int32_t) * i32.size(), hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_tree_u32_, u32.data(), sizeof(uint32_t) * u32.size(), hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_tree_i8_, i8.data(), ni, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_tree_f64_, f64.data(), sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
+  dev::DevTree t;
+  t.num_leaves = nl;
+  t.split_feature_inner = d_tree_i32_;
+  t.left_child = d_tree_i32_ + ni;
+  t.right_child = d_tree_i32_ + 2 * ni;
+  t.cat_boundaries_inner = d_tree_i32_ + 3 * ni;
+  t.threshold_in_bin = d_tree_u32_;
+  t.cat_threshold_inner = d_tree_u32_ + ni;
+  t.decision_type = d_tree_i8_;
+  t.leaf_value = d_tree_f64_;
+  const bool oob_only = oob_cnt_ > 0 && in_trained_update_;
+  if (oob_only) {
+    dev::AddTreeScore(args_, t, d_oob_, oob_cnt_, score, stream_);
+  } else {
+    dev::AddTreeScore(args_, t, nullptr, num_data_, score, stream_);
+  }
+  // host vectors must outlive the async copies
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
+  if (spec.kind == DeviceGradKind::None || spec.kind == DeviceGradKind::MulticlassOVA) return false;
+  if (spec.kind != DeviceGradKind::MulticlassSoftmax && ntpi != 1) return false;
+  if (spec.label == nullptr) return false;
+  const size_t n = static_cast<size_t>(num_data_);
+  if (uploaded_label_src_ != spec.label) {
+    if (d_label_ == nullptr) d_label_ = Alloc<float>(n);
+    HIPCHECK(hipMemcpy(d_label_, spec.label, sizeof(float) * n, hipMemcpyHostToDevice));
+    uploaded_label_src_ = spec.label;
+  }
+  if (spec.weights != nullptr && uploaded_weight_src_ != spec.weights) {
+    if (d_weights_ == nullptr) d_weights_ = Alloc<float>(n);
+    HIPCHECK(hipMemcpy(d_weights_, spec.weights, sizeof(float) * n, hipMemcpyHostToDevice));
+    uploaded_weight_src_ = spec.weights;
+  }
+  if (spec.label_weight_arr != nullptr && uploaded_lw_src_ != spec.label_weight_arr) {
+    if (d_label_weight_ == nullptr) d_label_weight_ = Alloc<float>(n);
+    HIPCHECK(hipMemcpy(d_label_weight_, spec.label_weight_arr, sizeof(float) * n, hipMemcpyHostToDevice));
+    uploaded_lw_src_ = spec.label_weight_arr;
+  }
+  dev::GradArgs g;
+  g.kind = static_cast<int32_t>(spec.kind);
+  g.num_class = spec.kind == DeviceGradKind::MulticlassSoftmax ? ntpi : 1;
+  g.num_data = num_data_;
+  g.p0 = spec.p0;
+  g.p1 = spec.p1;
+  g.p2 = spec.p2;
+  g.lw0 = spec.label_weight[0];
+  g.lw1 = spec.label_weight[1];
+  g.label = d_label_;
+  g.weights = spec.weights != nullptr ? d_weights_ : nullptr;
+  g.label_weight = spec.label_weight_arr != nullptr ? d_label_weight_ : nullptr;
+  g.score = d_score_;
+  g.grad = d_grad_;
+  g.hess = d_hess_;
+  dev::Gradients(g, stream_);
+  return true;
+}
+
+void GPUTreeLearner::UploadGradients(const score_t* g, const score_t* h, int64_t n) {
+  HIPCHECK(hipMemcpyAsync(d_grad_, g, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_hess_, h, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+void GPUTreeLearner::DownloadGradients(score_t* g, score_t* h, int64_t n) {
+  HIPCHECK(hipMemcpyAsync(g, d_grad_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipMemcpyAsync(h, d_hess_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+void GPUTreeLearner::Synchronize() { HIPCHECK(hipStreamSynchronize(stream_)); }
+
+}  // namespace lgbm_amd

@@ -1,0 +1,140 @@
+// MI355X tree learner: host orchestration of the HIP kernels in src/device/.
+//
+// Two growth modes share the same HBM state (row-major bin matrix, packed gradients,
+// partition indices, histogram pool):
+//  * device-resident (default): the whole tree -- split selection included -- runs as
+//    a fixed kernel sequence on one stream (optionally replayed from a hipGraph); the
+//    host reads the split records back once per tree.
+//  * host-assisted: the SerialTreeLearner loop runs on the host and only histogram
+//    construction and row partitioning are offloaded.  Used for features the device
+//    split scan does not implement (categorical splits, forced splits, interaction
+//    constraints, extra_trees, per-node column sampling, CEGB).
+// The reference's GPU learner (src/treelearner/gpu_tree_learner.cpp, OpenCL) offloads
+// only the histogram build; this learner keeps the training scores, gradients and the
+// data partition resident on the device across iterations.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../device/kernels.h"
+#include "lgbm_amd/device_learner.h"
+#include "serial_tree_learner.h"
+
+namespace lgbm_amd {
+
+class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
+ public:
+  GPUTreeLearner(const Config* config, bool data_parallel);
+  ~GPUTreeLearner() override;
+
+  // TreeLearner
+  void Init(const Dataset* train_data, bool is_constant_hessian) override;
+  void ResetTrainingData(const Dataset* train_data, bool is_constant_hessian) override;
+  void ResetConfig(const Config* config) override;
+  Tree* Train(const score_t* gradients, const score_t* hessians) override;
+  void SetBaggingData(const Dataset* subset, const data_size_t* used_indices, data_size_t num_data) override;
+  void AddPredictionToScore(const Tree* tree, double* out_score) const override;
+  void RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
+                       const std::function<double(const label_t*, int)>& residual_getter, data_size_t total_num_data,
+                       const data_size_t* bag_indices, data_size_t bag_cnt) const override;
+  bool IsDevice() const override { return true; }
+
+  // DeviceTreeLearner
+  void InitScores(int num_tree_per_iteration, const double* init_score) override;
+  void SyncScoreToHost(double* host, int tree_id) override;
+  void SyncScoreFromHost(const double* host, int tree_id) override;
+  void AddConstToScore(double v, int tree_id) override;
+  void MultiplyScore(double v, int tree_id) override;
+  void AddTrainedTreeToScore(const Tree* tree, int tree_id) override;
+  void AddTreeToScore(const Tree* tree, int tree_id) override;
+  bool ComputeGradients(const DeviceGradSpec& spec, int num_tree_per_iteration) override;
+  void UploadGradients(const score_t* g, const score_t* h, int64_t n) override;
+  void DownloadGradients(score_t* g, score_t* h, int64_t n) override;
+  score_t* device_gradients() override { return d_grad_; }
+  score_t* device_hessians() override { return d_hess_; }
+  void Synchronize() override;
+
+  bool device_mode() const { return device_mode_; }
+
+ protected:
+  // host-assisted mode hooks
+  void BeforeTrain() override;
+  void ConstructHistograms(const std::vector<int8_t>& feature_used, bool use_subtract) override;
+  data_size_t PartitionLeaf(int leaf, int inner_feature, const SplitInfo& s, int new_leaf) override;
+  void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) override;
+  data_size_t GetGlobalDataCountInLeaf(int leaf) const override;
+
+ private:
+  void UploadData();
+  void FreeAll();
+  void DecideMode();
+  Tree* TrainDeviceMode();
+  void BuildRangeHistogram(int leaf, int slot);
+  void DownloadPartitionToHost() const;
+  void AllreduceScratch();
+  void AllreduceRoot();
+  template <typename T>
+  T* Alloc(size_t n);
+
+  bool data_parallel_ = false;
+  bool device_mode_ = true;
+  int device_id_ = 0;
+  hipStream_t stream_ = nullptr;
+  dev::KArgs args_{};
+  std::vector<void*> allocs_;
+  // device buffers
+  void* d_bins_ = nullptr;
+  dev::Feature* d_feat_ = nullptr;
+  int32_t* d_group_off_ = nullptr;
+  int8_t* d_tree_mask_ = nullptr;
+  dev::GH* d_gh_ = nullptr;
+  int32_t* d_idx_ = nullptr;
+  int32_t* d_tmp_ = nullptr;
+  int32_t* d_oob_ = nullptr;
+  int32_t* d_bag_ = nullptr;  // pristine in-bag rows (the partition permutes d_idx_)
+  dev::Leaf* d_leaves_ = nullptr;
+  dev::Step* d_step_ = nullptr;
+  dev::SplitRecord* d_rec_ = nullptr;
+  DeviceSplit* d_best_ = nullptr;
+  float* d_hist_ = nullptr;
+  float* d_scratch_ = nullptr;
+  int32_t* d_blk_ = nullptr;
+  double* d_root_ = nullptr;
+  double* d_score_ = nullptr;
+  float* d_grad_ = nullptr;
+  float* d_hess_ = nullptr;
+  double* d_leaf_values_ = nullptr;
+  float* d_label_ = nullptr;
+  float* d_weights_ = nullptr;
+  float* d_label_weight_ = nullptr;
+  const label_t* uploaded_label_src_ = nullptr;
+  const label_t* uploaded_weight_src_ = nullptr;
+  const label_t* uploaded_lw_src_ = nullptr;
+  // tree upload staging for traversal
+  int32_t* d_tree_i32_ = nullptr;
+  uint32_t* d_tree_u32_ = nullptr;
+  int8_t* d_tree_i8_ = nullptr;
+  double* d_tree_f64_ = nullptr;
+  size_t tree_cap_ = 0;
+  size_t cat_cap_ = 0;
+  // pinned host staging
+  int8_t* h_mask_ = nullptr;
+  dev::SplitRecord* h_rec_ = nullptr;
+  dev::Step* h_step_ = nullptr;
+  double* h_root_ = nullptr;
+  // sizes
+  int num_groups_ = 0;
+  int total_bins_ = 0;
+  int num_tree_per_iteration_ = 1;
+  data_size_t root_rows_ = 0;
+  data_size_t oob_cnt_ = 0;
+  std::vector<data_size_t> global_count_;
+  mutable bool host_partition_fresh_ = false;
+  bool in_trained_update_ = false;
+};
+
+}  // namespace lgbm_amd

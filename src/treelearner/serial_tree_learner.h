@@ -66,7 +66,7 @@ class SerialTreeLearner : public TreeLearner {
     *cnt = leaf_count_[leaf];
     return indices_.data() + leaf_begin_[leaf];
   }
-  data_size_t PartitionLeaf(int leaf, int inner_feature, const SplitInfo& s, int new_leaf);
+  virtual data_size_t PartitionLeaf(int leaf, int inner_feature, const SplitInfo& s, int new_leaf);
 
   virtual void BeforeTrain();
   virtual bool BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf);

@@ -1,0 +1,36 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device) and the gfx950 build")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+def _lib_path():
+    return os.path.join(ROOT, "lightgbmv1_amd", "lib", "lib_lightgbmv1_amd.so")
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _native_library():
+    """Build the native library once if it is missing (CPU container or GPU box)."""
+    if not os.path.isfile(_lib_path()):
+        import subprocess
+        subprocess.check_call(["make", "-j" + str(min(16, os.cpu_count() or 8))], cwd=ROOT)
+    yield
+
+
+@pytest.fixture(scope="session")
+def gpu_available():
+    import lightgbmv1_amd as lgb
+    n = lgb.device_count()
+    if n < 1:
+        # GPU tests must fail loudly when the device path is unavailable on a GPU box
+        raise RuntimeError("gpu test requested but no HIP device is visible to lib_lightgbmv1_amd")
+    return n
