@@ -61,6 +61,8 @@ class DeviceComm {
   virtual int size() const = 0;
   virtual void AllreduceSumF64(double* buf, size_t count, void* stream) = 0;
   virtual void AllreduceSumF32(float* buf, size_t count, void* stream) = 0;
+  virtual void AllreduceSumI64(long long* buf, size_t count, void* stream) = 0;
+  virtual void AllreduceMaxU32(uint32_t* buf, size_t count, void* stream) = 0;
   virtual void Allgather(const void* send, void* recv, size_t bytes_per_rank, void* stream) = 0;
   virtual void ReduceScatterSumF64(const double* send, double* recv, size_t recv_count, void* stream) = 0;
   virtual void Broadcast(void* buf, size_t bytes, int root, void* stream) = 0;

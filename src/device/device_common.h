@@ -1,0 +1,103 @@
+// Device-side helpers shared by the HIP translation units of src/device/ (hipcc only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+
+#include "kernels.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+int NumCUs();  // compute units of the current device (SetNumCUs)
+
+constexpr int kWave = 64;
+constexpr int kMinRowsPerHistBlock = 2048;
+constexpr int kPartThreads = 256;
+constexpr int kPartRowsPerThread = 8;
+constexpr int kPartTile = kPartThreads * kPartRowsPerThread;
+
+inline int GridFor(int64_t n) {
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8 * NumCUs())));
+}
+
+__device__ __forceinline__ int RoundIntD(double x) { return static_cast<int>(x + 0.5f); }
+
+// bin of storage column `group` for `row`, column-major copy (partition kernels)
+__device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int group) {
+  if (a.bin_bytes == 1) return a.bins_col[static_cast<int64_t>(group) * a.num_data + row];
+  return reinterpret_cast<const uint16_t*>(a.bins_col)[static_cast<int64_t>(group) * a.num_data + row];
+}
+
+// bin of storage column `group` for `row`, row-major matrix
+__device__ __forceinline__ uint32_t RowBin(const KArgs& a, int64_t row, int group) {
+  if (a.bin_bytes == 1) return static_cast<const uint8_t*>(a.bins)[row * (4 * a.words_per_row) + group];
+  return static_cast<const uint16_t*>(a.bins)[row * (2 * a.words_per_row) + group];
+}
+
+// group bin -> feature bin (Dataset::FeatureBin)
+__device__ __forceinline__ uint32_t FeatureBinOf(const Feature& f, uint32_t gb) {
+  if (gb < static_cast<uint32_t>(f.sub_lo) || gb >= static_cast<uint32_t>(f.sub_hi)) return f.mfb;
+  return gb - f.sub_lo + f.offset;
+}
+
+// split decision on a feature bin (DataPartition::Split / Tree::DecisionInner semantics)
+struct SplitRule {
+  int32_t threshold;
+  int32_t default_left;
+  int32_t is_cat;
+  int32_t missing_type;
+  int32_t default_bin;
+  int32_t max_bin;  // num_bin - 1
+};
+
+__device__ __forceinline__ bool GoesLeft(const SplitRule& r, const uint32_t* cat_bits, uint32_t bin) {
+  if (r.is_cat) {
+    return bin < 32u * kMaxCatWords && ((cat_bits[bin >> 5] >> (bin & 31u)) & 1u);
+  }
+  if ((r.missing_type == 1 && bin == static_cast<uint32_t>(r.default_bin)) ||
+      (r.missing_type == 2 && bin == static_cast<uint32_t>(r.max_bin))) {
+    return r.default_left != 0;
+  }
+  return bin <= static_cast<uint32_t>(r.threshold);
+}
+
+template <typename T>
+__device__ __forceinline__ T WaveSum(T v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// block-wide sum (every thread gets the result); sh needs blockDim/64 entries
+template <typename T>
+__device__ T BlockSum(T v, T* sh) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = WaveSum(v);
+  __syncthreads();
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  T r = 0;
+  for (int i = 0; i < nw; ++i) r += sh[i];
+  return r;
+}
+
+// SplitInfo ordering: larger gain first, then smaller real feature index (NaN = -inf)
+__device__ __forceinline__ bool SplitBetter(double ga, int fa, double gb, int fb) {
+  if (ga != ga) ga = -INFINITY;
+  if (gb != gb) gb = -INFINITY;
+  if (fa < 0) fa = 0x7fffffff;
+  if (fb < 0) fb = 0x7fffffff;
+  if (ga != gb) return ga > gb;
+  return fa < fb;
+}
+
+// histogram buffer being built at the current step (double-buffered: see HistBody)
+__device__ __forceinline__ long long* StepScratch(const KArgs& a, int parity) {
+  return a.scratch + static_cast<size_t>(parity & 1) * 2 * a.p.total_bins;
+}
+
+}  // namespace dev
+}  // namespace lgbm_amd

@@ -75,7 +75,16 @@ struct Step {
   int32_t rows_per_block;
   int32_t part_begin;  // range of the leaf being split, before the split
   int32_t part_count;
+  int32_t hist_packed;  // the step's histogram was built directly as packed (g|h) u64 per bin
+  int32_t pad2;
   DeviceSplit split;
+};
+
+// best threshold of one feature for one leaf (output of one split-scan wave)
+struct FeatureBest {
+  double gain;
+  double lg, lh, rg, rh, lo, ro;
+  int32_t feature, real_feature, thr, default_left, lc, rc, mono, pad;
 };
 
 // record of one applied split, read back by the host to rebuild the Tree

@@ -27,8 +27,11 @@ struct KArgs {
   Step* st;
   SplitRecord* rec;          // [num_leaves - 1]
   DeviceSplit* best;         // [num_leaves]
-  float* hist;               // [num_leaves][total_bins][2]
-  float* scratch;            // [total_bins][2] (the histogram being built)
+  // histograms hold fixed-point sums: int64 (g * scale_g, h * scale_h) per bin, exact and
+  // order-independent (LDS float atomics are slow on gfx950; integer ones are not)
+  long long* hist;           // [num_leaves][total_bins][2]
+  long long* scratch;        // [total_bins][2] (the histogram being built)
+  const double* scales;      // [scale_g, scale_h, 1/scale_g, 1/scale_h] of the current tree
   int32_t* blk;              // partition block counts [kMaxPartBlocks]
   double* root;              // [sum_g, sum_h, count]
   int32_t num_rows;          // local rows in the root
@@ -39,6 +42,12 @@ struct KArgs {
   int32_t tile_words;        // words per column tile
   int32_t tile_bins;         // max histogram bins of one tile (LDS floats = 2 * tile_bins)
   int32_t range_begin;       // explicit-range histogram (host-assisted mode)
+  int32_t hist_rows_cap;     // max rows one histogram workgroup accumulates (fixed-point headroom)
+  const uint8_t* bins_col;   // column-major copy of the bin matrix ([group][rows], bin_bytes each)
+  int32_t num_data;          // rows of the matrix (column stride of bins_col)
+  int32_t pad2;
+  FeatureBest* feat_best;    // [2][num_features] per-feature best split of the two leaves
+  int32_t* tickets;          // [2] arrival counters of the split-scan workgroups
 };
 
 constexpr int kMaxPartBlocks = 1024;
@@ -47,7 +56,10 @@ constexpr int kHistBlockThreads = 256;
 int HistGridBlocks();  // blocks per column tile of a full-size histogram launch
 void SetNumCUs(int n);
 
-void PackGH(const float* g, const float* h, GH* gh, int64_t n, hipStream_t s);
+// interleave (g, h) and record max|g| / max h (as float bits) into absmax[0..1] (pre-zeroed)
+void PackGH(const float* g, const float* h, GH* gh, int64_t n, uint32_t* absmax, hipStream_t s);
+// fixed-point scales of this tree from absmax and the per-workgroup row cap
+void ComputeScales(const uint32_t* absmax, int rows_cap, double* scales, hipStream_t s);
 void TreeBegin(const KArgs& a, hipStream_t s);
 void RootSum(const KArgs& a, hipStream_t s);
 void HistRoot(const KArgs& a, hipStream_t s);
@@ -56,7 +68,9 @@ void HistStep(const KArgs& a, hipStream_t s);
 void HistRange(const KArgs& a, hipStream_t s);
 void FindRoot(const KArgs& a, hipStream_t s);
 void FindStep(const KArgs& a, hipStream_t s);
-void SelectSplit(const KArgs& a, hipStream_t s);
+// device mode: pick the best leaf, record the split and count left rows per workgroup
+void SelectAndCount(const KArgs& a, hipStream_t s);
+// host-assisted mode: count left rows of the split written into Step by the host
 void PartitionCount(const KArgs& a, hipStream_t s);
 void PartitionScatter(const KArgs& a, hipStream_t s);
 

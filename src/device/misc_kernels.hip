@@ -1,0 +1,165 @@
+// Small per-tree kernels of the MI355X learner: gradient packing + fixed-point scale
+// selection, tree reset, root statistics and score arithmetic.
+#include "device_common.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+namespace {
+int g_num_cus = 256;
+}  // namespace
+
+int NumCUs() { return g_num_cus; }
+void SetNumCUs(int n) { g_num_cus = n > 0 ? n : 256; }
+int HistGridBlocks() { return 2 * g_num_cus; }
+
+// ---------------------------------------------------------------- gradient packing
+// (g, h) interleaved so a gathered row costs one 8-byte load; also max|g| / max h of the
+// tree (one atomic per workgroup; non-negative floats order like their bit patterns)
+__global__ __launch_bounds__(256) void k_pack_gh(const float* __restrict__ g, const float* __restrict__ h,
+                                                 float2* __restrict__ gh, int64_t n, uint32_t* absmax) {
+  static_assert(sizeof(GH) == sizeof(float2), "GH layout");
+  float mg = 0.f, mh = 0.f;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const float a = g[i], b = h[i];
+    gh[i] = make_float2(a, b);
+    mg = fmaxf(mg, fabsf(a));
+    mh = fmaxf(mh, fabsf(b));
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
+    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+  }
+  __shared__ float smg[4], smh[4];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    smg[w] = mg;
+    smh[w] = mh;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < static_cast<int>(blockDim.x >> 6); ++i) {
+      mg = fmaxf(mg, smg[i]);
+      mh = fmaxf(mh, smh[i]);
+    }
+    atomicMax(&absmax[0], __float_as_uint(mg));
+    atomicMax(&absmax[1], __float_as_uint(mh));
+  }
+}
+
+void PackGH(const float* g, const float* h, GH* gh, int64_t n, uint32_t* absmax, hipStream_t s) {
+  const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4 * NumCUs())));
+  hipLaunchKernelGGL(k_pack_gh, dim3(blocks), dim3(256), 0, s, g, h, reinterpret_cast<float2*>(gh), n, absmax);
+}
+
+// scale = 2^k with rows_cap * max * scale <= 2^30 (g: signed high half of the packed
+// word) and <= 2^31 (h: low half); absmax[2] (if set) carries the row cap of all ranks
+__global__ void k_scales(const uint32_t* absmax, int rows_cap, double* scales) {
+  if (threadIdx.x != 0) return;
+  if (absmax[2] != 0u) rows_cap = static_cast<int>(absmax[2]);
+  const double lim[2] = {1073741824.0, 2147483648.0};
+  for (int k = 0; k < 2; ++k) {
+    const double m = static_cast<double>(__uint_as_float(absmax[k]));
+    double sc = 1.0;
+    if (m > 0.0 && isfinite(m)) {
+      int e = static_cast<int>(floor(log2(lim[k] / (static_cast<double>(rows_cap) * m))));
+      e = max(-120, min(120, e));
+      sc = ldexp(1.0, e);
+    }
+    scales[k] = sc;
+    scales[2 + k] = 1.0 / sc;
+  }
+}
+
+void ComputeScales(const uint32_t* absmax, int rows_cap, double* scales, hipStream_t s) {
+  hipLaunchKernelGGL(k_scales, dim3(1), dim3(64), 0, s, absmax, rows_cap, scales);
+}
+
+// ---------------------------------------------------------------- tree reset
+__global__ void k_tree_begin(KArgs a) {
+  const int L = a.p.num_leaves;
+  for (int l = threadIdx.x; l < L; l += blockDim.x) {
+    Leaf lf;
+    lf.begin = 0;
+    lf.count = l == 0 ? a.num_rows : 0;
+    lf.global_count = lf.count;
+    lf.depth = 0;
+    lf.slot = l;
+    lf.pad = 0;
+    lf.sum_g = lf.sum_h = lf.output = 0.0;
+    lf.cmin = -DBL_MAX;
+    lf.cmax = DBL_MAX;
+    a.leaves[l] = lf;
+    a.best[l].gain = -INFINITY;
+    a.best[l].feature = -1;
+    a.best[l].real_feature = -1;
+  }
+  if (threadIdx.x == 0) {
+    Step* st = a.st;
+    st->done = 0;
+    st->step = 0;
+    st->leaf = 0;
+    st->new_leaf = 0;
+    st->smaller = 0;
+    st->larger = -1;
+    st->skip_find = 0;
+    st->total_left = 0;
+    a.root[0] = a.root[1] = a.root[2] = 0.0;
+    a.tickets[0] = a.tickets[1] = 0;
+  }
+}
+
+void TreeBegin(const KArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_tree_begin, dim3(1), dim3(256), 0, s, a); }
+
+__global__ __launch_bounds__(256) void k_root_sum(KArgs a) {
+  __shared__ double sh[8];
+  double sg = 0.0, shh = 0.0;
+  const int n = a.num_rows;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int r = a.root_identity ? i : a.idx[i];
+    const float2 v = reinterpret_cast<const float2*>(a.gh)[r];
+    sg += v.x;
+    shh += v.y;
+  }
+  sg = BlockSum(sg, sh);
+  shh = BlockSum(shh, sh);
+  if (threadIdx.x == 0) {
+    atomicAdd(&a.root[0], sg);
+    atomicAdd(&a.root[1], shh);
+    if (blockIdx.x == 0) atomicAdd(&a.root[2], static_cast<double>(n));
+  }
+}
+
+void RootSum(const KArgs& a, hipStream_t s) {
+  const int blocks = std::max(1, std::min((a.num_rows + 255) / 256, 2 * NumCUs()));
+  hipLaunchKernelGGL(k_root_sum, dim3(blocks), dim3(256), 0, s, a);
+}
+
+// ---------------------------------------------------------------- elementwise
+__global__ void k_add_const(double* s, int64_t n, double v) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    s[i] += v;
+}
+__global__ void k_mul_const(double* s, int64_t n, double v) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    s[i] *= v;
+}
+__global__ void k_iota(int32_t* p, int64_t n) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+    p[i] = static_cast<int32_t>(i);
+}
+
+void Iota(int32_t* p, int64_t n, hipStream_t s) { hipLaunchKernelGGL(k_iota, dim3(GridFor(n)), dim3(256), 0, s, p, n); }
+void AddConst(double* score, int64_t n, double v, hipStream_t s) {
+  hipLaunchKernelGGL(k_add_const, dim3(GridFor(n)), dim3(256), 0, s, score, n, v);
+}
+void MulConst(double* score, int64_t n, double v, hipStream_t s) {
+  hipLaunchKernelGGL(k_mul_const, dim3(GridFor(n)), dim3(256), 0, s, score, n, v);
+}
+
+}  // namespace dev
+}  // namespace lgbm_amd

@@ -1,0 +1,134 @@
+// Training-score updates with a finished tree (reference ScoreUpdater::AddScore /
+// Tree::AddPredictionToScore, src/boosting/score_updater.hpp, src/io/tree.cpp).
+//
+// k_add_tree_score walks the tree for every (or every listed) row of the binned matrix:
+// the tree's nodes -- with each split feature's decode parameters -- are staged in LDS and
+// each thread stages its row's bin words in LDS, so a level costs two LDS reads.  Rows and
+// scores are streamed in order (coalesced), which beats scattering leaf values through
+// the partition order.
+#include "device_common.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+__global__ void k_add_leaf_score(KArgs a, const double* __restrict__ vals, int num_leaves, double* __restrict__ score) {
+  const int leaf = blockIdx.y;
+  if (leaf >= num_leaves) return;
+  const Leaf lf = a.leaves[leaf];
+  const double v = vals[leaf];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < lf.count; i += gridDim.x * blockDim.x) {
+    score[a.idx[lf.begin + i]] += v;
+  }
+}
+
+void AddLeafScore(const KArgs& a, const double* leaf_values, int num_leaves, double* score, hipStream_t s) {
+  const int bx = std::max(1, std::min(64, (a.num_rows / std::max(1, num_leaves) + 255) / 256));
+  hipLaunchKernelGGL(k_add_leaf_score, dim3(bx, num_leaves), dim3(256), 0, s, a, leaf_values, num_leaves, score);
+}
+
+namespace {
+constexpr int kMaxNodes = 255;
+constexpr int kMaxRowWords = 16;
+
+struct NodeInfo {
+  int16_t group, left_is_default;  // default direction for missing values
+  int16_t missing_type, is_cat;
+  int32_t sub_lo, sub_hi, offset, mfb, default_bin, max_bin;
+  uint32_t threshold;
+  int32_t left, right;
+};
+}  // namespace
+
+__device__ __forceinline__ NodeInfo MakeNode(const KArgs& a, const DevTree& t, int i) {
+    const int f = t.split_feature_inner[i];
+    const Feature F = a.feat[f];
+    const int8_t dt = t.decision_type[i];
+    NodeInfo nd;
+    nd.group = static_cast<int16_t>(F.group);
+    nd.left_is_default = (dt & 2) ? 1 : 0;
+    nd.missing_type = static_cast<int16_t>((dt >> 2) & 3);
+    nd.is_cat = (dt & 1) ? 1 : 0;
+    nd.sub_lo = F.sub_lo;
+    nd.sub_hi = F.sub_hi;
+    nd.offset = F.offset;
+    nd.mfb = F.mfb;
+    nd.default_bin = F.default_bin;
+    nd.max_bin = F.num_bin - 1;
+    nd.threshold = t.threshold_in_bin[i];
+    nd.left = t.left_child[i];
+    nd.right = t.right_child[i];
+    return nd;
+}
+
+// STAGED: tree (<= kMaxNodes internal nodes) cached in LDS; otherwise read from HBM
+template <bool STAGED>
+__global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, const int32_t* __restrict__ rows,
+                                                        int64_t n, double* __restrict__ score) {
+  __shared__ NodeInfo s_node[STAGED ? kMaxNodes : 1];
+  __shared__ double s_val[STAGED ? kMaxNodes + 1 : 1];
+  __shared__ uint32_t s_row[256 * kMaxRowWords];
+  const int ni = t.num_leaves - 1;
+  if (STAGED) {
+    for (int i = threadIdx.x; i < ni; i += blockDim.x) s_node[i] = MakeNode(a, t, i);
+    for (int i = threadIdx.x; i < t.num_leaves; i += blockDim.x) s_val[i] = t.leaf_value[i];
+  }
+  __syncthreads();
+  const int wpr = a.words_per_row;
+  const bool stage_row = wpr <= kMaxRowWords;
+  const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
+  uint32_t* my = s_row + threadIdx.x * kMaxRowWords;
+  const int bb = a.bin_bytes;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int row = rows ? rows[i] : static_cast<int>(i);
+    int node = 0;
+    if (t.num_leaves > 1) {
+      if (stage_row) {
+        for (int k = 0; k < wpr; ++k) my[k] = bins32[static_cast<int64_t>(row) * wpr + k];
+      }
+      while (node >= 0) {
+        const NodeInfo nd = STAGED ? s_node[node] : MakeNode(a, t, node);
+        uint32_t gb;
+        if (stage_row) {
+          gb = bb == 1 ? ((my[nd.group >> 2] >> (8 * (nd.group & 3))) & 0xffu)
+                       : ((my[nd.group >> 1] >> (16 * (nd.group & 1))) & 0xffffu);
+        } else {
+          gb = RowBin(a, row, nd.group);
+        }
+        const uint32_t bin = (gb < static_cast<uint32_t>(nd.sub_lo) || gb >= static_cast<uint32_t>(nd.sub_hi))
+                                 ? static_cast<uint32_t>(nd.mfb)
+                                 : gb - nd.sub_lo + nd.offset;
+        bool left;
+        if (nd.is_cat) {
+          const int ci = static_cast<int>(nd.threshold);
+          const int lo = t.cat_boundaries_inner[ci], hi = t.cat_boundaries_inner[ci + 1];
+          const int word = static_cast<int>(bin >> 5);
+          left = word < hi - lo && ((t.cat_threshold_inner[lo + word] >> (bin & 31u)) & 1u);
+        } else if ((nd.missing_type == 1 && bin == static_cast<uint32_t>(nd.default_bin)) ||
+                   (nd.missing_type == 2 && bin == static_cast<uint32_t>(nd.max_bin))) {
+          left = nd.left_is_default != 0;
+        } else {
+          left = bin <= nd.threshold;
+        }
+        node = left ? nd.left : nd.right;
+      }
+      node = ~node;
+    }
+    score[row] += STAGED ? s_val[node] : t.leaf_value[node];
+  }
+}
+
+void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
+                  hipStream_t s) {
+  if (num_rows <= 0) return;
+  // one row per thread: many rows in flight hide the per-row load latency
+  const int blocks = static_cast<int>(std::min<int64_t>((num_rows + 255) / 256, 1 << 20));
+  if (t.num_leaves - 1 <= kMaxNodes) {
+    hipLaunchKernelGGL(k_add_tree_score<true>, dim3(blocks), dim3(256), 0, s, a, t, rows, num_rows, score);
+  } else {
+    hipLaunchKernelGGL(k_add_tree_score<false>, dim3(blocks), dim3(256), 0, s, a, t, rows, num_rows, score);
+  }
+}
+
+}  // namespace dev
+}  // namespace lgbm_amd

@@ -43,6 +43,12 @@ class RcclComm : public DeviceComm {
   void AllreduceSumF32(float* buf, size_t count, void* stream) override {
     RCCLCHECK(ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, comm_, static_cast<hipStream_t>(stream)));
   }
+  void AllreduceSumI64(long long* buf, size_t count, void* stream) override {
+    RCCLCHECK(ncclAllReduce(buf, buf, count, ncclInt64, ncclSum, comm_, static_cast<hipStream_t>(stream)));
+  }
+  void AllreduceMaxU32(uint32_t* buf, size_t count, void* stream) override {
+    RCCLCHECK(ncclAllReduce(buf, buf, count, ncclUint32, ncclMax, comm_, static_cast<hipStream_t>(stream)));
+  }
   void Allgather(const void* send, void* recv, size_t bytes_per_rank, void* stream) override {
     RCCLCHECK(ncclAllGather(send, recv, bytes_per_rank, ncclUint8, comm_, static_cast<hipStream_t>(stream)));
   }

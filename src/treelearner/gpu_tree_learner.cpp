@@ -74,19 +74,15 @@ T* GPUTreeLearner::Alloc(size_t n) {
   return static_cast<T*>(p);
 }
 
-void GPUTreeLearner::FreeAll() {
+void GPUTreeLearner::FreeBuffers() {
   for (void* p : allocs_) (void)hipFree(p);
   allocs_.clear();
-  if (h_mask_) (void)hipHostFree(h_mask_);
-  if (h_rec_) (void)hipHostFree(h_rec_);
-  if (h_step_) (void)hipHostFree(h_step_);
-  if (h_root_) (void)hipHostFree(h_root_);
-  h_mask_ = nullptr;
-  h_rec_ = nullptr;
-  h_step_ = nullptr;
-  h_root_ = nullptr;
-  if (stream_) (void)hipStreamDestroy(stream_);
-  stream_ = nullptr;
+  for (void** hp : {reinterpret_cast<void**>(&h_mask_), reinterpret_cast<void**>(&h_rec_),
+                    reinterpret_cast<void**>(&h_step_), reinterpret_cast<void**>(&h_root_),
+                    reinterpret_cast<void**>(&h_absmax_), reinterpret_cast<void**>(&h_scales_)}) {
+    if (*hp) (void)hipHostFree(*hp);
+    *hp = nullptr;
+  }
   d_score_ = nullptr;
   d_grad_ = d_hess_ = nullptr;
   d_label_ = d_weights_ = d_label_weight_ = nullptr;
@@ -96,6 +92,12 @@ void GPUTreeLearner::FreeAll() {
   d_tree_i8_ = nullptr;
   d_tree_f64_ = nullptr;
   tree_cap_ = cat_cap_ = 0;
+}
+
+void GPUTreeLearner::FreeAll() {
+  FreeBuffers();
+  if (stream_) (void)hipStreamDestroy(stream_);
+  stream_ = nullptr;
 }
 
 void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
@@ -140,6 +142,26 @@ void GPUTreeLearner::UploadData() {
   d_bins_ = Alloc<uint8_t>(host.size());
   HIPCHECK(hipMemcpy(d_bins_, host.data(), host.size(), hipMemcpyHostToDevice));
   std::vector<uint8_t>().swap(host);
+  // column-major copy for the partition kernels (one byte / short per row of the split column)
+  {
+    std::vector<uint8_t> col(static_cast<size_t>(num_data_) * num_groups_ * bin_bytes);
+#pragma omp parallel for schedule(static)
+    for (int g = 0; g < num_groups_; ++g) {
+      const FeatureGroup& grp = data_->group(g);
+      uint8_t* dst = col.data() + static_cast<size_t>(g) * num_data_ * bin_bytes;
+      if (bin_bytes == 1 && grp.bin_bytes == 1) {
+        std::memcpy(dst, grp.data.data(), static_cast<size_t>(num_data_));
+      } else {
+        for (data_size_t r = 0; r < num_data_; ++r) {
+          const uint32_t v = grp.Get(r);
+          if (bin_bytes == 1) dst[r] = static_cast<uint8_t>(v);
+          else reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(v);
+        }
+      }
+    }
+    d_bins_col_ = Alloc<uint8_t>(col.size());
+    HIPCHECK(hipMemcpy(d_bins_col_, col.data(), col.size(), hipMemcpyHostToDevice));
+  }
   // features
   std::vector<dev::Feature> feats(num_features_);
   for (int f = 0; f < num_features_; ++f) {
@@ -177,9 +199,14 @@ void GPUTreeLearner::UploadData() {
     }
     return mx;
   };
+  // widest tile that fits: a workgroup reads whole rows (one cache line per gathered row,
+  // and the row's (g, h) once) -- 1-word tiles re-gather (g, h) per tile and measured
+  // ~40% slower on small leaves (profiles/r01_v2_*)
+  int max_tw = 1 << 20;
+  if (const char* e = std::getenv("LGBM_AMD_HIST_TILE_WORDS")) max_tw = std::max(1, std::atoi(e));
   int tile_words = 0;
   for (int limit : {8192, 16384}) {
-    for (int tw = std::min(wpr, dev::kHistBlockThreads); tw >= 1; --tw) {
+    for (int tw = std::min({wpr, dev::kHistBlockThreads, max_tw}); tw >= 1; --tw) {
       if (tile_bins_for(tw) <= limit) {
         tile_words = tw;
         break;
@@ -199,8 +226,13 @@ void GPUTreeLearner::UploadData() {
   d_step_ = Alloc<dev::Step>(1);
   d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
   d_best_ = Alloc<DeviceSplit>(n_leaves);
-  d_hist_ = Alloc<float>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
-  d_scratch_ = Alloc<float>(2 * static_cast<size_t>(total_bins_));
+  d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
+  d_scratch_ = Alloc<long long>(4 * static_cast<size_t>(total_bins_));  // two step buffers
+  d_scales_ = Alloc<double>(4);
+  d_absmax_ = Alloc<uint32_t>(4);
+  d_feat_best_ = Alloc<dev::FeatureBest>(2 * static_cast<size_t>(std::max(1, num_features_)));
+  d_tickets_ = Alloc<int32_t>(2);
+  HIPCHECK(hipMemset(d_tickets_, 0, sizeof(int32_t) * 2));
   d_blk_ = Alloc<int32_t>(dev::kMaxPartBlocks);
   d_root_ = Alloc<double>(4);
   d_leaf_values_ = Alloc<double>(n_leaves);
@@ -209,6 +241,8 @@ void GPUTreeLearner::UploadData() {
                          hipHostMallocDefault));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_step_), sizeof(dev::Step), hipHostMallocDefault));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_root_), sizeof(double) * 4, hipHostMallocDefault));
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_absmax_), sizeof(uint32_t) * 4, hipHostMallocDefault));
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_scales_), sizeof(double) * 4, hipHostMallocDefault));
 
   dev::KArgs& a = args_;
   a.p.sp = params_;
@@ -243,31 +277,24 @@ void GPUTreeLearner::UploadData() {
   a.hist_tiles = (wpr + tile_words - 1) / tile_words;
   a.tile_bins = tile_bins_for(tile_words);
   a.range_begin = 0;
+  a.scales = d_scales_;
+  a.bins_col = d_bins_col_;
+  a.num_data = num_data_;
+  a.pad2 = 0;
+  a.feat_best = d_feat_best_;
+  a.tickets = d_tickets_;
+  // per-workgroup row cap of the histogram kernels (fixed-point headroom): see HistBody
+  const int grid = dev::HistGridBlocks();
+  rows_cap_ = std::max(4096, (num_data_ + grid - 1) / grid);
+  a.hist_rows_cap = rows_cap_;
 }
 
 void GPUTreeLearner::ResetTrainingData(const Dataset* train_data, bool is_constant_hessian) {
   SerialTreeLearner::ResetTrainingData(train_data, is_constant_hessian);
   HIPCHECK(hipSetDevice(device_id_));
   // rebuild the device data for the new rows (bin mappers are aligned)
-  for (void* p : allocs_) (void)hipFree(p);
-  allocs_.clear();
-  d_score_ = nullptr;
-  d_grad_ = d_hess_ = nullptr;
-  d_label_ = d_weights_ = d_label_weight_ = nullptr;
-  uploaded_label_src_ = uploaded_weight_src_ = uploaded_lw_src_ = nullptr;
-  d_tree_i32_ = nullptr;
-  d_tree_u32_ = nullptr;
-  d_tree_i8_ = nullptr;
-  d_tree_f64_ = nullptr;
-  tree_cap_ = cat_cap_ = 0;
-  if (h_mask_) (void)hipHostFree(h_mask_);
-  if (h_rec_) (void)hipHostFree(h_rec_);
-  if (h_step_) (void)hipHostFree(h_step_);
-  if (h_root_) (void)hipHostFree(h_root_);
-  h_mask_ = nullptr;
-  h_rec_ = nullptr;
-  h_step_ = nullptr;
-  h_root_ = nullptr;
+  HIPCHECK(hipStreamSynchronize(stream_));
+  FreeBuffers();
   UploadData();
   oob_cnt_ = 0;
 }
@@ -285,7 +312,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     d_leaves_ = Alloc<dev::Leaf>(n_leaves);
     d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
     d_best_ = Alloc<DeviceSplit>(n_leaves);
-    d_hist_ = Alloc<float>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
+    d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
     d_leaf_values_ = Alloc<double>(n_leaves);
     if (h_rec_) (void)hipHostFree(h_rec_);
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_rec_), sizeof(dev::SplitRecord) * std::max(1, n_leaves - 1),
@@ -344,7 +371,14 @@ void GPUTreeLearner::SetBaggingData(const Dataset* subset, const data_size_t* us
 Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   common::ScopedTimer timer("GPUTreeLearner::Train");
   HIPCHECK(hipSetDevice(device_id_));
-  dev::PackGH(gradients, hessians, d_gh_, num_data_, stream_);
+  // fixed-point scales of this tree: max |g|, max h over all rows (and ranks)
+  h_absmax_[0] = h_absmax_[1] = 0u;
+  h_absmax_[2] = static_cast<uint32_t>(rows_cap_);
+  h_absmax_[3] = 0u;
+  HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 4, hipMemcpyHostToDevice, stream_));
+  dev::PackGH(gradients, hessians, d_gh_, num_data_, d_absmax_, stream_);
+  AllreduceAbsMax();
+  dev::ComputeScales(d_absmax_, rows_cap_, d_scales_, stream_);
   host_partition_fresh_ = false;
   DecideMode();
   if (device_mode_) return TrainDeviceMode();
@@ -365,20 +399,34 @@ void GPUTreeLearner::AllreduceRoot() {
   HIPCHECK(hipMemcpyAsync(d_root_, h_root_, sizeof(double) * 3, hipMemcpyHostToDevice, stream_));
 }
 
-void GPUTreeLearner::AllreduceScratch() {
+void GPUTreeLearner::AllreduceScratch(int parity) {
   if (!data_parallel_ || Network::num_machines() <= 1) return;
   DeviceComm* dc = Network::device_comm();
   const size_t n = 2 * static_cast<size_t>(total_bins_);
+  long long* buf = d_scratch_ + static_cast<size_t>(parity & 1) * n;
   if (dc != nullptr) {
-    dc->AllreduceSumF32(d_scratch_, n, stream_);
+    dc->AllreduceSumI64(buf, n, stream_);  // exact: fixed-point integers
     return;
   }
-  std::vector<float> h(n);
-  HIPCHECK(hipMemcpyAsync(h.data(), d_scratch_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  std::vector<long long> h(n);
+  HIPCHECK(hipMemcpyAsync(h.data(), buf, sizeof(long long) * n, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   auto v = Network::GlobalSum(h);
-  HIPCHECK(hipMemcpyAsync(d_scratch_, v.data(), sizeof(float) * n, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(buf, v.data(), sizeof(long long) * n, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+void GPUTreeLearner::AllreduceAbsMax() {
+  if (!data_parallel_ || Network::num_machines() <= 1) return;
+  DeviceComm* dc = Network::device_comm();
+  if (dc != nullptr) {
+    dc->AllreduceMaxU32(d_absmax_, 3, stream_);  // non-negative float bits order like the floats
+    return;
+  }
+  HIPCHECK(hipMemcpyAsync(h_absmax_, d_absmax_, sizeof(uint32_t) * 3, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  for (int k = 0; k < 3; ++k) h_absmax_[k] = Network::GlobalSyncUpByMax(h_absmax_[k]);
+  HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 3, hipMemcpyHostToDevice, stream_));
 }
 
 Tree* GPUTreeLearner::TrainDeviceMode() {
@@ -396,21 +444,20 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     a.root_identity = 1;
   }
   root_rows_ = a.num_rows;
-  const size_t scratch_bytes = sizeof(float) * 2 * static_cast<size_t>(total_bins_);
+  // both step buffers start at zero; afterwards each split-scan zeroes the next one
+  const size_t scratch_bytes = sizeof(long long) * 4 * static_cast<size_t>(total_bins_);
   dev::TreeBegin(a, stream_);
   dev::RootSum(a, stream_);
   AllreduceRoot();
   HIPCHECK(hipMemsetAsync(d_scratch_, 0, scratch_bytes, stream_));
   dev::HistRoot(a, stream_);
-  AllreduceScratch();
+  AllreduceScratch(0);
   dev::FindRoot(a, stream_);
   for (int s = 0; s < config_->num_leaves - 1; ++s) {
-    dev::SelectSplit(a, stream_);
-    dev::PartitionCount(a, stream_);
+    dev::SelectAndCount(a, stream_);
     dev::PartitionScatter(a, stream_);
-    HIPCHECK(hipMemsetAsync(d_scratch_, 0, scratch_bytes, stream_));
     dev::HistStep(a, stream_);
-    AllreduceScratch();
+    AllreduceScratch(s + 1);  // the step's buffer parity (Step::step after the scatter)
     dev::FindStep(a, stream_);
   }
   HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
@@ -484,14 +531,19 @@ void GPUTreeLearner::BuildRangeHistogram(int leaf, int slot) {
   a.range_begin = leaf_begin_[leaf];
   a.num_rows = leaf_count_[leaf];
   const size_t n = 2 * static_cast<size_t>(total_bins_);
-  HIPCHECK(hipMemsetAsync(d_scratch_, 0, sizeof(float) * n, stream_));
+  HIPCHECK(hipMemsetAsync(d_scratch_, 0, sizeof(long long) * n, stream_));
   if (a.num_rows > 0) dev::HistRange(a, stream_);
-  std::vector<float> h(n);
-  HIPCHECK(hipMemcpyAsync(h.data(), d_scratch_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
+  std::vector<long long> h(n);
+  HIPCHECK(hipMemcpyAsync(h.data(), d_scratch_, sizeof(long long) * n, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipMemcpyAsync(h_scales_, d_scales_, sizeof(double) * 4, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
+  if (data_parallel_ && Network::num_machines() > 1) h = Network::GlobalSum(h);
   std::vector<hist_t>& dst = hist_pool_[slot];
-  for (size_t i = 0; i < n; ++i) dst[i] = h[i];
-  if (data_parallel_ && Network::num_machines() > 1) dst = Network::GlobalSum(dst);
+  const double ig = h_scales_[2], ih = h_scales_[3];
+  for (size_t i = 0; i < n; i += 2) {
+    dst[i] = static_cast<double>(h[i]) * ig;
+    dst[i + 1] = static_cast<double>(h[i + 1]) * ih;
+  }
 }
 
 void GPUTreeLearner::ConstructHistograms(const std::vector<int8_t>&, bool use_subtract) {
@@ -613,6 +665,12 @@ void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
   double* score = d_score_ + static_cast<size_t>(k) * num_data_;
   if (nl <= 1) {
     AddConstToScore(tree->LeafOutput(0), k);
+    return;
+  }
+  if (nl <= 256) {
+    // streaming traversal of every row (coalesced row reads and score updates) beats the
+    // partition-ordered scatter of leaf values; it also covers out-of-bag rows
+    AddTreeToScore(tree, k);
     return;
   }
   std::vector<double> vals(nl);

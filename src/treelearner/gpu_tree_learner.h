@@ -71,12 +71,14 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
  private:
   void UploadData();
   void FreeAll();
+  void FreeBuffers();
   void DecideMode();
   Tree* TrainDeviceMode();
   void BuildRangeHistogram(int leaf, int slot);
   void DownloadPartitionToHost() const;
-  void AllreduceScratch();
+  void AllreduceScratch(int parity);
   void AllreduceRoot();
+  void AllreduceAbsMax();
   template <typename T>
   T* Alloc(size_t n);
 
@@ -100,8 +102,16 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   dev::Step* d_step_ = nullptr;
   dev::SplitRecord* d_rec_ = nullptr;
   DeviceSplit* d_best_ = nullptr;
-  float* d_hist_ = nullptr;
-  float* d_scratch_ = nullptr;
+  long long* d_hist_ = nullptr;
+  long long* d_scratch_ = nullptr;
+  double* d_scales_ = nullptr;
+  uint32_t* d_absmax_ = nullptr;
+  uint8_t* d_bins_col_ = nullptr;
+  dev::FeatureBest* d_feat_best_ = nullptr;
+  int32_t* d_tickets_ = nullptr;
+  uint32_t* h_absmax_ = nullptr;
+  double* h_scales_ = nullptr;
+  int rows_cap_ = 4096;
   int32_t* d_blk_ = nullptr;
   double* d_root_ = nullptr;
   double* d_score_ = nullptr;
