@@ -75,8 +75,21 @@ try:
     LGBMNotFittedError = NotFittedError
     _LGBMStratifiedKFold = StratifiedKFold
     _LGBMGroupKFold = GroupKFold
-    _LGBMCheckXY = check_X_y
-    _LGBMCheckArray = check_array
+    import inspect as _inspect
+    if "ensure_all_finite" in _inspect.signature(check_array).parameters:  # scikit-learn >= 1.6
+        def _finite_kw(kw):
+            if "force_all_finite" in kw:
+                kw["ensure_all_finite"] = kw.pop("force_all_finite")
+            return kw
+
+        def _LGBMCheckXY(*args, **kw):  # noqa: N802
+            return check_X_y(*args, **_finite_kw(kw))
+
+        def _LGBMCheckArray(*args, **kw):  # noqa: N802
+            return check_array(*args, **_finite_kw(kw))
+    else:
+        _LGBMCheckXY = check_X_y
+        _LGBMCheckArray = check_array
     _LGBMCheckSampleWeight = _check_sample_weight
     _LGBMAssertAllFinite = assert_all_finite
     _LGBMCheckClassificationTargets = check_classification_targets

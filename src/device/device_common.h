@@ -15,10 +15,8 @@ namespace dev {
 int NumCUs();  // compute units of the current device (SetNumCUs)
 
 constexpr int kWave = 64;
-constexpr int kMinRowsPerHistBlock = 2048;
-constexpr int kPartThreads = 256;
-constexpr int kPartRowsPerThread = 8;
-constexpr int kPartTile = kPartThreads * kPartRowsPerThread;
+constexpr int kFindLdsBins = 2048;  // split scan stages features up to this many bins in LDS
+constexpr int kFindThreads = 256;   // split-scan workgroup
 
 inline int GridFor(int64_t n) {
   return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8 * NumCUs())));
@@ -94,9 +92,45 @@ __device__ __forceinline__ bool SplitBetter(double ga, int fa, double gb, int fb
   return fa < fb;
 }
 
-// histogram buffer being built at the current step (double-buffered: see HistBody)
+// histogram buffers: the root uses buffer 0, split s buffer (s + 1) & 1; the split scan of
+// split s zeroes the other one for split s + 1
 __device__ __forceinline__ long long* StepScratch(const KArgs& a, int parity) {
   return a.scratch + static_cast<size_t>(parity & 1) * 2 * a.p.total_bins;
+}
+
+// outcome of the step's partition, derived from the Step record alone (every histogram
+// workgroup computes it; the first one also stores it): children ranges, which child is
+// histogrammed (smaller) and whether the children are searched at all
+struct ChildInfo {
+  int total_left;
+  int left_count, right_count;     // global counts (== local ones without data-parallel)
+  int smaller, larger;             // leaf ids
+  int skip;
+  int s_begin, s_count, buf;       // the smaller child's local rows
+};
+
+// a step histogram with this many row blocks is summed by the split scan itself (the
+// reduce kernel skips it); data-parallel training always reduces (the all-reduce needs it)
+__device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk) {
+  return !a.p.data_parallel && nblk <= kReduceChunk;
+}
+
+__device__ __forceinline__ ChildInfo StepChildren(const KArgs& a, const Step* st) {
+  ChildInfo c;
+  const int pb = st->part_begin, pc = st->part_count;
+  c.total_left = st->cur_left;
+  c.left_count = a.p.data_parallel ? st->split.left_count : c.total_left;
+  c.right_count = a.p.data_parallel ? st->split.right_count : pc - c.total_left;
+  const int md = a.p.sp.min_data_in_leaf;
+  c.skip = (a.p.max_depth > 0 && st->child_depth >= a.p.max_depth) ||
+           (c.right_count < 2 * md && c.left_count < 2 * md) || (st->step + 1 >= a.p.num_leaves - 1);
+  const bool left_smaller = c.left_count < c.right_count;
+  c.smaller = left_smaller ? st->leaf : st->new_leaf;
+  c.larger = left_smaller ? st->new_leaf : st->leaf;
+  c.s_begin = left_smaller ? pb : pb + c.total_left;
+  c.s_count = left_smaller ? c.total_left : pc - c.total_left;
+  c.buf = 1 - st->src_buf;
+  return c;
 }
 
 }  // namespace dev

@@ -47,7 +47,7 @@ struct Params {
   int32_t total_bins;  // histogram length in bins
   double monotone_penalty;
   int32_t data_parallel;  // leaf sizes/decisions from global (split-estimated) counts
-  int32_t pad;
+  int32_t max_feature_bins;  // max stored bins of one feature (split-scan LDS staging)
 };
 
 // per-leaf state
@@ -57,26 +57,30 @@ struct Leaf {
   int32_t global_count;  // rows over all ranks (== count without data-parallel)
   int32_t depth;
   int32_t slot;          // histogram slot
-  int32_t pad;
+  int32_t buf;           // which index buffer (KArgs::idx / tmp) holds the leaf's rows
   double sum_g, sum_h, output;
   double cmin, cmax;  // monotone constraint range
 };
 
-// one split step: written by the select kernel, consumed by partition/hist/find
+// one split step (split index `step`).  The pick kernel writes the split to apply (leaf ..
+// child_depth), the partition kernel moves the rows (cursors), the histogram kernel's first
+// workgroup derives the children's ranges, smaller/larger and skip_find from them, which
+// the reduce / split-scan / pick kernels of the step read.
 struct Step {
   int32_t done;       // tree finished: every later kernel of the tree exits
-  int32_t step;       // split index (0-based); new leaf id = step + 1
+  int32_t step;       // index of the split being applied (when done: splits applied)
   int32_t leaf;       // leaf being split (keeps its id as the left child)
   int32_t new_leaf;   // right child id
   int32_t smaller, larger;
-  int32_t skip_find;  // children can not be split further (depth / min_data)
-  int32_t total_left;  // local rows sent left (set by the scatter kernel)
-  int32_t num_blocks;  // partition blocks used
-  int32_t rows_per_block;
+  int32_t skip_find;  // children can not be split further (depth / min_data / last split)
+  int32_t child_depth;
   int32_t part_begin;  // range of the leaf being split, before the split
   int32_t part_count;
-  int32_t hist_packed;  // the step's histogram was built directly as packed (g|h) u64 per bin
-  int32_t pad2;
+  int32_t src_buf;     // index buffer holding the parent's rows (children go to the other)
+  int32_t cur_left;    // partition cursors: rows placed on the left / right so far
+  int32_t cur_right;
+  int32_t pad;
+  Feature sfeat;       // the split feature's record (saves the partition a dependent load)
   DeviceSplit split;
 };
 

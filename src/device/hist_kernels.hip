@@ -2,22 +2,26 @@
 // DenseBin::ConstructHistogram, src/treelearner/ocl/histogram256.cl, src/io/dense_bin.hpp).
 //
 // Layout: row-major bin matrix (one 32-bit word = 4 uint8 or 2 uint16 storage columns).
-// Grid: (row chunks, column tiles).  A workgroup accumulates a LDS-private histogram of
-// its tile's columns over its chunk of the leaf's rows, then adds the non-empty bins to
-// the global histogram with 64-bit integer atomics.
+// Grid: (row blocks, column tiles) of 1024-thread workgroups.  A workgroup accumulates a
+// LDS-private histogram of its tile's columns over its block of the leaf's rows and stores
+// it whole as a partial histogram -- no global atomics (on gfx950 those execute at the
+// memory side; a per-workgroup atomic flush of a 7K-bin tile took ~22 us).  k_hist_reduce
+// then sums the partials of every bin into the step's int64 histogram.
 //
 // Accumulation is fixed point: (g * scale_g, h * scale_h) rounded to integers and packed
 // into one uint64 (g in the signed high half, h in the low half) -> one ds_add_u64 per
 // row and feature.  ds_add_f32 runs at ~0.33 lane-ops/CU/clk on gfx950, ds_add_u64 at ~5
 // (tools/microbench/lds_atomics.hip); the scale (k_scales) leaves headroom for the largest
 // per-workgroup row count so the 32-bit halves never overflow, and global sums are int64
-// (exact, deterministic regardless of atomic order, and summable across ranks with RCCL).
+// (exact, deterministic regardless of the row order, and summable across ranks with RCCL).
 #include "device_common.h"
 
 namespace lgbm_amd {
 namespace dev {
 
 namespace {
+
+constexpr int kRowsInFlight = 8;  // independent row gathers per thread
 
 __device__ __forceinline__ unsigned long long PackFixed(float2 v, float sg, float sh) {
   const long long gq = __float2ll_rn(v.x * sg);
@@ -37,84 +41,81 @@ __device__ __forceinline__ void AddRow(unsigned long long* lds, const int* goff,
   }
 }
 
-// MODE 0 root (buffer 0), 1 split step (buffer = step parity), 2 explicit range (buffer 0)
-template <int MODE, int GPW>
-__device__ void HistBody(const KArgs& a, unsigned long long* lds) {
-  int begin, count;
-  const int32_t* src;
-  long long* out_buf = a.scratch;
+// rows of the histogram: MODE 0 root, 1 smaller child of the step, 2 explicit range
+template <int MODE>
+__device__ __forceinline__ bool HistRows(const KArgs& a, int* begin, int* count, const int32_t** src) {
   if (MODE == 0) {
-    begin = 0;
-    count = a.num_rows;
-    src = a.root_identity ? nullptr : a.idx;
+    *begin = 0;
+    *count = a.num_rows;
+    *src = a.root_identity ? nullptr : a.idx;
   } else if (MODE == 2) {
-    begin = a.range_begin;
-    count = a.num_rows;
-    src = a.idx;
+    *begin = a.range_begin;
+    *count = a.num_rows;
+    *src = a.idx;
   } else {
     const Step* st = a.st;
-    if (st->done) return;
-    // copy the partitioned range of the split leaf back into the index array
-    const int pb = st->part_begin, pc = st->part_count;
-    const int nthreads = gridDim.x * gridDim.y * blockDim.x;
-    const int gtid = (blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
-    for (int i = gtid; i < pc; i += nthreads) a.idx[pb + i] = a.tmp[pb + i];
-    if (st->skip_find) return;
-    const Leaf& sm = a.leaves[st->smaller];
-    begin = sm.begin;
-    count = sm.count;
-    src = a.tmp;
-    out_buf = StepScratch(a, st->step);
-    if (st->hist_packed) {
-      // small leaf: every (row, word) adds its packed (g|h) word straight to the global
-      // histogram -- no LDS zero/flush; count <= hist_rows_cap keeps the halves exact
-      unsigned long long* outp = reinterpret_cast<unsigned long long*>(out_buf);
-      const float sgs = static_cast<float>(a.scales[0]);
-      const float shs = static_cast<float>(a.scales[1]);
-      const int wpr = a.words_per_row;
-      const int64_t pairs = static_cast<int64_t>(count) * wpr;
-      const int64_t nthreads = static_cast<int64_t>(gridDim.x) * gridDim.y * blockDim.x;
-      const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
-      const float2* gh = reinterpret_cast<const float2*>(a.gh);
-      for (int64_t p = (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
-           p < pairs; p += nthreads) {
-        const int i = static_cast<int>(p / wpr);
-        const int w = static_cast<int>(p - static_cast<int64_t>(i) * wpr);
-        const int row = src[begin + i];
-        const uint32_t word = bins32[static_cast<int64_t>(row) * wpr + w];
-        if (word == 0u) continue;
-        const unsigned long long pk = PackFixed(gh[row], sgs, shs);
-#pragma unroll
-        for (int j = 0; j < GPW; ++j) {
-          const int g = w * GPW + j;
-          const uint32_t b = GPW == 4 ? ((word >> (8 * j)) & 0xffu) : ((word >> (16 * j)) & 0xffffu);
-          if (b != 0u && g < a.p.num_groups) atomicAdd(&outp[a.group_off[g] + b], pk);
-        }
-      }
-      return;
-    }
+    if (st->done) return false;
+    const ChildInfo c = StepChildren(a, st);
+    if (c.skip) return false;
+    *begin = c.s_begin;
+    *count = c.s_count;
+    *src = c.buf ? a.tmp : a.idx;
   }
-  if (count <= 0) return;
-  const int active = min(static_cast<int>(gridDim.x), max(1, count / kMinRowsPerHistBlock));
-  if (static_cast<int>(blockIdx.x) >= active) return;
-  const int chunk = (count + active - 1) / active;
-  const int r0 = begin + blockIdx.x * chunk;
-  const int r1 = min(begin + count, r0 + chunk);
+  return *count > 0;
+}
 
-  const int w0 = blockIdx.y * a.tile_words;
-  const int w1 = min(a.words_per_row, w0 + a.tile_words);
-  const int g0 = w0 * GPW;
-  const int g_end = min(a.p.num_groups, w1 * GPW);
-  const int lo_bin = a.group_off[g0];
-  const int hi_bin = g_end < a.p.num_groups ? a.group_off[g_end] : a.p.total_bins;
-  const int nbins = hi_bin - lo_bin;
-  for (int i = threadIdx.x; i < nbins; i += blockDim.x) lds[i] = 0ull;
+// the step's bookkeeping (one thread, first histogram workgroup): children ranges and
+// counts, histogram-slot hand-over to the larger child, split records, best[] reset
+__device__ void StepBookkeeping(const KArgs& a, Step* st) {
+  const ChildInfo c = StepChildren(a, st);
+  const int leaf = st->leaf, nl = st->new_leaf;
+  const int pb = st->part_begin, pc = st->part_count;
+  Leaf* P = &a.leaves[leaf];
+  Leaf* R = &a.leaves[nl];
+  P->begin = pb;
+  P->count = c.total_left;
+  R->begin = pb + c.total_left;
+  R->count = pc - c.total_left;
+  P->buf = c.buf;
+  R->buf = c.buf;
+  if (!a.p.data_parallel) {
+    P->global_count = c.left_count;
+    R->global_count = c.right_count;
+    SplitRecord& rec = a.rec[st->step];
+    rec.left_count = c.left_count;
+    rec.right_count = c.right_count;
+  }
+  if (!c.skip && c.smaller == leaf) {
+    // the parent's histogram stays with the larger (right) child
+    const int t = P->slot;
+    P->slot = R->slot;
+    R->slot = t;
+  }
+  a.best[leaf].gain = -INFINITY;
+  a.best[leaf].feature = -1;
+  a.best[leaf].real_feature = -1;
+  a.best[nl].gain = -INFINITY;
+  a.best[nl].feature = -1;
+  a.best[nl].real_feature = -1;
+  st->smaller = c.smaller;
+  st->larger = c.larger;
+  st->skip_find = c.skip;
+}
+
+}  // namespace
+
+// one row block [r0, r1) of one column tile -> its partial histogram `out`
+template <int MODE, int GPW>
+__device__ __forceinline__ void HistBlock(const KArgs& a, unsigned long long* lds, const int32_t* src, int r0, int r1,
+                                          int w0, int w1, int lo_bin, int nbins, unsigned long long* out) {
+  __syncthreads();  // LDS reuse across row blocks
+  for (int i = threadIdx.x; i < nbins; i += kHistThreads) lds[i] = 0ull;
   __syncthreads();
 
   const float sg = static_cast<float>(a.scales[0]);
   const float sh = static_cast<float>(a.scales[1]);
-  const int tpr = w1 - w0;  // threads per row
-  const int rpp = blockDim.x / tpr;
+  const int tpr = w1 - w0;  // threads per row: one per 32-bit word of the tile
+  const int rpp = kHistThreads / tpr;
   const int q = threadIdx.x % tpr;
   const int rs = threadIdx.x / tpr;
   if (rs < rpp) {
@@ -129,67 +130,117 @@ __device__ void HistBody(const KArgs& a, unsigned long long* lds) {
     const float2* gh = reinterpret_cast<const float2*>(a.gh);
     const int64_t wpr = a.words_per_row;
     const bool write_iota = MODE == 0 && src == nullptr && q == 0 && blockIdx.y == 0;
-    int i = r0 + rs;
-    // 4 rows in flight per thread
-    for (; i + 3 * rpp < r1; i += 4 * rpp) {
-      int r[4];
+    // kRowsInFlight independent (index -> gh, bin word) gathers per thread per batch;
+    // the last batch is predicated, so a small block is one round of loads
+    for (int i = r0 + rs; i < r1; i += kRowsInFlight * rpp) {
+      int r[kRowsInFlight];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) r[k] = src ? src[i + k * rpp] : i + k * rpp;
+      for (int k = 0; k < kRowsInFlight; ++k) {
+        const int ii = i + k * rpp;
+        r[k] = ii < r1 ? (src ? src[ii] : ii) : -1;
+      }
       if (write_iota) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) a.idx[i + k * rpp] = i + k * rpp;
+        for (int k = 0; k < kRowsInFlight; ++k) {
+          if (r[k] >= 0) a.idx[i + k * rpp] = r[k];
+        }
       }
-      float2 v[4];
-      uint32_t wd[4];
+      float2 v[kRowsInFlight];
+      uint32_t wd[kRowsInFlight];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[k] = gh[r[k]];
-        wd[k] = bins32[r[k] * wpr + w];
+      for (int k = 0; k < kRowsInFlight; ++k) {
+        const int rr = r[k] >= 0 ? r[k] : 0;
+        v[k] = gh[rr];
+        wd[k] = r[k] >= 0 ? bins32[rr * wpr + w] : 0u;  // word 0: every bin skipped
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) AddRow<GPW>(lds, goff, wd[k], PackFixed(v[k], sg, sh));
-    }
-    for (; i < r1; i += rpp) {
-      const int ra = src ? src[i] : i;
-      if (write_iota) a.idx[i] = i;
-      AddRow<GPW>(lds, goff, bins32[ra * wpr + w], PackFixed(gh[ra], sg, sh));
+      for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW>(lds, goff, wd[k], PackFixed(v[k], sg, sh));
     }
   }
   __syncthreads();
-  unsigned long long* out = reinterpret_cast<unsigned long long*>(out_buf) + 2 * lo_bin;
-  for (int i = threadIdx.x; i < nbins; i += blockDim.x) {
-    const unsigned long long v = lds[i];
-    if (v != 0ull) {
-      const long long gsum = static_cast<long long>(v) >> 32;  // h (low half) is non-negative
-      const unsigned long long hsum = v & 0xffffffffull;
-      atomicAdd(&out[2 * i], static_cast<unsigned long long>(gsum));
-      atomicAdd(&out[2 * i + 1], hsum);
-    }
+  for (int i = threadIdx.x; i < nbins; i += kHistThreads) out[i] = lds[i];
+}
+
+template <int MODE, int GPW>
+__global__ __launch_bounds__(kHistThreads) void k_hist(KArgs a) {
+  extern __shared__ unsigned long long lds[];
+  // bookkeeping by the last workgroup: small leaves leave it without row work
+  if (MODE == 1 && blockIdx.x == gridDim.x - 1 && blockIdx.y == 0 && threadIdx.x == 0 && !a.st->done) {
+    StepBookkeeping(a, a.st);
+  }
+  int begin, count;
+  const int32_t* src;
+  if (!HistRows<MODE>(a, &begin, &count, &src)) return;
+  const int nblk = HistBlocksFor(count, a.hist_max_blocks, a.hist_rows_cap);
+  const int chunk = (count + nblk - 1) / nblk;
+  const int w0 = blockIdx.y * a.tile_words;
+  const int w1 = min(a.words_per_row, w0 + a.tile_words);
+  const int g0 = w0 * GPW;
+  const int g_end = min(a.p.num_groups, w1 * GPW);
+  const int lo_bin = a.group_off[g0];
+  const int hi_bin = g_end < a.p.num_groups ? a.group_off[g_end] : a.p.total_bins;
+  const int nbins = hi_bin - lo_bin;
+  // the grid is one workgroup per CU (per tile); row blocks beyond it are strided
+  for (int kb = blockIdx.x; kb < nblk; kb += gridDim.x) {
+    HistBlock<MODE, GPW>(a, lds, src, begin + kb * chunk, min(begin + count, begin + kb * chunk + chunk), w0, w1,
+                         lo_bin, nbins, a.partials + static_cast<size_t>(kb) * a.p.total_bins + lo_bin);
   }
 }
 
-}  // namespace
-
-template <int MODE, int GPW>
-__global__ __launch_bounds__(kHistBlockThreads) void k_hist(KArgs a) {
-  extern __shared__ unsigned long long lds[];
-  HistBody<MODE, GPW>(a, lds);
+// partials [block][bin] -> int64 (g, h) pairs of the step's buffer.  Each thread sums up to
+// kReduceChunk partials of one bin; with more blocks than that the chunks are combined by
+// int64 atomics into the (pre-zeroed) buffer, otherwise the single chunk stores directly.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
+  int begin, count;
+  const int32_t* src;
+  if (!HistRows<MODE>(a, &begin, &count, &src)) return;
+  const int nblk = HistBlocksFor(count, a.hist_max_blocks, a.hist_rows_cap);
+  if (MODE == 1 && DirectPartials(a, nblk)) return;  // summed by the split scan
+  const int k0 = blockIdx.y * kReduceChunk;
+  if (k0 >= nblk) return;
+  const int bin = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = a.p.total_bins;
+  if (bin >= nb) return;
+  const unsigned long long* p = a.partials + static_cast<size_t>(k0) * nb + bin;
+  const int kn = min(kReduceChunk, nblk - k0);
+  unsigned long long v[kReduceChunk];
+#pragma unroll
+  for (int k = 0; k < kReduceChunk; ++k) v[k] = k < kn ? p[static_cast<size_t>(k) * nb] : 0ull;
+  long long g = 0, h = 0;
+#pragma unroll
+  for (int k = 0; k < kReduceChunk; ++k) {
+    g += static_cast<long long>(v[k]) >> 32;  // h (low half) is non-negative: no borrow
+    h += static_cast<long long>(v[k] & 0xffffffffull);
+  }
+  long long* out = MODE == 1 ? StepScratch(a, a.st->step + 1) : a.scratch;
+  if (nblk <= kReduceChunk) {
+    out[2 * bin] = g;
+    out[2 * bin + 1] = h;
+  } else {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin]), static_cast<unsigned long long>(g));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin + 1]), static_cast<unsigned long long>(h));
+  }
 }
 
 template <int MODE>
-static void LaunchHistMode(const KArgs& a, hipStream_t s) {
+static void LaunchHistMode(const KArgs& a, int grid_x, hipStream_t s) {
   const size_t lds_bytes = sizeof(unsigned long long) * static_cast<size_t>(a.tile_bins);
-  dim3 grid(HistGridBlocks(), a.hist_tiles);
+  dim3 grid(grid_x, a.hist_tiles);
   if (a.bin_bytes == 1) {
-    hipLaunchKernelGGL((k_hist<MODE, 4>), grid, dim3(kHistBlockThreads), lds_bytes, s, a);
+    hipLaunchKernelGGL((k_hist<MODE, 4>), grid, dim3(kHistThreads), lds_bytes, s, a);
   } else {
-    hipLaunchKernelGGL((k_hist<MODE, 2>), grid, dim3(kHistBlockThreads), lds_bytes, s, a);
+    hipLaunchKernelGGL((k_hist<MODE, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
   }
+  dim3 rgrid((a.p.total_bins + 255) / 256, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk);
+  hipLaunchKernelGGL(k_hist_reduce<MODE>, rgrid, dim3(256), 0, s, a);
 }
 
-void HistRoot(const KArgs& a, hipStream_t s) { LaunchHistMode<0>(a, s); }
-void HistStep(const KArgs& a, hipStream_t s) { LaunchHistMode<1>(a, s); }
-void HistRange(const KArgs& a, hipStream_t s) { LaunchHistMode<2>(a, s); }
+// the root fills the chip (two workgroups per CU); a step's leaf is usually small, and
+// dispatching workgroups that exit at once is not free (~3 us for 512 x 1024 threads)
+void HistRoot(const KArgs& a, hipStream_t s) { LaunchHistMode<0>(a, a.hist_max_blocks, s); }
+void HistStep(const KArgs& a, hipStream_t s) { LaunchHistMode<1>(a, std::min(a.hist_max_blocks, NumCUs()), s); }
+void HistRange(const KArgs& a, hipStream_t s) { LaunchHistMode<2>(a, a.hist_max_blocks, s); }
 
 }  // namespace dev
 }  // namespace lgbm_amd

@@ -21,8 +21,8 @@ struct KArgs {
   const int32_t* group_off;  // [num_groups] first histogram bin of each storage column
   const int8_t* tree_mask;   // [num_features] feature used by this tree
   const GH* gh;              // interleaved (gradient, hessian) per row
-  int32_t* idx;              // partition indices
-  int32_t* tmp;              // partition scratch
+  int32_t* idx;              // partition index buffer 0 (root rows)
+  int32_t* tmp;              // partition index buffer 1 (leaves alternate: Leaf::buf)
   Leaf* leaves;              // [num_leaves]
   Step* st;
   SplitRecord* rec;          // [num_leaves - 1]
@@ -30,30 +30,45 @@ struct KArgs {
   // histograms hold fixed-point sums: int64 (g * scale_g, h * scale_h) per bin, exact and
   // order-independent (LDS float atomics are slow on gfx950; integer ones are not)
   long long* hist;           // [num_leaves][total_bins][2]
-  long long* scratch;        // [total_bins][2] (the histogram being built)
+  long long* scratch;        // [2][total_bins][2] the histogram being built (step parity)
+  unsigned long long* partials;  // [hist_max_blocks][total_bins] per-workgroup packed (g|h)
   const double* scales;      // [scale_g, scale_h, 1/scale_g, 1/scale_h] of the current tree
-  int32_t* blk;              // partition block counts [kMaxPartBlocks]
   double* root;              // [sum_g, sum_h, count]
-  int32_t num_rows;          // local rows in the root
+  int32_t num_rows;          // local rows in the root (or the explicit range)
   int32_t root_identity;     // root rows are 0..num_rows-1 (indices written by the root pass)
   int32_t bin_bytes;         // 1 or 2
   int32_t words_per_row;     // 32-bit words per row
   int32_t hist_tiles;        // column tiles of the histogram kernel
   int32_t tile_words;        // words per column tile
-  int32_t tile_bins;         // max histogram bins of one tile (LDS floats = 2 * tile_bins)
+  int32_t tile_bins;         // max histogram bins of one tile (LDS words)
   int32_t range_begin;       // explicit-range histogram (host-assisted mode)
   int32_t hist_rows_cap;     // max rows one histogram workgroup accumulates (fixed-point headroom)
+  int32_t hist_max_blocks;   // row blocks of a histogram (partials capacity)
   const uint8_t* bins_col;   // column-major copy of the bin matrix ([group][rows], bin_bytes each)
   int32_t num_data;          // rows of the matrix (column stride of bins_col)
   int32_t pad2;
   FeatureBest* feat_best;    // [2][num_features] per-feature best split of the two leaves
-  int32_t* tickets;          // [2] arrival counters of the split-scan workgroups
 };
 
-constexpr int kMaxPartBlocks = 1024;
-constexpr int kHistBlockThreads = 256;
+constexpr int kHistThreads = 1024;     // histogram workgroup (16 waves)
+constexpr int kHistMinRows = 1024;     // rows per histogram workgroup, lower bound
+constexpr int kReduceChunk = 16;       // partial histograms summed per reduce thread
+constexpr int kPartThreads = 1024;
+constexpr int kPartRowsPerThread = 8;
+constexpr int kPartTile = kPartThreads * kPartRowsPerThread;
 
-int HistGridBlocks();  // blocks per column tile of a full-size histogram launch
+// row blocks (partial histograms) used for `count` rows: deterministic, shared by the
+// histogram and reduce kernels; rows per block never exceed the fixed-point row cap
+__host__ __device__ inline int HistBlocksFor(int count, int max_blocks, int rows_cap) {
+  if (count <= 0) return 0;
+  int rpb = (count + max_blocks - 1) / max_blocks;
+  if (rpb < kHistMinRows) rpb = kHistMinRows;
+  if (rpb > rows_cap) rpb = rows_cap;
+  int k = (count + rpb - 1) / rpb;
+  return k > max_blocks ? max_blocks : k;
+}
+
+int HistGridBlocks();  // max row blocks of a histogram (2 per CU)
 void SetNumCUs(int n);
 
 // interleave (g, h) and record max|g| / max h (as float bits) into absmax[0..1] (pre-zeroed)
@@ -62,17 +77,19 @@ void PackGH(const float* g, const float* h, GH* gh, int64_t n, uint32_t* absmax,
 void ComputeScales(const uint32_t* absmax, int rows_cap, double* scales, hipStream_t s);
 void TreeBegin(const KArgs& a, hipStream_t s);
 void RootSum(const KArgs& a, hipStream_t s);
+// histograms: per-workgroup packed partials, then an exact int64 reduction into the
+// step's scratch buffer (root: buffer 0; step: parity of Step::step; range: buffer 0)
 void HistRoot(const KArgs& a, hipStream_t s);
 void HistStep(const KArgs& a, hipStream_t s);
-// histogram of rows idx[range_begin, range_begin + num_rows) into scratch
-void HistRange(const KArgs& a, hipStream_t s);
+void HistRange(const KArgs& a, hipStream_t s);  // rows idx[range_begin, +num_rows)
+// split scans of the root / the two children of the step (per-feature results)
 void FindRoot(const KArgs& a, hipStream_t s);
 void FindStep(const KArgs& a, hipStream_t s);
-// device mode: pick the best leaf, record the split and count left rows per workgroup
-void SelectAndCount(const KArgs& a, hipStream_t s);
-// host-assisted mode: count left rows of the split written into Step by the host
-void PartitionCount(const KArgs& a, hipStream_t s);
-void PartitionScatter(const KArgs& a, hipStream_t s);
+// per-leaf best split from the per-feature results, then the next split to apply
+void PickRoot(const KArgs& a, hipStream_t s);
+void PickStep(const KArgs& a, hipStream_t s);
+// move the split leaf's rows into the children's ranges (device mode: plus bookkeeping)
+void Partition(const KArgs& a, hipStream_t s);
 
 // score[k] += value[leaf(row)] for every partitioned row of the finished tree
 void AddLeafScore(const KArgs& a, const double* leaf_values, int num_leaves, double* score, hipStream_t s);

@@ -86,7 +86,7 @@ __global__ void k_tree_begin(KArgs a) {
     lf.global_count = lf.count;
     lf.depth = 0;
     lf.slot = l;
-    lf.pad = 0;
+    lf.buf = 0;
     lf.sum_g = lf.sum_h = lf.output = 0.0;
     lf.cmin = -DBL_MAX;
     lf.cmax = DBL_MAX;
@@ -104,9 +104,10 @@ __global__ void k_tree_begin(KArgs a) {
     st->smaller = 0;
     st->larger = -1;
     st->skip_find = 0;
-    st->total_left = 0;
+    st->child_depth = 0;
+    st->src_buf = 0;
+    st->cur_left = st->cur_right = 0;
     a.root[0] = a.root[1] = a.root[2] = 0.0;
-    a.tickets[0] = a.tickets[1] = 0;
   }
 }
 

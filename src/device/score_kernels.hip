@@ -16,8 +16,9 @@ __global__ void k_add_leaf_score(KArgs a, const double* __restrict__ vals, int n
   if (leaf >= num_leaves) return;
   const Leaf lf = a.leaves[leaf];
   const double v = vals[leaf];
+  const int32_t* ids = lf.buf ? a.tmp : a.idx;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < lf.count; i += gridDim.x * blockDim.x) {
-    score[a.idx[lf.begin + i]] += v;
+    score[ids[lf.begin + i]] += v;
   }
 }
 

@@ -2,14 +2,18 @@
 // FindBestThresholdSequentially, FuncForNumricalL3, FixHistogram; serial_tree_learner.cpp
 // FindBestSplitsFromHistograms).
 //
-// Grid (num_features, 2 leaves), one 64-wide wave per workgroup.  A wave materialises its
-// feature's histogram in the leaf's pool slot (the built child copies the step buffer, its
-// sibling subtracts it from the parent slot -- exact in int64), then evaluates every
-// threshold of the forward / reverse scans in parallel (wave prefix sums) with the
-// reference's missing-value handling, min_data / min_hessian filters, hessian-estimated
-// counts, L1 / max_delta_step / path smoothing / monotone constraints.  Ties keep the
-// threshold the sequential scan would keep.  Per-feature results go to feat_best; the
-// last wave of a leaf to arrive (atomic ticket) picks the leaf's best split.
+// k_find: grid (num_features, 2 leaves), one 256-thread workgroup per (feature, leaf).  It
+// materialises the feature's histogram in the leaf's pool slot (the smaller child takes
+// the step's reduced histogram -- or sums the few partials of a small leaf itself -- the
+// larger one subtracts it from the parent slot, exact in int64), stages it dequantised in
+// LDS, then evaluates every threshold of the forward / reverse scans in parallel
+// (workgroup prefix sums) with the reference's missing-value handling,
+// min_data / min_hessian filters, hessian-estimated counts, L1 / max_delta_step / path
+// smoothing / monotone constraints.  Ties keep the threshold the sequential scan would
+// keep.  Per-feature results go to feat_best.
+// k_pick (one wave): per-leaf best split over the features (SplitInfo order), then the
+// next leaf to split over all leaves (serial_tree_learner.cpp Train: ArgMax of
+// best_split_per_leaf_), written as the Step the partition kernel applies.
 #include "device_common.h"
 
 namespace lgbm_amd {
@@ -73,27 +77,116 @@ __device__ __forceinline__ T WavePrefixIncl(T v) {
   return v;
 }
 
-// a feature's dequantised histogram with its most-frequent bin restored (FixHistogram)
+// block-wide scans / reductions of the split scan (kFindThreads threads); every thread
+// calls them, results are returned to every thread
+struct BlockScratch {
+  double d[2][kFindThreads / kWave];
+  int i[kFindThreads / kWave];
+  Cand c[kFindThreads / kWave];
+};
+constexpr int kFindWaves = kFindThreads / kWave;
+
+__device__ __forceinline__ void BlockScan3(double& a, double& b, int& c, bool suffix, BlockScratch* sc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a = suffix ? WaveSuffixIncl(a) : WavePrefixIncl(a);
+  b = suffix ? WaveSuffixIncl(b) : WavePrefixIncl(b);
+  c = suffix ? WaveSuffixIncl(c) : WavePrefixIncl(c);
+  if (lane == (suffix ? 0 : 63)) {
+    sc->d[0][w] = a;
+    sc->d[1][w] = b;
+    sc->i[w] = c;
+  }
+  __syncthreads();
+  double oa = 0.0, ob = 0.0;
+  int oc = 0;
+#pragma unroll
+  for (int j = 0; j < kFindWaves; ++j) {
+    if (suffix ? j > w : j < w) {
+      oa += sc->d[0][j];
+      ob += sc->d[1][j];
+      oc += sc->i[j];
+    }
+  }
+  __syncthreads();
+  a += oa;
+  b += ob;
+  c += oc;
+}
+
+__device__ __forceinline__ void BlockSum3(double& a, double& b, int& c, BlockScratch* sc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a = WaveSum(a);
+  b = WaveSum(b);
+  c = WaveSum(c);
+  if (lane == 0) {
+    sc->d[0][w] = a;
+    sc->d[1][w] = b;
+    sc->i[w] = c;
+  }
+  __syncthreads();
+  a = b = 0.0;
+  c = 0;
+#pragma unroll
+  for (int j = 0; j < kFindWaves; ++j) {  // fixed order: identical on every thread and run
+    a += sc->d[0][j];
+    b += sc->d[1][j];
+    c += sc->i[j];
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool BlockAny(bool v, BlockScratch* sc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const bool wv = __any(v);
+  if (lane == 0) sc->i[w] = wv ? 1 : 0;
+  __syncthreads();
+  int r = 0;
+#pragma unroll
+  for (int j = 0; j < kFindWaves; ++j) r |= sc->i[j];
+  __syncthreads();
+  return r != 0;
+}
+
+__device__ __forceinline__ Cand BlockBestCand(Cand c, bool reverse, BlockScratch* sc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  c = WaveBestCand(c, reverse);
+  if (lane == 0) sc->c[w] = c;
+  __syncthreads();
+  Cand b = sc->c[0];
+#pragma unroll
+  for (int j = 1; j < kFindWaves; ++j) {
+    if (CandBetter(sc->c[j], b, reverse)) b = sc->c[j];
+  }
+  __syncthreads();
+  return b;
+}
+
+// a feature's dequantised histogram with its most-frequent bin restored (FixHistogram);
+// bins come from LDS (staged by the wave) or, for very wide features, from the int64 slot
 struct HistView {
+  const double* lg;
+  const double* lh;
   const long long* h;
   double inv_g, inv_h;
   int fix_t;  // bin whose value is reconstructed from the leaf totals (-1: none)
   double fix_g, fix_h;
-  __device__ __forceinline__ double G(int t) const {
-    return t == fix_t ? fix_g : static_cast<double>(h[2 * t]) * inv_g;
+  __device__ __forceinline__ double RawG(int t) const {
+    return lg ? lg[t] : static_cast<double>(h[2 * t]) * inv_g;
   }
-  __device__ __forceinline__ double H(int t) const {
-    return t == fix_t ? fix_h : static_cast<double>(h[2 * t + 1]) * inv_h;
+  __device__ __forceinline__ double RawH(int t) const {
+    return lh ? lh[t] : static_cast<double>(h[2 * t + 1]) * inv_h;
   }
+  __device__ __forceinline__ double G(int t) const { return t == fix_t ? fix_g : RawG(t); }
+  __device__ __forceinline__ double H(int t) const { return t == fix_t ? fix_h : RawH(t); }
 };
 
-// one numerical scan of one feature by one wave
-__device__ Cand ScanNumericalWave(const HistView& hv, int nb, int offset, int default_bin, bool reverse,
-                                  bool skip_def, bool na, const LeafCtx& L, const SplitParams& p, int mono,
-                                  bool* splittable) {
-  const int lane = threadIdx.x & 63;
-  const int K = (nb + 63) / 64;
-  const int b0 = lane * K;
+// one numerical scan of one feature by one workgroup (each thread owns K consecutive bins)
+__device__ Cand ScanNumericalBlock(const HistView& hv, int nb, int offset, int default_bin, bool reverse,
+                                   bool skip_def, bool na, const LeafCtx& L, const SplitParams& p, int mono,
+                                   bool* splittable, BlockScratch* sc) {
+  const int tid = threadIdx.x;
+  const int K = (nb + kFindThreads - 1) / kFindThreads;
+  const int b0 = tid * K;
   const int b1 = min(nb, b0 + K);
   const int t_start_r = nb - 1 - (na ? 1 : 0);
   const int t_end_r = 1 - offset;
@@ -121,9 +214,10 @@ __device__ Cand ScanNumericalWave(const HistView& hv, int nb, int offset, int de
   const double min_h = p.min_sum_hessian_in_leaf;
   const int min_n = p.min_data_in_leaf;
   if (reverse) {
-    const double ig = WaveSuffixIncl(tg), ih = WaveSuffixIncl(th);
-    const int ic = WaveSuffixIncl(tc);
-    double rg = ig - tg, rh = ih - th;  // exclusive suffix (bins above this lane)
+    double ig = tg, ih = th;
+    int ic = tc;
+    BlockScan3(ig, ih, ic, true, sc);
+    double rg = ig - tg, rh = ih - th;  // exclusive suffix (bins above this thread's)
     int rc = ic - tc;
     rh += kEpsilon;
     for (int t = b1 - 1; t >= b0; --t) {
@@ -164,15 +258,14 @@ __device__ Cand ScanNumericalWave(const HistView& hv, int nb, int offset, int de
         ah += hh;
         ac += RoundIntD(hh * L.cnt_factor);
       }
-      ag = WaveSum(ag);
-      ah = WaveSum(ah);
-      ac = WaveSum(ac);
+      BlockSum3(ag, ah, ac, sc);
       lg0 = L.sg - ag;
       lh0 = L.sh - kEpsilon - ah;
       lc0 = L.n - ac;
     }
-    const double ig = WavePrefixIncl(tg), ih = WavePrefixIncl(th);
-    const int ic = WavePrefixIncl(tc);
+    double ig = tg, ih = th;
+    int ic = tc;
+    BlockScan3(ig, ih, ic, false, sc);
     double lg = lg0 + (ig - tg), lh = lh0 + (ih - th);
     int lc = lc0 + (ic - tc);
     auto eval = [&](int t, double xg, double xh, int xc) {
@@ -194,7 +287,7 @@ __device__ Cand ScanNumericalWave(const HistView& hv, int nb, int offset, int de
         best.lc = xc;
       }
     };
-    if (minus_one && lane == 0 && !(skip_def && offset - 1 == default_bin)) eval(-1, lg0, lh0, lc0);
+    if (minus_one && tid == 0 && !(skip_def && offset - 1 == default_bin)) eval(-1, lg0, lh0, lc0);
     for (int t = b0; t < b1; ++t) {
       if (!acc(t)) continue;
       const double g = hv.G(t), hh = hv.H(t);
@@ -204,31 +297,25 @@ __device__ Cand ScanNumericalWave(const HistView& hv, int nb, int offset, int de
       eval(t, lg, lh, lc);
     }
   }
-  if (__any(any)) *splittable = true;
-  return WaveBestCand(best, reverse);
+  if (BlockAny(any, sc)) *splittable = true;
+  return BlockBestCand(best, reverse, sc);
 }
 
-__device__ void FindNumericalWave(const Feature& F, const long long* h, double inv_g, double inv_h,
-                                  const LeafCtx& L, const SplitParams& p, int depth, double mono_penalty,
-                                  FeatureBest* out) {
+__device__ void FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
+                                   double mono_penalty, FeatureBest* out, BlockScratch* sc) {
   const int nb = F.num_bin - F.offset;
-  HistView hv;
-  hv.h = h;
-  hv.inv_g = inv_g;
-  hv.inv_h = inv_h;
   hv.fix_t = -1;
   hv.fix_g = hv.fix_h = 0.0;
   if (F.mfb > 0) {
     // FixHistogram: the most frequent bin is not accumulated; rebuild it from the leaf totals
     double sg = 0.0, sh = 0.0;
-    const int lane = threadIdx.x & 63;
-    for (int t = lane; t < nb; t += 64) {
+    int unused = 0;
+    for (int t = threadIdx.x; t < nb; t += kFindThreads) {
       if (t == F.mfb) continue;
-      sg += static_cast<double>(h[2 * t]) * inv_g;
-      sh += static_cast<double>(h[2 * t + 1]) * inv_h;
+      sg += hv.RawG(t);
+      sh += hv.RawH(t);
     }
-    sg = WaveSum(sg);
-    sh = WaveSum(sh);
+    BlockSum3(sg, sh, unused, sc);
     hv.fix_t = F.mfb;
     hv.fix_g = L.sg - sg;
     hv.fix_h = (L.sh - 2 * kEpsilon) - sh;
@@ -254,14 +341,14 @@ __device__ void FindNumericalWave(const Feature& F, const long long* h, double i
   };
   if (F.num_bin > 2 && F.missing_type != 0) {
     if (F.missing_type == 1) {
-      apply(ScanNumericalWave(hv, nb, F.offset, F.default_bin, true, true, false, L, p, F.monotone, &splittable), true);
-      apply(ScanNumericalWave(hv, nb, F.offset, F.default_bin, false, true, false, L, p, F.monotone, &splittable), false);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, true, false, L, p, F.monotone, &splittable, sc), true);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, true, false, L, p, F.monotone, &splittable, sc), false);
     } else {
-      apply(ScanNumericalWave(hv, nb, F.offset, F.default_bin, true, false, true, L, p, F.monotone, &splittable), true);
-      apply(ScanNumericalWave(hv, nb, F.offset, F.default_bin, false, false, true, L, p, F.monotone, &splittable), false);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, true, L, p, F.monotone, &splittable, sc), true);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, false, true, L, p, F.monotone, &splittable, sc), false);
     }
   } else {
-    apply(ScanNumericalWave(hv, nb, F.offset, F.default_bin, true, false, false, L, p, F.monotone, &splittable), true);
+    apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, false, L, p, F.monotone, &splittable, sc), true);
     if (F.missing_type == 2) out->default_left = 0;
   }
   out->gain *= F.penalty;
@@ -278,27 +365,30 @@ __device__ void FindNumericalWave(const Feature& F, const long long* h, double i
 }  // namespace
 
 template <bool ROOT>
-__global__ __launch_bounds__(kWave) void k_find(KArgs a) {
+__global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
+  extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
+  __shared__ BlockScratch sc;
   const int f = blockIdx.x;
   const int side = blockIdx.y;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x;
   const Feature F = a.feat[f];
-  const int nb2 = 2 * (F.num_bin - F.offset);
-  int parity = 0, leaf = 0;
-  bool packed = false;
+  const int nbf = F.num_bin - F.offset;
+  const int nb2 = 2 * nbf;
+  int parity = 0, leaf = 0, nblk_direct = -1;
   if (!ROOT) {
     const Step* st = a.st;
     if (st->done) return;
-    parity = st->step & 1;
-    packed = st->hist_packed != 0;
-    // zero this feature's bins (pair and packed layouts) of the buffer the next step uses
+    parity = (st->step + 1) & 1;
+    // zero this feature's bins of the buffer the next step reduces into
     if (side == 0) {
       long long* nxt = StepScratch(a, parity + 1);
-      for (int i = lane; i < nb2; i += kWave) nxt[2 * F.hist_offset + i] = 0;
-      for (int i = lane; i < nb2 / 2; i += kWave) nxt[F.hist_offset + i] = 0;
+      for (int i = tid; i < nb2; i += kFindThreads) nxt[2 * F.hist_offset + i] = 0;
     }
     if (st->skip_find) return;
     leaf = side == 0 ? st->smaller : st->larger;
+    const ChildInfo c = StepChildren(a, st);
+    const int nblk = HistBlocksFor(c.s_count, a.hist_max_blocks, a.hist_rows_cap);
+    if (DirectPartials(a, nblk)) nblk_direct = nblk;
   }
   const SplitParams& p = a.p.sp;
   LeafCtx L;
@@ -315,7 +405,7 @@ __global__ __launch_bounds__(kWave) void k_find(KArgs a) {
     rp.use_smoothing = 0;
     rp.use_mc = 1;
     const double out0 = LeafOutputConstrained(sg, sh, p.lambda_l2, rp, c, n, 0);
-    if (f == 0 && lane == 0) {
+    if (f == 0 && tid == 0) {
       Leaf& lf = a.leaves[0];
       lf.sum_g = sg;
       lf.sum_h = sh;
@@ -358,48 +448,89 @@ __global__ __launch_bounds__(kWave) void k_find(KArgs a) {
   if (a.tree_mask[f] && !F.is_cat) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
-    if (packed) {
-      // (g | h) packed words: g = arithmetic high half, h = low half
-      const unsigned long long* srcp =
-          reinterpret_cast<const unsigned long long*>(StepScratch(a, parity)) + F.hist_offset;
-      const int nb = nb2 / 2;
-      for (int i = lane; i < nb; i += kWave) {
-        const unsigned long long v = srcp[i];
-        const long long g = static_cast<long long>(v) >> 32;
-        const long long h = static_cast<long long>(v & 0xffffffffull);
-        if (side == 0) {
-          dst[2 * i] = g;
-          dst[2 * i + 1] = h;
-        } else {
-          dst[2 * i] -= g;
-          dst[2 * i + 1] -= h;
+    const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
+    const unsigned long long* part = a.partials + F.hist_offset;
+    const double ig = a.scales[2], ih = a.scales[3];
+    const bool stage = a.p.max_feature_bins <= kFindLdsBins;
+    double* sg = s_bins;
+    double* sh = s_bins + (stage ? a.p.max_feature_bins : 0);
+    for (int i = tid; i < nbf; i += kFindThreads) {
+      long long g = 0, h = 0;
+      if (nblk_direct >= 0) {
+        // small leaf: sum the few per-workgroup partials here (k_hist_reduce skipped them)
+        unsigned long long v[kReduceChunk];
+#pragma unroll
+        for (int k = 0; k < kReduceChunk; ++k)
+          v[k] = k < nblk_direct ? part[static_cast<size_t>(k) * a.p.total_bins + i] : 0ull;
+#pragma unroll
+        for (int k = 0; k < kReduceChunk; ++k) {
+          g += static_cast<long long>(v[k]) >> 32;
+          h += static_cast<long long>(v[k] & 0xffffffffull);
         }
-      }
-    } else {
-      const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
-      if (side == 0) {
-        for (int i = lane; i < nb2; i += kWave) dst[i] = src[i];
       } else {
-        for (int i = lane; i < nb2; i += kWave) dst[i] -= src[i];
+        g = src[2 * i];
+        h = src[2 * i + 1];
+      }
+      if (side == 1) {  // larger child = parent - smaller, in the parent's (now its) slot
+        g = dst[2 * i] - g;
+        h = dst[2 * i + 1] - h;
+      }
+      dst[2 * i] = g;
+      dst[2 * i + 1] = h;
+      if (stage) {
+        sg[i] = static_cast<double>(g) * ig;
+        sh[i] = static_cast<double>(h) * ih;
       }
     }
-    __syncthreads();  // the wave's own stores become visible to all its lanes
-    FindNumericalWave(F, dst, a.scales[2], a.scales[3], L, p, depth, a.p.monotone_penalty, &o);
+    __syncthreads();  // the workgroup's stores become visible to all its threads
+    HistView hv;
+    hv.lg = stage ? sg : nullptr;
+    hv.lh = stage ? sh : nullptr;
+    hv.h = dst;
+    hv.inv_g = ig;
+    hv.inv_h = ih;
+    FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
   } else {
     o.feature = -1;
   }
-  FeatureBest* fb = a.feat_best + side * a.p.num_features;
-  if (lane == 0) fb[f] = o;
-  // arrival ticket: the last wave of this leaf reduces the per-feature results
-  __shared__ int last;
-  if (lane == 0) {
-    __threadfence();
-    const int t = atomicAdd(&a.tickets[side], 1);
-    last = (t == a.p.num_features - 1) ? 1 : 0;
+  if (tid == 0) a.feat_best[side * a.p.num_features + f] = o;
+}
+
+namespace {
+
+// argmax of best[0..s] (host loop order: higher gain, then smaller real feature, then lower
+// leaf id), one wave
+__device__ int PickLeafWave(const KArgs& a, int s) {
+  double bg = -INFINITY;
+  int bf = -1, bl = 0x7fffffff;
+  for (int l = threadIdx.x; l <= s; l += kWave) {
+    const double g = a.best[l].gain;
+    const int f = a.best[l].real_feature;
+    if (bl == 0x7fffffff || SplitBetter(g, f, bg, bf)) {
+      bg = g;
+      bf = f;
+      bl = l;
+    }
   }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(bg, o, kWave);
+    const int of = __shfl_xor(bf, o, kWave);
+    const int ol = __shfl_xor(bl, o, kWave);
+    const bool take = ol != 0x7fffffff &&
+                      (bl == 0x7fffffff || SplitBetter(og, of, bg, bf) || (!SplitBetter(bg, bf, og, of) && ol < bl));
+    if (take) {
+      bg = og;
+      bf = of;
+      bl = ol;
+    }
+  }
+  return bl;
+}
+
+// best[leaf] = best of the per-feature results of one side
+__device__ void ReduceFeatureBest(const KArgs& a, int side, int leaf) {
+  const int lane = threadIdx.x;
+  const FeatureBest* fb = a.feat_best + side * a.p.num_features;
   int bi = -1;
   double bg = -INFINITY;
   int brf = -1;
@@ -422,7 +553,6 @@ __global__ __launch_bounds__(kWave) void k_find(KArgs a) {
     }
   }
   if (lane == 0) {
-    a.tickets[side] = 0;
     DeviceSplit& d = a.best[leaf];
     if (bi < 0 || fb[bi].gain == -INFINITY) {
       d.gain = -INFINITY;
@@ -450,12 +580,93 @@ __global__ __launch_bounds__(kWave) void k_find(KArgs a) {
   }
 }
 
+}  // namespace
+
+template <bool ROOT>
+__global__ __launch_bounds__(kWave) void k_pick(KArgs a) {
+  Step* st = a.st;
+  if (st->done) return;
+  if (ROOT) {
+    ReduceFeatureBest(a, 0, 0);
+  } else if (!st->skip_find) {
+    ReduceFeatureBest(a, 0, st->smaller);
+    ReduceFeatureBest(a, 1, st->larger);
+  }
+  __syncthreads();  // lane 0's best[] stores -> the whole wave
+  const int s = ROOT ? 0 : st->step + 1;  // index of the next split
+  if (s >= a.p.num_leaves - 1) {
+    if (threadIdx.x == 0) {
+      st->step = s;
+      st->done = 1;
+    }
+    return;
+  }
+  const int leaf = PickLeafWave(a, s);
+  if (threadIdx.x != 0) return;
+  const DeviceSplit sp = a.best[leaf];
+  st->step = s;
+  if (!(sp.gain > 0.0) || sp.feature < 0) {
+    st->done = 1;
+    return;
+  }
+  const int nl = s + 1;
+  Leaf* P = &a.leaves[leaf];
+  Leaf* R = &a.leaves[nl];
+  st->leaf = leaf;
+  st->new_leaf = nl;
+  st->split = sp;
+  st->part_begin = P->begin;
+  st->part_count = P->count;
+  st->src_buf = P->buf;
+  st->cur_left = 0;
+  st->cur_right = 0;
+  st->sfeat = a.feat[sp.feature];
+  SplitRecord& rec = a.rec[s];
+  rec.leaf = leaf;
+  rec.split = sp;
+  rec.left_count = sp.left_count;
+  rec.right_count = sp.right_count;
+  // children statistics (left keeps the leaf id); ranges are set by the partition
+  const int depth = P->depth + 1;
+  st->child_depth = depth;
+  double pmin = P->cmin, pmax = P->cmax, rmin = P->cmin, rmax = P->cmax;
+  if (!sp.is_categorical) {
+    const double mid = (sp.left_output + sp.right_output) / 2.0f;
+    if (sp.monotone_type < 0) {
+      pmin = fmax(pmin, mid);
+      rmax = fmin(rmax, mid);
+    } else if (sp.monotone_type > 0) {
+      pmax = fmin(pmax, mid);
+      rmin = fmax(rmin, mid);
+    }
+  }
+  R->depth = depth;
+  R->sum_g = sp.right_sum_gradient;
+  R->sum_h = sp.right_sum_hessian;
+  R->output = sp.right_output;
+  R->global_count = sp.right_count;
+  R->cmin = rmin;
+  R->cmax = rmax;
+  P->depth = depth;
+  P->sum_g = sp.left_sum_gradient;
+  P->sum_h = sp.left_sum_hessian;
+  P->output = sp.left_output;
+  P->global_count = sp.left_count;
+  P->cmin = pmin;
+  P->cmax = pmax;
+}
+
+static size_t FindLds(const KArgs& a) {
+  return a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
+}
 void FindRoot(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_find<true>, dim3(a.p.num_features, 1), dim3(kWave), 0, s, a);
+  hipLaunchKernelGGL(k_find<true>, dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
 }
 void FindStep(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_find<false>, dim3(a.p.num_features, 2), dim3(kWave), 0, s, a);
+  hipLaunchKernelGGL(k_find<false>, dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
 }
+void PickRoot(const KArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_pick<true>, dim3(1), dim3(kWave), 0, s, a); }
+void PickStep(const KArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_pick<false>, dim3(1), dim3(kWave), 0, s, a); }
 
 }  // namespace dev
 }  // namespace lgbm_amd

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -31,17 +32,6 @@ int PickDevice(const Config* cfg) {
   const char* lr = std::getenv("LOCAL_RANK");
   if (lr != nullptr) return std::atoi(lr) % count;
   return 0;
-}
-
-int PartBlocks(int count, int* rpb_out) {
-  int nb = (count + 4095) / 4096;
-  nb = std::max(1, std::min(dev::kMaxPartBlocks, nb));
-  int rpb = (count + nb - 1) / nb;
-  rpb = ((rpb + 255) / 256) * 256;
-  if (rpb == 0) rpb = 256;
-  nb = std::max(1, (count + rpb - 1) / rpb);
-  *rpb_out = rpb;
-  return nb;
 }
 
 }  // namespace
@@ -75,6 +65,7 @@ T* GPUTreeLearner::Alloc(size_t n) {
 }
 
 void GPUTreeLearner::FreeBuffers() {
+  DestroyGraph();
   for (void* p : allocs_) (void)hipFree(p);
   allocs_.clear();
   for (void** hp : {reinterpret_cast<void**>(&h_mask_), reinterpret_cast<void**>(&h_rec_),
@@ -184,6 +175,7 @@ void GPUTreeLearner::UploadData() {
   }
   d_feat_ = Alloc<dev::Feature>(num_features_);
   HIPCHECK(hipMemcpy(d_feat_, feats.data(), sizeof(dev::Feature) * num_features_, hipMemcpyHostToDevice));
+  h_feats_ = feats;
   std::vector<int32_t> goff(std::max(1, num_groups_), 0);
   for (int g = 0; g < num_groups_; ++g) goff[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
   d_group_off_ = Alloc<int32_t>(goff.size());
@@ -206,7 +198,7 @@ void GPUTreeLearner::UploadData() {
   if (const char* e = std::getenv("LGBM_AMD_HIST_TILE_WORDS")) max_tw = std::max(1, std::atoi(e));
   int tile_words = 0;
   for (int limit : {8192, 16384}) {
-    for (int tw = std::min({wpr, dev::kHistBlockThreads, max_tw}); tw >= 1; --tw) {
+    for (int tw = std::min({wpr, dev::kHistThreads, max_tw}); tw >= 1; --tw) {
       if (tile_bins_for(tw) <= limit) {
         tile_words = tw;
         break;
@@ -231,9 +223,8 @@ void GPUTreeLearner::UploadData() {
   d_scales_ = Alloc<double>(4);
   d_absmax_ = Alloc<uint32_t>(4);
   d_feat_best_ = Alloc<dev::FeatureBest>(2 * static_cast<size_t>(std::max(1, num_features_)));
-  d_tickets_ = Alloc<int32_t>(2);
-  HIPCHECK(hipMemset(d_tickets_, 0, sizeof(int32_t) * 2));
-  d_blk_ = Alloc<int32_t>(dev::kMaxPartBlocks);
+  const int hist_blocks = dev::HistGridBlocks();
+  d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_);
   d_root_ = Alloc<double>(4);
   d_leaf_values_ = Alloc<double>(n_leaves);
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_mask_), std::max(1, num_features_), hipHostMallocDefault));
@@ -267,7 +258,8 @@ void GPUTreeLearner::UploadData() {
   a.best = d_best_;
   a.hist = d_hist_;
   a.scratch = d_scratch_;
-  a.blk = d_blk_;
+  a.partials = d_partials_;
+  a.hist_max_blocks = hist_blocks;
   a.root = d_root_;
   a.num_rows = num_data_;
   a.root_identity = 1;
@@ -280,12 +272,12 @@ void GPUTreeLearner::UploadData() {
   a.scales = d_scales_;
   a.bins_col = d_bins_col_;
   a.num_data = num_data_;
-  a.pad2 = 0;
   a.feat_best = d_feat_best_;
-  a.tickets = d_tickets_;
-  // per-workgroup row cap of the histogram kernels (fixed-point headroom): see HistBody
-  const int grid = dev::HistGridBlocks();
-  rows_cap_ = std::max(4096, (num_data_ + grid - 1) / grid);
+  int max_fb = 1;
+  for (const auto& F : feats) max_fb = std::max(max_fb, F.num_bin - F.offset);
+  a.p.max_feature_bins = max_fb;
+  // per-workgroup row cap of the histogram kernels (fixed-point headroom): see k_hist
+  rows_cap_ = std::max(dev::kHistMinRows * 4, (num_data_ + hist_blocks - 1) / hist_blocks);
   a.hist_rows_cap = rows_cap_;
 }
 
@@ -302,6 +294,7 @@ void GPUTreeLearner::ResetTrainingData(const Dataset* train_data, bool is_consta
 void GPUTreeLearner::ResetConfig(const Config* config) {
   const int old_leaves = config_->num_leaves;
   SerialTreeLearner::ResetConfig(config);
+  DestroyGraph();  // kernel arguments are baked into the captured graph
   args_.p.sp = params_;
   args_.p.max_depth = config_->max_depth;
   args_.p.monotone_penalty = config_->monotone_penalty;
@@ -332,6 +325,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     feats[f].penalty = meta_[f].penalty;
   }
   HIPCHECK(hipMemcpy(d_feat_, feats.data(), sizeof(dev::Feature) * num_features_, hipMemcpyHostToDevice));
+  h_feats_ = feats;
 }
 
 void GPUTreeLearner::DecideMode() {
@@ -429,21 +423,44 @@ void GPUTreeLearner::AllreduceAbsMax() {
   HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 3, hipMemcpyHostToDevice, stream_));
 }
 
-Tree* GPUTreeLearner::TrainDeviceMode() {
-  col_sampler_.ResetByTree();
-  const auto& mask = col_sampler_.is_feature_used_bytree();
-  for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
-  HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
-  dev::KArgs a = args_;
+// diagnostics (LGBM_AMD_KERNEL_PROBE=1): the tree is finished (Step::done), so every step
+// kernel exits after reading the Step record; time N back-to-back launches of each
+void GPUTreeLearner::KernelFloorProbe(const dev::KArgs& a) {
+  hipEvent_t e0, e1;
+  HIPCHECK(hipEventCreate(&e0));
+  HIPCHECK(hipEventCreate(&e1));
+  const int n = 500;
+  struct P {
+    const char* name;
+    void (*fn)(const dev::KArgs&, hipStream_t);
+  };
+  const P probes[] = {{"partition", dev::Partition}, {"hist+reduce", dev::HistStep}, {"find", dev::FindStep},
+                      {"pick", dev::PickStep}};
+  for (const P& p : probes) {
+    for (int i = 0; i < 20; ++i) p.fn(a, stream_);
+    HIPCHECK(hipEventRecord(e0, stream_));
+    for (int i = 0; i < n; ++i) p.fn(a, stream_);
+    HIPCHECK(hipEventRecord(e1, stream_));
+    HIPCHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+    std::fprintf(stderr, "kernel probe %-12s %.2f us per launch (tree done: early exit)\n", p.name, 1000.f * ms / n);
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+}
+
+void GPUTreeLearner::DestroyGraph() {
+  if (graph_exec_ != nullptr) (void)hipGraphExecDestroy(graph_exec_);
+  graph_exec_ = nullptr;
+}
+
+// the whole tree as a stream-ordered kernel sequence (no host synchronisation inside)
+void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   if (use_bag_) {
     HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * bag_cnt_, hipMemcpyDeviceToDevice, stream_));
-    a.num_rows = bag_cnt_;
-    a.root_identity = 0;
-  } else {
-    a.num_rows = num_data_;
-    a.root_identity = 1;
   }
-  root_rows_ = a.num_rows;
+  HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
   // both step buffers start at zero; afterwards each split-scan zeroes the next one
   const size_t scratch_bytes = sizeof(long long) * 4 * static_cast<size_t>(total_bins_);
   dev::TreeBegin(a, stream_);
@@ -453,18 +470,61 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   dev::HistRoot(a, stream_);
   AllreduceScratch(0);
   dev::FindRoot(a, stream_);
+  dev::PickRoot(a, stream_);
+  // one split per step: partition -> smaller child's histogram -> split scans of both
+  // children -> next split.  The sequence is fixed; kernels of finished trees exit early.
   for (int s = 0; s < config_->num_leaves - 1; ++s) {
-    dev::SelectAndCount(a, stream_);
-    dev::PartitionScatter(a, stream_);
+    dev::Partition(a, stream_);
     dev::HistStep(a, stream_);
-    AllreduceScratch(s + 1);  // the step's buffer parity (Step::step after the scatter)
+    AllreduceScratch(s + 1);  // the step's buffer parity
     dev::FindStep(a, stream_);
+    dev::PickStep(a, stream_);
+  }
+}
+
+Tree* GPUTreeLearner::TrainDeviceMode() {
+  col_sampler_.ResetByTree();
+  const auto& mask = col_sampler_.is_feature_used_bytree();
+  for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
+  dev::KArgs a = args_;
+  if (use_bag_) {
+    a.num_rows = bag_cnt_;
+    a.root_identity = 0;
+  } else {
+    a.num_rows = num_data_;
+    a.root_identity = 1;
+  }
+  root_rows_ = a.num_rows;
+  // single process: the tree's fixed kernel sequence (~5 launches per split) is replayed
+  // from a hipGraph -- eager launches are host-bound at ~4 us each, longer than most of
+  // these kernels; with collectives between the kernels it is launched eagerly
+  const bool distributed = data_parallel_ && Network::num_machines() > 1;
+  const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
+  const bool use_graph = !distributed && !(ng != nullptr && ng[0] == '1');
+  if (use_graph) {
+    if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity) {
+      DestroyGraph();
+      hipGraph_t g = nullptr;
+      HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+      EnqueueTree(a);
+      HIPCHECK(hipStreamEndCapture(stream_, &g));
+      HIPCHECK(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
+      HIPCHECK(hipGraphDestroy(g));
+      graph_rows_ = a.num_rows;
+      graph_identity_ = a.root_identity;
+    }
+    HIPCHECK(hipGraphLaunch(graph_exec_, stream_));
+  } else {
+    EnqueueTree(a);
   }
   HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
                           hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   const int num_splits = h_step_->step;
+  if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {
+    if (kp[0] == '1') KernelFloorProbe(a);
+  }
   const bool track = !config_->interaction_constraints_vector.empty();
   std::unique_ptr<Tree> tree(new Tree(config_->num_leaves, track));
   for (int s = 0; s < num_splits; ++s) {
@@ -532,7 +592,7 @@ void GPUTreeLearner::BuildRangeHistogram(int leaf, int slot) {
   a.num_rows = leaf_count_[leaf];
   const size_t n = 2 * static_cast<size_t>(total_bins_);
   HIPCHECK(hipMemsetAsync(d_scratch_, 0, sizeof(long long) * n, stream_));
-  if (a.num_rows > 0) dev::HistRange(a, stream_);
+  if (a.num_rows > 0) dev::HistRange(a, stream_);  // partials + reduction into scratch buffer 0
   std::vector<long long> h(n);
   HIPCHECK(hipMemcpyAsync(h.data(), d_scratch_, sizeof(long long) * n, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipMemcpyAsync(h_scales_, d_scales_, sizeof(double) * 4, hipMemcpyDeviceToHost, stream_));
@@ -561,21 +621,19 @@ data_size_t GPUTreeLearner::PartitionLeaf(int leaf, int inner, const SplitInfo& 
   st.new_leaf = new_leaf;
   st.part_begin = begin;
   st.part_count = cnt;
-  int rpb = 0;
-  st.num_blocks = PartBlocks(cnt, &rpb);
-  st.rows_per_block = rpb;
+  st.src_buf = 0;  // host mode keeps every leaf in buffer 0 (copied back below)
   SplitInfo si = s;
   si.inner_feature = inner;
   si.ToDevice(&st.split, data_->FeatureBinMapper(inner)->bin_type() == BinType::Categorical);
+  st.sfeat = h_feats_[inner];
   HIPCHECK(hipMemcpyAsync(d_step_, h_step_, sizeof(dev::Step), hipMemcpyHostToDevice, stream_));
-  dev::PartitionCount(args_, stream_);
-  dev::PartitionScatter(args_, stream_);
+  dev::Partition(args_, stream_);
   if (cnt > 0) {
     HIPCHECK(hipMemcpyAsync(d_idx_ + begin, d_tmp_ + begin, sizeof(int32_t) * cnt, hipMemcpyDeviceToDevice, stream_));
   }
   HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
-  const data_size_t left = h_step_->total_left;
+  const data_size_t left = h_step_->cur_left;
   leaf_count_[leaf] = left;
   leaf_begin_[new_leaf] = begin + left;
   leaf_count_[new_leaf] = cnt - left;
@@ -598,14 +656,28 @@ void GPUTreeLearner::DownloadPartitionToHost() const {
   if (host_partition_fresh_) return;
   auto* self = const_cast<GPUTreeLearner*>(this);
   const int L = config_->num_leaves;
+  if (!device_mode_) {
+    // host-assisted growth keeps the partition in buffer 0 and its ranges on the host
+    HIPCHECK(hipMemcpyAsync(self->indices_.data(), d_idx_, sizeof(int32_t) * root_rows_, hipMemcpyDeviceToHost,
+                            stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
+    host_partition_fresh_ = true;
+    return;
+  }
   std::vector<dev::Leaf> leaves(L);
   HIPCHECK(hipMemcpyAsync(leaves.data(), d_leaves_, sizeof(dev::Leaf) * L, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipMemcpyAsync(self->indices_.data(), d_idx_, sizeof(int32_t) * root_rows_, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
+  // each leaf's rows sit in the index buffer its last split wrote (Leaf::buf)
+  const int num_leaves_now = h_step_->step + 1;
   for (int l = 0; l < L; ++l) {
     self->leaf_begin_[l] = leaves[l].begin;
-    self->leaf_count_[l] = leaves[l].count;
+    self->leaf_count_[l] = l < num_leaves_now ? leaves[l].count : 0;
+    if (self->leaf_count_[l] <= 0) continue;
+    const int32_t* srcbuf = leaves[l].buf ? d_tmp_ : d_idx_;
+    HIPCHECK(hipMemcpyAsync(self->indices_.data() + leaves[l].begin, srcbuf + leaves[l].begin,
+                            sizeof(int32_t) * leaves[l].count, hipMemcpyDeviceToHost, stream_));
   }
+  HIPCHECK(hipStreamSynchronize(stream_));
   host_partition_fresh_ = true;
 }
 

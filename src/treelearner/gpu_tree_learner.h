@@ -74,6 +74,9 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void FreeBuffers();
   void DecideMode();
   Tree* TrainDeviceMode();
+  void EnqueueTree(const dev::KArgs& a);
+  void DestroyGraph();
+  void KernelFloorProbe(const dev::KArgs& a);
   void BuildRangeHistogram(int leaf, int slot);
   void DownloadPartitionToHost() const;
   void AllreduceScratch(int parity);
@@ -108,11 +111,14 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   uint32_t* d_absmax_ = nullptr;
   uint8_t* d_bins_col_ = nullptr;
   dev::FeatureBest* d_feat_best_ = nullptr;
-  int32_t* d_tickets_ = nullptr;
   uint32_t* h_absmax_ = nullptr;
   double* h_scales_ = nullptr;
   int rows_cap_ = 4096;
-  int32_t* d_blk_ = nullptr;
+  unsigned long long* d_partials_ = nullptr;  // per-workgroup partial histograms
+  std::vector<dev::Feature> h_feats_;          // host copy of the feature records
+  hipGraphExec_t graph_exec_ = nullptr;        // captured tree (single-process device mode)
+  int graph_rows_ = -1;
+  int graph_identity_ = -1;
   double* d_root_ = nullptr;
   double* d_score_ = nullptr;
   float* d_grad_ = nullptr;
