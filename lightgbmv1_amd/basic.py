@@ -1126,7 +1126,10 @@ class Dataset(object):
         if weight is not None and np.all(weight == 1):
             weight = None
         self.weight = weight
-        if self.handle is not None and weight is not None:
+        if self.handle is not None:
+            if weight is None:
+                self.set_field("weight", None)  # clears the native weights
+                return self
             weight = list_to_1d_numpy(weight, name="weight")
             self.set_field("weight", weight)
             self.weight = self.get_field("weight")  # original values can be modified at cpp side
@@ -1135,7 +1138,9 @@ class Dataset(object):
     def set_init_score(self, init_score):
         """Set init score of Booster to start from."""
         self.init_score = init_score
-        if self.handle is not None and init_score is not None:
+        if self.handle is not None and init_score is None:
+            self.set_field("init_score", None)
+        elif self.handle is not None:
             init_score = list_to_1d_numpy(init_score, np.float64, name="init_score")
             self.set_field("init_score", init_score)
             self.init_score = self.get_field("init_score")  # original values can be modified at cpp side
@@ -1667,6 +1672,20 @@ class Booster(object):
         self.__num_class = out_num_class.value
         self.pandas_categorical = _load_pandas_categorical(model_str=model_str)
         return self
+
+    def model_to_if_else(self, num_iteration=None):
+        """Standalone C++ source of the model (the CLI's convert_model task).
+
+        The generated file defines ``extern "C"`` ``lgbm_predict_raw(const double* row,
+        double* out)`` and ``lgbm_predict_leaf``; compile it into any program to score rows
+        without this library.
+        """
+        if num_iteration is None:
+            num_iteration = self.best_iteration
+        with _TempFile() as f:
+            _safe_call(_load_lib().LGBM_AMD_BoosterSaveModelToIfElse(self.handle, ctypes.c_int(num_iteration),
+                                                                     c_str(f.name)))
+            return "".join(f.readlines())
 
     def model_to_string(self, num_iteration=None, start_iteration=0, importance_type="split"):
         """Save Booster to string."""

@@ -254,7 +254,11 @@ class Booster {
     boosting_.reset(GBDT::CreateBoosting(config_.boosting, nullptr));
     train_data_ = train;
     CreateObjectiveAndMetrics();
-    if (config_.tree_learner == "feature") Log::Fatal("Do not support feature parallel in c api");
+    // feature-parallel needs the same full dataset on every rank (the reference refuses it in
+    // the C API, c_api.cpp:133; here the caller is trusted to pass identical data)
+    if (config_.tree_learner == "feature" && Network::num_machines() > 1) {
+      Log::Info("feature-parallel training: every rank must hold the same rows");
+    }
     if (Network::num_machines() == 1 && config_.tree_learner != "serial") {
       Log::Warning("Only find one worker, will switch to serial tree learner");
       config_.tree_learner = "serial";

@@ -98,38 +98,39 @@ __device__ __forceinline__ long long* StepScratch(const KArgs& a, int parity) {
   return a.scratch + static_cast<size_t>(parity & 1) * 2 * a.p.total_bins;
 }
 
-// outcome of the step's partition, derived from the Step record alone (every histogram
-// workgroup computes it; the first one also stores it): children ranges, which child is
-// histogrammed (smaller) and whether the children are searched at all
-struct ChildInfo {
-  int total_left;
-  int left_count, right_count;     // global counts (== local ones without data-parallel)
-  int smaller, larger;             // leaf ids
-  int skip;
-  int s_begin, s_count, buf;       // the smaller child's local rows
-};
-
 // a step histogram with this many row blocks is summed by the split scan itself (the
 // reduce kernel skips it); data-parallel training always reduces (the all-reduce needs it)
 __device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk) {
   return !a.p.data_parallel && nblk <= kReduceChunk;
 }
 
+// outcome of the step's partition, derived from Step::cs and the final cursors (every
+// histogram workgroup computes it; one also stores it in Step for the later kernels)
+struct ChildInfo {
+  int total_left;
+  int left_count, right_count;  // global counts (== local ones without data-parallel)
+  int smaller, larger;          // leaf ids
+  int small_is_left;
+  int skip;
+  int s_begin, s_count, buf;    // the smaller child's local rows
+};
+
 __device__ __forceinline__ ChildInfo StepChildren(const KArgs& a, const Step* st) {
   ChildInfo c;
-  const int pb = st->part_begin, pc = st->part_count;
+  const CurSplit& cs = st->cs;
+  const int pb = cs.part_begin, pc = cs.part_count;
   c.total_left = st->cur_left;
-  c.left_count = a.p.data_parallel ? st->split.left_count : c.total_left;
-  c.right_count = a.p.data_parallel ? st->split.right_count : pc - c.total_left;
+  c.left_count = a.p.data_parallel ? cs.split.left_count : c.total_left;
+  c.right_count = a.p.data_parallel ? cs.split.right_count : pc - c.total_left;
   const int md = a.p.sp.min_data_in_leaf;
-  c.skip = (a.p.max_depth > 0 && st->child_depth >= a.p.max_depth) ||
-           (c.right_count < 2 * md && c.left_count < 2 * md) || (st->step + 1 >= a.p.num_leaves - 1);
-  const bool left_smaller = c.left_count < c.right_count;
-  c.smaller = left_smaller ? st->leaf : st->new_leaf;
-  c.larger = left_smaller ? st->new_leaf : st->leaf;
-  c.s_begin = left_smaller ? pb : pb + c.total_left;
-  c.s_count = left_smaller ? c.total_left : pc - c.total_left;
-  c.buf = 1 - st->src_buf;
+  c.skip = (a.p.max_depth > 0 && cs.child_depth >= a.p.max_depth) ||
+           (c.right_count < 2 * md && c.left_count < 2 * md) || (cs.s + 1 >= a.p.num_leaves - 1);
+  c.small_is_left = c.left_count < c.right_count;
+  c.smaller = c.small_is_left ? cs.leaf : cs.new_leaf;
+  c.larger = c.small_is_left ? cs.new_leaf : cs.leaf;
+  c.s_begin = c.small_is_left ? pb : pb + c.total_left;
+  c.s_count = c.small_is_left ? c.total_left : pc - c.total_left;
+  c.buf = 1 - cs.src_buf;
   return c;
 }
 

@@ -62,26 +62,41 @@ struct Leaf {
   double cmin, cmax;  // monotone constraint range
 };
 
-// one split step (split index `step`).  The pick kernel writes the split to apply (leaf ..
-// child_depth), the partition kernel moves the rows (cursors), the histogram kernel's first
-// workgroup derives the children's ranges, smaller/larger and skip_find from them, which
-// the reduce / split-scan / pick kernels of the step read.
+// a child's statistics as known from its parent's split (plus, once the partition is done,
+// its histogram slot)
+struct ChildStats {
+  double sum_g, sum_h, output, cmin, cmax;
+  int32_t global_count, depth, slot, leaf;
+};
+
+// the split being applied, as chosen by the partition kernel's pick
+struct CurSplit {
+  int32_t s;            // split index
+  int32_t leaf, new_leaf;
+  int32_t part_begin, part_count;  // the leaf's rows before the split
+  int32_t src_buf;      // index buffer holding them (the children go to the other one)
+  int32_t child_depth;
+  int32_t parent_slot;  // histogram slot of the leaf (the new leaf's slot is its own id)
+  Feature feat;         // the split feature's record
+  DeviceSplit split;
+};
+
+// per-tree control record.  Each field is written by one kernel of a step and only read by
+// later kernels (never by the writing kernel's other workgroups):
+//   partition: cs, lr (and done)        hist: smaller .. child, nsplit, fresh
+//   partition (atomics): cursors        reduce: cursor reset for the next split
 struct Step {
   int32_t done;       // tree finished: every later kernel of the tree exits
-  int32_t step;       // index of the split being applied (when done: splits applied)
-  int32_t leaf;       // leaf being split (keeps its id as the left child)
-  int32_t new_leaf;   // right child id
+  int32_t nsplit;     // splits applied (= index of the next split)
+  int32_t fresh;      // leaves with new per-feature results in feat_best: 0, 1 (root), 2
   int32_t smaller, larger;
   int32_t skip_find;  // children can not be split further (depth / min_data / last split)
-  int32_t child_depth;
-  int32_t part_begin;  // range of the leaf being split, before the split
-  int32_t part_count;
-  int32_t src_buf;     // index buffer holding the parent's rows (children go to the other)
-  int32_t cur_left;    // partition cursors: rows placed on the left / right so far
-  int32_t cur_right;
-  int32_t pad;
-  Feature sfeat;       // the split feature's record (saves the partition a dependent load)
-  DeviceSplit split;
+  int32_t total_left;
+  int32_t s_begin, s_count, s_buf;  // the histogrammed (smaller) child's rows
+  int32_t cur_left, cur_right;      // partition cursors: rows placed left / right so far
+  CurSplit cs;
+  ChildStats lr[2];     // left / right child of cs
+  ChildStats child[2];  // smaller / larger child of cs, with histogram slots
 };
 
 // best threshold of one feature for one leaf (output of one split-scan wave)

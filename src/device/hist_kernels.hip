@@ -41,9 +41,12 @@ __device__ __forceinline__ void AddRow(unsigned long long* lds, const int* goff,
   }
 }
 
-// rows of the histogram: MODE 0 root, 1 smaller child of the step, 2 explicit range
+// rows of the histogram: MODE 0 root, 1 smaller child of the step, 2 explicit range.
+// MODE 1 derives them from the partition's result (StepChildren); the reduce kernel (MODE
+// 1, after the histogram kernel's bookkeeping) passes from_step to read the stored copy.
 template <int MODE>
-__device__ __forceinline__ bool HistRows(const KArgs& a, int* begin, int* count, const int32_t** src) {
+__device__ __forceinline__ bool HistRows(const KArgs& a, bool from_step, int* begin, int* count,
+                                         const int32_t** src) {
   if (MODE == 0) {
     *begin = 0;
     *count = a.num_rows;
@@ -55,21 +58,30 @@ __device__ __forceinline__ bool HistRows(const KArgs& a, int* begin, int* count,
   } else {
     const Step* st = a.st;
     if (st->done) return false;
-    const ChildInfo c = StepChildren(a, st);
-    if (c.skip) return false;
-    *begin = c.s_begin;
-    *count = c.s_count;
-    *src = c.buf ? a.tmp : a.idx;
+    if (from_step) {
+      if (st->skip_find) return false;
+      *begin = st->s_begin;
+      *count = st->s_count;
+      *src = st->s_buf ? a.tmp : a.idx;
+    } else {
+      const ChildInfo c = StepChildren(a, st);
+      if (c.skip) return false;
+      *begin = c.s_begin;
+      *count = c.s_count;
+      *src = c.buf ? a.tmp : a.idx;
+    }
   }
   return *count > 0;
 }
 
-// the step's bookkeeping (one thread, first histogram workgroup): children ranges and
-// counts, histogram-slot hand-over to the larger child, split records, best[] reset
+// the step's bookkeeping (one thread of the histogram kernel): children ranges and counts,
+// histogram-slot hand-over to the larger child, split records, best[] reset, and the
+// smaller / larger children's records for the split scans
 __device__ void StepBookkeeping(const KArgs& a, Step* st) {
   const ChildInfo c = StepChildren(a, st);
-  const int leaf = st->leaf, nl = st->new_leaf;
-  const int pb = st->part_begin, pc = st->part_count;
+  const CurSplit& cs = st->cs;
+  const int leaf = cs.leaf, nl = cs.new_leaf;
+  const int pb = cs.part_begin, pc = cs.part_count;
   Leaf* P = &a.leaves[leaf];
   Leaf* R = &a.leaves[nl];
   P->begin = pb;
@@ -81,15 +93,30 @@ __device__ void StepBookkeeping(const KArgs& a, Step* st) {
   if (!a.p.data_parallel) {
     P->global_count = c.left_count;
     R->global_count = c.right_count;
-    SplitRecord& rec = a.rec[st->step];
+    SplitRecord& rec = a.rec[cs.s];
     rec.left_count = c.left_count;
     rec.right_count = c.right_count;
   }
-  if (!c.skip && c.smaller == leaf) {
+  const bool swap = !c.skip && c.small_is_left;
+  if (swap) {
     // the parent's histogram stays with the larger (right) child
-    const int t = P->slot;
-    P->slot = R->slot;
-    R->slot = t;
+    P->slot = nl;
+    R->slot = cs.parent_slot;
+  }
+  // smaller / larger child records for the split scans (field-wise: no private copies)
+  for (int k = 0; k < 2; ++k) {
+    const int lr = (k == 0) == (c.small_is_left != 0) ? 0 : 1;  // k: 0 smaller, 1 larger
+    const ChildStats& from = st->lr[lr];
+    ChildStats& to = st->child[k];
+    to.sum_g = from.sum_g;
+    to.sum_h = from.sum_h;
+    to.output = from.output;
+    to.cmin = from.cmin;
+    to.cmax = from.cmax;
+    to.depth = from.depth;
+    to.leaf = from.leaf;
+    to.global_count = a.p.data_parallel ? from.global_count : (lr == 0 ? c.left_count : c.right_count);
+    to.slot = swap ? (lr == 0 ? nl : cs.parent_slot) : from.slot;
   }
   a.best[leaf].gain = -INFINITY;
   a.best[leaf].feature = -1;
@@ -100,6 +127,12 @@ __device__ void StepBookkeeping(const KArgs& a, Step* st) {
   st->smaller = c.smaller;
   st->larger = c.larger;
   st->skip_find = c.skip;
+  st->total_left = c.total_left;
+  st->s_begin = c.s_begin;
+  st->s_count = c.s_count;
+  st->s_buf = c.buf;
+  st->fresh = c.skip ? 0 : 2;
+  st->nsplit = cs.s + 1;
 }
 
 }  // namespace
@@ -170,7 +203,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(KArgs a) {
   }
   int begin, count;
   const int32_t* src;
-  if (!HistRows<MODE>(a, &begin, &count, &src)) return;
+  if (!HistRows<MODE>(a, false, &begin, &count, &src)) return;
   const int nblk = HistBlocksFor(count, a.hist_max_blocks, a.hist_rows_cap);
   const int chunk = (count + nblk - 1) / nblk;
   const int w0 = blockIdx.y * a.tile_words;
@@ -192,9 +225,14 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(KArgs a) {
 // int64 atomics into the (pre-zeroed) buffer, otherwise the single chunk stores directly.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
+  if (MODE == 1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    // the partition cursors are final (read by the histogram kernel): reset for the next split
+    a.st->cur_left = 0;
+    a.st->cur_right = 0;
+  }
   int begin, count;
   const int32_t* src;
-  if (!HistRows<MODE>(a, &begin, &count, &src)) return;
+  if (!HistRows<MODE>(a, true, &begin, &count, &src)) return;
   const int nblk = HistBlocksFor(count, a.hist_max_blocks, a.hist_rows_cap);
   if (MODE == 1 && DirectPartials(a, nblk)) return;  // summed by the split scan
   const int k0 = blockIdx.y * kReduceChunk;
@@ -213,7 +251,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
     g += static_cast<long long>(v[k]) >> 32;  // h (low half) is non-negative: no borrow
     h += static_cast<long long>(v[k] & 0xffffffffull);
   }
-  long long* out = MODE == 1 ? StepScratch(a, a.st->step + 1) : a.scratch;
+  long long* out = MODE == 1 ? StepScratch(a, a.st->cs.s + 1) : a.scratch;
   if (nblk <= kReduceChunk) {
     out[2 * bin] = g;
     out[2 * bin + 1] = h;

@@ -46,7 +46,7 @@ struct KArgs {
   int32_t hist_max_blocks;   // row blocks of a histogram (partials capacity)
   const uint8_t* bins_col;   // column-major copy of the bin matrix ([group][rows], bin_bytes each)
   int32_t num_data;          // rows of the matrix (column stride of bins_col)
-  int32_t pad2;
+  int32_t host_mode;         // partition: the host wrote Step::cs (host-assisted growth)
   FeatureBest* feat_best;    // [2][num_features] per-feature best split of the two leaves
 };
 
@@ -85,10 +85,9 @@ void HistRange(const KArgs& a, hipStream_t s);  // rows idx[range_begin, +num_ro
 // split scans of the root / the two children of the step (per-feature results)
 void FindRoot(const KArgs& a, hipStream_t s);
 void FindStep(const KArgs& a, hipStream_t s);
-// per-leaf best split from the per-feature results, then the next split to apply
-void PickRoot(const KArgs& a, hipStream_t s);
-void PickStep(const KArgs& a, hipStream_t s);
-// move the split leaf's rows into the children's ranges (device mode: plus bookkeeping)
+// device mode: pick the next split (per-leaf bests from the per-feature results, argmax
+// over the leaves) and move the leaf's rows into the children's ranges; host mode: apply
+// the split the host wrote into Step::cs
 void Partition(const KArgs& a, hipStream_t s);
 
 // score[k] += value[leaf(row)] for every partitioned row of the finished tree

@@ -98,14 +98,11 @@ __global__ void k_tree_begin(KArgs a) {
   if (threadIdx.x == 0) {
     Step* st = a.st;
     st->done = 0;
-    st->step = 0;
-    st->leaf = 0;
-    st->new_leaf = 0;
+    st->nsplit = 0;
+    st->fresh = 1;  // the root's per-feature results (k_find<true>) are the first pick's input
     st->smaller = 0;
     st->larger = -1;
     st->skip_find = 0;
-    st->child_depth = 0;
-    st->src_buf = 0;
     st->cur_left = st->cur_right = 0;
     a.root[0] = a.root[1] = a.root[2] = 0.0;
   }

@@ -1,14 +1,23 @@
-// Split selection + data partition (reference serial_tree_learner.cpp Train/Split,
-// src/treelearner/data_partition.hpp Split, monotone_constraints.hpp BasicLeafConstraints).
+// Split selection + data partition (reference serial_tree_learner.cpp Train / Split,
+// FindBestSplitsFromHistograms' per-leaf argmax, src/treelearner/data_partition.hpp Split,
+// monotone_constraints.hpp BasicLeafConstraints).
 //
-// k_partition: the split leaf's index range [part_begin, +part_count) of buffer src_buf is
-// moved into the same range of the other buffer, lefts growing up from the front and
-// rights down from the back.  Each 8192-row tile reserves its output slots with one
-// device-scope atomic per side (no grid-wide prefix pass); rows keep their order inside a
-// tile, tiles land in arrival order -- histograms are exact integer sums, so the row order
-// never changes a result.  The cursors' final values are the children's sizes, read by
-// the histogram kernel (StepChildren).  Rows are read from the column-major copy of the
-// split column (1 byte per row).
+// k_partition, device mode, split s:
+//  1. pick (first wave of every workgroup, redundantly -- no extra launch, no cross-
+//     workgroup hand-off): the per-leaf best split of the children that were just scanned
+//     (argmax over their per-feature results, SplitInfo order), then the leaf to split
+//     (argmax over all leaves: higher gain, smaller real feature, lower leaf id -- the host
+//     loop's order).  All loads of the pick are independent of each other (one round trip)
+//     except the winner's records (a second one).  Workgroup 0 records the split (Step::cs,
+//     SplitRecord, children statistics, per-leaf bests).
+//  2. partition: the leaf's index range [begin, +count) of its buffer is moved into the same
+//     range of the other buffer, lefts growing up from the front and rights down from the
+//     back.  Each 8192-row tile reserves its output slots with one device-scope atomic per
+//     side (no grid-wide prefix pass); rows keep their order inside a tile, tiles land in
+//     arrival order -- histograms are exact integer sums, so the row order never changes a
+//     result.  The cursors' final values are the children's sizes (StepChildren).  Rows are
+//     read from the column-major copy of the split column (1 byte per row).
+// Host mode: the host wrote Step::cs; only step 2 runs.
 #include "device_common.h"
 
 namespace lgbm_amd {
@@ -29,24 +38,264 @@ __device__ __forceinline__ void MakeRule(const DeviceSplit& sp, const Feature& f
   }
 }
 
+// argmax over (gain, real feature, index) in SplitInfo order; ties on both -> lower index
+__device__ __forceinline__ void WaveArgBest(double* g, int* rf, int* idx) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(*g, o, kWave);
+    const int orf = __shfl_xor(*rf, o, kWave);
+    const int oi = __shfl_xor(*idx, o, kWave);
+    const bool take = oi >= 0 && (*idx < 0 || SplitBetter(og, orf, *g, *rf) ||
+                                  (!SplitBetter(*g, *rf, og, orf) && oi < *idx));
+    if (take) {
+      *g = og;
+      *rf = orf;
+      *idx = oi;
+    }
+  }
+}
+
+__device__ __forceinline__ void ToDeviceSplit(const FeatureBest& b, DeviceSplit* d) {
+  d->gain = b.gain;
+  d->feature = b.feature;
+  d->real_feature = b.real_feature;
+  d->threshold = b.thr;
+  d->left_count = b.lc;
+  d->right_count = b.rc;
+  d->left_output = b.lo;
+  d->right_output = b.ro;
+  d->left_sum_gradient = b.lg;
+  d->left_sum_hessian = b.lh;
+  d->right_sum_gradient = b.rg;
+  d->right_sum_hessian = b.rh;
+  d->default_left = static_cast<int8_t>(b.default_left);
+  d->monotone_type = static_cast<int8_t>(b.mono);
+  d->is_categorical = 0;
+  d->pad0 = 0;
+  d->num_cat_threshold = 0;
+}
+
+__device__ __forceinline__ void NoSplit(DeviceSplit* d) {
+  d->gain = -INFINITY;
+  d->feature = -1;
+  d->real_feature = -1;
+}
+
+struct PickResult {
+  int done;
+  int s, leaf;
+  int fresh_idx[2];  // winning feature of the fresh children (-1: none)
+  Leaf P;
+  Feature F;
+  DeviceSplit split;
+};
+
+// the pick, by the first wave; the result goes to LDS
+__device__ void PickWave(const KArgs& a, const Step* st, PickResult* out) {
+  const int lane = threadIdx.x;
+  const int L = a.p.num_leaves, NF = a.p.num_features;
+  const int s = st->nsplit;
+  const int fresh = st->fresh;
+  const int sm = st->smaller, lg = st->larger;
+  if (s >= L - 1) {
+    if (lane == 0) {
+      out->done = 1;
+      out->s = s;
+    }
+    return;
+  }
+  // per-leaf bests of the freshly scanned children, from the per-feature results
+  int fi[2] = {-1, -1};
+  double fg[2] = {-INFINITY, -INFINITY};
+  int frf[2] = {-1, -1};
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    if (side >= fresh) continue;
+    const FeatureBest* fb = a.feat_best + side * NF;
+    double g = -INFINITY;
+    int rf = -1, idx = -1;
+    for (int i = lane; i < NF; i += kWave) {
+      const double cg = fb[i].gain;
+      const int crf = fb[i].real_feature;
+      if (fb[i].feature >= 0 && (idx < 0 || SplitBetter(cg, crf, g, rf))) {
+        g = cg;
+        rf = crf;
+        idx = i;
+      }
+    }
+    WaveArgBest(&g, &rf, &idx);
+    if (idx >= 0 && g == -INFINITY) idx = -1;  // no valid threshold on any feature
+    fi[side] = idx;
+    fg[side] = idx >= 0 ? g : -INFINITY;
+    frf[side] = idx >= 0 ? rf : -1;
+  }
+  // the leaf to split: argmax over leaves 0..s (fresh children use the new results)
+  double g = -INFINITY;
+  int rf = -1, leaf = -1;
+  for (int l = lane; l <= s; l += kWave) {
+    double cg;
+    int crf;
+    if (fresh >= 1 && l == sm) {
+      cg = fg[0];
+      crf = frf[0];
+    } else if (fresh == 2 && l == lg) {
+      cg = fg[1];
+      crf = frf[1];
+    } else {
+      cg = a.best[l].gain;
+      crf = a.best[l].real_feature;
+    }
+    if (leaf < 0 || SplitBetter(cg, crf, g, rf)) {
+      g = cg;
+      rf = crf;
+      leaf = l;
+    }
+  }
+  WaveArgBest(&g, &rf, &leaf);
+  if (lane != 0) return;
+  out->s = s;
+  out->leaf = leaf;
+  out->fresh_idx[0] = fi[0];
+  out->fresh_idx[1] = fi[1];
+  DeviceSplit* sp = &out->split;  // straight into LDS (no private copy)
+  if (fresh >= 1 && leaf == sm) {
+    if (fi[0] >= 0) ToDeviceSplit(a.feat_best[fi[0]], sp);
+    else NoSplit(sp);
+  } else if (fresh == 2 && leaf == lg) {
+    if (fi[1] >= 0) ToDeviceSplit(a.feat_best[NF + fi[1]], sp);
+    else NoSplit(sp);
+  } else {
+    *sp = a.best[leaf];
+  }
+  if (!(sp->gain > 0.0) || sp->feature < 0) {
+    out->done = 1;
+    return;
+  }
+  out->done = 0;
+  out->P = a.leaves[leaf];
+  out->F = a.feat[sp->feature];
+}
+
+// workgroup 0, one thread: record the split for the later kernels and future picks
+__device__ void RecordSplit(const KArgs& a, Step* st, const PickResult& pk) {
+  const int fresh = st->fresh;
+  const int NF = a.p.num_features;
+  // the fresh children's bests become part of the per-leaf table
+  for (int side = 0; side < fresh; ++side) {
+    const int l = side == 0 ? st->smaller : st->larger;
+    DeviceSplit& d = a.best[l];
+    if (pk.fresh_idx[side] >= 0) ToDeviceSplit(a.feat_best[side * NF + pk.fresh_idx[side]], &d);
+    else NoSplit(&d);
+  }
+  const int s = pk.s, leaf = pk.leaf, nl = s + 1;
+  const DeviceSplit& sp = pk.split;
+  SplitRecord& rec = a.rec[s];
+  rec.leaf = leaf;
+  rec.split = sp;
+  rec.left_count = sp.left_count;
+  rec.right_count = sp.right_count;
+  // children statistics (left keeps the leaf id); ranges are set after the partition
+  const Leaf& P = pk.P;
+  const int depth = P.depth + 1;
+  double pmin = P.cmin, pmax = P.cmax, rmin = P.cmin, rmax = P.cmax;
+  if (!sp.is_categorical) {
+    const double mid = (sp.left_output + sp.right_output) / 2.0f;
+    if (sp.monotone_type < 0) {
+      pmin = fmax(pmin, mid);
+      rmax = fmin(rmax, mid);
+    } else if (sp.monotone_type > 0) {
+      pmax = fmin(pmax, mid);
+      rmin = fmax(rmin, mid);
+    }
+  }
+  ChildStats lc, rc;
+  lc.sum_g = sp.left_sum_gradient;
+  lc.sum_h = sp.left_sum_hessian;
+  lc.output = sp.left_output;
+  lc.cmin = pmin;
+  lc.cmax = pmax;
+  lc.global_count = sp.left_count;
+  lc.depth = depth;
+  lc.slot = P.slot;
+  lc.leaf = leaf;
+  rc.sum_g = sp.right_sum_gradient;
+  rc.sum_h = sp.right_sum_hessian;
+  rc.output = sp.right_output;
+  rc.cmin = rmin;
+  rc.cmax = rmax;
+  rc.global_count = sp.right_count;
+  rc.depth = depth;
+  rc.slot = nl;  // a new leaf's slot is its own id (k_tree_begin)
+  rc.leaf = nl;
+  Leaf* PL = &a.leaves[leaf];
+  Leaf* RL = &a.leaves[nl];
+  PL->depth = depth;
+  PL->sum_g = lc.sum_g;
+  PL->sum_h = lc.sum_h;
+  PL->output = lc.output;
+  PL->global_count = lc.global_count;
+  PL->cmin = pmin;
+  PL->cmax = pmax;
+  RL->depth = depth;
+  RL->sum_g = rc.sum_g;
+  RL->sum_h = rc.sum_h;
+  RL->output = rc.output;
+  RL->global_count = rc.global_count;
+  RL->cmin = rmin;
+  RL->cmax = rmax;
+  st->lr[0] = lc;
+  st->lr[1] = rc;
+  CurSplit& cs = st->cs;
+  cs.s = s;
+  cs.leaf = leaf;
+  cs.new_leaf = nl;
+  cs.part_begin = P.begin;
+  cs.part_count = P.count;
+  cs.src_buf = P.buf;
+  cs.child_depth = depth;
+  cs.parent_slot = P.slot;
+  cs.feat = pk.F;
+  cs.split = sp;
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(kPartThreads) void k_partition(KArgs a) {
   __shared__ uint32_t cat_bits[kMaxCatWords];
   __shared__ int wl[kPartRowsPerThread][kPartThreads / kWave];
   __shared__ int base[2];
+  __shared__ PickResult pk;
   Step* st = a.st;
   if (st->done) return;
-  const int pb = st->part_begin, pc = st->part_count;
-  const int src_buf = st->src_buf;
+  int pb, pc, src_buf;
+  const DeviceSplit* spp;
+  const Feature* fp;
+  if (a.host_mode) {
+    pb = st->cs.part_begin;
+    pc = st->cs.part_count;
+    src_buf = st->cs.src_buf;
+    spp = &st->cs.split;
+    fp = &st->cs.feat;
+  } else {
+    if (threadIdx.x < kWave) PickWave(a, st, &pk);
+    __syncthreads();
+    if (pk.done) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) st->done = 1;
+      return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) RecordSplit(a, st, pk);
+    pb = pk.P.begin;
+    pc = pk.P.count;
+    src_buf = pk.P.buf;
+    spp = &pk.split;
+    fp = &pk.F;
+  }
   const int32_t* src = src_buf ? a.tmp : a.idx;
   int32_t* dst = src_buf ? a.idx : a.tmp;
   const int ntiles = (pc + kPartTile - 1) / kPartTile;
   if (static_cast<int>(blockIdx.x) >= ntiles) return;
-  const DeviceSplit& sp = st->split;
-  const Feature F = st->sfeat;
+  const Feature F = *fp;
   SplitRule r;
-  MakeRule(sp, F, &r, cat_bits);
+  MakeRule(*spp, F, &r, cat_bits);
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   constexpr int nw = kPartThreads / kWave;

@@ -10,10 +10,7 @@
 // (workgroup prefix sums) with the reference's missing-value handling,
 // min_data / min_hessian filters, hessian-estimated counts, L1 / max_delta_step / path
 // smoothing / monotone constraints.  Ties keep the threshold the sequential scan would
-// keep.  Per-feature results go to feat_best.
-// k_pick (one wave): per-leaf best split over the features (SplitInfo order), then the
-// next leaf to split over all leaves (serial_tree_learner.cpp Train: ArgMax of
-// best_split_per_leaf_), written as the Step the partition kernel applies.
+// keep.  Per-feature results go to feat_best; the next partition kernel picks from them.
 #include "device_common.h"
 
 namespace lgbm_amd {
@@ -374,20 +371,18 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   const Feature F = a.feat[f];
   const int nbf = F.num_bin - F.offset;
   const int nb2 = 2 * nbf;
-  int parity = 0, leaf = 0, nblk_direct = -1;
+  int parity = 0, nblk_direct = -1;
+  const Step* st = a.st;
   if (!ROOT) {
-    const Step* st = a.st;
     if (st->done) return;
-    parity = (st->step + 1) & 1;
+    parity = (st->cs.s + 1) & 1;
     // zero this feature's bins of the buffer the next step reduces into
     if (side == 0) {
       long long* nxt = StepScratch(a, parity + 1);
       for (int i = tid; i < nb2; i += kFindThreads) nxt[2 * F.hist_offset + i] = 0;
     }
     if (st->skip_find) return;
-    leaf = side == 0 ? st->smaller : st->larger;
-    const ChildInfo c = StepChildren(a, st);
-    const int nblk = HistBlocksFor(c.s_count, a.hist_max_blocks, a.hist_rows_cap);
+    const int nblk = HistBlocksFor(st->s_count, a.hist_max_blocks, a.hist_rows_cap);
     if (DirectPartials(a, nblk)) nblk_direct = nblk;
   }
   const SplitParams& p = a.p.sp;
@@ -420,15 +415,15 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     depth = 0;
     slot = 0;
   } else {
-    const Leaf lf = a.leaves[leaf];
-    L.sg = lf.sum_g;
-    L.sh = lf.sum_h + 2 * kEpsilon;
-    L.n = lf.global_count;
-    L.parent_out = lf.output;
-    L.c.min = lf.cmin;
-    L.c.max = lf.cmax;
-    depth = lf.depth;
-    slot = lf.slot;
+    const ChildStats cl = st->child[side];  // written with the histogram (StepBookkeeping)
+    L.sg = cl.sum_g;
+    L.sh = cl.sum_h + 2 * kEpsilon;
+    L.n = cl.global_count;
+    L.parent_out = cl.output;
+    L.c.min = cl.cmin;
+    L.c.max = cl.cmax;
+    depth = cl.depth;
+    slot = cl.slot;
   }
   L.cnt_factor = L.n / L.sh;
   const double gain_shift = LeafGain(L.sg, L.sh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, L.n,
@@ -496,166 +491,6 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   if (tid == 0) a.feat_best[side * a.p.num_features + f] = o;
 }
 
-namespace {
-
-// argmax of best[0..s] (host loop order: higher gain, then smaller real feature, then lower
-// leaf id), one wave
-__device__ int PickLeafWave(const KArgs& a, int s) {
-  double bg = -INFINITY;
-  int bf = -1, bl = 0x7fffffff;
-  for (int l = threadIdx.x; l <= s; l += kWave) {
-    const double g = a.best[l].gain;
-    const int f = a.best[l].real_feature;
-    if (bl == 0x7fffffff || SplitBetter(g, f, bg, bf)) {
-      bg = g;
-      bf = f;
-      bl = l;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    const double og = __shfl_xor(bg, o, kWave);
-    const int of = __shfl_xor(bf, o, kWave);
-    const int ol = __shfl_xor(bl, o, kWave);
-    const bool take = ol != 0x7fffffff &&
-                      (bl == 0x7fffffff || SplitBetter(og, of, bg, bf) || (!SplitBetter(bg, bf, og, of) && ol < bl));
-    if (take) {
-      bg = og;
-      bf = of;
-      bl = ol;
-    }
-  }
-  return bl;
-}
-
-// best[leaf] = best of the per-feature results of one side
-__device__ void ReduceFeatureBest(const KArgs& a, int side, int leaf) {
-  const int lane = threadIdx.x;
-  const FeatureBest* fb = a.feat_best + side * a.p.num_features;
-  int bi = -1;
-  double bg = -INFINITY;
-  int brf = -1;
-  for (int i = lane; i < a.p.num_features; i += kWave) {
-    const FeatureBest& c = fb[i];
-    if (c.feature >= 0 && SplitBetter(c.gain, c.real_feature, bg, brf)) {
-      bg = c.gain;
-      brf = c.real_feature;
-      bi = i;
-    }
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    const double og = __shfl_xor(bg, off, kWave);
-    const int orf = __shfl_xor(brf, off, kWave);
-    const int oi = __shfl_xor(bi, off, kWave);
-    if (oi >= 0 && (bi < 0 || SplitBetter(og, orf, bg, brf))) {
-      bg = og;
-      brf = orf;
-      bi = oi;
-    }
-  }
-  if (lane == 0) {
-    DeviceSplit& d = a.best[leaf];
-    if (bi < 0 || fb[bi].gain == -INFINITY) {
-      d.gain = -INFINITY;
-      d.feature = -1;
-      d.real_feature = -1;
-    } else {
-      const FeatureBest b = fb[bi];
-      d.gain = b.gain;
-      d.feature = b.feature;
-      d.real_feature = b.real_feature;
-      d.threshold = b.thr;
-      d.left_count = b.lc;
-      d.right_count = b.rc;
-      d.left_output = b.lo;
-      d.right_output = b.ro;
-      d.left_sum_gradient = b.lg;
-      d.left_sum_hessian = b.lh;
-      d.right_sum_gradient = b.rg;
-      d.right_sum_hessian = b.rh;
-      d.default_left = static_cast<int8_t>(b.default_left);
-      d.monotone_type = static_cast<int8_t>(b.mono);
-      d.is_categorical = 0;
-      d.num_cat_threshold = 0;
-    }
-  }
-}
-
-}  // namespace
-
-template <bool ROOT>
-__global__ __launch_bounds__(kWave) void k_pick(KArgs a) {
-  Step* st = a.st;
-  if (st->done) return;
-  if (ROOT) {
-    ReduceFeatureBest(a, 0, 0);
-  } else if (!st->skip_find) {
-    ReduceFeatureBest(a, 0, st->smaller);
-    ReduceFeatureBest(a, 1, st->larger);
-  }
-  __syncthreads();  // lane 0's best[] stores -> the whole wave
-  const int s = ROOT ? 0 : st->step + 1;  // index of the next split
-  if (s >= a.p.num_leaves - 1) {
-    if (threadIdx.x == 0) {
-      st->step = s;
-      st->done = 1;
-    }
-    return;
-  }
-  const int leaf = PickLeafWave(a, s);
-  if (threadIdx.x != 0) return;
-  const DeviceSplit sp = a.best[leaf];
-  st->step = s;
-  if (!(sp.gain > 0.0) || sp.feature < 0) {
-    st->done = 1;
-    return;
-  }
-  const int nl = s + 1;
-  Leaf* P = &a.leaves[leaf];
-  Leaf* R = &a.leaves[nl];
-  st->leaf = leaf;
-  st->new_leaf = nl;
-  st->split = sp;
-  st->part_begin = P->begin;
-  st->part_count = P->count;
-  st->src_buf = P->buf;
-  st->cur_left = 0;
-  st->cur_right = 0;
-  st->sfeat = a.feat[sp.feature];
-  SplitRecord& rec = a.rec[s];
-  rec.leaf = leaf;
-  rec.split = sp;
-  rec.left_count = sp.left_count;
-  rec.right_count = sp.right_count;
-  // children statistics (left keeps the leaf id); ranges are set by the partition
-  const int depth = P->depth + 1;
-  st->child_depth = depth;
-  double pmin = P->cmin, pmax = P->cmax, rmin = P->cmin, rmax = P->cmax;
-  if (!sp.is_categorical) {
-    const double mid = (sp.left_output + sp.right_output) / 2.0f;
-    if (sp.monotone_type < 0) {
-      pmin = fmax(pmin, mid);
-      rmax = fmin(rmax, mid);
-    } else if (sp.monotone_type > 0) {
-      pmax = fmin(pmax, mid);
-      rmin = fmax(rmin, mid);
-    }
-  }
-  R->depth = depth;
-  R->sum_g = sp.right_sum_gradient;
-  R->sum_h = sp.right_sum_hessian;
-  R->output = sp.right_output;
-  R->global_count = sp.right_count;
-  R->cmin = rmin;
-  R->cmax = rmax;
-  P->depth = depth;
-  P->sum_g = sp.left_sum_gradient;
-  P->sum_h = sp.left_sum_hessian;
-  P->output = sp.left_output;
-  P->global_count = sp.left_count;
-  P->cmin = pmin;
-  P->cmax = pmax;
-}
-
 static size_t FindLds(const KArgs& a) {
   return a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
 }
@@ -665,8 +500,6 @@ void FindRoot(const KArgs& a, hipStream_t s) {
 void FindStep(const KArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_find<false>, dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
 }
-void PickRoot(const KArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_pick<true>, dim3(1), dim3(kWave), 0, s, a); }
-void PickStep(const KArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_pick<false>, dim3(1), dim3(kWave), 0, s, a); }
 
 }  // namespace dev
 }  // namespace lgbm_amd

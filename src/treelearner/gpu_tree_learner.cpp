@@ -260,6 +260,7 @@ void GPUTreeLearner::UploadData() {
   a.scratch = d_scratch_;
   a.partials = d_partials_;
   a.hist_max_blocks = hist_blocks;
+  a.host_mode = 0;
   a.root = d_root_;
   a.num_rows = num_data_;
   a.root_identity = 1;
@@ -434,8 +435,7 @@ void GPUTreeLearner::KernelFloorProbe(const dev::KArgs& a) {
     const char* name;
     void (*fn)(const dev::KArgs&, hipStream_t);
   };
-  const P probes[] = {{"partition", dev::Partition}, {"hist+reduce", dev::HistStep}, {"find", dev::FindStep},
-                      {"pick", dev::PickStep}};
+  const P probes[] = {{"partition", dev::Partition}, {"hist+reduce", dev::HistStep}, {"find", dev::FindStep}};
   for (const P& p : probes) {
     for (int i = 0; i < 20; ++i) p.fn(a, stream_);
     HIPCHECK(hipEventRecord(e0, stream_));
@@ -470,15 +470,14 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   dev::HistRoot(a, stream_);
   AllreduceScratch(0);
   dev::FindRoot(a, stream_);
-  dev::PickRoot(a, stream_);
-  // one split per step: partition -> smaller child's histogram -> split scans of both
-  // children -> next split.  The sequence is fixed; kernels of finished trees exit early.
+  // one split per step: pick + partition -> smaller child's histogram (+ reduction) ->
+  // split scans of both children.  The sequence is fixed; kernels of a finished tree exit
+  // at once.
   for (int s = 0; s < config_->num_leaves - 1; ++s) {
     dev::Partition(a, stream_);
     dev::HistStep(a, stream_);
     AllreduceScratch(s + 1);  // the step's buffer parity
     dev::FindStep(a, stream_);
-    dev::PickStep(a, stream_);
   }
 }
 
@@ -521,7 +520,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
                           hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
-  const int num_splits = h_step_->step;
+  const int num_splits = h_step_->nsplit;
   if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {
     if (kp[0] == '1') KernelFloorProbe(a);
   }
@@ -617,17 +616,19 @@ data_size_t GPUTreeLearner::PartitionLeaf(int leaf, int inner, const SplitInfo& 
   const data_size_t cnt = leaf_count_[leaf];
   dev::Step& st = *h_step_;
   std::memset(&st, 0, sizeof(st));
-  st.leaf = leaf;
-  st.new_leaf = new_leaf;
-  st.part_begin = begin;
-  st.part_count = cnt;
-  st.src_buf = 0;  // host mode keeps every leaf in buffer 0 (copied back below)
+  st.cs.leaf = leaf;
+  st.cs.new_leaf = new_leaf;
+  st.cs.part_begin = begin;
+  st.cs.part_count = cnt;
+  st.cs.src_buf = 0;  // host mode keeps every leaf in buffer 0 (copied back below)
   SplitInfo si = s;
   si.inner_feature = inner;
-  si.ToDevice(&st.split, data_->FeatureBinMapper(inner)->bin_type() == BinType::Categorical);
-  st.sfeat = h_feats_[inner];
+  si.ToDevice(&st.cs.split, data_->FeatureBinMapper(inner)->bin_type() == BinType::Categorical);
+  st.cs.feat = h_feats_[inner];
   HIPCHECK(hipMemcpyAsync(d_step_, h_step_, sizeof(dev::Step), hipMemcpyHostToDevice, stream_));
-  dev::Partition(args_, stream_);
+  dev::KArgs a = args_;
+  a.host_mode = 1;
+  dev::Partition(a, stream_);
   if (cnt > 0) {
     HIPCHECK(hipMemcpyAsync(d_idx_ + begin, d_tmp_ + begin, sizeof(int32_t) * cnt, hipMemcpyDeviceToDevice, stream_));
   }
@@ -668,7 +669,7 @@ void GPUTreeLearner::DownloadPartitionToHost() const {
   HIPCHECK(hipMemcpyAsync(leaves.data(), d_leaves_, sizeof(dev::Leaf) * L, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   // each leaf's rows sit in the index buffer its last split wrote (Leaf::buf)
-  const int num_leaves_now = h_step_->step + 1;
+  const int num_leaves_now = h_step_->nsplit + 1;
   for (int l = 0; l < L; ++l) {
     self->leaf_begin_[l] = leaves[l].begin;
     self->leaf_count_[l] = l < num_leaves_now ? leaves[l].count : 0;
