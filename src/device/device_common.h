@@ -18,6 +18,23 @@ constexpr int kWave = 64;
 constexpr int kFindLdsBins = 2048;  // split scan stages features up to this many bins in LDS
 constexpr int kFindThreads = 256;   // split-scan workgroup
 
+// in-kernel trace point: the first thread of workgroup (0, 0) stamps slot `slot` of split
+// `s` after its outstanding memory operations completed (LGBM_AMD_KTRACE diagnostics)
+__device__ __forceinline__ void KTrace(const KArgs& a, int s, int slot) {
+  if (a.ktrace != nullptr && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && s >= 0 &&
+      s < a.p.num_leaves) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    a.ktrace[s * kTraceSlots + slot] = wall_clock64();
+  }
+}
+
+__device__ __forceinline__ void KTraceAt(const KArgs& a, int s, int slot, long long t) {
+  if (a.ktrace != nullptr && threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0 && s >= 0 &&
+      s < a.p.num_leaves) {
+    a.ktrace[s * kTraceSlots + slot] = t;
+  }
+}
+
 inline int GridFor(int64_t n) {
   return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 8 * NumCUs())));
 }

@@ -137,45 +137,49 @@ __device__ void StepBookkeeping(const KArgs& a, Step* st) {
 
 }  // namespace
 
-// one row block [r0, r1) of one column tile -> its partial histogram `out`
+// per-thread constants of a column tile (one 32-bit word of a row per thread)
+struct TileCtx {
+  int w0, w1, lo_bin, nbins;
+  int tpr, rpp, q, rs;  // threads per row, rows per pass, my word, my row slot
+  int goff[4];          // histogram offset of each group of my word (-1: none)
+  float sg, sh;         // fixed-point scales
+};
+
+template <int MODE>
+__device__ __forceinline__ void LoadRowIdx(const int32_t* src, int i, int r1, int rpp, int* r) {
+#pragma unroll
+  for (int k = 0; k < kRowsInFlight; ++k) {
+    const int ii = i + k * rpp;
+    r[k] = ii < r1 ? (src ? src[ii] : ii) : -1;
+  }
+}
+
+// one row block [r0, r1) of one column tile -> its partial histogram `out`.  The index
+// loads of each batch are issued one batch ahead (the first ones while the LDS is cleared).
 template <int MODE, int GPW>
 __device__ __forceinline__ void HistBlock(const KArgs& a, unsigned long long* lds, const int32_t* src, int r0, int r1,
-                                          int w0, int w1, int lo_bin, int nbins, unsigned long long* out) {
+                                          const TileCtx& t, unsigned long long* out, int ts) {
+  const bool active = t.rs < t.rpp;
+  int i = r0 + t.rs;
+  int r[kRowsInFlight];
+  if (active) LoadRowIdx<MODE>(src, i, r1, t.rpp, r);
   __syncthreads();  // LDS reuse across row blocks
-  for (int i = threadIdx.x; i < nbins; i += kHistThreads) lds[i] = 0ull;
+  for (int j = threadIdx.x; j < t.nbins; j += kHistThreads) lds[j] = 0ull;
   __syncthreads();
-
-  const float sg = static_cast<float>(a.scales[0]);
-  const float sh = static_cast<float>(a.scales[1]);
-  const int tpr = w1 - w0;  // threads per row: one per 32-bit word of the tile
-  const int rpp = kHistThreads / tpr;
-  const int q = threadIdx.x % tpr;
-  const int rs = threadIdx.x / tpr;
-  if (rs < rpp) {
-    const int w = w0 + q;
-    int goff[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int g = w * GPW + j;
-      goff[j] = (j < GPW && g < a.p.num_groups) ? (a.group_off[g] - lo_bin) : -1;
-    }
+  KTrace(a, blockIdx.x == 0 ? ts : -1, kTrHistZeroed);
+  if (active) {
+    const int w = t.w0 + t.q;
     const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
     const float2* gh = reinterpret_cast<const float2*>(a.gh);
     const int64_t wpr = a.words_per_row;
-    const bool write_iota = MODE == 0 && src == nullptr && q == 0 && blockIdx.y == 0;
-    // kRowsInFlight independent (index -> gh, bin word) gathers per thread per batch;
-    // the last batch is predicated, so a small block is one round of loads
-    for (int i = r0 + rs; i < r1; i += kRowsInFlight * rpp) {
-      int r[kRowsInFlight];
-#pragma unroll
-      for (int k = 0; k < kRowsInFlight; ++k) {
-        const int ii = i + k * rpp;
-        r[k] = ii < r1 ? (src ? src[ii] : ii) : -1;
-      }
+    const bool write_iota = MODE == 0 && src == nullptr && t.q == 0 && blockIdx.y == 0;
+    const int stride = kRowsInFlight * t.rpp;
+    for (; i < r1; i += stride) {
+      if (i == r0 + t.rs) KTrace(a, blockIdx.x == 0 ? ts : -1, kTrHistIdx);
       if (write_iota) {
 #pragma unroll
         for (int k = 0; k < kRowsInFlight; ++k) {
-          if (r[k] >= 0) a.idx[i + k * rpp] = r[k];
+          if (r[k] >= 0) a.idx[i + k * t.rpp] = r[k];
         }
       }
       float2 v[kRowsInFlight];
@@ -186,38 +190,86 @@ __device__ __forceinline__ void HistBlock(const KArgs& a, unsigned long long* ld
         v[k] = gh[rr];
         wd[k] = r[k] >= 0 ? bins32[rr * wpr + w] : 0u;  // word 0: every bin skipped
       }
+      int rn[kRowsInFlight];
+      LoadRowIdx<MODE>(src, i + stride, r1, t.rpp, rn);  // next batch, in flight during the atomics
+      if (i == r0 + t.rs) KTrace(a, blockIdx.x == 0 ? ts : -1, kTrHistLoaded);
 #pragma unroll
-      for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW>(lds, goff, wd[k], PackFixed(v[k], sg, sh));
+      for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW>(lds, t.goff, wd[k], PackFixed(v[k], t.sg, t.sh));
+#pragma unroll
+      for (int k = 0; k < kRowsInFlight; ++k) r[k] = rn[k];
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < nbins; i += kHistThreads) out[i] = lds[i];
+  KTrace(a, blockIdx.x == 0 ? ts : -1, kTrHistAccum);
+  for (int j = threadIdx.x; j < t.nbins; j += kHistThreads) out[j] = lds[j];
 }
 
 template <int MODE, int GPW>
 __global__ __launch_bounds__(kHistThreads) void k_hist(KArgs a) {
   extern __shared__ unsigned long long lds[];
-  // bookkeeping by the last workgroup: small leaves leave it without row work
-  if (MODE == 1 && blockIdx.x == gridDim.x - 1 && blockIdx.y == 0 && threadIdx.x == 0 && !a.st->done) {
-    StepBookkeeping(a, a.st);
+  const long long t_entry = wall_clock64();
+  // ---- every load that does not depend on another one first (a single round trip):
+  // tile geometry, scales and the Step record (read before it is tested)
+  TileCtx t;
+  t.w0 = blockIdx.y * a.tile_words;
+  t.w1 = min(a.words_per_row, t.w0 + a.tile_words);
+  const int g0 = t.w0 * GPW;
+  const int g_end = min(a.p.num_groups, t.w1 * GPW);
+  t.tpr = t.w1 - t.w0;
+  t.rpp = kHistThreads / t.tpr;
+  t.q = threadIdx.x % t.tpr;
+  t.rs = threadIdx.x / t.tpr;
+  const int w = t.w0 + t.q;
+  int graw[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int g = w * GPW + j;
+    graw[j] = (j < GPW && g < a.p.num_groups) ? a.group_off[g] : -1;
   }
-  int begin, count;
-  const int32_t* src;
-  if (!HistRows<MODE>(a, false, &begin, &count, &src)) return;
+  t.lo_bin = a.group_off[g0];
+  const int hi_bin = g_end < a.p.num_groups ? a.group_off[g_end] : a.p.total_bins;
+  t.sg = static_cast<float>(a.scales[0]);
+  t.sh = static_cast<float>(a.scales[1]);
+  int begin = 0, count = 0, ts = -1;
+  const int32_t* src = nullptr;
+  if (MODE == 0) {
+    count = a.num_rows;
+    src = a.root_identity ? nullptr : a.idx;
+  } else if (MODE == 2) {
+    begin = a.range_begin;
+    count = a.num_rows;
+    src = a.idx;
+  } else {
+    Step* st = a.st;
+    const int done = st->done;
+    const ChildInfo c = StepChildren(a, st);
+    ts = st->cs.s;
+    if (done) return;
+    // bookkeeping by the last workgroup: small leaves leave it without row work
+    if (blockIdx.x == gridDim.x - 1 && blockIdx.y == 0 && threadIdx.x == 0) StepBookkeeping(a, st);
+    if (c.skip) return;
+    begin = c.s_begin;
+    count = c.s_count;
+    src = c.buf ? a.tmp : a.idx;
+  }
+  if (count <= 0) return;
+  if ((threadIdx.x & 63) == 0 && a.ktrace != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && ts >= 0 &&
+      ts < a.p.num_leaves) {
+    a.ktrace[ts * kTraceSlots + kTrHistWave0 + (threadIdx.x >> 6)] = t_entry;
+  }
+  t.nbins = hi_bin - t.lo_bin;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) t.goff[j] = graw[j] >= 0 ? graw[j] - t.lo_bin : -1;
+  KTraceAt(a, ts, kTrHistEntry, t_entry);
+  KTrace(a, ts, kTrHistRows);
   const int nblk = HistBlocksFor(count, a.hist_max_blocks, a.hist_rows_cap);
   const int chunk = (count + nblk - 1) / nblk;
-  const int w0 = blockIdx.y * a.tile_words;
-  const int w1 = min(a.words_per_row, w0 + a.tile_words);
-  const int g0 = w0 * GPW;
-  const int g_end = min(a.p.num_groups, w1 * GPW);
-  const int lo_bin = a.group_off[g0];
-  const int hi_bin = g_end < a.p.num_groups ? a.group_off[g_end] : a.p.total_bins;
-  const int nbins = hi_bin - lo_bin;
   // the grid is one workgroup per CU (per tile); row blocks beyond it are strided
   for (int kb = blockIdx.x; kb < nblk; kb += gridDim.x) {
-    HistBlock<MODE, GPW>(a, lds, src, begin + kb * chunk, min(begin + count, begin + kb * chunk + chunk), w0, w1,
-                         lo_bin, nbins, a.partials + static_cast<size_t>(kb) * a.p.total_bins + lo_bin);
+    HistBlock<MODE, GPW>(a, lds, src, begin + kb * chunk, min(begin + count, begin + kb * chunk + chunk), t,
+                         a.partials + static_cast<size_t>(kb) * a.p.total_bins + t.lo_bin, ts);
   }
+  KTrace(a, ts, kTrHistExit);
 }
 
 // partials [block][bin] -> int64 (g, h) pairs of the step's buffer.  Each thread sums up to
@@ -225,6 +277,9 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(KArgs a) {
 // int64 atomics into the (pre-zeroed) buffer, otherwise the single chunk stores directly.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
+  const long long t_entry = wall_clock64();
+  const int ts = MODE == 1 && !a.st->done ? a.st->cs.s : -1;
+  KTraceAt(a, ts, kTrRedEntry, t_entry);
   if (MODE == 1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     // the partition cursors are final (read by the histogram kernel): reset for the next split
     a.st->cur_left = 0;
@@ -234,7 +289,10 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
   const int32_t* src;
   if (!HistRows<MODE>(a, true, &begin, &count, &src)) return;
   const int nblk = HistBlocksFor(count, a.hist_max_blocks, a.hist_rows_cap);
-  if (MODE == 1 && DirectPartials(a, nblk)) return;  // summed by the split scan
+  if (MODE == 1 && DirectPartials(a, nblk)) {  // summed by the split scan
+    KTrace(a, ts, kTrRedExit);
+    return;
+  }
   const int k0 = blockIdx.y * kReduceChunk;
   if (k0 >= nblk) return;
   const int bin = blockIdx.x * blockDim.x + threadIdx.x;
@@ -259,6 +317,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
     atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin]), static_cast<unsigned long long>(g));
     atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin + 1]), static_cast<unsigned long long>(h));
   }
+  KTrace(a, ts, kTrRedExit);
 }
 
 template <int MODE>

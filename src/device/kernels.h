@@ -48,6 +48,18 @@ struct KArgs {
   int32_t num_data;          // rows of the matrix (column stride of bins_col)
   int32_t host_mode;         // partition: the host wrote Step::cs (host-assisted growth)
   FeatureBest* feat_best;    // [2][num_features] per-feature best split of the two leaves
+  long long* ktrace;         // optional [num_leaves][kTraceSlots] in-kernel timestamps (LGBM_AMD_KTRACE)
+};
+
+// in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)
+enum TraceSlot {
+  kTrPartEntry = 0, kTrPartPicked, kTrPartRows, kTrPartBins, kTrPartExit,
+  kTrHistEntry, kTrHistRows, kTrHistAccum, kTrHistExit,
+  kTrRedEntry, kTrRedExit,
+  kTrFindEntry, kTrFindLoaded, kTrFindScanned, kTrFindExit,
+  kTrHistZeroed, kTrHistIdx, kTrHistLoaded,
+  kTrHistWave0 = 24,  // 16 slots: entry time of each wave of the first histogram workgroup
+  kTraceSlots = 40
 };
 
 constexpr int kHistThreads = 1024;     // histogram workgroup (16 waves)
@@ -71,8 +83,9 @@ __host__ __device__ inline int HistBlocksFor(int count, int max_blocks, int rows
 int HistGridBlocks();  // max row blocks of a histogram (2 per CU)
 void SetNumCUs(int n);
 
-// interleave (g, h) and record max|g| / max h (as float bits) into absmax[0..1] (pre-zeroed)
-void PackGH(const float* g, const float* h, GH* gh, int64_t n, uint32_t* absmax, hipStream_t s);
+// interleave (g, h); per-workgroup max|g| / max h into max_parts[PackBlocks(n)][2]
+void PackGH(const float* g, const float* h, GH* gh, int64_t n, float* max_parts, hipStream_t s);
+int PackBlocks(int64_t n);
 // fixed-point scales of this tree from absmax and the per-workgroup row cap
 void ComputeScales(const uint32_t* absmax, int rows_cap, double* scales, hipStream_t s);
 void TreeBegin(const KArgs& a, hipStream_t s);
@@ -104,6 +117,8 @@ struct DevTree {
   const double* leaf_value;
   const int32_t* cat_boundaries_inner;
   const uint32_t* cat_threshold_inner;
+  unsigned long long* bm_work;  // [num_leaves - 1][4] decision bitmaps over 8-bit group bins (workspace)
+  int32_t* bm_meta;             // [num_leaves - 1] packed (group, left, right) (workspace)
 };
 void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
                   hipStream_t s);
@@ -127,8 +142,15 @@ struct GradArgs {
   const double* score;       // [num_class][num_data]
   float* grad;
   float* hess;
+  GH* gh;                    // optional fused packing (one model per iteration):
+  float* max_parts;          //   interleaved (g, h), per-workgroup max|g| / max h and
+  double* root_parts;        //   (sum g, sum h), [GradientBlocks][2] each
 };
 void Gradients(const GradArgs& g, hipStream_t s);
+int GradientBlocks(int64_t n);
+// absmax[0..1] (and root = (sum g, sum h, n) if root_parts) from per-workgroup partials
+void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, uint32_t* absmax,
+                 double* root, hipStream_t s);
 
 }  // namespace dev
 }  // namespace lgbm_amd

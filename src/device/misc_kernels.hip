@@ -14,11 +14,10 @@ void SetNumCUs(int n) { g_num_cus = n > 0 ? n : 256; }
 int HistGridBlocks() { return 2 * g_num_cus; }
 
 // ---------------------------------------------------------------- gradient packing
-// (g, h) interleaved so a gathered row costs one 8-byte load; also max|g| / max h of the
-// tree (one atomic per workgroup; non-negative floats order like their bit patterns)
+// (g, h) interleaved so a gathered row costs one 8-byte load; also the per-workgroup max|g|
+// / max h of the tree (reduced by k_reduce_parts: no contended atomics)
 __global__ __launch_bounds__(256) void k_pack_gh(const float* __restrict__ g, const float* __restrict__ h,
-                                                 float2* __restrict__ gh, int64_t n, uint32_t* absmax) {
-  static_assert(sizeof(GH) == sizeof(float2), "GH layout");
+                                                 float2* __restrict__ gh, int64_t n, float* max_parts) {
   float mg = 0.f, mh = 0.f;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -43,14 +42,18 @@ __global__ __launch_bounds__(256) void k_pack_gh(const float* __restrict__ g, co
       mg = fmaxf(mg, smg[i]);
       mh = fmaxf(mh, smh[i]);
     }
-    atomicMax(&absmax[0], __float_as_uint(mg));
-    atomicMax(&absmax[1], __float_as_uint(mh));
+    max_parts[2 * blockIdx.x] = mg;
+    max_parts[2 * blockIdx.x + 1] = mh;
   }
 }
 
-void PackGH(const float* g, const float* h, GH* gh, int64_t n, uint32_t* absmax, hipStream_t s) {
-  const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4 * NumCUs())));
-  hipLaunchKernelGGL(k_pack_gh, dim3(blocks), dim3(256), 0, s, g, h, reinterpret_cast<float2*>(gh), n, absmax);
+int PackBlocks(int64_t n) {
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4 * NumCUs())));
+}
+
+void PackGH(const float* g, const float* h, GH* gh, int64_t n, float* max_parts, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_gh, dim3(PackBlocks(n)), dim3(256), 0, s, g, h, reinterpret_cast<float2*>(gh), n,
+                     max_parts);
 }
 
 // scale = 2^k with rows_cap * max * scale <= 2^30 (g: signed high half of the packed
@@ -104,7 +107,6 @@ __global__ void k_tree_begin(KArgs a) {
     st->larger = -1;
     st->skip_find = 0;
     st->cur_left = st->cur_right = 0;
-    a.root[0] = a.root[1] = a.root[2] = 0.0;
   }
 }
 
@@ -130,6 +132,7 @@ __global__ __launch_bounds__(256) void k_root_sum(KArgs a) {
 }
 
 void RootSum(const KArgs& a, hipStream_t s) {
+  (void)hipMemsetAsync(a.root, 0, sizeof(double) * 3, s);  // accumulated with atomics below
   const int blocks = std::max(1, std::min((a.num_rows + 255) / 256, 2 * NumCUs()));
   hipLaunchKernelGGL(k_root_sum, dim3(blocks), dim3(256), 0, s, a);
 }

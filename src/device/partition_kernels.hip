@@ -89,13 +89,45 @@ struct PickResult {
   DeviceSplit split;
 };
 
-// the pick, by the first wave; the result goes to LDS
+// the pick, by the first wave; the result goes to LDS.  Every load that does not depend on
+// another one is issued first (Step, both sides' per-feature results, every leaf's best
+// gain): one round trip, then one more for the winner's records.
 __device__ void PickWave(const KArgs& a, const Step* st, PickResult* out) {
   const int lane = threadIdx.x;
   const int L = a.p.num_leaves, NF = a.p.num_features;
   const int s = st->nsplit;
   const int fresh = st->fresh;
   const int sm = st->smaller, lg = st->larger;
+  // per-feature candidates of both sides (lane-strided) and per-leaf candidates
+  double g0 = -INFINITY, g1 = -INFINITY;
+  int rf0 = -1, rf1 = -1, i0 = -1, i1 = -1;
+  for (int i = lane; i < NF; i += kWave) {
+    const FeatureBest& b0 = a.feat_best[i];
+    const FeatureBest& b1 = a.feat_best[NF + i];
+    const double cg0 = b0.gain, cg1 = b1.gain;
+    const int crf0 = b0.real_feature, crf1 = b1.real_feature;
+    const int cf0 = b0.feature, cf1 = b1.feature;
+    if (cf0 >= 0 && (i0 < 0 || SplitBetter(cg0, crf0, g0, rf0))) {
+      g0 = cg0;
+      rf0 = crf0;
+      i0 = i;
+    }
+    if (cf1 >= 0 && (i1 < 0 || SplitBetter(cg1, crf1, g1, rf1))) {
+      g1 = cg1;
+      rf1 = crf1;
+      i1 = i;
+    }
+  }
+  double lgain[kMaxLeaves / kWave];
+  int lrf[kMaxLeaves / kWave];
+#pragma unroll
+  for (int k = 0; k < kMaxLeaves / kWave; ++k) {
+    const int l = lane + k * kWave;
+    if (l < L) {
+      lgain[k] = a.best[l].gain;
+      lrf[k] = a.best[l].real_feature;
+    }
+  }
   if (s >= L - 1) {
     if (lane == 0) {
       out->done = 1;
@@ -103,46 +135,39 @@ __device__ void PickWave(const KArgs& a, const Step* st, PickResult* out) {
     }
     return;
   }
-  // per-leaf bests of the freshly scanned children, from the per-feature results
+  // per-leaf bests of the freshly scanned children
   int fi[2] = {-1, -1};
   double fg[2] = {-INFINITY, -INFINITY};
   int frf[2] = {-1, -1};
-#pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    if (side >= fresh) continue;
-    const FeatureBest* fb = a.feat_best + side * NF;
-    double g = -INFINITY;
-    int rf = -1, idx = -1;
-    for (int i = lane; i < NF; i += kWave) {
-      const double cg = fb[i].gain;
-      const int crf = fb[i].real_feature;
-      if (fb[i].feature >= 0 && (idx < 0 || SplitBetter(cg, crf, g, rf))) {
-        g = cg;
-        rf = crf;
-        idx = i;
-      }
-    }
-    WaveArgBest(&g, &rf, &idx);
-    if (idx >= 0 && g == -INFINITY) idx = -1;  // no valid threshold on any feature
-    fi[side] = idx;
-    fg[side] = idx >= 0 ? g : -INFINITY;
-    frf[side] = idx >= 0 ? rf : -1;
+  if (fresh >= 1) {
+    WaveArgBest(&g0, &rf0, &i0);
+    if (i0 >= 0 && g0 == -INFINITY) i0 = -1;  // no valid threshold on any feature
+    fi[0] = i0;
+    fg[0] = i0 >= 0 ? g0 : -INFINITY;
+    frf[0] = i0 >= 0 ? rf0 : -1;
+  }
+  if (fresh == 2) {
+    WaveArgBest(&g1, &rf1, &i1);
+    if (i1 >= 0 && g1 == -INFINITY) i1 = -1;
+    fi[1] = i1;
+    fg[1] = i1 >= 0 ? g1 : -INFINITY;
+    frf[1] = i1 >= 0 ? rf1 : -1;
   }
   // the leaf to split: argmax over leaves 0..s (fresh children use the new results)
   double g = -INFINITY;
   int rf = -1, leaf = -1;
-  for (int l = lane; l <= s; l += kWave) {
-    double cg;
-    int crf;
+#pragma unroll
+  for (int k = 0; k < kMaxLeaves / kWave; ++k) {
+    const int l = lane + k * kWave;
+    if (l > s) continue;
+    double cg = lgain[k];
+    int crf = lrf[k];
     if (fresh >= 1 && l == sm) {
       cg = fg[0];
       crf = frf[0];
     } else if (fresh == 2 && l == lg) {
       cg = fg[1];
       crf = frf[1];
-    } else {
-      cg = a.best[l].gain;
-      crf = a.best[l].real_feature;
     }
     if (leaf < 0 || SplitBetter(cg, crf, g, rf)) {
       g = cg;
@@ -264,6 +289,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(KArgs a) {
   __shared__ int wl[kPartRowsPerThread][kPartThreads / kWave];
   __shared__ int base[2];
   __shared__ PickResult pk;
+  const long long t_entry = wall_clock64();
   Step* st = a.st;
   if (st->done) return;
   int pb, pc, src_buf;
@@ -279,10 +305,16 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(KArgs a) {
     if (threadIdx.x < kWave) PickWave(a, st, &pk);
     __syncthreads();
     if (pk.done) {
-      if (blockIdx.x == 0 && threadIdx.x == 0) st->done = 1;
+      if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        st->done = 1;
+        st->nsplit = pk.s;
+      }
       return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) RecordSplit(a, st, pk);
+    // recorded by the last workgroup: it has no rows to move unless the leaf is large
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) RecordSplit(a, st, pk);
+    KTraceAt(a, pk.s, kTrPartEntry, t_entry);
+    KTrace(a, pk.s, kTrPartPicked);
     pb = pk.P.begin;
     pc = pk.P.count;
     src_buf = pk.P.buf;
@@ -308,9 +340,12 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(KArgs a) {
       const int i = t0 + k * kPartThreads + threadIdx.x;
       row[k] = i < pc ? src[pb + i] : -1;
     }
+    const int ts = a.host_mode ? -1 : (t == 0 ? pk.s : -1);
+    KTrace(a, ts, kTrPartRows);
     uint32_t gb[kPartRowsPerThread];
 #pragma unroll
     for (int k = 0; k < kPartRowsPerThread; ++k) gb[k] = row[k] >= 0 ? ColBin(a, row[k], F.group) : 0u;
+    KTrace(a, ts, kTrPartBins);
     bool left[kPartRowsPerThread];
     unsigned long long mask[kPartRowsPerThread];
 #pragma unroll
@@ -361,6 +396,7 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(KArgs a) {
     }
     __syncthreads();  // wl / base are rewritten by the next tile
   }
+  if (!a.host_mode) KTrace(a, pk.s, kTrPartExit);
 }
 
 void Partition(const KArgs& a, hipStream_t s) {

@@ -119,9 +119,95 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
   }
 }
 
+// ---------------------------------------------------------------- bitmap traversal
+// For 8-bit storage columns every decision of a node (numerical threshold, missing-value
+// routing, categorical set, the group-bin -> feature-bin mapping of bundles) collapses into
+// one 256-bit "goes left" set over the raw group bin: a level of the walk is then a byte
+// read of the row, a bit test and a child index, all from LDS.
+__global__ __launch_bounds__(256) void k_tree_bitmaps(KArgs a, DevTree t) {
+  const int node = blockIdx.x;
+  const NodeInfo nd = MakeNode(a, t, node);
+  const uint32_t gb = threadIdx.x;  // raw group bin 0..255
+  const uint32_t bin = (gb < static_cast<uint32_t>(nd.sub_lo) || gb >= static_cast<uint32_t>(nd.sub_hi))
+                           ? static_cast<uint32_t>(nd.mfb)
+                           : gb - nd.sub_lo + nd.offset;
+  bool left;
+  if (nd.is_cat) {
+    const int ci = static_cast<int>(nd.threshold);
+    const int lo = t.cat_boundaries_inner[ci], hi = t.cat_boundaries_inner[ci + 1];
+    const int word = static_cast<int>(bin >> 5);
+    left = word < hi - lo && ((t.cat_threshold_inner[lo + word] >> (bin & 31u)) & 1u);
+  } else if ((nd.missing_type == 1 && bin == static_cast<uint32_t>(nd.default_bin)) ||
+             (nd.missing_type == 2 && bin == static_cast<uint32_t>(nd.max_bin))) {
+    left = nd.left_is_default != 0;
+  } else {
+    left = bin <= nd.threshold;
+  }
+  const unsigned long long m = __ballot(left);
+  if ((threadIdx.x & 63) == 0) t.bm_work[node * 4 + (threadIdx.x >> 6)] = m;
+  if (threadIdx.x == 0) {
+    // group byte offset | left child (16 bits, two's complement leaves) | right child
+    t.bm_meta[node * 3 + 0] = nd.group;
+    t.bm_meta[node * 3 + 1] = nd.left;
+    t.bm_meta[node * 3 + 2] = nd.right;
+  }
+}
+
+constexpr int kBmRowsPerBlock = 256;
+constexpr int kBmMaxRowBytes = 64;
+
+__global__ __launch_bounds__(kBmRowsPerBlock) void k_add_tree_score_bm(KArgs a, DevTree t, int64_t n,
+                                                                        double* __restrict__ score) {
+  __shared__ unsigned long long s_bm[kMaxNodes * 4];
+  __shared__ int16_t s_group[kMaxNodes], s_left[kMaxNodes], s_right[kMaxNodes];
+  __shared__ double s_val[kMaxNodes + 1];
+  extern __shared__ uint32_t s_rows[];  // [kBmRowsPerBlock][words_per_row]
+  const int ni = t.num_leaves - 1;
+  for (int i = threadIdx.x; i < ni * 4; i += blockDim.x) s_bm[i] = t.bm_work[i];
+  for (int i = threadIdx.x; i < ni; i += blockDim.x) {
+    s_group[i] = static_cast<int16_t>(t.bm_meta[i * 3 + 0]);
+    s_left[i] = static_cast<int16_t>(t.bm_meta[i * 3 + 1]);
+    s_right[i] = static_cast<int16_t>(t.bm_meta[i * 3 + 2]);
+  }
+  for (int i = threadIdx.x; i < t.num_leaves; i += blockDim.x) s_val[i] = t.leaf_value[i];
+  const int wpr = a.words_per_row;
+  const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
+  const uint8_t* rows8 = reinterpret_cast<const uint8_t*>(s_rows);
+  for (int64_t r0 = static_cast<int64_t>(blockIdx.x) * kBmRowsPerBlock; r0 < n;
+       r0 += static_cast<int64_t>(gridDim.x) * kBmRowsPerBlock) {
+    const int nr = static_cast<int>(min<int64_t>(kBmRowsPerBlock, n - r0));
+    __syncthreads();
+    // the block's rows are one contiguous run of the row-major matrix: coalesced copy
+    const uint32_t* src = bins32 + r0 * wpr;
+    for (int i = threadIdx.x; i < nr * wpr; i += blockDim.x) s_rows[i] = src[i];
+    __syncthreads();
+    if (threadIdx.x < nr) {
+      const uint8_t* row = rows8 + threadIdx.x * wpr * 4;
+      int node = 0;
+      while (node >= 0) {
+        const uint32_t gb = row[s_group[node]];
+        const bool left = (s_bm[node * 4 + (gb >> 6)] >> (gb & 63u)) & 1ull;
+        node = left ? s_left[node] : s_right[node];
+      }
+      score[r0 + threadIdx.x] += s_val[~node];
+    }
+  }
+}
+
 void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
                   hipStream_t s) {
   if (num_rows <= 0) return;
+  const int ni = t.num_leaves - 1;
+  if (rows == nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.words_per_row * 4 <= kBmMaxRowBytes &&
+      t.bm_work != nullptr) {
+    hipLaunchKernelGGL(k_tree_bitmaps, dim3(ni), dim3(256), 0, s, a, t);
+    // one chunk of rows per workgroup: every chunk's loads are in flight at once
+    const int blocks = static_cast<int>(std::min<int64_t>((num_rows + kBmRowsPerBlock - 1) / kBmRowsPerBlock,
+                                                          1 << 30));
+    const size_t lds = sizeof(uint32_t) * kBmRowsPerBlock * a.words_per_row;
+    hipLaunchKernelGGL(k_add_tree_score_bm, dim3(blocks), dim3(kBmRowsPerBlock), lds, s, a, t, num_rows, score);
+    return;
+  }
   // one row per thread: many rows in flight hide the per-row load latency
   const int blocks = static_cast<int>(std::min<int64_t>((num_rows + 255) / 256, 1 << 20));
   if (t.num_leaves - 1 <= kMaxNodes) {

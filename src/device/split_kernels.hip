@@ -365,24 +365,39 @@ template <bool ROOT>
 __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
   __shared__ BlockScratch sc;
+  const long long t_entry = wall_clock64();
   const int f = blockIdx.x;
   const int side = blockIdx.y;
   const int tid = threadIdx.x;
+  // ---- independent loads first (one round trip): the feature, its mask, the scales and the
+  // Step record (read before it is tested)
   const Feature F = a.feat[f];
+  const int8_t used = a.tree_mask[f];
+  const double ig = a.scales[2], ih = a.scales[3];
+  const Step* st = a.st;
+  int done = 0, skip = 0, s = 0, s_count = 0;
+  ChildStats cl;
+  if (!ROOT) {
+    done = st->done;
+    skip = st->skip_find;
+    s = st->cs.s;
+    s_count = st->s_count;
+    cl = st->child[side];  // written with the histogram (StepBookkeeping)
+  }
   const int nbf = F.num_bin - F.offset;
   const int nb2 = 2 * nbf;
   int parity = 0, nblk_direct = -1;
-  const Step* st = a.st;
   if (!ROOT) {
-    if (st->done) return;
-    parity = (st->cs.s + 1) & 1;
+    if (done) return;
+    parity = (s + 1) & 1;
     // zero this feature's bins of the buffer the next step reduces into
     if (side == 0) {
       long long* nxt = StepScratch(a, parity + 1);
       for (int i = tid; i < nb2; i += kFindThreads) nxt[2 * F.hist_offset + i] = 0;
     }
-    if (st->skip_find) return;
-    const int nblk = HistBlocksFor(st->s_count, a.hist_max_blocks, a.hist_rows_cap);
+    if (skip) return;
+    KTraceAt(a, s, kTrFindEntry, t_entry);
+    const int nblk = HistBlocksFor(s_count, a.hist_max_blocks, a.hist_rows_cap);
     if (DirectPartials(a, nblk)) nblk_direct = nblk;
   }
   const SplitParams& p = a.p.sp;
@@ -415,7 +430,6 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     depth = 0;
     slot = 0;
   } else {
-    const ChildStats cl = st->child[side];  // written with the histogram (StepBookkeeping)
     L.sg = cl.sum_g;
     L.sh = cl.sum_h + 2 * kEpsilon;
     L.n = cl.global_count;
@@ -440,12 +454,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   o.mono = 0;
   o.pad = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
-  if (a.tree_mask[f] && !F.is_cat) {
+  if (used && !F.is_cat) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
     const unsigned long long* part = a.partials + F.hist_offset;
-    const double ig = a.scales[2], ih = a.scales[3];
     const bool stage = a.p.max_feature_bins <= kFindLdsBins;
     double* sg = s_bins;
     double* sh = s_bins + (stage ? a.p.max_feature_bins : 0);
@@ -478,6 +491,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
       }
     }
     __syncthreads();  // the workgroup's stores become visible to all its threads
+    if (!ROOT) KTrace(a, s, kTrFindLoaded);
     HistView hv;
     hv.lg = stage ? sg : nullptr;
     hv.lh = stage ? sh : nullptr;
@@ -485,10 +499,12 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     hv.inv_g = ig;
     hv.inv_h = ih;
     FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
+    if (!ROOT) KTrace(a, s, kTrFindScanned);
   } else {
     o.feature = -1;
   }
   if (tid == 0) a.feat_best[side * a.p.num_features + f] = o;
+  if (!ROOT) KTrace(a, s, kTrFindExit);
 }
 
 static size_t FindLds(const KArgs& a) {

@@ -82,6 +82,8 @@ void GPUTreeLearner::FreeBuffers() {
   d_tree_u32_ = nullptr;
   d_tree_i8_ = nullptr;
   d_tree_f64_ = nullptr;
+  d_tree_bm_ = nullptr;
+  d_tree_bm_meta_ = nullptr;
   tree_cap_ = cat_cap_ = 0;
 }
 
@@ -226,6 +228,9 @@ void GPUTreeLearner::UploadData() {
   const int hist_blocks = dev::HistGridBlocks();
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_);
   d_root_ = Alloc<double>(4);
+  d_root_parts_ = Alloc<double>(2 * static_cast<size_t>(dev::GradientBlocks(num_data_)));
+  d_max_parts_ = Alloc<float>(2 * static_cast<size_t>(std::max(dev::GradientBlocks(num_data_),
+                                                                dev::PackBlocks(num_data_))));
   d_leaf_values_ = Alloc<double>(n_leaves);
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_mask_), std::max(1, num_features_), hipHostMallocDefault));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_rec_), sizeof(dev::SplitRecord) * std::max(1, n_leaves - 1),
@@ -261,6 +266,13 @@ void GPUTreeLearner::UploadData() {
   a.partials = d_partials_;
   a.hist_max_blocks = hist_blocks;
   a.host_mode = 0;
+  a.ktrace = nullptr;
+  if (const char* kt = std::getenv("LGBM_AMD_KTRACE")) {
+    if (kt[0] == '1') {
+      d_ktrace_ = Alloc<long long>(static_cast<size_t>(n_leaves) * dev::kTraceSlots);
+      a.ktrace = d_ktrace_;
+    }
+  }
   a.root = d_root_;
   a.num_rows = num_data_;
   a.root_identity = 1;
@@ -363,15 +375,29 @@ void GPUTreeLearner::SetBaggingData(const Dataset* subset, const data_size_t* us
 }
 
 // ---------------------------------------------------------------- tree growth
-Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
-  common::ScopedTimer timer("GPUTreeLearner::Train");
-  HIPCHECK(hipSetDevice(device_id_));
-  // fixed-point scales of this tree: max |g|, max h over all rows (and ranks)
+void GPUTreeLearner::ResetAbsMax() {
   h_absmax_[0] = h_absmax_[1] = 0u;
   h_absmax_[2] = static_cast<uint32_t>(rows_cap_);
   h_absmax_[3] = 0u;
   HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 4, hipMemcpyHostToDevice, stream_));
-  dev::PackGH(gradients, hessians, d_gh_, num_data_, d_absmax_, stream_);
+}
+
+Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
+  common::ScopedTimer timer("GPUTreeLearner::Train");
+  HIPCHECK(hipSetDevice(device_id_));
+  // fixed-point scales of this tree: max |g|, max h over all rows (and ranks)
+  // the gradient kernel already interleaved (g, h) and found max|g| / max h when it wrote
+  // exactly these buffers (one model per iteration, not modified on the host since)
+  root_from_parts_ = gh_fresh_ && gradients == d_grad_ && hessians == d_hess_;
+  gh_fresh_ = false;
+  ResetAbsMax();
+  if (root_from_parts_) {
+    dev::ReduceParts(d_max_parts_, d_root_parts_, dev::GradientBlocks(num_data_), num_data_, d_absmax_, d_root_,
+                     stream_);
+  } else {
+    dev::PackGH(gradients, hessians, d_gh_, num_data_, d_max_parts_, stream_);
+    dev::ReduceParts(d_max_parts_, nullptr, dev::PackBlocks(num_data_), num_data_, d_absmax_, nullptr, stream_);
+  }
   AllreduceAbsMax();
   dev::ComputeScales(d_absmax_, rows_cap_, d_scales_, stream_);
   host_partition_fresh_ = false;
@@ -450,6 +476,66 @@ void GPUTreeLearner::KernelFloorProbe(const dev::KArgs& a) {
   (void)hipEventDestroy(e1);
 }
 
+// LGBM_AMD_KTRACE=1: in-kernel timestamps of the first workgroup of every step kernel
+// (100 MHz clock), averaged over the splits of each tree and printed to stderr
+void GPUTreeLearner::ReportKernelTrace(int num_splits) {
+  const int L = config_->num_leaves;
+  std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
+  HIPCHECK(hipMemcpy(t.data(), d_ktrace_, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
+  struct Seg {
+    const char* name;
+    int a, b;  // slots; b < 0: next split's slot -b-1
+  };
+  const Seg segs[] = {{"part.pick", dev::kTrPartEntry, dev::kTrPartPicked},
+                      {"part.rows", dev::kTrPartPicked, dev::kTrPartRows},
+                      {"part.bins", dev::kTrPartRows, dev::kTrPartBins},
+                      {"part.tail", dev::kTrPartBins, dev::kTrPartExit},
+                      {"gap>hist", dev::kTrPartExit, dev::kTrHistEntry},
+                      {"hist.rows", dev::kTrHistEntry, dev::kTrHistRows},
+                      {"hist.zero", dev::kTrHistRows, dev::kTrHistZeroed},
+                      {"hist.idx", dev::kTrHistZeroed, dev::kTrHistIdx},
+                      {"hist.gather", dev::kTrHistIdx, dev::kTrHistLoaded},
+                      {"hist.atomics", dev::kTrHistLoaded, dev::kTrHistAccum},
+                      {"hist.store", dev::kTrHistAccum, dev::kTrHistExit},
+                      {"gap>reduce", dev::kTrHistExit, dev::kTrRedEntry},
+                      {"reduce", dev::kTrRedEntry, dev::kTrRedExit},
+                      {"gap>find", dev::kTrRedExit, dev::kTrFindEntry},
+                      {"find.load", dev::kTrFindEntry, dev::kTrFindLoaded},
+                      {"find.scan", dev::kTrFindLoaded, dev::kTrFindScanned},
+                      {"find.tail", dev::kTrFindScanned, dev::kTrFindExit},
+                      {"gap>part", dev::kTrFindExit, -dev::kTrPartEntry - 1}};
+  std::string line = "ktrace (us, avg over splits " + std::to_string(std::min(num_splits, 8)) + ".." +
+                     std::to_string(num_splits - 1) + "):";
+  for (const Seg& sg : segs) {
+    double sum = 0.0;
+    int n = 0;
+    for (int s = std::min(num_splits, 8); s < num_splits; ++s) {
+      const long long ta = t[static_cast<size_t>(s) * dev::kTraceSlots + sg.a];
+      const long long tb = sg.b >= 0 ? t[static_cast<size_t>(s) * dev::kTraceSlots + sg.b]
+                                     : (s + 1 < num_splits ? t[static_cast<size_t>(s + 1) * dev::kTraceSlots - sg.b - 1]
+                                                           : 0);
+      if (ta <= 0 || tb <= 0 || tb < ta) continue;
+      sum += static_cast<double>(tb - ta) / 100.0;  // 100 MHz
+      ++n;
+    }
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), " %s=%.2f", sg.name, n ? sum / n : -1.0);
+    line += buf;
+  }
+  std::fprintf(stderr, "%s\n", line.c_str());
+  // entry skew of the first histogram workgroup's waves (split num_splits / 2)
+  const int sm = num_splits / 2;
+  std::string w = "ktrace hist wave entry offsets (us) split " + std::to_string(sm) + ":";
+  const long long* base = &t[static_cast<size_t>(sm) * dev::kTraceSlots];
+  for (int k = 0; k < 16; ++k) {
+    char buf[32];
+    const long long v = base[dev::kTrHistWave0 + k];
+    std::snprintf(buf, sizeof(buf), " %.2f", v > 0 ? (v - base[dev::kTrHistWave0]) / 100.0 : -1.0);
+    w += buf;
+  }
+  std::fprintf(stderr, "%s\n", w.c_str());
+}
+
 void GPUTreeLearner::DestroyGraph() {
   if (graph_exec_ != nullptr) (void)hipGraphExecDestroy(graph_exec_);
   graph_exec_ = nullptr;
@@ -463,8 +549,11 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
   // both step buffers start at zero; afterwards each split-scan zeroes the next one
   const size_t scratch_bytes = sizeof(long long) * 4 * static_cast<size_t>(total_bins_);
+  if (a.ktrace != nullptr) {
+    HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
+  }
   dev::TreeBegin(a, stream_);
-  dev::RootSum(a, stream_);
+  if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
   AllreduceRoot();
   HIPCHECK(hipMemsetAsync(d_scratch_, 0, scratch_bytes, stream_));
   dev::HistRoot(a, stream_);
@@ -501,7 +590,9 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
   const bool use_graph = !distributed && !(ng != nullptr && ng[0] == '1');
   if (use_graph) {
-    if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity) {
+    const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
+    if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
+        graph_root_mode_ != root_mode) {
       DestroyGraph();
       hipGraph_t g = nullptr;
       HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
@@ -511,6 +602,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       HIPCHECK(hipGraphDestroy(g));
       graph_rows_ = a.num_rows;
       graph_identity_ = a.root_identity;
+      graph_root_mode_ = root_mode;
     }
     HIPCHECK(hipGraphLaunch(graph_exec_, stream_));
   } else {
@@ -521,6 +613,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
                           hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   const int num_splits = h_step_->nsplit;
+  if (a.ktrace != nullptr) ReportKernelTrace(num_splits);
   if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {
     if (kp[0] == '1') KernelFloorProbe(a);
   }
@@ -781,6 +874,8 @@ void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
     d_tree_u32_ = Alloc<uint32_t>(cat_cap_);
     d_tree_i8_ = Alloc<int8_t>(std::max(cat_cap_, tree_cap_));
     d_tree_f64_ = Alloc<double>(std::max(cat_cap_, tree_cap_));
+    d_tree_bm_ = Alloc<unsigned long long>(4 * static_cast<size_t>(std::max(ni, config_->num_leaves)));
+    d_tree_bm_meta_ = Alloc<int32_t>(3 * static_cast<size_t>(std::max(ni, config_->num_leaves)));
   }
   std::vector<int32_t> i32(need_i32, 0);
   std::vector<uint32_t> u32(need_u32, 0);
@@ -810,6 +905,8 @@ void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
   t.cat_threshold_inner = d_tree_u32_ + ni;
   t.decision_type = d_tree_i8_;
   t.leaf_value = d_tree_f64_;
+  t.bm_work = d_tree_bm_;
+  t.bm_meta = d_tree_bm_meta_;
   const bool oob_only = oob_cnt_ > 0 && in_trained_update_;
   if (oob_only) {
     dev::AddTreeScore(args_, t, d_oob_, oob_cnt_, score, stream_);
@@ -855,11 +952,22 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   g.score = d_score_;
   g.grad = d_grad_;
   g.hess = d_hess_;
+  g.gh = nullptr;
+  g.max_parts = nullptr;
+  g.root_parts = nullptr;
+  const bool fuse = ntpi == 1 && spec.kind != DeviceGradKind::MulticlassSoftmax;
+  if (fuse) {
+    g.gh = d_gh_;
+    g.max_parts = d_max_parts_;
+    g.root_parts = d_root_parts_;
+  }
   dev::Gradients(g, stream_);
+  gh_fresh_ = fuse;
   return true;
 }
 
 void GPUTreeLearner::UploadGradients(const score_t* g, const score_t* h, int64_t n) {
+  gh_fresh_ = false;
   HIPCHECK(hipMemcpyAsync(d_grad_, g, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipMemcpyAsync(d_hess_, h, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));

@@ -77,6 +77,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void EnqueueTree(const dev::KArgs& a);
   void DestroyGraph();
   void KernelFloorProbe(const dev::KArgs& a);
+  void ResetAbsMax();
+  void ReportKernelTrace(int num_splits);
   void BuildRangeHistogram(int leaf, int slot);
   void DownloadPartitionToHost() const;
   void AllreduceScratch(int parity);
@@ -117,8 +119,14 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   unsigned long long* d_partials_ = nullptr;  // per-workgroup partial histograms
   std::vector<dev::Feature> h_feats_;          // host copy of the feature records
   hipGraphExec_t graph_exec_ = nullptr;        // captured tree (single-process device mode)
+  long long* d_ktrace_ = nullptr;              // LGBM_AMD_KTRACE timestamps
   int graph_rows_ = -1;
   int graph_identity_ = -1;
+  int graph_root_mode_ = -1;
+  bool gh_fresh_ = false;         // d_gh_ / absmax / root partials written by the gradient kernel
+  bool root_from_parts_ = false;  // this tree's gradients came packed from the gradient kernel
+  double* d_root_parts_ = nullptr;
+  float* d_max_parts_ = nullptr;
   double* d_root_ = nullptr;
   double* d_score_ = nullptr;
   float* d_grad_ = nullptr;
@@ -135,6 +143,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   uint32_t* d_tree_u32_ = nullptr;
   int8_t* d_tree_i8_ = nullptr;
   double* d_tree_f64_ = nullptr;
+  unsigned long long* d_tree_bm_ = nullptr;  // per-node decision bitmaps (score traversal)
+  int32_t* d_tree_bm_meta_ = nullptr;
   size_t tree_cap_ = 0;
   size_t cat_cap_ = 0;
   // pinned host staging

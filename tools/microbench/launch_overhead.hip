@@ -35,6 +35,29 @@ __global__ void k_dep(int* buf, int depth) {
   for (int d = 0; d < depth; ++d) idx = buf[16 + idx * 32 + d];
   if (threadIdx.x == 0) buf[16 + (blockIdx.x & 7) * 32 + 40] = idx;  // dirty a line
 }
+// every wave of a 1024-thread workgroup reads the same 16 words the previous kernel wrote
+__global__ __launch_bounds__(1024) void k_hot_all(int* buf) {
+  extern __shared__ int lds[];
+  int acc = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) acc += buf[8192 + k];
+  lds[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0 && blockIdx.x == 0) buf[8192 + (lds[5] & 15)] = acc + 1;
+}
+// only wave 0 reads them; the others get them through LDS
+__global__ __launch_bounds__(1024) void k_hot_one(int* buf) {
+  extern __shared__ int lds[];
+  if (threadIdx.x < 64) {
+    int acc = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) acc += buf[8192 + k];
+    lds[threadIdx.x] = acc;
+  }
+  __syncthreads();
+  const int acc = lds[threadIdx.x & 63];
+  if (threadIdx.x == 0 && blockIdx.x == 0) buf[8192 + (acc & 15)] = acc + 1;
+}
 __global__ void k_init(int* buf) {
   for (int i = threadIdx.x; i < 4096; i += blockDim.x) buf[16 + i] = 0;
 }
@@ -69,13 +92,17 @@ int main() {
       {"lds 256x1024 56K", 3, 256, 1024, 57344}, {"lds 512x1024 56K", 3, 512, 1024, 57344},
       {"dep1 1x64", 11, 1, 64, 0}, {"dep2 1x64", 12, 1, 64, 0}, {"dep4 1x64", 14, 1, 64, 0},
       {"dep8 1x64", 18, 1, 64, 0}, {"dep2 896x256", 12, 896, 256, 0}, {"dep4 256x256", 14, 256, 256, 0},
+      {"hot-all 256x1024", 30, 256, 1024, 8192}, {"hot-one 256x1024", 31, 256, 1024, 8192},
+      {"hot-all 64x1024", 30, 64, 1024, 8192}, {"hot-one 64x1024", 31, 64, 1024, 8192},
   };
   auto launch = [&](const Case& c) {
     if (c.kind == 0) hipLaunchKernelGGL(k_small, dim3(c.grid), dim3(c.block), 0, s, flag);
     if (c.kind == 1) hipLaunchKernelGGL(k_big, dim3(c.grid), dim3(c.block), 0, s, b, flag);
     if (c.kind == 2) hipLaunchKernelGGL(k_chain, dim3(c.grid), dim3(c.block), 0, s, flag);
     if (c.kind == 3) hipLaunchKernelGGL(k_lds, dim3(c.grid), dim3(c.block), c.lds, s, flag);
-    if (c.kind > 10) hipLaunchKernelGGL(k_dep, dim3(c.grid), dim3(c.block), 0, s, flag, c.kind - 10);
+    if (c.kind > 10 && c.kind < 30) hipLaunchKernelGGL(k_dep, dim3(c.grid), dim3(c.block), 0, s, flag, c.kind - 10);
+    if (c.kind == 30) hipLaunchKernelGGL(k_hot_all, dim3(c.grid), dim3(c.block), c.lds, s, flag);
+    if (c.kind == 31) hipLaunchKernelGGL(k_hot_one, dim3(c.grid), dim3(c.block), c.lds, s, flag);
   };
   hipLaunchKernelGGL(k_init, dim3(1), dim3(256), 0, s, flag);
   for (const Case& c : cases) {
