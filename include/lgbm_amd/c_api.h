@@ -206,6 +206,8 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_RcclUniqueIdSize(int* out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclGetUniqueId(char* out_id);
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclInit(int num_ranks, int rank, int device_id, const char* unique_id);
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclFree();
+/* runs every device collective on small buffers and checks the sums (1 = ok) */
+LIGHTGBM_C_EXPORT int LGBM_AMD_RcclSelfTest(int* out_ok);
 /* number of visible GPUs (0 without a device) */
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCount(int* out);
 /* phase timers (LGBM_AMD_TIMETAG) as "name=seconds;..." */

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "lgbm_amd/c_api.h"
 #include "lgbm_amd/log.h"
@@ -97,6 +98,60 @@ int LGBM_AMD_RcclInit(int num_ranks, int rank, int device_id, const char* unique
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
     Network::SetDeviceComm(std::make_shared<RcclComm>(num_ranks, rank, id));
+  } catch (std::exception& e) {
+    Log::Warning("%s", e.what());
+    return -1;
+  }
+  return 0;
+}
+
+// every collective of the device comm on small device buffers, checked on the host:
+// rank r contributes (r + 1) * i to element i, so sums are (n (n + 1) / 2) * i
+int LGBM_AMD_RcclSelfTest(int* out_ok) {
+  try {
+    DeviceComm* dc = Network::device_comm();
+    if (dc == nullptr) Log::Fatal("no device comm (call LGBM_AMD_RcclInit first)");
+    const int n = dc->size(), r = dc->rank();
+    const size_t cnt = 1000;
+    hipStream_t s;
+    if (hipStreamCreate(&s) != hipSuccess) Log::Fatal("hipStreamCreate failed");
+    long long* di64;
+    double* df64;
+    uint32_t* du32;
+    if (hipMalloc(&di64, cnt * sizeof(long long)) != hipSuccess || hipMalloc(&df64, cnt * sizeof(double)) != hipSuccess ||
+        hipMalloc(&du32, cnt * sizeof(uint32_t)) != hipSuccess) {
+      Log::Fatal("hipMalloc failed");
+    }
+    std::vector<long long> hi(cnt);
+    std::vector<double> hf(cnt);
+    std::vector<uint32_t> hu(cnt);
+    for (size_t i = 0; i < cnt; ++i) {
+      hi[i] = static_cast<long long>((r + 1) * i) - 500;
+      hf[i] = 0.5 * (r + 1) * i;
+      hu[i] = static_cast<uint32_t>(r * 7 + i);
+    }
+    (void)hipMemcpy(di64, hi.data(), cnt * sizeof(long long), hipMemcpyHostToDevice);
+    (void)hipMemcpy(df64, hf.data(), cnt * sizeof(double), hipMemcpyHostToDevice);
+    (void)hipMemcpy(du32, hu.data(), cnt * sizeof(uint32_t), hipMemcpyHostToDevice);
+    dc->AllreduceSumI64(di64, cnt, s);
+    dc->AllreduceSumF64(df64, cnt, s);
+    dc->AllreduceMaxU32(du32, cnt, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(hi.data(), di64, cnt * sizeof(long long), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hf.data(), df64, cnt * sizeof(double), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hu.data(), du32, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    const long long tri = static_cast<long long>(n) * (n + 1) / 2;
+    bool ok = true;
+    for (size_t i = 0; i < cnt; ++i) {
+      ok = ok && hi[i] == tri * static_cast<long long>(i) - 500LL * n;
+      ok = ok && hf[i] == 0.5 * static_cast<double>(tri) * static_cast<double>(i);
+      ok = ok && hu[i] == static_cast<uint32_t>((n - 1) * 7 + i);
+    }
+    (void)hipFree(di64);
+    (void)hipFree(df64);
+    (void)hipFree(du32);
+    (void)hipStreamDestroy(s);
+    *out_ok = ok ? 1 : 0;
   } catch (std::exception& e) {
     Log::Warning("%s", e.what());
     return -1;

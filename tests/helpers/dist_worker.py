@@ -24,11 +24,14 @@ def make_data(n=4000, f=10, seed=7):
 
 def main():
     learner, out_dir = sys.argv[1], sys.argv[2]
-    rank, world, _ = torch_dist.init_network(use_rccl=False)
+    device = os.environ.get("LGBM_TEST_DEVICE", "cpu")
+    # device collectives: RCCL needs one GPU per rank; with every rank on one GPU the
+    # device learner falls back to the host collectives (same code path above the comm)
+    rank, world, _ = torch_dist.init_network(use_rccl=os.environ.get("LGBM_TEST_RCCL", "0") == "1")
     X, y = make_data()
     params = {"objective": "binary", "num_leaves": 15, "learning_rate": 0.1, "verbose": -1,
               "tree_learner": learner, "num_machines": world, "min_data_in_leaf": 20, "seed": 3,
-              "deterministic": True}
+              "deterministic": True, "device_type": device}
     if learner in ("data", "voting"):
         # pre-partitioned rows: every rank holds its own shard
         idx = np.arange(rank, X.shape[0], world)

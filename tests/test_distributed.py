@@ -26,12 +26,14 @@ def _free_port():
     return port
 
 
-def _run(learner, tmp_path, world=2):
+def _run(learner, tmp_path, world=2, device="cpu"):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), OMP_NUM_THREADS="2", HIP_VISIBLE_DEVICES="")
+                   MASTER_PORT=str(port), OMP_NUM_THREADS="2", LGBM_TEST_DEVICE=device)
+        if device == "cpu":
+            env["HIP_VISIBLE_DEVICES"] = ""
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "helpers", "dist_worker.py"), learner,
                                        str(tmp_path)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     outs = []
@@ -79,3 +81,18 @@ def test_data_parallel_close_to_serial(tmp_path):
     serial = lgb.train(params, lgb.Dataset(X, y), num_boost_round=20)
     # bins are found on shards, so splits can differ slightly; the fit must not
     assert abs(roc_auc_score(y, preds[0]) - roc_auc_score(y, serial.predict(X))) < 0.01
+
+
+@pytest.mark.gpu
+def test_device_data_parallel_two_ranks_one_gpu(tmp_path, gpu_available):
+    """Data-parallel device learner, both ranks on one GPU (host collectives between them):
+    ranks agree, and the fit matches the CPU data-parallel run's quality."""
+    models, preds = _run("data", tmp_path, device="gpu")
+    assert _trees(models[0]) == _trees(models[1])
+    X, y = make_data()
+    auc = roc_auc_score(y, preds[0])
+    assert auc > 0.8
+    cpu_dir = tmp_path / "cpu"
+    cpu_dir.mkdir()
+    _, cpu_preds = _run("data", cpu_dir, device="cpu")
+    assert abs(auc - roc_auc_score(y, cpu_preds[0])) < 0.01

@@ -1,8 +1,9 @@
 """MI355X learner vs the CPU serial learner (same binned data, same parameters).
 
-Histograms are fp32 on the device and fp64 on the host, and the device scans evaluate
-thresholds with parallel prefix sums, so trees are compared structurally (split
-features / thresholds of the first tree) and by metric, not bit for bit.
+Device histograms are exact int64 sums of fixed-point (g, h) (per-tree power-of-two
+scales), the host's are fp64 sums, and the device scans evaluate thresholds with parallel
+prefix sums, so trees are compared structurally (split features / thresholds of the
+first tree) and by metric, not bit for bit.
 """
 import numpy as np
 import pytest
@@ -95,3 +96,23 @@ def test_multiclass_on_device(gpu_available):
     b = _train(X, y, "gpu", rounds=20, objective="multiclass", num_class=3)
     acc = np.mean(np.argmax(b.predict(X), axis=1) == y)
     assert acc > 0.85
+
+
+def test_rccl_comm_single_rank(gpu_available):
+    """The RCCL device communicator (the multi-GPU histogram all-reduce path) on one rank."""
+    import ctypes
+    import numpy as np
+    from lightgbmv1_amd.basic import _load_lib
+    lib = _load_lib()
+    size = ctypes.c_int(0)
+    assert lib.LGBM_AMD_RcclUniqueIdSize(ctypes.byref(size)) == 0
+    uid = np.zeros(size.value, dtype=np.uint8)
+    assert lib.LGBM_AMD_RcclGetUniqueId(uid.ctypes.data_as(ctypes.c_char_p)) == 0
+    assert lib.LGBM_AMD_RcclInit(ctypes.c_int(1), ctypes.c_int(0), ctypes.c_int(0),
+                                 uid.ctypes.data_as(ctypes.c_char_p)) == 0
+    ok = ctypes.c_int(0)
+    try:
+        assert lib.LGBM_AMD_RcclSelfTest(ctypes.byref(ok)) == 0
+        assert ok.value == 1
+    finally:
+        lib.LGBM_AMD_RcclFree()
