@@ -193,6 +193,11 @@ class GBDT {
   static constexpr data_size_t kBaggingRandBlock = 1024;
   bool balanced_bagging_ = false;
   bool need_re_bagging_ = false;
+  // device bagging / GOSS: the device generators restart (seed + block) when the host's would
+  bool device_sampler_reset_ = true;
+  int device_sampler_seed_ = 0;
+  // a device draw of the bag (or -1: draw on the host)
+  data_size_t DeviceBagging(bool goss);
   std::vector<bool> class_need_train_;
   bool is_constant_hessian_ = false;
   bool average_output_ = false;

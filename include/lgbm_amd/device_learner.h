@@ -12,6 +12,21 @@
 
 namespace lgbm_amd {
 
+// one bagging / GOSS draw on the device (reference gbdt.cpp:162-243, goss.hpp:103-179):
+// the generator of 1024-row block b starts at seed + b and persists across draws until
+// `reset` (the reference re-creates bagging_rands_ in ResetBaggingConfig / GOSS::ResetGoss)
+struct DeviceSampleSpec {
+  bool goss = false;
+  bool balanced = false;
+  bool reset = false;
+  int seed = 3;
+  double fraction = 1.0, pos_fraction = 1.0, neg_fraction = 1.0;
+  double top_rate = 0.2, other_rate = 0.1;
+  int num_tree_per_iteration = 1;
+  const label_t* label = nullptr;                    // balanced bagging
+  std::vector<data_size_t>* host_indices = nullptr;  // if set: the bag (in-bag, then out-of-bag) is copied back
+};
+
 class DeviceTreeLearner {
  public:
   virtual ~DeviceTreeLearner() = default;
@@ -28,6 +43,9 @@ class DeviceTreeLearner {
   // device gradients for a point-wise objective; false if the spec is unsupported
   virtual bool ComputeGradients(const DeviceGradSpec& spec, int num_tree_per_iteration) = 0;
   virtual void UploadGradients(const score_t* g, const score_t* h, int64_t n) = 0;
+  // draw a bag on the device and make it the learner's bagging data (GOSS also rescales
+  // the sampled rows' device gradients); returns the in-bag count
+  virtual data_size_t DeviceSample(const DeviceSampleSpec& spec) = 0;
   virtual void DownloadGradients(score_t* g, score_t* h, int64_t n) = 0;
   virtual score_t* device_gradients() = 0;
   virtual score_t* device_hessians() = 0;

@@ -20,7 +20,21 @@ namespace lgbm_amd {
 // kinds understood by the device gradient kernel
 enum class DeviceGradKind : int {
   None = 0, L2 = 1, L1 = 2, Huber = 3, Fair = 4, Poisson = 5, Quantile = 6, Mape = 7, Gamma = 8, Tweedie = 9,
-  Binary = 10, CrossEntropy = 11, CrossEntropyLambda = 12, MulticlassSoftmax = 13, MulticlassOVA = 14
+  Binary = 10, CrossEntropy = 11, CrossEntropyLambda = 12, MulticlassSoftmax = 13, MulticlassOVA = 14,
+  Lambdarank = 15, RankXendcg = 16  // listwise: one workgroup per query (src/device/rank_kernels.hip)
+};
+
+// query-level tables of the listwise objectives (host pointers, uploaded once)
+struct DeviceRankSpec {
+  data_size_t num_queries = 0;
+  data_size_t max_query_docs = 0;
+  const data_size_t* query_boundaries = nullptr;  // [num_queries + 1]
+  const double* inv_max_dcg = nullptr;            // [num_queries] (lambdarank)
+  const double* label_gain = nullptr;
+  int num_label_gain = 0;
+  bool norm = true;
+  double sigmoid = 1.0, sig_min = -25.0, sig_max = 25.0, sig_factor = 1.0;
+  const unsigned* rng_states = nullptr;  // [num_queries] per-query LCG states (xendcg); the device owns them after upload
 };
 
 struct DeviceGradSpec {
@@ -31,6 +45,7 @@ struct DeviceGradSpec {
   const label_t* label = nullptr;         // host pointers; uploaded by the learner
   const label_t* weights = nullptr;
   const label_t* label_weight_arr = nullptr;  // per-row factor (MAPE)
+  DeviceRankSpec rank;                        // Lambdarank / RankXendcg only
 };
 
 class ObjectiveFunction {

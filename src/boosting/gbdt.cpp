@@ -3,6 +3,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <fstream>
 #include <sstream>
 
@@ -239,6 +240,8 @@ void GBDT::ResetBaggingConfig(const Config* cfg, bool is_change_dataset) {
     for (data_size_t i = 0; i < (num_data_ + kBaggingRandBlock - 1) / kBaggingRandBlock; ++i) {
       bagging_rands_.emplace_back(config_->bagging_seed + i);
     }
+    device_sampler_seed_ = config_->bagging_seed;
+    device_sampler_reset_ = true;
     need_re_bagging_ = true;
   } else {
     bag_data_cnt_ = num_data_;
@@ -311,10 +314,42 @@ void GBDT::Bagging(int iter) {
   if ((bag_data_cnt_ < num_data_ && config_->bagging_freq > 0 && iter % config_->bagging_freq == 0) ||
       need_re_bagging_) {
     need_re_bagging_ = false;
+    const data_size_t dev_cnt = DeviceBagging(false);
+    if (dev_cnt >= 0) {
+      bag_data_cnt_ = dev_cnt;
+      Log::Debug("Re-bagging on the device, using %d data to train", bag_data_cnt_);
+      return;
+    }
     bag_data_cnt_ = RunBagging([this](data_size_t s, data_size_t c, data_size_t* b) { return BaggingHelper(s, c, b); });
     Log::Debug("Re-bagging, using %d data to train", bag_data_cnt_);
     tree_learner_->SetBaggingData(nullptr, bag_data_indices_.data(), bag_data_cnt_);
   }
+}
+
+// the MI355X learner draws the bag itself: same generators (Random(bagging_seed + block)
+// per 1024 rows), so bagging is bit-identical to the host draw; GOSS equals the
+// reference's draw with one sampling block per 1024 rows (see src/device/sample_kernels.hip)
+data_size_t GBDT::DeviceBagging(bool goss) {
+  if (device_learner_ == nullptr) return -1;
+  const char* e = std::getenv("LGBM_AMD_HOST_BAGGING");
+  if (e != nullptr && e[0] == '1') return -1;
+  DeviceSampleSpec sp;
+  sp.goss = goss;
+  sp.balanced = balanced_bagging_;
+  sp.reset = device_sampler_reset_;
+  sp.seed = device_sampler_seed_;
+  sp.fraction = config_->bagging_fraction;
+  sp.pos_fraction = config_->pos_bagging_fraction;
+  sp.neg_fraction = config_->neg_bagging_fraction;
+  sp.top_rate = config_->top_rate;
+  sp.other_rate = config_->other_rate;
+  sp.num_tree_per_iteration = num_tree_per_iteration_;
+  sp.label = train_data_->metadata().label();
+  // leaf-output renewal (L1 / quantile / MAPE) reads the bag on the host
+  const bool need_host = objective_ != nullptr && objective_->IsRenewTreeOutput();
+  sp.host_indices = need_host ? &bag_data_indices_ : nullptr;
+  device_sampler_reset_ = false;
+  return device_learner_->DeviceSample(sp);
 }
 
 double* GBDT::HostTrainScore() {

@@ -158,6 +158,8 @@ void GOSS::ResetGoss() {
   for (data_size_t i = 0; i < (num_data_ + kBaggingRandBlock - 1) / kBaggingRandBlock; ++i) {
     bagging_rands_.emplace_back(config_->bagging_seed + i);
   }
+  device_sampler_seed_ = config_->bagging_seed;
+  device_sampler_reset_ = true;
   bag_data_cnt_ = num_data_;
 }
 
@@ -221,6 +223,11 @@ data_size_t GOSS::BaggingHelper(data_size_t start, data_size_t cnt, data_size_t*
 void GOSS::Bagging(int iter) {
   bag_data_cnt_ = num_data_;
   if (iter < static_cast<int>(1.0f / config_->learning_rate)) return;
+  const data_size_t dev_cnt = DeviceBagging(true);
+  if (dev_cnt >= 0) {
+    bag_data_cnt_ = dev_cnt;
+    return;
+  }
   const int64_t total = static_cast<int64_t>(num_data_) * num_tree_per_iteration_;
   if (device_learner_ != nullptr) device_learner_->DownloadGradients(gradients_.data(), hessians_.data(), total);
   bag_data_cnt_ = RunBagging([this](data_size_t s, data_size_t c, data_size_t* b) { return BaggingHelper(s, c, b); });

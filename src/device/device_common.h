@@ -41,6 +41,10 @@ inline int GridFor(int64_t n) {
 
 __device__ __forceinline__ int RoundIntD(double x) { return static_cast<int>(x + 0.5f); }
 
+// rows of the tree's root: a device-drawn bag keeps its size on the device (so the tree's
+// captured graph does not depend on it)
+__device__ __forceinline__ int RootRows(const KArgs& a) { return a.num_rows_dev ? *a.num_rows_dev : a.num_rows; }
+
 // bin of storage column `group` for `row`, column-major copy (partition kernels)
 __device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int group) {
   if (a.bin_bytes == 1) return a.bins_col[static_cast<int64_t>(group) * a.num_data + row];

@@ -49,7 +49,7 @@ __device__ __forceinline__ bool HistRows(const KArgs& a, bool from_step, int* be
                                          const int32_t** src) {
   if (MODE == 0) {
     *begin = 0;
-    *count = a.num_rows;
+    *count = RootRows(a);
     *src = a.root_identity ? nullptr : a.idx;
   } else if (MODE == 2) {
     *begin = a.range_begin;
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(KArgs a) {
   int begin = 0, count = 0, ts = -1;
   const int32_t* src = nullptr;
   if (MODE == 0) {
-    count = a.num_rows;
+    count = RootRows(a);
     src = a.root_identity ? nullptr : a.idx;
   } else if (MODE == 2) {
     begin = a.range_begin;

@@ -34,7 +34,8 @@ struct KArgs {
   unsigned long long* partials;  // [hist_max_blocks][total_bins] per-workgroup packed (g|h)
   const double* scales;      // [scale_g, scale_h, 1/scale_g, 1/scale_h] of the current tree
   double* root;              // [sum_g, sum_h, count]
-  int32_t num_rows;          // local rows in the root (or the explicit range)
+  int32_t num_rows;          // local rows in the root (or the explicit range); upper bound if num_rows_dev
+  const int32_t* num_rows_dev;  // root rows held on the device (a bag drawn on the device), or null
   int32_t root_identity;     // root rows are 0..num_rows-1 (indices written by the root pass)
   int32_t bin_bytes;         // 1 or 2
   int32_t words_per_row;     // 32-bit words per row
@@ -147,6 +148,55 @@ struct GradArgs {
   double* root_parts;        //   (sum g, sum h), [GradientBlocks][2] each
 };
 void Gradients(const GradArgs& g, hipStream_t s);
+// listwise ranking gradients (LambdaRank-NDCG / XE-NDCG), one workgroup per query
+constexpr int kRankKindLambdarank = 15;
+constexpr int kRankKindXendcg = 16;
+constexpr int kRankMaxDocs = 2048;       // documents of one query staged in LDS
+constexpr int kRankSigmoidBins = 1024 * 1024;  // the reference's sigmoid table size
+struct RankArgs {
+  int32_t kind;
+  int32_t num_queries;
+  const int32_t* qb;          // [num_queries + 1] query boundaries
+  const float* label;
+  const float* weights;       // per-row weights, may be null
+  const double* score;
+  float* grad;
+  float* hess;
+  const double* inv_max_dcg;  // [num_queries] 1 / max DCG@truncation (lambdarank)
+  const double* label_gain;   // label -> gain
+  const double* discount;     // position -> 1 / log2(2 + i)
+  double sigmoid;
+  double sig_min, sig_max, sig_factor;  // sigmoid table domain and bins per unit
+  int32_t norm;               // lambdarank_norm
+  uint32_t* rng;              // [num_queries] LCG states (xendcg), advanced in place
+};
+void RankGradients(const RankArgs& ra, hipStream_t s);
+
+// row sampling (bagging / GOSS) with the reference's per-1024-row generators: in-bag rows
+// (ascending) then out-of-bag rows, and the in-bag count, written on the device
+constexpr int kSampleBlockRows = 1024;
+struct SampleArgs {
+  int64_t num_data;
+  int64_t num_blocks;      // SampleBlocks(num_data)
+  int32_t goss;            // 0 bagging, 1 GOSS
+  int32_t balanced;        // bagging with pos/neg fractions (label > 0 is positive)
+  int32_t num_class;       // GOSS: models per iteration (row weight = sum over them of |g * h|)
+  double fraction, pos_fraction, neg_fraction;
+  double top_rate, other_rate;
+  const float* label;      // balanced bagging
+  float* grad;             // GOSS: [num_class][num_data]; sampled small-gradient rows are rescaled
+  float* hess;
+  uint32_t* rng;           // [num_blocks] generator states, advanced in place
+  uint8_t* codes;          // [num_data] scratch
+  int32_t* block_cnt;      // [num_blocks] scratch
+  int32_t* block_off;      // [num_blocks] scratch
+  int32_t* bag;            // [num_data] out: in-bag rows
+  int32_t* oob;            // [num_data] out: out-of-bag rows
+  int32_t* bag_count;      // out: number of in-bag rows
+};
+int SampleBlocks(int64_t n);
+void SampleRows(const SampleArgs& s, hipStream_t st);
+
 int GradientBlocks(int64_t n);
 // absmax[0..1] (and root = (sum g, sum h, n) if root_parts) from per-workgroup partials
 void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, uint32_t* absmax,

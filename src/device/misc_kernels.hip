@@ -85,7 +85,7 @@ __global__ void k_tree_begin(KArgs a) {
   for (int l = threadIdx.x; l < L; l += blockDim.x) {
     Leaf lf;
     lf.begin = 0;
-    lf.count = l == 0 ? a.num_rows : 0;
+    lf.count = l == 0 ? RootRows(a) : 0;
     lf.global_count = lf.count;
     lf.depth = 0;
     lf.slot = l;
@@ -115,7 +115,7 @@ void TreeBegin(const KArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_tree_begin,
 __global__ __launch_bounds__(256) void k_root_sum(KArgs a) {
   __shared__ double sh[8];
   double sg = 0.0, shh = 0.0;
-  const int n = a.num_rows;
+  const int n = RootRows(a);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int r = a.root_identity ? i : a.idx[i];
     const float2 v = reinterpret_cast<const float2*>(a.gh)[r];

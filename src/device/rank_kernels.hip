@@ -1,0 +1,216 @@
+// Listwise ranking gradients on device: LambdaRank-NDCG and XE-NDCG, one workgroup per
+// query (reference src/objective/rank_objective.hpp:98-285 lambdarank, :288-366 xendcg).
+//
+// A query's documents are staged in LDS (score, label, rank position).  The stable
+// descending sort of the reference (std::stable_sort by score) is computed as a rank:
+// pos(d) = #{j : s_j > s_d} + #{j < d : s_j == s_d}, O(cnt^2 / threads) LDS broadcasts
+// (queries are short: MS-LTR averages ~120 documents).  Every document then accumulates
+// its lambda / hessian over the pairs it takes part in -- as the higher-labelled side
+// (the reference's inner loop) and as the lower-labelled side (its `lambdas[low] -=`) --
+// in double, so no atomics are needed and the result does not depend on scheduling.
+// The sum of |lambdas| used by lambdarank_norm is a workgroup reduction in double.
+#include "device_common.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+constexpr int kRankThreads = 128;  // two waves per query
+
+__device__ __forceinline__ double BlockSum(double v, double* red) {
+  for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  const int w = threadIdx.x / kWave;
+  __syncthreads();  // red may still be read by a previous reduction
+  if ((threadIdx.x & (kWave - 1)) == 0) red[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < kRankThreads / kWave; ++i) t += red[i];
+  return t;
+}
+
+// the reference's 1M-entry sigmoid table, evaluated at the same quantised abscissa
+__device__ __forceinline__ double RankSigmoid(const RankArgs& ra, double x) {
+  double q;
+  if (x <= ra.sig_min) {
+    q = ra.sig_min;
+  } else if (x >= ra.sig_max) {
+    q = static_cast<double>(kRankSigmoidBins - 1) / ra.sig_factor + ra.sig_min;
+  } else {
+    const size_t i = static_cast<size_t>((x - ra.sig_min) * ra.sig_factor);
+    q = static_cast<double>(i) / ra.sig_factor + ra.sig_min;
+  }
+  return 1.0f / (1.0f + exp(q * ra.sigmoid));
+}
+
+__global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
+  __shared__ double s_score[kRankMaxDocs];
+  __shared__ int s_label[kRankMaxDocs];
+  __shared__ int s_pos[kRankMaxDocs];
+  __shared__ double s_red[kRankThreads / kWave];
+  __shared__ double s_edge[3];  // score at sorted positions 0, cnt-1, cnt-2
+  const int q = blockIdx.x;
+  const int b = ra.qb[q];
+  const int cnt = ra.qb[q + 1] - b;
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+    s_score[i] = ra.score[b + i];
+    s_label[i] = static_cast<int>(ra.label[b + i]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+    const double si = s_score[i];
+    int p = 0;
+    for (int j = 0; j < cnt; ++j) {
+      const double sj = s_score[j];
+      p += (sj > si) | ((sj == si) & (j < i));
+    }
+    s_pos[i] = p;
+    if (p == 0) s_edge[0] = si;
+    if (p == cnt - 1) s_edge[1] = si;
+    if (p == cnt - 2) s_edge[2] = si;
+  }
+  __syncthreads();
+  const double best = s_edge[0];
+  const double worst = (cnt - 1 > 0 && s_edge[1] == kMinScore) ? s_edge[2] : s_edge[1];
+  const double inv_max = ra.inv_max_dcg[q];
+  const double sig = ra.sigmoid;
+  const bool norm = ra.norm != 0 && best != worst;
+  double sum_lambdas = 0.0;
+  for (int d = threadIdx.x; d < cnt; d += kRankThreads) {
+    const double sd = s_score[d];
+    double lam = 0.0, hes = 0.0;
+    if (sd != kMinScore) {
+      const int ld = s_label[d];
+      const double gd = ra.label_gain[ld];
+      const double discd = ra.discount[s_pos[d]];
+      for (int j = 0; j < cnt; ++j) {
+        const int lj = s_label[j];
+        const double sj = s_score[j];
+        if (j == d || lj == ld || sj == kMinScore) continue;
+        const bool d_high = ld > lj;
+        const double hs = d_high ? sd : sj, ls = d_high ? sj : sd;
+        const double ds = hs - ls;
+        const double gap = d_high ? gd - ra.label_gain[lj] : ra.label_gain[lj] - gd;
+        const double pd = fabs(discd - ra.discount[s_pos[j]]);
+        double dn = gap * pd * inv_max;
+        if (norm) dn /= (0.01f + fabs(ds));
+        double pl = RankSigmoid(ra, ds);
+        double ph = pl * (1.0f - pl);
+        pl *= -sig * dn;
+        ph *= sig * sig * dn;
+        hes += ph;
+        if (d_high) {
+          lam += pl;
+          sum_lambdas -= 2 * pl;
+        } else {
+          lam -= pl;
+        }
+      }
+    }
+    ra.grad[b + d] = static_cast<float>(lam);
+    ra.hess[b + d] = static_cast<float>(hes);
+  }
+  const double total = BlockSum(sum_lambdas, s_red);
+  const bool renorm = ra.norm != 0 && total > 0;
+  const double nf = renorm ? log2(1 + total) / total : 1.0;
+  if (!renorm && ra.weights == nullptr) return;
+  for (int d = threadIdx.x; d < cnt; d += kRankThreads) {
+    double g = ra.grad[b + d], h = ra.hess[b + d];
+    if (renorm) {
+      g = static_cast<float>(g * nf);
+      h = static_cast<float>(h * nf);
+    }
+    if (ra.weights != nullptr) {
+      g *= ra.weights[b + d];
+      h *= ra.weights[b + d];
+    }
+    ra.grad[b + d] = static_cast<float>(g);
+    ra.hess[b + d] = static_cast<float>(h);
+  }
+}
+
+// XE-NDCG (reference rank_objective.hpp:304-366): softmax over the query, per-document
+// gamma draws from the query's own LCG (state advanced in place across iterations).
+__global__ __launch_bounds__(kRankThreads) void k_xendcg(RankArgs ra) {
+  __shared__ double s_rho[kRankMaxDocs];
+  __shared__ double s_par[kRankMaxDocs];
+  __shared__ float s_lam[kRankMaxDocs];
+  __shared__ double s_red[kRankThreads / kWave];
+  const int q = blockIdx.x;
+  const int b = ra.qb[q];
+  const int cnt = ra.qb[q + 1] - b;
+  if (cnt <= 1) {
+    for (int i = threadIdx.x; i < cnt; i += kRankThreads) ra.grad[b + i] = ra.hess[b + i] = 0.0f;
+    return;
+  }
+  // softmax (common::Softmax: max shift, exp, normalise)
+  double mx = -INFINITY;
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) mx = fmax(mx, ra.score[b + i]);
+  for (int o = kWave / 2; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, kWave));
+  __syncthreads();
+  if ((threadIdx.x & (kWave - 1)) == 0) s_red[threadIdx.x / kWave] = mx;
+  __syncthreads();
+  mx = s_red[0];
+  for (int i = 1; i < kRankThreads / kWave; ++i) mx = fmax(mx, s_red[i]);
+  double den = 0.0;
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+    const double e = exp(ra.score[b + i] - mx);
+    s_rho[i] = e;
+    den += e;
+  }
+  den = BlockSum(den, s_red);
+  // gamma draws: the query's LCG is sequential over its documents
+  if (threadIdx.x == 0) {
+    unsigned st = ra.rng[q];
+    for (int i = 0; i < cnt; ++i) {
+      st = 214013u * st + 2531011u;
+      const float u = static_cast<float>(static_cast<int>((st >> 16) & 0x7FFF)) / 32768.0f;
+      s_par[i] = exp2(static_cast<double>(static_cast<int>(ra.label[b + i]))) - u;
+    }
+    ra.rng[q] = st;
+  }
+  __syncthreads();
+  double sp = 0.0;
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+    s_rho[i] /= den;
+    sp += s_par[i];
+  }
+  sp = BlockSum(sp, s_red);
+  const double inv_den = 1.0 / fmax(kEpsilon, sp);
+  double s1 = 0.0;
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+    const double term = -s_par[i] * inv_den + s_rho[i];
+    s_lam[i] = static_cast<float>(term);
+    s_par[i] = term / (1. - s_rho[i]);
+    s1 += s_par[i];
+  }
+  s1 = BlockSum(s1, s_red);
+  double s2 = 0.0;
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+    const double term = s_rho[i] * (s1 - s_par[i]);
+    s_lam[i] += static_cast<float>(term);
+    s_par[i] = term / (1. - s_rho[i]);
+    s2 += s_par[i];
+  }
+  s2 = BlockSum(s2, s_red);
+  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+    float lam = s_lam[i] + static_cast<float>(s_rho[i] * (s2 - s_par[i]));
+    float hes = static_cast<float>(s_rho[i] * (1.0 - s_rho[i]));
+    if (ra.weights != nullptr) {
+      lam = static_cast<float>(lam * ra.weights[b + i]);
+      hes = static_cast<float>(hes * ra.weights[b + i]);
+    }
+    ra.grad[b + i] = lam;
+    ra.hess[b + i] = hes;
+  }
+}
+
+void RankGradients(const RankArgs& ra, hipStream_t s) {
+  if (ra.num_queries <= 0) return;
+  if (ra.kind == kRankKindLambdarank) {
+    hipLaunchKernelGGL(k_lambdarank, dim3(ra.num_queries), dim3(kRankThreads), 0, s, ra);
+  } else {
+    hipLaunchKernelGGL(k_xendcg, dim3(ra.num_queries), dim3(kRankThreads), 0, s, ra);
+  }
+}
+
+}  // namespace dev
+}  // namespace lgbm_amd

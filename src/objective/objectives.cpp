@@ -831,6 +831,16 @@ class RankingObjective : public ObjectiveFunction {
   bool NeedAccuratePrediction() const override { return false; }
 
  protected:
+  DeviceGradSpec RankSpec(DeviceGradKind k) const {
+    DeviceGradSpec d;
+    d.kind = k;
+    d.label = label_;
+    d.weights = weights_;
+    d.rank.num_queries = nq_;
+    d.rank.query_boundaries = qb_;
+    for (data_size_t q = 0; q < nq_; ++q) d.rank.max_query_docs = std::max(d.rank.max_query_docs, qb_[q + 1] - qb_[q]);
+    return d;
+  }
   int seed_;
   data_size_t nq_ = 0, num_data_ = 0;
   const label_t* weights_ = nullptr;
@@ -923,6 +933,18 @@ class LambdarankNDCG : public RankingObjective {
     }
   }
   const char* GetName() const override { return "lambdarank"; }
+  DeviceGradSpec DeviceSpec() const override {
+    auto d = RankSpec(DeviceGradKind::Lambdarank);
+    d.rank.inv_max_dcg = inv_max_dcg_.data();
+    d.rank.label_gain = gain_.data();
+    d.rank.num_label_gain = static_cast<int>(gain_.size());
+    d.rank.norm = norm_;
+    d.rank.sigmoid = sigmoid_;
+    d.rank.sig_min = min_in_;
+    d.rank.sig_max = max_in_;
+    d.rank.sig_factor = idx_factor_;
+    return d;
+  }
 
  private:
   static constexpr size_t kBins = 1024 * 1024;
@@ -976,9 +998,17 @@ class RankXENDCG : public RankingObjective {
     }
   }
   const char* GetName() const override { return "rank_xendcg"; }
+  DeviceGradSpec DeviceSpec() const override {
+    auto d = RankSpec(DeviceGradKind::RankXendcg);
+    states_.resize(rands_.size());
+    for (size_t q = 0; q < rands_.size(); ++q) states_[q] = rands_[q].state();
+    d.rank.rng_states = states_.data();
+    return d;
+  }
 
  private:
   mutable std::vector<Random> rands_;
+  mutable std::vector<unsigned> states_;
 };
 
 }  // namespace

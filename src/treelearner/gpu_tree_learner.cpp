@@ -10,6 +10,7 @@
 #include <cstring>
 
 #include "lgbm_amd/common.h"
+#include "lgbm_amd/dcg.h"
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/network.h"
 
@@ -78,6 +79,14 @@ void GPUTreeLearner::FreeBuffers() {
   d_grad_ = d_hess_ = nullptr;
   d_label_ = d_weights_ = d_label_weight_ = nullptr;
   uploaded_label_src_ = uploaded_weight_src_ = uploaded_lw_src_ = nullptr;
+  d_qb_ = nullptr;
+  d_inv_max_dcg_ = d_label_gain_ = d_discount_ = nullptr;
+  d_rank_rng_ = nullptr;
+  uploaded_qb_src_ = nullptr;
+  d_sample_rng_ = nullptr;
+  d_sample_codes_ = nullptr;
+  d_sample_cnt_ = d_sample_off_ = d_bag_count_ = nullptr;
+  sample_seeded_ = false;
   d_tree_i32_ = nullptr;
   d_tree_u32_ = nullptr;
   d_tree_i8_ = nullptr;
@@ -216,6 +225,7 @@ void GPUTreeLearner::UploadData() {
   d_tmp_ = Alloc<int32_t>(num_data_);
   d_bag_ = Alloc<int32_t>(num_data_);
   d_oob_ = Alloc<int32_t>(num_data_);
+  d_bag_count_ = Alloc<int32_t>(1);
   d_leaves_ = Alloc<dev::Leaf>(n_leaves);
   d_step_ = Alloc<dev::Step>(1);
   d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
@@ -275,6 +285,7 @@ void GPUTreeLearner::UploadData() {
   }
   a.root = d_root_;
   a.num_rows = num_data_;
+  a.num_rows_dev = nullptr;
   a.root_identity = 1;
   a.bin_bytes = bin_bytes;
   a.words_per_row = wpr;
@@ -370,6 +381,8 @@ void GPUTreeLearner::SetBaggingData(const Dataset* subset, const data_size_t* us
     if (oob_cnt_ > 0) {
       HIPCHECK(hipMemcpyAsync(d_oob_, used_indices + n, sizeof(int32_t) * oob_cnt_, hipMemcpyHostToDevice, stream_));
     }
+    const int32_t cnt = n;
+    HIPCHECK(hipMemcpyAsync(d_bag_count_, &cnt, sizeof(int32_t), hipMemcpyHostToDevice, stream_));
     HIPCHECK(hipStreamSynchronize(stream_));
   }
 }
@@ -544,7 +557,8 @@ void GPUTreeLearner::DestroyGraph() {
 // the whole tree as a stream-ordered kernel sequence (no host synchronisation inside)
 void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   if (use_bag_) {
-    HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * bag_cnt_, hipMemcpyDeviceToDevice, stream_));
+    // the whole buffer: the copy (like the tree's graph) does not depend on the bag size
+    HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * num_data_, hipMemcpyDeviceToDevice, stream_));
   }
   HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
   // both step buffers start at zero; afterwards each split-scan zeroes the next one
@@ -576,13 +590,16 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
   dev::KArgs a = args_;
   if (use_bag_) {
-    a.num_rows = bag_cnt_;
+    // bag size read on the device: one captured graph serves every bag
+    a.num_rows = num_data_;
+    a.num_rows_dev = d_bag_count_;
     a.root_identity = 0;
+    root_rows_ = bag_cnt_;
   } else {
     a.num_rows = num_data_;
     a.root_identity = 1;
+    root_rows_ = num_data_;
   }
-  root_rows_ = a.num_rows;
   // single process: the tree's fixed kernel sequence (~5 launches per split) is replayed
   // from a hipGraph -- eager launches are host-bound at ~4 us each, longer than most of
   // these kernels; with collectives between the kernels it is launched eagerly
@@ -921,6 +938,10 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   if (spec.kind == DeviceGradKind::None || spec.kind == DeviceGradKind::MulticlassOVA) return false;
   if (spec.kind != DeviceGradKind::MulticlassSoftmax && ntpi != 1) return false;
   if (spec.label == nullptr) return false;
+  const bool listwise = spec.kind == DeviceGradKind::Lambdarank || spec.kind == DeviceGradKind::RankXendcg;
+  if (listwise && (spec.rank.query_boundaries == nullptr || spec.rank.max_query_docs > dev::kRankMaxDocs)) {
+    return false;  // queries larger than the LDS staging: host gradients
+  }
   const size_t n = static_cast<size_t>(num_data_);
   if (uploaded_label_src_ != spec.label) {
     if (d_label_ == nullptr) d_label_ = Alloc<float>(n);
@@ -936,6 +957,30 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     if (d_label_weight_ == nullptr) d_label_weight_ = Alloc<float>(n);
     HIPCHECK(hipMemcpy(d_label_weight_, spec.label_weight_arr, sizeof(float) * n, hipMemcpyHostToDevice));
     uploaded_lw_src_ = spec.label_weight_arr;
+  }
+  if (listwise) {
+    UploadRankTables(spec.rank, spec.kind);
+    dev::RankArgs ra;
+    ra.kind = spec.kind == DeviceGradKind::Lambdarank ? dev::kRankKindLambdarank : dev::kRankKindXendcg;
+    ra.num_queries = spec.rank.num_queries;
+    ra.qb = d_qb_;
+    ra.label = d_label_;
+    ra.weights = spec.weights != nullptr ? d_weights_ : nullptr;
+    ra.score = d_score_;
+    ra.grad = d_grad_;
+    ra.hess = d_hess_;
+    ra.inv_max_dcg = d_inv_max_dcg_;
+    ra.label_gain = d_label_gain_;
+    ra.discount = d_discount_;
+    ra.sigmoid = spec.rank.sigmoid;
+    ra.sig_min = spec.rank.sig_min;
+    ra.sig_max = spec.rank.sig_max;
+    ra.sig_factor = spec.rank.sig_factor;
+    ra.norm = spec.rank.norm ? 1 : 0;
+    ra.rng = d_rank_rng_;
+    dev::RankGradients(ra, stream_);
+    gh_fresh_ = false;
+    return true;
   }
   dev::GradArgs g;
   g.kind = static_cast<int32_t>(spec.kind);
@@ -964,6 +1009,92 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   dev::Gradients(g, stream_);
   gh_fresh_ = fuse;
   return true;
+}
+
+// query boundaries, 1 / max DCG, label gains and position discounts (lambdarank) or the
+// per-query generators (xendcg; from here on they advance on the device)
+void GPUTreeLearner::UploadRankTables(const DeviceRankSpec& r, DeviceGradKind kind) {
+  if (uploaded_qb_src_ == r.query_boundaries) return;
+  const size_t nq = static_cast<size_t>(r.num_queries);
+  d_qb_ = Alloc<int32_t>(nq + 1);
+  HIPCHECK(hipMemcpy(d_qb_, r.query_boundaries, sizeof(int32_t) * (nq + 1), hipMemcpyHostToDevice));
+  if (kind == DeviceGradKind::Lambdarank) {
+    d_inv_max_dcg_ = Alloc<double>(nq);
+    HIPCHECK(hipMemcpy(d_inv_max_dcg_, r.inv_max_dcg, sizeof(double) * nq, hipMemcpyHostToDevice));
+    d_label_gain_ = Alloc<double>(r.num_label_gain);
+    HIPCHECK(hipMemcpy(d_label_gain_, r.label_gain, sizeof(double) * r.num_label_gain, hipMemcpyHostToDevice));
+    std::vector<double> disc(std::max<data_size_t>(1, r.max_query_docs));
+    for (size_t i = 0; i < disc.size(); ++i) disc[i] = DCG::Discount(static_cast<data_size_t>(i));
+    d_discount_ = Alloc<double>(disc.size());
+    HIPCHECK(hipMemcpy(d_discount_, disc.data(), sizeof(double) * disc.size(), hipMemcpyHostToDevice));
+  } else {
+    d_rank_rng_ = Alloc<uint32_t>(nq);
+    HIPCHECK(hipMemcpy(d_rank_rng_, r.rng_states, sizeof(uint32_t) * nq, hipMemcpyHostToDevice));
+  }
+  uploaded_qb_src_ = r.query_boundaries;
+}
+
+data_size_t GPUTreeLearner::DeviceSample(const DeviceSampleSpec& sp) {
+  HIPCHECK(hipSetDevice(device_id_));
+  const int64_t nb = dev::SampleBlocks(num_data_);
+  if (d_sample_rng_ == nullptr) {
+    d_sample_rng_ = Alloc<uint32_t>(nb);
+    d_sample_codes_ = Alloc<uint8_t>(num_data_);
+    d_sample_cnt_ = Alloc<int32_t>(nb);
+    d_sample_off_ = Alloc<int32_t>(nb);
+  }
+  if (sp.reset || !sample_seeded_) {
+    // generator of block b: Random(seed + b) (reference bagging_rands_)
+    std::vector<uint32_t> st(nb);
+    for (int64_t b = 0; b < nb; ++b) st[b] = static_cast<uint32_t>(sp.seed + static_cast<int>(b));
+    HIPCHECK(hipMemcpy(d_sample_rng_, st.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice));
+    sample_seeded_ = true;
+  }
+  if (sp.balanced && uploaded_label_src_ != sp.label) {
+    if (d_label_ == nullptr) d_label_ = Alloc<float>(num_data_);
+    HIPCHECK(hipMemcpy(d_label_, sp.label, sizeof(float) * num_data_, hipMemcpyHostToDevice));
+    uploaded_label_src_ = sp.label;
+  }
+  dev::SampleArgs s;
+  s.num_data = num_data_;
+  s.num_blocks = nb;
+  s.goss = sp.goss ? 1 : 0;
+  s.balanced = sp.balanced ? 1 : 0;
+  s.num_class = sp.num_tree_per_iteration;
+  s.fraction = sp.fraction;
+  s.pos_fraction = sp.pos_fraction;
+  s.neg_fraction = sp.neg_fraction;
+  s.top_rate = sp.top_rate;
+  s.other_rate = sp.other_rate;
+  s.label = d_label_;
+  s.grad = d_grad_;
+  s.hess = d_hess_;
+  s.rng = d_sample_rng_;
+  s.codes = d_sample_codes_;
+  s.block_cnt = d_sample_cnt_;
+  s.block_off = d_sample_off_;
+  s.bag = d_bag_;
+  s.oob = d_oob_;
+  s.bag_count = d_bag_count_;
+  dev::SampleRows(s, stream_);
+  int32_t cnt = 0;
+  HIPCHECK(hipMemcpyAsync(&cnt, d_bag_count_, sizeof(int32_t), hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  if (sp.goss) gh_fresh_ = false;  // the sampled rows' gradients were rescaled in place
+  // SerialTreeLearner::SetBaggingData state; the rows themselves stay on the device
+  bag_indices_ = nullptr;
+  bag_cnt_ = cnt;
+  use_bag_ = cnt < num_data_;
+  oob_cnt_ = num_data_ - cnt;
+  if (sp.host_indices != nullptr) {
+    sp.host_indices->resize(num_data_);
+    HIPCHECK(hipMemcpy(sp.host_indices->data(), d_bag_, sizeof(int32_t) * cnt, hipMemcpyDeviceToHost));
+    if (oob_cnt_ > 0) {
+      HIPCHECK(hipMemcpy(sp.host_indices->data() + cnt, d_oob_, sizeof(int32_t) * oob_cnt_, hipMemcpyDeviceToHost));
+    }
+    bag_indices_ = sp.host_indices->data();
+  }
+  return cnt;
 }
 
 void GPUTreeLearner::UploadGradients(const score_t* g, const score_t* h, int64_t n) {

@@ -53,6 +53,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void AddTreeToScore(const Tree* tree, int tree_id) override;
   bool ComputeGradients(const DeviceGradSpec& spec, int num_tree_per_iteration) override;
   void UploadGradients(const score_t* g, const score_t* h, int64_t n) override;
+  data_size_t DeviceSample(const DeviceSampleSpec& spec) override;
   void DownloadGradients(score_t* g, score_t* h, int64_t n) override;
   score_t* device_gradients() override { return d_grad_; }
   score_t* device_hessians() override { return d_hess_; }
@@ -84,6 +85,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void AllreduceScratch(int parity);
   void AllreduceRoot();
   void AllreduceAbsMax();
+  void UploadRankTables(const DeviceRankSpec& r, DeviceGradKind kind);
   template <typename T>
   T* Alloc(size_t n);
 
@@ -138,6 +140,20 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   const label_t* uploaded_label_src_ = nullptr;
   const label_t* uploaded_weight_src_ = nullptr;
   const label_t* uploaded_lw_src_ = nullptr;
+  // listwise objectives: query tables (uploaded once) and the xendcg generators
+  int32_t* d_qb_ = nullptr;
+  double* d_inv_max_dcg_ = nullptr;
+  double* d_label_gain_ = nullptr;
+  double* d_discount_ = nullptr;
+  uint32_t* d_rank_rng_ = nullptr;
+  const data_size_t* uploaded_qb_src_ = nullptr;
+  // device row sampling (bagging / GOSS)
+  uint32_t* d_sample_rng_ = nullptr;
+  uint8_t* d_sample_codes_ = nullptr;
+  int32_t* d_sample_cnt_ = nullptr;
+  int32_t* d_sample_off_ = nullptr;
+  int32_t* d_bag_count_ = nullptr;  // in-bag rows of the current bag (read by the root kernels)
+  bool sample_seeded_ = false;
   // tree upload staging for traversal
   int32_t* d_tree_i32_ = nullptr;
   uint32_t* d_tree_u32_ = nullptr;

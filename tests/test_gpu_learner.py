@@ -116,3 +116,87 @@ def test_rccl_comm_single_rank(gpu_available):
         assert ok.value == 1
     finally:
         lib.LGBM_AMD_RcclFree()
+
+
+def _rank_data(nq=300, seed=6):
+    rng = np.random.RandomState(seed)
+    sizes = rng.randint(5, 60, size=nq)
+    n = int(sizes.sum())
+    X = rng.randn(n, 12).astype(np.float32)
+    rel = X[:, 0] + 0.5 * X[:, 1] + 0.3 * rng.randn(n)
+    y = np.clip(np.floor(rel + 1.5), 0, 4).astype(np.float32)
+    return X, y, sizes
+
+
+def _ndcg_at(y, p, group, k=10):
+    out, start = [], 0
+    for g in group:
+        yy, pp = y[start:start + g], p[start:start + g]
+        start += g
+        order = np.argsort(-pp, kind="stable")
+        disc = 1.0 / np.log2(np.arange(2, g + 2))
+        gain = 2.0 ** yy - 1
+        dcg = np.sum(gain[order][:k] * disc[:k])
+        idcg = np.sum(np.sort(gain)[::-1][:k] * disc[:k])
+        out.append(dcg / idcg if idcg > 0 else 1.0)
+    return float(np.mean(out))
+
+
+@pytest.mark.parametrize("objective", ["lambdarank", "rank_xendcg"])
+def test_listwise_gradients_on_device(gpu_available, objective):
+    """LambdaRank / XE-NDCG gradients from the per-query HIP kernel: NDCG parity with the CPU learner."""
+    X, y, group = _rank_data()
+    res = {}
+    for device in ("cpu", "gpu"):
+        params = {"objective": objective, "num_leaves": 15, "min_data_in_leaf": 5, "learning_rate": 0.1,
+                  "verbose": -1, "device_type": device, "seed": 3}
+        ds = lgb.Dataset(X, y, group=group, params=params)
+        b = lgb.train(params, ds, 30, verbose_eval=False)
+        res[device] = _ndcg_at(y, b.predict(X), group)
+    assert res["gpu"] > 0.7
+    assert abs(res["gpu"] - res["cpu"]) < 0.02
+
+
+def _bag_counts(device, boosting, rounds, fixed_gradients=False, **extra):
+    X, y = _data(50000, seed=9)
+    params = {"objective": "binary", "num_leaves": 15, "max_bin": 63, "verbose": -1, "device_type": device,
+              "boosting": boosting, "seed": 11}
+    params.update(extra)
+    fobj = None
+    if fixed_gradients:  # the sampler's input does not depend on the (device vs host) trees
+        rng = np.random.RandomState(0)
+        g = rng.randn(len(y)).astype(np.float32)
+        h = (rng.rand(len(y)) + 0.5).astype(np.float32)
+
+        def fobj(preds, ds):
+            return g, h
+    b = lgb.train(params, lgb.Dataset(X, y, params=params), rounds, fobj=fobj, verbose_eval=False)
+    out = []
+    for t in b.dump_model()["tree_info"]:
+        root = t["tree_structure"]
+        left = root.get("left_child", {})
+        # the root and its left child's row counts depend on exactly which rows are in the bag
+        out.append((root.get("internal_count"), left.get("internal_count", left.get("leaf_count"))))
+    return out
+
+
+def test_device_bagging_matches_host_draw(gpu_available):
+    """Device bagging uses the reference's per-1024-row generators: the bags are identical."""
+    kw = dict(bagging_fraction=0.6, bagging_freq=2, bagging_seed=5)
+    assert _bag_counts("gpu", "gbdt", 6, **kw) == _bag_counts("cpu", "gbdt", 6, **kw)
+
+
+def test_device_balanced_bagging_matches_host_draw(gpu_available):
+    kw = dict(pos_bagging_fraction=0.5, neg_bagging_fraction=0.8, bagging_freq=1)
+    assert _bag_counts("gpu", "gbdt", 4, **kw) == _bag_counts("cpu", "gbdt", 4, **kw)
+
+
+def test_device_goss_matches_reference_block_layout(gpu_available):
+    """Device GOSS = the reference's GOSS with one sampling block per 1024 rows
+    (num_threads >= ceil(n / 1024)): same sampled-set sizes as the host draw."""
+    n_blocks = (50000 + 1023) // 1024
+    kw = dict(learning_rate=0.5, top_rate=0.2, other_rate=0.1)
+    gpu = _bag_counts("gpu", "goss", 5, fixed_gradients=True, **kw)
+    cpu = _bag_counts("cpu", "goss", 5, fixed_gradients=True, num_threads=n_blocks, **kw)
+    assert [c[0] for c in gpu[:2]] == [50000, 50000]  # sampling starts at iteration 1 / learning_rate
+    assert gpu == cpu
