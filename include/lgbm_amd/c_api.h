@@ -208,7 +208,10 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_RcclInit(int num_ranks, int rank, int device_id, 
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclFree();
 /* runs every device collective on small buffers and checks the sums (1 = ok) */
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclSelfTest(int* out_ok);
+// the same all-reduces captured into a hipGraph and replayed (the device learner's tree graph)
+LIGHTGBM_C_EXPORT int LGBM_AMD_RcclGraphSelfTest(int* out_ok);
 /* number of visible GPUs (0 without a device) */
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceSynchronize();
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCount(int* out);
 /* phase timers (LGBM_AMD_TIMETAG) as "name=seconds;..." */
 LIGHTGBM_C_EXPORT int LGBM_AMD_GetTimers(int64_t buffer_len, int64_t* out_len, char* out_str);

@@ -5,7 +5,7 @@
 scikit-learn estimators and plotting helpers.  Set ``device_type='gpu'`` to train on the
 MI355X learner (HIP kernels in src/device/).
 """
-from .basic import Booster, Dataset, LightGBMError, device_count, get_timers
+from .basic import Booster, Dataset, LightGBMError, device_count, device_synchronize, get_timers
 from .callback import EarlyStopException, early_stopping, print_evaluation, record_evaluation, reset_parameter
 from .engine import CVBooster, cv, train
 
@@ -25,4 +25,4 @@ __all__ = ["Dataset", "Booster", "CVBooster", "LightGBMError",
            "LGBMModel", "LGBMRegressor", "LGBMClassifier", "LGBMRanker",
            "print_evaluation", "record_evaluation", "reset_parameter", "early_stopping", "EarlyStopException",
            "plot_importance", "plot_split_value_histogram", "plot_metric", "plot_tree", "create_tree_digraph",
-           "device_count", "get_timers"]
+           "device_count", "device_synchronize", "get_timers"]

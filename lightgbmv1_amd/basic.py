@@ -1973,3 +1973,8 @@ def device_count():
     n = ctypes.c_int(0)
     _safe_call(_load_lib().LGBM_AMD_DeviceCount(ctypes.byref(n)))
     return n.value
+
+
+def device_synchronize():
+    """Wait for all work queued on the current HIP device (no-op without a GPU)."""
+    _safe_call(_load_lib().LGBM_AMD_DeviceSynchronize())

@@ -159,9 +159,59 @@ int LGBM_AMD_RcclSelfTest(int* out_ok) {
   return 0;
 }
 
+// the device learner captures its per-split all-reduces into the tree's hipGraph: two
+// all-reduces captured from a stream, the graph replayed three times, result checked
+// (every rank contributes i to element i, so after 6 all-reduces it holds i * n^6)
+int LGBM_AMD_RcclGraphSelfTest(int* out_ok) {
+  try {
+    DeviceComm* dc = Network::device_comm();
+    if (dc == nullptr) Log::Fatal("no device comm (call LGBM_AMD_RcclInit first)");
+    const int n = dc->size();
+    const size_t cnt = 4096;
+    hipStream_t s;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) Log::Fatal("hipStreamCreate failed");
+    long long* d = nullptr;
+    if (hipMalloc(&d, cnt * sizeof(long long)) != hipSuccess) Log::Fatal("hipMalloc failed");
+    std::vector<long long> h(cnt);
+    for (size_t i = 0; i < cnt; ++i) h[i] = static_cast<long long>(i);
+    (void)hipMemcpy(d, h.data(), cnt * sizeof(long long), hipMemcpyHostToDevice);
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) Log::Fatal("begin capture failed");
+    dc->AllreduceSumI64(d, cnt, s);
+    dc->AllreduceSumI64(d, cnt, s);
+    if (hipStreamEndCapture(s, &g) != hipSuccess) Log::Fatal("end capture failed");
+    if (hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) != hipSuccess) Log::Fatal("graph instantiate failed");
+    for (int it = 0; it < 3; ++it) {
+      if (hipGraphLaunch(ge, s) != hipSuccess) Log::Fatal("graph launch failed");
+    }
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), d, cnt * sizeof(long long), hipMemcpyDeviceToHost);
+    long long f = 1;
+    for (int k = 0; k < 6; ++k) f *= n;
+    bool ok = true;
+    for (size_t i = 0; i < cnt; ++i) ok = ok && h[i] == static_cast<long long>(i) * f;
+    (void)hipGraphExecDestroy(ge);
+    (void)hipGraphDestroy(g);
+    (void)hipFree(d);
+    (void)hipStreamDestroy(s);
+    *out_ok = ok ? 1 : 0;
+  } catch (std::exception& e) {
+    Log::Warning("%s", e.what());
+    return -1;
+  }
+  return 0;
+}
+
 int LGBM_AMD_RcclFree() {
   Network::SetDeviceComm(nullptr);
   return 0;
+}
+
+int LGBM_AMD_DeviceSynchronize() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : -1;
 }
 
 int LGBM_AMD_DeviceCount(int* out) {

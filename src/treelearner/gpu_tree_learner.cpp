@@ -600,12 +600,18 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     a.root_identity = 1;
     root_rows_ = num_data_;
   }
-  // single process: the tree's fixed kernel sequence (~5 launches per split) is replayed
-  // from a hipGraph -- eager launches are host-bound at ~4 us each, longer than most of
-  // these kernels; with collectives between the kernels it is launched eagerly
+  // the tree's fixed kernel sequence (~4 launches per split) is replayed from a hipGraph:
+  // eager launches are host-bound at ~4 us each, longer than most of these kernels.  With
+  // data-parallel training the per-split RCCL all-reduces are captured into the same graph
+  // (they are stream-ordered; every rank enqueues the same collectives either way); with
+  // host collectives (no device communicator) the tree is launched eagerly.
   const bool distributed = data_parallel_ && Network::num_machines() > 1;
+  const bool dev_comm = distributed && Network::device_comm() != nullptr;
   const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
-  const bool use_graph = !distributed && !(ng != nullptr && ng[0] == '1');
+  const char* gc = std::getenv("LGBM_AMD_GRAPH_COLLECTIVES");
+  const bool graph_collectives = dev_comm && !(gc != nullptr && gc[0] == '0') && !graph_capture_failed_;
+  const bool use_graph = (!distributed || graph_collectives) && !(ng != nullptr && ng[0] == '1');
+  bool launched = false;
   if (use_graph) {
     const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
     if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
@@ -613,18 +619,35 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       DestroyGraph();
       hipGraph_t g = nullptr;
       HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-      EnqueueTree(a);
-      HIPCHECK(hipStreamEndCapture(stream_, &g));
-      HIPCHECK(hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0));
-      HIPCHECK(hipGraphDestroy(g));
-      graph_rows_ = a.num_rows;
-      graph_identity_ = a.root_identity;
-      graph_root_mode_ = root_mode;
+      std::string why;
+      try {
+        EnqueueTree(a);
+      } catch (const std::exception& e) {
+        why = e.what();
+      }
+      hipError_t ec = hipStreamEndCapture(stream_, &g);
+      if (why.empty() && ec == hipSuccess) ec = hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0);
+      if (g != nullptr) (void)hipGraphDestroy(g);
+      if (!why.empty() || ec != hipSuccess) {
+        if (why.empty()) why = hipGetErrorString(ec);
+        (void)hipGetLastError();
+        graph_exec_ = nullptr;
+        if (!distributed) Log::Fatal("device learner: capturing the tree graph failed: %s", why.c_str());
+        Log::Warning("device learner: capturing the RCCL collectives into the tree graph failed (%s); "
+                     "launching trees eagerly", why.c_str());
+        graph_capture_failed_ = true;
+      } else {
+        graph_rows_ = a.num_rows;
+        graph_identity_ = a.root_identity;
+        graph_root_mode_ = root_mode;
+      }
     }
-    HIPCHECK(hipGraphLaunch(graph_exec_, stream_));
-  } else {
-    EnqueueTree(a);
+    if (graph_exec_ != nullptr) {
+      HIPCHECK(hipGraphLaunch(graph_exec_, stream_));
+      launched = true;
+    }
   }
+  if (!launched) EnqueueTree(a);
   HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
                           hipMemcpyDeviceToHost, stream_));

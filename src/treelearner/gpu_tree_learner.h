@@ -125,6 +125,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int graph_rows_ = -1;
   int graph_identity_ = -1;
   int graph_root_mode_ = -1;
+  bool graph_capture_failed_ = false;  // RCCL collectives could not be captured: eager trees
   bool gh_fresh_ = false;         // d_gh_ / absmax / root partials written by the gradient kernel
   bool root_from_parts_ = false;  // this tree's gradients came packed from the gradient kernel
   double* d_root_parts_ = nullptr;

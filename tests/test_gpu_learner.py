@@ -114,6 +114,9 @@ def test_rccl_comm_single_rank(gpu_available):
     try:
         assert lib.LGBM_AMD_RcclSelfTest(ctypes.byref(ok)) == 0
         assert ok.value == 1
+        ok.value = 0
+        assert lib.LGBM_AMD_RcclGraphSelfTest(ctypes.byref(ok)) == 0
+        assert ok.value == 1
     finally:
         lib.LGBM_AMD_RcclFree()
 
