@@ -103,7 +103,8 @@ struct Step {
 struct FeatureBest {
   double gain;
   double lg, lh, rg, rh, lo, ro;
-  int32_t feature, real_feature, thr, default_left, lc, rc, mono, pad;
+  int32_t feature, real_feature, thr, default_left, lc, rc, mono;
+  int32_t ncat;  // categorical: categories in the left set (KArgs::feat_cat); 0: numerical
 };
 
 // record of one applied split, read back by the host to rebuild the Tree

@@ -49,6 +49,7 @@ struct KArgs {
   int32_t num_data;          // rows of the matrix (column stride of bins_col)
   int32_t host_mode;         // partition: the host wrote Step::cs (host-assisted growth)
   FeatureBest* feat_best;    // [2][num_features] per-feature best split of the two leaves
+  uint32_t* feat_cat;        // [2][num_features][kMaxCatWords] category sets of categorical bests
   long long* ktrace;         // optional [num_leaves][kTraceSlots] in-kernel timestamps (LGBM_AMD_KTRACE)
 };
 
@@ -63,6 +64,7 @@ enum TraceSlot {
   kTraceSlots = 40
 };
 
+constexpr int kFindMaxCatBins = 1024;  // categorical features scanned on device (<= 32 * kMaxCatWords)
 constexpr int kHistThreads = 1024;     // histogram workgroup (16 waves)
 constexpr int kHistMinRows = 1024;     // rows per histogram workgroup, lower bound
 constexpr int kReduceChunk = 16;       // partial histograms summed per reduce thread

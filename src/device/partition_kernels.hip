@@ -54,7 +54,8 @@ __device__ __forceinline__ void WaveArgBest(double* g, int* rf, int* idx) {
   }
 }
 
-__device__ __forceinline__ void ToDeviceSplit(const FeatureBest& b, DeviceSplit* d) {
+// cat: the feature's category set (KArgs::feat_cat) when b is a categorical split
+__device__ __forceinline__ void ToDeviceSplit(const FeatureBest& b, const uint32_t* cat, DeviceSplit* d) {
   d->gain = b.gain;
   d->feature = b.feature;
   d->real_feature = b.real_feature;
@@ -69,9 +70,16 @@ __device__ __forceinline__ void ToDeviceSplit(const FeatureBest& b, DeviceSplit*
   d->right_sum_hessian = b.rh;
   d->default_left = static_cast<int8_t>(b.default_left);
   d->monotone_type = static_cast<int8_t>(b.mono);
-  d->is_categorical = 0;
+  d->is_categorical = b.ncat > 0 ? 1 : 0;
   d->pad0 = 0;
-  d->num_cat_threshold = 0;
+  d->num_cat_threshold = b.ncat;
+  if (b.ncat > 0) {
+    for (int w = 0; w < kMaxCatWords; ++w) d->cat_bits[w] = cat[w];
+  }
+}
+
+__device__ __forceinline__ const uint32_t* FeatCat(const KArgs& a, int side, int f) {
+  return a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords;
 }
 
 __device__ __forceinline__ void NoSplit(DeviceSplit* d) {
@@ -183,10 +191,10 @@ __device__ void PickWave(const KArgs& a, const Step* st, PickResult* out) {
   out->fresh_idx[1] = fi[1];
   DeviceSplit* sp = &out->split;  // straight into LDS (no private copy)
   if (fresh >= 1 && leaf == sm) {
-    if (fi[0] >= 0) ToDeviceSplit(a.feat_best[fi[0]], sp);
+    if (fi[0] >= 0) ToDeviceSplit(a.feat_best[fi[0]], FeatCat(a, 0, fi[0]), sp);
     else NoSplit(sp);
   } else if (fresh == 2 && leaf == lg) {
-    if (fi[1] >= 0) ToDeviceSplit(a.feat_best[NF + fi[1]], sp);
+    if (fi[1] >= 0) ToDeviceSplit(a.feat_best[NF + fi[1]], FeatCat(a, 1, fi[1]), sp);
     else NoSplit(sp);
   } else {
     *sp = a.best[leaf];
@@ -208,7 +216,9 @@ __device__ void RecordSplit(const KArgs& a, Step* st, const PickResult& pk) {
   for (int side = 0; side < fresh; ++side) {
     const int l = side == 0 ? st->smaller : st->larger;
     DeviceSplit& d = a.best[l];
-    if (pk.fresh_idx[side] >= 0) ToDeviceSplit(a.feat_best[side * NF + pk.fresh_idx[side]], &d);
+    if (pk.fresh_idx[side] >= 0) {
+      ToDeviceSplit(a.feat_best[side * NF + pk.fresh_idx[side]], FeatCat(a, side, pk.fresh_idx[side]), &d);
+    }
     else NoSplit(&d);
   }
   const int s = pk.s, leaf = pk.leaf, nl = s + 1;

@@ -359,12 +359,185 @@ __device__ void FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
   }
 }
 
+// LDS of the categorical scan: per-bin ctr and the stable ctr order
+struct CatScratch {
+  double ctr[kFindMaxCatBins];
+  int sorted[kFindMaxCatBins];
+  int used_bin;
+};
+
+// categorical split of one feature (reference FindBestThresholdCategoricalInner,
+// feature_histogram.hpp:277-513): one-vs-rest for few categories (parallel over the bins),
+// otherwise the bins with enough data sorted by g / (h + cat_smooth) -- a stable rank
+// computed in parallel -- and the sequential prefix scan from both ends (<= 2 x
+// max_cat_threshold steps, thread 0) with the min_data_per_group rules.
+__device__ void FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
+                                     FeatureBest* out, uint32_t* cat_out, BlockScratch* sc, CatScratch* cs) {
+  const int tid = threadIdx.x;
+  const int nb = F.num_bin - F.offset;
+  hv.fix_t = -1;
+  hv.fix_g = hv.fix_h = 0.0;
+  if (F.mfb > 0) {  // FixHistogram
+    double sg = 0.0, sh = 0.0;
+    int unused = 0;
+    for (int t = tid; t < nb; t += kFindThreads) {
+      if (t == F.mfb) continue;
+      sg += hv.RawG(t);
+      sh += hv.RawH(t);
+    }
+    BlockSum3(sg, sh, unused, sc);
+    hv.fix_t = F.mfb;
+    hv.fix_g = L.sg - sg;
+    hv.fix_h = (L.sh - 2 * kEpsilon) - sh;
+  }
+  double gain_shift;
+  if (p.use_smoothing) {
+    gain_shift = LeafGainGivenOutput(L.sg, L.sh, p.lambda_l1, p.lambda_l2, L.parent_out, p.use_l1);
+  } else {
+    gain_shift = LeafGain(L.sg, L.sh, p.lambda_l1, p.lambda_l2, p.max_delta_step, 0, L.n, 0, p.use_l1,
+                          p.use_max_output, 0);
+  }
+  const double min_gain_shift = gain_shift + p.min_gain_to_split;
+  const int offset = F.offset;
+  const int bin_start = 1 - offset, bin_end = F.num_bin - offset;
+  const bool onehot = F.num_bin <= p.max_cat_to_onehot;
+  const double min_h = p.min_sum_hessian_in_leaf;
+  const int min_n = p.min_data_in_leaf;
+  out->gain = -INFINITY;
+  out->default_left = 0;
+  out->mono = 0;
+  out->thr = 0;
+  out->ncat = 0;
+  double l2 = p.lambda_l2;
+  bool splittable = false;
+  Cand best;
+  best.gain = -INFINITY;
+  best.thr = 0x7fffffff;
+  best.lg = best.lh = 0.0;
+  best.lc = 0;
+  int best_dir = 1;
+  if (onehot) {
+    bool any = false;
+    for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
+      const double g = hv.G(t), hh = hv.H(t);
+      const int cnt = RoundIntD(hh * L.cnt_factor);
+      if (cnt < min_n || hh < min_h) continue;
+      const int other = L.n - cnt;
+      if (other < min_n) continue;
+      const double oh = L.sh - hh - kEpsilon;
+      if (oh < min_h) continue;
+      const double og = L.sg - g;
+      const double gain = SplitGain(og, oh, g, hh + kEpsilon, l2, p, L.c, 0, other, cnt, L.parent_out);
+      if (gain <= min_gain_shift) continue;
+      any = true;
+      if (gain > best.gain || (gain == best.gain && t < best.thr)) {
+        best.gain = gain;
+        best.thr = t;
+        best.lg = g;
+        best.lh = hh + kEpsilon;
+        best.lc = cnt;
+      }
+    }
+    splittable = BlockAny(any, sc);
+    best = BlockBestCand(best, false, sc);
+  } else {
+    l2 += p.cat_l2;
+    // candidates and their ctr; non-candidates get NaN (never ranked)
+    for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
+      const double hh = hv.H(t);
+      const bool cand = static_cast<double>(RoundIntD(hh * L.cnt_factor)) >= p.cat_smooth;
+      cs->ctr[t] = cand ? hv.G(t) / (hh + p.cat_smooth) : NAN;
+    }
+    __syncthreads();
+    // stable rank among the candidates (std::stable_sort by ctr ascending)
+    int ncand = 0;
+    for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
+      const double c = cs->ctr[t];
+      if (c != c) continue;
+      ++ncand;
+      int r = 0;
+      for (int u = bin_start; u < bin_end; ++u) {
+        const double cu = cs->ctr[u];
+        r += (cu < c) | ((cu == c) & (u < t));
+      }
+      cs->sorted[r] = t;
+    }
+    double d0 = 0.0, d1 = 0.0;
+    BlockSum3(d0, d1, ncand, sc);
+    const int used_bin = ncand;
+    if (tid == 0) {
+      const int max_num_cat = min(p.max_cat_threshold, (used_bin + 1) / 2);
+      for (int o = 0; o < 2; ++o) {
+        const int dir = o == 0 ? 1 : -1;
+        int pos = o == 0 ? 0 : used_bin - 1;
+        int cnt_group = 0, lc = 0;
+        double lg = 0.0, lh = kEpsilon;
+        for (int i = 0; i < used_bin && i < max_num_cat; ++i) {
+          const int t = cs->sorted[pos];
+          pos += dir;
+          const double g = hv.G(t), hh = hv.H(t);
+          const int cnt = RoundIntD(hh * L.cnt_factor);
+          lg += g;
+          lh += hh;
+          lc += cnt;
+          cnt_group += cnt;
+          if (lc < min_n || lh < min_h) continue;
+          const int rc = L.n - lc;
+          if (rc < min_n || rc < p.min_data_per_group) break;
+          const double rh = L.sh - lh;
+          if (rh < min_h) break;
+          if (cnt_group < p.min_data_per_group) continue;
+          cnt_group = 0;
+          const double rg = L.sg - lg;
+          const double gain = SplitGain(lg, lh, rg, rh, l2, p, L.c, 0, lc, rc, L.parent_out);
+          if (gain <= min_gain_shift) continue;
+          splittable = true;
+          if (gain > best.gain) {
+            best.gain = gain;
+            best.thr = i;
+            best.lg = lg;
+            best.lh = lh;
+            best.lc = lc;
+            best_dir = dir;
+          }
+        }
+      }
+      cs->used_bin = used_bin;
+    }
+  }
+  if (tid != 0) return;
+  if (!splittable) return;
+  out->lo = LeafOutputConstrained(best.lg, best.lh, l2, p, L.c, best.lc, L.parent_out);
+  out->lc = best.lc;
+  out->lg = best.lg;
+  out->lh = best.lh - kEpsilon;
+  out->ro = LeafOutputConstrained(L.sg - best.lg, L.sh - best.lh, l2, p, L.c, L.n - best.lc, L.parent_out);
+  out->rc = L.n - best.lc;
+  out->rg = L.sg - best.lg;
+  out->rh = L.sh - best.lh - kEpsilon;
+  out->gain = (best.gain - min_gain_shift) * F.penalty;
+  for (int w = 0; w < kMaxCatWords; ++w) cat_out[w] = 0u;
+  if (onehot) {
+    const int b = best.thr + offset;
+    cat_out[b >> 5] |= 1u << (b & 31);
+    out->ncat = 1;
+  } else {
+    const int k = best.thr + 1;
+    for (int i = 0; i < k; ++i) {
+      const int b = (best_dir == 1 ? cs->sorted[i] : cs->sorted[cs->used_bin - 1 - i]) + offset;
+      cat_out[b >> 5] |= 1u << (b & 31);
+    }
+    out->ncat = k;
+  }
+}
+
 }  // namespace
 
 template <bool ROOT>
 __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
   __shared__ BlockScratch sc;
+  __shared__ CatScratch cat_sc;
   const long long t_entry = wall_clock64();
   const int f = blockIdx.x;
   const int side = blockIdx.y;
@@ -452,9 +625,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   o.default_left = 1;
   o.lc = o.rc = 0;
   o.mono = 0;
-  o.pad = 0;
+  o.ncat = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
-  if (used && !F.is_cat) {
+  if (used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
@@ -498,7 +671,13 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     hv.h = dst;
     hv.inv_g = ig;
     hv.inv_h = ih;
-    FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
+    if (F.is_cat) {
+      FindCategoricalBlock(F, hv, L, p, &o,
+                           a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
+                           &cat_sc);
+    } else {
+      FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
+    }
     if (!ROOT) KTrace(a, s, kTrFindScanned);
   } else {
     o.feature = -1;

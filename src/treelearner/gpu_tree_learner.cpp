@@ -235,6 +235,7 @@ void GPUTreeLearner::UploadData() {
   d_scales_ = Alloc<double>(4);
   d_absmax_ = Alloc<uint32_t>(4);
   d_feat_best_ = Alloc<dev::FeatureBest>(2 * static_cast<size_t>(std::max(1, num_features_)));
+  d_feat_cat_ = Alloc<uint32_t>(2 * static_cast<size_t>(std::max(1, num_features_)) * kMaxCatWords);
   const int hist_blocks = dev::HistGridBlocks();
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_);
   d_root_ = Alloc<double>(4);
@@ -297,6 +298,7 @@ void GPUTreeLearner::UploadData() {
   a.bins_col = d_bins_col_;
   a.num_data = num_data_;
   a.feat_best = d_feat_best_;
+  a.feat_cat = d_feat_cat_;
   int max_fb = 1;
   for (const auto& F : feats) max_fb = std::max(max_fb, F.num_bin - F.offset);
   a.p.max_feature_bins = max_fb;
@@ -357,7 +359,9 @@ void GPUTreeLearner::DecideMode() {
   const char* force = std::getenv("LGBM_AMD_HOST_ASSIST");
   if (force != nullptr && force[0] == '1') dm = false;
   for (int f = 0; f < num_features_ && dm; ++f) {
-    if (data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) dm = false;
+    // categorical splits are scanned on the device up to kFindMaxCatBins categories
+    const BinMapper* m = data_->FeatureBinMapper(f);
+    if (m->bin_type() == BinType::Categorical && m->num_bin() > dev::kFindMaxCatBins) dm = false;
   }
   if (has_forced_split_ || !config_->interaction_constraints_vector.empty() || config_->extra_trees ||
       config_->feature_fraction_bynode < 1.0 || config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
@@ -666,6 +670,20 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     const int inner = si.inner_feature;
     const BinMapper* m = data_->FeatureBinMapper(inner);
     const float gain = static_cast<float>(si.gain + config_->min_gain_to_split);
+    if (m->bin_type() == BinType::Categorical) {
+      // same tree records as SerialTreeLearner::SplitInner (bitsets over inner bins and raw values)
+      auto bits_inner = common::ConstructBitset(si.cat_threshold.data(), si.num_cat_threshold);
+      std::vector<int> cats(si.num_cat_threshold);
+      for (int i = 0; i < si.num_cat_threshold; ++i) {
+        cats[i] = static_cast<int>(data_->RealThreshold(inner, si.cat_threshold[i]));
+      }
+      auto bits = common::ConstructBitset(cats.data(), si.num_cat_threshold);
+      tree->SplitCategorical(r.leaf, inner, si.feature, bits_inner.data(), static_cast<int>(bits_inner.size()),
+                             bits.data(), static_cast<int>(bits.size()), si.left_output, si.right_output,
+                             r.left_count, r.right_count, si.left_sum_hessian, si.right_sum_hessian, gain,
+                             m->missing_type());
+      continue;
+    }
     tree->Split(r.leaf, inner, si.feature, si.threshold, data_->RealThreshold(inner, si.threshold), si.left_output,
                 si.right_output, r.left_count, r.right_count, si.left_sum_hessian, si.right_sum_hessian, gain,
                 m->missing_type(), si.default_left);

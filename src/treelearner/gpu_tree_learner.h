@@ -115,6 +115,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   uint32_t* d_absmax_ = nullptr;
   uint8_t* d_bins_col_ = nullptr;
   dev::FeatureBest* d_feat_best_ = nullptr;
+  uint32_t* d_feat_cat_ = nullptr;  // category sets of the per-feature categorical bests
   uint32_t* h_absmax_ = nullptr;
   double* h_scales_ = nullptr;
   int rows_cap_ = 4096;

@@ -203,3 +203,40 @@ def test_device_goss_matches_reference_block_layout(gpu_available):
     cpu = _bag_counts("cpu", "goss", 5, fixed_gradients=True, num_threads=n_blocks, **kw)
     assert [c[0] for c in gpu[:2]] == [50000, 50000]  # sampling starts at iteration 1 / learning_rate
     assert gpu == cpu
+
+
+def _cat_data(n=40000, seed=12):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(n, 6).astype(np.float32)
+    X[:, 0] = rng.randint(0, 24, size=n)   # many categories: sorted-ctr scan
+    X[:, 1] = rng.randint(0, 3, size=n)    # few categories: one-vs-rest
+    eff = np.sin(np.arange(24) * 1.7)
+    logit = 1.5 * eff[X[:, 0].astype(int)] + 0.8 * (X[:, 1] == 2) + X[:, 2] + 0.3 * rng.randn(n)
+    return X, (logit > 0.2).astype(np.float32)
+
+
+def test_categorical_splits_on_device(gpu_available):
+    """Categorical features are scanned by the device split kernel (no host-assisted fallback):
+    the first tree's categorical splits and the fit match the CPU learner."""
+    X, y = _cat_data()
+    models = {}
+    for device in ("cpu", "gpu"):
+        params = {"objective": "binary", "num_leaves": 15, "verbose": -1, "device_type": device,
+                  "max_cat_to_onehot": 4, "min_data_per_group": 50, "cat_smooth": 5}
+        ds = lgb.Dataset(X, y, params=params, categorical_feature=[0, 1])
+        models[device] = lgb.train(params, ds, 15, verbose_eval=False)
+    cpu_t = models["cpu"].dump_model()["tree_info"][0]["tree_structure"]
+    gpu_t = models["gpu"].dump_model()["tree_info"][0]["tree_structure"]
+    for path in ([], ["left_child"], ["right_child"]):
+        a, b = cpu_t, gpu_t
+        for k in path:
+            a, b = a[k], b[k]
+        if "split_feature" not in a:
+            continue
+        assert a["split_feature"] == b["split_feature"]
+        assert a["decision_type"] == b["decision_type"]
+        assert str(a["threshold"]) == str(b["threshold"])
+        assert a["internal_count"] == b["internal_count"]
+    assert any(t["num_cat"] > 0 for t in models["gpu"].dump_model()["tree_info"])
+    auc_c, auc_g = _auc(y, models["cpu"].predict(X)), _auc(y, models["gpu"].predict(X))
+    assert auc_g > 0.85 and abs(auc_c - auc_g) < 2e-3
