@@ -48,6 +48,7 @@ struct Params {
   double monotone_penalty;
   int32_t data_parallel;  // leaf sizes/decisions from global (split-estimated) counts
   int32_t max_feature_bins;  // max stored bins of one feature (split-scan LDS staging)
+  int32_t has_cat;           // some feature is categorical (split-scan instantiation)
 };
 
 // per-leaf state

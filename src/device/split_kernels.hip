@@ -11,6 +11,8 @@
 // min_data / min_hessian filters, hessian-estimated counts, L1 / max_delta_step / path
 // smoothing / monotone constraints.  Ties keep the threshold the sequential scan would
 // keep.  Per-feature results go to feat_best; the next partition kernel picks from them.
+#include <type_traits>
+
 #include "device_common.h"
 
 namespace lgbm_amd {
@@ -371,7 +373,7 @@ struct CatScratch {
 // otherwise the bins with enough data sorted by g / (h + cat_smooth) -- a stable rank
 // computed in parallel -- and the sequential prefix scan from both ends (<= 2 x
 // max_cat_threshold steps, thread 0) with the min_data_per_group rules.
-__device__ void FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
+__device__ __noinline__ void FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
                                      FeatureBest* out, uint32_t* cat_out, BlockScratch* sc, CatScratch* cs) {
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
@@ -533,11 +535,13 @@ __device__ void FindCategoricalBlock(const Feature& F, HistView hv, const LeafCt
 
 }  // namespace
 
-template <bool ROOT>
+// CAT: the dataset has categorical features.  The categorical scan doubles the kernel's
+// registers (and needs a stack), so numerical-only data runs the instantiation without it.
+template <bool ROOT, bool CAT>
 __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
   __shared__ BlockScratch sc;
-  __shared__ CatScratch cat_sc;
+  __shared__ typename std::conditional<CAT, CatScratch, int>::type cat_sc;
   const long long t_entry = wall_clock64();
   const int f = blockIdx.x;
   const int side = blockIdx.y;
@@ -627,7 +631,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   o.mono = 0;
   o.ncat = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
-  if (used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
+  if (used && (!F.is_cat || (CAT && F.num_bin <= kFindMaxCatBins))) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
@@ -671,10 +675,14 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     hv.h = dst;
     hv.inv_g = ig;
     hv.inv_h = ih;
-    if (F.is_cat) {
-      FindCategoricalBlock(F, hv, L, p, &o,
-                           a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
-                           &cat_sc);
+    if constexpr (CAT) {
+      if (F.is_cat) {
+        FindCategoricalBlock(F, hv, L, p, &o,
+                             a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
+                             &cat_sc);
+      } else {
+        FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
+      }
     } else {
       FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
     }
@@ -690,10 +698,18 @@ static size_t FindLds(const KArgs& a) {
   return a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
 }
 void FindRoot(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_find<true>, dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
+  if (a.p.has_cat) {
+    hipLaunchKernelGGL((k_find<true, true>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
+  } else {
+    hipLaunchKernelGGL((k_find<true, false>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
+  }
 }
 void FindStep(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_find<false>, dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
+  if (a.p.has_cat) {
+    hipLaunchKernelGGL((k_find<false, true>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
+  } else {
+    hipLaunchKernelGGL((k_find<false, false>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
+  }
 }
 
 }  // namespace dev

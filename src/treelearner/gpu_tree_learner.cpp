@@ -302,6 +302,8 @@ void GPUTreeLearner::UploadData() {
   int max_fb = 1;
   for (const auto& F : feats) max_fb = std::max(max_fb, F.num_bin - F.offset);
   a.p.max_feature_bins = max_fb;
+  a.p.has_cat = 0;
+  for (const auto& F : feats) a.p.has_cat |= F.is_cat;
   // per-workgroup row cap of the histogram kernels (fixed-point headroom): see k_hist
   rows_cap_ = std::max(dev::kHistMinRows * 4, (num_data_ + hist_blocks - 1) / hist_blocks);
   a.hist_rows_cap = rows_cap_;
