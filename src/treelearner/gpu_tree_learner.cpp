@@ -1,6 +1,8 @@
 // MI355X tree learner host orchestration (see gpu_tree_learner.h).
 #include "gpu_tree_learner.h"
 
+#include "parallel_tree_learner.h"
+
 #include <omp.h>
 
 #include <algorithm>
@@ -44,10 +46,7 @@ TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Conf
     Log::Warning("feature-parallel learning on the device learner uses the serial device learner on every rank");
     return new GPUTreeLearner(config, false);
   }
-  if (learner_type == "voting") {
-    Log::Warning("voting-parallel on the device learner runs as data-parallel (full histogram all-reduce)");
-    return new GPUTreeLearner(config, true);
-  }
+  if (learner_type == "voting") return new VotingParallelTreeLearner<GPUTreeLearner>(config);
   Log::Fatal("Unknown tree learner type %s", learner_type.c_str());
   return nullptr;
 }
@@ -239,6 +238,7 @@ void GPUTreeLearner::UploadData() {
   const int hist_blocks = dev::HistGridBlocks();
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_);
   d_root_ = Alloc<double>(4);
+  d_leaf_sums_ = Alloc<double>(4);
   d_root_parts_ = Alloc<double>(2 * static_cast<size_t>(dev::GradientBlocks(num_data_)));
   d_max_parts_ = Alloc<float>(2 * static_cast<size_t>(std::max(dev::GradientBlocks(num_data_),
                                                                 dev::PackBlocks(num_data_))));
@@ -359,7 +359,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
 void GPUTreeLearner::DecideMode() {
   bool dm = true;
   const char* force = std::getenv("LGBM_AMD_HOST_ASSIST");
-  if (force != nullptr && force[0] == '1') dm = false;
+  if ((force != nullptr && force[0] == '1') || force_host_mode_) dm = false;
   for (int f = 0; f < num_features_ && dm; ++f) {
     // categorical splits are scanned on the device up to kFindMaxCatBins categories
     const BinMapper* m = data_->FeatureBinMapper(f);
@@ -731,6 +731,27 @@ void GPUTreeLearner::BeforeTrain() {
   smaller_ = LeafState{0, static_cast<data_size_t>(cnt), sg, sh, 0.0};
   larger_ = LeafState{};
   larger_.leaf = -1;
+}
+
+// host-assisted growth keeps every leaf's rows in index buffer 0 at [leaf_begin, +count)
+SerialTreeLearner::LeafState GPUTreeLearner::LocalLeafSums(int leaf) const {
+  LeafState ls;
+  ls.leaf = leaf;
+  ls.num_data = leaf_count_[leaf];
+  if (ls.num_data <= 0) return ls;
+  dev::KArgs a = args_;
+  a.idx = d_idx_ + leaf_begin_[leaf];
+  a.num_rows = ls.num_data;
+  a.num_rows_dev = nullptr;
+  a.root_identity = 0;
+  a.root = d_leaf_sums_;
+  dev::RootSum(a, stream_);
+  double h[3];
+  HIPCHECK(hipMemcpyAsync(h, d_leaf_sums_, sizeof(double) * 3, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  ls.sum_g = h[0];
+  ls.sum_h = h[1];
+  return ls;
 }
 
 data_size_t GPUTreeLearner::GetGlobalDataCountInLeaf(int leaf) const {

@@ -29,6 +29,9 @@ namespace lgbm_amd {
 class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
  public:
   GPUTreeLearner(const Config* config, bool data_parallel);
+  explicit GPUTreeLearner(const Config* config) : GPUTreeLearner(config, false) {}
+  // host-assisted growth for every tree (the voting-parallel learner scans on the host)
+  void ForceHostMode() { force_host_mode_ = true; }
   ~GPUTreeLearner() override;
 
   // TreeLearner
@@ -68,6 +71,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   data_size_t PartitionLeaf(int leaf, int inner_feature, const SplitInfo& s, int new_leaf) override;
   void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) override;
   data_size_t GetGlobalDataCountInLeaf(int leaf) const override;
+  LeafState LocalLeafSums(int leaf) const override;
 
  private:
   void UploadData();
@@ -91,6 +95,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
 
   bool data_parallel_ = false;
   bool device_mode_ = true;
+  bool force_host_mode_ = false;
+  double* d_leaf_sums_ = nullptr;
   int device_id_ = 0;
   hipStream_t stream_ = nullptr;
   dev::KArgs args_{};

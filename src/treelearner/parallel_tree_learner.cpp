@@ -4,6 +4,8 @@
 // voting-parallel:  reference src/treelearner/voting_parallel_tree_learner.cpp:15-452
 #include "parallel_tree_learner.h"
 
+#include <type_traits>
+
 #include <omp.h>
 
 #include <algorithm>
@@ -11,6 +13,7 @@
 
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/network.h"
+#include "gpu_tree_learner.h"
 
 namespace lgbm_amd {
 
@@ -244,74 +247,72 @@ void DataParallelTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, i
 }
 
 // ------------------------------------------------------------------ voting parallel
-void VotingParallelTreeLearner::InitLocalParams() {
-  Config local = *config_;
+template <typename Base>
+void VotingParallelTreeLearner<Base>::InitLocalParams() {
+  Config local = *this->config_;
   local.min_data_in_leaf /= num_machines_;
   local.min_sum_hessian_in_leaf /= num_machines_;
   local_params_ = MakeSplitParams(local);
 }
 
-void VotingParallelTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
-  SerialTreeLearner::Init(train_data, is_constant_hessian);
+template <typename Base>
+void VotingParallelTreeLearner<Base>::Init(const Dataset* train_data, bool is_constant_hessian) {
+  if constexpr (std::is_base_of<DeviceTreeLearner, Base>::value) {
+    // the voting exchange runs between the host-side split scans of each step
+    this->ForceHostMode();
+  }
+  Base::Init(train_data, is_constant_hessian);
   rank_ = Network::rank();
   num_machines_ = Network::num_machines();
-  top_k_ = std::min(config_->top_k, num_features_);
+  top_k_ = std::min(this->config_->top_k, this->num_features_);
   InitLocalParams();
-  global_count_.assign(config_->num_leaves, 0);
-  global_small_hist_.assign(2 * data_->num_total_bin(), 0.0);
-  global_large_hist_.assign(2 * data_->num_total_bin(), 0.0);
-  in_buf_.resize(std::max<size_t>(4 * sizeof(hist_t) * data_->num_total_bin(),
-                                  2 * SplitInfoWireSize(config_->max_cat_threshold)));
+  global_count_.assign(this->config_->num_leaves, 0);
+  global_small_hist_.assign(2 * this->data_->num_total_bin(), 0.0);
+  global_large_hist_.assign(2 * this->data_->num_total_bin(), 0.0);
+  in_buf_.resize(std::max<size_t>(4 * sizeof(hist_t) * this->data_->num_total_bin(),
+                                  2 * SplitInfoWireSize(this->config_->max_cat_threshold)));
   out_buf_.resize(in_buf_.size());
 }
 
-void VotingParallelTreeLearner::ResetConfig(const Config* config) {
-  SerialTreeLearner::ResetConfig(config);
-  top_k_ = std::min(config_->top_k, num_features_);
+template <typename Base>
+void VotingParallelTreeLearner<Base>::ResetConfig(const Config* config) {
+  Base::ResetConfig(config);
+  top_k_ = std::min(this->config_->top_k, this->num_features_);
   InitLocalParams();
-  global_count_.assign(config_->num_leaves, 0);
+  global_count_.assign(this->config_->num_leaves, 0);
 }
 
-void VotingParallelTreeLearner::BeforeTrain() {
-  SerialTreeLearner::BeforeTrain();
-  double loc[3] = {static_cast<double>(smaller_.num_data), smaller_.sum_g, smaller_.sum_h};
+template <typename Base>
+void VotingParallelTreeLearner<Base>::BeforeTrain() {
+  Base::BeforeTrain();
+  double loc[3] = {static_cast<double>(this->smaller_.num_data), this->smaller_.sum_g, this->smaller_.sum_h};
   auto glob = Network::GlobalSum(std::vector<double>(loc, loc + 3));
   global_smaller_ = LeafState{0, static_cast<data_size_t>(glob[0]), glob[1], glob[2], 0.0};
   global_larger_ = LeafState{};
   global_count_[0] = global_smaller_.num_data;
 }
 
-SerialTreeLearner::LeafState VotingParallelTreeLearner::LocalLeafState(int leaf) const {
-  data_size_t cnt = 0;
-  const data_size_t* idx = LeafIndices(leaf, &cnt);
-  double sg = 0, sh = 0;
-#pragma omp parallel for schedule(static) reduction(+ : sg, sh)
-  for (data_size_t i = 0; i < cnt; ++i) {
-    sg += gradients_[idx[i]];
-    sh += hessians_[idx[i]];
-  }
-  return LeafState{leaf, cnt, sg, sh, 0.0};
-}
-
-bool VotingParallelTreeLearner::BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf) {
-  if (!SerialTreeLearner::BeforeFindBestSplit(tree, left_leaf, right_leaf)) return false;
+template <typename Base>
+bool VotingParallelTreeLearner<Base>::BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf) {
+  if (!Base::BeforeFindBestSplit(tree, left_leaf, right_leaf)) return false;
   if (right_leaf < 0) return true;
   // leaf roles follow the global counts; statistics for local voting are local
-  const int small = GetGlobalDataCountInLeaf(left_leaf) < GetGlobalDataCountInLeaf(right_leaf) ? left_leaf : right_leaf;
+  const int small = this->GetGlobalDataCountInLeaf(left_leaf) < this->GetGlobalDataCountInLeaf(right_leaf) ? left_leaf : right_leaf;
   const int large = small == left_leaf ? right_leaf : left_leaf;
-  smaller_ = LocalLeafState(small);
-  larger_ = LocalLeafState(large);
-  smaller_.output = global_smaller_.output;
-  larger_.output = global_larger_.output;
+  this->smaller_ = this->LocalLeafSums(small);
+  this->larger_ = this->LocalLeafSums(large);
+  this->smaller_.output = global_smaller_.output;
+  this->larger_.output = global_larger_.output;
   return true;
 }
 
-void VotingParallelTreeLearner::GlobalVoting(int leaf, const std::vector<LightSplitInfo>& splits,
+template <typename Base>
+void VotingParallelTreeLearner<Base>::GlobalVoting(int leaf, const std::vector<LightSplitInfo>& splits,
                                              std::vector<int>* out) const {
   out->clear();
   if (leaf < 0) return;
-  const score_t mean = GetGlobalDataCountInLeaf(leaf) / static_cast<score_t>(num_machines_);
-  std::vector<LightSplitInfo> best(data_->num_total_features());
+  const score_t mean = this->GetGlobalDataCountInLeaf(leaf) / static_cast<score_t>(num_machines_);
+  std::vector<LightSplitInfo> best(this->data_->num_total_features());
   for (const auto& s : splits) {
     if (s.feature < 0) continue;
     const double g = s.gain * (s.left_count + s.right_count) / mean;
@@ -327,38 +328,39 @@ void VotingParallelTreeLearner::GlobalVoting(int leaf, const std::vector<LightSp
   }
 }
 
-void VotingParallelTreeLearner::FindBestSplits(const Tree* tree) {
+template <typename Base>
+void VotingParallelTreeLearner<Base>::FindBestSplits(const Tree* tree) {
   // 1) local histograms + local per-feature best splits (local statistics & params)
-  std::vector<int8_t> used(num_features_, 0);
-  const auto& bytree = col_sampler_.is_feature_used_bytree();
-  for (int f = 0; f < num_features_; ++f) {
+  std::vector<int8_t> used(this->num_features_, 0);
+  const auto& bytree = this->col_sampler_.is_feature_used_bytree();
+  for (int f = 0; f < this->num_features_; ++f) {
     if (!bytree[f]) continue;
-    if (has_parent_hist_ && !splittable_[larger_slot_][f]) {
-      splittable_[smaller_slot_][f] = 0;
+    if (this->has_parent_hist_ && !this->splittable_[this->larger_slot_][f]) {
+      this->splittable_[this->smaller_slot_][f] = 0;
       continue;
     }
     used[f] = 1;
   }
-  ConstructHistograms(used, has_parent_hist_);
-  std::vector<SplitInfo> sbest(num_features_), lbest(num_features_);
-  const int sdepth = tree->leaf_depth(smaller_.leaf);
-  const int ldepth = larger_.leaf >= 0 ? tree->leaf_depth(larger_.leaf) : 0;
+  this->ConstructHistograms(used, this->has_parent_hist_);
+  std::vector<SplitInfo> sbest(this->num_features_), lbest(this->num_features_);
+  const int sdepth = tree->leaf_depth(this->smaller_.leaf);
+  const int ldepth = this->larger_.leaf >= 0 ? tree->leaf_depth(this->larger_.leaf) : 0;
 #pragma omp parallel for schedule(static)
-  for (int f = 0; f < num_features_; ++f) {
+  for (int f = 0; f < this->num_features_; ++f) {
     if (!used[f]) continue;
-    data_->FixHistogram(f, smaller_.sum_g, smaller_.sum_h, FeatureHist(smaller_slot_, f));
-    splittable_[smaller_slot_][f] = EvalFeature(FeatureHist(smaller_slot_, f), f, local_params_, smaller_, sdepth,
+    this->data_->FixHistogram(f, this->smaller_.sum_g, this->smaller_.sum_h, this->FeatureHist(this->smaller_slot_, f));
+    this->splittable_[this->smaller_slot_][f] = this->EvalFeature(this->FeatureHist(this->smaller_slot_, f), f, local_params_, this->smaller_, sdepth,
                                                 &sbest[f]) ? 1 : 0;
-    if (larger_.leaf < 0) continue;
-    hist_t* lh = FeatureHist(larger_slot_, f);
-    if (has_parent_hist_) {
-      const hist_t* sh = FeatureHist(smaller_slot_, f);
-      const int n = 2 * data_->FeatureHistSize(f);
+    if (this->larger_.leaf < 0) continue;
+    hist_t* lh = this->FeatureHist(this->larger_slot_, f);
+    if (this->has_parent_hist_) {
+      const hist_t* sh = this->FeatureHist(this->smaller_slot_, f);
+      const int n = 2 * this->data_->FeatureHistSize(f);
       for (int i = 0; i < n; ++i) lh[i] -= sh[i];
     } else {
-      data_->FixHistogram(f, larger_.sum_g, larger_.sum_h, lh);
+      this->data_->FixHistogram(f, this->larger_.sum_g, this->larger_.sum_h, lh);
     }
-    splittable_[larger_slot_][f] = EvalFeature(lh, f, local_params_, larger_, ldepth, &lbest[f]) ? 1 : 0;
+    this->splittable_[this->larger_slot_][f] = this->EvalFeature(lh, f, local_params_, this->larger_, ldepth, &lbest[f]) ? 1 : 0;
   }
   // 2) local top-k, allgather, global vote
   auto topk = [&](std::vector<SplitInfo> v) {
@@ -387,11 +389,11 @@ void VotingParallelTreeLearner::FindBestSplits(const Tree* tree) {
     lg.push_back(all[i + 1]);
   }
   std::vector<int> stop, ltop;
-  GlobalVoting(smaller_.leaf, sg, &stop);
-  GlobalVoting(larger_.leaf, lg, &ltop);
+  GlobalVoting(this->smaller_.leaf, sg, &stop);
+  GlobalVoting(this->larger_.leaf, lg, &ltop);
   // 3) reduce-scatter the elected histograms (alternating smaller/larger, even split)
-  std::vector<int8_t> s_agg(num_features_, 0), l_agg(num_features_, 0);
-  std::vector<size_t> s_read(num_features_, 0), l_read(num_features_, 0);
+  std::vector<int8_t> s_agg(this->num_features_, 0), l_agg(this->num_features_, 0);
+  std::vector<size_t> s_read(this->num_features_, 0), l_read(this->num_features_, 0);
   std::vector<comm_size_t> bstart(num_machines_, 0), blen(num_machines_, 0);
   const size_t total = stop.size() + ltop.size();
   const size_t avg = (total + num_machines_ - 1) / num_machines_;
@@ -402,27 +404,27 @@ void VotingParallelTreeLearner::FindBestSplits(const Tree* tree) {
     const size_t want = std::min(avg, total - used_n);
     while (cnt < want) {
       if (si < stop.size()) {
-        const int f = data_->InnerFeatureIndex(stop[si++]);
+        const int f = this->data_->InnerFeatureIndex(stop[si++]);
         ++cnt;
-        const size_t bytes = entry * data_->FeatureHistSize(f);
+        const size_t bytes = entry * this->data_->FeatureHistSize(f);
         if (m == rank_) {
           s_agg[f] = 1;
           s_read[f] = cur;
         }
-        std::memcpy(in_buf_.data() + rs, FeatureHist(smaller_slot_, f), bytes);
+        std::memcpy(in_buf_.data() + rs, this->FeatureHist(this->smaller_slot_, f), bytes);
         cur += bytes;
         rs += bytes;
       }
       if (cnt >= want) break;
       if (li < ltop.size()) {
-        const int f = data_->InnerFeatureIndex(ltop[li++]);
+        const int f = this->data_->InnerFeatureIndex(ltop[li++]);
         ++cnt;
-        const size_t bytes = entry * data_->FeatureHistSize(f);
+        const size_t bytes = entry * this->data_->FeatureHistSize(f);
         if (m == rank_) {
           l_agg[f] = 1;
           l_read[f] = cur;
         }
-        std::memcpy(in_buf_.data() + rs, FeatureHist(larger_slot_, f), bytes);
+        std::memcpy(in_buf_.data() + rs, this->FeatureHist(this->larger_slot_, f), bytes);
         cur += bytes;
         rs += bytes;
       }
@@ -434,27 +436,27 @@ void VotingParallelTreeLearner::FindBestSplits(const Tree* tree) {
   Network::ReduceScatter(in_buf_.data(), static_cast<comm_size_t>(rs), sizeof(hist_t), bstart.data(), blen.data(),
                          out_buf_.data(), static_cast<comm_size_t>(out_buf_.size()), &HistSumReducer);
   // 4) best splits on the global histograms this rank owns (global statistics & params)
-  auto s_node = col_sampler_.GetByNode(tree, global_smaller_.leaf);
+  auto s_node = this->col_sampler_.GetByNode(tree, global_smaller_.leaf);
   std::vector<int8_t> l_node;
-  if (global_larger_.leaf >= 0) l_node = col_sampler_.GetByNode(tree, global_larger_.leaf);
+  if (global_larger_.leaf >= 0) l_node = this->col_sampler_.GetByNode(tree, global_larger_.leaf);
   const int nt = omp_get_max_threads();
   std::vector<SplitInfo> sb(nt), lb(nt);
 #pragma omp parallel for schedule(static)
-  for (int f = 0; f < num_features_; ++f) {
+  for (int f = 0; f < this->num_features_; ++f) {
     const int tid = omp_get_thread_num();
-    const size_t off = 2 * static_cast<size_t>(data_->FeatureHistOffset(f));
-    const size_t bytes = entry * data_->FeatureHistSize(f);
+    const size_t off = 2 * static_cast<size_t>(this->data_->FeatureHistOffset(f));
+    const size_t bytes = entry * this->data_->FeatureHistSize(f);
     if (s_agg[f] && s_node[f]) {
       hist_t* h = global_small_hist_.data() + off;
       std::memcpy(h, out_buf_.data() + s_read[f], bytes);
-      data_->FixHistogram(f, global_smaller_.sum_g, global_smaller_.sum_h, h);
-      EvalFeature(h, f, params_, global_smaller_, sdepth, &sb[tid]);
+      this->data_->FixHistogram(f, global_smaller_.sum_g, global_smaller_.sum_h, h);
+      this->EvalFeature(h, f, this->params_, global_smaller_, sdepth, &sb[tid]);
     }
     if (l_agg[f] && global_larger_.leaf >= 0 && l_node[f]) {
       hist_t* h = global_large_hist_.data() + off;
       std::memcpy(h, out_buf_.data() + l_read[f], bytes);
-      data_->FixHistogram(f, global_larger_.sum_g, global_larger_.sum_h, h);
-      EvalFeature(h, f, params_, global_larger_, ldepth, &lb[tid]);
+      this->data_->FixHistogram(f, global_larger_.sum_g, global_larger_.sum_h, h);
+      this->EvalFeature(h, f, this->params_, global_larger_, ldepth, &lb[tid]);
     }
   }
   SplitInfo bs, bl;
@@ -462,19 +464,23 @@ void VotingParallelTreeLearner::FindBestSplits(const Tree* tree) {
     if (sb[t] > bs) bs = sb[t];
     if (lb[t] > bl) bl = lb[t];
   }
-  SyncUpGlobalBestSplit(&bs, &bl, config_->max_cat_threshold);
-  best_split_per_leaf_[global_smaller_.leaf] = bs;
-  if (bl.feature >= 0 && global_larger_.leaf >= 0) best_split_per_leaf_[global_larger_.leaf] = bl;
+  SyncUpGlobalBestSplit(&bs, &bl, this->config_->max_cat_threshold);
+  this->best_split_per_leaf_[global_smaller_.leaf] = bs;
+  if (bl.feature >= 0 && global_larger_.leaf >= 0) this->best_split_per_leaf_[global_larger_.leaf] = bl;
 }
 
-void VotingParallelTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) {
-  SplitInner(tree, best_leaf, left_leaf, right_leaf, false);
-  const SplitInfo& s = best_split_per_leaf_[best_leaf];
+template <typename Base>
+void VotingParallelTreeLearner<Base>::Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) {
+  this->SplitInner(tree, best_leaf, left_leaf, right_leaf, false);
+  const SplitInfo& s = this->best_split_per_leaf_[best_leaf];
   global_count_[*left_leaf] = s.left_count;
   global_count_[*right_leaf] = s.right_count;
-  // SplitInner set smaller_/larger_ from the (global) split statistics
-  global_smaller_ = smaller_;
-  global_larger_ = larger_;
+  // this->SplitInner set this->smaller_/this->larger_ from the (global) split statistics
+  global_smaller_ = this->smaller_;
+  global_larger_ = this->larger_;
 }
+
+template class VotingParallelTreeLearner<SerialTreeLearner>;
+template class VotingParallelTreeLearner<GPUTreeLearner>;
 
 }  // namespace lgbm_amd

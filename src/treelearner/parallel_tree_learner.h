@@ -59,13 +59,19 @@ class DataParallelTreeLearner : public SerialTreeLearner {
   std::vector<char> in_buf_, out_buf_;
 };
 
-class VotingParallelTreeLearner : public SerialTreeLearner {
+// Base = SerialTreeLearner (host histograms) or GPUTreeLearner in host-assisted growth
+// (device histograms and partitions), as the reference instantiates
+// VotingParallelTreeLearner<SerialTreeLearner | GPUTreeLearner>
+// (voting_parallel_tree_learner.cpp:456-458).
+template <typename Base>
+class VotingParallelTreeLearner : public Base {
  public:
-  explicit VotingParallelTreeLearner(const Config* config) : SerialTreeLearner(config) {}
+  explicit VotingParallelTreeLearner(const Config* config) : Base(config) {}
   void Init(const Dataset* train_data, bool is_constant_hessian) override;
   void ResetConfig(const Config* config) override;
 
  protected:
+  using LeafState = typename SerialTreeLearner::LeafState;
   void BeforeTrain() override;
   bool BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf) override;
   void FindBestSplits(const Tree* tree) override;
@@ -76,7 +82,6 @@ class VotingParallelTreeLearner : public SerialTreeLearner {
 
  private:
   void InitLocalParams();
-  LeafState LocalLeafState(int leaf) const;
   void GlobalVoting(int leaf, const std::vector<LightSplitInfo>& splits, std::vector<int>* out) const;
 
   int rank_ = 0, num_machines_ = 1, top_k_ = 20;

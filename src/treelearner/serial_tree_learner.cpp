@@ -570,4 +570,16 @@ Tree* SerialTreeLearner::FitByExistingTree(const Tree* old_tree, const std::vect
   return FitByExistingTree(old_tree, g, h);
 }
 
+SerialTreeLearner::LeafState SerialTreeLearner::LocalLeafSums(int leaf) const {
+  data_size_t cnt = 0;
+  const data_size_t* idx = LeafIndices(leaf, &cnt);
+  double sg = 0, sh = 0;
+#pragma omp parallel for schedule(static) reduction(+ : sg, sh)
+  for (data_size_t i = 0; i < cnt; ++i) {
+    sg += gradients_[idx[i]];
+    sh += hessians_[idx[i]];
+  }
+  return LeafState{leaf, cnt, sg, sh, 0.0};
+}
+
 }  // namespace lgbm_amd

@@ -76,6 +76,8 @@ class SerialTreeLearner : public TreeLearner {
                                             const Tree* tree);
   virtual void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf);
   virtual data_size_t GetGlobalDataCountInLeaf(int leaf) const { return leaf >= 0 ? leaf_count_[leaf] : 0; }
+  // (count, sum g, sum h) of the leaf's local rows; the device learner sums them on the device
+  virtual LeafState LocalLeafSums(int leaf) const;
   int ForceSplits(Tree* tree, int* left_leaf, int* right_leaf, int* cur_depth);
   void ComputeBestSplitForFeature(int slot, int inner, const std::vector<int8_t>& node_used, const LeafState& ls,
                                   int depth, SplitInfo* best);

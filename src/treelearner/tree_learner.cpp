@@ -17,7 +17,7 @@ TreeLearner* TreeLearner::CreateTreeLearner(const std::string& learner_type, con
     if (learner_type == "serial") return new SerialTreeLearner(config);
     if (learner_type == "feature") return new FeatureParallelTreeLearner(config);
     if (learner_type == "data") return new DataParallelTreeLearner(config);
-    if (learner_type == "voting") return new VotingParallelTreeLearner(config);
+    if (learner_type == "voting") return new VotingParallelTreeLearner<SerialTreeLearner>(config);
   } else if (device_type == "gpu") {
     return CreateDeviceTreeLearner(learner_type, config);
   }

@@ -96,3 +96,18 @@ def test_device_data_parallel_two_ranks_one_gpu(tmp_path, gpu_available):
     cpu_dir.mkdir()
     _, cpu_preds = _run("data", cpu_dir, device="cpu")
     assert abs(auc - roc_auc_score(y, cpu_preds[0])) < 0.01
+
+
+@pytest.mark.gpu
+def test_device_voting_parallel_two_ranks_one_gpu(tmp_path, gpu_available):
+    """Voting-parallel (PV-Tree) over the device learner: device histograms / partitions,
+    host voting exchange; ranks agree and the fit matches the CPU voting learner's quality."""
+    models, preds = _run("voting", tmp_path, device="gpu")
+    assert _trees(models[0]) == _trees(models[1])
+    X, y = make_data()
+    auc = roc_auc_score(y, preds[0])
+    assert auc > 0.8
+    cpu_dir = tmp_path / "cpu"
+    cpu_dir.mkdir()
+    _, cpu_preds = _run("voting", cpu_dir, device="cpu")
+    assert abs(auc - roc_auc_score(y, cpu_preds[0])) < 0.01
