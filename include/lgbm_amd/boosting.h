@@ -40,8 +40,17 @@ PredictionEarlyStopInstance CreatePredictionEarlyStopInstance(const std::string&
 class ScoreUpdater {
  public:
   ScoreUpdater(const Dataset* data, int num_tree_per_iteration);
-  double* score() { return score_.data(); }
-  const double* score() const { return score_.data(); }
+  // a validation updater may hand its scores to the device learner (slot): updates then run
+  // on the device and the host copy is refreshed when it is read
+  void AttachDevice(DeviceTreeLearner* dl, int slot);
+  double* score() {
+    SyncFromDevice();
+    return score_.data();
+  }
+  const double* score() const {
+    const_cast<ScoreUpdater*>(this)->SyncFromDevice();
+    return score_.data();
+  }
   data_size_t num_data() const { return num_data_; }
   bool has_init_score() const { return has_init_score_; }
   void AddScore(double v, int tree_id);
@@ -52,10 +61,15 @@ class ScoreUpdater {
   const Dataset* data() const { return data_; }
 
  private:
+  void SyncFromDevice();
   const Dataset* data_;
   data_size_t num_data_;
+  int num_tree_per_iteration_ = 1;
   std::vector<double> score_;
   bool has_init_score_ = false;
+  DeviceTreeLearner* device_ = nullptr;
+  int device_slot_ = -1;
+  bool host_stale_ = false;
 };
 
 class GBDT {
@@ -89,6 +103,10 @@ class GBDT {
 
   // ---- prediction
   void InitPredict(int start_iteration, int num_iteration, bool is_pred_contrib);
+  // normal / raw predictions of a dense float32 / float64 matrix on the MI355X (same results
+  // as the host predictor); false if not applicable (no device, too many classes)
+  bool PredictDenseOnDevice(const void* data, bool is_double, int64_t nrow, int ncol, bool row_major,
+                            int start_iteration, int num_iteration, bool raw, double* out);
   int NumPredictOneRow(int start_iteration, int num_iteration, bool is_pred_leaf, bool is_pred_contrib) const;
   void PredictRaw(const double* features, double* output, const PredictionEarlyStopInstance* es) const;
   void Predict(const double* features, double* output, const PredictionEarlyStopInstance* es) const;

@@ -50,6 +50,14 @@ class DeviceTreeLearner {
   virtual score_t* device_gradients() = 0;
   virtual score_t* device_hessians() = 0;
   virtual void Synchronize() = 0;
+  // validation sets (binned like the training data): rows and scores resident on the device.
+  // AddValidData uploads the current host scores ([tree_id][rows]) and returns a slot, or -1
+  // if the set can not be scored on the device (its group layout differs)
+  virtual int AddValidData(const Dataset* valid, int num_tree_per_iteration, const double* scores) = 0;
+  virtual void ValidAddConst(int slot, double v, int tree_id) = 0;
+  virtual void ValidMultiply(int slot, double v, int tree_id) = 0;
+  virtual void ValidAddTree(int slot, const Tree* tree, int tree_id) = 0;
+  virtual void ValidScoreToHost(int slot, double* host) = 0;
 };
 
 TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Config* config);

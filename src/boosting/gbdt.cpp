@@ -15,7 +15,8 @@
 namespace lgbm_amd {
 
 // ------------------------------------------------------------------ ScoreUpdater
-ScoreUpdater::ScoreUpdater(const Dataset* data, int ntpi) : data_(data), num_data_(data->num_data()) {
+ScoreUpdater::ScoreUpdater(const Dataset* data, int ntpi)
+    : data_(data), num_data_(data->num_data()), num_tree_per_iteration_(ntpi) {
   score_.assign(static_cast<size_t>(num_data_) * ntpi, 0.0);
   const double* init = data->metadata().init_score();
   if (init != nullptr) {
@@ -27,19 +28,46 @@ ScoreUpdater::ScoreUpdater(const Dataset* data, int ntpi) : data_(data), num_dat
   }
 }
 
+void ScoreUpdater::AttachDevice(DeviceTreeLearner* dl, int slot) {
+  device_ = dl;
+  device_slot_ = slot;
+  host_stale_ = false;
+}
+
+void ScoreUpdater::SyncFromDevice() {
+  if (device_ == nullptr || !host_stale_) return;
+  device_->ValidScoreToHost(device_slot_, score_.data());
+  host_stale_ = false;
+}
+
 void ScoreUpdater::AddScore(double v, int k) {
+  if (device_ != nullptr) {
+    device_->ValidAddConst(device_slot_, v, k);
+    host_stale_ = true;
+    return;
+  }
   double* s = score_.data() + static_cast<size_t>(k) * num_data_;
 #pragma omp parallel for schedule(static, 512) if (num_data_ >= 1024)
   for (data_size_t i = 0; i < num_data_; ++i) s[i] += v;
 }
 
 void ScoreUpdater::MultiplyScore(double v, int k) {
+  if (device_ != nullptr) {
+    device_->ValidMultiply(device_slot_, v, k);
+    host_stale_ = true;
+    return;
+  }
   double* s = score_.data() + static_cast<size_t>(k) * num_data_;
 #pragma omp parallel for schedule(static, 512) if (num_data_ >= 1024)
   for (data_size_t i = 0; i < num_data_; ++i) s[i] *= v;
 }
 
 void ScoreUpdater::AddScore(const Tree* tree, int k) {
+  if (device_ != nullptr) {
+    device_->ValidAddTree(device_slot_, tree, k);
+    host_stale_ = true;
+    return;
+  }
   tree->AddPredictionToScore(data_, num_data_, score_.data() + static_cast<size_t>(k) * num_data_);
 }
 
@@ -142,6 +170,12 @@ void GBDT::AddValidDataset(const Dataset* valid, const std::vector<const Metric*
     for (int k = 0; k < num_tree_per_iteration_; ++k) {
       su->AddScore(models_[(i + num_init_iteration_) * num_tree_per_iteration_ + k].get(), k);
     }
+  }
+  if (device_learner_ != nullptr) {
+    // binned validation rows and their scores move to the device: one traversal kernel per
+    // tree instead of a host pass (falls back to the host if the layouts differ)
+    const int slot = device_learner_->AddValidData(valid, num_tree_per_iteration_, su->score());
+    if (slot >= 0) su->AttachDevice(device_learner_, slot);
   }
   valid_score_updater_.push_back(std::move(su));
   valid_metrics_.emplace_back(metrics);

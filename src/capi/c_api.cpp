@@ -7,6 +7,7 @@
 #include <omp.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -403,6 +404,29 @@ class Booster {
     }
     if (!err.empty()) Log::Fatal("%s", err.c_str());
     *out_len = k * nrow;
+  }
+
+  // dense matrices from a booster trained (or predicted) with device_type=gpu go to the
+  // device forest kernel; single rows, leaf / contrib predictions and early stopping stay on
+  // the host
+  bool PredictDenseOnDevice(const void* data, int data_type, int32_t nrow, int32_t ncol, int is_row_major,
+                            int predict_type, int start_iteration, int num_iteration, const Config& cfg, double* out,
+                            int64_t* out_len) {
+    if (predict_type != C_API_PREDICT_NORMAL && predict_type != C_API_PREDICT_RAW_SCORE) return false;
+    if (cfg.pred_early_stop || nrow < 1024) return false;
+    if (data_type != C_API_DTYPE_FLOAT32 && data_type != C_API_DTYPE_FLOAT64) return false;
+    if (cfg.device_type != "gpu" && config_.device_type != "gpu") return false;
+    const char* e = std::getenv("LGBM_AMD_HOST_PREDICT");
+    if (e != nullptr && e[0] == '1') return false;
+    if (!cfg.predict_disable_shape_check && ncol != boosting_->MaxFeatureIdx() + 1) return false;  // host path reports it
+    std::lock_guard<std::mutex> l(mu_);
+    const bool raw = predict_type == C_API_PREDICT_RAW_SCORE;
+    if (!boosting_->PredictDenseOnDevice(data, data_type == C_API_DTYPE_FLOAT64, nrow, ncol, is_row_major != 0,
+                                         start_iteration, num_iteration, raw, out)) {
+      return false;
+    }
+    *out_len = static_cast<int64_t>(nrow) * boosting_->NumPredictOneRow(start_iteration, num_iteration, false, false);
+    return true;
   }
 
   void PredictFile(const char* data, int header, int predict_type, int start_iteration, int num_iteration,
@@ -1139,9 +1163,14 @@ int LGBM_BoosterPredictForMat(BoosterHandle handle, const void* data, int data_t
                               const char* parameter, int64_t* out_len, double* out_result) {
   API_BEGIN();
   Config cfg = ParamsToConfig(parameter);
+  Booster* b = static_cast<Booster*>(handle);
+  if (b->PredictDenseOnDevice(data, data_type, nrow, ncol, is_row_major, predict_type, start_iteration,
+                              num_iteration, cfg, out_result, out_len)) {
+    return 0;
+  }
   auto get = DenseRowPairFun(data, data_type, nrow, ncol, is_row_major);
-  static_cast<Booster*>(handle)->PredictRows([&get](int64_t r) { return get(static_cast<int>(r)); }, nrow, ncol,
-                                              predict_type, start_iteration, num_iteration, cfg, out_result, out_len);
+  b->PredictRows([&get](int64_t r) { return get(static_cast<int>(r)); }, nrow, ncol, predict_type, start_iteration,
+                 num_iteration, cfg, out_result, out_len);
   API_END();
 }
 

@@ -199,6 +199,32 @@ struct SampleArgs {
 int SampleBlocks(int64_t n);
 void SampleRows(const SampleArgs& s, hipStream_t st);
 
+// batch prediction of a flattened forest on raw feature values (row per thread)
+constexpr int kMaxPredClasses = 16;
+struct ForestArgs {
+  int32_t num_trees;
+  int32_t num_class;        // trees per iteration (<= kMaxPredClasses)
+  int32_t num_cols;
+  int32_t is_double;        // data: float64 (else float32)
+  int32_t row_major;
+  int64_t num_rows;
+  const void* data;
+  const int32_t* node_off;  // [num_trees + 1] first internal node of each tree
+  const int32_t* leaf_off;  // [num_trees] first leaf value of each tree
+  const int32_t* feature;   // [nodes] real feature index
+  const double* threshold;  // [nodes] (categorical: index into the tree's cat boundaries)
+  const int8_t* dtype;      // [nodes] decision type
+  const int32_t* left;      // [nodes] children, leaves as ~leaf
+  const int32_t* right;
+  const double* leaf_value;
+  const int32_t* cat_bound_off;  // [num_trees] offset of the tree's cat_boundaries
+  const int32_t* cat_bound;
+  const int32_t* cat_bits_off;   // [num_trees] offset of the tree's cat_threshold words
+  const uint32_t* cat_bits;
+  double* out;              // [num_rows][num_class] raw scores
+};
+void PredictForest(const ForestArgs& f, hipStream_t s);
+
 int GradientBlocks(int64_t n);
 // absmax[0..1] (and root = (sum g, sum h, n) if root_parts) from per-workgroup partials
 void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, uint32_t* absmax,

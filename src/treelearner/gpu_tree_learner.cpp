@@ -54,7 +54,10 @@ TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Conf
 GPUTreeLearner::GPUTreeLearner(const Config* config, bool data_parallel)
     : SerialTreeLearner(config), data_parallel_(data_parallel) {}
 
-GPUTreeLearner::~GPUTreeLearner() { FreeAll(); }
+GPUTreeLearner::~GPUTreeLearner() {
+  FreeAll();
+  for (void* p : valid_allocs_) (void)hipFree(p);
+}
 
 template <typename T>
 T* GPUTreeLearner::Alloc(size_t n) {
@@ -130,16 +133,9 @@ void GPUTreeLearner::UploadData() {
   const int wpr = std::max(1, (num_groups_ + gpw - 1) / gpw);
   const size_t row_bytes = static_cast<size_t>(wpr) * 4;
   // row-major bin matrix (the dataset stores columns)
-  std::vector<uint8_t> host(static_cast<size_t>(num_data_) * row_bytes, 0);
-#pragma omp parallel for schedule(static)
-  for (data_size_t r = 0; r < num_data_; ++r) {
-    uint8_t* row = host.data() + static_cast<size_t>(r) * row_bytes;
-    for (int g = 0; g < num_groups_; ++g) {
-      const uint32_t v = data_->group(g).Get(r);
-      if (bin_bytes == 1) row[g] = static_cast<uint8_t>(v);
-      else reinterpret_cast<uint16_t*>(row)[g] = static_cast<uint16_t>(v);
-    }
-  }
+  args_.bin_bytes = bin_bytes;
+  args_.words_per_row = wpr;
+  std::vector<uint8_t> host = RowMajorBins(data_);
   d_bins_ = Alloc<uint8_t>(host.size());
   HIPCHECK(hipMemcpy(d_bins_, host.data(), host.size(), hipMemcpyHostToDevice));
   std::vector<uint8_t>().swap(host);
@@ -870,6 +866,82 @@ void GPUTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
   SerialTreeLearner::RenewTreeOutput(tree, obj, residual, total_num_data, bag_indices, bag_cnt);
 }
 
+// ---------------------------------------------------------------- binned rows
+// row-major copy of a dataset's storage columns in this learner's layout (bin_bytes per
+// group, rows padded to whole 32-bit words)
+std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d) const {
+  const int bb = args_.bin_bytes;
+  const size_t row_bytes = static_cast<size_t>(args_.words_per_row) * 4;
+  const data_size_t n = d->num_data();
+  const int ng = d->num_groups();
+  std::vector<uint8_t> host(static_cast<size_t>(n) * row_bytes, 0);
+#pragma omp parallel for schedule(static)
+  for (data_size_t r = 0; r < n; ++r) {
+    uint8_t* row = host.data() + static_cast<size_t>(r) * row_bytes;
+    for (int g = 0; g < ng; ++g) {
+      const uint32_t v = d->group(g).Get(r);
+      if (bb == 1) row[g] = static_cast<uint8_t>(v);
+      else reinterpret_cast<uint16_t*>(row)[g] = static_cast<uint16_t>(v);
+    }
+  }
+  return host;
+}
+
+// ---------------------------------------------------------------- validation sets
+int GPUTreeLearner::AddValidData(const Dataset* valid, int ntpi, const double* scores) {
+  if (valid->num_groups() != num_groups_ || valid->num_total_bin() != data_->num_total_bin()) return -1;
+  for (int g = 0; g < num_groups_; ++g) {
+    if (valid->group_bin_boundary(g) != data_->group_bin_boundary(g) ||
+        valid->group(g).num_total_bin != data_->group(g).num_total_bin) {
+      return -1;
+    }
+  }
+  HIPCHECK(hipSetDevice(device_id_));
+  ValidSet vs;
+  vs.num_data = valid->num_data();
+  vs.ntpi = ntpi;
+  std::vector<uint8_t> host = RowMajorBins(valid);
+  HIPCHECK(hipMalloc(&vs.bins, std::max<size_t>(1, host.size())));
+  valid_allocs_.push_back(vs.bins);
+  HIPCHECK(hipMemcpy(vs.bins, host.data(), host.size(), hipMemcpyHostToDevice));
+  const size_t ns = static_cast<size_t>(vs.num_data) * ntpi;
+  HIPCHECK(hipMalloc(reinterpret_cast<void**>(&vs.score), std::max<size_t>(1, ns) * sizeof(double)));
+  valid_allocs_.push_back(vs.score);
+  HIPCHECK(hipMemcpy(vs.score, scores, ns * sizeof(double), hipMemcpyHostToDevice));
+  valid_.push_back(vs);
+  return static_cast<int>(valid_.size()) - 1;
+}
+
+void GPUTreeLearner::ValidAddConst(int slot, double v, int k) {
+  const ValidSet& vs = valid_[slot];
+  dev::AddConst(vs.score + static_cast<size_t>(k) * vs.num_data, vs.num_data, v, stream_);
+}
+
+void GPUTreeLearner::ValidMultiply(int slot, double v, int k) {
+  const ValidSet& vs = valid_[slot];
+  dev::MulConst(vs.score + static_cast<size_t>(k) * vs.num_data, vs.num_data, v, stream_);
+}
+
+void GPUTreeLearner::ValidAddTree(int slot, const Tree* tree, int k) {
+  const ValidSet& vs = valid_[slot];
+  double* score = vs.score + static_cast<size_t>(k) * vs.num_data;
+  if (tree->num_leaves() <= 1) {
+    dev::AddConst(score, vs.num_data, tree->LeafOutput(0), stream_);
+    return;
+  }
+  dev::DevTree t = StageTree(tree);
+  dev::KArgs a = args_;
+  a.bins = vs.bins;
+  dev::AddTreeScore(a, t, nullptr, vs.num_data, score, stream_);
+  HIPCHECK(hipStreamSynchronize(stream_));  // staging buffers are reused by the next tree
+}
+
+void GPUTreeLearner::ValidScoreToHost(int slot, double* host) {
+  const ValidSet& vs = valid_[slot];
+  HIPCHECK(hipMemcpyAsync(host, vs.score, sizeof(double) * vs.num_data * vs.ntpi, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+}
+
 // ---------------------------------------------------------------- scores & gradients
 void GPUTreeLearner::InitScores(int ntpi, const double* init_score) {
   HIPCHECK(hipSetDevice(device_id_));
@@ -934,15 +1006,8 @@ void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
   HIPCHECK(hipStreamSynchronize(stream_));
 }
 
-void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
-  // NOTE: called from AddTrainedTreeToScore for out-of-bag rows only (oob_cnt_ > 0 and the
-  // tree just trained), otherwise for every row
+dev::DevTree GPUTreeLearner::StageTree(const Tree* tree) {
   const int nl = tree->num_leaves();
-  double* score = d_score_ + static_cast<size_t>(k) * num_data_;
-  if (nl <= 1) {
-    AddConstToScore(tree->LeafOutput(0), k);
-    return;
-  }
   const int ni = nl - 1;
   const auto& cb = tree->cat_boundaries_inner();
   const auto& ct = tree->cat_threshold_inner();
@@ -958,24 +1023,24 @@ void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
     d_tree_bm_ = Alloc<unsigned long long>(4 * static_cast<size_t>(std::max(ni, config_->num_leaves)));
     d_tree_bm_meta_ = Alloc<int32_t>(3 * static_cast<size_t>(std::max(ni, config_->num_leaves)));
   }
-  std::vector<int32_t> i32(need_i32, 0);
-  std::vector<uint32_t> u32(need_u32, 0);
-  std::vector<int8_t> i8(ni);
-  std::vector<double> f64(nl);
+  stage_i32_.assign(need_i32, 0);
+  stage_u32_.assign(need_u32, 0);
+  stage_i8_.assign(std::max(1, ni), 0);
+  stage_f64_.assign(nl, 0.0);
   for (int j = 0; j < ni; ++j) {
-    i32[j] = tree->split_feature_inner(j);
-    i32[ni + j] = tree->left_child(j);
-    i32[2 * ni + j] = tree->right_child(j);
-    u32[j] = tree->threshold_in_bin(j);
-    i8[j] = tree->decision_type(j);
+    stage_i32_[j] = tree->split_feature_inner(j);
+    stage_i32_[ni + j] = tree->left_child(j);
+    stage_i32_[2 * ni + j] = tree->right_child(j);
+    stage_u32_[j] = tree->threshold_in_bin(j);
+    stage_i8_[j] = tree->decision_type(j);
   }
-  for (size_t j = 0; j < cb.size(); ++j) i32[3 * ni + j] = cb[j];
-  for (size_t j = 0; j < ct.size(); ++j) u32[ni + j] = ct[j];
-  for (int j = 0; j < nl; ++j) f64[j] = tree->LeafOutput(j);
-  HIPCHECK(hipMemcpyAsync(d_tree_i32_, i32.data(), sizeof(int32_t) * i32.size(), hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_tree_u32_, u32.data(), sizeof(uint32_t) * u32.size(), hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_tree_i8_, i8.data(), ni, hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_tree_f64_, f64.data(), sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
+  for (size_t j = 0; j < cb.size(); ++j) stage_i32_[3 * ni + j] = cb[j];
+  for (size_t j = 0; j < ct.size(); ++j) stage_u32_[ni + j] = ct[j];
+  for (int j = 0; j < nl; ++j) stage_f64_[j] = tree->LeafOutput(j);
+  HIPCHECK(hipMemcpyAsync(d_tree_i32_, stage_i32_.data(), sizeof(int32_t) * need_i32, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_tree_u32_, stage_u32_.data(), sizeof(uint32_t) * need_u32, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_tree_i8_, stage_i8_.data(), std::max(1, ni), hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_tree_f64_, stage_f64_.data(), sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
   dev::DevTree t;
   t.num_leaves = nl;
   t.split_feature_inner = d_tree_i32_;
@@ -988,13 +1053,25 @@ void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
   t.leaf_value = d_tree_f64_;
   t.bm_work = d_tree_bm_;
   t.bm_meta = d_tree_bm_meta_;
+  return t;
+}
+
+void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
+  // NOTE: called from AddTrainedTreeToScore for out-of-bag rows only (oob_cnt_ > 0 and the
+  // tree just trained), otherwise for every row
+  double* score = d_score_ + static_cast<size_t>(k) * num_data_;
+  if (tree->num_leaves() <= 1) {
+    AddConstToScore(tree->LeafOutput(0), k);
+    return;
+  }
+  dev::DevTree t = StageTree(tree);
   const bool oob_only = oob_cnt_ > 0 && in_trained_update_;
   if (oob_only) {
     dev::AddTreeScore(args_, t, d_oob_, oob_cnt_, score, stream_);
   } else {
     dev::AddTreeScore(args_, t, nullptr, num_data_, score, stream_);
   }
-  // host vectors must outlive the async copies
+  // the staging vectors must outlive the async copies
   HIPCHECK(hipStreamSynchronize(stream_));
 }
 

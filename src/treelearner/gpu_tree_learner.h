@@ -61,6 +61,11 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   score_t* device_gradients() override { return d_grad_; }
   score_t* device_hessians() override { return d_hess_; }
   void Synchronize() override;
+  int AddValidData(const Dataset* valid, int num_tree_per_iteration, const double* scores) override;
+  void ValidAddConst(int slot, double v, int tree_id) override;
+  void ValidMultiply(int slot, double v, int tree_id) override;
+  void ValidAddTree(int slot, const Tree* tree, int tree_id) override;
+  void ValidScoreToHost(int slot, double* host) override;
 
   bool device_mode() const { return device_mode_; }
 
@@ -90,6 +95,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void AllreduceRoot();
   void AllreduceAbsMax();
   void UploadRankTables(const DeviceRankSpec& r, DeviceGradKind kind);
+  // tree records for the traversal kernels (staged in d_tree_*; the host vectors must stay
+  // alive until the stream is synchronised)
+  dev::DevTree StageTree(const Tree* tree);
+  std::vector<uint8_t> RowMajorBins(const Dataset* d) const;
   template <typename T>
   T* Alloc(size_t n);
 
@@ -162,6 +171,19 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int32_t* d_sample_off_ = nullptr;
   int32_t* d_bag_count_ = nullptr;  // in-bag rows of the current bag (read by the root kernels)
   bool sample_seeded_ = false;
+  // validation sets on the device (own allocations: they survive ResetTrainingData)
+  struct ValidSet {
+    void* bins = nullptr;
+    double* score = nullptr;
+    data_size_t num_data = 0;
+    int ntpi = 1;
+  };
+  std::vector<ValidSet> valid_;
+  std::vector<void*> valid_allocs_;
+  std::vector<int32_t> stage_i32_;
+  std::vector<uint32_t> stage_u32_;
+  std::vector<int8_t> stage_i8_;
+  std::vector<double> stage_f64_;
   // tree upload staging for traversal
   int32_t* d_tree_i32_ = nullptr;
   uint32_t* d_tree_u32_ = nullptr;

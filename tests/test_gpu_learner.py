@@ -240,3 +240,54 @@ def test_categorical_splits_on_device(gpu_available):
     assert any(t["num_cat"] > 0 for t in models["gpu"].dump_model()["tree_info"])
     auc_c, auc_g = _auc(y, models["cpu"].predict(X)), _auc(y, models["gpu"].predict(X))
     assert auc_g > 0.85 and abs(auc_c - auc_g) < 2e-3
+
+
+def test_validation_scores_on_device(gpu_available):
+    """Validation sets are scored on the device (one traversal kernel per tree): the recorded
+    metric equals the metric of the booster's own predictions, and early stopping works."""
+    X, y = _data(40000, seed=21)
+    Xv, yv = _data(15000, seed=22)
+    params = {"objective": "binary", "metric": ["binary_logloss", "auc"], "num_leaves": 31, "max_bin": 63,
+              "verbose": -1, "device_type": "gpu", "bagging_fraction": 0.8, "bagging_freq": 1}
+    ds = lgb.Dataset(X, y, params=params)
+    dv = lgb.Dataset(Xv, yv, reference=ds)
+    rec = {}
+    b = lgb.train(params, ds, 40, valid_sets=[dv], valid_names=["v"], evals_result=rec, verbose_eval=False,
+                  early_stopping_rounds=5)
+    p = b.predict(Xv, num_iteration=b.best_iteration)
+    ll = -np.mean(yv * np.log(p) + (1 - yv) * np.log(1 - p))
+    assert rec["v"]["binary_logloss"][b.best_iteration - 1] == pytest.approx(ll, rel=1e-6)
+    assert rec["v"]["auc"][b.best_iteration - 1] == pytest.approx(_auc(yv, p), abs=1e-6)
+
+
+@pytest.mark.parametrize("kind", ["binary_nan", "categorical", "multiclass"])
+def test_device_batch_prediction_matches_host(gpu_available, kind, monkeypatch):
+    """LGBM_BoosterPredictForMat on the device forest kernel == the host predictor, bit for bit."""
+    if kind == "binary_nan":
+        X, y = _data(30000, seed=31)
+        params = {"objective": "binary"}
+        cats = "auto"
+    elif kind == "categorical":
+        X, y = _cat_data(30000, seed=32)
+        params = {"objective": "binary"}
+        cats = [0, 1]
+    else:
+        rng = np.random.RandomState(33)
+        X = rng.randn(30000, 8).astype(np.float32)
+        y = np.argmax(X[:, :3] + 0.3 * rng.randn(30000, 3), axis=1).astype(np.float32)
+        params = {"objective": "multiclass", "num_class": 3}
+        cats = "auto"
+    params.update({"num_leaves": 31, "verbose": -1, "device_type": "gpu"})
+    b = lgb.train(params, lgb.Dataset(X, y, params=params, categorical_feature=cats), 25, verbose_eval=False)
+    for data in (X, X.astype(np.float64)):
+        for raw in (False, True):
+            monkeypatch.delenv("LGBM_AMD_HOST_PREDICT", raising=False)
+            dev = b.predict(data, raw_score=raw)
+            monkeypatch.setenv("LGBM_AMD_HOST_PREDICT", "1")
+            host = b.predict(data, raw_score=raw)
+            np.testing.assert_array_equal(dev, host)
+    # an iteration window
+    monkeypatch.delenv("LGBM_AMD_HOST_PREDICT", raising=False)
+    dev = b.predict(X, num_iteration=10, start_iteration=5)
+    monkeypatch.setenv("LGBM_AMD_HOST_PREDICT", "1")
+    np.testing.assert_array_equal(dev, b.predict(X, num_iteration=10, start_iteration=5))
