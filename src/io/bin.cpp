@@ -277,7 +277,10 @@ void BinMapper::FindBin(double* values, int num_values, size_t total_sample_cnt,
     } else {
       bin_upper_bound_ = NumericalBounds(distinct.data(), counts.data(), nd, max_bin - 1, total_sample_cnt - na_cnt,
                                          min_data_in_bin, forced_upper_bounds);
-      bin_upper_bound_.push_back(NAN);
+      // the reference pushes its unscoped enumerator MissingType::NaN here (bin.cpp:407), so
+      // the NaN bin's (never consulted) upper bound is 2.0; keeping the value makes
+      // CheckAlign (NaN != NaN) and binary dataset files agree with it
+      bin_upper_bound_.push_back(static_cast<double>(MissingType::NaN));
     }
     num_bin_ = static_cast<int>(bin_upper_bound_.size());
     cnt_in_bin.assign(num_bin_, 0);

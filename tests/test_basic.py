@@ -179,3 +179,23 @@ def test_get_split_value_histogram():
     hist, edges = bst.get_split_value_histogram(feat)
     assert hist.sum() == bst.feature_importance()[feat]
     assert len(edges) == len(hist) + 1
+
+
+def test_validation_set_with_nan_feature_aligns():
+    """A validation set built by reference from data with NaN-missing features keeps the
+    training bin mappers (regression: the NaN bin's upper bound compared unequal to itself)."""
+    rng = np.random.RandomState(0)
+    X = rng.randn(3000, 4)
+    X[rng.rand(3000) < 0.1, 1] = np.nan
+    y = (X[:, 0] > 0).astype(float)
+    Xv = rng.randn(800, 4)
+    Xv[rng.rand(800) < 0.1, 1] = np.nan
+    yv = (Xv[:, 0] > 0).astype(float)
+    params = {"objective": "binary", "verbose": -1, "metric": "binary_logloss"}
+    ds = lgb.Dataset(X, y, params=params)
+    rec = {}
+    b = lgb.train(params, ds, 5, valid_sets=[lgb.Dataset(Xv, yv, reference=ds)], valid_names=["v"],
+                  evals_result=rec, verbose_eval=False)
+    p = b.predict(Xv)
+    ll = -np.mean(yv * np.log(p) + (1 - yv) * np.log(1 - p))
+    assert rec["v"]["binary_logloss"][-1] == pytest.approx(ll, rel=1e-9)
