@@ -119,10 +119,11 @@ __device__ __forceinline__ long long* StepScratch(const KArgs& a, int parity) {
   return a.scratch + static_cast<size_t>(parity & 1) * 2 * a.p.total_bins;
 }
 
-// a step histogram with this many row blocks is summed by the split scan itself (the
+// a step histogram with this many row blocks -- or any step from split direct_from_split
+// on, whose tree graph has no reduce kernel -- is summed by the split scan itself (the
 // reduce kernel skips it); data-parallel training always reduces (the all-reduce needs it)
-__device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk) {
-  return !a.p.data_parallel && nblk <= kReduceChunk;
+__device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk, int split) {
+  return !a.p.data_parallel && (nblk <= kReduceChunk || split >= a.p.direct_from_split);
 }
 
 // outcome of the step's partition, derived from Step::cs and the final cursors (every

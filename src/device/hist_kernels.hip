@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
   const int32_t* src;
   if (!HistRows<MODE>(a, true, &begin, &count, &src)) return;
   const int nblk = HistBlocksFor(count, a.hist_max_blocks, a.hist_rows_cap);
-  if (MODE == 1 && DirectPartials(a, nblk)) {  // summed by the split scan
+  if (MODE == 1 && DirectPartials(a, nblk, a.st->cs.s)) {  // summed by the split scan
     KTrace(a, ts, kTrRedExit);
     return;
   }
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
 }
 
 template <int MODE>
-static void LaunchHistMode(const KArgs& a, int grid_x, hipStream_t s) {
+static void LaunchHistMode(const KArgs& a, int grid_x, hipStream_t s, bool reduce = true) {
   const size_t lds_bytes = sizeof(unsigned long long) * static_cast<size_t>(a.tile_bins);
   dim3 grid(grid_x, a.hist_tiles);
   if (a.bin_bytes == 1) {
@@ -329,6 +329,7 @@ static void LaunchHistMode(const KArgs& a, int grid_x, hipStream_t s) {
   } else {
     hipLaunchKernelGGL((k_hist<MODE, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
   }
+  if (!reduce) return;
   dim3 rgrid((a.p.total_bins + 255) / 256, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk);
   hipLaunchKernelGGL(k_hist_reduce<MODE>, rgrid, dim3(256), 0, s, a);
 }
@@ -336,7 +337,9 @@ static void LaunchHistMode(const KArgs& a, int grid_x, hipStream_t s) {
 // the root fills the chip (two workgroups per CU); a step's leaf is usually small, and
 // dispatching workgroups that exit at once is not free (~3 us for 512 x 1024 threads)
 void HistRoot(const KArgs& a, hipStream_t s) { LaunchHistMode<0>(a, a.hist_max_blocks, s); }
-void HistStep(const KArgs& a, hipStream_t s) { LaunchHistMode<1>(a, std::min(a.hist_max_blocks, NumCUs()), s); }
+void HistStep(const KArgs& a, hipStream_t s, bool reduce) {
+  LaunchHistMode<1>(a, std::min(a.hist_max_blocks, NumCUs()), s, reduce);
+}
 void HistRange(const KArgs& a, hipStream_t s) { LaunchHistMode<2>(a, a.hist_max_blocks, s); }
 
 }  // namespace dev

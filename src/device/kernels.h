@@ -96,7 +96,8 @@ void RootSum(const KArgs& a, hipStream_t s);
 // histograms: per-workgroup packed partials, then an exact int64 reduction into the
 // step's scratch buffer (root: buffer 0; step: parity of Step::step; range: buffer 0)
 void HistRoot(const KArgs& a, hipStream_t s);
-void HistStep(const KArgs& a, hipStream_t s);
+// reduce=false: no reduce kernel (only for splits >= Params::direct_from_split)
+void HistStep(const KArgs& a, hipStream_t s, bool reduce = true);
 void HistRange(const KArgs& a, hipStream_t s);  // rows idx[range_begin, +num_rows)
 // split scans of the root / the two children of the step (per-feature results)
 void FindRoot(const KArgs& a, hipStream_t s);

@@ -566,6 +566,12 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   int parity = 0, nblk_direct = -1;
   if (!ROOT) {
     if (done) return;
+    if (f == 0 && side == 0 && tid == 0) {
+      // the partition cursors were final for the histogram kernel: reset for the next split
+      // (the reduce kernel, not launched for late splits, used to do it)
+      a.st->cur_left = 0;
+      a.st->cur_right = 0;
+    }
     parity = (s + 1) & 1;
     // zero this feature's bins of the buffer the next step reduces into
     if (side == 0) {
@@ -575,7 +581,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     if (skip) return;
     KTraceAt(a, s, kTrFindEntry, t_entry);
     const int nblk = HistBlocksFor(s_count, a.hist_max_blocks, a.hist_rows_cap);
-    if (DirectPartials(a, nblk)) nblk_direct = nblk;
+    if (DirectPartials(a, nblk, s)) nblk_direct = nblk;
   }
   const SplitParams& p = a.p.sp;
   LeafCtx L;
@@ -643,14 +649,17 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
       long long g = 0, h = 0;
       if (nblk_direct >= 0) {
         // small leaf: sum the few per-workgroup partials here (k_hist_reduce skipped them)
-        unsigned long long v[kReduceChunk];
+        // chunks of kReduceChunk independent loads in flight
+        for (int k0 = 0; k0 < nblk_direct; k0 += kReduceChunk) {
+          unsigned long long v[kReduceChunk];
 #pragma unroll
-        for (int k = 0; k < kReduceChunk; ++k)
-          v[k] = k < nblk_direct ? part[static_cast<size_t>(k) * a.p.total_bins + i] : 0ull;
+          for (int k = 0; k < kReduceChunk; ++k)
+            v[k] = k0 + k < nblk_direct ? part[static_cast<size_t>(k0 + k) * a.p.total_bins + i] : 0ull;
 #pragma unroll
-        for (int k = 0; k < kReduceChunk; ++k) {
-          g += static_cast<long long>(v[k]) >> 32;
-          h += static_cast<long long>(v[k] & 0xffffffffull);
+          for (int k = 0; k < kReduceChunk; ++k) {
+            g += static_cast<long long>(v[k]) >> 32;
+            h += static_cast<long long>(v[k] & 0xffffffffull);
+          }
         }
       } else {
         g = src[2 * i];

@@ -298,6 +298,10 @@ void GPUTreeLearner::UploadData() {
   int max_fb = 1;
   for (const auto& F : feats) max_fb = std::max(max_fb, F.num_bin - F.offset);
   a.p.max_feature_bins = max_fb;
+  // from this split on the tree's graph has no reduce kernel: smaller children are small
+  // enough for the split scan to sum their partial histograms (LGBM_AMD_DIRECT_FROM_SPLIT)
+  a.p.direct_from_split = 8;
+  if (const char* e = std::getenv("LGBM_AMD_DIRECT_FROM_SPLIT")) a.p.direct_from_split = std::atoi(e);
   a.p.has_cat = 0;
   for (const auto& F : feats) a.p.has_cat |= F.is_cat;
   // per-workgroup row cap of the histogram kernels (fixed-point headroom): see k_hist
@@ -476,7 +480,9 @@ void GPUTreeLearner::KernelFloorProbe(const dev::KArgs& a) {
     const char* name;
     void (*fn)(const dev::KArgs&, hipStream_t);
   };
-  const P probes[] = {{"partition", dev::Partition}, {"hist+reduce", dev::HistStep}, {"find", dev::FindStep}};
+  const P probes[] = {{"partition", dev::Partition},
+                      {"hist+reduce", [](const dev::KArgs& k, hipStream_t st) { dev::HistStep(k, st, true); }},
+                      {"find", dev::FindStep}};
   for (const P& p : probes) {
     for (int i = 0; i < 20; ++i) p.fn(a, stream_);
     HIPCHECK(hipEventRecord(e0, stream_));
@@ -580,7 +586,7 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   // at once.
   for (int s = 0; s < config_->num_leaves - 1; ++s) {
     dev::Partition(a, stream_);
-    dev::HistStep(a, stream_);
+    dev::HistStep(a, stream_, s < a.p.direct_from_split);
     AllreduceScratch(s + 1);  // the step's buffer parity
     dev::FindStep(a, stream_);
   }
