@@ -300,7 +300,7 @@ void GPUTreeLearner::UploadData() {
   a.p.max_feature_bins = max_fb;
   // from this split on the tree's graph has no reduce kernel: smaller children are small
   // enough for the split scan to sum their partial histograms (LGBM_AMD_DIRECT_FROM_SPLIT)
-  a.p.direct_from_split = 8;
+  a.p.direct_from_split = 16;
   if (const char* e = std::getenv("LGBM_AMD_DIRECT_FROM_SPLIT")) a.p.direct_from_split = std::atoi(e);
   a.p.has_cat = 0;
   for (const auto& F : feats) a.p.has_cat |= F.is_cat;
