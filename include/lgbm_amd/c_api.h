@@ -211,6 +211,13 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_RcclSelfTest(int* out_ok);
 // the same all-reduces captured into a hipGraph and replayed (the device learner's tree graph)
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclGraphSelfTest(int* out_ok);
 /* number of visible GPUs (0 without a device) */
+/* in-process ranks for tests: a hub of thread transports (timeout_s > 0 bounds every
+ * collective; fail_rank / fail_at_call inject a fault); each rank's thread then joins it
+ * and trains as that rank (Network state is thread-local) */
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkCreateThreadHub(int num_ranks, double timeout_s, int fail_rank,
+                                                      int fail_at_call, void** out);
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkJoinThreadHub(void* hub, int rank);
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkFreeThreadHub(void* hub);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceSynchronize();
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCount(int* out);
 /* phase timers (LGBM_AMD_TIMETAG) as "name=seconds;..." */

@@ -66,6 +66,13 @@ class DeviceComm {
   virtual void Allgather(const void* send, void* recv, size_t bytes_per_rank, void* stream) = 0;
   virtual void ReduceScatterSumF64(const double* send, double* recv, size_t recv_count, void* stream) = 0;
   virtual void Broadcast(void* buf, size_t bytes, int root, void* stream) = 0;
+  // failure detection (watchdog of the device learner): an asynchronous communicator error,
+  // and aborting every pending collective so that no rank stays blocked
+  virtual bool AsyncError(std::string* msg) {
+    (void)msg;
+    return false;
+  }
+  virtual void Abort() {}
 };
 
 class Network {
@@ -146,7 +153,10 @@ class Network {
   }
 };
 
-// in-process multi-rank transport (ranks are threads sharing a rendezvous object)
-std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks);
+// in-process multi-rank transport (ranks are threads sharing a rendezvous object).
+// timeout_s > 0: a collective waiting longer raises; fail_rank / fail_at_call inject a fault
+// (that rank raises at its fail_at_call-th collective, its peers then raise too)
+std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks, double timeout_s = 0,
+                                                                 int fail_rank = -1, int fail_at_call = 0);
 
 }  // namespace lgbm_amd

@@ -1,0 +1,76 @@
+"""In-process ranks: several training ranks as threads of one process.
+
+The native Network state is thread-local (as the reference's THREAD_LOCAL network,
+src/network/network.cpp:17-27), so each thread can join a shared hub of thread transports
+and train as one rank of a data- / feature- / voting-parallel job -- no sockets, no extra
+processes.  The hub bounds every collective with a timeout and can inject a fault into
+one rank: the failing rank raises, its peers raise "peer rank failed" instead of hanging
+(the fault-injecting fake backend of SURVEY.md §5.3).
+
+    ranks = ThreadRanks(world=2, timeout_s=30)
+    results = ranks.run(lambda rank: train_my_shard(rank))
+"""
+import ctypes
+import threading
+
+from ..basic import _load_lib, _safe_call
+
+
+class RankResult:
+    """Outcome of one rank: `value` if it returned, `error` (the exception) if it raised."""
+
+    def __init__(self, rank, value=None, error=None):
+        self.rank = rank
+        self.value = value
+        self.error = error
+
+    @property
+    def ok(self):
+        return self.error is None
+
+
+class ThreadRanks:
+    def __init__(self, world, timeout_s=0.0, fail_rank=-1, fail_at_call=0):
+        self.world = int(world)
+        self._hub = ctypes.c_void_p()
+        _safe_call(_load_lib().LGBM_AMD_NetworkCreateThreadHub(
+            ctypes.c_int(self.world), ctypes.c_double(timeout_s), ctypes.c_int(fail_rank),
+            ctypes.c_int(fail_at_call), ctypes.byref(self._hub)))
+
+    def run(self, fn):
+        """Call fn(rank) in one thread per rank (joined to the hub); returns [RankResult]."""
+        results = [None] * self.world
+        lib = _load_lib()
+
+        def body(rank):
+            try:
+                _safe_call(lib.LGBM_AMD_NetworkJoinThreadHub(self._hub, ctypes.c_int(rank)))
+                results[rank] = RankResult(rank, value=fn(rank))
+            except Exception as e:  # noqa: BLE001 -- reported per rank
+                results[rank] = RankResult(rank, error=e)
+            finally:
+                lib.LGBM_NetworkFree()
+
+        threads = [threading.Thread(target=body, args=(r,), daemon=True) for r in range(self.world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+        return results
+
+    def close(self):
+        if self._hub:
+            _load_lib().LGBM_AMD_NetworkFreeThreadHub(self._hub)
+            self._hub = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass

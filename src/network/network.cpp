@@ -3,8 +3,11 @@
 // collectives built on a pluggable HostTransport.
 #include "lgbm_amd/network.h"
 
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
+#include <stdexcept>
+#include <string>
 
 #include "lgbm_amd/common.h"
 #include "lgbm_amd/log.h"
@@ -55,30 +58,41 @@ class ExternalFnTransport : public HostTransport {
   AllgatherFunctionPtr ag_;
 };
 
-// threads-as-ranks rendezvous
+// threads-as-ranks rendezvous.  A rank that fails (an exception inside a collective, or
+// an injected fault) poisons the hub, so its peers raise instead of waiting forever; a
+// rank that never arrives is detected by the per-collective timeout.  This is the
+// in-process fake backend of SURVEY.md §5.3 (the reference only has socket timeouts).
 struct ThreadHub {
-  explicit ThreadHub(int n) : n(n), bufs(n), lens(n) {}
+  ThreadHub(int n, double timeout_s) : n(n), timeout_s(timeout_s), bufs(n), lens(n) {}
   int n;
+  double timeout_s;
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
   int generation = 0;
   int readers_done = 0;
+  bool failed = false;
+  std::string failure;
   std::vector<const char*> bufs;
   std::vector<comm_size_t> lens;
 };
 
 class ThreadTransport : public HostTransport {
  public:
-  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  ThreadTransport(std::shared_ptr<ThreadHub> hub, int rank, int fail_at_call)
+      : hub_(std::move(hub)), rank_(rank), fail_at_call_(fail_at_call) {}
   int rank() const override { return rank_; }
   int num_machines() const override { return hub_->n; }
   void Allgather(const char* input, comm_size_t input_size, const comm_size_t* block_start,
                  const comm_size_t* block_len, char* output, comm_size_t output_size) override {
     (void)output_size;
+    ++calls_;
     std::unique_lock<std::mutex> lk(hub_->mu);
+    if (fail_at_call_ > 0 && calls_ == fail_at_call_) {
+      Poison(&lk, "injected fault in rank " + std::to_string(rank_) + " at collective call " + std::to_string(calls_));
+    }
     // wait until the previous round's readers are done
-    hub_->cv.wait(lk, [&] { return hub_->readers_done == 0 || hub_->readers_done == hub_->n; });
+    Wait(&lk, [&] { return hub_->readers_done == 0 || hub_->readers_done == hub_->n; });
     if (hub_->readers_done == hub_->n) hub_->readers_done = 0;
     const int gen = hub_->generation;
     hub_->bufs[rank_] = input;
@@ -88,7 +102,7 @@ class ThreadTransport : public HostTransport {
       hub_->generation++;
       hub_->cv.notify_all();
     } else {
-      hub_->cv.wait(lk, [&] { return hub_->generation != gen; });
+      Wait(&lk, [&] { return hub_->generation != gen; });
     }
     lk.unlock();
     for (int r = 0; r < hub_->n; ++r) std::memcpy(output + block_start[r], hub_->bufs[r], block_len[r]);
@@ -96,20 +110,54 @@ class ThreadTransport : public HostTransport {
     hub_->readers_done++;
     hub_->cv.notify_all();
     // keep inputs alive until everyone has copied
-    hub_->cv.wait(lk, [&] { return hub_->readers_done == hub_->n || hub_->readers_done == 0; });
+    Wait(&lk, [&] { return hub_->readers_done == hub_->n || hub_->readers_done == 0; });
   }
 
  private:
+  [[noreturn]] void Poison(std::unique_lock<std::mutex>* lk, const std::string& why) {
+    if (!hub_->failed) {
+      hub_->failed = true;
+      hub_->failure = why;
+    }
+    hub_->cv.notify_all();
+    lk->unlock();
+    Log::Fatal("%s", why.c_str());
+    throw std::runtime_error(why);  // not reached
+  }
+  template <typename Pred>
+  void Wait(std::unique_lock<std::mutex>* lk, Pred ready) {
+    auto ok = [&] { return hub_->failed || ready(); };
+    if (hub_->timeout_s > 0) {
+      const auto limit = std::chrono::duration<double>(hub_->timeout_s);
+      if (!hub_->cv.wait_for(*lk, limit, ok)) {
+        Poison(lk, "collective timed out after " + std::to_string(hub_->timeout_s) + " s in rank " +
+                       std::to_string(rank_) + " (a peer rank did not arrive)");
+      }
+    } else {
+      hub_->cv.wait(*lk, ok);
+    }
+    if (hub_->failed) {
+      const std::string why = hub_->failure;
+      lk->unlock();
+      Log::Fatal("peer rank failed: %s", why.c_str());
+    }
+  }
+
   std::shared_ptr<ThreadHub> hub_;
   int rank_;
+  int fail_at_call_;
+  int calls_ = 0;
 };
 
 }  // namespace
 
-std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks) {
-  auto hub = std::make_shared<ThreadHub>(num_ranks);
+std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks, double timeout_s, int fail_rank,
+                                                                 int fail_at_call) {
+  auto hub = std::make_shared<ThreadHub>(num_ranks, timeout_s);
   std::vector<std::shared_ptr<HostTransport>> out;
-  for (int r = 0; r < num_ranks; ++r) out.push_back(std::make_shared<ThreadTransport>(hub, r));
+  for (int r = 0; r < num_ranks; ++r) {
+    out.push_back(std::make_shared<ThreadTransport>(hub, r, r == fail_rank ? fail_at_call : 0));
+  }
   return out;
 }
 

@@ -59,6 +59,17 @@ class RcclComm : public DeviceComm {
   void Broadcast(void* buf, size_t bytes, int root, void* stream) override {
     RCCLCHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, static_cast<hipStream_t>(stream)));
   }
+  bool AsyncError(std::string* msg) override {
+    ncclResult_t r = ncclSuccess;
+    if (comm_ == nullptr || ncclCommGetAsyncError(comm_, &r) != ncclSuccess) return false;
+    if (r == ncclSuccess || r == ncclInProgress) return false;
+    *msg = ncclGetErrorString(r);
+    return true;
+  }
+  void Abort() override {
+    if (comm_ != nullptr) (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
 
  private:
   ncclComm_t comm_ = nullptr;

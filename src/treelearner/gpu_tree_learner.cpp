@@ -6,10 +6,12 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 #include "lgbm_amd/common.h"
 #include "lgbm_amd/dcg.h"
@@ -425,6 +427,36 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   return SerialTreeLearner::Train(gradients, hessians);
 }
 
+// wait for the tree; with device collectives, poll the communicator for asynchronous
+// errors and bound the wait by time_out minutes (the reference's socket timeout): a failed
+// or vanished peer aborts the communicator and raises instead of hanging every rank
+void GPUTreeLearner::WatchdogSync() {
+  DeviceComm* dc = (data_parallel_ && Network::num_machines() > 1) ? Network::device_comm() : nullptr;
+  if (dc == nullptr) {
+    HIPCHECK(hipStreamSynchronize(stream_));
+    return;
+  }
+  const double limit_s = 60.0 * std::max(1, config_->time_out);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(stream_);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) HIPCHECK(q);
+    std::string err;
+    if (dc->AsyncError(&err)) {
+      dc->Abort();
+      Log::Fatal("device collective failed during tree growth: %s", err.c_str());
+    }
+    const double el = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (el > limit_s) {
+      dc->Abort();
+      Log::Fatal("device collectives timed out after %.0f s (time_out=%d min): a peer rank stopped", el,
+                 config_->time_out);
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 void GPUTreeLearner::AllreduceRoot() {
   if (!data_parallel_ || Network::num_machines() <= 1) return;
   DeviceComm* dc = Network::device_comm();
@@ -659,7 +691,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
                           hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
+  WatchdogSync();
   const int num_splits = h_step_->nsplit;
   if (a.ktrace != nullptr) ReportKernelTrace(num_splits);
   if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {

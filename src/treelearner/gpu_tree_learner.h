@@ -93,6 +93,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void DownloadPartitionToHost() const;
   void AllreduceScratch(int parity);
   void AllreduceRoot();
+  void WatchdogSync();
   void AllreduceAbsMax();
   void UploadRankTables(const DeviceRankSpec& r, DeviceGradKind kind);
   // tree records for the traversal kernels (staged in d_tree_*; the host vectors must stay

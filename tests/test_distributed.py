@@ -111,3 +111,49 @@ def test_device_voting_parallel_two_ranks_one_gpu(tmp_path, gpu_available):
     cpu_dir.mkdir()
     _, cpu_preds = _run("voting", cpu_dir, device="cpu")
     assert abs(auc - roc_auc_score(y, cpu_preds[0])) < 0.01
+
+
+def _thread_rank_train(rank, world=2, learner="data", rounds=10):
+    X, y = make_data()
+    idx = np.arange(rank, X.shape[0], world)
+    params = {"objective": "binary", "num_leaves": 15, "verbose": -1, "tree_learner": learner,
+              "num_machines": world, "pre_partition": True, "min_data_in_leaf": 20, "seed": 3,
+              "deterministic": True, "num_threads": 2}
+    if learner == "voting":
+        params["top_k"] = 5
+    ds = lgb.Dataset(X[idx], y[idx], params=params)
+    return lgb.train(params, ds, rounds).model_to_string()
+
+
+@pytest.mark.parametrize("learner", ["data", "voting"])
+def test_thread_ranks_in_one_process(learner):
+    """Ranks as threads of one process (in-process transport): ranks build identical models."""
+    from lightgbmv1_amd.parallel.inproc import ThreadRanks
+    with ThreadRanks(2, timeout_s=60) as tr:
+        res = tr.run(lambda r: _thread_rank_train(r, learner=learner))
+    assert all(r.ok for r in res), [str(r.error) for r in res]
+    assert _trees(res[0].value) == _trees(res[1].value)
+
+
+def test_injected_fault_fails_every_rank_promptly():
+    """A fault injected into rank 1's 4th collective: rank 1 raises it, rank 0 raises
+    'peer rank failed' instead of hanging."""
+    import time
+    from lightgbmv1_amd.parallel.inproc import ThreadRanks
+    t0 = time.time()
+    with ThreadRanks(2, timeout_s=60, fail_rank=1, fail_at_call=4) as tr:
+        res = tr.run(lambda r: _thread_rank_train(r))
+    assert time.time() - t0 < 30
+    assert not res[1].ok and "injected fault" in str(res[1].error)
+    assert not res[0].ok and "peer rank failed" in str(res[0].error)
+
+
+def test_collective_timeout_when_a_rank_never_arrives():
+    import time
+    from lightgbmv1_amd.parallel.inproc import ThreadRanks
+    t0 = time.time()
+    with ThreadRanks(2, timeout_s=2.0) as tr:
+        res = tr.run(lambda r: _thread_rank_train(r) if r == 0 else None)
+    assert time.time() - t0 < 30
+    assert not res[0].ok and "timed out" in str(res[0].error)
+    assert res[1].ok
