@@ -41,7 +41,24 @@ $(LIB): $(HOST_OBJS) $(DEV_OBJS)
 $(CLI): src/cli/main.cpp $(LIB)
 	$(CXX) $(CXXFLAGS) -o $@ src/cli/main.cpp -L$(LIBDIR) -l_lightgbmv1_amd -Wl,-rpath,'$$ORIGIN' -fopenmp
 
-clean:
-	rm -rf $(BUILD) $(LIB) $(CLI)
+# host-code sanitizer build (AddressSanitizer + UndefinedBehaviorSanitizer): the CLI linked
+# from ASan/UBSan-instrumented host objects and the regular gfx950 device objects.  Device
+# code is never instrumented (GPU sanitizers are not used on this platform); the CPU learner
+# paths run fully instrumented:  make sanitize && build_asan/lightgbm config=...
+ASAN_FLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
+ASAN_OBJS := $(patsubst src/%.cpp,build_asan/%.o,$(HOST_SRCS))
 
-.PHONY: all clean
+build_asan/%.o: src/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(filter-out -O3,$(CXXFLAGS)) $(ASAN_FLAGS) -c $< -o $@
+
+build_asan/lightgbm: $(ASAN_OBJS) $(DEV_OBJS) src/cli/main.cpp
+	$(CXX) $(filter-out -O3,$(CXXFLAGS)) $(ASAN_FLAGS) -o $@ src/cli/main.cpp $(ASAN_OBJS) $(DEV_OBJS) \
+	  -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
+
+sanitize: build_asan/lightgbm
+
+clean:
+	rm -rf $(BUILD) build_asan $(LIB) $(CLI)
+
+.PHONY: all clean sanitize

@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <cctype>
+#include <dlfcn.h>
+
 #include <chrono>
 #include <cmath>
 #include <cstdint>
@@ -378,12 +380,39 @@ class PhaseTimer {
   std::map<std::string, long> cnt_;
 };
 
+// roctx ranges under LGBM_AMD_ROCTX=1 (libroctx64 loaded at run time, so the library has no
+// link dependency on it): the same scope names as the reference's TIMETAG scopes, visible
+// in `rocprofv3 --marker-trace` next to the kernels they launch
+struct Roctx {
+  using Push = int (*)(const char*);
+  using Pop = int (*)();
+  Push push = nullptr;
+  Pop pop = nullptr;
+  static const Roctx& Get() {
+    static const Roctx r = [] {
+      Roctx x;
+      const char* e = getenv("LGBM_AMD_ROCTX");
+      if (e == nullptr || e[0] != '1') return x;
+      void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+      if (h == nullptr) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
+      if (h == nullptr) return x;
+      x.push = reinterpret_cast<Push>(dlsym(h, "roctxRangePushA"));
+      x.pop = reinterpret_cast<Pop>(dlsym(h, "roctxRangePop"));
+      if (x.push == nullptr || x.pop == nullptr) x.push = nullptr;
+      return x;
+    }();
+    return r;
+  }
+};
+
 class ScopedTimer {
  public:
   explicit ScopedTimer(const char* name) : name_(name) {
     if (PhaseTimer::Global().enabled()) start_ = std::chrono::steady_clock::now();
+    if (Roctx::Get().push != nullptr) Roctx::Get().push(name);
   }
   ~ScopedTimer() {
+    if (Roctx::Get().push != nullptr) Roctx::Get().pop();
     if (PhaseTimer::Global().enabled()) {
       auto d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - start_).count();
       PhaseTimer::Global().Add(name_, d);
