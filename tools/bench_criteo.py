@@ -1,0 +1,92 @@
+"""BASELINE.json config #5 proxy: Criteo-shaped sparse CTR data (67 count-encoded features,
+most of them sparse, bundled by EFB) at 100M rows per GPU, 255 leaves.
+
+The reference's distributed experiment (docs/Experiments.rst:188-242) trains Criteo
+1.7B x 67 with 255 leaves: 627.8 s per tree on one machine, 80 s on 8, 42 s on 16.  A
+1B-row job on 8 MI355X is 125M rows per GPU; this script measures the per-tree time of
+one GPU on a 100M-row shard of that shape (the multi-GPU run adds one histogram
+all-reduce per split on top).  Synthetic data: 13 dense heavy-tailed counts + 54 sparse
+count features (97-99.5% zeros), ~3.4% positives.
+
+  python tools/bench_criteo.py --rows 100000000 --steps 10 --warmup 2
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+REF_SEC_PER_TREE_1_MACHINE = 627.8   # 1.7B rows, 1 machine (docs/Experiments.rst:231)
+REF_SEC_PER_TREE_8_MACHINES = 80.0   # 1.7B rows, 8 machines (:237)
+
+
+def make_ctr(num_rows, seed):
+    rng = np.random.default_rng(seed)
+    X = np.zeros((num_rows, 67), dtype=np.float32)
+    y = np.empty(num_rows, dtype=np.float32)
+    wd = np.random.default_rng(99).normal(0, 0.35, size=13).astype(np.float32)
+    ws = np.random.default_rng(98).normal(0, 0.8, size=54).astype(np.float32)
+    dens = np.random.default_rng(97).uniform(0.005, 0.03, size=54)
+    chunk = 1 << 21
+    for s in range(0, num_rows, chunk):
+        e = min(num_rows, s + chunk)
+        n = e - s
+        d = np.floor(rng.pareto(1.5, size=(n, 13)).astype(np.float32) * 3.0)
+        X[s:e, :13] = d
+        logit = np.log1p(d) @ wd - 3.6
+        for j in range(54):
+            nz = rng.random(n) < dens[j]
+            cnt = nz.sum()
+            if cnt:
+                v = np.floor(rng.pareto(1.2, size=cnt).astype(np.float32) * 5.0) + 1.0
+                X[s:e, 13 + j][nz] = v
+                logit[nz] += ws[j] * np.log1p(v)
+        y[s:e] = (rng.random(n) < 1.0 / (1.0 + np.exp(-logit))).astype(np.float32)
+    return X, y
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--leaves", type=int, default=255)
+    ap.add_argument("--device", default="gpu")
+    args = ap.parse_args()
+    import lightgbmv1_amd as lgb
+
+    t0 = time.time()
+    X, y = make_ctr(args.rows, 5)
+    t_gen = time.time() - t0
+    params = {"objective": "binary", "num_leaves": args.leaves, "learning_rate": 0.1, "max_bin": 255,
+              "min_data_in_leaf": 20, "device_type": args.device, "verbose": -1,
+              "num_threads": min(16, os.cpu_count() or 8)}
+    train = lgb.Dataset(X, y, params=params, free_raw_data=True)
+    booster = lgb.Booster(params=params, train_set=train)
+    del X
+    setup_s = time.time() - t0
+    for _ in range(args.warmup):
+        booster.update()
+    lgb.device_synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        booster.update()
+    lgb.device_synchronize()
+    sec = (time.perf_counter() - t1) / max(1, args.steps)
+    # the reference's single-machine time scaled to this shard's rows (linear in rows)
+    ref_scaled = REF_SEC_PER_TREE_1_MACHINE * args.rows / 1.7e9
+    print(json.dumps({
+        "metric": "sec/tree, Criteo-shaped 67 sparse count features (EFB), 255 leaves, one GPU shard",
+        "value": round(sec, 6), "unit": "s/tree", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "higher_is_better": False, "rows": args.rows, "dtype": "fp32", "data": "synthetic",
+        "reference_1_machine_scaled_to_rows_s": round(ref_scaled, 3),
+        "reference_8_machines_1p7B_s": REF_SEC_PER_TREE_8_MACHINES,
+        "data_gen_s": round(t_gen, 1), "setup_s": round(setup_s, 1), "trees": booster.num_trees()}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

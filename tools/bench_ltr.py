@@ -33,7 +33,8 @@ def make_ltr(num_rows, num_features, seed):
     sizes[-1] -= int(cum[nq - 1] - num_rows)
     qid = np.repeat(np.arange(nq), sizes)
     q_off = rng.normal(0.0, 0.7, size=nq).astype(np.float32)
-    w = rng.normal(0.0, 1.0, size=40).astype(np.float32) / np.sqrt(40)
+    # the relevance function is shared by the training and held-out sets
+    w = np.random.default_rng(12345).normal(0.0, 1.0, size=40).astype(np.float32) / np.sqrt(40)
     X = np.empty((num_rows, num_features), dtype=np.float32)
     rel = np.empty(num_rows, dtype=np.float32)
     chunk = 1 << 19
