@@ -64,6 +64,17 @@ def _safe_call(ret):
         raise LightGBMError(_load_lib().LGBM_GetLastError().decode("utf-8"))
 
 
+def _from_tensor(data):
+    """torch.Tensor (CPU or a HIP device) -> numpy; anything else unchanged.
+
+    Device tensors are copied to the host once here; the library bins them and keeps its
+    own device copy of the binned matrix (PyTorch-ROCm interop)."""
+    mod = type(data).__module__
+    if mod.startswith("torch") and hasattr(data, "detach"):
+        return data.detach().cpu().numpy()
+    return data
+
+
 def is_numeric(obj):
     try:
         float(obj)
@@ -412,6 +423,7 @@ class _InnerPredictor(object):
         if pred_contrib:
             predict_type = C_API_PREDICT_CONTRIB
         int_data_has_header = 1 if data_has_header else 0
+        data = _from_tensor(data)
         if isinstance(data, string_type):
             with _TempFile() as f:
                 _safe_call(_load_lib().LGBM_BoosterPredictForFile(
@@ -737,6 +749,8 @@ class Dataset(object):
         if data is None:
             self.handle = None
             return self
+        data, label, weight, init_score = (_from_tensor(data), _from_tensor(label), _from_tensor(weight),
+                                           _from_tensor(init_score))
         if reference is not None:
             self.pandas_categorical = reference.pandas_categorical
             categorical_feature = reference.categorical_feature

@@ -199,3 +199,15 @@ def test_validation_set_with_nan_feature_aligns():
     p = b.predict(Xv)
     ll = -np.mean(yv * np.log(p) + (1 - yv) * np.log(1 - p))
     assert rec["v"]["binary_logloss"][-1] == pytest.approx(ll, rel=1e-9)
+
+
+def test_torch_tensor_inputs():
+    """Datasets and predictions accept torch tensors (host copies of CPU / device tensors)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.RandomState(3)
+    X = rng.randn(2000, 5).astype(np.float32)
+    y = (X[:, 0] + X[:, 1] > 0).astype(np.float32)
+    params = {"objective": "binary", "verbose": -1}
+    b_np = lgb.train(params, lgb.Dataset(X, y), 5)
+    b_t = lgb.train(params, lgb.Dataset(torch.from_numpy(X), torch.from_numpy(y)), 5)
+    np.testing.assert_array_equal(b_np.predict(X), b_t.predict(torch.from_numpy(X)))
