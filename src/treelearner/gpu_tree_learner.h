@@ -6,9 +6,10 @@
 //    a fixed kernel sequence on one stream (optionally replayed from a hipGraph); the
 //    host reads the split records back once per tree.
 //  * host-assisted: the SerialTreeLearner loop runs on the host and only histogram
-//    construction and row partitioning are offloaded.  Used for features the device
-//    split scan does not implement (categorical splits, forced splits, interaction
-//    constraints, extra_trees, per-node column sampling, CEGB).
+//    construction, row partitioning and leaf sums are offloaded.  Used for features the
+//    device split scan does not implement (forced splits, interaction constraints,
+//    extra_trees, per-node column sampling, CEGB, categorical features with > 1024
+//    categories) and under the voting-parallel learner.
 // The reference's GPU learner (src/treelearner/gpu_tree_learner.cpp, OpenCL) offloads
 // only the histogram build; this learner keeps the training scores, gradients and the
 // data partition resident on the device across iterations.
