@@ -43,6 +43,7 @@ class ScoreUpdater {
   // a validation updater may hand its scores to the device learner (slot): updates then run
   // on the device and the host copy is refreshed when it is read
   void AttachDevice(DeviceTreeLearner* dl, int slot);
+  int device_slot() const { return device_ != nullptr ? device_slot_ : -1; }
   double* score() {
     SyncFromDevice();
     return score_.data();
@@ -216,6 +217,8 @@ class GBDT {
   int device_sampler_seed_ = 0;
   // a device draw of the bag (or -1: draw on the host)
   data_size_t DeviceBagging(bool goss);
+  // metric j of validation set i: on the device when its scores live there, else on the host
+  std::vector<double> EvalValid(int i, int j) const;
   std::vector<bool> class_need_train_;
   bool is_constant_hessian_ = false;
   bool average_output_ = false;

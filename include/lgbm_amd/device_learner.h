@@ -7,6 +7,7 @@
 
 #include <vector>
 
+#include "lgbm_amd/metric.h"
 #include "lgbm_amd/objective.h"
 #include "lgbm_amd/tree_learner.h"
 
@@ -58,6 +59,8 @@ class DeviceTreeLearner {
   virtual void ValidMultiply(int slot, double v, int tree_id) = 0;
   virtual void ValidAddTree(int slot, const Tree* tree, int tree_id) = 0;
   virtual void ValidScoreToHost(int slot, double* host) = 0;
+  // a metric on the device-resident scores of a validation set; false: evaluate on the host
+  virtual bool ValidEval(int slot, const DeviceMetricSpec& spec, double* out) = 0;
 };
 
 TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Config* config);

@@ -13,8 +13,24 @@
 
 namespace lgbm_amd {
 
+// a metric the device learner can evaluate on device-resident validation scores
+// (kind: src/device/kernels.h kMetric*; 0 = host only)
+struct DeviceMetricSpec {
+  int kind = 0;
+  int convert = 0;  // score -> prediction: 0 identity, 1 sigmoid, 2 sign(s) * s^2
+  double sigmoid = 1.0;
+  double sum_weights = 0.0;
+  const label_t* label = nullptr;  // host pointers, uploaded once per validation set
+  const label_t* weights = nullptr;
+};
+
 class Metric {
  public:
+  // device evaluation of this metric for the objective's output transform (kind 0: none)
+  virtual DeviceMetricSpec DeviceSpec(const ObjectiveFunction* objective) const {
+    (void)objective;
+    return DeviceMetricSpec();
+  }
   virtual ~Metric() = default;
   virtual void Init(const Metadata& metadata, data_size_t num_data) = 0;
   virtual const std::vector<std::string>& GetName() const = 0;

@@ -71,6 +71,12 @@ class ObjectiveFunction {
   virtual bool NeedAccuratePrediction() const { return true; }
   virtual data_size_t NumPositiveData() const { return 0; }
   virtual void ConvertOutput(const double* input, double* output) const { output[0] = input[0]; }
+  // ConvertOutput as a device-evaluable form: 0 identity, 1 sigmoid(*param * s),
+  // 2 sign(s) * s^2 (regression with reg_sqrt); -1 other (host only)
+  virtual int DeviceOutputKind(double* param) const {
+    (void)param;
+    return -1;
+  }
   virtual std::string ToString() const = 0;
   // device description; kind None => host gradients (uploaded by the learner)
   virtual DeviceGradSpec DeviceSpec() const { return DeviceGradSpec(); }

@@ -386,6 +386,17 @@ data_size_t GBDT::DeviceBagging(bool goss) {
   return device_learner_->DeviceSample(sp);
 }
 
+std::vector<double> GBDT::EvalValid(int i, int j) const {
+  const Metric* m = valid_metrics_[i][j];
+  const int slot = valid_score_updater_[i]->device_slot();
+  if (slot >= 0 && device_learner_ != nullptr) {
+    const DeviceMetricSpec spec = m->DeviceSpec(objective_);
+    double v = 0.0;
+    if (spec.kind != 0 && device_learner_->ValidEval(slot, spec, &v)) return {v};
+  }
+  return m->Eval(valid_score_updater_[i]->score(), objective_);
+}
+
 double* GBDT::HostTrainScore() {
   if (device_learner_ != nullptr && !host_score_fresh_) {
     for (int k = 0; k < num_tree_per_iteration_; ++k) {
@@ -645,7 +656,7 @@ std::string GBDT::OutputMetric(int iter) {
   if (need_output || early_stopping_round_ > 0) {
     for (size_t i = 0; i < valid_metrics_.size(); ++i) {
       for (size_t j = 0; j < valid_metrics_[i].size(); ++j) {
-        auto scores = valid_metrics_[i][j]->Eval(valid_score_updater_[i]->score(), objective_);
+        auto scores = EvalValid(i, j);
         auto names = valid_metrics_[i][j]->GetName();
         for (size_t k = 0; k < names.size(); ++k) {
           std::stringstream t;

@@ -226,6 +226,23 @@ struct ForestArgs {
 };
 void PredictForest(const ForestArgs& f, hipStream_t s);
 
+// validation metrics on device scores (one model per iteration)
+constexpr int kMetricL2 = 1, kMetricRMSE = 2, kMetricL1 = 3, kMetricBinLogloss = 4, kMetricBinError = 5,
+              kMetricAUC = 6;
+struct MetricArgs {
+  int32_t kind;
+  int32_t convert;       // score -> prediction: 0 identity, 1 sigmoid(sigmoid * s), 2 sign(s) * s^2
+  double sigmoid;
+  int64_t n;
+  const double* score;
+  const float* label;
+  const float* weights;  // may be null
+  void* scratch;         // MetricScratchBytes(n)
+  double* out;           // [0] weighted loss sum (or AUC accumulator), [1] AUC positive weight
+};
+size_t MetricScratchBytes(int64_t n);
+void EvalMetric(const MetricArgs& m, hipStream_t s);
+
 int GradientBlocks(int64_t n);
 // absmax[0..1] (and root = (sum g, sum h, n) if root_parts) from per-workgroup partials
 void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, uint32_t* absmax,

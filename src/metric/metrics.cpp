@@ -24,6 +24,23 @@ class PointwiseMetric : public Metric {
   PointwiseMetric(const Config& cfg, const char* name, PointLoss loss, bool convert, double factor)
       : cfg_(cfg), loss_(loss), convert_(convert), factor_(factor) {
     name_.push_back(name);
+    const std::string n(name);
+    device_kind_ = n == "l2" ? 1 : n == "rmse" ? 2 : n == "l1" ? 3 : n == "binary_logloss" ? 4
+                 : n == "binary_error" ? 5 : 0;
+  }
+  DeviceMetricSpec DeviceSpec(const ObjectiveFunction* obj) const override {
+    DeviceMetricSpec d;
+    if (device_kind_ == 0) return d;
+    double param = 1.0;
+    const int conv = (convert_ && obj != nullptr) ? obj->DeviceOutputKind(&param) : 0;
+    if (conv < 0) return d;
+    d.kind = device_kind_;
+    d.convert = conv;
+    d.sigmoid = param;
+    d.sum_weights = sum_w_;
+    d.label = label_;
+    d.weights = weights_;
+    return d;
   }
   void Init(const Metadata& md, data_size_t n) override {
     num_data_ = n;
@@ -54,6 +71,7 @@ class PointwiseMetric : public Metric {
  protected:
   Config cfg_;
   PointLoss loss_;
+  int device_kind_ = 0;
   bool convert_;
   double factor_;
   std::vector<std::string> name_;
@@ -138,6 +156,14 @@ double XentPoint(label_t y, double p, const Config&) { return XentLoss(y, p); }
 class AUCMetric : public Metric {
  public:
   explicit AUCMetric(const Config&) { name_.push_back("auc"); }
+  DeviceMetricSpec DeviceSpec(const ObjectiveFunction*) const override {
+    DeviceMetricSpec d;
+    d.kind = 6;  // AUC ranks raw scores (no output transform)
+    d.sum_weights = sum_w_;
+    d.label = label_;
+    d.weights = weights_;
+    return d;
+  }
   void Init(const Metadata& md, data_size_t n) override {
     num_data_ = n;
     label_ = md.label();

@@ -100,6 +100,7 @@ class RegressionL2 : public ObjectiveFunction {
   void ConvertOutput(const double* in, double* out) const override {
     out[0] = sqrt_ ? common::Sign(in[0]) * in[0] * in[0] : in[0];
   }
+  int DeviceOutputKind(double*) const override { return sqrt_ ? 2 : 0; }
   std::string ToString() const override { return std::string(GetName()) + (sqrt_ ? " sqrt" : ""); }
   bool IsConstantHessian() const override { return weights_ == nullptr; }
   double BoostFromScore(int) const override {
@@ -255,6 +256,7 @@ class Poisson : public RegressionL2 {
     }
   }
   void ConvertOutput(const double* in, double* out) const override { out[0] = std::exp(in[0]); }
+  int DeviceOutputKind(double*) const override { return -1; }
   const char* GetName() const override { return "poisson"; }
   std::string ToString() const override { return GetName(); }
   double BoostFromScore(int) const override { return common::SafeLog(RegressionL2::BoostFromScore(0)); }
@@ -498,6 +500,10 @@ class BinaryLogloss : public ObjectiveFunction {
   const char* GetName() const override { return "binary"; }
   void ConvertOutput(const double* in, double* out) const override {
     out[0] = 1.0f / (1.0f + std::exp(-sigmoid_ * in[0]));
+  }
+  int DeviceOutputKind(double* param) const override {
+    *param = sigmoid_;
+    return 1;
   }
   std::string ToString() const override {
     std::stringstream s;

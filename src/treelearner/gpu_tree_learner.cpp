@@ -974,6 +974,57 @@ void GPUTreeLearner::ValidAddTree(int slot, const Tree* tree, int k) {
   HIPCHECK(hipStreamSynchronize(stream_));  // staging buffers are reused by the next tree
 }
 
+bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, double* out) {
+  ValidSet& vs = valid_[slot];
+  if (spec.kind == 0 || vs.ntpi != 1 || spec.label == nullptr || vs.num_data <= 0) return false;
+  HIPCHECK(hipSetDevice(device_id_));
+  const size_t n = static_cast<size_t>(vs.num_data);
+  auto dev_alloc = [&](size_t bytes) {
+    void* p = nullptr;
+    HIPCHECK(hipMalloc(&p, std::max<size_t>(1, bytes)));
+    valid_allocs_.push_back(p);
+    return p;
+  };
+  if (vs.label == nullptr) {
+    vs.label = static_cast<float*>(dev_alloc(sizeof(float) * n));
+    HIPCHECK(hipMemcpy(vs.label, spec.label, sizeof(float) * n, hipMemcpyHostToDevice));
+    if (spec.weights != nullptr) {
+      vs.weights = static_cast<float*>(dev_alloc(sizeof(float) * n));
+      HIPCHECK(hipMemcpy(vs.weights, spec.weights, sizeof(float) * n, hipMemcpyHostToDevice));
+    }
+    vs.metric_out = static_cast<double*>(dev_alloc(sizeof(double) * 2));
+  }
+  if (spec.kind == dev::kMetricAUC && vs.metric_scratch == nullptr) {
+    vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(vs.num_data));
+  } else if (vs.metric_scratch == nullptr) {
+    vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(0));
+  }
+  dev::MetricArgs m;
+  m.kind = spec.kind;
+  m.convert = spec.convert;
+  m.sigmoid = spec.sigmoid;
+  m.n = vs.num_data;
+  m.score = vs.score;
+  m.label = vs.label;
+  m.weights = vs.weights;
+  m.scratch = vs.metric_scratch;
+  m.out = vs.metric_out;
+  dev::EvalMetric(m, stream_);
+  double h[2] = {0.0, 0.0};
+  HIPCHECK(hipMemcpyAsync(h, vs.metric_out, sizeof(double) * 2, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  const double sw = spec.sum_weights;
+  if (spec.kind == dev::kMetricAUC) {
+    const double sum_pos = h[1];
+    *out = (sum_pos > 0.0 && sum_pos != sw) ? h[0] / (sum_pos * (sw - sum_pos)) : 1.0;
+  } else if (spec.kind == dev::kMetricRMSE) {
+    *out = std::sqrt(h[0] / sw);
+  } else {
+    *out = h[0] / sw;
+  }
+  return true;
+}
+
 void GPUTreeLearner::ValidScoreToHost(int slot, double* host) {
   const ValidSet& vs = valid_[slot];
   HIPCHECK(hipMemcpyAsync(host, vs.score, sizeof(double) * vs.num_data * vs.ntpi, hipMemcpyDeviceToHost, stream_));

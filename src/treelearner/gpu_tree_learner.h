@@ -67,6 +67,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void ValidMultiply(int slot, double v, int tree_id) override;
   void ValidAddTree(int slot, const Tree* tree, int tree_id) override;
   void ValidScoreToHost(int slot, double* host) override;
+  bool ValidEval(int slot, const DeviceMetricSpec& spec, double* out) override;
 
   bool device_mode() const { return device_mode_; }
 
@@ -179,6 +180,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
     double* score = nullptr;
     data_size_t num_data = 0;
     int ntpi = 1;
+    float* label = nullptr;    // metric inputs, uploaded on the first device evaluation
+    float* weights = nullptr;
+    void* metric_scratch = nullptr;
+    double* metric_out = nullptr;
   };
   std::vector<ValidSet> valid_;
   std::vector<void*> valid_allocs_;

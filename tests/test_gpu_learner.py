@@ -247,7 +247,8 @@ def test_validation_scores_on_device(gpu_available):
     metric equals the metric of the booster's own predictions, and early stopping works."""
     X, y = _data(40000, seed=21)
     Xv, yv = _data(15000, seed=22)
-    params = {"objective": "binary", "metric": ["binary_logloss", "auc"], "num_leaves": 31, "max_bin": 63,
+    params = {"objective": "binary", "metric": ["binary_logloss", "auc", "binary_error"], "num_leaves": 31,
+              "max_bin": 63,
               "verbose": -1, "device_type": "gpu", "bagging_fraction": 0.8, "bagging_freq": 1}
     ds = lgb.Dataset(X, y, params=params)
     dv = lgb.Dataset(Xv, yv, reference=ds)
@@ -258,6 +259,26 @@ def test_validation_scores_on_device(gpu_available):
     ll = -np.mean(yv * np.log(p) + (1 - yv) * np.log(1 - p))
     assert rec["v"]["binary_logloss"][b.best_iteration - 1] == pytest.approx(ll, rel=1e-6)
     assert rec["v"]["auc"][b.best_iteration - 1] == pytest.approx(_auc(yv, p), abs=1e-6)
+    assert rec["v"]["binary_error"][b.best_iteration - 1] == pytest.approx(np.mean((p > 0.5) != (yv > 0)), abs=1e-9)
+
+
+def test_regression_validation_metrics_on_device(gpu_available):
+    rng = np.random.RandomState(23)
+    X = rng.randn(30000, 8).astype(np.float32)
+    y = (X[:, 0] * 2 + np.sin(X[:, 1]) + 0.1 * rng.randn(30000)).astype(np.float32)
+    Xv = rng.randn(8000, 8).astype(np.float32)
+    yv = (Xv[:, 0] * 2 + np.sin(Xv[:, 1]) + 0.1 * rng.randn(8000)).astype(np.float32)
+    w = (rng.rand(8000) + 0.5).astype(np.float32)
+    params = {"objective": "regression", "metric": ["l2", "l1", "rmse"], "verbose": -1, "device_type": "gpu"}
+    ds = lgb.Dataset(X, y, params=params)
+    rec = {}
+    b = lgb.train(params, ds, 20, valid_sets=[lgb.Dataset(Xv, yv, weight=w, reference=ds)], valid_names=["v"],
+                  evals_result=rec, verbose_eval=False)
+    p = b.predict(Xv)
+    l2 = np.sum(w * (p - yv) ** 2) / np.sum(w)
+    assert rec["v"]["l2"][-1] == pytest.approx(l2, rel=1e-6)
+    assert rec["v"]["rmse"][-1] == pytest.approx(np.sqrt(l2), rel=1e-6)
+    assert rec["v"]["l1"][-1] == pytest.approx(np.sum(w * np.abs(p - yv)) / np.sum(w), rel=1e-6)
 
 
 @pytest.mark.parametrize("kind", ["binary_nan", "categorical", "multiclass"])
