@@ -312,3 +312,40 @@ def test_device_batch_prediction_matches_host(gpu_available, kind, monkeypatch):
     dev = b.predict(X, num_iteration=10, start_iteration=5)
     monkeypatch.setenv("LGBM_AMD_HOST_PREDICT", "1")
     np.testing.assert_array_equal(dev, b.predict(X, num_iteration=10, start_iteration=5))
+
+
+@pytest.mark.parametrize("extra", [
+    {"lambda_l1": 2.0, "lambda_l2": 5.0},
+    {"max_delta_step": 0.3},
+    {"path_smooth": 5.0, "min_data_in_leaf": 30},
+    {"min_gain_to_split": 5.0},
+    {"max_depth": 4},
+    {"monotone_constraints": [1, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0], "monotone_penalty": 0.5},
+    {"zero_as_missing": True},
+    {"feature_fraction": 0.6, "feature_fraction_seed": 4},
+], ids=["l1l2", "max_delta_step", "path_smooth", "min_gain", "max_depth", "monotone", "zero_missing",
+        "feature_fraction"])
+def test_device_split_rules_match_cpu(gpu_available, extra):
+    """The device split scan applies the reference's split rules like the CPU learner: same
+    first-tree splits near the root, and closely matching fits."""
+    X, y = _data(40000, seed=41)
+    w = np.random.RandomState(42).rand(len(y)).astype(np.float32) + 0.5
+    boosters = {}
+    for device in ("cpu", "gpu"):
+        params = {"objective": "binary", "num_leaves": 31, "max_bin": 63, "verbose": -1, "device_type": device,
+                  "seed": 7}
+        params.update(extra)
+        boosters[device] = lgb.train(params, lgb.Dataset(X, y, weight=w, params=params), 15, verbose_eval=False)
+    cpu_t = boosters["cpu"].dump_model()["tree_info"][0]["tree_structure"]
+    gpu_t = boosters["gpu"].dump_model()["tree_info"][0]["tree_structure"]
+    for path in ([], ["left_child"], ["right_child"]):
+        a, b = cpu_t, gpu_t
+        for k in path:
+            a, b = a.get(k, {}), b.get(k, {})
+        if "split_feature" not in a:
+            assert "split_feature" not in b
+            continue
+        assert a["split_feature"] == b["split_feature"]
+        assert a["threshold"] == pytest.approx(b["threshold"])
+    pc, pg = boosters["cpu"].predict(X[:5000]), boosters["gpu"].predict(X[:5000])
+    assert np.corrcoef(pc, pg)[0, 1] > 0.99
