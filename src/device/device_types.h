@@ -95,6 +95,7 @@ struct Step {
   int32_t skip_find;  // children can not be split further (depth / min_data / last split)
   int32_t total_left;
   int32_t s_begin, s_count, s_buf;  // the histogrammed (smaller) child's rows
+  int32_t bynode_base, bynode_next;  // per-node feature masks: this step's / next free mask index
   int32_t cur_left, cur_right;      // partition cursors: rows placed left / right so far
   CurSplit cs;
   ChildStats lr[2];     // left / right child of cs

@@ -127,6 +127,10 @@ __device__ void StepBookkeeping(const KArgs& a, Step* st) {
   st->smaller = c.smaller;
   st->larger = c.larger;
   st->skip_find = c.skip;
+  if (!c.skip) {  // the host learner samples the smaller, then the larger child
+    st->bynode_base = st->bynode_next;
+    st->bynode_next += 2;
+  }
   st->total_left = c.total_left;
   st->s_begin = c.s_begin;
   st->s_count = c.s_count;

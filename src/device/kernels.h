@@ -20,6 +20,7 @@ struct KArgs {
   const Feature* feat;       // [num_features]
   const int32_t* group_off;  // [num_groups] first histogram bin of each storage column
   const int8_t* tree_mask;   // [num_features] feature used by this tree
+  const int8_t* node_mask;   // [2 * num_leaves - 1][num_features] per-node samples (feature_fraction_bynode), or null
   const GH* gh;              // interleaved (gradient, hessian) per row
   int32_t* idx;              // partition index buffer 0 (root rows)
   int32_t* tmp;              // partition index buffer 1 (leaves alternate: Leaf::buf)

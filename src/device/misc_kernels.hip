@@ -103,6 +103,8 @@ __global__ void k_tree_begin(KArgs a) {
     st->done = 0;
     st->nsplit = 0;
     st->fresh = 1;  // the root's per-feature results (k_find<true>) are the first pick's input
+    st->bynode_base = 0;
+    st->bynode_next = 1;  // mask 0: the root
     st->smaller = 0;
     st->larger = -1;
     st->skip_find = 0;

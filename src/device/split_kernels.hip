@@ -549,7 +549,11 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   // ---- independent loads first (one round trip): the feature, its mask, the scales and the
   // Step record (read before it is tested)
   const Feature F = a.feat[f];
-  const int8_t used = a.tree_mask[f];
+  int8_t used = a.tree_mask[f];
+  if (a.node_mask != nullptr) {
+    const int mi = ROOT ? 0 : a.st->bynode_base + side;
+    used = used && a.node_mask[static_cast<size_t>(mi) * a.p.num_features + f];
+  }
   const double ig = a.scales[2], ih = a.scales[3];
   const Step* st = a.st;
   int done = 0, skip = 0, s = 0, s_count = 0;

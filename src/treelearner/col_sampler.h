@@ -117,6 +117,23 @@ class ColSampler {
     return ret;
   }
 
+  // per-node masks of the next `calls` GetByNode calls (no interaction constraints: the
+  // draws do not depend on the tree), from a copy of the generator -- the device learner
+  // uploads them before a tree and replays the calls the tree made (AdvanceByNode)
+  std::vector<int8_t> PeekByNodeMasks(int calls) const {
+    ColSampler copy(*this);
+    std::vector<int8_t> out;
+    out.reserve(static_cast<size_t>(calls) * data_->num_features());
+    for (int c = 0; c < calls; ++c) {
+      auto m = copy.GetByNode(nullptr, 0);
+      out.insert(out.end(), m.begin(), m.end());
+    }
+    return out;
+  }
+  void AdvanceByNode(int calls) {
+    for (int c = 0; c < calls; ++c) (void)GetByNode(nullptr, 0);
+  }
+
   const std::vector<int8_t>& is_feature_used_bytree() const { return used_; }
   bool has_interaction_constraints() const { return !constraints_.empty(); }
   bool need_by_node() const { return frac_node_ < 1.0f || !constraints_.empty(); }

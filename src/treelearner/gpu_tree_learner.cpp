@@ -217,6 +217,8 @@ void GPUTreeLearner::UploadData() {
   if (tile_words == 0) Log::Fatal("device learner: feature groups too wide for LDS histograms; reduce max_bin");
   const int n_leaves = config_->num_leaves;
   d_tree_mask_ = Alloc<int8_t>(num_features_);
+  d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
+  h_node_mask_.clear();
   d_gh_ = Alloc<dev::GH>(num_data_);
   d_idx_ = Alloc<int32_t>(num_data_);
   d_tmp_ = Alloc<int32_t>(num_data_);
@@ -263,6 +265,7 @@ void GPUTreeLearner::UploadData() {
   a.feat = d_feat_;
   a.group_off = d_group_off_;
   a.tree_mask = d_tree_mask_;
+  a.node_mask = nullptr;
   a.gh = d_gh_;
   a.idx = d_idx_;
   a.tmp = d_tmp_;
@@ -333,6 +336,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     HIPCHECK(hipSetDevice(device_id_));
     const int n_leaves = config_->num_leaves;
     d_leaves_ = Alloc<dev::Leaf>(n_leaves);
+    d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
     d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
     d_best_ = Alloc<DeviceSplit>(n_leaves);
     d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
@@ -368,7 +372,8 @@ void GPUTreeLearner::DecideMode() {
     if (m->bin_type() == BinType::Categorical && m->num_bin() > dev::kFindMaxCatBins) dm = false;
   }
   if (has_forced_split_ || !config_->interaction_constraints_vector.empty() || config_->extra_trees ||
-      config_->feature_fraction_bynode < 1.0 || config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
+      (config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
+      config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
       !config_->cegb_penalty_feature_lazy.empty() || !config_->cegb_penalty_feature_coupled.empty()) {
     dm = false;
   }
@@ -629,6 +634,14 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   const auto& mask = col_sampler_.is_feature_used_bytree();
   for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
   dev::KArgs a = args_;
+  const bool bynode = config_->feature_fraction_bynode < 1.0;
+  if (bynode) {
+    // every GetByNode draw the tree can make (root + two per split), from a copy of the
+    // generator; the draws actually made are replayed after the tree
+    h_node_mask_ = col_sampler_.PeekByNodeMasks(2 * (config_->num_leaves - 1) + 1);
+    HIPCHECK(hipMemcpyAsync(d_node_mask_, h_node_mask_.data(), h_node_mask_.size(), hipMemcpyHostToDevice, stream_));
+    a.node_mask = d_node_mask_;
+  }
   if (use_bag_) {
     // bag size read on the device: one captured graph serves every bag
     a.num_rows = num_data_;
@@ -693,6 +706,11 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
                           hipMemcpyDeviceToHost, stream_));
   WatchdogSync();
   const int num_splits = h_step_->nsplit;
+  if (bynode) {
+    // the root's draw happens only if the host learner would have scanned the root
+    const bool root_scanned = root_rows_ >= 2 * config_->min_data_in_leaf;
+    col_sampler_.AdvanceByNode(root_scanned ? h_step_->bynode_next : 0);
+  }
   if (a.ktrace != nullptr) ReportKernelTrace(num_splits);
   if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {
     if (kp[0] == '1') KernelFloorProbe(a);

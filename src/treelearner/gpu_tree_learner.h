@@ -118,6 +118,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   dev::Feature* d_feat_ = nullptr;
   int32_t* d_group_off_ = nullptr;
   int8_t* d_tree_mask_ = nullptr;
+  int8_t* d_node_mask_ = nullptr;       // per-node feature samples of the current tree
+  std::vector<int8_t> h_node_mask_;     // (kept alive for the async upload)
   dev::GH* d_gh_ = nullptr;
   int32_t* d_idx_ = nullptr;
   int32_t* d_tmp_ = nullptr;

@@ -26,7 +26,20 @@ def _free_port():
     return port
 
 
+_RENDEZVOUS_ERRORS = ("Address already in use", "EADDRINUSE", "Connection refused", "connect()", "Socket Timeout")
+
+
 def _run(learner, tmp_path, world=2, device="cpu"):
+    # the free port can be taken between the probe and the rendezvous: retry on that only
+    for attempt in range(3):
+        try:
+            return _run_once(learner, tmp_path, world, device)
+        except AssertionError as e:
+            if attempt == 2 or not any(m in str(e) for m in _RENDEZVOUS_ERRORS):
+                raise
+
+
+def _run_once(learner, tmp_path, world, device):
     port = _free_port()
     procs = []
     for r in range(world):

@@ -323,8 +323,10 @@ def test_device_batch_prediction_matches_host(gpu_available, kind, monkeypatch):
     {"monotone_constraints": [1, 0, 0, -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0], "monotone_penalty": 0.5},
     {"zero_as_missing": True},
     {"feature_fraction": 0.6, "feature_fraction_seed": 4},
+    {"feature_fraction_bynode": 0.5, "feature_fraction_seed": 5},
+    {"feature_fraction": 0.8, "feature_fraction_bynode": 0.6, "feature_fraction_seed": 6},
 ], ids=["l1l2", "max_delta_step", "path_smooth", "min_gain", "max_depth", "monotone", "zero_missing",
-        "feature_fraction"])
+        "feature_fraction", "bynode", "bytree_bynode"])
 def test_device_split_rules_match_cpu(gpu_available, extra):
     """The device split scan applies the reference's split rules like the CPU learner: same
     first-tree splits near the root, and closely matching fits."""
