@@ -60,6 +60,8 @@ struct Leaf {
   int32_t depth;
   int32_t slot;          // histogram slot
   int32_t buf;           // which index buffer (KArgs::idx / tmp) holds the leaf's rows
+  int32_t frow;          // row of KArgs::splittable (kept across trees)
+  int32_t pad_;
   double sum_g, sum_h, output;
   double cmin, cmax;  // monotone constraint range
 };
@@ -69,6 +71,7 @@ struct Leaf {
 struct ChildStats {
   double sum_g, sum_h, output, cmin, cmax;
   int32_t global_count, depth, slot, leaf;
+  int32_t frow, pad_;  // splittable row the child's scan writes
 };
 
 // the split being applied, as chosen by the partition kernel's pick
@@ -79,6 +82,7 @@ struct CurSplit {
   int32_t src_buf;      // index buffer holding them (the children go to the other one)
   int32_t child_depth;
   int32_t parent_slot;  // histogram slot of the leaf (the new leaf's slot is its own id)
+  int32_t parent_frow, new_frow;  // splittable rows of the leaf and of the new leaf
   Feature feat;         // the split feature's record
   DeviceSplit split;
 };

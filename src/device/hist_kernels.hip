@@ -102,6 +102,8 @@ __device__ void StepBookkeeping(const KArgs& a, Step* st) {
     // the parent's histogram stays with the larger (right) child
     P->slot = nl;
     R->slot = cs.parent_slot;
+    P->frow = cs.new_frow;  // the splittable rows follow (the host swaps its rows too)
+    R->frow = cs.parent_frow;
   }
   // smaller / larger child records for the split scans (field-wise: no private copies)
   for (int k = 0; k < 2; ++k) {
@@ -117,6 +119,7 @@ __device__ void StepBookkeeping(const KArgs& a, Step* st) {
     to.leaf = from.leaf;
     to.global_count = a.p.data_parallel ? from.global_count : (lr == 0 ? c.left_count : c.right_count);
     to.slot = swap ? (lr == 0 ? nl : cs.parent_slot) : from.slot;
+    to.frow = k == 0 ? cs.new_frow : cs.parent_frow;  // the larger child inherits the parent's row
   }
   a.best[leaf].gain = -INFINITY;
   a.best[leaf].feature = -1;

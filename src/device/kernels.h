@@ -52,6 +52,12 @@ struct KArgs {
   FeatureBest* feat_best;    // [2][num_features] per-feature best split of the two leaves
   uint32_t* feat_cat;        // [2][num_features][kMaxCatWords] category sets of categorical bests
   long long* ktrace;         // optional [num_leaves][kTraceSlots] in-kernel timestamps (LGBM_AMD_KTRACE)
+  // per-leaf "feature had a valid split" flags (the host learner's splittable_ rows): a
+  // child skips a feature its parent could not split.  Rows are reached through Leaf::frow
+  // (swapped with the histogram hand-over) and persist across trees, as the host rows do;
+  // parent_flags is the parent's row, snapshot by the partition kernel
+  int8_t* splittable;        // [num_leaves][num_features]
+  int8_t* parent_flags;      // [num_features]
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

@@ -84,6 +84,7 @@ __global__ void k_tree_begin(KArgs a) {
   const int L = a.p.num_leaves;
   for (int l = threadIdx.x; l < L; l += blockDim.x) {
     Leaf lf;
+    lf.frow = a.leaves[l].frow;  // splittable rows persist across trees
     lf.begin = 0;
     lf.count = l == 0 ? RootRows(a) : 0;
     lf.global_count = lf.count;

@@ -288,6 +288,8 @@ __device__ void RecordSplit(const KArgs& a, Step* st, const PickResult& pk) {
   cs.src_buf = P.buf;
   cs.child_depth = depth;
   cs.parent_slot = P.slot;
+  cs.parent_frow = P.frow;
+  cs.new_frow = a.leaves[nl].frow;
   cs.feat = pk.F;
   cs.split = sp;
 }
@@ -322,7 +324,12 @@ __global__ __launch_bounds__(kPartThreads) void k_partition(KArgs a) {
       return;
     }
     // recorded by the last workgroup: it has no rows to move unless the leaf is large
-    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) RecordSplit(a, st, pk);
+    if (blockIdx.x == gridDim.x - 1) {
+      if (threadIdx.x == 0) RecordSplit(a, st, pk);
+      // the parent's splittable row, before the children's scans overwrite it
+      const int8_t* row = a.splittable + static_cast<size_t>(pk.P.frow) * a.p.num_features;
+      for (int f = threadIdx.x; f < a.p.num_features; f += kPartThreads) a.parent_flags[f] = row[f];
+    }
     KTraceAt(a, pk.s, kTrPartEntry, t_entry);
     KTrace(a, pk.s, kTrPartPicked);
     pb = pk.P.begin;

@@ -300,7 +300,8 @@ __device__ Cand ScanNumericalBlock(const HistView& hv, int nb, int offset, int d
   return BlockBestCand(best, reverse, sc);
 }
 
-__device__ void FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
+// returns whether any threshold was valid (the host's is_splittable)
+__device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
                                    double mono_penalty, FeatureBest* out, BlockScratch* sc) {
   const int nb = F.num_bin - F.offset;
   hv.fix_t = -1;
@@ -359,6 +360,7 @@ __device__ void FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
     else pen = 1. - pow(2., mono_penalty - 1. - depth) + kEpsilon;
     out->gain *= pen;
   }
+  return splittable;
 }
 
 // LDS of the categorical scan: per-bin ctr and the stable ctr order
@@ -373,7 +375,8 @@ struct CatScratch {
 // otherwise the bins with enough data sorted by g / (h + cat_smooth) -- a stable rank
 // computed in parallel -- and the sequential prefix scan from both ends (<= 2 x
 // max_cat_threshold steps, thread 0) with the min_data_per_group rules.
-__device__ __noinline__ void FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
+// returns splittable (meaningful in thread 0)
+__device__ __noinline__ bool FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
                                      FeatureBest* out, uint32_t* cat_out, BlockScratch* sc, CatScratch* cs) {
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
@@ -507,8 +510,7 @@ __device__ __noinline__ void FindCategoricalBlock(const Feature& F, HistView hv,
       cs->used_bin = used_bin;
     }
   }
-  if (tid != 0) return;
-  if (!splittable) return;
+  if (tid != 0 || !splittable) return splittable;
   out->lo = LeafOutputConstrained(best.lg, best.lh, l2, p, L.c, best.lc, L.parent_out);
   out->lc = best.lc;
   out->lg = best.lg;
@@ -531,6 +533,7 @@ __device__ __noinline__ void FindCategoricalBlock(const Feature& F, HistView hv,
     }
     out->ncat = k;
   }
+  return true;
 }
 
 }  // namespace
@@ -549,11 +552,13 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   // ---- independent loads first (one round trip): the feature, its mask, the scales and the
   // Step record (read before it is tested)
   const Feature F = a.feat[f];
-  int8_t used = a.tree_mask[f];
+  const int8_t tree_used = a.tree_mask[f];
+  int8_t used = tree_used;  // evaluated at this node (feature_fraction_bynode)
   if (a.node_mask != nullptr) {
     const int mi = ROOT ? 0 : a.st->bynode_base + side;
     used = used && a.node_mask[static_cast<size_t>(mi) * a.p.num_features + f];
   }
+  const int8_t parent_ok = ROOT ? 1 : a.parent_flags[f];
   const double ig = a.scales[2], ih = a.scales[3];
   const Step* st = a.st;
   int done = 0, skip = 0, s = 0, s_count = 0;
@@ -626,6 +631,19 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     depth = cl.depth;
     slot = cl.slot;
   }
+  int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : cl.frow) * a.p.num_features;
+  if (tree_used && !parent_ok) {
+    // the parent could not split on f: neither child evaluates it, the smaller child's row
+    // says so and the larger child keeps the parent's row (SerialTreeLearner::FindBestSplits)
+    if (side == 0 && tid == 0) flags[f] = 0;
+    if (tid == 0) {
+      FeatureBest o;
+      o.gain = -INFINITY;
+      o.feature = -1;
+      a.feat_best[side * a.p.num_features + f] = o;
+    }
+    return;
+  }
   L.cnt_factor = L.n / L.sh;
   const double gain_shift = LeafGain(L.sg, L.sh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, L.n,
                                      L.parent_out, p.use_l1, p.use_max_output, p.use_smoothing);
@@ -641,7 +659,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   o.mono = 0;
   o.ncat = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
-  if (used && (!F.is_cat || (CAT && F.num_bin <= kFindMaxCatBins))) {
+  // a sampled-out feature (bynode) still materialises its histogram: descendants subtract it
+  if (tree_used && (!F.is_cat || (CAT && F.num_bin <= kFindMaxCatBins))) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
@@ -682,23 +701,32 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     }
     __syncthreads();  // the workgroup's stores become visible to all its threads
     if (!ROOT) KTrace(a, s, kTrFindLoaded);
+    if (!used) {
+      if (tid == 0) {
+        o.feature = -1;
+        a.feat_best[side * a.p.num_features + f] = o;
+      }
+      return;
+    }
     HistView hv;
     hv.lg = stage ? sg : nullptr;
     hv.lh = stage ? sh : nullptr;
     hv.h = dst;
     hv.inv_g = ig;
     hv.inv_h = ih;
+    bool splittable;
     if constexpr (CAT) {
       if (F.is_cat) {
-        FindCategoricalBlock(F, hv, L, p, &o,
-                             a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
-                             &cat_sc);
+        splittable = FindCategoricalBlock(
+            F, hv, L, p, &o, a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
+            &cat_sc);
       } else {
-        FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
+        splittable = FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
       }
     } else {
-      FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
+      splittable = FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
     }
+    if (tid == 0) flags[f] = splittable ? 1 : 0;
     if (!ROOT) KTrace(a, s, kTrFindScanned);
   } else {
     o.feature = -1;

@@ -312,6 +312,23 @@ void GPUTreeLearner::UploadData() {
   // per-workgroup row cap of the histogram kernels (fixed-point headroom): see k_hist
   rows_cap_ = std::max(dev::kHistMinRows * 4, (num_data_ + hist_blocks - 1) / hist_blocks);
   a.hist_rows_cap = rows_cap_;
+  AllocSplittable();
+}
+
+void GPUTreeLearner::AllocSplittable() {
+  const int n_leaves = config_->num_leaves, nf = std::max(1, num_features_);
+  d_splittable_ = Alloc<int8_t>(static_cast<size_t>(n_leaves) * nf);
+  d_parent_flags_ = Alloc<int8_t>(nf);
+  std::vector<dev::Leaf> leaves(n_leaves);
+  for (int l = 0; l < n_leaves; ++l) {
+    std::memset(&leaves[l], 0, sizeof(dev::Leaf));
+    leaves[l].frow = l;
+  }
+  HIPCHECK(hipMemsetAsync(d_splittable_, 1, static_cast<size_t>(n_leaves) * nf, stream_));
+  HIPCHECK(hipMemcpyAsync(d_leaves_, leaves.data(), sizeof(dev::Leaf) * n_leaves, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  args_.splittable = d_splittable_;
+  args_.parent_flags = d_parent_flags_;
 }
 
 void GPUTreeLearner::ResetTrainingData(const Dataset* train_data, bool is_constant_hessian) {
@@ -349,6 +366,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     args_.rec = d_rec_;
     args_.best = d_best_;
     args_.hist = d_hist_;
+    AllocSplittable();
     global_count_.assign(n_leaves, 0);
   }
   // monotone / penalty metadata may have changed
@@ -861,6 +879,7 @@ data_size_t GPUTreeLearner::PartitionLeaf(int leaf, int inner, const SplitInfo& 
   HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   const data_size_t left = h_step_->cur_left;
+  host_partition_fresh_ = false;
   leaf_count_[leaf] = left;
   leaf_begin_[new_leaf] = begin + left;
   leaf_count_[new_leaf] = cnt - left;

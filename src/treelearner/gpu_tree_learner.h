@@ -76,6 +76,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void BeforeTrain() override;
   void ConstructHistograms(const std::vector<int8_t>& feature_used, bool use_subtract) override;
   data_size_t PartitionLeaf(int leaf, int inner_feature, const SplitInfo& s, int new_leaf) override;
+  const data_size_t* HostLeafRows(int leaf, data_size_t* cnt) override {
+    DownloadPartitionToHost();
+    return LeafIndices(leaf, cnt);
+  }
   void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) override;
   data_size_t GetGlobalDataCountInLeaf(int leaf) const override;
   LeafState LocalLeafSums(int leaf) const override;
@@ -98,6 +102,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void WatchdogSync();
   void AllreduceAbsMax();
   void UploadRankTables(const DeviceRankSpec& r, DeviceGradKind kind);
+  void AllocSplittable();  // (re)allocate the splittable rows: all 1, leaf i -> row i (resets d_leaves_)
   // tree records for the traversal kernels (staged in d_tree_*; the host vectors must stay
   // alive until the stream is synchronised)
   dev::DevTree StageTree(const Tree* tree);
@@ -119,6 +124,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int32_t* d_group_off_ = nullptr;
   int8_t* d_tree_mask_ = nullptr;
   int8_t* d_node_mask_ = nullptr;       // per-node feature samples of the current tree
+  int8_t* d_splittable_ = nullptr;      // [num_leaves][num_features] (KArgs::splittable)
+  int8_t* d_parent_flags_ = nullptr;    // [num_features]
   std::vector<int8_t> h_node_mask_;     // (kept alive for the async upload)
   dev::GH* d_gh_ = nullptr;
   int32_t* d_idx_ = nullptr;

@@ -342,6 +342,7 @@ void VotingParallelTreeLearner<Base>::FindBestSplits(const Tree* tree) {
     used[f] = 1;
   }
   this->ConstructHistograms(used, this->has_parent_hist_);
+  this->PrepareCegbLeaves();
   std::vector<SplitInfo> sbest(this->num_features_), lbest(this->num_features_);
   const int sdepth = tree->leaf_depth(this->smaller_.leaf);
   const int ldepth = this->larger_.leaf >= 0 ? tree->leaf_depth(this->larger_.leaf) : 0;

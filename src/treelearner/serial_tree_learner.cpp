@@ -47,10 +47,6 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool /*is_constant_hessi
   if (config_->monotone_constraints_method == "intermediate") {
     Log::Warning("monotone_constraints_method=intermediate is handled with the basic method by this learner");
   }
-  if (config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 || !config_->cegb_penalty_feature_lazy.empty() ||
-      !config_->cegb_penalty_feature_coupled.empty()) {
-    Log::Warning("cost-effective gradient boosting penalties are not applied by this learner");
-  }
   InitFeatureMeta();
   col_sampler_.SetTrainingData(data_);
   best_split_per_leaf_.assign(config_->num_leaves, SplitInfo());
@@ -63,6 +59,7 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool /*is_constant_hessi
   leaf_count_.assign(config_->num_leaves, 0);
   tmp_left_.resize(num_data_);
   tmp_right_.resize(num_data_);
+  SetupCegb();
   Log::Info("Number of data points in the train set: %d, number of used features: %d", num_data_, num_features_);
 }
 
@@ -75,6 +72,23 @@ void SerialTreeLearner::ResetTrainingData(const Dataset* train_data, bool) {
   tmp_right_.resize(num_data_);
   col_sampler_.SetTrainingData(data_);
   use_bag_ = false;
+  SetupCegb();
+}
+
+void SerialTreeLearner::SetupCegb() {
+  if (!CostEffectiveGB::Enabled(*config_)) return;
+  if (!cegb_) cegb_.reset(new CostEffectiveGB());
+  cegb_->Init(config_, data_);
+}
+
+void SerialTreeLearner::PrepareCegbLeaves() {
+  if (!cegb_ || config_->cegb_penalty_feature_lazy.empty()) return;
+  for (int leaf : {smaller_.leaf, larger_.leaf}) {
+    if (leaf < 0) continue;
+    data_size_t cnt = 0;
+    const data_size_t* rows = HostLeafRows(leaf, &cnt);
+    cegb_->PrepareLeaf(leaf, rows, cnt);
+  }
 }
 
 void SerialTreeLearner::ResetConfig(const Config* config) {
@@ -91,6 +105,7 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
   col_sampler_.SetConfig(config_);
   constraints_.Init(config_->num_leaves);
   InitFeatureMeta();
+  SetupCegb();
 }
 
 void SerialTreeLearner::SetForcedSplit(const std::string& json_text) {
@@ -265,6 +280,7 @@ bool SerialTreeLearner::EvalFeature(hist_t* hist, int inner, const SplitParams& 
                     &ns, &splittable);
   ns.feature = data_->RealFeatureIndex(inner);
   ns.inner_feature = inner;
+  if (cegb_) ns.gain -= cegb_->DeltaGain(inner, ns.feature, ls.leaf, ls.num_data, ns);
   if (ns.monotone_type != 0) {
     // reference: penalty by the leaf's depth in the tree being grown
     ns.gain *= MonotoneSplitPenalty(depth, config_->monotone_penalty);
@@ -276,6 +292,7 @@ bool SerialTreeLearner::EvalFeature(hist_t* hist, int inner, const SplitParams& 
 void SerialTreeLearner::FindBestSplitsFromHistograms(const std::vector<int8_t>& used, bool use_subtract,
                                                      const Tree* tree) {
   common::ScopedTimer timer("SerialTreeLearner::FindBestSplitsFromHistograms");
+  PrepareCegbLeaves();
   auto small_node = col_sampler_.GetByNode(tree, smaller_.leaf);
   std::vector<int8_t> large_node;
   if (larger_.leaf >= 0) large_node = col_sampler_.GetByNode(tree, larger_.leaf);
@@ -367,6 +384,11 @@ void SerialTreeLearner::SplitInner(Tree* tree, int best_leaf, int* left_leaf, in
   common::ScopedTimer timer("SerialTreeLearner::SplitInner");
   SplitInfo& s = best_split_per_leaf_[best_leaf];
   const int inner = data_->InnerFeatureIndex(s.feature);
+  if (cegb_) {
+    data_size_t cnt = 0;
+    const data_size_t* rows = config_->cegb_penalty_feature_lazy.empty() ? nullptr : HostLeafRows(best_leaf, &cnt);
+    cegb_->OnSplit(tree, best_leaf, s, rows, cnt, &best_split_per_leaf_);
+  }
   *left_leaf = best_leaf;
   const int next = tree->NextLeafId();
   const BinMapper* m = data_->FeatureBinMapper(inner);

@@ -9,6 +9,7 @@
 #include <string>
 #include <vector>
 
+#include "cegb.h"
 #include "col_sampler.h"
 #include "lgbm_amd/json.h"
 #include "lgbm_amd/split_info.h"
@@ -67,6 +68,10 @@ class SerialTreeLearner : public TreeLearner {
     return indices_.data() + leaf_begin_[leaf];
   }
   virtual data_size_t PartitionLeaf(int leaf, int inner_feature, const SplitInfo& s, int new_leaf);
+  // the leaf's rows on the host (a device learner first mirrors its partition)
+  virtual const data_size_t* HostLeafRows(int leaf, data_size_t* cnt) { return LeafIndices(leaf, cnt); }
+  void SetupCegb();
+  void PrepareCegbLeaves();  // lazy CEGB costs of the leaves about to be scanned
 
   virtual void BeforeTrain();
   virtual bool BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf);
@@ -95,6 +100,7 @@ class SerialTreeLearner : public TreeLearner {
   SplitParams params_;
   std::vector<FeatureMeta> meta_;
   ColSampler col_sampler_;
+  std::unique_ptr<CostEffectiveGB> cegb_;  // cost-effective gradient boosting (null: off)
   LeafConstraints constraints_;
   std::vector<SplitInfo> best_split_per_leaf_;
 

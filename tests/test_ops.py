@@ -1,0 +1,200 @@
+"""Numerics of the stand-alone device ops (lightgbmv1_amd.ops -> src/capi/ops_api.cpp ->
+the HIP kernels of src/device/) against plain PyTorch float64 references of the same op:
+objective gradients (reference src/objective/*.hpp GetGradients), metrics (reference
+src/metric/*.hpp) and the bagging sampler (reference gbdt.cpp:162-243, Random = LCG
+214013 / 2531011)."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+N = 5000
+
+
+def _data(seed=0, kind="reg"):
+    rng = np.random.RandomState(seed)
+    score = rng.randn(N)
+    if kind == "bin":
+        y = (rng.rand(N) > 0.6).astype(np.float32)
+    elif kind == "pos":
+        y = rng.gamma(2.0, 1.5, N).astype(np.float32) + 0.1
+    elif kind == "prob":
+        y = rng.rand(N).astype(np.float32)
+    else:
+        y = rng.randn(N).astype(np.float32)
+    w = (rng.rand(N) + 0.5).astype(np.float32)
+    return score, y, w
+
+
+def _t(a):
+    return torch.tensor(a, dtype=torch.float64)
+
+
+def _ref_grad(obj, s, y, w, params):
+    """float64 torch reference of the objective's (grad, hess)."""
+    s, y = _t(s), _t(y)
+    w = _t(w) if w is not None else torch.ones_like(s)
+    if obj == "regression":
+        return (s - y) * w, w.clone()
+    if obj == "regression_l1":
+        return torch.sign(s - y) * w, w.clone()
+    if obj == "huber":
+        a = params["alpha"]
+        d = s - y
+        return torch.where(d.abs() <= a, d, torch.sign(d) * a) * w, w.clone()
+    if obj == "fair":
+        c = params["fair_c"]
+        x = s - y
+        return c * x / (x.abs() + c) * w, c * c / (x.abs() + c) ** 2 * w
+    if obj == "poisson":
+        return (torch.exp(s) - y) * w, torch.exp(s + params["poisson_max_delta_step"]) * w
+    if obj == "quantile":
+        a = params["alpha"]
+        return torch.where(s - y >= 0, 1 - a, -a) * w, w.clone()
+    if obj == "gamma":
+        return 1.0 - y / torch.exp(s) * w, y / torch.exp(s) * w
+    if obj == "tweedie":
+        r = params["tweedie_variance_power"]
+        e1, e2 = torch.exp((1 - r) * s), torch.exp((2 - r) * s)
+        return (-y * e1 + e2) * w, (-y * (1 - r) * e1 + (2 - r) * e2) * w
+    if obj == "binary":
+        sig = params.get("sigmoid", 1.0)
+        lab = torch.where(y > 0, 1.0, -1.0).double()
+        resp = -lab * sig / (1 + torch.exp(lab * sig * s))
+        return resp * w, resp.abs() * (sig - resp.abs()) * w
+    if obj == "cross_entropy":
+        z = torch.sigmoid(s)
+        return (z - y) * w, z * (1 - z) * w
+    raise KeyError(obj)
+
+
+GRAD_CASES = [
+    ("regression", "reg", {}), ("regression_l1", "reg", {}), ("huber", "reg", {"alpha": 0.7}),
+    ("fair", "reg", {"fair_c": 1.3}), ("poisson", "pos", {"poisson_max_delta_step": 0.7}),
+    ("quantile", "reg", {"alpha": 0.3}), ("gamma", "pos", {}), ("tweedie", "pos", {"tweedie_variance_power": 1.4}),
+    ("binary", "bin", {"sigmoid": 1.7}), ("cross_entropy", "prob", {}),
+]
+
+
+@pytest.mark.parametrize("obj,kind,params", GRAD_CASES, ids=[c[0] for c in GRAD_CASES])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_gradients_match_torch(obj, kind, params, weighted, gpu_available):
+    from lightgbmv1_amd import ops
+    s, y, w = _data(kind=kind)
+    w = w if weighted else None
+    p = dict(params, objective=obj, verbose=-1)
+    g, h = ops.gradients(p, torch.tensor(s, device="cuda"), y, w)
+    rg, rh = _ref_grad(obj, s, y, w, params)
+    # the kernels compute in float64 and store float32 (score_t)
+    np.testing.assert_allclose(g.cpu().double().numpy(), rg.float().double().numpy(), rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(h.cpu().double().numpy(), rh.float().double().numpy(), rtol=2e-6, atol=1e-6)
+
+
+def test_multiclass_softmax_gradients_match_torch(gpu_available):
+    from lightgbmv1_amd import ops
+    K = 4
+    rng = np.random.RandomState(1)
+    score = rng.randn(K, N)
+    y = rng.randint(0, K, N).astype(np.float32)
+    g, h = ops.gradients({"objective": "multiclass", "num_class": K, "verbose": -1},
+                         torch.tensor(score, device="cuda"), y)
+    p = torch.softmax(_t(score), dim=0)
+    onehot = torch.nn.functional.one_hot(torch.tensor(y, dtype=torch.long), K).T.double()
+    rg = p - onehot
+    rh = K / (K - 1.0) * p * (1 - p)
+    np.testing.assert_allclose(g.cpu().double().numpy(), rg.numpy(), rtol=2e-6, atol=1e-6)
+    np.testing.assert_allclose(h.cpu().double().numpy(), rh.numpy(), rtol=2e-6, atol=1e-6)
+
+
+def _ref_auc(s, y, w):
+    """weighted AUC with ties counted one half (Mann-Whitney), float64 torch."""
+    s, y, w = _t(s), _t(y), _t(w)
+    order = torch.argsort(s)
+    s, y, w = s[order], y[order], w[order]
+    pos_w = torch.where(y > 0, w, 0.0)
+    neg_w = torch.where(y > 0, 0.0, w)
+    uniq, inv = torch.unique_consecutive(s, return_inverse=True)
+    pw = torch.zeros(len(uniq), dtype=torch.float64).index_add_(0, inv, pos_w)
+    nw = torch.zeros(len(uniq), dtype=torch.float64).index_add_(0, inv, neg_w)
+    neg_below = torch.cumsum(nw, 0) - nw
+    acc = (pw * (neg_below + 0.5 * nw)).sum()
+    return float(acc / (pw.sum() * nw.sum()))
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_metrics_match_torch(weighted, gpu_available):
+    from lightgbmv1_amd import ops
+    s, y, w = _data(kind="bin")
+    s = np.round(s, 1)  # plenty of ties for the AUC
+    w = w if weighted else None
+    ww = w if w is not None else np.ones(N, np.float32)
+    ds = torch.tensor(s, device="cuda")
+    prob = torch.sigmoid(_t(s))
+    tw, ty = _t(ww), _t(y)
+    ref = {
+        "auc": _ref_auc(s, y, ww),
+        "binary_logloss": float((-(ty * torch.log(prob.clamp_min(1e-15)) +
+                                   (1 - ty) * torch.log((1 - prob).clamp_min(1e-15))) * tw).sum() / tw.sum()),
+        "binary_error": float((((prob > 0.5).double() != ty).double() * tw).sum() / tw.sum()),
+    }
+    for name, r in ref.items():
+        v = ops.metric({"metric": name, "objective": "binary", "verbose": -1}, ds, y, w)
+        assert abs(v - r) < 1e-9 * max(1.0, abs(r)), (name, v, r)
+    sr, yr, _ = _data(kind="reg")
+    dr = torch.tensor(sr, device="cuda")
+    d = _t(sr) - _t(yr)
+    for name, r in {"l2": float((d * d * tw).sum() / tw.sum()), "l1": float((d.abs() * tw).sum() / tw.sum()),
+                    "rmse": float(torch.sqrt((d * d * tw).sum() / tw.sum()))}.items():
+        v = ops.metric({"metric": name, "objective": "regression", "verbose": -1}, dr, yr, w)
+        assert abs(v - r) < 1e-9 * max(1.0, abs(r)), (name, v, r)
+
+
+def _ref_bag(n, fraction, seed):
+    """the reference's bagging: generator Random(seed + b) per 1024-row block b."""
+    keep = np.zeros(n, dtype=bool)
+    for b in range((n + 1023) // 1024):
+        x = (seed + b) & 0xFFFFFFFF
+        for r in range(b * 1024, min(n, (b + 1) * 1024)):
+            x = (214013 * x + 2531011) & 0xFFFFFFFF
+            keep[r] = ((x >> 16) & 0x7FFF) / 32768.0 < fraction
+    return np.nonzero(keep)[0], np.nonzero(~keep)[0]
+
+
+@pytest.mark.parametrize("fraction,seed", [(0.5, 3), (0.9, 17), (0.1, 12345)])
+def test_bagging_matches_reference_generator(fraction, seed, gpu_available):
+    from lightgbmv1_amd import ops
+    n = 10 * 1024 + 77
+    bag, oob = ops.sample_rows(n, fraction=fraction, seed=seed)
+    rb, ro = _ref_bag(n, fraction, seed)
+    np.testing.assert_array_equal(bag.cpu().numpy(), rb)
+    np.testing.assert_array_equal(oob.cpu().numpy(), ro)
+
+
+def test_goss_keeps_top_rows_and_rescales(gpu_available):
+    """GOSS per 1024-row block: the top_rate largest |g*h| are kept as they are, other_rate
+    of the rest are sampled and multiplied by (cnt - top_k) / other_k."""
+    from lightgbmv1_amd import ops
+    n = 4 * 1024
+    rng = np.random.RandomState(5)
+    g0 = rng.randn(n).astype(np.float32)
+    h0 = (rng.rand(n) + 0.1).astype(np.float32)
+    g, h = torch.tensor(g0, device="cuda"), torch.tensor(h0, device="cuda")
+    bag, _ = ops.sample_rows(n, goss=True, top_rate=0.2, other_rate=0.1, grad=g, hess=h, seed=9)
+    bag = bag.cpu().numpy()
+    gn, hn = g.cpu().numpy(), h.cpu().numpy()
+    top_k, other_k = int(1024 * 0.2), int(1024 * 0.1)
+    mult = np.float32(1024 - top_k) / other_k
+    for b in range(4):
+        rows = np.arange(b * 1024, (b + 1) * 1024)
+        wt = np.abs(g0[rows] * h0[rows])
+        thr = np.sort(wt)[::-1][top_k - 1]
+        top = rows[wt >= thr]
+        inbag = bag[(bag >= rows[0]) & (bag <= rows[-1])]
+        assert set(top) <= set(inbag)
+        small = np.setdiff1d(inbag, top)
+        assert len(small) == other_k
+        np.testing.assert_allclose(gn[small], g0[small] * mult, rtol=1e-6)
+        np.testing.assert_allclose(hn[small], h0[small] * mult, rtol=1e-6)
+        np.testing.assert_array_equal(gn[top], g0[top])
