@@ -29,32 +29,9 @@ BASELINE_SEC_PER_ITER = 0.232  # GTX 1080, Higgs 10.5M x 28, 255 bins (BASELINE.
 
 
 def make_rows(start, count, num_features=28, seed=20240601):
-    """Deterministic synthetic Higgs-like rows [start, start+count)."""
-    block = 1 << 20
-    X = np.empty((count, num_features), dtype=np.float32)
-    y = np.empty(count, dtype=np.float32)
-    done = 0
-    while done < count:
-        gidx = start + done
-        b = gidx // block
-        off = gidx % block
-        n = min(count - done, block - off)
-        rng = np.random.default_rng(seed + b)
-        low = rng.standard_normal((block, 21), dtype=np.float32)[off:off + n]
-        low[:, 0::3] = np.abs(low[:, 0::3]) * 0.7 + 0.3          # momenta-like (positive, skewed)
-        low[:, 1::3] = np.clip(low[:, 1::3], -2.5, 2.5)          # pseudo-rapidities
-        low[:, 2::3] = np.tanh(low[:, 2::3]) * 1.74              # angles
-        m = np.empty((n, num_features - 21), dtype=np.float32)   # high-level invariant masses
-        for j in range(num_features - 21):
-            a, c = low[:, (3 * j) % 21], low[:, (3 * j + 3) % 21]
-            m[:, j] = np.sqrt(np.abs(a * c * (1.0 + np.cos(low[:, (3 * j + 2) % 21] - low[:, (3 * j + 5) % 21]))))
-        X[done:done + n, :21] = low
-        X[done:done + n, 21:] = m
-        noise = np.random.default_rng(seed + 7919 + b).standard_normal(block, dtype=np.float32)[off:off + n]
-        logit = (1.2 * m[:, 0] - 0.8 * m[:, 1] + 0.6 * m[:, 2] * low[:, 0] - 0.5 * low[:, 3] ** 2
-                 + 0.4 * np.sin(2.0 * low[:, 4]) + 0.3 * m[:, 3] * m[:, 4] - 0.9 + 0.8 * noise)
-        y[done:done + n] = (logit > 0).astype(np.float32)
-        done += n
+    """Deterministic synthetic Higgs-like rows [start, start+count) (models/workloads.py)."""
+    from lightgbmv1_amd.models.workloads import make_higgs
+    X, y, _ = make_higgs(count, seed=seed, start=start, num_features=num_features)
     return X, y
 
 

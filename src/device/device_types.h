@@ -48,7 +48,7 @@ struct Params {
   double monotone_penalty;
   int32_t data_parallel;  // leaf sizes/decisions from global (split-estimated) counts
   int32_t max_feature_bins;  // max stored bins of one feature (split-scan LDS staging)
-  int32_t has_cat;           // some feature is categorical (split-scan instantiation)
+  int32_t has_cat;           // number of categorical features (KArgs::cat_list; their own split-scan kernel)
   int32_t direct_from_split; // splits >= this have no reduce kernel: the split scan sums the partials
 };
 

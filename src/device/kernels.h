@@ -58,6 +58,7 @@ struct KArgs {
   // parent_flags is the parent's row, snapshot by the partition kernel
   int8_t* splittable;        // [num_leaves][num_features]
   int8_t* parent_flags;      // [num_features]
+  const int32_t* cat_list;   // [Params::has_cat] the categorical features
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

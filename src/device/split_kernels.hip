@@ -364,10 +364,16 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
 }
 
 // LDS of the categorical scan: per-bin ctr and the stable ctr order
+constexpr int kCatPar = 128;  // prefix positions per direction scanned with the parallel path
+
 struct CatScratch {
   double ctr[kFindMaxCatBins];
   int sorted[kFindMaxCatBins];
   int used_bin;
+  // parallel prefix scan: per direction and position, the bin's then the cumulative
+  // (g, h, count) and the split gain there
+  double pg[2][kCatPar], ph[2][kCatPar], gain[2][kCatPar];
+  int pc[2][kCatPar], cnt[2][kCatPar];
 };
 
 // categorical split of one feature (reference FindBestThresholdCategoricalInner,
@@ -376,7 +382,7 @@ struct CatScratch {
 // computed in parallel -- and the sequential prefix scan from both ends (<= 2 x
 // max_cat_threshold steps, thread 0) with the min_data_per_group rules.
 // returns splittable (meaningful in thread 0)
-__device__ __noinline__ bool FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
+__device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
                                      FeatureBest* out, uint32_t* cat_out, BlockScratch* sc, CatScratch* cs) {
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
@@ -470,8 +476,71 @@ __device__ __noinline__ bool FindCategoricalBlock(const Feature& F, HistView hv,
     double d0 = 0.0, d1 = 0.0;
     BlockSum3(d0, d1, ncand, sc);
     const int used_bin = ncand;
-    if (tid == 0) {
-      const int max_num_cat = min(p.max_cat_threshold, (used_bin + 1) / 2);
+    const int max_num_cat = min(p.max_cat_threshold, (used_bin + 1) / 2);
+    const int npos = min(used_bin, max_num_cat);
+    if (npos <= kCatPar) {
+      // (1) every thread stages one position's bin statistics, (2) one thread per direction
+      // accumulates the prefix sums in the sequential order (bit-identical sums), (3) every
+      // thread evaluates the split gain of one position, (4) thread 0 applies the
+      // order-dependent min_data_per_group rules over the precomputed gains
+      for (int idx = tid; idx < 2 * npos; idx += kFindThreads) {
+        const int o = idx / npos, i = idx % npos;
+        const int t = cs->sorted[o == 0 ? i : used_bin - 1 - i];
+        const double hh = hv.H(t);
+        cs->pg[o][i] = hv.G(t);
+        cs->ph[o][i] = hh;
+        cs->cnt[o][i] = RoundIntD(hh * L.cnt_factor);
+      }
+      __syncthreads();
+      if (tid < 2) {
+        double lg = 0.0, lh = kEpsilon;
+        int lc = 0;
+        for (int i = 0; i < npos; ++i) {
+          lg += cs->pg[tid][i];
+          lh += cs->ph[tid][i];
+          lc += cs->cnt[tid][i];
+          cs->pg[tid][i] = lg;
+          cs->ph[tid][i] = lh;
+          cs->pc[tid][i] = lc;
+        }
+      }
+      __syncthreads();
+      for (int idx = tid; idx < 2 * npos; idx += kFindThreads) {
+        const int o = idx / npos, i = idx % npos;
+        const double lg = cs->pg[o][i], lh = cs->ph[o][i];
+        const int lc = cs->pc[o][i];
+        cs->gain[o][i] = SplitGain(lg, lh, L.sg - lg, L.sh - lh, l2, p, L.c, 0, lc, L.n - lc, L.parent_out);
+      }
+      __syncthreads();
+      if (tid == 0) {
+        for (int o = 0; o < 2; ++o) {
+          int cnt_group = 0;
+          for (int i = 0; i < npos; ++i) {
+            const int lc = cs->pc[o][i];
+            const double lh = cs->ph[o][i];
+            cnt_group += cs->cnt[o][i];
+            if (lc < min_n || lh < min_h) continue;
+            const int rc = L.n - lc;
+            if (rc < min_n || rc < p.min_data_per_group) break;
+            if (L.sh - lh < min_h) break;
+            if (cnt_group < p.min_data_per_group) continue;
+            cnt_group = 0;
+            const double gain = cs->gain[o][i];
+            if (gain <= min_gain_shift) continue;
+            splittable = true;
+            if (gain > best.gain) {
+              best.gain = gain;
+              best.thr = i;
+              best.lg = cs->pg[o][i];
+              best.lh = lh;
+              best.lc = lc;
+              best_dir = o == 0 ? 1 : -1;
+            }
+          }
+        }
+        cs->used_bin = used_bin;
+      }
+    } else if (tid == 0) {
       for (int o = 0; o < 2; ++o) {
         const int dir = o == 0 ? 1 : -1;
         int pos = o == 0 ? 0 : used_bin - 1;
@@ -538,15 +607,20 @@ __device__ __noinline__ bool FindCategoricalBlock(const Feature& F, HistView hv,
 
 }  // namespace
 
-// CAT: the dataset has categorical features.  The categorical scan doubles the kernel's
-// registers (and needs a stack), so numerical-only data runs the instantiation without it.
-template <bool ROOT, bool CAT>
+// KIND 0: every feature of a dataset without categorical features; 1: the numerical
+// features of a dataset with some (the categorical ones only get their bookkeeping here);
+// 2: the categorical features (grid over KArgs::cat_list).  The categorical scan has its
+// own register / LDS footprint, so it runs in a kernel of its own (inlined: a called
+// function costs ~700 B/lane of stack and ran ~10x slower).
+template <bool ROOT, int KIND>
 __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
+  constexpr bool CAT = KIND == 2;
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
   __shared__ BlockScratch sc;
   __shared__ typename std::conditional<CAT, CatScratch, int>::type cat_sc;
+  __shared__ unsigned long long s_red[2 * kFindThreads];  // direct partial sums of narrow features
   const long long t_entry = wall_clock64();
-  const int f = blockIdx.x;
+  const int f = CAT ? a.cat_list[blockIdx.x] : static_cast<int>(blockIdx.x);
   const int side = blockIdx.y;
   const int tid = threadIdx.x;
   // ---- independent loads first (one round trip): the feature, its mask, the scales and the
@@ -575,7 +649,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   int parity = 0, nblk_direct = -1;
   if (!ROOT) {
     if (done) return;
-    if (f == 0 && side == 0 && tid == 0) {
+    if (!CAT && f == 0 && side == 0 && tid == 0) {
       // the partition cursors were final for the histogram kernel: reset for the next split
       // (the reduce kernel, not launched for late splits, used to do it)
       a.st->cur_left = 0;
@@ -583,7 +657,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     }
     parity = (s + 1) & 1;
     // zero this feature's bins of the buffer the next step reduces into
-    if (side == 0) {
+    if (!CAT && side == 0) {
       long long* nxt = StepScratch(a, parity + 1);
       for (int i = tid; i < nb2; i += kFindThreads) nxt[2 * F.hist_offset + i] = 0;
     }
@@ -607,7 +681,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     rp.use_smoothing = 0;
     rp.use_mc = 1;
     const double out0 = LeafOutputConstrained(sg, sh, p.lambda_l2, rp, c, n, 0);
-    if (f == 0 && tid == 0) {
+    if (f == 0 && tid == 0 && KIND != 2) {
       Leaf& lf = a.leaves[0];
       lf.sum_g = sg;
       lf.sum_h = sh;
@@ -631,6 +705,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     depth = cl.depth;
     slot = cl.slot;
   }
+  if (KIND == 1 && F.is_cat) return;  // the categorical kernel scans it
   int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : cl.frow) * a.p.num_features;
   if (tree_used && !parent_ok) {
     // the parent could not split on f: neither child evaluates it, the smaller child's row
@@ -660,7 +735,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   o.ncat = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
   // a sampled-out feature (bynode) still materialises its histogram: descendants subtract it
-  if (tree_used && (!F.is_cat || (CAT && F.num_bin <= kFindMaxCatBins))) {
+  if (tree_used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
@@ -668,9 +743,42 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     const bool stage = a.p.max_feature_bins <= kFindLdsBins;
     double* sg = s_bins;
     double* sh = s_bins + (stage ? a.p.max_feature_bins : 0);
+    // a feature with fewer bins than threads sums its direct partials with every thread:
+    // kFindThreads / nbf threads per bin stride over the row blocks, then combine in LDS
+    // (one thread per bin walking hundreds of partials would be a chain of round trips)
+    const bool spread = nblk_direct > 1 && 2 * nbf <= kFindThreads;
+    if (spread) {
+      for (int j = tid; j < 2 * nbf; j += kFindThreads) s_red[j] = 0ull;
+      __syncthreads();
+      const int per = kFindThreads / nbf;
+      const int i = tid % nbf, r = tid / nbf;
+      if (r < per) {
+        constexpr int kC = 8;
+        long long g = 0, h = 0;
+        for (int k0 = r; k0 < nblk_direct; k0 += per * kC) {
+          unsigned long long v[kC];
+#pragma unroll
+          for (int c = 0; c < kC; ++c) {
+            const int k = k0 + c * per;
+            v[c] = k < nblk_direct ? part[static_cast<size_t>(k) * a.p.total_bins + i] : 0ull;
+          }
+#pragma unroll
+          for (int c = 0; c < kC; ++c) {
+            g += static_cast<long long>(v[c]) >> 32;
+            h += static_cast<long long>(v[c] & 0xffffffffull);
+          }
+        }
+        atomicAdd(&s_red[2 * i], static_cast<unsigned long long>(g));
+        atomicAdd(&s_red[2 * i + 1], static_cast<unsigned long long>(h));
+      }
+      __syncthreads();
+    }
     for (int i = tid; i < nbf; i += kFindThreads) {
       long long g = 0, h = 0;
-      if (nblk_direct >= 0) {
+      if (spread) {
+        g = static_cast<long long>(s_red[2 * i]);
+        h = static_cast<long long>(s_red[2 * i + 1]);
+      } else if (nblk_direct >= 0) {
         // small leaf: sum the few per-workgroup partials here (k_hist_reduce skipped them)
         // chunks of kReduceChunk independent loads in flight
         for (int k0 = 0; k0 < nblk_direct; k0 += kReduceChunk) {
@@ -716,13 +824,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     hv.inv_h = ih;
     bool splittable;
     if constexpr (CAT) {
-      if (F.is_cat) {
-        splittable = FindCategoricalBlock(
-            F, hv, L, p, &o, a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
-            &cat_sc);
-      } else {
-        splittable = FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
-      }
+      splittable = FindCategoricalBlock(
+          F, hv, L, p, &o, a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
+          &cat_sc);
     } else {
       splittable = FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
     }
@@ -740,16 +844,18 @@ static size_t FindLds(const KArgs& a) {
 }
 void FindRoot(const KArgs& a, hipStream_t s) {
   if (a.p.has_cat) {
-    hipLaunchKernelGGL((k_find<true, true>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
+    hipLaunchKernelGGL((k_find<true, 1>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
+    hipLaunchKernelGGL((k_find<true, 2>), dim3(a.p.has_cat, 1), dim3(kFindThreads), FindLds(a), s, a);
   } else {
-    hipLaunchKernelGGL((k_find<true, false>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
+    hipLaunchKernelGGL((k_find<true, 0>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
   }
 }
 void FindStep(const KArgs& a, hipStream_t s) {
   if (a.p.has_cat) {
-    hipLaunchKernelGGL((k_find<false, true>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
+    hipLaunchKernelGGL((k_find<false, 1>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
+    hipLaunchKernelGGL((k_find<false, 2>), dim3(a.p.has_cat, 2), dim3(kFindThreads), FindLds(a), s, a);
   } else {
-    hipLaunchKernelGGL((k_find<false, false>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
+    hipLaunchKernelGGL((k_find<false, 0>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
   }
 }
 

@@ -307,8 +307,16 @@ void GPUTreeLearner::UploadData() {
   // enough for the split scan to sum their partial histograms (LGBM_AMD_DIRECT_FROM_SPLIT)
   a.p.direct_from_split = 16;
   if (const char* e = std::getenv("LGBM_AMD_DIRECT_FROM_SPLIT")) a.p.direct_from_split = std::atoi(e);
-  a.p.has_cat = 0;
-  for (const auto& F : feats) a.p.has_cat |= F.is_cat;
+  std::vector<int32_t> cats;
+  for (int f = 0; f < num_features_; ++f) {
+    if (feats[f].is_cat) cats.push_back(f);
+  }
+  a.p.has_cat = static_cast<int32_t>(cats.size());
+  d_cat_list_ = Alloc<int32_t>(std::max<size_t>(1, cats.size()));
+  if (!cats.empty()) {
+    HIPCHECK(hipMemcpy(d_cat_list_, cats.data(), sizeof(int32_t) * cats.size(), hipMemcpyHostToDevice));
+  }
+  a.cat_list = d_cat_list_;
   // per-workgroup row cap of the histogram kernels (fixed-point headroom): see k_hist
   rows_cap_ = std::max(dev::kHistMinRows * 4, (num_data_ + hist_blocks - 1) / hist_blocks);
   a.hist_rows_cap = rows_cap_;

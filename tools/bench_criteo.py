@@ -25,27 +25,8 @@ REF_SEC_PER_TREE_8_MACHINES = 80.0   # 1.7B rows, 8 machines (:237)
 
 
 def make_ctr(num_rows, seed):
-    rng = np.random.default_rng(seed)
-    X = np.zeros((num_rows, 67), dtype=np.float32)
-    y = np.empty(num_rows, dtype=np.float32)
-    wd = np.random.default_rng(99).normal(0, 0.35, size=13).astype(np.float32)
-    ws = np.random.default_rng(98).normal(0, 0.8, size=54).astype(np.float32)
-    dens = np.random.default_rng(97).uniform(0.005, 0.03, size=54)
-    chunk = 1 << 21
-    for s in range(0, num_rows, chunk):
-        e = min(num_rows, s + chunk)
-        n = e - s
-        d = np.floor(rng.pareto(1.5, size=(n, 13)).astype(np.float32) * 3.0)
-        X[s:e, :13] = d
-        logit = np.log1p(d) @ wd - 3.6
-        for j in range(54):
-            nz = rng.random(n) < dens[j]
-            cnt = nz.sum()
-            if cnt:
-                v = np.floor(rng.pareto(1.2, size=cnt).astype(np.float32) * 5.0) + 1.0
-                X[s:e, 13 + j][nz] = v
-                logit[nz] += ws[j] * np.log1p(v)
-        y[s:e] = (rng.random(n) < 1.0 / (1.0 + np.exp(-logit))).astype(np.float32)
+    from lightgbmv1_amd.models.workloads import make_criteo
+    X, y, _ = make_criteo(num_rows, seed)
     return X, y
 
 

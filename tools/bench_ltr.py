@@ -25,32 +25,8 @@ BASELINE_SEC_PER_ITER = 111.0 / 500
 
 
 def make_ltr(num_rows, num_features, seed):
-    rng = np.random.default_rng(seed)
-    sizes = rng.integers(20, 221, size=num_rows // 60 + 16)
-    cum = np.cumsum(sizes)
-    nq = int(np.searchsorted(cum, num_rows)) + 1
-    sizes = sizes[:nq].copy()
-    sizes[-1] -= int(cum[nq - 1] - num_rows)
-    qid = np.repeat(np.arange(nq), sizes)
-    q_off = rng.normal(0.0, 0.7, size=nq).astype(np.float32)
-    # the relevance function is shared by the training and held-out sets
-    w = np.random.default_rng(12345).normal(0.0, 1.0, size=40).astype(np.float32) / np.sqrt(40)
-    X = np.empty((num_rows, num_features), dtype=np.float32)
-    rel = np.empty(num_rows, dtype=np.float32)
-    chunk = 1 << 19
-    n_dense = 40 + (num_features - 40) * 6 // 10
-    for s in range(0, num_rows, chunk):
-        e = min(num_rows, s + chunk)
-        n = e - s
-        inf = rng.standard_normal((n, 40), dtype=np.float32)
-        X[s:e, :40] = inf
-        X[s:e, 40:n_dense] = rng.standard_normal((n, n_dense - 40), dtype=np.float32)
-        sp = rng.poisson(0.15, size=(n, num_features - n_dense)).astype(np.float32)
-        X[s:e, n_dense:] = sp
-        rel[s:e] = inf @ w + q_off[qid[s:e]] + 0.6 * rng.standard_normal(n, dtype=np.float32)
-    cuts = np.quantile(rel, [0.50, 0.80, 0.95, 0.98])
-    y = np.searchsorted(cuts, rel).astype(np.float32)
-    return X, y, sizes
+    from lightgbmv1_amd.models.workloads import make_ltr as _make
+    return _make(num_rows, seed, num_features=num_features)
 
 
 def ndcg_at(y, p, group, k=10):
