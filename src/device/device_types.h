@@ -61,7 +61,7 @@ struct Leaf {
   int32_t slot;          // histogram slot
   int32_t buf;           // which index buffer (KArgs::idx / tmp) holds the leaf's rows
   int32_t frow;          // row of KArgs::splittable (kept across trees)
-  int32_t pad_;
+  uint32_t icmask;       // interaction constraints consistent with the leaf's branch (bit k: constraint k)
   double sum_g, sum_h, output;
   double cmin, cmax;  // monotone constraint range
 };
@@ -71,7 +71,8 @@ struct Leaf {
 struct ChildStats {
   double sum_g, sum_h, output, cmin, cmax;
   int32_t global_count, depth, slot, leaf;
-  int32_t frow, pad_;  // splittable row the child's scan writes
+  int32_t frow;        // splittable row the child's scan writes
+  uint32_t icmask;     // Leaf::icmask
 };
 
 // the split being applied, as chosen by the partition kernel's pick

@@ -120,6 +120,7 @@ __device__ void StepBookkeeping(const KArgs& a, Step* st) {
     to.global_count = a.p.data_parallel ? from.global_count : (lr == 0 ? c.left_count : c.right_count);
     to.slot = swap ? (lr == 0 ? nl : cs.parent_slot) : from.slot;
     to.frow = k == 0 ? cs.new_frow : cs.parent_frow;  // the larger child inherits the parent's row
+    to.icmask = from.icmask;
   }
   a.best[leaf].gain = -INFINITY;
   a.best[leaf].feature = -1;

@@ -59,6 +59,9 @@ struct KArgs {
   int8_t* splittable;        // [num_leaves][num_features]
   int8_t* parent_flags;      // [num_features]
   const int32_t* cat_list;   // [Params::has_cat] the categorical features
+  // interaction constraints (<= 32): bit k set iff constraint k holds the feature, or null.
+  // A leaf may split on f iff (Leaf::icmask & feat_icmask[f]) != 0 (ColSampler::GetByNode)
+  const uint32_t* feat_icmask;  // [num_features]
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

@@ -94,6 +94,7 @@ __global__ void k_tree_begin(KArgs a) {
     lf.sum_g = lf.sum_h = lf.output = 0.0;
     lf.cmin = -DBL_MAX;
     lf.cmax = DBL_MAX;
+    lf.icmask = 0xffffffffu;  // the root may use every constraint
     a.leaves[l] = lf;
     a.best[l].gain = -INFINITY;
     a.best[l].feature = -1;

@@ -242,7 +242,10 @@ __device__ void RecordSplit(const KArgs& a, Step* st, const PickResult& pk) {
       rmin = fmax(rmin, mid);
     }
   }
+  // both children keep the constraints that also hold the split feature
+  const uint32_t icm = a.feat_icmask != nullptr ? P.icmask & a.feat_icmask[sp.feature] : 0xffffffffu;
   ChildStats lc, rc;
+  lc.icmask = rc.icmask = icm;
   lc.sum_g = sp.left_sum_gradient;
   lc.sum_h = sp.left_sum_hessian;
   lc.output = sp.left_output;
@@ -277,6 +280,7 @@ __device__ void RecordSplit(const KArgs& a, Step* st, const PickResult& pk) {
   RL->global_count = rc.global_count;
   RL->cmin = rmin;
   RL->cmax = rmax;
+  PL->icmask = RL->icmask = icm;
   st->lr[0] = lc;
   st->lr[1] = rc;
   CurSplit& cs = st->cs;

@@ -706,6 +706,9 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     slot = cl.slot;
   }
   if (KIND == 1 && F.is_cat) return;  // the categorical kernel scans it
+  // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
+  // here but keeps its histogram and its splittable flag
+  if (a.feat_icmask != nullptr && ((ROOT ? 0xffffffffu : cl.icmask) & a.feat_icmask[f]) == 0u) used = 0;
   int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : cl.frow) * a.p.num_features;
   if (tree_used && !parent_ok) {
     // the parent could not split on f: neither child evaluates it, the smaller child's row
@@ -747,6 +750,13 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     // kFindThreads / nbf threads per bin stride over the row blocks, then combine in LDS
     // (one thread per bin walking hundreds of partials would be a chain of round trips)
     const bool spread = nblk_direct > 1 && 2 * nbf <= kFindThreads;
+    // the larger child's parent bins (first bin of each thread): loaded up front, so their
+    // round trip overlaps the partial-sum loads instead of following them
+    long long pg0 = 0, ph0 = 0;
+    if (side == 1 && tid < nbf) {
+      pg0 = dst[2 * tid];
+      ph0 = dst[2 * tid + 1];
+    }
     if (spread) {
       for (int j = tid; j < 2 * nbf; j += kFindThreads) s_red[j] = 0ull;
       __syncthreads();
@@ -797,8 +807,8 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
         h = src[2 * i + 1];
       }
       if (side == 1) {  // larger child = parent - smaller, in the parent's (now its) slot
-        g = dst[2 * i] - g;
-        h = dst[2 * i + 1] - h;
+        g = (i == tid ? pg0 : dst[2 * i]) - g;
+        h = (i == tid ? ph0 : dst[2 * i + 1]) - h;
       }
       dst[2 * i] = g;
       dst[2 * i + 1] = h;

@@ -317,6 +317,22 @@ void GPUTreeLearner::UploadData() {
     HIPCHECK(hipMemcpy(d_cat_list_, cats.data(), sizeof(int32_t) * cats.size(), hipMemcpyHostToDevice));
   }
   a.cat_list = d_cat_list_;
+  // interaction constraints as per-feature constraint bitmasks (device-resident growth
+  // supports up to 32 constraints, see DecideMode)
+  const auto& ic = config_->interaction_constraints_vector;
+  a.feat_icmask = nullptr;
+  if (!ic.empty() && ic.size() <= 32) {
+    std::vector<uint32_t> icm(std::max(1, num_features_), 0u);
+    for (int f = 0; f < num_features_; ++f) {
+      const int real = data_->RealFeatureIndex(f);
+      for (size_t k = 0; k < ic.size(); ++k) {
+        if (std::find(ic[k].begin(), ic[k].end(), real) != ic[k].end()) icm[f] |= 1u << k;
+      }
+    }
+    d_feat_icmask_ = Alloc<uint32_t>(icm.size());
+    HIPCHECK(hipMemcpy(d_feat_icmask_, icm.data(), sizeof(uint32_t) * icm.size(), hipMemcpyHostToDevice));
+    a.feat_icmask = d_feat_icmask_;
+  }
   // per-workgroup row cap of the histogram kernels (fixed-point headroom): see k_hist
   rows_cap_ = std::max(dev::kHistMinRows * 4, (num_data_ + hist_blocks - 1) / hist_blocks);
   a.hist_rows_cap = rows_cap_;
@@ -397,7 +413,11 @@ void GPUTreeLearner::DecideMode() {
     const BinMapper* m = data_->FeatureBinMapper(f);
     if (m->bin_type() == BinType::Categorical && m->num_bin() > dev::kFindMaxCatBins) dm = false;
   }
-  if (has_forced_split_ || !config_->interaction_constraints_vector.empty() || config_->extra_trees ||
+  // interaction constraints: on the device up to 32 constraints without per-node sampling
+  // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
+  const auto& ic = config_->interaction_constraints_vector;
+  if (!ic.empty() && (ic.size() > 32 || config_->feature_fraction_bynode < 1.0)) dm = false;
+  if (has_forced_split_ || config_->extra_trees ||
       (config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
       config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
       !config_->cegb_penalty_feature_lazy.empty() || !config_->cegb_penalty_feature_coupled.empty()) {

@@ -127,6 +127,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int8_t* d_splittable_ = nullptr;      // [num_leaves][num_features] (KArgs::splittable)
   int8_t* d_parent_flags_ = nullptr;    // [num_features]
   int32_t* d_cat_list_ = nullptr;       // categorical features (KArgs::cat_list)
+  uint32_t* d_feat_icmask_ = nullptr;   // KArgs::feat_icmask
   std::vector<int8_t> h_node_mask_;     // (kept alive for the async upload)
   dev::GH* d_gh_ = nullptr;
   int32_t* d_idx_ = nullptr;

@@ -325,8 +325,10 @@ def test_device_batch_prediction_matches_host(gpu_available, kind, monkeypatch):
     {"feature_fraction": 0.6, "feature_fraction_seed": 4},
     {"feature_fraction_bynode": 0.5, "feature_fraction_seed": 5},
     {"feature_fraction": 0.8, "feature_fraction_bynode": 0.6, "feature_fraction_seed": 6},
+    {"interaction_constraints": [[0, 1, 2], [3, 5, 7], [1, 6]]},
+    {"interaction_constraints": [[0, 1, 2], [2, 3, 4, 7]], "feature_fraction": 0.7, "feature_fraction_seed": 3},
 ], ids=["l1l2", "max_delta_step", "path_smooth", "min_gain", "max_depth", "monotone", "zero_missing",
-        "feature_fraction", "bynode", "bytree_bynode"])
+        "feature_fraction", "bynode", "bytree_bynode", "interaction", "interaction_bytree"])
 def test_device_split_rules_match_cpu(gpu_available, extra):
     """The device split scan applies the reference's split rules like the CPU learner: same
     first-tree splits near the root, and closely matching fits."""
@@ -351,3 +353,37 @@ def test_device_split_rules_match_cpu(gpu_available, extra):
         assert a["threshold"] == pytest.approx(b["threshold"])
     pc, pg = boosters["cpu"].predict(X[:5000]), boosters["gpu"].predict(X[:5000])
     assert np.corrcoef(pc, pg)[0, 1] > 0.99
+
+
+def _branches(node, path=()):
+    if "split_feature" not in node:
+        yield path
+        return
+    p = path + (node["split_feature"],)
+    yield from _branches(node["left_child"], p)
+    yield from _branches(node["right_child"], p)
+
+
+def test_interaction_constraints_device_resident(gpu_available, monkeypatch):
+    """Interaction constraints run in device-resident growth (per-leaf constraint bitmasks,
+    reference col_sampler.hpp:92-126): every root-to-leaf branch uses features of one
+    constraint, and the trees equal the host-assisted learner's (same device histograms,
+    host split loop)."""
+    X, y = _data(30000, seed=5)
+    ic = [[0, 1, 2], [3, 5, 7], [1, 6]]
+    models = {}
+    for mode in ("device", "host"):
+        if mode == "host":
+            monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+        b = _train(X, y, "gpu", rounds=8, interaction_constraints=ic)
+        monkeypatch.delenv("LGBM_AMD_HOST_ASSIST", raising=False)
+        models[mode] = b
+        for t in b.dump_model()["tree_info"]:
+            for br in _branches(t["tree_structure"]):
+                assert any(set(br) <= set(c) for c in ic), br
+    dt = models["device"].dump_model()["tree_info"]
+    ht = models["host"].dump_model()["tree_info"]
+    feats = lambda t: sorted(f for br in _branches(t["tree_structure"]) for f in br)
+    assert feats(dt[0]) == feats(ht[0])
+    pd, ph = models["device"].predict(X[:5000]), models["host"].predict(X[:5000])
+    assert np.corrcoef(pd, ph)[0, 1] > 0.995
