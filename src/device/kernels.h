@@ -62,6 +62,11 @@ struct KArgs {
   // interaction constraints (<= 32): bit k set iff constraint k holds the feature, or null.
   // A leaf may split on f iff (Leaf::icmask & feat_icmask[f]) != 0 (ColSampler::GetByNode)
   const uint32_t* feat_icmask;  // [num_features]
+  // extra_trees: each feature's generator state at the tree's start (FeatureMeta::rand) and the
+  // running count of its draws, one row per split step (row 0: the root scan, row s + 1: after
+  // step s; rows of steps not run stay 0), or null
+  const uint32_t* xt_base;   // [num_features]
+  int32_t* xt_cum;           // [num_leaves][num_features]
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

@@ -27,6 +27,8 @@ struct Cand {
   int lc;
 };
 
+constexpr int kNoRandThr = -(1 << 30);  // ScanNumericalBlock: every threshold (no extra_trees draw)
+
 // ties: reverse scan keeps the highest threshold (first met scanning down), forward the lowest
 __device__ __forceinline__ bool CandBetter(const Cand& x, const Cand& y, bool reverse) {
   if (x.gain > y.gain) return true;
@@ -182,7 +184,7 @@ struct HistView {
 // one numerical scan of one feature by one workgroup (each thread owns K consecutive bins)
 __device__ Cand ScanNumericalBlock(const HistView& hv, int nb, int offset, int default_bin, bool reverse,
                                    bool skip_def, bool na, const LeafCtx& L, const SplitParams& p, int mono,
-                                   bool* splittable, BlockScratch* sc) {
+                                   bool* splittable, BlockScratch* sc, int rthr) {
   const int tid = threadIdx.x;
   const int K = (nb + kFindThreads - 1) / kFindThreads;
   const int b0 = tid * K;
@@ -231,6 +233,7 @@ __device__ Cand ScanNumericalBlock(const HistView& hv, int nb, int offset, int d
       const double lh = L.sh - rh;
       if (lh < min_h) continue;
       const double lg = L.sg - rg;
+      if (rthr != kNoRandThr && t - 1 + offset != rthr) continue;  // extra_trees
       const double gain = SplitGain(lg, lh, rg, rh, p.lambda_l2, p, L.c, static_cast<int8_t>(mono), lc, rc,
                                     L.parent_out);
       if (gain <= L.min_gain_shift) continue;
@@ -274,6 +277,7 @@ __device__ Cand ScanNumericalBlock(const HistView& hv, int nb, int offset, int d
       const double rh = L.sh - xh;
       if (rh < min_h) return;
       const double rg = L.sg - xg;
+      if (rthr != kNoRandThr && t + offset != rthr) return;  // extra_trees
       const double gain = SplitGain(xg, xh, rg, rh, p.lambda_l2, p, L.c, static_cast<int8_t>(mono), xc, rc,
                                     L.parent_out);
       if (gain <= L.min_gain_shift) return;
@@ -302,7 +306,7 @@ __device__ Cand ScanNumericalBlock(const HistView& hv, int nb, int offset, int d
 
 // returns whether any threshold was valid (the host's is_splittable)
 __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
-                                   double mono_penalty, FeatureBest* out, BlockScratch* sc) {
+                                   double mono_penalty, FeatureBest* out, BlockScratch* sc, int rthr) {
   const int nb = F.num_bin - F.offset;
   hv.fix_t = -1;
   hv.fix_g = hv.fix_h = 0.0;
@@ -341,14 +345,14 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
   };
   if (F.num_bin > 2 && F.missing_type != 0) {
     if (F.missing_type == 1) {
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, true, false, L, p, F.monotone, &splittable, sc), true);
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, true, false, L, p, F.monotone, &splittable, sc), false);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, true, false, L, p, F.monotone, &splittable, sc, rthr), true);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, true, false, L, p, F.monotone, &splittable, sc, rthr), false);
     } else {
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, true, L, p, F.monotone, &splittable, sc), true);
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, false, true, L, p, F.monotone, &splittable, sc), false);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, true, L, p, F.monotone, &splittable, sc, rthr), true);
+      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, false, true, L, p, F.monotone, &splittable, sc, rthr), false);
     }
   } else {
-    apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, false, L, p, F.monotone, &splittable, sc), true);
+    apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, false, L, p, F.monotone, &splittable, sc, rthr), true);
     if (F.missing_type == 2) out->default_left = 0;
   }
   out->gain *= F.penalty;
@@ -612,6 +616,31 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
 // 2: the categorical features (grid over KArgs::cat_list).  The categorical scan has its
 // own register / LDS footprint, so it runs in a kernel of its own (inlined: a called
 // function costs ~700 B/lane of stack and ran ~10x slower).
+// extra_trees: Random::Step31 applied k times (x -> 214013 x + 2531011), by squaring the map
+__device__ __forceinline__ uint32_t LcgSkip(uint32_t x, int k) {
+  uint32_t am = 214013u, cm = 2531011u, ar = 1u, cr = 0u;
+  while (k > 0) {
+    if (k & 1) {
+      ar = am * ar;
+      cr = am * cr + cm;
+    }
+    cm = am * cm + cm;
+    am = am * am;
+    k >>= 1;
+  }
+  return ar * x + cr;
+}
+
+// extra_trees: whether the host learner scans f at node mi (the feature is used by the tree,
+// its parent could split on it, the node samples it and its constraints allow it) and so
+// draws FeatureMeta::rand.NextInt(0, num_bin - 2) (split_finder.cpp FindNumerical)
+__device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, int mi, uint32_t icmask, bool gate) {
+  if (!gate || F.num_bin - 2 <= 0) return 0;
+  if (a.node_mask != nullptr && !a.node_mask[static_cast<size_t>(mi) * a.p.num_features + f]) return 0;
+  if (a.feat_icmask != nullptr && (icmask & a.feat_icmask[f]) == 0u) return 0;
+  return 1;
+}
+
 template <bool ROOT, int KIND>
 __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   constexpr bool CAT = KIND == 2;
@@ -643,6 +672,24 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     s = st->cs.s;
     s_count = st->s_count;
     cl = st->child[side];  // written with the histogram (StepBookkeeping)
+  }
+  // extra_trees: per feature and node, the smaller child draws before the larger one
+  // (SerialTreeLearner::FindBestSplitsFromHistograms); draw k of the tree is the base state
+  // stepped k times.  The smaller child's workgroup appends the step's count row.
+  int xt_thr = kNoRandThr;
+  if (a.xt_base != nullptr && (ROOT || !done)) {
+    const int nf = a.p.num_features;
+    const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * nf + f];
+    const bool gate = tree_used && parent_ok && !skip;
+    const int d0 = ROOT ? XtDraws(a, F, f, 0, 0xffffffffu, gate)
+                        : XtDraws(a, F, f, st->bynode_base, st->child[0].icmask, gate);
+    const int d1 = ROOT ? 0 : XtDraws(a, F, f, st->bynode_base + 1, st->child[1].icmask, gate);
+    if (side == 0 && tid == 0) a.xt_cum[static_cast<size_t>(ROOT ? 0 : s + 1) * nf + f] = prev + d0 + d1;
+    xt_thr = 0;  // num_bin <= 2: no draw, threshold 0 only
+    if (side == 0 ? d0 : d1) {
+      const uint32_t x = LcgSkip(a.xt_base[f], prev + (side == 1 ? d0 : 0) + 1);
+      xt_thr = static_cast<int>(x & 0x7fffffffu) % (F.num_bin - 2);
+    }
   }
   const int nbf = F.num_bin - F.offset;
   const int nb2 = 2 * nbf;
@@ -838,7 +885,7 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
           F, hv, L, p, &o, a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
           &cat_sc);
     } else {
-      splittable = FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc);
+      splittable = FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc, xt_thr);
     }
     if (tid == 0) flags[f] = splittable ? 1 : 0;
     if (!ROOT) KTrace(a, s, kTrFindScanned);

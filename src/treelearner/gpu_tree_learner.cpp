@@ -219,6 +219,8 @@ void GPUTreeLearner::UploadData() {
   d_tree_mask_ = Alloc<int8_t>(num_features_);
   d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
   h_node_mask_.clear();
+  d_xt_base_ = Alloc<uint32_t>(std::max(1, num_features_));
+  d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
   d_gh_ = Alloc<dev::GH>(num_data_);
   d_idx_ = Alloc<int32_t>(num_data_);
   d_tmp_ = Alloc<int32_t>(num_data_);
@@ -321,6 +323,8 @@ void GPUTreeLearner::UploadData() {
   // supports up to 32 constraints, see DecideMode)
   const auto& ic = config_->interaction_constraints_vector;
   a.feat_icmask = nullptr;
+  a.xt_base = nullptr;
+  a.xt_cum = nullptr;
   if (!ic.empty() && ic.size() <= 32) {
     std::vector<uint32_t> icm(std::max(1, num_features_), 0u);
     for (int f = 0; f < num_features_; ++f) {
@@ -378,6 +382,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     const int n_leaves = config_->num_leaves;
     d_leaves_ = Alloc<dev::Leaf>(n_leaves);
     d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
+    d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
     d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
     d_best_ = Alloc<DeviceSplit>(n_leaves);
     d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
@@ -408,22 +413,28 @@ void GPUTreeLearner::DecideMode() {
   bool dm = true;
   const char* force = std::getenv("LGBM_AMD_HOST_ASSIST");
   if ((force != nullptr && force[0] == '1') || force_host_mode_) dm = false;
+  bool any_cat = false;
   for (int f = 0; f < num_features_ && dm; ++f) {
     // categorical splits are scanned on the device up to kFindMaxCatBins categories
     const BinMapper* m = data_->FeatureBinMapper(f);
+    if (m->bin_type() == BinType::Categorical) any_cat = true;
     if (m->bin_type() == BinType::Categorical && m->num_bin() > dev::kFindMaxCatBins) dm = false;
   }
+  // extra_trees: random numerical thresholds are drawn on the device (categorical draws
+  // depend on the sorted-category scan: host-assisted then)
+  if (config_->extra_trees && any_cat) dm = false;
   // interaction constraints: on the device up to 32 constraints without per-node sampling
   // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
   const auto& ic = config_->interaction_constraints_vector;
   if (!ic.empty() && (ic.size() > 32 || config_->feature_fraction_bynode < 1.0)) dm = false;
-  if (has_forced_split_ || config_->extra_trees ||
+  if (has_forced_split_ ||
       (config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
       config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
       !config_->cegb_penalty_feature_lazy.empty() || !config_->cegb_penalty_feature_coupled.empty()) {
     dm = false;
   }
-  if (dm != device_mode_) {
+  if (dm != device_mode_ || !mode_decided_) {
+    mode_decided_ = true;
     Log::Debug("device learner: %s growth", dm ? "device-resident" : "host-assisted");
   }
   device_mode_ = dm;
@@ -658,6 +669,9 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
     HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
   }
   dev::TreeBegin(a, stream_);
+  if (a.xt_cum != nullptr) {
+    HIPCHECK(hipMemsetAsync(a.xt_cum, 0, sizeof(int32_t) * config_->num_leaves * num_features_, stream_));
+  }
   if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
   AllreduceRoot();
   HIPCHECK(hipMemsetAsync(d_scratch_, 0, scratch_bytes, stream_));
@@ -688,6 +702,19 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     HIPCHECK(hipMemcpyAsync(d_node_mask_, h_node_mask_.data(), h_node_mask_.size(), hipMemcpyHostToDevice, stream_));
     a.node_mask = d_node_mask_;
   }
+  const bool xt = config_->extra_trees;
+  a.xt_base = nullptr;
+  a.xt_cum = nullptr;
+  if (xt) {
+    // each feature's generator state at the tree's start: the split scans derive their draws
+    // from it and the step rows of xt_cum; the host generators catch up after the tree
+    h_xt_base_.resize(num_features_);
+    for (int f = 0; f < num_features_; ++f) h_xt_base_[f] = meta_[f].rand.state();
+    HIPCHECK(hipMemcpyAsync(d_xt_base_, h_xt_base_.data(), sizeof(uint32_t) * num_features_, hipMemcpyHostToDevice,
+                            stream_));
+    a.xt_base = d_xt_base_;
+    a.xt_cum = d_xt_cum_;
+  }
   if (use_bag_) {
     // bag size read on the device: one captured graph serves every bag
     a.num_rows = num_data_;
@@ -714,7 +741,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   if (use_graph) {
     const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
     if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
-        graph_root_mode_ != root_mode) {
+        graph_root_mode_ != root_mode || graph_xt_ != (xt ? 1 : 0)) {
       DestroyGraph();
       hipGraph_t g = nullptr;
       HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
@@ -739,6 +766,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
         graph_rows_ = a.num_rows;
         graph_identity_ = a.root_identity;
         graph_root_mode_ = root_mode;
+        graph_xt_ = xt ? 1 : 0;
       }
     }
     if (graph_exec_ != nullptr) {
@@ -756,6 +784,17 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     // the root's draw happens only if the host learner would have scanned the root
     const bool root_scanned = root_rows_ >= 2 * config_->min_data_in_leaf;
     col_sampler_.AdvanceByNode(root_scanned ? h_step_->bynode_next : 0);
+  }
+  if (xt && root_rows_ >= 2 * config_->min_data_in_leaf) {
+    // replay the draws the split scans made: the rows are running counts, steps not run are 0
+    const int rows = config_->num_leaves;
+    h_xt_cum_.resize(static_cast<size_t>(rows) * num_features_);
+    HIPCHECK(hipMemcpy(h_xt_cum_.data(), d_xt_cum_, sizeof(int32_t) * h_xt_cum_.size(), hipMemcpyDeviceToHost));
+    for (int f = 0; f < num_features_; ++f) {
+      int n = 0;
+      for (int r = 0; r < rows; ++r) n = std::max(n, h_xt_cum_[static_cast<size_t>(r) * num_features_ + f]);
+      for (int k = 0; k < n; ++k) meta_[f].rand.NextInt(0, 2);
+    }
   }
   if (a.ktrace != nullptr) ReportKernelTrace(num_splits);
   if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {

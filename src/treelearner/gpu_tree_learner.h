@@ -112,6 +112,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
 
   bool data_parallel_ = false;
   bool device_mode_ = true;
+  bool mode_decided_ = false;  // the first decision is logged too
   bool force_host_mode_ = false;
   double* d_leaf_sums_ = nullptr;
   int device_id_ = 0;
@@ -129,6 +130,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int32_t* d_cat_list_ = nullptr;       // categorical features (KArgs::cat_list)
   uint32_t* d_feat_icmask_ = nullptr;   // KArgs::feat_icmask
   std::vector<int8_t> h_node_mask_;     // (kept alive for the async upload)
+  uint32_t* d_xt_base_ = nullptr;       // extra_trees: per-feature generator states, tree start
+  int32_t* d_xt_cum_ = nullptr;         // extra_trees: draws per feature after each step
+  std::vector<uint32_t> h_xt_base_;
+  std::vector<int32_t> h_xt_cum_;
   dev::GH* d_gh_ = nullptr;
   int32_t* d_idx_ = nullptr;
   int32_t* d_tmp_ = nullptr;
@@ -155,6 +160,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int graph_rows_ = -1;
   int graph_identity_ = -1;
   int graph_root_mode_ = -1;
+  int graph_xt_ = -1;
   bool graph_capture_failed_ = false;  // RCCL collectives could not be captured: eager trees
   bool gh_fresh_ = false;         // d_gh_ / absmax / root partials written by the gradient kernel
   bool root_from_parts_ = false;  // this tree's gradients came packed from the gradient kernel

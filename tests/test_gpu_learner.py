@@ -387,3 +387,45 @@ def test_interaction_constraints_device_resident(gpu_available, monkeypatch):
     assert feats(dt[0]) == feats(ht[0])
     pd, ph = models["device"].predict(X[:5000]), models["host"].predict(X[:5000])
     assert np.corrcoef(pd, ph)[0, 1] > 0.995
+
+
+def _splits(node):
+    if "split_feature" not in node:
+        return []
+    return ([(node["split_feature"], round(node["threshold"], 6))] + _splits(node["left_child"])
+            + _splits(node["right_child"]))
+
+
+@pytest.mark.parametrize("extra", [
+    {},
+    {"feature_fraction_bynode": 0.6, "feature_fraction_seed": 9},
+    {"interaction_constraints": [[0, 1, 2], [3, 5, 7], [1, 6]]},
+    {"num_leaves": 63, "min_data_in_leaf": 200, "extra_seed": 11},
+], ids=["plain", "bynode", "interaction", "wide_seed"])
+def test_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
+    """extra_trees in device-resident growth: the split scans draw each feature's random
+    threshold from its generator state at the tree's start (reference
+    feature_histogram.hpp:107-110, one Random per feature seeded extra_seed + i), stepped by the
+    draws of earlier nodes; the host generators replay the draws after the tree.  Trees equal
+    the host-assisted learner's (host split loop, host generators) tree for tree, so the
+    generators stay in step across trees."""
+    X, y = _data(30000, seed=13)
+    capfd.readouterr()
+    _train(X[:4000], y[:4000], "gpu", rounds=1, extra_trees=True, verbose=2, **extra)
+    assert "device-resident growth" in capfd.readouterr().out
+    models = {}
+    for mode in ("device", "host"):
+        if mode == "host":
+            monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+        models[mode] = _train(X, y, "gpu", rounds=6, extra_trees=True, **extra)
+        monkeypatch.delenv("LGBM_AMD_HOST_ASSIST", raising=False)
+    dt = models["device"].dump_model()["tree_info"]
+    ht = models["host"].dump_model()["tree_info"]
+    assert len(dt) == len(ht)
+    for i in range(3):
+        assert _splits(dt[i]["tree_structure"]) == _splits(ht[i]["tree_structure"]), i
+    pd, ph = models["device"].predict(X[:5000]), models["host"].predict(X[:5000])
+    assert np.corrcoef(pd, ph)[0, 1] > 0.999
+    # and the fit matches the CPU learner's extra-trees model in quality
+    cpu = _train(X, y, "cpu", rounds=6, extra_trees=True, **extra)
+    assert abs(_auc(y, models["device"].predict(X)) - _auc(y, cpu.predict(X))) < 0.01
