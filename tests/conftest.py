@@ -3,6 +3,12 @@ import sys
 
 import pytest
 
+# under pytest-xdist, give each worker its share of the cores: every worker's OpenMP pool
+# spinning on all of them oversubscribes the machine (set before the library loads)
+if os.environ.get("PYTEST_XDIST_WORKER_COUNT"):
+    _share = max(1, (os.cpu_count() or 8) // int(os.environ["PYTEST_XDIST_WORKER_COUNT"]))
+    os.environ.setdefault("OMP_NUM_THREADS", str(_share))
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
