@@ -90,6 +90,25 @@ __device__ __forceinline__ T WaveSum(T v) {
   return v;
 }
 
+template <typename T>
+__device__ __forceinline__ T WaveSuffixIncl(T v) {
+  const int lane = threadIdx.x & 63;
+  for (int o = 1; o < 64; o <<= 1) {
+    T t = __shfl_down(v, o, kWave);
+    if (lane + o < 64) v += t;
+  }
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T WavePrefixIncl(T v) {
+  const int lane = threadIdx.x & 63;
+  for (int o = 1; o < 64; o <<= 1) {
+    T t = __shfl_up(v, o, kWave);
+    if (lane >= o) v += t;
+  }
+  return v;
+}
+
 // block-wide sum (every thread gets the result); sh needs blockDim/64 entries
 template <typename T>
 __device__ T BlockSum(T v, T* sh) {
@@ -119,28 +138,21 @@ __device__ __forceinline__ long long* StepScratch(const KArgs& a, int parity) {
   return a.scratch + static_cast<size_t>(parity & 1) * 2 * a.p.total_bins;
 }
 
-// a step histogram with this many row blocks -- or any step from split direct_from_split
-// on, whose tree graph has no reduce kernel -- is summed by the split scan itself (the
-// reduce kernel skips it); data-parallel training always reduces (the all-reduce needs it)
-__device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk, int split) {
-  return !a.p.data_parallel && (nblk <= kReduceChunk || split >= a.p.direct_from_split);
-}
 
 // outcome of the step's partition, derived from Step::cs and the final cursors (every
-// histogram workgroup computes it; one also stores it in Step for the later kernels)
+// split-scan workgroup computes it; the pick stores what later steps need)
 struct ChildInfo {
-  int total_left;
+  int total_left;               // local rows that went left
   int left_count, right_count;  // global counts (== local ones without data-parallel)
-  int smaller, larger;          // leaf ids
+  int smaller, larger;          // leaf ids (exact counts; ties: the right child is smaller)
   int small_is_left;
-  int skip;
-  int s_begin, s_count, buf;    // the smaller child's local rows
+  int skip;                     // neither child can be split (depth / min_data / last split)
 };
 
 __device__ __forceinline__ ChildInfo StepChildren(const KArgs& a, const Step* st) {
   ChildInfo c;
   const CurSplit& cs = st->cs;
-  const int pb = cs.part_begin, pc = cs.part_count;
+  const int pc = cs.part_count;
   c.total_left = st->cur_left;
   c.left_count = a.p.data_parallel ? cs.split.left_count : c.total_left;
   c.right_count = a.p.data_parallel ? cs.split.right_count : pc - c.total_left;
@@ -150,10 +162,53 @@ __device__ __forceinline__ ChildInfo StepChildren(const KArgs& a, const Step* st
   c.small_is_left = c.left_count < c.right_count;
   c.smaller = c.small_is_left ? cs.leaf : cs.new_leaf;
   c.larger = c.small_is_left ? cs.new_leaf : cs.leaf;
-  c.s_begin = c.small_is_left ? pb : pb + c.total_left;
-  c.s_count = c.small_is_left ? c.total_left : pc - c.total_left;
-  c.buf = 1 - cs.src_buf;
   return c;
+}
+
+// one child of the step as seen by the split scan: k = 0 the smaller, 1 the larger child.
+// The child whose rows k_split histogrammed (Step::hist_left) takes the new leaf's slot; the
+// other one is parent - that histogram, computed in place in the parent's slot.
+struct SideInfo {
+  int lr;            // 0 left child (keeps the leaf id), 1 right child (the new leaf)
+  int leaf, slot, frow;
+  int is_hist;
+  int global_count;
+};
+
+__device__ __forceinline__ SideInfo StepSide(const KArgs& a, const Step* st, const ChildInfo& c, int k) {
+  const CurSplit& cs = st->cs;
+  SideInfo d;
+  d.lr = ((k == 0) == (c.small_is_left != 0)) ? 0 : 1;
+  d.leaf = d.lr == 0 ? cs.leaf : cs.new_leaf;
+  d.is_hist = (d.lr == 0) == (st->hist_left != 0);
+  d.slot = d.is_hist ? cs.new_leaf : cs.parent_slot;
+  d.frow = k == 0 ? cs.new_frow : cs.parent_frow;  // the larger child inherits the parent's row
+  d.global_count = a.p.data_parallel ? st->lr[d.lr].global_count : (d.lr == 0 ? c.left_count : c.right_count);
+  return d;
+}
+
+// row blocks of the step's histogram (k_split deals the parent's rows out in blocks)
+__device__ __forceinline__ int StepBlocks(const KArgs& a, int parent_count) {
+  return HistBlocksFor(parent_count, a.split_grid, a.hist_rows_cap, a.blk_min_rows);
+}
+
+// a step histogram with this many row blocks -- or any step from split direct_from_split
+// on, whose tree graph has no reduce kernel -- is summed by the split scan itself (the
+// reduce kernel skips it); data-parallel training always reduces (the collectives need it)
+__device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk, int split) {
+  return !a.p.data_parallel && (nblk <= kReduceChunk || split >= a.p.direct_from_split);
+}
+
+// (g, h) of partial word(s) v: packed (g in the signed high half, h in the low half) or wide
+__device__ __forceinline__ void UnpackPartial(unsigned long long v0, unsigned long long v1, int units, long long* g,
+                                              long long* h) {
+  if (units == 1) {
+    *g = static_cast<long long>(v0) >> 32;  // h (low half) is non-negative: no borrow
+    *h = static_cast<long long>(v0 & 0xffffffffull);
+  } else {
+    *g = static_cast<long long>(v0);
+    *h = static_cast<long long>(v1);
+  }
 }
 
 }  // namespace dev

@@ -50,6 +50,7 @@ struct Params {
   int32_t max_feature_bins;  // max stored bins of one feature (split-scan LDS staging)
   int32_t has_cat;           // number of categorical features (KArgs::cat_list; their own split-scan kernel)
   int32_t direct_from_split; // splits >= this have no reduce kernel: the split scan sums the partials
+  int32_t trace_repeat;      // diagnostics (LGBM_AMD_KTRACE_REPEAT): run the traced pick twice
 };
 
 // per-leaf state
@@ -89,22 +90,22 @@ struct CurSplit {
 };
 
 // per-tree control record.  Each field is written by one kernel of a step and only read by
-// later kernels (never by the writing kernel's other workgroups):
-//   partition: cs, lr (and done)        hist: smaller .. child, nsplit, fresh
-//   partition (atomics): cursors        reduce: cursor reset for the next split
+// later kernels (or by the writing workgroup itself):
+//   pick (last split-scan workgroup, or k_pick): cs, lr, hist_left, bookkeeping fields
+//   split (k_split, atomics): cursors
+//   split scan (atomics): find_count
 struct Step {
   int32_t done;       // tree finished: every later kernel of the tree exits
   int32_t nsplit;     // splits applied (= index of the next split)
   int32_t fresh;      // leaves with new per-feature results in feat_best: 0, 1 (root), 2
   int32_t smaller, larger;
-  int32_t skip_find;  // children can not be split further (depth / min_data / last split)
-  int32_t total_left;
-  int32_t s_begin, s_count, s_buf;  // the histogrammed (smaller) child's rows
+  int32_t hist_left;  // k_split histograms the left child of cs (the pick's estimated counts), else the right
+  uint32_t find_count;  // split-scan workgroups of the step that finished (the last one picks)
+  int32_t root_count;   // global rows of the tree's root
   int32_t bynode_base, bynode_next;  // per-node feature masks: this step's / next free mask index
   int32_t cur_left, cur_right;      // partition cursors: rows placed left / right so far
   CurSplit cs;
   ChildStats lr[2];     // left / right child of cs
-  ChildStats child[2];  // smaller / larger child of cs, with histogram slots
 };
 
 // best threshold of one feature for one leaf (output of one split-scan wave)

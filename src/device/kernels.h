@@ -32,7 +32,9 @@ struct KArgs {
   // order-independent (LDS float atomics are slow on gfx950; integer ones are not)
   long long* hist;           // [num_leaves][total_bins][2]
   long long* scratch;        // [2][total_bins][2] the histogram being built (step parity)
-  unsigned long long* partials;  // [hist_max_blocks][total_bins] per-workgroup packed (g|h)
+  // per-row-block partial histograms, [hist_max_blocks][total_bins][hist_units] u64: one packed
+  // (g | h) word per bin (hist_units 1) or int64 g, int64 h (hist_units 2, gpu_use_dp)
+  unsigned long long* partials;
   const double* scales;      // [scale_g, scale_h, 1/scale_g, 1/scale_h] of the current tree
   double* root;              // [sum_g, sum_h, count]
   int32_t num_rows;          // local rows in the root (or the explicit range); upper bound if num_rows_dev
@@ -44,8 +46,13 @@ struct KArgs {
   int32_t tile_words;        // words per column tile
   int32_t tile_bins;         // max histogram bins of one tile (LDS words)
   int32_t range_begin;       // explicit-range histogram (host-assisted mode)
-  int32_t hist_rows_cap;     // max rows one histogram workgroup accumulates (fixed-point headroom)
+  int32_t hist_rows_cap;     // max rows of one row block (packed fixed-point headroom; fixed, not a function of N)
   int32_t hist_max_blocks;   // row blocks of a histogram (partials capacity)
+  int32_t hist_units;        // u64 words per histogram bin in LDS / partials: 1 packed, 2 wide (gpu_use_dp)
+  int32_t split_grid;        // workgroups of a k_split launch (row blocks are dealt round-robin)
+  int32_t root_grid;         // workgroups of a root / range histogram launch
+  int32_t blk_min_rows;      // k_split: parent rows per row block, lower bound
+  int32_t pick_in_find;      // the last split-scan workgroup of a step picks the next split (else k_pick)
   const uint8_t* bins_col;   // column-major copy of the bin matrix ([group][rows], bin_bytes each)
   int32_t num_data;          // rows of the matrix (column stride of bins_col)
   int32_t host_mode;         // partition: the host wrote Step::cs (host-assisted growth)
@@ -71,57 +78,65 @@ struct KArgs {
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)
 enum TraceSlot {
-  kTrPartEntry = 0, kTrPartPicked, kTrPartRows, kTrPartBins, kTrPartExit,
-  kTrHistEntry, kTrHistRows, kTrHistAccum, kTrHistExit,
+  kTrSplitEntry = 0, kTrSplitRows, kTrSplitSide, kTrSplitResv, kTrSplitGather, kTrSplitAccum, kTrSplitExit,
   kTrRedEntry, kTrRedExit,
-  kTrFindEntry, kTrFindLoaded, kTrFindScanned, kTrFindExit,
-  kTrHistZeroed, kTrHistIdx, kTrHistLoaded,
-  kTrHistWave0 = 24,  // 16 slots: entry time of each wave of the first histogram workgroup
-  kTraceSlots = 40
+  kTrFindEntry, kTrFindLoaded, kTrFindScanned, kTrFindExit, kTrPickEntry, kTrPickExit,
+  kTrPick1, kTrPick2, kTrPick3, kTrPick4, kTrFindHdr, kTrPW1, kTrPW2, kTrPickRep,
+  kTrClk0 = 28, kTrClk1 = 29,  // s_memtime (shader clock) at kTrPick1 / kTrPickExit
+  kTraceSlots = 32
 };
 
 constexpr int kFindMaxCatBins = 1024;  // categorical features scanned on device (<= 32 * kMaxCatWords)
 constexpr int kHistThreads = 1024;     // histogram workgroup (16 waves)
-constexpr int kHistMinRows = 1024;     // rows per histogram workgroup, lower bound
+constexpr int kHistMinRows = 1024;     // rows per histogram row block, lower bound
+constexpr int kHistRowsCap = 16384;    // rows per row block, upper bound (packed fixed point)
 constexpr int kReduceChunk = 16;       // partial histograms summed per reduce thread
 constexpr int kPartThreads = 1024;
-constexpr int kPartRowsPerThread = 8;
-constexpr int kPartTile = kPartThreads * kPartRowsPerThread;
+constexpr int kSplitRows = 4;          // k_split: rows per thread of a sub-tile
+constexpr int kSplitSub = kPartThreads * kSplitRows;
 
-// row blocks (partial histograms) used for `count` rows: deterministic, shared by the
-// histogram and reduce kernels; rows per block never exceed the fixed-point row cap
-__host__ __device__ inline int HistBlocksFor(int count, int max_blocks, int rows_cap) {
+// row blocks (partial histograms) of `count` rows on a grid of `grid` workgroups: a multiple
+// of the grid once the rows exceed one block per workgroup (every workgroup then handles
+// the same number of blocks), blocks of at least min_rows and at most rows_cap rows.
+// Deterministic: shared by the histogram, reduce and split-scan kernels.
+__host__ __device__ inline int HistBlocksFor(int count, int grid, int rows_cap, int min_rows) {
   if (count <= 0) return 0;
-  int rpb = (count + max_blocks - 1) / max_blocks;
-  if (rpb < kHistMinRows) rpb = kHistMinRows;
-  if (rpb > rows_cap) rpb = rows_cap;
-  int k = (count + rpb - 1) / rpb;
-  return k > max_blocks ? max_blocks : k;
+  const long long per_round = static_cast<long long>(grid) * rows_cap;
+  const int rounds = static_cast<int>((count + per_round - 1) / per_round);
+  const long long target = static_cast<long long>(rounds) * grid;
+  int rpb = static_cast<int>((count + target - 1) / target);
+  if (rpb < min_rows) rpb = min_rows;
+  return (count + rpb - 1) / rpb;
 }
 
-int HistGridBlocks();  // max row blocks of a histogram (2 per CU)
+int HistGridBlocks();  // workgroups of a root histogram (2 per CU)
+void PrepareKernels();  // per-kernel attributes (large dynamic LDS); once per process, before any capture
 void SetNumCUs(int n);
 
 // interleave (g, h); per-workgroup max|g| / max h into max_parts[PackBlocks(n)][2]
 void PackGH(const float* g, const float* h, GH* gh, int64_t n, float* max_parts, hipStream_t s);
 int PackBlocks(int64_t n);
-// fixed-point scales of this tree from absmax and the per-workgroup row cap
-void ComputeScales(const uint32_t* absmax, int rows_cap, double* scales, hipStream_t s);
+// fixed-point scales of this tree from absmax: packed (hist_units 1) scales leave headroom
+// for rows_cap rows per row block; wide ones (2) quantise each row to 31 bits of max|g|
+void ComputeScales(const uint32_t* absmax, int rows_cap, int hist_units, double* scales, hipStream_t s);
 void TreeBegin(const KArgs& a, hipStream_t s);
 void RootSum(const KArgs& a, hipStream_t s);
-// histograms: per-workgroup packed partials, then an exact int64 reduction into the
-// step's scratch buffer (root: buffer 0; step: parity of Step::step; range: buffer 0)
+// histograms: per-row-block partials, then an exact int64 reduction into scratch buffer 0
 void HistRoot(const KArgs& a, hipStream_t s);
-// reduce=false: no reduce kernel (only for splits >= Params::direct_from_split)
-void HistStep(const KArgs& a, hipStream_t s, bool reduce = true);
 void HistRange(const KArgs& a, hipStream_t s);  // rows idx[range_begin, +num_rows)
-// split scans of the root / the two children of the step (per-feature results)
+// one split step: (k_split) the split picked into Step::cs is applied to the parent's rows
+// and one child's rows are histogrammed into row-block partials; (reduce=true) the partials
+// are summed into the step's scratch buffer unless the split scan sums them itself
+void SplitStep(const KArgs& a, hipStream_t s, bool reduce);
+// host-assisted growth: apply the split the host wrote into Step::cs (no histogram)
+void Partition(const KArgs& a, hipStream_t s);
+// split scans of the root / the two children of the step (per-feature results); with
+// KArgs::pick_in_find the last workgroup also records the step and picks the next split
 void FindRoot(const KArgs& a, hipStream_t s);
 void FindStep(const KArgs& a, hipStream_t s);
-// device mode: pick the next split (per-leaf bests from the per-feature results, argmax
-// over the leaves) and move the leaf's rows into the children's ranges; host mode: apply
-// the split the host wrote into Step::cs
-void Partition(const KArgs& a, hipStream_t s);
+// the step's bookkeeping and the next pick as a kernel of its own (distributed learners:
+// it runs after the per-feature results were gathered from every rank)
+void PickStep(const KArgs& a, hipStream_t s, bool root);
 
 // score[k] += value[leaf(row)] for every partitioned row of the finished tree
 void AddLeafScore(const KArgs& a, const double* leaf_values, int num_leaves, double* score, hipStream_t s);

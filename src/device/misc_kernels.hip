@@ -56,17 +56,21 @@ void PackGH(const float* g, const float* h, GH* gh, int64_t n, float* max_parts,
                      max_parts);
 }
 
-// scale = 2^k with rows_cap * max * scale <= 2^30 (g: signed high half of the packed
-// word) and <= 2^31 (h: low half); absmax[2] (if set) carries the row cap of all ranks
-__global__ void k_scales(const uint32_t* absmax, int rows_cap, double* scales) {
+// scale = 2^k per component.  Packed (units 1): rows_cap * max * scale <= 2^30 (g: signed
+// high half of the packed word) and <= 2^31 (h: low half) -- a row block never holds more
+// than rows_cap rows.  Wide (units 2): max * scale <= 2^31, so each row keeps 31 bits of
+// max |g| (every fp32 gradient within 2^-7 of the maximum exactly) and sums over up to 2^31
+// rows stay inside int64.  absmax[2] (if set) carries the row cap of all ranks.
+__global__ void k_scales(const uint32_t* absmax, int rows_cap, int units, double* scales) {
   if (threadIdx.x != 0) return;
   if (absmax[2] != 0u) rows_cap = static_cast<int>(absmax[2]);
-  const double lim[2] = {1073741824.0, 2147483648.0};
+  const double lim[2] = {units == 1 ? 1073741824.0 : 2147483648.0, 2147483648.0};
+  const double rows = units == 1 ? static_cast<double>(rows_cap) : 1.0;
   for (int k = 0; k < 2; ++k) {
     const double m = static_cast<double>(__uint_as_float(absmax[k]));
     double sc = 1.0;
     if (m > 0.0 && isfinite(m)) {
-      int e = static_cast<int>(floor(log2(lim[k] / (static_cast<double>(rows_cap) * m))));
+      int e = static_cast<int>(floor(log2(lim[k] / (rows * m))));
       e = max(-120, min(120, e));
       sc = ldexp(1.0, e);
     }
@@ -75,8 +79,8 @@ __global__ void k_scales(const uint32_t* absmax, int rows_cap, double* scales) {
   }
 }
 
-void ComputeScales(const uint32_t* absmax, int rows_cap, double* scales, hipStream_t s) {
-  hipLaunchKernelGGL(k_scales, dim3(1), dim3(64), 0, s, absmax, rows_cap, scales);
+void ComputeScales(const uint32_t* absmax, int rows_cap, int units, double* scales, hipStream_t s) {
+  hipLaunchKernelGGL(k_scales, dim3(1), dim3(64), 0, s, absmax, rows_cap, units, scales);
 }
 
 // ---------------------------------------------------------------- tree reset
@@ -109,7 +113,9 @@ __global__ void k_tree_begin(KArgs a) {
     st->bynode_next = 1;  // mask 0: the root
     st->smaller = 0;
     st->larger = -1;
-    st->skip_find = 0;
+    st->hist_left = 1;
+    st->find_count = 0u;
+    st->root_count = 0;
     st->cur_left = st->cur_right = 0;
   }
 }

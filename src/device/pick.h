@@ -1,0 +1,486 @@
+// Step bookkeeping and the choice of the next split (reference serial_tree_learner.cpp
+// Train loop: ArgMax over best_split_per_leaf_, SplitInner's leaf statistics;
+// monotone_constraints.hpp BasicLeafConstraints), as device functions of one workgroup.
+// Run by the last split-scan workgroup of a step (single process) or by k_pick after the
+// per-feature results were gathered from every rank (distributed learners).
+//
+//  1. bookkeeping of the step just scanned (thread 0): the children's index ranges from the
+//     partition cursors, histogram slots (the histogrammed child took the new leaf's slot),
+//     splittable rows, exact counts into the split record.
+//  2. pick (first wave): the per-leaf best split of the freshly scanned children (argmax over
+//     their per-feature results, SplitInfo order: larger gain, then smaller real feature),
+//     then the leaf to split (argmax over all leaves: gain, real feature, lower leaf id -- the
+//     host loop's order).  Every load of the pick is independent of the others (one round
+//     trip) except the winner's records.
+//  3. record (thread 0): Step::cs / lr / hist_left for the next k_split, the children's
+//     constraint ranges, the split record; the workgroup snapshots the parent's splittable
+//     row (the children's scans overwrite it).
+#pragma once
+
+#include "device_common.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+// argmax over (gain, real feature, index) in SplitInfo order; ties on both -> lower index.
+// `x` travels with the winner.  Rolled: this runs once per split on a cold I-cache.
+__device__ __forceinline__ void WaveArgBest(double* g, int* rf, int* idx, int* x) {
+#pragma unroll 1
+  for (int o = 32; o > 0; o >>= 1) {
+    const double og = __shfl_xor(*g, o, kWave);
+    const int orf = __shfl_xor(*rf, o, kWave);
+    const int oi = __shfl_xor(*idx, o, kWave);
+    const int ox = __shfl_xor(*x, o, kWave);
+    const bool take = oi >= 0 && (*idx < 0 || SplitBetter(og, orf, *g, *rf) ||
+                                  (!SplitBetter(*g, *rf, og, orf) && oi < *idx));
+    if (take) {
+      *g = og;
+      *rf = orf;
+      *idx = oi;
+      *x = ox;
+    }
+  }
+}
+
+// cat: the feature's category set (KArgs::feat_cat) when b is a categorical split
+__device__ __forceinline__ void ToDeviceSplit(const FeatureBest& b, const uint32_t* cat, DeviceSplit* d) {
+  d->gain = b.gain;
+  d->feature = b.feature;
+  d->real_feature = b.real_feature;
+  d->threshold = b.thr;
+  d->left_count = b.lc;
+  d->right_count = b.rc;
+  d->left_output = b.lo;
+  d->right_output = b.ro;
+  d->left_sum_gradient = b.lg;
+  d->left_sum_hessian = b.lh;
+  d->right_sum_gradient = b.rg;
+  d->right_sum_hessian = b.rh;
+  d->default_left = static_cast<int8_t>(b.default_left);
+  d->monotone_type = static_cast<int8_t>(b.mono);
+  d->is_categorical = b.ncat > 0 ? 1 : 0;
+  d->pad0 = 0;
+  d->num_cat_threshold = b.ncat;
+  if (b.ncat > 0) {
+    for (int w = 0; w < kMaxCatWords; ++w) d->cat_bits[w] = cat[w];
+  }
+}
+
+// per-feature results of side (0 smaller, 1 larger) for inner feature f
+__device__ __forceinline__ size_t FeatBestIndex(const KArgs& a, int side, int f) {
+  return static_cast<size_t>(side) * a.p.num_features + f;
+}
+__device__ __forceinline__ const uint32_t* FeatCat(const KArgs& a, int side, int f) {
+  return a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords;
+}
+
+__device__ __forceinline__ void NoSplit(DeviceSplit* d) {
+  d->gain = -INFINITY;
+  d->feature = -1;
+  d->real_feature = -1;
+}
+
+struct PickResult {
+  int done;
+  int s, leaf;
+  int fresh_idx[2];  // winning feature of the fresh children (-1: none)
+  Leaf P;
+  Feature F;
+  DeviceSplit split;
+};
+
+// workgroup-shared state of one pick.  Every global record the pick reads is copied into it
+// first (lane-parallel word copies, loads only), the decisions are made on the LDS copies and
+// every global write comes last: loads and stores of one wave complete in issue order, so an
+// interleaved copy would wait for each store before the next load.
+struct PickLds {
+  PickResult pk;
+  int s, fresh, sm, lg;        // the step's bookkeeping (nsplit, fresh sides, smaller / larger leaf)
+  int sm_frow, lg_frow;
+  int win_feature;             // the winner's inner feature (-1: none)
+  FeatureBest fb[2];           // the fresh children's winning per-feature results
+  uint32_t fcat[2][kMaxCatWords];
+  DeviceSplit fsplit[2];       // ... as split records
+  ChildStats lc, rc;
+  uint32_t icm;
+};
+
+template <typename T>
+__device__ __forceinline__ void CopyWords(const T* src, T* dst, int lane, int lanes) {
+  static_assert(sizeof(T) % 4 == 0, "word copy");
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+  uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+  for (int i = lane; i < static_cast<int>(sizeof(T) / 4); i += lanes) d[i] = s[i];
+}
+
+// 1. the step's bookkeeping (one thread): every load, then every store
+__device__ __forceinline__ void StepBookkeeping(const KArgs& a, Step* st, PickLds* pl) {
+  const ChildInfo c = StepChildren(a, st);
+  const CurSplit& cs = st->cs;
+  const int leaf = cs.leaf, nl = cs.new_leaf, s = cs.s;
+  const int pb = cs.part_begin, pc = cs.part_count, src_buf = cs.src_buf;
+  const int parent_slot = cs.parent_slot, new_frow = cs.new_frow, parent_frow = cs.parent_frow;
+  const int hist_left = st->hist_left;
+  const int bynode_next = st->bynode_next;
+  // ---- stores
+  Leaf* P = &a.leaves[leaf];
+  Leaf* R = &a.leaves[nl];
+  P->begin = pb;
+  P->count = c.total_left;
+  R->begin = pb + c.total_left;
+  R->count = pc - c.total_left;
+  P->buf = 1 - src_buf;
+  R->buf = 1 - src_buf;
+  if (!a.p.data_parallel) {
+    P->global_count = c.left_count;
+    R->global_count = c.right_count;
+    SplitRecord& rec = a.rec[s];
+    rec.left_count = c.left_count;
+    rec.right_count = c.right_count;
+  }
+  // the histogrammed child took the new leaf's slot, the other one the parent's (StepSide)
+  P->slot = hist_left ? nl : parent_slot;
+  R->slot = hist_left ? parent_slot : nl;
+  // the splittable rows follow the smaller child (the host swaps its rows too)
+  const bool swap = !c.skip && c.small_is_left;
+  if (swap) {
+    P->frow = new_frow;
+    R->frow = parent_frow;
+  }
+  const int pf = swap ? new_frow : parent_frow, rf = swap ? parent_frow : new_frow;
+  a.best[leaf].gain = -INFINITY;
+  a.best[leaf].feature = -1;
+  a.best[leaf].real_feature = -1;
+  a.best[nl].gain = -INFINITY;
+  a.best[nl].feature = -1;
+  a.best[nl].real_feature = -1;
+  st->smaller = c.smaller;
+  st->larger = c.larger;
+  if (!c.skip) {  // the host learner samples the smaller, then the larger child
+    st->bynode_base = bynode_next;
+    st->bynode_next = bynode_next + 2;
+  }
+  st->fresh = c.skip ? 0 : 2;
+  st->nsplit = s + 1;
+  pl->s = s + 1;
+  pl->fresh = c.skip ? 0 : 2;
+  pl->sm = c.smaller;
+  pl->lg = c.larger;
+  pl->sm_frow = c.small_is_left ? pf : rf;
+  pl->lg_frow = c.small_is_left ? rf : pf;
+}
+
+// 2. the pick, by the first wave, from the bookkeeping in LDS; loads only
+__device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
+  const int lane = threadIdx.x;
+  const int L = a.p.num_leaves, NF = a.p.num_features;
+  const int s = pl->s, fresh = pl->fresh, sm = pl->sm, lg = pl->lg;
+  PickResult* out = &pl->pk;
+  if (s >= L - 1) {
+    if (lane == 0) {
+      out->done = 1;
+      out->s = s;
+    }
+    return;
+  }
+  // every input in one round of loads: lanes take (side, feature) items of the fresh sides
+  // and leaves 0..s; then the per-side feature argmaxes, then the leaf argmax
+  double sg = -INFINITY;  // this lane's best feature of its side
+  int srf = -1, sidx = -1, unused = 0;
+  const int nitems = fresh * NF;
+  const int side_of_lane = nitems <= kWave ? (lane < NF ? 0 : 1) : -1;  // one item per lane
+  if (side_of_lane >= 0) {
+    const int i = lane - side_of_lane * NF;
+    if (lane < nitems) {
+      const FeatureBest& fbv = a.feat_best[FeatBestIndex(a, side_of_lane, i)];
+      const double cg = fbv.gain;
+      const int crf = fbv.real_feature, cf = fbv.feature;
+      if (cf >= 0) {
+        sg = cg;
+        srf = crf;
+        sidx = i;
+      }
+    }
+  }
+  double lgv = -INFINITY;  // this lane's leaf (l = lane, the common case s < 64)
+  int lrf = -1, lfv = -1;
+  if (lane <= s && lane < L) {
+    lgv = a.best[lane].gain;
+    lrf = a.best[lane].real_feature;
+    lfv = a.best[lane].feature;
+  }
+  int fi[2] = {-1, -1};
+  double fg[2] = {-INFINITY, -INFINITY};
+  int frf[2] = {-1, -1};
+#pragma unroll 1
+  for (int side = 0; side < fresh; ++side) {
+    double g = -INFINITY;
+    int rf = -1, idx = -1;
+    if (side_of_lane >= 0) {
+      if (side_of_lane == side) {
+        g = sg;
+        rf = srf;
+        idx = sidx;
+      }
+    } else {
+#pragma unroll 1
+      for (int i = lane; i < NF; i += kWave) {  // many features: strided, per side
+        const FeatureBest& fbv = a.feat_best[FeatBestIndex(a, side, i)];
+        const double cg = fbv.gain;
+        const int crf = fbv.real_feature, cf = fbv.feature;
+        if (cf >= 0 && (idx < 0 || SplitBetter(cg, crf, g, rf))) {
+          g = cg;
+          rf = crf;
+          idx = i;
+        }
+      }
+    }
+    WaveArgBest(&g, &rf, &idx, &unused);
+    if (idx >= 0 && g == -INFINITY) idx = -1;  // no valid threshold on any feature
+    fi[side] = idx;
+    fg[side] = idx >= 0 ? g : -INFINITY;
+    frf[side] = idx >= 0 ? rf : -1;
+  }
+  if (a.ktrace != nullptr && lane == 0 && s - 1 >= 0) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    a.ktrace[(s - 1) * kTraceSlots + kTrPW1] = wall_clock64();
+  }
+  // the leaf to split: argmax over leaves 0..s (fresh children use the new results); the
+  // winner's inner feature travels with it
+  double g = -INFINITY;
+  int rf = -1, leaf = -1, wf = -1;
+#pragma unroll 1
+  for (int l = lane; l <= s && l < L; l += kWave) {
+    double cg;
+    int crf, cf;
+    if (fresh >= 1 && l == sm) {
+      cg = fg[0];
+      crf = frf[0];
+      cf = fi[0];
+    } else if (fresh == 2 && l == lg) {
+      cg = fg[1];
+      crf = frf[1];
+      cf = fi[1];
+    } else if (l == lane) {
+      cg = lgv;
+      crf = lrf;
+      cf = lfv;
+    } else {
+      cg = a.best[l].gain;
+      crf = a.best[l].real_feature;
+      cf = a.best[l].feature;
+    }
+    if (leaf < 0 || SplitBetter(cg, crf, g, rf)) {
+      g = cg;
+      rf = crf;
+      leaf = l;
+      wf = cf;
+    }
+  }
+  WaveArgBest(&g, &rf, &leaf, &wf);
+  if (lane != 0) return;
+  if (a.ktrace != nullptr && s - 1 >= 0) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    a.ktrace[(s - 1) * kTraceSlots + kTrPW2] = wall_clock64();
+  }
+  out->s = s;
+  out->leaf = leaf;
+  out->fresh_idx[0] = fi[0];
+  out->fresh_idx[1] = fi[1];
+  pl->win_feature = wf;
+  out->done = (g > 0.0 && wf >= 0) ? 0 : 1;
+}
+
+// in-kernel stamp of the picking workgroup (LGBM_AMD_KTRACE)
+__device__ __forceinline__ void PickTrace(const KArgs& a, int s, int slot) {
+  if (a.ktrace != nullptr && threadIdx.x == 0 && s >= 0 && s < a.p.num_leaves) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    a.ktrace[s * kTraceSlots + slot] = wall_clock64();
+  }
+}
+
+__device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool root, PickLds* pl, int ts = -1) {
+  const int tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
+  PickResult* pk = &pl->pk;
+  // 1. bookkeeping, by a thread outside the picking wave (its stores do not hold up the
+  //    wave's loads)
+  if (root) {
+    if (tid == 0) {
+      pl->s = 0;
+      pl->fresh = 1;
+      pl->sm = 0;
+      pl->lg = -1;
+      pl->sm_frow = -1;
+      pl->lg_frow = -1;
+    }
+  } else if (tid == kWave) {
+    StepBookkeeping(a, st, pl);
+  }
+  __syncthreads();
+  PickTrace(a, ts, kTrPick1);
+  if (a.ktrace != nullptr && tid == 0 && ts >= 0 && ts < a.p.num_leaves) a.ktrace[ts * kTraceSlots + kTrClk0] = __builtin_amdgcn_s_memtime();
+  // 2. the pick
+  if (tid < kWave) PickWave(a, pl);
+  __syncthreads();
+  PickTrace(a, ts, kTrPick2);
+  if (a.ktrace != nullptr && a.p.trace_repeat) {  // diagnostics: the same pick again, warm
+    if (tid < kWave) PickWave(a, pl);
+    __syncthreads();
+    PickTrace(a, ts, kTrPickRep);
+  }
+  if (pk->done) {
+    if (tid == 0) {
+      st->done = 1;
+      st->nsplit = pk->s;
+    }
+  } else {
+    // 3. records into LDS: the fresh children's winners, the winning leaf and feature
+    const int fresh = pl->fresh, leaf = pk->leaf, w = tid >> 6;
+    const int nw = nthr >> 6;
+    const bool win_fresh = (fresh >= 1 && leaf == pl->sm) || (fresh == 2 && leaf == pl->lg);
+    for (int side = 0; side < fresh; ++side) {
+      if (w == (side % nw) && pk->fresh_idx[side] >= 0) {
+        CopyWords(&a.feat_best[FeatBestIndex(a, side, pk->fresh_idx[side])], &pl->fb[side], lane, kWave);
+        CopyWords(reinterpret_cast<const uint32_t(*)[kMaxCatWords]>(FeatCat(a, side, pk->fresh_idx[side])),
+                  &pl->fcat[side], lane, kWave);
+      }
+    }
+    if (!win_fresh && w == (2 % nw)) CopyWords(&a.best[leaf], &pk->split, lane, kWave);
+    if (w == (3 % nw)) {
+      CopyWords(&a.leaves[leaf], &pk->P, lane, kWave);
+      CopyWords(&a.feat[pl->win_feature], &pk->F, lane, kWave);
+    }
+    __syncthreads();
+    PickTrace(a, ts, kTrPick3);
+    // 4. conversions and the children's statistics (thread 0, LDS only)
+    if (tid == 0) {
+      for (int side = 0; side < fresh; ++side) {
+        if (pk->fresh_idx[side] >= 0) ToDeviceSplit(pl->fb[side], pl->fcat[side], &pl->fsplit[side]);
+        else NoSplit(&pl->fsplit[side]);
+      }
+      if (win_fresh) pk->split = pl->fsplit[leaf == pl->sm ? 0 : 1];
+      const DeviceSplit& sp = pk->split;
+      const Leaf& P = pk->P;
+      const int s = pk->s, nl = s + 1;
+      const int depth = P.depth + 1;
+      double pmin = P.cmin, pmax = P.cmax, rmin = P.cmin, rmax = P.cmax;
+      if (!sp.is_categorical) {
+        const double mid = (sp.left_output + sp.right_output) / 2.0f;
+        if (sp.monotone_type < 0) {
+          pmin = fmax(pmin, mid);
+          rmax = fmin(rmax, mid);
+        } else if (sp.monotone_type > 0) {
+          pmax = fmin(pmax, mid);
+          rmin = fmax(rmin, mid);
+        }
+      }
+      ChildStats& lc = pl->lc;
+      ChildStats& rc = pl->rc;
+      lc.sum_g = sp.left_sum_gradient;
+      lc.sum_h = sp.left_sum_hessian;
+      lc.output = sp.left_output;
+      lc.cmin = pmin;
+      lc.cmax = pmax;
+      lc.global_count = sp.left_count;
+      lc.depth = depth;
+      lc.slot = P.slot;
+      lc.leaf = leaf;
+      lc.frow = P.frow;
+      rc.sum_g = sp.right_sum_gradient;
+      rc.sum_h = sp.right_sum_hessian;
+      rc.output = sp.right_output;
+      rc.cmin = rmin;
+      rc.cmax = rmax;
+      rc.global_count = sp.right_count;
+      rc.depth = depth;
+      rc.slot = nl;
+      rc.leaf = nl;
+      rc.frow = -1;  // the new leaf's row (below)
+    }
+    __syncthreads();
+    PickTrace(a, ts, kTrPick4);
+    // 5. loads that depend on the winner: the new leaf's splittable row id, the constraint
+    //    mask of the split feature, the parent's splittable row
+    const DeviceSplit& sp = pk->split;
+    const int s = pk->s, nl = s + 1;
+    int new_frow = 0;
+    uint32_t fmask = 0xffffffffu;
+    if (tid == 0) {
+      new_frow = a.leaves[nl].frow;
+      if (a.feat_icmask != nullptr) fmask = a.feat_icmask[sp.feature];
+    }
+    const int8_t* prow = a.splittable + static_cast<size_t>(pk->P.frow) * a.p.num_features;
+    int8_t pflag[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int f = tid + k * nthr;
+      if (f < a.p.num_features) pflag[k] = prow[f];
+    }
+    for (int f = tid + 4 * nthr; f < a.p.num_features; f += nthr) a.parent_flags[f] = prow[f];
+    // ---- stores only from here
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int f = tid + k * nthr;
+      if (f < a.p.num_features) a.parent_flags[f] = pflag[k];  // before the children's scans overwrite it
+    }
+    // the fresh children's bests become part of the per-leaf table
+    for (int side = 0; side < fresh; ++side) {
+      const int l = side == 0 ? pl->sm : pl->lg;
+      CopyWords(&pl->fsplit[side], &a.best[l], tid, nthr);
+    }
+    CopyWords(&pk->split, &a.rec[s].split, tid, nthr);
+    CopyWords(&pk->split, &st->cs.split, tid, nthr);
+    CopyWords(&pk->F, &st->cs.feat, tid, nthr);
+    if (tid == 0) {
+      const Leaf& P = pk->P;
+      const uint32_t icm = P.icmask & fmask;  // both children keep the constraints that hold the feature
+      ChildStats lc = pl->lc, rc = pl->rc;
+      lc.icmask = rc.icmask = icm;
+      rc.frow = new_frow;
+      SplitRecord& rec = a.rec[s];
+      rec.leaf = leaf;
+      rec.left_count = sp.left_count;
+      rec.right_count = sp.right_count;
+      Leaf* PL = &a.leaves[leaf];
+      Leaf* RL = &a.leaves[nl];
+      PL->depth = lc.depth;
+      PL->sum_g = lc.sum_g;
+      PL->sum_h = lc.sum_h;
+      PL->output = lc.output;
+      PL->global_count = lc.global_count;
+      PL->cmin = lc.cmin;
+      PL->cmax = lc.cmax;
+      RL->depth = rc.depth;
+      RL->sum_g = rc.sum_g;
+      RL->sum_h = rc.sum_h;
+      RL->output = rc.output;
+      RL->global_count = rc.global_count;
+      RL->cmin = rc.cmin;
+      RL->cmax = rc.cmax;
+      PL->icmask = RL->icmask = icm;
+      st->lr[0] = lc;
+      st->lr[1] = rc;
+      CurSplit& cs = st->cs;
+      cs.s = s;
+      cs.leaf = leaf;
+      cs.new_leaf = nl;
+      cs.part_begin = P.begin;
+      cs.part_count = P.count;
+      cs.src_buf = P.buf;
+      cs.child_depth = lc.depth;
+      cs.parent_slot = P.slot;
+      cs.parent_frow = P.frow;
+      cs.new_frow = new_frow;
+      // k_split histograms the child with fewer rows by the estimated counts
+      st->hist_left = sp.left_count <= sp.right_count ? 1 : 0;
+    }
+  }
+  if (tid == 0) {
+    st->cur_left = 0;  // the next k_split's partition cursors
+    st->cur_right = 0;
+    st->find_count = 0u;
+  }
+}
+
+}  // namespace dev
+}  // namespace lgbm_amd

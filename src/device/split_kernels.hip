@@ -3,17 +3,20 @@
 // FindBestSplitsFromHistograms).
 //
 // k_find: grid (num_features, 2 leaves), one 256-thread workgroup per (feature, leaf).  It
-// materialises the feature's histogram in the leaf's pool slot (the smaller child takes
-// the step's reduced histogram -- or sums the few partials of a small leaf itself -- the
-// larger one subtracts it from the parent slot, exact in int64), stages it dequantised in
-// LDS, then evaluates every threshold of the forward / reverse scans in parallel
-// (workgroup prefix sums) with the reference's missing-value handling,
-// min_data / min_hessian filters, hessian-estimated counts, L1 / max_delta_step / path
-// smoothing / monotone constraints.  Ties keep the threshold the sequential scan would
-// keep.  Per-feature results go to feat_best; the next partition kernel picks from them.
+// materialises the feature's histogram in the leaf's pool slot -- the histogrammed child
+// takes the step's reduced histogram (or sums the few partials of a small leaf itself), the
+// other child subtracts it from the parent slot in place, exact in int64 -- stages it
+// dequantised in LDS, then evaluates every threshold of the forward and reverse scans in
+// parallel from ONE workgroup prefix scan (the reverse scan's right sums are the range total
+// minus the prefix), with the reference's missing-value handling, min_data / min_hessian
+// filters, hessian-estimated counts, L1 / max_delta_step / path smoothing / monotone
+// constraints.  Ties keep the threshold the sequential scan would keep.  Per-feature results
+// go to feat_best.  The last workgroup of the step to finish (a device-scope counter) then
+// records the step and picks the next split (pick.h), so the next k_split starts from one
+// small Step record.
 #include <type_traits>
 
-#include "device_common.h"
+#include "pick.h"
 
 namespace lgbm_amd {
 namespace dev {
@@ -58,25 +61,6 @@ struct LeafCtx {
   double min_gain_shift;
   ConstraintRange c;
 };
-
-template <typename T>
-__device__ __forceinline__ T WaveSuffixIncl(T v) {
-  const int lane = threadIdx.x & 63;
-  for (int o = 1; o < 64; o <<= 1) {
-    T t = __shfl_down(v, o, kWave);
-    if (lane + o < 64) v += t;
-  }
-  return v;
-}
-template <typename T>
-__device__ __forceinline__ T WavePrefixIncl(T v) {
-  const int lane = threadIdx.x & 63;
-  for (int o = 1; o < 64; o <<= 1) {
-    T t = __shfl_up(v, o, kWave);
-    if (lane >= o) v += t;
-  }
-  return v;
-}
 
 // block-wide scans / reductions of the split scan (kFindThreads threads); every thread
 // calls them, results are returned to every thread
@@ -181,182 +165,277 @@ struct HistView {
   __device__ __forceinline__ double H(int t) const { return t == fix_t ? fix_h : RawH(t); }
 };
 
-// one numerical scan of one feature by one workgroup (each thread owns K consecutive bins)
-__device__ Cand ScanNumericalBlock(const HistView& hv, int nb, int offset, int default_bin, bool reverse,
-                                   bool skip_def, bool na, const LeafCtx& L, const SplitParams& p, int mono,
-                                   bool* splittable, BlockScratch* sc, int rthr) {
+// block-wide exclusive prefix of (g, h, c) plus block totals of (g, h, c) and of three more
+// sums (ag, ah: every stored bin; na*: the NaN bin) in one LDS round
+struct ScanAcc {
+  double g, h;
+  int c;
+  double ag, ah, ng, nh;
+  int nc;
+};
+struct ScanScratch {
+  double d[6][kFindThreads / kWave];
+  int i[2][kFindThreads / kWave];
+};
+
+__device__ __forceinline__ void BlockScanNum(ScanAcc* v, ScanAcc* excl, ScanAcc* tot, ScanScratch* sc) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const double ig = WavePrefixIncl(v->g), ih = WavePrefixIncl(v->h);
+  const int ic = WavePrefixIncl(v->c);
+  const double ag = WaveSum(v->ag), ah = WaveSum(v->ah), ng = WaveSum(v->ng), nh = WaveSum(v->nh);
+  const int nc = WaveSum(v->nc);
+  if (lane == 63) {
+    sc->d[0][w] = ig;
+    sc->d[1][w] = ih;
+    sc->i[0][w] = ic;
+  }
+  if (lane == 0) {
+    sc->d[2][w] = ag;
+    sc->d[3][w] = ah;
+    sc->d[4][w] = ng;
+    sc->d[5][w] = nh;
+    sc->i[1][w] = nc;
+  }
+  __syncthreads();
+  ScanAcc e = {0.0, 0.0, 0, 0.0, 0.0, 0.0, 0.0, 0};
+  ScanAcc t = e;
+#pragma unroll
+  for (int j = 0; j < kFindWaves; ++j) {  // fixed order: identical on every thread and run
+    if (j < w) {
+      e.g += sc->d[0][j];
+      e.h += sc->d[1][j];
+      e.c += sc->i[0][j];
+    }
+    t.g += sc->d[0][j];
+    t.h += sc->d[1][j];
+    t.c += sc->i[0][j];
+    t.ag += sc->d[2][j];
+    t.ah += sc->d[3][j];
+    t.ng += sc->d[4][j];
+    t.nh += sc->d[5][j];
+    t.nc += sc->i[1][j];
+  }
+  __syncthreads();
+  e.g += ig - v->g;
+  e.h += ih - v->h;
+  e.c += ic - v->c;
+  *excl = e;
+  *tot = t;
+}
+
+// the best candidates of both scan directions and whether any threshold was valid, over
+// the workgroup (reverse ties: higher threshold; forward ties: lower)
+__device__ __forceinline__ void BlockBestPair(Cand* rv, Cand* fw, bool* any, BlockScratch* sc, Cand* sc2) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  *rv = WaveBestCand(*rv, true);
+  *fw = WaveBestCand(*fw, false);
+  const bool wa = __any(*any);
+  if (lane == 0) {
+    sc->c[w] = *rv;
+    sc2[w] = *fw;
+    sc->i[w] = wa ? 1 : 0;
+  }
+  __syncthreads();
+  Cand br = sc->c[0], bf = sc2[0];
+  int an = sc->i[0];
+#pragma unroll
+  for (int j = 1; j < kFindWaves; ++j) {
+    if (CandBetter(sc->c[j], br, true)) br = sc->c[j];
+    if (CandBetter(sc2[j], bf, false)) bf = sc2[j];
+    an |= sc->i[j];
+  }
+  __syncthreads();
+  *rv = br;
+  *fw = bf;
+  *any = an != 0;
+}
+
+// split gain / leaf output: the plain formulas (no L1, max_delta_step, path smoothing or
+// monotone constraints -- the reference's FuncForNumricalL3 with every flag off) or the
+// general ones, chosen at compile time so the common case stays a few instructions
+template <bool SIMPLE>
+__device__ __forceinline__ double GainOf(double lg, double lh, double rg, double rh, double l2, const SplitParams& p,
+                                         const ConstraintRange& c, int8_t mono, int lc, int rc, double parent_out) {
+  if (SIMPLE) return (lg * lg) / (lh + l2) + (rg * rg) / (rh + l2);
+  return SplitGain(lg, lh, rg, rh, l2, p, c, mono, lc, rc, parent_out);
+}
+template <bool SIMPLE>
+__device__ __forceinline__ double OutputOf(double sg, double sh, double l2, const SplitParams& p,
+                                           const ConstraintRange& c, int n, double parent_out) {
+  if (SIMPLE) return -sg / (sh + l2);
+  return LeafOutputConstrained(sg, sh, l2, p, c, n, parent_out);
+}
+
+// numerical split of one feature (FindBestThresholdSequentially, both directions and
+// FixHistogram); returns whether any threshold was valid (the host's is_splittable).
+// Every candidate -- reverse at t (right = bins t..t_start), forward at t (left = bins
+// 0..t), and the forward "nothing stored on the left" start -- goes through one evaluation
+// site (instruction footprint: these kernels run once per split on a cold I-cache).
+template <bool SIMPLE>
+__device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
+                                   double mono_penalty, FeatureBest* out, BlockScratch* sc, ScanScratch* ssc,
+                                   Cand* sc2, int rthr) {
   const int tid = threadIdx.x;
+  const int nb = F.num_bin - F.offset;
+  const int offset = F.offset;
+  const bool two = F.num_bin > 2 && F.missing_type != 0;  // reverse and forward scans
+  const bool skip_def = two && F.missing_type == 1;
+  const bool na = two && F.missing_type == 2;
+  const int fix_t = F.mfb > 0 ? F.mfb : -1;  // most frequent bin: not accumulated, rebuilt from the totals
+  const int def_t = skip_def ? F.default_bin - offset : -1;  // the default bin: in no scan
   const int K = (nb + kFindThreads - 1) / kFindThreads;
   const int b0 = tid * K;
   const int b1 = min(nb, b0 + K);
+  hv.fix_t = -1;
+  ScanAcc v = {0.0, 0.0, 0, 0.0, 0.0, 0.0, 0.0, 0};
+#pragma unroll 1
+  for (int t = b0; t < b1; ++t) {
+    if (t == fix_t) continue;
+    const double g = hv.RawG(t), h = hv.RawH(t);
+    const int c = RoundIntD(h * L.cnt_factor);
+    v.ag += g;
+    v.ah += h;
+    if (t != def_t) {
+      v.g += g;
+      v.h += h;
+      v.c += c;
+    }
+    if (t == nb - 1) {
+      v.ng = g;
+      v.nh = h;
+      v.nc = c;
+    }
+  }
+  ScanAcc ex, tot;
+  BlockScanNum(&v, &ex, &tot, ssc);
+  // FixHistogram
+  if (fix_t >= 0) {
+    const double fix_g = L.sg - tot.ag;
+    const double fix_h = (L.sh - 2 * kEpsilon) - tot.ah;
+    const int fix_c = RoundIntD(fix_h * L.cnt_factor);
+    hv.fix_t = fix_t;
+    hv.fix_g = fix_g;
+    hv.fix_h = fix_h;
+    if (fix_t != def_t) {
+      tot.g += fix_g;
+      tot.h += fix_h;
+      tot.c += fix_c;
+      if (fix_t < b0) {
+        ex.g += fix_g;
+        ex.h += fix_h;
+        ex.c += fix_c;
+      }
+    }
+    if (fix_t == nb - 1) {
+      tot.ng = fix_g;
+      tot.nh = fix_h;
+      tot.nc = fix_c;
+    }
+  }
+  // reverse: right(t) = P(t_start) - P(t - 1) over [t_end_r, t_start]; P(t_start) = total
+  // less the NaN bin when it is left out (na and skip_def exclude each other)
   const int t_start_r = nb - 1 - (na ? 1 : 0);
   const int t_end_r = 1 - offset;
   const int t_end_f = nb - 2;
-  auto acc = [&](int t) -> bool {
-    if (skip_def && t + offset == default_bin) return false;
-    if (reverse) return t >= t_end_r && t <= t_start_r;
-    return t >= 0 && t <= t_end_f;
-  };
-  double tg = 0.0, th = 0.0;
-  int tc = 0;
-  for (int t = b0; t < b1; ++t) {
-    if (!acc(t)) continue;
-    const double g = hv.G(t), hh = hv.H(t);
-    tg += g;
-    th += hh;
-    tc += RoundIntD(hh * L.cnt_factor);
-  }
-  Cand best;
-  best.gain = -INFINITY;
-  best.thr = reverse ? -1 : 0x7fffffff;
-  best.lg = best.lh = 0.0;
-  best.lc = 0;
-  bool any = false;
+  const double pr_g = na ? tot.g - tot.ng : tot.g;
+  const double pr_h = na ? tot.h - tot.nh : tot.h;
+  const int pr_c = na ? tot.c - tot.nc : tot.c;
+  // forward: left starts empty, or (NaN as missing with bin 0 not stored) with everything
+  // outside the stored bins
+  const bool minus_one = na && offset == 1;
+  const double lg0 = minus_one ? L.sg - tot.ag : 0.0;
+  const double lh0 = minus_one ? L.sh - kEpsilon - tot.ah : kEpsilon;
+  const int lc0 = minus_one ? L.n - tot.c : 0;  // (na: every stored bin is included)
   const double min_h = p.min_sum_hessian_in_leaf;
   const int min_n = p.min_data_in_leaf;
-  if (reverse) {
-    double ig = tg, ih = th;
-    int ic = tc;
-    BlockScan3(ig, ih, ic, true, sc);
-    double rg = ig - tg, rh = ih - th;  // exclusive suffix (bins above this thread's)
-    int rc = ic - tc;
-    rh += kEpsilon;
-    for (int t = b1 - 1; t >= b0; --t) {
-      if (!acc(t)) continue;
-      const double g = hv.G(t), hh = hv.H(t);
-      rg += g;
-      rh += hh;
-      rc += RoundIntD(hh * L.cnt_factor);
-      if (rc < min_n || rh < min_h) continue;
-      const int lc = L.n - rc;
-      if (lc < min_n) continue;
-      const double lh = L.sh - rh;
-      if (lh < min_h) continue;
-      const double lg = L.sg - rg;
-      if (rthr != kNoRandThr && t - 1 + offset != rthr) continue;  // extra_trees
-      const double gain = SplitGain(lg, lh, rg, rh, p.lambda_l2, p, L.c, static_cast<int8_t>(mono), lc, rc,
-                                    L.parent_out);
-      if (gain <= L.min_gain_shift) continue;
-      any = true;
-      if (gain > best.gain) {
-        best.gain = gain;
-        best.thr = t - 1 + offset;
-        best.lg = lg;
-        best.lh = lh;
-        best.lc = lc;
+  const int8_t mono = static_cast<int8_t>(F.monotone);
+  Cand rb, fb;
+  rb.gain = fb.gain = -INFINITY;
+  rb.thr = -1;
+  fb.thr = 0x7fffffff;
+  rb.lg = rb.lh = fb.lg = fb.lh = 0.0;
+  rb.lc = fb.lc = 0;
+  bool any = false;
+  double pg = ex.g, ph = ex.h;
+  int pc = ex.c;
+  const int cend = 2 * (b1 - b0);
+#pragma unroll 1
+  for (int c = (minus_one && tid == 0) ? -1 : 0; c < cend; ++c) {
+    // candidate c: -1 the forward start, 2i reverse at t = b0 + i, 2i + 1 forward at t
+    const int t = b0 + (c >> 1);
+    const bool rev = c >= 0 && (c & 1) == 0;
+    bool ok;
+    double xg, xh;
+    int xc, thr;
+    if (c < 0) {
+      ok = true;
+      xg = lg0;
+      xh = lh0;
+      xc = lc0;
+      thr = offset - 1;
+    } else if (rev) {
+      ok = t != def_t && t >= t_end_r && t <= t_start_r;
+      // left = total - right, right = bins t..t_start (the reference adds kEpsilon to it)
+      xg = L.sg - (pr_g - pg);
+      xh = L.sh - (pr_h - ph + kEpsilon);
+      xc = L.n - (pr_c - pc);
+      thr = t - 1 + offset;
+    } else {
+      if (t != def_t) {
+        const double h = hv.H(t);
+        pg += hv.G(t);
+        ph += h;
+        pc += RoundIntD(h * L.cnt_factor);
       }
+      ok = two && t != def_t && t <= t_end_f;
+      xg = lg0 + pg;
+      xh = lh0 + ph;
+      xc = lc0 + pc;
+      thr = t + offset;
     }
-  } else {
-    double lg0 = 0.0, lh0 = kEpsilon;
-    int lc0 = 0;
-    const bool minus_one = na && offset == 1;
-    if (minus_one) {
-      // left starts with everything outside the stored bins (the most frequent bin 0)
-      double ag = 0.0, ah = 0.0;
-      int ac = 0;
-      for (int t = b0; t < b1; ++t) {
-        const double hh = hv.H(t);
-        ag += hv.G(t);
-        ah += hh;
-        ac += RoundIntD(hh * L.cnt_factor);
-      }
-      BlockSum3(ag, ah, ac, sc);
-      lg0 = L.sg - ag;
-      lh0 = L.sh - kEpsilon - ah;
-      lc0 = L.n - ac;
-    }
-    double ig = tg, ih = th;
-    int ic = tc;
-    BlockScan3(ig, ih, ic, false, sc);
-    double lg = lg0 + (ig - tg), lh = lh0 + (ih - th);
-    int lc = lc0 + (ic - tc);
-    auto eval = [&](int t, double xg, double xh, int xc) {
-      if (xc < min_n || xh < min_h) return;
-      const int rc = L.n - xc;
-      if (rc < min_n) return;
-      const double rh = L.sh - xh;
-      if (rh < min_h) return;
-      const double rg = L.sg - xg;
-      if (rthr != kNoRandThr && t + offset != rthr) return;  // extra_trees
-      const double gain = SplitGain(xg, xh, rg, rh, p.lambda_l2, p, L.c, static_cast<int8_t>(mono), xc, rc,
-                                    L.parent_out);
-      if (gain <= L.min_gain_shift) return;
-      any = true;
-      if (gain > best.gain) {
-        best.gain = gain;
-        best.thr = t + offset;
-        best.lg = xg;
-        best.lh = xh;
-        best.lc = xc;
-      }
-    };
-    if (minus_one && tid == 0 && !(skip_def && offset - 1 == default_bin)) eval(-1, lg0, lh0, lc0);
-    for (int t = b0; t < b1; ++t) {
-      if (!acc(t)) continue;
-      const double g = hv.G(t), hh = hv.H(t);
-      lg += g;
-      lh += hh;
-      lc += RoundIntD(hh * L.cnt_factor);
-      eval(t, lg, lh, lc);
+    if (!ok || xc < min_n || xh < min_h) continue;
+    const int rc = L.n - xc;
+    const double rh = L.sh - xh;
+    if (rc < min_n || rh < min_h) continue;
+    if (rthr != kNoRandThr && thr != rthr) continue;  // extra_trees
+    const double gain = GainOf<SIMPLE>(xg, xh, L.sg - xg, rh, p.lambda_l2, p, L.c, mono, xc, rc, L.parent_out);
+    if (!(gain > L.min_gain_shift)) continue;
+    any = true;
+    const Cand& cur = rev ? rb : fb;
+    if (gain > cur.gain || (gain == cur.gain && (rev ? thr > cur.thr : thr < cur.thr))) {
+      Cand nc;
+      nc.gain = gain;
+      nc.thr = thr;
+      nc.lg = xg;
+      nc.lh = xh;
+      nc.lc = xc;
+      if (rev) rb = nc;
+      else fb = nc;
     }
   }
-  if (BlockAny(any, sc)) *splittable = true;
-  return BlockBestCand(best, reverse, sc);
-}
-
-// returns whether any threshold was valid (the host's is_splittable)
-__device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
-                                   double mono_penalty, FeatureBest* out, BlockScratch* sc, int rthr) {
-  const int nb = F.num_bin - F.offset;
-  hv.fix_t = -1;
-  hv.fix_g = hv.fix_h = 0.0;
-  if (F.mfb > 0) {
-    // FixHistogram: the most frequent bin is not accumulated; rebuild it from the leaf totals
-    double sg = 0.0, sh = 0.0;
-    int unused = 0;
-    for (int t = threadIdx.x; t < nb; t += kFindThreads) {
-      if (t == F.mfb) continue;
-      sg += hv.RawG(t);
-      sh += hv.RawH(t);
-    }
-    BlockSum3(sg, sh, unused, sc);
-    hv.fix_t = F.mfb;
-    hv.fix_g = L.sg - sg;
-    hv.fix_h = (L.sh - 2 * kEpsilon) - sh;
-  }
+  BlockBestPair(&rb, &fb, &any, sc, sc2);
   out->gain = -INFINITY;
-  out->default_left = 1;
+  out->default_left = two ? 1 : (F.missing_type == 2 ? 0 : 1);
   out->mono = F.monotone;
-  bool splittable = false;
-  auto apply = [&](const Cand& b, bool reverse) {
-    if (splittable && b.gain > out->gain + L.min_gain_shift) {
+#pragma unroll 1
+  for (int d = 0; d < (two ? 2 : 1); ++d) {
+    const Cand b = d == 0 ? rb : fb;
+    if (any && b.gain > out->gain + L.min_gain_shift) {
       out->thr = b.thr;
-      out->lo = LeafOutputConstrained(b.lg, b.lh, p.lambda_l2, p, L.c, b.lc, L.parent_out);
+      out->lo = OutputOf<SIMPLE>(b.lg, b.lh, p.lambda_l2, p, L.c, b.lc, L.parent_out);
       out->lc = b.lc;
       out->lg = b.lg;
       out->lh = b.lh - kEpsilon;
-      out->ro = LeafOutputConstrained(L.sg - b.lg, L.sh - b.lh, p.lambda_l2, p, L.c, L.n - b.lc, L.parent_out);
+      out->ro = OutputOf<SIMPLE>(L.sg - b.lg, L.sh - b.lh, p.lambda_l2, p, L.c, L.n - b.lc, L.parent_out);
       out->rc = L.n - b.lc;
       out->rg = L.sg - b.lg;
       out->rh = L.sh - b.lh - kEpsilon;
       out->gain = b.gain - L.min_gain_shift;
-      out->default_left = reverse ? 1 : 0;
+      out->default_left = d == 1 ? 0 : (!two && F.missing_type == 2 ? 0 : 1);
     }
-  };
-  if (F.num_bin > 2 && F.missing_type != 0) {
-    if (F.missing_type == 1) {
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, true, false, L, p, F.monotone, &splittable, sc, rthr), true);
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, true, false, L, p, F.monotone, &splittable, sc, rthr), false);
-    } else {
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, true, L, p, F.monotone, &splittable, sc, rthr), true);
-      apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, false, false, true, L, p, F.monotone, &splittable, sc, rthr), false);
-    }
-  } else {
-    apply(ScanNumericalBlock(hv, nb, F.offset, F.default_bin, true, false, false, L, p, F.monotone, &splittable, sc, rthr), true);
-    if (F.missing_type == 2) out->default_left = 0;
   }
   out->gain *= F.penalty;
-  if (F.monotone != 0) {
+  if (!SIMPLE && F.monotone != 0) {
     // MonotoneSplitPenalty(depth, penalization)
     double pen;
     if (mono_penalty >= depth + 1.) pen = kEpsilon;
@@ -364,7 +443,7 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
     else pen = 1. - pow(2., mono_penalty - 1. - depth) + kEpsilon;
     out->gain *= pen;
   }
-  return splittable;
+  return any;
 }
 
 // LDS of the categorical scan: per-bin ctr and the stable ctr order
@@ -642,48 +721,57 @@ __device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, 
 }
 
 template <bool ROOT, int KIND>
-__global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
+struct FindShared {
+  BlockScratch sc;
+  ScanScratch ssc;
+  Cand sc2[kFindWaves];
+  typename std::conditional<KIND == 2, CatScratch, int>::type cat_sc;
+  unsigned long long s_red[2 * kFindThreads];  // direct partial sums of narrow features
+};
+
+// the scan of one (feature, child) by one workgroup: every thread of the workgroup takes the
+// same path (the kernel's pick tail needs all of them)
+template <bool ROOT, int KIND, bool SIMPLE>
+__device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND>& sh) {
   constexpr bool CAT = KIND == 2;
-  extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
-  __shared__ BlockScratch sc;
-  __shared__ typename std::conditional<CAT, CatScratch, int>::type cat_sc;
-  __shared__ unsigned long long s_red[2 * kFindThreads];  // direct partial sums of narrow features
   const long long t_entry = wall_clock64();
   const int f = CAT ? a.cat_list[blockIdx.x] : static_cast<int>(blockIdx.x);
   const int side = blockIdx.y;
   const int tid = threadIdx.x;
+  const int units = a.hist_units;
   // ---- independent loads first (one round trip): the feature, its mask, the scales and the
-  // Step record (read before it is tested)
+  // Step record
   const Feature F = a.feat[f];
   const int8_t tree_used = a.tree_mask[f];
+  const Step* st = a.st;
+  const int mi_base = ROOT ? 0 : st->bynode_next;  // this step's per-node masks (advanced by the pick)
   int8_t used = tree_used;  // evaluated at this node (feature_fraction_bynode)
-  if (a.node_mask != nullptr) {
-    const int mi = ROOT ? 0 : a.st->bynode_base + side;
-    used = used && a.node_mask[static_cast<size_t>(mi) * a.p.num_features + f];
-  }
+  if (a.node_mask != nullptr) used = used && a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f];
   const int8_t parent_ok = ROOT ? 1 : a.parent_flags[f];
   const double ig = a.scales[2], ih = a.scales[3];
-  const Step* st = a.st;
-  int done = 0, skip = 0, s = 0, s_count = 0;
+  int s = 0, pc = 0, skip = 0;
+  ChildInfo c;
+  SideInfo sd;
   ChildStats cl;
   if (!ROOT) {
-    done = st->done;
-    skip = st->skip_find;
     s = st->cs.s;
-    s_count = st->s_count;
-    cl = st->child[side];  // written with the histogram (StepBookkeeping)
+    pc = st->cs.part_count;
+    c = StepChildren(a, st);
+    sd = StepSide(a, st, c, side);
+    cl = st->lr[sd.lr];
+    skip = c.skip;
   }
   // extra_trees: per feature and node, the smaller child draws before the larger one
   // (SerialTreeLearner::FindBestSplitsFromHistograms); draw k of the tree is the base state
   // stepped k times.  The smaller child's workgroup appends the step's count row.
   int xt_thr = kNoRandThr;
-  if (a.xt_base != nullptr && (ROOT || !done)) {
+  if (a.xt_base != nullptr) {
     const int nf = a.p.num_features;
     const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * nf + f];
     const bool gate = tree_used && parent_ok && !skip;
-    const int d0 = ROOT ? XtDraws(a, F, f, 0, 0xffffffffu, gate)
-                        : XtDraws(a, F, f, st->bynode_base, st->child[0].icmask, gate);
-    const int d1 = ROOT ? 0 : XtDraws(a, F, f, st->bynode_base + 1, st->child[1].icmask, gate);
+    const uint32_t icm = ROOT ? 0xffffffffu : cl.icmask;  // both children carry the same constraints
+    const int d0 = XtDraws(a, F, f, mi_base, icm, gate);
+    const int d1 = ROOT ? 0 : XtDraws(a, F, f, mi_base + 1, icm, gate);
     if (side == 0 && tid == 0) a.xt_cum[static_cast<size_t>(ROOT ? 0 : s + 1) * nf + f] = prev + d0 + d1;
     xt_thr = 0;  // num_bin <= 2: no draw, threshold 0 only
     if (side == 0 ? d0 : d1) {
@@ -695,13 +783,6 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
   const int nb2 = 2 * nbf;
   int parity = 0, nblk_direct = -1;
   if (!ROOT) {
-    if (done) return;
-    if (!CAT && f == 0 && side == 0 && tid == 0) {
-      // the partition cursors were final for the histogram kernel: reset for the next split
-      // (the reduce kernel, not launched for late splits, used to do it)
-      a.st->cur_left = 0;
-      a.st->cur_right = 0;
-    }
     parity = (s + 1) & 1;
     // zero this feature's bins of the buffer the next step reduces into
     if (!CAT && side == 0) {
@@ -710,62 +791,63 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     }
     if (skip) return;
     KTraceAt(a, s, kTrFindEntry, t_entry);
-    const int nblk = HistBlocksFor(s_count, a.hist_max_blocks, a.hist_rows_cap);
+    KTrace(a, s, kTrFindHdr);
+    const int nblk = StepBlocks(a, pc);
     if (DirectPartials(a, nblk, s)) nblk_direct = nblk;
   }
   const SplitParams& p = a.p.sp;
   LeafCtx L;
   int depth, slot;
   if (ROOT) {
-    const double sg = a.root[0], sh = a.root[1];
+    const double sg = a.root[0], shh = a.root[1];
     const int n = static_cast<int>(a.root[2]);
-    ConstraintRange c;
-    c.min = -DBL_MAX;
-    c.max = DBL_MAX;
+    ConstraintRange cr;
+    cr.min = -DBL_MAX;
+    cr.max = DBL_MAX;
     SplitParams rp = p;
     rp.use_l1 = 1;
     rp.use_max_output = 1;
     rp.use_smoothing = 0;
     rp.use_mc = 1;
-    const double out0 = LeafOutputConstrained(sg, sh, p.lambda_l2, rp, c, n, 0);
+    const double out0 = LeafOutputConstrained(sg, shh, p.lambda_l2, rp, cr, n, 0);
     if (f == 0 && tid == 0 && KIND != 2) {
       Leaf& lf = a.leaves[0];
       lf.sum_g = sg;
-      lf.sum_h = sh;
+      lf.sum_h = shh;
       lf.global_count = n;
       lf.output = out0;
+      a.st->root_count = n;
     }
     L.sg = sg;
-    L.sh = sh + 2 * kEpsilon;
+    L.sh = shh + 2 * kEpsilon;
     L.n = n;
     L.parent_out = out0;
-    L.c = c;
+    L.c = cr;
     depth = 0;
     slot = 0;
   } else {
     L.sg = cl.sum_g;
     L.sh = cl.sum_h + 2 * kEpsilon;
-    L.n = cl.global_count;
+    L.n = sd.global_count;
     L.parent_out = cl.output;
     L.c.min = cl.cmin;
     L.c.max = cl.cmax;
     depth = cl.depth;
-    slot = cl.slot;
+    slot = sd.slot;
   }
   if (KIND == 1 && F.is_cat) return;  // the categorical kernel scans it
   // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
   // here but keeps its histogram and its splittable flag
   if (a.feat_icmask != nullptr && ((ROOT ? 0xffffffffu : cl.icmask) & a.feat_icmask[f]) == 0u) used = 0;
-  int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : cl.frow) * a.p.num_features;
+  int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : sd.frow) * a.p.num_features;
+  FeatureBest* fb_out = &a.feat_best[FeatBestIndex(a, side, f)];
   if (tree_used && !parent_ok) {
     // the parent could not split on f: neither child evaluates it, the smaller child's row
     // says so and the larger child keeps the parent's row (SerialTreeLearner::FindBestSplits)
     if (side == 0 && tid == 0) flags[f] = 0;
     if (tid == 0) {
-      FeatureBest o;
-      o.gain = -INFINITY;
-      o.feature = -1;
-      a.feat_best[side * a.p.num_features + f] = o;
+      fb_out->gain = -INFINITY;
+      fb_out->feature = -1;
     }
     return;
   }
@@ -789,23 +871,25 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
-    const unsigned long long* part = a.partials + F.hist_offset;
+    const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
+    const unsigned long long* part = a.partials + static_cast<size_t>(units) * F.hist_offset;
     const bool stage = a.p.max_feature_bins <= kFindLdsBins;
     double* sg = s_bins;
-    double* sh = s_bins + (stage ? a.p.max_feature_bins : 0);
+    double* shv = s_bins + (stage ? a.p.max_feature_bins : 0);
+    const bool subtract = !ROOT && !sd.is_hist;  // parent - the histogrammed child, in place
     // a feature with fewer bins than threads sums its direct partials with every thread:
     // kFindThreads / nbf threads per bin stride over the row blocks, then combine in LDS
     // (one thread per bin walking hundreds of partials would be a chain of round trips)
     const bool spread = nblk_direct > 1 && 2 * nbf <= kFindThreads;
-    // the larger child's parent bins (first bin of each thread): loaded up front, so their
-    // round trip overlaps the partial-sum loads instead of following them
+    // the parent's bins (first bin of each thread): loaded up front, so their round trip
+    // overlaps the partial-sum loads instead of following them
     long long pg0 = 0, ph0 = 0;
-    if (side == 1 && tid < nbf) {
+    if (subtract && tid < nbf) {
       pg0 = dst[2 * tid];
       ph0 = dst[2 * tid + 1];
     }
     if (spread) {
-      for (int j = tid; j < 2 * nbf; j += kFindThreads) s_red[j] = 0ull;
+      for (int j = tid; j < 2 * nbf; j += kFindThreads) sh.s_red[j] = 0ull;
       __syncthreads();
       const int per = kFindThreads / nbf;
       const int i = tid % nbf, r = tid / nbf;
@@ -813,47 +897,56 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
         constexpr int kC = 8;
         long long g = 0, h = 0;
         for (int k0 = r; k0 < nblk_direct; k0 += per * kC) {
-          unsigned long long v[kC];
+          unsigned long long v0[kC], v1[kC];
 #pragma unroll
-          for (int c = 0; c < kC; ++c) {
-            const int k = k0 + c * per;
-            v[c] = k < nblk_direct ? part[static_cast<size_t>(k) * a.p.total_bins + i] : 0ull;
+          for (int cc = 0; cc < kC; ++cc) {
+            const int k = k0 + cc * per;
+            const unsigned long long* q = part + k * pstride + static_cast<size_t>(units) * i;
+            v0[cc] = k < nblk_direct ? q[0] : 0ull;
+            v1[cc] = (k < nblk_direct && units == 2) ? q[1] : 0ull;
           }
 #pragma unroll
-          for (int c = 0; c < kC; ++c) {
-            g += static_cast<long long>(v[c]) >> 32;
-            h += static_cast<long long>(v[c] & 0xffffffffull);
+          for (int cc = 0; cc < kC; ++cc) {
+            long long pgv, phv;
+            UnpackPartial(v0[cc], v1[cc], units, &pgv, &phv);
+            g += pgv;
+            h += phv;
           }
         }
-        atomicAdd(&s_red[2 * i], static_cast<unsigned long long>(g));
-        atomicAdd(&s_red[2 * i + 1], static_cast<unsigned long long>(h));
+        atomicAdd(&sh.s_red[2 * i], static_cast<unsigned long long>(g));
+        atomicAdd(&sh.s_red[2 * i + 1], static_cast<unsigned long long>(h));
       }
       __syncthreads();
     }
     for (int i = tid; i < nbf; i += kFindThreads) {
       long long g = 0, h = 0;
       if (spread) {
-        g = static_cast<long long>(s_red[2 * i]);
-        h = static_cast<long long>(s_red[2 * i + 1]);
+        g = static_cast<long long>(sh.s_red[2 * i]);
+        h = static_cast<long long>(sh.s_red[2 * i + 1]);
       } else if (nblk_direct >= 0) {
-        // small leaf: sum the few per-workgroup partials here (k_hist_reduce skipped them)
+        // small leaf: sum the few per-block partials here (k_hist_reduce skipped them),
         // chunks of kReduceChunk independent loads in flight
         for (int k0 = 0; k0 < nblk_direct; k0 += kReduceChunk) {
-          unsigned long long v[kReduceChunk];
-#pragma unroll
-          for (int k = 0; k < kReduceChunk; ++k)
-            v[k] = k0 + k < nblk_direct ? part[static_cast<size_t>(k0 + k) * a.p.total_bins + i] : 0ull;
+          unsigned long long v0[kReduceChunk], v1[kReduceChunk];
 #pragma unroll
           for (int k = 0; k < kReduceChunk; ++k) {
-            g += static_cast<long long>(v[k]) >> 32;
-            h += static_cast<long long>(v[k] & 0xffffffffull);
+            const unsigned long long* q = part + (k0 + k) * pstride + static_cast<size_t>(units) * i;
+            v0[k] = k0 + k < nblk_direct ? q[0] : 0ull;
+            v1[k] = (k0 + k < nblk_direct && units == 2) ? q[1] : 0ull;
+          }
+#pragma unroll
+          for (int k = 0; k < kReduceChunk; ++k) {
+            long long pgv, phv;
+            UnpackPartial(v0[k], v1[k], units, &pgv, &phv);
+            g += pgv;
+            h += phv;
           }
         }
       } else {
         g = src[2 * i];
         h = src[2 * i + 1];
       }
-      if (side == 1) {  // larger child = parent - smaller, in the parent's (now its) slot
+      if (subtract) {
         g = (i == tid ? pg0 : dst[2 * i]) - g;
         h = (i == tid ? ph0 : dst[2 * i + 1]) - h;
       }
@@ -861,59 +954,101 @@ __global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
       dst[2 * i + 1] = h;
       if (stage) {
         sg[i] = static_cast<double>(g) * ig;
-        sh[i] = static_cast<double>(h) * ih;
+        shv[i] = static_cast<double>(h) * ih;
       }
     }
     __syncthreads();  // the workgroup's stores become visible to all its threads
     if (!ROOT) KTrace(a, s, kTrFindLoaded);
     if (!used) {
-      if (tid == 0) {
-        o.feature = -1;
-        a.feat_best[side * a.p.num_features + f] = o;
-      }
+      if (tid == 0) fb_out->feature = -1;
       return;
     }
     HistView hv;
     hv.lg = stage ? sg : nullptr;
-    hv.lh = stage ? sh : nullptr;
+    hv.lh = stage ? shv : nullptr;
     hv.h = dst;
     hv.inv_g = ig;
     hv.inv_h = ih;
     bool splittable;
     if constexpr (CAT) {
-      splittable = FindCategoricalBlock(
-          F, hv, L, p, &o, a.feat_cat + (static_cast<size_t>(side) * a.p.num_features + f) * kMaxCatWords, &sc,
-          &cat_sc);
+      splittable = FindCategoricalBlock(F, hv, L, p, &o, a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords, &sh.sc,
+                                        &sh.cat_sc);
     } else {
-      splittable = FindNumericalBlock(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sc, xt_thr);
+      splittable = FindNumericalBlock<SIMPLE>(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc, sh.sc2,
+                                              xt_thr);
     }
     if (tid == 0) flags[f] = splittable ? 1 : 0;
     if (!ROOT) KTrace(a, s, kTrFindScanned);
   } else {
     o.feature = -1;
   }
-  if (tid == 0) a.feat_best[side * a.p.num_features + f] = o;
-  if (!ROOT) KTrace(a, s, kTrFindExit);
+  if (tid == 0) *fb_out = o;
+}
+
+template <bool ROOT, int KIND, bool SIMPLE>
+__global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
+  extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
+  __shared__ FindShared<ROOT, KIND> sh;
+  __shared__ PickLds pl;
+  __shared__ int s_last;
+  Step* st = a.st;
+  if (!ROOT && st->done) return;
+  FindBody<ROOT, KIND, SIMPLE>(a, s_bins, sh);
+  // single process: the last workgroup of the step records it and picks the next split
+  // (with categorical features the numerical kernel runs first and does not count)
+  if (!a.pick_in_find || (KIND == 1)) return;
+  __threadfence();  // release this workgroup's results (feat_best, flags, leaves, histograms)
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = atomicAdd(&st->find_count, 1u) == gridDim.x * gridDim.y - 1 ? 1 : 0;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // acquire every other workgroup's results
+  const int s = ROOT ? -1 : st->cs.s;
+  if (!ROOT && a.ktrace != nullptr && threadIdx.x == 0 && s < a.p.num_leaves) {
+    a.ktrace[s * kTraceSlots + kTrPickEntry] = wall_clock64();
+  }
+  PickAndRecord(a, st, ROOT, &pl, s);
+  if (!ROOT && a.ktrace != nullptr && threadIdx.x == 0 && s < a.p.num_leaves) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    a.ktrace[s * kTraceSlots + kTrPickExit] = wall_clock64();
+    a.ktrace[s * kTraceSlots + kTrClk1] = __builtin_amdgcn_s_memtime();
+  }
+}
+
+// the step's bookkeeping and the next pick alone (distributed learners)
+__global__ __launch_bounds__(kFindThreads) void k_pick(KArgs a, int root) {
+  __shared__ PickLds pl;
+  Step* st = a.st;
+  if (st->done) return;
+  PickAndRecord(a, st, root != 0, &pl);
 }
 
 static size_t FindLds(const KArgs& a) {
   return a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
 }
-void FindRoot(const KArgs& a, hipStream_t s) {
+// plain gain formulas (no L1 / max_delta_step / path smoothing / monotone constraints)
+static bool SimpleGains(const KArgs& a) {
+  const SplitParams& p = a.p.sp;
+  return !p.use_l1 && !p.use_max_output && !p.use_smoothing && !p.use_mc;
+}
+template <bool ROOT>
+static void LaunchFind(const KArgs& a, hipStream_t s) {
+  const dim3 g(a.p.num_features, ROOT ? 1 : 2), b(kFindThreads);
+  const size_t lds = FindLds(a);
+  const bool simple = SimpleGains(a);
   if (a.p.has_cat) {
-    hipLaunchKernelGGL((k_find<true, 1>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
-    hipLaunchKernelGGL((k_find<true, 2>), dim3(a.p.has_cat, 1), dim3(kFindThreads), FindLds(a), s, a);
+    if (simple) hipLaunchKernelGGL((k_find<ROOT, 1, true>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_find<ROOT, 1, false>), g, b, lds, s, a);
+    hipLaunchKernelGGL((k_find<ROOT, 2, false>), dim3(a.p.has_cat, ROOT ? 1 : 2), b, lds, s, a);
   } else {
-    hipLaunchKernelGGL((k_find<true, 0>), dim3(a.p.num_features, 1), dim3(kFindThreads), FindLds(a), s, a);
+    if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_find<ROOT, 0, false>), g, b, lds, s, a);
   }
 }
-void FindStep(const KArgs& a, hipStream_t s) {
-  if (a.p.has_cat) {
-    hipLaunchKernelGGL((k_find<false, 1>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
-    hipLaunchKernelGGL((k_find<false, 2>), dim3(a.p.has_cat, 2), dim3(kFindThreads), FindLds(a), s, a);
-  } else {
-    hipLaunchKernelGGL((k_find<false, 0>), dim3(a.p.num_features, 2), dim3(kFindThreads), FindLds(a), s, a);
-  }
+void FindRoot(const KArgs& a, hipStream_t s) { LaunchFind<true>(a, s); }
+void FindStep(const KArgs& a, hipStream_t s) { LaunchFind<false>(a, s); }
+void PickStep(const KArgs& a, hipStream_t s, bool root) {
+  hipLaunchKernelGGL(k_pick, dim3(1), dim3(kFindThreads), 0, s, a, root ? 1 : 0);
 }
 
 }  // namespace dev

@@ -116,6 +116,7 @@ void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
   int cus = 0;
   HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
   dev::SetNumCUs(cus);
+  dev::PrepareKernels();
   HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   UploadData();
   global_count_.assign(config_->num_leaves, 0);
@@ -188,7 +189,9 @@ void GPUTreeLearner::UploadData() {
   for (int g = 0; g < num_groups_; ++g) goff[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
   d_group_off_ = Alloc<int32_t>(goff.size());
   HIPCHECK(hipMemcpy(d_group_off_, goff.data(), sizeof(int32_t) * goff.size(), hipMemcpyHostToDevice));
-  // histogram column tiles: LDS per block <= 64 KiB (2 blocks / CU), else <= 128 KiB
+  // histogram column tiles: the split kernel's LDS is the tile histogram (8 or 16 bytes per
+  // bin) plus its 16 KiB row list; <= 80 KiB keeps two 1024-thread workgroups per CU
+  hist_units_ = config_->gpu_use_dp ? 2 : 1;
   auto tile_bins_for = [&](int tw) {
     int mx = 0;
     for (int w0 = 0; w0 < wpr; w0 += tw) {
@@ -205,7 +208,8 @@ void GPUTreeLearner::UploadData() {
   int max_tw = 1 << 20;
   if (const char* e = std::getenv("LGBM_AMD_HIST_TILE_WORDS")) max_tw = std::max(1, std::atoi(e));
   int tile_words = 0;
-  for (int limit : {8192, 16384}) {
+  const std::vector<int> limits = hist_units_ == 1 ? std::vector<int>{8192, 16384} : std::vector<int>{8192};
+  for (int limit : limits) {
     for (int tw = std::min({wpr, dev::kHistThreads, max_tw}); tw >= 1; --tw) {
       if (tile_bins_for(tw) <= limit) {
         tile_words = tw;
@@ -237,8 +241,20 @@ void GPUTreeLearner::UploadData() {
   d_absmax_ = Alloc<uint32_t>(4);
   d_feat_best_ = Alloc<dev::FeatureBest>(2 * static_cast<size_t>(std::max(1, num_features_)));
   d_feat_cat_ = Alloc<uint32_t>(2 * static_cast<size_t>(std::max(1, num_features_)) * kMaxCatWords);
-  const int hist_blocks = dev::HistGridBlocks();
-  d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_);
+  // row blocks: the root histogram runs on two workgroups per CU, a split step on one; a
+  // packed (hist_units 1) row block holds at most kHistRowsCap rows, so the fixed-point
+  // scale does not depend on the number of rows; wide blocks are unbounded
+  root_grid_ = dev::HistGridBlocks();
+  split_grid_ = std::max(1, dev::HistGridBlocks() / 2);
+  rows_cap_ = hist_units_ == 1 ? dev::kHistRowsCap : (1 << 30);
+  if (const char* e = std::getenv("LGBM_AMD_HIST_ROWS_CAP")) {
+    if (hist_units_ == 1) rows_cap_ = std::max(dev::kHistMinRows, std::min(dev::kHistRowsCap, std::atoi(e)));
+  }
+  blk_min_rows_ = 4096;
+  if (const char* e = std::getenv("LGBM_AMD_BLK_MIN_ROWS")) blk_min_rows_ = std::max(256, std::atoi(e));
+  const int hist_blocks = std::max({1, dev::HistBlocksFor(num_data_, root_grid_, rows_cap_, dev::kHistMinRows),
+                                    dev::HistBlocksFor(num_data_, split_grid_, rows_cap_, blk_min_rows_)});
+  d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_ * hist_units_);
   d_root_ = Alloc<double>(4);
   d_leaf_sums_ = Alloc<double>(4);
   d_root_parts_ = Alloc<double>(2 * static_cast<size_t>(dev::GradientBlocks(num_data_)));
@@ -279,6 +295,12 @@ void GPUTreeLearner::UploadData() {
   a.scratch = d_scratch_;
   a.partials = d_partials_;
   a.hist_max_blocks = hist_blocks;
+  a.hist_units = hist_units_;
+  a.root_grid = root_grid_;
+  a.split_grid = split_grid_;
+  a.blk_min_rows = blk_min_rows_;
+  a.hist_rows_cap = rows_cap_;
+  a.pick_in_find = data_parallel_ ? 0 : 1;
   a.host_mode = 0;
   a.ktrace = nullptr;
   if (const char* kt = std::getenv("LGBM_AMD_KTRACE")) {
@@ -307,7 +329,8 @@ void GPUTreeLearner::UploadData() {
   a.p.max_feature_bins = max_fb;
   // from this split on the tree's graph has no reduce kernel: smaller children are small
   // enough for the split scan to sum their partial histograms (LGBM_AMD_DIRECT_FROM_SPLIT)
-  a.p.direct_from_split = 16;
+  a.p.direct_from_split = 100;  // a reduce kernel for every step with > kReduceChunk blocks (r02 sweep)
+  a.p.trace_repeat = std::getenv("LGBM_AMD_KTRACE_REPEAT") != nullptr ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_DIRECT_FROM_SPLIT")) a.p.direct_from_split = std::atoi(e);
   std::vector<int32_t> cats;
   for (int f = 0; f < num_features_; ++f) {
@@ -319,28 +342,26 @@ void GPUTreeLearner::UploadData() {
     HIPCHECK(hipMemcpy(d_cat_list_, cats.data(), sizeof(int32_t) * cats.size(), hipMemcpyHostToDevice));
   }
   a.cat_list = d_cat_list_;
-  // interaction constraints as per-feature constraint bitmasks (device-resident growth
-  // supports up to 32 constraints, see DecideMode)
-  const auto& ic = config_->interaction_constraints_vector;
-  a.feat_icmask = nullptr;
-  a.xt_base = nullptr;
-  a.xt_cum = nullptr;
-  if (!ic.empty() && ic.size() <= 32) {
-    std::vector<uint32_t> icm(std::max(1, num_features_), 0u);
-    for (int f = 0; f < num_features_; ++f) {
-      const int real = data_->RealFeatureIndex(f);
-      for (size_t k = 0; k < ic.size(); ++k) {
-        if (std::find(ic[k].begin(), ic[k].end(), real) != ic[k].end()) icm[f] |= 1u << k;
-      }
-    }
-    d_feat_icmask_ = Alloc<uint32_t>(icm.size());
-    HIPCHECK(hipMemcpy(d_feat_icmask_, icm.data(), sizeof(uint32_t) * icm.size(), hipMemcpyHostToDevice));
-    a.feat_icmask = d_feat_icmask_;
-  }
-  // per-workgroup row cap of the histogram kernels (fixed-point headroom): see k_hist
-  rows_cap_ = std::max(dev::kHistMinRows * 4, (num_data_ + hist_blocks - 1) / hist_blocks);
-  a.hist_rows_cap = rows_cap_;
+  UploadInteractionMasks();
   AllocSplittable();
+}
+
+// interaction constraints as per-feature constraint bitmasks (device-resident growth
+// supports up to 32 constraints, see DecideMode); rebuilt when the config changes
+void GPUTreeLearner::UploadInteractionMasks() {
+  const auto& ic = config_->interaction_constraints_vector;
+  args_.feat_icmask = nullptr;
+  if (ic.empty() || ic.size() > 32) return;
+  std::vector<uint32_t> icm(std::max(1, num_features_), 0u);
+  for (int f = 0; f < num_features_; ++f) {
+    const int real = data_->RealFeatureIndex(f);
+    for (size_t k = 0; k < ic.size(); ++k) {
+      if (std::find(ic[k].begin(), ic[k].end(), real) != ic[k].end()) icm[f] |= 1u << k;
+    }
+  }
+  if (d_feat_icmask_ == nullptr) d_feat_icmask_ = Alloc<uint32_t>(icm.size());
+  HIPCHECK(hipMemcpy(d_feat_icmask_, icm.data(), sizeof(uint32_t) * icm.size(), hipMemcpyHostToDevice));
+  args_.feat_icmask = d_feat_icmask_;
 }
 
 void GPUTreeLearner::AllocSplittable() {
@@ -398,6 +419,11 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     AllocSplittable();
     global_count_.assign(n_leaves, 0);
   }
+  if (config_->gpu_use_dp != (hist_units_ == 2)) {
+    Log::Warning("device learner: gpu_use_dp cannot change after training started; keeping %s histograms",
+                 hist_units_ == 2 ? "wide" : "packed");
+  }
+  UploadInteractionMasks();
   // monotone / penalty metadata may have changed
   std::vector<dev::Feature> feats(num_features_);
   HIPCHECK(hipMemcpy(feats.data(), d_feat_, sizeof(dev::Feature) * num_features_, hipMemcpyDeviceToHost));
@@ -482,7 +508,7 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
     dev::ReduceParts(d_max_parts_, nullptr, dev::PackBlocks(num_data_), num_data_, d_absmax_, nullptr, stream_);
   }
   AllreduceAbsMax();
-  dev::ComputeScales(d_absmax_, rows_cap_, d_scales_, stream_);
+  dev::ComputeScales(d_absmax_, rows_cap_, hist_units_, d_scales_, stream_);
   host_partition_fresh_ = false;
   DecideMode();
   if (device_mode_) return TrainDeviceMode();
@@ -574,8 +600,7 @@ void GPUTreeLearner::KernelFloorProbe(const dev::KArgs& a) {
     const char* name;
     void (*fn)(const dev::KArgs&, hipStream_t);
   };
-  const P probes[] = {{"partition", dev::Partition},
-                      {"hist+reduce", [](const dev::KArgs& k, hipStream_t st) { dev::HistStep(k, st, true); }},
+  const P probes[] = {{"split+reduce", [](const dev::KArgs& k, hipStream_t st) { dev::SplitStep(k, st, true); }},
                       {"find", dev::FindStep}};
   for (const P& p : probes) {
     for (int i = 0; i < 20; ++i) p.fn(a, stream_);
@@ -591,64 +616,77 @@ void GPUTreeLearner::KernelFloorProbe(const dev::KArgs& a) {
   (void)hipEventDestroy(e1);
 }
 
-// LGBM_AMD_KTRACE=1: in-kernel timestamps of the first workgroup of every step kernel
-// (100 MHz clock), averaged over the splits of each tree and printed to stderr
+// LGBM_AMD_KTRACE=1: in-kernel timestamps of the first workgroup of every step kernel (and
+// of the picking workgroup), 100 MHz clock, averaged over the splits of each tree and printed
+// to stderr as the time between consecutive stamps (a stamp a split did not take -- no
+// reduce kernel, no split scan -- is skipped)
 void GPUTreeLearner::ReportKernelTrace(int num_splits) {
   const int L = config_->num_leaves;
   std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
   HIPCHECK(hipMemcpy(t.data(), d_ktrace_, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
-  struct Seg {
-    const char* name;
-    int a, b;  // slots; b < 0: next split's slot -b-1
-  };
-  const Seg segs[] = {{"part.pick", dev::kTrPartEntry, dev::kTrPartPicked},
-                      {"part.rows", dev::kTrPartPicked, dev::kTrPartRows},
-                      {"part.bins", dev::kTrPartRows, dev::kTrPartBins},
-                      {"part.tail", dev::kTrPartBins, dev::kTrPartExit},
-                      {"gap>hist", dev::kTrPartExit, dev::kTrHistEntry},
-                      {"hist.rows", dev::kTrHistEntry, dev::kTrHistRows},
-                      {"hist.zero", dev::kTrHistRows, dev::kTrHistZeroed},
-                      {"hist.idx", dev::kTrHistZeroed, dev::kTrHistIdx},
-                      {"hist.gather", dev::kTrHistIdx, dev::kTrHistLoaded},
-                      {"hist.atomics", dev::kTrHistLoaded, dev::kTrHistAccum},
-                      {"hist.store", dev::kTrHistAccum, dev::kTrHistExit},
-                      {"gap>reduce", dev::kTrHistExit, dev::kTrRedEntry},
-                      {"reduce", dev::kTrRedEntry, dev::kTrRedExit},
-                      {"gap>find", dev::kTrRedExit, dev::kTrFindEntry},
-                      {"find.load", dev::kTrFindEntry, dev::kTrFindLoaded},
-                      {"find.scan", dev::kTrFindLoaded, dev::kTrFindScanned},
-                      {"find.tail", dev::kTrFindScanned, dev::kTrFindExit},
-                      {"gap>part", dev::kTrFindExit, -dev::kTrPartEntry - 1}};
-  std::string line = "ktrace (us, avg over splits " + std::to_string(std::min(num_splits, 8)) + ".." +
-                     std::to_string(num_splits - 1) + "):";
-  for (const Seg& sg : segs) {
-    double sum = 0.0;
-    int n = 0;
-    for (int s = std::min(num_splits, 8); s < num_splits; ++s) {
-      const long long ta = t[static_cast<size_t>(s) * dev::kTraceSlots + sg.a];
-      const long long tb = sg.b >= 0 ? t[static_cast<size_t>(s) * dev::kTraceSlots + sg.b]
-                                     : (s + 1 < num_splits ? t[static_cast<size_t>(s + 1) * dev::kTraceSlots - sg.b - 1]
-                                                           : 0);
-      if (ta <= 0 || tb <= 0 || tb < ta) continue;
-      sum += static_cast<double>(tb - ta) / 100.0;  // 100 MHz
-      ++n;
+  static const int order[] = {dev::kTrSplitEntry, dev::kTrSplitRows,   dev::kTrSplitSide,   dev::kTrSplitResv,
+                              dev::kTrSplitGather, dev::kTrSplitAccum, dev::kTrSplitExit,   dev::kTrRedEntry,
+                              dev::kTrRedExit,     dev::kTrFindEntry,  dev::kTrFindHdr,     dev::kTrFindLoaded,
+                              dev::kTrFindScanned, dev::kTrFindExit,   dev::kTrPickEntry,   dev::kTrPick1,
+                              dev::kTrPW1,         dev::kTrPW2,        dev::kTrPick2,       dev::kTrPickRep,
+                              dev::kTrPick3,
+                              dev::kTrPick4,       dev::kTrPickExit};
+  static const char* names[] = {"split.entry", "split.rows",  "split.side", "split.resv", "split.gather",
+                                "split.accum", "split.exit",  "red.entry",  "red.exit",   "find.entry",
+                                "find.hdr",    "find.loaded", "find.scanned", "find.exit", "pick.entry",
+                                "pick.book",   "pick.fsides", "pick.leaves", "pick.wave",  "pick.again",
+                                "pick.copy",
+                                "pick.conv",   "pick.exit"};
+  const int n = static_cast<int>(sizeof(order) / sizeof(order[0]));
+  std::vector<double> sum(n + 1, 0.0);
+  std::vector<int> cnt(n + 1, 0);
+  const int s0 = std::min(num_splits, 8);
+  double total = 0.0;
+  int total_n = 0;
+  for (int s = s0; s + 1 < num_splits; ++s) {
+    const long long* row = &t[static_cast<size_t>(s) * dev::kTraceSlots];
+    long long prev = 0;
+    for (int k = 0; k <= n; ++k) {
+      const long long v = k < n ? row[order[k]] : t[static_cast<size_t>(s + 1) * dev::kTraceSlots + dev::kTrSplitEntry];
+      if (v <= 0) continue;
+      if (prev > 0 && v >= prev) {
+        sum[k] += static_cast<double>(v - prev) / 100.0;
+        ++cnt[k];
+      }
+      prev = v;
     }
+    const long long b = row[dev::kTrSplitEntry];
+    const long long e = t[static_cast<size_t>(s + 1) * dev::kTraceSlots + dev::kTrSplitEntry];
+    if (b > 0 && e > b) {
+      total += static_cast<double>(e - b) / 100.0;
+      ++total_n;
+    }
+  }
+  std::string line = "ktrace (us to each stamp, avg over splits " + std::to_string(s0) + ".." +
+                     std::to_string(num_splits - 2) + "):";
+  for (int k = 0; k <= n; ++k) {
+    if (cnt[k] == 0) continue;
     char buf[64];
-    std::snprintf(buf, sizeof(buf), " %s=%.2f", sg.name, n ? sum / n : -1.0);
+    std::snprintf(buf, sizeof(buf), " %s=%.2f", k < n ? names[k] : "next.split", sum[k] / cnt[k]);
+    line += buf;
+  }
+  char buf[64];
+  std::snprintf(buf, sizeof(buf), " | per split %.2f", total_n ? total / total_n : -1.0);
+  line += buf;
+  // shader clock over the picks (s_memtime cycles per 100 MHz wall tick)
+  double cyc = 0.0, wall = 0.0;
+  for (int s = s0; s + 1 < num_splits; ++s) {
+    const long long* row = &t[static_cast<size_t>(s) * dev::kTraceSlots];
+    if (row[dev::kTrClk1] > row[dev::kTrClk0] && row[dev::kTrPickExit] > row[dev::kTrPick1]) {
+      cyc += static_cast<double>(row[dev::kTrClk1] - row[dev::kTrClk0]);
+      wall += static_cast<double>(row[dev::kTrPickExit] - row[dev::kTrPick1]);
+    }
+  }
+  if (wall > 0) {
+    std::snprintf(buf, sizeof(buf), " | shader clock %.0f MHz", 100.0 * cyc / wall);
     line += buf;
   }
   std::fprintf(stderr, "%s\n", line.c_str());
-  // entry skew of the first histogram workgroup's waves (split num_splits / 2)
-  const int sm = num_splits / 2;
-  std::string w = "ktrace hist wave entry offsets (us) split " + std::to_string(sm) + ":";
-  const long long* base = &t[static_cast<size_t>(sm) * dev::kTraceSlots];
-  for (int k = 0; k < 16; ++k) {
-    char buf[32];
-    const long long v = base[dev::kTrHistWave0 + k];
-    std::snprintf(buf, sizeof(buf), " %.2f", v > 0 ? (v - base[dev::kTrHistWave0]) / 100.0 : -1.0);
-    w += buf;
-  }
-  std::fprintf(stderr, "%s\n", w.c_str());
 }
 
 void GPUTreeLearner::DestroyGraph() {
@@ -678,14 +716,15 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   dev::HistRoot(a, stream_);
   AllreduceScratch(0);
   dev::FindRoot(a, stream_);
-  // one split per step: pick + partition -> smaller child's histogram (+ reduction) ->
-  // split scans of both children.  The sequence is fixed; kernels of a finished tree exit
-  // at once.
+  if (!a.pick_in_find) dev::PickStep(a, stream_, true);
+  // one split per step: the picked split applied to the leaf's rows with one child's
+  // histogram (+ reduction) -> split scans of both children (+ the next pick).  The sequence
+  // is fixed; kernels of a finished tree exit at once.
   for (int s = 0; s < config_->num_leaves - 1; ++s) {
-    dev::Partition(a, stream_);
-    dev::HistStep(a, stream_, s < a.p.direct_from_split);
+    dev::SplitStep(a, stream_, s < a.p.direct_from_split || data_parallel_);
     AllreduceScratch(s + 1);  // the step's buffer parity
     dev::FindStep(a, stream_);
+    if (!a.pick_in_find) dev::PickStep(a, stream_, false);
   }
 }
 
@@ -782,10 +821,10 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   const int num_splits = h_step_->nsplit;
   if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
-    const bool root_scanned = root_rows_ >= 2 * config_->min_data_in_leaf;
+    const bool root_scanned = h_step_->root_count >= 2 * config_->min_data_in_leaf;  // global count
     col_sampler_.AdvanceByNode(root_scanned ? h_step_->bynode_next : 0);
   }
-  if (xt && root_rows_ >= 2 * config_->min_data_in_leaf) {
+  if (xt && h_step_->root_count >= 2 * config_->min_data_in_leaf) {
     // replay the draws the split scans made: the rows are running counts, steps not run are 0
     const int rows = config_->num_leaves;
     h_xt_cum_.resize(static_cast<size_t>(rows) * num_features_);

@@ -102,7 +102,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void WatchdogSync();
   void AllreduceAbsMax();
   void UploadRankTables(const DeviceRankSpec& r, DeviceGradKind kind);
-  void AllocSplittable();  // (re)allocate the splittable rows: all 1, leaf i -> row i (resets d_leaves_)
+  void AllocSplittable();
+  void UploadInteractionMasks();  // (re)allocate the splittable rows: all 1, leaf i -> row i (resets d_leaves_)
   // tree records for the traversal kernels (staged in d_tree_*; the host vectors must stay
   // alive until the stream is synchronised)
   dev::DevTree StageTree(const Tree* tree);
@@ -152,7 +153,11 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   uint32_t* d_feat_cat_ = nullptr;  // category sets of the per-feature categorical bests
   uint32_t* h_absmax_ = nullptr;
   double* h_scales_ = nullptr;
-  int rows_cap_ = 4096;
+  int rows_cap_ = 4096;      // rows per histogram row block (packed fixed-point headroom)
+  int hist_units_ = 1;       // 1 packed (g | h) u64 per bin, 2 wide int64 g / h (gpu_use_dp)
+  int root_grid_ = 512;
+  int split_grid_ = 256;
+  int blk_min_rows_ = 2048;
   unsigned long long* d_partials_ = nullptr;  // per-workgroup partial histograms
   std::vector<dev::Feature> h_feats_;          // host copy of the feature records
   hipGraphExec_t graph_exec_ = nullptr;        // captured tree (single-process device mode)

@@ -1,29 +1,15 @@
 #!/bin/bash
-# One GPU-box session: GPU tests, 1-GPU bench, optional rocprofv3 kernel stats.
-# Stops at the first step that times out, aborts or segfaults (exit 124/134/137/139).
-#   tools/gpu_check.sh [tests] [bench] [prof] [env VAR=VAL ...]
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+# GPU check used with gpurun: device tests, then (unless a test run crashed or hung) the
+# headline bench and an in-kernel trace run.  Output under gpurun_out/<tag>_*.
+# usage: tools/gpu_check.sh TAG [pytest-args...]
+tag=${1:-chk}; shift
 mkdir -p gpurun_out
-fatal() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
-want() { [[ " $STEPS " == *" $1 "* ]]; }
-STEPS="$*"
-[ -z "$STEPS" ] && STEPS="tests bench prof"
-if want tests; then
-  timeout -k 10 420 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
-  rc=$?; echo "pytest_exit=$rc" >> gpurun_out/pytest_gpu.log
-  fatal $rc && exit $rc
-fi
-if want bench; then
-  timeout -k 10 420 python bench.py --steps 30 --warmup 5 > gpurun_out/bench.log 2>&1
-  rc=$?; echo "bench_exit=$rc" >> gpurun_out/bench.log
-  fatal $rc && exit $rc
-fi
-if want prof; then
-  ROOT=$(pwd)
-  cd /tmp && export TMPDIR=/tmp
-  timeout -k 10 420 rocprofv3 --kernel-trace --stats -f csv -d "$ROOT/gpurun_out/prof" -o run -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 2 --test-rows 0 > "$ROOT/gpurun_out/prof.log" 2>&1
-  rc=$?; echo "prof_exit=$rc" >> "$ROOT/gpurun_out/prof.log"
-  fatal $rc && exit $rc
-fi
-exit 0
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread "$@" > gpurun_out/${tag}_pytest.log 2>&1
+rc=$?
+tail -3 gpurun_out/${tag}_pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi
+timeout -k 10 180 python bench.py --steps 200 --warmup 5 > gpurun_out/${tag}_bench.log 2>&1 || { echo "bench failed"; tail -5 gpurun_out/${tag}_bench.log; exit 3; }
+tail -1 gpurun_out/${tag}_bench.log
+LGBM_AMD_KTRACE=1 timeout -k 10 120 python bench.py --steps 3 --warmup 1 --test-rows 0 > gpurun_out/${tag}_ktrace.log 2>&1 || exit 4
+grep ktrace gpurun_out/${tag}_ktrace.log | tail -2
+exit $rc

@@ -1,27 +1,59 @@
 #!/usr/bin/env python3
-"""Per-step kernel durations of the last profiled tree from a rocprofv3 kernel trace.
+"""Per-step kernel durations and the gaps between them, for the last profiled tree, from a
+rocprofv3 kernel trace (device-resident growth: k_split [k_hist_reduce<1>] k_find<false>
+[k_pick] per split).
 
-  python tools/step_trace.py gpurun_out/prof/run_kernel_trace.csv [num_steps]
+  python tools/step_trace.py gpurun_out/prof/run_kernel_trace.csv
+
+Prints one line per split (kernel: gap-before/duration in us) and the totals.
 """
 import csv
 import sys
 
-tr = list(csv.DictReader(open(sys.argv[1])))
-tr.sort(key=lambda r: int(r["Start_Timestamp"]))
-n = int(sys.argv[2]) if len(sys.argv) > 2 else 62
-names = ["k_partition", "k_hist<1", "k_hist_reduce<1", "k_find<false", "k_pick<false"]
-cols = {k: [] for k in names}
-gaps = []
-for r in tr:
-    for k in names:
-        if k in r["Kernel_Name"]:
-            cols[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-# wall time of the last tree's steps: first partition start -> last pick end
-parts = [r for r in tr if "k_partition" in r["Kernel_Name"]][-n:]
-picks = [r for r in tr if "k_pick<false" in r["Kernel_Name"]][-n:]
-print("step " + " ".join(f"{k[:14]:>14}" for k in names))
-for i in range(n):
-    print(f"{i:4d} " + " ".join(f"{cols[k][-n + i]:14.1f}" for k in names))
-w = (int(picks[-1]["End_Timestamp"]) - int(parts[0]["Start_Timestamp"])) / 1e3
-busy = sum(sum(cols[k][-n:]) for k in names)
-print(f"steps wall {w:.1f} us, kernels {busy:.1f} us, gaps {w - busy:.1f} us ({(w - busy) / (5 * n):.2f} us per boundary)")
+
+def short(name):
+    for k in ("k_split", "k_hist_reduce<1", "k_find<false", "k_pick", "k_find<true", "k_hist<0", "k_hist_reduce<0"):
+        if k in name:
+            return k
+    return None
+
+
+def main():
+    tr = list(csv.DictReader(open(sys.argv[1])))
+    tr.sort(key=lambda r: int(r["Start_Timestamp"]))
+    ev = [(short(r["Kernel_Name"]), int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in tr]
+    ev = [e for e in ev if e[0] is not None]
+    roots = [i for i, e in enumerate(ev) if e[0] == "k_find<true"]
+    if not roots:
+        print("no tree found")
+        return
+    start = roots[-2] if len(roots) > 1 else roots[-1]  # the last complete tree
+    end = roots[-1] if len(roots) > 1 else len(ev)
+    tree = ev[start:end]
+    steps = []
+    cur = []
+    for e in tree[1:]:
+        if e[0] == "k_split" and cur:
+            steps.append(cur)
+            cur = []
+        cur.append(e)
+    if cur:
+        steps.append(cur)
+    tot_k = tot_g = 0.0
+    prev_end = tree[0][2]
+    for i, st in enumerate(steps):
+        parts = []
+        for name, b, en in st:
+            gap = (b - prev_end) / 1e3
+            dur = (en - b) / 1e3
+            tot_g += gap
+            tot_k += dur
+            parts.append(f"{name}: {gap:5.1f}/{dur:6.1f}")
+            prev_end = en
+        print(f"{i:3d}  " + "   ".join(parts))
+    n = max(1, len(steps))
+    print(f"splits {len(steps)}: kernels {tot_k:.1f} us, gaps {tot_g:.1f} us; per split {tot_k / n:.2f} + {tot_g / n:.2f} us")
+
+
+if __name__ == "__main__":
+    main()
