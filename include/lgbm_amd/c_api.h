@@ -218,6 +218,10 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkCreateThreadHub(int num_ranks, double time
                                                       int fail_at_call, void** out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkJoinThreadHub(void* hub, int rank);
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkFreeThreadHub(void* hub);
+// in-process device communicators (thread ranks sharing one GPU)
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, void** out);
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommJoinThreadHub(void* hub, int rank);
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommFreeThreadHub(void* hub);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceSynchronize();
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCount(int* out);
 /* phase timers (LGBM_AMD_TIMETAG) as "name=seconds;..." */

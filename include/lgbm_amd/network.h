@@ -65,7 +65,11 @@ class DeviceComm {
   virtual void AllreduceMaxU32(uint32_t* buf, size_t count, void* stream) = 0;
   virtual void Allgather(const void* send, void* recv, size_t bytes_per_rank, void* stream) = 0;
   virtual void ReduceScatterSumF64(const double* send, double* recv, size_t recv_count, void* stream) = 0;
+  // send holds size() blocks of recv_count elements; rank r receives the sum of block r
+  virtual void ReduceScatterSumI64(const long long* send, long long* recv, size_t recv_count, void* stream) = 0;
   virtual void Broadcast(void* buf, size_t bytes, int root, void* stream) = 0;
+  // the collectives can be captured into a hipGraph (stream-ordered, no host rendezvous)
+  virtual bool CaptureSafe() const { return true; }
   // failure detection (watchdog of the device learner): an asynchronous communicator error,
   // and aborting every pending collective so that no rank stays blocked
   virtual bool AsyncError(std::string* msg) {
@@ -158,5 +162,10 @@ class Network {
 // (that rank raises at its fail_at_call-th collective, its peers then raise too)
 std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks, double timeout_s = 0,
                                                                  int fail_rank = -1, int fail_at_call = 0);
+
+// in-process device collectives for ranks that are threads sharing one GPU (tests and
+// rehearsal of the distributed device learners without RCCL): each call rendezvouses the
+// threads, then device kernels read the peers' buffers directly.  Not graph-capturable.
+std::vector<std::shared_ptr<DeviceComm>> MakeThreadDeviceComms(int num_ranks, double timeout_s = 0);
 
 }  // namespace lgbm_amd

@@ -9,6 +9,10 @@ one rank: the failing rank raises, its peers raise "peer rank failed" instead of
 
     ranks = ThreadRanks(world=2, timeout_s=30)
     results = ranks.run(lambda rank: train_my_shard(rank))
+
+With device_comm=True every rank thread also joins an in-process device communicator (the
+threads share one GPU; collectives are device kernels over the peers' buffers), so the
+data- / feature-parallel device learners run their device collective path without RCCL.
 """
 import ctypes
 import threading
@@ -30,12 +34,17 @@ class RankResult:
 
 
 class ThreadRanks:
-    def __init__(self, world, timeout_s=0.0, fail_rank=-1, fail_at_call=0):
+    def __init__(self, world, timeout_s=0.0, fail_rank=-1, fail_at_call=0, device_comm=False):
         self.world = int(world)
         self._hub = ctypes.c_void_p()
-        _safe_call(_load_lib().LGBM_AMD_NetworkCreateThreadHub(
+        self._dev_hub = ctypes.c_void_p()
+        lib = _load_lib()
+        _safe_call(lib.LGBM_AMD_NetworkCreateThreadHub(
             ctypes.c_int(self.world), ctypes.c_double(timeout_s), ctypes.c_int(fail_rank),
             ctypes.c_int(fail_at_call), ctypes.byref(self._hub)))
+        if device_comm:
+            _safe_call(lib.LGBM_AMD_DeviceCommCreateThreadHub(
+                ctypes.c_int(self.world), ctypes.c_double(timeout_s), ctypes.byref(self._dev_hub)))
 
     def run(self, fn):
         """Call fn(rank) in one thread per rank (joined to the hub); returns [RankResult]."""
@@ -45,6 +54,8 @@ class ThreadRanks:
         def body(rank):
             try:
                 _safe_call(lib.LGBM_AMD_NetworkJoinThreadHub(self._hub, ctypes.c_int(rank)))
+                if self._dev_hub:
+                    _safe_call(lib.LGBM_AMD_DeviceCommJoinThreadHub(self._dev_hub, ctypes.c_int(rank)))
                 results[rank] = RankResult(rank, value=fn(rank))
             except Exception as e:  # noqa: BLE001 -- reported per rank
                 results[rank] = RankResult(rank, error=e)
@@ -62,6 +73,9 @@ class ThreadRanks:
         if self._hub:
             _load_lib().LGBM_AMD_NetworkFreeThreadHub(self._hub)
             self._hub = ctypes.c_void_p()
+        if self._dev_hub:
+            _load_lib().LGBM_AMD_DeviceCommFreeThreadHub(self._dev_hub)
+            self._dev_hub = ctypes.c_void_p()
 
     def __enter__(self):
         return self

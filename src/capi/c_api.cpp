@@ -1325,6 +1325,34 @@ int LGBM_AMD_NetworkFreeThreadHub(void* hub) {
   API_END();
 }
 
+// in-process device communicators for thread ranks sharing one GPU (src/network/
+// inproc_device_comm.cpp); a rank thread joins after joining the host hub
+struct DeviceRankHub {
+  std::vector<std::shared_ptr<DeviceComm>> ranks;
+};
+
+int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, void** out) {
+  API_BEGIN();
+  auto* h = new DeviceRankHub();
+  h->ranks = MakeThreadDeviceComms(num_ranks, timeout_s);
+  *out = h;
+  API_END();
+}
+
+int LGBM_AMD_DeviceCommJoinThreadHub(void* hub, int rank) {
+  API_BEGIN();
+  auto* h = static_cast<DeviceRankHub*>(hub);
+  if (rank < 0 || rank >= static_cast<int>(h->ranks.size())) Log::Fatal("rank %d out of range", rank);
+  Network::SetDeviceComm(h->ranks[rank]);
+  API_END();
+}
+
+int LGBM_AMD_DeviceCommFreeThreadHub(void* hub) {
+  API_BEGIN();
+  delete static_cast<DeviceRankHub*>(hub);
+  API_END();
+}
+
 int LGBM_AMD_GetTimers(int64_t buffer_len, int64_t* out_len, char* out_str) {
   API_BEGIN();
   std::string s;

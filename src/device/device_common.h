@@ -135,7 +135,7 @@ __device__ __forceinline__ bool SplitBetter(double ga, int fa, double gb, int fb
 // histogram buffers: the root uses buffer 0, split s buffer (s + 1) & 1; the split scan of
 // split s zeroes the other one for split s + 1
 __device__ __forceinline__ long long* StepScratch(const KArgs& a, int parity) {
-  return a.scratch + static_cast<size_t>(parity & 1) * 2 * a.p.total_bins;
+  return a.scratch + static_cast<size_t>(parity & 1) * a.scratch_stride;
 }
 
 

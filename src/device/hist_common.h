@@ -18,8 +18,8 @@ struct TileCtx {
 // every load is independent of the others (a single round trip)
 template <int GPW>
 __device__ __forceinline__ void InitTile(const KArgs& a, TileCtx* t) {
-  t->w0 = blockIdx.y * a.tile_words;
-  t->w1 = min(a.words_per_row, t->w0 + a.tile_words);
+  t->w0 = a.tile_w0 + blockIdx.y * a.tile_words;
+  t->w1 = min(a.tile_w1, t->w0 + a.tile_words);
   const int g0 = t->w0 * GPW;
   const int g_end = min(a.p.num_groups, t->w1 * GPW);
   t->tpr = t->w1 - t->w0;

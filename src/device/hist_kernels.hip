@@ -174,12 +174,13 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
       h += static_cast<long long>(v[k].y);
     }
   }
+  const int pos = a.rs_pos != nullptr ? a.rs_pos[bin] : bin;  // owner-major layout (data-parallel)
   if (nblk <= kReduceChunk) {
-    out[2 * bin] = g;
-    out[2 * bin + 1] = h;
+    out[2 * pos] = g;
+    out[2 * pos + 1] = h;
   } else {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin]), static_cast<unsigned long long>(g));
-    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin + 1]), static_cast<unsigned long long>(h));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * pos]), static_cast<unsigned long long>(g));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * pos + 1]), static_cast<unsigned long long>(h));
   }
   KTrace(a, ts, kTrRedExit);
 }

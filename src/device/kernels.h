@@ -31,7 +31,8 @@ struct KArgs {
   // histograms hold fixed-point sums: int64 (g * scale_g, h * scale_h) per bin, exact and
   // order-independent (LDS float atomics are slow on gfx950; integer ones are not)
   long long* hist;           // [num_leaves][total_bins][2]
-  long long* scratch;        // [2][total_bins][2] the histogram being built (step parity)
+  long long* scratch;        // [2][scratch_stride] the histogram being built (step parity)
+  int64_t scratch_stride;    // int64 per parity buffer: 2 * total_bins, or the padded owner-major layout
   // per-row-block partial histograms, [hist_max_blocks][total_bins][hist_units] u64: one packed
   // (g | h) word per bin (hist_units 1) or int64 g, int64 h (hist_units 2, gpu_use_dp)
   unsigned long long* partials;
@@ -53,6 +54,20 @@ struct KArgs {
   int32_t root_grid;         // workgroups of a root / range histogram launch
   int32_t blk_min_rows;      // k_split: parent rows per row block, lower bound
   int32_t pick_in_find;      // the last split-scan workgroup of a step picks the next split (else k_pick)
+  // distributed learners (reference data_parallel_tree_learner.cpp / feature_parallel_*):
+  // features are owned by ranks in contiguous storage-group blocks; a rank scans its own
+  const int32_t* feat_list;  // [num_scan] inner features this rank scans (null: all)
+  int32_t num_scan;          // features this rank scans
+  const int32_t* fb_index;   // feat_best slot of feature f for side 0 (null: f); side 1 adds fb_side
+  int32_t fb_side;
+  // data-parallel: the reduce kernel writes bin b at rs_pos[b] (owner-major blocks, padded
+  // to equal size for the reduce-scatter) and the split scan reads this rank's globally
+  // summed block from owned_hist (bin b at 2 * (b - owned_bin_lo)); null: the local scratch
+  const int32_t* rs_pos;
+  const long long* owned_hist;
+  int32_t owned_bin_lo;
+  // histogram column range (feature-parallel: the words of this rank's features)
+  int32_t tile_w0, tile_w1;
   const uint8_t* bins_col;   // column-major copy of the bin matrix ([group][rows], bin_bytes each)
   int32_t num_data;          // rows of the matrix (column stride of bins_col)
   int32_t host_mode;         // partition: the host wrote Step::cs (host-assisted growth)
@@ -159,6 +174,15 @@ void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t
                   hipStream_t s);
 
 void Iota(int32_t* p, int64_t n, hipStream_t s);
+
+// element-wise reduction over the buffers of up to kMaxPeerBufs ranks sharing the device
+// (the in-process device communicator): out[i] = op(src_0[off + i], ..., src_{n-1}[off + i])
+constexpr int kMaxPeerBufs = 16;
+struct PeerBufs {
+  const void* p[kMaxPeerBufs];
+};
+enum PeerOp { kPeerSumF64 = 0, kPeerSumF32 = 1, kPeerSumI64 = 2, kPeerMaxU32 = 3 };
+void ReducePeers(const PeerBufs& src, int n, size_t offset, void* out, size_t count, int op, hipStream_t s);
 
 // score scaling helpers
 void AddConst(double* score, int64_t n, double v, hipStream_t s);

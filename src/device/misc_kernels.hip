@@ -164,6 +164,41 @@ __global__ void k_iota(int32_t* p, int64_t n) {
     p[i] = static_cast<int32_t>(i);
 }
 
+template <typename T, int OP>
+__global__ void k_reduce_peers(PeerBufs src, int n, size_t offset, T* out, size_t count) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < count;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x) {
+    T v = static_cast<const T*>(src.p[0])[offset + i];
+    for (int r = 1; r < n; ++r) {
+      const T x = static_cast<const T*>(src.p[r])[offset + i];
+      v = OP == 3 ? (x > v ? x : v) : v + x;
+    }
+    out[i] = v;
+  }
+}
+
+void ReducePeers(const PeerBufs& src, int n, size_t offset, void* out, size_t count, int op, hipStream_t s) {
+  const int grid = GridFor(static_cast<int64_t>(count));
+  switch (op) {
+    case kPeerSumF64:
+      hipLaunchKernelGGL((k_reduce_peers<double, 0>), dim3(grid), dim3(256), 0, s, src, n, offset,
+                         static_cast<double*>(out), count);
+      break;
+    case kPeerSumF32:
+      hipLaunchKernelGGL((k_reduce_peers<float, 0>), dim3(grid), dim3(256), 0, s, src, n, offset,
+                         static_cast<float*>(out), count);
+      break;
+    case kPeerSumI64:
+      hipLaunchKernelGGL((k_reduce_peers<long long, 0>), dim3(grid), dim3(256), 0, s, src, n, offset,
+                         static_cast<long long*>(out), count);
+      break;
+    default:
+      hipLaunchKernelGGL((k_reduce_peers<uint32_t, 3>), dim3(grid), dim3(256), 0, s, src, n, offset,
+                         static_cast<uint32_t*>(out), count);
+      break;
+  }
+}
+
 void Iota(int32_t* p, int64_t n, hipStream_t s) { hipLaunchKernelGGL(k_iota, dim3(GridFor(n)), dim3(256), 0, s, p, n); }
 void AddConst(double* score, int64_t n, double v, hipStream_t s) {
   hipLaunchKernelGGL(k_add_const, dim3(GridFor(n)), dim3(256), 0, s, score, n, v);

@@ -66,8 +66,10 @@ __device__ __forceinline__ void ToDeviceSplit(const FeatureBest& b, const uint32
   }
 }
 
-// per-feature results of side (0 smaller, 1 larger) for inner feature f
+// per-feature results of side (0 smaller, 1 larger) for inner feature f (distributed
+// learners: rank-major blocks, gathered from every rank after the scans)
 __device__ __forceinline__ size_t FeatBestIndex(const KArgs& a, int side, int f) {
+  if (a.fb_index != nullptr) return static_cast<size_t>(a.fb_index[f]) + static_cast<size_t>(side) * a.fb_side;
   return static_cast<size_t>(side) * a.p.num_features + f;
 }
 __device__ __forceinline__ const uint32_t* FeatCat(const KArgs& a, int side, int f) {

@@ -735,7 +735,7 @@ template <bool ROOT, int KIND, bool SIMPLE>
 __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND>& sh) {
   constexpr bool CAT = KIND == 2;
   const long long t_entry = wall_clock64();
-  const int f = CAT ? a.cat_list[blockIdx.x] : static_cast<int>(blockIdx.x);
+  const int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
   const int side = blockIdx.y;
   const int tid = threadIdx.x;
   const int units = a.hist_units;
@@ -784,8 +784,9 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   int parity = 0, nblk_direct = -1;
   if (!ROOT) {
     parity = (s + 1) & 1;
-    // zero this feature's bins of the buffer the next step reduces into
-    if (!CAT && side == 0) {
+    // zero this feature's bins of the buffer the next step reduces into (data-parallel:
+    // the whole owner-major buffer is cleared before each reduction)
+    if (!CAT && side == 0 && a.rs_pos == nullptr) {
       long long* nxt = StepScratch(a, parity + 1);
       for (int i = tid; i < nb2; i += kFindThreads) nxt[2 * F.hist_offset + i] = 0;
     }
@@ -870,7 +871,8 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   if (tree_used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
-    const long long* src = StepScratch(a, parity) + 2 * F.hist_offset;
+    const long long* src = a.owned_hist != nullptr ? a.owned_hist + 2 * (F.hist_offset - a.owned_bin_lo)
+                                                   : StepScratch(a, parity) + 2 * F.hist_offset;
     const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
     const unsigned long long* part = a.partials + static_cast<size_t>(units) * F.hist_offset;
     const bool stage = a.p.max_feature_bins <= kFindLdsBins;
@@ -1033,13 +1035,14 @@ static bool SimpleGains(const KArgs& a) {
 }
 template <bool ROOT>
 static void LaunchFind(const KArgs& a, hipStream_t s) {
-  const dim3 g(a.p.num_features, ROOT ? 1 : 2), b(kFindThreads);
+  if (a.num_scan <= 0) return;  // a rank that owns no feature
+  const dim3 g(a.num_scan, ROOT ? 1 : 2), b(kFindThreads);
   const size_t lds = FindLds(a);
   const bool simple = SimpleGains(a);
   if (a.p.has_cat) {
     if (simple) hipLaunchKernelGGL((k_find<ROOT, 1, true>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_find<ROOT, 1, false>), g, b, lds, s, a);
-    hipLaunchKernelGGL((k_find<ROOT, 2, false>), dim3(a.p.has_cat, ROOT ? 1 : 2), b, lds, s, a);
+    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false>), dim3(a.p.has_cat, ROOT ? 1 : 2), b, lds, s, a);
   } else {
     if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_find<ROOT, 0, false>), g, b, lds, s, a);

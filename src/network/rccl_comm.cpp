@@ -56,6 +56,9 @@ class RcclComm : public DeviceComm {
   void ReduceScatterSumF64(const double* send, double* recv, size_t recv_count, void* stream) override {
     RCCLCHECK(ncclReduceScatter(send, recv, recv_count, ncclFloat64, ncclSum, comm_, static_cast<hipStream_t>(stream)));
   }
+  void ReduceScatterSumI64(const long long* send, long long* recv, size_t recv_count, void* stream) override {
+    RCCLCHECK(ncclReduceScatter(send, recv, recv_count, ncclInt64, ncclSum, comm_, static_cast<hipStream_t>(stream)));
+  }
   void Broadcast(void* buf, size_t bytes, int root, void* stream) override {
     RCCLCHECK(ncclBroadcast(buf, buf, bytes, ncclUint8, root, comm_, static_cast<hipStream_t>(stream)));
   }
@@ -116,8 +119,9 @@ int LGBM_AMD_RcclInit(int num_ranks, int rank, int device_id, const char* unique
   return 0;
 }
 
-// every collective of the device comm on small device buffers, checked on the host:
-// rank r contributes (r + 1) * i to element i, so sums are (n (n + 1) / 2) * i
+// every collective of the device comm (RCCL or the in-process one) on small device
+// buffers, checked on the host: rank r contributes (r + 1) * i to element i, so sums are
+// (n (n + 1) / 2) * i; plus an int64 reduce-scatter and an allgather
 int LGBM_AMD_RcclSelfTest(int* out_ok) {
   try {
     DeviceComm* dc = Network::device_comm();
@@ -147,12 +151,35 @@ int LGBM_AMD_RcclSelfTest(int* out_ok) {
     dc->AllreduceSumI64(di64, cnt, s);
     dc->AllreduceSumF64(df64, cnt, s);
     dc->AllreduceMaxU32(du32, cnt, s);
+    // reduce-scatter: block r of every rank holds (rank + 1) * (r * 10 + j); rank r receives
+    // sum over ranks = tri * (r * 10 + j); allgather of 8-byte records: rank q sends q + 1
+    const size_t blk = 10;
+    long long *rs_in = nullptr, *rs_out = nullptr, *ag = nullptr;
+    if (hipMalloc(&rs_in, blk * n * sizeof(long long)) != hipSuccess || hipMalloc(&rs_out, blk * sizeof(long long)) != hipSuccess ||
+        hipMalloc(&ag, n * sizeof(long long)) != hipSuccess) {
+      Log::Fatal("hipMalloc failed");
+    }
+    std::vector<long long> hrs(blk * n), hag(n, 0);
+    for (size_t i = 0; i < blk * n; ++i) hrs[i] = static_cast<long long>((r + 1) * i);
+    hag[r] = r + 1;
+    (void)hipMemcpy(rs_in, hrs.data(), hrs.size() * sizeof(long long), hipMemcpyHostToDevice);
+    (void)hipMemcpy(ag, hag.data(), hag.size() * sizeof(long long), hipMemcpyHostToDevice);
+    dc->ReduceScatterSumI64(rs_in, rs_out, blk, s);
+    dc->Allgather(ag + r, ag, sizeof(long long), s);
     (void)hipStreamSynchronize(s);
+    std::vector<long long> hro(blk);
+    (void)hipMemcpy(hro.data(), rs_out, blk * sizeof(long long), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(hag.data(), ag, n * sizeof(long long), hipMemcpyDeviceToHost);
+    (void)hipFree(rs_in);
+    (void)hipFree(rs_out);
+    (void)hipFree(ag);
     (void)hipMemcpy(hi.data(), di64, cnt * sizeof(long long), hipMemcpyDeviceToHost);
     (void)hipMemcpy(hf.data(), df64, cnt * sizeof(double), hipMemcpyDeviceToHost);
     (void)hipMemcpy(hu.data(), du32, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost);
     const long long tri = static_cast<long long>(n) * (n + 1) / 2;
     bool ok = true;
+    for (size_t j = 0; j < blk; ++j) ok = ok && hro[j] == tri * static_cast<long long>(r * blk + j);
+    for (int q = 0; q < n; ++q) ok = ok && hag[q] == q + 1;
     for (size_t i = 0; i < cnt; ++i) {
       ok = ok && hi[i] == tri * static_cast<long long>(i) - 500LL * n;
       ok = ok && hf[i] == 0.5 * static_cast<double>(tri) * static_cast<double>(i);

@@ -42,19 +42,15 @@ int PickDevice(const Config* cfg) {
 }  // namespace
 
 TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Config* config) {
-  if (learner_type == "serial") return new GPUTreeLearner(config, false);
-  if (learner_type == "data") return new GPUTreeLearner(config, true);
-  if (learner_type == "feature") {
-    Log::Warning("feature-parallel learning on the device learner uses the serial device learner on every rank");
-    return new GPUTreeLearner(config, false);
-  }
+  if (learner_type == "serial") return new GPUTreeLearner(config, GPUTreeLearner::Mode::kSerial);
+  if (learner_type == "data") return new GPUTreeLearner(config, GPUTreeLearner::Mode::kData);
+  if (learner_type == "feature") return new GPUTreeLearner(config, GPUTreeLearner::Mode::kFeature);
   if (learner_type == "voting") return new VotingParallelTreeLearner<GPUTreeLearner>(config);
   Log::Fatal("Unknown tree learner type %s", learner_type.c_str());
   return nullptr;
 }
 
-GPUTreeLearner::GPUTreeLearner(const Config* config, bool data_parallel)
-    : SerialTreeLearner(config), data_parallel_(data_parallel) {}
+GPUTreeLearner::GPUTreeLearner(const Config* config, Mode mode) : SerialTreeLearner(config), mode_(mode) {}
 
 GPUTreeLearner::~GPUTreeLearner() {
   FreeAll();
@@ -112,6 +108,10 @@ void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
     Log::Fatal("device learner supports num_leaves <= %d", dev::kMaxLeaves);
   }
   device_id_ = PickDevice(config_);
+  world_ = Network::num_machines();
+  rank_ = Network::rank();
+  distributed_ = mode_ != Mode::kSerial && world_ > 1;
+  data_parallel_ = mode_ == Mode::kData && world_ > 1;
   HIPCHECK(hipSetDevice(device_id_));
   int cus = 0;
   HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
@@ -219,6 +219,10 @@ void GPUTreeLearner::UploadData() {
     if (tile_words > 0) break;
   }
   if (tile_words == 0) Log::Fatal("device learner: feature groups too wide for LDS histograms; reduce max_bin");
+  num_cat_total_ = 0;
+  for (const auto& F : feats) num_cat_total_ += F.is_cat ? 1 : 0;
+  args_.tile_words = tile_words;
+  SetupOwnership();
   const int n_leaves = config_->num_leaves;
   d_tree_mask_ = Alloc<int8_t>(num_features_);
   d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
@@ -236,11 +240,17 @@ void GPUTreeLearner::UploadData() {
   d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
   d_best_ = Alloc<DeviceSplit>(n_leaves);
   d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
-  d_scratch_ = Alloc<long long>(4 * static_cast<size_t>(total_bins_));  // two step buffers
+  // two step buffers (data-parallel: owner-major blocks padded to equal size)
+  const int64_t scratch_stride =
+      std::max<int64_t>(2 * static_cast<int64_t>(total_bins_), 2 * static_cast<int64_t>(world_) * rs_block_);
+  d_scratch_ = Alloc<long long>(2 * static_cast<size_t>(scratch_stride));
   d_scales_ = Alloc<double>(4);
   d_absmax_ = Alloc<uint32_t>(4);
-  d_feat_best_ = Alloc<dev::FeatureBest>(2 * static_cast<size_t>(std::max(1, num_features_)));
-  d_feat_cat_ = Alloc<uint32_t>(2 * static_cast<size_t>(std::max(1, num_features_)) * kMaxCatWords);
+  // per-feature results: [2][num_features], or rank-major [world][2][max_owned] (gathered)
+  const size_t fb_slots = std::max<size_t>(2 * static_cast<size_t>(std::max(1, num_features_)),
+                                           2 * static_cast<size_t>(world_) * std::max(1, max_owned_));
+  d_feat_best_ = Alloc<dev::FeatureBest>(fb_slots);
+  d_feat_cat_ = Alloc<uint32_t>(fb_slots * kMaxCatWords);
   // row blocks: the root histogram runs on two workgroups per CU, a split step on one; a
   // packed (hist_units 1) row block holds at most kHistRowsCap rows, so the fixed-point
   // scale does not depend on the number of rows; wide blocks are unbounded
@@ -278,7 +288,7 @@ void GPUTreeLearner::UploadData() {
   a.p.row_stride = static_cast<int32_t>(row_bytes);
   a.p.total_bins = total_bins_;
   a.p.monotone_penalty = config_->monotone_penalty;
-  a.p.data_parallel = data_parallel_ ? 1 : 0;
+  a.p.data_parallel = data_parallel_ ? 1 : 0;  // global counts from the split estimates
   a.bins = d_bins_;
   a.feat = d_feat_;
   a.group_off = d_group_off_;
@@ -293,6 +303,7 @@ void GPUTreeLearner::UploadData() {
   a.best = d_best_;
   a.hist = d_hist_;
   a.scratch = d_scratch_;
+  a.scratch_stride = scratch_stride;
   a.partials = d_partials_;
   a.hist_max_blocks = hist_blocks;
   a.hist_units = hist_units_;
@@ -300,10 +311,10 @@ void GPUTreeLearner::UploadData() {
   a.split_grid = split_grid_;
   a.blk_min_rows = blk_min_rows_;
   a.hist_rows_cap = rows_cap_;
-  a.pick_in_find = data_parallel_ ? 0 : 1;
+  a.pick_in_find = distributed_ ? 0 : 1;  // distributed: k_pick after the gather
   a.host_mode = 0;
   a.ktrace = nullptr;
-  if (const char* kt = std::getenv("LGBM_AMD_KTRACE")) {
+  if (const char* kt = std::getenv("LGBM_AMD_KTRACE")) {  // (before the rest of the arguments)
     if (kt[0] == '1') {
       d_ktrace_ = Alloc<long long>(static_cast<size_t>(n_leaves) * dev::kTraceSlots);
       a.ktrace = d_ktrace_;
@@ -317,6 +328,15 @@ void GPUTreeLearner::UploadData() {
   a.words_per_row = wpr;
   a.tile_words = tile_words;
   a.hist_tiles = (wpr + tile_words - 1) / tile_words;
+  a.tile_w0 = 0;
+  a.tile_w1 = wpr;
+  a.feat_list = nullptr;
+  a.num_scan = num_features_;
+  a.fb_index = nullptr;
+  a.fb_side = num_features_;
+  a.rs_pos = nullptr;
+  a.owned_hist = nullptr;
+  a.owned_bin_lo = 0;
   a.tile_bins = tile_bins_for(tile_words);
   a.range_begin = 0;
   a.scales = d_scales_;
@@ -342,8 +362,113 @@ void GPUTreeLearner::UploadData() {
     HIPCHECK(hipMemcpy(d_cat_list_, cats.data(), sizeof(int32_t) * cats.size(), hipMemcpyHostToDevice));
   }
   a.cat_list = d_cat_list_;
+  if (distributed_) {
+    // this rank scans its own features; the per-feature results are gathered rank-major
+    a.feat_list = d_feat_list_;
+    a.num_scan = static_cast<int32_t>(owned_feats_.size());
+    a.fb_index = d_fb_index_;
+    a.fb_side = max_owned_;
+    int owned_cats = 0;
+    for (int f : owned_feats_) owned_cats += feats[f].is_cat ? 1 : 0;
+    a.p.has_cat = owned_cats;
+    a.cat_list = d_owned_cats_;
+    if (mode_ == Mode::kData) {
+      a.rs_pos = d_rs_pos_;
+      a.owned_hist = d_owned_hist_;
+      a.owned_bin_lo = owned_bin_lo_;
+    } else {
+      // feature-parallel: every rank has every row; histograms only over this rank's words
+      int g_lo = num_groups_, g_hi = 0;
+      for (int f : owned_feats_) {
+        g_lo = std::min(g_lo, feats[f].group);
+        g_hi = std::max(g_hi, feats[f].group + 1);
+      }
+      if (g_lo < g_hi) {
+        a.tile_w0 = g_lo / gpw;
+        a.tile_w1 = (g_hi + gpw - 1) / gpw;
+      } else {  // no features: one tile of redundant work keeps the partition's launch shape
+        a.tile_w0 = 0;
+        a.tile_w1 = std::min(wpr, tile_words);
+      }
+      a.hist_tiles = (a.tile_w1 - a.tile_w0 + tile_words - 1) / tile_words;
+    }
+  }
   UploadInteractionMasks();
   AllocSplittable();
+}
+
+// Feature ownership of the distributed learners (reference data_parallel_tree_learner.cpp
+// BeforeTrain :61-123 assigns used features to the least-loaded rank per tree; here the
+// storage groups are cut into `world` contiguous blocks balanced by histogram bins once, so
+// a rank's bins are one contiguous range of the histogram -- the reduce-scatter block it
+// receives -- and its features are gathered rank-major after each scan):
+//   owner(group g) = min(world - 1, mid(g) * world / total_bins), monotone in g.
+void GPUTreeLearner::SetupOwnership() {
+  owned_feats_.clear();
+  max_owned_ = 0;
+  rs_block_ = 0;
+  owned_bin_lo_ = 0;
+  if (!distributed_) return;
+  std::vector<int32_t> goff(num_groups_ + 1, total_bins_);
+  for (int g = 0; g < num_groups_; ++g) goff[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
+  std::vector<int> gown(num_groups_);
+  std::vector<int> lo(world_, -1), hi(world_, -1);
+  for (int g = 0; g < num_groups_; ++g) {
+    const long long mid2 = static_cast<long long>(goff[g]) + goff[g + 1];
+    gown[g] = static_cast<int>(std::min<long long>(world_ - 1, mid2 * world_ / (2LL * std::max(1, total_bins_))));
+    const int r = gown[g];
+    if (lo[r] < 0) lo[r] = goff[g];
+    hi[r] = goff[g + 1];
+  }
+  int prev_end = 0;
+  for (int r = 0; r < world_; ++r) {
+    if (lo[r] < 0) lo[r] = hi[r] = prev_end;  // a rank without groups: empty block
+    prev_end = hi[r];
+    rs_block_ = std::max(rs_block_, hi[r] - lo[r]);
+  }
+  rs_block_ = std::max(rs_block_, 1);
+  owned_bin_lo_ = lo[rank_];
+  std::vector<int> count(world_, 0), local(num_features_, 0), fown(num_features_, 0);
+  for (int f = 0; f < num_features_; ++f) {
+    fown[f] = gown[data_->Feature2Group(f)];
+    local[f] = count[fown[f]]++;
+    if (fown[f] == rank_) owned_feats_.push_back(f);
+  }
+  for (int r = 0; r < world_; ++r) max_owned_ = std::max(max_owned_, count[r]);
+  max_owned_ = std::max(max_owned_, 1);
+  std::vector<int32_t> fb_index(std::max(1, num_features_));
+  for (int f = 0; f < num_features_; ++f) fb_index[f] = fown[f] * 2 * max_owned_ + local[f];
+  std::vector<int32_t> rs_pos(std::max(1, total_bins_));
+  for (int g = 0; g < num_groups_; ++g) {
+    for (int b = goff[g]; b < goff[g + 1]; ++b) rs_pos[b] = gown[g] * rs_block_ + (b - lo[gown[g]]);
+  }
+  std::vector<int32_t> owned_cats;
+  for (int f : owned_feats_) {
+    if (data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) owned_cats.push_back(f);
+  }
+  auto upload = [&](const std::vector<int32_t>& v) {
+    int32_t* d = Alloc<int32_t>(std::max<size_t>(1, v.size()));
+    if (!v.empty()) HIPCHECK(hipMemcpy(d, v.data(), sizeof(int32_t) * v.size(), hipMemcpyHostToDevice));
+    return d;
+  };
+  d_feat_list_ = upload(std::vector<int32_t>(owned_feats_.begin(), owned_feats_.end()));
+  d_fb_index_ = upload(fb_index);
+  d_rs_pos_ = upload(rs_pos);
+  d_owned_cats_ = upload(owned_cats);
+  d_owned_hist_ = Alloc<long long>(2 * static_cast<size_t>(rs_block_));
+  const size_t fb_bytes = 2 * static_cast<size_t>(max_owned_) *
+                          (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0));
+  if (mode_ == Mode::kData) {
+    Log::Info("data-parallel device learner, rank %d of %d: %d features, histogram bins [%d, %d); per split "
+              "reduce-scatter %zu bytes in / %zu out, split-record allgather %zu bytes per rank",
+              rank_, world_, static_cast<int>(owned_feats_.size()), lo[rank_], hi[rank_],
+              sizeof(long long) * 2 * static_cast<size_t>(rs_block_) * world_,
+              sizeof(long long) * 2 * static_cast<size_t>(rs_block_), fb_bytes);
+  } else {
+    Log::Info("feature-parallel device learner, rank %d of %d: %d features, histogram bins [%d, %d); per split "
+              "split-record allgather %zu bytes per rank", rank_, world_, static_cast<int>(owned_feats_.size()),
+              lo[rank_], hi[rank_], fb_bytes);
+  }
 }
 
 // interaction constraints as per-feature constraint bitmasks (device-resident growth
@@ -519,7 +644,7 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
 // errors and bound the wait by time_out minutes (the reference's socket timeout): a failed
 // or vanished peer aborts the communicator and raises instead of hanging every rank
 void GPUTreeLearner::WatchdogSync() {
-  DeviceComm* dc = (data_parallel_ && Network::num_machines() > 1) ? Network::device_comm() : nullptr;
+  DeviceComm* dc = distributed_ ? Network::device_comm() : nullptr;
   if (dc == nullptr) {
     HIPCHECK(hipStreamSynchronize(stream_));
     return;
@@ -559,21 +684,52 @@ void GPUTreeLearner::AllreduceRoot() {
   HIPCHECK(hipMemcpyAsync(d_root_, h_root_, sizeof(double) * 3, hipMemcpyHostToDevice, stream_));
 }
 
-void GPUTreeLearner::AllreduceScratch(int parity) {
-  if (!data_parallel_ || Network::num_machines() <= 1) return;
+// data-parallel: this rank's owner block of the step's histogram, summed over every rank
+// (reference data_parallel_tree_learner.cpp:154-173 ReduceScatter into feature owners)
+void GPUTreeLearner::ReduceScatterStep(int parity) {
+  if (!data_parallel_) return;
   DeviceComm* dc = Network::device_comm();
-  const size_t n = 2 * static_cast<size_t>(total_bins_);
-  long long* buf = d_scratch_ + static_cast<size_t>(parity & 1) * n;
+  long long* send = d_scratch_ + static_cast<size_t>(parity & 1) * args_.scratch_stride;
+  const size_t block = 2 * static_cast<size_t>(rs_block_);
   if (dc != nullptr) {
-    dc->AllreduceSumI64(buf, n, stream_);  // exact: fixed-point integers
+    dc->ReduceScatterSumI64(send, d_owned_hist_, block, stream_);  // exact: fixed-point integers
     return;
   }
-  std::vector<long long> h(n);
-  HIPCHECK(hipMemcpyAsync(h.data(), buf, sizeof(long long) * n, hipMemcpyDeviceToHost, stream_));
+  // host collectives: the whole padded buffer, summed on the host
+  std::vector<long long> h(block * world_);
+  HIPCHECK(hipMemcpyAsync(h.data(), send, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   auto v = Network::GlobalSum(h);
-  HIPCHECK(hipMemcpyAsync(buf, v.data(), sizeof(long long) * n, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_owned_hist_, v.data() + block * rank_, sizeof(long long) * block, hipMemcpyHostToDevice,
+                          stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
+}
+
+// distributed: every rank's per-feature results (and category sets), rank-major, so each
+// rank picks the same split (reference SyncUpGlobalBestSplit, parallel_tree_learner.h:190)
+void GPUTreeLearner::GatherFeatureBests() {
+  if (!distributed_) return;
+  DeviceComm* dc = Network::device_comm();
+  const size_t fb_bytes = 2 * static_cast<size_t>(max_owned_) * sizeof(dev::FeatureBest);
+  const size_t cat_bytes = 2 * static_cast<size_t>(max_owned_) * kMaxCatWords * sizeof(uint32_t);
+  char* fb = reinterpret_cast<char*>(d_feat_best_);
+  char* fc = reinterpret_cast<char*>(d_feat_cat_);
+  if (dc != nullptr) {
+    dc->Allgather(fb + fb_bytes * rank_, fb, fb_bytes, stream_);
+    if (num_cat_total_ > 0) dc->Allgather(fc + cat_bytes * rank_, fc, cat_bytes, stream_);
+    return;
+  }
+  auto host_gather = [&](char* d, size_t bytes) {
+    std::vector<char> all(bytes * world_);
+    HIPCHECK(hipMemcpyAsync(all.data() + bytes * rank_, d + bytes * rank_, bytes, hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
+    std::vector<char> mine(all.begin() + bytes * rank_, all.begin() + bytes * (rank_ + 1));
+    Network::Allgather(mine.data(), static_cast<comm_size_t>(bytes), all.data());
+    HIPCHECK(hipMemcpyAsync(d, all.data(), all.size(), hipMemcpyHostToDevice, stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
+  };
+  host_gather(fb, fb_bytes);
+  if (num_cat_total_ > 0) host_gather(fc, cat_bytes);
 }
 
 void GPUTreeLearner::AllreduceAbsMax() {
@@ -702,7 +858,8 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   }
   HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
   // both step buffers start at zero; afterwards each split-scan zeroes the next one
-  const size_t scratch_bytes = sizeof(long long) * 4 * static_cast<size_t>(total_bins_);
+  // (data-parallel: the owner-major buffer is cleared before every reduction)
+  const size_t stride_bytes = sizeof(long long) * static_cast<size_t>(a.scratch_stride);
   if (a.ktrace != nullptr) {
     HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
   }
@@ -712,19 +869,30 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   }
   if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
   AllreduceRoot();
-  HIPCHECK(hipMemsetAsync(d_scratch_, 0, scratch_bytes, stream_));
+  HIPCHECK(hipMemsetAsync(d_scratch_, 0, 2 * stride_bytes, stream_));
   dev::HistRoot(a, stream_);
-  AllreduceScratch(0);
+  ReduceScatterStep(0);
   dev::FindRoot(a, stream_);
-  if (!a.pick_in_find) dev::PickStep(a, stream_, true);
+  if (distributed_) {
+    GatherFeatureBests();
+    dev::PickStep(a, stream_, true);
+  }
   // one split per step: the picked split applied to the leaf's rows with one child's
-  // histogram (+ reduction) -> split scans of both children (+ the next pick).  The sequence
-  // is fixed; kernels of a finished tree exit at once.
+  // histogram (+ reduction, + reduce-scatter to the feature owners) -> split scans of both
+  // children (+ the next pick; distributed: after gathering every rank's results).  The
+  // sequence is fixed; kernels of a finished tree exit at once.
   for (int s = 0; s < config_->num_leaves - 1; ++s) {
+    if (data_parallel_) {
+      HIPCHECK(hipMemsetAsync(d_scratch_ + static_cast<size_t>((s + 1) & 1) * a.scratch_stride, 0, stride_bytes,
+                              stream_));
+    }
     dev::SplitStep(a, stream_, s < a.p.direct_from_split || data_parallel_);
-    AllreduceScratch(s + 1);  // the step's buffer parity
+    ReduceScatterStep(s + 1);
     dev::FindStep(a, stream_);
-    if (!a.pick_in_find) dev::PickStep(a, stream_, false);
+    if (distributed_) {
+      GatherFeatureBests();
+      dev::PickStep(a, stream_, false);
+    }
   }
 }
 
@@ -770,8 +938,9 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   // data-parallel training the per-split RCCL all-reduces are captured into the same graph
   // (they are stream-ordered; every rank enqueues the same collectives either way); with
   // host collectives (no device communicator) the tree is launched eagerly.
-  const bool distributed = data_parallel_ && Network::num_machines() > 1;
-  const bool dev_comm = distributed && Network::device_comm() != nullptr;
+  const bool distributed = distributed_;
+  DeviceComm* dcomm = distributed ? Network::device_comm() : nullptr;
+  const bool dev_comm = dcomm != nullptr && dcomm->CaptureSafe();
   const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
   const char* gc = std::getenv("LGBM_AMD_GRAPH_COLLECTIVES");
   const bool graph_collectives = dev_comm && !(gc != nullptr && gc[0] == '0') && !graph_capture_failed_;

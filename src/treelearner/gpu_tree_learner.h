@@ -29,8 +29,12 @@ namespace lgbm_amd {
 
 class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
  public:
-  GPUTreeLearner(const Config* config, bool data_parallel);
-  explicit GPUTreeLearner(const Config* config) : GPUTreeLearner(config, false) {}
+  // serial: one device; data: rows sharded across ranks (owner-blocked reduce-scatter of the
+  // histograms, reference data_parallel_tree_learner.cpp); feature: every rank holds all
+  // rows and builds / scans only its own features (feature_parallel_tree_learner.cpp)
+  enum class Mode { kSerial, kData, kFeature };
+  GPUTreeLearner(const Config* config, Mode mode);
+  explicit GPUTreeLearner(const Config* config) : GPUTreeLearner(config, Mode::kSerial) {}
   // host-assisted growth for every tree (the voting-parallel learner scans on the host)
   void ForceHostMode() { force_host_mode_ = true; }
   ~GPUTreeLearner() override;
@@ -97,7 +101,6 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void ReportKernelTrace(int num_splits);
   void BuildRangeHistogram(int leaf, int slot);
   void DownloadPartitionToHost() const;
-  void AllreduceScratch(int parity);
   void AllreduceRoot();
   void WatchdogSync();
   void AllreduceAbsMax();
@@ -111,7 +114,24 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   template <typename T>
   T* Alloc(size_t n);
 
-  bool data_parallel_ = false;
+  void SetupOwnership();
+  void GatherFeatureBests();
+  void ReduceScatterStep(int parity);
+  Mode mode_ = Mode::kSerial;
+  bool data_parallel_ = false;  // kData on more than one rank (global counts from the split estimates)
+  bool distributed_ = false;    // kData / kFeature on more than one rank
+  int world_ = 1, rank_ = 0;
+  // feature ownership (distributed): contiguous storage-group blocks balanced by bins
+  std::vector<int> owned_feats_;
+  int max_owned_ = 0;           // features of the largest owner (feat_best block of a rank per side)
+  int owned_bin_lo_ = 0;
+  int rs_block_ = 0;            // padded owner block, histogram bins
+  int num_cat_total_ = 0;
+  int32_t* d_feat_list_ = nullptr;
+  int32_t* d_fb_index_ = nullptr;
+  int32_t* d_rs_pos_ = nullptr;
+  int32_t* d_owned_cats_ = nullptr;
+  long long* d_owned_hist_ = nullptr;
   bool device_mode_ = true;
   bool mode_decided_ = false;  // the first decision is logged too
   bool force_host_mode_ = false;

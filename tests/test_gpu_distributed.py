@@ -1,0 +1,103 @@
+"""Distributed device learners on one MI355X: ranks are threads of this process, each with
+its own stream, joined by the in-process device communicator (device kernels read the peer
+ranks' buffers; src/network/inproc_device_comm.cpp).  This runs the same collective
+sequence as RCCL on a multi-GPU node:
+  * data-parallel: per split the histogrammed child's int64 histogram is reduce-scattered
+    to the feature owners, owners scan their features, the per-feature split records are
+    all-gathered and every rank picks the same split (reference
+    src/treelearner/data_parallel_tree_learner.cpp:61-123, 154-247);
+  * feature-parallel: every rank holds all rows, builds and scans only its features, then
+    the records are gathered (feature_parallel_tree_learner.cpp:37-77).
+Checks: identical models on every rank; the same splits as the serial device learner (bin
+mappers shared through Dataset.subset); feature-parallel equal to serial to rounding."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import lightgbmv1_amd as lgb
+from lightgbmv1_amd.basic import _load_lib, _safe_call
+from lightgbmv1_amd.parallel.inproc import ThreadRanks
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "helpers"))
+from dist_worker import make_data  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+N = 20000
+BASE = {"objective": "binary", "num_leaves": 31, "verbose": -1, "device_type": "gpu", "min_data_in_leaf": 20,
+        "seed": 3, "deterministic": True, "max_bin": 63, "learning_rate": 0.1}
+
+
+def _trees(m):
+    return m[m.index("Tree=0"):m.index("end of trees")]
+
+
+def _splits(model_str, tree=0):
+    """(split_feature, threshold) lines of one tree of a text model."""
+    block = model_str.split("Tree=%d\n" % tree)[1].split("\n\n")[0]
+    rows = dict(line.split("=", 1) for line in block.splitlines() if "=" in line)
+    return rows.get("split_feature"), rows.get("threshold")
+
+
+def _run(learner, world, rounds=8):
+    X, y = make_data(N, 10)
+    full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
+    serial = lgb.train(BASE, full.subset(np.arange(N)), rounds)
+
+    def rank_fn(r):
+        params = dict(BASE, tree_learner=learner, num_machines=world)
+        if learner == "data":
+            params["pre_partition"] = True
+            ds = full.subset(np.arange(r, N, world))  # this rank's rows, the shared bin mappers
+        else:
+            ds = full.subset(np.arange(N))
+        bst = lgb.train(params, ds, rounds)
+        return bst.model_to_string(), bst.predict(X)
+
+    with ThreadRanks(world, timeout_s=120, device_comm=True) as tr:
+        res = tr.run(rank_fn)
+    assert all(r.ok for r in res), [str(r.error) for r in res]
+    return X, y, serial, [r.value for r in res]
+
+
+def test_device_comm_self_test_threads(gpu_available):
+    """Every device collective of the in-process communicator (all-reduce sum / max,
+    int64 reduce-scatter, allgather) on 3 thread ranks."""
+    lib = _load_lib()
+
+    def rank_fn(r):
+        ok = ctypes.c_int(0)
+        _safe_call(lib.LGBM_AMD_RcclSelfTest(ctypes.byref(ok)))
+        return ok.value
+
+    with ThreadRanks(3, timeout_s=60, device_comm=True) as tr:
+        res = tr.run(rank_fn)
+    assert all(r.ok for r in res), [str(r.error) for r in res]
+    assert [r.value for r in res] == [1, 1, 1]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_device_data_parallel_reduce_scatter(world, gpu_available):
+    X, y, serial, out = _run("data", world)
+    for m, _ in out[1:]:
+        assert _trees(m) == _trees(out[0][0])
+    # histograms are exact integer sums at the same fixed-point scale on every rank, so the
+    # global histograms equal the serial learner's: the first tree splits identically
+    assert _splits(out[0][0], 0) == _splits(serial.model_to_string(), 0)
+    from sklearn.metrics import roc_auc_score
+    assert abs(roc_auc_score(y, out[0][1]) - roc_auc_score(y, serial.predict(X))) < 0.005
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_device_feature_parallel(world, gpu_available):
+    X, y, serial, out = _run("feature", world)
+    for m, _ in out[1:]:
+        assert _trees(m) == _trees(out[0][0])
+    # every rank has every row: the same trees as the serial device learner
+    for t in range(3):
+        assert _splits(out[0][0], t) == _splits(serial.model_to_string(), t)
+    np.testing.assert_allclose(out[0][1], serial.predict(X), rtol=1e-9, atol=1e-12)
