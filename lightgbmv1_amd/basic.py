@@ -1,669 +1,184 @@
-"""Core Python wrapper: Dataset, Booster and the ctypes bridge to the native library.
+"""Dataset, Booster and the prediction front end (the LightGBM v3 Python API; reference
+python-package/lightgbm/basic.py defines the public contract -- lazy Dataset construction,
+reference datasets for validation binning, pandas categorical handling, Booster training /
+evaluation / prediction / model IO -- implemented here over the C API of
+``lib_lightgbmv1_amd.so``).  With ``device_type='gpu'`` training runs on the MI355X learner.
 
-Public behaviour mirrors reference python-package/lightgbm/basic.py (lazy Dataset
-construction, reference datasets for validation, pandas categorical handling, Booster
-training / evaluation / prediction / model IO).  The native side is
-``lib_lightgbmv1_amd.so`` (C API in include/lgbm_amd/c_api.h); with
-``device_type='gpu'`` training runs on the MI355X learner.
+Layout: `_native` (ctypes calls, enum codes, buffers), `_inputs` (torch / pandas / vector
+normalisation), and here the three objects built on them:
+  * `Dataset`: a recipe (raw data + fields + params) that `construct()` turns into a native
+    handle through one of the builders in `_BUILDERS` (file, dense, list of dense, CSR,
+    CSC) or as a row subset of a constructed reference;
+  * `_InnerPredictor`: prediction over a native booster handle, dispatched on the input
+    kind (`_PREDICT_KINDS`), with the SHAP sparse output re-assembled per class;
+  * `Booster`: a native booster plus the Python-side caches of evaluation metadata and of
+    per-dataset scores used by custom objectives / metrics.
 """
 import copy
 import ctypes
 import json
 import os
+import tempfile
 import warnings
 from collections import OrderedDict
-from tempfile import NamedTemporaryFile
 
 import numpy as np
 import scipy.sparse
 
-from .compat import (PANDAS_INSTALLED, dt_DataTable, integer_types, numeric_types, pd_DataFrame, pd_Series,
-                     string_type)
-from .libpath import find_lib_path
+from . import _inputs as inp
+from . import _native as nat
+from ._native import LightGBMError
+from .compat import PANDAS_INSTALLED, dt_DataTable, integer_types, string_type
 from .utils.param_table import PARAMETERS as _PARAMETERS
 
-
-def _log_callback(msg):
-    """Redirect native logs to Python's stdout."""
-    print("{0:s}".format(msg.decode("utf-8")), end="")
-
-
-_LIB = None
-_LOG_CALLBACK = None
+__all__ = ["Dataset", "Booster", "LightGBMError", "get_timers", "device_count", "device_synchronize"]
 
 
 def _load_lib():
-    global _LIB, _LOG_CALLBACK
-    if _LIB is not None:
-        return _LIB
-    lib_path = find_lib_path()
-    lib = ctypes.cdll.LoadLibrary(lib_path[0])
-    lib.LGBM_GetLastError.restype = ctypes.c_char_p
-    _LOG_CALLBACK = ctypes.CFUNCTYPE(None, ctypes.c_char_p)(_log_callback)
-    lib.callback = _LOG_CALLBACK
-    if lib.LGBM_RegisterLogCallback(_LOG_CALLBACK) != 0:
-        raise LightGBMError(lib.LGBM_GetLastError().decode("utf-8"))
-    _LIB = lib
-    return lib
-
-
-class _LazyLib(object):
-    def __getattr__(self, name):
-        return getattr(_load_lib(), name)
-
-
-_LIB_PROXY = _LazyLib()
-
-
-class LightGBMError(Exception):
-    """Error thrown by the native library."""
+    """The native library (kept for callers that use the C API directly)."""
+    return nat.lib()
 
 
 def _safe_call(ret):
-    if ret != 0:
-        raise LightGBMError(_load_lib().LGBM_GetLastError().decode("utf-8"))
+    nat.check(ret)
 
 
-def _from_tensor(data):
-    """torch.Tensor (CPU or a HIP device) -> numpy; anything else unchanged.
-
-    Device tensors are copied to the host once here; the library bins them and keeps its
-    own device copy of the binned matrix (PyTorch-ROCm interop)."""
-    mod = type(data).__module__
-    if mod.startswith("torch") and hasattr(data, "detach"):
-        return data.detach().cpu().numpy()
-    return data
-
-
-def is_numeric(obj):
-    try:
-        float(obj)
-        return True
-    except (TypeError, ValueError):
-        return False
-
-
-def is_numpy_1d_array(data):
-    return isinstance(data, np.ndarray) and len(data.shape) == 1
-
-
-def is_1d_list(data):
-    return isinstance(data, list) and (not data or is_numeric(data[0]))
-
-
-def list_to_1d_numpy(data, dtype=np.float32, name="list"):
-    if is_numpy_1d_array(data):
-        if data.dtype == dtype:
-            return data
-        return data.astype(dtype=dtype, copy=False)
-    if is_1d_list(data):
-        return np.asarray(data, dtype=dtype)
-    if isinstance(data, pd_Series):
-        if _get_bad_pandas_dtypes([data.dtypes]):
-            raise ValueError("Series.dtypes must be int, float or bool")
-        return np.asarray(data, dtype=dtype)
-    raise TypeError("Wrong type({0}) for {1}.\nIt should be list, numpy 1-D array or pandas Series".format(
-        type(data).__name__, name))
-
-
-def cfloat32_array_to_numpy(cptr, length):
-    if isinstance(cptr, ctypes.POINTER(ctypes.c_float)):
-        return np.ctypeslib.as_array(cptr, shape=(length,)).copy()
-    raise RuntimeError("Expected float pointer")
-
-
-def cfloat64_array_to_numpy(cptr, length):
-    if isinstance(cptr, ctypes.POINTER(ctypes.c_double)):
-        return np.ctypeslib.as_array(cptr, shape=(length,)).copy()
-    raise RuntimeError("Expected double pointer")
-
-
-def cint32_array_to_numpy(cptr, length):
-    if isinstance(cptr, ctypes.POINTER(ctypes.c_int32)):
-        return np.ctypeslib.as_array(cptr, shape=(length,)).copy()
-    raise RuntimeError("Expected int32 pointer")
-
-
-def cint64_array_to_numpy(cptr, length):
-    if isinstance(cptr, ctypes.POINTER(ctypes.c_int64)):
-        return np.ctypeslib.as_array(cptr, shape=(length,)).copy()
-    raise RuntimeError("Expected int64 pointer")
-
-
-def c_str(string):
-    return ctypes.c_char_p(string.encode("utf-8"))
-
-
-def c_array(ctype, values):
-    return (ctype * len(values))(*values)
-
-
-def param_dict_to_str(data):
-    """Convert a parameter dict to the native ``key=value`` string."""
-    if data is None or not data:
-        return ""
-    pairs = []
-    for key, val in data.items():
-        if isinstance(val, (list, tuple, set)) or is_numpy_1d_array(val):
-            def to_string(x):
-                if isinstance(x, list):
-                    return "[{}]".format(",".join(map(str, x)))
-                return str(x)
-            pairs.append(str(key) + "=" + ",".join(map(to_string, val)))
-        elif isinstance(val, string_type) or isinstance(val, numeric_types) or is_numeric(val):
-            pairs.append(str(key) + "=" + str(val))
-        elif val is not None:
-            raise TypeError("Unknown type of parameter:%s, got:%s" % (key, type(val).__name__))
-    return " ".join(pairs)
-
-
-class _TempFile(object):
-    def __enter__(self):
-        with NamedTemporaryFile(prefix="lightgbm_tmp_", delete=True) as f:
-            self.name = f.name
-        return self
-
-    def __exit__(self, exc_type, exc_val, exc_tb):
-        if os.path.isfile(self.name):
-            os.remove(self.name)
-
-    def readlines(self):
-        with open(self.name, "r+") as f:
-            ret = f.readlines()
-        return ret
-
-    def writelines(self, lines):
-        with open(self.name, "w+") as f:
-            f.writelines(lines)
-
-
-class _ConfigAliases(object):
-    """Alias table generated from the single parameter specification (tools/param_spec.py)."""
+class _ConfigAliases:
+    """Parameter alias table, generated from the single parameter spec (tools/param_spec.py)."""
 
     aliases = {name: {name} | set(spec["aliases"]) for name, spec in _PARAMETERS.items()}
-    # keys handled specially by the Python layer
     aliases.setdefault("group_column", {"group_column", "group", "group_id", "query_column", "query", "query_id"})
 
     @classmethod
-    def get(cls, *args):
-        ret = set()
-        for i in args:
-            ret |= cls.aliases.get(i, {i})
-        return ret
+    def get(cls, *names):
+        out = set()
+        for n in names:
+            out |= cls.aliases.get(n, {n})
+        return out
 
 
-MAX_INT32 = (1 << 31) - 1
-
-C_API_DTYPE_FLOAT32 = 0
-C_API_DTYPE_FLOAT64 = 1
-C_API_DTYPE_INT32 = 2
-C_API_DTYPE_INT64 = 3
-
-C_API_PREDICT_NORMAL = 0
-C_API_PREDICT_RAW_SCORE = 1
-C_API_PREDICT_LEAF_INDEX = 2
-C_API_PREDICT_CONTRIB = 3
-
-C_API_MATRIX_TYPE_CSR = 0
-C_API_MATRIX_TYPE_CSC = 1
-
-C_API_FEATURE_IMPORTANCE_SPLIT = 0
-C_API_FEATURE_IMPORTANCE_GAIN = 1
-
-FIELD_TYPE_MAPPER = {"label": C_API_DTYPE_FLOAT32,
-                     "weight": C_API_DTYPE_FLOAT32,
-                     "init_score": C_API_DTYPE_FLOAT64,
-                     "group": C_API_DTYPE_INT32}
-
-FEATURE_IMPORTANCE_TYPE_MAPPER = {"split": C_API_FEATURE_IMPORTANCE_SPLIT,
-                                  "gain": C_API_FEATURE_IMPORTANCE_GAIN}
+def _any_alias(params, name):
+    return any(params.get(a) for a in _ConfigAliases.get(name))
 
 
-def convert_from_sliced_object(data):
-    """Fix the memory of multi-dimensional sliced object."""
-    if isinstance(data, np.ndarray) and isinstance(data.base, np.ndarray):
-        if not data.flags.c_contiguous:
-            warnings.warn("Usage of np.ndarray subset (sliced data) is not recommended "
-                          "due to it will double the peak memory cost in LightGBM.")
-            return np.copy(data)
-    return data
+def _quiet(params, silent):
+    """`silent` means verbose=-1 unless the params set a verbosity themselves."""
+    if silent and not any(a in params for a in _ConfigAliases.get("verbosity")):
+        params["verbose"] = -1
+    return params
 
 
-def c_float_array(data):
-    if is_1d_list(data):
-        data = np.asarray(data)
-    if is_numpy_1d_array(data):
-        data = convert_from_sliced_object(data)
-        assert data.flags.c_contiguous
-        if data.dtype == np.float32:
-            ptr_data = data.ctypes.data_as(ctypes.POINTER(ctypes.c_float))
-            type_data = C_API_DTYPE_FLOAT32
-        elif data.dtype == np.float64:
-            ptr_data = data.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
-            type_data = C_API_DTYPE_FLOAT64
-        else:
-            raise TypeError("Expected np.float32 or np.float64, met type({})".format(data.dtype))
-    else:
-        raise TypeError("Unknown type({})".format(type(data).__name__))
-    return (ptr_data, type_data, data)
+# ---------------------------------------------------------------------------------- data
+_DATASET_PARAMS = ("bin_construct_sample_cnt", "categorical_feature", "data_random_seed", "enable_bundle",
+                   "feature_pre_filter", "forcedbins_filename", "group_column", "header", "ignore_column",
+                   "is_enable_sparse", "label_column", "max_bin", "max_bin_by_feature", "min_data_in_bin",
+                   "pre_partition", "two_round", "use_missing", "weight_column", "zero_as_missing")
+
+# field name -> numpy dtype on the Python side and the C API dtype code the library stores
+_FIELDS = {"label": (np.float32, nat.DTYPE_FLOAT32), "weight": (np.float32, nat.DTYPE_FLOAT32),
+           "init_score": (np.float64, nat.DTYPE_FLOAT64), "group": (np.int32, nat.DTYPE_INT32)}
 
 
-def c_int_array(data):
-    if is_1d_list(data):
-        data = np.asarray(data)
-    if is_numpy_1d_array(data):
-        data = convert_from_sliced_object(data)
-        assert data.flags.c_contiguous
-        if data.dtype == np.int32:
-            ptr_data = data.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
-            type_data = C_API_DTYPE_INT32
-        elif data.dtype == np.int64:
-            ptr_data = data.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
-            type_data = C_API_DTYPE_INT64
-        else:
-            raise TypeError("Expected np.int32 or np.int64, met type({})".format(data.dtype))
-    else:
-        raise TypeError("Unknown type({})".format(type(data).__name__))
-    return (ptr_data, type_data, data)
+def _dense_block(mat):
+    """2-D array -> (contiguous row-major float32/64 buffer, rows, cols)."""
+    mat = np.asarray(mat)
+    if mat.ndim != 2:
+        raise ValueError("Input numpy.ndarray must be 2 dimensional")
+    if mat.dtype not in (np.float32, np.float64):
+        mat = mat.astype(np.float32)
+    if isinstance(mat.base, np.ndarray) and not mat.flags.c_contiguous:
+        warnings.warn("Usage of np.ndarray subset (sliced data) is not recommended "
+                      "due to it will double the peak memory cost in LightGBM.")
+    return np.ascontiguousarray(mat).reshape(-1), mat.shape[0], mat.shape[1]
 
 
-def _get_bad_pandas_dtypes(dtypes):
-    pandas_dtype_mapper = {"int8", "int16", "int32", "int64", "uint8", "uint16", "uint32", "uint64",
-                           "float16", "float32", "float64", "bool"}
-    return [i for i, dtype in enumerate(dtypes) if str(getattr(dtype, "name", dtype)) not in pandas_dtype_mapper
-            and not str(dtype).startswith("Sparse")]
+def _sparse_parts(m):
+    """(indptr, int32 indices, data) buffers of a CSR / CSC matrix, kept alive by the caller."""
+    if len(m.indices) != len(m.data):
+        raise ValueError("Length mismatch: {} vs {}".format(len(m.indices), len(m.data)))
+    return (nat.as_index_vector(m.indptr), np.ascontiguousarray(m.indices, dtype=np.int32),
+            nat.as_float_vector(m.data))
 
 
-def _data_from_pandas(data, feature_name, categorical_feature, pandas_categorical):
-    if isinstance(data, pd_DataFrame):
-        if len(data.shape) != 2 or data.shape[0] < 1:
-            raise ValueError("Input data must be 2 dimensional and non empty.")
-        if feature_name == "auto" or feature_name is None:
-            data = data.rename(columns=str)
-        cat_cols = [col for col, dtype in zip(data.columns, data.dtypes) if str(dtype) == "category"]
-        cat_cols_not_ordered = [col for col in cat_cols if not data[col].cat.ordered]
-        if pandas_categorical is None:  # train dataset
-            pandas_categorical = [list(data[col].cat.categories) for col in cat_cols]
-        else:
-            if len(cat_cols) != len(pandas_categorical):
-                raise ValueError("train and valid dataset categorical_feature do not match.")
-            for col, category in zip(cat_cols, pandas_categorical):
-                if list(data[col].cat.categories) != list(category):
-                    data[col] = data[col].cat.set_categories(category)
-        if len(cat_cols):  # cat_cols is list
-            data = data.copy()  # not alter origin DataFrame
-            data[cat_cols] = data[cat_cols].apply(lambda x: x.cat.codes).replace({-1: np.nan})
-        if categorical_feature is not None:
-            if feature_name is None:
-                feature_name = list(data.columns)
-            if categorical_feature == "auto":  # use cat cols from DataFrame
-                categorical_feature = cat_cols_not_ordered
-            else:  # use cat cols specified by user
-                categorical_feature = list(categorical_feature)
-        if feature_name == "auto":
-            feature_name = list(data.columns)
-        bad_indices = _get_bad_pandas_dtypes(data.dtypes)
-        if bad_indices:
-            raise ValueError("DataFrame.dtypes for data must be int, float or bool.\n"
-                             "Did not expect the data types in the following fields: "
-                             + ", ".join(data.columns[bad_indices]))
-        data = data.values
-        if data.dtype != np.float32 and data.dtype != np.float64:
-            data = data.astype(np.float32)
-    else:
-        if feature_name == "auto":
-            feature_name = None
-        if categorical_feature == "auto":
-            categorical_feature = None
-    return data, feature_name, categorical_feature, pandas_categorical
+def _build_from_file(data, params_str, ref):
+    out = ctypes.c_void_p()
+    nat.call("LGBM_DatasetCreateFromFile", nat.cstr(data), nat.cstr(params_str), ref, ctypes.byref(out))
+    return out
 
 
-def _label_from_pandas(label):
-    if isinstance(label, pd_DataFrame):
-        if len(label.columns) > 1:
-            raise ValueError("DataFrame for label cannot have multiple columns")
-        if _get_bad_pandas_dtypes(label.dtypes):
-            raise ValueError("DataFrame.dtypes for label must be int, float or bool")
-        label = np.ravel(label.values.astype(np.float32, copy=False))
-    return label
+def _build_from_dense(data, params_str, ref):
+    buf, nrow, ncol = _dense_block(data)
+    ptr, code = nat.pointer(buf)
+    out = ctypes.c_void_p()
+    nat.call("LGBM_DatasetCreateFromMat", ptr, nat.c_int(code), ctypes.c_int32(nrow), ctypes.c_int32(ncol),
+             nat.c_int(1), nat.cstr(params_str), ref, ctypes.byref(out))
+    return out
 
 
-def _dump_pandas_categorical(pandas_categorical, file_name=None):
-    pandas_str = ("\npandas_categorical:" + json.dumps(pandas_categorical, default=_json_default_with_numpy) + "\n")
-    if file_name is not None:
-        with open(file_name, "a") as f:
-            f.write(pandas_str)
-    return pandas_str
+def _build_from_blocks(blocks, params_str, ref):
+    flat = [_dense_block(b) for b in blocks]
+    ncol = flat[0][2]
+    if any(f[2] != ncol for f in flat):
+        raise ValueError("Input arrays must have same number of columns")
+    dtype = flat[0][0].dtype
+    if any(f[0].dtype != dtype for f in flat):
+        raise ValueError("Input chunks must have same type")
+    code = nat.pointer(flat[0][0])[1]
+    elem = ctypes.c_double if dtype == np.float64 else ctypes.c_float
+    ptrs = (ctypes.POINTER(elem) * len(flat))(*[f[0].ctypes.data_as(ctypes.POINTER(elem)) for f in flat])
+    rows = np.array([f[1] for f in flat], dtype=np.int32)
+    out = ctypes.c_void_p()
+    nat.call("LGBM_DatasetCreateFromMats", ctypes.c_int32(len(flat)),
+             ctypes.cast(ptrs, ctypes.POINTER(ctypes.POINTER(ctypes.c_double))), nat.c_int(code),
+             rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.c_int32(ncol), nat.c_int(1),
+             nat.cstr(params_str), ref, ctypes.byref(out))
+    return out
 
 
-def _load_pandas_categorical(file_name=None, model_str=None):
-    pandas_key = "pandas_categorical:"
-    offset = -len(pandas_key)
-    if file_name is not None:
-        max_offset = -os.path.getsize(file_name)
-        with open(file_name, "rb") as f:
-            while True:
-                if offset < max_offset:
-                    offset = max_offset
-                f.seek(offset, os.SEEK_END)
-                lines = f.readlines()
-                if len(lines) >= 2:
-                    break
-                offset *= 2
-        last_line = lines[-1].decode("utf-8").strip()
-        if not last_line.startswith(pandas_key):
-            last_line = lines[-2].decode("utf-8").strip()
-    elif model_str is not None:
-        idx = model_str.rfind("\n", 0, offset)
-        last_line = model_str[idx:].strip()
-    if last_line.startswith(pandas_key):
-        return json.loads(last_line[len(pandas_key):])
+def _build_from_sparse(m, params_str, ref):
+    indptr, indices, values = _sparse_parts(m)
+    p_ptr, p_code = nat.pointer(indptr)
+    v_ptr, v_code = nat.pointer(values)
+    csr = scipy.sparse.isspmatrix_csr(m)
+    out = ctypes.c_void_p()
+    nat.call("LGBM_DatasetCreateFromCSR" if csr else "LGBM_DatasetCreateFromCSC", p_ptr, nat.c_int(p_code),
+             indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), v_ptr, nat.c_int(v_code),
+             ctypes.c_int64(len(indptr)), ctypes.c_int64(len(values)), ctypes.c_int64(m.shape[1] if csr else m.shape[0]),
+             nat.cstr(params_str), ref, ctypes.byref(out))
+    return out
+
+
+def _input_kind(data):
+    """Which builder / predictor handles `data` (None: try converting to CSR)."""
+    if isinstance(data, string_type):
+        return "file"
+    if scipy.sparse.isspmatrix_csr(data):
+        return "csr"
+    if scipy.sparse.isspmatrix_csc(data):
+        return "csc"
+    if isinstance(data, np.ndarray):
+        return "dense"
+    if dt_DataTable is not None and isinstance(data, dt_DataTable):
+        return "datatable"
+    if isinstance(data, list):
+        if data and all(isinstance(x, np.ndarray) for x in data):
+            return "blocks"
+        return "list"
     return None
 
 
-def _json_default_with_numpy(obj):
-    if isinstance(obj, (np.integer, np.floating, np.bool_)):
-        return obj.item()
-    if isinstance(obj, np.ndarray):
-        return obj.tolist()
-    return obj
+_BUILDERS = {
+    "file": _build_from_file,
+    "dense": _build_from_dense,
+    "blocks": _build_from_blocks,
+    "csr": _build_from_sparse,
+    "csc": _build_from_sparse,
+    "datatable": lambda d, p, r: _build_from_dense(d.to_numpy(), p, r),
+}
 
 
-class _InnerPredictor(object):
-    """Prediction-only handle (reference basic.py:455-905)."""
-
-    def __init__(self, model_file=None, booster_handle=None, pred_parameter=None):
-        self.handle = ctypes.c_void_p()
-        self.__is_manage_handle = True
-        if model_file is not None:
-            out_num_iterations = ctypes.c_int(0)
-            _safe_call(_load_lib().LGBM_BoosterCreateFromModelfile(c_str(model_file),
-                                                                   ctypes.byref(out_num_iterations),
-                                                                   ctypes.byref(self.handle)))
-            out_num_class = ctypes.c_int(0)
-            _safe_call(_load_lib().LGBM_BoosterGetNumClasses(self.handle, ctypes.byref(out_num_class)))
-            self.num_class = out_num_class.value
-            self.num_total_iteration = out_num_iterations.value
-            self.pandas_categorical = _load_pandas_categorical(file_name=model_file)
-        elif booster_handle is not None:
-            self.__is_manage_handle = False
-            self.handle = booster_handle
-            out_num_class = ctypes.c_int(0)
-            _safe_call(_load_lib().LGBM_BoosterGetNumClasses(self.handle, ctypes.byref(out_num_class)))
-            self.num_class = out_num_class.value
-            self.num_total_iteration = self.current_iteration()
-            self.pandas_categorical = None
-        else:
-            raise TypeError("Need model_file or booster_handle to create a predictor")
-        pred_parameter = {} if pred_parameter is None else pred_parameter
-        self.pred_parameter = param_dict_to_str(pred_parameter)
-
-    def __del__(self):
-        try:
-            if self.__is_manage_handle:
-                _safe_call(_load_lib().LGBM_BoosterFree(self.handle))
-        except AttributeError:
-            pass
-
-    def __getstate__(self):
-        this = self.__dict__.copy()
-        this.pop("handle", None)
-        return this
-
-    def predict(self, data, start_iteration=0, num_iteration=-1, raw_score=False, pred_leaf=False,
-                pred_contrib=False, data_has_header=False, is_reshape=True):
-        if isinstance(data, Dataset):
-            raise TypeError("Cannot use Dataset instance for prediction, please use raw data instead")
-        data = _data_from_pandas(data, None, None, self.pandas_categorical)[0]
-        predict_type = C_API_PREDICT_NORMAL
-        if raw_score:
-            predict_type = C_API_PREDICT_RAW_SCORE
-        if pred_leaf:
-            predict_type = C_API_PREDICT_LEAF_INDEX
-        if pred_contrib:
-            predict_type = C_API_PREDICT_CONTRIB
-        int_data_has_header = 1 if data_has_header else 0
-        data = _from_tensor(data)
-        if isinstance(data, string_type):
-            with _TempFile() as f:
-                _safe_call(_load_lib().LGBM_BoosterPredictForFile(
-                    self.handle, c_str(data), ctypes.c_int(int_data_has_header), ctypes.c_int(predict_type),
-                    ctypes.c_int(start_iteration), ctypes.c_int(num_iteration), c_str(self.pred_parameter),
-                    c_str(f.name)))
-                lines = f.readlines()
-                nrow = len(lines)
-                preds = [float(token) for line in lines for token in line.split("\t")]
-                preds = np.asarray(preds, dtype=np.float64)
-        elif isinstance(data, scipy.sparse.csr_matrix):
-            preds, nrow = self.__pred_for_csr(data, start_iteration, num_iteration, predict_type)
-        elif isinstance(data, scipy.sparse.csc_matrix):
-            preds, nrow = self.__pred_for_csc(data, start_iteration, num_iteration, predict_type)
-        elif isinstance(data, np.ndarray):
-            preds, nrow = self.__pred_for_np2d(data, start_iteration, num_iteration, predict_type)
-        elif isinstance(data, list):
-            try:
-                data = np.array(data)
-            except BaseException:
-                raise ValueError("Cannot convert data list to numpy array.")
-            preds, nrow = self.__pred_for_np2d(data, start_iteration, num_iteration, predict_type)
-        elif isinstance(data, dt_DataTable):
-            preds, nrow = self.__pred_for_np2d(data.to_numpy(), start_iteration, num_iteration, predict_type)
-        else:
-            try:
-                warnings.warn("Converting data to scipy sparse matrix.")
-                csr = scipy.sparse.csr_matrix(data)
-            except BaseException:
-                raise TypeError("Cannot predict data for type {}".format(type(data).__name__))
-            preds, nrow = self.__pred_for_csr(csr, start_iteration, num_iteration, predict_type)
-        if pred_leaf:
-            preds = preds.astype(np.int32)
-        is_sparse = scipy.sparse.issparse(preds) or isinstance(preds, list)
-        if is_reshape and not is_sparse and preds.size != nrow:
-            if preds.size % nrow == 0:
-                preds = preds.reshape(nrow, -1)
-            else:
-                raise ValueError("Length of predict result (%d) cannot be divide nrow (%d)" % (preds.size, nrow))
-        return preds
-
-    def __get_num_preds(self, start_iteration, num_iteration, nrow, predict_type):
-        if nrow > MAX_INT32:
-            raise LightGBMError("LightGBM cannot perform prediction for data with number of rows greater than "
-                                "MAX_INT32 (%d).\nYou can split your data into chunks and then concatenate "
-                                "predictions for them" % MAX_INT32)
-        n_preds = ctypes.c_int64(0)
-        _safe_call(_load_lib().LGBM_BoosterCalcNumPredict(self.handle, ctypes.c_int(nrow), ctypes.c_int(predict_type),
-                                                          ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
-                                                          ctypes.byref(n_preds)))
-        return n_preds.value
-
-    def __pred_for_np2d(self, mat, start_iteration, num_iteration, predict_type):
-        if len(mat.shape) != 2:
-            raise ValueError("Input numpy.ndarray or list must be 2 dimensional")
-
-        def inner_predict(mat, start_iteration, num_iteration, predict_type, preds=None):
-            if mat.dtype == np.float32 or mat.dtype == np.float64:
-                data = np.asarray(mat.reshape(mat.size), dtype=mat.dtype)
-            else:
-                data = np.array(mat.reshape(mat.size), dtype=np.float32)
-            ptr_data, type_ptr_data, _ = c_float_array(data)
-            n_preds = self.__get_num_preds(start_iteration, num_iteration, mat.shape[0], predict_type)
-            if preds is None:
-                preds = np.zeros(n_preds, dtype=np.float64)
-            elif len(preds.shape) != 1 or len(preds) != n_preds:
-                raise ValueError("Wrong length of pre-allocated predict array")
-            out_num_preds = ctypes.c_int64(0)
-            _safe_call(_load_lib().LGBM_BoosterPredictForMat(
-                self.handle, ptr_data, ctypes.c_int(type_ptr_data), ctypes.c_int32(mat.shape[0]),
-                ctypes.c_int32(mat.shape[1]), ctypes.c_int(1), ctypes.c_int(predict_type),
-                ctypes.c_int(start_iteration), ctypes.c_int(num_iteration), c_str(self.pred_parameter),
-                ctypes.byref(out_num_preds), preds.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
-            if n_preds != out_num_preds.value:
-                raise ValueError("Wrong length for predict results")
-            return preds, mat.shape[0]
-
-        nrow = mat.shape[0]
-        if nrow > MAX_INT32:
-            sections = np.arange(start=MAX_INT32, stop=nrow, step=MAX_INT32)
-            n_preds = [self.__get_num_preds(start_iteration, num_iteration, i, predict_type)
-                       for i in np.diff([0] + list(sections) + [nrow])]
-            n_preds_sections = np.array([0] + n_preds, dtype=np.intp).cumsum()
-            preds = np.zeros(sum(n_preds), dtype=np.float64)
-            for chunk, (start_idx_pred, end_idx_pred) in zip(np.array_split(mat, sections),
-                                                             zip(n_preds_sections, n_preds_sections[1:])):
-                inner_predict(chunk, start_iteration, num_iteration, predict_type, preds[start_idx_pred:end_idx_pred])
-            return preds, nrow
-        return inner_predict(mat, start_iteration, num_iteration, predict_type)
-
-    def __create_sparse_native(self, cs, out_shape, out_ptr_indptr, out_ptr_indices, out_ptr_data, indptr_type,
-                               data_type, is_csr=True):
-        data_indices_len = out_shape[0]
-        indptr_len = out_shape[1]
-        if indptr_type == C_API_DTYPE_INT32:
-            out_indptr = cint32_array_to_numpy(out_ptr_indptr, indptr_len)
-        elif indptr_type == C_API_DTYPE_INT64:
-            out_indptr = cint64_array_to_numpy(out_ptr_indptr, indptr_len)
-        else:
-            raise TypeError("Expected int32 or int64 type for indptr")
-        if data_type == C_API_DTYPE_FLOAT32:
-            out_data = cfloat32_array_to_numpy(out_ptr_data, data_indices_len)
-        elif data_type == C_API_DTYPE_FLOAT64:
-            out_data = cfloat64_array_to_numpy(out_ptr_data, data_indices_len)
-        else:
-            raise TypeError("Expected float32 or float64 type for data")
-        out_indices = cint32_array_to_numpy(out_ptr_indices, data_indices_len)
-        per_class_shape = [cs.shape[0], cs.shape[1] + 1]
-        if self.num_class > 1:
-            offset = 0
-            cs_output_matrices = []
-            step = per_class_shape[0] + 1 if is_csr else per_class_shape[1] + 1
-            for _ in range(self.num_class):
-                part_ptr = out_indptr[offset:offset + step]
-                start, end = part_ptr[0], part_ptr[-1]
-                part_ptr = part_ptr - start
-                if is_csr:
-                    m = scipy.sparse.csr_matrix((out_data[start:end], out_indices[start:end], part_ptr),
-                                                per_class_shape)
-                else:
-                    m = scipy.sparse.csc_matrix((out_data[start:end], out_indices[start:end], part_ptr),
-                                                per_class_shape)
-                cs_output_matrices.append(m)
-                offset += step
-        else:
-            if is_csr:
-                cs_output_matrices = scipy.sparse.csr_matrix((out_data, out_indices, out_indptr), per_class_shape)
-            else:
-                cs_output_matrices = scipy.sparse.csc_matrix((out_data, out_indices, out_indptr), per_class_shape)
-        _safe_call(_load_lib().LGBM_BoosterFreePredictSparse(out_ptr_indptr, out_ptr_indices, out_ptr_data,
-                                                             ctypes.c_int(indptr_type), ctypes.c_int(data_type)))
-        return cs_output_matrices
-
-    def __pred_for_csr(self, csr, start_iteration, num_iteration, predict_type):
-        nrow = len(csr.indptr) - 1
-
-        def inner_predict(csr, start_iteration, num_iteration, predict_type, preds=None):
-            ptr_indptr, type_ptr_indptr, __ = c_int_array(csr.indptr)
-            ptr_data, type_ptr_data, _ = c_float_array(csr.data)
-            csr_indices = csr.indices.astype(np.int32, copy=False)
-            n_preds = self.__get_num_preds(start_iteration, num_iteration, nrow, predict_type)
-            if preds is None:
-                preds = np.zeros(n_preds, dtype=np.float64)
-            out_num_preds = ctypes.c_int64(0)
-            _safe_call(_load_lib().LGBM_BoosterPredictForCSR(
-                self.handle, ptr_indptr, ctypes.c_int32(type_ptr_indptr),
-                csr_indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ptr_data, ctypes.c_int(type_ptr_data),
-                ctypes.c_int64(len(csr.indptr)), ctypes.c_int64(len(csr.data)), ctypes.c_int64(csr.shape[1]),
-                ctypes.c_int(predict_type), ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
-                c_str(self.pred_parameter), ctypes.byref(out_num_preds),
-                preds.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
-            if n_preds != out_num_preds.value:
-                raise ValueError("Wrong length for predict results")
-            return preds, nrow
-
-        def inner_predict_sparse(csr, start_iteration, num_iteration, predict_type):
-            ptr_indptr, type_ptr_indptr, __ = c_int_array(csr.indptr)
-            ptr_data, type_ptr_data, _ = c_float_array(csr.data)
-            csr_indices = csr.indices.astype(np.int32, copy=False)
-            matrix_type = C_API_MATRIX_TYPE_CSR
-            if type_ptr_indptr == C_API_DTYPE_INT32:
-                out_ptr_indptr = ctypes.POINTER(ctypes.c_int32)()
-            else:
-                out_ptr_indptr = ctypes.POINTER(ctypes.c_int64)()
-            out_ptr_indices = ctypes.POINTER(ctypes.c_int32)()
-            if type_ptr_data == C_API_DTYPE_FLOAT32:
-                out_ptr_data = ctypes.POINTER(ctypes.c_float)()
-            else:
-                out_ptr_data = ctypes.POINTER(ctypes.c_double)()
-            out_shape = np.zeros(2, dtype=np.int64)
-            _safe_call(_load_lib().LGBM_BoosterPredictSparseOutput(
-                self.handle, ptr_indptr, ctypes.c_int32(type_ptr_indptr),
-                csr_indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ptr_data, ctypes.c_int(type_ptr_data),
-                ctypes.c_int64(len(csr.indptr)), ctypes.c_int64(len(csr.data)), ctypes.c_int64(csr.shape[1]),
-                ctypes.c_int(predict_type), ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
-                c_str(self.pred_parameter), ctypes.c_int(matrix_type),
-                out_shape.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(out_ptr_indptr),
-                ctypes.byref(out_ptr_indices), ctypes.byref(out_ptr_data)))
-            matrices = self.__create_sparse_native(csr, out_shape, out_ptr_indptr, out_ptr_indices, out_ptr_data,
-                                                   type_ptr_indptr, type_ptr_data, is_csr=True)
-            return matrices, nrow
-
-        if predict_type == C_API_PREDICT_CONTRIB:
-            return inner_predict_sparse(csr, start_iteration, num_iteration, predict_type)
-        return inner_predict(csr, start_iteration, num_iteration, predict_type)
-
-    def __pred_for_csc(self, csc, start_iteration, num_iteration, predict_type):
-        nrow = csc.shape[0]
-        if nrow > MAX_INT32:
-            return self.__pred_for_csr(csc.tocsr(), start_iteration, num_iteration, predict_type)
-        if predict_type == C_API_PREDICT_CONTRIB:
-            ptr_indptr, type_ptr_indptr, __ = c_int_array(csc.indptr)
-            ptr_data, type_ptr_data, _ = c_float_array(csc.data)
-            csc_indices = csc.indices.astype(np.int32, copy=False)
-            if type_ptr_indptr == C_API_DTYPE_INT32:
-                out_ptr_indptr = ctypes.POINTER(ctypes.c_int32)()
-            else:
-                out_ptr_indptr = ctypes.POINTER(ctypes.c_int64)()
-            out_ptr_indices = ctypes.POINTER(ctypes.c_int32)()
-            if type_ptr_data == C_API_DTYPE_FLOAT32:
-                out_ptr_data = ctypes.POINTER(ctypes.c_float)()
-            else:
-                out_ptr_data = ctypes.POINTER(ctypes.c_double)()
-            out_shape = np.zeros(2, dtype=np.int64)
-            _safe_call(_load_lib().LGBM_BoosterPredictSparseOutput(
-                self.handle, ptr_indptr, ctypes.c_int32(type_ptr_indptr),
-                csc_indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ptr_data, ctypes.c_int(type_ptr_data),
-                ctypes.c_int64(len(csc.indptr)), ctypes.c_int64(len(csc.data)), ctypes.c_int64(csc.shape[0]),
-                ctypes.c_int(predict_type), ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
-                c_str(self.pred_parameter), ctypes.c_int(C_API_MATRIX_TYPE_CSC),
-                out_shape.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(out_ptr_indptr),
-                ctypes.byref(out_ptr_indices), ctypes.byref(out_ptr_data)))
-            matrices = self.__create_sparse_native(csc, out_shape, out_ptr_indptr, out_ptr_indices, out_ptr_data,
-                                                   type_ptr_indptr, type_ptr_data, is_csr=False)
-            return matrices, nrow
-        n_preds = self.__get_num_preds(start_iteration, num_iteration, nrow, predict_type)
-        preds = np.zeros(n_preds, dtype=np.float64)
-        out_num_preds = ctypes.c_int64(0)
-        ptr_indptr, type_ptr_indptr, __ = c_int_array(csc.indptr)
-        ptr_data, type_ptr_data, _ = c_float_array(csc.data)
-        csc_indices = csc.indices.astype(np.int32, copy=False)
-        _safe_call(_load_lib().LGBM_BoosterPredictForCSC(
-            self.handle, ptr_indptr, ctypes.c_int32(type_ptr_indptr),
-            csc_indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ptr_data, ctypes.c_int(type_ptr_data),
-            ctypes.c_int64(len(csc.indptr)), ctypes.c_int64(len(csc.data)), ctypes.c_int64(csc.shape[0]),
-            ctypes.c_int(predict_type), ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
-            c_str(self.pred_parameter), ctypes.byref(out_num_preds),
-            preds.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
-        if n_preds != out_num_preds.value:
-            raise ValueError("Wrong length for predict results")
-        return preds, nrow
-
-    def current_iteration(self):
-        out_cur_iter = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterGetCurrentIteration(self.handle, ctypes.byref(out_cur_iter)))
-        return out_cur_iter.value
-
-
-class Dataset(object):
-    """Dataset in LightGBM (lazily constructed on the native side)."""
+class Dataset:
+    """Training / validation data, constructed lazily on the native side."""
 
     def __init__(self, data, label=None, reference=None, weight=None, group=None, init_score=None, silent=False,
                  feature_name="auto", categorical_feature="auto", params=None, free_raw_data=True):
@@ -679,147 +194,98 @@ class Dataset(object):
         self.categorical_feature = categorical_feature
         self.params = copy.deepcopy(params)
         self.free_raw_data = free_raw_data
-        self.used_indices = None
-        self.need_slice = True
-        self._predictor = None
+        self.used_indices = None   # row subset of `reference` (Dataset.subset)
+        self.need_slice = True     # self.data not yet sliced from the reference's raw data
+        self._predictor = None     # init_model predictor: its raw scores become init_score
         self.pandas_categorical = None
         self.params_back_up = None
-        self.feature_penalty = None
-        self.monotone_constraints = None
-        self.version = 0
+        self.version = 0           # bumped by field updates (Booster.update re-syncs)
 
     def __del__(self):
         try:
             self._free_handle()
-        except AttributeError:
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
             pass
 
+    # ------------------------------------------------------------------ construction
     def get_params(self):
-        """Get the used parameters in the Dataset."""
-        if self.params is not None:
-            dataset_params = _ConfigAliases.get(
-                "bin_construct_sample_cnt", "categorical_feature", "data_random_seed", "enable_bundle",
-                "feature_pre_filter", "forcedbins_filename", "group_column", "header", "ignore_column",
-                "is_enable_sparse", "label_column", "max_bin", "max_bin_by_feature", "min_data_in_bin",
-                "pre_partition", "two_round", "use_missing", "weight_column", "zero_as_missing")
-            return {k: v for k, v in self.params.items() if k in dataset_params}
-        return {}
+        """The parameters that shape the binned data (those a validation set must share)."""
+        if not self.params:
+            return {}
+        keys = _ConfigAliases.get(*_DATASET_PARAMS)
+        return {k: v for k, v in self.params.items() if k in keys}
 
     def _free_handle(self):
         if self.handle is not None:
-            _safe_call(_load_lib().LGBM_DatasetFree(self.handle))
+            nat.call("LGBM_DatasetFree", self.handle)
             self.handle = None
         self.need_slice = True
         if self.used_indices is not None:
             self.data = None
         return self
 
-    def _set_init_score_by_predictor(self, predictor, data, used_indices=None):
-        data_has_header = False
-        if isinstance(data, string_type):
-            data_has_header = any(self.params.get(alias, False) for alias in _ConfigAliases.get("header"))
-        num_data = self.num_data()
-        if predictor is not None:
-            init_score = predictor.predict(data, raw_score=True, data_has_header=data_has_header, is_reshape=False)
-            if used_indices is not None:
-                assert not self.need_slice
-                if isinstance(data, string_type):
-                    sub_init_score = np.zeros(num_data * predictor.num_class, dtype=np.float32)
-                    assert num_data == len(used_indices)
-                    for i in range(len(used_indices)):
-                        for j in range(predictor.num_class):
-                            sub_init_score[i * predictor.num_class + j] = \
-                                init_score[used_indices[i] * predictor.num_class + j]
-                    init_score = sub_init_score
-            if predictor.num_class > 1:
-                # need to regroup init_score
-                new_init_score = np.zeros(init_score.size, dtype=np.float32)
-                for i in range(num_data):
-                    for j in range(predictor.num_class):
-                        new_init_score[j * num_data + i] = init_score[i * predictor.num_class + j]
-                init_score = new_init_score
-        elif self.init_score is not None:
-            init_score = np.zeros(self.init_score.shape, dtype=np.float32)
-        else:
+    def construct(self):
+        """Build the native dataset if not built yet; returns self."""
+        if self.handle is not None:
             return self
-        self.set_init_score(init_score)
+        if self.reference is None:
+            self._build(self.data, self.label, None, self.weight, self.group, self.init_score, self._predictor,
+                        self.feature_name, self.categorical_feature, self.params)
+        else:
+            ref_params = self.reference.get_params()
+            if self.get_params() != ref_params:
+                warnings.warn("Overriding the parameters from Reference Dataset.")
+                self._update_params(ref_params)
+            if self.used_indices is None:
+                self._build(self.data, self.label, self.reference, self.weight, self.group, self.init_score,
+                            self._predictor, self.feature_name, "auto", self.params)
+            else:
+                self._build_subset()
+        if self.free_raw_data:
+            self.data = None
+        return self
 
-    def _lazy_init(self, data, label=None, reference=None, weight=None, group=None, init_score=None,
-                   predictor=None, silent=False, feature_name="auto", categorical_feature="auto", params=None):
+    def _build(self, data, label, reference, weight, group, init_score, predictor, feature_name,
+               categorical_feature, params):
         if data is None:
             self.handle = None
             return self
-        data, label, weight, init_score = (_from_tensor(data), _from_tensor(label), _from_tensor(weight),
-                                           _from_tensor(init_score))
+        data, label, weight, init_score = (inp.to_host(x) for x in (data, label, weight, init_score))
         if reference is not None:
             self.pandas_categorical = reference.pandas_categorical
             categorical_feature = reference.categorical_feature
-        data, feature_name, categorical_feature, self.pandas_categorical = _data_from_pandas(
+        data, feature_name, categorical_feature, self.pandas_categorical = inp.frame_to_array(
             data, feature_name, categorical_feature, self.pandas_categorical)
-        label = _label_from_pandas(label)
-
-        # process for args
+        label = inp.label_vector(label)
         params = {} if params is None else params
-        args_names = (getattr(self.__class__, "_lazy_init").__code__.co_varnames[
-            :getattr(self.__class__, "_lazy_init").__code__.co_argcount])
-        for key, _ in params.items():
-            if key in args_names:
+        for key in params:
+            if key in ("data", "label", "reference", "weight", "group", "init_score", "predictor",
+                       "feature_name", "categorical_feature", "silent"):
                 warnings.warn("{0} keyword has been found in `params` and will be ignored.\n"
                               "Please use {0} argument of the Dataset constructor to pass this parameter."
                               .format(key))
-        # user can set verbose with params, it has higher priority
-        if not any(verbose_alias in params for verbose_alias in _ConfigAliases.get("verbosity")) and silent:
-            params["verbose"] = -1
-        # get categorical features
-        if categorical_feature is not None:
-            categorical_indices = set()
-            feature_dict = {}
-            if feature_name is not None:
-                feature_dict = {name: i for i, name in enumerate(feature_name)}
-            for name in categorical_feature:
-                if isinstance(name, string_type) and name in feature_dict:
-                    categorical_indices.add(feature_dict[name])
-                elif isinstance(name, integer_types):
-                    categorical_indices.add(name)
-                else:
-                    raise TypeError("Wrong type({}) or unknown name({}) in categorical_feature"
-                                    .format(type(name).__name__, name))
-            if categorical_indices:
-                for cat_alias in _ConfigAliases.get("categorical_feature"):
-                    if cat_alias in params:
-                        warnings.warn("{} in param dict is overridden.".format(cat_alias))
-                        params.pop(cat_alias, None)
-                params["categorical_column"] = sorted(categorical_indices)
-
-        params_str = param_dict_to_str(params)
+        _quiet(params, self.silent)
+        cat_idx = self._categorical_indices(categorical_feature, feature_name)
+        if cat_idx:
+            for alias in _ConfigAliases.get("categorical_feature"):
+                if alias in params:
+                    warnings.warn("{} in param dict is overridden.".format(alias))
+                    params.pop(alias)
+            params["categorical_column"] = sorted(cat_idx)
         self.params = params
-        # process for reference dataset
-        ref_dataset = None
-        if isinstance(reference, Dataset):
-            ref_dataset = reference.construct().handle
-        elif reference is not None:
+        if reference is not None and not isinstance(reference, Dataset):
             raise TypeError("Reference dataset should be None or dataset instance")
-        # start construct data
-        if isinstance(data, string_type):
-            self.handle = ctypes.c_void_p()
-            _safe_call(_load_lib().LGBM_DatasetCreateFromFile(c_str(data), c_str(params_str), ref_dataset,
-                                                              ctypes.byref(self.handle)))
-        elif isinstance(data, scipy.sparse.csr_matrix):
-            self.__init_from_csr(data, params_str, ref_dataset)
-        elif isinstance(data, scipy.sparse.csc_matrix):
-            self.__init_from_csc(data, params_str, ref_dataset)
-        elif isinstance(data, np.ndarray):
-            self.__init_from_np2d(data, params_str, ref_dataset)
-        elif isinstance(data, list) and len(data) > 0 and all(isinstance(x, np.ndarray) for x in data):
-            self.__init_from_list_np2d(data, params_str, ref_dataset)
-        elif isinstance(data, dt_DataTable):
-            self.__init_from_np2d(data.to_numpy(), params_str, ref_dataset)
-        else:
+        ref_handle = reference.construct().handle if reference is not None else None
+        kind = _input_kind(data)
+        if kind == "list":
+            kind = None
+        if kind is None:
             try:
-                csr = scipy.sparse.csr_matrix(data)
-                self.__init_from_csr(csr, params_str, ref_dataset)
-            except BaseException:
+                data = scipy.sparse.csr_matrix(data)
+            except Exception:  # noqa: BLE001
                 raise TypeError("Cannot initialize Dataset from {}".format(type(data).__name__))
+            kind = "csr"
+        self.handle = _BUILDERS[kind](data, nat.params_str(params), ref_handle)
         if label is not None:
             self.set_label(label)
         if self.get_label() is None:
@@ -831,136 +297,67 @@ class Dataset(object):
         if isinstance(predictor, _InnerPredictor):
             if self._predictor is None and init_score is not None:
                 warnings.warn("The init_score will be overridden by the prediction of init_model.")
-            self._set_init_score_by_predictor(predictor, data)
+            self._init_score_from(predictor, data)
         elif init_score is not None:
             self.set_init_score(init_score)
         elif predictor is not None:
             raise TypeError("Wrong predictor type {}".format(type(predictor).__name__))
-        # set feature names
         return self.set_feature_name(feature_name)
 
-    def __init_from_np2d(self, mat, params_str, ref_dataset):
-        if len(mat.shape) != 2:
-            raise ValueError("Input numpy.ndarray must be 2 dimensional")
-        self.handle = ctypes.c_void_p()
-        if mat.dtype == np.float32 or mat.dtype == np.float64:
-            data = np.asarray(mat.reshape(mat.size), dtype=mat.dtype)
-        else:
-            data = np.array(mat.reshape(mat.size), dtype=np.float32)
-        ptr_data, type_ptr_data, _ = c_float_array(data)
-        _safe_call(_load_lib().LGBM_DatasetCreateFromMat(
-            ptr_data, ctypes.c_int(type_ptr_data), ctypes.c_int32(mat.shape[0]), ctypes.c_int32(mat.shape[1]),
-            ctypes.c_int(1), c_str(params_str), ref_dataset, ctypes.byref(self.handle)))
-        return self
-
-    def __init_from_list_np2d(self, mats, params_str, ref_dataset):
-        ncol = mats[0].shape[1]
-        nrow = np.zeros((len(mats),), np.int32)
-        if mats[0].dtype == np.float64:
-            ptr_data = (ctypes.POINTER(ctypes.c_double) * len(mats))()
-        else:
-            ptr_data = (ctypes.POINTER(ctypes.c_float) * len(mats))()
-        holders = []
-        type_ptr_data = None
-        for i, mat in enumerate(mats):
-            if len(mat.shape) != 2:
-                raise ValueError("Input numpy.ndarray must be 2 dimensional")
-            if mat.shape[1] != ncol:
-                raise ValueError("Input arrays must have same number of columns")
-            nrow[i] = mat.shape[0]
-            if mat.dtype == np.float32 or mat.dtype == np.float64:
-                mats[i] = np.asarray(mat.reshape(mat.size), dtype=mat.dtype)
+    @staticmethod
+    def _categorical_indices(categorical_feature, feature_name):
+        if categorical_feature is None:
+            return set()
+        index_of = {name: i for i, name in enumerate(feature_name or [])}
+        out = set()
+        for c in categorical_feature:
+            if isinstance(c, string_type) and c in index_of:
+                out.add(index_of[c])
+            elif isinstance(c, integer_types):
+                out.add(int(c))
             else:
-                mats[i] = np.array(mat.reshape(mat.size), dtype=np.float32)
-            chunk_ptr_data, chunk_type_ptr_data, holder = c_float_array(mats[i])
-            if type_ptr_data is not None and chunk_type_ptr_data != type_ptr_data:
-                raise ValueError("Input chunks must have same type")
-            ptr_data[i] = chunk_ptr_data
-            type_ptr_data = chunk_type_ptr_data
-            holders.append(holder)
-        self.handle = ctypes.c_void_p()
-        _safe_call(_load_lib().LGBM_DatasetCreateFromMats(
-            ctypes.c_int32(len(mats)), ctypes.cast(ptr_data, ctypes.POINTER(ctypes.POINTER(ctypes.c_double))),
-            ctypes.c_int(type_ptr_data), nrow.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.c_int32(ncol),
-            ctypes.c_int(1), c_str(params_str), ref_dataset, ctypes.byref(self.handle)))
-        return self
+                raise TypeError("Wrong type({}) or unknown name({}) in categorical_feature".format(
+                    type(c).__name__, c))
+        return out
 
-    def __init_from_csr(self, csr, params_str, ref_dataset):
-        if len(csr.indices) != len(csr.data):
-            raise ValueError("Length mismatch: {} vs {}".format(len(csr.indices), len(csr.data)))
+    def _build_subset(self):
+        idx = np.ascontiguousarray(inp.vector(self.used_indices, np.int32, "used_indices"))
+        if self.reference.group is not None:
+            # group sizes of the subset: the reference's query of every kept row
+            query_of_row = np.repeat(np.arange(len(self.reference.group)), np.asarray(self.reference.group))
+            _, self.group = np.unique(query_of_row[idx], return_counts=True)
         self.handle = ctypes.c_void_p()
-        ptr_indptr, type_ptr_indptr, __ = c_int_array(csr.indptr)
-        ptr_data, type_ptr_data, _ = c_float_array(csr.data)
-        assert csr.shape[1] <= MAX_INT32
-        csr_indices = csr.indices.astype(np.int32, copy=False)
-        _safe_call(_load_lib().LGBM_DatasetCreateFromCSR(
-            ptr_indptr, ctypes.c_int(type_ptr_indptr), csr_indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-            ptr_data, ctypes.c_int(type_ptr_data), ctypes.c_int64(len(csr.indptr)), ctypes.c_int64(len(csr.data)),
-            ctypes.c_int64(csr.shape[1]), c_str(params_str), ref_dataset, ctypes.byref(self.handle)))
-        return self
+        nat.call("LGBM_DatasetGetSubset", self.reference.construct().handle,
+                 idx.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.c_int32(len(idx)),
+                 nat.cstr(nat.params_str(self.params)), ctypes.byref(self.handle))
+        if not self.free_raw_data:
+            self.get_data()
+        if self.group is not None:
+            self.set_group(self.group)
+        if self.get_label() is None:
+            raise ValueError("Label should not be None.")
+        if isinstance(self._predictor, _InnerPredictor) and self._predictor is not self.reference._predictor:
+            self.get_data()
+            self._init_score_from(self._predictor, self.data, idx)
 
-    def __init_from_csc(self, csc, params_str, ref_dataset):
-        if len(csc.indices) != len(csc.data):
-            raise ValueError("Length mismatch: {} vs {}".format(len(csc.indices), len(csc.data)))
-        self.handle = ctypes.c_void_p()
-        ptr_indptr, type_ptr_indptr, __ = c_int_array(csc.indptr)
-        ptr_data, type_ptr_data, _ = c_float_array(csc.data)
-        assert csc.shape[0] <= MAX_INT32
-        csc_indices = csc.indices.astype(np.int32, copy=False)
-        _safe_call(_load_lib().LGBM_DatasetCreateFromCSC(
-            ptr_indptr, ctypes.c_int(type_ptr_indptr), csc_indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-            ptr_data, ctypes.c_int(type_ptr_data), ctypes.c_int64(len(csc.indptr)), ctypes.c_int64(len(csc.data)),
-            ctypes.c_int64(csc.shape[0]), c_str(params_str), ref_dataset, ctypes.byref(self.handle)))
-        return self
-
-    def construct(self):
-        """Lazy init."""
-        if self.handle is None:
-            if self.reference is not None:
-                reference_params = self.reference.get_params()
-                if self.get_params() != reference_params:
-                    warnings.warn("Overriding the parameters from Reference Dataset.")
-                    self._update_params(reference_params)
-                if self.used_indices is None:
-                    # create valid
-                    self._lazy_init(self.data, label=self.label, reference=self.reference, weight=self.weight,
-                                    group=self.group, init_score=self.init_score, predictor=self._predictor,
-                                    silent=self.silent, feature_name=self.feature_name, params=self.params)
-                else:
-                    # construct subset
-                    used_indices = list_to_1d_numpy(self.used_indices, np.int32, name="used_indices")
-                    assert used_indices.flags.c_contiguous
-                    if self.reference.group is not None:
-                        group_info = np.array(self.reference.group).astype(np.int32, copy=False)
-                        _, self.group = np.unique(np.repeat(range(len(group_info)), repeats=group_info)[
-                            self.used_indices], return_counts=True)
-                    self.handle = ctypes.c_void_p()
-                    params_str = param_dict_to_str(self.params)
-                    _safe_call(_load_lib().LGBM_DatasetGetSubset(
-                        self.reference.construct().handle,
-                        used_indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
-                        ctypes.c_int32(used_indices.shape[0]), c_str(params_str), ctypes.byref(self.handle)))
-                    if not self.free_raw_data:
-                        self.get_data()
-                    if self.group is not None:
-                        self.set_group(self.group)
-                    if self.get_label() is None:
-                        raise ValueError("Label should not be None.")
-                    if isinstance(self._predictor, _InnerPredictor) and self._predictor is not self.reference._predictor:
-                        self.get_data()
-                        self._set_init_score_by_predictor(self._predictor, self.data, used_indices)
-            else:
-                # create train
-                self._lazy_init(self.data, label=self.label, weight=self.weight, group=self.group,
-                                init_score=self.init_score, predictor=self._predictor, silent=self.silent,
-                                feature_name=self.feature_name, categorical_feature=self.categorical_feature,
-                                params=self.params)
-            if self.free_raw_data:
-                self.data = None
-        return self
+    def _init_score_from(self, predictor, data, used_indices=None):
+        """Raw scores of the init_model on this dataset's rows (class-major for the library)."""
+        header = isinstance(data, string_type) and _any_alias(self.params or {}, "header")
+        n = self.num_data()
+        if predictor is None:
+            if self.init_score is not None:
+                self.set_init_score(np.zeros(np.shape(self.init_score), dtype=np.float32))
+            return self
+        k = predictor.num_class
+        score = predictor.predict(data, raw_score=True, data_has_header=header, is_reshape=False)
+        if used_indices is not None and isinstance(data, string_type):
+            score = score.reshape(-1, k)[used_indices].reshape(-1)
+        if k > 1:
+            score = score.reshape(n, k).T.reshape(-1)  # row-major (row, class) -> class-major
+        return self.set_init_score(score.astype(np.float32))
 
     def create_valid(self, data, label=None, weight=None, group=None, init_score=None, silent=False, params=None):
-        """Create validation data aligned with the current Dataset."""
+        """A validation Dataset binned like this one."""
         ret = Dataset(data, label=label, reference=self, weight=weight, group=group, init_score=init_score,
                       silent=silent, params=params, free_raw_data=self.free_raw_data)
         ret._predictor = self._predictor
@@ -968,45 +365,39 @@ class Dataset(object):
         return ret
 
     def subset(self, used_indices, params=None):
-        """Get subset of current Dataset."""
-        if params is None:
-            params = self.params
+        """A Dataset of some rows of this one (shares its bin mappers)."""
         ret = Dataset(None, reference=self, feature_name=self.feature_name,
-                      categorical_feature=self.categorical_feature, params=params, free_raw_data=self.free_raw_data)
+                      categorical_feature=self.categorical_feature,
+                      params=self.params if params is None else params, free_raw_data=self.free_raw_data)
         ret._predictor = self._predictor
         ret.pandas_categorical = self.pandas_categorical
         ret.used_indices = sorted(used_indices)
         return ret
 
     def save_binary(self, filename):
-        """Save Dataset to a binary file."""
-        _safe_call(_load_lib().LGBM_DatasetSaveBinary(self.construct().handle, c_str(filename)))
+        """Write the binned dataset (reloadable as a data file)."""
+        nat.call("LGBM_DatasetSaveBinary", self.construct().handle, nat.cstr(filename))
         return self
 
     def _update_params(self, params):
         if not params:
             return self
         params = copy.deepcopy(params)
-
-        def update():
-            if not self.params:
-                self.params = params
-            else:
+        if self.handle is None:
+            if self.params:
                 self.params_back_up = copy.deepcopy(self.params)
                 self.params.update(params)
-
-        if self.handle is None:
-            update()
-        elif params is not None:
-            ret = _load_lib().LGBM_DatasetUpdateParamChecking(c_str(param_dict_to_str(self.params)),
-                                                              c_str(param_dict_to_str(params)))
-            if ret != 0:
-                # could be updated if data is not freed
-                if self.data is not None:
-                    update()
-                    self._free_handle()
-                else:
-                    raise LightGBMError(_load_lib().LGBM_GetLastError().decode("utf-8"))
+            else:
+                self.params = params
+            return self
+        ok = nat.lib().LGBM_DatasetUpdateParamChecking(nat.cstr(nat.params_str(self.params)),
+                                                       nat.cstr(nat.params_str(params)))
+        if ok != 0:
+            if self.data is None:  # the binned data cannot be rebuilt
+                nat.check(ok)
+            self.params_back_up = copy.deepcopy(self.params)
+            self.params.update(params)
+            self._free_handle()
         return self
 
     def _reverse_update_params(self):
@@ -1015,348 +406,499 @@ class Dataset(object):
             self.params_back_up = None
         return self
 
+    # ------------------------------------------------------------------ fields
     def set_field(self, field_name, data):
-        """Set property into the Dataset."""
+        """Store a field (label, weight, init_score, group) on the native dataset."""
         if self.handle is None:
             raise Exception("Cannot set %s before construct dataset" % field_name)
+        np_dtype, code = _FIELDS[field_name]
         if data is None:
-            # set to None
-            _safe_call(_load_lib().LGBM_DatasetSetField(self.handle, c_str(field_name), None, ctypes.c_int(0),
-                                                        ctypes.c_int(FIELD_TYPE_MAPPER[field_name])))
+            nat.call("LGBM_DatasetSetField", self.handle, nat.cstr(field_name), None, nat.c_int(0), nat.c_int(code))
             return self
-        dtype = np.float32
-        if field_name == "group":
-            dtype = np.int32
-        elif field_name == "init_score":
-            dtype = np.float64
-        data = list_to_1d_numpy(data, dtype, name=field_name)
-        if data.dtype == np.float32 or data.dtype == np.float64:
-            ptr_data, type_data, _ = c_float_array(data)
-        elif data.dtype == np.int32:
-            ptr_data, type_data, _ = c_int_array(data)
-        else:
-            raise TypeError("Expected np.float32/64 or np.int32, met type({})".format(data.dtype))
-        if type_data != FIELD_TYPE_MAPPER[field_name]:
+        arr = np.ascontiguousarray(inp.vector(data, np_dtype, field_name))
+        ptr, got = nat.pointer(arr)
+        if got != code:
             raise TypeError("Input type error for set_field")
-        _safe_call(_load_lib().LGBM_DatasetSetField(self.handle, c_str(field_name), ptr_data,
-                                                    ctypes.c_int(len(data)), ctypes.c_int(type_data)))
+        nat.call("LGBM_DatasetSetField", self.handle, nat.cstr(field_name), ptr, nat.c_int(len(arr)), nat.c_int(code))
         self.version += 1
         return self
 
     def get_field(self, field_name):
-        """Get property from the Dataset."""
+        """A field of the native dataset as a numpy array (None if unset)."""
         if self.handle is None:
             raise Exception("Cannot get %s before construct Dataset" % field_name)
-        tmp_out_len = ctypes.c_int()
-        out_type = ctypes.c_int()
-        ret = ctypes.POINTER(ctypes.c_void_p)()
-        _safe_call(_load_lib().LGBM_DatasetGetField(self.handle, c_str(field_name), ctypes.byref(tmp_out_len),
-                                                    ctypes.byref(ret), ctypes.byref(out_type)))
-        if out_type.value != FIELD_TYPE_MAPPER[field_name]:
+        n = ctypes.c_int(0)
+        code = ctypes.c_int(0)
+        ptr = ctypes.c_void_p()
+        nat.call("LGBM_DatasetGetField", self.handle, nat.cstr(field_name), ctypes.byref(n), ctypes.byref(ptr),
+                 ctypes.byref(code))
+        if code.value != _FIELDS[field_name][1]:
             raise TypeError("Return type error for get_field")
-        if tmp_out_len.value == 0:
-            return None
-        if out_type.value == C_API_DTYPE_INT32:
-            return cint32_array_to_numpy(ctypes.cast(ret, ctypes.POINTER(ctypes.c_int32)), tmp_out_len.value)
-        if out_type.value == C_API_DTYPE_FLOAT32:
-            return cfloat32_array_to_numpy(ctypes.cast(ret, ctypes.POINTER(ctypes.c_float)), tmp_out_len.value)
-        if out_type.value == C_API_DTYPE_FLOAT64:
-            return cfloat64_array_to_numpy(ctypes.cast(ret, ctypes.POINTER(ctypes.c_double)), tmp_out_len.value)
-        raise TypeError("Unknown type")
-
-    def set_categorical_feature(self, categorical_feature):
-        """Set categorical features."""
-        if self.categorical_feature == categorical_feature:
-            return self
-        if self.data is not None:
-            if self.categorical_feature is None:
-                self.categorical_feature = categorical_feature
-                return self._free_handle()
-            if categorical_feature == "auto":
-                warnings.warn("Using categorical_feature in Dataset.")
-                return self
-            warnings.warn("categorical_feature in Dataset is overridden.\n"
-                          "New categorical_feature is {}".format(sorted(list(categorical_feature))))
-            self.categorical_feature = categorical_feature
-            return self._free_handle()
-        raise LightGBMError("Cannot set categorical feature after freed raw data, "
-                            "set free_raw_data=False when construct Dataset to avoid this.")
-
-    def _set_predictor(self, predictor):
-        if predictor is self._predictor and (predictor is None or predictor.current_iteration() ==
-                                             self._predictor.current_iteration()):
-            return self
-        if self.handle is None:
-            self._predictor = predictor
-        elif self.data is not None:
-            self._predictor = predictor
-            self._set_init_score_by_predictor(self._predictor, self.data)
-        elif self.used_indices is not None and self.reference is not None and self.reference.data is not None:
-            self._predictor = predictor
-            self._set_init_score_by_predictor(self._predictor, self.reference.data, self.used_indices)
-        else:
-            raise LightGBMError("Cannot set predictor after freed raw data, "
-                                "set free_raw_data=False when construct Dataset to avoid this.")
-        return self
-
-    def set_reference(self, reference):
-        """Set reference Dataset."""
-        self.set_categorical_feature(reference.categorical_feature) \
-            .set_feature_name(reference.feature_name) \
-            ._set_predictor(reference._predictor)
-        # we're done if self and reference share a common upstrem reference
-        if self.get_ref_chain().intersection(reference.get_ref_chain()):
-            return self
-        if self.data is not None:
-            self.reference = reference
-            return self._free_handle()
-        raise LightGBMError("Cannot set reference after freed raw data, "
-                            "set free_raw_data=False when construct Dataset to avoid this.")
-
-    def set_feature_name(self, feature_name):
-        """Set feature name."""
-        if feature_name != "auto":
-            self.feature_name = feature_name
-        if self.handle is not None and feature_name is not None and feature_name != "auto":
-            if len(feature_name) != self.num_feature():
-                raise ValueError("Length of feature_name({}) and num_feature({}) don't match"
-                                 .format(len(feature_name), self.num_feature()))
-            c_feature_name = [c_str(name) for name in feature_name]
-            _safe_call(_load_lib().LGBM_DatasetSetFeatureNames(self.handle, c_array(ctypes.c_char_p, c_feature_name),
-                                                               ctypes.c_int(len(feature_name))))
-        return self
+        return nat.copy_out(ptr, n.value, code.value) if n.value else None
 
     def set_label(self, label):
-        """Set label of Dataset."""
         self.label = label
         if self.handle is not None:
-            label = list_to_1d_numpy(_label_from_pandas(label), name="label")
-            self.set_field("label", label)
-            self.label = self.get_field("label")  # original values can be modified at cpp side
+            self.set_field("label", inp.vector(inp.label_vector(label), np.float32, "label"))
+            self.label = self.get_field("label")  # as the library stored it
         return self
 
     def set_weight(self, weight):
-        """Set weight of each instance."""
-        if weight is not None and np.all(weight == 1):
-            weight = None
+        if weight is not None and np.all(np.asarray(inp.to_host(weight)) == 1):
+            weight = None  # unit weights: none
         self.weight = weight
         if self.handle is not None:
-            if weight is None:
-                self.set_field("weight", None)  # clears the native weights
-                return self
-            weight = list_to_1d_numpy(weight, name="weight")
-            self.set_field("weight", weight)
-            self.weight = self.get_field("weight")  # original values can be modified at cpp side
+            self.set_field("weight", None if weight is None else inp.vector(weight, np.float32, "weight"))
+            if weight is not None:
+                self.weight = self.get_field("weight")
         return self
 
     def set_init_score(self, init_score):
-        """Set init score of Booster to start from."""
         self.init_score = init_score
-        if self.handle is not None and init_score is None:
-            self.set_field("init_score", None)
-        elif self.handle is not None:
-            init_score = list_to_1d_numpy(init_score, np.float64, name="init_score")
-            self.set_field("init_score", init_score)
-            self.init_score = self.get_field("init_score")  # original values can be modified at cpp side
+        if self.handle is not None:
+            self.set_field("init_score", None if init_score is None else
+                           inp.vector(init_score, np.float64, "init_score"))
+            if init_score is not None:
+                self.init_score = self.get_field("init_score")
         return self
 
     def set_group(self, group):
-        """Set group size of Dataset (used for ranking)."""
         self.group = group
         if self.handle is not None and group is not None:
-            group = list_to_1d_numpy(group, np.int32, name="group")
-            self.set_field("group", group)
+            self.set_field("group", inp.vector(group, np.int32, "group"))
         return self
 
-    def get_feature_name(self):
-        """Get the names of columns (features) in the Dataset."""
-        if self.handle is None:
-            raise LightGBMError("Cannot get feature_name before construct dataset")
-        num_feature = self.num_feature()
-        tmp_out_len = ctypes.c_int(0)
-        reserved_string_buffer_size = 255
-        required_string_buffer_size = ctypes.c_size_t(0)
-        string_buffers = [ctypes.create_string_buffer(reserved_string_buffer_size) for _ in range(num_feature)]
-        ptr_string_buffers = (ctypes.c_char_p * num_feature)(*map(ctypes.addressof, string_buffers))
-        _safe_call(_load_lib().LGBM_DatasetGetFeatureNames(
-            self.handle, ctypes.c_int(num_feature), ctypes.byref(tmp_out_len),
-            ctypes.c_size_t(reserved_string_buffer_size), ctypes.byref(required_string_buffer_size),
-            ptr_string_buffers))
-        if num_feature != tmp_out_len.value:
-            raise ValueError("Length of feature names doesn't equal with num_feature")
-        if reserved_string_buffer_size < required_string_buffer_size.value:
-            actual = required_string_buffer_size.value
-            string_buffers = [ctypes.create_string_buffer(actual) for _ in range(num_feature)]
-            ptr_string_buffers = (ctypes.c_char_p * num_feature)(*map(ctypes.addressof, string_buffers))
-            _safe_call(_load_lib().LGBM_DatasetGetFeatureNames(
-                self.handle, ctypes.c_int(num_feature), ctypes.byref(tmp_out_len), ctypes.c_size_t(actual),
-                ctypes.byref(required_string_buffer_size), ptr_string_buffers))
-        return [string_buffers[i].value.decode("utf-8") for i in range(num_feature)]
-
     def get_label(self):
-        """Get the label of the Dataset."""
         if self.label is None:
             self.label = self.get_field("label")
         return self.label
 
     def get_weight(self):
-        """Get the weight of the Dataset."""
         if self.weight is None:
             self.weight = self.get_field("weight")
         return self.weight
 
     def get_init_score(self):
-        """Get the initial score of the Dataset."""
         if self.init_score is None:
             self.init_score = self.get_field("init_score")
         return self.init_score
 
+    def get_group(self):
+        """Group sizes (the library keeps query boundaries)."""
+        if self.group is None:
+            bounds = self.get_field("group")
+            self.group = np.diff(bounds) if bounds is not None else None
+        return self.group
+
     def get_data(self):
-        """Get the raw data of the Dataset."""
+        """The raw data (sliced from the reference's for a subset)."""
         if self.handle is None:
             raise Exception("Cannot get data before construct Dataset")
         if self.need_slice and self.used_indices is not None and self.reference is not None:
-            self.data = self.reference.data
-            if self.data is not None:
-                if isinstance(self.data, np.ndarray) or scipy.sparse.issparse(self.data):
-                    self.data = self.data[self.used_indices, :]
-                elif isinstance(self.data, pd_DataFrame):
-                    self.data = self.data.iloc[self.used_indices].copy()
-                elif isinstance(self.data, dt_DataTable):
-                    self.data = self.data[self.used_indices, :]
+            src = self.reference.data
+            if src is not None:
+                if isinstance(src, np.ndarray) or scipy.sparse.issparse(src):
+                    src = src[self.used_indices, :]
+                elif inp.is_frame(src):
+                    src = src.iloc[self.used_indices].copy()
+                elif dt_DataTable is not None and isinstance(src, dt_DataTable):
+                    src = src[self.used_indices, :]
                 else:
-                    warnings.warn("Cannot subset {} type of raw data.\nReturning original raw data"
-                                  .format(type(self.data).__name__))
+                    warnings.warn("Cannot subset {} type of raw data.\nReturning original raw data".format(
+                        type(src).__name__))
+            self.data = src
             self.need_slice = False
         if self.data is None:
             raise LightGBMError("Cannot call `get_data` after freed raw data, "
                                 "set free_raw_data=False when construct Dataset to avoid this.")
         return self.data
 
-    def get_group(self):
-        """Get the group of the Dataset."""
-        if self.group is None:
-            self.group = self.get_field("group")
-            if self.group is not None:
-                # group data from LightGBM is boundaries data, need to convert to group size
-                self.group = np.diff(self.group)
-        return self.group
+    # ------------------------------------------------------------------ features / links
+    def set_categorical_feature(self, categorical_feature):
+        if self.categorical_feature == categorical_feature:
+            return self
+        if self.data is None:
+            raise LightGBMError("Cannot set categorical feature after freed raw data, "
+                                "set free_raw_data=False when construct Dataset to avoid this.")
+        if self.categorical_feature is None:
+            self.categorical_feature = categorical_feature
+            return self._free_handle()
+        if categorical_feature == "auto":
+            warnings.warn("Using categorical_feature in Dataset.")
+            return self
+        warnings.warn("categorical_feature in Dataset is overridden.\nNew categorical_feature is {}".format(
+            sorted(categorical_feature)))
+        self.categorical_feature = categorical_feature
+        return self._free_handle()
+
+    def _set_predictor(self, predictor):
+        same = predictor is self._predictor and (
+            predictor is None or predictor.current_iteration() == self._predictor.current_iteration())
+        if same:
+            return self
+        if self.handle is None:
+            self._predictor = predictor
+        elif self.data is not None:
+            self._predictor = predictor
+            self._init_score_from(predictor, self.data)
+        elif self.used_indices is not None and self.reference is not None and self.reference.data is not None:
+            self._predictor = predictor
+            self._init_score_from(predictor, self.reference.data, self.used_indices)
+        else:
+            raise LightGBMError("Cannot set predictor after freed raw data, "
+                                "set free_raw_data=False when construct Dataset to avoid this.")
+        return self
+
+    def set_reference(self, reference):
+        self.set_categorical_feature(reference.categorical_feature).set_feature_name(reference.feature_name)
+        self._set_predictor(reference._predictor)
+        if self.get_ref_chain() & reference.get_ref_chain():
+            return self  # already binned with the same upstream reference
+        if self.data is None:
+            raise LightGBMError("Cannot set reference after freed raw data, "
+                                "set free_raw_data=False when construct Dataset to avoid this.")
+        self.reference = reference
+        return self._free_handle()
+
+    def set_feature_name(self, feature_name):
+        if feature_name != "auto":
+            self.feature_name = feature_name
+        if self.handle is not None and feature_name not in (None, "auto"):
+            if len(feature_name) != self.num_feature():
+                raise ValueError("Length of feature_name({}) and num_feature({}) don't match".format(
+                    len(feature_name), self.num_feature()))
+            nat.call("LGBM_DatasetSetFeatureNames", self.handle, nat.string_array(list(feature_name)),
+                     nat.c_int(len(feature_name)))
+        return self
+
+    def get_feature_name(self):
+        if self.handle is None:
+            raise LightGBMError("Cannot get feature_name before construct dataset")
+        return nat.read_names(lambda n, got, size, need, bufs: nat.call(
+            "LGBM_DatasetGetFeatureNames", self.handle, n, got, size, need, bufs), self.num_feature())
 
     def num_data(self):
-        """Get the number of rows in the Dataset."""
-        if self.handle is not None:
-            ret = ctypes.c_int()
-            _safe_call(_load_lib().LGBM_DatasetGetNumData(self.handle, ctypes.byref(ret)))
-            return ret.value
-        raise LightGBMError("Cannot get num_data before construct dataset")
+        if self.handle is None:
+            raise LightGBMError("Cannot get num_data before construct dataset")
+        out = ctypes.c_int(0)
+        nat.call("LGBM_DatasetGetNumData", self.handle, ctypes.byref(out))
+        return out.value
 
     def num_feature(self):
-        """Get the number of columns (features) in the Dataset."""
-        if self.handle is not None:
-            ret = ctypes.c_int()
-            _safe_call(_load_lib().LGBM_DatasetGetNumFeature(self.handle, ctypes.byref(ret)))
-            return ret.value
-        raise LightGBMError("Cannot get num_feature before construct dataset")
+        if self.handle is None:
+            raise LightGBMError("Cannot get num_feature before construct dataset")
+        out = ctypes.c_int(0)
+        nat.call("LGBM_DatasetGetNumFeature", self.handle, ctypes.byref(out))
+        return out.value
 
     def get_ref_chain(self, ref_limit=100):
-        """Get a chain of Dataset objects."""
-        head = self
-        ref_chain = set()
-        while len(ref_chain) < ref_limit:
-            if isinstance(head, Dataset):
-                ref_chain.add(head)
-                if (head.reference is not None) and (head.reference not in ref_chain):
-                    head = head.reference
-                else:
-                    break
-            else:
-                break
-        return ref_chain
+        """This dataset and its chain of references."""
+        chain, node = set(), self
+        while isinstance(node, Dataset) and node not in chain and len(chain) < ref_limit:
+            chain.add(node)
+            node = node.reference
+        return chain
 
     def add_features_from(self, other):
-        """Add features from other Dataset to the current Dataset."""
         if self.handle is None or other.handle is None:
             raise ValueError("Both source and target Datasets must be constructed before adding features")
-        _safe_call(_load_lib().LGBM_DatasetAddFeaturesFrom(self.handle, other.handle))
+        nat.call("LGBM_DatasetAddFeaturesFrom", self.handle, other.handle)
         return self
 
     def _dump_text(self, filename):
-        """Save Dataset to a text file (for debugging)."""
-        _safe_call(_load_lib().LGBM_DatasetDumpText(self.construct().handle, c_str(filename)))
+        nat.call("LGBM_DatasetDumpText", self.construct().handle, nat.cstr(filename))
         return self
 
 
-class Booster(object):
-    """Booster in LightGBM."""
+# ---------------------------------------------------------------------------- predict
+def _num_preds(handle, nrow, ptype, start, num):
+    if nrow > nat.MAX_INT32:
+        raise LightGBMError("LightGBM cannot perform prediction for data with number of rows greater than "
+                            "MAX_INT32 (%d).\nYou can split your data into chunks and then concatenate "
+                            "predictions for them" % nat.MAX_INT32)
+    out = ctypes.c_int64(0)
+    nat.call("LGBM_BoosterCalcNumPredict", handle, nat.c_int(nrow), nat.c_int(ptype), nat.c_int(start),
+             nat.c_int(num), ctypes.byref(out))
+    return out.value
+
+
+class _InnerPredictor:
+    """Prediction over a native booster: from a model file (owned handle) or a Booster's
+    handle (borrowed)."""
+
+    def __init__(self, model_file=None, booster_handle=None, pred_parameter=None):
+        self.handle = ctypes.c_void_p()
+        self._owns = model_file is not None
+        if model_file is not None:
+            iters = ctypes.c_int(0)
+            nat.call("LGBM_BoosterCreateFromModelfile", nat.cstr(model_file), ctypes.byref(iters),
+                     ctypes.byref(self.handle))
+            self.num_total_iteration = iters.value
+            self.pandas_categorical = inp.categories_from_file(model_file)
+        elif booster_handle is not None:
+            self.handle = booster_handle
+            self.num_total_iteration = self.current_iteration()
+            self.pandas_categorical = None
+        else:
+            raise TypeError("Need model_file or booster_handle to create a predictor")
+        k = ctypes.c_int(0)
+        nat.call("LGBM_BoosterGetNumClasses", self.handle, ctypes.byref(k))
+        self.num_class = k.value
+        self.pred_parameter = nat.params_str(pred_parameter or {})
+
+    def __del__(self):
+        try:
+            if self._owns:
+                nat.call("LGBM_BoosterFree", self.handle)
+        except Exception:  # noqa: BLE001
+            pass
+
+    def __getstate__(self):
+        state = self.__dict__.copy()
+        state.pop("handle", None)
+        return state
+
+    def current_iteration(self):
+        out = ctypes.c_int(0)
+        nat.call("LGBM_BoosterGetCurrentIteration", self.handle, ctypes.byref(out))
+        return out.value
+
+    def predict(self, data, start_iteration=0, num_iteration=-1, raw_score=False, pred_leaf=False,
+                pred_contrib=False, data_has_header=False, is_reshape=True):
+        if isinstance(data, Dataset):
+            raise TypeError("Cannot use Dataset instance for prediction, please use raw data instead")
+        data = inp.frame_to_array(inp.to_host(data), None, None, self.pandas_categorical)[0]
+        ptype = (nat.PREDICT_CONTRIB if pred_contrib else nat.PREDICT_LEAF_INDEX if pred_leaf
+                 else nat.PREDICT_RAW_SCORE if raw_score else nat.PREDICT_NORMAL)
+        kind = _input_kind(data)
+        if kind == "list":
+            try:
+                data = np.array(data)
+            except Exception:  # noqa: BLE001
+                raise ValueError("Cannot convert data list to numpy array.")
+            kind = "dense"
+        elif kind == "datatable":
+            data, kind = data.to_numpy(), "dense"
+        elif kind is None:
+            try:
+                warnings.warn("Converting data to scipy sparse matrix.")
+                data, kind = scipy.sparse.csr_matrix(data), "csr"
+            except Exception:  # noqa: BLE001
+                raise TypeError("Cannot predict data for type {}".format(type(data).__name__))
+        if kind == "file":
+            preds, nrow = self._predict_file(data, data_has_header, ptype, start_iteration, num_iteration)
+        elif kind in ("csr", "csc"):
+            preds, nrow = self._predict_sparse(data, ptype, start_iteration, num_iteration)
+        else:
+            preds, nrow = self._predict_dense(data, ptype, start_iteration, num_iteration)
+        if pred_leaf:
+            preds = preds.astype(np.int32)
+        if is_reshape and isinstance(preds, np.ndarray) and preds.size != nrow:
+            if preds.size % nrow:
+                raise ValueError("Length of predict result (%d) cannot be divide nrow (%d)" % (preds.size, nrow))
+            preds = preds.reshape(nrow, -1)
+        return preds
+
+    def _predict_file(self, path, header, ptype, start, num):
+        fd, out_path = tempfile.mkstemp(prefix="lgbm_amd_pred_")
+        os.close(fd)
+        try:
+            nat.call("LGBM_BoosterPredictForFile", self.handle, nat.cstr(path), nat.c_int(1 if header else 0),
+                     nat.c_int(ptype), nat.c_int(start), nat.c_int(num), nat.cstr(self.pred_parameter),
+                     nat.cstr(out_path))
+            with open(out_path) as f:
+                rows = [line.split("\t") for line in f.read().splitlines() if line]
+        finally:
+            os.remove(out_path)
+        return np.asarray([float(v) for r in rows for v in r], dtype=np.float64), len(rows)
+
+    def _predict_dense(self, mat, ptype, start, num):
+        mat = np.asarray(mat)
+        if mat.ndim != 2:
+            raise ValueError("Input numpy.ndarray or list must be 2 dimensional")
+        nrow = mat.shape[0]
+        # the C API takes int32 row counts: cut very tall inputs into chunks
+        bounds = list(range(0, nrow, nat.MAX_INT32)) + [nrow]
+        counts = [_num_preds(self.handle, b - a, ptype, start, num) for a, b in zip(bounds[:-1], bounds[1:])]
+        out = np.zeros(sum(counts), dtype=np.float64)
+        at = 0
+        for (a, b), cnt in zip(zip(bounds[:-1], bounds[1:]), counts):
+            buf, rows, cols = _dense_block(mat[a:b])
+            ptr, code = nat.pointer(buf)
+            got = ctypes.c_int64(0)
+            view = out[at:at + cnt]
+            nat.call("LGBM_BoosterPredictForMat", self.handle, ptr, nat.c_int(code), ctypes.c_int32(rows),
+                     ctypes.c_int32(cols), nat.c_int(1), nat.c_int(ptype), nat.c_int(start), nat.c_int(num),
+                     nat.cstr(self.pred_parameter), ctypes.byref(got), view.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+            if got.value != cnt:
+                raise ValueError("Wrong length for predict results")
+            at += cnt
+        return out, nrow
+
+    def _predict_sparse(self, m, ptype, start, num):
+        csr = scipy.sparse.isspmatrix_csr(m)
+        nrow = m.shape[0]
+        if not csr and nrow > nat.MAX_INT32:
+            return self._predict_sparse(m.tocsr(), ptype, start, num)
+        indptr, indices, values = _sparse_parts(m)
+        p_ptr, p_code = nat.pointer(indptr)
+        v_ptr, v_code = nat.pointer(values)
+        i_ptr = indices.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+        ncross = m.shape[1] if csr else m.shape[0]  # columns (CSR) or rows (CSC)
+        common = (p_ptr, ctypes.c_int32(p_code), i_ptr, v_ptr, nat.c_int(v_code), ctypes.c_int64(len(indptr)),
+                  ctypes.c_int64(len(values)), ctypes.c_int64(ncross), nat.c_int(ptype), nat.c_int(start),
+                  nat.c_int(num), nat.cstr(self.pred_parameter))
+        if ptype == nat.PREDICT_CONTRIB:
+            return self._contrib_sparse(m, csr, common, p_code, v_code), nrow
+        cnt = _num_preds(self.handle, nrow, ptype, start, num)
+        out = np.zeros(cnt, dtype=np.float64)
+        got = ctypes.c_int64(0)
+        nat.call("LGBM_BoosterPredictForCSR" if csr else "LGBM_BoosterPredictForCSC", self.handle, *common,
+                 ctypes.byref(got), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        if got.value != cnt:
+            raise ValueError("Wrong length for predict results")
+        return out, nrow
+
+    def _contrib_sparse(self, m, csr, common, p_code, v_code):
+        """SHAP values of sparse input as sparse matrices (one per class if multiclass)."""
+        out_indptr = ctypes.c_void_p()
+        out_indices = ctypes.c_void_p()
+        out_data = ctypes.c_void_p()
+        shape = np.zeros(2, dtype=np.int64)
+        nat.call("LGBM_BoosterPredictSparseOutput", self.handle, *common,
+                 nat.c_int(nat.MATRIX_CSR if csr else nat.MATRIX_CSC),
+                 shape.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(out_indptr),
+                 ctypes.byref(out_indices), ctypes.byref(out_data))
+        nnz, nptr = int(shape[0]), int(shape[1])
+        try:
+            indptr = nat.copy_out(out_indptr, nptr, p_code)
+            indices = nat.copy_out(out_indices, nnz, nat.DTYPE_INT32)
+            values = nat.copy_out(out_data, nnz, v_code)
+        finally:
+            nat.call("LGBM_BoosterFreePredictSparse", out_indptr, out_indices, out_data, nat.c_int(p_code),
+                     nat.c_int(v_code))
+        shape_k = (m.shape[0], m.shape[1] + 1)
+        make = scipy.sparse.csr_matrix if csr else scipy.sparse.csc_matrix
+        if self.num_class <= 1:
+            return make((values, indices, indptr), shape_k)
+        # the classes' compressed arrays are concatenated, each indptr with its own offsets
+        per = (shape_k[0] if csr else shape_k[1]) + 1
+        mats = []
+        for c in range(self.num_class):
+            p = indptr[c * per:(c + 1) * per]
+            lo, hi = p[0], p[-1]
+            mats.append(make((values[lo:hi], indices[lo:hi], p - lo), shape_k))
+        return mats
+
+
+# ----------------------------------------------------------------------------- booster
+class _EvalInfo:
+    """Names / directions of the booster's built-in metrics (loaded once)."""
+
+    def __init__(self):
+        self.names = None
+        self.higher_better = None
+
+    def load(self, handle):
+        if self.names is not None:
+            return self
+        n = ctypes.c_int(0)
+        nat.call("LGBM_BoosterGetEvalCounts", handle, ctypes.byref(n))
+        self.names = [] if n.value == 0 else nat.read_names(
+            lambda c, got, size, need, bufs: nat.call("LGBM_BoosterGetEvalNames", handle, c, got, size, need, bufs),
+            n.value)
+        self.higher_better = [nm.startswith(("auc", "ndcg@", "map@", "average_precision")) for nm in self.names]
+        return self
+
+
+class _ScoreCache:
+    """Raw scores of the training / validation datasets, fetched once per iteration (for
+    custom objectives and metrics)."""
+
+    def __init__(self):
+        self.buffers = []
+        self.fresh = []
+
+    def add(self):
+        self.buffers.append(None)
+        self.fresh.append(False)
+
+    def invalidate(self):
+        self.fresh = [False] * len(self.buffers)
+
+    def get(self, handle, idx, n):
+        if self.buffers[idx] is None:
+            self.buffers[idx] = np.zeros(n, dtype=np.float64)
+        if not self.fresh[idx]:
+            got = ctypes.c_int64(0)
+            nat.call("LGBM_BoosterGetPredict", handle, nat.c_int(idx), ctypes.byref(got),
+                     self.buffers[idx].ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+            if got.value != n:
+                raise ValueError("Wrong length of predict results for data %d" % idx)
+            self.fresh[idx] = True
+        return self.buffers[idx]
+
+
+def _network_params(params):
+    """machines=... in params: (machine list string, count) or None."""
+    for alias in _ConfigAliases.get("machines"):
+        if alias in params:
+            m = params[alias]
+            if isinstance(m, string_type):
+                return m, len(m.split(","))
+            if isinstance(m, (list, set, tuple)):
+                return ",".join(m), len(m)
+            raise ValueError("Invalid machines in params.")
+    return None
+
+
+class Booster:
+    """A gradient boosting model: trained from a Dataset, or loaded from a file / string."""
 
     def __init__(self, params=None, train_set=None, model_file=None, model_str=None, silent=False):
         self.handle = None
         self.network = False
-        self.__need_reload_eval_info = True
         self._train_data_name = "training"
-        self.__attr = {}
-        self.__set_objective_to_none = False
+        self._attrs = {}
+        self._objective_none = False  # a custom objective replaced the built-in one
         self.best_iteration = -1
         self.best_score = {}
-        params = {} if params is None else copy.deepcopy(params)
-        # user can set verbose with params, it has higher priority
-        if not any(verbose_alias in params for verbose_alias in _ConfigAliases.get("verbosity")) and silent:
-            params["verbose"] = -1
+        self._evals = _EvalInfo()
+        self._scores = _ScoreCache()
+        self._num_class = 1
+        self._init_predictor = None
+        params = _quiet({} if params is None else copy.deepcopy(params), silent)
         if train_set is not None:
-            # Training task
             if not isinstance(train_set, Dataset):
                 raise TypeError("Training data should be Dataset instance, met {}".format(type(train_set).__name__))
-            params_str = param_dict_to_str(params)
-            # set network if necessary
-            for alias in _ConfigAliases.get("machines"):
-                if alias in params:
-                    machines = params[alias]
-                    if isinstance(machines, string_type):
-                        num_machines = len(machines.split(","))
-                    elif isinstance(machines, (list, set)):
-                        num_machines = len(machines)
-                        machines = ",".join(machines)
-                    else:
-                        raise ValueError("Invalid machines in params.")
-                    self.set_network(machines,
-                                     local_listen_port=params.get("local_listen_port", 12400),
-                                     listen_time_out=params.get("listen_time_out", 120),
-                                     num_machines=params.setdefault("num_machines", num_machines))
-                    break
-            # construct booster object
+            net = _network_params(params)
+            if net is not None:
+                self.set_network(net[0], local_listen_port=params.get("local_listen_port", 12400),
+                                 listen_time_out=params.get("listen_time_out", 120),
+                                 num_machines=params.setdefault("num_machines", net[1]))
             train_set.construct()
-            # copy the parameters from train_set
             params.update(train_set.get_params())
-            params_str = param_dict_to_str(params)
             self.handle = ctypes.c_void_p()
-            _safe_call(_load_lib().LGBM_BoosterCreate(train_set.handle, c_str(params_str), ctypes.byref(self.handle)))
-            # save reference to data
+            nat.call("LGBM_BoosterCreate", train_set.handle, nat.cstr(nat.params_str(params)),
+                     ctypes.byref(self.handle))
             self.train_set = train_set
             self.valid_sets = []
             self.name_valid_sets = []
-            self.__num_dataset = 1
-            self.__init_predictor = train_set._predictor
-            if self.__init_predictor is not None:
-                _safe_call(_load_lib().LGBM_BoosterMerge(self.handle, self.__init_predictor.handle))
-            out_num_class = ctypes.c_int(0)
-            _safe_call(_load_lib().LGBM_BoosterGetNumClasses(self.handle, ctypes.byref(out_num_class)))
-            self.__num_class = out_num_class.value
-            # buffer for inner predict
-            self.__inner_predict_buffer = [None]
-            self.__is_predicted_cur_iter = [False]
-            self.__get_eval_info()
+            self._scores.add()
+            self._init_predictor = train_set._predictor
+            if self._init_predictor is not None:
+                nat.call("LGBM_BoosterMerge", self.handle, self._init_predictor.handle)
+            self._num_class = self._query_int("LGBM_BoosterGetNumClasses")
+            self._evals.load(self.handle)
             self.pandas_categorical = train_set.pandas_categorical
             self.train_set_version = train_set.version
         elif model_file is not None:
-            # Prediction task
-            out_num_iterations = ctypes.c_int(0)
+            iters = ctypes.c_int(0)
             self.handle = ctypes.c_void_p()
-            _safe_call(_load_lib().LGBM_BoosterCreateFromModelfile(c_str(model_file), ctypes.byref(out_num_iterations),
-                                                                   ctypes.byref(self.handle)))
-            out_num_class = ctypes.c_int(0)
-            _safe_call(_load_lib().LGBM_BoosterGetNumClasses(self.handle, ctypes.byref(out_num_class)))
-            self.__num_class = out_num_class.value
-            self.pandas_categorical = _load_pandas_categorical(file_name=model_file)
+            nat.call("LGBM_BoosterCreateFromModelfile", nat.cstr(model_file), ctypes.byref(iters),
+                     ctypes.byref(self.handle))
+            self._num_class = self._query_int("LGBM_BoosterGetNumClasses")
+            self.pandas_categorical = inp.categories_from_file(model_file)
         elif model_str is not None:
             self.model_from_string(model_str, not silent)
         else:
@@ -1368,627 +910,411 @@ class Booster(object):
         try:
             if self.network:
                 self.free_network()
-        except AttributeError:
+        except Exception:  # noqa: BLE001
             pass
         try:
             if self.handle is not None:
-                _safe_call(_load_lib().LGBM_BoosterFree(self.handle))
-        except AttributeError:
+                nat.call("LGBM_BoosterFree", self.handle)
+        except Exception:  # noqa: BLE001
             pass
 
     def __copy__(self):
         return self.__deepcopy__(None)
 
     def __deepcopy__(self, _):
-        model_str = self.model_to_string(num_iteration=-1)
-        booster = Booster(model_str=model_str)
-        return booster
+        return Booster(model_str=self.model_to_string(num_iteration=-1))
 
     def __getstate__(self):
-        this = self.__dict__.copy()
-        handle = this["handle"]
-        this.pop("train_set", None)
-        this.pop("valid_sets", None)
-        if handle is not None:
-            this["handle"] = self.model_to_string(num_iteration=-1)
-        return this
+        state = self.__dict__.copy()
+        state.pop("train_set", None)
+        state.pop("valid_sets", None)
+        if state.get("handle") is not None:
+            state["handle"] = self.model_to_string(num_iteration=-1)
+        return state
 
     def __setstate__(self, state):
-        model_str = state.get("handle", None)
-        if model_str is not None:
+        text = state.get("handle")
+        if text is not None:
             handle = ctypes.c_void_p()
-            out_num_iterations = ctypes.c_int(0)
-            _safe_call(_load_lib().LGBM_BoosterLoadModelFromString(c_str(model_str), ctypes.byref(out_num_iterations),
-                                                                   ctypes.byref(handle)))
+            nat.call("LGBM_BoosterLoadModelFromString", nat.cstr(text), ctypes.byref(ctypes.c_int(0)),
+                     ctypes.byref(handle))
             state["handle"] = handle
         self.__dict__.update(state)
 
+    def _query_int(self, fn):
+        out = ctypes.c_int(0)
+        nat.call(fn, self.handle, ctypes.byref(out))
+        return out.value
+
+    def _query_double(self, fn):
+        out = ctypes.c_double(0)
+        nat.call(fn, self.handle, ctypes.byref(out))
+        return out.value
+
+    def _num_datasets(self):
+        return len(self._scores.buffers)
+
+    # ------------------------------------------------------------------ data / network
     def free_dataset(self):
-        """Free Booster's Datasets."""
         self.__dict__.pop("train_set", None)
         self.__dict__.pop("valid_sets", None)
-        self.__num_dataset = 0
+        self._scores = _ScoreCache()
         return self
 
     def _free_buffer(self):
-        self.__inner_predict_buffer = []
-        self.__is_predicted_cur_iter = []
+        self._scores = _ScoreCache()
         return self
 
     def set_network(self, machines, local_listen_port=12400, listen_time_out=120, num_machines=1):
-        """Set the network configuration (TCP mesh)."""
-        _safe_call(_load_lib().LGBM_NetworkInit(c_str(machines), ctypes.c_int(local_listen_port),
-                                                ctypes.c_int(listen_time_out), ctypes.c_int(num_machines)))
+        """Join a TCP mesh of training machines."""
+        nat.call("LGBM_NetworkInit", nat.cstr(machines), nat.c_int(local_listen_port), nat.c_int(listen_time_out),
+                 nat.c_int(num_machines))
         self.network = True
         return self
 
     def free_network(self):
-        """Free Booster's network."""
-        _safe_call(_load_lib().LGBM_NetworkFree())
+        nat.call("LGBM_NetworkFree")
         self.network = False
         return self
 
-    def trees_to_dataframe(self):
-        """Parse the fitted model and return in an easy-to-read pandas DataFrame."""
-        if not PANDAS_INSTALLED:
-            raise LightGBMError("This method cannot be run without pandas installed")
-        from pandas import DataFrame
-
-        if self.num_trees() == 0:
-            raise LightGBMError("There are no trees in this Booster and thus nothing to parse")
-
-        def _is_split_node(tree):
-            return "split_index" in tree.keys()
-
-        def create_node_record(tree, node_depth=1, tree_index=None, feature_names=None, parent_node=None):
-            def _get_node_index(tree, tree_index):
-                tree_num = str(tree_index) + "-" if tree_index is not None else ""
-                is_split = _is_split_node(tree)
-                node_type = "S" if is_split else "L"
-                # if a single node tree it won't have `leaf_index` so return 0
-                node_num = str(tree.get("split_index" if is_split else "leaf_index", 0))
-                return tree_num + node_type + node_num
-
-            def _get_split_feature(tree, feature_names):
-                if _is_split_node(tree):
-                    if feature_names is not None:
-                        feature_name = feature_names[tree["split_feature"]]
-                    else:
-                        feature_name = tree["split_feature"]
-                else:
-                    feature_name = None
-                return feature_name
-
-            def _is_single_node_tree(tree):
-                return set(tree.keys()) == {"leaf_value"}
-
-            node = OrderedDict()
-            node["tree_index"] = tree_index
-            node["node_depth"] = node_depth
-            node["node_index"] = _get_node_index(tree, tree_index)
-            node["left_child"] = None
-            node["right_child"] = None
-            node["parent_index"] = parent_node
-            node["split_feature"] = _get_split_feature(tree, feature_names)
-            node["split_gain"] = None
-            node["threshold"] = None
-            node["decision_type"] = None
-            node["missing_direction"] = None
-            node["missing_type"] = None
-            node["value"] = None
-            node["weight"] = None
-            node["count"] = None
-            if _is_split_node(tree):
-                node["left_child"] = _get_node_index(tree["left_child"], tree_index)
-                node["right_child"] = _get_node_index(tree["right_child"], tree_index)
-                node["split_gain"] = tree["split_gain"]
-                node["threshold"] = tree["threshold"]
-                node["decision_type"] = tree["decision_type"]
-                node["missing_direction"] = "left" if tree["default_left"] else "right"
-                node["missing_type"] = tree["missing_type"]
-                node["value"] = tree["internal_value"]
-                node["weight"] = tree["internal_weight"]
-                node["count"] = tree["internal_count"]
-            else:
-                node["value"] = tree["leaf_value"]
-                if not _is_single_node_tree(tree):
-                    node["weight"] = tree["leaf_weight"]
-                    node["count"] = tree["leaf_count"]
-            return node
-
-        def tree_dict_to_node_list(tree, node_depth=1, tree_index=None, feature_names=None, parent_node=None):
-            node = create_node_record(tree, node_depth=node_depth, tree_index=tree_index,
-                                      feature_names=feature_names, parent_node=parent_node)
-            res = [node]
-            if _is_split_node(tree):
-                # traverse the next level of the tree
-                children = ["left_child", "right_child"]
-                for child in children:
-                    subtree_list = tree_dict_to_node_list(tree[child], node_depth=node_depth + 1,
-                                                          tree_index=tree_index, feature_names=feature_names,
-                                                          parent_node=node["node_index"])
-                    # In tree format, "subtree_list" is a list of node records (dicts),
-                    # and we add node to the list.
-                    res.extend(subtree_list)
-            return res
-
-        model_dict = self.dump_model()
-        feature_names = model_dict["feature_names"]
-        model_list = []
-        for tree in model_dict["tree_info"]:
-            model_list.extend(tree_dict_to_node_list(tree["tree_structure"], tree_index=tree["tree_index"],
-                                                     feature_names=feature_names))
-        return DataFrame(model_list, columns=model_list[0].keys())
-
     def set_train_data_name(self, name):
-        """Set the name to the training Dataset."""
         self._train_data_name = name
         return self
 
     def add_valid(self, data, name):
-        """Add validation data."""
         if not isinstance(data, Dataset):
             raise TypeError("Validation data should be Dataset instance, met {}".format(type(data).__name__))
-        if data._predictor is not self.__init_predictor:
+        if data._predictor is not self._init_predictor:
             raise LightGBMError("Add validation data failed, you should use same predictor for these data")
-        _safe_call(_load_lib().LGBM_BoosterAddValidData(self.handle, data.construct().handle))
+        nat.call("LGBM_BoosterAddValidData", self.handle, data.construct().handle)
         self.valid_sets.append(data)
         self.name_valid_sets.append(name)
-        self.__num_dataset += 1
-        self.__inner_predict_buffer.append(None)
-        self.__is_predicted_cur_iter.append(False)
+        self._scores.add()
         return self
 
     def reset_parameter(self, params):
-        """Reset parameters of Booster."""
-        params_str = param_dict_to_str(params)
-        if params_str:
-            _safe_call(_load_lib().LGBM_BoosterResetParameter(self.handle, c_str(params_str)))
+        text = nat.params_str(params)
+        if text:
+            nat.call("LGBM_BoosterResetParameter", self.handle, nat.cstr(text))
         self.params.update(params)
         return self
 
+    # ------------------------------------------------------------------ training
     def update(self, train_set=None, fobj=None):
-        """Update Booster for one iteration."""
-        # need reset training data
-        if train_set is None and self.train_set_version != self.train_set.version:
+        """One boosting iteration; True when training cannot continue."""
+        stale = self.train_set_version != self.train_set.version
+        if train_set is None and stale:
             train_set = self.train_set
-            is_the_same_train_set = False
-        else:
-            is_the_same_train_set = train_set is self.train_set and self.train_set_version == train_set.version
-        if train_set is not None and not is_the_same_train_set:
+        if train_set is not None and (train_set is not self.train_set or stale):
             if not isinstance(train_set, Dataset):
                 raise TypeError("Training data should be Dataset instance, met {}".format(type(train_set).__name__))
-            if train_set._predictor is not self.__init_predictor:
+            if train_set._predictor is not self._init_predictor:
                 raise LightGBMError("Replace training data failed, you should use same predictor for these data")
             self.train_set = train_set
-            _safe_call(_load_lib().LGBM_BoosterResetTrainingData(self.handle, self.train_set.construct().handle))
-            self.__inner_predict_buffer[0] = None
-            self.train_set_version = self.train_set.version
-        is_finished = ctypes.c_int(0)
+            nat.call("LGBM_BoosterResetTrainingData", self.handle, train_set.construct().handle)
+            self._scores.buffers[0] = None
+            self.train_set_version = train_set.version
         if fobj is None:
-            if self.__set_objective_to_none:
+            if self._objective_none:
                 raise LightGBMError("Cannot update due to null objective function.")
-            _safe_call(_load_lib().LGBM_BoosterUpdateOneIter(self.handle, ctypes.byref(is_finished)))
-            self.__is_predicted_cur_iter = [False for _ in range(self.__num_dataset)]
-            return is_finished.value == 1
-        if not self.__set_objective_to_none:
-            self.reset_parameter({"objective": "none"}).__set_objective_to_none = True
-        grad, hess = fobj(self.__inner_predict(0), self.train_set)
-        return self.__boost(grad, hess)
+            finished = ctypes.c_int(0)
+            nat.call("LGBM_BoosterUpdateOneIter", self.handle, ctypes.byref(finished))
+            self._scores.invalidate()
+            return finished.value == 1
+        if not self._objective_none:
+            self.reset_parameter({"objective": "none"})
+            self._objective_none = True
+        grad, hess = fobj(self._dataset_scores(0), self.train_set)
+        return self._boost_custom(grad, hess)
 
-    def __boost(self, grad, hess):
-        grad = list_to_1d_numpy(grad, name="gradient")
-        hess = list_to_1d_numpy(hess, name="hessian")
-        assert grad.flags.c_contiguous
-        assert hess.flags.c_contiguous
+    def _boost_custom(self, grad, hess):
+        grad = np.ascontiguousarray(inp.vector(grad, np.float32, "gradient"))
+        hess = np.ascontiguousarray(inp.vector(hess, np.float32, "hessian"))
         if len(grad) != len(hess):
             raise ValueError("Lengths of gradient({}) and hessian({}) don't match".format(len(grad), len(hess)))
-        is_finished = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterUpdateOneIterCustom(
-            self.handle, grad.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
-            hess.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(is_finished)))
-        self.__is_predicted_cur_iter = [False for _ in range(self.__num_dataset)]
-        return is_finished.value == 1
+        finished = ctypes.c_int(0)
+        nat.call("LGBM_BoosterUpdateOneIterCustom", self.handle, grad.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                 hess.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(finished))
+        self._scores.invalidate()
+        return finished.value == 1
 
     def rollback_one_iter(self):
-        """Rollback one iteration."""
-        _safe_call(_load_lib().LGBM_BoosterRollbackOneIter(self.handle))
-        self.__is_predicted_cur_iter = [False for _ in range(self.__num_dataset)]
+        nat.call("LGBM_BoosterRollbackOneIter", self.handle)
+        self._scores.invalidate()
         return self
 
     def current_iteration(self):
-        """Get the index of the current iteration."""
-        out_cur_iter = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterGetCurrentIteration(self.handle, ctypes.byref(out_cur_iter)))
-        return out_cur_iter.value
+        return self._query_int("LGBM_BoosterGetCurrentIteration")
 
     def num_model_per_iteration(self):
-        """Get number of models per iteration."""
-        model_per_iter = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterNumModelPerIteration(self.handle, ctypes.byref(model_per_iter)))
-        return model_per_iter.value
+        return self._query_int("LGBM_BoosterNumModelPerIteration")
 
     def num_trees(self):
-        """Get number of weak sub-models."""
-        num_trees = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterNumberOfTotalModel(self.handle, ctypes.byref(num_trees)))
-        return num_trees.value
+        return self._query_int("LGBM_BoosterNumberOfTotalModel")
 
     def upper_bound(self):
-        """Get upper bound value of a model."""
-        ret = ctypes.c_double(0)
-        _safe_call(_load_lib().LGBM_BoosterGetUpperBoundValue(self.handle, ctypes.byref(ret)))
-        return ret.value
+        return self._query_double("LGBM_BoosterGetUpperBoundValue")
 
     def lower_bound(self):
-        """Get lower bound value of a model."""
-        ret = ctypes.c_double(0)
-        _safe_call(_load_lib().LGBM_BoosterGetLowerBoundValue(self.handle, ctypes.byref(ret)))
-        return ret.value
+        return self._query_double("LGBM_BoosterGetLowerBoundValue")
+
+    # ------------------------------------------------------------------ evaluation
+    def _dataset_scores(self, idx):
+        ds = self.train_set if idx == 0 else self.valid_sets[idx - 1]
+        return self._scores.get(self.handle, idx, ds.num_data() * self._num_class)
+
+    def _evaluate(self, name, idx, feval):
+        if idx >= self._num_datasets():
+            raise ValueError("Data_idx should be smaller than number of dataset")
+        info = self._evals.load(self.handle)
+        out = []
+        if info.names:
+            vals = np.zeros(len(info.names), dtype=np.float64)
+            got = ctypes.c_int(0)
+            nat.call("LGBM_BoosterGetEval", self.handle, nat.c_int(idx), ctypes.byref(got),
+                     vals.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+            if got.value != len(info.names):
+                raise ValueError("Wrong length of eval results")
+            out += [(name, m, v, hb) for m, v, hb in zip(info.names, vals, info.higher_better)]
+        fns = [feval] if callable(feval) else (feval or [])
+        if fns:
+            data = self.train_set if idx == 0 else self.valid_sets[idx - 1]
+            for fn in fns:
+                if fn is None:
+                    continue
+                res = fn(self._dataset_scores(idx), data)
+                for metric, val, hb in (res if isinstance(res, list) else [res]):
+                    out.append((name, metric, val, hb))
+        return out
 
     def eval(self, data, name, feval=None):
-        """Evaluate for data."""
         if not isinstance(data, Dataset):
             raise TypeError("Can only eval for Dataset instance")
-        data_idx = -1
         if data is self.train_set:
-            data_idx = 0
+            idx = 0
         else:
-            for i in range(len(self.valid_sets)):
-                if data is self.valid_sets[i]:
-                    data_idx = i + 1
-                    break
-        # need to push new valid data
-        if data_idx == -1:
-            self.add_valid(data, name)
-            data_idx = self.__num_dataset - 1
-        return self.__inner_eval(name, data_idx, feval)
+            idx = next((i + 1 for i, v in enumerate(self.valid_sets) if v is data), -1)
+            if idx < 0:
+                self.add_valid(data, name)
+                idx = self._num_datasets() - 1
+        return self._evaluate(name, idx, feval)
 
     def eval_train(self, feval=None):
-        """Evaluate for training data."""
-        return self.__inner_eval(self._train_data_name, 0, feval)
+        return self._evaluate(self._train_data_name, 0, feval)
 
     def eval_valid(self, feval=None):
-        """Evaluate for validation data."""
-        return [item for i in range(1, self.__num_dataset)
-                for item in self.__inner_eval(self.name_valid_sets[i - 1], i, feval)]
+        return [r for i, nm in enumerate(self.name_valid_sets) for r in self._evaluate(nm, i + 1, feval)]
+
+    # ------------------------------------------------------------------ model IO
+    def _iterations(self, num_iteration):
+        return self.best_iteration if num_iteration is None else num_iteration
 
     def save_model(self, filename, num_iteration=None, start_iteration=0, importance_type="split"):
-        """Save Booster to file."""
-        if num_iteration is None:
-            num_iteration = self.best_iteration
-        importance_type_int = FEATURE_IMPORTANCE_TYPE_MAPPER[importance_type]
-        _safe_call(_load_lib().LGBM_BoosterSaveModel(self.handle, ctypes.c_int(start_iteration),
-                                                     ctypes.c_int(num_iteration), ctypes.c_int(importance_type_int),
-                                                     c_str(filename)))
-        _dump_pandas_categorical(self.pandas_categorical, filename)
+        nat.call("LGBM_BoosterSaveModel", self.handle, nat.c_int(start_iteration),
+                 nat.c_int(self._iterations(num_iteration)), nat.c_int(nat.IMPORTANCE_TYPES[importance_type]),
+                 nat.cstr(filename))
+        with open(filename, "a") as f:
+            f.write(inp.categories_line(self.pandas_categorical))
         return self
 
-    def shuffle_models(self, start_iteration=0, end_iteration=-1):
-        """Shuffle models."""
-        _safe_call(_load_lib().LGBM_BoosterShuffleModels(self.handle, ctypes.c_int(start_iteration),
-                                                         ctypes.c_int(end_iteration)))
-        return self
+    def model_to_string(self, num_iteration=None, start_iteration=0, importance_type="split"):
+        args = (self.handle, nat.c_int(start_iteration), nat.c_int(self._iterations(num_iteration)),
+                nat.c_int(nat.IMPORTANCE_TYPES[importance_type]))
+        text = nat.read_string(lambda size, need, buf: nat.call("LGBM_BoosterSaveModelToString", *args, size, need, buf))
+        return text + inp.categories_line(self.pandas_categorical)
+
+    def dump_model(self, num_iteration=None, start_iteration=0, importance_type="split"):
+        args = (self.handle, nat.c_int(start_iteration), nat.c_int(self._iterations(num_iteration)),
+                nat.c_int(nat.IMPORTANCE_TYPES[importance_type]))
+        out = json.loads(nat.read_string(lambda size, need, buf: nat.call("LGBM_BoosterDumpModel", *args, size, need,
+                                                                          buf)))
+        out["pandas_categorical"] = inp.categories_json(self.pandas_categorical)
+        return out
 
     def model_from_string(self, model_str, verbose=True):
-        """Load Booster from a string."""
         if self.handle is not None:
-            _safe_call(_load_lib().LGBM_BoosterFree(self.handle))
+            nat.call("LGBM_BoosterFree", self.handle)
         self._free_buffer()
         self.handle = ctypes.c_void_p()
-        out_num_iterations = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterLoadModelFromString(c_str(model_str), ctypes.byref(out_num_iterations),
-                                                               ctypes.byref(self.handle)))
-        out_num_class = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterGetNumClasses(self.handle, ctypes.byref(out_num_class)))
+        iters = ctypes.c_int(0)
+        nat.call("LGBM_BoosterLoadModelFromString", nat.cstr(model_str), ctypes.byref(iters), ctypes.byref(self.handle))
+        self._num_class = self._query_int("LGBM_BoosterGetNumClasses")
         if verbose:
-            print("Finished loading model, total used %d iterations" % int(out_num_iterations.value))
-        self.__num_class = out_num_class.value
-        self.pandas_categorical = _load_pandas_categorical(model_str=model_str)
+            print("Finished loading model, total used %d iterations" % iters.value)
+        self.pandas_categorical = inp.categories_from_text(model_str)
         return self
 
     def model_to_if_else(self, num_iteration=None):
-        """Standalone C++ source of the model (the CLI's convert_model task).
+        """Standalone C++ source of the model (the CLI's convert_model task): it defines
+        ``extern "C"`` ``lgbm_predict_raw(const double* row, double* out)`` and
+        ``lgbm_predict_leaf``, so rows can be scored without this library."""
+        fd, path = tempfile.mkstemp(prefix="lgbm_amd_ifelse_", suffix=".cpp")
+        os.close(fd)
+        try:
+            nat.call("LGBM_AMD_BoosterSaveModelToIfElse", self.handle, nat.c_int(self._iterations(num_iteration)),
+                     nat.cstr(path))
+            with open(path) as f:
+                return f.read()
+        finally:
+            os.remove(path)
 
-        The generated file defines ``extern "C"`` ``lgbm_predict_raw(const double* row,
-        double* out)`` and ``lgbm_predict_leaf``; compile it into any program to score rows
-        without this library.
-        """
-        if num_iteration is None:
-            num_iteration = self.best_iteration
-        with _TempFile() as f:
-            _safe_call(_load_lib().LGBM_AMD_BoosterSaveModelToIfElse(self.handle, ctypes.c_int(num_iteration),
-                                                                     c_str(f.name)))
-            return "".join(f.readlines())
+    def shuffle_models(self, start_iteration=0, end_iteration=-1):
+        nat.call("LGBM_BoosterShuffleModels", self.handle, nat.c_int(start_iteration), nat.c_int(end_iteration))
+        return self
 
-    def model_to_string(self, num_iteration=None, start_iteration=0, importance_type="split"):
-        """Save Booster to string."""
-        if num_iteration is None:
-            num_iteration = self.best_iteration
-        importance_type_int = FEATURE_IMPORTANCE_TYPE_MAPPER[importance_type]
-        buffer_len = 1 << 20
-        tmp_out_len = ctypes.c_int64(0)
-        string_buffer = ctypes.create_string_buffer(buffer_len)
-        ptr_string_buffer = ctypes.c_char_p(*[ctypes.addressof(string_buffer)])
-        _safe_call(_load_lib().LGBM_BoosterSaveModelToString(
-            self.handle, ctypes.c_int(start_iteration), ctypes.c_int(num_iteration), ctypes.c_int(importance_type_int),
-            ctypes.c_int64(buffer_len), ctypes.byref(tmp_out_len), ptr_string_buffer))
-        actual_len = tmp_out_len.value
-        # if buffer length is not long enough, re-allocate a buffer
-        if actual_len > buffer_len:
-            string_buffer = ctypes.create_string_buffer(actual_len)
-            ptr_string_buffer = ctypes.c_char_p(*[ctypes.addressof(string_buffer)])
-            _safe_call(_load_lib().LGBM_BoosterSaveModelToString(
-                self.handle, ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
-                ctypes.c_int(importance_type_int), ctypes.c_int64(actual_len), ctypes.byref(tmp_out_len),
-                ptr_string_buffer))
-        ret = string_buffer.value.decode("utf-8")
-        ret += _dump_pandas_categorical(self.pandas_categorical)
-        return ret
-
-    def dump_model(self, num_iteration=None, start_iteration=0, importance_type="split"):
-        """Dump Booster to JSON format."""
-        if num_iteration is None:
-            num_iteration = self.best_iteration
-        importance_type_int = FEATURE_IMPORTANCE_TYPE_MAPPER[importance_type]
-        buffer_len = 1 << 20
-        tmp_out_len = ctypes.c_int64(0)
-        string_buffer = ctypes.create_string_buffer(buffer_len)
-        ptr_string_buffer = ctypes.c_char_p(*[ctypes.addressof(string_buffer)])
-        _safe_call(_load_lib().LGBM_BoosterDumpModel(
-            self.handle, ctypes.c_int(start_iteration), ctypes.c_int(num_iteration), ctypes.c_int(importance_type_int),
-            ctypes.c_int64(buffer_len), ctypes.byref(tmp_out_len), ptr_string_buffer))
-        actual_len = tmp_out_len.value
-        if actual_len > buffer_len:
-            string_buffer = ctypes.create_string_buffer(actual_len)
-            ptr_string_buffer = ctypes.c_char_p(*[ctypes.addressof(string_buffer)])
-            _safe_call(_load_lib().LGBM_BoosterDumpModel(
-                self.handle, ctypes.c_int(start_iteration), ctypes.c_int(num_iteration),
-                ctypes.c_int(importance_type_int), ctypes.c_int64(actual_len), ctypes.byref(tmp_out_len),
-                ptr_string_buffer))
-        ret = json.loads(string_buffer.value.decode("utf-8"))
-        ret["pandas_categorical"] = json.loads(json.dumps(self.pandas_categorical, default=_json_default_with_numpy))
-        return ret
+    # ------------------------------------------------------------------ prediction
+    def _to_predictor(self, pred_parameter=None):
+        pred = _InnerPredictor(booster_handle=self.handle, pred_parameter=pred_parameter)
+        pred.pandas_categorical = self.pandas_categorical
+        return pred
 
     def predict(self, data, start_iteration=0, num_iteration=None, raw_score=False, pred_leaf=False,
                 pred_contrib=False, data_has_header=False, is_reshape=True, **kwargs):
-        """Make a prediction."""
-        predictor = self._to_predictor(copy.deepcopy(kwargs))
+        """Predictions for raw data (numpy, pandas, scipy sparse, lists, torch tensors or a file)."""
         if num_iteration is None:
-            if start_iteration <= 0:
-                num_iteration = self.best_iteration
-            else:
-                num_iteration = -1
-        return predictor.predict(data, start_iteration, num_iteration, raw_score, pred_leaf, pred_contrib,
-                                 data_has_header, is_reshape)
+            num_iteration = self.best_iteration if start_iteration <= 0 else -1
+        return self._to_predictor(copy.deepcopy(kwargs)).predict(
+            data, start_iteration, num_iteration, raw_score, pred_leaf, pred_contrib, data_has_header, is_reshape)
 
     def refit(self, data, label, decay_rate=0.9, **kwargs):
-        """Refit the existing Booster by new data."""
-        if self.__set_objective_to_none:
+        """A copy of the model with leaf values refitted on new data."""
+        if self._objective_none:
             raise LightGBMError("Cannot refit due to null objective function.")
-        predictor = self._to_predictor(copy.deepcopy(kwargs))
-        leaf_preds = predictor.predict(data, -1, pred_leaf=True)
-        nrow, ncol = leaf_preds.shape
-        out_is_linear = False  # noqa: F841  (linear trees are not part of this model version)
-        train_set = Dataset(data, label, silent=True)
-        new_params = copy.deepcopy(self.params)
-        new_params["refit_decay_rate"] = decay_rate
-        new_booster = Booster(new_params, train_set)
-        # Copy models
-        _safe_call(_load_lib().LGBM_BoosterMerge(new_booster.handle, predictor.handle))
-        leaf_preds = leaf_preds.reshape(-1)
-        ptr_data, _, _ = c_int_array(leaf_preds)
-        _safe_call(_load_lib().LGBM_BoosterRefit(new_booster.handle, ptr_data, ctypes.c_int32(nrow),
-                                                 ctypes.c_int32(ncol)))
-        new_booster.network = self.network
-        new_booster.__attr = self.__attr.copy()
-        return new_booster
+        pred = self._to_predictor(copy.deepcopy(kwargs))
+        leaves = pred.predict(data, -1, pred_leaf=True)
+        nrow, ncol = leaves.shape
+        params = copy.deepcopy(self.params)
+        params["refit_decay_rate"] = decay_rate
+        refitted = Booster(params, Dataset(data, label, silent=True))
+        nat.call("LGBM_BoosterMerge", refitted.handle, pred.handle)
+        flat = np.ascontiguousarray(leaves.reshape(-1), dtype=np.int32)
+        nat.call("LGBM_BoosterRefit", refitted.handle, flat.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                 ctypes.c_int32(nrow), ctypes.c_int32(ncol))
+        refitted.network = self.network
+        refitted._attrs = dict(self._attrs)
+        return refitted
 
     def get_leaf_output(self, tree_id, leaf_id):
-        """Get the output of a leaf."""
-        ret = ctypes.c_double(0)
-        _safe_call(_load_lib().LGBM_BoosterGetLeafValue(self.handle, ctypes.c_int(tree_id), ctypes.c_int(leaf_id),
-                                                        ctypes.byref(ret)))
-        return ret.value
+        out = ctypes.c_double(0)
+        nat.call("LGBM_BoosterGetLeafValue", self.handle, nat.c_int(tree_id), nat.c_int(leaf_id), ctypes.byref(out))
+        return out.value
 
-    def _to_predictor(self, pred_parameter=None):
-        predictor = _InnerPredictor(booster_handle=self.handle, pred_parameter=pred_parameter)
-        predictor.pandas_categorical = self.pandas_categorical
-        return predictor
-
+    # ------------------------------------------------------------------ introspection
     def num_feature(self):
-        """Get number of features."""
-        out_num_feature = ctypes.c_int(0)
-        _safe_call(_load_lib().LGBM_BoosterGetNumFeature(self.handle, ctypes.byref(out_num_feature)))
-        return out_num_feature.value
+        return self._query_int("LGBM_BoosterGetNumFeature")
 
     def feature_name(self):
-        """Get names of features."""
-        num_feature = self.num_feature()
-        tmp_out_len = ctypes.c_int(0)
-        reserved_string_buffer_size = 255
-        required_string_buffer_size = ctypes.c_size_t(0)
-        string_buffers = [ctypes.create_string_buffer(reserved_string_buffer_size) for _ in range(num_feature)]
-        ptr_string_buffers = (ctypes.c_char_p * num_feature)(*map(ctypes.addressof, string_buffers))
-        _safe_call(_load_lib().LGBM_BoosterGetFeatureNames(
-            self.handle, ctypes.c_int(num_feature), ctypes.byref(tmp_out_len),
-            ctypes.c_size_t(reserved_string_buffer_size), ctypes.byref(required_string_buffer_size),
-            ptr_string_buffers))
-        if num_feature != tmp_out_len.value:
-            raise ValueError("Length of feature names doesn't equal with num_feature")
-        if reserved_string_buffer_size < required_string_buffer_size.value:
-            actual = required_string_buffer_size.value
-            string_buffers = [ctypes.create_string_buffer(actual) for _ in range(num_feature)]
-            ptr_string_buffers = (ctypes.c_char_p * num_feature)(*map(ctypes.addressof, string_buffers))
-            _safe_call(_load_lib().LGBM_BoosterGetFeatureNames(
-                self.handle, ctypes.c_int(num_feature), ctypes.byref(tmp_out_len), ctypes.c_size_t(actual),
-                ctypes.byref(required_string_buffer_size), ptr_string_buffers))
-        return [string_buffers[i].value.decode("utf-8") for i in range(num_feature)]
+        return nat.read_names(lambda n, got, size, need, bufs: nat.call(
+            "LGBM_BoosterGetFeatureNames", self.handle, n, got, size, need, bufs), self.num_feature())
 
     def feature_importance(self, importance_type="split", iteration=None):
-        """Get feature importances."""
-        if iteration is None:
-            iteration = self.best_iteration
-        importance_type_int = FEATURE_IMPORTANCE_TYPE_MAPPER[importance_type]
-        result = np.zeros(self.num_feature(), dtype=np.float64)
-        _safe_call(_load_lib().LGBM_BoosterFeatureImportance(self.handle, ctypes.c_int(iteration),
-                                                             ctypes.c_int(importance_type_int),
-                                                             result.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
-        if importance_type_int == 0:
-            return result.astype(np.int32)
-        return result
+        kind = nat.IMPORTANCE_TYPES[importance_type]
+        out = np.zeros(self.num_feature(), dtype=np.float64)
+        nat.call("LGBM_BoosterFeatureImportance", self.handle, nat.c_int(self._iterations(iteration)),
+                 nat.c_int(kind), out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        return out.astype(np.int32) if kind == 0 else out
+
+    def _walk_trees(self):
+        """(tree index, node dict, depth, parent node id) over every node of the JSON dump."""
+        model = self.dump_model()
+        for info in model["tree_info"]:
+            stack = [(info["tree_structure"], 1, None)]
+            while stack:
+                node, depth, parent = stack.pop()
+                yield info["tree_index"], node, depth, parent, model.get("feature_names")
+                if "split_index" in node:
+                    me = "{}-S{}".format(info["tree_index"], node["split_index"])
+                    stack.append((node["right_child"], depth + 1, me))
+                    stack.append((node["left_child"], depth + 1, me))
 
     def get_split_value_histogram(self, feature, bins=None, xgboost_style=False):
-        """Get split value histogram for the specified feature."""
-        def add(root):
-            """Recursively add thresholds."""
-            if "split_index" in root:  # non-leaf
-                if feature_names is not None and isinstance(feature, string_type):
-                    split_feature = feature_names[root["split_feature"]]
-                else:
-                    split_feature = root["split_feature"]
-                if split_feature == feature:
-                    if isinstance(root["threshold"], string_type):
-                        raise LightGBMError("Cannot compute split value histogram for the categorical feature")
-                    values.append(root["threshold"])
-                add(root["left_child"])
-                add(root["right_child"])
-
-        model = self.dump_model()
-        feature_names = model.get("feature_names")
-        tree_infos = model["tree_info"]
+        """Histogram of the thresholds the model uses for one numerical feature."""
         values = []
-        for tree_info in tree_infos:
-            add(tree_info["tree_structure"])
-
-        if bins is None or isinstance(bins, integer_types) and xgboost_style:
+        for _, node, _, _, names in self._walk_trees():
+            if "split_index" not in node:
+                continue
+            f = node["split_feature"]
+            if names is not None and isinstance(feature, string_type):
+                f = names[f]
+            if f == feature:
+                if isinstance(node["threshold"], string_type):
+                    raise LightGBMError("Cannot compute split value histogram for the categorical feature")
+                values.append(node["threshold"])
+        if bins is None or (isinstance(bins, integer_types) and xgboost_style):
             n_unique = len(np.unique(values))
             bins = max(min(n_unique, bins) if bins is not None else n_unique, 1)
-        hist, bin_edges = np.histogram(values, bins=bins)
-        if xgboost_style:
-            ret = np.column_stack((bin_edges[1:], hist))
-            ret = ret[ret[:, 1] > 0]
-            if PANDAS_INSTALLED:
-                from pandas import DataFrame
-                return DataFrame(ret, columns=["SplitValue", "Count"])
-            return ret
-        return hist, bin_edges
+        hist, edges = np.histogram(values, bins=bins)
+        if not xgboost_style:
+            return hist, edges
+        table = np.column_stack((edges[1:], hist))
+        table = table[table[:, 1] > 0]
+        if PANDAS_INSTALLED:
+            from pandas import DataFrame
+            return DataFrame(table, columns=["SplitValue", "Count"])
+        return table
 
-    def __inner_eval(self, data_name, data_idx, feval=None):
-        if data_idx >= self.__num_dataset:
-            raise ValueError("Data_idx should be smaller than number of dataset")
-        self.__get_eval_info()
-        ret = []
-        if self.__num_inner_eval > 0:
-            result = np.zeros(self.__num_inner_eval, dtype=np.float64)
-            tmp_out_len = ctypes.c_int(0)
-            _safe_call(_load_lib().LGBM_BoosterGetEval(self.handle, ctypes.c_int(data_idx), ctypes.byref(tmp_out_len),
-                                                       result.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
-            if tmp_out_len.value != self.__num_inner_eval:
-                raise ValueError("Wrong length of eval results")
-            for i in range(self.__num_inner_eval):
-                ret.append((data_name, self.__name_inner_eval[i], result[i], self.__higher_better_inner_eval[i]))
-        if callable(feval):
-            feval = [feval]
-        if feval is not None:
-            if data_idx == 0:
-                cur_data = self.train_set
-            else:
-                cur_data = self.valid_sets[data_idx - 1]
-            for eval_function in feval:
-                if eval_function is None:
-                    continue
-                feval_ret = eval_function(self.__inner_predict(data_idx), cur_data)
-                if isinstance(feval_ret, list):
-                    for eval_name, val, is_higher_better in feval_ret:
-                        ret.append((data_name, eval_name, val, is_higher_better))
-                else:
-                    eval_name, val, is_higher_better = feval_ret
-                    ret.append((data_name, eval_name, val, is_higher_better))
-        return ret
+    def trees_to_dataframe(self):
+        """One row per node of every tree (pandas DataFrame)."""
+        if not PANDAS_INSTALLED:
+            raise LightGBMError("This method cannot be run without pandas installed")
+        if self.num_trees() == 0:
+            raise LightGBMError("There are no trees in this Booster and thus nothing to parse")
+        from pandas import DataFrame
 
-    def __inner_predict(self, data_idx):
-        if data_idx >= self.__num_dataset:
-            raise ValueError("Data_idx should be smaller than number of dataset")
-        if self.__inner_predict_buffer[data_idx] is None:
-            if data_idx == 0:
-                n_preds = self.train_set.num_data() * self.__num_class
-            else:
-                n_preds = self.valid_sets[data_idx - 1].num_data() * self.__num_class
-            self.__inner_predict_buffer[data_idx] = np.zeros(n_preds, dtype=np.float64)
-        # avoid to predict many time in one iteration
-        if not self.__is_predicted_cur_iter[data_idx]:
-            tmp_out_len = ctypes.c_int64(0)
-            data_ptr = self.__inner_predict_buffer[data_idx].ctypes.data_as(ctypes.POINTER(ctypes.c_double))
-            _safe_call(_load_lib().LGBM_BoosterGetPredict(self.handle, ctypes.c_int(data_idx), ctypes.byref(tmp_out_len),
-                                                          data_ptr))
-            if tmp_out_len.value != len(self.__inner_predict_buffer[data_idx]):
-                raise ValueError("Wrong length of predict results for data %d" % (data_idx))
-            self.__is_predicted_cur_iter[data_idx] = True
-        return self.__inner_predict_buffer[data_idx]
+        def node_id(tree, node):
+            split = "split_index" in node
+            return "{}-{}{}".format(tree, "S" if split else "L", node.get("split_index" if split else "leaf_index", 0))
 
-    def __get_eval_info(self):
-        if self.__need_reload_eval_info:
-            self.__need_reload_eval_info = False
-            out_num_eval = ctypes.c_int(0)
-            # Get num of inner evals
-            _safe_call(_load_lib().LGBM_BoosterGetEvalCounts(self.handle, ctypes.byref(out_num_eval)))
-            self.__num_inner_eval = out_num_eval.value
-            if self.__num_inner_eval > 0:
-                # Get name of evals
-                tmp_out_len = ctypes.c_int(0)
-                reserved_string_buffer_size = 255
-                required_string_buffer_size = ctypes.c_size_t(0)
-                string_buffers = [ctypes.create_string_buffer(reserved_string_buffer_size)
-                                  for _ in range(self.__num_inner_eval)]
-                ptr_string_buffers = (ctypes.c_char_p * self.__num_inner_eval)(*map(ctypes.addressof, string_buffers))
-                _safe_call(_load_lib().LGBM_BoosterGetEvalNames(
-                    self.handle, ctypes.c_int(self.__num_inner_eval), ctypes.byref(tmp_out_len),
-                    ctypes.c_size_t(reserved_string_buffer_size), ctypes.byref(required_string_buffer_size),
-                    ptr_string_buffers))
-                if self.__num_inner_eval != tmp_out_len.value:
-                    raise ValueError("Length of eval names doesn't equal with num_evals")
-                self.__name_inner_eval = [string_buffers[i].value.decode("utf-8")
-                                          for i in range(self.__num_inner_eval)]
-                self.__higher_better_inner_eval = [name.startswith(("auc", "ndcg@", "map@", "average_precision"))
-                                                   for name in self.__name_inner_eval]
+        rows = []
+        for tree, node, depth, parent, names in self._walk_trees():
+            split = "split_index" in node
+            row = OrderedDict([
+                ("tree_index", tree), ("node_depth", depth), ("node_index", node_id(tree, node)),
+                ("left_child", node_id(tree, node["left_child"]) if split else None),
+                ("right_child", node_id(tree, node["right_child"]) if split else None),
+                ("parent_index", parent),
+                ("split_feature", (names[node["split_feature"]] if names is not None else node["split_feature"])
+                 if split else None),
+                ("split_gain", node.get("split_gain") if split else None),
+                ("threshold", node.get("threshold") if split else None),
+                ("decision_type", node.get("decision_type") if split else None),
+                ("missing_direction", ("left" if node["default_left"] else "right") if split else None),
+                ("missing_type", node.get("missing_type") if split else None),
+                ("value", node["internal_value"] if split else node["leaf_value"]),
+                ("weight", node["internal_weight"] if split else node.get("leaf_weight")),
+                ("count", node["internal_count"] if split else node.get("leaf_count")),
+            ])
+            rows.append(row)
+        return DataFrame(rows, columns=list(rows[0].keys()))
 
     def attr(self, key):
-        """Get attribute string from the Booster."""
-        return self.__attr.get(key, None)
+        return self._attrs.get(key)
 
     def set_attr(self, **kwargs):
-        """Set attributes to the Booster."""
         for key, value in kwargs.items():
-            if value is not None:
-                if not isinstance(value, string_type):
-                    raise ValueError("Only string values are accepted")
-                self.__attr[key] = value
+            if value is None:
+                self._attrs.pop(key, None)
+            elif not isinstance(value, string_type):
+                raise ValueError("Only string values are accepted")
             else:
-                self.__attr.pop(key, None)
+                self._attrs[key] = value
         return self
 
 
+# ------------------------------------------------------------------------ device helpers
 def get_timers():
     """Phase timers of the native library (enabled with LGBM_AMD_TIMETAG=1) as {name: seconds}."""
-    buf = ctypes.create_string_buffer(1 << 16)
-    out_len = ctypes.c_int64(0)
-    _safe_call(_load_lib().LGBM_AMD_GetTimers(ctypes.c_int64(1 << 16), ctypes.byref(out_len), buf))
-    ret = {}
-    for item in buf.value.decode("utf-8").split(";"):
-        if "=" in item:
-            k, v = item.split("=", 1)
-            ret[k] = float(v)
-    return ret
+    text = nat.read_string(lambda size, need, buf: nat.call("LGBM_AMD_GetTimers", size, need, buf), 1 << 16)
+    return {k: float(v) for k, v in (item.split("=", 1) for item in text.split(";") if "=" in item)}
 
 
 def device_count():
     """Number of HIP devices visible to the native library (0 without a GPU)."""
     n = ctypes.c_int(0)
-    _safe_call(_load_lib().LGBM_AMD_DeviceCount(ctypes.byref(n)))
+    nat.call("LGBM_AMD_DeviceCount", ctypes.byref(n))
     return n.value
 
 
 def device_synchronize():
     """Wait for all work queued on the current HIP device (no-op without a GPU)."""
-    _safe_call(_load_lib().LGBM_AMD_DeviceSynchronize())
+    nat.call("LGBM_AMD_DeviceSynchronize")

@@ -1,21 +1,22 @@
-"""Training callbacks (reference python-package/lightgbm/callback.py).
+"""Training callbacks (the callback contract of the LightGBM v3 Python API; reference
+python-package/lightgbm/callback.py).
 
-Callbacks receive a ``CallbackEnv`` after every boosting round; ``before_iteration``
-callbacks run before it.  ``early_stopping`` raises ``EarlyStopException`` which the
-training loops in engine.py catch.
+A callback is a callable taking a ``CallbackEnv`` with two attributes the training loops in
+engine.py read: ``order`` (callbacks run sorted by it) and ``before_iteration`` (run before
+the boosting round instead of after).  Here each callback is a small class; ``early_stopping``
+raises ``EarlyStopException`` which the loops catch to truncate the model.
 """
 import collections
 import warnings
-from operator import gt, lt
 
 from .basic import _ConfigAliases
 
 
 class EarlyStopException(Exception):
-    """Exception of early stopping."""
+    """Raised by early_stopping; carries the best iteration (0-based) and its evaluation list."""
 
     def __init__(self, best_iteration, best_score):
-        super(EarlyStopException, self).__init__()
+        super().__init__()
         self.best_iteration = best_iteration
         self.best_score = best_score
 
@@ -26,136 +27,162 @@ CallbackEnv = collections.namedtuple(
 
 
 def _format_eval_result(value, show_stdv=True):
-    """Format metric string."""
-    if len(value) == 4:
-        return "%s's %s: %g" % (value[0], value[1], value[2])
-    if len(value) == 5:
-        if show_stdv:
-            return "%s's %s: %g + %g" % (value[0], value[1], value[2], value[4])
-        return "%s's %s: %g" % (value[0], value[1], value[2])
-    raise ValueError("Wrong metric value")
+    """'<data>'s <metric>: <value>[ + <stdv>]' of one (data, metric, value, higher_better[, stdv]) tuple."""
+    if len(value) not in (4, 5):
+        raise ValueError("Wrong metric value")
+    text = "%s's %s: %g" % (value[0], value[1], value[2])
+    if len(value) == 5 and show_stdv:
+        text += " + %g" % value[4]
+    return text
+
+
+def _format_results(results, show_stdv=True):
+    return "\t".join(_format_eval_result(r, show_stdv) for r in results)
+
+
+class _Callback:
+    order = 0
+    before_iteration = False
+
+
+class _PrintEvaluation(_Callback):
+    order = 10
+
+    def __init__(self, period, show_stdv):
+        self.period = period
+        self.show_stdv = show_stdv
+
+    def __call__(self, env):
+        rnd = env.iteration + 1
+        if self.period > 0 and env.evaluation_result_list and rnd % self.period == 0:
+            print("[%d]\t%s" % (rnd, _format_results(env.evaluation_result_list, self.show_stdv)))
 
 
 def print_evaluation(period=1, show_stdv=True):
-    """Create a callback that prints the evaluation results every ``period`` rounds."""
-    def _callback(env):
-        if period > 0 and env.evaluation_result_list and (env.iteration + 1) % period == 0:
-            result = "\t".join([_format_eval_result(x, show_stdv) for x in env.evaluation_result_list])
-            print("[%d]\t%s" % (env.iteration + 1, result))
-    _callback.order = 10
-    return _callback
+    """Print the evaluation results every ``period`` rounds."""
+    return _PrintEvaluation(period, show_stdv)
+
+
+class _RecordEvaluation(_Callback):
+    order = 20
+
+    def __init__(self, store):
+        self.store = store
+
+    def __call__(self, env):
+        for data_name, metric, value in (r[:3] for r in env.evaluation_result_list):
+            self.store.setdefault(data_name, collections.OrderedDict()).setdefault(metric, []).append(value)
 
 
 def record_evaluation(eval_result):
-    """Create a callback that records the evaluation history into ``eval_result``."""
+    """Record the evaluation history into the dict ``eval_result``:
+    ``{data_name: {metric: [value per round]}}`` (cleared first)."""
     if not isinstance(eval_result, dict):
         raise TypeError("eval_result should be a dictionary")
     eval_result.clear()
+    return _RecordEvaluation(eval_result)
 
-    def _init(env):
-        for data_name, eval_name, _, _ in env.evaluation_result_list:
-            eval_result.setdefault(data_name, collections.OrderedDict())
-            eval_result[data_name].setdefault(eval_name, [])
 
-    def _callback(env):
-        if not eval_result:
-            _init(env)
-        for data_name, eval_name, result, _ in env.evaluation_result_list:
-            eval_result[data_name][eval_name].append(result)
-    _callback.order = 20
-    return _callback
+class _ResetParameter(_Callback):
+    order = 10
+    before_iteration = True
+
+    def __init__(self, schedules):
+        self.schedules = schedules
+
+    def __call__(self, env):
+        rnd = env.iteration - env.begin_iteration
+        changed = {}
+        for key, schedule in self.schedules.items():
+            if isinstance(schedule, list):
+                if len(schedule) != env.end_iteration - env.begin_iteration:
+                    raise ValueError("Length of list {} has to equal to 'num_boost_round'.".format(repr(key)))
+                value = schedule[rnd]
+            else:
+                value = schedule(rnd)
+            if value != env.params.get(key, None):
+                changed[key] = value
+        if changed:
+            env.model.reset_parameter(changed)
+            env.params.update(changed)
 
 
 def reset_parameter(**kwargs):
-    """Create a callback that resets parameters after the first iteration.
-
-    Each value is a list (one value per round) or a function ``f(current_round)``.
-    """
-    def _callback(env):
-        new_parameters = {}
-        for key, value in kwargs.items():
-            if isinstance(value, list):
-                if len(value) != env.end_iteration - env.begin_iteration:
-                    raise ValueError("Length of list {} has to equal to 'num_boost_round'.".format(repr(key)))
-                new_param = value[env.iteration - env.begin_iteration]
-            else:
-                new_param = value(env.iteration - env.begin_iteration)
-            if new_param != env.params.get(key, None):
-                new_parameters[key] = new_param
-        if new_parameters:
-            env.model.reset_parameter(new_parameters)
-            env.params.update(new_parameters)
-    _callback.before_iteration = True
-    _callback.order = 10
-    return _callback
+    """Reset parameters before every round: each value is a list (one entry per round) or a
+    function of the round index (counted from the first round of this training call)."""
+    return _ResetParameter(kwargs)
 
 
-def early_stopping(stopping_rounds, first_metric_only=False, verbose=True):
-    """Create a callback that stops training when no validation metric improves for ``stopping_rounds``."""
-    best_score = []
-    best_iter = []
-    best_score_list = []
-    cmp_op = []
-    enabled = [True]
-    first_metric = [""]
+class _MetricTracker:
+    """Best value so far of one (dataset, metric) entry of the evaluation list."""
 
-    def _init(env):
-        enabled[0] = not any(env.params.get(boost_alias, "") == "dart"
-                             for boost_alias in _ConfigAliases.get("boosting"))
-        if not enabled[0]:
+    def __init__(self, higher_better):
+        self.higher_better = higher_better
+        self.best = None
+        self.best_iter = 0
+        self.best_results = None
+
+    def offer(self, value, iteration, results):
+        if self.best is None or (value > self.best if self.higher_better else value < self.best):
+            self.best = value
+            self.best_iter = iteration
+            self.best_results = results
+
+
+class _EarlyStopping(_Callback):
+    order = 30
+
+    def __init__(self, stopping_rounds, first_metric_only, verbose):
+        self.stopping_rounds = stopping_rounds
+        self.first_metric_only = first_metric_only
+        self.verbose = verbose
+        self.trackers = None
+        self.enabled = True
+        self.first_metric = ""
+
+    def _start(self, env):
+        self.trackers = []
+        self.enabled = not any(env.params.get(a, "") == "dart" for a in _ConfigAliases.get("boosting"))
+        if not self.enabled:
             warnings.warn("Early stopping is not available in dart mode")
             return
         if not env.evaluation_result_list:
             raise ValueError("For early stopping, at least one dataset and eval metric is required for evaluation")
-        if verbose:
-            print("Training until validation scores don't improve for {} rounds".format(stopping_rounds))
-        # split is needed for "<dataset type> <metric>" case (e.g. "train l1")
-        first_metric[0] = env.evaluation_result_list[0][1].split(" ")[-1]
-        for eval_ret in env.evaluation_result_list:
-            best_iter.append(0)
-            best_score_list.append(None)
-            if eval_ret[3]:
-                best_score.append(float("-inf"))
-                cmp_op.append(gt)
-            else:
-                best_score.append(float("inf"))
-                cmp_op.append(lt)
+        if self.verbose:
+            print("Training until validation scores don't improve for {} rounds".format(self.stopping_rounds))
+        # cv reports "<dataset> <metric>" names: the metric is the last word
+        self.first_metric = env.evaluation_result_list[0][1].split(" ")[-1]
+        self.trackers = [_MetricTracker(r[3]) for r in env.evaluation_result_list]
 
-    def _final_iteration_check(env, eval_name_splitted, i):
-        if env.iteration == env.end_iteration - 1:
-            if verbose:
-                print("Did not meet early stopping. Best iteration is:\n[%d]\t%s" % (
-                    best_iter[i] + 1, "\t".join([_format_eval_result(x) for x in best_score_list[i]])))
-                if first_metric_only:
-                    print("Evaluated only: {}".format(eval_name_splitted[-1]))
-            raise EarlyStopException(best_iter[i], best_score_list[i])
+    def _stop(self, tracker, metric_words, headline):
+        if self.verbose:
+            print("%s\n[%d]\t%s" % (headline, tracker.best_iter + 1, _format_results(tracker.best_results)))
+            if self.first_metric_only:
+                print("Evaluated only: {}".format(metric_words[-1]))
+        raise EarlyStopException(tracker.best_iter, tracker.best_results)
 
-    def _callback(env):
-        if not cmp_op:
-            _init(env)
-        if not enabled[0]:
+    def __call__(self, env):
+        if self.trackers is None:
+            self._start(env)
+        if not self.enabled:
             return
-        for i in range(len(env.evaluation_result_list)):
-            score = env.evaluation_result_list[i][2]
-            if best_score_list[i] is None or cmp_op[i](score, best_score[i]):
-                best_score[i] = score
-                best_iter[i] = env.iteration
-                best_score_list[i] = env.evaluation_result_list
-            # split is needed for "<dataset type> <metric>" case (e.g. "train l1")
-            eval_name_splitted = env.evaluation_result_list[i][1].split(" ")
-            if first_metric_only and first_metric[0] != eval_name_splitted[-1]:
-                continue  # use only the first metric for early stopping
-            if ((env.evaluation_result_list[i][0] == "cv_agg" and eval_name_splitted[0] == "train"
-                 or env.evaluation_result_list[i][0] == env.model._train_data_name)):
-                _final_iteration_check(env, eval_name_splitted, i)
-                continue  # train data for lgb.cv or sklearn wrapper (underlying lgb.train)
-            if env.iteration - best_iter[i] >= stopping_rounds:
-                if verbose:
-                    print("Early stopping, best iteration is:\n[%d]\t%s" % (
-                        best_iter[i] + 1, "\t".join([_format_eval_result(x) for x in best_score_list[i]])))
-                    if first_metric_only:
-                        print("Evaluated only: {}".format(eval_name_splitted[-1]))
-                raise EarlyStopException(best_iter[i], best_score_list[i])
-            _final_iteration_check(env, eval_name_splitted, i)
-    _callback.order = 30
-    return _callback
+        last_round = env.iteration == env.end_iteration - 1
+        results = env.evaluation_result_list
+        for tracker, (data_name, metric, value) in zip(self.trackers, (r[:3] for r in results)):
+            tracker.offer(value, env.iteration, results)
+            words = metric.split(" ")
+            if self.first_metric_only and words[-1] != self.first_metric:
+                continue
+            # training-set entries (lgb.cv's "train ..." aggregates, the booster's own training
+            # data) never trigger a stop; they only report at the last round
+            on_train = (data_name == "cv_agg" and words[0] == "train") or data_name == env.model._train_data_name
+            if not on_train and env.iteration - tracker.best_iter >= self.stopping_rounds:
+                self._stop(tracker, words, "Early stopping, best iteration is:")
+            if last_round:
+                self._stop(tracker, words, "Did not meet early stopping. Best iteration is:")
+
+
+def early_stopping(stopping_rounds, first_metric_only=False, verbose=True):
+    """Stop training when no validation metric improved for ``stopping_rounds`` rounds (all
+    metrics, or only the first with ``first_metric_only``); disabled for dart."""
+    return _EarlyStopping(stopping_rounds, first_metric_only, verbose)

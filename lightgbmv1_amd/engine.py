@@ -59,7 +59,8 @@ def _user_callbacks(callbacks):
     if callbacks is None:
         return set()
     for pos, cb in enumerate(callbacks):
-        cb.__dict__.setdefault("order", pos - len(callbacks))
+        if not hasattr(cb, "order"):
+            cb.order = pos - len(callbacks)
     return set(callbacks)
 
 

@@ -18,7 +18,8 @@ import ctypes
 
 import numpy as np
 
-from ..basic import LightGBMError, _load_lib, param_dict_to_str
+from .._native import LightGBMError, params_str as param_dict_to_str
+from ..basic import _load_lib
 
 __all__ = ["gradients", "metric", "sample_rows"]
 
