@@ -218,6 +218,18 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkCreateThreadHub(int num_ranks, double time
                                                       int fail_at_call, void** out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkJoinThreadHub(void* hub, int rank);
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkFreeThreadHub(void* hub);
+// for external collective functions (LGBM_NetworkInitWithFunctions) that fail: makes the
+// collective that called them raise on this thread instead of using an unfilled buffer
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkReportExternalError(const char* msg);
+// raw host collectives of the calling thread's network (the mesh training uses): allgather of
+// block_len[r] bytes from every rank r; reduce-scatter / all-reduce sums of doubles
+// (block_count[r] items of the input go to rank r)
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkRank(int* out);
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkNumMachines(int* out);
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkAllgather(const void* input, const int64_t* block_len, void* output);
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkReduceScatterSumF64(const double* input, const int64_t* block_count,
+                                                          double* output);
+LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkAllreduceSumF64(const double* input, int64_t count, double* output);
 // in-process device communicators (thread ranks sharing one GPU)
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, void** out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommJoinThreadHub(void* hub, int rank);

@@ -43,6 +43,13 @@ class HostTransport {
   // variable-size allgather: every rank contributes block_len[rank] bytes
   virtual void Allgather(const char* input, comm_size_t input_size, const comm_size_t* block_start,
                          const comm_size_t* block_len, char* output, comm_size_t output_size) = 0;
+  // optional point-to-point exchange: send `send_len` bytes to rank `to` while receiving
+  // `recv_len` bytes from rank `from` (either length may be 0).  When available, Network runs
+  // its own collective algorithms over it (src/network/collectives.cpp).
+  virtual bool HasPointToPoint() const { return false; }
+  virtual void SendRecv(int to, const char* send, comm_size_t send_len, int from, char* recv, comm_size_t recv_len) {
+    (void)to; (void)send; (void)send_len; (void)from; (void)recv; (void)recv_len;
+  }
   // optional native reduce-scatter; default implemented with Allgather + local reduce
   virtual bool ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
                              const comm_size_t* block_len, char* output, comm_size_t output_size,
@@ -86,6 +93,9 @@ class Network {
   static void InitWithTransport(std::shared_ptr<HostTransport> t);
   static void InitWithFunctions(int num_machines, int rank, ReduceScatterFunctionPtr rs, AllgatherFunctionPtr ag);
   static void Dispose();
+  // called from inside an external collective function that failed: the collective raises
+  // on this thread once the function returns
+  static void ReportExternalError(const std::string& msg);
   static int rank();
   static int num_machines();
   static bool IsDistributed() { return num_machines() > 1; }

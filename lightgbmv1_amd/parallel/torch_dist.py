@@ -30,6 +30,15 @@ def _make_allgather(dist, group):
     import torch
 
     def allgather(input_ptr, input_size, block_start, block_len, num_block, output_ptr, output_size):
+        # an exception must not escape a ctypes callback (ctypes would print it and return,
+        # leaving the native caller with an unfilled buffer): report it, the caller raises
+        try:
+            _allgather(input_ptr, input_size, block_start, block_len, num_block, output_ptr)
+        except BaseException as e:  # noqa: BLE001
+            _load_lib().LGBM_AMD_NetworkReportExternalError(
+                ("%s: %s" % (type(e).__name__, e)).encode("utf-8", "replace"))
+
+    def _allgather(input_ptr, input_size, block_start, block_len, num_block, output_ptr):
         lens = [block_len[i] for i in range(num_block)]
         starts = [block_start[i] for i in range(num_block)]
         max_len = max(lens) if lens else 0
@@ -115,6 +124,10 @@ def shutdown():
     try:
         import torch.distributed as dist
         if dist.is_initialized():
+            # every rank is done with the group before any destroys it: rank 0 hosts the
+            # rendezvous store, and a peer still using the group when the store goes away
+            # fails inside c10d's own threads (a process abort, not a Python error)
+            dist.barrier()
             dist.destroy_process_group()
     except Exception:  # pragma: no cover
         pass

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <limits>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -1295,6 +1296,75 @@ int LGBM_NetworkInitWithFunctions(int num_machines, int rank, void* reduce_scatt
     Network::InitWithFunctions(num_machines, rank, reinterpret_cast<ReduceScatterFunctionPtr>(reduce_scatter_ext_fun),
                                reinterpret_cast<AllgatherFunctionPtr>(allgather_ext_fun));
   }
+  API_END();
+}
+
+int LGBM_AMD_NetworkReportExternalError(const char* msg) {
+  API_BEGIN();
+  Network::ReportExternalError(msg ? msg : "");
+  API_END();
+}
+
+int LGBM_AMD_NetworkRank(int* out) {
+  API_BEGIN();
+  *out = Network::rank();
+  API_END();
+}
+
+int LGBM_AMD_NetworkNumMachines(int* out) {
+  API_BEGIN();
+  *out = Network::num_machines();
+  API_END();
+}
+
+int LGBM_AMD_NetworkAllgather(const void* input, const int64_t* block_len, void* output) {
+  API_BEGIN();
+  const int n = Network::num_machines();
+  std::vector<comm_size_t> start(n), len(n);
+  int64_t at = 0;
+  for (int i = 0; i < n; ++i) {
+    start[i] = static_cast<comm_size_t>(at);
+    len[i] = static_cast<comm_size_t>(block_len[i]);
+    at += block_len[i];
+  }
+  if (at > std::numeric_limits<comm_size_t>::max()) Log::Fatal("allgather of %lld bytes is too large", static_cast<long long>(at));
+  Network::Allgather(static_cast<char*>(const_cast<void*>(input)), start.data(), len.data(), static_cast<char*>(output),
+                     static_cast<comm_size_t>(at));
+  API_END();
+}
+
+namespace {
+void SumF64(const char* src, char* dst, int type_size, comm_size_t len) {
+  (void)type_size;
+  const double* s = reinterpret_cast<const double*>(src);
+  double* d = reinterpret_cast<double*>(dst);
+  for (comm_size_t i = 0; i < len / static_cast<comm_size_t>(sizeof(double)); ++i) d[i] += s[i];
+}
+}  // namespace
+
+int LGBM_AMD_NetworkReduceScatterSumF64(const double* input, const int64_t* block_count, double* output) {
+  API_BEGIN();
+  const int n = Network::num_machines();
+  std::vector<comm_size_t> start(n), len(n);
+  int64_t at = 0;
+  for (int i = 0; i < n; ++i) {
+    start[i] = static_cast<comm_size_t>(at);
+    len[i] = static_cast<comm_size_t>(block_count[i] * sizeof(double));
+    at += block_count[i] * static_cast<int64_t>(sizeof(double));
+  }
+  if (at > std::numeric_limits<comm_size_t>::max()) Log::Fatal("reduce-scatter of %lld bytes is too large", static_cast<long long>(at));
+  Network::ReduceScatter(reinterpret_cast<char*>(const_cast<double*>(input)), static_cast<comm_size_t>(at),
+                         sizeof(double), start.data(), len.data(), reinterpret_cast<char*>(output),
+                         len[Network::rank()], SumF64);
+  API_END();
+}
+
+int LGBM_AMD_NetworkAllreduceSumF64(const double* input, int64_t count, double* output) {
+  API_BEGIN();
+  const int64_t bytes = count * static_cast<int64_t>(sizeof(double));
+  if (bytes > std::numeric_limits<comm_size_t>::max()) Log::Fatal("all-reduce of %lld bytes is too large", static_cast<long long>(bytes));
+  Network::Allreduce(reinterpret_cast<char*>(const_cast<double*>(input)), static_cast<comm_size_t>(bytes),
+                     sizeof(double), reinterpret_cast<char*>(output), SumF64);
   API_END();
 }
 

@@ -5,10 +5,12 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <mutex>
 #include <stdexcept>
 #include <string>
 
+#include "collectives.h"
 #include "lgbm_amd/common.h"
 #include "lgbm_amd/log.h"
 
@@ -28,6 +30,21 @@ NetState& State() {
   return s;
 }
 
+// an error the external collective functions reported through
+// LGBM_AMD_NetworkReportExternalError while they ran on this thread (their C signature
+// returns void, so a failing Python / MPI callback has no other way to stop the caller)
+std::string& ReportedError() {
+  static thread_local std::string msg;
+  return msg;
+}
+
+void RaiseReported() {
+  if (ReportedError().empty()) return;
+  const std::string why = ReportedError();
+  ReportedError().clear();
+  Log::Fatal("external collective failed: %s", why.c_str());
+}
+
 // adapter for the reference's external function pair
 class ExternalFnTransport : public HostTransport {
  public:
@@ -38,6 +55,7 @@ class ExternalFnTransport : public HostTransport {
   void Allgather(const char* input, comm_size_t input_size, const comm_size_t* block_start,
                  const comm_size_t* block_len, char* output, comm_size_t output_size) override {
     ag_(const_cast<char*>(input), input_size, block_start, block_len, n_, output, output_size);
+    RaiseReported();
   }
   bool ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
                      const comm_size_t* block_len, char* output, comm_size_t output_size,
@@ -49,6 +67,7 @@ class ExternalFnTransport : public HostTransport {
     ReduceFunctionPtr tramp = [](const char* in, char* out, int ts, comm_size_t len) { (*active)(in, out, ts, len); };
     rs_(input, input_size, type_size, block_start, block_len, n_, output, output_size, tramp);
     active = nullptr;
+    RaiseReported();
     return true;
   }
 
@@ -63,7 +82,7 @@ class ExternalFnTransport : public HostTransport {
 // rank that never arrives is detected by the per-collective timeout.  This is the
 // in-process fake backend of SURVEY.md §5.3 (the reference only has socket timeouts).
 struct ThreadHub {
-  ThreadHub(int n, double timeout_s) : n(n), timeout_s(timeout_s), bufs(n), lens(n) {}
+  ThreadHub(int n, double timeout_s) : n(n), timeout_s(timeout_s), bufs(n), lens(n), mail(n * n) {}
   int n;
   double timeout_s;
   std::mutex mu;
@@ -75,6 +94,8 @@ struct ThreadHub {
   std::string failure;
   std::vector<const char*> bufs;
   std::vector<comm_size_t> lens;
+  // point-to-point mailboxes: mail[src * n + dst] holds the messages src sent to dst, in order
+  std::vector<std::deque<std::vector<char>>> mail;
 };
 
 class ThreadTransport : public HostTransport {
@@ -83,14 +104,31 @@ class ThreadTransport : public HostTransport {
       : hub_(std::move(hub)), rank_(rank), fail_at_call_(fail_at_call) {}
   int rank() const override { return rank_; }
   int num_machines() const override { return hub_->n; }
+  bool HasPointToPoint() const override { return true; }
+  // eager buffered send into the (rank, to) mailbox, then wait for the (from, rank) one
+  void SendRecv(int to, const char* send, comm_size_t send_len, int from, char* recv,
+                comm_size_t recv_len) override {
+    std::unique_lock<std::mutex> lk(hub_->mu);
+    CountCall(&lk);
+    if (send_len > 0) {
+      hub_->mail[rank_ * hub_->n + to].emplace_back(send, send + send_len);
+      hub_->cv.notify_all();
+    }
+    if (recv_len > 0) {
+      auto& box = hub_->mail[from * hub_->n + rank_];
+      Wait(&lk, [&] { return !box.empty(); });
+      if (static_cast<comm_size_t>(box.front().size()) != recv_len) {
+        Poison(&lk, "message size mismatch from rank " + std::to_string(from) + " to rank " + std::to_string(rank_));
+      }
+      std::memcpy(recv, box.front().data(), recv_len);
+      box.pop_front();
+    }
+  }
   void Allgather(const char* input, comm_size_t input_size, const comm_size_t* block_start,
                  const comm_size_t* block_len, char* output, comm_size_t output_size) override {
     (void)output_size;
-    ++calls_;
     std::unique_lock<std::mutex> lk(hub_->mu);
-    if (fail_at_call_ > 0 && calls_ == fail_at_call_) {
-      Poison(&lk, "injected fault in rank " + std::to_string(rank_) + " at collective call " + std::to_string(calls_));
-    }
+    CountCall(&lk);
     // wait until the previous round's readers are done
     Wait(&lk, [&] { return hub_->readers_done == 0 || hub_->readers_done == hub_->n; });
     if (hub_->readers_done == hub_->n) hub_->readers_done = 0;
@@ -114,6 +152,12 @@ class ThreadTransport : public HostTransport {
   }
 
  private:
+  void CountCall(std::unique_lock<std::mutex>* lk) {
+    ++calls_;
+    if (fail_at_call_ > 0 && calls_ == fail_at_call_) {
+      Poison(lk, "injected fault in rank " + std::to_string(rank_) + " at collective call " + std::to_string(calls_));
+    }
+  }
   [[noreturn]] void Poison(std::unique_lock<std::mutex>* lk, const std::string& why) {
     if (!hub_->failed) {
       hub_->failed = true;
@@ -149,6 +193,17 @@ class ThreadTransport : public HostTransport {
   int calls_ = 0;
 };
 
+// collective algorithm choice (bytes)
+constexpr comm_size_t kRingAllgatherBytes = 8 << 20;  // Bruck below (log2 n rounds), ring above
+constexpr comm_size_t kAllreduceSplitBytes = 4096;    // allgather + local reduce below
+
+bool RankOrdered(int n, const comm_size_t* block_start, const comm_size_t* block_len) {
+  for (int i = 1; i < n; ++i) {
+    if (block_start[i] != block_start[i - 1] + block_len[i - 1]) return false;
+  }
+  return true;
+}
+
 }  // namespace
 
 std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks, double timeout_s, int fail_rank,
@@ -178,6 +233,8 @@ void Network::InitWithFunctions(int num_machines, int rank, ReduceScatterFunctio
   State().transport = std::make_shared<ExternalFnTransport>(num_machines, rank, rs, ag);
 }
 
+void Network::ReportExternalError(const std::string& msg) { ReportedError() = msg.empty() ? "unknown error" : msg; }
+
 void Network::Dispose() {
   State().transport.reset();
   State().device.reset();
@@ -206,7 +263,14 @@ void Network::Allgather(char* input, const comm_size_t* block_start, const comm_
     std::memcpy(output, input, block_len[0]);
     return;
   }
-  State().transport->Allgather(input, block_len[rank()], block_start, block_len, output, all_size);
+  HostTransport* t = State().transport.get();
+  if (!t->HasPointToPoint()) {
+    t->Allgather(input, block_len[rank()], block_start, block_len, output, all_size);
+  } else if (all_size <= kRingAllgatherBytes) {
+    collectives::BruckAllgather(t, input, block_start, block_len, output);
+  } else {
+    collectives::RingAllgather(t, input, block_start, block_len, output);
+  }
 }
 
 void Network::ReduceScatter(char* input, comm_size_t input_size, int type_size, const comm_size_t* block_start,
@@ -218,8 +282,17 @@ void Network::ReduceScatter(char* input, comm_size_t input_size, int type_size, 
     std::memcpy(output, input, input_size);
     return;
   }
-  if (State().transport->ReduceScatter(input, input_size, type_size, block_start, block_len, output, output_size,
-                                       reducer)) {
+  HostTransport* t = State().transport.get();
+  if (t->HasPointToPoint() && RankOrdered(n, block_start, block_len)) {
+    if ((n & (n - 1)) == 0) {
+      collectives::RecursiveHalvingReduceScatter(t, input, input_size, type_size, block_start, block_len, output,
+                                                 reducer);
+    } else {
+      collectives::RingReduceScatter(t, input, input_size, type_size, block_start, block_len, output, reducer);
+    }
+    return;
+  }
+  if (t->ReduceScatter(input, input_size, type_size, block_start, block_len, output, output_size, reducer)) {
     return;
   }
   // allgather every rank's full input, reduce own block locally
@@ -241,7 +314,21 @@ void Network::Allreduce(char* input, comm_size_t input_size, int type_size, char
     if (output != input) std::memcpy(output, input, input_size);
     return;
   }
-  // allgather + fixed-order local reduce: every rank gets bitwise identical results
+  const comm_size_t items = input_size / type_size;
+  if (State().transport->HasPointToPoint() && input_size >= kAllreduceSplitBytes && items >= n) {
+    // reduce-scatter over n item-aligned blocks, then allgather them: each block is reduced
+    // by exactly one rank, so every rank still ends with bitwise identical results
+    std::vector<comm_size_t> st(n), ln(n);
+    for (int i = 0; i < n; ++i) {
+      st[i] = static_cast<comm_size_t>(items * i / n) * type_size;
+      ln[i] = static_cast<comm_size_t>(items * (i + 1) / n) * type_size - st[i];
+    }
+    std::vector<char> mine(static_cast<size_t>(ln[rank()]));
+    ReduceScatter(input, input_size, type_size, st.data(), ln.data(), mine.data(), ln[rank()], reducer);
+    Allgather(mine.data(), st.data(), ln.data(), output, input_size);
+    return;
+  }
+  // small payloads: allgather + fixed-order local reduce (bitwise identical on every rank)
   std::vector<comm_size_t> st(n), ln(n, input_size);
   for (int i = 0; i < n; ++i) st[i] = i * input_size;
   std::vector<char> all(static_cast<size_t>(input_size) * n);

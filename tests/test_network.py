@@ -1,0 +1,106 @@
+"""Host collective algorithms and the TCP mesh transport (reference: src/network/network.cpp
+Bruck allgather / recursive-halving reduce-scatter; linkers_socket.cpp machine list +
+rank discovery).  In-process thread ranks exercise every algorithm branch (power-of-two
+and other world sizes, empty blocks, small and large all-reduce); separate processes on
+127.0.0.1 exercise the socket transport, a data-parallel training run over it, and a peer
+that dies mid-run (the survivors must raise, not hang or abort)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import lightgbmv1_amd as lgb  # noqa: F401
+from lightgbmv1_amd.parallel import host
+from lightgbmv1_amd.parallel.inproc import ThreadRanks
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "helpers"))
+import net_worker  # noqa: E402
+
+WORKER = os.path.join(os.path.dirname(__file__), "helpers", "net_worker.py")
+
+
+def _expected(world):
+    vec = net_worker.rank_vector
+    gathered = [vec(r, 0 if r == 1 and world > 2 else r * 3 + 1).tolist() for r in range(world)]
+    counts = [(i * 7) % 5 + 2 for i in range(world)]
+    total = sum(vec(r, sum(counts)) for r in range(world))
+    bounds = np.concatenate([[0], np.cumsum(counts)])
+    rs = [total[bounds[r]:bounds[r + 1]].tolist() for r in range(world)]
+    ar = {"allreduce_%d" % n: float(sum(vec(r, n, salt=1) for r in range(world)).sum()) for n in (5, 100000)}
+    return gathered, rs, ar
+
+
+def _check(world, results):
+    gathered, rs, ar = _expected(world)
+    for r, res in enumerate(results):
+        assert res["allgather"] == gathered
+        assert res["reduce_scatter"] == rs[r]
+        for k, v in ar.items():
+            assert res[k] == v, (r, k)
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
+def test_thread_rank_collectives(world, tmp_path):
+    with ThreadRanks(world, timeout_s=60) as tr:
+        out = tr.run(lambda r: net_worker.collectives(r, world, str(tmp_path)) or host.world())
+    assert all(o.ok for o in out), [str(o.error) for o in out]
+    assert [o.value for o in out] == [(r, world) for r in range(world)]
+    _check(world, [json.load(open(tmp_path / ("coll_%d.json" % r))) for r in range(world)])
+
+
+def _free_ports(n):
+    socks, ports = [], []
+    for _ in range(n):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        socks.append(s)
+        ports.append(s.getsockname()[1])
+    for s in socks:
+        s.close()
+    return ports
+
+
+def _spawn(modes, tmp_path, timeout=120):
+    ports = _free_ports(len(modes))
+    machines = ",".join("127.0.0.1:%d" % p for p in ports)
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    procs = [subprocess.Popen([sys.executable, WORKER, m, str(r), machines, str(tmp_path)], env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r, m in enumerate(modes)]
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out.decode("utf-8", "replace")))
+    return outs
+
+
+def test_tcp_mesh_collectives(tmp_path):
+    world = 3
+    outs = _spawn(["collectives"] * world, tmp_path)
+    assert all(rc == 0 for rc, _ in outs), outs
+    _check(world, [json.load(open(tmp_path / ("coll_%d.json" % r))) for r in range(world)])
+
+
+def test_tcp_mesh_data_parallel_training(tmp_path):
+    outs = _spawn(["train"] * 2, tmp_path)
+    assert all(rc == 0 for rc, _ in outs), outs
+    models = [open(tmp_path / ("model_%d.txt" % r)).read() for r in range(2)]
+    trees = [m[m.index("Tree=0"):m.index("end of trees")] for m in models]
+    assert trees[0] == trees[1]
+
+
+def test_tcp_peer_failure_raises_on_survivor(tmp_path):
+    """Rank 1 exits right after joining the mesh; rank 0's next collective must raise a
+    LightGBMError naming the lost peer (no hang, no process abort)."""
+    outs = _spawn(["survive", "die"], tmp_path, timeout=90)
+    assert outs[0][0] == 0, outs[0][1]
+    text = open(tmp_path / "survivor_0.txt").read()
+    assert text.startswith("error:") and "rank 1" in text, text
