@@ -7,6 +7,9 @@
 //   * external functions (C API; the Python package plugs torch.distributed in),
 //   * built-in TCP full mesh for `machines=` / `machine_list_filename` configs,
 //   * in-process "fake" ranks (threads) for tests.
+// Transports with a point-to-point SendRecv (TCP, threads) get Network's own algorithms:
+// Bruck / ring allgather, recursive-halving (power-of-two) / ring reduce-scatter, and
+// reduce-scatter + allgather all-reduce (src/network/collectives.cpp).
 // Device collectives (histogram all-reduce over xGMI) go through `DeviceComm`,
 // implemented with RCCL in src/network/rccl_comm.cpp.
 #pragma once
