@@ -143,6 +143,7 @@ class GBDT {
   const std::vector<std::string>& FeatureNames() const { return feature_names_; }
   const std::vector<std::string>& FeatureInfos() const { return feature_infos_; }
   const Tree* model(int i) const { return models_[i].get(); }
+  DeviceTreeLearner* device_learner() const { return device_learner_; }
   bool average_output() const { return average_output_; }
   const ObjectiveFunction* objective() const { return objective_; }
   std::string SubModelName() const { return "tree"; }

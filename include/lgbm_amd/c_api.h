@@ -218,6 +218,22 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkCreateThreadHub(int num_ranks, double time
                                                       int fail_at_call, void** out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkJoinThreadHub(void* hub, int rank);
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkFreeThreadHub(void* hub);
+// test support of the device learner (tests/test_gpu_kernels.py): group-bin matrix of a
+// dataset (row-major num_data x num_groups; boundaries: first histogram bin of each group,
+// num_groups + 1 entries); call with null buffers to get num_groups first
+LIGHTGBM_C_EXPORT int LGBM_AMD_DatasetGetGroupBins(DatasetHandle handle, int32_t* bins, int64_t* boundaries,
+                                                   int* num_groups);
+// the state the last device-grown tree left in HBM: a leaf's rows (count first with rows ==
+// null), its raw fixed-point histogram slot (2 * total_bins int64: g, h) and sums
+// (sum_g, sum_h, count); the rows' packed (g, h) and the fixed-point scales
+LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceLeafState(BoosterHandle handle, int leaf, int32_t* rows, int* count,
+                                                      int64_t* hist, int8_t* bin_valid, int64_t* hist_len,
+                                                      double* sums);
+LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceGradients(BoosterHandle handle, float* grad, float* hess,
+                                                      double* scales);
+// JSON report of the leaves' device best splits checked against the CPU split finder
+LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceCheckSplits(BoosterHandle handle, int64_t buffer_len, int64_t* out_len,
+                                                        char* out_str);
 // for external collective functions (LGBM_NetworkInitWithFunctions) that fail: makes the
 // collective that called them raise on this thread instead of using an unfilled buffer
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkReportExternalError(const char* msg);

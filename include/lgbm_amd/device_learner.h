@@ -5,6 +5,7 @@
 // It is a mix-in next to TreeLearner; GBDT discovers it with dynamic_cast.
 #pragma once
 
+#include <string>
 #include <vector>
 
 #include "lgbm_amd/metric.h"
@@ -61,6 +62,30 @@ class DeviceTreeLearner {
   virtual void ValidScoreToHost(int slot, double* host) = 0;
   // a metric on the device-resident scores of a validation set; false: evaluate on the host
   virtual bool ValidEval(int slot, const DeviceMetricSpec& spec, double* out) = 0;
+
+  // test support (tests/test_gpu_kernels.py): the state the last device-grown tree left in HBM.
+  // A leaf's rows (partition), its raw fixed-point histogram slot, which histogram bins are
+  // meaningful (the slices of features evaluated for the leaf: a feature its parent could not
+  // split on is never materialised again) and (sum_g, sum_h, count); false if the last tree
+  // was not grown device-resident.
+  // `tree` is that last tree: the children of its last split (and of splits whose children
+  // can not split further) never get histograms, their bin_valid is all 0.
+  virtual bool DebugLeafState(const Tree* tree, int leaf, std::vector<int32_t>* rows, std::vector<long long>* hist,
+                              std::vector<int8_t>* bin_valid, double* sums) {
+    (void)tree; (void)leaf; (void)rows; (void)hist; (void)bin_valid; (void)sums;
+    return false;
+  }
+  // the per-row (g, h) the histograms were built from and the fixed-point scales (g, h)
+  virtual bool DebugGradients(std::vector<float>* g, std::vector<float>* h, double* scales) {
+    (void)g; (void)h; (void)scales;
+    return false;
+  }
+  // differential check of every leaf's device best split against the CPU split finder run
+  // on the same (dequantised) histogram; a JSON report
+  virtual std::string DebugCheckSplits(const Tree* tree) {
+    (void)tree;
+    return "{}";
+  }
 };
 
 TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Config* config);

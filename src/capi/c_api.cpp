@@ -1299,6 +1299,74 @@ int LGBM_NetworkInitWithFunctions(int num_machines, int rank, void* reduce_scatt
   API_END();
 }
 
+int LGBM_AMD_DatasetGetGroupBins(DatasetHandle handle, int32_t* bins, int64_t* boundaries, int* num_groups) {
+  API_BEGIN();
+  const Dataset* d = static_cast<const Dataset*>(handle);
+  const int ng = d->num_groups();
+  *num_groups = ng;
+  if (boundaries != nullptr) {
+    for (int g = 0; g <= ng; ++g) {
+      boundaries[g] = static_cast<int64_t>(g < ng ? d->group_bin_boundary(g) : d->num_total_bin());
+    }
+  }
+  if (bins != nullptr) {
+    const data_size_t n = d->num_data();
+#pragma omp parallel for schedule(static)
+    for (data_size_t r = 0; r < n; ++r) {
+      for (int g = 0; g < ng; ++g) bins[static_cast<size_t>(r) * ng + g] = static_cast<int32_t>(d->group(g).Get(r));
+    }
+  }
+  API_END();
+}
+
+namespace {
+DeviceTreeLearner* DeviceLearnerOf(BoosterHandle handle) {
+  DeviceTreeLearner* dl = static_cast<Booster*>(handle)->boosting()->device_learner();
+  if (dl == nullptr) Log::Fatal("the booster does not train on a device (device_type=gpu)");
+  return dl;
+}
+}  // namespace
+
+int LGBM_AMD_BoosterDeviceLeafState(BoosterHandle handle, int leaf, int32_t* rows, int* count, int64_t* hist,
+                                    int8_t* bin_valid, int64_t* hist_len, double* sums) {
+  API_BEGIN();
+  std::vector<int32_t> r;
+  std::vector<long long> h;
+  std::vector<int8_t> valid;
+  double s[3];
+  GBDT* b = static_cast<Booster*>(handle)->boosting();
+  const int nm = b->NumberOfTotalModel();
+  if (!DeviceLearnerOf(handle)->DebugLeafState(nm > 0 ? b->model(nm - 1) : nullptr, leaf, &r, &h, &valid, s)) {
+    Log::Fatal("no device-resident tree state for leaf %d", leaf);
+  }
+  *count = static_cast<int>(r.size());
+  *hist_len = static_cast<int64_t>(h.size());
+  if (rows != nullptr) std::memcpy(rows, r.data(), sizeof(int32_t) * r.size());
+  if (hist != nullptr) std::memcpy(hist, h.data(), sizeof(long long) * h.size());
+  if (bin_valid != nullptr) std::memcpy(bin_valid, valid.data(), valid.size());
+  if (sums != nullptr) std::memcpy(sums, s, sizeof(s));
+  API_END();
+}
+
+int LGBM_AMD_BoosterDeviceGradients(BoosterHandle handle, float* grad, float* hess, double* scales) {
+  API_BEGIN();
+  std::vector<float> g, h;
+  if (!DeviceLearnerOf(handle)->DebugGradients(&g, &h, scales)) Log::Fatal("no device gradients");
+  std::memcpy(grad, g.data(), sizeof(float) * g.size());
+  std::memcpy(hess, h.data(), sizeof(float) * h.size());
+  API_END();
+}
+
+int LGBM_AMD_BoosterDeviceCheckSplits(BoosterHandle handle, int64_t buffer_len, int64_t* out_len, char* out_str) {
+  API_BEGIN();
+  GBDT* b = static_cast<Booster*>(handle)->boosting();
+  const int n = b->NumberOfTotalModel();
+  const std::string rep = DeviceLearnerOf(handle)->DebugCheckSplits(n > 0 ? b->model(n - 1) : nullptr);
+  *out_len = static_cast<int64_t>(rep.size()) + 1;
+  if (buffer_len >= *out_len) std::memcpy(out_str, rep.c_str(), rep.size() + 1);
+  API_END();
+}
+
 int LGBM_AMD_NetworkReportExternalError(const char* msg) {
   API_BEGIN();
   Network::ReportExternalError(msg ? msg : "");

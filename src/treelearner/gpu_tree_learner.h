@@ -72,6 +72,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void ValidAddTree(int slot, const Tree* tree, int tree_id) override;
   void ValidScoreToHost(int slot, double* host) override;
   bool ValidEval(int slot, const DeviceMetricSpec& spec, double* out) override;
+  bool DebugLeafState(const Tree* tree, int leaf, std::vector<int32_t>* rows, std::vector<long long>* hist,
+                      std::vector<int8_t>* bin_valid, double* sums) override;
+  bool DebugGradients(std::vector<float>* g, std::vector<float>* h, double* scales) override;
+  std::string DebugCheckSplits(const Tree* tree) override;  // gpu_self_check.cpp
 
   bool device_mode() const { return device_mode_; }
 

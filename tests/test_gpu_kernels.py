@@ -1,0 +1,174 @@
+"""Kernel-level checks of the device learner's hot path, on the state the last device-grown
+tree leaves in HBM (read back through LGBM_AMD_BoosterDevice* in the C API):
+
+* histograms (k_hist root pass, fused k_split partition + histogram, k_hist_reduce, and the
+  parent - sibling subtraction in k_find): every leaf's raw fixed-point slot must EQUAL a
+  torch fp64 scatter-add of the leaf's rows' quantised (g, h) at the kernel's own scale --
+  exact integers, so any off-by-one in a bin, a row or a block boundary fails;
+* partition (k_split): the leaves' row lists are disjoint, cover the bag, and every row sits
+  in the leaf the CPU predictor routes its raw feature values to;
+* split scan (k_find + pick): every leaf's device best split equals the CPU split finder's
+  (src/treelearner/split_finder.cpp) on the same dequantised histogram -- NaN / zero missing
+  values, most-frequent-bin offset, categorical (one-hot and sorted), monotone, L1 /
+  max_delta_step / path smoothing, wide int64 histograms (gpu_use_dp), bagging, EFB bundles,
+  and multi-block leaves (> 16k rows).
+"""
+import ctypes
+import json
+
+import numpy as np
+import pytest
+
+import lightgbmv1_amd as lgb
+from lightgbmv1_amd import _native as nat
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, seed=5, f=10):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(n, f)
+    X[rng.rand(n) < 0.08, 1] = np.nan                          # NaN missing
+    X[:, 2] = np.where(rng.rand(n) < 0.7, 0.0, X[:, 2])        # most frequent bin 0 (offset 1)
+    X[:, 3] = np.where(rng.rand(n) < 0.6, 1.5, X[:, 3])        # most frequent bin not 0
+    X[:, 4] = rng.randint(0, 24, n)                            # categorical, many categories
+    X[:, 5] = rng.randint(0, 4, n)                             # categorical, one-hot sized
+    X[:, 6] = np.round(X[:, 6], 1)                             # ties between thresholds
+    logit = (X[:, 0] + 0.8 * np.nan_to_num(X[:, 1]) - 0.6 * X[:, 2] + 0.5 * (X[:, 3] > 1)
+             + 0.3 * (X[:, 4] % 5 == 1) - 0.4 * (X[:, 5] == 2) + 0.3 * X[:, 6] * X[:, 7])
+    y = (logit + 0.5 * rng.randn(n) > 0).astype(np.float64)
+    return X, y
+
+
+def _efb_data(n, seed=9):
+    """Mutually exclusive sparse columns (bundled by EFB into shared groups) + dense ones."""
+    rng = np.random.RandomState(seed)
+    X = np.zeros((n, 12))
+    owner = rng.randint(0, 8, n)
+    for j in range(8):
+        rows = owner == j
+        X[rows, j] = rng.rand(rows.sum()) * (j + 1)
+    X[:, 8:] = rng.randn(n, 4)
+    y = (X[:, 0] + X[:, 3] - X[:, 5] + X[:, 8] + 0.3 * rng.randn(n) > 0.5).astype(np.float64)
+    return X, y
+
+
+BASE = {"objective": "binary", "num_leaves": 31, "max_bin": 63, "learning_rate": 0.1, "min_data_in_leaf": 20,
+        "verbose": -1, "device_type": "gpu", "seed": 7, "deterministic": True}
+
+CASES = {
+    "numeric": ({}, 20000),
+    "categorical": ({"categorical_feature": [4, 5]}, 20000),
+    "zero_missing": ({"zero_as_missing": True}, 20000),
+    "monotone": ({"monotone_constraints": [1, 0, -1, 0, 0, 0, 0, 0, 0, 0]}, 20000),
+    "regularised": ({"lambda_l1": 0.5, "lambda_l2": 1.0, "max_delta_step": 0.7, "path_smooth": 2.0,
+                     "min_gain_to_split": 0.01}, 20000),
+    "wide_dp": ({"gpu_use_dp": True}, 20000),
+    "bagging": ({"bagging_fraction": 0.7, "bagging_freq": 1, "bagging_seed": 3}, 20000),
+    "multi_block": ({"num_leaves": 63}, 150000),
+    "efb": ({"max_bin": 31}, 30000),
+}
+
+
+def _group_bins(ds):
+    ng = ctypes.c_int(0)
+    nat.call("LGBM_AMD_DatasetGetGroupBins", ds.handle, None, None, ctypes.byref(ng))
+    bins = np.zeros((ds.num_data(), ng.value), dtype=np.int32)
+    bounds = np.zeros(ng.value + 1, dtype=np.int64)
+    nat.call("LGBM_AMD_DatasetGetGroupBins", ds.handle, bins.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+             bounds.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), ctypes.byref(ng))
+    return bins, bounds
+
+
+def _gradients(bst, n):
+    g = np.zeros(n, dtype=np.float32)
+    h = np.zeros(n, dtype=np.float32)
+    scales = np.zeros(2, dtype=np.float64)
+    nat.call("LGBM_AMD_BoosterDeviceGradients", bst.handle, g.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+             h.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), scales.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return g, h, scales
+
+
+def _leaf_state(bst, leaf):
+    cnt = ctypes.c_int(0)
+    hlen = ctypes.c_int64(0)
+    nat.call("LGBM_AMD_BoosterDeviceLeafState", bst.handle, ctypes.c_int(leaf), None, ctypes.byref(cnt), None,
+             None, ctypes.byref(hlen), None)
+    rows = np.zeros(cnt.value, dtype=np.int32)
+    hist = np.zeros(hlen.value, dtype=np.int64)
+    valid = np.zeros(hlen.value // 2, dtype=np.int8)
+    sums = np.zeros(3, dtype=np.float64)
+    nat.call("LGBM_AMD_BoosterDeviceLeafState", bst.handle, ctypes.c_int(leaf),
+             rows.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)), ctypes.byref(cnt),
+             hist.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), valid.ctypes.data_as(ctypes.POINTER(ctypes.c_int8)),
+             ctypes.byref(hlen), sums.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    return rows, hist.reshape(-1, 2), valid.astype(bool), sums
+
+
+def _check_splits(bst):
+    text = nat.read_string(lambda size, need, buf: nat.call("LGBM_AMD_BoosterDeviceCheckSplits", bst.handle, size,
+                                                            need, buf), 1 << 16)
+    return json.loads(text)
+
+
+def _quantise(v, scale):
+    # the kernels' __float2ll_rn(v * (float)scale): an fp32 product by a power of two, rounded
+    # half to even
+    return np.rint(v.astype(np.float32) * np.float32(scale)).astype(np.float64)
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_device_tree_state(gpu_available, case):
+    import torch
+    extra, n = CASES[case]
+    X, y = (_efb_data if case == "efb" else _data)(n)
+    params = dict(BASE, **extra)
+    cat = params.pop("categorical_feature", "auto")
+    ds = lgb.Dataset(X, y, params=params, categorical_feature=cat, free_raw_data=False)
+    bst = lgb.train(params, ds, 4, verbose_eval=False, keep_training_booster=True)
+    num_leaves = bst.dump_model()["tree_info"][-1]["num_leaves"]
+    assert num_leaves > 4
+
+    bins, bounds = _group_bins(ds)
+    g, h, scales = _gradients(bst, n)
+    gq = torch.from_numpy(_quantise(g, scales[0]))
+    hq = torch.from_numpy(_quantise(h, scales[1]))
+    nbins = int(bounds[-1])
+    # hist index of every (row, group): the group's first bin + the row's group bin; group
+    # bin 0 (every member feature at its most frequent bin) is never accumulated
+    gidx = torch.from_numpy(bins.astype(np.int64) + bounds[:-1][None, :])
+    stored = torch.from_numpy(bins != 0)
+
+    leaf_of_row = bst.predict(X, pred_leaf=True)[:, -1]
+    seen = np.zeros(n, dtype=np.int32)
+    checked_bins = 0
+    for leaf in range(num_leaves):
+        rows, hist, valid, sums = _leaf_state(bst, leaf)
+        checked_bins += int(valid.sum())
+        assert len(rows) == int(sums[2])
+        # partition: every row of the leaf is routed to it by the CPU predictor
+        assert np.all(leaf_of_row[rows] == leaf), (case, leaf)
+        seen[rows] += 1
+        # histogram: torch fp64 scatter-add of the rows' quantised (g, h)
+        r = torch.from_numpy(rows.astype(np.int64))
+        idx = gidx[r][stored[r]]
+        exp_g = torch.zeros(nbins, dtype=torch.float64).scatter_add_(
+            0, idx, gq[r].unsqueeze(1).expand(-1, bins.shape[1])[stored[r]])
+        exp_h = torch.zeros(nbins, dtype=torch.float64).scatter_add_(
+            0, idx, hq[r].unsqueeze(1).expand(-1, bins.shape[1])[stored[r]])
+        dev_g = hist[:, 0].astype(np.float64)
+        dev_h = hist[:, 1].astype(np.float64)
+        # only the slices of features evaluated for the leaf are materialised (group bin 0
+        # belongs to no feature; a feature the parent could not split on is skipped)
+        bad_g = np.flatnonzero((dev_g != exp_g.numpy()) & valid)
+        bad_h = np.flatnonzero((dev_h != exp_h.numpy()) & valid)
+        assert bad_g.size == 0 and bad_h.size == 0, (case, leaf, bad_g[:5], bad_h[:5])
+    assert checked_bins > num_leaves * 10
+    # the leaves partition the bag: no row twice; without bagging, every row once
+    assert seen.max() <= 1
+    if "bagging_fraction" not in extra:
+        assert seen.min() == 1
+
+    rep = _check_splits(bst)
+    assert rep["device_mode"] and rep["checked"] > 0, rep
+    assert rep["mismatched"] == 0, json.dumps(rep)

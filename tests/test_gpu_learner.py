@@ -401,7 +401,10 @@ def _splits(node):
     {"feature_fraction_bynode": 0.6, "feature_fraction_seed": 9},
     {"interaction_constraints": [[0, 1, 2], [3, 5, 7], [1, 6]]},
     {"num_leaves": 63, "min_data_in_leaf": 200, "extra_seed": 11},
-], ids=["plain", "bynode", "interaction", "wide_seed"])
+    {"bagging_fraction": 0.6, "bagging_freq": 1, "bagging_seed": 5},
+    {"max_depth": 3, "num_leaves": 31},
+    {"min_data_in_leaf": 1500, "num_leaves": 31},
+], ids=["plain", "bynode", "interaction", "wide_seed", "bagging", "early_end_depth", "early_end_min_data"])
 def test_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
     """extra_trees in device-resident growth: the split scans draw each feature's random
     threshold from its generator state at the tree's start (reference
@@ -422,7 +425,7 @@ def test_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
     dt = models["device"].dump_model()["tree_info"]
     ht = models["host"].dump_model()["tree_info"]
     assert len(dt) == len(ht)
-    for i in range(3):
+    for i in range(len(dt)):  # every tree: the generators stay in step across trees
         assert _splits(dt[i]["tree_structure"]) == _splits(ht[i]["tree_structure"]), i
     pd, ph = models["device"].predict(X[:5000]), models["host"].predict(X[:5000])
     assert np.corrcoef(pd, ph)[0, 1] > 0.999
