@@ -51,6 +51,12 @@ struct Params {
   int32_t has_cat;           // number of categorical features (KArgs::cat_list; their own split-scan kernel)
   int32_t direct_from_split; // splits >= this have no reduce kernel: the split scan sums the partials
   int32_t trace_repeat;      // diagnostics (LGBM_AMD_KTRACE_REPEAT): run the traced pick twice
+  // voting-parallel split scans (reference voting_parallel_tree_learner.cpp): 0 off, 1 the
+  // local scan (rank-local sums / counts / parameters, every feature), 2 the global scan of the
+  // elected features (KArgs::vote_list, histograms in KArgs::vote_hist)
+  int32_t vote_phase;
+  int32_t vote_k;  // top_k: features each rank proposes and the vote elects, per leaf
+  int32_t world;   // ranks
 };
 
 // per-leaf state
@@ -64,6 +70,7 @@ struct Leaf {
   int32_t frow;          // row of KArgs::splittable (kept across trees)
   uint32_t icmask;       // interaction constraints consistent with the leaf's branch (bit k: constraint k)
   double sum_g, sum_h, output;
+  double lsum_g, lsum_h;  // voting-parallel: this rank's (local) sums of the leaf's rows
   double cmin, cmax;  // monotone constraint range
 };
 
@@ -85,6 +92,7 @@ struct CurSplit {
   int32_t child_depth;
   int32_t parent_slot;  // histogram slot of the leaf (the new leaf's slot is its own id)
   int32_t parent_frow, new_frow;  // splittable rows of the leaf and of the new leaf
+  double plsum_g, plsum_h;  // voting-parallel: the leaf's local sums (Leaf::lsum_*)
   Feature feat;         // the split feature's record
   DeviceSplit split;
 };
@@ -104,6 +112,9 @@ struct Step {
   int32_t root_count;   // global rows of the tree's root
   int32_t bynode_base, bynode_next;  // per-node feature masks: this step's / next free mask index
   int32_t cur_left, cur_right;      // partition cursors: rows placed left / right so far
+  // voting-parallel: fixed-point (g, h) sums of the rows k_split histogrammed (the local sums
+  // of that child), accumulated with atomics; cleared by the pick
+  unsigned long long loc_acc[2];
   CurSplit cs;
   ChildStats lr[2];     // left / right child of cs
 };
@@ -114,6 +125,14 @@ struct FeatureBest {
   double lg, lh, rg, rh, lo, ro;
   int32_t feature, real_feature, thr, default_left, lc, rc, mono;
   int32_t ncat;  // categorical: categories in the left set (KArgs::feat_cat); 0: numerical
+};
+
+// voting-parallel: one rank's proposal for a leaf (reference LightSplitInfo: the local best
+// split's gain and its local row count)
+struct VoteEntry {
+  double gain;
+  int32_t feature;  // inner feature index, -1: none
+  int32_t count;    // local rows of the leaf (left + right count of the local split)
 };
 
 // record of one applied split, read back by the host to rebuild the Tree

@@ -89,6 +89,15 @@ struct KArgs {
   // step s; rows of steps not run stay 0), or null
   const uint32_t* xt_base;   // [num_features]
   int32_t* xt_cum;           // [num_leaves][num_features]
+  // voting-parallel (Params::vote_phase): this rank's root sums before the all-reduce, the
+  // proposals of every rank ([world][2][vote_k], this rank's block at rank), the elected
+  // features per leaf ([2][vote_k], -1 padded) and their histograms ([2][vote_k][max_feature_bins]
+  // (g, h) int64, summed over the ranks before the global scan)
+  const double* root_local;
+  VoteEntry* vote_buf;
+  int32_t vote_rank;
+  int32_t* vote_list;
+  long long* vote_hist;
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)
@@ -152,6 +161,12 @@ void FindStep(const KArgs& a, hipStream_t s);
 // the step's bookkeeping and the next pick as a kernel of its own (distributed learners:
 // it runs after the per-feature results were gathered from every rank)
 void PickStep(const KArgs& a, hipStream_t s, bool root);
+// voting-parallel: this rank's top-k proposals per leaf from the local scan (into its block
+// of vote_buf); after the allgather, the election and the elected features' local histograms
+// (into vote_hist, for the all-reduce); the global scan is FindRoot / FindStep with
+// Params::vote_phase = 2
+void VoteLocal(const KArgs& a, hipStream_t s, bool root);
+void VoteElect(const KArgs& a, hipStream_t s, bool root);
 
 // score[k] += value[leaf(row)] for every partitioned row of the finished tree
 void AddLeafScore(const KArgs& a, const double* leaf_values, int num_leaves, double* score, hipStream_t s);

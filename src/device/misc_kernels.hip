@@ -96,6 +96,7 @@ __global__ void k_tree_begin(KArgs a) {
     lf.slot = l;
     lf.buf = 0;
     lf.sum_g = lf.sum_h = lf.output = 0.0;
+    lf.lsum_g = lf.lsum_h = 0.0;
     lf.cmin = -DBL_MAX;
     lf.cmax = DBL_MAX;
     lf.icmask = 0xffffffffu;  // the root may use every constraint
@@ -115,6 +116,7 @@ __global__ void k_tree_begin(KArgs a) {
     st->larger = -1;
     st->hist_left = 1;
     st->find_count = 0u;
+    st->loc_acc[0] = st->loc_acc[1] = 0ull;
     st->root_count = 0;
     st->cur_left = st->cur_right = 0;
   }

@@ -84,6 +84,10 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   const bool hl = hist_left != 0;
+  // voting-parallel: the histogrammed rows' fixed-point (g, h), summed by the threads of
+  // word 0 of column tile 0 (each row once) -- that child's local sums
+  const bool loc_sums = HIST && a.p.vote_phase != 0 && blockIdx.y == 0;
+  long long loc_g = 0, loc_h = 0;
   for (int kb = blockIdx.x; kb < nblk; kb += gridDim.x) {
     const int r0 = kb * chunk, r1 = min(pc, r0 + chunk);
     const bool first_trace = kb == static_cast<int>(blockIdx.x);
@@ -190,6 +194,15 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
           if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
 #pragma unroll
           for (int k = 0; k < kGatherRows; ++k) AddRow<GPW, UNITS>(lds, t.goff, wd[k], v[k], t.sg, t.sh);
+          if (loc_sums && t.q == 0) {
+#pragma unroll
+            for (int k = 0; k < kGatherRows; ++k) {
+              if (rr[k] >= 0) {
+                loc_g += __float2ll_rn(v[k].x * t.sg);
+                loc_h += __float2ll_rn(v[k].y * t.sh);
+              }
+            }
+          }
         }
       }
       __syncthreads();  // row list, wave counts and bases are rewritten by the next sub-tile
@@ -199,6 +212,14 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
       unsigned long long* out = a.partials + static_cast<size_t>(kb) * UNITS * a.p.total_bins +
                                 static_cast<size_t>(UNITS) * t.lo_bin;
       for (int j = threadIdx.x; j < UNITS * t.nbins; j += kPartThreads) out[j] = lds[j];
+    }
+  }
+  if (loc_sums) {
+    loc_g = WaveSum(loc_g);
+    loc_h = WaveSum(loc_h);
+    if (lane == 0 && (loc_g != 0 || loc_h != 0)) {
+      atomicAdd(&st->loc_acc[0], static_cast<unsigned long long>(loc_g));
+      atomicAdd(&st->loc_acc[1], static_cast<unsigned long long>(loc_h));
     }
   }
   KTrace(a, ts, kTrSplitExit);

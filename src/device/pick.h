@@ -473,6 +473,8 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
       cs.parent_slot = P.slot;
       cs.parent_frow = P.frow;
       cs.new_frow = new_frow;
+      cs.plsum_g = P.lsum_g;
+      cs.plsum_h = P.lsum_h;
       // k_split histograms the child with fewer rows by the estimated counts
       st->hist_left = sp.left_count <= sp.right_count ? 1 : 0;
     }
@@ -481,6 +483,8 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     st->cur_left = 0;  // the next k_split's partition cursors
     st->cur_right = 0;
     st->find_count = 0u;
+    st->loc_acc[0] = 0ull;  // voting: the next k_split's local sums
+    st->loc_acc[1] = 0ull;
   }
 }
 

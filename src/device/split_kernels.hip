@@ -735,7 +735,13 @@ template <bool ROOT, int KIND, bool SIMPLE>
 __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND>& sh) {
   constexpr bool CAT = KIND == 2;
   const long long t_entry = wall_clock64();
-  const int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
+  // voting-parallel global scan: the features the vote elected for this side's leaf (an
+  // empty slot still takes part in the step's workgroup count)
+  const bool vote_global = a.p.vote_phase == 2;
+  int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
+  if (vote_global) f = a.vote_list[blockIdx.y * a.p.vote_k + blockIdx.x];
+  const bool vote_empty = vote_global && f < 0;
+  if (vote_empty) f = 0;
   const int side = blockIdx.y;
   const int tid = threadIdx.x;
   const int units = a.hist_units;
@@ -747,7 +753,8 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   const int mi_base = ROOT ? 0 : st->bynode_next;  // this step's per-node masks (advanced by the pick)
   int8_t used = tree_used;  // evaluated at this node (feature_fraction_bynode)
   if (a.node_mask != nullptr) used = used && a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f];
-  const int8_t parent_ok = ROOT ? 1 : a.parent_flags[f];
+  // (voting: every feature is scanned -- the vote may elect one this rank could not split)
+  const int8_t parent_ok = (ROOT || a.p.vote_phase != 0) ? 1 : a.parent_flags[f];
   const double ig = a.scales[2], ih = a.scales[3];
   int s = 0, pc = 0, skip = 0;
   ChildInfo c;
@@ -786,7 +793,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     parity = (s + 1) & 1;
     // zero this feature's bins of the buffer the next step reduces into (data-parallel:
     // the whole owner-major buffer is cleared before each reduction)
-    if (!CAT && side == 0 && a.rs_pos == nullptr) {
+    if (!CAT && side == 0 && a.rs_pos == nullptr && !vote_global) {
       long long* nxt = StepScratch(a, parity + 1);
       for (int i = tid; i < nb2; i += kFindThreads) nxt[2 * F.hist_offset + i] = 0;
     }
@@ -794,14 +801,15 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     KTraceAt(a, s, kTrFindEntry, t_entry);
     KTrace(a, s, kTrFindHdr);
     const int nblk = StepBlocks(a, pc);
-    if (DirectPartials(a, nblk, s)) nblk_direct = nblk;
+    if (DirectPartials(a, nblk, s) && !vote_global) nblk_direct = nblk;
   }
   const SplitParams& p = a.p.sp;
   LeafCtx L;
   int depth, slot;
   if (ROOT) {
-    const double sg = a.root[0], shh = a.root[1];
-    const int n = static_cast<int>(a.root[2]);
+    const double* rsum = a.p.vote_phase == 1 ? a.root_local : a.root;  // voting: local, then global
+    const double sg = rsum[0], shh = rsum[1];
+    const int n = static_cast<int>(rsum[2]);
     ConstraintRange cr;
     cr.min = -DBL_MAX;
     cr.max = DBL_MAX;
@@ -811,13 +819,19 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     rp.use_smoothing = 0;
     rp.use_mc = 1;
     const double out0 = LeafOutputConstrained(sg, shh, p.lambda_l2, rp, cr, n, 0);
-    if (f == 0 && tid == 0 && KIND != 2) {
+    const bool first = vote_global ? blockIdx.x == 0 : f == 0;
+    if (first && tid == 0 && KIND != 2) {
       Leaf& lf = a.leaves[0];
-      lf.sum_g = sg;
-      lf.sum_h = shh;
-      lf.global_count = n;
-      lf.output = out0;
-      a.st->root_count = n;
+      if (a.p.vote_phase == 1) {
+        lf.lsum_g = sg;
+        lf.lsum_h = shh;
+      } else {
+        lf.sum_g = sg;
+        lf.sum_h = shh;
+        lf.global_count = n;
+        lf.output = out0;
+        a.st->root_count = n;
+      }
     }
     L.sg = sg;
     L.sh = shh + 2 * kEpsilon;
@@ -835,8 +849,25 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     L.c.max = cl.cmax;
     depth = cl.depth;
     slot = sd.slot;
+    if (a.p.vote_phase == 1) {
+      // voting local scan: this rank's rows of the child -- the histogrammed child's sums from
+      // k_split, the other one's as the parent's minus those
+      const double hg = static_cast<double>(static_cast<long long>(st->loc_acc[0])) * ig;
+      const double hh = static_cast<double>(static_cast<long long>(st->loc_acc[1])) * ih;
+      const double lsg = sd.is_hist ? hg : st->cs.plsum_g - hg;
+      const double lsh = sd.is_hist ? hh : st->cs.plsum_h - hh;
+      L.sg = lsg;
+      L.sh = lsh + 2 * kEpsilon;
+      L.n = sd.lr == 0 ? c.total_left : pc - c.total_left;
+      if (blockIdx.x == 0 && tid == 0) {
+        a.leaves[sd.leaf].lsum_g = lsg;
+        a.leaves[sd.leaf].lsum_h = lsh;
+      }
+    }
   }
+  if (vote_empty) return;
   if (KIND == 1 && F.is_cat) return;  // the categorical kernel scans it
+  if (CAT && !F.is_cat) return;       // (voting global scan: an elected numerical feature)
   // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
   // here but keeps its histogram and its splittable flag
   if (a.feat_icmask != nullptr && ((ROOT ? 0xffffffffu : cl.icmask) & a.feat_icmask[f]) == 0u) used = 0;
@@ -870,15 +901,19 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   // a sampled-out feature (bynode) still materialises its histogram: descendants subtract it
   if (tree_used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
     const int nh = 2 * a.p.total_bins;
-    long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
-    const long long* src = a.owned_hist != nullptr ? a.owned_hist + 2 * (F.hist_offset - a.owned_bin_lo)
-                                                   : StepScratch(a, parity) + 2 * F.hist_offset;
+    // (voting global scan: the elected feature's histogram summed over the ranks, read in place)
+    long long* dst = vote_global ? a.vote_hist + static_cast<size_t>(side * a.p.vote_k + blockIdx.x) * 2 *
+                                                     a.p.max_feature_bins
+                                 : a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
+    const long long* src = vote_global ? dst
+                           : a.owned_hist != nullptr ? a.owned_hist + 2 * (F.hist_offset - a.owned_bin_lo)
+                                                     : StepScratch(a, parity) + 2 * F.hist_offset;
     const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
     const unsigned long long* part = a.partials + static_cast<size_t>(units) * F.hist_offset;
     const bool stage = a.p.max_feature_bins <= kFindLdsBins;
     double* sg = s_bins;
     double* shv = s_bins + (stage ? a.p.max_feature_bins : 0);
-    const bool subtract = !ROOT && !sd.is_hist;  // parent - the histogrammed child, in place
+    const bool subtract = !ROOT && !sd.is_hist && !vote_global;  // parent - the histogrammed child, in place
     // a feature with fewer bins than threads sums its direct partials with every thread:
     // kFindThreads / nbf threads per bin stride over the row blocks, then combine in LDS
     // (one thread per bin walking hundreds of partials would be a chain of round trips)
@@ -979,7 +1014,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       splittable = FindNumericalBlock<SIMPLE>(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc, sh.sc2,
                                               xt_thr);
     }
-    if (tid == 0) flags[f] = splittable ? 1 : 0;
+    if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (the local scan's flags stay)
     if (!ROOT) KTrace(a, s, kTrFindScanned);
   } else {
     o.feature = -1;
@@ -1042,7 +1077,8 @@ static void LaunchFind(const KArgs& a, hipStream_t s) {
   if (a.p.has_cat) {
     if (simple) hipLaunchKernelGGL((k_find<ROOT, 1, true>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_find<ROOT, 1, false>), g, b, lds, s, a);
-    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false>), dim3(a.p.has_cat, ROOT ? 1 : 2), b, lds, s, a);
+    const int ncat = a.p.vote_phase == 2 ? a.num_scan : a.p.has_cat;  // voting: every elected slot
+    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false>), dim3(ncat, ROOT ? 1 : 2), b, lds, s, a);
   } else {
     if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_find<ROOT, 0, false>), g, b, lds, s, a);

@@ -112,6 +112,7 @@ void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
   rank_ = Network::rank();
   distributed_ = mode_ != Mode::kSerial && world_ > 1;
   data_parallel_ = mode_ == Mode::kData && world_ > 1;
+  voting_ = mode_ == Mode::kVoting && world_ > 1;
   HIPCHECK(hipSetDevice(device_id_));
   int cus = 0;
   HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
@@ -288,7 +289,15 @@ void GPUTreeLearner::UploadData() {
   a.p.row_stride = static_cast<int32_t>(row_bytes);
   a.p.total_bins = total_bins_;
   a.p.monotone_penalty = config_->monotone_penalty;
-  a.p.data_parallel = data_parallel_ ? 1 : 0;  // global counts from the split estimates
+  a.p.data_parallel = (data_parallel_ || voting_) ? 1 : 0;  // global counts from the split estimates
+  a.p.vote_phase = 0;
+  a.p.vote_k = 0;
+  a.p.world = world_;
+  a.root_local = nullptr;
+  a.vote_buf = nullptr;
+  a.vote_rank = rank_;
+  a.vote_list = nullptr;
+  a.vote_hist = nullptr;
   a.bins = d_bins_;
   a.feat = d_feat_;
   a.group_off = d_group_off_;
@@ -362,7 +371,33 @@ void GPUTreeLearner::UploadData() {
     HIPCHECK(hipMemcpy(d_cat_list_, cats.data(), sizeof(int32_t) * cats.size(), hipMemcpyHostToDevice));
   }
   a.cat_list = d_cat_list_;
-  if (distributed_) {
+  if (voting_) {
+    // every rank scans every feature locally (phase 1), then the elected ones globally (phase 2,
+    // the arguments of VoteExchange); the per-leaf election buffers
+    vote_k_ = std::max(1, std::min(config_->top_k, num_features_));
+    if (vote_k_ > 64 || world_ * vote_k_ > 1024) {
+      Log::Fatal("device voting-parallel supports top_k <= 64 and num_machines * top_k <= 1024");
+    }
+    a.p.vote_phase = 1;
+    a.p.vote_k = vote_k_;
+    a.p.sp = [&] {
+      Config local = *config_;
+      local.min_data_in_leaf /= world_;
+      local.min_sum_hessian_in_leaf /= world_;
+      return MakeSplitParams(local);
+    }();
+    d_root_local_ = Alloc<double>(3);
+    d_vote_buf_ = Alloc<dev::VoteEntry>(static_cast<size_t>(world_) * 2 * vote_k_);
+    d_vote_list_ = Alloc<int32_t>(2 * static_cast<size_t>(vote_k_));
+    d_vote_hist_ = Alloc<long long>(static_cast<size_t>(2 * vote_k_) * 2 * max_fb);
+    a.root_local = d_root_local_;
+    a.vote_buf = d_vote_buf_;
+    a.vote_list = d_vote_list_;
+    a.vote_hist = d_vote_hist_;
+    Log::Info("voting-parallel device learner, rank %d of %d: top_k %d; per split: proposal allgather %zu bytes "
+              "per rank, elected-histogram all-reduce %zu bytes", rank_, world_, vote_k_,
+              sizeof(dev::VoteEntry) * 2 * vote_k_, sizeof(long long) * 4 * static_cast<size_t>(vote_k_) * max_fb);
+  } else if (distributed_) {
     // this rank scans its own features; the per-feature results are gathered rank-major
     a.feat_list = d_feat_list_;
     a.num_scan = static_cast<int32_t>(owned_feats_.size());
@@ -408,7 +443,7 @@ void GPUTreeLearner::SetupOwnership() {
   max_owned_ = 0;
   rs_block_ = 0;
   owned_bin_lo_ = 0;
-  if (!distributed_) return;
+  if (!distributed_ || mode_ == Mode::kVoting) return;
   std::vector<int32_t> goff(num_groups_ + 1, total_bins_);
   for (int g = 0; g < num_groups_; ++g) goff[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
   std::vector<int> gown(num_groups_);
@@ -578,6 +613,8 @@ void GPUTreeLearner::DecideMode() {
   // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
   const auto& ic = config_->interaction_constraints_vector;
   if (!ic.empty() && (ic.size() > 32 || config_->feature_fraction_bynode < 1.0)) dm = false;
+  // voting: per-node sampling and extra_trees draws stay with the host voting loop
+  if (voting_ && (config_->feature_fraction_bynode < 1.0 || config_->extra_trees)) dm = false;
   if (has_forced_split_ ||
       (config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
       config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
@@ -671,7 +708,9 @@ void GPUTreeLearner::WatchdogSync() {
 }
 
 void GPUTreeLearner::AllreduceRoot() {
-  if (!data_parallel_ || Network::num_machines() <= 1) return;
+  if (!(data_parallel_ || voting_) || Network::num_machines() <= 1) return;
+  // voting: the local scan of the root needs this rank's sums too
+  if (voting_) HIPCHECK(hipMemcpyAsync(d_root_local_, d_root_, sizeof(double) * 3, hipMemcpyDeviceToDevice, stream_));
   DeviceComm* dc = Network::device_comm();
   if (dc != nullptr) {
     dc->AllreduceSumF64(d_root_, 3, stream_);
@@ -708,7 +747,7 @@ void GPUTreeLearner::ReduceScatterStep(int parity) {
 // distributed: every rank's per-feature results (and category sets), rank-major, so each
 // rank picks the same split (reference SyncUpGlobalBestSplit, parallel_tree_learner.h:190)
 void GPUTreeLearner::GatherFeatureBests() {
-  if (!distributed_) return;
+  if (!distributed_ || voting_) return;
   DeviceComm* dc = Network::device_comm();
   const size_t fb_bytes = 2 * static_cast<size_t>(max_owned_) * sizeof(dev::FeatureBest);
   const size_t cat_bytes = 2 * static_cast<size_t>(max_owned_) * kMaxCatWords * sizeof(uint32_t);
@@ -733,7 +772,7 @@ void GPUTreeLearner::GatherFeatureBests() {
 }
 
 void GPUTreeLearner::AllreduceAbsMax() {
-  if (!data_parallel_ || Network::num_machines() <= 1) return;
+  if (!(data_parallel_ || voting_) || Network::num_machines() <= 1) return;
   DeviceComm* dc = Network::device_comm();
   if (dc != nullptr) {
     dc->AllreduceMaxU32(d_absmax_, 3, stream_);  // non-negative float bits order like the floats
@@ -873,7 +912,16 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   dev::HistRoot(a, stream_);
   ReduceScatterStep(0);
   dev::FindRoot(a, stream_);
-  if (distributed_) {
+  // voting: the global scan of the elected features picks (pick_in_find); the local scan does not
+  dev::KArgs glob = a;
+  if (voting_) {
+    glob.p.vote_phase = 2;
+    glob.p.sp = params_;
+    glob.pick_in_find = 1;
+    glob.num_scan = vote_k_;
+    VoteExchange(glob, true);
+    dev::FindRoot(glob, stream_);
+  } else if (distributed_) {
     GatherFeatureBests();
     dev::PickStep(a, stream_, true);
   }
@@ -889,10 +937,45 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
     dev::SplitStep(a, stream_, s < a.p.direct_from_split || data_parallel_);
     ReduceScatterStep(s + 1);
     dev::FindStep(a, stream_);
-    if (distributed_) {
+    if (voting_) {
+      VoteExchange(glob, false);
+      dev::FindStep(glob, stream_);
+    } else if (distributed_) {
       GatherFeatureBests();
       dev::PickStep(a, stream_, false);
     }
+  }
+}
+
+// voting: proposals -> allgather -> election + elected local histograms -> all-reduce
+// (reference voting_parallel_tree_learner.cpp:300-343); the global scan follows
+void GPUTreeLearner::VoteExchange(const dev::KArgs& glob, bool root) {
+  dev::VoteLocal(glob, stream_, root);
+  DeviceComm* dc = Network::device_comm();
+  const size_t prop_bytes = sizeof(dev::VoteEntry) * 2 * static_cast<size_t>(vote_k_);
+  char* vb = reinterpret_cast<char*>(d_vote_buf_);
+  if (dc != nullptr) {
+    dc->Allgather(vb + prop_bytes * rank_, vb, prop_bytes, stream_);
+  } else {
+    std::vector<char> all(prop_bytes * world_);
+    HIPCHECK(hipMemcpyAsync(all.data() + prop_bytes * rank_, vb + prop_bytes * rank_, prop_bytes,
+                            hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
+    std::vector<char> mine(all.begin() + prop_bytes * rank_, all.begin() + prop_bytes * (rank_ + 1));
+    Network::Allgather(mine.data(), static_cast<comm_size_t>(prop_bytes), all.data());
+    HIPCHECK(hipMemcpyAsync(vb, all.data(), all.size(), hipMemcpyHostToDevice, stream_));
+  }
+  dev::VoteElect(glob, stream_, root);
+  const size_t n = static_cast<size_t>(2 * vote_k_) * 2 * glob.p.max_feature_bins;
+  if (dc != nullptr) {
+    dc->AllreduceSumI64(d_vote_hist_, n, stream_);  // exact: fixed-point integers
+  } else {
+    std::vector<long long> h(n);
+    HIPCHECK(hipMemcpyAsync(h.data(), d_vote_hist_, sizeof(long long) * n, hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
+    h = Network::GlobalSum(h);
+    HIPCHECK(hipMemcpyAsync(d_vote_hist_, h.data(), sizeof(long long) * n, hipMemcpyHostToDevice, stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
   }
 }
 

@@ -32,11 +32,15 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   // serial: one device; data: rows sharded across ranks (owner-blocked reduce-scatter of the
   // histograms, reference data_parallel_tree_learner.cpp); feature: every rank holds all
   // rows and builds / scans only its own features (feature_parallel_tree_learner.cpp)
-  enum class Mode { kSerial, kData, kFeature };
+  // voting: rows sharded; each rank scans its local histograms, the ranks elect top_k features
+  // per leaf and only their histograms are summed (reference voting_parallel_tree_learner.cpp)
+  enum class Mode { kSerial, kData, kFeature, kVoting };
   GPUTreeLearner(const Config* config, Mode mode);
   explicit GPUTreeLearner(const Config* config) : GPUTreeLearner(config, Mode::kSerial) {}
   // host-assisted growth for every tree (the voting-parallel learner scans on the host)
   void ForceHostMode() { force_host_mode_ = true; }
+  // device-resident voting (before Init); host-assisted trees keep the wrapper's host voting
+  void UseDeviceVoting() { mode_ = Mode::kVoting; }
   ~GPUTreeLearner() override;
 
   // TreeLearner
@@ -123,6 +127,13 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void ReduceScatterStep(int parity);
   Mode mode_ = Mode::kSerial;
   bool data_parallel_ = false;  // kData on more than one rank (global counts from the split estimates)
+  bool voting_ = false;         // kVoting on more than one rank
+  int vote_k_ = 0;
+  double* d_root_local_ = nullptr;      // voting: this rank's root sums
+  dev::VoteEntry* d_vote_buf_ = nullptr;  // [world][2][vote_k]
+  int32_t* d_vote_list_ = nullptr;        // [2][vote_k]
+  long long* d_vote_hist_ = nullptr;      // [2][vote_k][max_feature_bins][2]
+  void VoteExchange(const dev::KArgs& glob, bool root);
   bool distributed_ = false;    // kData / kFeature on more than one rank
   int world_ = 1, rank_ = 0;
   // feature ownership (distributed): contiguous storage-group blocks balanced by bins

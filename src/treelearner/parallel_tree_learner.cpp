@@ -258,8 +258,10 @@ void VotingParallelTreeLearner<Base>::InitLocalParams() {
 template <typename Base>
 void VotingParallelTreeLearner<Base>::Init(const Dataset* train_data, bool is_constant_hessian) {
   if constexpr (std::is_base_of<DeviceTreeLearner, Base>::value) {
-    // the voting exchange runs between the host-side split scans of each step
-    this->ForceHostMode();
+    // device-resident trees run the whole exchange on the device (GPUTreeLearner kVoting);
+    // host-assisted ones (per-node sampling, extra_trees, forced splits, CEGB) use this class's
+    // host loop between the device histogram builds
+    this->UseDeviceVoting();
   }
   Base::Init(train_data, is_constant_hessian);
   rank_ = Network::rank();

@@ -7,7 +7,11 @@ sequence as RCCL on a multi-GPU node:
     all-gathered and every rank picks the same split (reference
     src/treelearner/data_parallel_tree_learner.cpp:61-123, 154-247);
   * feature-parallel: every rank holds all rows, builds and scans only its features, then
-    the records are gathered (feature_parallel_tree_learner.cpp:37-77).
+    the records are gathered (feature_parallel_tree_learner.cpp:37-77);
+  * voting-parallel: every rank scans its local histograms, proposes its top_k features per
+    leaf, the proposals are all-gathered and every rank runs the same election; only the
+    elected features' histograms are all-reduced and scanned globally
+    (voting_parallel_tree_learner.cpp:151-343).
 Checks: identical models on every rank; the same splits as the serial device learner (bin
 mappers shared through Dataset.subset); feature-parallel equal to serial to rounding."""
 import ctypes
@@ -43,14 +47,14 @@ def _splits(model_str, tree=0):
     return rows.get("split_feature"), rows.get("threshold")
 
 
-def _run(learner, world, rounds=8):
+def _run(learner, world, rounds=8, **extra):
     X, y = make_data(N, 10)
     full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
     serial = lgb.train(BASE, full.subset(np.arange(N)), rounds)
 
     def rank_fn(r):
-        params = dict(BASE, tree_learner=learner, num_machines=world)
-        if learner == "data":
+        params = dict(BASE, tree_learner=learner, num_machines=world, **extra)
+        if learner in ("data", "voting"):
             params["pre_partition"] = True
             ds = full.subset(np.arange(r, N, world))  # this rank's rows, the shared bin mappers
         else:
@@ -101,3 +105,20 @@ def test_device_feature_parallel(world, gpu_available):
     for t in range(3):
         assert _splits(out[0][0], t) == _splits(serial.model_to_string(), t)
     np.testing.assert_allclose(out[0][1], serial.predict(X), rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_device_voting_parallel(world, gpu_available, capfd, monkeypatch):
+    capfd.readouterr()
+    X, y, serial, out = _run("voting", world, top_k=4, verbose=2)
+    log = capfd.readouterr().out
+    assert "voting-parallel device learner" in log and "device-resident growth" in log
+    assert "host-assisted growth" not in log
+    for m, _ in out[1:]:
+        assert _trees(m) == _trees(out[0][0])
+    from sklearn.metrics import roc_auc_score
+    assert abs(roc_auc_score(y, out[0][1]) - roc_auc_score(y, serial.predict(X))) < 0.01
+    # the host voting loop (host-assisted growth, same election rules) grows the same first tree
+    monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    _, _, _, host = _run("voting", world, top_k=4)
+    assert _splits(out[0][0], 0) == _splits(host[0][0], 0)
