@@ -63,6 +63,10 @@ def main():
     ap.add_argument("--max-bin", type=int, default=255)
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--test-rows", type=int, default=500_000)
+    ap.add_argument("--hist-precision", choices=["fx32", "fx64"], default="fx32",
+                    help="fx32: 32-bit fixed-point (g, h) per row, packed in one 64-bit histogram word; "
+                         "fx64 (gpu_use_dp): 2x 64-bit words, 31-bit row resolution")
+    ap.add_argument("--params", default="{}", help="extra training parameters (JSON)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -91,7 +95,9 @@ def main():
         "pre_partition": True,
         "verbose": -1,
         "num_threads": min(16, os.cpu_count() or 8),
+        "gpu_use_dp": args.hist_precision == "fx64",
     }
+    params.update(json.loads(args.params))
     train = lgb.Dataset(X, y, params=params, free_raw_data=True)
     booster = lgb.Booster(params=params, train_set=train)
     del X
@@ -124,7 +130,10 @@ def main():
             "higher_is_better": False,
             "scaling": "strong",
             "vs_baseline": round(sec_per_iter / BASELINE_SEC_PER_ITER, 6),
-            "dtype": "fp32",
+            # (g, h) are fp32; histogram inputs are fixed-point at a per-tree power-of-two scale
+            # (fx32: 2^30 / (16384 * max|g|), i.e. ~16 bits below max|g| per row; fx64: 2^31 /
+            # max|g|), summed exactly in int64, independent of the row count; scans in fp64
+            "dtype": "fp32-grad/{}-hist/fp64-scan".format(args.hist_precision),
             "data": "synthetic",
             "config": {"model": "gbdt binary, num_leaves={}, max_bin={}".format(args.leaves, args.max_bin),
                        "global_batch": n_total, "seq_len": args.features,
