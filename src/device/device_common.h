@@ -46,15 +46,18 @@ __device__ __forceinline__ int RoundIntD(double x) { return static_cast<int>(x +
 __device__ __forceinline__ int RootRows(const KArgs& a) { return a.num_rows_dev ? *a.num_rows_dev : a.num_rows; }
 
 // bin of storage column `group` for `row`, column-major copy (partition kernels)
-__device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int group) {
-  if (a.bin_bytes == 1) return a.bins_col[static_cast<int64_t>(group) * a.num_data + row];
-  return reinterpret_cast<const uint16_t*>(a.bins_col)[static_cast<int64_t>(group) * a.num_data + row];
-}
-
 // bin of storage column `group` for `row`, row-major matrix
 __device__ __forceinline__ uint32_t RowBin(const KArgs& a, int64_t row, int group) {
   if (a.bin_bytes == 1) return static_cast<const uint8_t*>(a.bins)[row * (4 * a.words_per_row) + group];
   return static_cast<const uint16_t*>(a.bins)[row * (2 * a.words_per_row) + group];
+}
+
+// the split column's bin for the partition: from the column-major copy when there is one,
+// else from the row-major matrix (whose line the histogram pass then reads again)
+__device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int group) {
+  if (a.bins_col == nullptr) return RowBin(a, row, group);
+  if (a.bin_bytes == 1) return a.bins_col[static_cast<int64_t>(group) * a.num_data + row];
+  return reinterpret_cast<const uint16_t*>(a.bins_col)[static_cast<int64_t>(group) * a.num_data + row];
 }
 
 // group bin -> feature bin (Dataset::FeatureBin)
