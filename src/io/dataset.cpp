@@ -312,12 +312,40 @@ void Dataset::ConstructFromBinMappers(std::vector<std::unique_ptr<BinMapper>>* m
   for (int f : used) fig.emplace_back(1, f);
   const bool can_bundle = sample_indices != nullptr && sample_values != nullptr &&
                           static_cast<int>(sample_indices->size()) > 0;
-  // bundling depends on the local sample; with several ranks it could differ per rank and
-  // break the shared feature layout, so distributed datasets keep one group per feature
-  if (cfg.enable_bundle && !used.empty() && can_bundle && Network::num_machines() <= 1) {
+  const int nm = Network::num_machines();
+  if (cfg.enable_bundle && !used.empty() && can_bundle && (nm <= 1 || Network::rank() == 0)) {
     fig = BundleFeatures(*mappers, sample_indices, sample_values, static_cast<int>(sample_indices->size()),
                          static_cast<data_size_t>(total_sample_cnt), used, num_data, cfg.device_type == "gpu",
                          cfg.is_enable_sparse, &multi_val);
+  }
+  if (nm > 1) {
+    // bundling depends on the sample, which is rank-local: every rank takes rank 0's groups so
+    // the feature layout (and every histogram offset) is the same everywhere
+    std::vector<int32_t> wire;  // [groups] then per group [size][multi][features...]
+    wire.push_back(static_cast<int32_t>(fig.size()));
+    for (size_t g = 0; g < fig.size(); ++g) {
+      wire.push_back(static_cast<int32_t>(fig[g].size()));
+      wire.push_back(multi_val[g]);
+      wire.insert(wire.end(), fig[g].begin(), fig[g].end());
+    }
+    const comm_size_t mine = Network::rank() == 0 ? static_cast<comm_size_t>(sizeof(int32_t) * wire.size()) : 0;
+    auto sizes = Network::GlobalArray<comm_size_t>(mine);
+    std::vector<comm_size_t> starts(nm, 0);
+    for (int r = 1; r < nm; ++r) starts[r] = starts[r - 1] + sizes[r - 1];
+    std::vector<int32_t> got(sizes[0] / sizeof(int32_t));
+    Network::Allgather(reinterpret_cast<char*>(wire.data()), starts.data(), sizes.data(),
+                       reinterpret_cast<char*>(got.data()), sizes[0]);
+    fig.clear();
+    multi_val.clear();
+    size_t p = 1;
+    for (int32_t g = 0; g < got[0]; ++g) {
+      const int n = got[p++];
+      multi_val.push_back(static_cast<int8_t>(got[p++]));
+      fig.emplace_back(got.begin() + p, got.begin() + p + n);
+      p += n;
+    }
+  }
+  {
     // multi-value groups are stored as singleton dense groups (same inner feature order)
     std::vector<std::vector<int>> expanded;
     for (size_t g = 0; g < fig.size(); ++g) {

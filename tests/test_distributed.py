@@ -170,3 +170,38 @@ def test_collective_timeout_when_a_rank_never_arrives():
     assert time.time() - t0 < 30
     assert not res[0].ok and "timed out" in str(res[0].error)
     assert res[1].ok
+
+
+def _efb_rank_train(rank, world, learner):
+    import ctypes
+    from lightgbmv1_amd import _native as nat
+    rng = np.random.RandomState(17)
+    n = 6000
+    X = np.zeros((n, 14))
+    owner = rng.randint(0, 10, n)
+    for j in range(10):  # ten mutually exclusive sparse columns: bundled by EFB
+        X[owner == j, j] = rng.rand((owner == j).sum()) + 0.5
+    X[:, 10:] = rng.randn(n, 4)
+    y = (X[:, 0] + X[:, 4] - X[:, 7] + X[:, 10] + 0.3 * rng.randn(n) > 0.6).astype(np.float64)
+    idx = np.arange(rank, n, world)
+    params = {"objective": "binary", "num_leaves": 15, "verbose": -1, "tree_learner": learner,
+              "num_machines": world, "pre_partition": True, "min_data_in_leaf": 20, "seed": 3,
+              "deterministic": True, "num_threads": 2, "top_k": 6}
+    ds = lgb.Dataset(X[idx], y[idx], params=params).construct()
+    ng = ctypes.c_int(0)
+    nat.call("LGBM_AMD_DatasetGetGroupBins", ds.handle, None, None, ctypes.byref(ng))
+    bst = lgb.train(params, ds, 8)
+    return ng.value, bst.model_to_string()
+
+
+@pytest.mark.parametrize("learner", ["data", "voting"])
+def test_efb_bundles_under_distributed_training(learner):
+    """EFB with several ranks: rank 0's bundles are used by every rank (their samples differ),
+    so the feature layout is shared and every rank builds the same model."""
+    from lightgbmv1_amd.parallel.inproc import ThreadRanks
+    with ThreadRanks(3, timeout_s=60) as tr:
+        res = tr.run(lambda r: _efb_rank_train(r, 3, learner))
+    assert all(r.ok for r in res), [str(r.error) for r in res]
+    groups = [r.value[0] for r in res]
+    assert len(set(groups)) == 1 and groups[0] < 14, groups
+    assert len({_trees(r.value[1]) for r in res}) == 1

@@ -122,3 +122,28 @@ def test_device_voting_parallel(world, gpu_available, capfd, monkeypatch):
     monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
     _, _, _, host = _run("voting", world, top_k=4)
     assert _splits(out[0][0], 0) == _splits(host[0][0], 0)
+
+
+@pytest.mark.parametrize("learner", ["data", "voting"])
+def test_device_distributed_with_efb_bundles(learner, gpu_available):
+    """Sparse mutually exclusive columns bundled by EFB (rank 0's bundles shared by every rank)
+    under the device data- / voting-parallel learners: identical models on every rank."""
+    rng = np.random.RandomState(17)
+    n, world = 24000, 2
+    X = np.zeros((n, 14))
+    owner = rng.randint(0, 10, n)
+    for j in range(10):
+        X[owner == j, j] = rng.rand((owner == j).sum()) + 0.5
+    X[:, 10:] = rng.randn(n, 4)
+    y = (X[:, 0] + X[:, 4] - X[:, 7] + X[:, 10] + 0.3 * rng.randn(n) > 0.6).astype(np.float64)
+
+    def rank_fn(r):
+        params = dict(BASE, tree_learner=learner, num_machines=world, pre_partition=True, top_k=6)
+        idx = np.arange(r, n, world)
+        bst = lgb.train(params, lgb.Dataset(X[idx], y[idx], params=params), 6)
+        return bst.model_to_string()
+
+    with ThreadRanks(world, timeout_s=120, device_comm=True) as tr:
+        res = tr.run(rank_fn)
+    assert all(r.ok for r in res), [str(r.error) for r in res]
+    assert _trees(res[0].value) == _trees(res[1].value)
