@@ -620,6 +620,13 @@ void GPUTreeLearner::DecideMode() {
   // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
   const auto& ic = config_->interaction_constraints_vector;
   if (!ic.empty() && (ic.size() > 32 || config_->feature_fraction_bynode < 1.0)) dm = false;
+  // intermediate monotone constraints re-bound (and re-scan) leaves all over the tree after a
+  // split: the host loop does that between the device histogram builds
+  if (config_->monotone_constraints_method == "intermediate" &&
+      std::any_of(config_->monotone_constraints.begin(), config_->monotone_constraints.end(),
+                  [](int8_t m) { return m != 0; })) {
+    dm = false;
+  }
   // voting: per-node sampling and extra_trees draws stay with the host voting loop
   if (voting_ && (config_->feature_fraction_bynode < 1.0 || config_->extra_trees)) dm = false;
   if (has_forced_split_ ||

@@ -44,13 +44,10 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool /*is_constant_hessi
   data_ = train_data;
   num_data_ = data_->num_data();
   num_features_ = data_->num_features();
-  if (config_->monotone_constraints_method == "intermediate") {
-    Log::Warning("monotone_constraints_method=intermediate is handled with the basic method by this learner");
-  }
   InitFeatureMeta();
   col_sampler_.SetTrainingData(data_);
   best_split_per_leaf_.assign(config_->num_leaves, SplitInfo());
-  constraints_.Init(config_->num_leaves);
+  constraints_.Init(config_->num_leaves, config_);
   const size_t total_bins = data_->num_total_bin();
   hist_pool_.assign(config_->num_leaves, std::vector<hist_t>(2 * total_bins, 0.0));
   splittable_.assign(config_->num_leaves, std::vector<char>(num_features_, 1));
@@ -103,7 +100,7 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
     leaf_count_.assign(config_->num_leaves, 0);
   }
   col_sampler_.SetConfig(config_);
-  constraints_.Init(config_->num_leaves);
+  constraints_.Init(config_->num_leaves, config_);
   InitFeatureMeta();
   SetupCegb();
 }
@@ -135,7 +132,7 @@ void SerialTreeLearner::BeforeTrain() {
     for (data_size_t i = 0; i < n; ++i) indices_[i] = i;
   }
   leaf_count_[0] = n;
-  constraints_.Init(config_->num_leaves);
+  constraints_.Init(config_->num_leaves, config_);
   for (auto& s : best_split_per_leaf_) s.Reset();
   double sg = 0, sh = 0;
   if (use_bag_) {
@@ -393,6 +390,7 @@ void SerialTreeLearner::SplitInner(Tree* tree, int best_leaf, int* left_leaf, in
   const int next = tree->NextLeafId();
   const BinMapper* m = data_->FeatureBinMapper(inner);
   const bool is_num = m->bin_type() == BinType::Numerical;
+  constraints_.BeforeSplit(tree, best_leaf, next, s.monotone_type);
   PartitionLeaf(best_leaf, inner, s, next);
   if (update_cnt) {
     s.left_count = leaf_count_[best_leaf];
@@ -427,7 +425,31 @@ void SerialTreeLearner::SplitInner(Tree* tree, int best_leaf, int* left_leaf, in
     smaller_.num_data = smaller_.leaf == *left_leaf ? s.left_count : s.right_count;
     larger_.num_data = larger_.leaf == *left_leaf ? s.left_count : s.right_count;
   }
-  constraints_.Update(is_num, *left_leaf, *right_leaf, s.monotone_type, s.right_output, s.left_output);
+  const auto stale = constraints_.Update(tree, is_num, *left_leaf, *right_leaf, s.monotone_type, s.right_output,
+                                         s.left_output, inner, s, best_split_per_leaf_);
+  for (int leaf : stale) RecomputeBestSplitForLeaf(tree, leaf);
+}
+
+void SerialTreeLearner::RecomputeBestSplitForLeaf(const Tree* tree, int leaf) {
+  SplitInfo& cur = best_split_per_leaf_[leaf];
+  const int slot = leaf;  // a leaf's histogram lives in the pool slot of its id (BeforeFindBestSplit)
+  // the leaf's statistics as its current best split saw them (reference: a fresh LeafSplits,
+  // whose output -- the smoothing parent -- is 0)
+  LeafState ls{leaf, cur.left_count + cur.right_count, cur.left_sum_gradient + cur.right_sum_gradient,
+               cur.left_sum_hessian + cur.right_sum_hessian, 0.0};
+  const auto& bytree = col_sampler_.is_feature_used_bytree();
+  const int depth = tree->leaf_depth(leaf);
+  std::vector<SplitInfo> bests(num_features_);
+#pragma omp parallel for schedule(static)
+  for (int f = 0; f < num_features_; ++f) {
+    if (!bytree[f] || !splittable_[slot][f]) continue;
+    EvalFeature(FeatureHist(slot, f), f, params_, ls, depth, &bests[f]);
+  }
+  SplitInfo best;
+  for (const auto& b : bests) {
+    if (b > best) best = b;
+  }
+  cur = best;
 }
 
 int SerialTreeLearner::ForceSplits(Tree* tree, int* left_leaf, int* right_leaf, int* cur_depth) {

@@ -14,27 +14,10 @@
 #include "lgbm_amd/json.h"
 #include "lgbm_amd/split_info.h"
 #include "lgbm_amd/tree_learner.h"
+#include "monotone_constraints.h"
 #include "split_finder.h"
 
 namespace lgbm_amd {
-
-// per-leaf monotone bounds ("basic" method, reference monotone_constraints.hpp:98-145)
-struct LeafConstraints {
-  std::vector<ConstraintRange> entries;
-  void Init(int n) { entries.assign(n, ConstraintRange{-std::numeric_limits<double>::max(), std::numeric_limits<double>::max()}); }
-  void Update(bool is_numerical, int leaf, int new_leaf, int8_t mono, double right_out, double left_out) {
-    entries[new_leaf] = entries[leaf];
-    if (!is_numerical) return;
-    double mid = (left_out + right_out) / 2.0f;
-    if (mono < 0) {
-      entries[leaf].min = std::max(entries[leaf].min, mid);
-      entries[new_leaf].max = std::min(entries[new_leaf].max, mid);
-    } else if (mono > 0) {
-      entries[leaf].max = std::min(entries[leaf].max, mid);
-      entries[new_leaf].min = std::max(entries[new_leaf].min, mid);
-    }
-  }
-};
 
 double MonotoneSplitPenalty(int depth, double penalization);
 
@@ -91,6 +74,9 @@ class SerialTreeLearner : public TreeLearner {
   void SplitInner(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf, bool update_cnt);
   hist_t* FeatureHist(int slot, int inner) { return hist_pool_[slot].data() + 2 * data_->FeatureHistOffset(inner); }
   void InitFeatureMeta();
+  // intermediate monotone constraints: a leaf whose bounds another split tightened gets its
+  // best split recomputed from its stored histogram (reference RecomputeBestSplitForLeaf)
+  void RecomputeBestSplitForLeaf(const Tree* tree, int leaf);
   std::vector<int8_t> GroupsUsed(const std::vector<int8_t>& feature_used) const;
 
   const Config* config_;
@@ -104,10 +90,9 @@ class SerialTreeLearner : public TreeLearner {
   LeafConstraints constraints_;
   std::vector<SplitInfo> best_split_per_leaf_;
 
-  // histogram pool: one full histogram per slot, slot_of_leaf_ maps leaves to slots
+  // histogram pool: one full histogram per leaf id (the parent's moves to its larger child)
   std::vector<std::vector<hist_t>> hist_pool_;
   std::vector<std::vector<char>> splittable_;  // per slot, per inner feature
-  std::vector<int> slot_of_leaf_;
   int smaller_slot_ = -1, larger_slot_ = -1;
   bool has_parent_hist_ = false;
   LeafState smaller_, larger_;

@@ -326,6 +326,34 @@ def test_monotone_constraints():
         assert np.all(np.diff(dec) <= 1e-12)
 
 
+@pytest.mark.parametrize("method", ["basic", "intermediate"])
+def test_monotone_constraints_methods(method):
+    """Both methods give predictions monotone in the constrained features at any values of the
+    others (reference test_engine.py test_monotone_constraints); the intermediate method
+    (bounds from neighbouring leaves' outputs, leaves re-scanned when their bounds tighten)
+    fits the training data at least about as well as the basic one's mid-point bounds."""
+    rng = np.random.RandomState(1)
+    n = 4000
+    X = rng.rand(n, 3)
+    y = (5 * X[:, 0] + np.sin(10 * np.pi * X[:, 0]) - 5 * X[:, 1] - np.cos(10 * np.pi * X[:, 1])
+         + 2 * np.sin(6 * X[:, 2]) + rng.rand(n) * 0.01)
+    params = {"verbose": -1, "monotone_constraints": [1, -1, 0], "min_data": 20, "num_leaves": 31,
+              "monotone_constraints_method": method}
+    gbm = lgb.train(params, lgb.Dataset(X, y), num_boost_round=40)
+    grid = np.linspace(0, 1, 60)
+    for base in rng.rand(12, 3):
+        for f, sign in ((0, 1), (1, -1)):
+            pts = np.tile(base, (60, 1))
+            pts[:, f] = grid
+            d = np.diff(gbm.predict(pts)) * sign
+            assert np.all(d >= -1e-12), (method, f)
+    l2 = np.mean((gbm.predict(X) - y) ** 2)
+    basic = lgb.train(dict(params, monotone_constraints_method="basic"), lgb.Dataset(X, y), num_boost_round=40)
+    assert l2 <= np.mean((basic.predict(X) - y) ** 2) * 1.02
+    if method == "intermediate":
+        assert gbm.model_to_string() != basic.model_to_string()
+
+
 def test_max_bin_by_feature():
     X = np.column_stack([np.arange(100), np.arange(100) % 7]).astype(float)
     y = np.arange(100, dtype=float)

@@ -432,3 +432,27 @@ def test_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
     # and the fit matches the CPU learner's extra-trees model in quality
     cpu = _train(X, y, "cpu", rounds=6, extra_trees=True, **extra)
     assert abs(_auc(y, models["device"].predict(X)) - _auc(y, cpu.predict(X))) < 0.01
+
+
+def test_intermediate_monotone_on_gpu(gpu_available):
+    """monotone_constraints_method=intermediate runs host-assisted (leaves re-bounded and
+    re-scanned across the tree after each split) on device histograms: monotone predictions
+    and the CPU learner's first tree."""
+    rng = np.random.RandomState(1)
+    n = 6000
+    X = rng.rand(n, 3)
+    y = (5 * X[:, 0] + np.sin(10 * np.pi * X[:, 0]) - 5 * X[:, 1] - np.cos(10 * np.pi * X[:, 1])
+         + 2 * np.sin(6 * X[:, 2]) + rng.rand(n) * 0.01)
+    params = {"verbose": -1, "monotone_constraints": [1, -1, 0], "min_data": 20, "num_leaves": 31,
+              "monotone_constraints_method": "intermediate", "max_bin": 63}
+    gpu = lgb.train(dict(params, device_type="gpu"), lgb.Dataset(X, y), 20)
+    cpu = lgb.train(dict(params, device_type="cpu"), lgb.Dataset(X, y), 20)
+    grid = np.linspace(0, 1, 40)
+    for base in rng.rand(6, 3):
+        for f, sign in ((0, 1), (1, -1)):
+            pts = np.tile(base, (40, 1))
+            pts[:, f] = grid
+            assert np.all(np.diff(gpu.predict(pts)) * sign >= -1e-12)
+    assert _splits(gpu.dump_model()["tree_info"][0]["tree_structure"]) == \
+        _splits(cpu.dump_model()["tree_info"][0]["tree_structure"])
+    assert np.corrcoef(gpu.predict(X), cpu.predict(X))[0, 1] > 0.999
