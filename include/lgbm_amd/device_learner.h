@@ -60,8 +60,10 @@ class DeviceTreeLearner {
   virtual void ValidMultiply(int slot, double v, int tree_id) = 0;
   virtual void ValidAddTree(int slot, const Tree* tree, int tree_id) = 0;
   virtual void ValidScoreToHost(int slot, double* host) = 0;
-  // a metric on the device-resident scores of a validation set; false: evaluate on the host
-  virtual bool ValidEval(int slot, const DeviceMetricSpec& spec, double* out) = 0;
+  // a metric on the device-resident scores of a validation set: the raw sums of
+  // DeviceMetricSpec::nout values (Metric::FinishDevice turns them into the metric's values);
+  // false: evaluate on the host
+  virtual bool ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) = 0;
 
   // test support (tests/test_gpu_kernels.py): the state the last device-grown tree left in HBM.
   // A leaf's rows (partition), its raw fixed-point histogram slot, which histogram bins are

@@ -16,12 +16,26 @@ namespace lgbm_amd {
 // a metric the device learner can evaluate on device-resident validation scores
 // (kind: src/device/kernels.h kMetric*; 0 = host only)
 struct DeviceMetricSpec {
-  int kind = 0;
-  int convert = 0;  // score -> prediction: 0 identity, 1 sigmoid, 2 sign(s) * s^2
+  int kind = 0;     // dev::kMetric* (0: evaluate on the host)
+  int convert = 0;  // score -> prediction: 0 identity, 1 sigmoid, 2 sign(s) * s^2, 3 exp,
+                    // 4 softmax over the classes, 5 sigmoid per class
   double sigmoid = 1.0;
-  double sum_weights = 0.0;
+  double param = 0.0;  // alpha (quantile / huber), fair_c, tweedie_variance_power
+  int num_class = 1;   // multiclass metrics: class-major scores
+  int top_k = 1;       // multi_error@k
+  int nout = 1;        // sums the device returns (Metric::FinishDevice turns them into values)
   const label_t* label = nullptr;  // host pointers, uploaded once per validation set
   const label_t* weights = nullptr;
+  // query metrics (NDCG / MAP): boundaries, weights, eval_at, per-query constants ([nq][nk]
+  // inverse max DCG, or [nq] relevant documents) and the DCG tables; `key` identifies the
+  // metric whose device copies they are
+  const void* key = nullptr;
+  const data_size_t* qb = nullptr;
+  int nq = 0;
+  const label_t* qw = nullptr;
+  std::vector<int> eval_at;
+  std::vector<double> qconst;
+  std::vector<double> label_gain, discount;
 };
 
 class Metric {
@@ -31,6 +45,8 @@ class Metric {
     (void)objective;
     return DeviceMetricSpec();
   }
+  // the metric's values from the sums the device evaluation returned (DeviceSpec().nout)
+  virtual std::vector<double> FinishDevice(const std::vector<double>& sums) const { return sums; }
   virtual ~Metric() = default;
   virtual void Init(const Metadata& metadata, data_size_t num_data) = 0;
   virtual const std::vector<std::string>& GetName() const = 0;

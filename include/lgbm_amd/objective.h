@@ -72,7 +72,8 @@ class ObjectiveFunction {
   virtual data_size_t NumPositiveData() const { return 0; }
   virtual void ConvertOutput(const double* input, double* output) const { output[0] = input[0]; }
   // ConvertOutput as a device-evaluable form: 0 identity, 1 sigmoid(*param * s),
-  // 2 sign(s) * s^2 (regression with reg_sqrt); -1 other (host only)
+  // 2 sign(s) * s^2 (regression with reg_sqrt), 3 exp(s), 4 softmax over the classes,
+  // 5 sigmoid(*param * s) per class; -1 other (host only)
   virtual int DeviceOutputKind(double* param) const {
     (void)param;
     return -1;

@@ -85,10 +85,11 @@ def gradients(params, score, label, weight=None):
 
 
 def metric(params, score, label, weight=None):
-    """Value of ``params["metric"]`` on raw GPU scores (float64 ``[n]``), with the output
-    transform of ``params["objective"]`` (e.g. sigmoid for binary)."""
+    """Value of ``params["metric"]`` on raw GPU scores (float64 ``[n]``, or class-major
+    ``[num_class, n]`` for multiclass metrics), with the output transform of
+    ``params["objective"]`` (e.g. sigmoid for binary, softmax for multiclass)."""
     torch = _torch()
-    n = score.shape[0]
+    n = score.shape[-1]
     lab, lab_p = _host_f32(label, n, "label")
     w, w_p = _host_f32(weight, n, "weight")
     out = ctypes.c_double(0.0)

@@ -389,10 +389,12 @@ data_size_t GBDT::DeviceBagging(bool goss) {
 std::vector<double> GBDT::EvalValid(int i, int j) const {
   const Metric* m = valid_metrics_[i][j];
   const int slot = valid_score_updater_[i]->device_slot();
-  if (slot >= 0 && device_learner_ != nullptr) {
+  const char* hm = std::getenv("LGBM_AMD_HOST_METRICS");  // =1: every metric on the host (A/B)
+  const bool host_metrics = hm != nullptr && hm[0] == '1';
+  if (slot >= 0 && device_learner_ != nullptr && !host_metrics) {
     const DeviceMetricSpec spec = m->DeviceSpec(objective_);
-    double v = 0.0;
-    if (spec.kind != 0 && device_learner_->ValidEval(slot, spec, &v)) return {v};
+    std::vector<double> sums;
+    if (spec.kind != 0 && device_learner_->ValidEval(slot, spec, &sums)) return m->FinishDevice(sums);
   }
   return m->Eval(valid_score_updater_[i]->score(), objective_);
 }
@@ -691,8 +693,8 @@ std::vector<double> GBDT::GetEvalAt(int data_idx) {
     }
   } else {
     const int i = data_idx - 1;
-    for (auto* m : valid_metrics_[i]) {
-      for (double v : m->Eval(valid_score_updater_[i]->score(), objective_)) ret.push_back(v);
+    for (size_t j = 0; j < valid_metrics_[i].size(); ++j) {
+      for (double v : EvalValid(i, static_cast<int>(j))) ret.push_back(v);  // device-resident scores when possible
     }
   }
   return ret;

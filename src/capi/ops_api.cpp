@@ -150,27 +150,25 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpMetric(const char* params, const float* label, c
     if (spec.kind == 0) Log::Fatal("op metric: '%s' has no device kernel for this objective", c.metric[0].c_str());
     Scratch sc;
     dev::MetricArgs a;
+    std::memset(&a, 0, sizeof(a));
     a.kind = spec.kind;
     a.convert = spec.convert;
     a.sigmoid = spec.sigmoid;
+    a.param = spec.param;
+    a.num_class = spec.num_class;
+    a.top_k = spec.top_k;
     a.n = n;
     a.score = d_score;
     a.label = sc.Upload(spec.label, n);
     a.weights = sc.Upload(spec.weights, n);
     a.scratch = sc.Alloc<char>(dev::MetricScratchBytes(n));
+    if (spec.kind == dev::kMetricNDCG || spec.kind == dev::kMetricMAP) Log::Fatal("op metric: query metrics need queries");
     a.out = sc.Alloc<double>(2);
     dev::EvalMetric(a, nullptr);
     OPCHECK(hipGetLastError());
-    double h[2] = {0.0, 0.0};
-    OPCHECK(hipMemcpy(h, a.out, sizeof(h), hipMemcpyDeviceToHost));
-    const double sw = spec.sum_weights;
-    if (spec.kind == dev::kMetricAUC) {
-      *out = (h[1] > 0.0 && h[1] != sw) ? h[0] / (h[1] * (sw - h[1])) : 1.0;
-    } else if (spec.kind == dev::kMetricRMSE) {
-      *out = std::sqrt(h[0] / sw);
-    } else {
-      *out = h[0] / sw;
-    }
+    std::vector<double> h(2, 0.0);
+    OPCHECK(hipMemcpy(h.data(), a.out, sizeof(double) * 2, hipMemcpyDeviceToHost));
+    *out = m->FinishDevice(h)[0];
   });
 }
 

@@ -298,19 +298,32 @@ void PredictForest(const ForestArgs& f, hipStream_t s);
 
 // validation metrics on device scores (one model per iteration)
 constexpr int kMetricL2 = 1, kMetricRMSE = 2, kMetricL1 = 3, kMetricBinLogloss = 4, kMetricBinError = 5,
-              kMetricAUC = 6;
+              kMetricAUC = 6, kMetricQuantile = 7, kMetricHuber = 8, kMetricFair = 9, kMetricPoisson = 10,
+              kMetricMape = 11, kMetricGamma = 12, kMetricGammaDeviance = 13, kMetricTweedie = 14, kMetricXent = 15,
+              kMetricMultiLogloss = 20, kMetricMultiError = 21, kMetricNDCG = 30, kMetricMAP = 31;
 struct MetricArgs {
   int32_t kind;
-  int32_t convert;       // score -> prediction: 0 identity, 1 sigmoid(sigmoid * s), 2 sign(s) * s^2
+  int32_t convert;       // score -> prediction: 0 identity, 1 sigmoid(sigmoid * s), 2 sign(s) * s^2, 3 exp,
+                         // 4 softmax over the classes, 5 sigmoid per class
   double sigmoid;
+  double param;          // alpha (quantile, huber), fair_c, tweedie_variance_power
   int64_t n;
-  const double* score;
+  const double* score;   // [num_class][n]
   const float* label;
   const float* weights;  // may be null
-  void* scratch;         // MetricScratchBytes(n)
-  double* out;           // [0] weighted loss sum (or AUC accumulator), [1] AUC positive weight
+  int32_t num_class, top_k;
+  // query metrics: per query [nk] values, summed over queries in fixed order
+  int32_t nq, nk;
+  const int32_t* qb;       // [nq + 1]
+  const float* qw;         // [nq] or null
+  const int32_t* eval_at;  // [nk]
+  const double* qconst;    // NDCG: [nq][nk] 1 / max DCG (<= 0: no relevant document); MAP: [nq] relevant documents
+  const double* label_gain;
+  const double* discount;  // [kRankMaxDocs]
+  void* scratch;         // MetricScratchBytes(n, nq * nk)
+  double* out;           // [0] weighted loss sum (or AUC accumulator), [1] AUC positive weight; query: [nk]
 };
-size_t MetricScratchBytes(int64_t n);
+size_t MetricScratchBytes(int64_t n, int64_t query_values = 0);
 void EvalMetric(const MetricArgs& m, hipStream_t s);
 
 int GradientBlocks(int64_t n);

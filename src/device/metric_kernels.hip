@@ -22,11 +22,16 @@ constexpr double kEps = 1e-15f;  // kEpsilon
 __device__ __forceinline__ double ConvertScore(const MetricArgs& m, double s) {
   if (m.convert == 1) return 1.0f / (1.0f + exp(-m.sigmoid * s));
   if (m.convert == 2) return (s > 0.0 ? 1.0 : (s < 0.0 ? -1.0 : 0.0)) * s * s;
+  if (m.convert == 3) return exp(s);
   return s;
 }
 
-__device__ __forceinline__ double PointLoss(int kind, double y, double p) {
-  switch (kind) {
+__device__ __forceinline__ double SafeLog(double x) { return x > 0 ? log(x) : -INFINITY; }
+
+// the per-row losses of src/metric/metrics.cpp (reference regression_metric.hpp,
+// binary_metric.hpp, xentropy_metric.hpp), with their float-literal constants
+__device__ __forceinline__ double PointLoss(const MetricArgs& m, double y, double p) {
+  switch (m.kind) {
     case kMetricL2:
     case kMetricRMSE:
       return (p - y) * (p - y);
@@ -37,17 +42,87 @@ __device__ __forceinline__ double PointLoss(int kind, double y, double p) {
       return p > kEps ? -log(p) : -log(kEps);
     case kMetricBinError:
       return p <= 0.5f ? (y > 0 ? 1.0 : 0.0) : (y <= 0 ? 1.0 : 0.0);
+    case kMetricQuantile: {
+      const double d = y - p;
+      return d < 0 ? (m.param - 1.0f) * d : m.param * d;
+    }
+    case kMetricHuber: {
+      const double d = p - y;
+      return fabs(d) <= m.param ? 0.5f * d * d : m.param * (fabs(d) - 0.5f * m.param);
+    }
+    case kMetricFair: {
+      const double x = fabs(p - y), c = m.param;
+      return c * x - c * c * log(1.0f + x / c);
+    }
+    case kMetricPoisson: {
+      const double e = 1e-10f;
+      const double s = p < e ? e : p;
+      return s - y * log(s);
+    }
+    case kMetricMape:
+      return fabs(y - p) / fmax(1.0f, fabs(y));
+    case kMetricGamma: {
+      const double theta = -1.0 / p;
+      const double b = -SafeLog(-theta);
+      const double c = SafeLog(y) - SafeLog(y);  // 1/psi * log(y/psi) - log(y), psi = 1
+      return -((y * theta - b) + c);
+    }
+    case kMetricGammaDeviance: {
+      const double t = y / (p + 1.0e-9);
+      return t - SafeLog(t) - 1;
+    }
+    case kMetricTweedie: {
+      const double rho = m.param, e = 1e-10f;
+      const double s = p < e ? e : p;
+      return -y * exp((1 - rho) * log(s)) / (1 - rho) + exp((2 - rho) * log(s)) / (2 - rho);
+    }
+    case kMetricXent: {
+      const double e = 1.0e-12;
+      const double a = y * (p > e ? log(p) : log(e));
+      const double b = (1.0f - y) * (1.0f - p > e ? log(1.0f - p) : log(e));
+      return -(a + b);
+    }
     default:
       return 0.0;
   }
 }
 
+// multiclass row loss: converted class scores (softmax / per-class sigmoid / raw), then
+// -log p[label] or the top-k error (a class counts as larger when it is >= the label's)
+__device__ __forceinline__ double MulticlassLoss(const MetricArgs& m, int64_t i) {
+  const int K = m.num_class;
+  const int y = static_cast<int>(m.label[i]);
+  double mx = -INFINITY;
+  if (m.convert == 4) {
+    for (int k = 0; k < K; ++k) mx = fmax(mx, m.score[static_cast<int64_t>(k) * m.n + i]);
+  }
+  double denom = 0.0;
+  if (m.convert == 4) {
+    for (int k = 0; k < K; ++k) denom += exp(m.score[static_cast<int64_t>(k) * m.n + i] - mx);
+  }
+  auto rec = [&](int k) {
+    const double s = m.score[static_cast<int64_t>(k) * m.n + i];
+    if (m.convert == 4) return exp(s - mx) / denom;
+    if (m.convert == 5) return 1.0f / (1.0f + exp(-m.sigmoid * s));
+    return s;
+  };
+  const double ry = rec(y);
+  if (m.kind == kMetricMultiLogloss) return ry > kEps ? -log(ry) : -log(kEps);
+  int larger = 0;
+  for (int k = 0; k < K; ++k) {
+    if (rec(k) >= ry) ++larger;
+    if (larger > m.top_k) return 1.0;
+  }
+  return 0.0;
+}
+
 __global__ __launch_bounds__(kMetricThreads) void k_point_loss(MetricArgs m, double* partials) {
   __shared__ double sh[kMetricThreads / kWave];
   double acc = 0.0;
+  const bool multi = m.kind == kMetricMultiLogloss || m.kind == kMetricMultiError;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(kMetricThreads) + threadIdx.x; i < m.n;
        i += static_cast<int64_t>(gridDim.x) * kMetricThreads) {
-    const double l = PointLoss(m.kind, m.label[i], ConvertScore(m, m.score[i]));
+    const double l = multi ? MulticlassLoss(m, i) : PointLoss(m, m.label[i], ConvertScore(m, m.score[i]));
     acc += m.weights ? l * m.weights[i] : l;
   }
   acc = BlockSum(acc, sh);
@@ -118,6 +193,83 @@ T* Carve(char** p, size_t count) {
   return reinterpret_cast<T*>(q);
 }
 
+// ---------------------------------------------------------------- query metrics
+// one workgroup per query: the documents' stable descending score order as ranks (as in
+// rank_kernels.hip), then the query's NDCG@k / MAP@k for every k into partials[q][nk]
+constexpr int kQueryThreads = 128;
+
+__device__ __forceinline__ double QBlockSum(double v, double* red) {
+  for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  const int w = threadIdx.x / kWave;
+  __syncthreads();
+  if ((threadIdx.x & (kWave - 1)) == 0) red[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < kQueryThreads / kWave; ++i) t += red[i];
+  return t;
+}
+
+__global__ __launch_bounds__(kQueryThreads) void k_query_metric(MetricArgs m, double* partials) {
+  __shared__ double s_score[kRankMaxDocs];
+  __shared__ int s_pos[kRankMaxDocs];
+  __shared__ char s_rel[kRankMaxDocs];
+  __shared__ int s_label[kRankMaxDocs];
+  __shared__ double red[kQueryThreads / kWave];
+  const int q = blockIdx.x;
+  const int b = m.qb[q], cnt = m.qb[q + 1] - b;
+  for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+    s_score[i] = m.score[b + i];
+    s_label[i] = static_cast<int>(m.label[b + i]);
+    s_rel[i] = m.label[b + i] > 0.5f ? 1 : 0;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+    const double si = s_score[i];
+    int p = 0;
+    for (int j = 0; j < cnt; ++j) p += (s_score[j] > si) || (s_score[j] == si && j < i);
+    s_pos[i] = p;
+  }
+  __syncthreads();
+  const double w = m.qw != nullptr ? m.qw[q] : 1.0;
+  for (int kk = 0; kk < m.nk; ++kk) {
+    const int k = min(m.eval_at[kk], cnt);
+    double v = 0.0;
+    if (m.kind == kMetricNDCG) {
+      const double inv = m.qconst[static_cast<int64_t>(q) * m.nk + kk];
+      if (m.qconst[static_cast<int64_t>(q) * m.nk] <= 0.0) {
+        v = threadIdx.x == 0 ? 1.0 : 0.0;  // no relevant document: NDCG 1
+      } else {
+        for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+          if (s_pos[i] < k) v += m.label_gain[s_label[i]] * m.discount[s_pos[i]];
+        }
+        v *= inv;
+      }
+    } else {
+      const int npos = static_cast<int>(m.qconst[q]);
+      // precision at every relevant document ranked within k: (relevant ranked above + 1) / (rank + 1)
+      for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+        if (!s_rel[i] || s_pos[i] >= k) continue;
+        int hits = 0;
+        for (int j = 0; j < cnt; ++j) hits += s_rel[j] && s_pos[j] < s_pos[i];
+        v += static_cast<double>(hits + 1) / (s_pos[i] + 1.0f);
+      }
+      v = npos > 0 ? v / min(npos, k) : (threadIdx.x == 0 ? 1.0 : 0.0);
+    }
+    const double t = QBlockSum(v, red);
+    if (threadIdx.x == 0) partials[static_cast<int64_t>(q) * m.nk + kk] = t * w;
+  }
+}
+
+// one workgroup per k: the queries' values summed in query order (block-strided, then a
+// fixed-shape block sum)
+__global__ __launch_bounds__(kMetricThreads) void k_query_sum(const double* partials, int nq, int nk, double* out) {
+  __shared__ double sh[kMetricThreads / kWave];
+  double acc = 0.0;
+  for (int q = threadIdx.x; q < nq; q += kMetricThreads) acc += partials[static_cast<int64_t>(q) * nk + blockIdx.x];
+  acc = BlockSum(acc, sh);
+  if (threadIdx.x == 0) out[blockIdx.x] = acc;
+}
+
 size_t CubTempBytes(int64_t n) {
   const int nn = static_cast<int>(n);
   size_t a = 0, b = 0, c = 0;
@@ -134,14 +286,21 @@ size_t CubTempBytes(int64_t n) {
 
 }  // namespace
 
-size_t MetricScratchBytes(int64_t n) {
+size_t MetricScratchBytes(int64_t n, int64_t query_values) {
   const size_t un = static_cast<size_t>(std::max<int64_t>(1, n));
-  return 16 * 256 + sizeof(double) * kMetricBlocks + un * (4 * sizeof(double) + 2 * sizeof(int32_t)) +
-         2 * un * sizeof(PosNeg) + 2 * un * sizeof(double) + sizeof(int) + CubTempBytes(n);
+  return 16 * 256 + sizeof(double) * std::max<int64_t>(kMetricBlocks, query_values) +
+         un * (4 * sizeof(double) + 2 * sizeof(int32_t)) + 2 * un * sizeof(PosNeg) + 2 * un * sizeof(double) +
+         sizeof(int) + CubTempBytes(n);
 }
 
 void EvalMetric(const MetricArgs& m, hipStream_t s) {
   char* p = static_cast<char*>(m.scratch);
+  if (m.kind == kMetricNDCG || m.kind == kMetricMAP) {
+    double* qpart = Carve<double>(&p, static_cast<size_t>(std::max(1, m.nq * m.nk)));
+    hipLaunchKernelGGL(k_query_metric, dim3(m.nq), dim3(kQueryThreads), 0, s, m, qpart);
+    hipLaunchKernelGGL(k_query_sum, dim3(m.nk), dim3(kMetricThreads), 0, s, qpart, m.nq, m.nk, m.out);
+    return;
+  }
   double* partials = Carve<double>(&p, kMetricBlocks);
   const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((m.n + kMetricThreads - 1) / kMetricThreads,
                                                                              kMetricBlocks)));

@@ -24,24 +24,31 @@ class PointwiseMetric : public Metric {
   PointwiseMetric(const Config& cfg, const char* name, PointLoss loss, bool convert, double factor)
       : cfg_(cfg), loss_(loss), convert_(convert), factor_(factor) {
     name_.push_back(name);
-    const std::string n(name);
-    device_kind_ = n == "l2" ? 1 : n == "rmse" ? 2 : n == "l1" ? 3 : n == "binary_logloss" ? 4
-                 : n == "binary_error" ? 5 : 0;
+    // device kinds (src/device/kernels.h kMetric*) and the loss parameter they take
+    static const struct { const char* name; int kind; } kinds[] = {
+        {"l2", 1}, {"rmse", 2}, {"l1", 3}, {"binary_logloss", 4}, {"binary_error", 5}, {"quantile", 7},
+        {"huber", 8}, {"fair", 9}, {"poisson", 10}, {"mape", 11}, {"gamma", 12}, {"gamma_deviance", 13},
+        {"tweedie", 14}, {"cross_entropy", 15}, {"kullback_leibler", 15}};
+    for (const auto& k : kinds) {
+      if (std::string(name) == k.name) device_kind_ = k.kind;
+    }
+    device_param_ = device_kind_ == 9 ? cfg.fair_c : device_kind_ == 14 ? cfg.tweedie_variance_power : cfg.alpha;
   }
   DeviceMetricSpec DeviceSpec(const ObjectiveFunction* obj) const override {
     DeviceMetricSpec d;
     if (device_kind_ == 0) return d;
     double param = 1.0;
     const int conv = (convert_ && obj != nullptr) ? obj->DeviceOutputKind(&param) : 0;
-    if (conv < 0) return d;
+    if (conv < 0 || conv > 3) return d;
     d.kind = device_kind_;
     d.convert = conv;
     d.sigmoid = param;
-    d.sum_weights = sum_w_;
+    d.param = device_param_;
     d.label = label_;
     d.weights = weights_;
     return d;
   }
+  std::vector<double> FinishDevice(const std::vector<double>& sums) const override { return {Average(sums[0])}; }
   void Init(const Metadata& md, data_size_t n) override {
     num_data_ = n;
     label_ = md.label();
@@ -72,6 +79,7 @@ class PointwiseMetric : public Metric {
   Config cfg_;
   PointLoss loss_;
   int device_kind_ = 0;
+  double device_param_ = 0.0;
   bool convert_;
   double factor_;
   std::vector<std::string> name_;
@@ -159,10 +167,14 @@ class AUCMetric : public Metric {
   DeviceMetricSpec DeviceSpec(const ObjectiveFunction*) const override {
     DeviceMetricSpec d;
     d.kind = 6;  // AUC ranks raw scores (no output transform)
-    d.sum_weights = sum_w_;
+    d.nout = 2;  // tie-aware accumulator, positive weight
     d.label = label_;
     d.weights = weights_;
     return d;
+  }
+  std::vector<double> FinishDevice(const std::vector<double>& sums) const override {
+    const double pos = sums[1];
+    return {(pos > 0.0 && pos != sum_w_) ? sums[0] / (pos * (sum_w_ - pos)) : 1.0};
   }
   void Init(const Metadata& md, data_size_t n) override {
     num_data_ = n;
@@ -234,6 +246,21 @@ class MulticlassMetric : public Metric {
   }
   const std::vector<std::string>& GetName() const override { return name_; }
   double factor_to_bigger_better() const override { return -1.0; }
+  DeviceMetricSpec DeviceSpec(const ObjectiveFunction* obj) const override {
+    DeviceMetricSpec d;
+    double param = 1.0;
+    const int conv = obj != nullptr ? obj->DeviceOutputKind(&param) : 0;
+    if (conv != 0 && conv != 4 && conv != 5) return d;
+    d.kind = is_error_ ? 21 : 20;
+    d.convert = conv;
+    d.sigmoid = param;
+    d.num_class = num_class_;
+    d.top_k = cfg_.multi_error_top_k;
+    d.label = label_;
+    d.weights = weights_;
+    return d;
+  }
+  std::vector<double> FinishDevice(const std::vector<double>& sums) const override { return {sums[0] / sum_w_}; }
   std::vector<double> Eval(const double* score, const ObjectiveFunction* obj) const override {
     double s = 0;
     const int nk = num_class_;
@@ -362,8 +389,30 @@ class QueryMetricBase : public Metric {
   }
   const std::vector<std::string>& GetName() const override { return name_; }
   double factor_to_bigger_better() const override { return 1.0; }
+  std::vector<double> FinishDevice(const std::vector<double>& sums) const override {
+    std::vector<double> r(sums);
+    for (auto& v : r) v /= sum_qw_;
+    return r;
+  }
 
  protected:
+  DeviceMetricSpec QuerySpec(int kind) const {
+    DeviceMetricSpec d;
+    if (qb_ == nullptr || nq_ <= 0) return d;
+    for (data_size_t q = 0; q < nq_; ++q) {
+      if (qb_[q + 1] - qb_[q] > kDeviceMaxQueryDocs) return d;  // long queries: host
+    }
+    d.kind = kind;
+    d.nout = static_cast<int>(eval_at_.size());
+    d.label = label_;
+    d.key = this;
+    d.qb = qb_;
+    d.nq = nq_;
+    d.qw = qw_;
+    d.eval_at.assign(eval_at_.begin(), eval_at_.end());
+    return d;
+  }
+  static constexpr data_size_t kDeviceMaxQueryDocs = 2048;  // src/device/kernels.h kRankMaxDocs
   std::vector<std::string> name_;
   std::vector<data_size_t> eval_at_;
   data_size_t num_data_ = 0, nq_ = 0;
@@ -394,6 +443,19 @@ class NDCGMetric : public QueryMetricBase {
       DCG::MaxDCG(eval_at_, label_ + qb_[q], qb_[q + 1] - qb_[q], &inv_max_[q]);
       for (auto& v : inv_max_[q]) v = v > 0.0 ? 1.0 / v : -1.0;
     }
+  }
+  DeviceMetricSpec DeviceSpec(const ObjectiveFunction*) const override {
+    DeviceMetricSpec d = QuerySpec(30);
+    if (d.kind == 0) return d;
+    const size_t K = eval_at_.size();
+    d.qconst.resize(static_cast<size_t>(nq_) * K);
+    for (data_size_t q = 0; q < nq_; ++q) {
+      for (size_t j = 0; j < K; ++j) d.qconst[q * K + j] = inv_max_[q][j];
+    }
+    d.label_gain = DCG::label_gain();
+    d.discount.resize(kDeviceMaxQueryDocs);
+    for (data_size_t i = 0; i < kDeviceMaxQueryDocs; ++i) d.discount[i] = DCG::Discount(i);
+    return d;
   }
   std::vector<double> Eval(const double* score, const ObjectiveFunction*) const override {
     const size_t K = eval_at_.size();
@@ -462,6 +524,12 @@ class MapMetric : public QueryMetricBase {
       (*out)[i] = npos > 0 ? sum_ap / std::min(npos, k) : 1.0;
       left = k;
     }
+  }
+  DeviceMetricSpec DeviceSpec(const ObjectiveFunction*) const override {
+    DeviceMetricSpec d = QuerySpec(31);
+    if (d.kind == 0) return d;
+    d.qconst.assign(npos_.begin(), npos_.end());
+    return d;
   }
   std::vector<double> Eval(const double* score, const ObjectiveFunction*) const override {
     const size_t K = eval_at_.size();

@@ -256,7 +256,7 @@ class Poisson : public RegressionL2 {
     }
   }
   void ConvertOutput(const double* in, double* out) const override { out[0] = std::exp(in[0]); }
-  int DeviceOutputKind(double*) const override { return -1; }
+  int DeviceOutputKind(double*) const override { return 3; }
   const char* GetName() const override { return "poisson"; }
   std::string ToString() const override { return GetName(); }
   double BoostFromScore(int) const override { return common::SafeLog(RegressionL2::BoostFromScore(0)); }
@@ -593,6 +593,7 @@ class MulticlassSoftmax : public ObjectiveFunction {
     }
   }
   void ConvertOutput(const double* in, double* out) const override { common::Softmax(in, out, num_class_); }
+  int DeviceOutputKind(double*) const override { return 4; }
   const char* GetName() const override { return "multiclass"; }
   std::string ToString() const override {
     std::stringstream s;
@@ -651,6 +652,10 @@ class MulticlassOVA : public ObjectiveFunction {
   const char* GetName() const override { return "multiclassova"; }
   void ConvertOutput(const double* in, double* out) const override {
     for (int k = 0; k < num_class_; ++k) out[k] = 1.0f / (1.0f + std::exp(-sigmoid_ * in[k]));
+  }
+  int DeviceOutputKind(double* param) const override {
+    *param = sigmoid_;
+    return 5;
   }
   std::string ToString() const override {
     std::stringstream s;
@@ -713,6 +718,10 @@ class CrossEntropy : public ObjectiveFunction {
   }
   const char* GetName() const override { return "cross_entropy"; }
   void ConvertOutput(const double* in, double* out) const override { out[0] = 1.0f / (1.0f + std::exp(-in[0])); }
+  int DeviceOutputKind(double* param) const override {
+    *param = 1.0;
+    return 1;
+  }
   std::string ToString() const override { return GetName(); }
   double BoostFromScore(int) const override {
     double sl = 0, sw = 0;

@@ -1383,9 +1383,13 @@ void GPUTreeLearner::ValidAddTree(int slot, const Tree* tree, int k) {
   HIPCHECK(hipStreamSynchronize(stream_));  // staging buffers are reused by the next tree
 }
 
-bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, double* out) {
+bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) {
   ValidSet& vs = valid_[slot];
-  if (spec.kind == 0 || vs.ntpi != 1 || spec.label == nullptr || vs.num_data <= 0) return false;
+  if (spec.kind == 0 || spec.label == nullptr || vs.num_data <= 0) return false;
+  const bool multi = spec.kind == dev::kMetricMultiLogloss || spec.kind == dev::kMetricMultiError;
+  const bool query = spec.kind == dev::kMetricNDCG || spec.kind == dev::kMetricMAP;
+  if (vs.ntpi != (multi ? spec.num_class : 1)) return false;
+  if (query && (spec.qb == nullptr || spec.nq <= 0 || spec.eval_at.empty())) return false;
   HIPCHECK(hipSetDevice(device_id_));
   const size_t n = static_cast<size_t>(vs.num_data);
   auto dev_alloc = [&](size_t bytes) {
@@ -1394,43 +1398,73 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, double* o
     valid_allocs_.push_back(p);
     return p;
   };
+  auto upload = [&](const void* src, size_t bytes) {
+    void* d = dev_alloc(bytes);
+    if (bytes > 0) HIPCHECK(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice));
+    return d;
+  };
   if (vs.label == nullptr) {
-    vs.label = static_cast<float*>(dev_alloc(sizeof(float) * n));
-    HIPCHECK(hipMemcpy(vs.label, spec.label, sizeof(float) * n, hipMemcpyHostToDevice));
-    if (spec.weights != nullptr) {
-      vs.weights = static_cast<float*>(dev_alloc(sizeof(float) * n));
-      HIPCHECK(hipMemcpy(vs.weights, spec.weights, sizeof(float) * n, hipMemcpyHostToDevice));
-    }
-    vs.metric_out = static_cast<double*>(dev_alloc(sizeof(double) * 2));
+    vs.label = static_cast<float*>(upload(spec.label, sizeof(float) * n));
+    if (spec.weights != nullptr) vs.weights = static_cast<float*>(upload(spec.weights, sizeof(float) * n));
+    vs.metric_out = static_cast<double*>(dev_alloc(sizeof(double) * 64));
   }
-  if (spec.kind == dev::kMetricAUC && vs.metric_scratch == nullptr) {
-    vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(vs.num_data));
-  } else if (vs.metric_scratch == nullptr) {
-    vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(0));
-  }
+  if (spec.nout > 64) return false;
   dev::MetricArgs m;
+  std::memset(&m, 0, sizeof(m));
+  if (query) {
+    // the metric's query inputs, uploaded on its first evaluation
+    auto it = vs.queries.find(spec.key);
+    if (it == vs.queries.end()) {
+      ValidSet::QueryInputs qi;
+      std::vector<int32_t> qb(spec.qb, spec.qb + spec.nq + 1);
+      qi.qb = static_cast<int32_t*>(upload(qb.data(), sizeof(int32_t) * qb.size()));
+      if (spec.qw != nullptr) qi.qw = static_cast<float*>(upload(spec.qw, sizeof(float) * spec.nq));
+      std::vector<int32_t> at(spec.eval_at.begin(), spec.eval_at.end());
+      qi.eval_at = static_cast<int32_t*>(upload(at.data(), sizeof(int32_t) * at.size()));
+      qi.qconst = static_cast<double*>(upload(spec.qconst.data(), sizeof(double) * spec.qconst.size()));
+      qi.label_gain = static_cast<double*>(upload(spec.label_gain.data(), sizeof(double) * spec.label_gain.size()));
+      qi.discount = static_cast<double*>(upload(spec.discount.data(), sizeof(double) * spec.discount.size()));
+      qi.scratch = dev_alloc(dev::MetricScratchBytes(0, static_cast<int64_t>(spec.nq) * spec.eval_at.size()));
+      it = vs.queries.emplace(spec.key, qi).first;
+    }
+    const ValidSet::QueryInputs& qi = it->second;
+    m.nq = spec.nq;
+    m.nk = static_cast<int32_t>(spec.eval_at.size());
+    m.qb = qi.qb;
+    m.qw = qi.qw;
+    m.eval_at = qi.eval_at;
+    m.qconst = qi.qconst;
+    m.label_gain = qi.label_gain;
+    m.discount = qi.discount;
+    m.scratch = qi.scratch;
+  } else {
+    if (spec.kind == dev::kMetricAUC && vs.metric_scratch_rows < vs.num_data) {
+      vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(vs.num_data));
+      vs.metric_scratch_rows = vs.num_data;
+    } else if (vs.metric_scratch == nullptr) {
+      vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(0));
+    }
+    m.scratch = vs.metric_scratch;
+  }
   m.kind = spec.kind;
   m.convert = spec.convert;
   m.sigmoid = spec.sigmoid;
+  m.param = spec.param;
   m.n = vs.num_data;
   m.score = vs.score;
   m.label = vs.label;
   m.weights = vs.weights;
-  m.scratch = vs.metric_scratch;
+  m.num_class = spec.num_class;
+  m.top_k = spec.top_k;
   m.out = vs.metric_out;
   dev::EvalMetric(m, stream_);
-  double h[2] = {0.0, 0.0};
-  HIPCHECK(hipMemcpyAsync(h, vs.metric_out, sizeof(double) * 2, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  const double sw = spec.sum_weights;
-  if (spec.kind == dev::kMetricAUC) {
-    const double sum_pos = h[1];
-    *out = (sum_pos > 0.0 && sum_pos != sw) ? h[0] / (sum_pos * (sw - sum_pos)) : 1.0;
-  } else if (spec.kind == dev::kMetricRMSE) {
-    *out = std::sqrt(h[0] / sw);
-  } else {
-    *out = h[0] / sw;
+  if (vs.logged_kinds.insert(spec.kind).second) {
+    Log::Debug("device metric (kind %d) on validation set %d", spec.kind, slot);
   }
+  sums->assign(std::max(2, spec.nout), 0.0);
+  HIPCHECK(hipMemcpyAsync(sums->data(), vs.metric_out, sizeof(double) * sums->size(), hipMemcpyDeviceToHost,
+                          stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
   return true;
 }
 

@@ -19,6 +19,8 @@
 
 #include <memory>
 #include <string>
+#include <set>
+#include <unordered_map>
 #include <vector>
 
 #include "../device/kernels.h"
@@ -75,7 +77,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void ValidMultiply(int slot, double v, int tree_id) override;
   void ValidAddTree(int slot, const Tree* tree, int tree_id) override;
   void ValidScoreToHost(int slot, double* host) override;
-  bool ValidEval(int slot, const DeviceMetricSpec& spec, double* out) override;
+  bool ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) override;
   bool DebugLeafState(const Tree* tree, int leaf, std::vector<int32_t>* rows, std::vector<long long>* hist,
                       std::vector<int8_t>* bin_valid, double* sums) override;
   bool DebugGradients(std::vector<float>* g, std::vector<float>* h, double* scales) override;
@@ -240,7 +242,19 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
     float* label = nullptr;    // metric inputs, uploaded on the first device evaluation
     float* weights = nullptr;
     void* metric_scratch = nullptr;
+    data_size_t metric_scratch_rows = 0;  // rows metric_scratch is sized for (AUC)
     double* metric_out = nullptr;
+    struct QueryInputs {  // one query metric's device inputs (NDCG / MAP)
+      int32_t* qb = nullptr;
+      float* qw = nullptr;
+      int32_t* eval_at = nullptr;
+      double* qconst = nullptr;
+      double* label_gain = nullptr;
+      double* discount = nullptr;
+      void* scratch = nullptr;
+    };
+    std::unordered_map<const void*, QueryInputs> queries;
+    std::set<int> logged_kinds;  // metric kinds evaluated here so far (debug log)
   };
   std::vector<ValidSet> valid_;
   std::vector<void*> valid_allocs_;

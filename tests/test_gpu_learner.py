@@ -456,3 +456,52 @@ def test_intermediate_monotone_on_gpu(gpu_available):
     assert _splits(gpu.dump_model()["tree_info"][0]["tree_structure"]) == \
         _splits(cpu.dump_model()["tree_info"][0]["tree_structure"])
     assert np.corrcoef(gpu.predict(X), cpu.predict(X))[0, 1] > 0.999
+
+
+
+@pytest.mark.parametrize("task", ["lambdarank", "multiclass", "regression_family"])
+def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, capfd):
+    """Validation metrics evaluated on device-resident scores (NDCG / MAP one workgroup per
+    query, multiclass on class-major scores, point-wise regression losses) equal the host
+    evaluation of the same model (LGBM_AMD_HOST_METRICS=1 forces it)."""
+    rng = np.random.RandomState(3)
+    n, nv = 8000, 3000
+    X, Xv = rng.randn(n, 8), rng.randn(nv, 8)
+    if task == "lambdarank":
+        y = np.clip(np.round(X[:, 0] + X[:, 1] + rng.randn(n)), 0, 4)
+        yv = np.clip(np.round(Xv[:, 0] + Xv[:, 1] + rng.randn(nv)), 0, 4)
+        group, gv = [40] * (n // 40), [30] * (nv // 30)
+        params = {"objective": "lambdarank", "metric": ["ndcg", "map"], "eval_at": [1, 3, 5, 10]}
+    elif task == "multiclass":
+        y = (np.argmax(X[:, :4] + 0.5 * rng.randn(n, 4), axis=1)).astype(float)
+        yv = (np.argmax(Xv[:, :4] + 0.5 * rng.randn(nv, 4), axis=1)).astype(float)
+        group = gv = None
+        params = {"objective": "multiclass", "num_class": 4, "metric": ["multi_logloss", "multi_error"],
+                  "multi_error_top_k": 2}
+    else:
+        y = np.exp(0.3 * X[:, 0]) + rng.rand(n)
+        yv = np.exp(0.3 * Xv[:, 0]) + rng.rand(nv)
+        group = gv = None
+        params = {"objective": "poisson", "metric": ["poisson", "gamma_deviance", "quantile", "huber", "mape"]}
+    params.update({"verbose": -1, "device_type": "gpu", "num_leaves": 15, "seed": 1})
+
+    def run():
+        ds = lgb.Dataset(X, y, group=group, params=params)
+        dv = ds.create_valid(Xv, yv, group=gv)
+        res = {}
+        lgb.train(params, ds, 6, valid_sets=[dv], valid_names=["v"], evals_result=res, verbose_eval=False)
+        return res["v"]
+
+    capfd.readouterr()
+    params["verbose"] = 2
+    dev = run()
+    logged = capfd.readouterr().out
+    kinds = {"lambdarank": (30, 31), "multiclass": (20, 21), "regression_family": (10, 13, 7, 8, 11)}[task]
+    for k in kinds:  # the device path ran
+        assert "device metric (kind %d)" % k in logged, k
+    params["verbose"] = -1
+    monkeypatch.setenv("LGBM_AMD_HOST_METRICS", "1")
+    host = run()
+    assert set(dev) == set(host) and len(dev) >= 2
+    for name in dev:
+        np.testing.assert_allclose(dev[name], host[name], rtol=1e-9, atol=1e-12, err_msg=name)

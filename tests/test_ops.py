@@ -198,3 +198,72 @@ def test_goss_keeps_top_rows_and_rescales(gpu_available):
         np.testing.assert_allclose(gn[small], g0[small] * mult, rtol=1e-6)
         np.testing.assert_allclose(hn[small], h0[small] * mult, rtol=1e-6)
         np.testing.assert_array_equal(gn[top], g0[top])
+
+
+def test_regression_family_metrics_match_torch(gpu_available):
+    """Point-wise regression / cross-entropy metrics on device scores (with their objective's
+    output transform) against float64 torch references of the reference formulas
+    (regression_metric.hpp, xentropy_metric.hpp)."""
+    from lightgbmv1_amd import ops
+    s, y, w = _data(seed=3, kind="reg")
+    sp, yp, _ = _data(seed=4, kind="pos")
+    sq, yq, _ = _data(seed=5, kind="prob")
+    tw = _t(w)
+
+    def wmean(v):
+        return float((v * tw).sum() / tw.sum())
+
+    ts, ty = _t(s), _t(y)
+    cases = []
+    d = ty - ts
+    cases.append(({"metric": "quantile", "objective": "quantile", "alpha": 0.7}, s, y,
+                  wmean(torch.where(d < 0, (0.7 - 1) * d, 0.7 * d))))
+    d = ts - ty
+    cases.append(({"metric": "huber", "objective": "huber", "alpha": 0.9}, s, y,
+                  wmean(torch.where(d.abs() <= 0.9, 0.5 * d * d, 0.9 * (d.abs() - 0.45)))))
+    x = (ts - ty).abs()
+    cases.append(({"metric": "fair", "objective": "fair", "fair_c": 1.3}, s, y,
+                  wmean(1.3 * x - 1.3 * 1.3 * torch.log1p(x / 1.3))))
+    cases.append(({"metric": "mape", "objective": "mape"}, s, y,
+                  wmean((ty - ts).abs() / torch.clamp(ty.abs(), min=1.0))))
+    p, typ = torch.exp(_t(sp)), _t(yp)
+    cases.append(({"metric": "poisson", "objective": "poisson"}, sp, yp, wmean(p - typ * torch.log(p))))
+    cases.append(({"metric": "gamma", "objective": "gamma"}, sp, yp, wmean(typ / p + torch.log(p))))
+    t = typ / (p + 1e-9)
+    cases.append(({"metric": "gamma_deviance", "objective": "gamma"}, sp, yp,
+                  2 * float(((t - torch.log(t) - 1) * tw).sum())))
+    r = 1.5
+    cases.append(({"metric": "tweedie", "objective": "tweedie", "tweedie_variance_power": r}, sp, yp,
+                  wmean(-typ * p ** (1 - r) / (1 - r) + p ** (2 - r) / (2 - r))))
+    pq, tyq = torch.sigmoid(_t(sq)), _t(yq)
+    xent = -(tyq * torch.log(pq.clamp_min(1e-12)) + (1 - tyq) * torch.log((1 - pq).clamp_min(1e-12)))
+    cases.append(({"metric": "cross_entropy", "objective": "cross_entropy"}, sq, yq, wmean(xent)))
+    ent = tyq * torch.log(tyq) + (1 - tyq) * torch.log(1 - tyq)
+    cases.append(({"metric": "kullback_leibler", "objective": "cross_entropy"}, sq, yq, wmean(xent + ent)))
+    for params, sc, lab, ref in cases:
+        v = ops.metric(dict(params, verbose=-1), torch.tensor(sc, device="cuda"), lab, w)
+        assert abs(v - ref) < 1e-8 * max(1.0, abs(ref)), (params["metric"], v, ref)
+
+
+@pytest.mark.parametrize("objective", ["multiclass", "multiclassova"])
+def test_multiclass_metrics_match_torch(objective, gpu_available):
+    from lightgbmv1_amd import ops
+    K = 4
+    rng = np.random.RandomState(7)
+    s = rng.randn(K, N)
+    y = rng.randint(0, K, N).astype(np.float32)
+    w = (rng.rand(N) + 0.5).astype(np.float32)
+    ts, tw = _t(s), _t(w)
+    prob = torch.softmax(ts, dim=0) if objective == "multiclass" else torch.sigmoid(ts)
+    py = prob[_t(y).long(), torch.arange(N)]
+    refs = {"multi_logloss": float((-torch.log(py.clamp_min(1e-15)) * tw).sum() / tw.sum())}
+    for k in (1, 2):
+        larger = (prob >= py.unsqueeze(0)).sum(dim=0)
+        refs["multi_error@%d" % k] = float(((larger > k).double() * tw).sum() / tw.sum())
+    ds = torch.tensor(s, device="cuda").contiguous()
+    for name, ref in refs.items():
+        params = {"metric": name.split("@")[0], "objective": objective, "num_class": K, "verbose": -1}
+        if "@" in name:
+            params["multi_error_top_k"] = int(name.split("@")[1])
+        v = ops.metric(params, ds, y, w)
+        assert abs(v - ref) < 1e-9 * max(1.0, abs(ref)), (name, v, ref)
