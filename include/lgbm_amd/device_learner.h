@@ -65,6 +65,14 @@ class DeviceTreeLearner {
   // false: evaluate on the host
   virtual bool ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) = 0;
 
+  // percentile leaf renewal (L1 / quantile / MAPE) of the tree just grown, on the device from
+  // the partition and the device-resident scores of class `tree_id`; false: not possible here
+  // (the caller renews on the host)
+  virtual bool RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction* obj, int tree_id) {
+    (void)tree; (void)obj; (void)tree_id;
+    return false;
+  }
+
   // test support (tests/test_gpu_kernels.py): the state the last device-grown tree left in HBM.
   // A leaf's rows (partition), its raw fixed-point histogram slot, which histogram bins are
   // meaningful (the slices of features evaluated for the leaf: a feature its parent could not

@@ -37,6 +37,13 @@ struct DeviceRankSpec {
   const unsigned* rng_states = nullptr;  // [num_queries] per-query LCG states (xendcg); the device owns them after upload
 };
 
+// percentile leaf renewal on the device: the residual percentile and its weights
+struct DeviceRenewSpec {
+  double alpha = 0.5;
+  const label_t* label = nullptr;    // host pointers; uploaded by the learner
+  const label_t* weights = nullptr;  // null: unweighted percentile
+};
+
 struct DeviceGradSpec {
   DeviceGradKind kind = DeviceGradKind::None;
   int num_class = 1;
@@ -56,6 +63,11 @@ class ObjectiveFunction {
   virtual const char* GetName() const = 0;
   virtual bool IsConstantHessian() const { return false; }
   virtual bool IsRenewTreeOutput() const { return false; }
+  // RenewTreeOutput as a device percentile (L1 / quantile / MAPE); false: host only
+  virtual bool DeviceRenew(DeviceRenewSpec* spec) const {
+    (void)spec;
+    return false;
+  }
   // new leaf output from the residuals of the rows in the leaf (L1/quantile/MAPE)
   virtual double RenewTreeOutput(double ori_output, const std::function<double(const label_t*, int)>& residual,
                                  const data_size_t* index_mapper, const data_size_t* bagging_mapper,

@@ -380,7 +380,8 @@ data_size_t GBDT::DeviceBagging(bool goss) {
   sp.num_tree_per_iteration = num_tree_per_iteration_;
   sp.label = train_data_->metadata().label();
   // leaf-output renewal (L1 / quantile / MAPE) reads the bag on the host
-  const bool need_host = objective_ != nullptr && objective_->IsRenewTreeOutput();
+  DeviceRenewSpec renew;
+  const bool need_host = objective_ != nullptr && objective_->IsRenewTreeOutput() && !objective_->DeviceRenew(&renew);
   sp.host_indices = need_host ? &bag_data_indices_ : nullptr;
   device_sampler_reset_ = false;
   return device_learner_->DeviceSample(sp);
@@ -513,7 +514,8 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
     }
     if (tree->num_leaves() > 1) {
       should_continue = true;
-      if (objective_ != nullptr && objective_->IsRenewTreeOutput()) {
+      if (objective_ != nullptr && objective_->IsRenewTreeOutput() &&
+          !(device_learner_ != nullptr && device_learner_->RenewTreeOutputOnDevice(tree.get(), objective_, k))) {
         const double* sp = HostTrainScore() + off;
         auto residual = [sp](const label_t* label, int i) { return static_cast<double>(label[i]) - sp[i]; };
         tree_learner_->RenewTreeOutput(tree.get(), objective_, residual, num_data_, bag_data_indices_.data(),

@@ -326,6 +326,26 @@ struct MetricArgs {
 size_t MetricScratchBytes(int64_t n, int64_t query_values = 0);
 void EvalMetric(const MetricArgs& m, hipStream_t s);
 
+// percentile leaf-output renewal (L1 / quantile / MAPE): per leaf of the finished tree, the
+// alpha-percentile of its rows' residuals label - score (weighted if weights != null)
+struct RenewArgs {
+  const Leaf* leaves;
+  const int32_t* idx;
+  const int32_t* tmp;
+  const float* label;
+  const double* score;
+  const float* weights;    // or null
+  const int64_t* offsets;  // [num_leaves + 1] first row of each leaf in the gathered order
+  int32_t num_leaves;
+  double alpha;
+  double* keys;  // (carved from scratch)
+  double* vals;
+  double* out;   // [num_leaves]
+  void* scratch;  // RenewScratchBytes
+};
+size_t RenewScratchBytes(int64_t n, int leaves);
+void RenewLeafOutputs(RenewArgs r, int64_t n, hipStream_t s);
+
 int GradientBlocks(int64_t n);
 // absmax[0..1] (and root = (sum g, sum h, n) if root_parts) from per-workgroup partials
 void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, uint32_t* absmax,

@@ -164,6 +164,12 @@ class RegressionL1 : public RegressionL2 {
     }
     return Percentile(rd, n, 0.5);
   }
+  bool DeviceRenew(DeviceRenewSpec* d) const override {
+    d->alpha = 0.5;
+    d->label = label_;
+    d->weights = weights_;
+    return !sqrt_;
+  }
   const char* GetName() const override { return "regression_l1"; }
   std::string ToString() const override { return std::string(GetName()) + (sqrt_ ? " sqrt" : ""); }
   DeviceGradSpec DeviceSpec() const override { return Spec(DeviceGradKind::L1); }
@@ -312,6 +318,12 @@ class Quantile : public RegressionL2 {
     }
     return Percentile(rd, n, alpha_);
   }
+  bool DeviceRenew(DeviceRenewSpec* d) const override {
+    d->alpha = alpha_;
+    d->label = label_;
+    d->weights = weights_;
+    return !sqrt_;
+  }
   DeviceGradSpec DeviceSpec() const override {
     auto d = Spec(DeviceGradKind::Quantile);
     d.p0 = alpha_;
@@ -355,6 +367,12 @@ class Mape : public RegressionL1 {
     auto rd = [&](data_size_t i) { return res(label_, bm ? bm[im[i]] : im[i]); };
     auto wr = [&](data_size_t i) { return static_cast<double>(lw_[bm ? bm[im[i]] : im[i]]); };
     return WeightedPercentile(rd, wr, n, 0.5);
+  }
+  bool DeviceRenew(DeviceRenewSpec* d) const override {
+    d->alpha = 0.5;
+    d->label = label_;
+    d->weights = lw_.data();
+    return !sqrt_;
   }
   const char* GetName() const override { return "mape"; }
   std::string ToString() const override { return GetName(); }

@@ -1313,6 +1313,73 @@ void GPUTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
   SerialTreeLearner::RenewTreeOutput(tree, obj, residual, total_num_data, bag_indices, bag_cnt);
 }
 
+// percentile renewal on the device (reference regression_objective.hpp RenewTreeOutput): the
+// leaves' rows straight from the partition, residuals from the device scores; leaf outputs
+// averaged over the ranks like the host path
+bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction* obj, int tree_id) {
+  DeviceRenewSpec spec;
+  if (!device_mode_ || obj == nullptr || !obj->DeviceRenew(&spec) || spec.label == nullptr || d_score_ == nullptr) {
+    return false;
+  }
+  const char* hr = std::getenv("LGBM_AMD_HOST_RENEW");  // =1: the host path (A/B, tests)
+  if (hr != nullptr && hr[0] == '1') return false;
+  HIPCHECK(hipSetDevice(device_id_));
+  const int L = tree->num_leaves();
+  const size_t n = static_cast<size_t>(num_data_);
+  if (uploaded_label_src_ != spec.label) {
+    if (d_label_ == nullptr) d_label_ = Alloc<float>(n);
+    HIPCHECK(hipMemcpy(d_label_, spec.label, sizeof(float) * n, hipMemcpyHostToDevice));
+    uploaded_label_src_ = spec.label;
+  }
+  if (spec.weights != nullptr && renew_weight_src_ != spec.weights) {
+    if (d_renew_weights_ == nullptr) d_renew_weights_ = Alloc<float>(n);
+    HIPCHECK(hipMemcpy(d_renew_weights_, spec.weights, sizeof(float) * n, hipMemcpyHostToDevice));
+    renew_weight_src_ = spec.weights;
+  }
+  if (d_renew_scratch_ == nullptr) {
+    d_renew_scratch_ = Alloc<char>(dev::RenewScratchBytes(num_data_, config_->num_leaves));
+    d_renew_off_ = Alloc<int64_t>(config_->num_leaves + 1);
+    d_renew_out_ = Alloc<double>(config_->num_leaves);
+  }
+  // the leaves' row counts -> gathered offsets
+  std::vector<dev::Leaf> leaves(L);
+  HIPCHECK(hipMemcpyAsync(leaves.data(), d_leaves_, sizeof(dev::Leaf) * L, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  std::vector<int64_t> off(L + 1, 0);
+  for (int l = 0; l < L; ++l) off[l + 1] = off[l] + leaves[l].count;
+  HIPCHECK(hipMemcpyAsync(d_renew_off_, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, stream_));
+  dev::RenewArgs r;
+  r.leaves = d_leaves_;
+  r.idx = d_idx_;
+  r.tmp = d_tmp_;
+  r.label = d_label_;
+  r.score = d_score_ + static_cast<size_t>(tree_id) * n;
+  r.weights = spec.weights != nullptr ? d_renew_weights_ : nullptr;
+  r.offsets = d_renew_off_;
+  r.num_leaves = L;
+  r.alpha = spec.alpha;
+  r.out = d_renew_out_;
+  r.scratch = d_renew_scratch_;
+  dev::RenewLeafOutputs(r, off[L], stream_);
+  std::vector<double> out(L);
+  HIPCHECK(hipMemcpyAsync(out.data(), d_renew_out_, sizeof(double) * L, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));
+  std::vector<int> nonzero(L, 1);
+  for (int l = 0; l < L; ++l) {
+    if (leaves[l].count <= 0) {
+      out[l] = 0.0;
+      nonzero[l] = 0;
+    }
+  }
+  if (Network::num_machines() > 1) {
+    out = Network::GlobalSum(out);
+    nonzero = Network::GlobalSum(nonzero);
+    for (int l = 0; l < L; ++l) out[l] /= nonzero[l];
+  }
+  for (int l = 0; l < L; ++l) tree->SetLeafOutput(l, out[l]);
+  return true;
+}
+
 // ---------------------------------------------------------------- binned rows
 // row-major copy of a dataset's storage columns in this learner's layout (bin_bytes per
 // group, rows padded to whole 32-bit words)

@@ -82,6 +82,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
                       std::vector<int8_t>* bin_valid, double* sums) override;
   bool DebugGradients(std::vector<float>* g, std::vector<float>* h, double* scales) override;
   std::string DebugCheckSplits(const Tree* tree) override;  // gpu_self_check.cpp
+  bool RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction* obj, int tree_id) override;
 
   bool device_mode() const { return device_mode_; }
 
@@ -130,6 +131,11 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   Mode mode_ = Mode::kSerial;
   bool data_parallel_ = false;  // kData on more than one rank (global counts from the split estimates)
   bool voting_ = false;         // kVoting on more than one rank
+  void* d_renew_scratch_ = nullptr;  // percentile renewal (RenewTreeOutputOnDevice)
+  int64_t* d_renew_off_ = nullptr;
+  double* d_renew_out_ = nullptr;
+  const label_t* renew_weight_src_ = nullptr;
+  float* d_renew_weights_ = nullptr;
   int vote_k_ = 0;
   double* d_root_local_ = nullptr;      // voting: this rank's root sums
   dev::VoteEntry* d_vote_buf_ = nullptr;  // [world][2][vote_k]
