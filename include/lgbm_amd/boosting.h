@@ -104,6 +104,8 @@ class GBDT {
 
   // ---- prediction
   void InitPredict(int start_iteration, int num_iteration, bool is_pred_contrib);
+  // InitPredict(start_iteration, num_iteration, false) would change nothing
+  bool PredictRangeIs(int start_iteration, int num_iteration) const;
   // normal / raw predictions of a dense float32 / float64 matrix on the MI355X (same results
   // as the host predictor); false if not applicable (no device, too many classes)
   bool PredictDenseOnDevice(const void* data, bool is_double, int64_t nrow, int ncol, bool row_major,

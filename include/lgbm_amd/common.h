@@ -6,6 +6,9 @@
 #pragma once
 
 #include <algorithm>
+#include <atomic>
+#include <exception>
+#include <mutex>
 #include <cctype>
 #include <dlfcn.h>
 
@@ -422,6 +425,33 @@ class ScopedTimer {
  private:
   const char* name_;
   std::chrono::steady_clock::time_point start_;
+};
+
+// Exceptions may not leave an OpenMP structured block (the runtime would terminate the
+// process): parallel loop bodies run through Run(), which keeps the first exception, and the
+// thread that opened the region rethrows it with Check() after the loop (reference
+// OMP_INIT_EX / OMP_LOOP_EX_BEGIN / OMP_THROW_EX, include/LightGBM/utils/openmp_wrapper.h).
+class OmpErrors {
+ public:
+  template <typename F>
+  void Run(F&& body) {
+    if (failed_.load(std::memory_order_relaxed)) return;  // stop early once a body failed
+    try {
+      body();
+    } catch (...) {
+      std::lock_guard<std::mutex> l(mu_);
+      if (!error_) error_ = std::current_exception();
+      failed_.store(true, std::memory_order_relaxed);
+    }
+  }
+  void Check() {
+    if (error_) std::rethrow_exception(error_);
+  }
+
+ private:
+  std::exception_ptr error_;
+  std::atomic<bool> failed_{false};
+  std::mutex mu_;
 };
 
 }  // namespace common

@@ -26,8 +26,11 @@ class Predictor {
  public:
   using Row = std::vector<std::pair<int, double>>;
 
+  // init_predict = false: the booster's prediction range is already this one (concurrent
+  // predictors under a shared lock must not write it)
   Predictor(GBDT* boosting, int start_iteration, int num_iteration, bool is_raw_score, bool predict_leaf_index,
-            bool predict_contrib, bool early_stop, int early_stop_freq, double early_stop_margin)
+            bool predict_contrib, bool early_stop, int early_stop_freq, double early_stop_margin,
+            bool init_predict = true)
       : boosting_(boosting) {
     early_stop_ = CreatePredictionEarlyStopInstance("none", PredictionEarlyStopConfig());
     if (early_stop && !boosting->NeedAccuratePrediction()) {
@@ -38,7 +41,7 @@ class Predictor {
       c.round_period = early_stop_freq;
       early_stop_ = CreatePredictionEarlyStopInstance(boosting->NumberOfClasses() == 1 ? "binary" : "multiclass", c);
     }
-    boosting->InitPredict(start_iteration, num_iteration, predict_contrib);
+    if (init_predict) boosting->InitPredict(start_iteration, num_iteration, predict_contrib);
     num_pred_one_row_ = boosting->NumPredictOneRow(start_iteration, num_iteration, predict_leaf_index, predict_contrib);
     num_feature_ = boosting->MaxFeatureIdx() + 1;
     buf_.assign(omp_get_max_threads(), std::vector<double>(num_feature_, 0.0));
@@ -132,22 +135,26 @@ class Predictor {
     lines.reserve(kChunk);
     auto flush = [&]() {
       std::vector<std::string> res(lines.size());
+      common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
       for (int64_t i = 0; i < static_cast<int64_t>(lines.size()); ++i) {
-        Row feats;
-        double label;
-        parser->ParseOneLine(lines[i].c_str(), &feats, &label);
-        if (need_adjust) {
-          Row kept;
-          for (auto& kv : feats) {
-            if (kv.first < static_cast<int>(remap.size()) && remap[kv.first] >= 0) kept.emplace_back(remap[kv.first], kv.second);
+        errors.Run([&] {
+          Row feats;
+          double label;
+          parser->ParseOneLine(lines[i].c_str(), &feats, &label);
+          if (need_adjust) {
+            Row kept;
+            for (auto& kv : feats) {
+              if (kv.first < static_cast<int>(remap.size()) && remap[kv.first] >= 0) kept.emplace_back(remap[kv.first], kv.second);
+            }
+            feats.swap(kept);
           }
-          feats.swap(kept);
-        }
-        std::vector<double> r(num_pred_one_row_);
-        fun_(feats, r.data());
-        res[i] = common::Join(r, "\t");
+          std::vector<double> r(num_pred_one_row_);
+          fun_(feats, r.data());
+          res[i] = common::Join(r, "\t");
+        });
       }
+      errors.Check();
       for (auto& s : res) out << s << '\n';
       lines.clear();
     };

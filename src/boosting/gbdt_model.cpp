@@ -175,27 +175,22 @@ bool GBDT::LoadModelFromString(const char* buffer, size_t len) {
     std::vector<size_t> bounds(sizes.size() + 1, 0);
     for (size_t i = 0; i < sizes.size(); ++i) bounds[i + 1] = bounds[i] + sizes[i];
     models_.resize(sizes.size());
-    std::string err;
+    common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < static_cast<int>(sizes.size()); ++i) {
-      const char* cp = p + bounds[i];
-      size_t ll = common::GetLine(cp);
-      std::string line(cp, ll);
-      if (!common::StartsWith(line, "Tree=")) {
-#pragma omp critical
-        err = line;
-        continue;
-      }
-      cp = common::SkipNewLine(cp + ll);
-      size_t used = 0;
-      try {
+      errors.Run([&] {
+        const char* cp = p + bounds[i];
+        size_t ll = common::GetLine(cp);
+        std::string line(cp, ll);
+        if (!common::StartsWith(line, "Tree=")) {
+          Log::Fatal("Model format error, expect a tree here. met %s", line.c_str());
+        }
+        cp = common::SkipNewLine(cp + ll);
+        size_t used = 0;
         models_[i].reset(new Tree(cp, &used));
-      } catch (std::exception& e) {
-#pragma omp critical
-        err = e.what();
-      }
+      });
     }
-    if (!err.empty()) Log::Fatal("Model format error, expect a tree here. met %s", err.c_str());
+    errors.Check();
     p += bounds.back();
   }
   num_iteration_for_pred_ = static_cast<int>(models_.size()) / num_tree_per_iteration_;
@@ -361,6 +356,13 @@ void GBDT::SetLeafValue(int tree_idx, int leaf_idx, double val) {
 }
 
 // ----------------------------------------------------------------------- prediction
+bool GBDT::PredictRangeIs(int start_iteration, int num_iteration) const {
+  int num = static_cast<int>(models_.size()) / num_tree_per_iteration_;
+  start_iteration = std::min(std::max(start_iteration, 0), num);
+  num = num_iteration > 0 ? std::min(num_iteration, num - start_iteration) : num - start_iteration;
+  return start_iteration == start_iteration_for_pred_ && num == num_iteration_for_pred_;
+}
+
 void GBDT::InitPredict(int start_iteration, int num_iteration, bool is_pred_contrib) {
   num_iteration_for_pred_ = static_cast<int>(models_.size()) / num_tree_per_iteration_;
   start_iteration = std::min(std::max(start_iteration, 0), num_iteration_for_pred_);

@@ -13,6 +13,7 @@
 #include <limits>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -216,17 +217,12 @@ Dataset* DatasetFromRows(const std::function<Row(int64_t)>& get_row, data_size_t
     ds->CreateValid(*reference, nrow);
     ds->metadata().Init(nrow, false, false);
   }
-  std::string err;
+  common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
   for (int64_t r = 0; r < nrow; ++r) {
-    try {
-      ds->PushSparseRow(static_cast<data_size_t>(r), get_row(r));
-    } catch (std::exception& e) {
-#pragma omp critical
-      err = e.what();
-    }
+    errors.Run([&] { ds->PushSparseRow(static_cast<data_size_t>(r), get_row(r)); });
   }
-  if (!err.empty()) Log::Fatal("%s", err.c_str());
+  errors.Check();
   ds->FinishLoad();
   return ds.release();
 }
@@ -275,13 +271,13 @@ class Booster {
   }
 
   void MergeFrom(const Booster* other) {
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     boosting_->MergeFrom(other->boosting_.get());
   }
 
   void ResetTrainingData(const Dataset* train) {
     if (train != train_data_) {
-      std::lock_guard<std::mutex> l(mu_);
+      std::unique_lock<std::shared_mutex> l(mu_);
       train_data_ = train;
       CreateObjectiveAndMetrics();
       boosting_->ResetTrainingData(train_data_, objective_.get(), Ptrs(train_metric_));
@@ -318,7 +314,7 @@ class Booster {
   }
 
   void ResetConfig(const char* parameters) {
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     auto param = Config::Str2Map(parameters);
     if (param.count("num_class")) Log::Fatal("Cannot change num_class during training");
     if (param.count("boosting")) Log::Fatal("Cannot change boosting during training");
@@ -336,7 +332,7 @@ class Booster {
   }
 
   void AddValidData(const Dataset* valid) {
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     valid_metrics_.emplace_back();
     for (auto& t : config_.metric) {
       std::unique_ptr<Metric> m(Metric::CreateMetric(t, config_));
@@ -349,12 +345,12 @@ class Booster {
   }
 
   bool TrainOneIter() {
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     return boosting_->TrainOneIter(nullptr, nullptr);
   }
 
   void Refit(const int32_t* leaf_preds, int32_t nrow, int32_t ncol) {
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     std::vector<std::vector<int32_t>> v(nrow, std::vector<int32_t>(ncol));
     for (int32_t i = 0; i < nrow; ++i) {
       for (int32_t j = 0; j < ncol; ++j) v[i][j] = leaf_preds[static_cast<size_t>(i) * ncol + j];
@@ -363,24 +359,42 @@ class Booster {
   }
 
   bool TrainOneIter(const score_t* g, const score_t* h) {
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     return boosting_->TrainOneIter(g, h);
   }
 
   void RollbackOneIter() {
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     boosting_->RollbackOneIter();
   }
 
+  // the lock a host prediction holds while it runs: shared when the booster's prediction range
+  // already is this one (and no SHAP, whose setup rewrites the trees' depths), else exclusive
+  // after setting it
+  struct PredictLock {
+    std::shared_lock<std::shared_mutex> shared;
+    std::unique_lock<std::shared_mutex> unique;
+    bool init = false;  // the predictor must run InitPredict (exclusive lock held)
+  };
+  void LockForPredict(int predict_type, int start_iteration, int num_iteration, PredictLock* pl) {
+    if (predict_type != C_API_PREDICT_CONTRIB) {
+      pl->shared = std::shared_lock<std::shared_mutex>(mu_);
+      if (boosting_->PredictRangeIs(start_iteration, num_iteration)) return;
+      pl->shared.unlock();
+    }
+    pl->unique = std::unique_lock<std::shared_mutex>(mu_);
+    pl->init = true;
+  }
+
   std::unique_ptr<Predictor> MakePredictor(int predict_type, int start_iteration, int num_iteration,
-                                           const Config& cfg) {
+                                           const Config& cfg, bool init_predict = true) {
     bool raw = false, leaf = false, contrib = false;
     if (predict_type == C_API_PREDICT_LEAF_INDEX) leaf = true;
     else if (predict_type == C_API_PREDICT_RAW_SCORE) raw = true;
     else if (predict_type == C_API_PREDICT_CONTRIB) contrib = true;
     return std::unique_ptr<Predictor>(new Predictor(boosting_.get(), start_iteration, num_iteration, raw, leaf,
                                                     contrib, cfg.pred_early_stop, cfg.pred_early_stop_freq,
-                                                    cfg.pred_early_stop_margin));
+                                                    cfg.pred_early_stop_margin, init_predict));
   }
 
   void PredictRows(const std::function<Row(int64_t)>& get_row, int64_t nrow, int64_t ncol, int predict_type,
@@ -390,20 +404,16 @@ class Booster {
                  "You can set ``predict_disable_shape_check=true`` to discard this error, but please be aware what you are doing.",
                  static_cast<int>(ncol), boosting_->MaxFeatureIdx() + 1);
     }
-    std::lock_guard<std::mutex> l(mu_);
-    auto pred = MakePredictor(predict_type, start_iteration, num_iteration, cfg);
+    PredictLock pl;
+    LockForPredict(predict_type, start_iteration, num_iteration, &pl);
+    auto pred = MakePredictor(predict_type, start_iteration, num_iteration, cfg, pl.init);
     const int k = pred->num_pred_one_row();
-    std::string err;
+    common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < nrow; ++i) {
-      try {
-        pred->Predict(get_row(i), out + k * i);
-      } catch (std::exception& e) {
-#pragma omp critical
-        err = e.what();
-      }
+      errors.Run([&] { pred->Predict(get_row(i), out + k * i); });
     }
-    if (!err.empty()) Log::Fatal("%s", err.c_str());
+    errors.Check();
     *out_len = k * nrow;
   }
 
@@ -420,7 +430,7 @@ class Booster {
     const char* e = std::getenv("LGBM_AMD_HOST_PREDICT");
     if (e != nullptr && e[0] == '1') return false;
     if (!cfg.predict_disable_shape_check && ncol != boosting_->MaxFeatureIdx() + 1) return false;  // host path reports it
-    std::lock_guard<std::mutex> l(mu_);
+    std::unique_lock<std::shared_mutex> l(mu_);
     const bool raw = predict_type == C_API_PREDICT_RAW_SCORE;
     if (!boosting_->PredictDenseOnDevice(data, data_type == C_API_DTYPE_FLOAT64, nrow, ncol, is_row_major != 0,
                                          start_iteration, num_iteration, raw, out)) {
@@ -432,15 +442,16 @@ class Booster {
 
   void PredictFile(const char* data, int header, int predict_type, int start_iteration, int num_iteration,
                    const Config& cfg, const char* result) {
-    std::lock_guard<std::mutex> l(mu_);
-    auto pred = MakePredictor(predict_type, start_iteration, num_iteration, cfg);
+    PredictLock pl;
+    LockForPredict(predict_type, start_iteration, num_iteration, &pl);
+    auto pred = MakePredictor(predict_type, start_iteration, num_iteration, cfg, pl.init);
     pred->PredictFile(data, result, header != 0, cfg.predict_disable_shape_check);
   }
 
   std::vector<double> GetEval(int idx) { return boosting_->GetEvalAt(idx); }
   GBDT* boosting() { return boosting_.get(); }
   const Config& config() const { return config_; }
-  std::mutex& mutex() { return mu_; }
+  std::shared_mutex& mutex() { return mu_; }
 
  private:
   template <typename T>
@@ -469,7 +480,9 @@ class Booster {
   std::unique_ptr<ObjectiveFunction> objective_;
   std::vector<std::unique_ptr<Metric>> train_metric_;
   std::vector<std::vector<std::unique_ptr<Metric>>> valid_metrics_;
-  std::mutex mu_;
+  // exclusive: training, model changes, device prediction; shared: host predictions of the
+  // current prediction range (reference c_api.cpp SHARED_LOCK / UNIQUE_LOCK)
+  std::shared_mutex mu_;
 };
 
 struct FastConfig {
@@ -548,8 +561,12 @@ int LGBM_DatasetPushRows(DatasetHandle dataset, const void* data, int data_type,
   API_BEGIN();
   auto* ds = static_cast<Dataset*>(dataset);
   auto get = DenseRowPairFun(data, data_type, nrow, ncol, 1);
+  common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
-  for (int i = 0; i < nrow; ++i) ds->PushSparseRow(start_row + i, get(i));
+  for (int i = 0; i < nrow; ++i) {
+    errors.Run([&] { ds->PushSparseRow(start_row + i, get(i)); });
+  }
+  errors.Check();
   if (start_row + nrow == ds->num_data()) ds->FinishLoad();
   API_END();
 }
@@ -561,8 +578,12 @@ int LGBM_DatasetPushRowsByCSR(DatasetHandle dataset, const void* indptr, int ind
   auto* ds = static_cast<Dataset*>(dataset);
   auto get = CSRRowFun(indptr, indptr_type, indices, data, data_type, nindptr, nelem);
   const int64_t nrow = nindptr - 1;
+  common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
-  for (int64_t i = 0; i < nrow; ++i) ds->PushSparseRow(static_cast<data_size_t>(start_row + i), get(i));
+  for (int64_t i = 0; i < nrow; ++i) {
+    errors.Run([&] { ds->PushSparseRow(static_cast<data_size_t>(start_row + i), get(i)); });
+  }
+  errors.Check();
   if (start_row + nrow == ds->num_data()) ds->FinishLoad();
   API_END();
 }
@@ -635,21 +656,25 @@ int LGBM_DatasetCreateFromMat(const void* data, int data_type, int32_t nrow, int
     ds->metadata().Init(nrow, false, false);
   }
   const int64_t rs = is_row_major ? ncol : 1, cs = is_row_major ? 1 : nrow;
+  common::OmpErrors errors;
 #pragma omp parallel
   {
     std::vector<double> buf(ncol);
 #pragma omp for schedule(static)
     for (int32_t r = 0; r < nrow; ++r) {
-      if (data_type == C_API_DTYPE_FLOAT32) {
-        const float* p = static_cast<const float*>(data) + rs * r;
-        for (int j = 0; j < ncol; ++j) buf[j] = p[cs * j];
-      } else {
-        const double* p = static_cast<const double*>(data) + rs * r;
-        for (int j = 0; j < ncol; ++j) buf[j] = p[cs * j];
-      }
-      ds->PushDenseRow(r, buf.data(), ncol);
+      errors.Run([&] {
+        if (data_type == C_API_DTYPE_FLOAT32) {
+          const float* p = static_cast<const float*>(data) + rs * r;
+          for (int j = 0; j < ncol; ++j) buf[j] = p[cs * j];
+        } else {
+          const double* p = static_cast<const double*>(data) + rs * r;
+          for (int j = 0; j < ncol; ++j) buf[j] = p[cs * j];
+        }
+        ds->PushDenseRow(r, buf.data(), ncol);
+      });
     }
   }
+  errors.Check();
   ds->FinishLoad();
   *out = ds.release();
   API_END();
@@ -1141,7 +1166,7 @@ int LGBM_BoosterPredictForCSRSingleRowFast(FastConfigHandle fastConfig_handle, c
   API_BEGIN();
   auto* fc = static_cast<FastConfig*>(fastConfig_handle);
   auto get = CSRRowFun(indptr, indptr_type, indices, data, fc->data_type, nindptr, nelem);
-  std::lock_guard<std::mutex> l(fc->booster->mutex());
+  std::unique_lock<std::shared_mutex> l(fc->booster->mutex());
   fc->predictor->Predict(get(0), out_result);
   *out_len = fc->predictor->num_pred_one_row();
   API_END();
@@ -1195,7 +1220,7 @@ int LGBM_BoosterPredictForMatSingleRowFast(FastConfigHandle fastConfig_handle, c
   API_BEGIN();
   auto* fc = static_cast<FastConfig*>(fastConfig_handle);
   auto get = DenseRowPairFun(data, fc->data_type, 1, static_cast<int>(fc->ncol), 1);
-  std::lock_guard<std::mutex> l(fc->booster->mutex());
+  std::unique_lock<std::shared_mutex> l(fc->booster->mutex());
   fc->predictor->Predict(get(0), out_result);
   *out_len = fc->predictor->num_pred_one_row();
   API_END();
@@ -1249,7 +1274,7 @@ int LGBM_BoosterGetLeafValue(BoosterHandle handle, int tree_idx, int leaf_idx, d
 int LGBM_BoosterSetLeafValue(BoosterHandle handle, int tree_idx, int leaf_idx, double val) {
   API_BEGIN();
   auto* b = static_cast<Booster*>(handle);
-  std::lock_guard<std::mutex> l(b->mutex());
+  std::unique_lock<std::shared_mutex> l(b->mutex());
   b->boosting()->SetLeafValue(tree_idx, leaf_idx, val);
   API_END();
 }

@@ -222,6 +222,7 @@ void Dataset::ConstructFromSample(std::vector<std::vector<double>>* sample_value
   const data_size_t filter_cnt =
       static_cast<data_size_t>(static_cast<double>(cfg.min_data_in_leaf * total_sample_cnt) / num_data);
   std::string err;
+  common::OmpErrors errors;
   // distributed: each rank bins a contiguous block of columns from its local sample and
   // the serialized mappers are allgathered, so every rank ends with identical bins
   // (reference dataset_loader.cpp:680-760)
@@ -250,9 +251,12 @@ void Dataset::ConstructFromSample(std::vector<std::vector<double>>* sample_value
     std::vector<double> vals = (*sample_values)[i];
     static const std::vector<double> kNoForced;
     const std::vector<double>& fb = i < static_cast<int>(forced_bins.size()) ? forced_bins[i] : kNoForced;
-    mappers[i]->FindBin(vals.data(), static_cast<int>(vals.size()), total_sample_cnt, mb, cfg.min_data_in_bin,
-                        filter_cnt, cfg.feature_pre_filter, t, cfg.use_missing, cfg.zero_as_missing, fb);
+    errors.Run([&] {
+      mappers[i]->FindBin(vals.data(), static_cast<int>(vals.size()), total_sample_cnt, mb, cfg.min_data_in_bin,
+                          filter_cnt, cfg.feature_pre_filter, t, cfg.use_missing, cfg.zero_as_missing, fb);
+    });
   }
+  errors.Check();
   if (!err.empty()) Log::Fatal("%s", err.c_str());
   if (nm > 1) {
     // wire: per column [int8 present][mapper bytes]

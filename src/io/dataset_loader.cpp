@@ -280,18 +280,17 @@ void DatasetLoader::ExtractFeatures(const std::vector<std::string>& lines, const
   const data_size_t n = static_cast<data_size_t>(lines.size());
   Metadata& md = ds->metadata();
   md.Init(n, weight_idx_ >= 0, group_idx_ >= 0);
-  std::string err;
+  common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
   for (data_size_t i = 0; i < n; ++i) {
     std::vector<std::pair<int, double>> feats;
     double label = 0;
-    try {
+    bool parsed = false;
+    errors.Run([&] {
       parser.ParseOneLine(lines[i].c_str(), &feats, &label);
-    } catch (std::exception& e) {
-#pragma omp critical
-      err = e.what();
-      continue;
-    }
+      parsed = true;
+    });
+    if (!parsed) continue;
     md.SetLabelAt(i, static_cast<label_t>(label));
     std::vector<std::pair<int, double>> kept;
     kept.reserve(feats.size());
@@ -300,9 +299,9 @@ void DatasetLoader::ExtractFeatures(const std::vector<std::string>& lines, const
       else if (kv.first == group_idx_) md.SetQueryIdAt(i, static_cast<data_size_t>(kv.second));
       if (!ignored_.count(kv.first)) kept.push_back(kv);
     }
-    ds->PushSparseRow(i, kept);
+    errors.Run([&] { ds->PushSparseRow(i, kept); });
   }
-  if (!err.empty()) Log::Fatal("%s", err.c_str());
+  errors.Check();
   md.FinishQueryIds();
 }
 

@@ -211,3 +211,44 @@ def test_torch_tensor_inputs():
     b_np = lgb.train(params, lgb.Dataset(X, y), 5)
     b_t = lgb.train(params, lgb.Dataset(torch.from_numpy(X), torch.from_numpy(y)), 5)
     np.testing.assert_array_equal(b_np.predict(X), b_t.predict(torch.from_numpy(X)))
+
+
+def test_concurrent_predictions_on_one_booster():
+    """Host predictions of one booster from several threads at once (shared lock for the
+    current prediction range, exclusive when a thread switches num_iteration) give the same
+    results as sequential calls."""
+    import threading
+    rng = np.random.RandomState(5)
+    X = rng.rand(3000, 6)
+    y = X[:, 0] + np.sin(6 * X[:, 1]) + 0.1 * rng.rand(3000)
+    bst = lgb.train({"verbose": -1, "num_leaves": 15}, lgb.Dataset(X, y), 30)
+    ref = {k: bst.predict(X[:500], num_iteration=k) for k in (10, 20, 30)}
+    errors = []
+
+    def worker(seed):
+        r = np.random.RandomState(seed)
+        for _ in range(20):
+            k = int(r.choice([10, 20, 30]))
+            if not np.array_equal(bst.predict(X[:500], num_iteration=k), ref[k]):
+                errors.append(k)
+
+    threads = [threading.Thread(target=worker, args=(s,)) for s in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors
+
+
+def test_errors_inside_parallel_loops_raise(tmp_path):
+    """A bad token met by one of the parser threads (or by a prediction thread) surfaces as a
+    LightGBMError on the caller (common::OmpErrors), not as a terminated process."""
+    bad = tmp_path / "bad.csv"
+    bad.write_text("1,2,3\n" * 500 + "0,abc,4\n" + "1,5,6\n" * 500)
+    with pytest.raises(lgb.LightGBMError, match="abc"):
+        lgb.Dataset(str(bad), params={"verbose": -1}).construct()
+    rng = np.random.RandomState(0)
+    X = rng.rand(200, 2)
+    bst = lgb.train({"verbose": -1}, lgb.Dataset(X, X[:, 0]), 3)
+    with pytest.raises(lgb.LightGBMError, match="abc"):
+        bst.predict(str(bad))
