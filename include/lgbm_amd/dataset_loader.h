@@ -51,7 +51,18 @@ class DatasetLoader {
 
  private:
   std::vector<std::string> ReadLines(const std::string& filename, bool keep_header_line);
-  void ExtractFeatures(const std::vector<std::string>& lines, const Parser& parser, Dataset* ds);
+  // parse `lines` (rows first_row, first_row + 1, ...) into the dataset and its metadata
+  // (Metadata::Init before the first chunk, FinishQueryIds after the last)
+  void ExtractFeatures(const std::vector<std::string>& lines, const Parser& parser, Dataset* ds,
+                       data_size_t first_row = 0);
+  // bin mappers from sampled lines, then the dataset of n rows
+  std::unique_ptr<Dataset> ConstructFromSampleLines(const std::vector<std::string>& sample_lines, const Parser& parser,
+                                                    data_size_t n);
+  // two_round: pass 1 indexes the (local) lines, the sample is read by offset, pass 2 streams
+  // the rows into the dataset -- the file is never held in memory
+  std::unique_ptr<Dataset> LoadTwoRound(const std::string& filename, const Parser& parser, data_size_t* num_all);
+  // side files (.weight / .query / .init) and the binary cache
+  void FinishFromFile(const std::string& filename, data_size_t num_all, Dataset* ds);
 
   Config cfg_;
   int num_machines_;

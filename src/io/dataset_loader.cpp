@@ -15,6 +15,7 @@
 #include "lgbm_amd/common.h"
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/random.h"
+#include "text_reader.h"
 
 namespace lgbm_amd {
 
@@ -276,18 +277,19 @@ std::vector<std::string> DatasetLoader::ReadLines(const std::string& filename, b
   return lines;
 }
 
-void DatasetLoader::ExtractFeatures(const std::vector<std::string>& lines, const Parser& parser, Dataset* ds) {
+void DatasetLoader::ExtractFeatures(const std::vector<std::string>& lines, const Parser& parser, Dataset* ds,
+                                    data_size_t first_row) {
   const data_size_t n = static_cast<data_size_t>(lines.size());
   Metadata& md = ds->metadata();
-  md.Init(n, weight_idx_ >= 0, group_idx_ >= 0);
   common::OmpErrors errors;
 #pragma omp parallel for schedule(static)
-  for (data_size_t i = 0; i < n; ++i) {
+  for (data_size_t j = 0; j < n; ++j) {
+    const data_size_t i = first_row + j;
     std::vector<std::pair<int, double>> feats;
     double label = 0;
     bool parsed = false;
     errors.Run([&] {
-      parser.ParseOneLine(lines[i].c_str(), &feats, &label);
+      parser.ParseOneLine(lines[j].c_str(), &feats, &label);
       parsed = true;
     });
     if (!parsed) continue;
@@ -302,7 +304,85 @@ void DatasetLoader::ExtractFeatures(const std::vector<std::string>& lines, const
     errors.Run([&] { ds->PushSparseRow(i, kept); });
   }
   errors.Check();
-  md.FinishQueryIds();
+}
+
+std::unique_ptr<Dataset> DatasetLoader::ConstructFromSampleLines(const std::vector<std::string>& sample_lines,
+                                                                 const Parser& parser, data_size_t n) {
+  int num_col = parser.NumFeatures();
+  std::vector<std::vector<double>> svals(num_col);
+  std::vector<std::vector<int>> sidx(num_col);
+  for (size_t i = 0; i < sample_lines.size(); ++i) {
+    std::vector<std::pair<int, double>> feats;
+    double label;
+    parser.ParseOneLine(sample_lines[i].c_str(), &feats, &label);
+    for (auto& kv : feats) {
+      if (kv.first >= num_col) {
+        num_col = kv.first + 1;
+        svals.resize(num_col);
+        sidx.resize(num_col);
+      }
+      if (std::fabs(kv.second) > kZeroThreshold || std::isnan(kv.second)) {
+        svals[kv.first].push_back(kv.second);
+        sidx[kv.first].push_back(static_cast<int>(i));
+      }
+    }
+  }
+  std::unique_ptr<Dataset> ds(new Dataset(n));
+  if (feature_names_.size() == static_cast<size_t>(num_col)) ds->set_feature_names(feature_names_);
+  auto forced = GetForcedBins(cfg_.forcedbins_filename, num_col, categorical_);
+  ds->ConstructFromSample(&svals, &sidx, num_col, sample_lines.size(), n, cfg_, categorical_, ignored_, forced);
+  if (feature_names_.size() == static_cast<size_t>(num_col)) ds->set_feature_names(feature_names_);
+  ds->set_label_idx(label_idx_);
+  ds->metadata().Init(n, weight_idx_ >= 0, group_idx_ >= 0);
+  return ds;
+}
+
+std::unique_ptr<Dataset> DatasetLoader::LoadTwoRound(const std::string& filename, const Parser& parser,
+                                                     data_size_t* num_all) {
+  // pass 1: the local lines' offsets (row sharding draws exactly as the one-round path)
+  Random rnd(cfg_.data_random_seed);
+  const bool shard = num_machines_ > 1 && !cfg_.pre_partition;
+  std::vector<int64_t> offsets;
+  data_size_t total = 0;
+  used_rows_.clear();
+  TextReader::ForEachLine(filename, cfg_.header, [&](const char*, size_t, int64_t off) {
+    if (!shard || rnd.NextShort(0, num_machines_) == rank_) {
+      if (shard) used_rows_.push_back(total);
+      offsets.push_back(off);
+    }
+    ++total;
+  });
+  *num_all = total;
+  const data_size_t n = static_cast<data_size_t>(offsets.size());
+  if (n == 0) Log::Fatal("Data file %s is empty", filename.c_str());
+  const int sample_cnt = std::min<int>(n, cfg_.bin_construct_sample_cnt);
+  auto sample_rows = rnd.Sample(n, sample_cnt);
+  std::vector<int64_t> sample_off(sample_rows.size());
+  for (size_t i = 0; i < sample_rows.size(); ++i) sample_off[i] = offsets[sample_rows[i]];
+  auto ds = ConstructFromSampleLines(TextReader::ReadAt(filename, sample_off), parser, n);
+  std::vector<int64_t>().swap(offsets);
+  // pass 2: stream the local rows into the dataset in chunks
+  const size_t kChunk = size_t(1) << 18;
+  std::vector<std::string> chunk;
+  chunk.reserve(kChunk);
+  data_size_t line = 0, row = 0;
+  size_t next_used = 0;
+  auto flush = [&] {
+    ExtractFeatures(chunk, parser, ds.get(), row);
+    row += static_cast<data_size_t>(chunk.size());
+    chunk.clear();
+  };
+  TextReader::ForEachLine(filename, cfg_.header, [&](const char* p, size_t len, int64_t) {
+    const bool mine = !shard || (next_used < used_rows_.size() && used_rows_[next_used] == line);
+    ++line;
+    if (!mine) return;
+    if (shard) ++next_used;
+    chunk.emplace_back(p, len);
+    if (chunk.size() >= kChunk) flush();
+  });
+  if (!chunk.empty()) flush();
+  if (row != n) Log::Fatal("Data file %s changed while it was loaded", filename.c_str());
+  return ds;
 }
 
 std::unique_ptr<Dataset> DatasetLoader::LoadFromFile(const std::string& filename) {
@@ -324,6 +404,13 @@ std::unique_ptr<Dataset> DatasetLoader::LoadFromFile(const std::string& filename
   }
   SetHeader(header_names);
   auto parser = Parser::Create(filename, cfg_.header, 0, label_idx_);
+  if (cfg_.two_round) {
+    data_size_t num_all = 0;
+    auto ds = LoadTwoRound(filename, *parser, &num_all);
+    ds->metadata().FinishQueryIds();
+    FinishFromFile(filename, num_all, ds.get());
+    return ds;
+  }
   auto lines = ReadLines(filename, cfg_.header);
   Random rnd(cfg_.data_random_seed);
   const data_size_t num_all = static_cast<data_size_t>(lines.size());
@@ -343,32 +430,16 @@ std::unique_ptr<Dataset> DatasetLoader::LoadFromFile(const std::string& filename
   // bin-construction sample
   int sample_cnt = std::min<int>(n, cfg_.bin_construct_sample_cnt);
   auto sample_rows = rnd.Sample(n, sample_cnt);
-  int num_col = parser->NumFeatures();
-  std::vector<std::vector<double>> svals(num_col);
-  std::vector<std::vector<int>> sidx(num_col);
-  for (size_t i = 0; i < sample_rows.size(); ++i) {
-    std::vector<std::pair<int, double>> feats;
-    double label;
-    parser->ParseOneLine(lines[sample_rows[i]].c_str(), &feats, &label);
-    for (auto& kv : feats) {
-      if (kv.first >= num_col) {
-        num_col = kv.first + 1;
-        svals.resize(num_col);
-        sidx.resize(num_col);
-      }
-      if (std::fabs(kv.second) > kZeroThreshold || std::isnan(kv.second)) {
-        svals[kv.first].push_back(kv.second);
-        sidx[kv.first].push_back(static_cast<int>(i));
-      }
-    }
-  }
-  std::unique_ptr<Dataset> ds(new Dataset(n));
-  if (feature_names_.size() == static_cast<size_t>(num_col)) ds->set_feature_names(feature_names_);
-  auto forced = GetForcedBins(cfg_.forcedbins_filename, num_col, categorical_);
-  ds->ConstructFromSample(&svals, &sidx, num_col, sample_rows.size(), n, cfg_, categorical_, ignored_, forced);
-  if (feature_names_.size() == static_cast<size_t>(num_col)) ds->set_feature_names(feature_names_);
-  ds->set_label_idx(label_idx_);
+  std::vector<std::string> sample_lines(sample_rows.size());
+  for (size_t i = 0; i < sample_rows.size(); ++i) sample_lines[i] = lines[sample_rows[i]];
+  auto ds = ConstructFromSampleLines(sample_lines, *parser, n);
   ExtractFeatures(lines, *parser, ds.get());
+  ds->metadata().FinishQueryIds();
+  FinishFromFile(filename, num_all, ds.get());
+  return ds;
+}
+
+void DatasetLoader::FinishFromFile(const std::string& filename, data_size_t num_all, Dataset* ds) {
   // side files override in-file weights/queries (reference metadata.cpp:23-60)
   Metadata side;
   side.InitFromFile(filename);
@@ -396,7 +467,6 @@ std::unique_ptr<Dataset> DatasetLoader::LoadFromFile(const std::string& filename
   }
   ds->FinishLoad();
   if (cfg_.save_binary) ds->SaveBinaryFile(filename + ".bin");
-  return ds;
 }
 
 std::unique_ptr<Dataset> DatasetLoader::LoadFromFileAlignWithOtherDataset(const std::string& filename,
@@ -415,7 +485,9 @@ std::unique_ptr<Dataset> DatasetLoader::LoadFromFileAlignWithOtherDataset(const 
   const data_size_t n = static_cast<data_size_t>(lines.size());
   std::unique_ptr<Dataset> ds(new Dataset(n));
   ds->CreateValid(train, n);
+  ds->metadata().Init(n, weight_idx_ >= 0, group_idx_ >= 0);
   ExtractFeatures(lines, *parser, ds.get());
+  ds->metadata().FinishQueryIds();
   Metadata side;
   side.InitFromFile(filename);
   if (side.weights()) ds->metadata().SetWeights(side.weights(), n);
