@@ -57,6 +57,10 @@ struct Params {
   int32_t vote_phase;
   int32_t vote_k;  // top_k: features each rank proposes and the vote elects, per leaf
   int32_t world;   // ranks
+  // cost-effective gradient boosting (split and coupled feature penalties): a candidate's gain
+  // loses cegb_split * rows_in_leaf + KArgs::cegb_coupled[f] while f is unused by the model
+  int32_t cegb;
+  double cegb_split;
 };
 
 // per-leaf state

@@ -93,6 +93,13 @@ struct KArgs {
   // proposals of every rank ([world][2][vote_k], this rank's block at rank), the elected
   // features per leaf ([2][vote_k], -1 padded) and their histograms ([2][vote_k][max_feature_bins]
   // (g, h) int64, summed over the ranks before the global scan)
+  // CEGB (Params::cegb): tradeoff * coupled penalty per inner feature (or null), the model-wide
+  // "feature already split on" flags, and every (leaf, feature) raw candidate ([num_leaves]
+  // [num_features], category sets alongside) for the refund when a feature is first used
+  const double* cegb_coupled;
+  int8_t* cegb_used;
+  FeatureBest* cegb_mem;
+  uint32_t* cegb_mem_cat;
   const double* root_local;
   VoteEntry* vote_buf;
   int32_t vote_rank;

@@ -430,6 +430,32 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
       const int l = side == 0 ? pl->sm : pl->lg;
       CopyWords(&pl->fsplit[side], &a.best[l], tid, nthr);
     }
+    if (a.p.cegb && a.cegb_coupled != nullptr) {
+      // CEGB (CostEffectiveGB::OnSplit): the winner's feature is used by the model from now on;
+      // the other leaves' remembered candidates on it get its coupled penalty back and replace
+      // their best split if they now beat it
+      __syncthreads();
+      const int f = sp.feature;
+      const bool first_use = f >= 0 && !a.cegb_used[f];
+      __syncthreads();
+      if (first_use) {
+        if (tid == 0) a.cegb_used[f] = 1;
+        const double refund = a.cegb_coupled[f];
+        const int nf = a.p.num_features;
+        for (int i = tid; i < s + 1; i += nthr) {
+          if (i == leaf) continue;
+          const size_t mi = static_cast<size_t>(i) * nf + f;
+          FeatureBest cand = a.cegb_mem[mi];
+          cand.gain += refund;
+          DeviceSplit& cur = a.best[i];
+          const int cf = cur.real_feature < 0 ? 0x7fffffff : cur.real_feature;
+          const int nf_real = cand.feature < 0 ? 0x7fffffff : cand.real_feature;
+          if (cur.gain > -INFINITY && (cand.gain > cur.gain || (cand.gain == cur.gain && nf_real < cf))) {
+            ToDeviceSplit(cand, a.cegb_mem_cat + mi * kMaxCatWords, &cur);
+          }
+        }
+      }
+    }
     CopyWords(&pk->split, &a.rec[s].split, tid, nthr);
     CopyWords(&pk->split, &st->cs.split, tid, nthr);
     CopyWords(&pk->F, &st->cs.feat, tid, nthr);

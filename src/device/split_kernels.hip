@@ -434,16 +434,17 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
       out->default_left = d == 1 ? 0 : (!two && F.missing_type == 2 ? 0 : 1);
     }
   }
-  out->gain *= F.penalty;
-  if (!SIMPLE && F.monotone != 0) {
-    // MonotoneSplitPenalty(depth, penalization)
-    double pen;
-    if (mono_penalty >= depth + 1.) pen = kEpsilon;
-    else if (mono_penalty <= 1.) pen = 1. - mono_penalty / pow(2., depth) + kEpsilon;
-    else pen = 1. - pow(2., mono_penalty - 1. - depth) + kEpsilon;
-    out->gain *= pen;
-  }
+  out->gain *= F.penalty;  // (CEGB and the monotone depth penalty follow in FindBody)
+  (void)depth;
+  (void)mono_penalty;
   return any;
+}
+
+// MonotoneSplitPenalty(depth, penalization)
+__device__ __forceinline__ double MonotonePenalty(int depth, double mono_penalty) {
+  if (mono_penalty >= depth + 1.) return kEpsilon;
+  if (mono_penalty <= 1.) return 1. - mono_penalty / pow(2., depth) + kEpsilon;
+  return 1. - pow(2., mono_penalty - 1. - depth) + kEpsilon;
 }
 
 // LDS of the categorical scan: per-bin ctr and the stable ctr order
@@ -1015,6 +1016,22 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
                                               xt_thr);
     }
     if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (the local scan's flags stay)
+    // SerialTreeLearner::EvalFeature order: the CEGB cost (the raw candidate remembered for the
+    // coupled-penalty refund), then the monotone depth penalty
+    if (a.p.cegb && tid == 0) {
+      const int leaf = ROOT ? 0 : sd.leaf;
+      if (a.cegb_mem != nullptr) {
+        const size_t mi = static_cast<size_t>(leaf) * a.p.num_features + f;
+        a.cegb_mem[mi] = o;
+        if (CAT) CopyWords(reinterpret_cast<const uint32_t(*)[kMaxCatWords]>(
+                               a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords),
+                           reinterpret_cast<uint32_t(*)[kMaxCatWords]>(a.cegb_mem_cat + mi * kMaxCatWords), 0, 1);
+      }
+      double delta = a.p.cegb_split * L.n;
+      if (a.cegb_coupled != nullptr && !a.cegb_used[f]) delta += a.cegb_coupled[f];
+      o.gain -= delta;
+    }
+    if (!CAT && !SIMPLE && F.monotone != 0) o.gain *= MonotonePenalty(depth, a.p.monotone_penalty);
     if (!ROOT) KTrace(a, s, kTrFindScanned);
   } else {
     o.feature = -1;

@@ -42,6 +42,9 @@ class CostEffectiveGB {
   // before `best_leaf` is split by `split`: refund coupled penalties, mark lazy rows paid
   void OnSplit(const Tree* tree, int best_leaf, const SplitInfo& split, const data_size_t* rows, data_size_t cnt,
                std::vector<SplitInfo>* best_per_leaf);
+  // features the model has split on (coupled penalties paid); the device learner mirrors them
+  const std::vector<char>& used_in_split() const { return used_in_split_; }
+  void set_used_in_split(const std::vector<char>& u) { used_in_split_ = u; }
 
  private:
   bool RowPaid(int inner, data_size_t row) const {

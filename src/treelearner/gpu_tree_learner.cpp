@@ -299,6 +299,12 @@ void GPUTreeLearner::UploadData() {
   a.p.data_parallel = (data_parallel_ || voting_) ? 1 : 0;  // global counts from the split estimates
   a.p.vote_phase = 0;
   a.p.vote_k = 0;
+  a.p.cegb = 0;
+  a.p.cegb_split = 0.0;
+  a.cegb_coupled = nullptr;
+  a.cegb_used = nullptr;
+  a.cegb_mem = nullptr;
+  a.cegb_mem_cat = nullptr;
   a.p.world = world_;
   a.root_local = nullptr;
   a.vote_buf = nullptr;
@@ -562,6 +568,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
   SerialTreeLearner::ResetConfig(config);
   DestroyGraph();  // kernel arguments are baked into the captured graph
   args_.p.sp = params_;
+  args_.p.cegb = 0;  // re-derived from the new penalties by the next DecideMode
   args_.p.max_depth = config_->max_depth;
   args_.p.monotone_penalty = config_->monotone_penalty;
   if (config_->num_leaves != old_leaves) {
@@ -629,12 +636,15 @@ void GPUTreeLearner::DecideMode() {
   }
   // voting: per-node sampling and extra_trees draws stay with the host voting loop
   if (voting_ && (config_->feature_fraction_bynode < 1.0 || config_->extra_trees)) dm = false;
+  // CEGB: split and coupled feature penalties are applied by the device scans (single rank);
+  // lazy penalties (per-row usage bitsets) and distributed CEGB run host-assisted
+  const bool cegb = CostEffectiveGB::Enabled(*config_);
   if (has_forced_split_ ||
       (config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
-      config_->cegb_tradeoff < 1.0 || config_->cegb_penalty_split > 0.0 ||
-      !config_->cegb_penalty_feature_lazy.empty() || !config_->cegb_penalty_feature_coupled.empty()) {
+      (cegb && (!config_->cegb_penalty_feature_lazy.empty() || distributed_))) {
     dm = false;
   }
+  if (cegb && dm && !args_.p.cegb) SetupCegb();
   if (dm != device_mode_ || !mode_decided_) {
     mode_decided_ = true;
     Log::Debug("device learner: %s growth", dm ? "device-resident" : "host-assisted");
@@ -1043,6 +1053,11 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   const bool graph_collectives = dev_comm && !(gc != nullptr && gc[0] == '0') && !graph_capture_failed_;
   const bool use_graph = (!distributed || graph_collectives) && !(ng != nullptr && ng[0] == '1');
   bool launched = false;
+  if (a.p.cegb && cegb_) {  // the model-wide used-feature flags of the host CEGB state
+    h_cegb_used_ = cegb_->used_in_split();
+    h_cegb_used_.resize(std::max(1, num_features_), 0);
+    HIPCHECK(hipMemcpyAsync(d_cegb_used_, h_cegb_used_.data(), h_cegb_used_.size(), hipMemcpyHostToDevice, stream_));
+  }
   if (use_graph) {
     const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
     if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
@@ -1084,6 +1099,10 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
                           hipMemcpyDeviceToHost, stream_));
   WatchdogSync();
+  if (a.p.cegb && cegb_) {
+    HIPCHECK(hipMemcpy(h_cegb_used_.data(), d_cegb_used_, h_cegb_used_.size(), hipMemcpyDeviceToHost));
+    cegb_->set_used_in_split(std::vector<char>(h_cegb_used_.begin(), h_cegb_used_.begin() + num_features_));
+  }
   const int num_splits = h_step_->nsplit;
   if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
@@ -1311,6 +1330,36 @@ void GPUTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
   if (obj == nullptr || !obj->IsRenewTreeOutput()) return;
   DownloadPartitionToHost();
   SerialTreeLearner::RenewTreeOutput(tree, obj, residual, total_num_data, bag_indices, bag_cnt);
+}
+
+// CEGB on the device (split + coupled penalties): the penalties, the model-wide used flags
+// (mirrored from / back to the host CostEffectiveGB around every device tree) and the
+// (leaf, feature) candidate memory
+void GPUTreeLearner::SetupCegb() {
+  const Config& c = *config_;
+  args_.p.cegb = 1;
+  args_.p.cegb_split = c.cegb_tradeoff * c.cegb_penalty_split;
+  args_.cegb_coupled = nullptr;
+  const int nf = std::max(1, num_features_);
+  if (d_cegb_used_ == nullptr) d_cegb_used_ = Alloc<int8_t>(nf);
+  args_.cegb_used = d_cegb_used_;
+  if (!c.cegb_penalty_feature_coupled.empty()) {
+    std::vector<double> coupled(nf, 0.0);
+    for (int f = 0; f < num_features_; ++f) {
+      coupled[f] = c.cegb_tradeoff * c.cegb_penalty_feature_coupled[data_->RealFeatureIndex(f)];
+    }
+    if (d_cegb_coupled_ == nullptr) d_cegb_coupled_ = Alloc<double>(nf);
+    HIPCHECK(hipMemcpy(d_cegb_coupled_, coupled.data(), sizeof(double) * nf, hipMemcpyHostToDevice));
+    args_.cegb_coupled = d_cegb_coupled_;
+    const size_t cells = static_cast<size_t>(c.num_leaves) * nf;
+    if (d_cegb_mem_ == nullptr) {
+      d_cegb_mem_ = Alloc<dev::FeatureBest>(cells);
+      d_cegb_mem_cat_ = Alloc<uint32_t>(cells * kMaxCatWords);
+    }
+  }
+  args_.cegb_mem = d_cegb_mem_;
+  args_.cegb_mem_cat = d_cegb_mem_cat_;
+  DestroyGraph();
 }
 
 // percentile renewal on the device (reference regression_objective.hpp RenewTreeOutput): the

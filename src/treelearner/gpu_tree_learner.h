@@ -131,6 +131,12 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   Mode mode_ = Mode::kSerial;
   bool data_parallel_ = false;  // kData on more than one rank (global counts from the split estimates)
   bool voting_ = false;         // kVoting on more than one rank
+  void SetupCegb();
+  int8_t* d_cegb_used_ = nullptr;
+  double* d_cegb_coupled_ = nullptr;
+  dev::FeatureBest* d_cegb_mem_ = nullptr;
+  uint32_t* d_cegb_mem_cat_ = nullptr;
+  std::vector<char> h_cegb_used_;
   void* d_renew_scratch_ = nullptr;  // percentile renewal (RenewTreeOutputOnDevice)
   int64_t* d_renew_off_ = nullptr;
   double* d_renew_out_ = nullptr;

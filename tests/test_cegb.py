@@ -17,7 +17,8 @@ def _data(seed=0):
 
 def _train(params, rounds=10, device="cpu"):
     X, y = _data()
-    p = dict(params, verbose=-1, num_threads=2, device_type=device)
+    p = dict({"verbose": -1}, **params)
+    p.update(num_threads=2, device_type=device)
     ds = lgb.Dataset(X, y, feature_name=["col_%d" % i for i in range(5)], params=p)
     b = lgb.Booster(params=p, train_set=ds)
     for _ in range(rounds):
@@ -76,9 +77,30 @@ def test_cegb_coupled_penalty_is_paid_once():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=["coupled", "lazy", "split"])
-def test_cegb_device_learner_matches_cpu(case, gpu_available):
-    """The device learner grows CEGB trees host-assisted (device histograms, host scan with
-    the penalties, device partitions): same trees as the CPU learner."""
+def test_cegb_device_learner_matches_cpu(case, gpu_available, capfd):
+    """Split and coupled penalties are applied by the device scans (the coupled refund by the
+    device pick) in device-resident growth; lazy penalties run host-assisted.  Same trees as
+    the CPU learner either way."""
     cpu = _train(case, rounds=5)
-    gpu = _train(case, rounds=5, device="gpu")
+    capfd.readouterr()
+    gpu = _train(dict(case, verbose=2), rounds=5, device="gpu")
+    log = capfd.readouterr().out
+    lazy = "cegb_penalty_feature_lazy" in case
+    assert ("host-assisted growth" in log) == lazy and ("device-resident growth" in log) != lazy
     np.testing.assert_allclose(gpu.predict(_data()[0]), cpu.predict(_data()[0]), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_cegb_device_coupled_paid_once_and_scaling(gpu_available):
+    b = _train({"cegb_penalty_feature_coupled": [0, 1e6, 1e6, 1e6, 1e6]}, rounds=5, device="gpu")
+    used = set()
+    for t in b.dump_model()["tree_info"]:
+        stack = [t["tree_structure"]]
+        while stack:
+            n = stack.pop()
+            if "split_feature" in n:
+                used.add(n["split_feature"])
+                stack += [n["left_child"], n["right_child"]]
+    assert used == {0}
+    p1, p2 = PAIRS[0]
+    assert _trees(_train(p1, device="gpu").model_to_string()) == _trees(_train(p2, device="gpu").model_to_string())
