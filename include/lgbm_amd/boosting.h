@@ -7,6 +7,7 @@
 // device learner (DeviceTreeLearner); the host keeps only trees and metric mirrors.
 #pragma once
 
+#include <fstream>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -182,6 +183,13 @@ class GBDT {
   const Dataset* train_data_ = nullptr;
   std::unique_ptr<Config> config_;
   std::unique_ptr<TreeLearner> tree_learner_;
+  // LGBM_AMD_ITER_LOG=<path>: one JSON line per boosting iteration (phase times, trees, device
+  // collectives); distributed ranks write <path>.rank<r>
+  std::unique_ptr<std::ofstream> iter_log_;
+  bool iter_log_checked_ = false;
+  void LogIteration(double grad_ms, double bag_ms, const std::vector<double>& tree_ms, double renew_ms,
+                    double score_ms, double total_ms, const std::vector<int>& leaves, const std::vector<int>& device,
+                    double coll_bytes);
   DeviceTreeLearner* device_learner_ = nullptr;
   const ObjectiveFunction* objective_ = nullptr;
   std::unique_ptr<ObjectiveFunction> loaded_objective_;

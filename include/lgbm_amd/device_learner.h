@@ -65,6 +65,13 @@ class DeviceTreeLearner {
   // false: evaluate on the host
   virtual bool ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) = 0;
 
+  // the last tree: grown device-resident, splits applied, bytes moved by device collectives
+  struct TreeStats {
+    bool device_mode = false;
+    int splits = 0;
+    double collective_bytes = 0.0;
+  };
+  virtual TreeStats LastTreeStats() const { return TreeStats(); }
   // percentile leaf renewal (L1 / quantile / MAPE) of the tree just grown, on the device from
   // the partition and the device-resident scores of class `tree_id`; false: not possible here
   // (the caller renews on the host)

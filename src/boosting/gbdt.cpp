@@ -483,8 +483,40 @@ double GBDT::BoostFromAverage(int class_id, bool update_scorer) {
   return 0.0;
 }
 
+void GBDT::LogIteration(double grad_ms, double bag_ms, const std::vector<double>& tree_ms, double renew_ms,
+                        double score_ms, double total_ms, const std::vector<int>& leaves,
+                        const std::vector<int>& device, double coll_bytes) {
+  std::ostringstream o;
+  o.precision(6);
+  o << "{\"iter\": " << iter_ << ", \"rank\": " << Network::rank() << ", \"ms\": " << total_ms
+    << ", \"gradients_ms\": " << grad_ms << ", \"bagging_ms\": " << bag_ms << ", \"tree_ms\": [";
+  for (size_t i = 0; i < tree_ms.size(); ++i) o << (i ? ", " : "") << tree_ms[i];
+  o << "], \"renew_ms\": " << renew_ms << ", \"score_update_ms\": " << score_ms << ", \"leaves\": [";
+  for (size_t i = 0; i < leaves.size(); ++i) o << (i ? ", " : "") << leaves[i];
+  o << "], \"device_resident\": [";
+  for (size_t i = 0; i < device.size(); ++i) o << (i ? ", " : "") << (device[i] ? "true" : "false");
+  o << "], \"collective_bytes\": " << coll_bytes << "}\n";
+  *iter_log_ << o.str();
+  iter_log_->flush();
+}
+
 bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
   common::ScopedTimer timer("GBDT::TrainOneIter");
+  if (!iter_log_checked_) {
+    iter_log_checked_ = true;
+    if (const char* path = std::getenv("LGBM_AMD_ITER_LOG")) {
+      std::string p(path);
+      if (Network::num_machines() > 1) p += ".rank" + std::to_string(Network::rank());
+      iter_log_.reset(new std::ofstream(p, std::ios::app));
+      if (!*iter_log_) iter_log_.reset();
+    }
+  }
+  using Clock = std::chrono::steady_clock;
+  auto ms_since = [](Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); };
+  const auto t_iter = Clock::now();
+  double grad_ms = 0, bag_ms = 0, renew_ms = 0, score_ms = 0, coll_bytes = 0;
+  std::vector<double> tree_ms;
+  std::vector<int> leaves, device;
   std::vector<double> init_scores(num_tree_per_iteration_, 0.0);
   const score_t* grad = gradients;
   const score_t* hess = hessians;
@@ -504,16 +536,31 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
     grad = device_learner_->device_gradients();
     hess = device_learner_->device_hessians();
   }
+  if (iter_log_) {
+    if (device_learner_ != nullptr) device_learner_->Synchronize();
+    grad_ms = ms_since(t_iter);
+  }
+  auto t_phase = Clock::now();
   Bagging(iter_);
+  if (iter_log_) bag_ms = ms_since(t_phase);
   bool should_continue = false;
   for (int k = 0; k < num_tree_per_iteration_; ++k) {
     const size_t off = static_cast<size_t>(k) * num_data_;
     std::unique_ptr<Tree> tree(new Tree(2, false));
+    t_phase = Clock::now();
     if (class_need_train_[k] && train_data_->num_features() > 0) {
       tree.reset(tree_learner_->Train(grad + off, hess + off));
     }
+    if (iter_log_) {
+      tree_ms.push_back(ms_since(t_phase));
+      leaves.push_back(tree->num_leaves());
+      const auto st = device_learner_ != nullptr ? device_learner_->LastTreeStats() : DeviceTreeLearner::TreeStats();
+      device.push_back(st.device_mode ? 1 : 0);
+      coll_bytes += st.collective_bytes;
+    }
     if (tree->num_leaves() > 1) {
       should_continue = true;
+      t_phase = Clock::now();
       if (objective_ != nullptr && objective_->IsRenewTreeOutput() &&
           !(device_learner_ != nullptr && device_learner_->RenewTreeOutputOnDevice(tree.get(), objective_, k))) {
         const double* sp = HostTrainScore() + off;
@@ -521,8 +568,14 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
         tree_learner_->RenewTreeOutput(tree.get(), objective_, residual, num_data_, bag_data_indices_.data(),
                                        bag_data_cnt_);
       }
+      if (iter_log_) renew_ms += ms_since(t_phase);
       tree->Shrinkage(shrinkage_rate_);
+      t_phase = Clock::now();
       UpdateScore(tree.get(), k);
+      if (iter_log_) {
+        if (device_learner_ != nullptr) device_learner_->Synchronize();
+        score_ms += ms_since(t_phase);
+      }
       if (std::fabs(init_scores[k]) > kEpsilon) tree->AddBias(init_scores[k]);
     } else if (models_.size() < static_cast<size_t>(num_tree_per_iteration_)) {
       double output = 0.0;
@@ -543,6 +596,10 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
       for (int k = 0; k < num_tree_per_iteration_; ++k) models_.pop_back();
     }
     return true;
+  }
+  if (iter_log_) {
+    if (device_learner_ != nullptr) device_learner_->Synchronize();
+    LogIteration(grad_ms, bag_ms, tree_ms, renew_ms, score_ms, ms_since(t_iter), leaves, device, coll_bytes);
   }
   ++iter_;
   return false;

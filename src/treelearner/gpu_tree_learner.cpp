@@ -407,6 +407,9 @@ void GPUTreeLearner::UploadData() {
     a.vote_buf = d_vote_buf_;
     a.vote_list = d_vote_list_;
     a.vote_hist = d_vote_hist_;
+    split_collective_bytes_ = static_cast<double>(sizeof(dev::VoteEntry) * 2 * vote_k_ * world_) +
+                              sizeof(long long) * 4.0 * vote_k_ * max_fb;
+    root_collective_bytes_ = split_collective_bytes_ + 3 * sizeof(double) + 3 * sizeof(uint32_t);
     Log::Info("voting-parallel device learner, rank %d of %d: top_k %d; per split: proposal allgather %zu bytes "
               "per rank, elected-histogram all-reduce %zu bytes", rank_, world_, vote_k_,
               sizeof(dev::VoteEntry) * 2 * vote_k_, sizeof(long long) * 4 * static_cast<size_t>(vote_k_) * max_fb);
@@ -506,6 +509,9 @@ void GPUTreeLearner::SetupOwnership() {
   d_owned_hist_ = Alloc<long long>(2 * static_cast<size_t>(rs_block_));
   const size_t fb_bytes = 2 * static_cast<size_t>(max_owned_) *
                           (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0));
+  const double rs_bytes = mode_ == Mode::kData ? sizeof(long long) * 2.0 * rs_block_ * world_ : 0.0;
+  split_collective_bytes_ = rs_bytes + static_cast<double>(fb_bytes) * world_;
+  root_collective_bytes_ = split_collective_bytes_ + 3 * sizeof(double) + 3 * sizeof(uint32_t);
   if (mode_ == Mode::kData) {
     Log::Info("data-parallel device learner, rank %d of %d: %d features, histogram bins [%d, %d); per split "
               "reduce-scatter %zu bytes in / %zu out, split-record allgather %zu bytes per rank",
@@ -698,7 +704,10 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   host_partition_fresh_ = false;
   DecideMode();
   if (device_mode_) return TrainDeviceMode();
-  return SerialTreeLearner::Train(gradients, hessians);
+  last_stats_ = TreeStats();
+  Tree* t = SerialTreeLearner::Train(gradients, hessians);
+  last_stats_.splits = t->num_leaves() - 1;
+  return t;
 }
 
 // wait for the tree; with device collectives, poll the communicator for asynchronous
@@ -1104,6 +1113,11 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     cegb_->set_used_in_split(std::vector<char>(h_cegb_used_.begin(), h_cegb_used_.begin() + num_features_));
   }
   const int num_splits = h_step_->nsplit;
+  last_stats_.device_mode = true;
+  last_stats_.splits = num_splits;
+  // every step's collectives run (exiting early once the tree is done): the sequence is fixed
+  last_stats_.collective_bytes =
+      distributed_ ? root_collective_bytes_ + split_collective_bytes_ * (config_->num_leaves - 1) : 0.0;
   if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
     const bool root_scanned = h_step_->root_count >= 2 * config_->min_data_in_leaf;  // global count

@@ -83,6 +83,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool DebugGradients(std::vector<float>* g, std::vector<float>* h, double* scales) override;
   std::string DebugCheckSplits(const Tree* tree) override;  // gpu_self_check.cpp
   bool RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction* obj, int tree_id) override;
+  TreeStats LastTreeStats() const override { return last_stats_; }
 
   bool device_mode() const { return device_mode_; }
 
@@ -132,6 +133,9 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool data_parallel_ = false;  // kData on more than one rank (global counts from the split estimates)
   bool voting_ = false;         // kVoting on more than one rank
   void SetupCegb();
+  TreeStats last_stats_;
+  double split_collective_bytes_ = 0.0;  // device collectives per split step (distributed)
+  double root_collective_bytes_ = 0.0;
   int8_t* d_cegb_used_ = nullptr;
   double* d_cegb_coupled_ = nullptr;
   dev::FeatureBest* d_cegb_mem_ = nullptr;

@@ -286,3 +286,19 @@ def test_two_round_loading_matches_one_round(fmt, tmp_path, monkeypatch):
         assert ds.num_data() == n
         models.append(bst.model_to_string())
     assert models[0].split("end of trees")[0] == models[1].split("end of trees")[0]
+
+
+def test_iteration_log_jsonl(tmp_path, monkeypatch):
+    """LGBM_AMD_ITER_LOG: one JSON line per boosting iteration with phase times and trees."""
+    import json
+    log = tmp_path / "iters.jsonl"
+    monkeypatch.setenv("LGBM_AMD_ITER_LOG", str(log))
+    rng = np.random.RandomState(2)
+    X = rng.rand(500, 4)
+    lgb.train({"verbose": -1, "objective": "multiclass", "num_class": 3},
+              lgb.Dataset(X, rng.randint(0, 3, 500)), 4)
+    lines = [json.loads(l) for l in log.read_text().splitlines()]
+    assert [l["iter"] for l in lines] == [0, 1, 2, 3]
+    for l in lines:
+        assert len(l["tree_ms"]) == 3 and len(l["leaves"]) == 3 and l["ms"] >= sum(l["tree_ms"])
+        assert l["device_resident"] == [False, False, False] and l["collective_bytes"] == 0

@@ -545,3 +545,18 @@ def test_percentile_renewal_on_device(extra, gpu_available, monkeypatch):
             assert a == b, t  # bit for bit
         else:  # later trees: last-bit differences in the scores may appear (seen once in 120 leaves)
             np.testing.assert_allclose(a, b, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("extra", [{}, {"bagging_fraction": 0.7, "bagging_freq": 1},
+                                   {"objective": "multiclass", "num_class": 3}, {"gpu_use_dp": True}],
+                         ids=["binary", "bagging", "multiclass", "wide"])
+def test_device_training_is_bitwise_deterministic(extra, gpu_available):
+    """Run-to-run determinism of device training: histograms are exact integer sums and every
+    reduction has a fixed order, so two runs give the same model text, bit for bit."""
+    X, y = _data(40000, seed=21)
+    if extra.get("objective") == "multiclass":
+        y = (np.digitize(X[:, 0], [-0.5, 0.5])).astype(np.float32)
+    params = {"objective": "binary", "verbose": -1, "device_type": "gpu", "num_leaves": 31, "seed": 5}
+    params.update(extra)
+    runs = [lgb.train(params, lgb.Dataset(X, y), 10).model_to_string() for _ in range(2)]
+    assert runs[0] == runs[1]
