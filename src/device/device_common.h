@@ -45,19 +45,19 @@ __device__ __forceinline__ int RoundIntD(double x) { return static_cast<int>(x +
 // captured graph does not depend on it)
 __device__ __forceinline__ int RootRows(const KArgs& a) { return a.num_rows_dev ? *a.num_rows_dev : a.num_rows; }
 
-// bin of storage column `group` for `row`, column-major copy (partition kernels)
-// bin of storage column `group` for `row`, row-major matrix
-__device__ __forceinline__ uint32_t RowBin(const KArgs& a, int64_t row, int group) {
-  if (a.bin_bytes == 1) return static_cast<const uint8_t*>(a.bins)[row * (4 * a.words_per_row) + group];
-  return static_cast<const uint16_t*>(a.bins)[row * (2 * a.words_per_row) + group];
+// bin of a storage column for `row` in the row-major matrix, from the group's byte offset
+// in a row and its width (Feature::gbyte / gwide)
+__device__ __forceinline__ uint32_t RowBin(const KArgs& a, int64_t row, int gbyte, int gwide) {
+  const uint8_t* p = static_cast<const uint8_t*>(a.bins) + row * (4 * static_cast<int64_t>(a.words_per_row)) + gbyte;
+  return gwide ? static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(p)) : static_cast<uint32_t>(*p);
 }
 
 // the split column's bin for the partition: from the column-major copy when there is one,
 // else from the row-major matrix (whose line the histogram pass then reads again)
-__device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int group) {
-  if (a.bins_col == nullptr) return RowBin(a, row, group);
-  if (a.bin_bytes == 1) return a.bins_col[static_cast<int64_t>(group) * a.num_data + row];
-  return reinterpret_cast<const uint16_t*>(a.bins_col)[static_cast<int64_t>(group) * a.num_data + row];
+__device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int gbyte, int gwide, int64_t col_off) {
+  if (a.bins_col == nullptr) return RowBin(a, row, gbyte, gwide);
+  if (gwide) return reinterpret_cast<const uint16_t*>(a.bins_col + col_off)[row];
+  return a.bins_col[col_off + row];
 }
 
 // group bin -> feature bin (Dataset::FeatureBin)

@@ -33,6 +33,11 @@ struct Feature {
   int32_t sub_lo, sub_hi;  // this feature's [lo, hi) range inside the group's bin space
   int32_t real_index;
   int32_t monotone;
+  // where the group's bin sits: byte offset inside a row of the row-major matrix, 16-bit
+  // (1) or 8-bit (0), and the byte offset of its column in the column-major copy
+  int32_t gbyte;
+  int32_t gwide;
+  int64_t col_off;
   double penalty;
 };
 

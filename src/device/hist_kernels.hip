@@ -4,7 +4,8 @@
 // src/treelearner/ocl/histogram256.cl, src/io/dense_bin.hpp).  The per-split histograms
 // are built by k_split (partition_kernels.hip) together with the row partition.
 //
-// Layout: row-major bin matrix (one 32-bit word = 4 uint8 or 2 uint16 storage columns).
+// Layout: row-major bin matrix (one 32-bit word = 4 uint8 or 2 uint16 storage columns; a
+// mixed layout keeps 8-bit groups 4 to a word next to words of 16-bit groups).
 // Grid: (row workgroups, column tiles) of 1024-thread workgroups.  A workgroup accumulates
 // an LDS-private histogram of its tile's columns over one row block at a time and stores it
 // whole as that block's partial histogram -- no global atomics (on gfx950 those execute at
@@ -86,7 +87,7 @@ __device__ __forceinline__ void HistBlock(const KArgs& a, unsigned long long* ld
       int rn[kRowsInFlight];
       LoadRowIdx(src, i + stride, r1, t.rpp, rn);  // next batch, in flight during the atomics
 #pragma unroll
-      for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW, UNITS>(lds, t.goff, wd[k], v[k], t.sg, t.sh);
+      for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
 #pragma unroll
       for (int k = 0; k < kRowsInFlight; ++k) r[k] = rn[k];
     }
@@ -211,10 +212,12 @@ static void LaunchHist(const KArgs& a, hipStream_t s) {
   const dim3 grid(a.root_grid, a.hist_tiles);
   if (a.hist_units == 1) {
     if (a.bin_bytes == 1) hipLaunchKernelGGL((k_hist<MODE, 4, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
-    else hipLaunchKernelGGL((k_hist<MODE, 2, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_hist<MODE, 2, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    else hipLaunchKernelGGL((k_hist<MODE, 0, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
   } else {
     if (a.bin_bytes == 1) hipLaunchKernelGGL((k_hist<MODE, 4, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
-    else hipLaunchKernelGGL((k_hist<MODE, 2, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_hist<MODE, 2, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    else hipLaunchKernelGGL((k_hist<MODE, 0, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
   }
   LaunchReduce<MODE>(a, s);
 }
@@ -241,6 +244,10 @@ void PrepareKernels() {
   AllowLds(k_hist<2, 2, 1>);
   AllowLds(k_hist<2, 4, 2>);
   AllowLds(k_hist<2, 2, 2>);
+  AllowLds(k_hist<0, 0, 1>);
+  AllowLds(k_hist<0, 0, 2>);
+  AllowLds(k_hist<2, 0, 1>);
+  AllowLds(k_hist<2, 0, 2>);
   PrepareSplitKernels(MaxDynLds());
 }
 

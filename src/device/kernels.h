@@ -41,8 +41,13 @@ struct KArgs {
   int32_t num_rows;          // local rows in the root (or the explicit range); upper bound if num_rows_dev
   const int32_t* num_rows_dev;  // root rows held on the device (a bag drawn on the device), or null
   int32_t root_identity;     // root rows are 0..num_rows-1 (indices written by the root pass)
-  int32_t bin_bytes;         // 1 or 2
+  // row layout: every group 8-bit (bin_bytes 1, 4 per word), every group 16-bit (2, 2 per
+  // word), or mixed (0): each word holds 8-bit groups or 16-bit groups only, in group order
+  // (a 16-bit group starts a new word), word_g0 / word_wide describe the words
+  int32_t bin_bytes;
   int32_t words_per_row;     // 32-bit words per row
+  const int32_t* word_g0;    // [words_per_row + 1] first group of each word (mixed layouts)
+  const int8_t* word_wide;   // [words_per_row] word holds 16-bit groups (mixed layouts)
   int32_t hist_tiles;        // column tiles of the histogram kernel
   int32_t tile_words;        // words per column tile
   int32_t tile_bins;         // max histogram bins of one tile (LDS words)
@@ -68,7 +73,7 @@ struct KArgs {
   int32_t owned_bin_lo;
   // histogram column range (feature-parallel: the words of this rank's features)
   int32_t tile_w0, tile_w1;
-  const uint8_t* bins_col;   // column-major copy of the bin matrix ([group][rows], bin_bytes each)
+  const uint8_t* bins_col;   // column-major copy of the bin matrix (group columns at Feature::col_off)
   int32_t num_data;          // rows of the matrix (column stride of bins_col)
   int32_t host_mode;         // partition: the host wrote Step::cs (host-assisted growth)
   FeatureBest* feat_best;    // [2][num_features] per-feature best split of the two leaves

@@ -54,7 +54,8 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
   const int s = cs.s;
   const int pb = cs.part_begin, pc = cs.part_count, src_buf = cs.src_buf;
   const int hist_left = st->hist_left;
-  const int fgroup = cs.feat.group;
+  const int fbyte = cs.feat.gbyte, fwide = cs.feat.gwide;
+  const int64_t fcol = cs.feat.col_off;
   Feature F;
   F.sub_lo = cs.feat.sub_lo;
   F.sub_hi = cs.feat.sub_hi;
@@ -108,7 +109,7 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
       if (tr) KTrace(a, ts, kTrSplitRows);
       uint32_t gb[kSplitRows];
 #pragma unroll
-      for (int k = 0; k < kSplitRows; ++k) gb[k] = row[k] >= 0 ? ColBin(a, row[k], fgroup) : 0u;
+      for (int k = 0; k < kSplitRows; ++k) gb[k] = row[k] >= 0 ? ColBin(a, row[k], fbyte, fwide, fcol) : 0u;
       if (tr) KTrace(a, ts, kTrSplitSide);
       bool left[kSplitRows];
       unsigned long long mask[kSplitRows];
@@ -193,7 +194,7 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
           }
           if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
 #pragma unroll
-          for (int k = 0; k < kGatherRows; ++k) AddRow<GPW, UNITS>(lds, t.goff, wd[k], v[k], t.sg, t.sh);
+          for (int k = 0; k < kGatherRows; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
           if (loc_sums && t.q == 0) {
 #pragma unroll
             for (int k = 0; k < kGatherRows; ++k) {
@@ -244,10 +245,12 @@ void SplitStep(const KArgs& a, hipStream_t s, bool reduce) {
 
   if (a.hist_units == 1) {
     if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 1, true>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_split<2, 1, true>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 1, true>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_split<0, 1, true>), grid, dim3(kPartThreads), lds, s, a);
   } else {
     if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 2, true>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_split<2, 2, true>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 2, true>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_split<0, 2, true>), grid, dim3(kPartThreads), lds, s, a);
   }
   if (reduce) LaunchReduce<1>(a, s);
 }
@@ -257,6 +260,8 @@ void PrepareSplitKernels(int mx) {
   AllowLds(k_split<2, 1, true>, mx);
   AllowLds(k_split<4, 2, true>, mx);
   AllowLds(k_split<2, 2, true>, mx);
+  AllowLds(k_split<0, 1, true>, mx);
+  AllowLds(k_split<0, 2, true>, mx);
 }
 
 void Partition(const KArgs& a, hipStream_t s) {

@@ -32,7 +32,8 @@ constexpr int kMaxNodes = 255;
 constexpr int kMaxRowWords = 16;
 
 struct NodeInfo {
-  int16_t group, left_is_default;  // default direction for missing values
+  int32_t gbyte;                   // the split group's byte offset in a row (Feature::gbyte)
+  int16_t gwide, left_is_default;  // 16-bit group; default direction for missing values
   int16_t missing_type, is_cat;
   int32_t sub_lo, sub_hi, offset, mfb, default_bin, max_bin;
   uint32_t threshold;
@@ -45,7 +46,8 @@ __device__ __forceinline__ NodeInfo MakeNode(const KArgs& a, const DevTree& t, i
     const Feature F = a.feat[f];
     const int8_t dt = t.decision_type[i];
     NodeInfo nd;
-    nd.group = static_cast<int16_t>(F.group);
+    nd.gbyte = F.gbyte;
+    nd.gwide = static_cast<int16_t>(F.gwide);
     nd.left_is_default = (dt & 2) ? 1 : 0;
     nd.missing_type = static_cast<int16_t>((dt >> 2) & 3);
     nd.is_cat = (dt & 1) ? 1 : 0;
@@ -78,7 +80,6 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
   const bool stage_row = wpr <= kMaxRowWords;
   const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
   uint32_t* my = s_row + threadIdx.x * kMaxRowWords;
-  const int bb = a.bin_bytes;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int row = rows ? rows[i] : static_cast<int>(i);
@@ -91,10 +92,10 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
         const NodeInfo nd = STAGED ? s_node[node] : MakeNode(a, t, node);
         uint32_t gb;
         if (stage_row) {
-          gb = bb == 1 ? ((my[nd.group >> 2] >> (8 * (nd.group & 3))) & 0xffu)
-                       : ((my[nd.group >> 1] >> (16 * (nd.group & 1))) & 0xffffu);
+          const uint8_t* rb = reinterpret_cast<const uint8_t*>(my) + nd.gbyte;
+          gb = nd.gwide ? static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(rb)) : static_cast<uint32_t>(*rb);
         } else {
-          gb = RowBin(a, row, nd.group);
+          gb = RowBin(a, row, nd.gbyte, nd.gwide);
         }
         const uint32_t bin = (gb < static_cast<uint32_t>(nd.sub_lo) || gb >= static_cast<uint32_t>(nd.sub_hi))
                                  ? static_cast<uint32_t>(nd.mfb)
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256) void k_tree_bitmaps(KArgs a, DevTree t) {
   if ((threadIdx.x & 63) == 0) t.bm_work[node * 4 + (threadIdx.x >> 6)] = m;
   if (threadIdx.x == 0) {
     // group byte offset | left child (16 bits, two's complement leaves) | right child
-    t.bm_meta[node * 3 + 0] = nd.group;
+    t.bm_meta[node * 3 + 0] = nd.gbyte;
     t.bm_meta[node * 3 + 1] = nd.left;
     t.bm_meta[node * 3 + 2] = nd.right;
   }

@@ -122,7 +122,7 @@ void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
   UploadData();
   global_count_.assign(config_->num_leaves, 0);
   Log::Info("MI355X learner on device %d (%d CUs): %d rows, %d groups, %d histogram bins, %s bins, %d hist tiles",
-            device_id_, cus, num_data_, num_groups_, total_bins_, args_.bin_bytes == 1 ? "8-bit" : "16-bit",
+            device_id_, cus, num_data_, num_groups_, total_bins_, args_.bin_bytes == 1 ? "8-bit" : (args_.bin_bytes == 2 ? "16-bit" : "8/16-bit"),
             args_.hist_tiles);
 }
 
@@ -132,10 +132,45 @@ void GPUTreeLearner::UploadData() {
   int max_group_bins = 0;
   for (int g = 0; g < num_groups_; ++g) max_group_bins = std::max(max_group_bins, data_->group(g).num_total_bin);
   if (max_group_bins > 65536) Log::Fatal("device learner: a feature group has more than 65536 bins");
-  const int bin_bytes = max_group_bins <= 256 ? 1 : 2;
-  const int gpw = 4 / bin_bytes;
-  const int wpr = std::max(1, (num_groups_ + gpw - 1) / gpw);
+  // row layout: groups in order, 8-bit groups four to a 32-bit word, 16-bit groups (more than
+  // 256 bins) two to a word; a group of the other width starts a new word.  One wide group no
+  // longer widens every column (LGBM_AMD_UNIFORM_BINS=1: the uniform layout, for A/B runs)
+  const bool uniform = std::getenv("LGBM_AMD_UNIFORM_BINS") != nullptr && std::getenv("LGBM_AMD_UNIFORM_BINS")[0] == '1';
+  h_gwide_.assign(num_groups_, 0);
+  h_gbyte_.assign(num_groups_, 0);
+  h_word_of_group_.assign(num_groups_, 0);
+  h_word_g0_.clear();
+  h_word_wide_.clear();
+  int n_wide = 0;
+  for (int g = 0; g < num_groups_; ++g) {
+    h_gwide_[g] = (data_->group(g).num_total_bin > 256 || (uniform && max_group_bins > 256)) ? 1 : 0;
+    n_wide += h_gwide_[g];
+  }
+  int slot = 0;
+  for (int g = 0; g < num_groups_; ++g) {
+    const int wide = h_gwide_[g], per = wide ? 2 : 4;
+    if (h_word_g0_.empty() || h_word_wide_.back() != wide || slot == per) {
+      h_word_g0_.push_back(g);
+      h_word_wide_.push_back(static_cast<int8_t>(wide));
+      slot = 0;
+    }
+    const int w = static_cast<int>(h_word_g0_.size()) - 1;
+    h_word_of_group_[g] = w;
+    h_gbyte_[g] = 4 * w + slot * (wide ? 2 : 1);
+    ++slot;
+  }
+  if (h_word_g0_.empty()) {
+    h_word_g0_.push_back(0);
+    h_word_wide_.push_back(0);
+  }
+  const int wpr = static_cast<int>(h_word_g0_.size());
+  h_word_g0_.push_back(num_groups_);  // sentinel
+  const int bin_bytes = n_wide == 0 ? 1 : (n_wide == num_groups_ ? 2 : 0);
   const size_t row_bytes = static_cast<size_t>(wpr) * 4;
+  d_word_g0_ = Alloc<int32_t>(h_word_g0_.size());
+  HIPCHECK(hipMemcpy(d_word_g0_, h_word_g0_.data(), sizeof(int32_t) * h_word_g0_.size(), hipMemcpyHostToDevice));
+  d_word_wide_ = Alloc<int8_t>(h_word_wide_.size());
+  HIPCHECK(hipMemcpy(d_word_wide_, h_word_wide_.data(), h_word_wide_.size(), hipMemcpyHostToDevice));
   // row-major bin matrix (the dataset stores columns)
   args_.bin_bytes = bin_bytes;
   args_.words_per_row = wpr;
@@ -148,21 +183,23 @@ void GPUTreeLearner::UploadData() {
   // second copy of the matrix -- kept when that copy is under 8 GiB (LGBM_AMD_COLUMN_COPY=0/1
   // forces it off / on); without it the partition reads the row-major matrix
   d_bins_col_ = nullptr;
-  const size_t col_bytes = static_cast<size_t>(num_data_) * num_groups_ * bin_bytes;
+  std::vector<int64_t> col_off(num_groups_ + 1, 0);
+  for (int g = 0; g < num_groups_; ++g) col_off[g + 1] = col_off[g] + static_cast<int64_t>(num_data_) * (h_gwide_[g] ? 2 : 1);
+  const size_t col_bytes = static_cast<size_t>(col_off[num_groups_]);
   bool col_copy = col_bytes <= (size_t(8) << 30);
   if (const char* cc = std::getenv("LGBM_AMD_COLUMN_COPY")) col_copy = cc[0] == '1';
   if (col_copy) {
-    std::vector<uint8_t> col(static_cast<size_t>(num_data_) * num_groups_ * bin_bytes);
+    std::vector<uint8_t> col(std::max<size_t>(1, col_bytes));
 #pragma omp parallel for schedule(static)
     for (int g = 0; g < num_groups_; ++g) {
       const FeatureGroup& grp = data_->group(g);
-      uint8_t* dst = col.data() + static_cast<size_t>(g) * num_data_ * bin_bytes;
-      if (bin_bytes == 1 && grp.bin_bytes == 1) {
+      uint8_t* dst = col.data() + col_off[g];
+      if (!h_gwide_[g] && grp.bin_bytes == 1) {
         std::memcpy(dst, grp.data.data(), static_cast<size_t>(num_data_));
       } else {
         for (data_size_t r = 0; r < num_data_; ++r) {
           const uint32_t v = grp.Get(r);
-          if (bin_bytes == 1) dst[r] = static_cast<uint8_t>(v);
+          if (!h_gwide_[g]) dst[r] = static_cast<uint8_t>(v);
           else reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(v);
         }
       }
@@ -188,6 +225,9 @@ void GPUTreeLearner::UploadData() {
     F.sub_hi = static_cast<int32_t>(data_->group(g).bin_offsets[sub + 1]);
     F.real_index = data_->RealFeatureIndex(f);
     F.monotone = meta_[f].monotone_type;
+    F.gbyte = h_gbyte_[g];
+    F.gwide = h_gwide_[g];
+    F.col_off = col_off[g];
     F.penalty = meta_[f].penalty;
   }
   d_feat_ = Alloc<dev::Feature>(num_features_);
@@ -203,7 +243,7 @@ void GPUTreeLearner::UploadData() {
   auto tile_bins_for = [&](int tw) {
     int mx = 0;
     for (int w0 = 0; w0 < wpr; w0 += tw) {
-      const int g0 = w0 * gpw, g1 = std::min(num_groups_, (w0 + tw) * gpw);
+      const int g0 = h_word_g0_[w0], g1 = h_word_g0_[std::min(wpr, w0 + tw)];
       if (g0 >= num_groups_) break;
       const int lo = goff[g0], hi = g1 < num_groups_ ? goff[g1] : total_bins_;
       mx = std::max(mx, hi - lo);
@@ -348,6 +388,8 @@ void GPUTreeLearner::UploadData() {
   a.root_identity = 1;
   a.bin_bytes = bin_bytes;
   a.words_per_row = wpr;
+  a.word_g0 = d_word_g0_;
+  a.word_wide = d_word_wide_;
   a.tile_words = tile_words;
   a.hist_tiles = (wpr + tile_words - 1) / tile_words;
   a.tile_w0 = 0;
@@ -435,8 +477,8 @@ void GPUTreeLearner::UploadData() {
         g_hi = std::max(g_hi, feats[f].group + 1);
       }
       if (g_lo < g_hi) {
-        a.tile_w0 = g_lo / gpw;
-        a.tile_w1 = (g_hi + gpw - 1) / gpw;
+        a.tile_w0 = h_word_of_group_[g_lo];
+        a.tile_w1 = h_word_of_group_[g_hi - 1] + 1;
       } else {  // no features: one tile of redundant work keeps the partition's launch shape
         a.tile_w0 = 0;
         a.tile_w1 = std::min(wpr, tile_words);
@@ -1444,10 +1486,9 @@ bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction
 }
 
 // ---------------------------------------------------------------- binned rows
-// row-major copy of a dataset's storage columns in this learner's layout (bin_bytes per
-// group, rows padded to whole 32-bit words)
+// row-major copy of a dataset's storage columns in this learner's layout (each group at its
+// byte of the row, 8 or 16 bits; rows padded to whole 32-bit words)
 std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d) const {
-  const int bb = args_.bin_bytes;
   const size_t row_bytes = static_cast<size_t>(args_.words_per_row) * 4;
   const data_size_t n = d->num_data();
   const int ng = d->num_groups();
@@ -1457,8 +1498,8 @@ std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d) const {
     uint8_t* row = host.data() + static_cast<size_t>(r) * row_bytes;
     for (int g = 0; g < ng; ++g) {
       const uint32_t v = d->group(g).Get(r);
-      if (bb == 1) row[g] = static_cast<uint8_t>(v);
-      else reinterpret_cast<uint16_t*>(row)[g] = static_cast<uint16_t>(v);
+      if (!h_gwide_[g]) row[h_gbyte_[g]] = static_cast<uint8_t>(v);
+      else reinterpret_cast<uint16_t*>(row + h_gbyte_[g])[0] = static_cast<uint16_t>(v);
     }
   }
   return host;

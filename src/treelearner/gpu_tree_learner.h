@@ -202,6 +202,12 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   double* d_scales_ = nullptr;
   uint32_t* d_absmax_ = nullptr;
   uint8_t* d_bins_col_ = nullptr;
+  // row layout (KArgs::bin_bytes / word_g0): per group its byte in a row and width, the
+  // word holding it; per word its first group (+ sentinel) and width
+  std::vector<int32_t> h_gbyte_, h_word_of_group_, h_word_g0_;
+  std::vector<int8_t> h_gwide_, h_word_wide_;
+  int32_t* d_word_g0_ = nullptr;
+  int8_t* d_word_wide_ = nullptr;
   dev::FeatureBest* d_feat_best_ = nullptr;
   uint32_t* d_feat_cat_ = nullptr;  // category sets of the per-feature categorical bests
   uint32_t* h_absmax_ = nullptr;

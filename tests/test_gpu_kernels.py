@@ -67,6 +67,12 @@ CASES = {
     "bagging": ({"bagging_fraction": 0.7, "bagging_freq": 1, "bagging_seed": 3}, 20000),
     "multi_block": ({"num_leaves": 63}, 150000),
     "efb": ({"max_bin": 31}, 30000),
+    # one 511-bin group among 63-bin ones: 16-bit words next to 8-bit words in each row
+    "mixed_width": ({"max_bin_by_feature": [63] * 7 + [511] + [63] * 2}, 20000),
+    "mixed_width_dp": ({"max_bin_by_feature": [511] + [63] * 9, "gpu_use_dp": True}, 20000),
+    # the same data with every group widened to 16 bits (LGBM_AMD_UNIFORM_BINS=1)
+    "uniform_wide": ({"max_bin_by_feature": [63] * 7 + [511] + [63] * 2, "_env": {"LGBM_AMD_UNIFORM_BINS": "1"}},
+                     20000),
 }
 
 
@@ -118,14 +124,23 @@ def _quantise(v, scale):
 
 
 @pytest.mark.parametrize("case", list(CASES))
-def test_device_tree_state(gpu_available, case):
+def test_device_tree_state(gpu_available, case, monkeypatch):
     import torch
     extra, n = CASES[case]
     X, y = (_efb_data if case == "efb" else _data)(n)
     params = dict(BASE, **extra)
     cat = params.pop("categorical_feature", "auto")
+    for k, v in params.pop("_env", {}).items():
+        monkeypatch.setenv(k, v)
     ds = lgb.Dataset(X, y, params=params, categorical_feature=cat, free_raw_data=False)
     bst = lgb.train(params, ds, 4, verbose_eval=False, keep_training_booster=True)
+    # the device training scores (tree walks over the binned rows) equal the CPU predictor's
+    got = ctypes.c_int64(0)
+    train_pred = np.zeros(n, dtype=np.float64)
+    nat.call("LGBM_BoosterGetPredict", bst.handle, ctypes.c_int(0), ctypes.byref(got),
+             train_pred.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    assert got.value == n
+    np.testing.assert_allclose(train_pred, bst.predict(X), rtol=1e-9, atol=1e-12)
     num_leaves = bst.dump_model()["tree_info"][-1]["num_leaves"]
     assert num_leaves > 4
 

@@ -54,6 +54,15 @@ def main():
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--verbose", type=int, default=-1)
     args = ap.parse_args()
+    import threading
+    t_start = time.time()
+    stop = threading.Event()
+
+    def heartbeat():  # long setups (11M x 700) print progress for job monitors
+        while not stop.wait(30.0):
+            print("[bench_workload] %.0f s elapsed" % (time.time() - t_start), file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     import lightgbmv1_amd as lgb
     from lightgbmv1_amd import models
 
@@ -89,7 +98,9 @@ def main():
         "speedup_vs_ref": None if ref is None else round(ref / 500.0 / sec, 2),
         "rows_scaled": rows != w.rows, "trees": args.warmup + args.steps, **quality,
         "setup_s": round(setup_s, 1), "data": "synthetic",
+        "env": {k: v for k, v in os.environ.items() if k.startswith("LGBM_AMD_")},
     }))
+    stop.set()
 
 
 if __name__ == "__main__":
