@@ -125,6 +125,37 @@ __device__ T BlockSum(T v, T* sh) {
   return r;
 }
 
+// Write-through publication of a record that another workgroup of the same launch reads
+// (the split scans' per-feature results, read by the picking workgroup): 8-byte agent-scope
+// relaxed atomic stores are `global_store ... sc1` on gfx950 -- the bytes leave the XCD's L2
+// at once, so no release fence (an L2 write-back, serialised per XCD: ~15 ns per workgroup
+// of a 4000-workgroup launch, tools/microbench/wg_throughput.hip) is needed.  The writing
+// waves drain them (s_waitcnt vmcnt(0)) before the arrival counter is bumped; the picker
+// takes one agent-scope acquire (cdna_hip_programming.md Guideline 16, R1).
+typedef __attribute__((address_space(1))) unsigned long long GlobalU64;
+template <typename T>
+__device__ __forceinline__ void PublishRecord(T* dst, const T& v) {
+  static_assert(sizeof(T) % 8 == 0, "8-byte words");
+  GlobalU64* d = (GlobalU64*)(dst);
+#pragma unroll
+  for (int i = 0; i < static_cast<int>(sizeof(T) / 8); ++i) {
+    unsigned long long w;  // (memcpy: the record's fields are not u64 -- no type-punned loads)
+    __builtin_memcpy(&w, reinterpret_cast<const char*>(&v) + 8 * i, 8);
+    __hip_atomic_store(d + i, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+__device__ __forceinline__ void PublishF64(double* dst, double v) {
+  __hip_atomic_store((GlobalU64*)(dst), static_cast<unsigned long long>(__double_as_longlong(v)), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void PublishI32(int32_t* dst, int32_t v) {
+  typedef __attribute__((address_space(1))) int32_t GlobalI32;
+  __hip_atomic_store((GlobalI32*)(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+struct CatWords {
+  uint32_t w[kMaxCatWords];
+};
+
 // SplitInfo ordering: larger gain first, then smaller real feature index (NaN = -inf)
 __device__ __forceinline__ bool SplitBetter(double ga, int fa, double gb, int fb) {
   if (ga != ga) ga = -INFINITY;

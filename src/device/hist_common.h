@@ -16,10 +16,30 @@ struct TileCtx {
   float sg, sh;         // fixed-point scales
 };
 
+// row-sparse storage (KArgs::sp_ptr) takes the GPW slot of the kernels' templates
+constexpr int kSparseGPW = 1;
+constexpr int kSparseTeam = 4;  // threads per row of a row-sparse gather
+constexpr int kSparsePer = 4;   // entries per thread and row loaded up front
+
 // GPW: groups per word (4: 8-bit layout, 2: 16-bit layout, 0: mixed layout, one more round
-// trip for the word table); otherwise every load is independent of the others
+// trip for the word table) or kSparseGPW; otherwise every load is independent of the others
 template <int GPW>
 __device__ __forceinline__ void InitTile(const KArgs& a, TileCtx* t) {
+  if (GPW == kSparseGPW) {  // tile = bin range; kSparseTeam threads per row
+    t->lo_bin = (a.tile_w0 + blockIdx.y) * a.tile_bins;
+    t->nbins = min(a.p.total_bins, t->lo_bin + a.tile_bins) - t->lo_bin;
+    t->w0 = t->w1 = 0;
+    t->tpr = kSparseTeam;
+    t->rpp = kHistThreads / kSparseTeam;
+    t->q = threadIdx.x % kSparseTeam;
+    t->rs = threadIdx.x / kSparseTeam;
+    t->bits = 0;
+    t->sg = static_cast<float>(a.scales[0]);
+    t->sh = static_cast<float>(a.scales[1]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) t->goff[j] = -1;
+    return;
+  }
   t->w0 = a.tile_w0 + blockIdx.y * a.tile_words;
   t->w1 = min(a.tile_w1, t->w0 + a.tile_words);
   t->tpr = t->w1 - t->w0;
@@ -82,6 +102,54 @@ __device__ __forceinline__ void AddRow(unsigned long long* lds, const int* goff,
         atomicAdd(&lds[2 * (goff[j] + b) + 1], static_cast<unsigned long long>(hq));
       }
     }
+  }
+}
+
+// row-sparse gather of K rows (rr[k] < 0: none) with values v[k]: the kSparseTeam threads of
+// a row take its entries round robin; the first kSparsePer entries of each thread and row are
+// loaded together (rows of up to kSparseTeam * kSparsePer entries cost one round trip after
+// their bounds), longer rows finish in a loop.  Entries outside the tile's bin range are skipped.
+template <int K, int UNITS>
+__device__ __forceinline__ void AddSparseRows(const KArgs& a, unsigned long long* lds, const TileCtx& t,
+                                              const int* rr, const float2* v) {
+  int64_t beg[K];
+  int cnt[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int x = rr[k] >= 0 ? rr[k] : 0;
+    beg[k] = a.sp_ptr[x];
+    const int64_t end = a.sp_ptr[x + 1];
+    cnt[k] = rr[k] >= 0 ? static_cast<int>(end - beg[k]) : 0;
+  }
+  uint32_t e[K][kSparsePer];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int m = 0; m < kSparsePer; ++m) {
+      const int j = t.q + m * kSparseTeam;
+      e[k][m] = j < cnt[k] ? static_cast<uint32_t>(a.sp_bin[beg[k] + j]) : 0xffffffffu;
+    }
+  }
+  const uint32_t lo = static_cast<uint32_t>(t.lo_bin), nb = static_cast<uint32_t>(t.nbins);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const long long gq = __float2ll_rn(v[k].x * t.sg);
+    const long long hq = __float2ll_rn(v[k].y * t.sh);
+    const unsigned long long pk = (static_cast<unsigned long long>(gq) << 32) + static_cast<unsigned long long>(hq);
+    auto add = [&](uint32_t bin) {
+      const uint32_t b = bin - lo;
+      if (b < nb) {
+        if (UNITS == 1) {
+          atomicAdd(&lds[b], pk);
+        } else {
+          atomicAdd(&lds[2 * b], static_cast<unsigned long long>(gq));
+          atomicAdd(&lds[2 * b + 1], static_cast<unsigned long long>(hq));
+        }
+      }
+    };
+#pragma unroll
+    for (int m = 0; m < kSparsePer; ++m) add(e[k][m]);
+    for (int j = t.q + kSparseTeam * kSparsePer; j < cnt[k]; j += kSparseTeam) add(a.sp_bin[beg[k] + j]);
   }
 }
 

@@ -5,7 +5,8 @@
 // are built by k_split (partition_kernels.hip) together with the row partition.
 //
 // Layout: row-major bin matrix (one 32-bit word = 4 uint8 or 2 uint16 storage columns; a
-// mixed layout keeps 8-bit groups 4 to a word next to words of 16-bit groups).
+// mixed layout keeps 8-bit groups 4 to a word next to words of 16-bit groups), or row-sparse
+// lists of each row's stored bins (hist_common.h AddSparseRows).
 // Grid: (row workgroups, column tiles) of 1024-thread workgroups.  A workgroup accumulates
 // an LDS-private histogram of its tile's columns over one row block at a time and stores it
 // whole as that block's partial histogram -- no global atomics (on gfx950 those execute at
@@ -77,17 +78,24 @@ __device__ __forceinline__ void HistBlock(const KArgs& a, unsigned long long* ld
         }
       }
       float2 v[kRowsInFlight];
-      uint32_t wd[kRowsInFlight];
-#pragma unroll
-      for (int k = 0; k < kRowsInFlight; ++k) {
-        const int rr = r[k] >= 0 ? r[k] : 0;
-        v[k] = gh[rr];
-        wd[k] = r[k] >= 0 ? bins32[rr * wpr + w] : 0u;  // word 0: every bin skipped
-      }
       int rn[kRowsInFlight];
-      LoadRowIdx(src, i + stride, r1, t.rpp, rn);  // next batch, in flight during the atomics
+      if constexpr (GPW == kSparseGPW) {
 #pragma unroll
-      for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
+        for (int k = 0; k < kRowsInFlight; ++k) v[k] = gh[r[k] >= 0 ? r[k] : 0];
+        LoadRowIdx(src, i + stride, r1, t.rpp, rn);
+        AddSparseRows<kRowsInFlight, UNITS>(a, lds, t, r, v);
+      } else {
+        uint32_t wd[kRowsInFlight];
+#pragma unroll
+        for (int k = 0; k < kRowsInFlight; ++k) {
+          const int rr = r[k] >= 0 ? r[k] : 0;
+          v[k] = gh[rr];
+          wd[k] = r[k] >= 0 ? bins32[rr * wpr + w] : 0u;  // word 0: every bin skipped
+        }
+        LoadRowIdx(src, i + stride, r1, t.rpp, rn);  // next batch, in flight during the atomics
+#pragma unroll
+        for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
+      }
 #pragma unroll
       for (int k = 0; k < kRowsInFlight; ++k) r[k] = rn[k];
     }
@@ -210,7 +218,10 @@ static void LaunchHist(const KArgs& a, hipStream_t s) {
   const size_t lds_bytes = sizeof(unsigned long long) * a.hist_units * static_cast<size_t>(a.tile_bins);
 
   const dim3 grid(a.root_grid, a.hist_tiles);
-  if (a.hist_units == 1) {
+  if (a.sp_ptr != nullptr) {
+    if (a.hist_units == 1) hipLaunchKernelGGL((k_hist<MODE, kSparseGPW, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    else hipLaunchKernelGGL((k_hist<MODE, kSparseGPW, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
+  } else if (a.hist_units == 1) {
     if (a.bin_bytes == 1) hipLaunchKernelGGL((k_hist<MODE, 4, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_hist<MODE, 2, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
     else hipLaunchKernelGGL((k_hist<MODE, 0, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
@@ -248,6 +259,10 @@ void PrepareKernels() {
   AllowLds(k_hist<0, 0, 2>);
   AllowLds(k_hist<2, 0, 1>);
   AllowLds(k_hist<2, 0, 2>);
+  AllowLds(k_hist<0, kSparseGPW, 1>);
+  AllowLds(k_hist<0, kSparseGPW, 2>);
+  AllowLds(k_hist<2, kSparseGPW, 1>);
+  AllowLds(k_hist<2, kSparseGPW, 2>);
   PrepareSplitKernels(MaxDynLds());
 }
 

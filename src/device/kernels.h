@@ -48,6 +48,12 @@ struct KArgs {
   int32_t words_per_row;     // 32-bit words per row
   const int32_t* word_g0;    // [words_per_row + 1] first group of each word (mixed layouts)
   const int8_t* word_wide;   // [words_per_row] word holds 16-bit groups (mixed layouts)
+  // row-sparse storage (reference MultiValSparseBin, multi_val_sparse_bin.hpp): the stored
+  // histogram bins of row r -- group_off[g] + bin for every group whose bin is not 0,
+  // ascending -- are sp_bin[sp_ptr[r] .. sp_ptr[r + 1]); null: the word matrix `bins`.  The
+  // histogram column tiles are then plain bin ranges of tile_bins each
+  const int64_t* sp_ptr;
+  const uint16_t* sp_bin;
   int32_t hist_tiles;        // column tiles of the histogram kernel
   int32_t tile_words;        // words per column tile
   int32_t tile_bins;         // max histogram bins of one tile (LDS words)

@@ -13,8 +13,9 @@
 //     exact integer sums, so the order never changes a result); the rows of the histogrammed
 //     child are compacted into an LDS row list.  Only column tile 0 writes the partition.
 //  B. word per thread: the listed rows' bin words and (g, h) are gathered and added to the
-//     LDS histogram of the tile (hist_common.h); the block's histogram is stored as a
-//     partial when its sub-tiles are done.
+//     LDS histogram of the tile (hist_common.h); row-sparse storage: kSparseTeam threads per
+//     listed row walk its stored bins.  The block's histogram is stored as a partial when
+//     its sub-tiles are done.
 // The histogrammed child is the one with fewer rows by the split's estimated counts (the
 // pick sets Step::hist_left): if the estimate is off, the larger child is histogrammed and
 // the smaller one derived -- exact integer sums make both ways bit-identical.  The final
@@ -71,6 +72,12 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
   TileCtx t;
   if (HIST) InitTile<GPW>(a, &t);
   if (done) return;
+  if (HIST && blockIdx.x == 0 && blockIdx.y == 0) {
+    // the parent's splittable row, before the children's scans overwrite it (their scans skip
+    // what the parent could not split on)
+    const int8_t* prow = a.splittable + static_cast<size_t>(cs.parent_frow) * a.p.num_features;
+    for (int f = threadIdx.x; f < a.p.num_features; f += kPartThreads) a.parent_flags[f] = prow[f];
+  }
   const int ts = a.host_mode ? -1 : s;
   KTraceAt(a, ts, kTrSplitEntry, t_entry);
   const int nblk = HIST ? StepBlocks(a, pc) : (pc + kSplitSub - 1) / kSplitSub;
@@ -185,16 +192,23 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
             rr[k] = j < nh ? rowlist[j] : -1;
           }
           float2 v[kGatherRows];
-          uint32_t wd[kGatherRows];
+          if constexpr (GPW == kSparseGPW) {
 #pragma unroll
-          for (int k = 0; k < kGatherRows; ++k) {
-            const int x = rr[k] >= 0 ? rr[k] : 0;
-            v[k] = gh[x];
-            wd[k] = rr[k] >= 0 ? bins32[x * wpr + wi] : 0u;  // word 0: every bin skipped
+            for (int k = 0; k < kGatherRows; ++k) v[k] = gh[rr[k] >= 0 ? rr[k] : 0];
+            if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
+            AddSparseRows<kGatherRows, UNITS>(a, lds, t, rr, v);
+          } else {
+            uint32_t wd[kGatherRows];
+#pragma unroll
+            for (int k = 0; k < kGatherRows; ++k) {
+              const int x = rr[k] >= 0 ? rr[k] : 0;
+              v[k] = gh[x];
+              wd[k] = rr[k] >= 0 ? bins32[x * wpr + wi] : 0u;  // word 0: every bin skipped
+            }
+            if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
+#pragma unroll
+            for (int k = 0; k < kGatherRows; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
           }
-          if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
-#pragma unroll
-          for (int k = 0; k < kGatherRows; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
           if (loc_sums && t.q == 0) {
 #pragma unroll
             for (int k = 0; k < kGatherRows; ++k) {
@@ -243,7 +257,10 @@ void SplitStep(const KArgs& a, hipStream_t s, bool reduce) {
   const dim3 grid(a.split_grid, a.hist_tiles);
   const size_t lds = SplitLds(a);
 
-  if (a.hist_units == 1) {
+  if (a.sp_ptr != nullptr) {
+    if (a.hist_units == 1) hipLaunchKernelGGL((k_split<kSparseGPW, 1, true>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_split<kSparseGPW, 2, true>), grid, dim3(kPartThreads), lds, s, a);
+  } else if (a.hist_units == 1) {
     if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 1, true>), grid, dim3(kPartThreads), lds, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 1, true>), grid, dim3(kPartThreads), lds, s, a);
     else hipLaunchKernelGGL((k_split<0, 1, true>), grid, dim3(kPartThreads), lds, s, a);
@@ -262,6 +279,8 @@ void PrepareSplitKernels(int mx) {
   AllowLds(k_split<2, 2, true>, mx);
   AllowLds(k_split<0, 1, true>, mx);
   AllowLds(k_split<0, 2, true>, mx);
+  AllowLds(k_split<kSparseGPW, 1, true>, mx);
+  AllowLds(k_split<kSparseGPW, 2, true>, mx);
 }
 
 void Partition(const KArgs& a, hipStream_t s) {

@@ -13,8 +13,8 @@
 //     host loop's order).  Every load of the pick is independent of the others (one round
 //     trip) except the winner's records.
 //  3. record (thread 0): Step::cs / lr / hist_left for the next k_split, the children's
-//     constraint ranges, the split record; the workgroup snapshots the parent's splittable
-//     row (the children's scans overwrite it).
+//     constraint ranges, the split record (k_split snapshots the parent's splittable row
+//     before the children's scans overwrite it).
 #pragma once
 
 #include "device_common.h"
@@ -211,9 +211,9 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
     lrf = a.best[lane].real_feature;
     lfv = a.best[lane].feature;
   }
-  int fi[2] = {-1, -1};
-  double fg[2] = {-INFINITY, -INFINITY};
-  int frf[2] = {-1, -1};
+  // (scalars, not arrays indexed by the rolled side loop: those would live in scratch)
+  int fi0 = -1, fi1 = -1, frf0 = -1, frf1 = -1;
+  double fg0 = -INFINITY, fg1 = -INFINITY;
 #pragma unroll 1
   for (int side = 0; side < fresh; ++side) {
     double g = -INFINITY;
@@ -239,9 +239,15 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
     }
     WaveArgBest(&g, &rf, &idx, &unused);
     if (idx >= 0 && g == -INFINITY) idx = -1;  // no valid threshold on any feature
-    fi[side] = idx;
-    fg[side] = idx >= 0 ? g : -INFINITY;
-    frf[side] = idx >= 0 ? rf : -1;
+    if (side == 0) {
+      fi0 = idx;
+      fg0 = idx >= 0 ? g : -INFINITY;
+      frf0 = idx >= 0 ? rf : -1;
+    } else {
+      fi1 = idx;
+      fg1 = idx >= 0 ? g : -INFINITY;
+      frf1 = idx >= 0 ? rf : -1;
+    }
   }
   if (a.ktrace != nullptr && lane == 0 && s - 1 >= 0) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -256,13 +262,13 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
     double cg;
     int crf, cf;
     if (fresh >= 1 && l == sm) {
-      cg = fg[0];
-      crf = frf[0];
-      cf = fi[0];
+      cg = fg0;
+      crf = frf0;
+      cf = fi0;
     } else if (fresh == 2 && l == lg) {
-      cg = fg[1];
-      crf = frf[1];
-      cf = fi[1];
+      cg = fg1;
+      crf = frf1;
+      cf = fi1;
     } else if (l == lane) {
       cg = lgv;
       crf = lrf;
@@ -287,8 +293,8 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
   }
   out->s = s;
   out->leaf = leaf;
-  out->fresh_idx[0] = fi[0];
-  out->fresh_idx[1] = fi[1];
+  out->fresh_idx[0] = fi0;
+  out->fresh_idx[1] = fi1;
   pl->win_feature = wf;
   out->done = (g > 0.0 && wf >= 0) ? 0 : 1;
 }
@@ -305,7 +311,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
   const int tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
   PickResult* pk = &pl->pk;
   // 1. bookkeeping, by a thread outside the picking wave (its stores do not hold up the
-  //    wave's loads)
+  //    wave's loads; one-wave workgroups: by the wave's first thread, before the pick)
   if (root) {
     if (tid == 0) {
       pl->s = 0;
@@ -315,7 +321,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
       pl->sm_frow = -1;
       pl->lg_frow = -1;
     }
-  } else if (tid == kWave) {
+  } else if (tid == (nthr > kWave ? kWave : 0)) {
     StepBookkeeping(a, st, pl);
   }
   __syncthreads();
@@ -402,7 +408,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     __syncthreads();
     PickTrace(a, ts, kTrPick4);
     // 5. loads that depend on the winner: the new leaf's splittable row id, the constraint
-    //    mask of the split feature, the parent's splittable row
+    //    mask of the split feature (the parent's splittable row is snapshot by k_split)
     const DeviceSplit& sp = pk->split;
     const int s = pk->s, nl = s + 1;
     int new_frow = 0;
@@ -411,20 +417,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
       new_frow = a.leaves[nl].frow;
       if (a.feat_icmask != nullptr) fmask = a.feat_icmask[sp.feature];
     }
-    const int8_t* prow = a.splittable + static_cast<size_t>(pk->P.frow) * a.p.num_features;
-    int8_t pflag[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int f = tid + k * nthr;
-      if (f < a.p.num_features) pflag[k] = prow[f];
-    }
-    for (int f = tid + 4 * nthr; f < a.p.num_features; f += nthr) a.parent_flags[f] = prow[f];
     // ---- stores only from here
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int f = tid + k * nthr;
-      if (f < a.p.num_features) a.parent_flags[f] = pflag[k];  // before the children's scans overwrite it
-    }
     // the fresh children's bests become part of the per-leaf table
     for (int side = 0; side < fresh; ++side) {
       const int l = side == 0 ? pl->sm : pl->lg;

@@ -38,6 +38,7 @@ struct NodeInfo {
   int32_t sub_lo, sub_hi, offset, mfb, default_bin, max_bin;
   uint32_t threshold;
   int32_t left, right;
+  int64_t col_off;                 // the group's column (row-sparse training storage)
 };
 }  // namespace
 
@@ -48,6 +49,7 @@ __device__ __forceinline__ NodeInfo MakeNode(const KArgs& a, const DevTree& t, i
     NodeInfo nd;
     nd.gbyte = F.gbyte;
     nd.gwide = static_cast<int16_t>(F.gwide);
+    nd.col_off = F.col_off;
     nd.left_is_default = (dt & 2) ? 1 : 0;
     nd.missing_type = static_cast<int16_t>((dt >> 2) & 3);
     nd.is_cat = (dt & 1) ? 1 : 0;
@@ -77,7 +79,8 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
   }
   __syncthreads();
   const int wpr = a.words_per_row;
-  const bool stage_row = wpr <= kMaxRowWords;
+  const bool words = a.bins != nullptr;  // else row-sparse training storage: the column copy
+  const bool stage_row = words && wpr <= kMaxRowWords;
   const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
   uint32_t* my = s_row + threadIdx.x * kMaxRowWords;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
           const uint8_t* rb = reinterpret_cast<const uint8_t*>(my) + nd.gbyte;
           gb = nd.gwide ? static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(rb)) : static_cast<uint32_t>(*rb);
         } else {
-          gb = RowBin(a, row, nd.gbyte, nd.gwide);
+          gb = words ? RowBin(a, row, nd.gbyte, nd.gwide) : ColBin(a, row, nd.gbyte, nd.gwide, nd.col_off);
         }
         const uint32_t bin = (gb < static_cast<uint32_t>(nd.sub_lo) || gb >= static_cast<uint32_t>(nd.sub_hi))
                                  ? static_cast<uint32_t>(nd.mfb)
@@ -199,7 +202,7 @@ void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t
                   hipStream_t s) {
   if (num_rows <= 0) return;
   const int ni = t.num_leaves - 1;
-  if (rows == nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.words_per_row * 4 <= kBmMaxRowBytes &&
+  if (rows == nullptr && a.bins != nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.words_per_row * 4 <= kBmMaxRowBytes &&
       t.bm_work != nullptr) {
     hipLaunchKernelGGL(k_tree_bitmaps, dim3(ni), dim3(256), 0, s, a, t);
     // one chunk of rows per workgroup: every chunk's loads are in flight at once

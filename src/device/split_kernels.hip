@@ -62,16 +62,18 @@ struct LeafCtx {
   ConstraintRange c;
 };
 
-// block-wide scans / reductions of the split scan (kFindThreads threads); every thread
-// calls them, results are returned to every thread
+// block-wide scans / reductions of the split scan (NT threads: kFindThreads, or one wave per
+// workgroup for narrow features); every thread calls them, results are returned to every thread
+template <int NT>
 struct BlockScratch {
-  double d[2][kFindThreads / kWave];
-  int i[kFindThreads / kWave];
-  Cand c[kFindThreads / kWave];
+  double d[2][NT / kWave];
+  int i[NT / kWave];
+  Cand c[NT / kWave];
 };
-constexpr int kFindWaves = kFindThreads / kWave;
 
-__device__ __forceinline__ void BlockScan3(double& a, double& b, int& c, bool suffix, BlockScratch* sc) {
+template <int NT>
+__device__ __forceinline__ void BlockScan3(double& a, double& b, int& c, bool suffix, BlockScratch<NT>* sc) {
+  constexpr int kFindWaves = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   a = suffix ? WaveSuffixIncl(a) : WavePrefixIncl(a);
   b = suffix ? WaveSuffixIncl(b) : WavePrefixIncl(b);
@@ -98,7 +100,9 @@ __device__ __forceinline__ void BlockScan3(double& a, double& b, int& c, bool su
   c += oc;
 }
 
-__device__ __forceinline__ void BlockSum3(double& a, double& b, int& c, BlockScratch* sc) {
+template <int NT>
+__device__ __forceinline__ void BlockSum3(double& a, double& b, int& c, BlockScratch<NT>* sc) {
+  constexpr int kFindWaves = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   a = WaveSum(a);
   b = WaveSum(b);
@@ -120,7 +124,9 @@ __device__ __forceinline__ void BlockSum3(double& a, double& b, int& c, BlockScr
   __syncthreads();
 }
 
-__device__ __forceinline__ bool BlockAny(bool v, BlockScratch* sc) {
+template <int NT>
+__device__ __forceinline__ bool BlockAny(bool v, BlockScratch<NT>* sc) {
+  constexpr int kFindWaves = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const bool wv = __any(v);
   if (lane == 0) sc->i[w] = wv ? 1 : 0;
@@ -132,7 +138,9 @@ __device__ __forceinline__ bool BlockAny(bool v, BlockScratch* sc) {
   return r != 0;
 }
 
-__device__ __forceinline__ Cand BlockBestCand(Cand c, bool reverse, BlockScratch* sc) {
+template <int NT>
+__device__ __forceinline__ Cand BlockBestCand(Cand c, bool reverse, BlockScratch<NT>* sc) {
+  constexpr int kFindWaves = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   c = WaveBestCand(c, reverse);
   if (lane == 0) sc->c[w] = c;
@@ -173,12 +181,15 @@ struct ScanAcc {
   double ag, ah, ng, nh;
   int nc;
 };
+template <int NT>
 struct ScanScratch {
-  double d[6][kFindThreads / kWave];
-  int i[2][kFindThreads / kWave];
+  double d[6][NT / kWave];
+  int i[2][NT / kWave];
 };
 
-__device__ __forceinline__ void BlockScanNum(ScanAcc* v, ScanAcc* excl, ScanAcc* tot, ScanScratch* sc) {
+template <int NT>
+__device__ __forceinline__ void BlockScanNum(ScanAcc* v, ScanAcc* excl, ScanAcc* tot, ScanScratch<NT>* sc) {
+  constexpr int kFindWaves = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const double ig = WavePrefixIncl(v->g), ih = WavePrefixIncl(v->h);
   const int ic = WavePrefixIncl(v->c);
@@ -225,7 +236,9 @@ __device__ __forceinline__ void BlockScanNum(ScanAcc* v, ScanAcc* excl, ScanAcc*
 
 // the best candidates of both scan directions and whether any threshold was valid, over
 // the workgroup (reverse ties: higher threshold; forward ties: lower)
-__device__ __forceinline__ void BlockBestPair(Cand* rv, Cand* fw, bool* any, BlockScratch* sc, Cand* sc2) {
+template <int NT>
+__device__ __forceinline__ void BlockBestPair(Cand* rv, Cand* fw, bool* any, BlockScratch<NT>* sc, Cand* sc2) {
+  constexpr int kFindWaves = NT / kWave;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   *rv = WaveBestCand(*rv, true);
   *fw = WaveBestCand(*fw, false);
@@ -271,9 +284,9 @@ __device__ __forceinline__ double OutputOf(double sg, double sh, double l2, cons
 // Every candidate -- reverse at t (right = bins t..t_start), forward at t (left = bins
 // 0..t), and the forward "nothing stored on the left" start -- goes through one evaluation
 // site (instruction footprint: these kernels run once per split on a cold I-cache).
-template <bool SIMPLE>
+template <bool SIMPLE, int NT>
 __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
-                                   double mono_penalty, FeatureBest* out, BlockScratch* sc, ScanScratch* ssc,
+                                   double mono_penalty, FeatureBest* out, BlockScratch<NT>* sc, ScanScratch<NT>* ssc,
                                    Cand* sc2, int rthr) {
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
@@ -283,7 +296,7 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
   const bool na = two && F.missing_type == 2;
   const int fix_t = F.mfb > 0 ? F.mfb : -1;  // most frequent bin: not accumulated, rebuilt from the totals
   const int def_t = skip_def ? F.default_bin - offset : -1;  // the default bin: in no scan
-  const int K = (nb + kFindThreads - 1) / kFindThreads;
+  const int K = (nb + NT - 1) / NT;
   const int b0 = tid * K;
   const int b1 = min(nb, b0 + K);
   hv.fix_t = -1;
@@ -466,8 +479,10 @@ struct CatScratch {
 // computed in parallel -- and the sequential prefix scan from both ends (<= 2 x
 // max_cat_threshold steps, thread 0) with the min_data_per_group rules.
 // returns splittable (meaningful in thread 0)
+template <int NT>
 __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
-                                     FeatureBest* out, uint32_t* cat_out, BlockScratch* sc, CatScratch* cs) {
+                                     FeatureBest* out, uint32_t* cat_out, BlockScratch<NT>* sc, CatScratch* cs) {
+  constexpr int kFindThreads = NT;
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
   hv.fix_t = -1;
@@ -673,19 +688,21 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
   out->rg = L.sg - best.lg;
   out->rh = L.sh - best.lh - kEpsilon;
   out->gain = (best.gain - min_gain_shift) * F.penalty;
-  for (int w = 0; w < kMaxCatWords; ++w) cat_out[w] = 0u;
+  CatWords bits;  // (published whole: the picking workgroup reads the winner's set)
+  for (int w = 0; w < kMaxCatWords; ++w) bits.w[w] = 0u;
   if (onehot) {
     const int b = best.thr + offset;
-    cat_out[b >> 5] |= 1u << (b & 31);
+    bits.w[b >> 5] |= 1u << (b & 31);
     out->ncat = 1;
   } else {
     const int k = best.thr + 1;
     for (int i = 0; i < k; ++i) {
       const int b = (best_dir == 1 ? cs->sorted[i] : cs->sorted[cs->used_bin - 1 - i]) + offset;
-      cat_out[b >> 5] |= 1u << (b & 31);
+      bits.w[b >> 5] |= 1u << (b & 31);
     }
     out->ncat = k;
   }
+  PublishRecord(reinterpret_cast<CatWords*>(cat_out), bits);
   return true;
 }
 
@@ -721,20 +738,21 @@ __device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, 
   return 1;
 }
 
-template <bool ROOT, int KIND>
+template <bool ROOT, int KIND, int NT>
 struct FindShared {
-  BlockScratch sc;
-  ScanScratch ssc;
-  Cand sc2[kFindWaves];
+  BlockScratch<NT> sc;
+  ScanScratch<NT> ssc;
+  Cand sc2[NT / kWave];
   typename std::conditional<KIND == 2, CatScratch, int>::type cat_sc;
-  unsigned long long s_red[2 * kFindThreads];  // direct partial sums of narrow features
+  unsigned long long s_red[2 * NT];  // direct partial sums of narrow features
 };
 
 // the scan of one (feature, child) by one workgroup: every thread of the workgroup takes the
 // same path (the kernel's pick tail needs all of them)
-template <bool ROOT, int KIND, bool SIMPLE>
-__device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND>& sh) {
+template <bool ROOT, int KIND, bool SIMPLE, int NT>
+__device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND, NT>& sh) {
   constexpr bool CAT = KIND == 2;
+  constexpr int kFindThreads = NT;
   const long long t_entry = wall_clock64();
   // voting-parallel global scan: the features the vote elected for this side's leaf (an
   // empty slot still takes part in the step's workgroup count)
@@ -821,17 +839,17 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     rp.use_mc = 1;
     const double out0 = LeafOutputConstrained(sg, shh, p.lambda_l2, rp, cr, n, 0);
     const bool first = vote_global ? blockIdx.x == 0 : f == 0;
-    if (first && tid == 0 && KIND != 2) {
+    if (first && tid == 0 && KIND != 2) {  // (write-through: the root pick rewrites leaf 0)
       Leaf& lf = a.leaves[0];
       if (a.p.vote_phase == 1) {
-        lf.lsum_g = sg;
-        lf.lsum_h = shh;
+        PublishF64(&lf.lsum_g, sg);
+        PublishF64(&lf.lsum_h, shh);
       } else {
-        lf.sum_g = sg;
-        lf.sum_h = shh;
-        lf.global_count = n;
-        lf.output = out0;
-        a.st->root_count = n;
+        PublishF64(&lf.sum_g, sg);
+        PublishF64(&lf.sum_h, shh);
+        PublishI32(&lf.global_count, n);
+        PublishF64(&lf.output, out0);
+        PublishI32(&a.st->root_count, n);
       }
     }
     L.sg = sg;
@@ -879,8 +897,10 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     // says so and the larger child keeps the parent's row (SerialTreeLearner::FindBestSplits)
     if (side == 0 && tid == 0) flags[f] = 0;
     if (tid == 0) {
-      fb_out->gain = -INFINITY;
-      fb_out->feature = -1;
+      FeatureBest none = {};
+      none.gain = -INFINITY;
+      none.feature = none.real_feature = -1;
+      PublishRecord(fb_out, none);
     }
     return;
   }
@@ -998,7 +1018,12 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     __syncthreads();  // the workgroup's stores become visible to all its threads
     if (!ROOT) KTrace(a, s, kTrFindLoaded);
     if (!used) {
-      if (tid == 0) fb_out->feature = -1;
+      if (tid == 0) {
+        FeatureBest none = {};
+        none.gain = -INFINITY;
+        none.feature = none.real_feature = -1;
+        PublishRecord(fb_out, none);
+      }
       return;
     }
     HistView hv;
@@ -1012,7 +1037,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       splittable = FindCategoricalBlock(F, hv, L, p, &o, a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords, &sh.sc,
                                         &sh.cat_sc);
     } else {
-      splittable = FindNumericalBlock<SIMPLE>(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc, sh.sc2,
+      splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc, sh.sc2,
                                               xt_thr);
     }
     if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (the local scan's flags stay)
@@ -1020,12 +1045,13 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     // coupled-penalty refund), then the monotone depth penalty
     if (a.p.cegb && tid == 0) {
       const int leaf = ROOT ? 0 : sd.leaf;
-      if (a.cegb_mem != nullptr) {
+      if (a.cegb_mem != nullptr) {  // (read by the pick's refunds: write-through)
         const size_t mi = static_cast<size_t>(leaf) * a.p.num_features + f;
-        a.cegb_mem[mi] = o;
-        if (CAT) CopyWords(reinterpret_cast<const uint32_t(*)[kMaxCatWords]>(
-                               a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords),
-                           reinterpret_cast<uint32_t(*)[kMaxCatWords]>(a.cegb_mem_cat + mi * kMaxCatWords), 0, 1);
+        PublishRecord(&a.cegb_mem[mi], o);
+        if (CAT) {
+          const CatWords bits = *reinterpret_cast<const CatWords*>(a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords);
+          PublishRecord(reinterpret_cast<CatWords*>(a.cegb_mem_cat + mi * kMaxCatWords), bits);
+        }
       }
       double delta = a.p.cegb_split * L.n;
       if (a.cegb_coupled != nullptr && !a.cegb_used[f]) delta += a.cegb_coupled[f];
@@ -1036,27 +1062,56 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   } else {
     o.feature = -1;
   }
-  if (tid == 0) *fb_out = o;
+  if (tid == 0) PublishRecord(fb_out, o);
 }
 
-template <bool ROOT, int KIND, bool SIMPLE>
-__global__ __launch_bounds__(kFindThreads) void k_find(KArgs a) {
+constexpr unsigned kFindFlatMax = 128;  // split-scan grids up to this size count arrivals on one counter
+
+// NT: threads per workgroup -- kFindThreads, or one wave (kWave) when every feature has at
+// most kWave stored bins (many narrow features: four times the workgroups in flight, and no
+// cross-wave steps in the scans)
+template <bool ROOT, int KIND, bool SIMPLE, int NT>
+__global__ __launch_bounds__(NT) void k_find(KArgs a) {
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
-  __shared__ FindShared<ROOT, KIND> sh;
+  __shared__ FindShared<ROOT, KIND, NT> sh;
   __shared__ PickLds pl;
   __shared__ int s_last;
   Step* st = a.st;
   if (!ROOT && st->done) return;
-  FindBody<ROOT, KIND, SIMPLE>(a, s_bins, sh);
+  FindBody<ROOT, KIND, SIMPLE, NT>(a, s_bins, sh);
   // single process: the last workgroup of the step records it and picks the next split
   // (with categorical features the numerical kernel runs first and does not count)
   if (!a.pick_in_find || (KIND == 1)) return;
-  __threadfence();  // release this workgroup's results (feat_best, flags, leaves, histograms)
+  // hand-off to the picking workgroup: what it reads of this launch (per-feature results,
+  // category sets, CEGB candidates, the root's leaf record) was stored write-through
+  // (PublishRecord); every wave drains its stores, then one lane counts the arrival.  Other
+  // results (histograms, flags) are read by later kernels only.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) s_last = atomicAdd(&st->find_count, 1u) == gridDim.x * gridDim.y - 1 ? 1 : 0;
+  if (threadIdx.x == 0) {
+    const unsigned nwg = gridDim.x * gridDim.y;
+    int last = 0;
+    if (nwg <= kFindFlatMax) {
+      last = atomicAdd(&st->find_count, 1u) == nwg - 1 ? 1 : 0;
+    } else {
+      // one counter serialises thousands of arrivals (~12 ns each at the memory-side atomic
+      // unit, tools/microbench/wg_throughput.hip): kFindSub counters take a share each, the last
+      // of a share reports to find_count (and resets its counter for the next step)
+      const unsigned id = blockIdx.y * gridDim.x + blockIdx.x, g = id % kFindSub;
+      const unsigned members = (nwg - g + kFindSub - 1) / kFindSub;
+      if (atomicAdd(&st->find_sub[g], 1u) == members - 1) {
+        atomicExch(&st->find_sub[g], 0u);
+        last = atomicAdd(&st->find_count, 1u) == kFindSub - 1 ? 1 : 0;
+      }
+    }
+    if (last) {  // one agent-scope acquire for the workgroup (then the barrier below)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();  // acquire every other workgroup's results
   const int s = ROOT ? -1 : st->cs.s;
   if (!ROOT && a.ktrace != nullptr && threadIdx.x == 0 && s < a.p.num_leaves) {
     a.ktrace[s * kTraceSlots + kTrPickEntry] = wall_clock64();
@@ -1088,17 +1143,27 @@ static bool SimpleGains(const KArgs& a) {
 template <bool ROOT>
 static void LaunchFind(const KArgs& a, hipStream_t s) {
   if (a.num_scan <= 0) return;  // a rank that owns no feature
-  const dim3 g(a.num_scan, ROOT ? 1 : 2), b(kFindThreads);
+  const dim3 g(a.num_scan, ROOT ? 1 : 2);
   const size_t lds = FindLds(a);
   const bool simple = SimpleGains(a);
+  const bool narrow = a.p.max_feature_bins <= kWave;  // (categorical scans keep kFindThreads)
+  const dim3 b(narrow ? kWave : kFindThreads), bc(kFindThreads);
   if (a.p.has_cat) {
-    if (simple) hipLaunchKernelGGL((k_find<ROOT, 1, true>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_find<ROOT, 1, false>), g, b, lds, s, a);
+    if (narrow) {
+      if (simple) hipLaunchKernelGGL((k_find<ROOT, 1, true, kWave>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_find<ROOT, 1, false, kWave>), g, b, lds, s, a);
+    } else {
+      if (simple) hipLaunchKernelGGL((k_find<ROOT, 1, true, kFindThreads>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_find<ROOT, 1, false, kFindThreads>), g, b, lds, s, a);
+    }
     const int ncat = a.p.vote_phase == 2 ? a.num_scan : a.p.has_cat;  // voting: every elected slot
-    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false>), dim3(ncat, ROOT ? 1 : 2), b, lds, s, a);
+    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false, kFindThreads>), dim3(ncat, ROOT ? 1 : 2), bc, lds, s, a);
+  } else if (narrow) {
+    if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true, kWave>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_find<ROOT, 0, false, kWave>), g, b, lds, s, a);
   } else {
-    if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_find<ROOT, 0, false>), g, b, lds, s, a);
+    if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true, kFindThreads>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_find<ROOT, 0, false, kFindThreads>), g, b, lds, s, a);
   }
 }
 void FindRoot(const KArgs& a, hipStream_t s) { LaunchFind<true>(a, s); }

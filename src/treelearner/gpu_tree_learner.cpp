@@ -121,9 +121,10 @@ void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
   HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   UploadData();
   global_count_.assign(config_->num_leaves, 0);
-  Log::Info("MI355X learner on device %d (%d CUs): %d rows, %d groups, %d histogram bins, %s bins, %d hist tiles",
-            device_id_, cus, num_data_, num_groups_, total_bins_, args_.bin_bytes == 1 ? "8-bit" : (args_.bin_bytes == 2 ? "16-bit" : "8/16-bit"),
-            args_.hist_tiles);
+  const char* layout = sparse_rows_ ? "row-sparse"
+                       : (args_.bin_bytes == 1 ? "8-bit" : (args_.bin_bytes == 2 ? "16-bit" : "8/16-bit"));
+  Log::Info("MI355X learner on device %d (%d CUs): %d rows, %d groups, %d histogram bins, %s rows, %d hist tiles",
+            device_id_, cus, num_data_, num_groups_, total_bins_, layout, args_.hist_tiles);
 }
 
 void GPUTreeLearner::UploadData() {
@@ -171,13 +172,21 @@ void GPUTreeLearner::UploadData() {
   HIPCHECK(hipMemcpy(d_word_g0_, h_word_g0_.data(), sizeof(int32_t) * h_word_g0_.size(), hipMemcpyHostToDevice));
   d_word_wide_ = Alloc<int8_t>(h_word_wide_.size());
   HIPCHECK(hipMemcpy(d_word_wide_, h_word_wide_.data(), h_word_wide_.size(), hipMemcpyHostToDevice));
-  // row-major bin matrix (the dataset stores columns)
   args_.bin_bytes = bin_bytes;
   args_.words_per_row = wpr;
-  std::vector<uint8_t> host = RowMajorBins(data_);
-  d_bins_ = Alloc<uint8_t>(host.size());
-  HIPCHECK(hipMemcpy(d_bins_, host.data(), host.size(), hipMemcpyHostToDevice));
-  std::vector<uint8_t>().swap(host);
+  // training rows: the row-major word matrix, or row-sparse lists of stored bins (validation
+  // sets always use the word layout)
+  sparse_rows_ = UseSparseRows(wpr);
+  d_sp_ptr_ = nullptr;
+  d_sp_bin_ = nullptr;
+  d_bins_ = nullptr;
+  if (sparse_rows_) {
+    UploadSparseRows();
+  } else {
+    std::vector<uint8_t> host = RowMajorBins(data_);
+    d_bins_ = Alloc<uint8_t>(host.size());
+    HIPCHECK(hipMemcpy(d_bins_, host.data(), host.size(), hipMemcpyHostToDevice));
+  }
   // column-major copy for the partition kernels (one byte / short per row of the split column):
   // ~3% faster trees on the headline shape (profiles/r02_column_copy_ab.txt), at the price of a
   // second copy of the matrix -- kept when that copy is under 8 GiB (LGBM_AMD_COLUMN_COPY=0/1
@@ -188,6 +197,7 @@ void GPUTreeLearner::UploadData() {
   const size_t col_bytes = static_cast<size_t>(col_off[num_groups_]);
   bool col_copy = col_bytes <= (size_t(8) << 30);
   if (const char* cc = std::getenv("LGBM_AMD_COLUMN_COPY")) col_copy = cc[0] == '1';
+  col_copy = col_copy || sparse_rows_;  // (the partition's only source of the split column)
   if (col_copy) {
     std::vector<uint8_t> col(std::max<size_t>(1, col_bytes));
 #pragma omp parallel for schedule(static)
@@ -255,9 +265,10 @@ void GPUTreeLearner::UploadData() {
   // ~40% slower on small leaves (profiles/r01_v2_*)
   int max_tw = 1 << 20;
   if (const char* e = std::getenv("LGBM_AMD_HIST_TILE_WORDS")) max_tw = std::max(1, std::atoi(e));
-  int tile_words = 0;
+  int tile_words = sparse_rows_ ? 1 : 0;  // (row-sparse tiles are bin ranges, below)
   const std::vector<int> limits = hist_units_ == 1 ? std::vector<int>{8192, 16384} : std::vector<int>{8192};
   for (int limit : limits) {
+    if (sparse_rows_) break;
     for (int tw = std::min({wpr, dev::kHistThreads, max_tw}); tw >= 1; --tw) {
       if (tile_bins_for(tw) <= limit) {
         tile_words = tw;
@@ -402,6 +413,15 @@ void GPUTreeLearner::UploadData() {
   a.owned_hist = nullptr;
   a.owned_bin_lo = 0;
   a.tile_bins = tile_bins_for(tile_words);
+  a.sp_ptr = d_sp_ptr_;
+  a.sp_bin = d_sp_bin_;
+  if (sparse_rows_) {  // column tiles = bin ranges of at most 16384 (packed) / 8192 (wide) bins
+    const int limit = hist_units_ == 1 ? 16384 : 8192;
+    a.hist_tiles = (total_bins_ + limit - 1) / limit;
+    a.tile_bins = (total_bins_ + a.hist_tiles - 1) / a.hist_tiles;
+    a.tile_w0 = 0;
+    a.tile_w1 = a.hist_tiles;
+  }
   a.range_begin = 0;
   a.scales = d_scales_;
   a.bins_col = d_bins_col_;
@@ -1486,6 +1506,62 @@ bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction
 }
 
 // ---------------------------------------------------------------- binned rows
+// Row-sparse training storage (reference MultiValSparseBin, src/io/multi_val_sparse_bin.hpp,
+// chosen by Dataset::GetMultiBinFromSparseFeatures for sparse data): a histogram gather then
+// reads a row's ~2-byte stored bins instead of its whole word row.  Chosen when a sample of
+// rows stores at most half the bytes that way; needs <= 65535 histogram bins (16-bit entries)
+// and a full histogram range per rank (not feature-parallel).  LGBM_AMD_SPARSE_ROWS=0/1
+// forces the word matrix / the sparse lists (when allowed).
+bool GPUTreeLearner::UseSparseRows(int wpr) const {
+  if (total_bins_ > 65535 || num_data_ <= 0 || (distributed_ && mode_ == Mode::kFeature)) return false;
+  if (const char* e = std::getenv("LGBM_AMD_SPARSE_ROWS")) return e[0] == '1';
+  const data_size_t step = std::max<data_size_t>(1, num_data_ / 65536);
+  int64_t stored = 0, rows = 0;
+  for (data_size_t r = 0; r < num_data_; r += step, ++rows) {
+    for (int g = 0; g < num_groups_; ++g) stored += data_->group(g).Get(r) != 0 ? 1 : 0;
+  }
+  const double per_row = static_cast<double>(stored) / std::max<int64_t>(1, rows);
+  return (2.0 * per_row + 8.0) * 2.0 <= 4.0 * wpr;
+}
+
+// rows' stored bins (group_bin_boundary(g) + bin, bin != 0), ascending, as CSR lists; built
+// in blocks of rows so each group column is read sequentially within a block
+void GPUTreeLearner::UploadSparseRows() {
+  const data_size_t n = num_data_;
+  constexpr data_size_t kBlk = 1 << 15;
+  const int nblk = static_cast<int>((n + kBlk - 1) / kBlk);
+  std::vector<int64_t> ptr(static_cast<size_t>(n) + 1, 0);
+#pragma omp parallel for schedule(dynamic)
+  for (int b = 0; b < nblk; ++b) {
+    const data_size_t r0 = static_cast<data_size_t>(b) * kBlk, r1 = std::min(n, r0 + kBlk);
+    for (int g = 0; g < num_groups_; ++g) {
+      const FeatureGroup& grp = data_->group(g);
+      for (data_size_t r = r0; r < r1; ++r) ptr[r + 1] += grp.Get(r) != 0 ? 1 : 0;
+    }
+  }
+  for (data_size_t r = 0; r < n; ++r) ptr[r + 1] += ptr[r];
+  std::vector<uint16_t> ent(std::max<int64_t>(1, ptr[n]));
+#pragma omp parallel for schedule(dynamic)
+  for (int b = 0; b < nblk; ++b) {
+    const data_size_t r0 = static_cast<data_size_t>(b) * kBlk, r1 = std::min(n, r0 + kBlk);
+    std::vector<int64_t> cur(ptr.begin() + r0, ptr.begin() + r1);
+    for (int g = 0; g < num_groups_; ++g) {
+      const FeatureGroup& grp = data_->group(g);
+      const uint32_t goff = static_cast<uint32_t>(data_->group_bin_boundary(g));
+      for (data_size_t r = r0; r < r1; ++r) {
+        const uint32_t v = grp.Get(r);
+        if (v != 0) ent[cur[r - r0]++] = static_cast<uint16_t>(goff + v);
+      }
+    }
+  }
+  d_sp_ptr_ = Alloc<int64_t>(ptr.size());
+  HIPCHECK(hipMemcpy(d_sp_ptr_, ptr.data(), sizeof(int64_t) * ptr.size(), hipMemcpyHostToDevice));
+  d_sp_bin_ = Alloc<uint16_t>(ent.size());
+  HIPCHECK(hipMemcpy(d_sp_bin_, ent.data(), sizeof(uint16_t) * ent.size(), hipMemcpyHostToDevice));
+  Log::Info("device learner: row-sparse storage, %.2f stored bins per row (%d groups)",
+            static_cast<double>(ptr[n]) / std::max<data_size_t>(1, n), num_groups_);
+}
+
 // row-major copy of a dataset's storage columns in this learner's layout (each group at its
 // byte of the row, 8 or 16 bits; rows padded to whole 32-bit words)
 std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d) const {

@@ -122,6 +122,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   // tree records for the traversal kernels (staged in d_tree_*; the host vectors must stay
   // alive until the stream is synchronised)
   dev::DevTree StageTree(const Tree* tree);
+  bool UseSparseRows(int wpr) const;
+  void UploadSparseRows();
   std::vector<uint8_t> RowMajorBins(const Dataset* d) const;
   template <typename T>
   T* Alloc(size_t n);
@@ -208,6 +210,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   std::vector<int8_t> h_gwide_, h_word_wide_;
   int32_t* d_word_g0_ = nullptr;
   int8_t* d_word_wide_ = nullptr;
+  // row-sparse training storage (KArgs::sp_ptr / sp_bin) instead of the word matrix
+  bool sparse_rows_ = false;
+  int64_t* d_sp_ptr_ = nullptr;
+  uint16_t* d_sp_bin_ = nullptr;
   dev::FeatureBest* d_feat_best_ = nullptr;
   uint32_t* d_feat_cat_ = nullptr;  // category sets of the per-feature categorical bests
   uint32_t* h_absmax_ = nullptr;

@@ -53,6 +53,17 @@ def _efb_data(n, seed=9):
     return X, y
 
 
+def _sparse_data(n, seed=13, f=320, density=0.03):
+    """Mostly-zero continuous columns (63 bins each: > 16384 histogram bins in all, two
+    row-sparse bin tiles) and a few dense ones."""
+    rng = np.random.RandomState(seed)
+    X = np.where(rng.rand(n, f) < density, rng.randn(n, f), 0.0)
+    X[:, :3] = rng.randn(n, 3)
+    logit = X[:, 0] - X[:, 1] + 2.0 * X[:, 5:40].sum(1) - 1.5 * X[:, 200:240].sum(1)
+    y = (logit + 0.3 * rng.randn(n) > 0).astype(np.float64)
+    return X, y
+
+
 BASE = {"objective": "binary", "num_leaves": 31, "max_bin": 63, "learning_rate": 0.1, "min_data_in_leaf": 20,
         "verbose": -1, "device_type": "gpu", "seed": 7, "deterministic": True}
 
@@ -73,6 +84,14 @@ CASES = {
     # the same data with every group widened to 16 bits (LGBM_AMD_UNIFORM_BINS=1)
     "uniform_wide": ({"max_bin_by_feature": [63] * 7 + [511] + [63] * 2, "_env": {"LGBM_AMD_UNIFORM_BINS": "1"}},
                      20000),
+    # row-sparse storage (lists of each row's stored bins) forced on dense data, with EFB
+    # bundles, wide histograms, a 16-bit group and bagging; chosen by itself on sparse data
+    # with two bin tiles
+    "sparse_rows": ({"_env": {"LGBM_AMD_SPARSE_ROWS": "1"}, "categorical_feature": [4, 5]}, 20000),
+    "sparse_rows_efb": ({"max_bin": 31, "_env": {"LGBM_AMD_SPARSE_ROWS": "1"}}, 30000),
+    "sparse_rows_dp_wide": ({"gpu_use_dp": True, "max_bin_by_feature": [511] + [63] * 9, "bagging_fraction": 0.7,
+                             "bagging_freq": 1, "_env": {"LGBM_AMD_SPARSE_ROWS": "1"}}, 20000),
+    "sparse_auto_tiles": ({"min_data_in_leaf": 5}, 20000),
 }
 
 
@@ -127,7 +146,8 @@ def _quantise(v, scale):
 def test_device_tree_state(gpu_available, case, monkeypatch):
     import torch
     extra, n = CASES[case]
-    X, y = (_efb_data if case == "efb" else _data)(n)
+    make = _efb_data if case in ("efb", "sparse_rows_efb") else _sparse_data if case == "sparse_auto_tiles" else _data
+    X, y = make(n)
     params = dict(BASE, **extra)
     cat = params.pop("categorical_feature", "auto")
     for k, v in params.pop("_env", {}).items():
@@ -187,3 +207,10 @@ def test_device_tree_state(gpu_available, case, monkeypatch):
     rep = _check_splits(bst)
     assert rep["device_mode"] and rep["checked"] > 0, rep
     assert rep["mismatched"] == 0, json.dumps(rep)
+    expect_layout = {"mixed_width": "mixed", "mixed_width_dp": "mixed", "uniform_wide": "16", "numeric": "8",
+                     "sparse_rows": "sparse", "sparse_rows_efb": "sparse", "sparse_rows_dp_wide": "sparse",
+                     "sparse_auto_tiles": "sparse"}
+    if case in expect_layout:
+        assert rep["layout"] == expect_layout[case], rep["layout"]
+    if case == "sparse_auto_tiles":
+        assert rep["hist_tiles"] == 2

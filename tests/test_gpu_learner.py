@@ -560,3 +560,22 @@ def test_device_training_is_bitwise_deterministic(extra, gpu_available):
     params.update(extra)
     runs = [lgb.train(params, lgb.Dataset(X, y), 10).model_to_string() for _ in range(2)]
     assert runs[0] == runs[1]
+
+
+@pytest.mark.parametrize("env", [{"LGBM_AMD_SPARSE_ROWS": "1"}, {"LGBM_AMD_UNIFORM_BINS": "1"}])
+def test_storage_layouts_give_identical_models(gpu_available, monkeypatch, env):
+    """Histograms are exact integer sums, so the training rows' storage (word matrix with
+    per-group widths, every group widened to 16 bits, or row-sparse lists) cannot change a
+    model: identical model strings."""
+    rng = np.random.RandomState(21)
+    n = 30000
+    X = np.where(rng.rand(n, 40) < 0.1, rng.randn(n, 40), 0.0)
+    X[:, :4] = rng.randn(n, 4)
+    y = (X[:, 0] + X[:, 1] * X[:, 2] + X[:, 4:20].sum(1) + 0.3 * rng.randn(n) > 0).astype(np.float32)
+    extra = dict(num_leaves=63, max_bin_by_feature=[511] + [63] * 39, bagging_fraction=0.8, bagging_freq=1)
+    monkeypatch.setenv("LGBM_AMD_SPARSE_ROWS", "0")
+    base = _train(X, y, "gpu", rounds=15, **extra).model_to_string()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    other = _train(X, y, "gpu", rounds=15, **extra).model_to_string()
+    assert base == other
