@@ -13,7 +13,8 @@ namespace lgbm_amd {
 namespace dev {
 
 constexpr int kMaxLeaves = 1024;  // device-mode tree size limit (num_leaves)
-constexpr int kFindSub = 32;      // split-scan arrival sub-counters (Step::find_sub)
+constexpr int kFindSub = 32;      // split-scan arrival sub-counters (KArgs::find_sub)
+constexpr int kFindSubStride = 32;  // uint32 words between sub-counters: one 128-byte line each
 
 // interleaved (gradient, hessian) of one row: one 8-byte gather per row
 struct alignas(8) GH {
@@ -119,7 +120,6 @@ struct Step {
   int32_t smaller, larger;
   int32_t hist_left;  // k_split histograms the left child of cs (the pick's estimated counts), else the right
   uint32_t find_count;  // split-scan workgroups of the step that finished (the last one picks)
-  uint32_t find_sub[kFindSub];  // large split-scan grids: arrivals per share of workgroups
   int32_t root_count;   // global rows of the tree's root
   int32_t bynode_base, bynode_next;  // per-node feature masks: this step's / next free mask index
   int32_t cur_left, cur_right;      // partition cursors: rows placed left / right so far

@@ -111,6 +111,9 @@ struct KArgs {
   int8_t* cegb_used;
   FeatureBest* cegb_mem;
   uint32_t* cegb_mem_cat;
+  // arrival sub-counters of large split-scan grids, [kFindSub] at kFindSubStride words: each on
+  // a cache line of its own (atomics to one line serialise like atomics to one word)
+  uint32_t* find_sub;
   const double* root_local;
   VoteEntry* vote_buf;
   int32_t vote_rank;

@@ -116,7 +116,7 @@ __global__ void k_tree_begin(KArgs a) {
     st->larger = -1;
     st->hist_left = 1;
     st->find_count = 0u;
-    for (int i = 0; i < kFindSub; ++i) st->find_sub[i] = 0u;
+    for (int i = 0; i < kFindSub; ++i) a.find_sub[i * kFindSubStride] = 0u;
     st->loc_acc[0] = st->loc_acc[1] = 0ull;
     st->root_count = 0;
     st->cur_left = st->cur_right = 0;

@@ -225,15 +225,32 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
         idx = sidx;
       }
     } else {
+      // many features: strided per lane, kPickBatch independent loads in flight per round
+      // trip (a rolled one-load loop costs a memory round trip per 64 features: ~60 us for
+      // 2 x 2000 features)
+      constexpr int kPickBatch = 8;
 #pragma unroll 1
-      for (int i = lane; i < NF; i += kWave) {  // many features: strided, per side
-        const FeatureBest& fbv = a.feat_best[FeatBestIndex(a, side, i)];
-        const double cg = fbv.gain;
-        const int crf = fbv.real_feature, cf = fbv.feature;
-        if (cf >= 0 && (idx < 0 || SplitBetter(cg, crf, g, rf))) {
-          g = cg;
-          rf = crf;
-          idx = i;
+      for (int i0 = lane; i0 < NF; i0 += kPickBatch * kWave) {
+        double cg[kPickBatch];
+        int crf[kPickBatch], cf[kPickBatch];
+#pragma unroll
+        for (int k = 0; k < kPickBatch; ++k) {
+          const int i = i0 + k * kWave;
+          cf[k] = -1;
+          if (i < NF) {
+            const FeatureBest& fbv = a.feat_best[FeatBestIndex(a, side, i)];
+            cg[k] = fbv.gain;
+            crf[k] = fbv.real_feature;
+            cf[k] = fbv.feature;
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < kPickBatch; ++k) {  // ascending feature order, as the rolled loop
+          if (cf[k] >= 0 && (idx < 0 || SplitBetter(cg[k], crf[k], g, rf))) {
+            g = cg[k];
+            rf = crf[k];
+            idx = i0 + k * kWave;
+          }
         }
       }
     }

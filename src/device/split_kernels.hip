@@ -1099,8 +1099,9 @@ __global__ __launch_bounds__(NT) void k_find(KArgs a) {
       // of a share reports to find_count (and resets its counter for the next step)
       const unsigned id = blockIdx.y * gridDim.x + blockIdx.x, g = id % kFindSub;
       const unsigned members = (nwg - g + kFindSub - 1) / kFindSub;
-      if (atomicAdd(&st->find_sub[g], 1u) == members - 1) {
-        atomicExch(&st->find_sub[g], 0u);
+      uint32_t* sub = a.find_sub + g * kFindSubStride;
+      if (atomicAdd(sub, 1u) == members - 1) {
+        atomicExch(sub, 0u);
         last = atomicAdd(&st->find_count, 1u) == kFindSub - 1 ? 1 : 0;
       }
     }

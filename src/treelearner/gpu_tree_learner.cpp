@@ -296,6 +296,8 @@ void GPUTreeLearner::UploadData() {
   d_bag_count_ = Alloc<int32_t>(1);
   d_leaves_ = Alloc<dev::Leaf>(n_leaves);
   d_step_ = Alloc<dev::Step>(1);
+  d_find_sub_ = Alloc<uint32_t>(static_cast<size_t>(dev::kFindSub) * dev::kFindSubStride);
+  HIPCHECK(hipMemset(d_find_sub_, 0, sizeof(uint32_t) * dev::kFindSub * dev::kFindSubStride));
   d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
   d_best_ = Alloc<DeviceSplit>(n_leaves);
   d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
@@ -372,6 +374,7 @@ void GPUTreeLearner::UploadData() {
   a.tmp = d_tmp_;
   a.leaves = d_leaves_;
   a.st = d_step_;
+  a.find_sub = d_find_sub_;
   a.rec = d_rec_;
   a.best = d_best_;
   a.hist = d_hist_;

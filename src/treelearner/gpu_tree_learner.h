@@ -197,6 +197,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int32_t* d_bag_ = nullptr;  // pristine in-bag rows (the partition permutes d_idx_)
   dev::Leaf* d_leaves_ = nullptr;
   dev::Step* d_step_ = nullptr;
+  uint32_t* d_find_sub_ = nullptr;  // KArgs::find_sub
   dev::SplitRecord* d_rec_ = nullptr;
   DeviceSplit* d_best_ = nullptr;
   long long* d_hist_ = nullptr;
