@@ -1071,7 +1071,7 @@ constexpr unsigned kFindFlatMax = 128;  // split-scan grids up to this size coun
 // most kWave stored bins (many narrow features: four times the workgroups in flight, and no
 // cross-wave steps in the scans)
 template <bool ROOT, int KIND, bool SIMPLE, int NT>
-__global__ __launch_bounds__(NT) void k_find(KArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave ? 4 : 1))) void k_find(KArgs a) {
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
   __shared__ FindShared<ROOT, KIND, NT> sh;
   __shared__ PickLds pl;
