@@ -18,21 +18,20 @@ struct TileCtx {
 
 // row-sparse storage (KArgs::sp_ptr) takes the GPW slot of the kernels' templates
 constexpr int kSparseGPW = 1;
-constexpr int kSparseTeam = 4;  // threads per row of a row-sparse gather
-constexpr int kSparsePer = 4;   // entries per thread and row loaded up front
+constexpr int kSparsePer = kSparsePerThread;  // (KArgs::sp_team threads per row)
 
 // GPW: groups per word (4: 8-bit layout, 2: 16-bit layout, 0: mixed layout, one more round
 // trip for the word table) or kSparseGPW; otherwise every load is independent of the others
 template <int GPW>
 __device__ __forceinline__ void InitTile(const KArgs& a, TileCtx* t) {
-  if (GPW == kSparseGPW) {  // tile = bin range; kSparseTeam threads per row
+  if (GPW == kSparseGPW) {  // tile = bin range; KArgs::sp_team threads per row
     t->lo_bin = (a.tile_w0 + blockIdx.y) * a.tile_bins;
     t->nbins = min(a.p.total_bins, t->lo_bin + a.tile_bins) - t->lo_bin;
     t->w0 = t->w1 = 0;
-    t->tpr = kSparseTeam;
-    t->rpp = kHistThreads / kSparseTeam;
-    t->q = threadIdx.x % kSparseTeam;
-    t->rs = threadIdx.x / kSparseTeam;
+    t->tpr = a.sp_team;
+    t->rpp = kHistThreads / a.sp_team;
+    t->q = threadIdx.x % a.sp_team;
+    t->rs = threadIdx.x / a.sp_team;
     t->bits = 0;
     t->sg = static_cast<float>(a.scales[0]);
     t->sh = static_cast<float>(a.scales[1]);
@@ -105,13 +104,15 @@ __device__ __forceinline__ void AddRow(unsigned long long* lds, const int* goff,
   }
 }
 
-// row-sparse gather of K rows (rr[k] < 0: none) with values v[k]: the kSparseTeam threads of
-// a row take its entries round robin; the first kSparsePer entries of each thread and row are
-// loaded together (rows of up to kSparseTeam * kSparsePer entries cost one round trip after
-// their bounds), longer rows finish in a loop.  Entries outside the tile's bin range are skipped.
+// row-sparse gather of K rows (rr[k] < 0: none) with values v[k]: the t.tpr threads of a row
+// take its entries round robin.  The first kSparsePer entries of each thread and row are loaded
+// together (one round trip after the rows' bounds; the team size is chosen so that a mean row
+// fits); longer rows continue with the K rows' next entries loaded together per round trip.
+// Entries outside the tile's bin range are skipped.
 template <int K, int UNITS>
 __device__ __forceinline__ void AddSparseRows(const KArgs& a, unsigned long long* lds, const TileCtx& t,
                                               const int* rr, const float2* v) {
+  const int T = t.tpr;
   int64_t beg[K];
   int cnt[K];
 #pragma unroll
@@ -126,30 +127,41 @@ __device__ __forceinline__ void AddSparseRows(const KArgs& a, unsigned long long
   for (int k = 0; k < K; ++k) {
 #pragma unroll
     for (int m = 0; m < kSparsePer; ++m) {
-      const int j = t.q + m * kSparseTeam;
+      const int j = t.q + m * T;
       e[k][m] = j < cnt[k] ? static_cast<uint32_t>(a.sp_bin[beg[k] + j]) : 0xffffffffu;
     }
   }
   const uint32_t lo = static_cast<uint32_t>(t.lo_bin), nb = static_cast<uint32_t>(t.nbins);
+  long long gq[K], hq[K];
+  int longest = 0;
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const long long gq = __float2ll_rn(v[k].x * t.sg);
-    const long long hq = __float2ll_rn(v[k].y * t.sh);
-    const unsigned long long pk = (static_cast<unsigned long long>(gq) << 32) + static_cast<unsigned long long>(hq);
-    auto add = [&](uint32_t bin) {
-      const uint32_t b = bin - lo;
-      if (b < nb) {
-        if (UNITS == 1) {
-          atomicAdd(&lds[b], pk);
-        } else {
-          atomicAdd(&lds[2 * b], static_cast<unsigned long long>(gq));
-          atomicAdd(&lds[2 * b + 1], static_cast<unsigned long long>(hq));
-        }
+    gq[k] = __float2ll_rn(v[k].x * t.sg);
+    hq[k] = __float2ll_rn(v[k].y * t.sh);
+    longest = max(longest, cnt[k]);
+  }
+  auto add = [&](int k, uint32_t bin) {
+    const uint32_t b = bin - lo;
+    if (b < nb) {
+      if (UNITS == 1) {
+        atomicAdd(&lds[b], (static_cast<unsigned long long>(gq[k]) << 32) + static_cast<unsigned long long>(hq[k]));
+      } else {
+        atomicAdd(&lds[2 * b], static_cast<unsigned long long>(gq[k]));
+        atomicAdd(&lds[2 * b + 1], static_cast<unsigned long long>(hq[k]));
       }
-    };
+    }
+  };
 #pragma unroll
-    for (int m = 0; m < kSparsePer; ++m) add(e[k][m]);
-    for (int j = t.q + kSparseTeam * kSparsePer; j < cnt[k]; j += kSparseTeam) add(a.sp_bin[beg[k] + j]);
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int m = 0; m < kSparsePer; ++m) add(k, e[k][m]);
+  }
+  for (int j = t.q + kSparsePer * T; j < longest; j += T) {
+    uint32_t x[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) x[k] = j < cnt[k] ? static_cast<uint32_t>(a.sp_bin[beg[k] + j]) : 0xffffffffu;
+#pragma unroll
+    for (int k = 0; k < K; ++k) add(k, x[k]);
   }
 }
 

@@ -54,6 +54,7 @@ struct KArgs {
   // histogram column tiles are then plain bin ranges of tile_bins each
   const int64_t* sp_ptr;
   const uint16_t* sp_bin;
+  int32_t sp_team;           // threads per row of a row-sparse gather (4..64, by the mean stored bins)
   int32_t hist_tiles;        // column tiles of the histogram kernel
   int32_t tile_words;        // words per column tile
   int32_t tile_bins;         // max histogram bins of one tile (LDS words)
@@ -133,6 +134,7 @@ enum TraceSlot {
 
 constexpr int kFindMaxCatBins = 1024;  // categorical features scanned on device (<= 32 * kMaxCatWords)
 constexpr int kHistThreads = 1024;     // histogram workgroup (16 waves)
+constexpr int kSparsePerThread = 4;    // row-sparse gathers: entries per thread and row loaded up front
 constexpr int kHistMinRows = 1024;     // rows per histogram row block, lower bound
 constexpr int kHistRowsCap = 16384;    // rows per row block, upper bound (packed fixed point)
 constexpr int kReduceChunk = 16;       // partial histograms summed per reduce thread

@@ -418,6 +418,7 @@ void GPUTreeLearner::UploadData() {
   a.tile_bins = tile_bins_for(tile_words);
   a.sp_ptr = d_sp_ptr_;
   a.sp_bin = d_sp_bin_;
+  a.sp_team = sp_team_;
   if (sparse_rows_) {  // column tiles = bin ranges of at most 16384 (packed) / 8192 (wide) bins
     const int limit = hist_units_ == 1 ? 16384 : 8192;
     a.hist_tiles = (total_bins_ + limit - 1) / limit;
@@ -1512,7 +1513,7 @@ bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction
 // Row-sparse training storage (reference MultiValSparseBin, src/io/multi_val_sparse_bin.hpp,
 // chosen by Dataset::GetMultiBinFromSparseFeatures for sparse data): a histogram gather then
 // reads a row's ~2-byte stored bins instead of its whole word row.  Chosen when a sample of
-// rows stores at most half the bytes that way; needs <= 65535 histogram bins (16-bit entries)
+// rows stores at most a quarter of the bytes that way; needs <= 65535 histogram bins (16-bit entries)
 // and a full histogram range per rank (not feature-parallel).  LGBM_AMD_SPARSE_ROWS=0/1
 // forces the word matrix / the sparse lists (when allowed).
 bool GPUTreeLearner::UseSparseRows(int wpr) const {
@@ -1524,7 +1525,10 @@ bool GPUTreeLearner::UseSparseRows(int wpr) const {
     for (int g = 0; g < num_groups_; ++g) stored += data_->group(g).Get(r) != 0 ? 1 : 0;
   }
   const double per_row = static_cast<double>(stored) / std::max<int64_t>(1, rows);
-  return (2.0 * per_row + 8.0) * 2.0 <= 4.0 * wpr;
+  // a stored bin costs about as much as a whole word of a word row (scattered 2-byte reads vs
+  // one line per row): measured break-even near 4x fewer bytes (Bosch 190 stored bins per row vs
+  // 238 words: word rows 22.8 vs sparse 28.2 ms/iter; Expo 14 vs 176: 54.3 vs 34.7)
+  return (2.0 * per_row + 8.0) * 4.0 <= 4.0 * wpr;
 }
 
 // rows' stored bins (group_bin_boundary(g) + bin, bin != 0), ascending, as CSR lists; built
@@ -1561,8 +1565,12 @@ void GPUTreeLearner::UploadSparseRows() {
   HIPCHECK(hipMemcpy(d_sp_ptr_, ptr.data(), sizeof(int64_t) * ptr.size(), hipMemcpyHostToDevice));
   d_sp_bin_ = Alloc<uint16_t>(ent.size());
   HIPCHECK(hipMemcpy(d_sp_bin_, ent.data(), sizeof(uint16_t) * ent.size(), hipMemcpyHostToDevice));
-  Log::Info("device learner: row-sparse storage, %.2f stored bins per row (%d groups)",
-            static_cast<double>(ptr[n]) / std::max<data_size_t>(1, n), num_groups_);
+  // threads per row: a row of mean length fits the kSparsePer entries each thread loads up front
+  const double mean = static_cast<double>(ptr[n]) / std::max<data_size_t>(1, n);
+  sp_team_ = 4;
+  while (sp_team_ < 64 && sp_team_ * dev::kSparsePerThread < mean) sp_team_ *= 2;
+  Log::Info("device learner: row-sparse storage, %.2f stored bins per row (%d groups), %d threads per row", mean,
+            num_groups_, sp_team_);
 }
 
 // row-major copy of a dataset's storage columns in this learner's layout (each group at its

@@ -215,6 +215,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool sparse_rows_ = false;
   int64_t* d_sp_ptr_ = nullptr;
   uint16_t* d_sp_bin_ = nullptr;
+  int sp_team_ = 4;  // KArgs::sp_team
   dev::FeatureBest* d_feat_best_ = nullptr;
   uint32_t* d_feat_cat_ = nullptr;  // category sets of the per-feature categorical bests
   uint32_t* h_absmax_ = nullptr;
