@@ -210,6 +210,9 @@ struct DevTree {
 };
 void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
                   hipStream_t s);
+// whether AddTreeScore walks every row with the bitmap kernel (8-bit word rows of <= 64 bytes,
+// <= 255 internal nodes); otherwise a partition-ordered scatter of leaf values is cheaper
+bool TreeBitmapsApply(const KArgs& a, int num_leaves);
 
 void Iota(int32_t* p, int64_t n, hipStream_t s);
 

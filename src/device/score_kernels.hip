@@ -198,12 +198,16 @@ __global__ __launch_bounds__(kBmRowsPerBlock) void k_add_tree_score_bm(KArgs a, 
   }
 }
 
+bool TreeBitmapsApply(const KArgs& a, int num_leaves) {
+  const int ni = num_leaves - 1;
+  return a.bins != nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.words_per_row * 4 <= kBmMaxRowBytes;
+}
+
 void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
                   hipStream_t s) {
   if (num_rows <= 0) return;
   const int ni = t.num_leaves - 1;
-  if (rows == nullptr && a.bins != nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.words_per_row * 4 <= kBmMaxRowBytes &&
-      t.bm_work != nullptr) {
+  if (rows == nullptr && TreeBitmapsApply(a, t.num_leaves) && t.bm_work != nullptr) {
     hipLaunchKernelGGL(k_tree_bitmaps, dim3(ni), dim3(256), 0, s, a, t);
     // one chunk of rows per workgroup: every chunk's loads are in flight at once
     const int blocks = static_cast<int>(std::min<int64_t>((num_rows + kBmRowsPerBlock - 1) / kBmRowsPerBlock,

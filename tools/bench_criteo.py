@@ -38,6 +38,15 @@ def main():
     ap.add_argument("--leaves", type=int, default=255)
     ap.add_argument("--device", default="gpu")
     args = ap.parse_args()
+    import threading
+    t_start = time.time()
+
+    def heartbeat():  # long data generation: progress lines for job monitors
+        while True:
+            time.sleep(30.0)
+            print("[bench] %.0f s elapsed" % (time.time() - t_start), file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     import lightgbmv1_amd as lgb
 
     t0 = time.time()
@@ -63,7 +72,7 @@ def main():
     print(json.dumps({
         "metric": "sec/tree, Criteo-shaped 67 sparse count features (EFB), 255 leaves, one GPU shard",
         "value": round(sec, 6), "unit": "s/tree", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "higher_is_better": False, "rows": args.rows, "dtype": "fp32", "data": "synthetic",
+        "higher_is_better": False, "rows": args.rows, "dtype": "fp32-grad/fx32-hist/fp64-scan", "data": "synthetic",
         "reference_1_machine_scaled_to_rows_s": round(ref_scaled, 3),
         "reference_8_machines_1p7B_s": REF_SEC_PER_TREE_8_MACHINES,
         "data_gen_s": round(t_gen, 1), "setup_s": round(setup_s, 1), "trees": booster.num_trees()}), flush=True)

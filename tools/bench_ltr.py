@@ -54,6 +54,15 @@ def main():
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--test-rows", type=int, default=200_000)
     args = ap.parse_args()
+    import threading
+    t_start = time.time()
+
+    def heartbeat():  # long data generation: progress lines for job monitors
+        while True:
+            time.sleep(30.0)
+            print("[bench] %.0f s elapsed" % (time.time() - t_start), file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     import lightgbmv1_amd as lgb
 
     t0 = time.time()
@@ -79,7 +88,7 @@ def main():
         "metric": "sec/iteration lambdarank + GOSS on MS-LTR-shaped 3Mx700 (255 leaves, 63 bins); NDCG@10",
         "value": round(sec, 6), "unit": "s/iter", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1000 * sec, 4), "higher_is_better": False,
-        "vs_baseline": round(sec / BASELINE_SEC_PER_ITER, 6), "dtype": "fp32", "data": "synthetic",
+        "vs_baseline": round(sec / BASELINE_SEC_PER_ITER, 6), "dtype": "fp32-grad/fx32-hist/fp64-scan", "data": "synthetic",
         "config": {"model": "gbdt lambdarank goss, num_leaves={}, max_bin={}".format(args.leaves, args.max_bin),
                    "rows": args.rows, "features": args.features, "queries": int(len(group))},
         "ndcg10_heldout": round(ndcg, 6), "trees": booster.num_trees(), "setup_s": round(setup_s, 1)}), flush=True)
