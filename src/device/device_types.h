@@ -123,6 +123,7 @@ struct Step {
   int32_t root_count;   // global rows of the tree's root
   int32_t bynode_base, bynode_next;  // per-node feature masks: this step's / next free mask index
   int32_t cur_left, cur_right;      // partition cursors: rows placed left / right so far
+  int32_t forced_abort;             // forced splits: a forced split was invalid; normal picks from then on
   // voting-parallel: fixed-point (g, h) sums of the rows k_split histogrammed (the local sums
   // of that child), accumulated with atomics; cleared by the pick
   unsigned long long loc_acc[2];

@@ -112,6 +112,19 @@ struct KArgs {
   int8_t* cegb_used;
   FeatureBest* cegb_mem;
   uint32_t* cegb_mem_cat;
+  // forced splits (reference serial_tree_learner.cpp ForceSplits), in the static BFS order of
+  // the forced-split JSON tree: node k is applied as split k (while every earlier one was valid)
+  // to leaf forced_leaf[k] on inner feature forced_feat[k] at bin forced_thr[k]; the children
+  // of split s carry nodes forced_child[2s] (left) / forced_child[2s + 1] (right) or -1.  The
+  // split scan of such a child's feature fills forced_best / forced_cat[k] (the reference's
+  // GatherInfoForThreshold), the pick applies it
+  int32_t forced_n;
+  const int32_t* forced_feat;
+  const int32_t* forced_thr;
+  const int32_t* forced_leaf;
+  const int32_t* forced_child;
+  FeatureBest* forced_best;
+  uint32_t* forced_cat;
   // arrival sub-counters of large split-scan grids, [kFindSub] at kFindSubStride words: each on
   // a cache line of its own (atomics to one line serialise like atomics to one word)
   uint32_t* find_sub;

@@ -120,6 +120,11 @@ __global__ void k_tree_begin(KArgs a) {
     st->loc_acc[0] = st->loc_acc[1] = 0ull;
     st->root_count = 0;
     st->cur_left = st->cur_right = 0;
+    st->forced_abort = 0;
+  }
+  for (int k = threadIdx.x; k < a.forced_n; k += blockDim.x) {  // no stale forced results
+    a.forced_best[k].gain = -INFINITY;
+    a.forced_best[k].feature = -1;
   }
 }
 

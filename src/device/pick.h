@@ -84,6 +84,7 @@ __device__ __forceinline__ void NoSplit(DeviceSplit* d) {
 
 struct PickResult {
   int done;
+  int forced;  // the split is forced node s (reference ForceSplits)
   int s, leaf;
   int fresh_idx[2];  // winning feature of the fresh children (-1: none)
   Leaf P;
@@ -105,6 +106,8 @@ struct PickLds {
   DeviceSplit fsplit[2];       // ... as split records
   ChildStats lc, rc;
   uint32_t icm;
+  FeatureBest ffb;  // the forced split's record and category set
+  uint32_t ffcat[kMaxCatWords];
 };
 
 template <typename T>
@@ -314,6 +317,20 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
   out->fresh_idx[1] = fi1;
   pl->win_feature = wf;
   out->done = (g > 0.0 && wf >= 0) ? 0 : 1;
+  out->forced = 0;
+  // forced splits: node s, while every earlier one was valid; an invalid one ends them and
+  // the normal pick above stands (reference ForceSplits' abort)
+  if (s < a.forced_n && !a.st->forced_abort) {
+    const FeatureBest& fb = a.forced_best[s];
+    if (fb.feature >= 0 && fb.gain > -INFINITY) {
+      out->forced = 1;
+      out->leaf = a.forced_leaf[s];
+      pl->win_feature = fb.feature;
+      out->done = 0;
+    } else {
+      a.st->forced_abort = 1;
+    }
+  }
 }
 
 // in-kernel stamp of the picking workgroup (LGBM_AMD_KTRACE)
@@ -362,7 +379,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     // 3. records into LDS: the fresh children's winners, the winning leaf and feature
     const int fresh = pl->fresh, leaf = pk->leaf, w = tid >> 6;
     const int nw = nthr >> 6;
-    const bool win_fresh = (fresh >= 1 && leaf == pl->sm) || (fresh == 2 && leaf == pl->lg);
+    const bool win_fresh = !pk->forced && ((fresh >= 1 && leaf == pl->sm) || (fresh == 2 && leaf == pl->lg));
     for (int side = 0; side < fresh; ++side) {
       if (w == (side % nw) && pk->fresh_idx[side] >= 0) {
         CopyWords(&a.feat_best[FeatBestIndex(a, side, pk->fresh_idx[side])], &pl->fb[side], lane, kWave);
@@ -370,7 +387,15 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
                   &pl->fcat[side], lane, kWave);
       }
     }
-    if (!win_fresh && w == (2 % nw)) CopyWords(&a.best[leaf], &pk->split, lane, kWave);
+    if (pk->forced) {
+      if (w == (2 % nw)) {
+        CopyWords(&a.forced_best[pk->s], &pl->ffb, lane, kWave);
+        CopyWords(reinterpret_cast<const uint32_t(*)[kMaxCatWords]>(a.forced_cat + static_cast<size_t>(pk->s) * kMaxCatWords),
+                  &pl->ffcat, lane, kWave);
+      }
+    } else if (!win_fresh && w == (2 % nw)) {
+      CopyWords(&a.best[leaf], &pk->split, lane, kWave);
+    }
     if (w == (3 % nw)) {
       CopyWords(&a.leaves[leaf], &pk->P, lane, kWave);
       CopyWords(&a.feat[pl->win_feature], &pk->F, lane, kWave);
@@ -384,6 +409,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
         else NoSplit(&pl->fsplit[side]);
       }
       if (win_fresh) pk->split = pl->fsplit[leaf == pl->sm ? 0 : 1];
+      if (pk->forced) ToDeviceSplit(pl->ffb, pl->ffcat, &pk->split);
       const DeviceSplit& sp = pk->split;
       const Leaf& P = pk->P;
       const int s = pk->s, nl = s + 1;

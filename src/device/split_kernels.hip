@@ -738,6 +738,94 @@ __device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, 
   return 1;
 }
 
+// GatherInfoForThreshold (reference feature_histogram.hpp; host split_finder.cpp): the split of
+// a forced node at bin `thr` from the leaf's histogram, one thread.  hv holds the raw bins;
+// the most frequent bin is rebuilt from the leaf totals first (FixHistogram).  Invalid (gain
+// no better than the leaf's own): gain -inf, the pick then drops the forced splits.
+__device__ void ForcedGather(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int thr,
+                             FeatureBest* out, CatWords* bits) {
+  const int nb = F.num_bin - F.offset, offset = F.offset;
+  const double sum_g = L.sg, sum_h = L.sh - 2 * kEpsilon;  // the leaf's raw sums
+  hv.fix_t = -1;
+  if (F.mfb > 0) {
+    double og = 0.0, oh = 0.0;
+    for (int t = 0; t < nb; ++t) {
+      if (t == F.mfb) continue;
+      og += hv.RawG(t);
+      oh += hv.RawH(t);
+    }
+    hv.fix_t = F.mfb;
+    hv.fix_g = sum_g - og;
+    hv.fix_h = sum_h - oh;
+  }
+  const int smooth = p.use_smoothing;
+  const double gain_shift = LeafGainGivenOutput(sum_g, sum_h, p.lambda_l1, p.lambda_l2, L.parent_out, 1);
+  const double min_gain_shift = gain_shift + p.min_gain_to_split;
+  const double cnt_factor = L.n / sum_h;
+  FeatureBest o = {};
+  o.gain = -INFINITY;
+  o.feature = -1;
+  o.real_feature = -1;
+  for (int w = 0; w < kMaxCatWords; ++w) bits->w[w] = 0u;
+  double lg, lh, rg, rh;
+  int lc, rc;
+  if (!F.is_cat) {
+    rg = 0.0;
+    rh = kEpsilon;
+    rc = 0;
+    const bool skip_default = F.missing_type == 1, na = F.missing_type == 2;
+    for (int t = nb - 1 - (na ? 1 : 0); t >= 1 - offset; --t) {
+      if (static_cast<uint32_t>(t + offset) < static_cast<uint32_t>(thr)) break;
+      if (skip_default && t + offset == F.default_bin) continue;
+      rg += hv.G(t);
+      rh += hv.H(t);
+      rc += RoundIntD(hv.H(t) * cnt_factor);
+    }
+    lg = sum_g - rg;
+    lh = sum_h - rh;
+    lc = L.n - rc;
+    o.default_left = 1;
+  } else {
+    if (thr >= F.num_bin || thr == 0) {
+      *out = o;
+      return;
+    }
+    const double hh = hv.H(thr - offset);
+    lc = RoundIntD(hh * cnt_factor);
+    rc = L.n - lc;
+    lh = hh + kEpsilon;
+    rh = sum_h - lh;
+    lg = hv.G(thr - offset);
+    rg = sum_g - lg;
+    o.default_left = 0;
+    o.ncat = 1;
+    bits->w[thr >> 5] |= 1u << (thr & 31);
+  }
+  const double gain = LeafGain(lg, lh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, lc, L.parent_out, 1, 1,
+                               smooth) +
+                      LeafGain(rg, rh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, rc, L.parent_out, 1, 1,
+                               smooth);
+  if (!(gain > min_gain_shift)) {  // (NaN included)
+    *out = o;
+    return;
+  }
+  o.thr = F.is_cat ? 0 : thr;
+  o.lo = LeafOutputRaw(lg, lh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, lc, L.parent_out, 1, 1,
+                       smooth);
+  o.ro = LeafOutputRaw(sum_g - lg, sum_h - lh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, rc,
+                       L.parent_out, 1, 1, smooth);
+  o.lc = lc;
+  o.rc = L.n - lc;
+  o.lg = lg;
+  o.lh = lh - kEpsilon;
+  o.rg = sum_g - lg;
+  o.rh = sum_h - lh - kEpsilon;
+  o.gain = gain - min_gain_shift;
+  o.mono = 0;
+  o.feature = -2;  // (set by the caller)
+  *out = o;
+}
+
 template <bool ROOT, int KIND, int NT>
 struct FindShared {
   BlockScratch<NT> sc;
@@ -1058,6 +1146,22 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       o.gain -= delta;
     }
     if (!CAT && !SIMPLE && F.monotone != 0) o.gain *= MonotonePenalty(depth, a.p.monotone_penalty);
+    // a forced node on this child and feature: its split at the forced threshold (published
+    // for the pick, which applies it as split k)
+    if (a.forced_n > 0 && tid == 0 && !vote_global) {
+      const int k = ROOT ? 0 : (s < a.forced_n ? a.forced_child[2 * s + sd.lr] : -1);
+      if (k >= 0 && k < a.forced_n && a.forced_feat[k] == f) {
+        FeatureBest fo;
+        CatWords fbits;
+        ForcedGather(F, hv, L, p, a.forced_thr[k], &fo, &fbits);
+        if (fo.feature == -2) {
+          fo.feature = f;
+          fo.real_feature = F.real_index;
+        }
+        PublishRecord(reinterpret_cast<CatWords*>(a.forced_cat + static_cast<size_t>(k) * kMaxCatWords), fbits);
+        PublishRecord(&a.forced_best[k], fo);
+      }
+    }
     if (!ROOT) KTrace(a, s, kTrFindScanned);
   } else {
     o.feature = -1;

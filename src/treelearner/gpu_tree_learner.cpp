@@ -711,8 +711,11 @@ void GPUTreeLearner::DecideMode() {
   // CEGB: split and coupled feature penalties are applied by the device scans (single rank);
   // lazy penalties (per-row usage bitsets) and distributed CEGB run host-assisted
   const bool cegb = CostEffectiveGB::Enabled(*config_);
-  if (has_forced_split_ ||
-      (config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
+  // forced splits: applied by the pick on one process (the static BFS schedule of the JSON
+  // tree); distributed learners run them host-assisted
+  if (has_forced_split_ && (distributed_ || !SetupForcedSplits())) dm = false;
+  if (!has_forced_split_ && args_.forced_n > 0) SetupForcedSplits();  // (cleared)
+  if ((config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
       (cegb && (!config_->cegb_penalty_feature_lazy.empty() || distributed_))) {
     dm = false;
   }
@@ -1506,6 +1509,71 @@ bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction
     for (int l = 0; l < L; ++l) out[l] /= nonzero[l];
   }
   for (int l = 0; l < L; ++l) tree->SetLeafOutput(l, out[l]);
+  return true;
+}
+
+// ---------------------------------------------------------------- forced splits
+// The reference's ForceSplits (serial_tree_learner.cpp) walks the forced-split JSON tree in
+// BFS order before the leaf-wise loop: node k is split k, applied to the leaf that node's
+// parent split created (a left child keeps its parent's leaf id, a right child of split k is
+// leaf k + 1), as long as every forced split so far was valid.  That order and those leaves
+// are static, so the schedule is built once: per node its inner feature, bin threshold and
+// leaf, per split the node indices of its two children.
+bool GPUTreeLearner::SetupForcedSplits() {
+  const std::string text = has_forced_split_ ? forced_split_text_ : std::string();
+  if (text == forced_text_built_ && (forced_ok_ || text.empty())) return forced_ok_;
+  forced_text_built_ = text;
+  forced_ok_ = false;
+  if (args_.forced_n != 0) DestroyGraph();
+  args_.forced_n = 0;
+  if (!has_forced_split_) return false;
+  std::vector<Json> nodes{forced_split_};
+  std::vector<int32_t> feat, thr, leaf{0}, child;
+  const int max_nodes = config_->num_leaves - 1;
+  auto valid = [](const Json& n) { return n.is_object() && n.has("feature") && n.has("threshold"); };
+  for (size_t i = 0; i < nodes.size() && static_cast<int>(i) < max_nodes; ++i) {
+    const Json n = nodes[i];
+    const int inner = data_->InnerFeatureIndex(n["feature"].int_value());
+    feat.push_back(inner);
+    thr.push_back(inner >= 0 ? static_cast<int32_t>(data_->BinThreshold(inner, n["threshold"].number_value())) : 0);
+    int32_t lc = -1, rc = -1;
+    if (n.has("left") && valid(n["left"])) {
+      lc = static_cast<int32_t>(nodes.size());
+      nodes.push_back(n["left"]);
+      leaf.push_back(leaf[i]);
+    }
+    if (n.has("right") && valid(n["right"])) {
+      rc = static_cast<int32_t>(nodes.size());
+      nodes.push_back(n["right"]);
+      leaf.push_back(static_cast<int32_t>(i) + 1);
+    }
+    child.push_back(lc);
+    child.push_back(rc);
+  }
+  const int n = static_cast<int>(feat.size());
+  for (auto& c : child) {
+    if (c >= n) c = -1;  // beyond num_leaves - 1 splits
+  }
+  leaf.resize(n);
+  // one int32 block: feat | thr | leaf | child[2n]
+  std::vector<int32_t> blk;
+  blk.insert(blk.end(), feat.begin(), feat.end());
+  blk.insert(blk.end(), thr.begin(), thr.end());
+  blk.insert(blk.end(), leaf.begin(), leaf.end());
+  blk.insert(blk.end(), child.begin(), child.end());
+  d_forced_i32_ = Alloc<int32_t>(blk.size());
+  HIPCHECK(hipMemcpy(d_forced_i32_, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
+  d_forced_best_ = Alloc<dev::FeatureBest>(n);
+  d_forced_cat_ = Alloc<uint32_t>(static_cast<size_t>(n) * kMaxCatWords);
+  args_.forced_feat = d_forced_i32_;
+  args_.forced_thr = d_forced_i32_ + n;
+  args_.forced_leaf = d_forced_i32_ + 2 * n;
+  args_.forced_child = d_forced_i32_ + 3 * n;
+  args_.forced_best = d_forced_best_;
+  args_.forced_cat = d_forced_cat_;
+  args_.forced_n = n;
+  forced_ok_ = true;
+  DestroyGraph();  // (the captured tree holds the kernel arguments)
   return true;
 }
 

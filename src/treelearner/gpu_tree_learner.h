@@ -123,6 +123,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   // alive until the stream is synchronised)
   dev::DevTree StageTree(const Tree* tree);
   bool UseSparseRows(int wpr) const;
+  bool SetupForcedSplits();  // KArgs::forced_*; false: the forced splits need host-assisted growth
   void UploadSparseRows();
   std::vector<uint8_t> RowMajorBins(const Dataset* d) const;
   template <typename T>
@@ -216,6 +217,12 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int64_t* d_sp_ptr_ = nullptr;
   uint16_t* d_sp_bin_ = nullptr;
   int sp_team_ = 4;  // KArgs::sp_team
+  // device forced-split schedule (SetupForcedSplits), rebuilt when the JSON text changes
+  std::string forced_text_built_;
+  bool forced_ok_ = false;
+  int32_t* d_forced_i32_ = nullptr;
+  dev::FeatureBest* d_forced_best_ = nullptr;
+  uint32_t* d_forced_cat_ = nullptr;
   dev::FeatureBest* d_feat_best_ = nullptr;
   uint32_t* d_feat_cat_ = nullptr;  // category sets of the per-feature categorical bests
   uint32_t* h_absmax_ = nullptr;

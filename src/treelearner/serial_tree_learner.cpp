@@ -107,6 +107,7 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
 
 void SerialTreeLearner::SetForcedSplit(const std::string& json_text) {
   has_forced_split_ = false;
+  forced_split_text_ = json_text;
   if (json_text.empty()) return;
   forced_split_ = Json::Parse(json_text);
   has_forced_split_ = forced_split_.is_object() && forced_split_.has("feature");

@@ -108,6 +108,7 @@ class SerialTreeLearner : public TreeLearner {
   const score_t* gradients_ = nullptr;
   const score_t* hessians_ = nullptr;
   Json forced_split_;
+  std::string forced_split_text_;  // (the JSON text forced_split_ was parsed from)
   bool has_forced_split_ = false;
   // features owned by this rank (feature-parallel); empty = all
   std::vector<int8_t> feature_mask_;

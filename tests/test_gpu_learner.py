@@ -579,3 +579,57 @@ def test_storage_layouts_give_identical_models(gpu_available, monkeypatch, env):
         monkeypatch.setenv(k, v)
     other = _train(X, y, "gpu", rounds=15, **extra).model_to_string()
     assert base == other
+
+
+def _forced_trees(monkeypatch, tmp_path, forced, host, cat=None, rounds=3):
+    import json as _json
+    rng = np.random.RandomState(31)
+    n = 30000
+    X = rng.randn(n, 8).astype(np.float32)
+    X[:, 5] = rng.randint(0, 6, size=n)
+    y = (X[:, 0] + X[:, 1] * X[:, 2] - 0.5 * (X[:, 5] == 3) + 0.3 * rng.randn(n) > 0).astype(np.float32)
+    f = tmp_path / ("forced_%d.json" % int(host))
+    f.write_text(_json.dumps(forced))
+    if host:
+        monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    else:
+        monkeypatch.delenv("LGBM_AMD_HOST_ASSIST", raising=False)
+    params = {"objective": "binary", "num_leaves": 15, "verbose": -1, "device_type": "gpu", "seed": 3,
+              "forcedsplits_filename": str(f), "max_cat_to_onehot": 8}
+    ds = lgb.Dataset(X, y, params=params, categorical_feature=cat or [5], free_raw_data=False)
+    bst = lgb.train(params, ds, rounds, verbose_eval=False, keep_training_booster=True)
+    from lightgbmv1_amd import _native as nat
+    rep = _json.loads(nat.read_string(lambda size, need, buf: nat.call(
+        "LGBM_AMD_BoosterDeviceCheckSplits", bst.handle, size, need, buf), 1 << 16))
+    return bst, rep, X
+
+
+def _structure(node, depth):
+    if "split_feature" not in node or depth == 0:
+        return ("leaf", node.get("leaf_count", node.get("internal_count")))
+    return (node["split_feature"], str(node["threshold"]), node["internal_count"],
+            _structure(node["left_child"], depth - 1), _structure(node["right_child"], depth - 1))
+
+
+@pytest.mark.parametrize("forced", [
+    # numerical root, numerical and categorical children, a grandchild
+    {"feature": 0, "threshold": 0.1, "left": {"feature": 1, "threshold": -0.2, "left": {"feature": 2, "threshold": 0.5}},
+     "right": {"feature": 5, "threshold": 3}},
+    # an invalid node (an unknown feature) ends the forced splits early
+    {"feature": 0, "threshold": 0.0, "left": {"feature": 99, "threshold": 1.0}, "right": {"feature": 2, "threshold": 0.0}},
+])
+def test_forced_splits_on_device(gpu_available, monkeypatch, tmp_path, forced):
+    """Forced splits are applied by the device pick (the static BFS schedule of the JSON tree,
+    each node's split gathered by the split scan of its leaf): the trees equal the host-assisted
+    learner's, and the trees grew device-resident."""
+    dev, rep_dev, X = _forced_trees(monkeypatch, tmp_path, forced, host=False)
+    host, rep_host, _ = _forced_trees(monkeypatch, tmp_path, forced, host=True)
+    assert rep_dev["device_mode"] and not rep_host["device_mode"]
+    # the forced levels (and the children they create) are identical; deeper normal splits may
+    # differ in near-ties (device fixed-point scan vs host fp64 scan)
+    for t_dev, t_host in zip(dev.dump_model()["tree_info"], host.dump_model()["tree_info"]):
+        assert _structure(t_dev["tree_structure"], 3) == _structure(t_host["tree_structure"], 3)
+    y = (X[:, 0] + X[:, 1] * X[:, 2] - 0.5 * (X[:, 5] == 3) > 0).astype(np.float32)
+    assert abs(_auc(y, dev.predict(X)) - _auc(y, host.predict(X))) < 5e-3
+    root = dev.dump_model()["tree_info"][0]["tree_structure"]
+    assert root["split_feature"] == forced["feature"]
