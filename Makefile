@@ -58,7 +58,23 @@ build_asan/lightgbm: $(ASAN_OBJS) $(DEV_OBJS) src/cli/main.cpp
 
 sanitize: build_asan/lightgbm
 
-clean:
-	rm -rf $(BUILD) build_asan $(LIB) $(CLI)
+# ThreadSanitizer build of the host code: the C API driver
+# tests/native/tsan_driver.cpp linked from TSan-instrumented host objects (device objects
+# uninstrumented); OpenMP runs at one thread (libgomp is not instrumented)
+TSAN_FLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=thread
+TSAN_OBJS := $(patsubst src/%.cpp,build_tsan/%.o,$(HOST_SRCS))
 
-.PHONY: all clean sanitize
+build_tsan/%.o: src/%.cpp $(HEADERS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(filter-out -O3,$(CXXFLAGS)) $(TSAN_FLAGS) -c $< -o $@
+
+build_tsan/tsan_driver: $(TSAN_OBJS) $(DEV_OBJS) tests/native/tsan_driver.cpp
+	$(CXX) $(filter-out -O3,$(CXXFLAGS)) $(TSAN_FLAGS) -o $@ tests/native/tsan_driver.cpp $(TSAN_OBJS) $(DEV_OBJS) \
+	  -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
+
+tsan: build_tsan/tsan_driver
+
+clean:
+	rm -rf $(BUILD) build_asan build_tsan $(LIB) $(CLI)
+
+.PHONY: all clean sanitize tsan

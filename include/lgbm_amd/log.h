@@ -3,6 +3,7 @@
 // Fatal throws std::runtime_error; the C API converts it into an error code.
 #pragma once
 
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <stdexcept>
@@ -15,9 +16,11 @@ enum class LogLevel : int { Fatal = -1, Warning = 0, Info = 1, Debug = 2 };
 class Log {
  public:
   using Callback = void (*)(const char*);
-  static void ResetLevel(LogLevel level) { level_() = level; }
-  static LogLevel Level() { return level_(); }
-  static void ResetCallback(Callback cb) { callback_() = cb; }
+  // (atomics: every C API call sets the level from its parameters, concurrently with the
+  // log calls of other threads)
+  static void ResetLevel(LogLevel level) { level_().store(level, std::memory_order_relaxed); }
+  static LogLevel Level() { return level_().load(std::memory_order_relaxed); }
+  static void ResetCallback(Callback cb) { callback_().store(cb, std::memory_order_relaxed); }
 
   static void Debug(const char* fmt, ...) {
     va_list ap; va_start(ap, fmt); Write(LogLevel::Debug, "Debug", fmt, ap); va_end(ap);
@@ -38,19 +41,20 @@ class Log {
 
  private:
   static void Write(LogLevel lvl, const char* tag, const char* fmt, va_list ap) {
-    if (static_cast<int>(lvl) > static_cast<int>(level_())) return;
+    if (static_cast<int>(lvl) > static_cast<int>(Level())) return;
     char buf[4096];
     vsnprintf(buf, sizeof(buf), fmt, ap);
-    if (callback_() != nullptr) {
+    const Callback cb = callback_().load(std::memory_order_relaxed);
+    if (cb != nullptr) {
       std::string s = std::string("[LightGBM] [") + tag + "] " + buf + "\n";
-      callback_()(s.c_str());
+      cb(s.c_str());
     } else {
       fprintf(stdout, "[LightGBM] [%s] %s\n", tag, buf);
       fflush(stdout);
     }
   }
-  static LogLevel& level_() { static LogLevel l = LogLevel::Info; return l; }
-  static Callback& callback_() { static Callback c = nullptr; return c; }
+  static std::atomic<LogLevel>& level_() { static std::atomic<LogLevel> l{LogLevel::Info}; return l; }
+  static std::atomic<Callback>& callback_() { static std::atomic<Callback> c{nullptr}; return c; }
 };
 
 #define LGBM_CHECK(cond) \

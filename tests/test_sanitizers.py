@@ -28,3 +28,23 @@ def test_examples_clean_under_asan_ubsan(tmp_path, example, extra):
     assert out.returncode == 0, log[-4000:]
     assert "AddressSanitizer" not in log and "runtime error" not in log, log[-4000:]
     assert (tmp_path / "m.txt").exists()
+
+
+TSAN_DRIVER = os.path.join(ROOT, "build_tsan", "tsan_driver")
+
+
+@pytest.mark.skipif(not os.path.isdir(EXAMPLES), reason="reference examples not mounted")
+def test_threads_clean_under_tsan(tmp_path):
+    """ThreadSanitizer (`make tsan`): two_round loading's reader thread, and training under the
+    booster's exclusive lock while three threads predict and one reads evaluations through the
+    C API (tests/native/tsan_driver.cpp).  Found and fixed with it: the log level written by
+    every C API call, and booster getters reading the model without the lock."""
+    if not os.path.isfile(TSAN_DRIVER):
+        subprocess.run(["make", "-j" + str(min(8, os.cpu_count() or 4)), "tsan"], cwd=ROOT, check=True,
+                       capture_output=True, timeout=900)
+    env = dict(os.environ, OMP_NUM_THREADS="1", TSAN_OPTIONS="exitcode=66 halt_on_error=0")
+    out = subprocess.run([TSAN_DRIVER, os.path.join(EXAMPLES, "binary_classification", "binary.train"), "28"],
+                         cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
+    log = out.stdout + out.stderr
+    assert "ThreadSanitizer" not in log, log[-6000:]
+    assert out.returncode == 0 and "tsan driver ok: 15 iterations" in log, log[-3000:]
