@@ -13,6 +13,7 @@ CLI := $(LIBDIR)/lightgbm
 
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -fopenmp -Wall -Wno-unused-function -Wno-sign-compare -Iinclude -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -munsafe-fp-atomics -Wno-unused-result
+HIPEXTRA ?=
 LDFLAGS := -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
 
 HOST_SRCS := $(filter-out src/cli/main.cpp,$(shell find src -name '*.cpp'))
@@ -32,7 +33,7 @@ $(BUILD)/%.o: src/%.cpp $(HEADERS)
 
 $(BUILD)/%.hip.o: src/%.hip $(HEADERS)
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(HIPEXTRA) -c $< -o $@
 
 $(LIB): $(HOST_OBJS) $(DEV_OBJS)
 	@mkdir -p $(LIBDIR)

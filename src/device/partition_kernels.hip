@@ -30,7 +30,10 @@ namespace {
 
 constexpr int kPartWaves = kPartThreads / kWave;
 static_assert(kSplitRows * kPartWaves == kWave, "k_split: one wave lane per (row slot, wave) piece");
-constexpr int kGatherRows = 8;  // phase B: independent row gathers per thread
+#ifndef LGBM_GATHER_ROWS
+#define LGBM_GATHER_ROWS 2
+#endif
+constexpr int kGatherRows = LGBM_GATHER_ROWS;  // phase B: independent row gathers per thread
 
 __device__ __forceinline__ int ValidInWave(int valid, int k, int w) {
   return min(kWave, max(0, valid - k * kPartThreads - w * kWave));

@@ -22,23 +22,50 @@
 namespace lgbm_amd {
 namespace dev {
 
-// argmax over (gain, real feature, index) in SplitInfo order; ties on both -> lower index.
-// `x` travels with the winner.  Rolled: this runs once per split on a cold I-cache.
-__device__ __forceinline__ void WaveArgBest(double* g, int* rf, int* idx, int* x) {
+// an argmax candidate in SplitInfo order: larger gain, then smaller real feature, then lower
+// index; `x` travels with it (idx < 0: no candidate)
+struct ArgC {
+  double g;
+  int rf, idx, x;
+};
+
+__device__ __forceinline__ ArgC ArgNone() {
+  ArgC c;
+  c.g = -INFINITY;
+  c.rf = -1;
+  c.idx = -1;
+  c.x = -1;
+  return c;
+}
+
+__device__ __forceinline__ void ArgTake(ArgC* c, const ArgC& o) {
+  const bool take = o.idx >= 0 && (c->idx < 0 || SplitBetter(o.g, o.rf, c->g, c->rf) ||
+                                   (!SplitBetter(c->g, c->rf, o.g, o.rf) && o.idx < c->idx));
+  if (take) *c = o;
+}
+
+__device__ __forceinline__ ArgC ArgShflXor(const ArgC& c, int o) {
+  ArgC r;
+  r.g = __shfl_xor(c.g, o, kWave);
+  r.rf = __shfl_xor(c.rf, o, kWave);
+  r.idx = __shfl_xor(c.idx, o, kWave);
+  r.x = __shfl_xor(c.x, o, kWave);
+  return r;
+}
+
+// three independent wave argmaxes, interleaved: each butterfly step issues the cross-lane
+// moves of all three chains before any comparison, so their latencies (ds_bpermute, ~100+
+// cycles each) overlap -- three back-to-back reductions cost ~5 us per pick.  Rolled: this
+// runs once per split on a cold I-cache.
+__device__ __forceinline__ void WaveArgBest3(ArgC* a, ArgC* b, ArgC* c) {
 #pragma unroll 1
   for (int o = 32; o > 0; o >>= 1) {
-    const double og = __shfl_xor(*g, o, kWave);
-    const int orf = __shfl_xor(*rf, o, kWave);
-    const int oi = __shfl_xor(*idx, o, kWave);
-    const int ox = __shfl_xor(*x, o, kWave);
-    const bool take = oi >= 0 && (*idx < 0 || SplitBetter(og, orf, *g, *rf) ||
-                                  (!SplitBetter(*g, *rf, og, orf) && oi < *idx));
-    if (take) {
-      *g = og;
-      *rf = orf;
-      *idx = oi;
-      *x = ox;
-    }
+    const ArgC oa = ArgShflXor(*a, o);
+    const ArgC ob = ArgShflXor(*b, o);
+    const ArgC oc = ArgShflXor(*c, o);
+    ArgTake(a, oa);
+    ArgTake(b, ob);
+    ArgTake(c, oc);
   }
 }
 
@@ -189,49 +216,40 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
     return;
   }
   // every input in one round of loads: lanes take (side, feature) items of the fresh sides
-  // and leaves 0..s; then the per-side feature argmaxes, then the leaf argmax
-  double sg = -INFINITY;  // this lane's best feature of its side
-  int srf = -1, sidx = -1, unused = 0;
-  const int nitems = fresh * NF;
-  const int side_of_lane = nitems <= kWave ? (lane < NF ? 0 : 1) : -1;  // one item per lane
-  if (side_of_lane >= 0) {
-    const int i = lane - side_of_lane * NF;
-    if (lane < nitems) {
-      const FeatureBest& fbv = a.feat_best[FeatBestIndex(a, side_of_lane, i)];
-      const double cg = fbv.gain;
-      const int crf = fbv.real_feature, cf = fbv.feature;
-      if (cf >= 0) {
-        sg = cg;
-        srf = crf;
-        sidx = i;
-      }
-    }
-  }
-  double lgv = -INFINITY;  // this lane's leaf (l = lane, the common case s < 64)
+  // and leaves 0..s; then the two per-side feature argmaxes and the argmax over the other
+  // leaves in one interleaved reduction; the fresh children join the leaf argmax last (the
+  // order is total, so folding them in afterwards picks the same leaf as one pass)
+  double lgv = -INFINITY;  // this lane's leaf (l = lane, the common case s < 64), loaded first
   int lrf = -1, lfv = -1;
   if (lane <= s && lane < L) {
     lgv = a.best[lane].gain;
     lrf = a.best[lane].real_feature;
     lfv = a.best[lane].feature;
   }
-  // (scalars, not arrays indexed by the rolled side loop: those would live in scratch)
-  int fi0 = -1, fi1 = -1, frf0 = -1, frf1 = -1;
-  double fg0 = -INFINITY, fg1 = -INFINITY;
-#pragma unroll 1
-  for (int side = 0; side < fresh; ++side) {
-    double g = -INFINITY;
-    int rf = -1, idx = -1;
-    if (side_of_lane >= 0) {
-      if (side_of_lane == side) {
-        g = sg;
-        rf = srf;
-        idx = sidx;
+  ArgC c0 = ArgNone(), c1 = ArgNone();  // this lane's best feature of side 0 / 1
+  const int nitems = fresh * NF;
+  if (nitems <= kWave) {  // one item per lane
+    const int side_of_lane = lane < NF ? 0 : 1;
+    const int i = lane - side_of_lane * NF;
+    if (lane < nitems) {
+      const FeatureBest& fbv = a.feat_best[FeatBestIndex(a, side_of_lane, i)];
+      const double cg = fbv.gain;
+      const int crf = fbv.real_feature, cf = fbv.feature;
+      if (cf >= 0) {
+        ArgC& c = side_of_lane == 0 ? c0 : c1;
+        c.g = cg;
+        c.rf = crf;
+        c.idx = i;
       }
-    } else {
-      // many features: strided per lane, kPickBatch independent loads in flight per round
-      // trip (a rolled one-load loop costs a memory round trip per 64 features: ~60 us for
-      // 2 x 2000 features)
-      constexpr int kPickBatch = 8;
+    }
+  } else {
+    // many features: strided per lane, kPickBatch independent loads in flight per round
+    // trip (a rolled one-load loop costs a memory round trip per 64 features: ~60 us for
+    // 2 x 2000 features)
+    constexpr int kPickBatch = 8;
+#pragma unroll 1
+    for (int side = 0; side < fresh; ++side) {
+      ArgC c = ArgNone();
 #pragma unroll 1
       for (int i0 = lane; i0 < NF; i0 += kPickBatch * kWave) {
         double cg[kPickBatch];
@@ -248,48 +266,27 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
           }
         }
 #pragma unroll
-        for (int k = 0; k < kPickBatch; ++k) {  // ascending feature order, as the rolled loop
-          if (cf[k] >= 0 && (idx < 0 || SplitBetter(cg[k], crf[k], g, rf))) {
-            g = cg[k];
-            rf = crf[k];
-            idx = i0 + k * kWave;
+        for (int k = 0; k < kPickBatch; ++k) {  // ascending feature order, as a rolled loop
+          if (cf[k] >= 0 && (c.idx < 0 || SplitBetter(cg[k], crf[k], c.g, c.rf))) {
+            c.g = cg[k];
+            c.rf = crf[k];
+            c.idx = i0 + k * kWave;
           }
         }
       }
-    }
-    WaveArgBest(&g, &rf, &idx, &unused);
-    if (idx >= 0 && g == -INFINITY) idx = -1;  // no valid threshold on any feature
-    if (side == 0) {
-      fi0 = idx;
-      fg0 = idx >= 0 ? g : -INFINITY;
-      frf0 = idx >= 0 ? rf : -1;
-    } else {
-      fi1 = idx;
-      fg1 = idx >= 0 ? g : -INFINITY;
-      frf1 = idx >= 0 ? rf : -1;
+      if (side == 0) c0 = c;
+      else c1 = c;
     }
   }
-  if (a.ktrace != nullptr && lane == 0 && s - 1 >= 0) {
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    a.ktrace[(s - 1) * kTraceSlots + kTrPW1] = wall_clock64();
-  }
-  // the leaf to split: argmax over leaves 0..s (fresh children use the new results); the
-  // winner's inner feature travels with it
-  double g = -INFINITY;
-  int rf = -1, leaf = -1, wf = -1;
+  // the leaves other than the fresh children (their records are final); the winner's inner
+  // feature travels with it
+  ArgC cl = ArgNone();
 #pragma unroll 1
   for (int l = lane; l <= s && l < L; l += kWave) {
+    if ((fresh >= 1 && l == sm) || (fresh == 2 && l == lg)) continue;
     double cg;
     int crf, cf;
-    if (fresh >= 1 && l == sm) {
-      cg = fg0;
-      crf = frf0;
-      cf = fi0;
-    } else if (fresh == 2 && l == lg) {
-      cg = fg1;
-      crf = frf1;
-      cf = fi1;
-    } else if (l == lane) {
+    if (l == lane) {
       cg = lgv;
       crf = lrf;
       cf = lfv;
@@ -298,15 +295,42 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
       crf = a.best[l].real_feature;
       cf = a.best[l].feature;
     }
-    if (leaf < 0 || SplitBetter(cg, crf, g, rf)) {
-      g = cg;
-      rf = crf;
-      leaf = l;
-      wf = cf;
+    if (cl.idx < 0 || SplitBetter(cg, crf, cl.g, cl.rf)) {
+      cl.g = cg;
+      cl.rf = crf;
+      cl.idx = l;
+      cl.x = cf;
     }
   }
-  WaveArgBest(&g, &rf, &leaf, &wf);
+  WaveArgBest3(&c0, &c1, &cl);
+  if (c0.idx >= 0 && c0.g == -INFINITY) c0.idx = -1;  // no valid threshold on any feature
+  if (c1.idx >= 0 && c1.g == -INFINITY) c1.idx = -1;
+  const int fi0 = c0.idx, fi1 = c1.idx;
+  if (a.ktrace != nullptr && lane == 0 && s - 1 >= 0) {
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    a.ktrace[(s - 1) * kTraceSlots + kTrPW1] = wall_clock64();
+  }
+  // the leaf to split: the fresh children's bests join the other leaves' winner
+  ArgC win = cl;
+  if (fresh >= 1) {
+    ArgC f;
+    f.g = fi0 >= 0 ? c0.g : -INFINITY;
+    f.rf = fi0 >= 0 ? c0.rf : -1;
+    f.idx = sm;
+    f.x = fi0;
+    ArgTake(&win, f);
+  }
+  if (fresh == 2) {
+    ArgC f;
+    f.g = fi1 >= 0 ? c1.g : -INFINITY;
+    f.rf = fi1 >= 0 ? c1.rf : -1;
+    f.idx = lg;
+    f.x = fi1;
+    ArgTake(&win, f);
+  }
   if (lane != 0) return;
+  const double g = win.g;
+  const int leaf = win.idx, wf = win.x;
   if (a.ktrace != nullptr && s - 1 >= 0) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     a.ktrace[(s - 1) * kTraceSlots + kTrPW2] = wall_clock64();
