@@ -361,6 +361,11 @@ inline void SortPairsByKey(std::vector<K>* keys, std::vector<V>* vals, bool desc
 
 // Phase timer: accumulates named scopes, printed at exit when enabled (reference USE_TIMETAG,
 // include/LightGBM/utils/common.h:1054-1135).  Always compiled; enabled by LGBM_AMD_TIMETAG=1.
+// monotonic wall clock in seconds
+inline double NowSeconds() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
 class PhaseTimer {
  public:
   static PhaseTimer& Global() { static PhaseTimer t; return t; }

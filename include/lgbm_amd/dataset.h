@@ -169,8 +169,11 @@ class Dataset {
   // --- CPU training kernels -----------------------------------------------------
   // Accumulate gradient/hessian histograms (double) of rows `indices[0..n)` (or all rows
   // when indices == nullptr) for groups with group_used[g] != 0.  hist has 2*num_total_bin entries.
+  // col-wise (reference dataset.cpp:1283-1384): threads over groups, each walks its column;
+  // row-wise (dataset.cpp:1046-1281, MultiValDenseBin): threads over row blocks of a row-major
+  // copy (built on first use), private histograms merged over bin blocks
   void ConstructHistograms(const std::vector<int8_t>& group_used, const data_size_t* indices, data_size_t n,
-                           const score_t* grad, const score_t* hess, hist_t* hist) const;
+                           const score_t* grad, const score_t* hess, hist_t* hist, bool row_wise = false) const;
   // reconstruct the most-frequent-bin entry of a feature slice from the leaf totals
   void FixHistogram(int inner, double sum_grad, double sum_hess, hist_t* feature_hist) const;
 
@@ -190,6 +193,15 @@ class Dataset {
 
  private:
   void BuildGroups(const std::vector<std::vector<int>>& features_in_group);
+  void ConstructHistogramsRowWise(const std::vector<int8_t>& group_used, const data_size_t* indices, data_size_t n,
+                                  const score_t* grad, const score_t* hess, hist_t* hist) const;
+  void BuildRowMajor() const;
+
+  // row-wise histograms: every group's bin of a row, contiguous (bytes per group as stored)
+  mutable std::vector<uint8_t> row_major_;
+  mutable std::vector<uint32_t> row_goff_;  // byte offset of each group in a row
+  mutable size_t row_stride_ = 0;
+  mutable std::vector<std::vector<hist_t>> row_bufs_;  // per-thread private histograms
 
   data_size_t num_data_ = 0;
   int num_total_features_ = 0;

@@ -526,8 +526,96 @@ bool Dataset::CheckAlign(const Dataset& o) const {
   return true;
 }
 
+void Dataset::BuildRowMajor() const {
+  if (row_stride_ > 0 || groups_.empty()) return;
+  row_goff_.assign(groups_.size(), 0);
+  size_t off = 0;
+  for (size_t g = 0; g < groups_.size(); ++g) {
+    row_goff_[g] = static_cast<uint32_t>(off);
+    off += groups_[g].bin_bytes;
+  }
+  row_stride_ = off;
+  row_major_.assign(static_cast<size_t>(num_data_) * row_stride_, 0);
+#pragma omp parallel for schedule(static)
+  for (data_size_t r = 0; r < num_data_; ++r) {
+    uint8_t* dst = row_major_.data() + static_cast<size_t>(r) * row_stride_;
+    for (size_t g = 0; g < groups_.size(); ++g) {
+      const FeatureGroup& grp = groups_[g];
+      std::memcpy(dst + row_goff_[g], grp.data.data() + static_cast<size_t>(r) * grp.bin_bytes, grp.bin_bytes);
+    }
+  }
+}
+
+void Dataset::ConstructHistogramsRowWise(const std::vector<int8_t>& group_used, const data_size_t* indices,
+                                         data_size_t n, const score_t* grad, const score_t* hess,
+                                         hist_t* hist) const {
+  BuildRowMajor();
+  std::vector<int> used;
+  for (int g = 0; g < num_groups(); ++g) {
+    if (group_used[g]) used.push_back(g);
+  }
+  if (used.empty()) return;
+  const size_t nb = 2 * static_cast<size_t>(num_total_bin());
+  // row blocks of at least 1024 rows, one private histogram per block
+  const int nt = std::max(1, std::min(omp_get_max_threads(), static_cast<int>((n + 1023) / 1024)));
+  if (static_cast<int>(row_bufs_.size()) < nt) row_bufs_.resize(nt);
+  for (int t = 0; t < nt; ++t) {
+    if (row_bufs_[t].size() != nb) row_bufs_[t].assign(nb, 0.0);
+  }
+  const bool narrow = std::all_of(used.begin(), used.end(), [&](int g) { return groups_[g].bin_bytes == 1; });
+#pragma omp parallel for schedule(static, 1) num_threads(nt)
+  for (int t = 0; t < nt; ++t) {
+    hist_t* h = row_bufs_[t].data();
+    for (int g : used) std::fill(h + 2 * group_bin_boundaries_[g], h + 2 * group_bin_boundaries_[g + 1], 0.0);
+    const data_size_t i0 = static_cast<data_size_t>(static_cast<int64_t>(n) * t / nt);
+    const data_size_t i1 = static_cast<data_size_t>(static_cast<int64_t>(n) * (t + 1) / nt);
+    for (data_size_t i = i0; i < i1; ++i) {
+      const data_size_t r = indices ? indices[i] : i;
+      const uint8_t* row = row_major_.data() + static_cast<size_t>(r) * row_stride_;
+      const double g = grad[r], hs = hess[r];
+      if (narrow) {
+        for (int grp : used) {
+          const size_t b = 2 * (group_bin_boundaries_[grp] + row[row_goff_[grp]]);
+          h[b] += g;
+          h[b + 1] += hs;
+        }
+      } else {
+        for (int grp : used) {
+          const uint8_t* p = row + row_goff_[grp];
+          const int bytes = groups_[grp].bin_bytes;
+          const uint32_t v = bytes == 1 ? *p : bytes == 2 ? *reinterpret_cast<const uint16_t*>(p)
+                                                          : *reinterpret_cast<const uint32_t*>(p);
+          const size_t b = 2 * (group_bin_boundaries_[grp] + v);
+          h[b] += g;
+          h[b + 1] += hs;
+        }
+      }
+    }
+  }
+  // merge the private histograms, threads over bin blocks of the used groups (fixed block
+  // order per bin: the sums do not depend on the thread schedule)
+  std::vector<std::pair<size_t, size_t>> ranges;
+  for (int g : used) {
+    const size_t lo = 2 * group_bin_boundaries_[g], hi = 2 * group_bin_boundaries_[g + 1];
+    for (size_t b = lo; b < hi; b += 1024) ranges.emplace_back(b, std::min(hi, b + 1024));
+  }
+#pragma omp parallel for schedule(static)
+  for (int k = 0; k < static_cast<int>(ranges.size()); ++k) {
+    for (size_t b = ranges[k].first; b < ranges[k].second; ++b) {
+      double v = 0.0;
+      for (int t = 0; t < nt; ++t) v += row_bufs_[t][b];
+      hist[b] = v;
+    }
+  }
+}
+
 void Dataset::ConstructHistograms(const std::vector<int8_t>& group_used, const data_size_t* indices,
-                                  data_size_t n, const score_t* grad, const score_t* hess, hist_t* hist) const {
+                                  data_size_t n, const score_t* grad, const score_t* hess, hist_t* hist,
+                                  bool row_wise) const {
+  if (row_wise) {
+    ConstructHistogramsRowWise(group_used, indices, n, grad, hess, hist);
+    return;
+  }
   const int ng = num_groups();
   // gather gradients once in leaf order (the reference's "ordered gradients")
   std::vector<score_t> og, oh;
@@ -739,6 +827,8 @@ void Dataset::DumpText(const std::string& path) const {
 
 void Dataset::AddFeaturesFrom(const Dataset& other) {
   if (other.num_data_ != num_data_) Log::Fatal("Cannot add features from other Dataset with a different number of rows");
+  row_stride_ = 0;  // the row-major copy follows the new groups
+  row_major_.clear();
   const int old_total = num_total_features_;
   const int old_inner = num_features_;
   const int old_groups = num_groups();

@@ -1315,7 +1315,7 @@ void GPUTreeLearner::BuildRangeHistogram(int leaf, int slot) {
   HIPCHECK(hipMemcpyAsync(h_scales_, d_scales_, sizeof(double) * 4, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   if (data_parallel_ && Network::num_machines() > 1) h = Network::GlobalSum(h);
-  std::vector<hist_t>& dst = hist_pool_[slot];
+  std::vector<hist_t>& dst = LeafHist(slot);
   const double ig = h_scales_[2], ih = h_scales_[3];
   for (size_t i = 0; i < n; i += 2) {
     dst[i] = static_cast<double>(h[i]) * ig;

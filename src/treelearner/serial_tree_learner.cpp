@@ -48,9 +48,9 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool /*is_constant_hessi
   col_sampler_.SetTrainingData(data_);
   best_split_per_leaf_.assign(config_->num_leaves, SplitInfo());
   constraints_.Init(config_->num_leaves, config_);
-  const size_t total_bins = data_->num_total_bin();
-  hist_pool_.assign(config_->num_leaves, std::vector<hist_t>(2 * total_bins, 0.0));
+  ResetPool();
   splittable_.assign(config_->num_leaves, std::vector<char>(num_features_, 1));
+  hist_mode_ = config_->force_row_wise ? 2 : config_->force_col_wise ? 1 : 0;
   indices_.resize(num_data_);
   leaf_begin_.assign(config_->num_leaves, 0);
   leaf_count_.assign(config_->num_leaves, 0);
@@ -93,16 +93,73 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
   config_ = config;
   if (leaves_changed) {
     best_split_per_leaf_.assign(config_->num_leaves, SplitInfo());
-    const size_t total_bins = data_->num_total_bin();
-    hist_pool_.assign(config_->num_leaves, std::vector<hist_t>(2 * total_bins, 0.0));
     splittable_.assign(config_->num_leaves, std::vector<char>(num_features_, 1));
     leaf_begin_.assign(config_->num_leaves, 0);
     leaf_count_.assign(config_->num_leaves, 0);
   }
+  ResetPool();
+  if (config_->force_row_wise) hist_mode_ = 2;
+  else if (config_->force_col_wise) hist_mode_ = 1;
   col_sampler_.SetConfig(config_);
   constraints_.Init(config_->num_leaves, config_);
   InitFeatureMeta();
   SetupCegb();
+}
+
+void SerialTreeLearner::ResetPool() {
+  const size_t total_bins = data_->num_total_bin();
+  int slots = config_->num_leaves;
+  if (config_->histogram_pool_size > 0) {  // (reference SerialTreeLearner::Init's cache size)
+    const double bytes = sizeof(hist_t) * 2.0 * static_cast<double>(total_bins);
+    slots = static_cast<int>(config_->histogram_pool_size * 1024 * 1024 / bytes);
+  }
+  slots = std::min(config_->num_leaves, std::max(2, slots));
+  if (static_cast<int>(hist_pool_.size()) != slots) {
+    hist_pool_.assign(slots, std::vector<hist_t>(2 * total_bins, 0.0));
+    if (slots < config_->num_leaves) {
+      Log::Info("Histogram pool: %d of %d leaves' histograms cached (histogram_pool_size=%g MB)", slots,
+                config_->num_leaves, config_->histogram_pool_size);
+    }
+  }
+  leaf_slot_.assign(config_->num_leaves, -1);
+  slot_leaf_.assign(slots, -1);
+  slot_stamp_.assign(slots, 0);
+  pool_clock_ = 0;
+}
+
+void SerialTreeLearner::PoolTouch(int leaf) {
+  if (leaf_slot_[leaf] >= 0) slot_stamp_[leaf_slot_[leaf]] = ++pool_clock_;
+}
+
+void SerialTreeLearner::PoolAssign(int leaf, int keep_leaf) {
+  if (leaf_slot_[leaf] >= 0) {
+    PoolTouch(leaf);
+    return;
+  }
+  int best = -1;
+  for (int k = 0; k < static_cast<int>(slot_leaf_.size()); ++k) {
+    if (slot_leaf_[k] < 0) {
+      best = k;
+      break;
+    }
+    if (slot_leaf_[k] == keep_leaf) continue;
+    if (best < 0 || slot_stamp_[k] < slot_stamp_[best]) best = k;
+  }
+  if (slot_leaf_[best] >= 0) leaf_slot_[slot_leaf_[best]] = -1;  // evict the least recently used
+  slot_leaf_[best] = leaf;
+  leaf_slot_[leaf] = best;
+  slot_stamp_[best] = ++pool_clock_;
+}
+
+void SerialTreeLearner::PoolMove(int from_leaf, int to_leaf) {
+  const int k = leaf_slot_[from_leaf];
+  if (leaf_slot_[to_leaf] >= 0) slot_leaf_[leaf_slot_[to_leaf]] = -1;
+  leaf_slot_[to_leaf] = k;
+  leaf_slot_[from_leaf] = -1;
+  if (k >= 0) {
+    slot_leaf_[k] = to_leaf;
+    slot_stamp_[k] = ++pool_clock_;
+  }
 }
 
 void SerialTreeLearner::SetForcedSplit(const std::string& json_text) {
@@ -121,6 +178,7 @@ void SerialTreeLearner::SetBaggingData(const Dataset*, const data_size_t* used_i
 
 void SerialTreeLearner::BeforeTrain() {
   col_sampler_.ResetByTree();
+  ResetPool();  // every leaf's slot is free at the root
   // partition: every used row in leaf 0
   std::fill(leaf_begin_.begin(), leaf_begin_.end(), 0);
   std::fill(leaf_count_.begin(), leaf_count_.end(), 0);
@@ -199,18 +257,25 @@ bool SerialTreeLearner::BeforeFindBestSplit(const Tree* tree, int left_leaf, int
   if (right_leaf < 0) {
     smaller_slot_ = left_leaf;
     larger_slot_ = -1;
-  } else if (nl < nr) {
-    // parent histogram (slot of left) moves to the larger (right) leaf
-    std::swap(hist_pool_[left_leaf], hist_pool_[right_leaf]);
+    PoolAssign(left_leaf, -1);
+    return true;
+  }
+  // the parent's histogram (held by the left leaf id) moves to the larger child; the smaller
+  // child takes a new slot.  A parent evicted from a bounded pool: both children from rows.
+  const bool parent_cached = leaf_slot_[left_leaf] >= 0;
+  if (nl < nr) {
     std::swap(splittable_[left_leaf], splittable_[right_leaf]);
     larger_slot_ = right_leaf;
     smaller_slot_ = left_leaf;
-    has_parent_hist_ = true;
+    PoolMove(left_leaf, right_leaf);
   } else {
     larger_slot_ = left_leaf;
     smaller_slot_ = right_leaf;
-    has_parent_hist_ = true;
+    PoolTouch(left_leaf);
   }
+  has_parent_hist_ = parent_cached;
+  PoolAssign(larger_slot_, -1);
+  PoolAssign(smaller_slot_, larger_slot_);
   return true;
 }
 
@@ -244,12 +309,30 @@ void SerialTreeLearner::ConstructHistograms(const std::vector<int8_t>& feature_u
   data_size_t cnt = 0;
   const data_size_t* idx = LeafIndices(smaller_.leaf, &cnt);
   const bool all_rows = !use_bag_ && cnt == num_data_;
+  if (hist_mode_ == 0) hist_mode_ = ChooseHistogramThreading(groups, all_rows ? nullptr : idx, cnt);
+  const bool row_wise = hist_mode_ == 2;
   data_->ConstructHistograms(groups, all_rows ? nullptr : idx, cnt, gradients_, hessians_,
-                             hist_pool_[smaller_slot_].data());
+                             LeafHist(smaller_slot_).data(), row_wise);
   if (larger_slot_ >= 0 && !use_subtract) {
     const data_size_t* idx2 = LeafIndices(larger_.leaf, &cnt);
-    data_->ConstructHistograms(groups, idx2, cnt, gradients_, hessians_, hist_pool_[larger_slot_].data());
+    data_->ConstructHistograms(groups, idx2, cnt, gradients_, hessians_, LeafHist(larger_slot_).data(), row_wise);
   }
+}
+
+// auto threading (reference Dataset::TestMultiThreadingMethod, dataset.cpp:589-684): the
+// first histogram is built both ways and the faster one is kept for the rest of training
+int SerialTreeLearner::ChooseHistogramThreading(const std::vector<int8_t>& groups, const data_size_t* idx,
+                                                data_size_t cnt) {
+  const double t0 = common::NowSeconds();
+  data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, LeafHist(smaller_slot_).data(), false);
+  const double t1 = common::NowSeconds();
+  data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, LeafHist(smaller_slot_).data(), true);
+  const double t2 = common::NowSeconds();
+  const bool row = (t2 - t1) < (t1 - t0);
+  Log::Info("Auto-choosing %s-wise multi-threading, the overhead of testing was %f seconds.\n"
+            "You can set `force_%s_wise=true` to remove the overhead.",
+            row ? "row" : "col", t2 - t0, row ? "row" : "col");
+  return row ? 2 : 1;
 }
 
 void SerialTreeLearner::ComputeBestSplitForFeature(int slot, int inner, const std::vector<int8_t>& node_used,
@@ -433,7 +516,11 @@ void SerialTreeLearner::SplitInner(Tree* tree, int best_leaf, int* left_leaf, in
 
 void SerialTreeLearner::RecomputeBestSplitForLeaf(const Tree* tree, int leaf) {
   SplitInfo& cur = best_split_per_leaf_[leaf];
-  const int slot = leaf;  // a leaf's histogram lives in the pool slot of its id (BeforeFindBestSplit)
+  const int slot = leaf;  // (FeatureHist maps the leaf to its pool slot)
+  if (leaf_slot_[leaf] < 0) {  // evicted from a bounded pool (reference: skipped with a warning)
+    Log::Warning("Get historical Histogram for leaf %d failed, will skip the ``RecomputeBestSplitForLeaf``", leaf);
+    return;
+  }
   // the leaf's statistics as its current best split saw them (reference: a fresh LeafSplits,
   // whose output -- the smoothing parent -- is 0)
   LeafState ls{leaf, cur.left_count + cur.right_count, cur.left_sum_gradient + cur.right_sum_gradient,

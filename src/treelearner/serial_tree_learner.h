@@ -60,6 +60,7 @@ class SerialTreeLearner : public TreeLearner {
   virtual bool BeforeFindBestSplit(const Tree* tree, int left_leaf, int right_leaf);
   virtual void FindBestSplits(const Tree* tree);
   virtual void ConstructHistograms(const std::vector<int8_t>& feature_used, bool use_subtract);
+  int ChooseHistogramThreading(const std::vector<int8_t>& groups, const data_size_t* idx, data_size_t cnt);
   virtual void FindBestSplitsFromHistograms(const std::vector<int8_t>& feature_used, bool use_subtract,
                                             const Tree* tree);
   virtual void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf);
@@ -72,7 +73,9 @@ class SerialTreeLearner : public TreeLearner {
   // evaluate one feature histogram with explicit params; returns splittability
   bool EvalFeature(hist_t* hist, int inner, const SplitParams& p, const LeafState& ls, int depth, SplitInfo* best);
   void SplitInner(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf, bool update_cnt);
-  hist_t* FeatureHist(int slot, int inner) { return hist_pool_[slot].data() + 2 * data_->FeatureHistOffset(inner); }
+  // a leaf's histogram (the leaf must hold a pool slot: BeforeFindBestSplit assigns them)
+  std::vector<hist_t>& LeafHist(int leaf) { return hist_pool_[leaf_slot_[leaf]]; }
+  hist_t* FeatureHist(int leaf, int inner) { return LeafHist(leaf).data() + 2 * data_->FeatureHistOffset(inner); }
   void InitFeatureMeta();
   // intermediate monotone constraints: a leaf whose bounds another split tightened gets its
   // best split recomputed from its stored histogram (reference RecomputeBestSplitForLeaf)
@@ -90,10 +93,25 @@ class SerialTreeLearner : public TreeLearner {
   LeafConstraints constraints_;
   std::vector<SplitInfo> best_split_per_leaf_;
 
-  // histogram pool: one full histogram per leaf id (the parent's moves to its larger child)
+  // histogram pool (reference HistogramPool, feature_histogram.hpp:1061-1301): full
+  // histograms in slots, leaves mapped to slots; the parent's slot moves to its larger child.
+  // histogram_pool_size (MB) bounds the slots below num_leaves: the least recently used leaf
+  // is evicted, and a child whose parent was evicted is histogrammed from its rows
+  void ResetPool();
+  void PoolTouch(int leaf);
+  void PoolAssign(int leaf, int keep_leaf);  // a slot for `leaf`, never evicting keep_leaf
+  void PoolMove(int from_leaf, int to_leaf);
   std::vector<std::vector<hist_t>> hist_pool_;
-  std::vector<std::vector<char>> splittable_;  // per slot, per inner feature
+  std::vector<int> leaf_slot_;         // leaf -> slot (-1: not cached)
+  std::vector<int> slot_leaf_;         // slot -> leaf (-1: free)
+  std::vector<long long> slot_stamp_;  // last use (LRU)
+  long long pool_clock_ = 0;
+  std::vector<std::vector<char>> splittable_;  // per leaf, per inner feature
+  // the step's smaller / larger leaf ids (their histograms: LeafHist)
   int smaller_slot_ = -1, larger_slot_ = -1;
+  // CPU histogram threading (reference Dataset::TestMultiThreadingMethod): 0 undecided (auto),
+  // 1 col-wise (threads over feature groups), 2 row-wise (threads over row blocks)
+  int hist_mode_ = 0;
   bool has_parent_hist_ = false;
   LeafState smaller_, larger_;
 
