@@ -99,27 +99,47 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
   // word 0 of column tile 0 (each row once) -- that child's local sums
   const bool loc_sums = HIST && a.p.vote_phase != 0 && blockIdx.y == 0;
   long long loc_g = 0, loc_h = 0;
+  // software pipeline over the workgroup's sub-tiles: the next sub-tile's row indices are
+  // loaded while this one is processed, and its split-column bins before the sub-tile ends
+  // (two dependent round trips off every sub-tile but the first; large parents run ~10
+  // sub-tiles per workgroup)
+  int row[kSplitRows];
+  uint32_t gb[kSplitRows];
+  auto load_rows = [&](int t0n, int r1n, int* rr) {
+    const int vn = min(kSplitSub, r1n - t0n);
+#pragma unroll
+    for (int k = 0; k < kSplitRows; ++k) {
+      const int i = k * kPartThreads + threadIdx.x;
+      rr[k] = i < vn ? src[pb + t0n + i] : -1;
+    }
+  };
+  if (static_cast<int>(blockIdx.x) < nblk) {
+    const int r0 = blockIdx.x * chunk;
+    load_rows(r0, min(pc, r0 + chunk), row);
+#pragma unroll
+    for (int k = 0; k < kSplitRows; ++k) gb[k] = row[k] >= 0 ? ColBin(a, row[k], fbyte, fwide, fcol) : 0u;
+  }
   for (int kb = blockIdx.x; kb < nblk; kb += gridDim.x) {
     const int r0 = kb * chunk, r1 = min(pc, r0 + chunk);
     const bool first_trace = kb == static_cast<int>(blockIdx.x);
     for (int t0 = r0; t0 < r1; t0 += kSplitSub) {
       const int valid = min(kSplitSub, r1 - t0);
       const bool tr = first_trace && t0 == r0;
-      // ---- A: sides
-      int row[kSplitRows];
-#pragma unroll
-      for (int k = 0; k < kSplitRows; ++k) {
-        const int i = k * kPartThreads + threadIdx.x;
-        row[k] = i < valid ? src[pb + t0 + i] : -1;
+      // the next sub-tile of this workgroup (this block's next one, or the next block's first)
+      int nt0 = t0 + kSplitSub, nr1 = r1;
+      if (nt0 >= r1) {
+        const int nkb = kb + gridDim.x;
+        nt0 = nkb < nblk ? nkb * chunk : pc;
+        nr1 = nkb < nblk ? min(pc, nt0 + chunk) : pc;
       }
+      int nrow[kSplitRows];
+      load_rows(nt0, nr1, nrow);
+      // ---- A: sides
       if (HIST && t0 == r0) {
         __syncthreads();  // the previous block's partial was stored from this LDS
         for (int j = threadIdx.x; j < UNITS * t.nbins; j += kPartThreads) lds[j] = 0ull;
       }
       if (tr) KTrace(a, ts, kTrSplitRows);
-      uint32_t gb[kSplitRows];
-#pragma unroll
-      for (int k = 0; k < kSplitRows; ++k) gb[k] = row[k] >= 0 ? ColBin(a, row[k], fbyte, fwide, fcol) : 0u;
       if (tr) KTrace(a, ts, kTrSplitSide);
       bool left[kSplitRows];
       unsigned long long mask[kSplitRows];
@@ -222,6 +242,12 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
             }
           }
         }
+      }
+      // the next sub-tile's split-column bins (its rows arrived during this one)
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) {
+        row[k] = nrow[k];
+        gb[k] = row[k] >= 0 ? ColBin(a, row[k], fbyte, fwide, fcol) : 0u;
       }
       __syncthreads();  // row list, wave counts and bases are rewritten by the next sub-tile
       if (tr) KTrace(a, ts, kTrSplitAccum);
