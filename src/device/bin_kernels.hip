@@ -48,15 +48,26 @@ struct BinGroup {
 
 constexpr int kBinThreads = 256;
 constexpr int kGroupsPerThread = 8;
+constexpr int kBinLdsDoubles = 6144;  // 48 KiB of staged upper bounds per workgroup
 
 template <typename T>
 __global__ __launch_bounds__(kBinThreads) void k_value_to_bin(const T* x, int rows, long long rs, long long cs,
                                                               const BinGroup* groups, int ngroups,
                                                               const BinFeat* feats, const double* ub,
                                                               uint8_t* out) {
+  // the slice's upper bounds staged in LDS when they fit (the binary search is a chain of
+  // dependent loads: from L2 it took ~0.85 ms per 2.4M x 28 chunk)
+  extern __shared__ double s_ub[];
+  const int g0 = blockIdx.y * kGroupsPerThread, g1 = min(ngroups, g0 + kGroupsPerThread);
+  const int ub_lo = feats[groups[g0].fbegin].ub_off;
+  const int ub_n = g1 > g0 ? feats[groups[g1 - 1].fend - 1].ub_off + feats[groups[g1 - 1].fend - 1].hi + 1 - ub_lo : 0;
+  const bool staged = ub_n <= kBinLdsDoubles;
+  if (staged) {
+    for (int j = threadIdx.x; j < ub_n; j += kBinThreads) s_ub[j] = ub[ub_lo + j];
+    __syncthreads();
+  }
   const int r = blockIdx.x * kBinThreads + threadIdx.x;
   if (r >= rows) return;
-  const int g0 = blockIdx.y * kGroupsPerThread, g1 = min(ngroups, g0 + kGroupsPerThread);
   const T* xr = x + rs * r;
   for (int g = g0; g < g1; ++g) {
     const BinGroup G = groups[g];
@@ -69,7 +80,7 @@ __global__ __launch_bounds__(kBinThreads) void k_value_to_bin(const T* x, int ro
         bin = F.nan_bin;
       } else {
         if (isnan(value)) value = 0.0;
-        const double* u = ub + F.ub_off;
+        const double* u = staged ? s_ub + (F.ub_off - ub_lo) : ub + F.ub_off;
         int lo = 0, hi = F.hi;
         while (lo < hi) {
           const int mid = (lo + hi - 1) / 2;
@@ -200,10 +211,10 @@ std::vector<char> DeviceBinDenseMatrix(Dataset* ds, const void* data, bool is_f6
     }
     const dim3 grid((rows + kBinThreads - 1) / kBinThreads, (ngroups + kGroupsPerThread - 1) / kGroupsPerThread);
     if (is_f64) {
-      hipLaunchKernelGGL(k_value_to_bin<double>, grid, dim3(kBinThreads), 0, 0, static_cast<const double*>(d_x), rows,
+      hipLaunchKernelGGL(k_value_to_bin<double>, grid, dim3(kBinThreads), sizeof(double) * kBinLdsDoubles, 0, static_cast<const double*>(d_x), rows,
                          rs, cs, d_groups, ngroups, d_feats, d_ub, d_out);
     } else {
-      hipLaunchKernelGGL(k_value_to_bin<float>, grid, dim3(kBinThreads), 0, 0, static_cast<const float*>(d_x), rows,
+      hipLaunchKernelGGL(k_value_to_bin<float>, grid, dim3(kBinThreads), sizeof(double) * kBinLdsDoubles, 0, static_cast<const float*>(d_x), rows,
                          rs, cs, d_groups, ngroups, d_feats, d_ub, d_out);
     }
     BINCHECK(hipGetLastError());
