@@ -339,7 +339,8 @@ void PredictForest(const ForestArgs& f, hipStream_t s);
 constexpr int kMetricL2 = 1, kMetricRMSE = 2, kMetricL1 = 3, kMetricBinLogloss = 4, kMetricBinError = 5,
               kMetricAUC = 6, kMetricQuantile = 7, kMetricHuber = 8, kMetricFair = 9, kMetricPoisson = 10,
               kMetricMape = 11, kMetricGamma = 12, kMetricGammaDeviance = 13, kMetricTweedie = 14, kMetricXent = 15,
-              kMetricMultiLogloss = 20, kMetricMultiError = 21, kMetricNDCG = 30, kMetricMAP = 31;
+              kMetricMultiLogloss = 20, kMetricMultiError = 21, kMetricAucMu = 22, kMetricNDCG = 30,
+              kMetricMAP = 31;
 struct MetricArgs {
   int32_t kind;
   int32_t convert;       // score -> prediction: 0 identity, 1 sigmoid(sigmoid * s), 2 sign(s) * s^2, 3 exp,
@@ -356,11 +357,13 @@ struct MetricArgs {
   const int32_t* qb;       // [nq + 1]
   const float* qw;         // [nq] or null
   const int32_t* eval_at;  // [nk]
-  const double* qconst;    // NDCG: [nq][nk] 1 / max DCG (<= 0: no relevant document); MAP: [nq] relevant documents
+  const double* qconst;    // NDCG: [nq][nk] 1 / max DCG (<= 0: no relevant document); MAP: [nq] relevant documents;
+                           // AUC-mu: [num_class][num_class] auc_mu_weights
   const double* label_gain;
   const double* discount;  // [kRankMaxDocs]
   void* scratch;         // MetricScratchBytes(n, nq * nk)
-  double* out;           // [0] weighted loss sum (or AUC accumulator), [1] AUC positive weight; query: [nk]
+  double* out;           // [0] weighted loss sum (or AUC accumulator), [1] AUC positive weight; query: [nk];
+                         // AUC-mu: per class pair (i < j) accumulator and class-j count
 };
 size_t MetricScratchBytes(int64_t n, int64_t query_values = 0);
 void EvalMetric(const MetricArgs& m, hipStream_t s);

@@ -185,6 +185,39 @@ __global__ __launch_bounds__(kMetricThreads) void k_auc_accum(const PosNeg* agg,
   if (blockIdx.x == 0 && threadIdx.x == 0) out[1] = n > 0 ? pos_before[n - 1] + agg[n - 1].pos : 0.0;
 }
 
+// AUC-mu (reference multiclass_metric.hpp AucMuMetric): the pair (i, j)'s binary AUC with
+// class j as positives over the keys -t1 * (v . score), v = W[i] - W[j], t1 = v[i] - v[j];
+// rows of other classes weigh nothing.  Products and sums are rounded one by one (no fused
+// multiply-add) as on the host.
+__global__ __launch_bounds__(kMetricThreads) void k_aucmu_keys(MetricArgs m, int ci, int cj, double* keys,
+                                                               int32_t* idx) {
+  const int K = m.num_class;
+  const double* wi = m.qconst + static_cast<int64_t>(ci) * K;
+  const double* wj = m.qconst + static_cast<int64_t>(cj) * K;
+  const double t1 = __dadd_rn(wi[ci] - wj[ci], -(wi[cj] - wj[cj]));
+  for (int64_t r = blockIdx.x * static_cast<int64_t>(kMetricThreads) + threadIdx.x; r < m.n;
+       r += static_cast<int64_t>(gridDim.x) * kMetricThreads) {
+    const int lab = static_cast<int>(m.label[r]);
+    double key = 0.0;
+    if (lab == ci || lab == cj) {
+      double va = 0.0;
+      for (int k = 0; k < K; ++k) va = __dadd_rn(va, __dmul_rn(wi[k] - wj[k], m.score[static_cast<int64_t>(k) * m.n + r]));
+      key = -__dmul_rn(t1, va) + 0.0;  // (+0.0: no negative zero key apart from 0.0)
+    }
+    keys[r] = key;
+    idx[r] = static_cast<int32_t>(r);
+  }
+}
+
+__global__ __launch_bounds__(kMetricThreads) void k_aucmu_weights(MetricArgs m, int ci, int cj, const int32_t* idx,
+                                                                  PosNeg* pn) {
+  for (int64_t k = blockIdx.x * static_cast<int64_t>(kMetricThreads) + threadIdx.x; k < m.n;
+       k += static_cast<int64_t>(gridDim.x) * kMetricThreads) {
+    const int lab = static_cast<int>(m.label[idx[k]]);
+    pn[k] = PosNeg{lab == cj ? 1.0 : 0.0, lab == ci ? 1.0 : 0.0};
+  }
+}
+
 template <typename T>
 T* Carve(char** p, size_t count) {
   const size_t a = 256;
@@ -304,7 +337,7 @@ void EvalMetric(const MetricArgs& m, hipStream_t s) {
   double* partials = Carve<double>(&p, kMetricBlocks);
   const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((m.n + kMetricThreads - 1) / kMetricThreads,
                                                                              kMetricBlocks)));
-  if (m.kind != kMetricAUC) {
+  if (m.kind != kMetricAUC && m.kind != kMetricAucMu) {
     hipLaunchKernelGGL(k_point_loss, dim3(blocks), dim3(kMetricThreads), 0, s, m, partials);
     hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kMetricThreads), 0, s, partials, blocks, m.out, 0);
     return;
@@ -323,18 +356,39 @@ void EvalMetric(const MetricArgs& m, hipStream_t s) {
   size_t temp_bytes = CubTempBytes(m.n);
   void* temp = Carve<char>(&p, temp_bytes);
   const int nn = static_cast<int>(m.n);
-  hipLaunchKernelGGL(k_auc_keys, dim3(blocks), dim3(kMetricThreads), 0, s, m, keys, idx);
-  (void)hipcub::DeviceRadixSort::SortPairsDescending(temp, temp_bytes, keys, keys_sorted, idx, idx_sorted, nn, 0,
-                                                     sizeof(double) * 8, s);
-  hipLaunchKernelGGL(k_auc_weights, dim3(blocks), dim3(kMetricThreads), 0, s, m, idx_sorted, pn);
-  temp_bytes = CubTempBytes(m.n);
-  (void)hipcub::DeviceReduce::ReduceByKey(temp, temp_bytes, keys_sorted, uniq, pn, agg, num_runs, PosNegSum(), nn, s);
-  hipLaunchKernelGGL(k_auc_pos, dim3(blocks), dim3(kMetricThreads), 0, s, agg, num_runs, runpos);
-  temp_bytes = CubTempBytes(m.n);
-  // runs beyond num_runs hold stale values; the exclusive sum of the first num_runs is all that is read
-  (void)hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, runpos, pos_before, nn, s);
-  hipLaunchKernelGGL(k_auc_accum, dim3(blocks), dim3(kMetricThreads), 0, s, agg, pos_before, num_runs, partials, m.out);
-  hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kMetricThreads), 0, s, partials, blocks, m.out, 0);
+  // one binary AUC: keys (descending), the rows' (positive, negative) weights in that order,
+  // tie runs, positives before each run, accumulated into out[0] / out[1]
+  auto auc = [&](int ci, int cj, double* out) {
+    size_t tb = temp_bytes;
+    if (m.kind == kMetricAucMu) {
+      hipLaunchKernelGGL(k_aucmu_keys, dim3(blocks), dim3(kMetricThreads), 0, s, m, ci, cj, keys, idx);
+    } else {
+      hipLaunchKernelGGL(k_auc_keys, dim3(blocks), dim3(kMetricThreads), 0, s, m, keys, idx);
+    }
+    (void)hipcub::DeviceRadixSort::SortPairsDescending(temp, tb, keys, keys_sorted, idx, idx_sorted, nn, 0,
+                                                       sizeof(double) * 8, s);
+    if (m.kind == kMetricAucMu) {
+      hipLaunchKernelGGL(k_aucmu_weights, dim3(blocks), dim3(kMetricThreads), 0, s, m, ci, cj, idx_sorted, pn);
+    } else {
+      hipLaunchKernelGGL(k_auc_weights, dim3(blocks), dim3(kMetricThreads), 0, s, m, idx_sorted, pn);
+    }
+    tb = temp_bytes;
+    (void)hipcub::DeviceReduce::ReduceByKey(temp, tb, keys_sorted, uniq, pn, agg, num_runs, PosNegSum(), nn, s);
+    hipLaunchKernelGGL(k_auc_pos, dim3(blocks), dim3(kMetricThreads), 0, s, agg, num_runs, runpos);
+    tb = temp_bytes;
+    // runs beyond num_runs hold stale values; the exclusive sum of the first num_runs is all that is read
+    (void)hipcub::DeviceScan::ExclusiveSum(temp, tb, runpos, pos_before, nn, s);
+    hipLaunchKernelGGL(k_auc_accum, dim3(blocks), dim3(kMetricThreads), 0, s, agg, pos_before, num_runs, partials, out);
+    hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kMetricThreads), 0, s, partials, blocks, out, 0);
+  };
+  if (m.kind == kMetricAUC) {
+    auc(0, 0, m.out);
+    return;
+  }
+  int pair = 0;
+  for (int ci = 0; ci < m.num_class; ++ci) {
+    for (int cj = ci + 1; cj < m.num_class; ++cj) auc(ci, cj, m.out + 2 * pair++);
+  }
 }
 
 }  // namespace dev

@@ -303,6 +303,27 @@ class AucMuMetric : public Metric {
   explicit AucMuMetric(const Config& c) : num_class_(c.num_class), w_(c.auc_mu_weights_matrix) {
     name_.push_back("auc_mu");
   }
+  DeviceMetricSpec DeviceSpec(const ObjectiveFunction*) const override {
+    DeviceMetricSpec d;
+    d.kind = 22;  // dev::kMetricAucMu: per class pair, the tie-aware binary AUC on the device
+    d.num_class = num_class_;
+    d.nout = num_class_ * (num_class_ - 1);  // (accumulator, class-j count) per pair
+    d.label = label_;
+    d.key = this;
+    for (const auto& row : w_) d.qconst.insert(d.qconst.end(), row.begin(), row.end());
+    if (static_cast<int>(d.qconst.size()) != num_class_ * num_class_) d.kind = 0;
+    return d;
+  }
+  std::vector<double> FinishDevice(const std::vector<double>& sums) const override {
+    std::vector<data_size_t> cs(num_class_, 0);
+    for (data_size_t i = 0; i < num_data_; ++i) ++cs[static_cast<int>(label_[i])];
+    double ans = 0;
+    int pair = 0;
+    for (int i = 0; i < num_class_; ++i) {
+      for (int j = i + 1; j < num_class_; ++j, ++pair) ans += (sums[2 * pair] / cs[i]) / cs[j];
+    }
+    return {(2 * ans / num_class_) / (num_class_ - 1)};
+  }
   void Init(const Metadata& md, data_size_t n) override {
     num_data_ = n;
     label_ = md.label();

@@ -1712,7 +1712,8 @@ void GPUTreeLearner::ValidAddTree(int slot, const Tree* tree, int k) {
 bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) {
   ValidSet& vs = valid_[slot];
   if (spec.kind == 0 || spec.label == nullptr || vs.num_data <= 0) return false;
-  const bool multi = spec.kind == dev::kMetricMultiLogloss || spec.kind == dev::kMetricMultiError;
+  const bool aucmu = spec.kind == dev::kMetricAucMu;
+  const bool multi = spec.kind == dev::kMetricMultiLogloss || spec.kind == dev::kMetricMultiError || aucmu;
   const bool query = spec.kind == dev::kMetricNDCG || spec.kind == dev::kMetricMAP;
   if (vs.ntpi != (multi ? spec.num_class : 1)) return false;
   if (query && (spec.qb == nullptr || spec.nq <= 0 || spec.eval_at.empty())) return false;
@@ -1764,7 +1765,16 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
     m.discount = qi.discount;
     m.scratch = qi.scratch;
   } else {
-    if (spec.kind == dev::kMetricAUC && vs.metric_scratch_rows < vs.num_data) {
+    if (aucmu) {  // the class weight matrix, uploaded on the metric's first evaluation
+      auto it = vs.queries.find(spec.key);
+      if (it == vs.queries.end()) {
+        ValidSet::QueryInputs qi;
+        qi.qconst = static_cast<double*>(upload(spec.qconst.data(), sizeof(double) * spec.qconst.size()));
+        it = vs.queries.emplace(spec.key, qi).first;
+      }
+      m.qconst = it->second.qconst;
+    }
+    if ((spec.kind == dev::kMetricAUC || aucmu) && vs.metric_scratch_rows < vs.num_data) {
       vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(vs.num_data));
       vs.metric_scratch_rows = vs.num_data;
     } else if (vs.metric_scratch == nullptr) {

@@ -231,12 +231,11 @@ def test_device_binning_matches_host(tmp_path, monkeypatch, dtype, order):
     X = np.hstack([X, sp])
     X[:50, 0] = np.linspace(-1, 1, 50)                   # values on and around bin bounds
     X = np.asarray(X, dtype=dtype, order=order)
-    params = {"objective": "binary", "max_bin": 63, "verbose": -1, "device_type": "gpu",
-              "categorical_feature": [4, 5]}
+    params = {"objective": "binary", "max_bin": 63, "verbose": -1, "device_type": "gpu"}
     files = []
     for mode in ("0", "1"):
         monkeypatch.setenv("LGBM_AMD_DEVICE_BINNING", mode)
-        ds = lgb.Dataset(X, y, params=params).construct()
+        ds = lgb.Dataset(X, y, params=params, categorical_feature=[4, 5]).construct()
         f = tmp_path / ("bins_%s.bin" % mode)
         ds.save_binary(str(f))
         files.append(f.read_bytes())
@@ -244,7 +243,7 @@ def test_device_binning_matches_host(tmp_path, monkeypatch, dtype, order):
     # and a small bound check of one value: the validation set binned on the device against
     # the training set's mappers gives the same model predictions
     monkeypatch.setenv("LGBM_AMD_DEVICE_BINNING", "1")
-    tr = lgb.Dataset(X, y, params=params)
-    va = lgb.Dataset(X[:20000], y[:20000], reference=tr)
+    tr = lgb.Dataset(X, y, params=params, categorical_feature=[4, 5])
+    va = lgb.Dataset(X[:20000], y[:20000], reference=tr, categorical_feature=[4, 5])
     bst = lgb.train(dict(params, num_leaves=15), tr, num_boost_round=3, valid_sets=[va])
     assert bst.num_trees() == 3

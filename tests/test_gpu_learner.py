@@ -459,7 +459,7 @@ def test_intermediate_monotone_on_gpu(gpu_available):
 
 
 
-@pytest.mark.parametrize("task", ["lambdarank", "multiclass", "regression_family"])
+@pytest.mark.parametrize("task", ["lambdarank", "multiclass", "aucmu_weighted", "regression_family"])
 def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, capfd):
     """Validation metrics evaluated on device-resident scores (NDCG / MAP one workgroup per
     query, multiclass on class-major scores, point-wise regression losses) equal the host
@@ -472,12 +472,16 @@ def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, cap
         yv = np.clip(np.round(Xv[:, 0] + Xv[:, 1] + rng.randn(nv)), 0, 4)
         group, gv = [40] * (n // 40), [30] * (nv // 30)
         params = {"objective": "lambdarank", "metric": ["ndcg", "map"], "eval_at": [1, 3, 5, 10]}
-    elif task == "multiclass":
+    elif task in ("multiclass", "aucmu_weighted"):
         y = (np.argmax(X[:, :4] + 0.5 * rng.randn(n, 4), axis=1)).astype(float)
         yv = (np.argmax(Xv[:, :4] + 0.5 * rng.randn(nv, 4), axis=1)).astype(float)
         group = gv = None
-        params = {"objective": "multiclass", "num_class": 4, "metric": ["multi_logloss", "multi_error"],
+        params = {"objective": "multiclass", "num_class": 4, "metric": ["multi_logloss", "multi_error", "auc_mu"],
                   "multi_error_top_k": 2}
+        if task == "aucmu_weighted":  # AUC-mu with a class-cost matrix (zero diagonal)
+            w = np.array([[0, 1, 2, 3], [1, 0, 1, 2], [2, 1, 0, 1], [3, 2, 1, 0]], dtype=float)
+            params = {"objective": "multiclassova", "num_class": 4, "metric": ["auc_mu"],
+                      "auc_mu_weights": list(w.ravel())}
     else:
         y = np.exp(0.3 * X[:, 0]) + rng.rand(n)
         yv = np.exp(0.3 * Xv[:, 0]) + rng.rand(nv)
@@ -496,13 +500,14 @@ def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, cap
     params["verbose"] = 2
     dev = run()
     logged = capfd.readouterr().out
-    kinds = {"lambdarank": (30, 31), "multiclass": (20, 21), "regression_family": (10, 13, 7, 8, 11)}[task]
+    kinds = {"lambdarank": (30, 31), "multiclass": (20, 21, 22), "aucmu_weighted": (22,),
+             "regression_family": (10, 13, 7, 8, 11)}[task]
     for k in kinds:  # the device path ran
         assert "device metric (kind %d)" % k in logged, k
     params["verbose"] = -1
     monkeypatch.setenv("LGBM_AMD_HOST_METRICS", "1")
     host = run()
-    assert set(dev) == set(host) and len(dev) >= 2
+    assert set(dev) == set(host) and len(dev) >= (1 if task == "aucmu_weighted" else 2)
     for name in dev:
         np.testing.assert_allclose(dev[name], host[name], rtol=1e-9, atol=1e-12, err_msg=name)
 
