@@ -230,7 +230,7 @@ __device__ __forceinline__ int StepBlocks(const KArgs& a, int parent_count) {
 // on, whose tree graph has no reduce kernel -- is summed by the split scan itself (the
 // reduce kernel skips it); data-parallel training always reduces (the collectives need it)
 __device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk, int split) {
-  return !a.p.data_parallel && (nblk <= kReduceChunk || split >= a.p.direct_from_split);
+  return !a.p.data_parallel && (nblk <= kDirectChunk || split >= a.p.direct_from_split);
 }
 
 // (g, h) of partial word(s) v: packed (g in the signed high half, h in the low half) or wide

@@ -151,6 +151,12 @@ constexpr int kSparsePerThread = 4;    // row-sparse gathers: entries per thread
 constexpr int kHistMinRows = 1024;     // rows per histogram row block, lower bound
 constexpr int kHistRowsCap = 16384;    // rows per row block, upper bound (packed fixed point)
 constexpr int kReduceChunk = 16;       // partial histograms summed per reduce thread
+#ifndef LGBM_DIRECT_CHUNK
+#define LGBM_DIRECT_CHUNK 16
+#endif
+// a step histogram of at most this many row blocks is summed by the split scan itself, every
+// block's partial of a bin loaded in one round of independent loads (no reduce kernel)
+constexpr int kDirectChunk = LGBM_DIRECT_CHUNK;
 constexpr int kPartThreads = 1024;
 constexpr int kSplitRows = 4;          // k_split: rows per thread of a sub-tile
 constexpr int kSplitSub = kPartThreads * kSplitRows;

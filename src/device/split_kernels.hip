@@ -1071,17 +1071,17 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
         h = static_cast<long long>(sh.s_red[2 * i + 1]);
       } else if (nblk_direct >= 0) {
         // small leaf: sum the few per-block partials here (k_hist_reduce skipped them),
-        // chunks of kReduceChunk independent loads in flight
-        for (int k0 = 0; k0 < nblk_direct; k0 += kReduceChunk) {
-          unsigned long long v0[kReduceChunk], v1[kReduceChunk];
+        // chunks of kDirectChunk independent loads in flight
+        for (int k0 = 0; k0 < nblk_direct; k0 += kDirectChunk) {
+          unsigned long long v0[kDirectChunk], v1[kDirectChunk];
 #pragma unroll
-          for (int k = 0; k < kReduceChunk; ++k) {
+          for (int k = 0; k < kDirectChunk; ++k) {
             const unsigned long long* q = part + (k0 + k) * pstride + static_cast<size_t>(units) * i;
             v0[k] = k0 + k < nblk_direct ? q[0] : 0ull;
             v1[k] = (k0 + k < nblk_direct && units == 2) ? q[1] : 0ull;
           }
 #pragma unroll
-          for (int k = 0; k < kReduceChunk; ++k) {
+          for (int k = 0; k < kDirectChunk; ++k) {
             long long pgv, phv;
             UnpackPartial(v0[k], v1[k], units, &pgv, &phv);
             g += pgv;
