@@ -30,10 +30,11 @@ namespace {
 
 constexpr int kPartWaves = kPartThreads / kWave;
 static_assert(kSplitRows * kPartWaves == kWave, "k_split: one wave lane per (row slot, wave) piece");
-#ifndef LGBM_GATHER_ROWS
-#define LGBM_GATHER_ROWS 2
-#endif
-constexpr int kGatherRows = LGBM_GATHER_ROWS;  // phase B: independent row gathers per thread
+// phase B: independent row gathers per thread and pass (k_split's GR).  Narrow rows (<= 8
+// words per tile) gather 2 (fewer VGPRs, ~150 rows per pass already), wide rows 8 (few rows
+// per pass): A/B on the headline 10M x 28 (7 words) 8/4/2/1 rows = 4.39/4.28/4.21/4.26
+// ms/iter; Yahoo 175 words 2 vs 8 rows = 23.3 vs 21.2, MS-LTR 35 words 19.1 vs 18.3
+constexpr int kGatherNarrow = 2, kGatherWide = 8, kGatherNarrowMaxWords = 8;
 
 __device__ __forceinline__ int ValidInWave(int valid, int k, int w) {
   return min(kWave, max(0, valid - k * kPartThreads - w * kWave));
@@ -41,7 +42,7 @@ __device__ __forceinline__ int ValidInWave(int valid, int k, int w) {
 
 }  // namespace
 
-template <int GPW, int UNITS, bool HIST>
+template <int GPW, int UNITS, bool HIST, int GR>
 __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
   extern __shared__ unsigned long long lds[];  // [UNITS * tile_bins] histogram, then the row list
   __shared__ uint32_t cat_bits[kMaxCatWords];
@@ -207,34 +208,34 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
         const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
         const float2* gh = reinterpret_cast<const float2*>(a.gh);
         const int64_t wpr = a.words_per_row;
-        for (int j0 = t.rs; j0 < nh; j0 += kGatherRows * t.rpp) {
-          int rr[kGatherRows];
+        for (int j0 = t.rs; j0 < nh; j0 += GR * t.rpp) {
+          int rr[GR];
 #pragma unroll
-          for (int k = 0; k < kGatherRows; ++k) {
+          for (int k = 0; k < GR; ++k) {
             const int j = j0 + k * t.rpp;
             rr[k] = j < nh ? rowlist[j] : -1;
           }
-          float2 v[kGatherRows];
+          float2 v[GR];
           if constexpr (GPW == kSparseGPW) {
 #pragma unroll
-            for (int k = 0; k < kGatherRows; ++k) v[k] = gh[rr[k] >= 0 ? rr[k] : 0];
+            for (int k = 0; k < GR; ++k) v[k] = gh[rr[k] >= 0 ? rr[k] : 0];
             if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
-            AddSparseRows<kGatherRows, UNITS>(a, lds, t, rr, v);
+            AddSparseRows<GR, UNITS>(a, lds, t, rr, v);
           } else {
-            uint32_t wd[kGatherRows];
+            uint32_t wd[GR];
 #pragma unroll
-            for (int k = 0; k < kGatherRows; ++k) {
+            for (int k = 0; k < GR; ++k) {
               const int x = rr[k] >= 0 ? rr[k] : 0;
               v[k] = gh[x];
               wd[k] = rr[k] >= 0 ? bins32[x * wpr + wi] : 0u;  // word 0: every bin skipped
             }
             if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
 #pragma unroll
-            for (int k = 0; k < kGatherRows; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
+            for (int k = 0; k < GR; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
           }
           if (loc_sums && t.q == 0) {
 #pragma unroll
-            for (int k = 0; k < kGatherRows; ++k) {
+            for (int k = 0; k < GR; ++k) {
               if (rr[k] >= 0) {
                 loc_g += __float2ll_rn(v[k].x * t.sg);
                 loc_h += __float2ll_rn(v[k].y * t.sh);
@@ -282,40 +283,52 @@ static void AllowLds(K kernel, int bytes) {
   }
 }
 
-void SplitStep(const KArgs& a, hipStream_t s, bool reduce) {
+template <int GR>
+static void LaunchSplit(const KArgs& a, hipStream_t s) {
   const dim3 grid(a.split_grid, a.hist_tiles);
   const size_t lds = SplitLds(a);
 
   if (a.sp_ptr != nullptr) {
-    if (a.hist_units == 1) hipLaunchKernelGGL((k_split<kSparseGPW, 1, true>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_split<kSparseGPW, 2, true>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.hist_units == 1) hipLaunchKernelGGL((k_split<kSparseGPW, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_split<kSparseGPW, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
   } else if (a.hist_units == 1) {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 1, true>), grid, dim3(kPartThreads), lds, s, a);
-    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 1, true>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_split<0, 1, true>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_split<0, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
   } else {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 2, true>), grid, dim3(kPartThreads), lds, s, a);
-    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 2, true>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_split<0, 2, true>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_split<0, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
   }
+}
+
+void SplitStep(const KArgs& a, hipStream_t s, bool reduce) {
+  if (a.sp_ptr != nullptr || a.tile_words <= kGatherNarrowMaxWords) LaunchSplit<kGatherNarrow>(a, s);
+  else LaunchSplit<kGatherWide>(a, s);
   if (reduce) LaunchReduce<1>(a, s);
 }
 
+template <int GR>
+static void AllowSplitLds(int mx) {
+  AllowLds(k_split<4, 1, true, GR>, mx);
+  AllowLds(k_split<2, 1, true, GR>, mx);
+  AllowLds(k_split<4, 2, true, GR>, mx);
+  AllowLds(k_split<2, 2, true, GR>, mx);
+  AllowLds(k_split<0, 1, true, GR>, mx);
+  AllowLds(k_split<0, 2, true, GR>, mx);
+  AllowLds(k_split<kSparseGPW, 1, true, GR>, mx);
+  AllowLds(k_split<kSparseGPW, 2, true, GR>, mx);
+}
+
 void PrepareSplitKernels(int mx) {
-  AllowLds(k_split<4, 1, true>, mx);
-  AllowLds(k_split<2, 1, true>, mx);
-  AllowLds(k_split<4, 2, true>, mx);
-  AllowLds(k_split<2, 2, true>, mx);
-  AllowLds(k_split<0, 1, true>, mx);
-  AllowLds(k_split<0, 2, true>, mx);
-  AllowLds(k_split<kSparseGPW, 1, true>, mx);
-  AllowLds(k_split<kSparseGPW, 2, true>, mx);
+  AllowSplitLds<kGatherNarrow>(mx);
+  AllowSplitLds<kGatherWide>(mx);
 }
 
 void Partition(const KArgs& a, hipStream_t s) {
   // one workgroup per CU: at most ~num_data / (kSplitSub * CUs) tile reservations each
   const int grid = std::max(1, std::min((a.num_data + kSplitSub - 1) / kSplitSub, NumCUs()));
-  hipLaunchKernelGGL((k_split<4, 1, false>), dim3(grid), dim3(kPartThreads), 0, s, a);
+  hipLaunchKernelGGL((k_split<4, 1, false, kGatherNarrow>), dim3(grid), dim3(kPartThreads), 0, s, a);
 }
 
 }  // namespace dev
