@@ -87,10 +87,60 @@ __device__ __forceinline__ bool GoesLeft(const SplitRule& r, const uint32_t* cat
   return bin <= static_cast<uint32_t>(r.threshold);
 }
 
+// Wave-wide prefix sums and sums over DPP lane moves (row_shr within rows of 16 lanes, then
+// row_bcast:15 / row_bcast:31 across rows): six VALU-issued moves per 32-bit half instead of
+// six ds_bpermute round trips through the LDS crossbar.  Every lane of the wave must be active.
+#ifndef LGBM_DPP_SCAN
+#define LGBM_DPP_SCAN 1
+#endif
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ int DppI32(int v) {
+  // (disabled rows and lanes without a source read 0: the identity of the sums)
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, 0xf, true);
+}
+template <int CTRL, int ROW_MASK = 0xf, typename T>
+__device__ __forceinline__ T DppMove(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, DppI32<CTRL, ROW_MASK>(__builtin_bit_cast(int, v)));
+  } else {
+    static_assert(sizeof(T) == 8, "DppMove: 4- or 8-byte values");
+    const long long x = __builtin_bit_cast(long long, v);
+    const int lo = DppI32<CTRL, ROW_MASK>(static_cast<int>(x));
+    const int hi = DppI32<CTRL, ROW_MASK>(static_cast<int>(x >> 32));
+    return __builtin_bit_cast(T, static_cast<long long>((static_cast<unsigned long long>(static_cast<unsigned>(hi)) << 32) |
+                                                        static_cast<unsigned>(lo)));
+  }
+}
+template <typename T>
+__device__ __forceinline__ T WavePrefixInclDpp(T v) {
+  v += DppMove<0x111>(v);       // row_shr:1
+  v += DppMove<0x112>(v);       // row_shr:2
+  v += DppMove<0x114>(v);       // row_shr:4
+  v += DppMove<0x118>(v);       // row_shr:8
+  v += DppMove<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += DppMove<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+template <typename T>
+__device__ __forceinline__ T WaveLane63(T v) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+  } else {
+    const long long x = __builtin_bit_cast(long long, v);
+    const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x), 63));
+    const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x >> 32), 63));
+    return __builtin_bit_cast(T, static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T WaveSum(T v) {
+#if LGBM_DPP_SCAN
+  return WaveLane63(WavePrefixInclDpp(v));
+#else
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   return v;
+#endif
 }
 
 template <typename T>
@@ -104,12 +154,16 @@ __device__ __forceinline__ T WaveSuffixIncl(T v) {
 }
 template <typename T>
 __device__ __forceinline__ T WavePrefixIncl(T v) {
+#if LGBM_DPP_SCAN
+  return WavePrefixInclDpp(v);
+#else
   const int lane = threadIdx.x & 63;
   for (int o = 1; o < 64; o <<= 1) {
     T t = __shfl_up(v, o, kWave);
     if (lane >= o) v += t;
   }
   return v;
+#endif
 }
 
 // block-wide sum (every thread gets the result); sh needs blockDim/64 entries
