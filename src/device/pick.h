@@ -128,6 +128,7 @@ struct PickLds {
   int s, fresh, sm, lg;        // the step's bookkeeping (nsplit, fresh sides, smaller / larger leaf)
   int sm_frow, lg_frow;
   int win_feature;             // the winner's inner feature (-1: none)
+  int new_frow;                // splittable row of leaf s + 1 (the new leaf of the next split)
   FeatureBest fb[2];           // the fresh children's winning per-feature results
   uint32_t fcat[2][kMaxCatWords];
   DeviceSplit fsplit[2];       // ... as split records
@@ -219,6 +220,9 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
   // and leaves 0..s; then the two per-side feature argmaxes and the argmax over the other
   // leaves in one interleaved reduction; the fresh children join the leaf argmax last (the
   // order is total, so folding them in afterwards picks the same leaf as one pass)
+  // the next new leaf's splittable row (leaf s + 1: untouched by the bookkeeping), with the
+  // pick's other loads instead of after the pick
+  const int pre_frow = (lane == 0 && s + 1 < L) ? a.leaves[s + 1].frow : 0;
   double lgv = -INFINITY;  // this lane's leaf (l = lane, the common case s < 64), loaded first
   int lrf = -1, lfv = -1;
   if (lane <= s && lane < L) {
@@ -329,6 +333,7 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
     ArgTake(&win, f);
   }
   if (lane != 0) return;
+  pl->new_frow = pre_frow;
   const double g = win.g;
   const int leaf = win.idx, wf = win.x;
   if (a.ktrace != nullptr && s - 1 >= 0) {
@@ -426,14 +431,17 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     }
     __syncthreads();
     PickTrace(a, ts, kTrPick3);
-    // 4. conversions and the children's statistics (thread 0, LDS only)
+    // 4. conversions (lane k: fresh side k, lane 2: the forced split -- side by side in one
+    //    wave) and the children's statistics (thread 0), LDS only
+    if (tid < fresh) {
+      if (pk->fresh_idx[tid] >= 0) ToDeviceSplit(pl->fb[tid], pl->fcat[tid], &pl->fsplit[tid]);
+      else NoSplit(&pl->fsplit[tid]);
+    } else if (tid == 2 && pk->forced) {
+      ToDeviceSplit(pl->ffb, pl->ffcat, &pk->split);
+    }
+    __syncthreads();
     if (tid == 0) {
-      for (int side = 0; side < fresh; ++side) {
-        if (pk->fresh_idx[side] >= 0) ToDeviceSplit(pl->fb[side], pl->fcat[side], &pl->fsplit[side]);
-        else NoSplit(&pl->fsplit[side]);
-      }
       if (win_fresh) pk->split = pl->fsplit[leaf == pl->sm ? 0 : 1];
-      if (pk->forced) ToDeviceSplit(pl->ffb, pl->ffcat, &pk->split);
       const DeviceSplit& sp = pk->split;
       const Leaf& P = pk->P;
       const int s = pk->s, nl = s + 1;
@@ -478,12 +486,9 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     //    mask of the split feature (the parent's splittable row is snapshot by k_split)
     const DeviceSplit& sp = pk->split;
     const int s = pk->s, nl = s + 1;
-    int new_frow = 0;
+    const int new_frow = pl->new_frow;
     uint32_t fmask = 0xffffffffu;
-    if (tid == 0) {
-      new_frow = a.leaves[nl].frow;
-      if (a.feat_icmask != nullptr) fmask = a.feat_icmask[sp.feature];
-    }
+    if (tid == 0 && a.feat_icmask != nullptr) fmask = a.feat_icmask[sp.feature];
     // ---- stores only from here
     // the fresh children's bests become part of the per-leaf table
     for (int side = 0; side < fresh; ++side) {
