@@ -317,6 +317,7 @@ void GPUTreeLearner::UploadData() {
   // scale does not depend on the number of rows; wide blocks are unbounded
   root_grid_ = dev::HistGridBlocks();
   split_grid_ = std::max(1, dev::HistGridBlocks() / 2);
+  if (const char* e = std::getenv("LGBM_AMD_SPLIT_GRID")) split_grid_ = std::max(1, std::atoi(e));
   rows_cap_ = hist_units_ == 1 ? dev::kHistRowsCap : (1 << 30);
   if (const char* e = std::getenv("LGBM_AMD_HIST_ROWS_CAP")) {
     if (hist_units_ == 1) rows_cap_ = std::max(dev::kHistMinRows, std::min(dev::kHistRowsCap, std::atoi(e)));
