@@ -28,7 +28,10 @@ namespace dev {
 
 namespace {
 
-constexpr int kRowsInFlight = 8;  // independent row gathers per thread
+#ifndef LGBM_ROOT_ROWS
+#define LGBM_ROOT_ROWS 8
+#endif
+constexpr int kRowsInFlight = LGBM_ROOT_ROWS;  // independent row gathers per thread
 
 template <int MODE>
 __device__ __forceinline__ void HistRowSet(const KArgs& a, int* begin, int* count, const int32_t** src) {

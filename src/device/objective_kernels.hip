@@ -129,7 +129,10 @@ __device__ __forceinline__ bool RowGrad(const GradArgs& ga, int64_t i, int64_t n
   return true;
 }
 
-constexpr int kGradRows = 4;  // rows per thread per iteration (independent loads in flight)
+#ifndef LGBM_GRAD_ROWS
+#define LGBM_GRAD_ROWS 4
+#endif
+constexpr int kGradRows = LGBM_GRAD_ROWS;  // rows per thread per iteration (independent loads in flight)
 
 __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
   const int64_t n = ga.num_data;
