@@ -174,6 +174,12 @@ class Dataset {
   // copy (built on first use), private histograms merged over bin blocks
   void ConstructHistograms(const std::vector<int8_t>& group_used, const data_size_t* indices, data_size_t n,
                            const score_t* grad, const score_t* hess, hist_t* hist, bool row_wise = false) const;
+  // drop the row-major copy (col-wise threading chosen)
+  void ReleaseRowMajor() const {
+    std::vector<uint8_t>().swap(row_major_);
+    std::vector<std::vector<hist_t>>().swap(row_bufs_);
+    row_stride_ = 0;
+  }
   // reconstruct the most-frequent-bin entry of a feature slice from the leaf totals
   void FixHistogram(int inner, double sum_grad, double sum_hess, hist_t* feature_hist) const;
 

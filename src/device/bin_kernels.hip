@@ -185,6 +185,18 @@ std::vector<char> DeviceBinDenseMatrix(Dataset* ds, const void* data, bool is_f6
   BinGroup* d_groups = nullptr;
   BinFeat* d_feats = nullptr;
   double* d_ub = nullptr;
+  struct Release {  // device buffers and the caller's device, also when a HIP call throws
+    void** p[5];
+    int dev;
+    ~Release() {
+      for (void** q : p) {
+        if (*q != nullptr) (void)hipFree(*q);
+      }
+      (void)hipSetDevice(dev);
+    }
+  } release{{&d_x, reinterpret_cast<void**>(&d_out), reinterpret_cast<void**>(&d_groups),
+             reinterpret_cast<void**>(&d_feats), reinterpret_cast<void**>(&d_ub)},
+            prev};
   BINCHECK(hipMalloc(&d_x, esz * static_cast<size_t>(chunk) * ncol));
   BINCHECK(hipMalloc(reinterpret_cast<void**>(&d_out), static_cast<size_t>(out_row_bytes * chunk)));
   BINCHECK(hipMalloc(reinterpret_cast<void**>(&d_groups), sizeof(BinGroup) * groups.size()));
@@ -224,12 +236,6 @@ std::vector<char> DeviceBinDenseMatrix(Dataset* ds, const void* data, bool is_f6
                          static_cast<size_t>(rows) * fg.bin_bytes, hipMemcpyDeviceToHost));
     }
   }
-  (void)hipFree(d_x);
-  (void)hipFree(d_out);
-  (void)hipFree(d_groups);
-  (void)hipFree(d_feats);
-  (void)hipFree(d_ub);
-  (void)hipSetDevice(prev);
   for (const auto& F : feats) done_col[F.col] = 1;
   return done_col;
 }

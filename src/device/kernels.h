@@ -150,7 +150,10 @@ constexpr int kHistThreads = 1024;     // histogram workgroup (16 waves)
 constexpr int kSparsePerThread = 4;    // row-sparse gathers: entries per thread and row loaded up front
 constexpr int kHistMinRows = 1024;     // rows per histogram row block, lower bound
 constexpr int kHistRowsCap = 16384;    // rows per row block, upper bound (packed fixed point)
-constexpr int kReduceChunk = 16;       // partial histograms summed per reduce thread
+#ifndef LGBM_REDUCE_CHUNK
+#define LGBM_REDUCE_CHUNK 16
+#endif
+constexpr int kReduceChunk = LGBM_REDUCE_CHUNK;  // partial histograms summed per reduce thread
 #ifndef LGBM_DIRECT_CHUNK
 #define LGBM_DIRECT_CHUNK 16
 #endif

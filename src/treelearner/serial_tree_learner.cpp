@@ -329,6 +329,7 @@ int SerialTreeLearner::ChooseHistogramThreading(const std::vector<int8_t>& group
   data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, LeafHist(smaller_slot_).data(), true);
   const double t2 = common::NowSeconds();
   const bool row = (t2 - t1) < (t1 - t0);
+  if (!row) data_->ReleaseRowMajor();
   Log::Info("Auto-choosing %s-wise multi-threading, the overhead of testing was %f seconds.\n"
             "You can set `force_%s_wise=true` to remove the overhead.",
             row ? "row" : "col", t2 - t0, row ? "row" : "col");
