@@ -151,7 +151,7 @@ constexpr int kSparsePerThread = 4;    // row-sparse gathers: entries per thread
 constexpr int kHistMinRows = 1024;     // rows per histogram row block, lower bound
 constexpr int kHistRowsCap = 16384;    // rows per row block, upper bound (packed fixed point)
 #ifndef LGBM_REDUCE_CHUNK
-#define LGBM_REDUCE_CHUNK 16
+#define LGBM_REDUCE_CHUNK 32
 #endif
 constexpr int kReduceChunk = LGBM_REDUCE_CHUNK;  // partial histograms summed per reduce thread
 #ifndef LGBM_DIRECT_CHUNK
