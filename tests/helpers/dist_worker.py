@@ -3,6 +3,7 @@
   RANK=r WORLD_SIZE=n MASTER_ADDR=127.0.0.1 MASTER_PORT=p python dist_worker.py LEARNER OUT_DIR
 Writes OUT_DIR/model_<rank>.txt and OUT_DIR/pred_<rank>.npy (predictions on the full data).
 """
+import json
 import os
 import sys
 
@@ -32,6 +33,7 @@ def main():
     params = {"objective": "binary", "num_leaves": 15, "learning_rate": 0.1, "verbose": -1,
               "tree_learner": learner, "num_machines": world, "min_data_in_leaf": 20, "seed": 3,
               "deterministic": True, "device_type": device}
+    params.update(json.loads(os.environ.get("LGBM_TEST_PARAMS", "{}")))  # extra parameters of a test
     if learner in ("data", "voting"):
         # pre-partitioned rows: every rank holds its own shard
         idx = np.arange(rank, X.shape[0], world)

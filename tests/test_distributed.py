@@ -2,6 +2,7 @@
 127.0.0.1): data-parallel (reduce-scatter of histograms), voting-parallel (PV-Tree) and
 feature-parallel learners (reference src/treelearner/{data,voting,feature}_parallel_tree_learner.cpp).
 Every rank must end with the same model, of the expected quality."""
+import json
 import os
 import socket
 import subprocess
@@ -29,22 +30,23 @@ def _free_port():
 _RENDEZVOUS_ERRORS = ("Address already in use", "EADDRINUSE", "Connection refused", "connect()", "Socket Timeout")
 
 
-def _run(learner, tmp_path, world=2, device="cpu"):
+def _run(learner, tmp_path, world=2, device="cpu", extra=None):
     # the free port can be taken between the probe and the rendezvous: retry on that only
     for attempt in range(3):
         try:
-            return _run_once(learner, tmp_path, world, device)
+            return _run_once(learner, tmp_path, world, device, extra)
         except AssertionError as e:
             if attempt == 2 or not any(m in str(e) for m in _RENDEZVOUS_ERRORS):
                 raise
 
 
-def _run_once(learner, tmp_path, world, device):
+def _run_once(learner, tmp_path, world, device, extra=None):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), OMP_NUM_THREADS="2", LGBM_TEST_DEVICE=device)
+                   MASTER_PORT=str(port), OMP_NUM_THREADS="2", LGBM_TEST_DEVICE=device,
+                   LGBM_TEST_PARAMS=json.dumps(extra or {}))
         if device == "cpu":
             env["HIP_VISIBLE_DEVICES"] = ""
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "helpers", "dist_worker.py"), learner,
@@ -73,6 +75,16 @@ def test_parallel_learners_agree_across_ranks(learner, tmp_path):
     models, preds = _run(learner, tmp_path)
     assert _trees(models[0]) == _trees(models[1])
     np.testing.assert_array_equal(preds[0], preds[1])
+    X, y = make_data()
+    assert roc_auc_score(y, preds[0]) > 0.8
+
+
+@pytest.mark.parametrize("learner", ["data", "voting"])
+def test_row_wise_histograms_and_bounded_pool_across_ranks(learner, tmp_path):
+    """The reference fork's headline setting (train.conf: data-parallel, force_row_wise=true)
+    with a bounded histogram pool: ranks agree and the fit holds."""
+    models, preds = _run(learner, tmp_path, extra={"force_row_wise": True, "histogram_pool_size": 0.01})
+    assert _trees(models[0]) == _trees(models[1])
     X, y = make_data()
     assert roc_auc_score(y, preds[0]) > 0.8
 
