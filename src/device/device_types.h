@@ -71,6 +71,11 @@ struct Params {
 };
 
 // per-leaf state
+// interaction-constraint sets of a leaf / feature (bit k: constraint k; up to 64 constraints)
+using IcMask = uint64_t;
+constexpr IcMask kIcAll = ~IcMask{0};
+constexpr int kMaxIcConstraints = 64;
+
 struct Leaf {
   int32_t begin;         // local index range in the partition array
   int32_t count;         // local rows
@@ -79,7 +84,7 @@ struct Leaf {
   int32_t slot;          // histogram slot
   int32_t buf;           // which index buffer (KArgs::idx / tmp) holds the leaf's rows
   int32_t frow;          // row of KArgs::splittable (kept across trees)
-  uint32_t icmask;       // interaction constraints consistent with the leaf's branch (bit k: constraint k)
+  IcMask icmask;         // interaction constraints consistent with the leaf's branch (bit k: constraint k)
   double sum_g, sum_h, output;
   double lsum_g, lsum_h;  // voting-parallel: this rank's (local) sums of the leaf's rows
   double cmin, cmax;  // monotone constraint range
@@ -91,7 +96,7 @@ struct ChildStats {
   double sum_g, sum_h, output, cmin, cmax;
   int32_t global_count, depth, slot, leaf;
   int32_t frow;        // splittable row the child's scan writes
-  uint32_t icmask;     // Leaf::icmask
+  IcMask icmask;       // Leaf::icmask
 };
 
 // the split being applied, as chosen by the partition kernel's pick

@@ -95,7 +95,7 @@ struct KArgs {
   const int32_t* cat_list;   // [Params::has_cat] the categorical features
   // interaction constraints (<= 32): bit k set iff constraint k holds the feature, or null.
   // A leaf may split on f iff (Leaf::icmask & feat_icmask[f]) != 0 (ColSampler::GetByNode)
-  const uint32_t* feat_icmask;  // [num_features]
+  const IcMask* feat_icmask;  // [num_features]
   // extra_trees: each feature's generator state at the tree's start (FeatureMeta::rand) and the
   // running count of its draws, one row per split step (row 0: the root scan, row s + 1: after
   // step s; rows of steps not run stay 0), or null

@@ -99,7 +99,7 @@ __global__ void k_tree_begin(KArgs a) {
     lf.lsum_g = lf.lsum_h = 0.0;
     lf.cmin = -DBL_MAX;
     lf.cmax = DBL_MAX;
-    lf.icmask = 0xffffffffu;  // the root may use every constraint
+    lf.icmask = kIcAll;  // the root may use every constraint
     a.leaves[l] = lf;
     a.best[l].gain = -INFINITY;
     a.best[l].feature = -1;

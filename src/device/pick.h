@@ -133,7 +133,7 @@ struct PickLds {
   uint32_t fcat[2][kMaxCatWords];
   DeviceSplit fsplit[2];       // ... as split records
   ChildStats lc, rc;
-  uint32_t icm;
+  IcMask icm;
   FeatureBest ffb;  // the forced split's record and category set
   uint32_t ffcat[kMaxCatWords];
 };
@@ -487,7 +487,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     const DeviceSplit& sp = pk->split;
     const int s = pk->s, nl = s + 1;
     const int new_frow = pl->new_frow;
-    uint32_t fmask = 0xffffffffu;
+    IcMask fmask = kIcAll;
     if (tid == 0 && a.feat_icmask != nullptr) fmask = a.feat_icmask[sp.feature];
     // ---- stores only from here
     // the fresh children's bests become part of the per-leaf table
@@ -526,7 +526,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     CopyWords(&pk->F, &st->cs.feat, tid, nthr);
     if (tid == 0) {
       const Leaf& P = pk->P;
-      const uint32_t icm = P.icmask & fmask;  // both children keep the constraints that hold the feature
+      const IcMask icm = P.icmask & fmask;  // both children keep the constraints that hold the feature
       ChildStats lc = pl->lc, rc = pl->rc;
       lc.icmask = rc.icmask = icm;
       rc.frow = new_frow;

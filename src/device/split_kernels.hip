@@ -731,10 +731,10 @@ __device__ __forceinline__ uint32_t LcgSkip(uint32_t x, int k) {
 // extra_trees: whether the host learner scans f at node mi (the feature is used by the tree,
 // its parent could split on it, the node samples it and its constraints allow it) and so
 // draws FeatureMeta::rand.NextInt(0, num_bin - 2) (split_finder.cpp FindNumerical)
-__device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, int mi, uint32_t icmask, bool gate) {
+__device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, int mi, IcMask icmask, bool gate) {
   if (!gate || F.num_bin - 2 <= 0) return 0;
   if (a.node_mask != nullptr && !a.node_mask[static_cast<size_t>(mi) * a.p.num_features + f]) return 0;
-  if (a.feat_icmask != nullptr && (icmask & a.feat_icmask[f]) == 0u) return 0;
+  if (a.feat_icmask != nullptr && (icmask & a.feat_icmask[f]) == 0) return 0;
   return 1;
 }
 
@@ -883,7 +883,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     const int nf = a.p.num_features;
     const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * nf + f];
     const bool gate = tree_used && parent_ok && !skip;
-    const uint32_t icm = ROOT ? 0xffffffffu : cl.icmask;  // both children carry the same constraints
+    const IcMask icm = ROOT ? kIcAll : cl.icmask;  // both children carry the same constraints
     const int d0 = XtDraws(a, F, f, mi_base, icm, gate);
     const int d1 = ROOT ? 0 : XtDraws(a, F, f, mi_base + 1, icm, gate);
     if (side == 0 && tid == 0) a.xt_cum[static_cast<size_t>(ROOT ? 0 : s + 1) * nf + f] = prev + d0 + d1;
@@ -977,7 +977,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   if (CAT && !F.is_cat) return;       // (voting global scan: an elected numerical feature)
   // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
   // here but keeps its histogram and its splittable flag
-  if (a.feat_icmask != nullptr && ((ROOT ? 0xffffffffu : cl.icmask) & a.feat_icmask[f]) == 0u) used = 0;
+  if (a.feat_icmask != nullptr && ((ROOT ? kIcAll : cl.icmask) & a.feat_icmask[f]) == 0) used = 0;
   int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : sd.frow) * a.p.num_features;
   FeatureBest* fb_out = &a.feat_best[FeatBestIndex(a, side, f)];
   if (tree_used && !parent_ok) {

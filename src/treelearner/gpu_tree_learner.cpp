@@ -593,20 +593,20 @@ void GPUTreeLearner::SetupOwnership() {
 }
 
 // interaction constraints as per-feature constraint bitmasks (device-resident growth
-// supports up to 32 constraints, see DecideMode); rebuilt when the config changes
+// supports up to 64 constraints, see DecideMode); rebuilt when the config changes
 void GPUTreeLearner::UploadInteractionMasks() {
   const auto& ic = config_->interaction_constraints_vector;
   args_.feat_icmask = nullptr;
-  if (ic.empty() || ic.size() > 32) return;
-  std::vector<uint32_t> icm(std::max(1, num_features_), 0u);
+  if (ic.empty() || ic.size() > static_cast<size_t>(dev::kMaxIcConstraints)) return;
+  std::vector<dev::IcMask> icm(std::max(1, num_features_), 0);
   for (int f = 0; f < num_features_; ++f) {
     const int real = data_->RealFeatureIndex(f);
     for (size_t k = 0; k < ic.size(); ++k) {
-      if (std::find(ic[k].begin(), ic[k].end(), real) != ic[k].end()) icm[f] |= 1u << k;
+      if (std::find(ic[k].begin(), ic[k].end(), real) != ic[k].end()) icm[f] |= dev::IcMask{1} << k;
     }
   }
-  if (d_feat_icmask_ == nullptr) d_feat_icmask_ = Alloc<uint32_t>(icm.size());
-  HIPCHECK(hipMemcpy(d_feat_icmask_, icm.data(), sizeof(uint32_t) * icm.size(), hipMemcpyHostToDevice));
+  if (d_feat_icmask_ == nullptr) d_feat_icmask_ = Alloc<dev::IcMask>(icm.size());
+  HIPCHECK(hipMemcpy(d_feat_icmask_, icm.data(), sizeof(dev::IcMask) * icm.size(), hipMemcpyHostToDevice));
   args_.feat_icmask = d_feat_icmask_;
 }
 
@@ -696,10 +696,10 @@ void GPUTreeLearner::DecideMode() {
   // extra_trees: random numerical thresholds are drawn on the device (categorical draws
   // depend on the sorted-category scan: host-assisted then)
   if (config_->extra_trees && any_cat) dm = false;
-  // interaction constraints: on the device up to 32 constraints without per-node sampling
+  // interaction constraints: on the device up to 64 constraints without per-node sampling
   // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
   const auto& ic = config_->interaction_constraints_vector;
-  if (!ic.empty() && (ic.size() > 32 || config_->feature_fraction_bynode < 1.0)) dm = false;
+  if (!ic.empty() && (ic.size() > static_cast<size_t>(dev::kMaxIcConstraints) || config_->feature_fraction_bynode < 1.0)) dm = false;
   // intermediate monotone constraints re-bound (and re-scan) leaves all over the tree after a
   // split: the host loop does that between the device histogram builds
   if (config_->monotone_constraints_method == "intermediate" &&

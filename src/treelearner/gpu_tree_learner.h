@@ -185,7 +185,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int8_t* d_splittable_ = nullptr;      // [num_leaves][num_features] (KArgs::splittable)
   int8_t* d_parent_flags_ = nullptr;    // [num_features]
   int32_t* d_cat_list_ = nullptr;       // categorical features (KArgs::cat_list)
-  uint32_t* d_feat_icmask_ = nullptr;   // KArgs::feat_icmask
+  dev::IcMask* d_feat_icmask_ = nullptr;  // KArgs::feat_icmask
   std::vector<int8_t> h_node_mask_;     // (kept alive for the async upload)
   uint32_t* d_xt_base_ = nullptr;       // extra_trees: per-feature generator states, tree start
   int32_t* d_xt_cum_ = nullptr;         // extra_trees: draws per feature after each step

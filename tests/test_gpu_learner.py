@@ -364,13 +364,16 @@ def _branches(node, path=()):
     yield from _branches(node["right_child"], p)
 
 
-def test_interaction_constraints_device_resident(gpu_available, monkeypatch):
-    """Interaction constraints run in device-resident growth (per-leaf constraint bitmasks,
-    reference col_sampler.hpp:92-126): every root-to-leaf branch uses features of one
+@pytest.mark.parametrize("wide", [False, True], ids=["3_constraints", "40_constraints"])
+def test_interaction_constraints_device_resident(gpu_available, monkeypatch, wide):
+    """Interaction constraints run in device-resident growth (per-leaf 64-bit constraint
+    bitmasks, reference col_sampler.hpp:92-126): every root-to-leaf branch uses features of one
     constraint, and the trees equal the host-assisted learner's (same device histograms,
-    host split loop)."""
+    host split loop).  The wide case puts the useful constraints at bits 37-39."""
     X, y = _data(30000, seed=5)
     ic = [[0, 1, 2], [3, 5, 7], [1, 6]]
+    if wide:
+        ic = [[k % 8] for k in range(37)] + ic
     models = {}
     for mode in ("device", "host"):
         if mode == "host":
