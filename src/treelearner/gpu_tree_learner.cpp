@@ -316,7 +316,15 @@ void GPUTreeLearner::UploadData() {
   // packed (hist_units 1) row block holds at most kHistRowsCap rows, so the fixed-point
   // scale does not depend on the number of rows; wide blocks are unbounded
   root_grid_ = dev::HistGridBlocks();
-  split_grid_ = std::max(1, dev::HistGridBlocks() / 2);
+  // a split step launches split_grid x hist_tiles workgroups of 1024 threads: about one per
+  // CU in all, since the smaller leaves' blocks exit at once and their launches alone cost
+  // tens of microseconds (Epsilon, 8 column tiles: 37.4 ms/iter at 256 x 8, 28.7 at 32 x 8;
+  // Yahoo, 3 tiles: 20.8 at 256 x 3, 20.6 at 64 x 3 -- profiles/r02_v10_split_grid_wide.txt)
+  {
+    const int tiles = sparse_rows_ ? (total_bins_ + (hist_units_ == 1 ? 16384 : 8192) - 1) / (hist_units_ == 1 ? 16384 : 8192)
+                                   : (wpr + tile_words - 1) / tile_words;
+    split_grid_ = std::max(std::min(8, dev::HistGridBlocks() / 2), dev::HistGridBlocks() / 2 / std::max(1, tiles));
+  }
   if (const char* e = std::getenv("LGBM_AMD_SPLIT_GRID")) split_grid_ = std::max(1, std::atoi(e));
   rows_cap_ = hist_units_ == 1 ? dev::kHistRowsCap : (1 << 30);
   if (const char* e = std::getenv("LGBM_AMD_HIST_ROWS_CAP")) {
