@@ -154,36 +154,39 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
     nblk = HistBlocksFor(count, a.root_grid, a.hist_rows_cap, kHistMinRows);
     out = a.scratch;
   }
-  const int k0 = blockIdx.y * kReduceChunk;
-  if (k0 >= nblk) return;
+  if (static_cast<int>(blockIdx.y) * kReduceChunk >= nblk) return;
   const int bin = blockIdx.x * blockDim.x + threadIdx.x;
   const int nb = a.p.total_bins;
   if (bin >= nb) return;
   const size_t pstride = static_cast<size_t>(UNITS) * nb;
-  const unsigned long long* p = a.partials + k0 * pstride + static_cast<size_t>(UNITS) * bin;
-  const int kn = min(kReduceChunk, nblk - k0);
   long long g = 0, h = 0;
-  if (UNITS == 1) {
-    unsigned long long v[kReduceChunk];
+  // chunks blockIdx.y, + gridDim.y, ...: a few workgroup rows walk all the chunks (every
+  // launched workgroup costs launch time even when it exits at once)
+  for (int k0 = blockIdx.y * kReduceChunk; k0 < nblk; k0 += gridDim.y * kReduceChunk) {
+    const unsigned long long* p = a.partials + k0 * pstride + static_cast<size_t>(UNITS) * bin;
+    const int kn = min(kReduceChunk, nblk - k0);
+    if (UNITS == 1) {
+      unsigned long long v[kReduceChunk];
 #pragma unroll
-    for (int k = 0; k < kReduceChunk; ++k) v[k] = k < kn ? p[k * pstride] : 0ull;
+      for (int k = 0; k < kReduceChunk; ++k) v[k] = k < kn ? p[k * pstride] : 0ull;
 #pragma unroll
-    for (int k = 0; k < kReduceChunk; ++k) {
-      long long pg, ph;
-      UnpackPartial(v[k], 0ull, 1, &pg, &ph);
-      g += pg;
-      h += ph;
-    }
-  } else {
-    ulonglong2 v[kReduceChunk];
+      for (int k = 0; k < kReduceChunk; ++k) {
+        long long pg, ph;
+        UnpackPartial(v[k], 0ull, 1, &pg, &ph);
+        g += pg;
+        h += ph;
+      }
+    } else {
+      ulonglong2 v[kReduceChunk];
 #pragma unroll
-    for (int k = 0; k < kReduceChunk; ++k) {
-      v[k] = k < kn ? *reinterpret_cast<const ulonglong2*>(p + k * pstride) : make_ulonglong2(0ull, 0ull);
-    }
+      for (int k = 0; k < kReduceChunk; ++k) {
+        v[k] = k < kn ? *reinterpret_cast<const ulonglong2*>(p + k * pstride) : make_ulonglong2(0ull, 0ull);
+      }
 #pragma unroll
-    for (int k = 0; k < kReduceChunk; ++k) {
-      g += static_cast<long long>(v[k].x);
-      h += static_cast<long long>(v[k].y);
+      for (int k = 0; k < kReduceChunk; ++k) {
+        g += static_cast<long long>(v[k].x);
+        h += static_cast<long long>(v[k].y);
+      }
     }
   }
   const int pos = a.rs_pos != nullptr ? a.rs_pos[bin] : bin;  // owner-major layout (data-parallel)
@@ -238,9 +241,15 @@ static void LaunchHist(const KArgs& a, hipStream_t s) {
 
 }  // namespace
 
+#ifndef LGBM_REDUCE_ROWS
+#define LGBM_REDUCE_ROWS 4
+#endif
+constexpr int kReduceRows = LGBM_REDUCE_ROWS;  // workgroup rows of a reduction (each walks chunks)
+
 template <int MODE>
 void LaunchReduce(const KArgs& a, hipStream_t s) {
-  const dim3 rgrid((a.p.total_bins + 255) / 256, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk);
+  const dim3 rgrid((a.p.total_bins + 255) / 256,
+                   std::min(kReduceRows, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk));
   if (a.hist_units == 1) hipLaunchKernelGGL((k_hist_reduce<MODE, 1>), rgrid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_hist_reduce<MODE, 2>), rgrid, dim3(256), 0, s, a);
 }
