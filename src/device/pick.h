@@ -239,11 +239,14 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
       const FeatureBest& fbv = a.feat_best[FeatBestIndex(a, side_of_lane, i)];
       const double cg = fbv.gain;
       const int crf = fbv.real_feature, cf = fbv.feature;
-      if (cf >= 0) {
-        ArgC& c = side_of_lane == 0 ? c0 : c1;
+      if (cf >= 0) {  // (no reference to c0 / c1 chosen at run time: it would put both in scratch)
+        ArgC c;
         c.g = cg;
         c.rf = crf;
         c.idx = i;
+        c.x = -1;
+        if (side_of_lane == 0) c0 = c;
+        else c1 = c;
       }
     }
   } else {
