@@ -1169,13 +1169,16 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   if (tid == 0) PublishRecord(fb_out, o);
 }
 
+#ifndef LGBM_FIND_WAVE_OCC
+#define LGBM_FIND_WAVE_OCC 4  // one-wave split scans: waves per SIMD the register budget allows
+#endif
 constexpr unsigned kFindFlatMax = 128;  // split-scan grids up to this size count arrivals on one counter
 
 // NT: threads per workgroup -- kFindThreads, or one wave (kWave) when every feature has at
 // most kWave stored bins (many narrow features: four times the workgroups in flight, and no
 // cross-wave steps in the scans)
 template <bool ROOT, int KIND, bool SIMPLE, int NT>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave ? 4 : 1))) void k_find(KArgs a) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave ? LGBM_FIND_WAVE_OCC : 1))) void k_find(KArgs a) {
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
   __shared__ FindShared<ROOT, KIND, NT> sh;
   __shared__ PickLds pl;
