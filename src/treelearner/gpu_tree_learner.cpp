@@ -330,7 +330,15 @@ void GPUTreeLearner::UploadData() {
   if (const char* e = std::getenv("LGBM_AMD_HIST_ROWS_CAP")) {
     if (hist_units_ == 1) rows_cap_ = std::max(dev::kHistMinRows, std::min(dev::kHistRowsCap, std::atoi(e)));
   }
-  blk_min_rows_ = 4096;
+  // rows per split row block, lower bound: 4096 for one column tile (headline 10M x 28), 2048
+  // for 2-5 tiles (Bosch 16.7 -> 16.0), 1024 from 6 (the split kernel's grid shrinks with the tiles, so smaller
+  // blocks keep its workgroups busy: Epsilon, 8 tiles, 4096/2048/1024 = 23.0/21.7/20.8 ms/iter;
+  // profiles/r02_v11_blk_min_rows_wide.txt)
+  {
+    const int tiles = sparse_rows_ ? (total_bins_ + (hist_units_ == 1 ? 16384 : 8192) - 1) / (hist_units_ == 1 ? 16384 : 8192)
+                                   : (wpr + tile_words - 1) / tile_words;
+    blk_min_rows_ = tiles >= 6 ? 1024 : tiles > 1 ? 2048 : 4096;
+  }
   if (const char* e = std::getenv("LGBM_AMD_BLK_MIN_ROWS")) blk_min_rows_ = std::max(256, std::atoi(e));
   const int hist_blocks = std::max({1, dev::HistBlocksFor(num_data_, root_grid_, rows_cap_, dev::kHistMinRows),
                                     dev::HistBlocksFor(num_data_, split_grid_, rows_cap_, blk_min_rows_)});
