@@ -69,6 +69,7 @@ class DeviceTreeLearner {
   struct TreeStats {
     bool device_mode = false;
     int splits = 0;
+    int rounds = 0;  // round growth: expansion rounds of the tree (0: one split per step)
     double collective_bytes = 0.0;
   };
   virtual TreeStats LastTreeStats() const { return TreeStats(); }

@@ -84,6 +84,7 @@ struct Leaf {
   int32_t slot;          // histogram slot
   int32_t buf;           // which index buffer (KArgs::idx / tmp) holds the leaf's rows
   int32_t frow;          // row of KArgs::splittable (kept across trees)
+  int32_t expanded;      // round growth: the leaf's best split was applied speculatively (ExpResult)
   IcMask icmask;         // interaction constraints consistent with the leaf's branch (bit k: constraint k)
   double sum_g, sum_h, output;
   double lsum_g, lsum_h;  // voting-parallel: this rank's (local) sums of the leaf's rows
@@ -158,6 +159,53 @@ struct SplitRecord {
   int32_t left_count, right_count;  // counts stored in the model (global)
   int32_t pad;
   DeviceSplit split;
+};
+
+// ---- round growth (speculative multi-leaf expansion, round_kernels.hip)
+// Leaf-wise growth applies one split at a time, but expanding a leaf -- partitioning its rows
+// by its best split, histogramming and scanning both children -- depends on that leaf's rows
+// only.  A round expands up to KArgs::round_k leaves at once (the current leaves of highest
+// gain); the planner then replays the sequential best-first order (reference
+// serial_tree_learner.cpp:152-202): it accepts the argmax leaf while its expansion is
+// computed and stops at the first one whose expansion is not, which the next round expands.
+// Expansions never accepted only cost work: histograms are exact integer sums, so the rows a
+// pending expansion reordered inside its leaf's range change nothing.
+constexpr int kMaxRoundExp = 16;  // leaves expanded per round, upper bound
+
+// one leaf being expanded by the current round (written by the planner)
+struct ExpPlan {
+  int32_t leaf;
+  int32_t part_begin, part_count, src_buf;
+  int32_t hist_left;             // the left child's rows are histogrammed (fewer by the estimate), else the right's
+  int32_t blk_off, nblk;         // the expansion's row blocks inside the round's partial histograms
+  int32_t slot_parent, slot_new;  // histogram slots: the subtracted child keeps the parent's, the histogrammed one is new
+  int32_t frow_parent;           // the leaf's splittable row (its children skip what it could not split)
+  int32_t frow_child[2];         // the children's rows (fresh rows)
+  Feature feat;                  // the split feature's record
+  DeviceSplit split;
+  ChildStats lr[2];              // left / right child as known from the split
+};
+
+// an expanded leaf's children (indexed by leaf id, valid while Leaf::expanded)
+struct ExpResult {
+  int32_t begin, count, buf;  // the leaf's rows (children: [begin, +total_left) left, the rest right) in buf
+  int32_t total_left;         // local rows that went left
+  ChildStats lr[2];
+};
+
+// per-tree control record of round growth
+struct Round {
+  int32_t done;       // tree finished: every later kernel of the tree exits
+  int32_t nsplit;     // splits accepted so far
+  int32_t nexp;       // expansions of the current round
+  int32_t round;      // index of the current round (reduce-buffer parity)
+  int32_t rpb;        // rows per row block of the current round
+  int32_t nblk;       // row blocks of the current round (all expansions)
+  int32_t next_slot, next_frow;  // next free histogram slot / splittable row
+  int32_t rounds;     // rounds planned (diagnostics)
+  int32_t accepted_max;  // most splits accepted by one round (diagnostics)
+  int32_t cur[kMaxRoundExp][2];  // partition cursors of each expansion: rows placed left / right
+  ExpPlan e[kMaxRoundExp];
 };
 
 }  // namespace dev

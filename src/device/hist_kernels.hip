@@ -256,6 +256,7 @@ void LaunchReduce(const KArgs& a, hipStream_t s) {
 template void LaunchReduce<1>(const KArgs&, hipStream_t);
 
 void PrepareSplitKernels(int max_lds);
+void PrepareRoundKernels(int max_lds);
 
 // dynamic LDS above 64 KiB must be enabled per kernel (outside any graph capture)
 void PrepareKernels() {
@@ -276,6 +277,7 @@ void PrepareKernels() {
   AllowLds(k_hist<2, kSparseGPW, 1>);
   AllowLds(k_hist<2, kSparseGPW, 2>);
   PrepareSplitKernels(MaxDynLds());
+  PrepareRoundKernels(MaxDynLds());
 }
 
 void HistRoot(const KArgs& a, hipStream_t s) { LaunchHist<0>(a, s); }

@@ -133,6 +133,18 @@ struct KArgs {
   int32_t vote_rank;
   int32_t* vote_list;
   long long* vote_hist;
+  // round growth (round_kernels.hip; null rd: one split per step): up to round_k leaves are
+  // expanded per round.  Their children's per-feature results go to feat_best rows 2j + lr,
+  // each child's best split to cbest[2 * leaf + lr] (category sets in cbest_cat); child_cnt
+  // holds each child's split-scan arrival counters ([2 * kMaxRoundExp][kFindSub], kFindSubStride
+  // apart); the reduced histogram of expansion j sits at scratch + (parity * round_k + j) * 2 *
+  // total_bins
+  Round* rd;
+  ExpResult* exres;        // [num_leaves]
+  FeatureBest* cbest;      // [num_leaves][2]
+  uint32_t* cbest_cat;     // [num_leaves][2][kMaxCatWords]
+  uint32_t* child_cnt;
+  int32_t round_k;
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)
@@ -206,6 +218,13 @@ void FindStep(const KArgs& a, hipStream_t s);
 // the step's bookkeeping and the next pick as a kernel of its own (distributed learners:
 // it runs after the per-feature results were gathered from every rank)
 void PickStep(const KArgs& a, hipStream_t s, bool root);
+// round growth (KArgs::rd): the root's pick and first plan (after FindRoot without a pick),
+// then per round the fused partition + histogram of every expansion, the reduction of their
+// large histograms, the children's split scans (+ each child's best split), and the plan
+// (replay of the best-first order, next expansions).  A finished tree's kernels exit at once.
+void RoundRootPlan(const KArgs& a, hipStream_t s);
+void RoundStep(const KArgs& a, hipStream_t s);
+size_t RoundPlanLds(int num_leaves);
 // voting-parallel: this rank's top-k proposals per leaf from the local scan (into its block
 // of vote_buf); after the allgather, the election and the elected features' local histograms
 // (into vote_hist, for the all-reduce); the global scan is FindRoot / FindStep with

@@ -88,7 +88,9 @@ __global__ void k_tree_begin(KArgs a) {
   const int L = a.p.num_leaves;
   for (int l = threadIdx.x; l < L; l += blockDim.x) {
     Leaf lf;
-    lf.frow = a.leaves[l].frow;  // splittable rows persist across trees
+    // splittable rows persist across trees; round growth hands out fresh rows from 0 (the root)
+    lf.frow = a.rd != nullptr ? (l == 0 ? 0 : -1) : a.leaves[l].frow;
+    lf.expanded = 0;
     lf.begin = 0;
     lf.count = l == 0 ? RootRows(a) : 0;
     lf.global_count = lf.count;
@@ -121,6 +123,19 @@ __global__ void k_tree_begin(KArgs a) {
     st->root_count = 0;
     st->cur_left = st->cur_right = 0;
     st->forced_abort = 0;
+    if (a.rd != nullptr) {
+      Round* rd = a.rd;
+      rd->done = 0;
+      rd->nsplit = 0;
+      rd->nexp = 0;
+      rd->round = 0;
+      rd->rpb = 0;
+      rd->nblk = 0;
+      rd->next_slot = 1;  // slot 0: the root
+      rd->next_frow = 1;  // row 0: the root
+      rd->rounds = 0;
+      rd->accepted_max = 0;
+    }
   }
   for (int k = threadIdx.x; k < a.forced_n; k += blockDim.x) {  // no stale forced results
     a.forced_best[k].gain = -INFINITY;

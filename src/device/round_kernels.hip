@@ -1,0 +1,1015 @@
+// Round growth: speculative multi-leaf expansion of leaf-wise trees (device_types.h Round).
+//
+// The reference grows a tree one split at a time (serial_tree_learner.cpp:152-202: argmax over
+// the leaves' best splits, split it, histogram + scan its children).  On the device every such
+// step is a chain of dependent kernels whose latency (~50 us) does not shrink with the leaf, so
+// a 63-leaf tree was 62 latency chains.  Expanding a leaf -- partitioning its rows by its best
+// split, histogramming and scanning both children -- depends on that leaf's rows only, so a
+// round expands the round_k current leaves of highest gain at once:
+//
+//   k_round_split   the fused partition + smaller-child histogram of every expansion; the
+//                   round's rows are dealt out in row blocks of one common size, each block
+//                   belongs to one expansion (partition_kernels.hip k_split, per expansion)
+//   k_round_reduce  exact int64 sums of the partials of expansions with many row blocks
+//   k_round_find    split scans of both children of every expansion, grid (features, 2 x
+//                   round_k); the last workgroup of each child folds its per-feature results
+//                   into the child's best split (cbest)
+//   k_round_plan    one workgroup replays the sequential best-first order over the leaves:
+//                   while the argmax leaf is expanded its split is accepted (split record,
+//                   children become leaves 'leaf' and s + 1 with the expansion's statistics);
+//                   the first argmax leaf that is not expanded ends the replay.  Then the next
+//                   round's expansions are planned: the current unexpanded leaves of highest
+//                   gain (the one that ended the replay first).
+//
+// The accepted sequence is the sequential one: a leaf's best split and its children's results
+// depend only on its own rows, and the replay uses the host loop's argmax order (gain, real
+// feature, leaf id).  Expansions not accepted before the tree is full cost work only.
+// Pending expansions stay valid across rounds (leaves are only ever split by their best
+// split), so no expansion is computed twice.
+#include "hist_common.h"
+#include "split_scan.h"
+
+namespace lgbm_amd {
+namespace dev {
+
+namespace {
+
+#ifndef LGBM_FIND_WAVE_OCC
+#define LGBM_FIND_WAVE_OCC 4
+#endif
+constexpr unsigned kRoundFlatMax = 128;  // split-scan grid rows up to this size count on one counter
+constexpr int kRPartWaves = kPartThreads / kWave;
+constexpr int kRGatherNarrow = 2, kRGatherWide = 8, kRGatherNarrowMaxWords = 8;
+constexpr int kPlanThreads = 256;
+
+__device__ __forceinline__ long long* RoundScratch(const KArgs& a, int parity, int j) {
+  return a.scratch + (static_cast<size_t>(parity & 1) * a.round_k + j) * 2 * static_cast<size_t>(a.p.total_bins);
+}
+
+__device__ __forceinline__ int RValidInWave(int valid, int k, int w) {
+  return min(kWave, max(0, valid - k * kPartThreads - w * kWave));
+}
+
+// per-expansion constants of the split kernel, staged in LDS once per workgroup
+struct SplitExp {
+  int pb, pc, src, blk_off, nblk, hl, single;
+  int fbyte, fwide;
+  int sub_lo, sub_hi, offset, mfb;
+  long long fcol;
+  SplitRule r;
+};
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- k_round_split
+// grid (split_grid, hist_tiles) of 1024-thread workgroups.  Row block kb of the round belongs
+// to the expansion j with blk_off[j] <= kb < blk_off[j] + nblk[j]; it holds rows
+// [(kb - blk_off[j]) * rpb, +rpb) of the expansion's parent range, processed in sub-tiles of
+// kSplitSub rows exactly like k_split: sides by the split rule, per-wave ballots, one
+// reservation per side and sub-tile on the expansion's cursors (lefts from the front of the
+// range, rights from its back, in the other index buffer), the histogrammed child's rows
+// compacted into an LDS row list and gathered into the tile's LDS histogram, stored as
+// partial kb.  Only column tile 0 writes the partition.
+template <int GPW, int UNITS, int GR>
+__global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
+  extern __shared__ unsigned long long lds[];  // [UNITS * tile_bins] histogram, then the row list
+  __shared__ SplitExp ex[kMaxRoundExp];
+  __shared__ uint32_t cat_bits[kMaxRoundExp][kMaxCatWords];
+  __shared__ int wl[kSplitRows][kRPartWaves];
+  __shared__ int lpre[kSplitRows][kRPartWaves];
+  __shared__ int hpre[kSplitRows][kRPartWaves];
+  __shared__ int base[2];
+  __shared__ int nh_s;
+  Round* rd = a.rd;
+  const int done = rd->done;
+  const int nexp = rd->nexp, nblk = rd->nblk, rpb = rd->rpb;
+  TileCtx t;
+  InitTile<GPW>(a, &t);
+  if (done || nexp <= 0 || static_cast<int>(blockIdx.x) >= nblk) return;
+  if (threadIdx.x < static_cast<unsigned>(nexp)) {
+    const ExpPlan& e = rd->e[threadIdx.x];
+    SplitExp x;
+    x.pb = e.part_begin;
+    x.pc = e.part_count;
+    x.src = e.src_buf;
+    x.blk_off = e.blk_off;
+    x.nblk = e.nblk;
+    x.hl = e.hist_left;
+    x.single = e.nblk == 1 && e.part_count <= kSplitSub;
+    x.fbyte = e.feat.gbyte;
+    x.fwide = e.feat.gwide;
+    x.fcol = e.feat.col_off;
+    x.sub_lo = e.feat.sub_lo;
+    x.sub_hi = e.feat.sub_hi;
+    x.offset = e.feat.offset;
+    x.mfb = e.feat.mfb;
+    x.r.threshold = e.split.threshold;
+    x.r.default_left = e.split.default_left;
+    x.r.is_cat = e.split.is_categorical;
+    x.r.missing_type = e.feat.missing_type;
+    x.r.default_bin = e.feat.default_bin;
+    x.r.max_bin = e.feat.num_bin - 1;
+    ex[threadIdx.x] = x;
+  }
+  for (int i = threadIdx.x; i < nexp * kMaxCatWords; i += kPartThreads) {
+    const int j = i / kMaxCatWords;
+    cat_bits[j][i % kMaxCatWords] = rd->e[j].split.is_categorical ? rd->e[j].split.cat_bits[i % kMaxCatWords] : 0u;
+  }
+  __syncthreads();
+  // the expansion of row block kb
+  auto exp_of = [&](int kb) {
+    int j = 0;
+    while (j + 1 < nexp && kb >= ex[j + 1].blk_off) ++j;
+    return j;
+  };
+  int* rowlist = reinterpret_cast<int*>(lds + static_cast<size_t>(UNITS) * a.tile_bins);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const bool writer = blockIdx.y == 0;
+  int row[kSplitRows];
+  uint32_t gb[kSplitRows];
+  auto load_rows = [&](int jn, int t0n, int r1n, int* rr) {
+    const int vn = min(kSplitSub, r1n - t0n);
+    const int32_t* s = ex[jn].src ? a.tmp : a.idx;
+    const int pbn = ex[jn].pb;
+#pragma unroll
+    for (int k = 0; k < kSplitRows; ++k) {
+      const int i = k * kPartThreads + threadIdx.x;
+      rr[k] = i < vn ? s[pbn + t0n + i] : -1;
+    }
+  };
+  auto col_bins = [&](int jn, const int* rr, uint32_t* g) {
+#pragma unroll
+    for (int k = 0; k < kSplitRows; ++k) g[k] = rr[k] >= 0 ? ColBin(a, rr[k], ex[jn].fbyte, ex[jn].fwide, ex[jn].fcol) : 0u;
+  };
+  {
+    const int j = exp_of(blockIdx.x);
+    const int r0 = (blockIdx.x - ex[j].blk_off) * rpb;
+    load_rows(j, r0, min(ex[j].pc, r0 + rpb), row);
+    col_bins(j, row, gb);
+  }
+  for (int kb = blockIdx.x; kb < nblk; kb += gridDim.x) {
+    const int j = exp_of(kb);
+    const SplitExp& X = ex[j];
+    const int r0 = (kb - X.blk_off) * rpb, r1 = min(X.pc, r0 + rpb);
+    const bool hl = X.hl != 0;
+    Feature F;
+    F.sub_lo = X.sub_lo;
+    F.sub_hi = X.sub_hi;
+    F.offset = X.offset;
+    F.mfb = X.mfb;
+    const SplitRule r = X.r;
+    const uint32_t* cb = cat_bits[j];
+    int32_t* dst = X.src ? a.idx : a.tmp;
+    for (int t0 = r0; t0 < r1; t0 += kSplitSub) {
+      const int valid = min(kSplitSub, r1 - t0);
+      // the next sub-tile of this workgroup: this block's next one, or the next block's first
+      int nj = j, nt0 = t0 + kSplitSub, nr1 = r1;
+      if (nt0 >= r1) {
+        const int nkb = kb + gridDim.x;
+        if (nkb < nblk) {
+          nj = exp_of(nkb);
+          nt0 = (nkb - ex[nj].blk_off) * rpb;
+          nr1 = min(ex[nj].pc, nt0 + rpb);
+        } else {
+          nt0 = nr1 = 0;
+        }
+      }
+      int nrow[kSplitRows];
+      load_rows(nj, nt0, nr1, nrow);
+      if (t0 == r0) {
+        __syncthreads();  // the previous block's partial was stored from this LDS
+        for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) lds[i] = 0ull;
+      }
+      bool left[kSplitRows];
+      unsigned long long mask[kSplitRows];
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) {
+        left[k] = row[k] >= 0 && GoesLeft(r, cb, FeatureBinOf(F, gb[k]));
+        mask[k] = __ballot(left[k]);
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < kSplitRows; ++k) wl[k][w] = __popcll(mask[k]);
+      }
+      __syncthreads();
+      if (w == 0) {
+        const int k = lane / kRPartWaves, jj = lane % kRPartWaves;
+        const int c = wl[k][jj];
+        const int hc = hl ? c : RValidInWave(valid, k, jj) - c;
+        const int ci = WavePrefixIncl(c), hi = WavePrefixIncl(hc);
+        lpre[k][jj] = ci - c;
+        hpre[k][jj] = hi - hc;
+        const int nl = __shfl(ci, kWave - 1, kWave);
+        if (lane == kWave - 1) nh_s = hi;
+        if (lane == 0 && writer) {
+          if (X.single) {
+            base[0] = base[1] = 0;
+            rd->cur[j][0] = nl;
+            rd->cur[j][1] = valid - nl;
+          } else {
+            base[0] = atomicAdd(&rd->cur[j][0], nl);
+            base[1] = atomicAdd(&rd->cur[j][1], valid - nl);
+          }
+        }
+      }
+      __syncthreads();
+      const int nh = nh_s;
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) {
+        const unsigned long long vm = __ballot(row[k] >= 0);
+        const unsigned long long hm = hl ? mask[k] : (~mask[k] & vm);
+        if (row[k] >= 0 && left[k] == hl) rowlist[hpre[k][w] + __popcll(hm & lt)] = row[k];
+      }
+      if (writer) {
+        const int lbase = X.pb + base[0];
+        const int rbase = X.pb + X.pc - 1 - base[1];
+#pragma unroll
+        for (int k = 0; k < kSplitRows; ++k) {
+          if (row[k] >= 0) {
+            const int lpos = lpre[k][w] + __popcll(mask[k] & lt);
+            const int pos = k * kPartThreads + threadIdx.x;
+            if (left[k]) dst[lbase + lpos] = row[k];
+            else dst[rbase - (pos - lpos)] = row[k];
+          }
+        }
+      }
+      __syncthreads();  // the row list is complete
+      if (t.rs < t.rpp) {
+        const int wi = t.w0 + t.q;
+        const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
+        const float2* gh = reinterpret_cast<const float2*>(a.gh);
+        const int64_t wpr = a.words_per_row;
+        for (int j0 = t.rs; j0 < nh; j0 += GR * t.rpp) {
+          int rr[GR];
+#pragma unroll
+          for (int k = 0; k < GR; ++k) {
+            const int jr = j0 + k * t.rpp;
+            rr[k] = jr < nh ? rowlist[jr] : -1;
+          }
+          float2 v[GR];
+          if constexpr (GPW == kSparseGPW) {
+#pragma unroll
+            for (int k = 0; k < GR; ++k) v[k] = gh[rr[k] >= 0 ? rr[k] : 0];
+            AddSparseRows<GR, UNITS>(a, lds, t, rr, v);
+          } else {
+            uint32_t wd[GR];
+#pragma unroll
+            for (int k = 0; k < GR; ++k) {
+              const int x = rr[k] >= 0 ? rr[k] : 0;
+              v[k] = gh[x];
+              wd[k] = rr[k] >= 0 ? bins32[x * wpr + wi] : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < GR; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) row[k] = nrow[k];
+      col_bins(nj, row, gb);
+      __syncthreads();  // row list, wave counts and bases are rewritten by the next sub-tile
+    }
+    if (r0 >= r1) {  // (an empty block still stores a zero partial)
+      __syncthreads();
+      for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) lds[i] = 0ull;
+      __syncthreads();
+    }
+    unsigned long long* out = a.partials + static_cast<size_t>(kb) * UNITS * a.p.total_bins +
+                              static_cast<size_t>(UNITS) * t.lo_bin;
+    for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) out[i] = lds[i];
+  }
+}
+
+// --------------------------------------------------------------------------- k_round_reduce
+// grid (bins / 256, kReduceRows, round_k): the partials of expansion blockIdx.z with more than
+// kDirectChunk row blocks summed into its reduce buffer (pre-zeroed by the previous round's
+// split scans when the chunks combine with atomics)
+template <int UNITS>
+__global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
+  const Round* rd = a.rd;
+  if (rd->done) return;
+  const int j = blockIdx.z;
+  if (j >= rd->nexp) return;
+  const int nblk = rd->e[j].nblk;
+  if (nblk <= kDirectChunk) return;  // summed by the split scan
+  if (static_cast<int>(blockIdx.y) * kReduceChunk >= nblk) return;
+  const int bin = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = a.p.total_bins;
+  if (bin >= nb) return;
+  const size_t pstride = static_cast<size_t>(UNITS) * nb;
+  const unsigned long long* part = a.partials + static_cast<size_t>(rd->e[j].blk_off) * pstride;
+  long long g = 0, h = 0;
+  for (int k0 = blockIdx.y * kReduceChunk; k0 < nblk; k0 += gridDim.y * kReduceChunk) {
+    const unsigned long long* p = part + k0 * pstride + static_cast<size_t>(UNITS) * bin;
+    const int kn = min(kReduceChunk, nblk - k0);
+    unsigned long long v0[kReduceChunk], v1[kReduceChunk];
+#pragma unroll
+    for (int k = 0; k < kReduceChunk; ++k) {
+      v0[k] = k < kn ? p[k * pstride] : 0ull;
+      v1[k] = (UNITS == 2 && k < kn) ? p[k * pstride + 1] : 0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < kReduceChunk; ++k) {
+      long long pg, ph;
+      UnpackPartial(v0[k], v1[k], UNITS, &pg, &ph);
+      g += pg;
+      h += ph;
+    }
+  }
+  long long* out = RoundScratch(a, rd->round, j);
+  if (nblk <= kReduceChunk) {
+    out[2 * bin] = g;
+    out[2 * bin + 1] = h;
+  } else {
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin]), static_cast<unsigned long long>(g));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin + 1]), static_cast<unsigned long long>(h));
+  }
+}
+
+// ----------------------------------------------------------------------------- k_round_find
+template <int KIND, int NT>
+struct RoundFindShared {
+  BlockScratch<NT> sc;
+  ScanScratch<NT> ssc;
+  Cand sc2[NT / kWave];
+  typename std::conditional<KIND == 2, CatScratch, int>::type cat_sc;
+  unsigned long long s_red[2 * NT];
+  ArgC arg[NT / kWave];
+};
+
+__device__ __forceinline__ ArgC ArgWaveBest(ArgC c) {
+#pragma unroll 1
+  for (int o = 32; o > 0; o >>= 1) ArgTake(&c, ArgShflXor(c, o));
+  return c;
+}
+
+// the best split of child y (2j + lr) of the round from its per-feature results, by the
+// child's last split-scan workgroup (SplitInfo order: larger gain, then smaller real feature)
+template <int KIND, int NT>
+__device__ void ChildBest(const KArgs& a, int y, int leaf, int lr, RoundFindShared<KIND, NT>& sh) {
+  const int NF = a.p.num_features, tid = threadIdx.x;
+  const FeatureBest* fb = a.feat_best + static_cast<size_t>(y) * NF;
+  constexpr int kB = 8;
+  ArgC c = ArgNone();
+#pragma unroll 1
+  for (int i0 = tid; i0 < NF; i0 += kB * NT) {
+    double cg[kB];
+    int crf[kB], cf[kB];
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      const int i = i0 + k * NT;
+      cf[k] = -1;
+      if (i < NF) {
+        cg[k] = fb[i].gain;
+        crf[k] = fb[i].real_feature;
+        cf[k] = fb[i].feature;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kB; ++k) {
+      if (cf[k] >= 0 && (c.idx < 0 || SplitBetter(cg[k], crf[k], c.g, c.rf))) {
+        c.g = cg[k];
+        c.rf = crf[k];
+        c.idx = i0 + k * NT;
+      }
+    }
+  }
+  c = ArgWaveBest(c);
+  if ((tid & 63) == 0) sh.arg[tid >> 6] = c;
+  __syncthreads();
+  ArgC b = sh.arg[0];
+#pragma unroll
+  for (int k = 1; k < NT / kWave; ++k) ArgTake(&b, sh.arg[k]);
+  const size_t ci = 2 * static_cast<size_t>(leaf) + lr;
+  FeatureBest* dst = a.cbest + ci;
+  if (b.idx >= 0 && b.g != -INFINITY) {
+    CopyWords(&fb[b.idx], dst, tid, NT);
+    const uint32_t* cat = a.feat_cat + (static_cast<size_t>(y) * NF + b.idx) * kMaxCatWords;
+    for (int w = tid; w < kMaxCatWords; w += NT) a.cbest_cat[ci * kMaxCatWords + w] = cat[w];
+  } else if (tid == 0) {
+    FeatureBest none = {};
+    none.gain = -INFINITY;
+    none.feature = none.real_feature = -1;
+    *dst = none;
+  }
+}
+
+// split scan of one (feature, child of expansion j): grid (num_scan or categorical features,
+// 2 x round_k); child y = 2j + lr (0 left, 1 right).  The histogrammed child takes the
+// expansion's reduced histogram (or sums its few partials itself) into its new slot; the
+// other one subtracts it from the parent's slot in place (exact int64).  Children of an
+// expansion that cannot be split (max_depth, min_data_in_leaf) are not scanned.
+template <int KIND, bool SIMPLE, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave ? LGBM_FIND_WAVE_OCC : 1))) void k_round_find(KArgs a) {
+  constexpr bool CAT = KIND == 2;
+  extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
+  __shared__ RoundFindShared<KIND, NT> sh;
+  __shared__ int s_last;
+  Round* rd = a.rd;
+  if (rd->done) return;
+  const int y = blockIdx.y, j = y >> 1, lr = y & 1;
+  const int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
+  const int tid = threadIdx.x;
+  const int NF = a.p.num_features;
+  const int units = a.hist_units;
+  const Feature F = a.feat[f];
+  const int8_t tree_used = a.tree_mask[f];
+  const int nexp = rd->nexp, parity = rd->round & 1;
+  const int nbf = F.num_bin - F.offset;
+  const double ig = a.scales[2], ih = a.scales[3];
+  // this feature's bins of expansion j's reduce buffer for the next round (every expansion
+  // slot: the next round may use any)
+  if (!CAT && lr == 0) {
+    long long* nxt = RoundScratch(a, parity + 1, j);
+    for (int i = tid; i < 2 * nbf; i += NT) nxt[2 * F.hist_offset + i] = 0;
+  }
+  if (j >= nexp) return;
+  const ExpPlan& E = rd->e[j];
+  const int pc = E.part_count;
+  const int tl = rd->cur[j][0];
+  const int lc = tl, rc = pc - tl;
+  const ChildStats cl = E.lr[lr];
+  const int leaf = E.leaf;
+  const int md = a.p.sp.min_data_in_leaf;
+  const bool skip = (a.p.max_depth > 0 && cl.depth >= a.p.max_depth) || (lc < 2 * md && rc < 2 * md);
+  const bool is_hist = (lr == 0) == (E.hist_left != 0);
+  const int slot = is_hist ? E.slot_new : E.slot_parent;
+  const int frow = E.frow_child[lr];
+  const int nblk = E.nblk, blk_off = E.blk_off;
+  const int8_t parent_ok = a.splittable[static_cast<size_t>(E.frow_parent) * NF + f];
+  FeatureBest* fb_out = &a.feat_best[static_cast<size_t>(y) * NF + f];
+  int8_t* flags = a.splittable + static_cast<size_t>(frow) * NF;
+  const SplitParams& p = a.p.sp;
+  FeatureBest o;
+  o.gain = -INFINITY;
+  o.feature = -1;
+  o.real_feature = -1;
+  o.thr = 0;
+  o.default_left = 1;
+  o.lc = o.rc = 0;
+  o.mono = 0;
+  o.ncat = 0;
+  o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
+  bool write = true;
+  if (KIND == 1 && F.is_cat) {
+    write = false;  // the categorical kernel scans it
+  } else if (skip) {
+    // (both children keep gain -inf: never split)
+  } else if (tree_used && !parent_ok) {
+    // the parent could not split on f: neither child evaluates it (SerialTreeLearner::FindBestSplits)
+    if (tid == 0) flags[f] = 0;
+  } else if (tree_used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
+    // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
+    // but keeps its histogram (descendants subtract it)
+    bool used = true;
+    if (a.feat_icmask != nullptr && (cl.icmask & a.feat_icmask[f]) == 0) used = false;
+    LeafCtx L;
+    L.sg = cl.sum_g;
+    L.sh = cl.sum_h + 2 * kEpsilon;
+    L.n = lr == 0 ? lc : rc;
+    L.parent_out = cl.output;
+    L.c.min = cl.cmin;
+    L.c.max = cl.cmax;
+    const int nh = 2 * a.p.total_bins;
+    long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
+    const long long* src = RoundScratch(a, parity, j) + 2 * F.hist_offset;
+    const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
+    const unsigned long long* part = a.partials + static_cast<size_t>(blk_off) * pstride + static_cast<size_t>(units) * F.hist_offset;
+    const bool stage = a.p.max_feature_bins <= kFindLdsBins;
+    double* sgv = s_bins;
+    double* shv = s_bins + (stage ? a.p.max_feature_bins : 0);
+    const bool subtract = !is_hist;
+    const int nblk_direct = nblk <= kDirectChunk ? nblk : -1;
+    const bool spread = nblk_direct > 1 && 2 * nbf <= NT;
+    long long pg0 = 0, ph0 = 0;
+    if (subtract && tid < nbf) {
+      pg0 = dst[2 * tid];
+      ph0 = dst[2 * tid + 1];
+    }
+    if (spread) {
+      for (int i = tid; i < 2 * nbf; i += NT) sh.s_red[i] = 0ull;
+      __syncthreads();
+      const int per = NT / nbf;
+      const int i = tid % nbf, r = tid / nbf;
+      if (r < per) {
+        constexpr int kC = 8;
+        long long g = 0, h = 0;
+        for (int k0 = r; k0 < nblk_direct; k0 += per * kC) {
+          unsigned long long v0[kC], v1[kC];
+#pragma unroll
+          for (int cc = 0; cc < kC; ++cc) {
+            const int k = k0 + cc * per;
+            const unsigned long long* q = part + k * pstride + static_cast<size_t>(units) * i;
+            v0[cc] = k < nblk_direct ? q[0] : 0ull;
+            v1[cc] = (k < nblk_direct && units == 2) ? q[1] : 0ull;
+          }
+#pragma unroll
+          for (int cc = 0; cc < kC; ++cc) {
+            long long pgv, phv;
+            UnpackPartial(v0[cc], v1[cc], units, &pgv, &phv);
+            g += pgv;
+            h += phv;
+          }
+        }
+        atomicAdd(&sh.s_red[2 * i], static_cast<unsigned long long>(g));
+        atomicAdd(&sh.s_red[2 * i + 1], static_cast<unsigned long long>(h));
+      }
+      __syncthreads();
+    }
+    for (int i = tid; i < nbf; i += NT) {
+      long long g = 0, h = 0;
+      if (spread) {
+        g = static_cast<long long>(sh.s_red[2 * i]);
+        h = static_cast<long long>(sh.s_red[2 * i + 1]);
+      } else if (nblk_direct >= 0) {
+        for (int k0 = 0; k0 < nblk_direct; k0 += kDirectChunk) {
+          unsigned long long v0[kDirectChunk], v1[kDirectChunk];
+#pragma unroll
+          for (int k = 0; k < kDirectChunk; ++k) {
+            const unsigned long long* q = part + (k0 + k) * pstride + static_cast<size_t>(units) * i;
+            v0[k] = k0 + k < nblk_direct ? q[0] : 0ull;
+            v1[k] = (k0 + k < nblk_direct && units == 2) ? q[1] : 0ull;
+          }
+#pragma unroll
+          for (int k = 0; k < kDirectChunk; ++k) {
+            long long pgv, phv;
+            UnpackPartial(v0[k], v1[k], units, &pgv, &phv);
+            g += pgv;
+            h += phv;
+          }
+        }
+      } else {
+        g = src[2 * i];
+        h = src[2 * i + 1];
+      }
+      if (subtract) {
+        g = (i == tid ? pg0 : dst[2 * i]) - g;
+        h = (i == tid ? ph0 : dst[2 * i + 1]) - h;
+      }
+      dst[2 * i] = g;
+      dst[2 * i + 1] = h;
+      if (stage) {
+        sgv[i] = static_cast<double>(g) * ig;
+        shv[i] = static_cast<double>(h) * ih;
+      }
+    }
+    __syncthreads();
+    if (used) {
+      L.cnt_factor = L.n / L.sh;
+      const double gain_shift = LeafGain(L.sg, L.sh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, L.n,
+                                         L.parent_out, p.use_l1, p.use_max_output, p.use_smoothing);
+      L.min_gain_shift = gain_shift + p.min_gain_to_split;
+      o.feature = f;
+      o.real_feature = F.real_index;
+      HistView hv;
+      hv.lg = stage ? sgv : nullptr;
+      hv.lh = stage ? shv : nullptr;
+      hv.h = dst;
+      hv.inv_g = ig;
+      hv.inv_h = ih;
+      bool splittable;
+      if constexpr (CAT) {
+        splittable = FindCategoricalBlock(F, hv, L, p, &o, a.feat_cat + (static_cast<size_t>(y) * NF + f) * kMaxCatWords,
+                                          &sh.sc, &sh.cat_sc);
+      } else {
+        splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, cl.depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc,
+                                                    sh.sc2, kNoRandThr);
+      }
+      if (tid == 0) flags[f] = splittable ? 1 : 0;
+      if (!CAT && !SIMPLE && F.monotone != 0) o.gain *= MonotonePenalty(cl.depth, a.p.monotone_penalty);
+      if (o.gain == -INFINITY) o.feature = -1;
+    }
+  }
+  if (write && tid == 0) PublishRecord(fb_out, o);
+  if (KIND == 1) return;  // the categorical kernel counts the arrivals
+  // arrival: the child's last workgroup folds the child's per-feature results
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned nwg = gridDim.x;
+    uint32_t* cc = a.child_cnt + static_cast<size_t>(y) * (kFindSub + 1) * kFindSubStride;
+    int last = 0;
+    if (nwg <= kRoundFlatMax) {
+      if (atomicAdd(cc, 1u) == nwg - 1) {
+        last = 1;
+        *cc = 0u;  // (every other workgroup of the child has counted)
+      }
+    } else {
+      const unsigned g = blockIdx.x % kFindSub;
+      const unsigned members = (nwg - g + kFindSub - 1) / kFindSub;
+      uint32_t* sub = cc + g * kFindSubStride;
+      if (atomicAdd(sub, 1u) == members - 1) {
+        *sub = 0u;
+        uint32_t* top = cc + kFindSub * kFindSubStride;
+        if (atomicAdd(top, 1u) == kFindSub - 1) {
+          last = 1;
+          *top = 0u;
+        }
+      }
+    }
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  ChildBest<KIND, NT>(a, y, leaf, lr, sh);
+}
+
+// ----------------------------------------------------------------------------- k_round_plan
+// One workgroup.  ROOT: the root's best split from its per-feature results (FindRoot), then
+// the first plan.  Otherwise: fold the round's partition counts into the expansions, replay
+// the best-first order, apply the accepted splits, plan the next round.
+template <bool ROOT>
+__global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
+  extern __shared__ unsigned char plan_lds[];
+  __shared__ int s_go[2], s_done, s_nexp;
+  __shared__ ArgC s_arg[kPlanThreads / kWave];
+  __shared__ int s_pick[kMaxRoundExp];
+  __shared__ int s_pc[kMaxRoundExp];
+  Round* rd = a.rd;
+  if (rd->done) return;
+  const int L = a.p.num_leaves, NF = a.p.num_features, tid = threadIdx.x, lane = tid & 63;
+  // per-leaf tables: gain, real feature, inner feature, expanded; the expanded leaves'
+  // children (2 per leaf); the accepted leaves
+  double* tg = reinterpret_cast<double*>(plan_lds);
+  double* tcg = tg + L;
+  int* trf = reinterpret_cast<int*>(tcg + 2 * L);
+  int* tfi = trf + L;
+  int* tex = tfi + L;
+  int* tcrf = tex + L;
+  int* tcfi = tcrf + 2 * L;
+  int* acc = tcfi + 2 * L;
+  const int s0 = rd->nsplit;
+  if (ROOT) {
+    // argmax over the root's per-feature results (side 0 of feat_best)
+    ArgC c = ArgNone();
+    for (int f = tid; f < NF; f += kPlanThreads) {
+      const FeatureBest& fb = a.feat_best[f];
+      if (fb.feature >= 0 && (c.idx < 0 || SplitBetter(fb.gain, fb.real_feature, c.g, c.rf))) {
+        c.g = fb.gain;
+        c.rf = fb.real_feature;
+        c.idx = f;
+      }
+    }
+    c = ArgWaveBest(c);
+    if (lane == 0) s_arg[tid >> 6] = c;
+    __syncthreads();
+    ArgC b = s_arg[0];
+    for (int k = 1; k < kPlanThreads / kWave; ++k) ArgTake(&b, s_arg[k]);
+    if (b.idx >= 0 && b.g == -INFINITY) b.idx = -1;
+    if (tid == 0) {
+      if (b.idx >= 0) {
+        ToDeviceSplit(a.feat_best[b.idx], a.feat_cat + static_cast<size_t>(b.idx) * kMaxCatWords, &a.best[0]);
+      } else {
+        NoSplit(&a.best[0]);
+      }
+      tg[0] = b.idx >= 0 ? b.g : -INFINITY;
+      trf[0] = b.idx >= 0 ? b.rf : -1;
+      tfi[0] = b.idx;
+      tex[0] = 0;
+    }
+  } else {
+    if (tid < rd->nexp) a.exres[rd->e[tid].leaf].total_left = rd->cur[tid][0];
+    for (int l = tid; l <= s0 && l < L; l += kPlanThreads) {
+      tg[l] = a.best[l].gain;
+      trf[l] = a.best[l].real_feature;
+      tfi[l] = a.best[l].feature;
+      const int e = a.leaves[l].expanded;
+      tex[l] = e;
+      if (e) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const FeatureBest& cb = a.cbest[2 * l + k];
+          tcg[2 * l + k] = cb.gain;
+          tcrf[2 * l + k] = cb.real_feature;
+          tcfi[2 * l + k] = cb.feature;
+        }
+      }
+    }
+  }
+  if (tid == 0) s_done = 0;
+  if (tid < kMaxRoundExp) s_pick[tid] = -1;
+  __syncthreads();
+  // replay of the sequential order: the argmax leaf (gain, real feature, leaf id) is split
+  // while its expansion is computed.  Wave 0 decides; the decision flag is double-buffered by
+  // iteration (a slow wave may still read the previous one while wave 0 writes the next)
+  int s = s0;
+  for (int it = 0;; ++it) {
+    if (s >= L - 1) {
+      if (tid == 0) s_done = 1;
+      break;
+    }
+    if (tid < kWave) {
+      ArgC c = ArgNone();
+      for (int l = lane; l <= s; l += kWave) {
+        if (c.idx < 0 || SplitBetter(tg[l], trf[l], c.g, c.rf)) {
+          c.g = tg[l];
+          c.rf = trf[l];
+          c.idx = l;
+        }
+      }
+      c = ArgWaveBest(c);
+      if (lane == 0) {
+        const int w = c.idx;
+        const bool ok = c.g > 0.0 && tfi[w] >= 0;
+        const int go = ok && tex[w];
+        s_go[it & 1] = go;
+        if (!ok) s_done = 1;
+        if (go) {
+          const int nl = s + 1;
+          acc[s - s0] = w;
+          tg[w] = tcg[2 * w];
+          trf[w] = tcrf[2 * w];
+          tfi[w] = tcfi[2 * w];
+          tex[w] = 0;
+          tg[nl] = tcg[2 * w + 1];
+          trf[nl] = tcrf[2 * w + 1];
+          tfi[nl] = tcfi[2 * w + 1];
+          tex[nl] = 0;
+        }
+      }
+    }
+    __syncthreads();
+    if (!s_go[it & 1]) break;
+    ++s;
+  }
+  const int s1 = s, nacc = s - s0;
+  // apply the accepted splits: split records and children leaves, then the children's bests
+  // (the record copies the parent's best first)
+  constexpr int kSplitWords = sizeof(DeviceSplit) / 4;
+  for (int i = tid; i < nacc * kSplitWords; i += kPlanThreads) {
+    const int k = i / kSplitWords, wd = i % kSplitWords;
+    reinterpret_cast<uint32_t*>(&a.rec[s0 + k].split)[wd] = reinterpret_cast<const uint32_t*>(&a.best[acc[k]])[wd];
+  }
+  for (int k = tid; k < nacc; k += kPlanThreads) {
+    const int w = acc[k], s = s0 + k, nl = s + 1;
+    const ExpResult R = a.exres[w];
+    SplitRecord& rec = a.rec[s];
+    rec.leaf = w;
+    rec.left_count = R.total_left;
+    rec.right_count = R.count - R.total_left;
+    for (int c = 0; c < 2; ++c) {
+      Leaf& lf = a.leaves[c == 0 ? w : nl];
+      const ChildStats& cs = R.lr[c];
+      lf.begin = c == 0 ? R.begin : R.begin + R.total_left;
+      lf.count = c == 0 ? R.total_left : R.count - R.total_left;
+      lf.global_count = lf.count;
+      lf.depth = cs.depth;
+      lf.slot = cs.slot;
+      lf.buf = R.buf;
+      lf.frow = cs.frow;
+      lf.expanded = 0;
+      lf.icmask = cs.icmask;
+      lf.sum_g = cs.sum_g;
+      lf.sum_h = cs.sum_h;
+      lf.output = cs.output;
+      lf.lsum_g = lf.lsum_h = 0.0;
+      lf.cmin = cs.cmin;
+      lf.cmax = cs.cmax;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < 2 * nacc; i += kPlanThreads) {
+    const int k = i >> 1, c = i & 1, w = acc[k];
+    const FeatureBest& cb = a.cbest[2 * w + c];
+    DeviceSplit* d = &a.best[c == 0 ? w : s0 + k + 1];
+    if (cb.feature >= 0 && cb.gain != -INFINITY) ToDeviceSplit(cb, a.cbest_cat + (2 * static_cast<size_t>(w) + c) * kMaxCatWords, d);
+    else NoSplit(d);
+  }
+  __syncthreads();
+  if (s_done) {
+    if (tid == 0) {
+      rd->done = 1;
+      rd->nsplit = s1;
+      rd->nexp = 0;
+      rd->accepted_max = max(rd->accepted_max, nacc);
+    }
+    return;
+  }
+  // the next round: the current unexpanded leaves of highest gain (rank in the replay's order)
+  const int kmax = min(a.round_k, L - 1 - s1);
+  for (int l = tid; l <= s1; l += kPlanThreads) {
+    const bool cand = !tex[l] && tg[l] > 0.0 && tfi[l] >= 0;
+    if (!cand) continue;
+    int r = 0;
+    for (int m = 0; m <= s1 && r < kmax; ++m) {
+      if (m == l || tex[m] || !(tg[m] > 0.0) || tfi[m] < 0) continue;
+      if (SplitBetter(tg[m], trf[m], tg[l], trf[l]) || (!SplitBetter(tg[l], trf[l], tg[m], trf[m]) && m < l)) ++r;
+    }
+    if (r < kmax) s_pick[r] = l;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int n = 0;  // (ranks are dense: the candidates fill s_pick[0 .. min(count, kmax)))
+    while (n < kmax && s_pick[n] >= 0) ++n;
+    // histogram slots / splittable rows left (bounded by construction; guarded anyway)
+    n = min(n, 2 * L - rd->next_slot);
+    n = min(n, (4 * L - rd->next_frow) / 2);
+    s_nexp = max(n, 0);
+  }
+  __syncthreads();
+  const int nexp = s_nexp;
+  const int next_slot = rd->next_slot, next_frow = rd->next_frow;
+  if (tid < nexp) {
+    const int j = tid, l = s_pick[j];
+    const Leaf P = a.leaves[l];
+    s_pc[j] = P.count;
+    ExpPlan& e = rd->e[j];
+    const DeviceSplit& sp = a.best[l];
+    const int hl = sp.left_count <= sp.right_count ? 1 : 0;
+    e.leaf = l;
+    e.part_begin = P.begin;
+    e.part_count = P.count;
+    e.src_buf = P.buf;
+    e.hist_left = hl;
+    e.slot_parent = P.slot;
+    e.slot_new = next_slot + j;
+    e.frow_parent = P.frow;
+    e.frow_child[0] = next_frow + 2 * j;
+    e.frow_child[1] = next_frow + 2 * j + 1;
+    e.feat = a.feat[sp.feature];
+    // children's statistics from the split (basic monotone constraints: the mid-point bound)
+    const int depth = P.depth + 1;
+    double pmin = P.cmin, pmax = P.cmax, rmin = P.cmin, rmax = P.cmax;
+    if (!sp.is_categorical) {
+      const double mid = (sp.left_output + sp.right_output) / 2.0f;
+      if (sp.monotone_type < 0) {
+        pmin = fmax(pmin, mid);
+        rmax = fmin(rmax, mid);
+      } else if (sp.monotone_type > 0) {
+        pmax = fmin(pmax, mid);
+        rmin = fmax(rmin, mid);
+      }
+    }
+    const IcMask icm = P.icmask & (a.feat_icmask != nullptr ? a.feat_icmask[sp.feature] : kIcAll);
+    ChildStats lc, rc;
+    lc.sum_g = sp.left_sum_gradient;
+    lc.sum_h = sp.left_sum_hessian;
+    lc.output = sp.left_output;
+    lc.cmin = pmin;
+    lc.cmax = pmax;
+    lc.global_count = sp.left_count;
+    lc.depth = depth;
+    lc.slot = hl ? e.slot_new : P.slot;
+    lc.leaf = l;
+    lc.frow = e.frow_child[0];
+    lc.icmask = icm;
+    rc.sum_g = sp.right_sum_gradient;
+    rc.sum_h = sp.right_sum_hessian;
+    rc.output = sp.right_output;
+    rc.cmin = rmin;
+    rc.cmax = rmax;
+    rc.global_count = sp.right_count;
+    rc.depth = depth;
+    rc.slot = hl ? P.slot : e.slot_new;
+    rc.leaf = -1;
+    rc.frow = e.frow_child[1];
+    rc.icmask = icm;
+    e.lr[0] = lc;
+    e.lr[1] = rc;
+    ExpResult& R = a.exres[l];
+    R.begin = P.begin;
+    R.count = P.count;
+    R.buf = 1 - P.buf;
+    R.total_left = 0;
+    R.lr[0] = lc;
+    R.lr[1] = rc;
+    a.leaves[l].expanded = 1;
+    a.leaves[l].buf = 1 - P.buf;  // the round moves every row of the leaf to the other buffer
+  }
+  // the split record of each expansion (whole, categories included)
+  for (int i = tid; i < nexp * kSplitWords; i += kPlanThreads) {
+    const int k = i / kSplitWords, wd = i % kSplitWords;
+    reinterpret_cast<uint32_t*>(&rd->e[k].split)[wd] = reinterpret_cast<const uint32_t*>(&a.best[s_pick[k]])[wd];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    // row blocks: one size for the round (at least blk_min_rows, at most the packed headroom)
+    long long rows = 0;
+    for (int j = 0; j < nexp; ++j) rows += s_pc[j];
+    long long rpb = (rows + a.split_grid - 1) / max(1, a.split_grid);
+    rpb = max(rpb, static_cast<long long>(a.blk_min_rows));
+    rpb = min(rpb, static_cast<long long>(a.hist_rows_cap));
+    rpb = max(rpb, 1ll);
+    int off = 0;
+    for (int j = 0; j < nexp; ++j) {
+      const int nb = static_cast<int>((s_pc[j] + rpb - 1) / rpb);
+      rd->e[j].blk_off = off;
+      rd->e[j].nblk = nb;
+      off += nb;
+    }
+    rd->rpb = static_cast<int>(rpb);
+    rd->nblk = off;
+    rd->nexp = nexp;
+    rd->nsplit = s1;
+    rd->next_slot = next_slot + nexp;
+    rd->next_frow = next_frow + 2 * nexp;
+    rd->round = ROOT ? 1 : rd->round + 1;  // (parity 0 of the first round holds the root histogram)
+    rd->rounds = rd->rounds + 1;
+    rd->accepted_max = max(rd->accepted_max, nacc);
+    for (int j = 0; j < kMaxRoundExp; ++j) rd->cur[j][0] = rd->cur[j][1] = 0;
+    if (nexp == 0) {
+      rd->done = 1;  // (no candidate: cannot happen while the replay did not stop the tree)
+    }
+  }
+}
+
+size_t RoundPlanLds(int num_leaves) {
+  const size_t L = static_cast<size_t>(num_leaves);
+  return L * sizeof(double) * 3 + L * sizeof(int) * (3 + 4 + 1);
+}
+
+namespace {
+
+template <int GR>
+void LaunchRoundSplit(const KArgs& a, hipStream_t s) {
+  const dim3 grid(a.split_grid, a.hist_tiles);
+  const size_t lds = sizeof(unsigned long long) * a.hist_units * static_cast<size_t>(a.tile_bins) + sizeof(int) * kSplitSub;
+  if (a.sp_ptr != nullptr) {
+    if (a.hist_units == 1) hipLaunchKernelGGL((k_round_split<kSparseGPW, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_round_split<kSparseGPW, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+  } else if (a.hist_units == 1) {
+    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_round_split<0, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
+  } else {
+    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_round_split<0, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+  }
+}
+
+template <int GR>
+void AllowRoundSplitLds(int mx) {
+  auto allow = [mx](const void* k) {
+    if (mx > 65536 && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess) {
+      (void)hipGetLastError();
+    }
+  };
+  allow(reinterpret_cast<const void*>(k_round_split<4, 1, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<2, 1, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<0, 1, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<4, 2, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<2, 2, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<0, 2, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<kSparseGPW, 1, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<kSparseGPW, 2, GR>));
+}
+
+bool RoundSimpleGains(const KArgs& a) {
+  const SplitParams& p = a.p.sp;
+  return !p.use_l1 && !p.use_max_output && !p.use_smoothing && !p.use_mc;
+}
+
+void LaunchRoundFind(const KArgs& a, hipStream_t s) {
+  const int ny = 2 * a.round_k;
+  const size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
+  const bool simple = RoundSimpleGains(a);
+  const bool narrow = a.p.max_feature_bins <= kWave;
+  const dim3 g(a.num_scan, ny), b(narrow ? kWave : kFindThreads), bc(kFindThreads);
+  if (a.p.has_cat) {
+    if (narrow) {
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kWave>), g, b, lds, s, a);
+    } else {
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads>), g, b, lds, s, a);
+    }
+    hipLaunchKernelGGL((k_round_find<2, false, kFindThreads>), dim3(a.p.has_cat, ny), bc, lds, s, a);
+  } else if (narrow) {
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kWave>), g, b, lds, s, a);
+  } else {
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads>), g, b, lds, s, a);
+  }
+}
+
+}  // namespace
+
+void PrepareRoundKernels(int max_lds) {
+  AllowRoundSplitLds<kRGatherNarrow>(max_lds);
+  AllowRoundSplitLds<kRGatherWide>(max_lds);
+}
+
+void RoundRootPlan(const KArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL((k_round_plan<true>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
+}
+
+void RoundStep(const KArgs& a, hipStream_t s) {
+  if (a.sp_ptr != nullptr || a.tile_words <= kRGatherNarrowMaxWords) LaunchRoundSplit<kRGatherNarrow>(a, s);
+  else LaunchRoundSplit<kRGatherWide>(a, s);
+  const dim3 rgrid((a.p.total_bins + 255) / 256,
+                   std::min(4, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk), a.round_k);
+  if (a.hist_units == 1) hipLaunchKernelGGL((k_round_reduce<1>), rgrid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((k_round_reduce<2>), rgrid, dim3(256), 0, s, a);
+  LaunchRoundFind(a, s);
+  hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
+}
+
+}  // namespace dev
+}  // namespace lgbm_amd

@@ -14,699 +14,11 @@
 // go to feat_best.  The last workgroup of the step to finish (a device-scope counter) then
 // records the step and picks the next split (pick.h), so the next k_split starts from one
 // small Step record.
-#include <type_traits>
-
-#include "pick.h"
+#include "split_scan.h"
 
 namespace lgbm_amd {
 namespace dev {
 
-namespace {
-
-struct Cand {
-  double gain;
-  int thr;
-  double lg, lh;
-  int lc;
-};
-
-constexpr int kNoRandThr = -(1 << 30);  // ScanNumericalBlock: every threshold (no extra_trees draw)
-
-// ties: reverse scan keeps the highest threshold (first met scanning down), forward the lowest
-__device__ __forceinline__ bool CandBetter(const Cand& x, const Cand& y, bool reverse) {
-  if (x.gain > y.gain) return true;
-  if (x.gain < y.gain || x.gain != x.gain) return false;
-  if (y.gain != y.gain) return true;
-  return reverse ? x.thr > y.thr : x.thr < y.thr;
-}
-
-__device__ __forceinline__ Cand WaveBestCand(Cand c, bool reverse) {
-  for (int o = 32; o > 0; o >>= 1) {
-    Cand o2;
-    o2.gain = __shfl_xor(c.gain, o, kWave);
-    o2.thr = __shfl_xor(c.thr, o, kWave);
-    o2.lg = __shfl_xor(c.lg, o, kWave);
-    o2.lh = __shfl_xor(c.lh, o, kWave);
-    o2.lc = __shfl_xor(c.lc, o, kWave);
-    if (CandBetter(o2, c, reverse)) c = o2;
-  }
-  return c;
-}
-
-struct LeafCtx {
-  double sg, sh;  // sh already includes + 2*kEpsilon
-  int n;
-  double cnt_factor;
-  double parent_out;
-  double min_gain_shift;
-  ConstraintRange c;
-};
-
-// block-wide scans / reductions of the split scan (NT threads: kFindThreads, or one wave per
-// workgroup for narrow features); every thread calls them, results are returned to every thread
-template <int NT>
-struct BlockScratch {
-  double d[2][NT / kWave];
-  int i[NT / kWave];
-  Cand c[NT / kWave];
-};
-
-template <int NT>
-__device__ __forceinline__ void BlockScan3(double& a, double& b, int& c, bool suffix, BlockScratch<NT>* sc) {
-  constexpr int kFindWaves = NT / kWave;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  a = suffix ? WaveSuffixIncl(a) : WavePrefixIncl(a);
-  b = suffix ? WaveSuffixIncl(b) : WavePrefixIncl(b);
-  c = suffix ? WaveSuffixIncl(c) : WavePrefixIncl(c);
-  if (lane == (suffix ? 0 : 63)) {
-    sc->d[0][w] = a;
-    sc->d[1][w] = b;
-    sc->i[w] = c;
-  }
-  __syncthreads();
-  double oa = 0.0, ob = 0.0;
-  int oc = 0;
-#pragma unroll
-  for (int j = 0; j < kFindWaves; ++j) {
-    if (suffix ? j > w : j < w) {
-      oa += sc->d[0][j];
-      ob += sc->d[1][j];
-      oc += sc->i[j];
-    }
-  }
-  __syncthreads();
-  a += oa;
-  b += ob;
-  c += oc;
-}
-
-template <int NT>
-__device__ __forceinline__ void BlockSum3(double& a, double& b, int& c, BlockScratch<NT>* sc) {
-  constexpr int kFindWaves = NT / kWave;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  a = WaveSum(a);
-  b = WaveSum(b);
-  c = WaveSum(c);
-  if (lane == 0) {
-    sc->d[0][w] = a;
-    sc->d[1][w] = b;
-    sc->i[w] = c;
-  }
-  __syncthreads();
-  a = b = 0.0;
-  c = 0;
-#pragma unroll
-  for (int j = 0; j < kFindWaves; ++j) {  // fixed order: identical on every thread and run
-    a += sc->d[0][j];
-    b += sc->d[1][j];
-    c += sc->i[j];
-  }
-  __syncthreads();
-}
-
-template <int NT>
-__device__ __forceinline__ bool BlockAny(bool v, BlockScratch<NT>* sc) {
-  constexpr int kFindWaves = NT / kWave;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const bool wv = __any(v);
-  if (lane == 0) sc->i[w] = wv ? 1 : 0;
-  __syncthreads();
-  int r = 0;
-#pragma unroll
-  for (int j = 0; j < kFindWaves; ++j) r |= sc->i[j];
-  __syncthreads();
-  return r != 0;
-}
-
-template <int NT>
-__device__ __forceinline__ Cand BlockBestCand(Cand c, bool reverse, BlockScratch<NT>* sc) {
-  constexpr int kFindWaves = NT / kWave;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  c = WaveBestCand(c, reverse);
-  if (lane == 0) sc->c[w] = c;
-  __syncthreads();
-  Cand b = sc->c[0];
-#pragma unroll
-  for (int j = 1; j < kFindWaves; ++j) {
-    if (CandBetter(sc->c[j], b, reverse)) b = sc->c[j];
-  }
-  __syncthreads();
-  return b;
-}
-
-// a feature's dequantised histogram with its most-frequent bin restored (FixHistogram);
-// bins come from LDS (staged by the wave) or, for very wide features, from the int64 slot
-struct HistView {
-  const double* lg;
-  const double* lh;
-  const long long* h;
-  double inv_g, inv_h;
-  int fix_t;  // bin whose value is reconstructed from the leaf totals (-1: none)
-  double fix_g, fix_h;
-  __device__ __forceinline__ double RawG(int t) const {
-    return lg ? lg[t] : static_cast<double>(h[2 * t]) * inv_g;
-  }
-  __device__ __forceinline__ double RawH(int t) const {
-    return lh ? lh[t] : static_cast<double>(h[2 * t + 1]) * inv_h;
-  }
-  __device__ __forceinline__ double G(int t) const { return t == fix_t ? fix_g : RawG(t); }
-  __device__ __forceinline__ double H(int t) const { return t == fix_t ? fix_h : RawH(t); }
-};
-
-// block-wide exclusive prefix of (g, h, c) plus block totals of (g, h, c) and of three more
-// sums (ag, ah: every stored bin; na*: the NaN bin) in one LDS round
-struct ScanAcc {
-  double g, h;
-  int c;
-  double ag, ah, ng, nh;
-  int nc;
-};
-template <int NT>
-struct ScanScratch {
-  double d[6][NT / kWave];
-  int i[2][NT / kWave];
-};
-
-template <int NT>
-__device__ __forceinline__ void BlockScanNum(ScanAcc* v, ScanAcc* excl, ScanAcc* tot, ScanScratch<NT>* sc) {
-  constexpr int kFindWaves = NT / kWave;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const double ig = WavePrefixIncl(v->g), ih = WavePrefixIncl(v->h);
-  const int ic = WavePrefixIncl(v->c);
-  const double ag = WaveSum(v->ag), ah = WaveSum(v->ah), ng = WaveSum(v->ng), nh = WaveSum(v->nh);
-  const int nc = WaveSum(v->nc);
-  if (lane == 63) {
-    sc->d[0][w] = ig;
-    sc->d[1][w] = ih;
-    sc->i[0][w] = ic;
-  }
-  if (lane == 0) {
-    sc->d[2][w] = ag;
-    sc->d[3][w] = ah;
-    sc->d[4][w] = ng;
-    sc->d[5][w] = nh;
-    sc->i[1][w] = nc;
-  }
-  __syncthreads();
-  ScanAcc e = {0.0, 0.0, 0, 0.0, 0.0, 0.0, 0.0, 0};
-  ScanAcc t = e;
-#pragma unroll
-  for (int j = 0; j < kFindWaves; ++j) {  // fixed order: identical on every thread and run
-    if (j < w) {
-      e.g += sc->d[0][j];
-      e.h += sc->d[1][j];
-      e.c += sc->i[0][j];
-    }
-    t.g += sc->d[0][j];
-    t.h += sc->d[1][j];
-    t.c += sc->i[0][j];
-    t.ag += sc->d[2][j];
-    t.ah += sc->d[3][j];
-    t.ng += sc->d[4][j];
-    t.nh += sc->d[5][j];
-    t.nc += sc->i[1][j];
-  }
-  __syncthreads();
-  e.g += ig - v->g;
-  e.h += ih - v->h;
-  e.c += ic - v->c;
-  *excl = e;
-  *tot = t;
-}
-
-// the best candidates of both scan directions and whether any threshold was valid, over
-// the workgroup (reverse ties: higher threshold; forward ties: lower)
-template <int NT>
-__device__ __forceinline__ void BlockBestPair(Cand* rv, Cand* fw, bool* any, BlockScratch<NT>* sc, Cand* sc2) {
-  constexpr int kFindWaves = NT / kWave;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  *rv = WaveBestCand(*rv, true);
-  *fw = WaveBestCand(*fw, false);
-  const bool wa = __any(*any);
-  if (lane == 0) {
-    sc->c[w] = *rv;
-    sc2[w] = *fw;
-    sc->i[w] = wa ? 1 : 0;
-  }
-  __syncthreads();
-  Cand br = sc->c[0], bf = sc2[0];
-  int an = sc->i[0];
-#pragma unroll
-  for (int j = 1; j < kFindWaves; ++j) {
-    if (CandBetter(sc->c[j], br, true)) br = sc->c[j];
-    if (CandBetter(sc2[j], bf, false)) bf = sc2[j];
-    an |= sc->i[j];
-  }
-  __syncthreads();
-  *rv = br;
-  *fw = bf;
-  *any = an != 0;
-}
-
-// split gain / leaf output: the plain formulas (no L1, max_delta_step, path smoothing or
-// monotone constraints -- the reference's FuncForNumricalL3 with every flag off) or the
-// general ones, chosen at compile time so the common case stays a few instructions
-template <bool SIMPLE>
-__device__ __forceinline__ double GainOf(double lg, double lh, double rg, double rh, double l2, const SplitParams& p,
-                                         const ConstraintRange& c, int8_t mono, int lc, int rc, double parent_out) {
-  if (SIMPLE) return (lg * lg) / (lh + l2) + (rg * rg) / (rh + l2);
-  return SplitGain(lg, lh, rg, rh, l2, p, c, mono, lc, rc, parent_out);
-}
-template <bool SIMPLE>
-__device__ __forceinline__ double OutputOf(double sg, double sh, double l2, const SplitParams& p,
-                                           const ConstraintRange& c, int n, double parent_out) {
-  if (SIMPLE) return -sg / (sh + l2);
-  return LeafOutputConstrained(sg, sh, l2, p, c, n, parent_out);
-}
-
-// numerical split of one feature (FindBestThresholdSequentially, both directions and
-// FixHistogram); returns whether any threshold was valid (the host's is_splittable).
-// Every candidate -- reverse at t (right = bins t..t_start), forward at t (left = bins
-// 0..t), and the forward "nothing stored on the left" start -- goes through one evaluation
-// site (instruction footprint: these kernels run once per split on a cold I-cache).
-template <bool SIMPLE, int NT>
-__device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
-                                   double mono_penalty, FeatureBest* out, BlockScratch<NT>* sc, ScanScratch<NT>* ssc,
-                                   Cand* sc2, int rthr) {
-  const int tid = threadIdx.x;
-  const int nb = F.num_bin - F.offset;
-  const int offset = F.offset;
-  const bool two = F.num_bin > 2 && F.missing_type != 0;  // reverse and forward scans
-  const bool skip_def = two && F.missing_type == 1;
-  const bool na = two && F.missing_type == 2;
-  const int fix_t = F.mfb > 0 ? F.mfb : -1;  // most frequent bin: not accumulated, rebuilt from the totals
-  const int def_t = skip_def ? F.default_bin - offset : -1;  // the default bin: in no scan
-  const int K = (nb + NT - 1) / NT;
-  const int b0 = tid * K;
-  const int b1 = min(nb, b0 + K);
-  hv.fix_t = -1;
-  ScanAcc v = {0.0, 0.0, 0, 0.0, 0.0, 0.0, 0.0, 0};
-#pragma unroll 1
-  for (int t = b0; t < b1; ++t) {
-    if (t == fix_t) continue;
-    const double g = hv.RawG(t), h = hv.RawH(t);
-    const int c = RoundIntD(h * L.cnt_factor);
-    v.ag += g;
-    v.ah += h;
-    if (t != def_t) {
-      v.g += g;
-      v.h += h;
-      v.c += c;
-    }
-    if (t == nb - 1) {
-      v.ng = g;
-      v.nh = h;
-      v.nc = c;
-    }
-  }
-  ScanAcc ex, tot;
-  BlockScanNum(&v, &ex, &tot, ssc);
-  // FixHistogram
-  if (fix_t >= 0) {
-    const double fix_g = L.sg - tot.ag;
-    const double fix_h = (L.sh - 2 * kEpsilon) - tot.ah;
-    const int fix_c = RoundIntD(fix_h * L.cnt_factor);
-    hv.fix_t = fix_t;
-    hv.fix_g = fix_g;
-    hv.fix_h = fix_h;
-    if (fix_t != def_t) {
-      tot.g += fix_g;
-      tot.h += fix_h;
-      tot.c += fix_c;
-      if (fix_t < b0) {
-        ex.g += fix_g;
-        ex.h += fix_h;
-        ex.c += fix_c;
-      }
-    }
-    if (fix_t == nb - 1) {
-      tot.ng = fix_g;
-      tot.nh = fix_h;
-      tot.nc = fix_c;
-    }
-  }
-  // reverse: right(t) = P(t_start) - P(t - 1) over [t_end_r, t_start]; P(t_start) = total
-  // less the NaN bin when it is left out (na and skip_def exclude each other)
-  const int t_start_r = nb - 1 - (na ? 1 : 0);
-  const int t_end_r = 1 - offset;
-  const int t_end_f = nb - 2;
-  const double pr_g = na ? tot.g - tot.ng : tot.g;
-  const double pr_h = na ? tot.h - tot.nh : tot.h;
-  const int pr_c = na ? tot.c - tot.nc : tot.c;
-  // forward: left starts empty, or (NaN as missing with bin 0 not stored) with everything
-  // outside the stored bins
-  const bool minus_one = na && offset == 1;
-  const double lg0 = minus_one ? L.sg - tot.ag : 0.0;
-  const double lh0 = minus_one ? L.sh - kEpsilon - tot.ah : kEpsilon;
-  const int lc0 = minus_one ? L.n - tot.c : 0;  // (na: every stored bin is included)
-  const double min_h = p.min_sum_hessian_in_leaf;
-  const int min_n = p.min_data_in_leaf;
-  const int8_t mono = static_cast<int8_t>(F.monotone);
-  Cand rb, fb;
-  rb.gain = fb.gain = -INFINITY;
-  rb.thr = -1;
-  fb.thr = 0x7fffffff;
-  rb.lg = rb.lh = fb.lg = fb.lh = 0.0;
-  rb.lc = fb.lc = 0;
-  bool any = false;
-  double pg = ex.g, ph = ex.h;
-  int pc = ex.c;
-  const int cend = 2 * (b1 - b0);
-#pragma unroll 1
-  for (int c = (minus_one && tid == 0) ? -1 : 0; c < cend; ++c) {
-    // candidate c: -1 the forward start, 2i reverse at t = b0 + i, 2i + 1 forward at t
-    const int t = b0 + (c >> 1);
-    const bool rev = c >= 0 && (c & 1) == 0;
-    bool ok;
-    double xg, xh;
-    int xc, thr;
-    if (c < 0) {
-      ok = true;
-      xg = lg0;
-      xh = lh0;
-      xc = lc0;
-      thr = offset - 1;
-    } else if (rev) {
-      ok = t != def_t && t >= t_end_r && t <= t_start_r;
-      // left = total - right, right = bins t..t_start (the reference adds kEpsilon to it)
-      xg = L.sg - (pr_g - pg);
-      xh = L.sh - (pr_h - ph + kEpsilon);
-      xc = L.n - (pr_c - pc);
-      thr = t - 1 + offset;
-    } else {
-      if (t != def_t) {
-        const double h = hv.H(t);
-        pg += hv.G(t);
-        ph += h;
-        pc += RoundIntD(h * L.cnt_factor);
-      }
-      ok = two && t != def_t && t <= t_end_f;
-      xg = lg0 + pg;
-      xh = lh0 + ph;
-      xc = lc0 + pc;
-      thr = t + offset;
-    }
-    if (!ok || xc < min_n || xh < min_h) continue;
-    const int rc = L.n - xc;
-    const double rh = L.sh - xh;
-    if (rc < min_n || rh < min_h) continue;
-    if (rthr != kNoRandThr && thr != rthr) continue;  // extra_trees
-    const double gain = GainOf<SIMPLE>(xg, xh, L.sg - xg, rh, p.lambda_l2, p, L.c, mono, xc, rc, L.parent_out);
-    if (!(gain > L.min_gain_shift)) continue;
-    any = true;
-    const Cand& cur = rev ? rb : fb;
-    if (gain > cur.gain || (gain == cur.gain && (rev ? thr > cur.thr : thr < cur.thr))) {
-      Cand nc;
-      nc.gain = gain;
-      nc.thr = thr;
-      nc.lg = xg;
-      nc.lh = xh;
-      nc.lc = xc;
-      if (rev) rb = nc;
-      else fb = nc;
-    }
-  }
-  BlockBestPair(&rb, &fb, &any, sc, sc2);
-  out->gain = -INFINITY;
-  out->default_left = two ? 1 : (F.missing_type == 2 ? 0 : 1);
-  out->mono = F.monotone;
-#pragma unroll 1
-  for (int d = 0; d < (two ? 2 : 1); ++d) {
-    const Cand b = d == 0 ? rb : fb;
-    if (any && b.gain > out->gain + L.min_gain_shift) {
-      out->thr = b.thr;
-      out->lo = OutputOf<SIMPLE>(b.lg, b.lh, p.lambda_l2, p, L.c, b.lc, L.parent_out);
-      out->lc = b.lc;
-      out->lg = b.lg;
-      out->lh = b.lh - kEpsilon;
-      out->ro = OutputOf<SIMPLE>(L.sg - b.lg, L.sh - b.lh, p.lambda_l2, p, L.c, L.n - b.lc, L.parent_out);
-      out->rc = L.n - b.lc;
-      out->rg = L.sg - b.lg;
-      out->rh = L.sh - b.lh - kEpsilon;
-      out->gain = b.gain - L.min_gain_shift;
-      out->default_left = d == 1 ? 0 : (!two && F.missing_type == 2 ? 0 : 1);
-    }
-  }
-  out->gain *= F.penalty;  // (CEGB and the monotone depth penalty follow in FindBody)
-  (void)depth;
-  (void)mono_penalty;
-  return any;
-}
-
-// MonotoneSplitPenalty(depth, penalization)
-__device__ __forceinline__ double MonotonePenalty(int depth, double mono_penalty) {
-  if (mono_penalty >= depth + 1.) return kEpsilon;
-  if (mono_penalty <= 1.) return 1. - mono_penalty / pow(2., depth) + kEpsilon;
-  return 1. - pow(2., mono_penalty - 1. - depth) + kEpsilon;
-}
-
-// LDS of the categorical scan: per-bin ctr and the stable ctr order
-constexpr int kCatPar = 128;  // prefix positions per direction scanned with the parallel path
-
-struct CatScratch {
-  double ctr[kFindMaxCatBins];
-  int sorted[kFindMaxCatBins];
-  int used_bin;
-  // parallel prefix scan: per direction and position, the bin's then the cumulative
-  // (g, h, count) and the split gain there
-  double pg[2][kCatPar], ph[2][kCatPar], gain[2][kCatPar];
-  int pc[2][kCatPar], cnt[2][kCatPar];
-};
-
-// categorical split of one feature (reference FindBestThresholdCategoricalInner,
-// feature_histogram.hpp:277-513): one-vs-rest for few categories (parallel over the bins),
-// otherwise the bins with enough data sorted by g / (h + cat_smooth) -- a stable rank
-// computed in parallel -- and the sequential prefix scan from both ends (<= 2 x
-// max_cat_threshold steps, thread 0) with the min_data_per_group rules.
-// returns splittable (meaningful in thread 0)
-template <int NT>
-__device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
-                                     FeatureBest* out, uint32_t* cat_out, BlockScratch<NT>* sc, CatScratch* cs) {
-  constexpr int kFindThreads = NT;
-  const int tid = threadIdx.x;
-  const int nb = F.num_bin - F.offset;
-  hv.fix_t = -1;
-  hv.fix_g = hv.fix_h = 0.0;
-  if (F.mfb > 0) {  // FixHistogram
-    double sg = 0.0, sh = 0.0;
-    int unused = 0;
-    for (int t = tid; t < nb; t += kFindThreads) {
-      if (t == F.mfb) continue;
-      sg += hv.RawG(t);
-      sh += hv.RawH(t);
-    }
-    BlockSum3(sg, sh, unused, sc);
-    hv.fix_t = F.mfb;
-    hv.fix_g = L.sg - sg;
-    hv.fix_h = (L.sh - 2 * kEpsilon) - sh;
-  }
-  double gain_shift;
-  if (p.use_smoothing) {
-    gain_shift = LeafGainGivenOutput(L.sg, L.sh, p.lambda_l1, p.lambda_l2, L.parent_out, p.use_l1);
-  } else {
-    gain_shift = LeafGain(L.sg, L.sh, p.lambda_l1, p.lambda_l2, p.max_delta_step, 0, L.n, 0, p.use_l1,
-                          p.use_max_output, 0);
-  }
-  const double min_gain_shift = gain_shift + p.min_gain_to_split;
-  const int offset = F.offset;
-  const int bin_start = 1 - offset, bin_end = F.num_bin - offset;
-  const bool onehot = F.num_bin <= p.max_cat_to_onehot;
-  const double min_h = p.min_sum_hessian_in_leaf;
-  const int min_n = p.min_data_in_leaf;
-  out->gain = -INFINITY;
-  out->default_left = 0;
-  out->mono = 0;
-  out->thr = 0;
-  out->ncat = 0;
-  double l2 = p.lambda_l2;
-  bool splittable = false;
-  Cand best;
-  best.gain = -INFINITY;
-  best.thr = 0x7fffffff;
-  best.lg = best.lh = 0.0;
-  best.lc = 0;
-  int best_dir = 1;
-  if (onehot) {
-    bool any = false;
-    for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
-      const double g = hv.G(t), hh = hv.H(t);
-      const int cnt = RoundIntD(hh * L.cnt_factor);
-      if (cnt < min_n || hh < min_h) continue;
-      const int other = L.n - cnt;
-      if (other < min_n) continue;
-      const double oh = L.sh - hh - kEpsilon;
-      if (oh < min_h) continue;
-      const double og = L.sg - g;
-      const double gain = SplitGain(og, oh, g, hh + kEpsilon, l2, p, L.c, 0, other, cnt, L.parent_out);
-      if (gain <= min_gain_shift) continue;
-      any = true;
-      if (gain > best.gain || (gain == best.gain && t < best.thr)) {
-        best.gain = gain;
-        best.thr = t;
-        best.lg = g;
-        best.lh = hh + kEpsilon;
-        best.lc = cnt;
-      }
-    }
-    splittable = BlockAny(any, sc);
-    best = BlockBestCand(best, false, sc);
-  } else {
-    l2 += p.cat_l2;
-    // candidates and their ctr; non-candidates get NaN (never ranked)
-    for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
-      const double hh = hv.H(t);
-      const bool cand = static_cast<double>(RoundIntD(hh * L.cnt_factor)) >= p.cat_smooth;
-      cs->ctr[t] = cand ? hv.G(t) / (hh + p.cat_smooth) : NAN;
-    }
-    __syncthreads();
-    // stable rank among the candidates (std::stable_sort by ctr ascending)
-    int ncand = 0;
-    for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
-      const double c = cs->ctr[t];
-      if (c != c) continue;
-      ++ncand;
-      int r = 0;
-      for (int u = bin_start; u < bin_end; ++u) {
-        const double cu = cs->ctr[u];
-        r += (cu < c) | ((cu == c) & (u < t));
-      }
-      cs->sorted[r] = t;
-    }
-    double d0 = 0.0, d1 = 0.0;
-    BlockSum3(d0, d1, ncand, sc);
-    const int used_bin = ncand;
-    const int max_num_cat = min(p.max_cat_threshold, (used_bin + 1) / 2);
-    const int npos = min(used_bin, max_num_cat);
-    if (npos <= kCatPar) {
-      // (1) every thread stages one position's bin statistics, (2) one thread per direction
-      // accumulates the prefix sums in the sequential order (bit-identical sums), (3) every
-      // thread evaluates the split gain of one position, (4) thread 0 applies the
-      // order-dependent min_data_per_group rules over the precomputed gains
-      for (int idx = tid; idx < 2 * npos; idx += kFindThreads) {
-        const int o = idx / npos, i = idx % npos;
-        const int t = cs->sorted[o == 0 ? i : used_bin - 1 - i];
-        const double hh = hv.H(t);
-        cs->pg[o][i] = hv.G(t);
-        cs->ph[o][i] = hh;
-        cs->cnt[o][i] = RoundIntD(hh * L.cnt_factor);
-      }
-      __syncthreads();
-      if (tid < 2) {
-        double lg = 0.0, lh = kEpsilon;
-        int lc = 0;
-        for (int i = 0; i < npos; ++i) {
-          lg += cs->pg[tid][i];
-          lh += cs->ph[tid][i];
-          lc += cs->cnt[tid][i];
-          cs->pg[tid][i] = lg;
-          cs->ph[tid][i] = lh;
-          cs->pc[tid][i] = lc;
-        }
-      }
-      __syncthreads();
-      for (int idx = tid; idx < 2 * npos; idx += kFindThreads) {
-        const int o = idx / npos, i = idx % npos;
-        const double lg = cs->pg[o][i], lh = cs->ph[o][i];
-        const int lc = cs->pc[o][i];
-        cs->gain[o][i] = SplitGain(lg, lh, L.sg - lg, L.sh - lh, l2, p, L.c, 0, lc, L.n - lc, L.parent_out);
-      }
-      __syncthreads();
-      if (tid == 0) {
-        for (int o = 0; o < 2; ++o) {
-          int cnt_group = 0;
-          for (int i = 0; i < npos; ++i) {
-            const int lc = cs->pc[o][i];
-            const double lh = cs->ph[o][i];
-            cnt_group += cs->cnt[o][i];
-            if (lc < min_n || lh < min_h) continue;
-            const int rc = L.n - lc;
-            if (rc < min_n || rc < p.min_data_per_group) break;
-            if (L.sh - lh < min_h) break;
-            if (cnt_group < p.min_data_per_group) continue;
-            cnt_group = 0;
-            const double gain = cs->gain[o][i];
-            if (gain <= min_gain_shift) continue;
-            splittable = true;
-            if (gain > best.gain) {
-              best.gain = gain;
-              best.thr = i;
-              best.lg = cs->pg[o][i];
-              best.lh = lh;
-              best.lc = lc;
-              best_dir = o == 0 ? 1 : -1;
-            }
-          }
-        }
-        cs->used_bin = used_bin;
-      }
-    } else if (tid == 0) {
-      for (int o = 0; o < 2; ++o) {
-        const int dir = o == 0 ? 1 : -1;
-        int pos = o == 0 ? 0 : used_bin - 1;
-        int cnt_group = 0, lc = 0;
-        double lg = 0.0, lh = kEpsilon;
-        for (int i = 0; i < used_bin && i < max_num_cat; ++i) {
-          const int t = cs->sorted[pos];
-          pos += dir;
-          const double g = hv.G(t), hh = hv.H(t);
-          const int cnt = RoundIntD(hh * L.cnt_factor);
-          lg += g;
-          lh += hh;
-          lc += cnt;
-          cnt_group += cnt;
-          if (lc < min_n || lh < min_h) continue;
-          const int rc = L.n - lc;
-          if (rc < min_n || rc < p.min_data_per_group) break;
-          const double rh = L.sh - lh;
-          if (rh < min_h) break;
-          if (cnt_group < p.min_data_per_group) continue;
-          cnt_group = 0;
-          const double rg = L.sg - lg;
-          const double gain = SplitGain(lg, lh, rg, rh, l2, p, L.c, 0, lc, rc, L.parent_out);
-          if (gain <= min_gain_shift) continue;
-          splittable = true;
-          if (gain > best.gain) {
-            best.gain = gain;
-            best.thr = i;
-            best.lg = lg;
-            best.lh = lh;
-            best.lc = lc;
-            best_dir = dir;
-          }
-        }
-      }
-      cs->used_bin = used_bin;
-    }
-  }
-  if (tid != 0 || !splittable) return splittable;
-  out->lo = LeafOutputConstrained(best.lg, best.lh, l2, p, L.c, best.lc, L.parent_out);
-  out->lc = best.lc;
-  out->lg = best.lg;
-  out->lh = best.lh - kEpsilon;
-  out->ro = LeafOutputConstrained(L.sg - best.lg, L.sh - best.lh, l2, p, L.c, L.n - best.lc, L.parent_out);
-  out->rc = L.n - best.lc;
-  out->rg = L.sg - best.lg;
-  out->rh = L.sh - best.lh - kEpsilon;
-  out->gain = (best.gain - min_gain_shift) * F.penalty;
-  CatWords bits;  // (published whole: the picking workgroup reads the winner's set)
-  for (int w = 0; w < kMaxCatWords; ++w) bits.w[w] = 0u;
-  if (onehot) {
-    const int b = best.thr + offset;
-    bits.w[b >> 5] |= 1u << (b & 31);
-    out->ncat = 1;
-  } else {
-    const int k = best.thr + 1;
-    for (int i = 0; i < k; ++i) {
-      const int b = (best_dir == 1 ? cs->sorted[i] : cs->sorted[cs->used_bin - 1 - i]) + offset;
-      bits.w[b >> 5] |= 1u << (b & 31);
-    }
-    out->ncat = k;
-  }
-  PublishRecord(reinterpret_cast<CatWords*>(cat_out), bits);
-  return true;
-}
-
-}  // namespace
 
 // KIND 0: every feature of a dataset without categorical features; 1: the numerical
 // features of a dataset with some (the categorical ones only get their bookkeeping here);

@@ -58,10 +58,7 @@ bool GPUTreeLearner::DebugLeafState(const Tree* tree, int leaf, std::vector<int3
   if (lf.count > 0) {
     HIPCHECK(hipMemcpy(rows->data(), buf + lf.begin, sizeof(int32_t) * lf.count, hipMemcpyDeviceToHost));
   }
-  const size_t nh = 2 * static_cast<size_t>(total_bins_);
-  hist->assign(nh, 0);
-  HIPCHECK(hipMemcpy(hist->data(), d_hist_ + static_cast<size_t>(lf.slot) * nh, sizeof(long long) * nh,
-                     hipMemcpyDeviceToHost));
+  ReadHist(lf, leaf, hist);
   std::vector<int8_t> flags(num_features_);
   HIPCHECK(hipMemcpy(flags.data(), d_splittable_ + static_cast<size_t>(lf.frow) * num_features_, num_features_,
                      hipMemcpyDeviceToHost));
@@ -115,8 +112,7 @@ std::string GPUTreeLearner::DebugCheckSplits(const Tree* tree) {
   for (int l = 0; l < L; ++l) {
     const dev::Leaf& lf = leaves[l];
     if (!LeafScanned(tree, l, *config_)) continue;  // no split is evaluated
-    HIPCHECK(hipMemcpy(raw.data(), d_hist_ + static_cast<size_t>(lf.slot) * nh, sizeof(long long) * nh,
-                       hipMemcpyDeviceToHost));
+    ReadHist(lf, l, &raw);
     ConstraintRange c;
     c.min = lf.cmin;
     c.max = lf.cmax;

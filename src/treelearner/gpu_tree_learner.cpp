@@ -71,7 +71,8 @@ void GPUTreeLearner::FreeBuffers() {
   allocs_.clear();
   for (void** hp : {reinterpret_cast<void**>(&h_mask_), reinterpret_cast<void**>(&h_rec_),
                     reinterpret_cast<void**>(&h_step_), reinterpret_cast<void**>(&h_root_),
-                    reinterpret_cast<void**>(&h_absmax_), reinterpret_cast<void**>(&h_scales_)}) {
+                    reinterpret_cast<void**>(&h_absmax_), reinterpret_cast<void**>(&h_scales_),
+                    reinterpret_cast<void**>(&h_round_)}) {
     if (*hp) (void)hipHostFree(*hp);
     *hp = nullptr;
   }
@@ -283,6 +284,16 @@ void GPUTreeLearner::UploadData() {
   args_.tile_words = tile_words;
   SetupOwnership();
   const int n_leaves = config_->num_leaves;
+  // round growth: up to round_k_ leaves expanded per round (single process; LGBM_AMD_ROUND_K,
+  // 1 = one split per step)
+  round_k_ = 1;
+  if (!distributed_ && !voting_) {
+    round_k_ = 8;
+    if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) round_k_ = std::atoi(e);
+    round_k_ = std::max(1, std::min(dev::kMaxRoundExp, round_k_));
+  }
+  hist_slots_ = round_k_ > 1 ? 2 * n_leaves : n_leaves;
+  split_rows_ = round_k_ > 1 ? 4 * n_leaves : n_leaves;
   d_tree_mask_ = Alloc<int8_t>(num_features_);
   d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
   h_node_mask_.clear();
@@ -300,15 +311,17 @@ void GPUTreeLearner::UploadData() {
   HIPCHECK(hipMemset(d_find_sub_, 0, sizeof(uint32_t) * dev::kFindSub * dev::kFindSubStride));
   d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
   d_best_ = Alloc<DeviceSplit>(n_leaves);
-  d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
-  // two step buffers (data-parallel: owner-major blocks padded to equal size)
+  d_hist_ = Alloc<long long>(static_cast<size_t>(hist_slots_) * 2 * total_bins_);
+  // two step buffers (data-parallel: owner-major blocks padded to equal size); round growth:
+  // two parities of round_k_ expansion buffers
   const int64_t scratch_stride =
       std::max<int64_t>(2 * static_cast<int64_t>(total_bins_), 2 * static_cast<int64_t>(world_) * rs_block_);
-  d_scratch_ = Alloc<long long>(2 * static_cast<size_t>(scratch_stride));
+  d_scratch_ = Alloc<long long>(std::max<size_t>(2 * static_cast<size_t>(scratch_stride),
+                                                 round_k_ > 1 ? 4 * static_cast<size_t>(round_k_) * total_bins_ : 0));
   d_scales_ = Alloc<double>(4);
   d_absmax_ = Alloc<uint32_t>(4);
   // per-feature results: [2][num_features], or rank-major [world][2][max_owned] (gathered)
-  const size_t fb_slots = std::max<size_t>(2 * static_cast<size_t>(std::max(1, num_features_)),
+  const size_t fb_slots = std::max<size_t>(2 * static_cast<size_t>(round_k_) * std::max(1, num_features_),
                                            2 * static_cast<size_t>(world_) * std::max(1, max_owned_));
   d_feat_best_ = Alloc<dev::FeatureBest>(fb_slots);
   d_feat_cat_ = Alloc<uint32_t>(fb_slots * kMaxCatWords);
@@ -340,8 +353,14 @@ void GPUTreeLearner::UploadData() {
     blk_min_rows_ = tiles >= 6 ? 1024 : tiles > 1 ? 2048 : 4096;
   }
   if (const char* e = std::getenv("LGBM_AMD_BLK_MIN_ROWS")) blk_min_rows_ = std::max(256, std::atoi(e));
-  const int hist_blocks = std::max({1, dev::HistBlocksFor(num_data_, root_grid_, rows_cap_, dev::kHistMinRows),
-                                    dev::HistBlocksFor(num_data_, split_grid_, rows_cap_, blk_min_rows_)});
+  int hist_blocks = std::max({1, dev::HistBlocksFor(num_data_, root_grid_, rows_cap_, dev::kHistMinRows),
+                              dev::HistBlocksFor(num_data_, split_grid_, rows_cap_, blk_min_rows_)});
+  if (round_k_ > 1) {
+    // a round's blocks share one size: at most split_grid (or the rows at the headroom cap)
+    // plus one partial block per expansion
+    const int64_t capped = (static_cast<int64_t>(num_data_) + rows_cap_ - 1) / rows_cap_;
+    hist_blocks = std::max<int>(hist_blocks, static_cast<int>(std::max<int64_t>(split_grid_, capped)) + dev::kMaxRoundExp);
+  }
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_ * hist_units_);
   d_root_ = Alloc<double>(4);
   d_leaf_sums_ = Alloc<double>(4);
@@ -527,8 +546,37 @@ void GPUTreeLearner::UploadData() {
       a.hist_tiles = (a.tile_w1 - a.tile_w0 + tile_words - 1) / tile_words;
     }
   }
+  a.rd = nullptr;
+  a.round_k = round_k_;
+  AllocRoundState();
   UploadInteractionMasks();
   AllocSplittable();
+}
+
+void GPUTreeLearner::AllocRoundState() {
+  const int n_leaves = config_->num_leaves;
+  dev::KArgs& a = args_;
+  a.exres = nullptr;
+  a.cbest = nullptr;
+  a.cbest_cat = nullptr;
+  a.child_cnt = nullptr;
+  if (round_k_ <= 1) return;
+  d_round_ = Alloc<dev::Round>(1);
+  d_exres_ = Alloc<dev::ExpResult>(n_leaves);
+  d_cbest_ = Alloc<dev::FeatureBest>(2 * static_cast<size_t>(n_leaves));
+  d_cbest_cat_ = Alloc<uint32_t>(2 * static_cast<size_t>(n_leaves) * kMaxCatWords);
+  const size_t cnt = 2 * static_cast<size_t>(dev::kMaxRoundExp) * (dev::kFindSub + 1) * dev::kFindSubStride;
+  d_child_cnt_ = Alloc<uint32_t>(cnt);
+  HIPCHECK(hipMemset(d_child_cnt_, 0, sizeof(uint32_t) * cnt));
+  HIPCHECK(hipMemset(d_round_, 0, sizeof(dev::Round)));
+  if (h_round_ == nullptr) {
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_round_), sizeof(dev::Round), hipHostMallocDefault));
+  }
+  a.exres = d_exres_;
+  a.cbest = d_cbest_;
+  a.cbest_cat = d_cbest_cat_;
+  a.child_cnt = d_child_cnt_;
+  round_pred_ = 0;
 }
 
 // Feature ownership of the distributed learners (reference data_parallel_tree_learner.cpp
@@ -628,14 +676,14 @@ void GPUTreeLearner::UploadInteractionMasks() {
 
 void GPUTreeLearner::AllocSplittable() {
   const int n_leaves = config_->num_leaves, nf = std::max(1, num_features_);
-  d_splittable_ = Alloc<int8_t>(static_cast<size_t>(n_leaves) * nf);
+  d_splittable_ = Alloc<int8_t>(static_cast<size_t>(std::max(n_leaves, split_rows_)) * nf);
   d_parent_flags_ = Alloc<int8_t>(nf);
   std::vector<dev::Leaf> leaves(n_leaves);
   for (int l = 0; l < n_leaves; ++l) {
     std::memset(&leaves[l], 0, sizeof(dev::Leaf));
     leaves[l].frow = l;
   }
-  HIPCHECK(hipMemsetAsync(d_splittable_, 1, static_cast<size_t>(n_leaves) * nf, stream_));
+  HIPCHECK(hipMemsetAsync(d_splittable_, 1, static_cast<size_t>(std::max(n_leaves, split_rows_)) * nf, stream_));
   HIPCHECK(hipMemcpyAsync(d_leaves_, leaves.data(), sizeof(dev::Leaf) * n_leaves, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   args_.splittable = d_splittable_;
@@ -669,7 +717,9 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
     d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
     d_best_ = Alloc<DeviceSplit>(n_leaves);
-    d_hist_ = Alloc<long long>(static_cast<size_t>(n_leaves) * 2 * total_bins_);
+    hist_slots_ = round_k_ > 1 ? 2 * n_leaves : n_leaves;
+    split_rows_ = round_k_ > 1 ? 4 * n_leaves : n_leaves;
+    d_hist_ = Alloc<long long>(static_cast<size_t>(hist_slots_) * 2 * total_bins_);
     d_leaf_values_ = Alloc<double>(n_leaves);
     if (h_rec_) (void)hipHostFree(h_rec_);
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_rec_), sizeof(dev::SplitRecord) * std::max(1, n_leaves - 1),
@@ -679,6 +729,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     args_.rec = d_rec_;
     args_.best = d_best_;
     args_.hist = d_hist_;
+    AllocRoundState();
     AllocSplittable();
     global_count_.assign(n_leaves, 0);
   }
@@ -1006,31 +1057,14 @@ void GPUTreeLearner::ReportKernelTrace(int num_splits) {
 void GPUTreeLearner::DestroyGraph() {
   if (graph_exec_ != nullptr) (void)hipGraphExecDestroy(graph_exec_);
   graph_exec_ = nullptr;
+  if (round_root_exec_ != nullptr) (void)hipGraphExecDestroy(round_root_exec_);
+  if (round_seg_exec_ != nullptr) (void)hipGraphExecDestroy(round_seg_exec_);
+  round_root_exec_ = round_seg_exec_ = nullptr;
 }
 
 // the whole tree as a stream-ordered kernel sequence (no host synchronisation inside)
 void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
-  if (use_bag_) {
-    // the whole buffer: the copy (like the tree's graph) does not depend on the bag size
-    HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * num_data_, hipMemcpyDeviceToDevice, stream_));
-  }
-  HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
-  // both step buffers start at zero; afterwards each split-scan zeroes the next one
-  // (data-parallel: the owner-major buffer is cleared before every reduction)
-  const size_t stride_bytes = sizeof(long long) * static_cast<size_t>(a.scratch_stride);
-  if (a.ktrace != nullptr) {
-    HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
-  }
-  dev::TreeBegin(a, stream_);
-  if (a.xt_cum != nullptr) {
-    HIPCHECK(hipMemsetAsync(a.xt_cum, 0, sizeof(int32_t) * config_->num_leaves * num_features_, stream_));
-  }
-  if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
-  AllreduceRoot();
-  HIPCHECK(hipMemsetAsync(d_scratch_, 0, 2 * stride_bytes, stream_));
-  dev::HistRoot(a, stream_);
-  ReduceScatterStep(0);
-  dev::FindRoot(a, stream_);
+  EnqueueRoot(a);
   // voting: the global scan of the elected features picks (pick_in_find); the local scan does not
   dev::KArgs glob = a;
   if (voting_) {
@@ -1044,6 +1078,7 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
     GatherFeatureBests();
     dev::PickStep(a, stream_, true);
   }
+  const size_t stride_bytes = sizeof(long long) * static_cast<size_t>(a.scratch_stride);
   // one split per step: the picked split applied to the leaf's rows with one child's
   // histogram (+ reduction, + reduce-scatter to the feature owners) -> split scans of both
   // children (+ the next pick; distributed: after gathering every rank's results).  The
@@ -1064,6 +1099,153 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
       dev::PickStep(a, stream_, false);
     }
   }
+}
+
+// the tree's root: row set, sums, histogram and split scan (+ the first pick / plan)
+void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
+  if (use_bag_) {
+    // the whole buffer: the copy (like the tree's graph) does not depend on the bag size
+    HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * num_data_, hipMemcpyDeviceToDevice, stream_));
+  }
+  HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
+  // both step buffers start at zero; afterwards each split-scan zeroes the next one
+  // (data-parallel: the owner-major buffer is cleared before every reduction)
+  // both step buffers start at zero (round growth: every expansion buffer of both parities)
+  const size_t stride_bytes = sizeof(long long) * static_cast<size_t>(a.scratch_stride);
+  const size_t zero_bytes = a.rd != nullptr ? sizeof(long long) * 4 * static_cast<size_t>(a.round_k) * total_bins_
+                                            : 2 * stride_bytes;
+  if (a.ktrace != nullptr) {
+    HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
+  }
+  dev::TreeBegin(a, stream_);
+  if (a.xt_cum != nullptr) {
+    HIPCHECK(hipMemsetAsync(a.xt_cum, 0, sizeof(int32_t) * config_->num_leaves * num_features_, stream_));
+  }
+  if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
+  AllreduceRoot();
+  HIPCHECK(hipMemsetAsync(d_scratch_, 0, zero_bytes, stream_));
+  dev::HistRoot(a, stream_);
+  ReduceScatterStep(0);
+  dev::FindRoot(a, stream_);
+  if (a.rd != nullptr) dev::RoundRootPlan(a, stream_);
+}
+
+// ---------------------------------------------------------------- round growth
+bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
+  if (round_k_ <= 1 || distributed_ || voting_ || d_round_ == nullptr) return false;
+  // the split order depends on more than each leaf's own rows: per-node feature samples and
+  // extra_trees draws are consumed in the sequential order, CEGB's coupled penalties change
+  // other leaves' gains, forced splits follow their own schedule
+  if (a.node_mask != nullptr || a.xt_base != nullptr || a.p.cegb || a.forced_n > 0) return false;
+  return true;
+}
+
+// rounds of kRoundSeg expansions per graph launch: the root graph (root + one segment) and as
+// many segment graphs as the previous tree needed are enqueued back to back; the host then
+// checks the Round record and adds segments until the tree is done (a finished tree's
+// kernels exit at once, so over-provisioning costs ~1.6 us per kernel)
+namespace {
+constexpr int kRoundSeg = 4;
+}
+
+int GPUTreeLearner::RunRounds(dev::KArgs a) {
+  a.rd = d_round_;
+  a.pick_in_find = 0;  // the root's split scan only publishes; RoundRootPlan picks
+  a.ktrace = nullptr;
+  const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
+  const bool use_graph = !(ng != nullptr && ng[0] == '1');
+  const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
+  auto capture = [&](hipGraphExec_t* exec, bool root) {
+    hipGraph_t g = nullptr;
+    HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    std::string why;
+    try {
+      if (root) EnqueueRoot(a);
+      for (int r = 0; r < kRoundSeg; ++r) dev::RoundStep(a, stream_);
+    } catch (const std::exception& e) {
+      why = e.what();
+    }
+    hipError_t ec = hipStreamEndCapture(stream_, &g);
+    if (why.empty() && ec == hipSuccess) ec = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    if (g != nullptr) (void)hipGraphDestroy(g);
+    if (!why.empty() || ec != hipSuccess) {
+      if (why.empty()) why = hipGetErrorString(ec);
+      Log::Fatal("device learner: capturing the round graphs failed: %s", why.c_str());
+    }
+  };
+  if (use_graph && (round_root_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
+                    round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
+    DestroyGraph();
+    capture(&round_root_exec_, true);
+    capture(&round_seg_exec_, false);
+    round_graph_rows_ = a.num_rows;
+    round_graph_identity_ = a.root_identity;
+    round_graph_root_mode_ = root_mode;
+  }
+  auto launch_seg = [&]() {
+    if (use_graph) {
+      HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
+    } else {
+      for (int r = 0; r < kRoundSeg; ++r) dev::RoundStep(a, stream_);
+    }
+  };
+  if (use_graph) {
+    HIPCHECK(hipGraphLaunch(round_root_exec_, stream_));
+  } else {
+    EnqueueRoot(a);
+    for (int r = 0; r < kRoundSeg; ++r) dev::RoundStep(a, stream_);
+  }
+  const int L = config_->num_leaves;
+  int launched = kRoundSeg;
+  const int want = round_pred_ > 0 ? round_pred_ : L - 1;
+  while (launched < want) {
+    launch_seg();
+    launched += kRoundSeg;
+  }
+  const size_t rec_bytes = sizeof(dev::SplitRecord) * std::max(1, L - 1);
+  for (;;) {
+    HIPCHECK(hipMemcpyAsync(h_round_, d_round_, sizeof(dev::Round), hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, rec_bytes, hipMemcpyDeviceToHost, stream_));
+    WatchdogSync();
+    if (h_round_->done) break;
+    if (launched > 2 * L + kRoundSeg) {
+      Log::Fatal("device learner: round growth did not finish the tree after %d rounds (%d splits)", launched,
+                 h_round_->nsplit);
+    }
+    launch_seg();
+    launched += kRoundSeg;
+  }
+  // the next tree enqueues as many rounds as this one took (rounded up to whole segments)
+  round_pred_ = h_round_->rounds + 1;
+  last_stats_.rounds = h_round_->rounds;
+  return h_round_->nsplit;
+}
+
+// a leaf's raw histogram: its slot, or -- for a leaf whose pending expansion reused its slot
+// for the subtracted child -- the sum of its children's slots (self checks only)
+void GPUTreeLearner::ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const {
+  const size_t nh = 2 * static_cast<size_t>(total_bins_);
+  raw->assign(nh, 0);
+  bool children = false;
+  dev::ExpResult r{};
+  if (lf.expanded && d_exres_ != nullptr) {
+    HIPCHECK(hipMemcpy(&r, d_exres_ + leaf, sizeof(r), hipMemcpyDeviceToHost));
+    const int md = config_->min_data_in_leaf;
+    const int lc = r.total_left, rc = r.count - r.total_left;
+    const bool skip = (config_->max_depth > 0 && r.lr[0].depth >= config_->max_depth) || (lc < 2 * md && rc < 2 * md);
+    children = !skip;
+  }
+  if (!children) {
+    HIPCHECK(hipMemcpy(raw->data(), d_hist_ + static_cast<size_t>(lf.slot) * nh, sizeof(long long) * nh,
+                       hipMemcpyDeviceToHost));
+    return;
+  }
+  std::vector<long long> other(nh);
+  HIPCHECK(hipMemcpy(raw->data(), d_hist_ + static_cast<size_t>(r.lr[0].slot) * nh, sizeof(long long) * nh,
+                     hipMemcpyDeviceToHost));
+  HIPCHECK(hipMemcpy(other.data(), d_hist_ + static_cast<size_t>(r.lr[1].slot) * nh, sizeof(long long) * nh,
+                     hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < nh; ++i) (*raw)[i] += other[i];
 }
 
 // voting: proposals -> allgather -> election + elected local histograms -> all-reduce
@@ -1135,70 +1317,86 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     a.root_identity = 1;
     root_rows_ = num_data_;
   }
-  // the tree's fixed kernel sequence (~4 launches per split) is replayed from a hipGraph:
-  // eager launches are host-bound at ~4 us each, longer than most of these kernels.  With
-  // data-parallel training the per-split RCCL all-reduces are captured into the same graph
-  // (they are stream-ordered; every rank enqueues the same collectives either way); with
-  // host collectives (no device communicator) the tree is launched eagerly.
-  const bool distributed = distributed_;
-  DeviceComm* dcomm = distributed ? Network::device_comm() : nullptr;
-  const bool dev_comm = dcomm != nullptr && dcomm->CaptureSafe();
-  const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
-  const char* gc = std::getenv("LGBM_AMD_GRAPH_COLLECTIVES");
-  const bool graph_collectives = dev_comm && !(gc != nullptr && gc[0] == '0') && !graph_capture_failed_;
-  const bool use_graph = (!distributed || graph_collectives) && !(ng != nullptr && ng[0] == '1');
-  bool launched = false;
-  if (a.p.cegb && cegb_) {  // the model-wide used-feature flags of the host CEGB state
-    h_cegb_used_ = cegb_->used_in_split();
-    h_cegb_used_.resize(std::max(1, num_features_), 0);
-    HIPCHECK(hipMemcpyAsync(d_cegb_used_, h_cegb_used_.data(), h_cegb_used_.size(), hipMemcpyHostToDevice, stream_));
+  last_stats_.rounds = 0;
+  const bool rounds = RoundGrowth(a);
+  if (!rounds && last_tree_rounds_) {
+    // one split per step after round trees: splittable rows follow the leaf ids again
+    std::vector<dev::Leaf> lv(config_->num_leaves);
+    HIPCHECK(hipMemcpyAsync(lv.data(), d_leaves_, sizeof(dev::Leaf) * lv.size(), hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipStreamSynchronize(stream_));
+    for (int l = 0; l < config_->num_leaves; ++l) lv[l].frow = l;
+    HIPCHECK(hipMemcpy(d_leaves_, lv.data(), sizeof(dev::Leaf) * lv.size(), hipMemcpyHostToDevice));
   }
-  if (use_graph) {
-    const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
-    if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
-        graph_root_mode_ != root_mode || graph_xt_ != (xt ? 1 : 0)) {
-      DestroyGraph();
-      hipGraph_t g = nullptr;
-      HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-      std::string why;
-      try {
-        EnqueueTree(a);
-      } catch (const std::exception& e) {
-        why = e.what();
+  last_tree_rounds_ = rounds;
+  int num_splits = 0;
+  if (rounds) {
+    num_splits = RunRounds(a);
+  } else {
+    // the tree's fixed kernel sequence (~4 launches per split) is replayed from a hipGraph:
+    // eager launches are host-bound at ~4 us each, longer than most of these kernels.  With
+    // data-parallel training the per-split RCCL all-reduces are captured into the same graph
+    // (they are stream-ordered; every rank enqueues the same collectives either way); with
+    // host collectives (no device communicator) the tree is launched eagerly.
+    const bool distributed = distributed_;
+    DeviceComm* dcomm = distributed ? Network::device_comm() : nullptr;
+    const bool dev_comm = dcomm != nullptr && dcomm->CaptureSafe();
+    const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
+    const char* gc = std::getenv("LGBM_AMD_GRAPH_COLLECTIVES");
+    const bool graph_collectives = dev_comm && !(gc != nullptr && gc[0] == '0') && !graph_capture_failed_;
+    const bool use_graph = (!distributed || graph_collectives) && !(ng != nullptr && ng[0] == '1');
+    bool launched = false;
+    if (a.p.cegb && cegb_) {  // the model-wide used-feature flags of the host CEGB state
+      h_cegb_used_ = cegb_->used_in_split();
+      h_cegb_used_.resize(std::max(1, num_features_), 0);
+      HIPCHECK(hipMemcpyAsync(d_cegb_used_, h_cegb_used_.data(), h_cegb_used_.size(), hipMemcpyHostToDevice, stream_));
+    }
+    if (use_graph) {
+      const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
+      if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
+          graph_root_mode_ != root_mode || graph_xt_ != (xt ? 1 : 0)) {
+        DestroyGraph();
+        hipGraph_t g = nullptr;
+        HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+        std::string why;
+        try {
+          EnqueueTree(a);
+        } catch (const std::exception& e) {
+          why = e.what();
+        }
+        hipError_t ec = hipStreamEndCapture(stream_, &g);
+        if (why.empty() && ec == hipSuccess) ec = hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0);
+        if (g != nullptr) (void)hipGraphDestroy(g);
+        if (!why.empty() || ec != hipSuccess) {
+          if (why.empty()) why = hipGetErrorString(ec);
+          (void)hipGetLastError();
+          graph_exec_ = nullptr;
+          if (!distributed) Log::Fatal("device learner: capturing the tree graph failed: %s", why.c_str());
+          Log::Warning("device learner: capturing the RCCL collectives into the tree graph failed (%s); "
+                       "launching trees eagerly", why.c_str());
+          graph_capture_failed_ = true;
+        } else {
+          graph_rows_ = a.num_rows;
+          graph_identity_ = a.root_identity;
+          graph_root_mode_ = root_mode;
+          graph_xt_ = xt ? 1 : 0;
+        }
       }
-      hipError_t ec = hipStreamEndCapture(stream_, &g);
-      if (why.empty() && ec == hipSuccess) ec = hipGraphInstantiate(&graph_exec_, g, nullptr, nullptr, 0);
-      if (g != nullptr) (void)hipGraphDestroy(g);
-      if (!why.empty() || ec != hipSuccess) {
-        if (why.empty()) why = hipGetErrorString(ec);
-        (void)hipGetLastError();
-        graph_exec_ = nullptr;
-        if (!distributed) Log::Fatal("device learner: capturing the tree graph failed: %s", why.c_str());
-        Log::Warning("device learner: capturing the RCCL collectives into the tree graph failed (%s); "
-                     "launching trees eagerly", why.c_str());
-        graph_capture_failed_ = true;
-      } else {
-        graph_rows_ = a.num_rows;
-        graph_identity_ = a.root_identity;
-        graph_root_mode_ = root_mode;
-        graph_xt_ = xt ? 1 : 0;
+      if (graph_exec_ != nullptr) {
+        HIPCHECK(hipGraphLaunch(graph_exec_, stream_));
+        launched = true;
       }
     }
-    if (graph_exec_ != nullptr) {
-      HIPCHECK(hipGraphLaunch(graph_exec_, stream_));
-      launched = true;
+    if (!launched) EnqueueTree(a);
+    HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
+                            hipMemcpyDeviceToHost, stream_));
+    WatchdogSync();
+    if (a.p.cegb && cegb_) {
+      HIPCHECK(hipMemcpy(h_cegb_used_.data(), d_cegb_used_, h_cegb_used_.size(), hipMemcpyDeviceToHost));
+      cegb_->set_used_in_split(std::vector<char>(h_cegb_used_.begin(), h_cegb_used_.begin() + num_features_));
     }
+    num_splits = h_step_->nsplit;
   }
-  if (!launched) EnqueueTree(a);
-  HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
-                          hipMemcpyDeviceToHost, stream_));
-  WatchdogSync();
-  if (a.p.cegb && cegb_) {
-    HIPCHECK(hipMemcpy(h_cegb_used_.data(), d_cegb_used_, h_cegb_used_.size(), hipMemcpyDeviceToHost));
-    cegb_->set_used_in_split(std::vector<char>(h_cegb_used_.begin(), h_cegb_used_.begin() + num_features_));
-  }
-  const int num_splits = h_step_->nsplit;
   last_stats_.device_mode = true;
   last_stats_.splits = num_splits;
   // every step's collectives run (exiting early once the tree is done): the sequence is fixed
@@ -1220,9 +1418,9 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       for (int k = 0; k < n; ++k) meta_[f].rand.NextInt(0, 2);
     }
   }
-  if (a.ktrace != nullptr) ReportKernelTrace(num_splits);
+  if (a.ktrace != nullptr && !rounds) ReportKernelTrace(num_splits);
   if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {
-    if (kp[0] == '1') KernelFloorProbe(a);
+    if (kp[0] == '1' && !rounds) KernelFloorProbe(a);
   }
   const bool track = !config_->interaction_constraints_vector.empty();
   std::unique_ptr<Tree> tree(new Tree(config_->num_leaves, track));

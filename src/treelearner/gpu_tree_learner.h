@@ -129,6 +129,30 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   template <typename T>
   T* Alloc(size_t n);
 
+  // round growth (speculative multi-leaf expansion, src/device/round_kernels.hip): up to
+  // round_k_ leaves expanded per round; trees whose split order depends on more than each
+  // leaf's own rows (per-node sampling, extra_trees draws, CEGB, forced splits) and the
+  // distributed learners grow one split per step
+  bool RoundGrowth(const dev::KArgs& a) const;
+  int RunRounds(dev::KArgs a);  // the tree's splits; h_rec_ holds their records
+  void EnqueueRoot(const dev::KArgs& a);
+  void AllocRoundState();
+  void ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const;  // (self checks)
+  int round_k_ = 1;
+  int hist_slots_ = 0;      // histogram pool slots (round growth: 2 per leaf)
+  int split_rows_ = 0;      // rows of the splittable flags (round growth: 4 per leaf)
+  dev::Round* d_round_ = nullptr;
+  dev::Round* h_round_ = nullptr;
+  dev::ExpResult* d_exres_ = nullptr;
+  dev::FeatureBest* d_cbest_ = nullptr;
+  uint32_t* d_cbest_cat_ = nullptr;
+  uint32_t* d_child_cnt_ = nullptr;
+  hipGraphExec_t round_root_exec_ = nullptr;  // root + kRoundSeg rounds
+  hipGraphExec_t round_seg_exec_ = nullptr;   // kRoundSeg rounds
+  int round_graph_rows_ = -1, round_graph_identity_ = -1, round_graph_root_mode_ = -1;
+  int round_pred_ = 0;        // rounds the next tree is expected to take (enqueued before the first check)
+  bool last_tree_rounds_ = false;
+
   void SetupOwnership();
   void GatherFeatureBests();
   void ReduceScatterStep(int parity);

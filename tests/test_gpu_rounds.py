@@ -1,0 +1,134 @@
+"""Round growth (speculative multi-leaf expansion, src/device/round_kernels.hip) grows the
+trees of one-split-per-step growth, bit for bit.
+
+Each round expands the current leaves of highest gain at once (partition + children's
+histograms and split scans); the planner replays the reference's best-first order
+(serial_tree_learner.cpp:152-202: argmax over the leaves' best splits, gain then real feature
+then leaf id) and accepts expansions while the argmax leaf is expanded.  Histograms are exact
+integer sums, so the trees -- and the whole model text -- must equal those of
+LGBM_AMD_ROUND_K=1 (the one-split-per-step kernels) for every case below.
+"""
+import json
+
+import numpy as np
+import pytest
+
+import lightgbmv1_amd as lgb
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n=40000, f=12, seed=3):
+    rng = np.random.RandomState(seed)
+    X = rng.randn(n, f).astype(np.float32)
+    X[:, 3] = np.abs(X[:, 3])
+    X[rng.rand(n) < 0.05, 5] = np.nan
+    X[:, 6] = np.where(rng.rand(n) < 0.6, 0.0, X[:, 6])
+    X[:, 7] = np.where(rng.rand(n) < 0.7, 2.5, X[:, 7])
+    X[:, 9] = rng.randint(0, 12, size=n)  # categorical
+    logit = (X[:, 0] + 0.7 * X[:, 1] * X[:, 2] - 0.5 * X[:, 3] + 0.3 * np.nan_to_num(X[:, 5]) + 0.4 * X[:, 7]
+             + 0.6 * np.isin(X[:, 9], [1, 4, 7]))
+    y = (logit + 0.3 * rng.randn(n) > 0).astype(np.float32)
+    return X, y
+
+
+def _model(monkeypatch, tmp_path, k, X, y, params, rounds=12, tag=""):
+    monkeypatch.setenv("LGBM_AMD_ROUND_K", str(k))
+    log = tmp_path / ("iters_%s_%d.jsonl" % (tag, k))
+    monkeypatch.setenv("LGBM_AMD_ITER_LOG", str(log))
+    p = {"verbose": -1, "device_type": "gpu", "seed": 11, "num_leaves": 31, "max_bin": 63}
+    p.update(params)
+    cat = p.pop("_cat", None)
+    ds = lgb.Dataset(X, y, params=p, categorical_feature=cat if cat is not None else "auto")
+    bst = lgb.train(p, ds, rounds)
+    monkeypatch.delenv("LGBM_AMD_ITER_LOG")
+    rows = [json.loads(line) for line in log.read_text().splitlines()]
+    return bst.model_to_string(), rows
+
+
+CASES = {
+    "binary": {"objective": "binary"},
+    "binary_63": {"objective": "binary", "num_leaves": 63, "max_bin": 255},
+    "categorical": {"objective": "binary", "_cat": [9]},
+    "bagging": {"objective": "binary", "bagging_fraction": 0.7, "bagging_freq": 1},
+    "goss": {"objective": "binary", "boosting": "goss", "learning_rate": 0.3},
+    "max_depth": {"objective": "binary", "num_leaves": 63, "max_depth": 5},
+    "min_data": {"objective": "binary", "min_data_in_leaf": 1500},
+    "monotone": {"objective": "binary", "monotone_constraints": [1, 0, 0, -1, 0, 0, 0, 1, 0, 0, 0, 0]},
+    "l1_reg": {"objective": "regression", "lambda_l1": 0.5, "max_delta_step": 2.0, "path_smooth": 1.0},
+    "interaction": {"objective": "binary", "interaction_constraints": [[0, 1, 2], [3, 4, 5, 6, 7], [8, 9, 10, 11]]},
+    "wide": {"objective": "binary", "gpu_use_dp": True},
+    "multiclass": {"objective": "multiclass", "num_class": 3},
+    "quantile": {"objective": "quantile", "alpha": 0.3},
+    "ff_bytree": {"objective": "binary", "feature_fraction": 0.6},
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_round_growth_equals_one_split_per_step(case, monkeypatch, tmp_path, gpu_available):
+    X, y = _data()
+    params = dict(CASES[case])
+    if params["objective"] == "multiclass":
+        y = np.digitize(X[:, 0] + 0.5 * X[:, 1], [-0.5, 0.5]).astype(np.float32)
+    elif params["objective"] in ("regression", "quantile"):
+        y = (X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.2 * np.random.RandomState(4).randn(len(y))).astype(np.float32)
+    base, base_rows = _model(monkeypatch, tmp_path, 1, X, y, params, tag=case)
+    spec, spec_rows = _model(monkeypatch, tmp_path, 8, X, y, params, tag=case)
+    assert all(r == 0 for row in base_rows for r in row["rounds"])
+    # round growth ran (device-resident) and needed fewer rounds than splits
+    rounds = [r for row in spec_rows for r in row["rounds"]]
+    splits = [lv - 1 for row in spec_rows for lv in row["leaves"]]
+    assert all(row["device_resident"][0] for row in spec_rows)
+    assert all(r > 0 for r, s in zip(rounds, splits) if s > 0)
+    if case in ("binary", "binary_63"):
+        assert sum(rounds) < 0.7 * sum(splits), (rounds, splits)
+    assert base == spec
+
+
+@pytest.mark.parametrize("k", [2, 5, 16])
+def test_round_width_does_not_change_trees(k, monkeypatch, tmp_path, gpu_available):
+    X, y = _data(seed=8)
+    params = {"objective": "binary", "num_leaves": 127, "min_data_in_leaf": 5}
+    base, _ = _model(monkeypatch, tmp_path, 1, X, y, params, rounds=6, tag="w")
+    spec, rows = _model(monkeypatch, tmp_path, k, X, y, params, rounds=6, tag="w")
+    assert base == spec
+    assert all(r > 0 for row in rows for r in row["rounds"])
+
+
+def test_round_growth_many_row_blocks(monkeypatch, tmp_path, gpu_available):
+    """Leaves of many row blocks: the round's reduce kernel (chunks combined with atomics into
+    the parity buffers the previous round's scans zeroed) instead of direct partial sums."""
+    X, y = _data(n=600000, seed=9)
+    params = {"objective": "binary", "num_leaves": 63, "max_bin": 255, "bagging_fraction": 0.9, "bagging_freq": 1}
+    base, _ = _model(monkeypatch, tmp_path, 1, X, y, params, rounds=5, tag="big")
+    spec, rows = _model(monkeypatch, tmp_path, 8, X, y, params, rounds=5, tag="big")
+    assert [lv for row in rows for lv in row["leaves"]] == [63] * 5
+    assert base == spec
+
+
+def test_round_growth_sparse_rows(monkeypatch, tmp_path, gpu_available):
+    """Row-sparse storage and EFB bundles through the round kernels."""
+    rng = np.random.RandomState(21)
+    n = 30000
+    X = np.where(rng.rand(n, 40) < 0.1, rng.randn(n, 40), 0.0)
+    X[:, :4] = rng.randn(n, 4)
+    y = (X[:, 0] + X[:, 1] * X[:, 2] + X[:, 4:20].sum(1) + 0.3 * rng.randn(n) > 0).astype(np.float32)
+    params = {"objective": "binary", "num_leaves": 63, "max_bin_by_feature": [511] + [63] * 39}
+    monkeypatch.setenv("LGBM_AMD_SPARSE_ROWS", "1")
+    base, _ = _model(monkeypatch, tmp_path, 1, X, y, params, rounds=8, tag="sp")
+    spec, _ = _model(monkeypatch, tmp_path, 8, X, y, params, rounds=8, tag="sp")
+    assert base == spec
+
+
+def test_round_growth_self_check(monkeypatch, gpu_available):
+    """Every leaf's device best split against the CPU split finder on the device histograms
+    (pending expansions: the leaf's histogram is the sum of its children's slots)."""
+    from lightgbmv1_amd import _native as nat
+    monkeypatch.setenv("LGBM_AMD_ROUND_K", "8")
+    X, y = _data(seed=5)
+    p = {"objective": "binary", "verbose": -1, "device_type": "gpu", "num_leaves": 63, "max_bin": 63, "seed": 3}
+    bst = lgb.train(p, lgb.Dataset(X, y, params=p), 3, keep_training_booster=True)
+    res = json.loads(nat.read_string(lambda size, need, buf: nat.call(
+        "LGBM_AMD_BoosterDeviceCheckSplits", bst.handle, size, need, buf), 1 << 16))
+    assert res["device_mode"] and res["checked"] > 0
+    assert res["mismatched"] == 0, res
