@@ -121,6 +121,7 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpGradients(const char* params, const float* label
     g.grad = d_grad;
     g.hess = d_hess;
     g.gh = nullptr;
+    g.gh_stride = 1;
     g.max_parts = nullptr;
     g.root_parts = nullptr;
     dev::Gradients(g, nullptr);

@@ -48,8 +48,13 @@ __device__ __forceinline__ int RootRows(const KArgs& a) { return a.num_rows_dev 
 // bin of a storage column for `row` in the row-major matrix, from the group's byte offset
 // in a row and its width (Feature::gbyte / gwide)
 __device__ __forceinline__ uint32_t RowBin(const KArgs& a, int64_t row, int gbyte, int gwide) {
-  const uint8_t* p = static_cast<const uint8_t*>(a.bins) + row * (4 * static_cast<int64_t>(a.words_per_row)) + gbyte;
+  const uint8_t* p = static_cast<const uint8_t*>(a.bins) + row * (4 * static_cast<int64_t>(a.row_words)) + gbyte;
   return gwide ? static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(p)) : static_cast<uint32_t>(*p);
+}
+
+// (g, h) of a row (KArgs::gh_stride)
+__device__ __forceinline__ float2 GhAt(const KArgs& a, int64_t row) {
+  return reinterpret_cast<const float2*>(a.gh)[row * a.gh_stride];
 }
 
 // the split column's bin for the partition: from the column-major copy when there is one,

@@ -28,11 +28,6 @@ namespace dev {
 
 namespace {
 
-#ifndef LGBM_ROOT_ROWS
-#define LGBM_ROOT_ROWS 8
-#endif
-constexpr int kRowsInFlight = LGBM_ROOT_ROWS;  // independent row gathers per thread
-
 template <int MODE>
 __device__ __forceinline__ void HistRowSet(const KArgs& a, int* begin, int* count, const int32_t** src) {
   if (MODE == 0) {
@@ -44,67 +39,6 @@ __device__ __forceinline__ void HistRowSet(const KArgs& a, int* begin, int* coun
     *count = a.num_rows;
     *src = a.idx;
   }
-}
-
-__device__ __forceinline__ void LoadRowIdx(const int32_t* src, int i, int r1, int rpp, int* r) {
-#pragma unroll
-  for (int k = 0; k < kRowsInFlight; ++k) {
-    const int ii = i + k * rpp;
-    r[k] = ii < r1 ? (src ? src[ii] : ii) : -1;
-  }
-}
-
-// one row block [r0, r1) of one column tile -> its partial histogram `out`.  The index
-// loads of each batch are issued one batch ahead (the first ones while the LDS is cleared).
-template <int MODE, int GPW, int UNITS>
-__device__ __forceinline__ void HistBlock(const KArgs& a, unsigned long long* lds, const int32_t* src, int r0, int r1,
-                                          const TileCtx& t, unsigned long long* out) {
-  const bool active = t.rs < t.rpp;
-  int i = r0 + t.rs;
-  int r[kRowsInFlight];
-  if (active) LoadRowIdx(src, i, r1, t.rpp, r);
-  __syncthreads();  // LDS reuse across row blocks
-  for (int j = threadIdx.x; j < UNITS * t.nbins; j += kHistThreads) lds[j] = 0ull;
-  __syncthreads();
-  if (active) {
-    const int w = t.w0 + t.q;
-    const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
-    const float2* gh = reinterpret_cast<const float2*>(a.gh);
-    const int64_t wpr = a.words_per_row;
-    const bool write_iota = MODE == 0 && src == nullptr && t.q == 0 && blockIdx.y == 0;
-    const int stride = kRowsInFlight * t.rpp;
-    for (; i < r1; i += stride) {
-      if (write_iota) {
-#pragma unroll
-        for (int k = 0; k < kRowsInFlight; ++k) {
-          if (r[k] >= 0) a.idx[i + k * t.rpp] = r[k];
-        }
-      }
-      float2 v[kRowsInFlight];
-      int rn[kRowsInFlight];
-      if constexpr (GPW == kSparseGPW) {
-#pragma unroll
-        for (int k = 0; k < kRowsInFlight; ++k) v[k] = gh[r[k] >= 0 ? r[k] : 0];
-        LoadRowIdx(src, i + stride, r1, t.rpp, rn);
-        AddSparseRows<kRowsInFlight, UNITS>(a, lds, t, r, v);
-      } else {
-        uint32_t wd[kRowsInFlight];
-#pragma unroll
-        for (int k = 0; k < kRowsInFlight; ++k) {
-          const int rr = r[k] >= 0 ? r[k] : 0;
-          v[k] = gh[rr];
-          wd[k] = r[k] >= 0 ? bins32[rr * wpr + w] : 0u;  // word 0: every bin skipped
-        }
-        LoadRowIdx(src, i + stride, r1, t.rpp, rn);  // next batch, in flight during the atomics
-#pragma unroll
-        for (int k = 0; k < kRowsInFlight; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
-      }
-#pragma unroll
-      for (int k = 0; k < kRowsInFlight; ++k) r[k] = rn[k];
-    }
-  }
-  __syncthreads();
-  for (int j = threadIdx.x; j < UNITS * t.nbins; j += kHistThreads) out[j] = lds[j];
 }
 
 template <int MODE, int GPW, int UNITS>
@@ -120,7 +54,7 @@ __global__ __launch_bounds__(kHistThreads) void k_hist(KArgs a) {
   const int chunk = (count + nblk - 1) / nblk;
   const size_t pstride = static_cast<size_t>(UNITS) * a.p.total_bins;
   for (int kb = blockIdx.x; kb < nblk; kb += gridDim.x) {
-    HistBlock<MODE, GPW, UNITS>(a, lds, src, begin + kb * chunk, min(begin + count, begin + kb * chunk + chunk), t,
+    HistBlock<MODE == 0, GPW, UNITS>(a, lds, src, begin + kb * chunk, min(begin + count, begin + kb * chunk + chunk), t,
                                 a.partials + kb * pstride + static_cast<size_t>(UNITS) * t.lo_bin);
   }
 }

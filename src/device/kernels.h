@@ -45,7 +45,12 @@ struct KArgs {
   // word), or mixed (0): each word holds 8-bit groups or 16-bit groups only, in group order
   // (a 16-bit group starts a new word), word_g0 / word_wide describe the words
   int32_t bin_bytes;
-  int32_t words_per_row;     // 32-bit words per row
+  int32_t words_per_row;     // 32-bit words of bins per row
+  // 32-bit words between consecutive rows of `bins` (>= words_per_row).  With gh_stride > 1 the
+  // rows carry their (g, h) in their last two words (gh points at row 0's): a gathered row is
+  // one 64-B (or 128-B) line instead of a bins row straddling lines plus a separate (g, h) line
+  int32_t row_words;
+  int64_t gh_stride;         // GH elements between consecutive rows' (g, h): 1 (compact array) or row_words / 2
   const int32_t* word_g0;    // [words_per_row + 1] first group of each word (mixed layouts)
   const int8_t* word_wide;   // [words_per_row] word holds 16-bit groups (mixed layouts)
   // row-sparse storage (reference MultiValSparseBin, multi_val_sparse_bin.hpp): the stored
@@ -145,6 +150,9 @@ struct KArgs {
   uint32_t* cbest_cat;     // [num_leaves][2][kMaxCatWords]
   uint32_t* child_cnt;
   int32_t round_k;
+  int32_t round_grid;  // workgroups of a round's split kernel (row blocks: the round's rows / round_grid)
+  int32_t round_gr;    // independent row gathers per thread in its histogram phase (2, 4, 8)
+  int32_t round_fused;  // 1: partition + histograms in one kernel (k_round_split), 0: two (k_round_part, k_round_hist)
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)
@@ -195,7 +203,7 @@ void PrepareKernels();  // per-kernel attributes (large dynamic LDS); once per p
 void SetNumCUs(int n);
 
 // interleave (g, h); per-workgroup max|g| / max h into max_parts[PackBlocks(n)][2]
-void PackGH(const float* g, const float* h, GH* gh, int64_t n, float* max_parts, hipStream_t s);
+void PackGH(const float* g, const float* h, GH* gh, int64_t gh_stride, int64_t n, float* max_parts, hipStream_t s);
 int PackBlocks(int64_t n);
 // fixed-point scales of this tree from absmax: packed (hist_units 1) scales leave headroom
 // for rows_cap rows per row block; wide ones (2) quantise each row to 31 bits of max|g|
@@ -283,7 +291,8 @@ struct GradArgs {
   const double* score;       // [num_class][num_data]
   float* grad;
   float* hess;
-  GH* gh;                    // optional fused packing (one model per iteration):
+  GH* gh;                    // optional fused packing (one model per iteration; rows gh_stride apart):
+  int64_t gh_stride;
   float* max_parts;          //   interleaved (g, h), per-workgroup max|g| / max h and
   double* root_parts;        //   (sum g, sum h), [GradientBlocks][2] each
 };

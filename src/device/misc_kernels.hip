@@ -17,12 +17,12 @@ int HistGridBlocks() { return 2 * g_num_cus; }
 // (g, h) interleaved so a gathered row costs one 8-byte load; also the per-workgroup max|g|
 // / max h of the tree (reduced by k_reduce_parts: no contended atomics)
 __global__ __launch_bounds__(256) void k_pack_gh(const float* __restrict__ g, const float* __restrict__ h,
-                                                 float2* __restrict__ gh, int64_t n, float* max_parts) {
+                                                 float2* __restrict__ gh, int64_t stride, int64_t n, float* max_parts) {
   float mg = 0.f, mh = 0.f;
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const float a = g[i], b = h[i];
-    gh[i] = make_float2(a, b);
+    gh[i * stride] = make_float2(a, b);
     mg = fmaxf(mg, fabsf(a));
     mh = fmaxf(mh, fabsf(b));
   }
@@ -51,8 +51,8 @@ int PackBlocks(int64_t n) {
   return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4 * NumCUs())));
 }
 
-void PackGH(const float* g, const float* h, GH* gh, int64_t n, float* max_parts, hipStream_t s) {
-  hipLaunchKernelGGL(k_pack_gh, dim3(PackBlocks(n)), dim3(256), 0, s, g, h, reinterpret_cast<float2*>(gh), n,
+void PackGH(const float* g, const float* h, GH* gh, int64_t gh_stride, int64_t n, float* max_parts, hipStream_t s) {
+  hipLaunchKernelGGL(k_pack_gh, dim3(PackBlocks(n)), dim3(256), 0, s, g, h, reinterpret_cast<float2*>(gh), gh_stride, n,
                      max_parts);
 }
 
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void k_root_sum(KArgs a) {
   const int n = RootRows(a);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const int r = a.root_identity ? i : a.idx[i];
-    const float2 v = reinterpret_cast<const float2*>(a.gh)[r];
+    const float2 v = GhAt(a, r);
     sg += v.x;
     shh += v.y;
   }

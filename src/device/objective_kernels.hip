@@ -163,7 +163,7 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
       ga.grad[i] = gf;
       ga.hess[i] = hf;
       if (ga.gh != nullptr) {
-        reinterpret_cast<float2*>(ga.gh)[i] = make_float2(gf, hf);
+        reinterpret_cast<float2*>(ga.gh)[i * ga.gh_stride] = make_float2(gf, hf);
         mg = fmaxf(mg, fabsf(gf));
         mh = fmaxf(mh, fabsf(hf));
         sg += gf;

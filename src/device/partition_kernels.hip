@@ -206,8 +206,7 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
       if (HIST && t.rs < t.rpp) {
         const int wi = t.w0 + t.q;
         const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
-        const float2* gh = reinterpret_cast<const float2*>(a.gh);
-        const int64_t wpr = a.words_per_row;
+        const int64_t wpr = a.row_words;
         for (int j0 = t.rs; j0 < nh; j0 += GR * t.rpp) {
           int rr[GR];
 #pragma unroll
@@ -218,7 +217,7 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
           float2 v[GR];
           if constexpr (GPW == kSparseGPW) {
 #pragma unroll
-            for (int k = 0; k < GR; ++k) v[k] = gh[rr[k] >= 0 ? rr[k] : 0];
+            for (int k = 0; k < GR; ++k) v[k] = GhAt(a, rr[k] >= 0 ? rr[k] : 0);
             if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);
             AddSparseRows<GR, UNITS>(a, lds, t, rr, v);
           } else {
@@ -226,7 +225,7 @@ __global__ __launch_bounds__(kPartThreads) void k_split(KArgs a) {
 #pragma unroll
             for (int k = 0; k < GR; ++k) {
               const int x = rr[k] >= 0 ? rr[k] : 0;
-              v[k] = gh[x];
+              v[k] = GhAt(a, x);
               wd[k] = rr[k] >= 0 ? bins32[x * wpr + wi] : 0u;  // word 0: every bin skipped
             }
             if (tr && j0 == t.rs) KTrace(a, ts, kTrSplitGather);

@@ -238,8 +238,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
       if (t.rs < t.rpp) {
         const int wi = t.w0 + t.q;
         const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
-        const float2* gh = reinterpret_cast<const float2*>(a.gh);
-        const int64_t wpr = a.words_per_row;
+        const int64_t wpr = a.row_words;
         for (int j0 = t.rs; j0 < nh; j0 += GR * t.rpp) {
           int rr[GR];
 #pragma unroll
@@ -250,14 +249,14 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
           float2 v[GR];
           if constexpr (GPW == kSparseGPW) {
 #pragma unroll
-            for (int k = 0; k < GR; ++k) v[k] = gh[rr[k] >= 0 ? rr[k] : 0];
+            for (int k = 0; k < GR; ++k) v[k] = GhAt(a, rr[k] >= 0 ? rr[k] : 0);
             AddSparseRows<GR, UNITS>(a, lds, t, rr, v);
           } else {
             uint32_t wd[GR];
 #pragma unroll
             for (int k = 0; k < GR; ++k) {
               const int x = rr[k] >= 0 ? rr[k] : 0;
-              v[k] = gh[x];
+              v[k] = GhAt(a, x);
               wd[k] = rr[k] >= 0 ? bins32[x * wpr + wi] : 0u;
             }
 #pragma unroll
@@ -281,6 +280,210 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
   }
 }
 
+// ----------------------------------------------------------------- k_round_part / k_round_hist
+// The same round as k_round_split in two streaming kernels (KArgs::round_fused = 0): the
+// partition alone (index + split-column byte per row, ballots, one reservation per side and
+// sub-tile, no LDS histogram), then the histograms of the histogrammed children, whose rows
+// are now one contiguous range of the other index buffer each -- row blocks of rpb rows read
+// with kRowsInFlight independent gathers per thread, like the root histogram.  Block k of
+// expansion j's child is partial blk_off[j] + k (blk_off reserves ceil(parent rows / rpb)).
+__device__ __forceinline__ int RoundHistRows(const Round* rd, int j, int* begin) {
+  const ExpPlan& e = rd->e[j];
+  const int tl = rd->cur[j][0];
+  *begin = e.part_begin + (e.hist_left ? 0 : tl);
+  return e.hist_left ? tl : e.part_count - tl;
+}
+// row blocks of expansion j's histogram (fused: blocks of the parent's rows)
+__device__ __forceinline__ int RoundHistBlocks(const KArgs& a, const Round* rd, int j) {
+  if (a.round_fused) return rd->e[j].nblk;
+  int b;
+  const int h = RoundHistRows(rd, j, &b);
+  return (h + rd->rpb - 1) / rd->rpb;
+}
+
+__global__ __launch_bounds__(kPartThreads) void k_round_part(KArgs a) {
+  __shared__ SplitExp ex[kMaxRoundExp];
+  __shared__ uint32_t cat_bits[kMaxRoundExp][kMaxCatWords];
+  __shared__ int wl[kSplitRows][kRPartWaves];
+  __shared__ int lpre[kSplitRows][kRPartWaves];
+  __shared__ int base[2];
+  Round* rd = a.rd;
+  const int done = rd->done;
+  const int nexp = rd->nexp, nblk = rd->nblk, rpb = rd->rpb;
+  if (done || nexp <= 0 || static_cast<int>(blockIdx.x) >= nblk) return;
+  if (threadIdx.x < static_cast<unsigned>(nexp)) {
+    const ExpPlan& e = rd->e[threadIdx.x];
+    SplitExp x;
+    x.pb = e.part_begin;
+    x.pc = e.part_count;
+    x.src = e.src_buf;
+    x.blk_off = e.blk_off;
+    x.nblk = e.nblk;
+    x.hl = e.hist_left;
+    x.single = e.nblk == 1 && e.part_count <= kSplitSub;
+    x.fbyte = e.feat.gbyte;
+    x.fwide = e.feat.gwide;
+    x.fcol = e.feat.col_off;
+    x.sub_lo = e.feat.sub_lo;
+    x.sub_hi = e.feat.sub_hi;
+    x.offset = e.feat.offset;
+    x.mfb = e.feat.mfb;
+    x.r.threshold = e.split.threshold;
+    x.r.default_left = e.split.default_left;
+    x.r.is_cat = e.split.is_categorical;
+    x.r.missing_type = e.feat.missing_type;
+    x.r.default_bin = e.feat.default_bin;
+    x.r.max_bin = e.feat.num_bin - 1;
+    ex[threadIdx.x] = x;
+  }
+  for (int i = threadIdx.x; i < nexp * kMaxCatWords; i += kPartThreads) {
+    const int j = i / kMaxCatWords;
+    cat_bits[j][i % kMaxCatWords] = rd->e[j].split.is_categorical ? rd->e[j].split.cat_bits[i % kMaxCatWords] : 0u;
+  }
+  __syncthreads();
+  auto exp_of = [&](int kb) {
+    int j = 0;
+    while (j + 1 < nexp && kb >= ex[j + 1].blk_off) ++j;
+    return j;
+  };
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  int row[kSplitRows];
+  uint32_t gb[kSplitRows];
+  auto load_rows = [&](int jn, int t0n, int r1n, int* rr) {
+    const int vn = min(kSplitSub, r1n - t0n);
+    const int32_t* s = ex[jn].src ? a.tmp : a.idx;
+    const int pbn = ex[jn].pb;
+#pragma unroll
+    for (int k = 0; k < kSplitRows; ++k) {
+      const int i = k * kPartThreads + threadIdx.x;
+      rr[k] = i < vn ? s[pbn + t0n + i] : -1;
+    }
+  };
+  auto col_bins = [&](int jn, const int* rr, uint32_t* g) {
+#pragma unroll
+    for (int k = 0; k < kSplitRows; ++k) g[k] = rr[k] >= 0 ? ColBin(a, rr[k], ex[jn].fbyte, ex[jn].fwide, ex[jn].fcol) : 0u;
+  };
+  {
+    const int j = exp_of(blockIdx.x);
+    const int r0 = (blockIdx.x - ex[j].blk_off) * rpb;
+    load_rows(j, r0, min(ex[j].pc, r0 + rpb), row);
+    col_bins(j, row, gb);
+  }
+  for (int kb = blockIdx.x; kb < nblk; kb += gridDim.x) {
+    const int j = exp_of(kb);
+    const SplitExp& X = ex[j];
+    const int r0 = (kb - X.blk_off) * rpb, r1 = min(X.pc, r0 + rpb);
+    Feature F;
+    F.sub_lo = X.sub_lo;
+    F.sub_hi = X.sub_hi;
+    F.offset = X.offset;
+    F.mfb = X.mfb;
+    const SplitRule r = X.r;
+    const uint32_t* cb = cat_bits[j];
+    int32_t* dst = X.src ? a.idx : a.tmp;
+    for (int t0 = r0; t0 < r1; t0 += kSplitSub) {
+      const int valid = min(kSplitSub, r1 - t0);
+      int nj = j, nt0 = t0 + kSplitSub, nr1 = r1;
+      if (nt0 >= r1) {
+        const int nkb = kb + gridDim.x;
+        if (nkb < nblk) {
+          nj = exp_of(nkb);
+          nt0 = (nkb - ex[nj].blk_off) * rpb;
+          nr1 = min(ex[nj].pc, nt0 + rpb);
+        } else {
+          nt0 = nr1 = 0;
+        }
+      }
+      int nrow[kSplitRows];
+      load_rows(nj, nt0, nr1, nrow);
+      bool left[kSplitRows];
+      unsigned long long mask[kSplitRows];
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) {
+        left[k] = row[k] >= 0 && GoesLeft(r, cb, FeatureBinOf(F, gb[k]));
+        mask[k] = __ballot(left[k]);
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < kSplitRows; ++k) wl[k][w] = __popcll(mask[k]);
+      }
+      __syncthreads();
+      if (w == 0) {
+        const int k = lane / kRPartWaves, jj = lane % kRPartWaves;
+        const int c = wl[k][jj];
+        const int ci = WavePrefixIncl(c);
+        lpre[k][jj] = ci - c;
+        const int nl = __shfl(ci, kWave - 1, kWave);
+        if (lane == 0) {
+          if (X.single) {
+            base[0] = base[1] = 0;
+            rd->cur[j][0] = nl;
+            rd->cur[j][1] = valid - nl;
+          } else {
+            base[0] = atomicAdd(&rd->cur[j][0], nl);
+            base[1] = atomicAdd(&rd->cur[j][1], valid - nl);
+          }
+        }
+      }
+      __syncthreads();
+      const int lbase = X.pb + base[0];
+      const int rbase = X.pb + X.pc - 1 - base[1];
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) {
+        if (row[k] >= 0) {
+          const int lpos = lpre[k][w] + __popcll(mask[k] & lt);
+          const int pos = k * kPartThreads + threadIdx.x;
+          if (left[k]) dst[lbase + lpos] = row[k];
+          else dst[rbase - (pos - lpos)] = row[k];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) row[k] = nrow[k];
+      col_bins(nj, row, gb);
+      __syncthreads();  // wave counts and bases are rewritten by the next sub-tile
+    }
+  }
+}
+
+template <int GPW, int UNITS>
+__global__ __launch_bounds__(kHistThreads) void k_round_hist(KArgs a) {
+  extern __shared__ unsigned long long lds[];
+  __shared__ int s_off[kMaxRoundExp + 1], s_beg[kMaxRoundExp], s_rows[kMaxRoundExp], s_buf[kMaxRoundExp],
+      s_cap[kMaxRoundExp];
+  const Round* rd = a.rd;
+  if (rd->done) return;
+  const int nexp = rd->nexp, rpb = rd->rpb;
+  if (nexp <= 0) return;
+  TileCtx t;
+  InitTile<GPW>(a, &t);
+  if (threadIdx.x == 0) {
+    int off = 0;
+    for (int j = 0; j < nexp; ++j) {
+      int b;
+      const int h = RoundHistRows(rd, j, &b);
+      s_off[j] = off;
+      s_beg[j] = b;
+      s_rows[j] = h;
+      s_buf[j] = 1 - rd->e[j].src_buf;
+      s_cap[j] = rd->e[j].blk_off;
+      off += (h + rpb - 1) / rpb;
+    }
+    s_off[nexp] = off;
+  }
+  __syncthreads();
+  const int total = s_off[nexp];
+  const size_t pstride = static_cast<size_t>(UNITS) * a.p.total_bins;
+  for (int kb = blockIdx.x; kb < total; kb += gridDim.x) {
+    int j = 0;
+    while (j + 1 < nexp && kb >= s_off[j + 1]) ++j;
+    const int k = kb - s_off[j];
+    const int r0 = s_beg[j] + k * rpb, r1 = min(s_beg[j] + s_rows[j], r0 + rpb);
+    HistBlock<false, GPW, UNITS>(a, lds, s_buf[j] ? a.tmp : a.idx, r0, r1, t,
+                                 a.partials + static_cast<size_t>(s_cap[j] + k) * pstride + static_cast<size_t>(UNITS) * t.lo_bin);
+  }
+}
+
 // --------------------------------------------------------------------------- k_round_reduce
 // grid (bins / 256, kReduceRows, round_k): the partials of expansion blockIdx.z with more than
 // kDirectChunk row blocks summed into its reduce buffer (pre-zeroed by the previous round's
@@ -291,7 +494,7 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
   if (rd->done) return;
   const int j = blockIdx.z;
   if (j >= rd->nexp) return;
-  const int nblk = rd->e[j].nblk;
+  const int nblk = RoundHistBlocks(a, rd, j);
   if (nblk <= kDirectChunk) return;  // summed by the split scan
   if (static_cast<int>(blockIdx.y) * kReduceChunk >= nblk) return;
   const int bin = blockIdx.x * blockDim.x + threadIdx.x;
@@ -436,7 +639,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const bool is_hist = (lr == 0) == (E.hist_left != 0);
   const int slot = is_hist ? E.slot_new : E.slot_parent;
   const int frow = E.frow_child[lr];
-  const int nblk = E.nblk, blk_off = E.blk_off;
+  const int nblk = RoundHistBlocks(a, rd, j), blk_off = E.blk_off;
   const int8_t parent_ok = a.splittable[static_cast<size_t>(E.frow_parent) * NF + f];
   FeatureBest* fb_out = &a.feat_best[static_cast<size_t>(y) * NF + f];
   int8_t* flags = a.splittable + static_cast<size_t>(frow) * NF;
@@ -620,21 +823,70 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
 }
 
 // ----------------------------------------------------------------------------- k_round_plan
+// ordered keys of the replay's argmax (SplitInfo order over leaves): larger gain first (NaN =
+// -inf), then smaller real feature, then lower leaf id -- two wave max-reductions over DPP
+// lane moves instead of a shuffle butterfly carrying five values
+__device__ __forceinline__ unsigned long long GainKey(double g) {
+  if (g != g) g = -INFINITY;
+  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(g));
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ uint32_t TieKey(int rf, int leaf) {
+  const uint32_t r = rf < 0 ? 0x3fffffu : min(static_cast<uint32_t>(rf), 0x3ffffeu);
+  return ~((r << 10) | static_cast<uint32_t>(leaf));
+}
+template <typename T>
+__device__ __forceinline__ T WaveMaxDpp(T v) {  // every lane of the wave active; 0 is the identity
+  v = max(v, DppMove<0x111>(v));
+  v = max(v, DppMove<0x112>(v));
+  v = max(v, DppMove<0x114>(v));
+  v = max(v, DppMove<0x118>(v));
+  v = max(v, DppMove<0x142, 0xa>(v));
+  v = max(v, DppMove<0x143, 0xc>(v));
+  return WaveLane63(v);
+}
+// the argmax leaf among l <= s with take(l) (one wave; -1: none)
+template <typename Take>
+__device__ __forceinline__ int WaveArgmaxLeaf(const double* tg, const int* trf, int s, Take take) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long gk = 0;
+  uint32_t tk = 0;
+  for (int l = lane; l <= s; l += kWave) {
+    if (!take(l)) continue;
+    const unsigned long long k = GainKey(tg[l]);
+    const uint32_t t = TieKey(trf[l], l);
+    if (k > gk || (k == gk && t > tk)) {
+      gk = k;
+      tk = t;
+    }
+  }
+  const unsigned long long gm = WaveMaxDpp(gk);
+  if (gm == 0) return -1;
+  const uint32_t tm = WaveMaxDpp(gk == gm ? tk : 0u);
+  return static_cast<int>((~tm) & 1023u);
+}
+__device__ __forceinline__ void WaveLdsSync() {  // lane 0's LDS stores before the wave's next loads
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // One workgroup.  ROOT: the root's best split from its per-feature results (FindRoot), then
 // the first plan.  Otherwise: fold the round's partition counts into the expansions, replay
-// the best-first order, apply the accepted splits, plan the next round.
+// the best-first order (wave 0, LDS tables), apply the accepted splits, plan the next round.
+// Global loads are issued in few independent batches: every one is a ~1-2 us round trip.
 template <bool ROOT>
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
   extern __shared__ unsigned char plan_lds[];
-  __shared__ int s_go[2], s_done, s_nexp;
+  __shared__ int s_done, s_s1, s_nexp;
   __shared__ ArgC s_arg[kPlanThreads / kWave];
   __shared__ int s_pick[kMaxRoundExp];
   __shared__ int s_pc[kMaxRoundExp];
   Round* rd = a.rd;
   if (rd->done) return;
   const int L = a.p.num_leaves, NF = a.p.num_features, tid = threadIdx.x, lane = tid & 63;
-  // per-leaf tables: gain, real feature, inner feature, expanded; the expanded leaves'
-  // children (2 per leaf); the accepted leaves
+  // per-leaf tables: gain, real feature, inner feature, expanded (2: picked for the next
+  // round); the expanded leaves' children (2 per leaf); the accepted leaves
   double* tg = reinterpret_cast<double*>(plan_lds);
   double* tcg = tg + L;
   int* trf = reinterpret_cast<int*>(tcg + 2 * L);
@@ -644,8 +896,8 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
   int* tcfi = tcrf + 2 * L;
   int* acc = tcfi + 2 * L;
   const int s0 = rd->nsplit;
+  const int nexp_prev = rd->nexp;
   if (ROOT) {
-    // argmax over the root's per-feature results (side 0 of feat_best)
     ArgC c = ArgNone();
     for (int f = tid; f < NF; f += kPlanThreads) {
       const FeatureBest& fb = a.feat_best[f];
@@ -673,71 +925,86 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
       tex[0] = 0;
     }
   } else {
-    if (tid < rd->nexp) a.exres[rd->e[tid].leaf].total_left = rd->cur[tid][0];
+    // one batch of independent loads: every leaf's best, expanded flag and children's bests
+    if (tid < nexp_prev) a.exres[rd->e[tid].leaf].total_left = rd->cur[tid][0];
     for (int l = tid; l <= s0 && l < L; l += kPlanThreads) {
-      tg[l] = a.best[l].gain;
-      trf[l] = a.best[l].real_feature;
-      tfi[l] = a.best[l].feature;
+      const double g = a.best[l].gain;
+      const int rf = a.best[l].real_feature, fi = a.best[l].feature;
       const int e = a.leaves[l].expanded;
+      const FeatureBest& c0 = a.cbest[2 * l];
+      const FeatureBest& c1 = a.cbest[2 * l + 1];
+      const double g0 = c0.gain, g1 = c1.gain;
+      const int r0 = c0.real_feature, r1 = c1.real_feature, f0 = c0.feature, f1 = c1.feature;
+      tg[l] = g;
+      trf[l] = rf;
+      tfi[l] = fi;
       tex[l] = e;
-      if (e) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-          const FeatureBest& cb = a.cbest[2 * l + k];
-          tcg[2 * l + k] = cb.gain;
-          tcrf[2 * l + k] = cb.real_feature;
-          tcfi[2 * l + k] = cb.feature;
-        }
-      }
+      tcg[2 * l] = g0;
+      tcg[2 * l + 1] = g1;
+      tcrf[2 * l] = r0;
+      tcrf[2 * l + 1] = r1;
+      tcfi[2 * l] = (f0 >= 0 && g0 != -INFINITY) ? f0 : -1;
+      tcfi[2 * l + 1] = (f1 >= 0 && g1 != -INFINITY) ? f1 : -1;
     }
   }
-  if (tid == 0) s_done = 0;
-  if (tid < kMaxRoundExp) s_pick[tid] = -1;
   __syncthreads();
-  // replay of the sequential order: the argmax leaf (gain, real feature, leaf id) is split
-  // while its expansion is computed.  Wave 0 decides; the decision flag is double-buffered by
-  // iteration (a slow wave may still read the previous one while wave 0 writes the next)
-  int s = s0;
-  for (int it = 0;; ++it) {
-    if (s >= L - 1) {
-      if (tid == 0) s_done = 1;
-      break;
-    }
-    if (tid < kWave) {
-      ArgC c = ArgNone();
-      for (int l = lane; l <= s; l += kWave) {
-        if (c.idx < 0 || SplitBetter(tg[l], trf[l], c.g, c.rf)) {
-          c.g = tg[l];
-          c.rf = trf[l];
-          c.idx = l;
-        }
+  // replay of the sequential order by wave 0: the argmax leaf is split while its expansion is
+  // computed; its children (leaf ids w and s + 1) join the tables
+  if (tid < kWave) {
+    int s = s0, done = 0;
+    for (;;) {
+      if (s >= L - 1) {
+        done = 1;
+        break;
       }
-      c = ArgWaveBest(c);
+      const int w = WaveArgmaxLeaf(tg, trf, s, [](int) { return true; });
+      if (!(tg[w] > 0.0 && tfi[w] >= 0)) {
+        done = 1;
+        break;
+      }
+      if (!tex[w]) break;
       if (lane == 0) {
-        const int w = c.idx;
-        const bool ok = c.g > 0.0 && tfi[w] >= 0;
-        const int go = ok && tex[w];
-        s_go[it & 1] = go;
-        if (!ok) s_done = 1;
-        if (go) {
-          const int nl = s + 1;
-          acc[s - s0] = w;
-          tg[w] = tcg[2 * w];
-          trf[w] = tcrf[2 * w];
-          tfi[w] = tcfi[2 * w];
-          tex[w] = 0;
-          tg[nl] = tcg[2 * w + 1];
-          trf[nl] = tcrf[2 * w + 1];
-          tfi[nl] = tcfi[2 * w + 1];
-          tex[nl] = 0;
-        }
+        const int nl = s + 1;
+        acc[s - s0] = w;
+        tg[w] = tcg[2 * w];
+        trf[w] = tcrf[2 * w];
+        tfi[w] = tcfi[2 * w];
+        tex[w] = 0;
+        tg[nl] = tcg[2 * w + 1];
+        trf[nl] = tcrf[2 * w + 1];
+        tfi[nl] = tcfi[2 * w + 1];
+        tex[nl] = 0;
       }
+      WaveLdsSync();
+      ++s;
     }
-    __syncthreads();
-    if (!s_go[it & 1]) break;
-    ++s;
+    // the next round's expansions: the current unexpanded leaves of highest gain, in order
+    int n = 0;
+    if (!done) {
+      const int kmax = min(a.round_k, L - 1 - s);
+      for (; n < kmax; ++n) {
+        const int l = WaveArgmaxLeaf(tg, trf, s, [&](int m) { return tex[m] == 0 && tg[m] > 0.0 && tfi[m] >= 0; });
+        if (l < 0) break;
+        if (lane == 0) {
+          s_pick[n] = l;
+          tex[l] = 2;
+        }
+        WaveLdsSync();
+      }
+      // histogram slots / splittable rows left (bounded by construction; guarded anyway)
+      n = min(n, 2 * L - rd->next_slot);
+      n = min(n, (4 * L - rd->next_frow) / 2);
+      n = max(n, 0);
+      if (n == 0) done = 1;
+    }
+    if (lane == 0) {
+      s_s1 = s;
+      s_done = done;
+      s_nexp = done ? 0 : n;
+    }
   }
-  const int s1 = s, nacc = s - s0;
+  __syncthreads();
+  const int s1 = s_s1, nacc = s1 - s0, nexp = s_nexp;
   // apply the accepted splits: split records and children leaves, then the children's bests
   // (the record copies the parent's best first)
   constexpr int kSplitWords = sizeof(DeviceSplit) / 4;
@@ -753,7 +1020,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     rec.left_count = R.total_left;
     rec.right_count = R.count - R.total_left;
     for (int c = 0; c < 2; ++c) {
-      Leaf& lf = a.leaves[c == 0 ? w : nl];
+      Leaf lf;
       const ChildStats& cs = R.lr[c];
       lf.begin = c == 0 ? R.begin : R.begin + R.total_left;
       lf.count = c == 0 ? R.total_left : R.count - R.total_left;
@@ -770,6 +1037,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
       lf.lsum_g = lf.lsum_h = 0.0;
       lf.cmin = cs.cmin;
       lf.cmax = cs.cmax;
+      a.leaves[c == 0 ? w : nl] = lf;
     }
   }
   __syncthreads();
@@ -777,7 +1045,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     const int k = i >> 1, c = i & 1, w = acc[k];
     const FeatureBest& cb = a.cbest[2 * w + c];
     DeviceSplit* d = &a.best[c == 0 ? w : s0 + k + 1];
-    if (cb.feature >= 0 && cb.gain != -INFINITY) ToDeviceSplit(cb, a.cbest_cat + (2 * static_cast<size_t>(w) + c) * kMaxCatWords, d);
+    if (tcfi[2 * w + c] >= 0) ToDeviceSplit(cb, a.cbest_cat + (2 * static_cast<size_t>(w) + c) * kMaxCatWords, d);
     else NoSplit(d);
   }
   __syncthreads();
@@ -790,37 +1058,22 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     }
     return;
   }
-  // the next round: the current unexpanded leaves of highest gain (rank in the replay's order)
-  const int kmax = min(a.round_k, L - 1 - s1);
-  for (int l = tid; l <= s1; l += kPlanThreads) {
-    const bool cand = !tex[l] && tg[l] > 0.0 && tfi[l] >= 0;
-    if (!cand) continue;
-    int r = 0;
-    for (int m = 0; m <= s1 && r < kmax; ++m) {
-      if (m == l || tex[m] || !(tg[m] > 0.0) || tfi[m] < 0) continue;
-      if (SplitBetter(tg[m], trf[m], tg[l], trf[l]) || (!SplitBetter(tg[l], trf[l], tg[m], trf[m]) && m < l)) ++r;
-    }
-    if (r < kmax) s_pick[r] = l;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int n = 0;  // (ranks are dense: the candidates fill s_pick[0 .. min(count, kmax)))
-    while (n < kmax && s_pick[n] >= 0) ++n;
-    // histogram slots / splittable rows left (bounded by construction; guarded anyway)
-    n = min(n, 2 * L - rd->next_slot);
-    n = min(n, (4 * L - rd->next_frow) / 2);
-    s_nexp = max(n, 0);
-  }
-  __syncthreads();
-  const int nexp = s_nexp;
   const int next_slot = rd->next_slot, next_frow = rd->next_frow;
   if (tid < nexp) {
     const int j = tid, l = s_pick[j];
+    // independent loads: the leaf, its best split and the split feature's record (inner
+    // feature from the table)
     const Leaf P = a.leaves[l];
-    s_pc[j] = P.count;
-    ExpPlan& e = rd->e[j];
     const DeviceSplit& sp = a.best[l];
-    const int hl = sp.left_count <= sp.right_count ? 1 : 0;
+    const double lsg = sp.left_sum_gradient, lsh = sp.left_sum_hessian, lo = sp.left_output;
+    const double rsg = sp.right_sum_gradient, rsh = sp.right_sum_hessian, ro = sp.right_output;
+    const int lcnt = sp.left_count, rcnt = sp.right_count, mono = sp.monotone_type, iscat = sp.is_categorical;
+    const int fi = tfi[l];
+    const IcMask fmask = a.feat_icmask != nullptr ? a.feat_icmask[fi] : kIcAll;
+    ExpPlan& e = rd->e[j];
+    CopyWords(&a.feat[fi], &e.feat, 0, 1);
+    s_pc[j] = P.count;
+    const int hl = lcnt <= rcnt ? 1 : 0;
     e.leaf = l;
     e.part_begin = P.begin;
     e.part_count = P.count;
@@ -831,39 +1084,38 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     e.frow_parent = P.frow;
     e.frow_child[0] = next_frow + 2 * j;
     e.frow_child[1] = next_frow + 2 * j + 1;
-    e.feat = a.feat[sp.feature];
     // children's statistics from the split (basic monotone constraints: the mid-point bound)
     const int depth = P.depth + 1;
     double pmin = P.cmin, pmax = P.cmax, rmin = P.cmin, rmax = P.cmax;
-    if (!sp.is_categorical) {
-      const double mid = (sp.left_output + sp.right_output) / 2.0f;
-      if (sp.monotone_type < 0) {
+    if (!iscat) {
+      const double mid = (lo + ro) / 2.0f;
+      if (mono < 0) {
         pmin = fmax(pmin, mid);
         rmax = fmin(rmax, mid);
-      } else if (sp.monotone_type > 0) {
+      } else if (mono > 0) {
         pmax = fmin(pmax, mid);
         rmin = fmax(rmin, mid);
       }
     }
-    const IcMask icm = P.icmask & (a.feat_icmask != nullptr ? a.feat_icmask[sp.feature] : kIcAll);
+    const IcMask icm = P.icmask & fmask;
     ChildStats lc, rc;
-    lc.sum_g = sp.left_sum_gradient;
-    lc.sum_h = sp.left_sum_hessian;
-    lc.output = sp.left_output;
+    lc.sum_g = lsg;
+    lc.sum_h = lsh;
+    lc.output = lo;
     lc.cmin = pmin;
     lc.cmax = pmax;
-    lc.global_count = sp.left_count;
+    lc.global_count = lcnt;
     lc.depth = depth;
     lc.slot = hl ? e.slot_new : P.slot;
     lc.leaf = l;
     lc.frow = e.frow_child[0];
     lc.icmask = icm;
-    rc.sum_g = sp.right_sum_gradient;
-    rc.sum_h = sp.right_sum_hessian;
-    rc.output = sp.right_output;
+    rc.sum_g = rsg;
+    rc.sum_h = rsh;
+    rc.output = ro;
     rc.cmin = rmin;
     rc.cmax = rmax;
-    rc.global_count = sp.right_count;
+    rc.global_count = rcnt;
     rc.depth = depth;
     rc.slot = hl ? P.slot : e.slot_new;
     rc.leaf = -1;
@@ -891,7 +1143,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     // row blocks: one size for the round (at least blk_min_rows, at most the packed headroom)
     long long rows = 0;
     for (int j = 0; j < nexp; ++j) rows += s_pc[j];
-    long long rpb = (rows + a.split_grid - 1) / max(1, a.split_grid);
+    long long rpb = (rows + a.round_grid - 1) / max(1, a.round_grid);
     rpb = max(rpb, static_cast<long long>(a.blk_min_rows));
     rpb = min(rpb, static_cast<long long>(a.hist_rows_cap));
     rpb = max(rpb, 1ll);
@@ -911,11 +1163,8 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     rd->round = ROOT ? 1 : rd->round + 1;  // (parity 0 of the first round holds the root histogram)
     rd->rounds = rd->rounds + 1;
     rd->accepted_max = max(rd->accepted_max, nacc);
-    for (int j = 0; j < kMaxRoundExp; ++j) rd->cur[j][0] = rd->cur[j][1] = 0;
-    if (nexp == 0) {
-      rd->done = 1;  // (no candidate: cannot happen while the replay did not stop the tree)
-    }
   }
+  if (tid < kMaxRoundExp) rd->cur[tid][0] = rd->cur[tid][1] = 0;
 }
 
 size_t RoundPlanLds(int num_leaves) {
@@ -927,7 +1176,7 @@ namespace {
 
 template <int GR>
 void LaunchRoundSplit(const KArgs& a, hipStream_t s) {
-  const dim3 grid(a.split_grid, a.hist_tiles);
+  const dim3 grid(a.round_grid, a.hist_tiles);
   const size_t lds = sizeof(unsigned long long) * a.hist_units * static_cast<size_t>(a.tile_bins) + sizeof(int) * kSplitSub;
   if (a.sp_ptr != nullptr) {
     if (a.hist_units == 1) hipLaunchKernelGGL((k_round_split<kSparseGPW, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
@@ -992,8 +1241,22 @@ void LaunchRoundFind(const KArgs& a, hipStream_t s) {
 }  // namespace
 
 void PrepareRoundKernels(int max_lds) {
-  AllowRoundSplitLds<kRGatherNarrow>(max_lds);
-  AllowRoundSplitLds<kRGatherWide>(max_lds);
+  auto allow = [max_lds](const void* k) {
+    if (max_lds > 65536 && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, max_lds) != hipSuccess) {
+      (void)hipGetLastError();
+    }
+  };
+  allow(reinterpret_cast<const void*>(k_round_hist<4, 1>));
+  allow(reinterpret_cast<const void*>(k_round_hist<2, 1>));
+  allow(reinterpret_cast<const void*>(k_round_hist<0, 1>));
+  allow(reinterpret_cast<const void*>(k_round_hist<4, 2>));
+  allow(reinterpret_cast<const void*>(k_round_hist<2, 2>));
+  allow(reinterpret_cast<const void*>(k_round_hist<0, 2>));
+  allow(reinterpret_cast<const void*>(k_round_hist<kSparseGPW, 1>));
+  allow(reinterpret_cast<const void*>(k_round_hist<kSparseGPW, 2>));
+  AllowRoundSplitLds<2>(max_lds);
+  AllowRoundSplitLds<4>(max_lds);
+  AllowRoundSplitLds<8>(max_lds);
 }
 
 void RoundRootPlan(const KArgs& a, hipStream_t s) {
@@ -1001,8 +1264,29 @@ void RoundRootPlan(const KArgs& a, hipStream_t s) {
 }
 
 void RoundStep(const KArgs& a, hipStream_t s) {
-  if (a.sp_ptr != nullptr || a.tile_words <= kRGatherNarrowMaxWords) LaunchRoundSplit<kRGatherNarrow>(a, s);
-  else LaunchRoundSplit<kRGatherWide>(a, s);
+  if (a.round_fused) {
+    const int gr = a.round_gr > 0 ? a.round_gr
+                   : ((a.sp_ptr != nullptr || a.tile_words <= kRGatherNarrowMaxWords) ? kRGatherNarrow : kRGatherWide);
+    if (gr >= 8) LaunchRoundSplit<8>(a, s);
+    else if (gr >= 4) LaunchRoundSplit<4>(a, s);
+    else LaunchRoundSplit<2>(a, s);
+  } else {
+    hipLaunchKernelGGL(k_round_part, dim3(a.round_grid), dim3(kPartThreads), 0, s, a);
+    const dim3 grid(a.root_grid, a.hist_tiles);
+    const size_t lds = sizeof(unsigned long long) * a.hist_units * static_cast<size_t>(a.tile_bins);
+    if (a.sp_ptr != nullptr) {
+      if (a.hist_units == 1) hipLaunchKernelGGL((k_round_hist<kSparseGPW, 1>), grid, dim3(kHistThreads), lds, s, a);
+      else hipLaunchKernelGGL((k_round_hist<kSparseGPW, 2>), grid, dim3(kHistThreads), lds, s, a);
+    } else if (a.hist_units == 1) {
+      if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_hist<4, 1>), grid, dim3(kHistThreads), lds, s, a);
+      else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_hist<2, 1>), grid, dim3(kHistThreads), lds, s, a);
+      else hipLaunchKernelGGL((k_round_hist<0, 1>), grid, dim3(kHistThreads), lds, s, a);
+    } else {
+      if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_hist<4, 2>), grid, dim3(kHistThreads), lds, s, a);
+      else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_hist<2, 2>), grid, dim3(kHistThreads), lds, s, a);
+      else hipLaunchKernelGGL((k_round_hist<0, 2>), grid, dim3(kHistThreads), lds, s, a);
+    }
+  }
   const dim3 rgrid((a.p.total_bins + 255) / 256,
                    std::min(4, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk), a.round_k);
   if (a.hist_units == 1) hipLaunchKernelGGL((k_round_reduce<1>), rgrid, dim3(256), 0, s, a);

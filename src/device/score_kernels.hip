@@ -81,6 +81,7 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
   }
   __syncthreads();
   const int wpr = a.words_per_row;
+  const int64_t stride = a.row_words;
   const bool words = a.bins != nullptr;  // else row-sparse training storage: the column copy
   const bool stage_row = words && wpr <= kMaxRowWords;
   const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
@@ -91,7 +92,7 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
     int node = 0;
     if (t.num_leaves > 1) {
       if (stage_row) {
-        for (int k = 0; k < wpr; ++k) my[k] = bins32[static_cast<int64_t>(row) * wpr + k];
+        for (int k = 0; k < wpr; ++k) my[k] = bins32[static_cast<int64_t>(row) * stride + k];
       }
       while (node >= 0) {
         const NodeInfo nd = STAGED ? s_node[node] : MakeNode(a, t, node);
@@ -176,7 +177,7 @@ __global__ __launch_bounds__(kBmRowsPerBlock) void k_add_tree_score_bm(KArgs a, 
     s_right[i] = static_cast<int16_t>(t.bm_meta[i * 3 + 2]);
   }
   for (int i = threadIdx.x; i < t.num_leaves; i += blockDim.x) s_val[i] = t.leaf_value[i];
-  const int wpr = a.words_per_row;
+  const int wpr = a.row_words;  // (whole rows, (g, h) of interleaved rows included)
   const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
   const uint8_t* rows8 = reinterpret_cast<const uint8_t*>(s_rows);
   // a workgroup walks several chunks: the next chunk's row words (one contiguous run of the
@@ -223,7 +224,7 @@ __global__ __launch_bounds__(kBmRowsPerBlock) void k_add_tree_score_bm(KArgs a, 
 
 bool TreeBitmapsApply(const KArgs& a, int num_leaves) {
   const int ni = num_leaves - 1;
-  return a.bins != nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.words_per_row * 4 <= kBmMaxRowBytes;
+  return a.bins != nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.row_words * 4 <= kBmMaxRowBytes;
 }
 
 void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
@@ -241,7 +242,7 @@ void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t
     int64_t blocks64 = (num_rows + kBmRowsPerBlock - 1) / kBmRowsPerBlock;
     if (per_cu > 0) blocks64 = std::min<int64_t>(blocks64, static_cast<int64_t>(per_cu) * NumCUs());
     const int blocks = static_cast<int>(std::min<int64_t>(blocks64, 1 << 30));
-    const size_t lds = sizeof(uint32_t) * kBmRowsPerBlock * a.words_per_row;
+    const size_t lds = sizeof(uint32_t) * kBmRowsPerBlock * a.row_words;
     hipLaunchKernelGGL(k_add_tree_score_bm, dim3(blocks), dim3(kBmRowsPerBlock), lds, s, a, t, num_rows, score);
     return;
   }

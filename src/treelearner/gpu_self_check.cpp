@@ -80,7 +80,9 @@ bool GPUTreeLearner::DebugGradients(std::vector<float>* g, std::vector<float>* h
   HIPCHECK(hipSetDevice(device_id_));
   HIPCHECK(hipStreamSynchronize(stream_));
   std::vector<dev::GH> gh(static_cast<size_t>(num_data_));
-  HIPCHECK(hipMemcpy(gh.data(), d_gh_, sizeof(dev::GH) * gh.size(), hipMemcpyDeviceToHost));
+  // (rows of the bin matrix may carry their (g, h): a strided copy)
+  HIPCHECK(hipMemcpy2D(gh.data(), sizeof(dev::GH), d_gh_, sizeof(dev::GH) * static_cast<size_t>(args_.gh_stride),
+                       sizeof(dev::GH), gh.size(), hipMemcpyDeviceToHost));
   g->resize(gh.size());
   h->resize(gh.size());
   for (size_t i = 0; i < gh.size(); ++i) {

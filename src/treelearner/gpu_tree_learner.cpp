@@ -175,18 +175,36 @@ void GPUTreeLearner::UploadData() {
   HIPCHECK(hipMemcpy(d_word_wide_, h_word_wide_.data(), h_word_wide_.size(), hipMemcpyHostToDevice));
   args_.bin_bytes = bin_bytes;
   args_.words_per_row = wpr;
+  args_.row_words = wpr;
+  args_.gh_stride = 1;
   // training rows: the row-major word matrix, or row-sparse lists of stored bins (validation
   // sets always use the word layout)
   sparse_rows_ = UseSparseRows(wpr);
   d_sp_ptr_ = nullptr;
   d_sp_bin_ = nullptr;
   d_bins_ = nullptr;
+  d_gh_ = nullptr;
   if (sparse_rows_) {
     UploadSparseRows();
   } else {
-    std::vector<uint8_t> host = RowMajorBins(data_);
+    // (g, h) interleaved at the end of each row, rows padded to 64 / 128 B (or 32-B multiples
+    // when wider): a gathered row of the histogrammed child is then one cache line, where a
+    // 28-B bins row straddling lines plus a separate 8-B (g, h) line took ~2.2 lines
+    // (LGBM_AMD_GH_IN_ROWS=0: separate compact (g, h) array)
+    int row_words = wpr + 2;
+    row_words = row_words <= 16 ? 16 : (row_words <= 32 ? 32 : (row_words + 7) / 8 * 8);
+    // A/B on the headline 10M x 28 (7 bin words -> 64-B rows): 2.52 ms/iter separate, 2.71
+    // interleaved -- off by default
+    bool gh_rows = false;
+    if (const char* e = std::getenv("LGBM_AMD_GH_IN_ROWS")) gh_rows = e[0] == '1';
+    if (gh_rows) {
+      args_.row_words = row_words;
+      args_.gh_stride = row_words / 2;
+    }
+    std::vector<uint8_t> host = RowMajorBins(data_, args_.row_words);
     d_bins_ = Alloc<uint8_t>(host.size());
     HIPCHECK(hipMemcpy(d_bins_, host.data(), host.size(), hipMemcpyHostToDevice));
+    if (gh_rows) d_gh_ = reinterpret_cast<dev::GH*>(static_cast<uint8_t*>(d_bins_) + 4 * static_cast<size_t>(row_words - 2));
   }
   // column-major copy for the partition kernels (one byte / short per row of the split column):
   // ~3% faster trees on the headline shape (profiles/r02_column_copy_ab.txt), at the price of a
@@ -299,7 +317,7 @@ void GPUTreeLearner::UploadData() {
   h_node_mask_.clear();
   d_xt_base_ = Alloc<uint32_t>(std::max(1, num_features_));
   d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
-  d_gh_ = Alloc<dev::GH>(num_data_);
+  if (d_gh_ == nullptr) d_gh_ = Alloc<dev::GH>(num_data_);
   d_idx_ = Alloc<int32_t>(num_data_);
   d_tmp_ = Alloc<int32_t>(num_data_);
   d_bag_ = Alloc<int32_t>(num_data_);
@@ -359,7 +377,9 @@ void GPUTreeLearner::UploadData() {
     // a round's blocks share one size: at most split_grid (or the rows at the headroom cap)
     // plus one partial block per expansion
     const int64_t capped = (static_cast<int64_t>(num_data_) + rows_cap_ - 1) / rows_cap_;
-    hist_blocks = std::max<int>(hist_blocks, static_cast<int>(std::max<int64_t>(split_grid_, capped)) + dev::kMaxRoundExp);
+    int rg = 2 * split_grid_;
+    if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) rg = std::max(rg, std::atoi(e));
+    hist_blocks = std::max<int>(hist_blocks, static_cast<int>(std::max<int64_t>(rg, capped)) + dev::kMaxRoundExp);
   }
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_ * hist_units_);
   d_root_ = Alloc<double>(4);
@@ -548,6 +568,14 @@ void GPUTreeLearner::UploadData() {
   }
   a.rd = nullptr;
   a.round_k = round_k_;
+  // rounds hold more rows than one split: two workgroups per CU (A/B 256 / 512 on the headline:
+  // 2.53 / 2.47 ms/iter)
+  a.round_grid = 2 * split_grid_;
+  a.round_gr = 0;
+  a.round_fused = 1;
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_FUSED")) a.round_fused = e[0] == '1' ? 1 : 0;
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) a.round_grid = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_GR")) a.round_gr = std::atoi(e);
   AllocRoundState();
   UploadInteractionMasks();
   AllocSplittable();
@@ -833,7 +861,7 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
     dev::ReduceParts(d_max_parts_, d_root_parts_, dev::GradientBlocks(num_data_), num_data_, d_absmax_, d_root_,
                      stream_);
   } else {
-    dev::PackGH(gradients, hessians, d_gh_, num_data_, d_max_parts_, stream_);
+    dev::PackGH(gradients, hessians, d_gh_, args_.gh_stride, num_data_, d_max_parts_, stream_);
     dev::ReduceParts(d_max_parts_, nullptr, dev::PackBlocks(num_data_), num_data_, d_absmax_, nullptr, stream_);
   }
   AllreduceAbsMax();
@@ -1603,7 +1631,7 @@ void GPUTreeLearner::DownloadPartitionToHost() const {
   HIPCHECK(hipMemcpyAsync(leaves.data(), d_leaves_, sizeof(dev::Leaf) * L, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   // each leaf's rows sit in the index buffer its last split wrote (Leaf::buf)
-  const int num_leaves_now = h_step_->nsplit + 1;
+  const int num_leaves_now = last_stats_.splits + 1;  // (either growth mode)
   for (int l = 0; l < L; ++l) {
     self->leaf_begin_[l] = leaves[l].begin;
     self->leaf_count_[l] = l < num_leaves_now ? leaves[l].count : 0;
@@ -1858,8 +1886,8 @@ void GPUTreeLearner::UploadSparseRows() {
 
 // row-major copy of a dataset's storage columns in this learner's layout (each group at its
 // byte of the row, 8 or 16 bits; rows padded to whole 32-bit words)
-std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d) const {
-  const size_t row_bytes = static_cast<size_t>(args_.words_per_row) * 4;
+std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d, int row_words) const {
+  const size_t row_bytes = static_cast<size_t>(row_words) * 4;
   const data_size_t n = d->num_data();
   const int ng = d->num_groups();
   std::vector<uint8_t> host(static_cast<size_t>(n) * row_bytes, 0);
@@ -1888,7 +1916,7 @@ int GPUTreeLearner::AddValidData(const Dataset* valid, int ntpi, const double* s
   ValidSet vs;
   vs.num_data = valid->num_data();
   vs.ntpi = ntpi;
-  std::vector<uint8_t> host = RowMajorBins(valid);
+  std::vector<uint8_t> host = RowMajorBins(valid, args_.words_per_row);
   HIPCHECK(hipMalloc(&vs.bins, std::max<size_t>(1, host.size())));
   valid_allocs_.push_back(vs.bins);
   HIPCHECK(hipMemcpy(vs.bins, host.data(), host.size(), hipMemcpyHostToDevice));
@@ -1920,6 +1948,7 @@ void GPUTreeLearner::ValidAddTree(int slot, const Tree* tree, int k) {
   dev::DevTree t = StageTree(tree);
   dev::KArgs a = args_;
   a.bins = vs.bins;
+  a.row_words = a.words_per_row;  // (validation rows carry no (g, h))
   dev::AddTreeScore(a, t, nullptr, vs.num_data, score, stream_);
   HIPCHECK(hipStreamSynchronize(stream_));  // staging buffers are reused by the next tree
 }
@@ -2223,6 +2252,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   g.grad = d_grad_;
   g.hess = d_hess_;
   g.gh = nullptr;
+  g.gh_stride = args_.gh_stride;
   g.max_parts = nullptr;
   g.root_parts = nullptr;
   const bool fuse = ntpi == 1 && spec.kind != DeviceGradKind::MulticlassSoftmax;

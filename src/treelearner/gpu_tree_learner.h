@@ -125,7 +125,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool UseSparseRows(int wpr) const;
   bool SetupForcedSplits();  // KArgs::forced_*; false: the forced splits need host-assisted growth
   void UploadSparseRows();
-  std::vector<uint8_t> RowMajorBins(const Dataset* d) const;
+  std::vector<uint8_t> RowMajorBins(const Dataset* d, int row_words) const;
   template <typename T>
   T* Alloc(size_t n);
 

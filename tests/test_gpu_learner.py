@@ -570,7 +570,7 @@ def test_device_training_is_bitwise_deterministic(extra, gpu_available):
     assert runs[0] == runs[1]
 
 
-@pytest.mark.parametrize("env", [{"LGBM_AMD_SPARSE_ROWS": "1"}, {"LGBM_AMD_UNIFORM_BINS": "1"}])
+@pytest.mark.parametrize("env", [{"LGBM_AMD_SPARSE_ROWS": "1"}, {"LGBM_AMD_UNIFORM_BINS": "1"}, {"LGBM_AMD_GH_IN_ROWS": "1"}])
 def test_storage_layouts_give_identical_models(gpu_available, monkeypatch, env):
     """Histograms are exact integer sums, so the training rows' storage (word matrix with
     per-group widths, every group widened to 16 bits, or row-sparse lists) cannot change a

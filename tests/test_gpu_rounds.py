@@ -106,6 +106,17 @@ def test_round_growth_many_row_blocks(monkeypatch, tmp_path, gpu_available):
     assert base == spec
 
 
+@pytest.mark.parametrize("fused", ["0", "1"])
+def test_round_kernel_variants(fused, monkeypatch, tmp_path, gpu_available):
+    """The fused partition + histogram kernel and the partition / per-child histogram pair."""
+    X, y = _data(n=300000, seed=10)
+    params = {"objective": "binary", "num_leaves": 63, "max_bin": 255}
+    base, _ = _model(monkeypatch, tmp_path, 1, X, y, params, rounds=4, tag="v" + fused)
+    monkeypatch.setenv("LGBM_AMD_ROUND_FUSED", fused)
+    spec, _ = _model(monkeypatch, tmp_path, 8, X, y, params, rounds=4, tag="v" + fused)
+    assert base == spec
+
+
 def test_round_growth_sparse_rows(monkeypatch, tmp_path, gpu_available):
     """Row-sparse storage and EFB bundles through the round kernels."""
     rng = np.random.RandomState(21)
