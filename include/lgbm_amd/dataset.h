@@ -11,6 +11,7 @@
 #pragma once
 
 #include <memory>
+#include <mutex>
 #include <string>
 #include <unordered_set>
 #include <utility>
@@ -172,14 +173,16 @@ class Dataset {
   // col-wise (reference dataset.cpp:1283-1384): threads over groups, each walks its column;
   // row-wise (dataset.cpp:1046-1281, MultiValDenseBin): threads over row blocks of a row-major
   // copy (built on first use), private histograms merged over bin blocks
+  // Row-wise mode: `scratch` holds the caller's per-thread private histograms -- each learner
+  // owns its own, since one Dataset may train several boosters at once (reference: the
+  // per-learner TrainingShareStates).  The row-major copy is built once, under a lock, and kept
+  // for the Dataset's lifetime.
+  struct RowWiseScratch {
+    std::vector<std::vector<hist_t>> bufs;
+  };
   void ConstructHistograms(const std::vector<int8_t>& group_used, const data_size_t* indices, data_size_t n,
-                           const score_t* grad, const score_t* hess, hist_t* hist, bool row_wise = false) const;
-  // drop the row-major copy (col-wise threading chosen)
-  void ReleaseRowMajor() const {
-    std::vector<uint8_t>().swap(row_major_);
-    std::vector<std::vector<hist_t>>().swap(row_bufs_);
-    row_stride_ = 0;
-  }
+                           const score_t* grad, const score_t* hess, hist_t* hist, bool row_wise = false,
+                           RowWiseScratch* scratch = nullptr) const;
   // reconstruct the most-frequent-bin entry of a feature slice from the leaf totals
   void FixHistogram(int inner, double sum_grad, double sum_hess, hist_t* feature_hist) const;
 
@@ -200,14 +203,15 @@ class Dataset {
  private:
   void BuildGroups(const std::vector<std::vector<int>>& features_in_group);
   void ConstructHistogramsRowWise(const std::vector<int8_t>& group_used, const data_size_t* indices, data_size_t n,
-                                  const score_t* grad, const score_t* hess, hist_t* hist) const;
+                                  const score_t* grad, const score_t* hess, hist_t* hist, RowWiseScratch* scratch) const;
   void BuildRowMajor() const;
 
-  // row-wise histograms: every group's bin of a row, contiguous (bytes per group as stored)
+  // row-wise histograms: every group's bin of a row, contiguous (bytes per group as stored);
+  // built on first use under row_major_mu_ (concurrent learners on one Dataset), then read-only
   mutable std::vector<uint8_t> row_major_;
   mutable std::vector<uint32_t> row_goff_;  // byte offset of each group in a row
   mutable size_t row_stride_ = 0;
-  mutable std::vector<std::vector<hist_t>> row_bufs_;  // per-thread private histograms
+  std::unique_ptr<std::mutex> row_major_mu_ = std::make_unique<std::mutex>();
 
   data_size_t num_data_ = 0;
   int num_total_features_ = 0;

@@ -192,6 +192,18 @@ __device__ T BlockSum(T v, T* sh) {
 // waves drain them (s_waitcnt vmcnt(0)) before the arrival counter is bumped; the picker
 // takes one agent-scope acquire (cdna_hip_programming.md Guideline 16, R1).
 typedef __attribute__((address_space(1))) unsigned long long GlobalU64;
+// (Other targets: agent-scope relaxed stores may stay in a non-coherent cache; there the
+// stores are followed by a release fence before the arrival count -- ArrivalRelease.)
+#if !defined(__gfx942__) && !defined(__gfx950__) && defined(__HIP_DEVICE_COMPILE__)
+#define LGBM_PUBLISH_NEEDS_FENCE 1
+#else
+#define LGBM_PUBLISH_NEEDS_FENCE 0
+#endif
+__device__ __forceinline__ void ArrivalRelease() {
+#if LGBM_PUBLISH_NEEDS_FENCE
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
+}
 template <typename T>
 __device__ __forceinline__ void PublishRecord(T* dst, const T& v) {
   static_assert(sizeof(T) % 8 == 0, "8-byte words");

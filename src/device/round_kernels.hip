@@ -46,6 +46,15 @@ __device__ __forceinline__ long long* RoundScratch(const KArgs& a, int parity, i
   return a.scratch + (static_cast<size_t>(parity & 1) * a.round_k + j) * 2 * static_cast<size_t>(a.p.total_bins);
 }
 
+// a workgroup barrier ordering LDS only: nothing in the round's split kernel reads another
+// wave's global stores, so the partition's stores (and the prefetched loads queued behind them
+// on vmcnt) stay in flight across it -- __syncthreads' workgroup fence would drain them
+__device__ __forceinline__ void LdsBarrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ int RValidInWave(int valid, int k, int w) {
   return min(kWave, max(0, valid - k * kPartThreads - w * kWave));
 }
@@ -115,7 +124,24 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
     const int j = i / kMaxCatWords;
     cat_bits[j][i % kMaxCatWords] = rd->e[j].split.is_categorical ? rd->e[j].split.cat_bits[i % kMaxCatWords] : 0u;
   }
-  __syncthreads();
+  LdsBarrier();
+  // LGBM_AMD_KTRACE: phase times of workgroup (0, 0) per round (wall clock, 10 ns ticks):
+  // [stage, side, reserve, write, gather, tail, store, sub-tiles, rows, total]
+  const bool tr = a.ktrace != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && rd->round < a.p.num_leaves;
+  long long tacc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  long long tprev = 0, tstart = 0;
+  if (tr) {
+    tstart = wall_clock64();
+    tprev = tstart;
+  }
+  auto stamp = [&](int k) {
+    if (tr) {
+      const long long now = wall_clock64();
+      tacc[k] += now - tprev;
+      tprev = now;
+    }
+  };
+  stamp(0);
   // the expansion of row block kb
   auto exp_of = [&](int kb) {
     int j = 0;
@@ -178,7 +204,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
       int nrow[kSplitRows];
       load_rows(nj, nt0, nr1, nrow);
       if (t0 == r0) {
-        __syncthreads();  // the previous block's partial was stored from this LDS
+        LdsBarrier();  // the previous block's partial was stored from this LDS
         for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) lds[i] = 0ull;
       }
       bool left[kSplitRows];
@@ -192,7 +218,12 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
 #pragma unroll
         for (int k = 0; k < kSplitRows; ++k) wl[k][w] = __popcll(mask[k]);
       }
-      __syncthreads();
+      LdsBarrier();
+      stamp(1);
+      if (tr) {
+        tacc[7] += 1;
+        tacc[8] += valid;
+      }
       if (w == 0) {
         const int k = lane / kRPartWaves, jj = lane % kRPartWaves;
         const int c = wl[k][jj];
@@ -213,7 +244,8 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
           }
         }
       }
-      __syncthreads();
+      LdsBarrier();
+      stamp(2);
       const int nh = nh_s;
 #pragma unroll
       for (int k = 0; k < kSplitRows; ++k) {
@@ -234,49 +266,78 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
           }
         }
       }
-      __syncthreads();  // the row list is complete
+      LdsBarrier();  // the row list is complete
+      stamp(3);
       if (t.rs < t.rpp) {
         const int wi = t.w0 + t.q;
         const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
         const int64_t wpr = a.row_words;
-        for (int j0 = t.rs; j0 < nh; j0 += GR * t.rpp) {
-          int rr[GR];
+        if constexpr (GPW == kSparseGPW) {
+          for (int j0 = t.rs; j0 < nh; j0 += GR * t.rpp) {
+            int rr[GR];
 #pragma unroll
-          for (int k = 0; k < GR; ++k) {
-            const int jr = j0 + k * t.rpp;
-            rr[k] = jr < nh ? rowlist[jr] : -1;
-          }
-          float2 v[GR];
-          if constexpr (GPW == kSparseGPW) {
+            for (int k = 0; k < GR; ++k) {
+              const int jr = j0 + k * t.rpp;
+              rr[k] = jr < nh ? rowlist[jr] : -1;
+            }
+            float2 v[GR];
 #pragma unroll
             for (int k = 0; k < GR; ++k) v[k] = GhAt(a, rr[k] >= 0 ? rr[k] : 0);
             AddSparseRows<GR, UNITS>(a, lds, t, rr, v);
-          } else {
-            uint32_t wd[GR];
+          }
+        } else {
+          // software-pipelined: the next batch's row words and (g, h) are in flight while this
+          // batch's LDS atomics run
+          const int step = GR * t.rpp;
+          uint32_t wd[GR];
+          float2 v[GR];
+          auto fetch = [&](int j0, uint32_t* w_, float2* v_) {
 #pragma unroll
             for (int k = 0; k < GR; ++k) {
-              const int x = rr[k] >= 0 ? rr[k] : 0;
-              v[k] = GhAt(a, x);
-              wd[k] = rr[k] >= 0 ? bins32[x * wpr + wi] : 0u;
+              const int jr = j0 + k * t.rpp;
+              const int x = jr < nh ? rowlist[jr] : -1;
+              v_[k] = GhAt(a, x >= 0 ? x : 0);
+              w_[k] = x >= 0 ? bins32[static_cast<int64_t>(x) * wpr + wi] : 0u;  // word 0: every bin skipped
             }
+          };
+          if (t.rs < nh) fetch(t.rs, wd, v);
+          for (int j0 = t.rs; j0 < nh; j0 += step) {
+            uint32_t wn[GR];
+            float2 vn[GR];
+            if (j0 + step < nh) fetch(j0 + step, wn, vn);
 #pragma unroll
             for (int k = 0; k < GR; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
+#pragma unroll
+            for (int k = 0; k < GR; ++k) {
+              wd[k] = wn[k];
+              v[k] = vn[k];
+            }
           }
         }
       }
+      stamp(4);
 #pragma unroll
       for (int k = 0; k < kSplitRows; ++k) row[k] = nrow[k];
       col_bins(nj, row, gb);
-      __syncthreads();  // row list, wave counts and bases are rewritten by the next sub-tile
+      LdsBarrier();  // row list, wave counts and bases are rewritten by the next sub-tile
+      stamp(5);
     }
     if (r0 >= r1) {  // (an empty block still stores a zero partial)
-      __syncthreads();
+      LdsBarrier();
       for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) lds[i] = 0ull;
-      __syncthreads();
+      LdsBarrier();
     }
     unsigned long long* out = a.partials + static_cast<size_t>(kb) * UNITS * a.p.total_bins +
                               static_cast<size_t>(UNITS) * t.lo_bin;
     for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) out[i] = lds[i];
+    stamp(6);
+  }
+  if (tr) {
+    tacc[9] = wall_clock64() - tstart;
+    long long* o = a.ktrace + static_cast<size_t>(rd->round) * kTraceSlots;
+    for (int k = 0; k < 10; ++k) o[k] = tacc[k];
+    o[10] = nexp;
+    o[11] = nblk;
   }
 }
 
@@ -788,6 +849,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   if (KIND == 1) return;  // the categorical kernel counts the arrivals
   // arrival: the child's last workgroup folds the child's per-feature results
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ArrivalRelease();
   __syncthreads();
   if (tid == 0) {
     const unsigned nwg = gridDim.x;
@@ -1143,9 +1205,15 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     // row blocks: one size for the round (at least blk_min_rows, at most the packed headroom)
     long long rows = 0;
     for (int j = 0; j < nexp; ++j) rows += s_pc[j];
-    long long rpb = (rows + a.round_grid - 1) / max(1, a.round_grid);
+    // balanced over the grid: the smallest m with blocks of ceil(rows / (m * grid - nexp))
+    // rows under the packed headroom; every workgroup then takes m blocks at most (one
+    // partial block per expansion rounds up)
+    const long long g = max(1, a.round_grid), cap = a.hist_rows_cap;
+    long long m = 1;
+    while (m * g - nexp > 0 && (rows + m * g - nexp - 1) / (m * g - nexp) > cap) ++m;
+    long long rpb = m * g - nexp > 0 ? (rows + m * g - nexp - 1) / (m * g - nexp) : cap;
     rpb = max(rpb, static_cast<long long>(a.blk_min_rows));
-    rpb = min(rpb, static_cast<long long>(a.hist_rows_cap));
+    rpb = min(rpb, cap);
     rpb = max(rpb, 1ll);
     int off = 0;
     for (int j = 0; j < nexp; ++j) {

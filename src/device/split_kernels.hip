@@ -506,6 +506,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   // (PublishRecord); every wave drains its stores, then one lane counts the arrival.  Other
   // results (histograms, flags) are read by later kernels only.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ArrivalRelease();
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned nwg = gridDim.x * gridDim.y;

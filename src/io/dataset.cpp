@@ -527,6 +527,7 @@ bool Dataset::CheckAlign(const Dataset& o) const {
 }
 
 void Dataset::BuildRowMajor() const {
+  std::lock_guard<std::mutex> lock(*row_major_mu_);
   if (row_stride_ > 0 || groups_.empty()) return;
   row_goff_.assign(groups_.size(), 0);
   size_t off = 0;
@@ -548,8 +549,10 @@ void Dataset::BuildRowMajor() const {
 
 void Dataset::ConstructHistogramsRowWise(const std::vector<int8_t>& group_used, const data_size_t* indices,
                                          data_size_t n, const score_t* grad, const score_t* hess,
-                                         hist_t* hist) const {
+                                         hist_t* hist, RowWiseScratch* scratch) const {
   BuildRowMajor();
+  RowWiseScratch local;
+  std::vector<std::vector<hist_t>>& row_bufs_ = (scratch != nullptr ? scratch : &local)->bufs;
   std::vector<int> used;
   for (int g = 0; g < num_groups(); ++g) {
     if (group_used[g]) used.push_back(g);
@@ -611,9 +614,9 @@ void Dataset::ConstructHistogramsRowWise(const std::vector<int8_t>& group_used, 
 
 void Dataset::ConstructHistograms(const std::vector<int8_t>& group_used, const data_size_t* indices,
                                   data_size_t n, const score_t* grad, const score_t* hess, hist_t* hist,
-                                  bool row_wise) const {
+                                  bool row_wise, RowWiseScratch* scratch) const {
   if (row_wise) {
-    ConstructHistogramsRowWise(group_used, indices, n, grad, hess, hist);
+    ConstructHistogramsRowWise(group_used, indices, n, grad, hess, hist, scratch);
     return;
   }
   const int ng = num_groups();
@@ -827,8 +830,11 @@ void Dataset::DumpText(const std::string& path) const {
 
 void Dataset::AddFeaturesFrom(const Dataset& other) {
   if (other.num_data_ != num_data_) Log::Fatal("Cannot add features from other Dataset with a different number of rows");
-  row_stride_ = 0;  // the row-major copy follows the new groups
-  row_major_.clear();
+  {
+    std::lock_guard<std::mutex> lock(*row_major_mu_);
+    row_stride_ = 0;  // the row-major copy follows the new groups
+    row_major_.clear();
+  }
   const int old_total = num_total_features_;
   const int old_inner = num_features_;
   const int old_groups = num_groups();

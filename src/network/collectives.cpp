@@ -1,4 +1,5 @@
 // Host collective algorithms over HostTransport::SendRecv (see collectives.h).
+#include <cstring>
 #include "collectives.h"
 
 #include <algorithm>

@@ -351,11 +351,11 @@ void GPUTreeLearner::UploadData() {
   // CU in all, since the smaller leaves' blocks exit at once and their launches alone cost
   // tens of microseconds (Epsilon, 8 column tiles: 37.4 ms/iter at 256 x 8, 28.7 at 32 x 8;
   // Yahoo, 3 tiles: 20.8 at 256 x 3, 20.6 at 64 x 3 -- profiles/r02_v10_split_grid_wide.txt)
-  {
-    const int tiles = sparse_rows_ ? (total_bins_ + (hist_units_ == 1 ? 16384 : 8192) - 1) / (hist_units_ == 1 ? 16384 : 8192)
-                                   : (wpr + tile_words - 1) / tile_words;
-    split_grid_ = std::max(std::min(8, dev::HistGridBlocks() / 2), dev::HistGridBlocks() / 2 / std::max(1, tiles));
-  }
+  // column tiles of the histogram kernels (row-sparse: bin ranges of 16384 packed / 8192 wide bins)
+  const int sparse_tile_bins = hist_units_ == 1 ? 16384 : 8192;
+  const int col_tiles = sparse_rows_ ? (total_bins_ + sparse_tile_bins - 1) / sparse_tile_bins
+                                     : (wpr + tile_words - 1) / tile_words;
+  split_grid_ = std::max(std::min(8, dev::HistGridBlocks() / 2), dev::HistGridBlocks() / 2 / std::max(1, col_tiles));
   if (const char* e = std::getenv("LGBM_AMD_SPLIT_GRID")) split_grid_ = std::max(1, std::atoi(e));
   rows_cap_ = hist_units_ == 1 ? dev::kHistRowsCap : (1 << 30);
   if (const char* e = std::getenv("LGBM_AMD_HIST_ROWS_CAP")) {
@@ -365,11 +365,7 @@ void GPUTreeLearner::UploadData() {
   // for 2-5 tiles (Bosch 16.7 -> 16.0), 1024 from 6 (the split kernel's grid shrinks with the tiles, so smaller
   // blocks keep its workgroups busy: Epsilon, 8 tiles, 4096/2048/1024 = 23.0/21.7/20.8 ms/iter;
   // profiles/r02_v11_blk_min_rows_wide.txt)
-  {
-    const int tiles = sparse_rows_ ? (total_bins_ + (hist_units_ == 1 ? 16384 : 8192) - 1) / (hist_units_ == 1 ? 16384 : 8192)
-                                   : (wpr + tile_words - 1) / tile_words;
-    blk_min_rows_ = tiles >= 6 ? 1024 : tiles > 1 ? 2048 : 4096;
-  }
+  blk_min_rows_ = col_tiles >= 6 ? 1024 : col_tiles > 1 ? 2048 : 4096;
   if (const char* e = std::getenv("LGBM_AMD_BLK_MIN_ROWS")) blk_min_rows_ = std::max(256, std::atoi(e));
   int hist_blocks = std::max({1, dev::HistBlocksFor(num_data_, root_grid_, rows_cap_, dev::kHistMinRows),
                               dev::HistBlocksFor(num_data_, split_grid_, rows_cap_, blk_min_rows_)});
@@ -379,7 +375,8 @@ void GPUTreeLearner::UploadData() {
     const int64_t capped = (static_cast<int64_t>(num_data_) + rows_cap_ - 1) / rows_cap_;
     int rg = 2 * split_grid_;
     if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) rg = std::max(rg, std::atoi(e));
-    hist_blocks = std::max<int>(hist_blocks, static_cast<int>(std::max<int64_t>(rg, capped)) + dev::kMaxRoundExp);
+    // (k_round_plan: blocks <= rows / rows_cap + expansions + grid)
+    hist_blocks = std::max<int>(hist_blocks, static_cast<int>(capped + rg + dev::kMaxRoundExp + 1));
   }
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_ * hist_units_);
   d_root_ = Alloc<double>(4);
@@ -461,7 +458,7 @@ void GPUTreeLearner::UploadData() {
   a.word_g0 = d_word_g0_;
   a.word_wide = d_word_wide_;
   a.tile_words = tile_words;
-  a.hist_tiles = (wpr + tile_words - 1) / tile_words;
+  a.hist_tiles = col_tiles;
   a.tile_w0 = 0;
   a.tile_w1 = wpr;
   a.feat_list = nullptr;
@@ -476,8 +473,6 @@ void GPUTreeLearner::UploadData() {
   a.sp_bin = d_sp_bin_;
   a.sp_team = sp_team_;
   if (sparse_rows_) {  // column tiles = bin ranges of at most 16384 (packed) / 8192 (wide) bins
-    const int limit = hist_units_ == 1 ? 16384 : 8192;
-    a.hist_tiles = (total_bins_ + limit - 1) / limit;
     a.tile_bins = (total_bins_ + a.hist_tiles - 1) / a.hist_tiles;
     a.tile_w0 = 0;
     a.tile_w1 = a.hist_tiles;
@@ -1179,7 +1174,8 @@ constexpr int kRoundSeg = 4;
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
   a.rd = d_round_;
   a.pick_in_find = 0;  // the root's split scan only publishes; RoundRootPlan picks
-  a.ktrace = nullptr;
+  // (LGBM_AMD_KTRACE: k_round_split's phase times of one workgroup per round)
+  if (a.ktrace != nullptr) HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
   const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
   const bool use_graph = !(ng != nullptr && ng[0] == '1');
   const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
@@ -1242,6 +1238,24 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     }
     launch_seg();
     launched += kRoundSeg;
+  }
+  if (a.ktrace != nullptr) {
+    std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
+    HIPCHECK(hipMemcpy(t.data(), a.ktrace, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
+    static const char* names[] = {"stage", "side", "resv", "write", "gather", "tail", "store"};
+    for (int r = 1; r <= h_round_->rounds && r < L; ++r) {
+      const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
+      std::string line = "round " + std::to_string(r) + " exp " + std::to_string(o[10]) + " blocks " +
+                         std::to_string(o[11]) + " wg0: subtiles " + std::to_string(o[7]) + " rows " +
+                         std::to_string(o[8]) + " us";
+      char buf[64];
+      for (int k = 0; k < 7; ++k) {
+        std::snprintf(buf, sizeof(buf), " %s=%.2f", names[k], o[k] / 100.0);
+        line += buf;
+      }
+      std::snprintf(buf, sizeof(buf), " total=%.2f", o[9] / 100.0);
+      std::fprintf(stderr, "%s%s\n", line.c_str(), buf);
+    }
   }
   // the next tree enqueues as many rounds as this one took (rounded up to whole segments)
   round_pred_ = h_round_->rounds + 1;

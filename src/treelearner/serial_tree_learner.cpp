@@ -309,27 +309,46 @@ void SerialTreeLearner::ConstructHistograms(const std::vector<int8_t>& feature_u
   data_size_t cnt = 0;
   const data_size_t* idx = LeafIndices(smaller_.leaf, &cnt);
   const bool all_rows = !use_bag_ && cnt == num_data_;
-  if (hist_mode_ == 0) hist_mode_ = ChooseHistogramThreading(groups, all_rows ? nullptr : idx, cnt);
+  bool built = false;
+  if (hist_mode_ == 0) {
+    // deterministic: col-wise (the two modes sum in different orders, a timing choice would
+    // make models differ between runs); else the timing test, whose winning build is kept
+    if (config_->deterministic) {
+      hist_mode_ = 1;
+    } else {
+      hist_mode_ = ChooseHistogramThreading(groups, all_rows ? nullptr : idx, cnt);
+      built = true;
+    }
+  }
   const bool row_wise = hist_mode_ == 2;
-  data_->ConstructHistograms(groups, all_rows ? nullptr : idx, cnt, gradients_, hessians_,
-                             LeafHist(smaller_slot_).data(), row_wise);
+  if (!built) {
+    data_->ConstructHistograms(groups, all_rows ? nullptr : idx, cnt, gradients_, hessians_,
+                               LeafHist(smaller_slot_).data(), row_wise, &row_scratch_);
+  }
   if (larger_slot_ >= 0 && !use_subtract) {
     const data_size_t* idx2 = LeafIndices(larger_.leaf, &cnt);
-    data_->ConstructHistograms(groups, idx2, cnt, gradients_, hessians_, LeafHist(larger_slot_).data(), row_wise);
+    data_->ConstructHistograms(groups, idx2, cnt, gradients_, hessians_, LeafHist(larger_slot_).data(), row_wise,
+                               &row_scratch_);
   }
 }
 
 // auto threading (reference Dataset::TestMultiThreadingMethod, dataset.cpp:589-684): the
 // first histogram is built both ways and the faster one is kept for the rest of training
+// (the leaf's histogram is left built by the faster mode)
 int SerialTreeLearner::ChooseHistogramThreading(const std::vector<int8_t>& groups, const data_size_t* idx,
                                                 data_size_t cnt) {
+  std::vector<hist_t>& leaf = LeafHist(smaller_slot_);
+  std::vector<hist_t> other(leaf.size());
   const double t0 = common::NowSeconds();
-  data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, LeafHist(smaller_slot_).data(), false);
+  data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, leaf.data(), false);
   const double t1 = common::NowSeconds();
-  data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, LeafHist(smaller_slot_).data(), true);
+  data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, other.data(), true, &row_scratch_);
   const double t2 = common::NowSeconds();
   const bool row = (t2 - t1) < (t1 - t0);
-  if (!row) data_->ReleaseRowMajor();
+  if (row) leaf.swap(other);
+  // (the Dataset keeps its row-major copy: it may be shared by other boosters; this learner
+  // drops only its own per-thread buffers)
+  if (!row) Dataset::RowWiseScratch().bufs.swap(row_scratch_.bufs);
   Log::Info("Auto-choosing %s-wise multi-threading, the overhead of testing was %f seconds.\n"
             "You can set `force_%s_wise=true` to remove the overhead.",
             row ? "row" : "col", t2 - t0, row ? "row" : "col");

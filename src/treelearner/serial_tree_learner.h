@@ -112,6 +112,7 @@ class SerialTreeLearner : public TreeLearner {
   // CPU histogram threading (reference Dataset::TestMultiThreadingMethod): 0 undecided (auto),
   // 1 col-wise (threads over feature groups), 2 row-wise (threads over row blocks)
   int hist_mode_ = 0;
+  Dataset::RowWiseScratch row_scratch_;  // this learner's row-wise per-thread histograms
   bool has_parent_hist_ = false;
   LeafState smaller_, larger_;
 
