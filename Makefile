@@ -12,7 +12,10 @@ LIB := $(LIBDIR)/lib_lightgbmv1_amd.so
 CLI := $(LIBDIR)/lightgbm
 
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -fopenmp -Wall -Wno-unused-function -Wno-sign-compare -Iinclude -I$(ROCM)/include -D__HIP_PLATFORM_AMD__
-HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -munsafe-fp-atomics -Wno-unused-result
+# -amdgpu-atomic-optimizer-strategy=None: the device code's global atomics come from one lane
+# (reservations, arrival counters); the optimizer's wave loop would wait for each one's return
+# at once instead of when its result is used
+HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -munsafe-fp-atomics -mllvm -amdgpu-atomic-optimizer-strategy=None -Wno-unused-result
 HIPEXTRA ?=
 LDFLAGS := -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
 

@@ -55,6 +55,32 @@ __device__ __forceinline__ void LdsBarrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// the split column's bin of a row without branches (ColBin's source / width branches compile
+// to divergent blocks whose waits drain every load in flight): one aligned dword load and a
+// shift, from the column copy or the row-major matrix
+struct ColSrc {
+  const uint32_t* base;  // 4-byte aligned allocation (column copy or row-major matrix)
+  int64_t off0;          // byte offset of row 0's bin
+  int64_t stride;        // bytes between rows
+  uint32_t mask;
+};
+__device__ __forceinline__ ColSrc ColSource(const KArgs& a, int gbyte, int gwide, int64_t col_off) {
+  ColSrc c;
+  const bool col = a.bins_col != nullptr;
+  c.base = col ? reinterpret_cast<const uint32_t*>(a.bins_col) : static_cast<const uint32_t*>(a.bins);
+  c.off0 = col ? col_off : gbyte;
+  c.stride = col ? (gwide ? 2 : 1) : 4 * static_cast<int64_t>(a.row_words);
+  c.mask = gwide ? 0xffffu : 0xffu;
+  return c;
+}
+// (row < 0: none -- row 0 is read and the result dropped, so the load is unconditional)
+__device__ __forceinline__ uint32_t ColBinNB(const ColSrc& c, int row) {
+  const int64_t off = c.off0 + static_cast<int64_t>(max(row, 0)) * c.stride;
+  const uint32_t wd = c.base[off >> 2];
+  const uint32_t v = (wd >> ((static_cast<uint32_t>(off) & 3u) * 8u)) & c.mask;
+  return row < 0 ? 0u : v;
+}
+
 __device__ __forceinline__ int RValidInWave(int valid, int k, int w) {
   return min(kWave, max(0, valid - k * kPartThreads - w * kWave));
 }
@@ -165,8 +191,9 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
     }
   };
   auto col_bins = [&](int jn, const int* rr, uint32_t* g) {
+    const ColSrc c = ColSource(a, ex[jn].fbyte, ex[jn].fwide, ex[jn].fcol);
 #pragma unroll
-    for (int k = 0; k < kSplitRows; ++k) g[k] = rr[k] >= 0 ? ColBin(a, rr[k], ex[jn].fbyte, ex[jn].fwide, ex[jn].fcol) : 0u;
+    for (int k = 0; k < kSplitRows; ++k) g[k] = ColBinNB(c, rr[k]);
   };
   {
     const int j = exp_of(blockIdx.x);
@@ -207,6 +234,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
         LdsBarrier();  // the previous block's partial was stored from this LDS
         for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) lds[i] = 0ull;
       }
+      // ---- sides (this sub-tile's split-column bins were loaded during the previous one)
       bool left[kSplitRows];
       unsigned long long mask[kSplitRows];
 #pragma unroll
@@ -224,6 +252,10 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
         tacc[7] += 1;
         tacc[8] += valid;
       }
+      // ---- prefixes; the reservation is issued now and consumed after the gathers (its round
+      // trip overlaps them)
+      int res_l = 0, res_r = 0;
+      int nl_w0 = 0;
       if (w == 0) {
         const int k = lane / kRPartWaves, jj = lane % kRPartWaves;
         const int c = wl[k][jj];
@@ -231,18 +263,8 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
         const int ci = WavePrefixIncl(c), hi = WavePrefixIncl(hc);
         lpre[k][jj] = ci - c;
         hpre[k][jj] = hi - hc;
-        const int nl = __shfl(ci, kWave - 1, kWave);
+        nl_w0 = __shfl(ci, kWave - 1, kWave);
         if (lane == kWave - 1) nh_s = hi;
-        if (lane == 0 && writer) {
-          if (X.single) {
-            base[0] = base[1] = 0;
-            rd->cur[j][0] = nl;
-            rd->cur[j][1] = valid - nl;
-          } else {
-            base[0] = atomicAdd(&rd->cur[j][0], nl);
-            base[1] = atomicAdd(&rd->cur[j][1], valid - nl);
-          }
-        }
       }
       LdsBarrier();
       stamp(2);
@@ -253,18 +275,13 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
         const unsigned long long hm = hl ? mask[k] : (~mask[k] & vm);
         if (row[k] >= 0 && left[k] == hl) rowlist[hpre[k][w] + __popcll(hm & lt)] = row[k];
       }
-      if (writer) {
-        const int lbase = X.pb + base[0];
-        const int rbase = X.pb + X.pc - 1 - base[1];
-#pragma unroll
-        for (int k = 0; k < kSplitRows; ++k) {
-          if (row[k] >= 0) {
-            const int lpos = lpre[k][w] + __popcll(mask[k] & lt);
-            const int pos = k * kPartThreads + threadIdx.x;
-            if (left[k]) dst[lbase + lpos] = row[k];
-            else dst[rbase - (pos - lpos)] = row[k];
-          }
-        }
+      // the next sub-tile's split-column bins: in flight during the gathers
+      uint32_t ngb[kSplitRows];
+      col_bins(nj, nrow, ngb);
+      // (issued after the column loads: a wait for those would otherwise cover the atomics)
+      if (w == 0 && lane == 0 && writer && !X.single) {
+        res_l = atomicAdd(&rd->cur[j][0], nl_w0);
+        res_r = atomicAdd(&rd->cur[j][1], valid - nl_w0);
       }
       LdsBarrier();  // the row list is complete
       stamp(3);
@@ -316,10 +333,37 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
         }
       }
       stamp(4);
+      // ---- the partition (column tile 0): slots from the reservation
+      if (w == 0 && lane == 0 && writer) {
+        if (X.single) {
+          base[0] = base[1] = 0;
+          rd->cur[j][0] = nl_w0;
+          rd->cur[j][1] = valid - nl_w0;
+        } else {
+          base[0] = res_l;
+          base[1] = res_r;
+        }
+      }
+      LdsBarrier();
+      if (writer) {
+        const int lbase = X.pb + base[0];
+        const int rbase = X.pb + X.pc - 1 - base[1];
 #pragma unroll
-      for (int k = 0; k < kSplitRows; ++k) row[k] = nrow[k];
-      col_bins(nj, row, gb);
-      LdsBarrier();  // row list, wave counts and bases are rewritten by the next sub-tile
+        for (int k = 0; k < kSplitRows; ++k) {
+          if (row[k] >= 0) {
+            const int lpos = lpre[k][w] + __popcll(mask[k] & lt);
+            const int pos = k * kPartThreads + threadIdx.x;
+            if (left[k]) dst[lbase + lpos] = row[k];
+            else dst[rbase - (pos - lpos)] = row[k];
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kSplitRows; ++k) {
+        row[k] = nrow[k];
+        gb[k] = ngb[k];
+      }
+      LdsBarrier();  // row list, wave counts, prefixes and bases are rewritten by the next sub-tile
       stamp(5);
     }
     if (r0 >= r1) {  // (an empty block still stores a zero partial)
@@ -422,8 +466,9 @@ __global__ __launch_bounds__(kPartThreads) void k_round_part(KArgs a) {
     }
   };
   auto col_bins = [&](int jn, const int* rr, uint32_t* g) {
+    const ColSrc c = ColSource(a, ex[jn].fbyte, ex[jn].fwide, ex[jn].fcol);
 #pragma unroll
-    for (int k = 0; k < kSplitRows; ++k) g[k] = rr[k] >= 0 ? ColBin(a, rr[k], ex[jn].fbyte, ex[jn].fwide, ex[jn].fcol) : 0u;
+    for (int k = 0; k < kSplitRows; ++k) g[k] = ColBinNB(c, rr[k]);
   };
   {
     const int j = exp_of(blockIdx.x);
