@@ -204,6 +204,8 @@ struct Round {
   int32_t next_slot, next_frow;  // next free histogram slot / splittable row
   int32_t rounds;     // rounds planned (diagnostics)
   int32_t accepted_max;  // most splits accepted by one round (diagnostics)
+  uint32_t child_done;   // children of the round whose best split is folded (plan in the split scan)
+  int32_t pad;
   int32_t cur[kMaxRoundExp][2];  // partition cursors of each expansion: rows placed left / right
   ExpPlan e[kMaxRoundExp];
 };

@@ -153,6 +153,17 @@ struct KArgs {
   int32_t round_grid;  // workgroups of a round's split kernel (row blocks: the round's rows / round_grid)
   int32_t round_gr;    // independent row gathers per thread in its histogram phase (2, 4, 8)
   int32_t round_fused;  // 1: partition + histograms in one kernel (k_round_split), 0: two (k_round_part, k_round_hist)
+  int32_t plan_in_find;  // the round's last split-scan workgroup plans (else k_round_plan)
+  // distributed round growth (data- / feature-parallel): per-feature results rank-major,
+  // [world][2 * round_k][max_owned] (a rank's local feature index from fb_index), all-gathered
+  // before k_round_childbest; data-parallel: the round's histograms reduced into round_send
+  // ([world][round_k][rs_block][2] int64, owner-major), reduce-scattered into round_owned
+  // ([round_k][rs_block][2]: this rank's owned bins of every expansion)
+  int32_t round_dist;
+  int32_t max_owned;
+  int32_t rs_block;
+  long long* round_send;
+  long long* round_owned;
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)
@@ -231,7 +242,11 @@ void PickStep(const KArgs& a, hipStream_t s, bool root);
 // large histograms, the children's split scans (+ each child's best split), and the plan
 // (replay of the best-first order, next expansions).  A finished tree's kernels exit at once.
 void RoundRootPlan(const KArgs& a, hipStream_t s);
-void RoundStep(const KArgs& a, hipStream_t s);
+void RoundStep(const KArgs& a, hipStream_t s);  // single process: split + reduce + scans (+ plan)
+// distributed rounds: the collectives go between the parts
+void RoundSplitReduce(const KArgs& a, hipStream_t s);
+void RoundFind(const KArgs& a, hipStream_t s);
+void RoundChildBestAndPlan(const KArgs& a, hipStream_t s);
 size_t RoundPlanLds(int num_leaves);
 // voting-parallel: this rank's top-k proposals per leaf from the local scan (into its block
 // of vote_buf); after the allgather, the election and the elected features' local histograms

@@ -135,6 +135,7 @@ __global__ void k_tree_begin(KArgs a) {
       rd->next_frow = 1;  // row 0: the root
       rd->rounds = 0;
       rd->accepted_max = 0;
+      rd->child_done = 0u;
     }
   }
   for (int k = threadIdx.x; k < a.forced_n; k += blockDim.x) {  // no stale forced results

@@ -601,7 +601,8 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
   const int j = blockIdx.z;
   if (j >= rd->nexp) return;
   const int nblk = RoundHistBlocks(a, rd, j);
-  if (nblk <= kDirectChunk) return;  // summed by the split scan
+  const bool dp = a.p.data_parallel != 0;  // every expansion reduced, into the owner-major send buffer
+  if (!dp && nblk <= kDirectChunk) return;  // summed by the split scan
   if (static_cast<int>(blockIdx.y) * kReduceChunk >= nblk) return;
   const int bin = blockIdx.x * blockDim.x + threadIdx.x;
   const int nb = a.p.total_bins;
@@ -627,12 +628,18 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
     }
   }
   long long* out = RoundScratch(a, rd->round, j);
+  int pos = bin;
+  if (dp) {
+    const int rp = a.rs_pos[bin], owner = rp / a.rs_block;
+    out = a.round_send;
+    pos = (owner * a.round_k + j) * a.rs_block + (rp - owner * a.rs_block);
+  }
   if (nblk <= kReduceChunk) {
-    out[2 * bin] = g;
-    out[2 * bin + 1] = h;
+    out[2 * pos] = g;
+    out[2 * pos + 1] = h;
   } else {
-    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin]), static_cast<unsigned long long>(g));
-    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * bin + 1]), static_cast<unsigned long long>(h));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * pos]), static_cast<unsigned long long>(g));
+    atomicAdd(reinterpret_cast<unsigned long long*>(&out[2 * pos + 1]), static_cast<unsigned long long>(h));
   }
 }
 
@@ -655,10 +662,18 @@ __device__ __forceinline__ ArgC ArgWaveBest(ArgC c) {
 
 // the best split of child y (2j + lr) of the round from its per-feature results, by the
 // child's last split-scan workgroup (SplitInfo order: larger gain, then smaller real feature)
+// per-feature result slot of child y, inner feature f (distributed: rank-major blocks)
+__device__ __forceinline__ size_t RoundFbIndex(const KArgs& a, int y, int f) {
+  if (!a.round_dist) return static_cast<size_t>(y) * a.p.num_features + f;
+  const int fi = a.fb_index[f], per = 2 * a.max_owned;
+  const int owner = fi / per, local = fi - owner * per;
+  return (static_cast<size_t>(owner) * 2 * a.round_k + y) * a.max_owned + local;
+}
+
 template <int KIND, int NT>
 __device__ void ChildBest(const KArgs& a, int y, int leaf, int lr, RoundFindShared<KIND, NT>& sh) {
   const int NF = a.p.num_features, tid = threadIdx.x;
-  const FeatureBest* fb = a.feat_best + static_cast<size_t>(y) * NF;
+  const FeatureBest* fb0 = a.feat_best;
   constexpr int kB = 8;
   ArgC c = ArgNone();
 #pragma unroll 1
@@ -670,9 +685,10 @@ __device__ void ChildBest(const KArgs& a, int y, int leaf, int lr, RoundFindShar
       const int i = i0 + k * NT;
       cf[k] = -1;
       if (i < NF) {
-        cg[k] = fb[i].gain;
-        crf[k] = fb[i].real_feature;
-        cf[k] = fb[i].feature;
+        const FeatureBest& r = fb0[RoundFbIndex(a, y, i)];
+        cg[k] = r.gain;
+        crf[k] = r.real_feature;
+        cf[k] = r.feature;
       }
     }
 #pragma unroll
@@ -692,15 +708,22 @@ __device__ void ChildBest(const KArgs& a, int y, int leaf, int lr, RoundFindShar
   for (int k = 1; k < NT / kWave; ++k) ArgTake(&b, sh.arg[k]);
   const size_t ci = 2 * static_cast<size_t>(leaf) + lr;
   FeatureBest* dst = a.cbest + ci;
-  if (b.idx >= 0 && b.g != -INFINITY) {
-    CopyWords(&fb[b.idx], dst, tid, NT);
-    const uint32_t* cat = a.feat_cat + (static_cast<size_t>(y) * NF + b.idx) * kMaxCatWords;
-    for (int w = tid; w < kMaxCatWords; w += NT) a.cbest_cat[ci * kMaxCatWords + w] = cat[w];
-  } else if (tid == 0) {
-    FeatureBest none = {};
-    none.gain = -INFINITY;
-    none.feature = none.real_feature = -1;
-    *dst = none;
+  // (write-through: with KArgs::plan_in_find another workgroup of this launch plans from them)
+  if (tid == 0) {
+    if (b.idx >= 0 && b.g != -INFINITY) {
+      const size_t wi = RoundFbIndex(a, y, b.idx);
+      const FeatureBest w = fb0[wi];
+      PublishRecord(dst, w);
+      if (w.ncat > 0) {
+        const CatWords cat = *reinterpret_cast<const CatWords*>(a.feat_cat + wi * kMaxCatWords);
+        PublishRecord(reinterpret_cast<CatWords*>(a.cbest_cat + ci * kMaxCatWords), cat);
+      }
+    } else {
+      FeatureBest none = {};
+      none.gain = -INFINITY;
+      none.feature = none.real_feature = -1;
+      PublishRecord(dst, none);
+    }
   }
 }
 
@@ -729,7 +752,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const double ig = a.scales[2], ih = a.scales[3];
   // this feature's bins of expansion j's reduce buffer for the next round (every expansion
   // slot: the next round may use any)
-  if (!CAT && lr == 0) {
+  const bool dp = a.p.data_parallel != 0;
+  if (!CAT && lr == 0 && !dp) {
     long long* nxt = RoundScratch(a, parity + 1, j);
     for (int i = tid; i < 2 * nbf; i += NT) nxt[2 * F.hist_offset + i] = 0;
   }
@@ -737,7 +761,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const ExpPlan& E = rd->e[j];
   const int pc = E.part_count;
   const int tl = rd->cur[j][0];
-  const int lc = tl, rc = pc - tl;
+  // data-parallel: the children's global counts from the split's estimates (reference
+  // data_parallel_tree_learner.cpp: global leaf counts from the SplitInfo)
+  const int lc = dp ? E.lr[0].global_count : tl, rc = dp ? E.lr[1].global_count : pc - tl;
   const ChildStats cl = E.lr[lr];
   const int leaf = E.leaf;
   const int md = a.p.sp.min_data_in_leaf;
@@ -747,7 +773,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const int frow = E.frow_child[lr];
   const int nblk = RoundHistBlocks(a, rd, j), blk_off = E.blk_off;
   const int8_t parent_ok = a.splittable[static_cast<size_t>(E.frow_parent) * NF + f];
-  FeatureBest* fb_out = &a.feat_best[static_cast<size_t>(y) * NF + f];
+  FeatureBest* fb_out = &a.feat_best[RoundFbIndex(a, y, f)];
   int8_t* flags = a.splittable + static_cast<size_t>(frow) * NF;
   const SplitParams& p = a.p.sp;
   FeatureBest o;
@@ -782,14 +808,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     L.c.max = cl.cmax;
     const int nh = 2 * a.p.total_bins;
     long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
-    const long long* src = RoundScratch(a, parity, j) + 2 * F.hist_offset;
+    const long long* src = dp ? a.round_owned + 2 * (static_cast<size_t>(j) * a.rs_block + (F.hist_offset - a.owned_bin_lo))
+                              : RoundScratch(a, parity, j) + 2 * F.hist_offset;
     const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
     const unsigned long long* part = a.partials + static_cast<size_t>(blk_off) * pstride + static_cast<size_t>(units) * F.hist_offset;
     const bool stage = a.p.max_feature_bins <= kFindLdsBins;
     double* sgv = s_bins;
     double* shv = s_bins + (stage ? a.p.max_feature_bins : 0);
     const bool subtract = !is_hist;
-    const int nblk_direct = nblk <= kDirectChunk ? nblk : -1;
+    const int nblk_direct = (!dp && nblk <= kDirectChunk) ? nblk : -1;
     const bool spread = nblk_direct > 1 && 2 * nbf <= NT;
     long long pg0 = 0, ph0 = 0;
     if (subtract && tid < nbf) {
@@ -879,7 +906,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
       hv.inv_h = ih;
       bool splittable;
       if constexpr (CAT) {
-        splittable = FindCategoricalBlock(F, hv, L, p, &o, a.feat_cat + (static_cast<size_t>(y) * NF + f) * kMaxCatWords,
+        splittable = FindCategoricalBlock(F, hv, L, p, &o, a.feat_cat + RoundFbIndex(a, y, f) * kMaxCatWords,
                                           &sh.sc, &sh.cat_sc);
       } else {
         splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, cl.depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc,
@@ -891,7 +918,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     }
   }
   if (write && tid == 0) PublishRecord(fb_out, o);
-  if (KIND == 1) return;  // the categorical kernel counts the arrivals
+  // (distributed: the results are gathered from every rank first, k_round_childbest folds them)
+  if (KIND == 1 || a.round_dist) return;  // (the categorical kernel counts the arrivals)
   // arrival: the child's last workgroup folds the child's per-feature results
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   ArrivalRelease();
@@ -927,6 +955,26 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   __syncthreads();
   if (!s_last) return;
   ChildBest<KIND, NT>(a, y, leaf, lr, sh);
+  if (!a.plan_in_find) return;
+  // the last child of the round to finish plans the next round (its scans' results were
+  // published write-through; one agent-scope acquire)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ArrivalRelease();
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned n = 2u * static_cast<unsigned>(nexp);
+    int last = 0;
+    if (atomicAdd(&rd->child_done, 1u) == n - 1) {
+      last = 1;
+      rd->child_done = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  RoundPlanBody<false, NT>(a, reinterpret_cast<unsigned char*>(s_bins));
 }
 
 // ----------------------------------------------------------------------------- k_round_plan
@@ -982,15 +1030,14 @@ __device__ __forceinline__ void WaveLdsSync() {  // lane 0's LDS stores before t
 // the first plan.  Otherwise: fold the round's partition counts into the expansions, replay
 // the best-first order (wave 0, LDS tables), apply the accepted splits, plan the next round.
 // Global loads are issued in few independent batches: every one is a ~1-2 us round trip.
-template <bool ROOT>
-__global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
-  extern __shared__ unsigned char plan_lds[];
+template <bool ROOT, int NT>
+__device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
+  constexpr int kPlanThreads = NT;
   __shared__ int s_done, s_s1, s_nexp;
   __shared__ ArgC s_arg[kPlanThreads / kWave];
   __shared__ int s_pick[kMaxRoundExp];
   __shared__ int s_pc[kMaxRoundExp];
   Round* rd = a.rd;
-  if (rd->done) return;
   const int L = a.p.num_leaves, NF = a.p.num_features, tid = threadIdx.x, lane = tid & 63;
   // per-leaf tables: gain, real feature, inner feature, expanded (2: picked for the next
   // round); the expanded leaves' children (2 per leaf); the accepted leaves
@@ -1007,7 +1054,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
   if (ROOT) {
     ArgC c = ArgNone();
     for (int f = tid; f < NF; f += kPlanThreads) {
-      const FeatureBest& fb = a.feat_best[f];
+      const FeatureBest& fb = a.feat_best[FeatBestIndex(a, 0, f)];
       if (fb.feature >= 0 && (c.idx < 0 || SplitBetter(fb.gain, fb.real_feature, c.g, c.rf))) {
         c.g = fb.gain;
         c.rf = fb.real_feature;
@@ -1022,7 +1069,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     if (b.idx >= 0 && b.g == -INFINITY) b.idx = -1;
     if (tid == 0) {
       if (b.idx >= 0) {
-        ToDeviceSplit(a.feat_best[b.idx], a.feat_cat + static_cast<size_t>(b.idx) * kMaxCatWords, &a.best[0]);
+        ToDeviceSplit(a.feat_best[FeatBestIndex(a, 0, b.idx)], FeatCat(a, 0, b.idx), &a.best[0]);
       } else {
         NoSplit(&a.best[0]);
       }
@@ -1123,15 +1170,16 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
     const int w = acc[k], s = s0 + k, nl = s + 1;
     const ExpResult R = a.exres[w];
     SplitRecord& rec = a.rec[s];
+    const bool dp = a.p.data_parallel != 0;  // (global counts: the split's estimates)
     rec.leaf = w;
-    rec.left_count = R.total_left;
-    rec.right_count = R.count - R.total_left;
+    rec.left_count = dp ? R.lr[0].global_count : R.total_left;
+    rec.right_count = dp ? R.lr[1].global_count : R.count - R.total_left;
     for (int c = 0; c < 2; ++c) {
       Leaf lf;
       const ChildStats& cs = R.lr[c];
       lf.begin = c == 0 ? R.begin : R.begin + R.total_left;
       lf.count = c == 0 ? R.total_left : R.count - R.total_left;
-      lf.global_count = lf.count;
+      lf.global_count = dp ? cs.global_count : lf.count;
       lf.depth = cs.depth;
       lf.slot = cs.slot;
       lf.buf = R.buf;
@@ -1280,6 +1328,13 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
   if (tid < kMaxRoundExp) rd->cur[tid][0] = rd->cur[tid][1] = 0;
 }
 
+template <bool ROOT>
+__global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
+  extern __shared__ unsigned char plan_lds[];
+  if (a.rd->done) return;
+  RoundPlanBody<ROOT, kPlanThreads>(a, plan_lds);
+}
+
 size_t RoundPlanLds(int num_leaves) {
   const size_t L = static_cast<size_t>(num_leaves);
   return L * sizeof(double) * 3 + L * sizeof(int) * (3 + 4 + 1);
@@ -1329,7 +1384,8 @@ bool RoundSimpleGains(const KArgs& a) {
 
 void LaunchRoundFind(const KArgs& a, hipStream_t s) {
   const int ny = 2 * a.round_k;
-  const size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
+  size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
+  if (a.plan_in_find) lds = std::max(lds, RoundPlanLds(a.p.num_leaves));
   const bool simple = RoundSimpleGains(a);
   const bool narrow = a.p.max_feature_bins <= kWave;
   const dim3 g(a.num_scan, ny), b(narrow ? kWave : kFindThreads), bc(kFindThreads);
@@ -1352,6 +1408,16 @@ void LaunchRoundFind(const KArgs& a, hipStream_t s) {
 }
 
 }  // namespace
+
+// distributed rounds: each child's best split from the gathered per-feature results
+__global__ __launch_bounds__(kFindThreads) void k_round_childbest(KArgs a) {
+  __shared__ RoundFindShared<0, kFindThreads> sh;
+  const Round* rd = a.rd;
+  if (rd->done) return;
+  const int y = blockIdx.x;
+  if (y >= 2 * rd->nexp) return;
+  ChildBest<0, kFindThreads>(a, y, rd->e[y >> 1].leaf, y & 1, sh);
+}
 
 void PrepareRoundKernels(int max_lds) {
   auto allow = [max_lds](const void* k) {
@@ -1377,6 +1443,21 @@ void RoundRootPlan(const KArgs& a, hipStream_t s) {
 }
 
 void RoundStep(const KArgs& a, hipStream_t s) {
+  RoundSplitReduce(a, s);
+  RoundFind(a, s);
+  if (!a.plan_in_find) {
+    hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
+  }
+}
+
+void RoundFind(const KArgs& a, hipStream_t s) { LaunchRoundFind(a, s); }
+
+void RoundChildBestAndPlan(const KArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_round_childbest, dim3(2 * a.round_k), dim3(kFindThreads), 0, s, a);
+  hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
+}
+
+void RoundSplitReduce(const KArgs& a, hipStream_t s) {
   if (a.round_fused) {
     const int gr = a.round_gr > 0 ? a.round_gr
                    : ((a.sp_ptr != nullptr || a.tile_words <= kRGatherNarrowMaxWords) ? kRGatherNarrow : kRGatherWide);
@@ -1404,8 +1485,6 @@ void RoundStep(const KArgs& a, hipStream_t s) {
                    std::min(4, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk), a.round_k);
   if (a.hist_units == 1) hipLaunchKernelGGL((k_round_reduce<1>), rgrid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((k_round_reduce<2>), rgrid, dim3(256), 0, s, a);
-  LaunchRoundFind(a, s);
-  hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
 }
 
 }  // namespace dev

@@ -305,7 +305,7 @@ void GPUTreeLearner::UploadData() {
   // round growth: up to round_k_ leaves expanded per round (single process; LGBM_AMD_ROUND_K,
   // 1 = one split per step)
   round_k_ = 1;
-  if (!distributed_ && !voting_) {
+  if (!voting_) {  // (distributed data- / feature-parallel: rounds with a device communicator)
     round_k_ = 8;
     if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) round_k_ = std::atoi(e);
     round_k_ = std::max(1, std::min(dev::kMaxRoundExp, round_k_));
@@ -340,7 +340,7 @@ void GPUTreeLearner::UploadData() {
   d_absmax_ = Alloc<uint32_t>(4);
   // per-feature results: [2][num_features], or rank-major [world][2][max_owned] (gathered)
   const size_t fb_slots = std::max<size_t>(2 * static_cast<size_t>(round_k_) * std::max(1, num_features_),
-                                           2 * static_cast<size_t>(world_) * std::max(1, max_owned_));
+                                           2 * static_cast<size_t>(world_) * round_k_ * std::max(1, max_owned_));
   d_feat_best_ = Alloc<dev::FeatureBest>(fb_slots);
   d_feat_cat_ = Alloc<uint32_t>(fb_slots * kMaxCatWords);
   // row blocks: the root histogram runs on two workgroups per CU, a split step on one; a
@@ -563,11 +563,25 @@ void GPUTreeLearner::UploadData() {
   }
   a.rd = nullptr;
   a.round_k = round_k_;
+  a.round_dist = distributed_ ? 1 : 0;
+  a.max_owned = max_owned_;
+  a.rs_block = rs_block_;
+  a.round_send = nullptr;
+  a.round_owned = nullptr;
+  if (round_k_ > 1 && data_parallel_) {
+    d_round_send_ = Alloc<long long>(static_cast<size_t>(world_) * round_k_ * rs_block_ * 2);
+    d_round_owned_ = Alloc<long long>(static_cast<size_t>(round_k_) * rs_block_ * 2);
+    a.round_send = d_round_send_;
+    a.round_owned = d_round_owned_;
+  }
   // rounds hold more rows than one split: two workgroups per CU (A/B 256 / 512 on the headline:
   // 2.53 / 2.47 ms/iter)
   a.round_grid = 2 * split_grid_;
   a.round_gr = 0;
   a.round_fused = 1;
+  // the plan in the split scan's last workgroup while its tables fit the scan's LDS budget
+  a.plan_in_find = (!distributed_ && dev::RoundPlanLds(n_leaves) <= 16384) ? 1 : 0;
+  if (const char* e = std::getenv("LGBM_AMD_PLAN_IN_FIND")) a.plan_in_find = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_FUSED")) a.round_fused = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) a.round_grid = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GR")) a.round_gr = std::atoi(e);
@@ -1150,12 +1164,49 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   dev::HistRoot(a, stream_);
   ReduceScatterStep(0);
   dev::FindRoot(a, stream_);
-  if (a.rd != nullptr) dev::RoundRootPlan(a, stream_);
+  if (a.rd != nullptr) {
+    if (distributed_) GatherFeatureBests();  // (the root's results, side-0 layout)
+    dev::RoundRootPlan(a, stream_);
+  }
+}
+
+// one round: single process, every kernel back to back; distributed, the histograms
+// reduce-scattered to their owners (data-parallel) and the per-feature results of every rank
+// gathered before the children's bests and the plan -- two collectives per round where one
+// split per step took two per split (reference data_parallel_tree_learner.cpp:154-247)
+void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
+  if (!distributed_) {
+    dev::RoundStep(a, stream_);
+    return;
+  }
+  DeviceComm* dc = Network::device_comm();
+  const size_t owned = static_cast<size_t>(round_k_) * rs_block_ * 2;
+  if (data_parallel_) HIPCHECK(hipMemsetAsync(d_round_send_, 0, sizeof(long long) * owned * world_, stream_));
+  dev::RoundSplitReduce(a, stream_);
+  if (data_parallel_) dc->ReduceScatterSumI64(d_round_send_, d_round_owned_, owned, stream_);
+  dev::RoundFind(a, stream_);
+  const size_t per = 2 * static_cast<size_t>(round_k_) * std::max(1, max_owned_);
+  char* fb = reinterpret_cast<char*>(d_feat_best_);
+  dc->Allgather(fb + per * sizeof(dev::FeatureBest) * rank_, fb, per * sizeof(dev::FeatureBest), stream_);
+  if (num_cat_total_ > 0) {
+    char* fc = reinterpret_cast<char*>(d_feat_cat_);
+    const size_t cb = per * kMaxCatWords * sizeof(uint32_t);
+    dc->Allgather(fc + cb * rank_, fc, cb, stream_);
+  }
+  dev::RoundChildBestAndPlan(a, stream_);
+}
+
+double GPUTreeLearner::RoundCollectiveBytes() const {
+  if (!distributed_) return 0.0;
+  const double per = 2.0 * round_k_ * std::max(1, max_owned_) *
+                     (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0)) * world_;
+  return per + (data_parallel_ ? sizeof(long long) * 2.0 * round_k_ * rs_block_ * world_ : 0.0);
 }
 
 // ---------------------------------------------------------------- round growth
 bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
-  if (round_k_ <= 1 || distributed_ || voting_ || d_round_ == nullptr) return false;
+  if (round_k_ <= 1 || voting_ || d_round_ == nullptr) return false;
+  if (distributed_ && Network::device_comm() == nullptr) return false;  // (host collectives: one split per step)
   // the split order depends on more than each leaf's own rows: per-node feature samples and
   // extra_trees draws are consumed in the sequential order, CEGB's coupled penalties change
   // other leaves' gains, forced splits follow their own schedule
@@ -1177,7 +1228,10 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   // (LGBM_AMD_KTRACE: k_round_split's phase times of one workgroup per round)
   if (a.ktrace != nullptr) HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
   const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
-  const bool use_graph = !(ng != nullptr && ng[0] == '1');
+  // distributed: the collectives are captured with the kernels when the communicator allows it
+  // (RCCL); the in-process communicator rendezvouses on the host, so its rounds run eagerly
+  DeviceComm* dc = distributed_ ? Network::device_comm() : nullptr;
+  const bool use_graph = !(ng != nullptr && ng[0] == '1') && (dc == nullptr || dc->CaptureSafe()) && !graph_capture_failed_;
   const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
   auto capture = [&](hipGraphExec_t* exec, bool root) {
     hipGraph_t g = nullptr;
@@ -1185,7 +1239,7 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     std::string why;
     try {
       if (root) EnqueueRoot(a);
-      for (int r = 0; r < kRoundSeg; ++r) dev::RoundStep(a, stream_);
+      for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
     } catch (const std::exception& e) {
       why = e.what();
     }
@@ -1194,30 +1248,38 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     if (g != nullptr) (void)hipGraphDestroy(g);
     if (!why.empty() || ec != hipSuccess) {
       if (why.empty()) why = hipGetErrorString(ec);
-      Log::Fatal("device learner: capturing the round graphs failed: %s", why.c_str());
+      (void)hipGetLastError();
+      *exec = nullptr;
+      if (!distributed_) Log::Fatal("device learner: capturing the round graphs failed: %s", why.c_str());
+      Log::Warning("device learner: capturing the round collectives failed (%s); launching rounds eagerly", why.c_str());
+      graph_capture_failed_ = true;
+      return false;
     }
+    return true;
   };
-  if (use_graph && (round_root_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
-                    round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
+  bool graph = use_graph;
+  if (graph && (round_root_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
+                round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
     DestroyGraph();
-    capture(&round_root_exec_, true);
-    capture(&round_seg_exec_, false);
+    graph = capture(&round_root_exec_, true) && capture(&round_seg_exec_, false);
+    if (!graph) DestroyGraph();
     round_graph_rows_ = a.num_rows;
     round_graph_identity_ = a.root_identity;
     round_graph_root_mode_ = root_mode;
   }
+  last_stats_.graph = graph;
   auto launch_seg = [&]() {
-    if (use_graph) {
+    if (graph) {
       HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
     } else {
-      for (int r = 0; r < kRoundSeg; ++r) dev::RoundStep(a, stream_);
+      for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
     }
   };
-  if (use_graph) {
+  if (graph) {
     HIPCHECK(hipGraphLaunch(round_root_exec_, stream_));
   } else {
     EnqueueRoot(a);
-    for (int r = 0; r < kRoundSeg; ++r) dev::RoundStep(a, stream_);
+    for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
   }
   const int L = config_->num_leaves;
   int launched = kRoundSeg;
@@ -1260,6 +1322,8 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   // the next tree enqueues as many rounds as this one took (rounded up to whole segments)
   round_pred_ = h_round_->rounds + 1;
   last_stats_.rounds = h_round_->rounds;
+  // (every enqueued round's collectives run; a finished tree's exit at once)
+  last_stats_.collective_bytes = distributed_ ? root_collective_bytes_ + RoundCollectiveBytes() * launched : 0.0;
   return h_round_->nsplit;
 }
 
@@ -1360,6 +1424,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     root_rows_ = num_data_;
   }
   last_stats_.rounds = 0;
+  last_stats_.graph = false;
   const bool rounds = RoundGrowth(a);
   if (!rounds && last_tree_rounds_) {
     // one split per step after round trees: splittable rows follow the leaf ids again
@@ -1426,6 +1491,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       if (graph_exec_ != nullptr) {
         HIPCHECK(hipGraphLaunch(graph_exec_, stream_));
         launched = true;
+        last_stats_.graph = true;
       }
     }
     if (!launched) EnqueueTree(a);
@@ -1442,8 +1508,10 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   last_stats_.device_mode = true;
   last_stats_.splits = num_splits;
   // every step's collectives run (exiting early once the tree is done): the sequence is fixed
-  last_stats_.collective_bytes =
-      distributed_ ? root_collective_bytes_ + split_collective_bytes_ * (config_->num_leaves - 1) : 0.0;
+  if (!rounds) {
+    last_stats_.collective_bytes =
+        distributed_ ? root_collective_bytes_ + split_collective_bytes_ * (config_->num_leaves - 1) : 0.0;
+  }
   if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
     const bool root_scanned = h_step_->root_count >= 2 * config_->min_data_in_leaf;  // global count

@@ -136,6 +136,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool RoundGrowth(const dev::KArgs& a) const;
   int RunRounds(dev::KArgs a);  // the tree's splits; h_rec_ holds their records
   void EnqueueRoot(const dev::KArgs& a);
+  void EnqueueRound(const dev::KArgs& a);
+  double RoundCollectiveBytes() const;  // device collectives of one distributed round
+  long long* d_round_send_ = nullptr;
+  long long* d_round_owned_ = nullptr;
   void AllocRoundState();
   void ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const;  // (self checks)
   int round_k_ = 1;

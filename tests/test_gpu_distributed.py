@@ -147,3 +147,25 @@ def test_device_distributed_with_efb_bundles(learner, gpu_available):
         res = tr.run(rank_fn)
     assert all(r.ok for r in res), [str(r.error) for r in res]
     assert _trees(res[0].value) == _trees(res[1].value)
+
+
+@pytest.mark.parametrize("learner,world", [("data", 2), ("data", 4), ("feature", 3)])
+def test_distributed_round_growth_equals_one_split_per_step(learner, world, gpu_available, monkeypatch, tmp_path):
+    """Distributed round growth (round_kernels.hip: up to 8 leaves expanded per round, the
+    histograms reduce-scattered and the per-feature records gathered once per round instead of
+    once per split) grows the same trees as one split per step (LGBM_AMD_ROUND_K=1), on every
+    rank; the iteration log shows the rounds (fewer than the splits)."""
+    monkeypatch.setenv("LGBM_AMD_ROUND_K", "1")
+    _, _, _, base = _run(learner, world, rounds=6)
+    monkeypatch.setenv("LGBM_AMD_ROUND_K", "8")
+    log = tmp_path / "iters.jsonl"
+    monkeypatch.setenv("LGBM_AMD_ITER_LOG", str(log))
+    _, _, _, spec = _run(learner, world, rounds=6)
+    monkeypatch.delenv("LGBM_AMD_ITER_LOG")
+    for (mb, _), (ms, _) in zip(base, spec):
+        assert _trees(mb) == _trees(ms)
+    import glob
+    import json
+    rows = [json.loads(line) for f in glob.glob(str(log) + "*") for line in open(f)]
+    assert rows and all(row["rounds"][0] > 0 for row in rows)
+    assert sum(row["rounds"][0] for row in rows) < sum(row["leaves"][0] - 1 for row in rows)
