@@ -189,7 +189,8 @@ class GBDT {
   bool iter_log_checked_ = false;
   void LogIteration(double grad_ms, double bag_ms, const std::vector<double>& tree_ms, double renew_ms,
                     double score_ms, double total_ms, const std::vector<int>& leaves, const std::vector<int>& device,
-                    const std::vector<int>& rounds, const std::vector<int>& graphs, double coll_bytes);
+                    const std::vector<int>& rounds, const std::vector<int>& expansions, const std::vector<int>& graphs,
+                    double coll_bytes);
   DeviceTreeLearner* device_learner_ = nullptr;
   const ObjectiveFunction* objective_ = nullptr;
   std::unique_ptr<ObjectiveFunction> loaded_objective_;

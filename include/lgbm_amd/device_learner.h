@@ -70,6 +70,7 @@ class DeviceTreeLearner {
     bool device_mode = false;
     int splits = 0;
     int rounds = 0;  // round growth: expansion rounds of the tree (0: one split per step)
+    int expansions = 0;  // round growth: nodes expanded (accepted splits + speculation never accepted)
     bool graph = false;  // the tree's kernels (and collectives) were replayed from hipGraphs
     double collective_bytes = 0.0;
   };

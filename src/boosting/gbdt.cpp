@@ -486,7 +486,7 @@ double GBDT::BoostFromAverage(int class_id, bool update_scorer) {
 void GBDT::LogIteration(double grad_ms, double bag_ms, const std::vector<double>& tree_ms, double renew_ms,
                         double score_ms, double total_ms, const std::vector<int>& leaves,
                         const std::vector<int>& device, const std::vector<int>& rounds,
-                        const std::vector<int>& graphs, double coll_bytes) {
+                        const std::vector<int>& expansions, const std::vector<int>& graphs, double coll_bytes) {
   std::ostringstream o;
   o.precision(6);
   o << "{\"iter\": " << iter_ << ", \"rank\": " << Network::rank() << ", \"ms\": " << total_ms
@@ -498,6 +498,8 @@ void GBDT::LogIteration(double grad_ms, double bag_ms, const std::vector<double>
   for (size_t i = 0; i < device.size(); ++i) o << (i ? ", " : "") << (device[i] ? "true" : "false");
   o << "], \"rounds\": [";
   for (size_t i = 0; i < rounds.size(); ++i) o << (i ? ", " : "") << rounds[i];
+  o << "], \"expansions\": [";
+  for (size_t i = 0; i < expansions.size(); ++i) o << (i ? ", " : "") << expansions[i];
   o << "], \"graph\": [";
   for (size_t i = 0; i < graphs.size(); ++i) o << (i ? ", " : "") << (graphs[i] ? "true" : "false");
   o << "], \"collective_bytes\": " << coll_bytes << "}\n";
@@ -521,7 +523,7 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
   const auto t_iter = Clock::now();
   double grad_ms = 0, bag_ms = 0, renew_ms = 0, score_ms = 0, coll_bytes = 0;
   std::vector<double> tree_ms;
-  std::vector<int> leaves, device, rounds, graphs;
+  std::vector<int> leaves, device, rounds, expansions, graphs;
   std::vector<double> init_scores(num_tree_per_iteration_, 0.0);
   const score_t* grad = gradients;
   const score_t* hess = hessians;
@@ -562,6 +564,7 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
       const auto st = device_learner_ != nullptr ? device_learner_->LastTreeStats() : DeviceTreeLearner::TreeStats();
       device.push_back(st.device_mode ? 1 : 0);
       rounds.push_back(st.rounds);
+      expansions.push_back(st.expansions);
       graphs.push_back(st.graph ? 1 : 0);
       coll_bytes += st.collective_bytes;
     }
@@ -606,7 +609,7 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
   }
   if (iter_log_) {
     if (device_learner_ != nullptr) device_learner_->Synchronize();
-    LogIteration(grad_ms, bag_ms, tree_ms, renew_ms, score_ms, ms_since(t_iter), leaves, device, rounds, graphs, coll_bytes);
+    LogIteration(grad_ms, bag_ms, tree_ms, renew_ms, score_ms, ms_since(t_iter), leaves, device, rounds, expansions, graphs, coll_bytes);
   }
   ++iter_;
   return false;

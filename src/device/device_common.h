@@ -57,6 +57,15 @@ __device__ __forceinline__ float2 GhAt(const KArgs& a, int64_t row) {
   return reinterpret_cast<const float2*>(a.gh)[row * a.gh_stride];
 }
 
+// index buffer b (Leaf::buf): 0 idx, 1 tmp, b > 1 (round growth) tmp + (b - 1) * stride
+__host__ __device__ __forceinline__ int32_t* RowBuf(int32_t* idx, int32_t* tmp, int64_t stride, int b) {
+  return b == 0 ? idx : tmp + static_cast<int64_t>(b - 1) * stride;
+}
+__host__ __device__ __forceinline__ const int32_t* RowBuf(const int32_t* idx, const int32_t* tmp, int64_t stride, int b) {
+  return b == 0 ? idx : tmp + static_cast<int64_t>(b - 1) * stride;
+}
+__device__ __forceinline__ int32_t* RowBuf(const KArgs& a, int b) { return RowBuf(a.idx, a.tmp, a.buf_stride, b); }
+
 // the split column's bin for the partition: from the column-major copy when there is one,
 // else from the row-major matrix (whose line the histogram pass then reads again)
 __device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int gbyte, int gwide, int64_t col_off) {

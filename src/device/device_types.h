@@ -83,9 +83,9 @@ struct Leaf {
   int32_t depth;
   int32_t slot;          // histogram slot
   int32_t buf;           // which index buffer (KArgs::idx / tmp) holds the leaf's rows
-  int32_t frow;          // row of KArgs::splittable (kept across trees)
-  int32_t expanded;      // round growth: the leaf's best split was applied speculatively (ExpResult)
-  IcMask icmask;         // interaction constraints consistent with the leaf's branch (bit k: constraint k)
+  int32_t frow;          // row of KArgs::splittable (kept across trees; round growth: the leaf's RNode)
+  int32_t pad;
+  IcMask icmask;        // interaction constraints consistent with the leaf's branch (bit k: constraint k)
   double sum_g, sum_h, output;
   double lsum_g, lsum_h;  // voting-parallel: this rank's (local) sums of the leaf's rows
   double cmin, cmax;  // monotone constraint range
@@ -170,12 +170,22 @@ struct SplitRecord {
 // computed and stops at the first one whose expansion is not, which the next round expands.
 // Expansions never accepted only cost work: histograms are exact integer sums, so the rows a
 // pending expansion reordered inside its leaf's range change nothing.
-constexpr int kMaxRoundExp = 16;  // leaves expanded per round, upper bound
+//
+// Speculation also reaches below the leaves: the children of an expanded leaf that is not
+// accepted yet are 'virtual' nodes with exact best splits, rows (in the expansion's output
+// buffer) and histograms, so the planner may expand them too (up to KArgs::round_vmax levels
+// below a leaf), and a replay then accepts whole chains of splits.  Nodes are indexed by their
+// splittable row (Leaf::frow).  A node at depth d reads index buffer d mod M and writes its
+// children to (d + 1) mod M, M = round_vmax + 2 buffers: no expansion at most round_vmax
+// levels below a leaf rewrites the buffer holding that leaf's rows, so every leaf's rows stay
+// valid whichever of the speculative expansions below it the tree never accepts.
+constexpr int kMaxRoundExp = 16;  // nodes expanded per round, upper bound
+constexpr int kMaxRoundVmax = 14;  // speculation depth below a leaf, upper bound (buffers: + 2)
 
-// one leaf being expanded by the current round (written by the planner)
+// one node being expanded by the current round (written by the planner)
 struct ExpPlan {
-  int32_t leaf;
-  int32_t part_begin, part_count, src_buf;
+  int32_t node;                  // the node (its splittable row)
+  int32_t part_begin, part_count, src_buf, dst_buf;
   int32_t hist_left;             // the left child's rows are histogrammed (fewer by the estimate), else the right's
   int32_t blk_off, nblk;         // the expansion's row blocks inside the round's partial histograms
   int32_t slot_parent, slot_new;  // histogram slots: the subtracted child keeps the parent's, the histogrammed one is new
@@ -186,11 +196,14 @@ struct ExpPlan {
   ChildStats lr[2];              // left / right child as known from the split
 };
 
-// an expanded leaf's children (indexed by leaf id, valid while Leaf::expanded)
-struct ExpResult {
-  int32_t begin, count, buf;  // the leaf's rows (children: [begin, +total_left) left, the rest right) in buf
-  int32_t total_left;         // local rows that went left
-  ChildStats lr[2];
+// one node of a tree under round growth (index: its splittable row): the root and both
+// children of every expansion; written by the planner only
+struct RNode {
+  int32_t begin, count, buf;  // rows (local; known once the round expanding its parent is partitioned)
+  int32_t expanded;           // its best split was applied: children child, child + 1
+  int32_t child;
+  int32_t total_left;         // expanded: local rows that went left
+  ChildStats st;              // statistics from the parent's split (the root: its leaf's)
 };
 
 // per-tree control record of round growth

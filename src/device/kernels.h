@@ -23,7 +23,8 @@ struct KArgs {
   const int8_t* node_mask;   // [2 * num_leaves - 1][num_features] per-node samples (feature_fraction_bynode), or null
   const GH* gh;              // interleaved (gradient, hessian) per row
   int32_t* idx;              // partition index buffer 0 (root rows)
-  int32_t* tmp;              // partition index buffer 1 (leaves alternate: Leaf::buf)
+  int32_t* tmp;              // partition index buffer 1 (leaves alternate: Leaf::buf), then 2.. at buf_stride
+  int64_t buf_stride;        // int32 between index buffers 1, 2, ... (round growth: RowBuf)
   Leaf* leaves;              // [num_leaves]
   Step* st;
   SplitRecord* rec;          // [num_leaves - 1]
@@ -138,18 +139,21 @@ struct KArgs {
   int32_t vote_rank;
   int32_t* vote_list;
   long long* vote_hist;
-  // round growth (round_kernels.hip; null rd: one split per step): up to round_k leaves are
+  // round growth (round_kernels.hip; null rd: one split per step): up to round_k nodes are
   // expanded per round.  Their children's per-feature results go to feat_best rows 2j + lr,
-  // each child's best split to cbest[2 * leaf + lr] (category sets in cbest_cat); child_cnt
-  // holds each child's split-scan arrival counters ([2 * kMaxRoundExp][kFindSub], kFindSubStride
+  // each child node's best split to cbest[node] (category sets in cbest_cat); child_cnt holds
+  // each child's split-scan arrival counters ([2 * kMaxRoundExp][kFindSub], kFindSubStride
   // apart); the reduced histogram of expansion j sits at scratch + (parity * round_k + j) * 2 *
   // total_bins
   Round* rd;
-  ExpResult* exres;        // [num_leaves]
-  FeatureBest* cbest;      // [num_leaves][2]
-  uint32_t* cbest_cat;     // [num_leaves][2][kMaxCatWords]
+  RNode* rnode;            // [round_nodes] the tree's nodes (index: splittable row)
+  FeatureBest* cbest;      // [round_nodes] each node's best split
+  uint32_t* cbest_cat;     // [round_nodes][kMaxCatWords]
   uint32_t* child_cnt;
   int32_t round_k;
+  int32_t round_vmax;   // speculation depth below a leaf (index buffers: round_vmax + 2)
+  int32_t round_nodes;  // node capacity (splittable rows of a tree)
+  int32_t round_emax;   // expansions of a tree, upper bound (histogram slots - 1, (round_nodes - 1) / 2)
   int32_t round_grid;  // workgroups of a round's split kernel (row blocks: the round's rows / round_grid)
   int32_t round_gr;    // independent row gathers per thread in its histogram phase (2, 4, 8)
   int32_t round_fused;  // 1: partition + histograms in one kernel (k_round_split), 0: two (k_round_part, k_round_hist)
@@ -247,7 +251,7 @@ void RoundStep(const KArgs& a, hipStream_t s);  // single process: split + reduc
 void RoundSplitReduce(const KArgs& a, hipStream_t s);
 void RoundFind(const KArgs& a, hipStream_t s);
 void RoundChildBestAndPlan(const KArgs& a, hipStream_t s);
-size_t RoundPlanLds(int num_leaves);
+size_t RoundPlanLds(int num_leaves, int nodes);
 // voting-parallel: this rank's top-k proposals per leaf from the local scan (into its block
 // of vote_buf); after the allgather, the election and the elected features' local histograms
 // (into vote_hist, for the all-reduce); the global scan is FindRoot / FindStep with
@@ -426,6 +430,7 @@ struct RenewArgs {
   const Leaf* leaves;
   const int32_t* idx;
   const int32_t* tmp;
+  int64_t buf_stride;  // KArgs::buf_stride
   const float* label;
   const double* score;
   const float* weights;    // or null

@@ -90,7 +90,7 @@ __global__ void k_tree_begin(KArgs a) {
     Leaf lf;
     // splittable rows persist across trees; round growth hands out fresh rows from 0 (the root)
     lf.frow = a.rd != nullptr ? (l == 0 ? 0 : -1) : a.leaves[l].frow;
-    lf.expanded = 0;
+    lf.pad = 0;
     lf.begin = 0;
     lf.count = l == 0 ? RootRows(a) : 0;
     lf.global_count = lf.count;

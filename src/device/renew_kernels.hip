@@ -30,7 +30,7 @@ T* CarveR(char** p, size_t n) {
 __global__ __launch_bounds__(kRenewThreads) void k_renew_gather(RenewArgs r) {
   const int l = blockIdx.y;
   const Leaf lf = r.leaves[l];
-  const int32_t* rows = (lf.buf == 0 ? r.idx : r.tmp) + lf.begin;
+  const int32_t* rows = RowBuf(r.idx, r.tmp, r.buf_stride, lf.buf) + lf.begin;
   const int64_t out0 = r.offsets[l];
   for (int i = blockIdx.x * kRenewThreads + threadIdx.x; i < lf.count; i += gridDim.x * kRenewThreads) {
     const int row = rows[i];

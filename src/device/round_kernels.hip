@@ -87,7 +87,7 @@ __device__ __forceinline__ int RValidInWave(int valid, int k, int w) {
 
 // per-expansion constants of the split kernel, staged in LDS once per workgroup
 struct SplitExp {
-  int pb, pc, src, blk_off, nblk, hl, single;
+  int pb, pc, src, dst, blk_off, nblk, hl, single;
   int fbyte, fwide;
   int sub_lo, sub_hi, offset, mfb;
   long long fcol;
@@ -127,6 +127,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
     x.pb = e.part_begin;
     x.pc = e.part_count;
     x.src = e.src_buf;
+    x.dst = e.dst_buf;
     x.blk_off = e.blk_off;
     x.nblk = e.nblk;
     x.hl = e.hist_left;
@@ -182,7 +183,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
   uint32_t gb[kSplitRows];
   auto load_rows = [&](int jn, int t0n, int r1n, int* rr) {
     const int vn = min(kSplitSub, r1n - t0n);
-    const int32_t* s = ex[jn].src ? a.tmp : a.idx;
+    const int32_t* s = RowBuf(a, ex[jn].src);
     const int pbn = ex[jn].pb;
 #pragma unroll
     for (int k = 0; k < kSplitRows; ++k) {
@@ -213,7 +214,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
     F.mfb = X.mfb;
     const SplitRule r = X.r;
     const uint32_t* cb = cat_bits[j];
-    int32_t* dst = X.src ? a.idx : a.tmp;
+    int32_t* dst = RowBuf(a, X.dst);
     for (int t0 = r0; t0 < r1; t0 += kSplitSub) {
       const int valid = min(kSplitSub, r1 - t0);
       // the next sub-tile of this workgroup: this block's next one, or the next block's first
@@ -422,6 +423,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_part(KArgs a) {
     x.pb = e.part_begin;
     x.pc = e.part_count;
     x.src = e.src_buf;
+    x.dst = e.dst_buf;
     x.blk_off = e.blk_off;
     x.nblk = e.nblk;
     x.hl = e.hist_left;
@@ -457,7 +459,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_part(KArgs a) {
   uint32_t gb[kSplitRows];
   auto load_rows = [&](int jn, int t0n, int r1n, int* rr) {
     const int vn = min(kSplitSub, r1n - t0n);
-    const int32_t* s = ex[jn].src ? a.tmp : a.idx;
+    const int32_t* s = RowBuf(a, ex[jn].src);
     const int pbn = ex[jn].pb;
 #pragma unroll
     for (int k = 0; k < kSplitRows; ++k) {
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(kPartThreads) void k_round_part(KArgs a) {
     F.mfb = X.mfb;
     const SplitRule r = X.r;
     const uint32_t* cb = cat_bits[j];
-    int32_t* dst = X.src ? a.idx : a.tmp;
+    int32_t* dst = RowBuf(a, X.dst);
     for (int t0 = r0; t0 < r1; t0 += kSplitSub) {
       const int valid = min(kSplitSub, r1 - t0);
       int nj = j, nt0 = t0 + kSplitSub, nr1 = r1;
@@ -571,7 +573,7 @@ __global__ __launch_bounds__(kHistThreads) void k_round_hist(KArgs a) {
       s_off[j] = off;
       s_beg[j] = b;
       s_rows[j] = h;
-      s_buf[j] = 1 - rd->e[j].src_buf;
+      s_buf[j] = rd->e[j].dst_buf;
       s_cap[j] = rd->e[j].blk_off;
       off += (h + rpb - 1) / rpb;
     }
@@ -585,7 +587,7 @@ __global__ __launch_bounds__(kHistThreads) void k_round_hist(KArgs a) {
     while (j + 1 < nexp && kb >= s_off[j + 1]) ++j;
     const int k = kb - s_off[j];
     const int r0 = s_beg[j] + k * rpb, r1 = min(s_beg[j] + s_rows[j], r0 + rpb);
-    HistBlock<false, GPW, UNITS>(a, lds, s_buf[j] ? a.tmp : a.idx, r0, r1, t,
+    HistBlock<false, GPW, UNITS>(a, lds, RowBuf(a, s_buf[j]), r0, r1, t,
                                  a.partials + static_cast<size_t>(s_cap[j] + k) * pstride + static_cast<size_t>(UNITS) * t.lo_bin);
   }
 }
@@ -660,8 +662,6 @@ __device__ __forceinline__ ArgC ArgWaveBest(ArgC c) {
   return c;
 }
 
-// the best split of child y (2j + lr) of the round from its per-feature results, by the
-// child's last split-scan workgroup (SplitInfo order: larger gain, then smaller real feature)
 // per-feature result slot of child y, inner feature f (distributed: rank-major blocks)
 __device__ __forceinline__ size_t RoundFbIndex(const KArgs& a, int y, int f) {
   if (!a.round_dist) return static_cast<size_t>(y) * a.p.num_features + f;
@@ -670,8 +670,11 @@ __device__ __forceinline__ size_t RoundFbIndex(const KArgs& a, int y, int f) {
   return (static_cast<size_t>(owner) * 2 * a.round_k + y) * a.max_owned + local;
 }
 
+// the best split of child y (2j + lr) of the round, node `node`, from its per-feature
+// results, by the child's last split-scan workgroup (SplitInfo order: larger gain, then
+// smaller real feature)
 template <int KIND, int NT>
-__device__ void ChildBest(const KArgs& a, int y, int leaf, int lr, RoundFindShared<KIND, NT>& sh) {
+__device__ void ChildBest(const KArgs& a, int y, int node, RoundFindShared<KIND, NT>& sh) {
   const int NF = a.p.num_features, tid = threadIdx.x;
   const FeatureBest* fb0 = a.feat_best;
   constexpr int kB = 8;
@@ -706,7 +709,7 @@ __device__ void ChildBest(const KArgs& a, int y, int leaf, int lr, RoundFindShar
   ArgC b = sh.arg[0];
 #pragma unroll
   for (int k = 1; k < NT / kWave; ++k) ArgTake(&b, sh.arg[k]);
-  const size_t ci = 2 * static_cast<size_t>(leaf) + lr;
+  const size_t ci = static_cast<size_t>(node);
   FeatureBest* dst = a.cbest + ci;
   // (write-through: with KArgs::plan_in_find another workgroup of this launch plans from them)
   if (tid == 0) {
@@ -765,7 +768,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   // data_parallel_tree_learner.cpp: global leaf counts from the SplitInfo)
   const int lc = dp ? E.lr[0].global_count : tl, rc = dp ? E.lr[1].global_count : pc - tl;
   const ChildStats cl = E.lr[lr];
-  const int leaf = E.leaf;
   const int md = a.p.sp.min_data_in_leaf;
   const bool skip = (a.p.max_depth > 0 && cl.depth >= a.p.max_depth) || (lc < 2 * md && rc < 2 * md);
   const bool is_hist = (lr == 0) == (E.hist_left != 0);
@@ -954,7 +956,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   }
   __syncthreads();
   if (!s_last) return;
-  ChildBest<KIND, NT>(a, y, leaf, lr, sh);
+  ChildBest<KIND, NT>(a, y, frow, sh);
   if (!a.plan_in_find) return;
   // the last child of the round to finish plans the next round (its scans' results were
   // published write-through; one agent-scope acquire)
@@ -1026,9 +1028,37 @@ __device__ __forceinline__ void WaveLdsSync() {  // lane 0's LDS stores before t
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// the argmax node among m < nn with take(m) (one wave; -1: none), for the speculation order:
+// larger gain, then lower node id
+template <typename Take>
+__device__ __forceinline__ int WaveArgmaxNode(const double* ng, int nn, Take take) {
+  const int lane = threadIdx.x & 63;
+  unsigned long long gk = 0;
+  uint32_t tk = 0;
+  for (int m = lane; m < nn; m += kWave) {
+    if (!take(m)) continue;
+    const unsigned long long k = GainKey(ng[m]);
+    const uint32_t t = ~static_cast<uint32_t>(m);
+    if (k > gk || (k == gk && t > tk)) {
+      gk = k;
+      tk = t;
+    }
+  }
+  const unsigned long long gm = WaveMaxDpp(gk);
+  if (gm == 0) return -1;
+  const uint32_t tm = WaveMaxDpp(gk == gm ? tk : 0u);
+  return static_cast<int>(~tm);
+}
+
+constexpr int kNoVd = 0x7fff;  // RoundPlanBody nvd: not on the speculation frontier
+
 // One workgroup.  ROOT: the root's best split from its per-feature results (FindRoot), then
-// the first plan.  Otherwise: fold the round's partition counts into the expansions, replay
-// the best-first order (wave 0, LDS tables), apply the accepted splits, plan the next round.
+// the first plan.  Otherwise: fold the round's partition counts into its nodes, replay the
+// best-first order over the leaves (wave 0, LDS tables): while the argmax leaf's node is
+// expanded its split is accepted and its children nodes become the leaves w and s + 1 -- so a
+// chain of speculative expansions is accepted in one replay.  Then the next round: the leaf
+// that ended the replay first, then the unexpanded nodes of highest gain at most round_vmax
+// levels below a leaf, within the tree's expansion budget.
 // Global loads are issued in few independent batches: every one is a ~1-2 us round trip.
 template <bool ROOT, int NT>
 __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
@@ -1038,19 +1068,23 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   __shared__ int s_pick[kMaxRoundExp];
   __shared__ int s_pc[kMaxRoundExp];
   Round* rd = a.rd;
-  const int L = a.p.num_leaves, NF = a.p.num_features, tid = threadIdx.x, lane = tid & 63;
-  // per-leaf tables: gain, real feature, inner feature, expanded (2: picked for the next
-  // round); the expanded leaves' children (2 per leaf); the accepted leaves
-  double* tg = reinterpret_cast<double*>(plan_lds);
-  double* tcg = tg + L;
-  int* trf = reinterpret_cast<int*>(tcg + 2 * L);
-  int* tfi = trf + L;
-  int* tex = tfi + L;
-  int* tcrf = tex + L;
-  int* tcfi = tcrf + 2 * L;
-  int* acc = tcfi + 2 * L;
+  const int L = a.p.num_leaves, NF = a.p.num_features, NN = a.round_nodes, tid = threadIdx.x, lane = tid & 63;
+  // node tables (gain, -inf when the node has no split; real feature; first child or -1;
+  // speculation depth) and leaf tables (gain, real feature, node; accepted leaves / nodes)
+  double* ng = reinterpret_cast<double*>(plan_lds);
+  double* tg = ng + NN;
+  int* nrf = reinterpret_cast<int*>(tg + L);
+  int* nch = nrf + NN;
+  int* nvd = nch + NN;
+  int* trf = nvd + NN;
+  int* tnode = trf + L;
+  int* acc = tnode + L;
+  int* accn = acc + L;
   const int s0 = rd->nsplit;
   const int nexp_prev = rd->nexp;
+  const int nn = rd->next_frow;  // nodes of the tree so far
+  const int next_slot = rd->next_slot;
+  const bool dp = a.p.data_parallel != 0;  // (global counts: the split's estimates)
   if (ROOT) {
     ArgC c = ArgNone();
     for (int f = tid; f < NF; f += kPlanThreads) {
@@ -1068,88 +1102,160 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     for (int k = 1; k < kPlanThreads / kWave; ++k) ArgTake(&b, s_arg[k]);
     if (b.idx >= 0 && b.g == -INFINITY) b.idx = -1;
     if (tid == 0) {
+      // node 0: the root leaf and its best split
+      FeatureBest fb = {};
+      fb.gain = -INFINITY;
+      fb.feature = fb.real_feature = -1;
       if (b.idx >= 0) {
-        ToDeviceSplit(a.feat_best[FeatBestIndex(a, 0, b.idx)], FeatCat(a, 0, b.idx), &a.best[0]);
+        fb = a.feat_best[FeatBestIndex(a, 0, b.idx)];
+        const uint32_t* cat = FeatCat(a, 0, b.idx);
+        if (fb.ncat > 0) {
+          for (int w = 0; w < kMaxCatWords; ++w) a.cbest_cat[w] = cat[w];
+        }
+        ToDeviceSplit(fb, cat, &a.best[0]);
       } else {
         NoSplit(&a.best[0]);
       }
-      tg[0] = b.idx >= 0 ? b.g : -INFINITY;
-      trf[0] = b.idx >= 0 ? b.rf : -1;
-      tfi[0] = b.idx;
-      tex[0] = 0;
+      a.cbest[0] = fb;
+      const Leaf R = a.leaves[0];
+      RNode r;
+      r.begin = R.begin;
+      r.count = R.count;
+      r.buf = R.buf;
+      r.expanded = 0;
+      r.child = -1;
+      r.total_left = 0;
+      r.st.sum_g = R.sum_g;
+      r.st.sum_h = R.sum_h;
+      r.st.output = R.output;
+      r.st.cmin = R.cmin;
+      r.st.cmax = R.cmax;
+      r.st.global_count = R.global_count;
+      r.st.depth = R.depth;
+      r.st.slot = R.slot;
+      r.st.leaf = 0;
+      r.st.frow = 0;
+      r.st.icmask = R.icmask;
+      a.rnode[0] = r;
+      ng[0] = b.idx >= 0 ? b.g : -INFINITY;
+      nrf[0] = b.idx >= 0 ? b.rf : -1;
+      nch[0] = -1;
+      nvd[0] = kNoVd;
+      tnode[0] = 0;
+      tg[0] = ng[0];
+      trf[0] = nrf[0];
     }
   } else {
-    // one batch of independent loads: every leaf's best, expanded flag and children's bests
-    if (tid < nexp_prev) a.exres[rd->e[tid].leaf].total_left = rd->cur[tid][0];
+    // the previous round's partition counts: its children's rows
+    if (tid < nexp_prev) {
+      const ExpPlan& E = rd->e[tid];
+      const int tl = rd->cur[tid][0];
+      const int pb = E.part_begin, pc = E.part_count, db = E.dst_buf, c = E.frow_child[0];
+      a.rnode[E.node].total_left = tl;
+      RNode* cn = a.rnode + c;
+      cn[0].begin = pb;
+      cn[0].count = tl;
+      cn[0].buf = db;
+      cn[1].begin = pb + tl;
+      cn[1].count = pc - tl;
+      cn[1].buf = db;
+    }
+    // one batch of independent loads: every node's best and children, every leaf's node
+    for (int n = tid; n < nn; n += kPlanThreads) {
+      const FeatureBest& cb = a.cbest[n];
+      const double g = cb.gain;
+      const int rf = cb.real_feature, fi = cb.feature;
+      const int ex = a.rnode[n].expanded, ch = a.rnode[n].child;
+      ng[n] = fi >= 0 ? g : -INFINITY;
+      nrf[n] = rf;
+      nch[n] = ex ? ch : -1;
+      nvd[n] = kNoVd;
+    }
+    for (int l = tid; l <= s0 && l < L; l += kPlanThreads) tnode[l] = a.leaves[l].frow;
+    __syncthreads();
     for (int l = tid; l <= s0 && l < L; l += kPlanThreads) {
-      const double g = a.best[l].gain;
-      const int rf = a.best[l].real_feature, fi = a.best[l].feature;
-      const int e = a.leaves[l].expanded;
-      const FeatureBest& c0 = a.cbest[2 * l];
-      const FeatureBest& c1 = a.cbest[2 * l + 1];
-      const double g0 = c0.gain, g1 = c1.gain;
-      const int r0 = c0.real_feature, r1 = c1.real_feature, f0 = c0.feature, f1 = c1.feature;
-      tg[l] = g;
-      trf[l] = rf;
-      tfi[l] = fi;
-      tex[l] = e;
-      tcg[2 * l] = g0;
-      tcg[2 * l + 1] = g1;
-      tcrf[2 * l] = r0;
-      tcrf[2 * l + 1] = r1;
-      tcfi[2 * l] = (f0 >= 0 && g0 != -INFINITY) ? f0 : -1;
-      tcfi[2 * l + 1] = (f1 >= 0 && g1 != -INFINITY) ? f1 : -1;
+      tg[l] = ng[tnode[l]];
+      trf[l] = nrf[tnode[l]];
     }
   }
   __syncthreads();
-  // replay of the sequential order by wave 0: the argmax leaf is split while its expansion is
-  // computed; its children (leaf ids w and s + 1) join the tables
+  // replay of the sequential order by wave 0: the argmax leaf is split while its node is
+  // expanded; its children nodes become leaves w and s + 1
   if (tid < kWave) {
-    int s = s0, done = 0;
+    int s = s0, done = 0, blocker = -1;
     for (;;) {
       if (s >= L - 1) {
         done = 1;
         break;
       }
       const int w = WaveArgmaxLeaf(tg, trf, s, [](int) { return true; });
-      if (!(tg[w] > 0.0 && tfi[w] >= 0)) {
+      if (!(tg[w] > 0.0)) {
         done = 1;
         break;
       }
-      if (!tex[w]) break;
+      const int n = tnode[w], c = nch[n];
+      if (c < 0) {
+        blocker = w;
+        break;
+      }
       if (lane == 0) {
         const int nl = s + 1;
         acc[s - s0] = w;
-        tg[w] = tcg[2 * w];
-        trf[w] = tcrf[2 * w];
-        tfi[w] = tcfi[2 * w];
-        tex[w] = 0;
-        tg[nl] = tcg[2 * w + 1];
-        trf[nl] = tcrf[2 * w + 1];
-        tfi[nl] = tcfi[2 * w + 1];
-        tex[nl] = 0;
+        accn[s - s0] = n;
+        tnode[w] = c;
+        tg[w] = ng[c];
+        trf[w] = nrf[c];
+        tnode[nl] = c + 1;
+        tg[nl] = ng[c + 1];
+        trf[nl] = nrf[c + 1];
       }
       WaveLdsSync();
       ++s;
     }
-    // the next round's expansions: the current unexpanded leaves of highest gain, in order
+    // the next round's expansions
     int n = 0;
     if (!done) {
-      const int kmax = min(a.round_k, L - 1 - s);
-      for (; n < kmax; ++n) {
-        const int l = WaveArgmaxLeaf(tg, trf, s, [&](int m) { return tex[m] == 0 && tg[m] > 0.0 && tfi[m] >= 0; });
-        if (l < 0) break;
+      // budget: after this round, one expansion per split the tree may still need stays
+      // available (each round then accepts at least its first pick, the blocker)
+      const int need = L - 1 - s, used = (nn - 1) / 2;
+      int kmax = min(a.round_k, need);
+      kmax = min(kmax, a.round_emax - used - (need - 1));
+      kmax = max(kmax, min(1, a.round_emax - used));
+      if (kmax > 0) {
+        // the speculation frontier: levels of the nodes below the leaves through expanded nodes
+        for (int l = lane; l <= s; l += kWave) nvd[tnode[l]] = 0;
+        WaveLdsSync();
+        for (int k = 1; k <= a.round_vmax; ++k) {
+          int any = 0;
+          for (int m = lane; m < nn; m += kWave) {
+            const int c = nch[m];
+            if (nvd[m] == k - 1 && c >= 0) {
+              nvd[c] = k;
+              nvd[c + 1] = k;
+              any = 1;
+            }
+          }
+          WaveLdsSync();
+          if (__ballot(any) == 0ull) break;
+        }
         if (lane == 0) {
-          s_pick[n] = l;
-          tex[l] = 2;
+          s_pick[0] = tnode[blocker];
+          nvd[tnode[blocker]] = kNoVd;
         }
         WaveLdsSync();
+        const int vmax = a.round_vmax;
+        for (n = 1; n < kmax; ++n) {
+          const int m = WaveArgmaxNode(ng, nn, [&](int q) { return nvd[q] <= vmax && nch[q] < 0 && ng[q] > 0.0; });
+          if (m < 0) break;
+          if (lane == 0) {
+            s_pick[n] = m;
+            nvd[m] = kNoVd;
+          }
+          WaveLdsSync();
+        }
+      } else {
+        done = 1;  // (unreachable: the budget keeps room for the blocker)
       }
-      // histogram slots / splittable rows left (bounded by construction; guarded anyway)
-      n = min(n, 2 * L - rd->next_slot);
-      n = min(n, (4 * L - rd->next_frow) / 2);
-      n = max(n, 0);
-      if (n == 0) done = 1;
     }
     if (lane == 0) {
       s_s1 = s;
@@ -1159,51 +1265,45 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   }
   __syncthreads();
   const int s1 = s_s1, nacc = s1 - s0, nexp = s_nexp;
-  // apply the accepted splits: split records and children leaves, then the children's bests
-  // (the record copies the parent's best first)
-  constexpr int kSplitWords = sizeof(DeviceSplit) / 4;
-  for (int i = tid; i < nacc * kSplitWords; i += kPlanThreads) {
-    const int k = i / kSplitWords, wd = i % kSplitWords;
-    reinterpret_cast<uint32_t*>(&a.rec[s0 + k].split)[wd] = reinterpret_cast<const uint32_t*>(&a.best[acc[k]])[wd];
-  }
+  // the accepted splits: split records (the node's best split, its partition counts)
   for (int k = tid; k < nacc; k += kPlanThreads) {
-    const int w = acc[k], s = s0 + k, nl = s + 1;
-    const ExpResult R = a.exres[w];
-    SplitRecord& rec = a.rec[s];
-    const bool dp = a.p.data_parallel != 0;  // (global counts: the split's estimates)
-    rec.leaf = w;
-    rec.left_count = dp ? R.lr[0].global_count : R.total_left;
-    rec.right_count = dp ? R.lr[1].global_count : R.count - R.total_left;
-    for (int c = 0; c < 2; ++c) {
-      Leaf lf;
-      const ChildStats& cs = R.lr[c];
-      lf.begin = c == 0 ? R.begin : R.begin + R.total_left;
-      lf.count = c == 0 ? R.total_left : R.count - R.total_left;
-      lf.global_count = dp ? cs.global_count : lf.count;
-      lf.depth = cs.depth;
-      lf.slot = cs.slot;
-      lf.buf = R.buf;
-      lf.frow = cs.frow;
-      lf.expanded = 0;
-      lf.icmask = cs.icmask;
-      lf.sum_g = cs.sum_g;
-      lf.sum_h = cs.sum_h;
-      lf.output = cs.output;
-      lf.lsum_g = lf.lsum_h = 0.0;
-      lf.cmin = cs.cmin;
-      lf.cmax = cs.cmax;
-      a.leaves[c == 0 ? w : nl] = lf;
-    }
+    const int n = accn[k];
+    const FeatureBest& cb = a.cbest[n];
+    const int tl = a.rnode[n].total_left, cnt = a.rnode[n].count;
+    SplitRecord& rec = a.rec[s0 + k];
+    rec.leaf = acc[k];
+    rec.left_count = dp ? cb.lc : tl;
+    rec.right_count = dp ? cb.rc : cnt - tl;
+    ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, &rec.split);
   }
-  __syncthreads();
+  // the leaves the replay changed, from their final nodes (a leaf changed twice is written
+  // twice with the same record)
   for (int i = tid; i < 2 * nacc; i += kPlanThreads) {
-    const int k = i >> 1, c = i & 1, w = acc[k];
-    const FeatureBest& cb = a.cbest[2 * w + c];
-    DeviceSplit* d = &a.best[c == 0 ? w : s0 + k + 1];
-    if (tcfi[2 * w + c] >= 0) ToDeviceSplit(cb, a.cbest_cat + (2 * static_cast<size_t>(w) + c) * kMaxCatWords, d);
+    const int k = i >> 1;
+    const int l = (i & 1) == 0 ? acc[k] : s0 + k + 1;
+    const int n = tnode[l];
+    const RNode R = a.rnode[n];
+    Leaf lf;
+    lf.begin = R.begin;
+    lf.count = R.count;
+    lf.global_count = dp ? R.st.global_count : R.count;
+    lf.depth = R.st.depth;
+    lf.slot = R.st.slot;
+    lf.buf = R.buf;
+    lf.frow = n;
+    lf.pad = 0;
+    lf.icmask = R.st.icmask;
+    lf.sum_g = R.st.sum_g;
+    lf.sum_h = R.st.sum_h;
+    lf.output = R.st.output;
+    lf.lsum_g = lf.lsum_h = 0.0;
+    lf.cmin = R.st.cmin;
+    lf.cmax = R.st.cmax;
+    a.leaves[l] = lf;
+    DeviceSplit* d = &a.best[l];
+    if (ng[n] != -INFINITY) ToDeviceSplit(a.cbest[n], a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, d);
     else NoSplit(d);
   }
-  __syncthreads();
   if (s_done) {
     if (tid == 0) {
       rd->done = 1;
@@ -1213,35 +1313,37 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     }
     return;
   }
-  const int next_slot = rd->next_slot, next_frow = rd->next_frow;
+  const int next_frow = nn;
+  const int nbuf = a.round_vmax + 2;
   if (tid < nexp) {
-    const int j = tid, l = s_pick[j];
-    // independent loads: the leaf, its best split and the split feature's record (inner
-    // feature from the table)
-    const Leaf P = a.leaves[l];
-    const DeviceSplit& sp = a.best[l];
-    const double lsg = sp.left_sum_gradient, lsh = sp.left_sum_hessian, lo = sp.left_output;
-    const double rsg = sp.right_sum_gradient, rsh = sp.right_sum_hessian, ro = sp.right_output;
-    const int lcnt = sp.left_count, rcnt = sp.right_count, mono = sp.monotone_type, iscat = sp.is_categorical;
-    const int fi = tfi[l];
+    const int j = tid, node = s_pick[j];
+    // independent loads: the node, its best split and the split feature's record
+    const RNode P = a.rnode[node];
+    const FeatureBest& cb = a.cbest[node];
+    const double lsg = cb.lg, lsh = cb.lh, lo = cb.lo;
+    const double rsg = cb.rg, rsh = cb.rh, ro = cb.ro;
+    const int lcnt = cb.lc, rcnt = cb.rc, mono = cb.mono, iscat = cb.ncat > 0 ? 1 : 0;
+    const int fi = cb.feature;
     const IcMask fmask = a.feat_icmask != nullptr ? a.feat_icmask[fi] : kIcAll;
     ExpPlan& e = rd->e[j];
     CopyWords(&a.feat[fi], &e.feat, 0, 1);
+    ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(node) * kMaxCatWords, &e.split);
     s_pc[j] = P.count;
     const int hl = lcnt <= rcnt ? 1 : 0;
-    e.leaf = l;
+    e.node = node;
     e.part_begin = P.begin;
     e.part_count = P.count;
     e.src_buf = P.buf;
+    e.dst_buf = P.buf + 1 == nbuf ? 0 : P.buf + 1;
     e.hist_left = hl;
-    e.slot_parent = P.slot;
+    e.slot_parent = P.st.slot;
     e.slot_new = next_slot + j;
-    e.frow_parent = P.frow;
+    e.frow_parent = node;
     e.frow_child[0] = next_frow + 2 * j;
     e.frow_child[1] = next_frow + 2 * j + 1;
     // children's statistics from the split (basic monotone constraints: the mid-point bound)
-    const int depth = P.depth + 1;
-    double pmin = P.cmin, pmax = P.cmax, rmin = P.cmin, rmax = P.cmax;
+    const int depth = P.st.depth + 1;
+    double pmin = P.st.cmin, pmax = P.st.cmax, rmin = P.st.cmin, rmax = P.st.cmax;
     if (!iscat) {
       const double mid = (lo + ro) / 2.0f;
       if (mono < 0) {
@@ -1252,7 +1354,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         rmin = fmax(rmin, mid);
       }
     }
-    const IcMask icm = P.icmask & fmask;
+    const IcMask icm = P.st.icmask & fmask;
     ChildStats lc, rc;
     lc.sum_g = lsg;
     lc.sum_h = lsh;
@@ -1261,8 +1363,8 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     lc.cmax = pmax;
     lc.global_count = lcnt;
     lc.depth = depth;
-    lc.slot = hl ? e.slot_new : P.slot;
-    lc.leaf = l;
+    lc.slot = hl ? e.slot_new : P.st.slot;
+    lc.leaf = -1;
     lc.frow = e.frow_child[0];
     lc.icmask = icm;
     rc.sum_g = rsg;
@@ -1272,26 +1374,24 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     rc.cmax = rmax;
     rc.global_count = rcnt;
     rc.depth = depth;
-    rc.slot = hl ? P.slot : e.slot_new;
+    rc.slot = hl ? P.st.slot : e.slot_new;
     rc.leaf = -1;
     rc.frow = e.frow_child[1];
     rc.icmask = icm;
     e.lr[0] = lc;
     e.lr[1] = rc;
-    ExpResult& R = a.exres[l];
-    R.begin = P.begin;
-    R.count = P.count;
-    R.buf = 1 - P.buf;
-    R.total_left = 0;
-    R.lr[0] = lc;
-    R.lr[1] = rc;
-    a.leaves[l].expanded = 1;
-    a.leaves[l].buf = 1 - P.buf;  // the round moves every row of the leaf to the other buffer
-  }
-  // the split record of each expansion (whole, categories included)
-  for (int i = tid; i < nexp * kSplitWords; i += kPlanThreads) {
-    const int k = i / kSplitWords, wd = i % kSplitWords;
-    reinterpret_cast<uint32_t*>(&rd->e[k].split)[wd] = reinterpret_cast<const uint32_t*>(&a.best[s_pick[k]])[wd];
+    a.rnode[node].expanded = 1;
+    a.rnode[node].child = e.frow_child[0];
+    RNode C;
+    C.begin = C.count = 0;  // (set by the next plan, from the partition counts)
+    C.buf = e.dst_buf;
+    C.expanded = 0;
+    C.child = -1;
+    C.total_left = 0;
+    C.st = lc;
+    a.rnode[e.frow_child[0]] = C;
+    C.st = rc;
+    a.rnode[e.frow_child[1]] = C;
   }
   __syncthreads();
   if (tid == 0) {
@@ -1335,9 +1435,9 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
   RoundPlanBody<ROOT, kPlanThreads>(a, plan_lds);
 }
 
-size_t RoundPlanLds(int num_leaves) {
-  const size_t L = static_cast<size_t>(num_leaves);
-  return L * sizeof(double) * 3 + L * sizeof(int) * (3 + 4 + 1);
+size_t RoundPlanLds(int num_leaves, int nodes) {
+  const size_t L = static_cast<size_t>(num_leaves), N = static_cast<size_t>(nodes);
+  return (N + L) * sizeof(double) + N * sizeof(int) * 3 + L * sizeof(int) * 4;
 }
 
 namespace {
@@ -1385,7 +1485,7 @@ bool RoundSimpleGains(const KArgs& a) {
 void LaunchRoundFind(const KArgs& a, hipStream_t s) {
   const int ny = 2 * a.round_k;
   size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
-  if (a.plan_in_find) lds = std::max(lds, RoundPlanLds(a.p.num_leaves));
+  if (a.plan_in_find) lds = std::max(lds, RoundPlanLds(a.p.num_leaves, a.round_nodes));
   const bool simple = RoundSimpleGains(a);
   const bool narrow = a.p.max_feature_bins <= kWave;
   const dim3 g(a.num_scan, ny), b(narrow ? kWave : kFindThreads), bc(kFindThreads);
@@ -1416,7 +1516,7 @@ __global__ __launch_bounds__(kFindThreads) void k_round_childbest(KArgs a) {
   if (rd->done) return;
   const int y = blockIdx.x;
   if (y >= 2 * rd->nexp) return;
-  ChildBest<0, kFindThreads>(a, y, rd->e[y >> 1].leaf, y & 1, sh);
+  ChildBest<0, kFindThreads>(a, y, rd->e[y >> 1].frow_child[y & 1], sh);
 }
 
 void PrepareRoundKernels(int max_lds) {
@@ -1439,14 +1539,14 @@ void PrepareRoundKernels(int max_lds) {
 }
 
 void RoundRootPlan(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_round_plan<true>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
+  hipLaunchKernelGGL((k_round_plan<true>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves, a.round_nodes), s, a);
 }
 
 void RoundStep(const KArgs& a, hipStream_t s) {
   RoundSplitReduce(a, s);
   RoundFind(a, s);
   if (!a.plan_in_find) {
-    hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
+    hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves, a.round_nodes), s, a);
   }
 }
 
@@ -1454,7 +1554,7 @@ void RoundFind(const KArgs& a, hipStream_t s) { LaunchRoundFind(a, s); }
 
 void RoundChildBestAndPlan(const KArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_round_childbest, dim3(2 * a.round_k), dim3(kFindThreads), 0, s, a);
-  hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves), s, a);
+  hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves, a.round_nodes), s, a);
 }
 
 void RoundSplitReduce(const KArgs& a, hipStream_t s) {

@@ -18,7 +18,7 @@ __global__ void k_add_leaf_score(KArgs a, const double* __restrict__ vals, int n
   if (leaf >= num_leaves) return;
   const Leaf lf = a.leaves[leaf];
   const double v = vals[leaf];
-  const int32_t* ids = lf.buf ? a.tmp : a.idx;
+  const int32_t* ids = RowBuf(a, lf.buf);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < lf.count; i += gridDim.x * blockDim.x) {
     score[ids[lf.begin + i]] += v;
   }

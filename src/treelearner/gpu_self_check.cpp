@@ -54,7 +54,7 @@ bool GPUTreeLearner::DebugLeafState(const Tree* tree, int leaf, std::vector<int3
   dev::Leaf lf;
   HIPCHECK(hipMemcpy(&lf, d_leaves_ + leaf, sizeof(lf), hipMemcpyDeviceToHost));
   rows->assign(static_cast<size_t>(lf.count), 0);
-  const int32_t* buf = lf.buf == 0 ? d_idx_ : d_tmp_;
+  const int32_t* buf = lf.buf == 0 ? d_idx_ : d_tmp_ + static_cast<int64_t>(lf.buf - 1) * num_data_;
   if (lf.count > 0) {
     HIPCHECK(hipMemcpy(rows->data(), buf + lf.begin, sizeof(int32_t) * lf.count, hipMemcpyDeviceToHost));
   }

@@ -310,8 +310,14 @@ void GPUTreeLearner::UploadData() {
     if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) round_k_ = std::atoi(e);
     round_k_ = std::max(1, std::min(dev::kMaxRoundExp, round_k_));
   }
-  hist_slots_ = round_k_ > 1 ? 2 * n_leaves : n_leaves;
-  split_rows_ = round_k_ > 1 ? 4 * n_leaves : n_leaves;
+  // speculation below the leaves (LGBM_AMD_ROUND_VMAX levels, 0: leaves only): one index
+  // buffer per level + 2 (device_types.h), bounded to 32 GiB of row indices
+  round_vmax_ = 6;
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_VMAX")) round_vmax_ = std::atoi(e);
+  round_vmax_ = std::max(0, std::min(dev::kMaxRoundVmax, round_vmax_));
+  while (round_vmax_ > 0 && static_cast<double>(num_data_) * 4.0 * (round_vmax_ + 1) > 32.0 * (1ull << 30)) --round_vmax_;
+  if (round_k_ <= 1) round_vmax_ = 0;
+  SizeRoundPools(n_leaves);
   d_tree_mask_ = Alloc<int8_t>(num_features_);
   d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
   h_node_mask_.clear();
@@ -319,7 +325,7 @@ void GPUTreeLearner::UploadData() {
   d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
   if (d_gh_ == nullptr) d_gh_ = Alloc<dev::GH>(num_data_);
   d_idx_ = Alloc<int32_t>(num_data_);
-  d_tmp_ = Alloc<int32_t>(num_data_);
+  d_tmp_ = Alloc<int32_t>(static_cast<size_t>(num_data_) * (round_vmax_ + 1));
   d_bag_ = Alloc<int32_t>(num_data_);
   d_oob_ = Alloc<int32_t>(num_data_);
   d_bag_count_ = Alloc<int32_t>(1);
@@ -425,6 +431,7 @@ void GPUTreeLearner::UploadData() {
   a.gh = d_gh_;
   a.idx = d_idx_;
   a.tmp = d_tmp_;
+  a.buf_stride = num_data_;
   a.leaves = d_leaves_;
   a.st = d_step_;
   a.find_sub = d_find_sub_;
@@ -580,7 +587,7 @@ void GPUTreeLearner::UploadData() {
   a.round_gr = 0;
   a.round_fused = 1;
   // the plan in the split scan's last workgroup while its tables fit the scan's LDS budget
-  a.plan_in_find = (!distributed_ && dev::RoundPlanLds(n_leaves) <= 16384) ? 1 : 0;
+  a.plan_in_find = (!distributed_ && dev::RoundPlanLds(n_leaves, split_rows_) <= 16384) ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_PLAN_IN_FIND")) a.plan_in_find = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_FUSED")) a.round_fused = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) a.round_grid = std::max(1, std::atoi(e));
@@ -590,18 +597,35 @@ void GPUTreeLearner::UploadData() {
   AllocSplittable();
 }
 
+// histogram slots and splittable rows (nodes) of a tree: one slot per leaf, or -- round
+// growth -- one per expansion (the root's, then the histogrammed child's of each), two nodes
+// per expansion; 3 * num_leaves expansions leave the speculation 2 * num_leaves of waste,
+// 2 * num_leaves when the slots would pass 16 GiB
+void GPUTreeLearner::SizeRoundPools(int n_leaves) {
+  hist_slots_ = n_leaves;
+  split_rows_ = n_leaves;
+  if (round_k_ > 1) {
+    const double slot_bytes = 16.0 * static_cast<double>(total_bins_);
+    const int per = slot_bytes * 3.0 * n_leaves > 16.0 * (1ull << 30) ? 2 : 3;
+    hist_slots_ = per * n_leaves;
+    split_rows_ = 2 * per * n_leaves;
+  }
+  args_.round_nodes = split_rows_;
+  args_.round_emax = std::min(hist_slots_ - 1, (split_rows_ - 1) / 2);
+  args_.round_vmax = round_vmax_;
+}
+
 void GPUTreeLearner::AllocRoundState() {
-  const int n_leaves = config_->num_leaves;
   dev::KArgs& a = args_;
-  a.exres = nullptr;
+  a.rnode = nullptr;
   a.cbest = nullptr;
   a.cbest_cat = nullptr;
   a.child_cnt = nullptr;
   if (round_k_ <= 1) return;
   d_round_ = Alloc<dev::Round>(1);
-  d_exres_ = Alloc<dev::ExpResult>(n_leaves);
-  d_cbest_ = Alloc<dev::FeatureBest>(2 * static_cast<size_t>(n_leaves));
-  d_cbest_cat_ = Alloc<uint32_t>(2 * static_cast<size_t>(n_leaves) * kMaxCatWords);
+  d_rnode_ = Alloc<dev::RNode>(split_rows_);
+  d_cbest_ = Alloc<dev::FeatureBest>(split_rows_);
+  d_cbest_cat_ = Alloc<uint32_t>(static_cast<size_t>(split_rows_) * kMaxCatWords);
   const size_t cnt = 2 * static_cast<size_t>(dev::kMaxRoundExp) * (dev::kFindSub + 1) * dev::kFindSubStride;
   d_child_cnt_ = Alloc<uint32_t>(cnt);
   HIPCHECK(hipMemset(d_child_cnt_, 0, sizeof(uint32_t) * cnt));
@@ -609,7 +633,7 @@ void GPUTreeLearner::AllocRoundState() {
   if (h_round_ == nullptr) {
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_round_), sizeof(dev::Round), hipHostMallocDefault));
   }
-  a.exres = d_exres_;
+  a.rnode = d_rnode_;
   a.cbest = d_cbest_;
   a.cbest_cat = d_cbest_cat_;
   a.child_cnt = d_child_cnt_;
@@ -754,8 +778,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
     d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
     d_best_ = Alloc<DeviceSplit>(n_leaves);
-    hist_slots_ = round_k_ > 1 ? 2 * n_leaves : n_leaves;
-    split_rows_ = round_k_ > 1 ? 4 * n_leaves : n_leaves;
+    SizeRoundPools(n_leaves);
     d_hist_ = Alloc<long long>(static_cast<size_t>(hist_slots_) * 2 * total_bins_);
     d_leaf_values_ = Alloc<double>(n_leaves);
     if (h_rec_) (void)hipHostFree(h_rec_);
@@ -1322,36 +1345,48 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   // the next tree enqueues as many rounds as this one took (rounded up to whole segments)
   round_pred_ = h_round_->rounds + 1;
   last_stats_.rounds = h_round_->rounds;
+  last_stats_.expansions = (h_round_->next_frow - 1) / 2;
   // (every enqueued round's collectives run; a finished tree's exit at once)
   last_stats_.collective_bytes = distributed_ ? root_collective_bytes_ + RoundCollectiveBytes() * launched : 0.0;
   return h_round_->nsplit;
 }
 
-// a leaf's raw histogram: its slot, or -- for a leaf whose pending expansion reused its slot
-// for the subtracted child -- the sum of its children's slots (self checks only)
+// a leaf's raw histogram: its slot, or -- round growth, for a node whose pending expansion
+// reused its slot for the subtracted child -- the sum over its children, recursively (self
+// checks only)
 void GPUTreeLearner::ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const {
+  (void)leaf;
   const size_t nh = 2 * static_cast<size_t>(total_bins_);
   raw->assign(nh, 0);
-  bool children = false;
-  dev::ExpResult r{};
-  if (lf.expanded && d_exres_ != nullptr) {
-    HIPCHECK(hipMemcpy(&r, d_exres_ + leaf, sizeof(r), hipMemcpyDeviceToHost));
-    const int md = config_->min_data_in_leaf;
-    const int lc = r.total_left, rc = r.count - r.total_left;
-    const bool skip = (config_->max_depth > 0 && r.lr[0].depth >= config_->max_depth) || (lc < 2 * md && rc < 2 * md);
-    children = !skip;
-  }
-  if (!children) {
-    HIPCHECK(hipMemcpy(raw->data(), d_hist_ + static_cast<size_t>(lf.slot) * nh, sizeof(long long) * nh,
+  std::vector<long long> part(nh);
+  std::vector<int> stack;
+  stack.push_back(d_rnode_ != nullptr ? lf.frow : -1);
+  while (!stack.empty()) {
+    const int n = stack.back();
+    stack.pop_back();
+    int slot = lf.slot;
+    if (n >= 0) {
+      dev::RNode r{};
+      HIPCHECK(hipMemcpy(&r, d_rnode_ + n, sizeof(r), hipMemcpyDeviceToHost));
+      slot = r.st.slot;
+      if (r.expanded) {
+        // (children of an expansion that cannot be split are not histogrammed)
+        dev::RNode c{};
+        HIPCHECK(hipMemcpy(&c, d_rnode_ + r.child, sizeof(c), hipMemcpyDeviceToHost));
+        const int md = config_->min_data_in_leaf;
+        const int lc = r.total_left, rc = r.count - r.total_left;
+        const bool skip = (config_->max_depth > 0 && c.st.depth >= config_->max_depth) || (lc < 2 * md && rc < 2 * md);
+        if (!skip) {
+          stack.push_back(r.child);
+          stack.push_back(r.child + 1);
+          continue;
+        }
+      }
+    }
+    HIPCHECK(hipMemcpy(part.data(), d_hist_ + static_cast<size_t>(slot) * nh, sizeof(long long) * nh,
                        hipMemcpyDeviceToHost));
-    return;
+    for (size_t i = 0; i < nh; ++i) (*raw)[i] += part[i];
   }
-  std::vector<long long> other(nh);
-  HIPCHECK(hipMemcpy(raw->data(), d_hist_ + static_cast<size_t>(r.lr[0].slot) * nh, sizeof(long long) * nh,
-                     hipMemcpyDeviceToHost));
-  HIPCHECK(hipMemcpy(other.data(), d_hist_ + static_cast<size_t>(r.lr[1].slot) * nh, sizeof(long long) * nh,
-                     hipMemcpyDeviceToHost));
-  for (size_t i = 0; i < nh; ++i) (*raw)[i] += other[i];
 }
 
 // voting: proposals -> allgather -> election + elected local histograms -> all-reduce
@@ -1424,6 +1459,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     root_rows_ = num_data_;
   }
   last_stats_.rounds = 0;
+  last_stats_.expansions = 0;
   last_stats_.graph = false;
   const bool rounds = RoundGrowth(a);
   if (!rounds && last_tree_rounds_) {
@@ -1718,7 +1754,7 @@ void GPUTreeLearner::DownloadPartitionToHost() const {
     self->leaf_begin_[l] = leaves[l].begin;
     self->leaf_count_[l] = l < num_leaves_now ? leaves[l].count : 0;
     if (self->leaf_count_[l] <= 0) continue;
-    const int32_t* srcbuf = leaves[l].buf ? d_tmp_ : d_idx_;
+    const int32_t* srcbuf = leaves[l].buf == 0 ? d_idx_ : d_tmp_ + static_cast<int64_t>(leaves[l].buf - 1) * num_data_;
     HIPCHECK(hipMemcpyAsync(self->indices_.data() + leaves[l].begin, srcbuf + leaves[l].begin,
                             sizeof(int32_t) * leaves[l].count, hipMemcpyDeviceToHost, stream_));
   }
@@ -1809,6 +1845,7 @@ bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction
   r.leaves = d_leaves_;
   r.idx = d_idx_;
   r.tmp = d_tmp_;
+  r.buf_stride = num_data_;
   r.label = d_label_;
   r.score = d_score_ + static_cast<size_t>(tree_id) * n;
   r.weights = spec.weights != nullptr ? d_renew_weights_ : nullptr;

@@ -141,13 +141,15 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   long long* d_round_send_ = nullptr;
   long long* d_round_owned_ = nullptr;
   void AllocRoundState();
+  void SizeRoundPools(int n_leaves);
   void ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const;  // (self checks)
   int round_k_ = 1;
-  int hist_slots_ = 0;      // histogram pool slots (round growth: 2 per leaf)
-  int split_rows_ = 0;      // rows of the splittable flags (round growth: 4 per leaf)
+  int round_vmax_ = 0;      // speculation levels below the leaves (index buffers: + 2)
+  int hist_slots_ = 0;      // histogram pool slots (round growth: one per expansion + the root's)
+  int split_rows_ = 0;      // rows of the splittable flags (round growth: the tree's nodes)
   dev::Round* d_round_ = nullptr;
   dev::Round* h_round_ = nullptr;
-  dev::ExpResult* d_exres_ = nullptr;
+  dev::RNode* d_rnode_ = nullptr;
   dev::FeatureBest* d_cbest_ = nullptr;
   uint32_t* d_cbest_cat_ = nullptr;
   uint32_t* d_child_cnt_ = nullptr;

@@ -106,6 +106,28 @@ def test_round_growth_many_row_blocks(monkeypatch, tmp_path, gpu_available):
     assert base == spec
 
 
+@pytest.mark.parametrize("vmax", ["0", "1", "3", "14"])
+def test_round_speculation_depth_does_not_change_trees(vmax, monkeypatch, tmp_path, gpu_available):
+    """Speculation below the leaves (expansions of the children of expanded, not yet accepted
+    leaves, LGBM_AMD_ROUND_VMAX levels deep, one index buffer per level + 2): the replay
+    accepts whole chains; the trees, and every leaf's rows (scores, quantile renewal), stay
+    those of one split per step."""
+    X, y = _data(n=200000, seed=12)
+    y = (X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.2 * np.random.RandomState(4).randn(len(y))).astype(np.float32)
+    params = {"objective": "quantile", "alpha": 0.4, "num_leaves": 63, "max_bin": 255, "bagging_fraction": 0.8,
+              "bagging_freq": 1}
+    base, _ = _model(monkeypatch, tmp_path, 1, X, y, params, rounds=8, tag="vd" + vmax)
+    monkeypatch.setenv("LGBM_AMD_ROUND_VMAX", vmax)
+    spec, rows = _model(monkeypatch, tmp_path, 8, X, y, params, rounds=8, tag="vd" + vmax)
+    assert base == spec
+    rounds = [r for row in rows for r in row["rounds"]]
+    splits = [lv - 1 for row in rows for lv in row["leaves"]]
+    assert all(r > 0 for r, s in zip(rounds, splits) if s > 0)
+    if vmax != "0":
+        # chains are accepted in one replay
+        assert sum(rounds) < 0.5 * sum(splits), (rounds, splits)
+
+
 @pytest.mark.parametrize("fused", ["0", "1"])
 def test_round_kernel_variants(fused, monkeypatch, tmp_path, gpu_available):
     """The fused partition + histogram kernel and the partition / per-child histogram pair."""
