@@ -1028,37 +1028,13 @@ __device__ __forceinline__ void WaveLdsSync() {  // lane 0's LDS stores before t
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// the argmax node among m < nn with take(m) (one wave; -1: none), for the speculation order:
-// larger gain, then lower node id
-template <typename Take>
-__device__ __forceinline__ int WaveArgmaxNode(const double* ng, int nn, Take take) {
-  const int lane = threadIdx.x & 63;
-  unsigned long long gk = 0;
-  uint32_t tk = 0;
-  for (int m = lane; m < nn; m += kWave) {
-    if (!take(m)) continue;
-    const unsigned long long k = GainKey(ng[m]);
-    const uint32_t t = ~static_cast<uint32_t>(m);
-    if (k > gk || (k == gk && t > tk)) {
-      gk = k;
-      tk = t;
-    }
-  }
-  const unsigned long long gm = WaveMaxDpp(gk);
-  if (gm == 0) return -1;
-  const uint32_t tm = WaveMaxDpp(gk == gm ? tk : 0u);
-  return static_cast<int>(~tm);
-}
-
-constexpr int kNoVd = 0x7fff;  // RoundPlanBody nvd: not on the speculation frontier
-
 // One workgroup.  ROOT: the root's best split from its per-feature results (FindRoot), then
 // the first plan.  Otherwise: fold the round's partition counts into its nodes, replay the
 // best-first order over the leaves (wave 0, LDS tables): while the argmax leaf's node is
 // expanded its split is accepted and its children nodes become the leaves w and s + 1 -- so a
-// chain of speculative expansions is accepted in one replay.  Then the next round: the leaf
-// that ended the replay first, then the unexpanded nodes of highest gain at most round_vmax
-// levels below a leaf, within the tree's expansion budget.
+// chain of speculative expansions is accepted in one replay.  Then the next round: the nodes
+// the sequential order is predicted to need next, the leaf that ended the replay first,
+// within the tree's expansion budget.
 // Global loads are issued in few independent batches: every one is a ~1-2 us round trip.
 template <bool ROOT, int NT>
 __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
@@ -1069,17 +1045,21 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   __shared__ int s_pc[kMaxRoundExp];
   Round* rd = a.rd;
   const int L = a.p.num_leaves, NF = a.p.num_features, NN = a.round_nodes, tid = threadIdx.x, lane = tid & 63;
-  // node tables (gain, -inf when the node has no split; real feature; first child or -1;
-  // speculation depth) and leaf tables (gain, real feature, node; accepted leaves / nodes)
+  // node tables (gain, -inf when the node has no split; real feature; first child or -1),
+  // leaf tables (gain, real feature, node; accepted leaves / nodes) and the prediction's copies
+  // of the leaf tables (+ levels below the real leaf)
   double* ng = reinterpret_cast<double*>(plan_lds);
   double* tg = ng + NN;
-  int* nrf = reinterpret_cast<int*>(tg + L);
+  double* sg = tg + L;
+  int* nrf = reinterpret_cast<int*>(sg + L);
   int* nch = nrf + NN;
-  int* nvd = nch + NN;
-  int* trf = nvd + NN;
+  int* trf = nch + NN;
   int* tnode = trf + L;
   int* acc = tnode + L;
   int* accn = acc + L;
+  int* srf = accn + L;
+  int* snode = srf + L;
+  int* svd = snode + L;
   const int s0 = rd->nsplit;
   const int nexp_prev = rd->nexp;
   const int nn = rd->next_frow;  // nodes of the tree so far
@@ -1140,7 +1120,6 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       ng[0] = b.idx >= 0 ? b.g : -INFINITY;
       nrf[0] = b.idx >= 0 ? b.rf : -1;
       nch[0] = -1;
-      nvd[0] = kNoVd;
       tnode[0] = 0;
       tg[0] = ng[0];
       trf[0] = nrf[0];
@@ -1169,7 +1148,6 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       ng[n] = fi >= 0 ? g : -INFINITY;
       nrf[n] = rf;
       nch[n] = ex ? ch : -1;
-      nvd[n] = kNoVd;
     }
     for (int l = tid; l <= s0 && l < L; l += kPlanThreads) tnode[l] = a.leaves[l].frow;
     __syncthreads();
@@ -1212,7 +1190,10 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       WaveLdsSync();
       ++s;
     }
-    // the next round's expansions
+    // the next round's expansions: the sequential order predicted past the blocker from the
+    // splits known so far (copies of the leaf tables): an expanded argmax joins its children,
+    // an unexpanded one is needed next -- picked (within round_vmax levels below its leaf)
+    // with its children unknown.  The blocker is the first pick.
     int n = 0;
     if (!done) {
       // budget: after this round, one expansion per split the tree may still need stays
@@ -1221,41 +1202,43 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       int kmax = min(a.round_k, need);
       kmax = min(kmax, a.round_emax - used - (need - 1));
       kmax = max(kmax, min(1, a.round_emax - used));
-      if (kmax > 0) {
-        // the speculation frontier: levels of the nodes below the leaves through expanded nodes
-        for (int l = lane; l <= s; l += kWave) nvd[tnode[l]] = 0;
-        WaveLdsSync();
-        for (int k = 1; k <= a.round_vmax; ++k) {
-          int any = 0;
-          for (int m = lane; m < nn; m += kWave) {
-            const int c = nch[m];
-            if (nvd[m] == k - 1 && c >= 0) {
-              nvd[c] = k;
-              nvd[c + 1] = k;
-              any = 1;
-            }
-          }
-          WaveLdsSync();
-          if (__ballot(any) == 0ull) break;
-        }
-        if (lane == 0) {
-          s_pick[0] = tnode[blocker];
-          nvd[tnode[blocker]] = kNoVd;
-        }
-        WaveLdsSync();
-        const int vmax = a.round_vmax;
-        for (n = 1; n < kmax; ++n) {
-          const int m = WaveArgmaxNode(ng, nn, [&](int q) { return nvd[q] <= vmax && nch[q] < 0 && ng[q] > 0.0; });
-          if (m < 0) break;
-          if (lane == 0) {
-            s_pick[n] = m;
-            nvd[m] = kNoVd;
-          }
-          WaveLdsSync();
-        }
-      } else {
-        done = 1;  // (unreachable: the budget keeps room for the blocker)
+      if (kmax <= 0) done = 1;  // (unreachable: the budget keeps room for the blocker)
+      for (int l = lane; l <= s; l += kWave) {
+        sg[l] = tg[l];
+        srf[l] = trf[l];
+        snode[l] = tnode[l];
+        svd[l] = 0;
       }
+      WaveLdsSync();
+      const int vmax = a.round_vmax;
+      for (int ss = s; !done && n < kmax && ss < L - 1; ++ss) {
+        const int w = WaveArgmaxLeaf(sg, srf, ss, [](int) { return true; });
+        if (!(sg[w] > 0.0)) break;
+        const int nd = snode[w], c = nch[nd], v = svd[w];
+        if (lane == 0) {
+          const int nl = ss + 1;
+          if (c >= 0) {
+            snode[w] = c;
+            sg[w] = ng[c];
+            srf[w] = nrf[c];
+            svd[w] = v + 1;
+            snode[nl] = c + 1;
+            sg[nl] = ng[c + 1];
+            srf[nl] = nrf[c + 1];
+            svd[nl] = v + 1;
+          } else {
+            if (v <= vmax) s_pick[n] = nd;
+            sg[w] = -INFINITY;
+            srf[w] = -1;
+            sg[nl] = -INFINITY;
+            srf[nl] = -1;
+            snode[nl] = -1;
+          }
+        }
+        if (c < 0 && v <= vmax) ++n;
+        WaveLdsSync();
+      }
+      if (n == 0) done = 1;  // (unreachable: the blocker is the first argmax)
     }
     if (lane == 0) {
       s_s1 = s;
@@ -1437,7 +1420,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
 
 size_t RoundPlanLds(int num_leaves, int nodes) {
   const size_t L = static_cast<size_t>(num_leaves), N = static_cast<size_t>(nodes);
-  return (N + L) * sizeof(double) + N * sizeof(int) * 3 + L * sizeof(int) * 4;
+  return (N + 2 * L) * sizeof(double) + N * sizeof(int) * 2 + L * sizeof(int) * 7;
 }
 
 namespace {
