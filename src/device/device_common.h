@@ -147,6 +147,19 @@ __device__ __forceinline__ T WaveLane63(T v) {
   }
 }
 
+// lane l's value (l wave-uniform)
+template <typename T>
+__device__ __forceinline__ T ReadLane(T v, int l) {
+  if constexpr (sizeof(T) == 4) {
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+  } else {
+    const long long x = __builtin_bit_cast(long long, v);
+    const unsigned lo = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x), l));
+    const unsigned hi = static_cast<unsigned>(__builtin_amdgcn_readlane(static_cast<int>(x >> 32), l));
+    return __builtin_bit_cast(T, static_cast<long long>((static_cast<unsigned long long>(hi) << 32) | lo));
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ T WaveSum(T v) {
 #if LGBM_DPP_SCAN

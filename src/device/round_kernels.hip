@@ -743,6 +743,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   __shared__ int s_last;
   Round* rd = a.rd;
   if (rd->done) return;
+  if (a.ktrace != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && rd->round < a.p.num_leaves) {
+    a.ktrace[static_cast<size_t>(rd->round) * kTraceSlots + 25] = wall_clock64();
+  }
   const int y = blockIdx.y, j = y >> 1, lr = y & 1;
   const int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
   const int tid = threadIdx.x;
@@ -1028,6 +1031,93 @@ __device__ __forceinline__ void WaveLdsSync() {  // lane 0's LDS stores before t
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Replay + prediction with one leaf per lane in registers (num_leaves <= 64, wave 0): a step
+// is one 64-bit DPP max over the gain keys (the tie key's max only when gains tie exactly),
+// reads of the winner's lane, and LDS reads of the node tables by the two lanes whose leaf
+// changes -- no LDS round trip through every lane per step.  Same order and picks as the LDS
+// tables' loop below.
+struct RegLeaf {
+  double g;
+  int rf, node, ch;
+};
+__device__ __forceinline__ int RegArgmax(const RegLeaf& x, bool live) {
+  const int lane = threadIdx.x & 63;
+  const unsigned long long gk = live ? GainKey(x.g) : 0ull;
+  const unsigned long long gm = WaveMaxDpp(gk);
+  const unsigned long long tied = __ballot(gk == gm);
+  if (__popcll(tied) == 1) return __builtin_amdgcn_readfirstlane(static_cast<int>(__builtin_ctzll(tied)));
+  const uint32_t tm = WaveMaxDpp(gk == gm ? TieKey(x.rf, lane) : 0u);
+  return static_cast<int>((~tm) & 1023u);
+}
+__device__ __forceinline__ void RegLoad(RegLeaf* x, int node, const double* ng, const int* nrf, const int* nch) {
+  x->node = node;
+  x->g = node >= 0 ? ng[node] : -INFINITY;
+  x->rf = node >= 0 ? nrf[node] : -1;
+  x->ch = node >= 0 ? nch[node] : -1;
+}
+// returns s (splits after the replay); *done, *npick; acc / accn / s_pick / tnode as the LDS path
+__device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, const double* ng, const int* nrf,
+                                 const int* nch, int* tnode, int* acc, int* accn, int* s_pick, int* done_out,
+                                 int* npick_out) {
+  const int lane = threadIdx.x & 63;
+  RegLeaf x;
+  RegLoad(&x, lane <= s0 ? tnode[lane] : -1, ng, nrf, nch);
+  int s = s0, done = 0;
+  for (;;) {
+    if (s >= L - 1) {
+      done = 1;
+      break;
+    }
+    const int w = RegArgmax(x, lane <= s);
+    if (!(ReadLane(x.g, w) > 0.0)) {
+      done = 1;
+      break;
+    }
+    const int c = ReadLane(x.ch, w);
+    if (c < 0) break;
+    const int nl = s + 1;
+    if (lane == 0) {
+      acc[s - s0] = w;
+      accn[s - s0] = ReadLane(x.node, w);
+    }
+    if (lane == w) RegLoad(&x, c, ng, nrf, nch);
+    if (lane == nl) RegLoad(&x, c + 1, ng, nrf, nch);
+    ++s;
+  }
+  if (lane <= s) tnode[lane] = x.node;
+  int n = 0;
+  if (!done) {
+    const int need = L - 1 - s;
+    int kmax = min(a.round_k, need);
+    kmax = min(kmax, a.round_emax - used - (need - 1));
+    kmax = max(kmax, min(1, a.round_emax - used));
+    if (kmax <= 0) done = 1;
+    const int vmax = a.round_vmax;
+    int vd = 0;
+    for (int ss = s; !done && n < kmax && ss < L - 1; ++ss) {
+      const int w = RegArgmax(x, lane <= ss);
+      if (!(ReadLane(x.g, w) > 0.0)) break;
+      const int c = ReadLane(x.ch, w), v = ReadLane(vd, w);
+      const int nl = ss + 1;
+      if (c >= 0) {
+        if (lane == w) RegLoad(&x, c, ng, nrf, nch);
+        if (lane == nl) RegLoad(&x, c + 1, ng, nrf, nch);
+        if (lane == w || lane == nl) vd = v + 1;
+      } else {
+        if (v <= vmax) {
+          if (lane == 0) s_pick[n] = ReadLane(x.node, w);
+          ++n;
+        }
+        if (lane == w || lane == nl) RegLoad(&x, -1, ng, nrf, nch);
+      }
+    }
+    if (n == 0) done = 1;
+  }
+  *done_out = done;
+  *npick_out = n;
+  return s;
+}
+
 // One workgroup.  ROOT: the root's best split from its per-feature results (FindRoot), then
 // the first plan.  Otherwise: fold the round's partition counts into its nodes, replay the
 // best-first order over the leaves (wave 0, LDS tables): while the argmax leaf's node is
@@ -1062,9 +1152,21 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   int* svd = snode + L;
   const int s0 = rd->nsplit;
   const int nexp_prev = rd->nexp;
+  const int round0 = rd->round, rounds0 = rd->rounds, accmax0 = rd->accepted_max;
   const int nn = rd->next_frow;  // nodes of the tree so far
   const int next_slot = rd->next_slot;
   const bool dp = a.p.data_parallel != 0;  // (global counts: the split's estimates)
+  // LGBM_AMD_KTRACE: phase times of the plan (slots 16..24 of the round it ends)
+  long long* ktr = (a.ktrace != nullptr && tid == 0 && rd->round < L) ? a.ktrace + static_cast<size_t>(rd->round) * kTraceSlots : nullptr;
+  long long tprev = ktr != nullptr ? wall_clock64() : 0;
+  if (ktr != nullptr) ktr[16] = tprev;
+  auto stamp = [&](int k) {
+    if (ktr != nullptr) {
+      const long long now = wall_clock64();
+      ktr[k] = now - tprev;
+      tprev = now;
+    }
+  };
   if (ROOT) {
     ArgC c = ArgNone();
     for (int f = tid; f < NF; f += kPlanThreads) {
@@ -1157,9 +1259,18 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     }
   }
   __syncthreads();
+  stamp(17);
   // replay of the sequential order by wave 0: the argmax leaf is split while its node is
   // expanded; its children nodes become leaves w and s + 1
-  if (tid < kWave) {
+  if (tid < kWave && L <= kWave) {
+    int done = 0, n = 0;
+    const int s = ReplayPredictRegs(a, L, s0, (nn - 1) / 2, ng, nrf, nch, tnode, acc, accn, s_pick, &done, &n);
+    if (lane == 0) {
+      s_s1 = s;
+      s_done = done;
+      s_nexp = done ? 0 : n;
+    }
+  } else if (tid < kWave) {
     int s = s0, done = 0, blocker = -1;
     for (;;) {
       if (s >= L - 1) {
@@ -1248,6 +1359,11 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   }
   __syncthreads();
   const int s1 = s_s1, nacc = s1 - s0, nexp = s_nexp;
+  stamp(18);
+  if (ktr != nullptr) {
+    ktr[22] = nacc;
+    ktr[23] = nexp;
+  }
   // the accepted splits: split records (the node's best split, its partition counts)
   for (int k = tid; k < nacc; k += kPlanThreads) {
     const int n = accn[k];
@@ -1287,12 +1403,13 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     if (ng[n] != -INFINITY) ToDeviceSplit(a.cbest[n], a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, d);
     else NoSplit(d);
   }
+  stamp(19);
   if (s_done) {
     if (tid == 0) {
       rd->done = 1;
       rd->nsplit = s1;
       rd->nexp = 0;
-      rd->accepted_max = max(rd->accepted_max, nacc);
+      rd->accepted_max = max(accmax0, nacc);
     }
     return;
   }
@@ -1377,6 +1494,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     a.rnode[e.frow_child[1]] = C;
   }
   __syncthreads();
+  stamp(20);
   if (tid == 0) {
     // row blocks: one size for the round (at least blk_min_rows, at most the packed headroom)
     long long rows = 0;
@@ -1404,11 +1522,12 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     rd->nsplit = s1;
     rd->next_slot = next_slot + nexp;
     rd->next_frow = next_frow + 2 * nexp;
-    rd->round = ROOT ? 1 : rd->round + 1;  // (parity 0 of the first round holds the root histogram)
-    rd->rounds = rd->rounds + 1;
-    rd->accepted_max = max(rd->accepted_max, nacc);
+    rd->round = ROOT ? 1 : round0 + 1;  // (parity 0 of the first round holds the root histogram)
+    rd->rounds = rounds0 + 1;
+    rd->accepted_max = max(accmax0, nacc);
   }
   if (tid < kMaxRoundExp) rd->cur[tid][0] = rd->cur[tid][1] = 0;
+  stamp(21);
 }
 
 template <bool ROOT>

@@ -637,7 +637,7 @@ void GPUTreeLearner::AllocRoundState() {
   a.cbest = d_cbest_;
   a.cbest_cat = d_cbest_cat_;
   a.child_cnt = d_child_cnt_;
-  round_pred_ = 0;
+  round_hist_.clear();
 }
 
 // Feature ownership of the distributed learners (reference data_parallel_tree_learner.cpp
@@ -1117,9 +1117,12 @@ void GPUTreeLearner::ReportKernelTrace(int num_splits) {
 void GPUTreeLearner::DestroyGraph() {
   if (graph_exec_ != nullptr) (void)hipGraphExecDestroy(graph_exec_);
   graph_exec_ = nullptr;
-  if (round_root_exec_ != nullptr) (void)hipGraphExecDestroy(round_root_exec_);
+  for (hipGraphExec_t& e : round_root_execs_) {
+    if (e != nullptr) (void)hipGraphExecDestroy(e);
+  }
+  round_root_execs_.clear();
   if (round_seg_exec_ != nullptr) (void)hipGraphExecDestroy(round_seg_exec_);
-  round_root_exec_ = round_seg_exec_ = nullptr;
+  round_seg_exec_ = nullptr;
 }
 
 // the whole tree as a stream-ordered kernel sequence (no host synchronisation inside)
@@ -1237,12 +1240,14 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
   return true;
 }
 
-// rounds of kRoundSeg expansions per graph launch: the root graph (root + one segment) and as
-// many segment graphs as the previous tree needed are enqueued back to back; the host then
-// checks the Round record and adds segments until the tree is done (a finished tree's
-// kernels exit at once, so over-provisioning costs ~1.6 us per kernel)
+// rounds of kRoundSeg expansions per graph launch: one root graph (the root + as many
+// segments as the recent trees needed, one cached graph per segment count) is launched; the
+// host then checks the Round record and adds segment graphs until the tree is done (a finished
+// tree's kernels exit at once: an over-provisioned round costs ~12 us, a missing one a host
+// round trip of ~60 us and a graph launch of ~8 us per segment)
 namespace {
 constexpr int kRoundSeg = 4;
+constexpr int kRoundFirstPred = 16;  // rounds enqueued for the first tree
 }
 
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
@@ -1256,13 +1261,13 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   DeviceComm* dc = distributed_ ? Network::device_comm() : nullptr;
   const bool use_graph = !(ng != nullptr && ng[0] == '1') && (dc == nullptr || dc->CaptureSafe()) && !graph_capture_failed_;
   const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
-  auto capture = [&](hipGraphExec_t* exec, bool root) {
+  auto capture = [&](hipGraphExec_t* exec, bool root, int rounds) {
     hipGraph_t g = nullptr;
     HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
     std::string why;
     try {
       if (root) EnqueueRoot(a);
-      for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
+      for (int r = 0; r < rounds; ++r) EnqueueRound(a);
     } catch (const std::exception& e) {
       why = e.what();
     }
@@ -1280,15 +1285,28 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     }
     return true;
   };
+  const int L = config_->num_leaves;
+  // segments of the root graph: the most rounds of the last trees (+1), rounded up
+  int want = kRoundFirstPred;
+  if (!round_hist_.empty()) want = *std::max_element(round_hist_.begin(), round_hist_.end()) + 1;
+  want = std::max(1, std::min(want, L - 1));
+  const int nseg = (want + kRoundSeg - 1) / kRoundSeg;
   bool graph = use_graph;
-  if (graph && (round_root_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
+  if (graph && (round_seg_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
                 round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
     DestroyGraph();
-    graph = capture(&round_root_exec_, true) && capture(&round_seg_exec_, false);
+    graph = capture(&round_seg_exec_, false, kRoundSeg);
     if (!graph) DestroyGraph();
     round_graph_rows_ = a.num_rows;
     round_graph_identity_ = a.root_identity;
     round_graph_root_mode_ = root_mode;
+  }
+  if (graph) {
+    if (static_cast<int>(round_root_execs_.size()) <= nseg) round_root_execs_.resize(nseg + 1, nullptr);
+    if (round_root_execs_[nseg] == nullptr) {
+      graph = capture(&round_root_execs_[nseg], true, nseg * kRoundSeg);
+      if (!graph) DestroyGraph();
+    }
   }
   last_stats_.graph = graph;
   auto launch_seg = [&]() {
@@ -1299,18 +1317,12 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     }
   };
   if (graph) {
-    HIPCHECK(hipGraphLaunch(round_root_exec_, stream_));
+    HIPCHECK(hipGraphLaunch(round_root_execs_[nseg], stream_));
   } else {
     EnqueueRoot(a);
-    for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
+    for (int r = 0; r < nseg * kRoundSeg; ++r) EnqueueRound(a);
   }
-  const int L = config_->num_leaves;
-  int launched = kRoundSeg;
-  const int want = round_pred_ > 0 ? round_pred_ : L - 1;
-  while (launched < want) {
-    launch_seg();
-    launched += kRoundSeg;
-  }
+  int launched = nseg * kRoundSeg;
   const size_t rec_bytes = sizeof(dev::SplitRecord) * std::max(1, L - 1);
   for (;;) {
     HIPCHECK(hipMemcpyAsync(h_round_, d_round_, sizeof(dev::Round), hipMemcpyDeviceToHost, stream_));
@@ -1328,6 +1340,15 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
     HIPCHECK(hipMemcpy(t.data(), a.ktrace, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
     static const char* names[] = {"stage", "side", "resv", "write", "gather", "tail", "store"};
+    // plans: slot 16 entry time, 17..21 phase times (loads, replay + prediction, acceptance,
+    // entries, sizing), 22 accepted, 23 planned, 25 the split scan's start
+    for (int r = 0; r <= h_round_->rounds && r < L; ++r) {
+      const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
+      if (o[16] == 0) continue;
+      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay+predict=%.2f accept=%.2f entries=%.2f sizing=%.2f us; accepted %lld planned %lld\n",
+                   r, o[25] != 0 ? (o[16] - o[25]) / 100.0 : 0.0, o[17] / 100.0, o[18] / 100.0, o[19] / 100.0,
+                   o[20] / 100.0, o[21] / 100.0, o[22], o[23]);
+    }
     for (int r = 1; r <= h_round_->rounds && r < L; ++r) {
       const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
       std::string line = "round " + std::to_string(r) + " exp " + std::to_string(o[10]) + " blocks " +
@@ -1342,8 +1363,9 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
       std::fprintf(stderr, "%s%s\n", line.c_str(), buf);
     }
   }
-  // the next tree enqueues as many rounds as this one took (rounded up to whole segments)
-  round_pred_ = h_round_->rounds + 1;
+  // the next tree enqueues the most rounds of the last kRoundHist trees (+1)
+  round_hist_.push_back(h_round_->rounds);
+  if (round_hist_.size() > kRoundHist) round_hist_.erase(round_hist_.begin());
   last_stats_.rounds = h_round_->rounds;
   last_stats_.expansions = (h_round_->next_frow - 1) / 2;
   // (every enqueued round's collectives run; a finished tree's exit at once)

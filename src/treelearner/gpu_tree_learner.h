@@ -153,10 +153,11 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   dev::FeatureBest* d_cbest_ = nullptr;
   uint32_t* d_cbest_cat_ = nullptr;
   uint32_t* d_child_cnt_ = nullptr;
-  hipGraphExec_t round_root_exec_ = nullptr;  // root + kRoundSeg rounds
-  hipGraphExec_t round_seg_exec_ = nullptr;   // kRoundSeg rounds
+  std::vector<hipGraphExec_t> round_root_execs_;  // [n]: root + n * kRoundSeg rounds (captured on first use)
+  hipGraphExec_t round_seg_exec_ = nullptr;        // kRoundSeg rounds
   int round_graph_rows_ = -1, round_graph_identity_ = -1, round_graph_root_mode_ = -1;
-  int round_pred_ = 0;        // rounds the next tree is expected to take (enqueued before the first check)
+  static constexpr size_t kRoundHist = 3;
+  std::vector<int> round_hist_;  // rounds of the last kRoundHist trees (the next one enqueues their max + 1)
   bool last_tree_rounds_ = false;
 
   void SetupOwnership();
