@@ -310,12 +310,15 @@ struct GradArgs {
   const double* score;       // [num_class][num_data]
   float* grad;
   float* hess;
+  int32_t write_split;       // also write grad / hess (else only gh: UnpackGH materialises them on demand)
   GH* gh;                    // optional fused packing (one model per iteration; rows gh_stride apart):
   int64_t gh_stride;
   float* max_parts;          //   interleaved (g, h), per-workgroup max|g| / max h and
   double* root_parts;        //   (sum g, sum h), [GradientBlocks][2] each
 };
 void Gradients(const GradArgs& g, hipStream_t s);
+// grad / hess from the interleaved (g, h) (rows gh_stride apart)
+void UnpackGH(const GH* gh, int64_t gh_stride, int64_t n, float* grad, float* hess, hipStream_t s);
 // listwise ranking gradients (LambdaRank-NDCG / XE-NDCG), one workgroup per query
 constexpr int kRankKindLambdarank = 15;
 constexpr int kRankKindXendcg = 16;
@@ -446,9 +449,10 @@ size_t RenewScratchBytes(int64_t n, int leaves);
 void RenewLeafOutputs(RenewArgs r, int64_t n, hipStream_t s);
 
 int GradientBlocks(int64_t n);
-// absmax[0..1] (and root = (sum g, sum h, n) if root_parts) from per-workgroup partials
-void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, uint32_t* absmax,
-                 double* root, hipStream_t s);
+// absmax = (max |g|, max h, rows_cap, 0) (and root = (sum g, sum h, n) if root_parts) from
+// per-workgroup partials
+void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, int rows_cap,
+                 uint32_t* absmax, double* root, hipStream_t s);
 
 }  // namespace dev
 }  // namespace lgbm_amd

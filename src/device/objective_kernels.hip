@@ -160,8 +160,10 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
       double g, h;
       if (!RowGrad(ga, i, n, yv[k], sv[k], wv[k], g, h)) continue;
       const float gf = static_cast<float>(g), hf = static_cast<float>(h);
-      ga.grad[i] = gf;
-      ga.hess[i] = hf;
+      if (ga.write_split) {
+        ga.grad[i] = gf;
+        ga.hess[i] = hf;
+      }
       if (ga.gh != nullptr) {
         reinterpret_cast<float2*>(ga.gh)[i * ga.gh_stride] = make_float2(gf, hf);
         mg = fmaxf(mg, fabsf(gf));
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
 
 // per-workgroup maxima (and root sums) of the gradient / packing kernels, fixed order
 __global__ void k_reduce_parts(const float* max_parts, const double* root_parts, int nparts, int64_t n,
-                               uint32_t* absmax, double* root) {
+                               int rows_cap, uint32_t* absmax, double* root) {
   __shared__ double sg[256], sh[256];
   __shared__ float mg[256], mh[256];
   double a = 0.0, b = 0.0;
@@ -235,6 +237,8 @@ __global__ void k_reduce_parts(const float* max_parts, const double* root_parts,
   if (threadIdx.x == 0) {
     absmax[0] = __float_as_uint(mg[0]);  // non-negative floats order like their bit patterns
     absmax[1] = __float_as_uint(mh[0]);
+    absmax[2] = static_cast<uint32_t>(rows_cap);  // (the row cap, max over ranks after the all-reduce)
+    absmax[3] = 0u;
     if (root != nullptr) {
       root[0] = sg[0];
       root[1] = sh[0];
@@ -245,13 +249,29 @@ __global__ void k_reduce_parts(const float* max_parts, const double* root_parts,
 
 int GradientBlocks(int64_t n) { return GridFor(n); }
 
-void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, uint32_t* absmax,
-                 double* root, hipStream_t s) {
-  hipLaunchKernelGGL(k_reduce_parts, dim3(1), dim3(256), 0, s, max_parts, root_parts, nparts, n, absmax, root);
+void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, int rows_cap,
+                 uint32_t* absmax, double* root, hipStream_t s) {
+  hipLaunchKernelGGL(k_reduce_parts, dim3(1), dim3(256), 0, s, max_parts, root_parts, nparts, n, rows_cap, absmax,
+                     root);
 }
 
 void Gradients(const GradArgs& g, hipStream_t s) {
   hipLaunchKernelGGL(k_gradients, dim3(GradientBlocks(g.num_data)), dim3(256), 0, s, g);
+}
+
+__global__ __launch_bounds__(256) void k_unpack_gh(const float2* __restrict__ gh, int64_t stride, int64_t n,
+                                                   float* __restrict__ grad, float* __restrict__ hess) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const float2 v = gh[i * stride];
+    grad[i] = v.x;
+    hess[i] = v.y;
+  }
+}
+
+void UnpackGH(const GH* gh, int64_t gh_stride, int64_t n, float* grad, float* hess, hipStream_t s) {
+  hipLaunchKernelGGL(k_unpack_gh, dim3(GridFor(n)), dim3(256), 0, s, reinterpret_cast<const float2*>(gh), gh_stride, n,
+                     grad, hess);
 }
 
 }  // namespace dev

@@ -6,6 +6,7 @@
 #include <omp.h>
 
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -88,13 +89,19 @@ void GPUTreeLearner::FreeBuffers() {
   d_sample_codes_ = nullptr;
   d_sample_cnt_ = d_sample_off_ = d_bag_count_ = nullptr;
   sample_seeded_ = false;
-  d_tree_i32_ = nullptr;
-  d_tree_u32_ = nullptr;
-  d_tree_i8_ = nullptr;
-  d_tree_f64_ = nullptr;
+  d_tree_blob_ = nullptr;
+  tree_blob_cap_ = 0;
   d_tree_bm_ = nullptr;
   d_tree_bm_meta_ = nullptr;
-  tree_cap_ = cat_cap_ = 0;
+  tree_bm_cap_ = 0;
+  for (StageSlot& sl : stage_slots_) {
+    if (sl.done != nullptr) {
+      (void)hipEventSynchronize(sl.done);
+      (void)hipEventDestroy(sl.done);
+    }
+    if (sl.host != nullptr) (void)hipHostFree(sl.host);
+    sl = StageSlot();
+  }
 }
 
 void GPUTreeLearner::FreeAll() {
@@ -873,11 +880,12 @@ void GPUTreeLearner::SetBaggingData(const Dataset* subset, const data_size_t* us
 }
 
 // ---------------------------------------------------------------- tree growth
-void GPUTreeLearner::ResetAbsMax() {
-  h_absmax_[0] = h_absmax_[1] = 0u;
-  h_absmax_[2] = static_cast<uint32_t>(rows_cap_);
-  h_absmax_[3] = 0u;
-  HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 4, hipMemcpyHostToDevice, stream_));
+// the fused gradient kernel writes only the interleaved (g, h): grad / hess are unpacked
+// when something reads them (GOSS, a download, a host-assisted tree, a repack)
+void GPUTreeLearner::MaterializeSplitGradients() {
+  if (!split_stale_) return;
+  dev::UnpackGH(d_gh_, args_.gh_stride, num_data_, d_grad_, d_hess_, stream_);
+  split_stale_ = false;
 }
 
 Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
@@ -888,19 +896,22 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   // exactly these buffers (one model per iteration, not modified on the host since)
   root_from_parts_ = gh_fresh_ && gradients == d_grad_ && hessians == d_hess_;
   gh_fresh_ = false;
-  ResetAbsMax();
+  // (the reduction writes the whole absmax record: no reset copy)
   if (root_from_parts_) {
-    dev::ReduceParts(d_max_parts_, d_root_parts_, dev::GradientBlocks(num_data_), num_data_, d_absmax_, d_root_,
-                     stream_);
+    dev::ReduceParts(d_max_parts_, d_root_parts_, dev::GradientBlocks(num_data_), num_data_, rows_cap_, d_absmax_,
+                     d_root_, stream_);
   } else {
+    MaterializeSplitGradients();
     dev::PackGH(gradients, hessians, d_gh_, args_.gh_stride, num_data_, d_max_parts_, stream_);
-    dev::ReduceParts(d_max_parts_, nullptr, dev::PackBlocks(num_data_), num_data_, d_absmax_, nullptr, stream_);
+    dev::ReduceParts(d_max_parts_, nullptr, dev::PackBlocks(num_data_), num_data_, rows_cap_, d_absmax_, nullptr,
+                     stream_);
   }
   AllreduceAbsMax();
   dev::ComputeScales(d_absmax_, rows_cap_, hist_units_, d_scales_, stream_);
   host_partition_fresh_ = false;
   DecideMode();
   if (device_mode_) return TrainDeviceMode();
+  MaterializeSplitGradients();
   last_stats_ = TreeStats();
   Tree* t = SerialTreeLearner::Train(gradients, hessians);
   last_stats_.splits = t->num_leaves() - 1;
@@ -1374,41 +1385,48 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
 }
 
 // a leaf's raw histogram: its slot, or -- round growth, for a node whose pending expansion
-// reused its slot for the subtracted child -- the sum over its children, recursively (self
-// checks only)
+// reused its slot for the subtracted child -- per feature the sum over its children where the
+// node evaluated the feature (its children materialised it), recursively; elsewhere the
+// node's slot, which its subtracted descendants inherit without touching that feature's bins
+// (self checks only)
 void GPUTreeLearner::ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const {
   (void)leaf;
   const size_t nh = 2 * static_cast<size_t>(total_bins_);
   raw->assign(nh, 0);
-  std::vector<long long> part(nh);
-  std::vector<int> stack;
-  stack.push_back(d_rnode_ != nullptr ? lf.frow : -1);
-  while (!stack.empty()) {
-    const int n = stack.back();
-    stack.pop_back();
-    int slot = lf.slot;
-    if (n >= 0) {
-      dev::RNode r{};
-      HIPCHECK(hipMemcpy(&r, d_rnode_ + n, sizeof(r), hipMemcpyDeviceToHost));
-      slot = r.st.slot;
-      if (r.expanded) {
-        // (children of an expansion that cannot be split are not histogrammed)
-        dev::RNode c{};
-        HIPCHECK(hipMemcpy(&c, d_rnode_ + r.child, sizeof(c), hipMemcpyDeviceToHost));
-        const int md = config_->min_data_in_leaf;
-        const int lc = r.total_left, rc = r.count - r.total_left;
-        const bool skip = (config_->max_depth > 0 && c.st.depth >= config_->max_depth) || (lc < 2 * md && rc < 2 * md);
-        if (!skip) {
-          stack.push_back(r.child);
-          stack.push_back(r.child + 1);
-          continue;
-        }
-      }
-    }
-    HIPCHECK(hipMemcpy(part.data(), d_hist_ + static_cast<size_t>(slot) * nh, sizeof(long long) * nh,
+  auto read_slot = [&](int slot, std::vector<long long>* out) {
+    out->resize(nh);
+    HIPCHECK(hipMemcpy(out->data(), d_hist_ + static_cast<size_t>(slot) * nh, sizeof(long long) * nh,
                        hipMemcpyDeviceToHost));
-    for (size_t i = 0; i < nh; ++i) (*raw)[i] += part[i];
+  };
+  if (d_rnode_ == nullptr || last_stats_.rounds == 0 || lf.frow < 0) {  // (one split per step: Leaf::frow is no node)
+    read_slot(lf.slot, raw);
+    return;
   }
+  std::function<void(int, std::vector<long long>*)> node_hist = [&](int n, std::vector<long long>* out) {
+    dev::RNode r{};
+    HIPCHECK(hipMemcpy(&r, d_rnode_ + n, sizeof(r), hipMemcpyDeviceToHost));
+    read_slot(r.st.slot, out);
+    if (!r.expanded) return;
+    dev::RNode c{};
+    HIPCHECK(hipMemcpy(&c, d_rnode_ + r.child, sizeof(c), hipMemcpyDeviceToHost));
+    const int md = config_->min_data_in_leaf;
+    const int lc = r.total_left, rc = r.count - r.total_left;
+    // (children of an expansion that cannot be split are not histogrammed)
+    if ((config_->max_depth > 0 && c.st.depth >= config_->max_depth) || (lc < 2 * md && rc < 2 * md)) return;
+    std::vector<int8_t> flags(num_features_);
+    HIPCHECK(hipMemcpy(flags.data(), d_splittable_ + static_cast<size_t>(n) * num_features_, num_features_,
+                       hipMemcpyDeviceToHost));
+    std::vector<long long> h0, h1;
+    node_hist(r.child, &h0);
+    node_hist(r.child + 1, &h1);
+    for (int f = 0; f < num_features_; ++f) {
+      if (!flags[f]) continue;
+      const size_t off = 2 * static_cast<size_t>(data_->FeatureHistOffset(f));
+      const size_t len = 2 * static_cast<size_t>(data_->FeatureHistSize(f));
+      for (size_t i = off; i < off + len; ++i) (*out)[i] = h0[i] + h1[i];
+    }
+  };
+  node_hist(lf.frow, raw);
 }
 
 // voting: proposals -> allgather -> election + elected local histograms -> all-reduce
@@ -2091,7 +2109,6 @@ void GPUTreeLearner::ValidAddTree(int slot, const Tree* tree, int k) {
   a.bins = vs.bins;
   a.row_words = a.words_per_row;  // (validation rows carry no (g, h))
   dev::AddTreeScore(a, t, nullptr, vs.num_data, score, stream_);
-  HIPCHECK(hipStreamSynchronize(stream_));  // staging buffers are reused by the next tree
 }
 
 bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) {
@@ -2265,46 +2282,59 @@ dev::DevTree GPUTreeLearner::StageTree(const Tree* tree) {
   const int ni = nl - 1;
   const auto& cb = tree->cat_boundaries_inner();
   const auto& ct = tree->cat_threshold_inner();
-  const size_t need_i32 = 3 * static_cast<size_t>(ni) + cb.size() + 1;
-  const size_t need_u32 = static_cast<size_t>(ni) + ct.size() + 1;
-  if (tree_cap_ < need_i32 || cat_cap_ < need_u32) {
-    tree_cap_ = std::max(need_i32, 3 * static_cast<size_t>(config_->num_leaves) + 64);
-    cat_cap_ = std::max(need_u32, static_cast<size_t>(config_->num_leaves) + 1024);
-    d_tree_i32_ = Alloc<int32_t>(tree_cap_);
-    d_tree_u32_ = Alloc<uint32_t>(cat_cap_);
-    d_tree_i8_ = Alloc<int8_t>(std::max(cat_cap_, tree_cap_));
-    d_tree_f64_ = Alloc<double>(std::max(cat_cap_, tree_cap_));
-    d_tree_bm_ = Alloc<unsigned long long>(4 * static_cast<size_t>(std::max(ni, config_->num_leaves)));
-    d_tree_bm_meta_ = Alloc<int32_t>(3 * static_cast<size_t>(std::max(ni, config_->num_leaves)));
+  // blob: [i32: split feature, left, right, category boundaries][u32: thresholds, category
+  // words][f64: leaf values][i8: decision types], 8-byte aligned sections
+  auto up8 = [](size_t x) { return (x + 7) & ~static_cast<size_t>(7); };
+  const size_t n_i32 = 3 * static_cast<size_t>(ni) + cb.size() + 1;
+  const size_t n_u32 = static_cast<size_t>(ni) + ct.size() + 1;
+  const size_t o_u32 = up8(4 * n_i32), o_f64 = o_u32 + up8(4 * n_u32), o_i8 = o_f64 + 8 * static_cast<size_t>(nl);
+  const size_t bytes = up8(o_i8 + std::max(1, ni));
+  if (tree_blob_cap_ < bytes) {
+    tree_blob_cap_ = std::max(bytes, 64 * static_cast<size_t>(config_->num_leaves) + 4096);
+    d_tree_blob_ = Alloc<char>(tree_blob_cap_);
   }
-  stage_i32_.assign(need_i32, 0);
-  stage_u32_.assign(need_u32, 0);
-  stage_i8_.assign(std::max(1, ni), 0);
-  stage_f64_.assign(nl, 0.0);
+  const int nbm = std::max(ni, config_->num_leaves);
+  if (tree_bm_cap_ < nbm) {
+    tree_bm_cap_ = nbm;
+    d_tree_bm_ = Alloc<unsigned long long>(4 * static_cast<size_t>(nbm));
+    d_tree_bm_meta_ = Alloc<int32_t>(3 * static_cast<size_t>(nbm));
+  }
+  StageSlot& sl = stage_slots_[stage_next_];
+  stage_next_ = (stage_next_ + 1) % kStageSlots;
+  if (sl.done != nullptr) HIPCHECK(hipEventSynchronize(sl.done));  // (its previous copy: long done)
+  if (sl.cap < bytes) {
+    if (sl.host != nullptr) HIPCHECK(hipHostFree(sl.host));
+    sl.cap = std::max(bytes, tree_blob_cap_);
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.host), sl.cap, hipHostMallocDefault));
+  }
+  if (sl.done == nullptr) HIPCHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+  int32_t* hi = reinterpret_cast<int32_t*>(sl.host);
+  uint32_t* hu = reinterpret_cast<uint32_t*>(sl.host + o_u32);
+  double* hf = reinterpret_cast<double*>(sl.host + o_f64);
+  int8_t* hb = reinterpret_cast<int8_t*>(sl.host + o_i8);
   for (int j = 0; j < ni; ++j) {
-    stage_i32_[j] = tree->split_feature_inner(j);
-    stage_i32_[ni + j] = tree->left_child(j);
-    stage_i32_[2 * ni + j] = tree->right_child(j);
-    stage_u32_[j] = tree->threshold_in_bin(j);
-    stage_i8_[j] = tree->decision_type(j);
+    hi[j] = tree->split_feature_inner(j);
+    hi[ni + j] = tree->left_child(j);
+    hi[2 * ni + j] = tree->right_child(j);
+    hu[j] = tree->threshold_in_bin(j);
+    hb[j] = tree->decision_type(j);
   }
-  for (size_t j = 0; j < cb.size(); ++j) stage_i32_[3 * ni + j] = cb[j];
-  for (size_t j = 0; j < ct.size(); ++j) stage_u32_[ni + j] = ct[j];
-  for (int j = 0; j < nl; ++j) stage_f64_[j] = tree->LeafOutput(j);
-  HIPCHECK(hipMemcpyAsync(d_tree_i32_, stage_i32_.data(), sizeof(int32_t) * need_i32, hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_tree_u32_, stage_u32_.data(), sizeof(uint32_t) * need_u32, hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_tree_i8_, stage_i8_.data(), std::max(1, ni), hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_tree_f64_, stage_f64_.data(), sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
+  for (size_t j = 0; j < cb.size(); ++j) hi[3 * ni + j] = cb[j];
+  for (size_t j = 0; j < ct.size(); ++j) hu[ni + j] = ct[j];
+  for (int j = 0; j < nl; ++j) hf[j] = tree->LeafOutput(j);
+  HIPCHECK(hipMemcpyAsync(d_tree_blob_, sl.host, bytes, hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipEventRecord(sl.done, stream_));
+  const int32_t* di = reinterpret_cast<const int32_t*>(d_tree_blob_);
   dev::DevTree t;
   t.num_leaves = nl;
-  t.split_feature_inner = d_tree_i32_;
-  t.left_child = d_tree_i32_ + ni;
-  t.right_child = d_tree_i32_ + 2 * ni;
-  t.cat_boundaries_inner = d_tree_i32_ + 3 * ni;
-  t.threshold_in_bin = d_tree_u32_;
-  t.cat_threshold_inner = d_tree_u32_ + ni;
-  t.decision_type = d_tree_i8_;
-  t.leaf_value = d_tree_f64_;
+  t.split_feature_inner = di;
+  t.left_child = di + ni;
+  t.right_child = di + 2 * ni;
+  t.cat_boundaries_inner = di + 3 * ni;
+  t.threshold_in_bin = reinterpret_cast<const uint32_t*>(d_tree_blob_ + o_u32);
+  t.cat_threshold_inner = t.threshold_in_bin + ni;
+  t.decision_type = reinterpret_cast<const int8_t*>(d_tree_blob_ + o_i8);
+  t.leaf_value = reinterpret_cast<const double*>(d_tree_blob_ + o_f64);
   t.bm_work = d_tree_bm_;
   t.bm_meta = d_tree_bm_meta_;
   return t;
@@ -2325,8 +2355,6 @@ void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
   } else {
     dev::AddTreeScore(args_, t, nullptr, num_data_, score, stream_);
   }
-  // the staging vectors must outlive the async copies
-  HIPCHECK(hipStreamSynchronize(stream_));
 }
 
 bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
@@ -2375,6 +2403,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     ra.rng = d_rank_rng_;
     dev::RankGradients(ra, stream_);
     gh_fresh_ = false;
+    split_stale_ = false;
     return true;
   }
   dev::GradArgs g;
@@ -2392,6 +2421,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   g.score = d_score_;
   g.grad = d_grad_;
   g.hess = d_hess_;
+  g.write_split = 1;
   g.gh = nullptr;
   g.gh_stride = args_.gh_stride;
   g.max_parts = nullptr;
@@ -2401,9 +2431,11 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     g.gh = d_gh_;
     g.max_parts = d_max_parts_;
     g.root_parts = d_root_parts_;
+    g.write_split = 0;
   }
   dev::Gradients(g, stream_);
   gh_fresh_ = fuse;
+  split_stale_ = fuse;
   return true;
 }
 
@@ -2451,6 +2483,7 @@ data_size_t GPUTreeLearner::DeviceSample(const DeviceSampleSpec& sp) {
     HIPCHECK(hipMemcpy(d_label_, sp.label, sizeof(float) * num_data_, hipMemcpyHostToDevice));
     uploaded_label_src_ = sp.label;
   }
+  if (sp.goss) MaterializeSplitGradients();  // (GOSS reads and rescales grad / hess)
   dev::SampleArgs s;
   s.num_data = num_data_;
   s.num_blocks = nb;
@@ -2495,12 +2528,14 @@ data_size_t GPUTreeLearner::DeviceSample(const DeviceSampleSpec& sp) {
 
 void GPUTreeLearner::UploadGradients(const score_t* g, const score_t* h, int64_t n) {
   gh_fresh_ = false;
+  split_stale_ = false;
   HIPCHECK(hipMemcpyAsync(d_grad_, g, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipMemcpyAsync(d_hess_, h, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
 }
 
 void GPUTreeLearner::DownloadGradients(score_t* g, score_t* h, int64_t n) {
+  MaterializeSplitGradients();
   HIPCHECK(hipMemcpyAsync(g, d_grad_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipMemcpyAsync(h, d_hess_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));

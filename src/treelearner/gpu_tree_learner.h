@@ -109,7 +109,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void EnqueueTree(const dev::KArgs& a);
   void DestroyGraph();
   void KernelFloorProbe(const dev::KArgs& a);
-  void ResetAbsMax();
+  void MaterializeSplitGradients();
   void ReportKernelTrace(int num_splits);
   void BuildRangeHistogram(int leaf, int slot);
   void DownloadPartitionToHost() const;
@@ -273,6 +273,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int graph_xt_ = -1;
   bool graph_capture_failed_ = false;  // RCCL collectives could not be captured: eager trees
   bool gh_fresh_ = false;         // d_gh_ / absmax / root partials written by the gradient kernel
+  bool split_stale_ = false;      // d_grad_ / d_hess_ behind d_gh_ (MaterializeSplitGradients)
   bool root_from_parts_ = false;  // this tree's gradients came packed from the gradient kernel
   double* d_root_parts_ = nullptr;
   float* d_max_parts_ = nullptr;
@@ -326,19 +327,22 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   };
   std::vector<ValidSet> valid_;
   std::vector<void*> valid_allocs_;
-  std::vector<int32_t> stage_i32_;
-  std::vector<uint32_t> stage_u32_;
-  std::vector<int8_t> stage_i8_;
-  std::vector<double> stage_f64_;
-  // tree upload staging for traversal
-  int32_t* d_tree_i32_ = nullptr;
-  uint32_t* d_tree_u32_ = nullptr;
-  int8_t* d_tree_i8_ = nullptr;
-  double* d_tree_f64_ = nullptr;
+  // tree upload for the score traversal: one blob (node arrays, category sets, leaf values)
+  // per tree, one H2D copy from a ring of pinned staging slots (each reused once its event --
+  // recorded after its copy -- has completed: no stream synchronisation per tree)
+  struct StageSlot {
+    char* host = nullptr;
+    size_t cap = 0;
+    hipEvent_t done = nullptr;
+  };
+  static constexpr int kStageSlots = 4;
+  StageSlot stage_slots_[kStageSlots];
+  int stage_next_ = 0;
+  char* d_tree_blob_ = nullptr;
+  size_t tree_blob_cap_ = 0;
   unsigned long long* d_tree_bm_ = nullptr;  // per-node decision bitmaps (score traversal)
   int32_t* d_tree_bm_meta_ = nullptr;
-  size_t tree_cap_ = 0;
-  size_t cat_cap_ = 0;
+  int tree_bm_cap_ = 0;
   // pinned host staging
   int8_t* h_mask_ = nullptr;
   dev::SplitRecord* h_rec_ = nullptr;
