@@ -1,7 +1,7 @@
 """Host-code sanitizer run: the CLI built with AddressSanitizer +
-UndefinedBehaviorSanitizer (`make sanitize`) trains the reference's example configs on the
-CPU learner; any ASan / UBSan report fails the test.  Skipped when the instrumented CLI has
-not been built."""
+UndefinedBehaviorSanitizer (`make sanitize`, built by the first test that needs it, ~1 min on
+8 cores) trains the reference's example configs on the CPU learner; any ASan / UBSan report
+fails the test."""
 import os
 import shutil
 import subprocess
@@ -13,16 +13,28 @@ ASAN_CLI = os.path.join(ROOT, "build_asan", "lightgbm")
 EXAMPLES = "/root/reference/examples"
 
 
-@pytest.mark.skipif(not os.path.isfile(ASAN_CLI), reason="make sanitize not built")
+def _build(target, path):
+    if not os.path.isfile(path):
+        subprocess.run(["make", "-j" + str(min(8, os.cpu_count() or 4)), target], cwd=ROOT, check=True,
+                       capture_output=True, timeout=1500)
+    assert os.path.isfile(path), target
+
+
+@pytest.fixture(scope="module")
+def asan_cli():
+    _build("sanitize", ASAN_CLI)
+    return ASAN_CLI
+
+
 @pytest.mark.skipif(not os.path.isdir(EXAMPLES), reason="reference examples not mounted")
 @pytest.mark.parametrize("example,extra", [("binary_classification", ["num_trees=10"]),
                                            ("regression", ["num_trees=10"]),
                                            ("lambdarank", ["num_trees=5"])])
-def test_examples_clean_under_asan_ubsan(tmp_path, example, extra):
+def test_examples_clean_under_asan_ubsan(tmp_path, asan_cli, example, extra):
     work = tmp_path / example
     shutil.copytree(os.path.join(EXAMPLES, example), work)
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
-    out = subprocess.run([ASAN_CLI, "config=train.conf", "output_model=" + str(tmp_path / "m.txt")] + extra,
+    out = subprocess.run([asan_cli, "config=train.conf", "output_model=" + str(tmp_path / "m.txt")] + extra,
                          cwd=work, env=env, capture_output=True, text=True, timeout=600)
     log = out.stdout + out.stderr
     assert out.returncode == 0, log[-4000:]
@@ -39,9 +51,7 @@ def test_threads_clean_under_tsan(tmp_path):
     booster's exclusive lock while three threads predict and one reads evaluations through the
     C API (tests/native/tsan_driver.cpp).  Found and fixed with it: the log level written by
     every C API call, and booster getters reading the model without the lock."""
-    if not os.path.isfile(TSAN_DRIVER):
-        subprocess.run(["make", "-j" + str(min(8, os.cpu_count() or 4)), "tsan"], cwd=ROOT, check=True,
-                       capture_output=True, timeout=900)
+    _build("tsan", TSAN_DRIVER)
     env = dict(os.environ, OMP_NUM_THREADS="1", TSAN_OPTIONS="exitcode=66 halt_on_error=0")
     out = subprocess.run([TSAN_DRIVER, os.path.join(EXAMPLES, "binary_classification", "binary.train"), "28"],
                          cwd=tmp_path, env=env, capture_output=True, text=True, timeout=600)
