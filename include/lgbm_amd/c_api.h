@@ -247,7 +247,8 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkReduceScatterSumF64(const double* input, c
                                                           double* output);
 LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkAllreduceSumF64(const double* input, int64_t count, double* output);
 // in-process device communicators (thread ranks sharing one GPU)
-LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, void** out);
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, int fail_rank, int fail_at_call,
+                                                         void** out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommJoinThreadHub(void* hub, int rank);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommFreeThreadHub(void* hub);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceSynchronize();

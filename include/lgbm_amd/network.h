@@ -179,6 +179,9 @@ std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks, 
 // in-process device collectives for ranks that are threads sharing one GPU (tests and
 // rehearsal of the distributed device learners without RCCL): each call rendezvouses the
 // threads, then device kernels read the peers' buffers directly.  Not graph-capturable.
-std::vector<std::shared_ptr<DeviceComm>> MakeThreadDeviceComms(int num_ranks, double timeout_s = 0);
+// fail_rank / fail_at_call inject a fault into that rank's fail_at_call-th device collective
+// (it raises before touching any peer buffer; the peers raise at their rendezvous)
+std::vector<std::shared_ptr<DeviceComm>> MakeThreadDeviceComms(int num_ranks, double timeout_s = 0, int fail_rank = -1,
+                                                               int fail_at_call = 0);
 
 }  // namespace lgbm_amd

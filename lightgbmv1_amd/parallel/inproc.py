@@ -12,7 +12,8 @@ one rank: the failing rank raises, its peers raise "peer rank failed" instead of
 
 With device_comm=True every rank thread also joins an in-process device communicator (the
 threads share one GPU; collectives are device kernels over the peers' buffers), so the
-data- / feature-parallel device learners run their device collective path without RCCL.
+data- / feature-parallel device learners run their device collective path without RCCL;
+device_fail_at_call injects a fault into rank fail_rank's device collectives instead.
 """
 import ctypes
 import threading
@@ -34,7 +35,7 @@ class RankResult:
 
 
 class ThreadRanks:
-    def __init__(self, world, timeout_s=0.0, fail_rank=-1, fail_at_call=0, device_comm=False):
+    def __init__(self, world, timeout_s=0.0, fail_rank=-1, fail_at_call=0, device_comm=False, device_fail_at_call=0):
         self.world = int(world)
         self._hub = ctypes.c_void_p()
         self._dev_hub = ctypes.c_void_p()
@@ -44,7 +45,8 @@ class ThreadRanks:
             ctypes.c_int(fail_at_call), ctypes.byref(self._hub)))
         if device_comm:
             _safe_call(lib.LGBM_AMD_DeviceCommCreateThreadHub(
-                ctypes.c_int(self.world), ctypes.c_double(timeout_s), ctypes.byref(self._dev_hub)))
+                ctypes.c_int(self.world), ctypes.c_double(timeout_s), ctypes.c_int(fail_rank),
+                ctypes.c_int(device_fail_at_call), ctypes.byref(self._dev_hub)))
 
     def run(self, fn):
         """Call fn(rank) in one thread per rank (joined to the hub); returns [RankResult]."""

@@ -1538,10 +1538,10 @@ struct DeviceRankHub {
   std::vector<std::shared_ptr<DeviceComm>> ranks;
 };
 
-int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, void** out) {
+int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, int fail_rank, int fail_at_call, void** out) {
   API_BEGIN();
   auto* h = new DeviceRankHub();
-  h->ranks = MakeThreadDeviceComms(num_ranks, timeout_s);
+  h->ranks = MakeThreadDeviceComms(num_ranks, timeout_s, fail_rank, fail_at_call);
   *out = h;
   API_END();
 }

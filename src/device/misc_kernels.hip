@@ -10,6 +10,7 @@ int g_num_cus = 256;
 }  // namespace
 
 int NumCUs() { return g_num_cus; }
+
 void SetNumCUs(int n) { g_num_cus = n > 0 ? n : 256; }
 int HistGridBlocks() { return 2 * g_num_cus; }
 

@@ -46,7 +46,8 @@ struct DeviceHub {
 
 class ThreadDeviceComm : public DeviceComm {
  public:
-  ThreadDeviceComm(std::shared_ptr<DeviceHub> hub, int rank) : hub_(std::move(hub)), rank_(rank) {}
+  ThreadDeviceComm(std::shared_ptr<DeviceHub> hub, int rank, int fail_at_call)
+      : hub_(std::move(hub)), rank_(rank), fail_at_call_(fail_at_call) {}
   ~ThreadDeviceComm() override {
     if (tmp_ != nullptr) (void)hipFree(tmp_);
   }
@@ -73,6 +74,7 @@ class ThreadDeviceComm : public DeviceComm {
     Reduce(send, recv, recv_count * rank_, recv_count, sizeof(long long), dev::kPeerSumI64, stream);
   }
   void Allgather(const void* send, void* recv, size_t bytes_per_rank, void* stream) override {
+    Enter();
     hipStream_t s = static_cast<hipStream_t>(stream);
     HIPCK(hipStreamSynchronize(s));
     Rendezvous(send);
@@ -84,6 +86,7 @@ class ThreadDeviceComm : public DeviceComm {
     Rendezvous(nullptr);  // every rank has copied: the inputs may change again
   }
   void Broadcast(void* buf, size_t bytes, int root, void* stream) override {
+    Enter();
     hipStream_t s = static_cast<hipStream_t>(stream);
     HIPCK(hipStreamSynchronize(s));
     Rendezvous(buf);
@@ -111,6 +114,7 @@ class ThreadDeviceComm : public DeviceComm {
   // all-reduces overwrite inputs the peers still read), then copied out after the second
   // rendezvous
   void Reduce(const void* in, void* out, size_t offset, size_t count, size_t elem, int op, void* stream) {
+    Enter();
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (hub_->n > dev::kMaxPeerBufs) Log::Fatal("in-process device comm supports at most %d ranks", dev::kMaxPeerBufs);
     EnsureTmp(count * elem);
@@ -122,6 +126,22 @@ class ThreadDeviceComm : public DeviceComm {
     HIPCK(hipStreamSynchronize(s));
     Rendezvous(nullptr);
     if (count > 0) HIPCK(hipMemcpyAsync(out, tmp_, count * elem, hipMemcpyDeviceToDevice, s));
+  }
+  // a collective starts: the injected fault fires before any peer buffer is touched
+  void Enter() {
+    ++calls_;
+    if (fail_at_call_ <= 0 || calls_ != fail_at_call_) return;
+    std::string why = "injected fault in rank " + std::to_string(rank_) + " at device collective call " +
+                      std::to_string(calls_);
+    {
+      std::lock_guard<std::mutex> lk(hub_->mu);
+      if (!hub_->failed) {
+        hub_->failed = true;
+        hub_->failure = why;
+      }
+      hub_->cv.notify_all();
+    }
+    Log::Fatal("device collective failed: %s", why.c_str());
   }
   void EnsureTmp(size_t bytes) {
     if (bytes <= tmp_bytes_) return;
@@ -160,16 +180,21 @@ class ThreadDeviceComm : public DeviceComm {
 
   std::shared_ptr<DeviceHub> hub_;
   int rank_;
+  int fail_at_call_;
+  long long calls_ = 0;
   void* tmp_ = nullptr;
   size_t tmp_bytes_ = 0;
 };
 
 }  // namespace
 
-std::vector<std::shared_ptr<DeviceComm>> MakeThreadDeviceComms(int num_ranks, double timeout_s) {
+std::vector<std::shared_ptr<DeviceComm>> MakeThreadDeviceComms(int num_ranks, double timeout_s, int fail_rank,
+                                                               int fail_at_call) {
   auto hub = std::make_shared<DeviceHub>(num_ranks, timeout_s);
   std::vector<std::shared_ptr<DeviceComm>> out;
-  for (int r = 0; r < num_ranks; ++r) out.push_back(std::make_shared<ThreadDeviceComm>(hub, r));
+  for (int r = 0; r < num_ranks; ++r) {
+    out.push_back(std::make_shared<ThreadDeviceComm>(hub, r, r == fail_rank ? fail_at_call : 0));
+  }
   return out;
 }
 

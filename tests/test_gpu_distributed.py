@@ -169,3 +169,28 @@ def test_distributed_round_growth_equals_one_split_per_step(learner, world, gpu_
     rows = [json.loads(line) for f in glob.glob(str(log) + "*") for line in open(f)]
     assert rows and all(row["rounds"][0] > 0 for row in rows)
     assert sum(row["rounds"][0] for row in rows) < sum(row["leaves"][0] - 1 for row in rows)
+
+
+def test_device_collective_fault_mid_tree_raises_on_every_rank(gpu_available):
+    """A rank fails inside a device collective in the middle of a data-parallel tree (fault
+    injected into its 30th device collective, within the second tree's rounds): the failing
+    rank raises, its peer raises at its next rendezvous instead of waiting, well within the
+    timeout -- and the GPU stays usable (a serial model trains afterwards)."""
+    import time
+    X, y = make_data(N, 10)
+    full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
+    world = 2
+
+    def rank_fn(r):
+        params = dict(BASE, tree_learner="data", num_machines=world, pre_partition=True)
+        return lgb.train(params, full.subset(np.arange(r, N, world)), 8).model_to_string()
+
+    t0 = time.time()
+    with ThreadRanks(world, timeout_s=60, fail_rank=1, device_comm=True, device_fail_at_call=30) as tr:
+        res = tr.run(rank_fn)
+    assert time.time() - t0 < 45
+    assert not res[1].ok and "injected fault in rank 1 at device collective call 30" in str(res[1].error)
+    assert not res[0].ok and "injected fault" in str(res[0].error), str(res[0].error)
+    # the device is left usable
+    bst = lgb.train(BASE, full.subset(np.arange(N)), 2)
+    assert bst.num_trees() == 2
