@@ -1088,7 +1088,7 @@ __device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, const 
   int n = 0;
   if (!done) {
     const int need = L - 1 - s;
-    int kmax = min(a.round_k, need);
+    int kmax = min(a.round_k, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
     kmax = min(kmax, a.round_emax - used - (need - 1));
     kmax = max(kmax, min(1, a.round_emax - used));
     if (kmax <= 0) done = 1;
@@ -1310,7 +1310,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       // budget: after this round, one expansion per split the tree may still need stays
       // available (each round then accepts at least its first pick, the blocker)
       const int need = L - 1 - s, used = (nn - 1) / 2;
-      int kmax = min(a.round_k, need);
+      int kmax = min(a.round_k, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
       kmax = min(kmax, a.round_emax - used - (need - 1));
       kmax = max(kmax, min(1, a.round_emax - used));
       if (kmax <= 0) done = 1;  // (unreachable: the budget keeps room for the blocker)

@@ -599,6 +599,8 @@ void GPUTreeLearner::UploadData() {
   if (const char* e = std::getenv("LGBM_AMD_ROUND_FUSED")) a.round_fused = e[0] == '1' ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) a.round_grid = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GR")) a.round_gr = std::atoi(e);
+  a.round_need_div = 0;
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_NEED_DIV")) a.round_need_div = std::max(0, std::atoi(e));
   AllocRoundState();
   UploadInteractionMasks();
   AllocSplittable();
