@@ -318,6 +318,13 @@ struct GradArgs {
   double* root_parts;        //   (sum g, sum h), [GradientBlocks][2] each
 };
 void Gradients(const GradArgs& g, hipStream_t s);
+// the bitmap score walk (TreeBitmapsApply, every row) that also writes the next iteration's
+// (g, h) into ga.gh and the ga.max_parts / ga.root_parts partials of AddTreeScoreGradParts
+// workgroups (point-wise objectives, one model per iteration)
+void AddTreeScoreGrad(const KArgs& a, const DevTree& t, int64_t num_rows, double* score, const GradArgs& ga,
+                      hipStream_t s);
+int AddTreeScoreGradParts(int64_t num_rows);
+bool AddTreeScoreGradKind(int kind);  // objectives AddTreeScoreGrad supports
 // grad / hess from the interleaved (g, h) (rows gh_stride apart)
 void UnpackGH(const GH* gh, int64_t gh_stride, int64_t n, float* grad, float* hess, hipStream_t s);
 // listwise ranking gradients (LambdaRank-NDCG / XE-NDCG), one workgroup per query

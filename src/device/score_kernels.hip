@@ -7,8 +7,9 @@
 // scores are streamed in order (coalesced), which beats scattering leaf values through
 // the partition order.
 #include <cstdlib>
+#include <type_traits>
 
-#include "device_common.h"
+#include "objective_common.h"
 
 namespace lgbm_amd {
 namespace dev {
@@ -222,9 +223,166 @@ __global__ __launch_bounds__(kBmRowsPerBlock) void k_add_tree_score_bm(KArgs a, 
   }
 }
 
+// The bitmap walk that also computes the next iteration's gradients from the updated score
+// (point-wise objectives, one model per iteration): the next gradient kernel would re-read
+// every row's score and label right after this pass wrote them.  Writes the interleaved
+// (g, h) and the per-workgroup max |g| / max h and (sum g, sum h) partials of k_gradients
+// (reduced in a fixed order by k_reduce_parts); grad / hess are not written.
+#ifndef LGBM_BMG_WAVES
+#define LGBM_BMG_WAVES 5
+#endif
+// KIND: the objective (GradArgs::kind), a compile-time constant so that only its math is
+// inlined (every kind inlined takes 171 VGPRs: 2 waves per SIMD against the walk's 7)
+// W: row words prefetched per thread and chunk (>= row_words; 8 or 16)
+template <int KIND, int W>
+__global__ __launch_bounds__(kBmRowsPerBlock) __attribute__((amdgpu_waves_per_eu(LGBM_BMG_WAVES))) void k_add_tree_score_bm_grad(KArgs a, DevTree t, int64_t n,
+                                                                             double* __restrict__ score, GradArgs ga) {
+  ga.kind = KIND;
+  __shared__ unsigned long long s_bm[kMaxNodes * 4];
+  __shared__ int16_t s_group[kMaxNodes], s_left[kMaxNodes], s_right[kMaxNodes];
+  __shared__ double s_val[kMaxNodes + 1];
+  __shared__ float smg[kBmRowsPerBlock / kWave], smh[kBmRowsPerBlock / kWave];
+  __shared__ double ssg[kBmRowsPerBlock / kWave], ssh[kBmRowsPerBlock / kWave];
+  extern __shared__ uint32_t s_rows[];  // [kBmRowsPerBlock][row_words]
+  const int ni = t.num_leaves - 1;
+  for (int i = threadIdx.x; i < ni * 4; i += blockDim.x) s_bm[i] = t.bm_work[i];
+  for (int i = threadIdx.x; i < ni; i += blockDim.x) {
+    s_group[i] = static_cast<int16_t>(t.bm_meta[i * 3 + 0]);
+    s_left[i] = static_cast<int16_t>(t.bm_meta[i * 3 + 1]);
+    s_right[i] = static_cast<int16_t>(t.bm_meta[i * 3 + 2]);
+  }
+  for (int i = threadIdx.x; i < t.num_leaves; i += blockDim.x) s_val[i] = t.leaf_value[i];
+  const int wpr = a.row_words;
+  const uint32_t* bins32 = static_cast<const uint32_t*>(a.bins);
+  const uint8_t* rows8 = reinterpret_cast<const uint8_t*>(s_rows);
+  constexpr int kW = W;
+  const int64_t step = static_cast<int64_t>(gridDim.x) * kBmRowsPerBlock;
+  uint32_t pre[kW];
+  double sc = 0.0, yv = 0.0, wv = 1.0;
+  auto load = [&](int64_t r0) {
+    const int nr = static_cast<int>(min<int64_t>(kBmRowsPerBlock, n - r0));
+    const uint32_t* src = bins32 + r0 * wpr;
+#pragma unroll
+    for (int k = 0; k < kW; ++k) {
+      const int i = threadIdx.x + k * kBmRowsPerBlock;
+      pre[k] = (k < wpr && i < nr * wpr) ? src[i] : 0u;
+    }
+    const bool ok = threadIdx.x < nr;
+    sc = ok ? score[r0 + threadIdx.x] : 0.0;
+    yv = ok ? static_cast<double>(ga.label[r0 + threadIdx.x]) : 0.0;
+    wv = ok && ga.weights != nullptr ? static_cast<double>(ga.weights[r0 + threadIdx.x]) : 1.0;
+  };
+  float mg = 0.f, mh = 0.f;
+  double sg = 0.0, shh = 0.0;
+  int64_t r0 = static_cast<int64_t>(blockIdx.x) * kBmRowsPerBlock;
+  if (r0 < n) load(r0);
+  for (; r0 < n; r0 += step) {
+    const int nr = static_cast<int>(min<int64_t>(kBmRowsPerBlock, n - r0));
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kW; ++k) {
+      const int i = threadIdx.x + k * kBmRowsPerBlock;
+      if (k < wpr && i < nr * wpr) s_rows[i] = pre[k];
+    }
+    const double my = sc, y = yv, w = wv;
+    __syncthreads();
+    if (r0 + step < n) load(r0 + step);
+    if (threadIdx.x < nr) {
+      const uint8_t* row = rows8 + threadIdx.x * wpr * 4;
+      int node = 0;
+      while (node >= 0) {
+        const uint32_t gb = row[s_group[node]];
+        const bool left = (s_bm[node * 4 + (gb >> 6)] >> (gb & 63u)) & 1ull;
+        node = left ? s_left[node] : s_right[node];
+      }
+      const int64_t i = r0 + threadIdx.x;
+      const double s1 = my + s_val[~node];
+      score[i] = s1;
+      double g, h;
+      RowGrad(ga, i, n, y, s1, w, g, h);
+      const float gf = static_cast<float>(g), hf = static_cast<float>(h);
+      reinterpret_cast<float2*>(ga.gh)[i * ga.gh_stride] = make_float2(gf, hf);
+      mg = fmaxf(mg, fabsf(gf));
+      mh = fmaxf(mh, fabsf(hf));
+      sg += gf;
+      shh += hf;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
+    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+    sg += __shfl_xor(sg, o, kWave);
+    shh += __shfl_xor(shh, o, kWave);
+  }
+  const int wv_ = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    smg[wv_] = mg;
+    smh[wv_] = mh;
+    ssg[wv_] = sg;
+    ssh[wv_] = shh;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tg = 0.0, th = 0.0;
+    for (int i = 0; i < kBmRowsPerBlock / kWave; ++i) {
+      mg = fmaxf(mg, smg[i]);
+      mh = fmaxf(mh, smh[i]);
+      tg += ssg[i];
+      th += ssh[i];
+    }
+    ga.max_parts[2 * blockIdx.x] = mg;
+    ga.max_parts[2 * blockIdx.x + 1] = mh;
+    ga.root_parts[2 * blockIdx.x] = tg;
+    ga.root_parts[2 * blockIdx.x + 1] = th;
+  }
+}
+
 bool TreeBitmapsApply(const KArgs& a, int num_leaves) {
   const int ni = num_leaves - 1;
   return a.bins != nullptr && a.bin_bytes == 1 && ni >= 1 && ni <= kMaxNodes && a.row_words * 4 <= kBmMaxRowBytes;
+}
+
+namespace {
+int BmBlocks(int64_t num_rows) {
+  // 32 workgroups per CU walk the chunks (LGBM_AMD_BM_WG_PER_CU; 0: one chunk per
+  // workgroup).  Headline A/B at 0/4/8/16/32: 4.146/4.135/4.133/4.120/4.109 ms/iter
+  static const int per_cu = [] {
+    const char* e = std::getenv("LGBM_AMD_BM_WG_PER_CU");
+    return e != nullptr ? std::atoi(e) : 32;
+  }();
+  int64_t blocks64 = (num_rows + kBmRowsPerBlock - 1) / kBmRowsPerBlock;
+  if (per_cu > 0) blocks64 = std::min<int64_t>(blocks64, static_cast<int64_t>(per_cu) * NumCUs());
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(blocks64, 1 << 30)));
+}
+}  // namespace
+
+int AddTreeScoreGradParts(int64_t num_rows) { return BmBlocks(num_rows); }
+
+// the objectives whose gradients the score walk computes: L2, L1, Huber, quantile, binary,
+// cross-entropy (the others keep the separate gradient kernel)
+bool AddTreeScoreGradKind(int kind) {
+  return kind == 1 || kind == 2 || kind == 3 || kind == 6 || kind == 10 || kind == 11;
+}
+
+void AddTreeScoreGrad(const KArgs& a, const DevTree& t, int64_t num_rows, double* score, const GradArgs& ga,
+                      hipStream_t s) {
+  const int ni = t.num_leaves - 1;
+  hipLaunchKernelGGL(k_tree_bitmaps, dim3(ni), dim3(256), 0, s, a, t);
+  const size_t lds = sizeof(uint32_t) * kBmRowsPerBlock * a.row_words;
+  const dim3 grid(BmBlocks(num_rows)), block(kBmRowsPerBlock);
+  auto go = [&](auto kind) {
+    constexpr int K = decltype(kind)::value;
+    if (a.row_words <= 8) hipLaunchKernelGGL((k_add_tree_score_bm_grad<K, 8>), grid, block, lds, s, a, t, num_rows, score, ga);
+    else hipLaunchKernelGGL((k_add_tree_score_bm_grad<K, 16>), grid, block, lds, s, a, t, num_rows, score, ga);
+  };
+  switch (ga.kind) {
+    case 1: go(std::integral_constant<int, 1>()); break;
+    case 2: go(std::integral_constant<int, 2>()); break;
+    case 3: go(std::integral_constant<int, 3>()); break;
+    case 6: go(std::integral_constant<int, 6>()); break;
+    case 10: go(std::integral_constant<int, 10>()); break;
+    default: go(std::integral_constant<int, 11>()); break;
+  }
 }
 
 void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
@@ -233,17 +391,9 @@ void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t
   const int ni = t.num_leaves - 1;
   if (rows == nullptr && TreeBitmapsApply(a, t.num_leaves) && t.bm_work != nullptr) {
     hipLaunchKernelGGL(k_tree_bitmaps, dim3(ni), dim3(256), 0, s, a, t);
-    // 32 workgroups per CU walk the chunks (LGBM_AMD_BM_WG_PER_CU; 0: one chunk per
-    // workgroup).  Headline A/B at 0/4/8/16/32: 4.146/4.135/4.133/4.120/4.109 ms/iter
-    static const int per_cu = [] {
-      const char* e = std::getenv("LGBM_AMD_BM_WG_PER_CU");
-      return e != nullptr ? std::atoi(e) : 32;
-    }();
-    int64_t blocks64 = (num_rows + kBmRowsPerBlock - 1) / kBmRowsPerBlock;
-    if (per_cu > 0) blocks64 = std::min<int64_t>(blocks64, static_cast<int64_t>(per_cu) * NumCUs());
-    const int blocks = static_cast<int>(std::min<int64_t>(blocks64, 1 << 30));
     const size_t lds = sizeof(uint32_t) * kBmRowsPerBlock * a.row_words;
-    hipLaunchKernelGGL(k_add_tree_score_bm, dim3(blocks), dim3(kBmRowsPerBlock), lds, s, a, t, num_rows, score);
+    hipLaunchKernelGGL(k_add_tree_score_bm, dim3(BmBlocks(num_rows)), dim3(kBmRowsPerBlock), lds, s, a, t, num_rows,
+                       score);
     return;
   }
   // one row per thread: many rows in flight hide the per-row load latency

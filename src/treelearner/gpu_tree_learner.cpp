@@ -394,9 +394,12 @@ void GPUTreeLearner::UploadData() {
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_ * hist_units_);
   d_root_ = Alloc<double>(4);
   d_leaf_sums_ = Alloc<double>(4);
-  d_root_parts_ = Alloc<double>(2 * static_cast<size_t>(dev::GradientBlocks(num_data_)));
-  d_max_parts_ = Alloc<float>(2 * static_cast<size_t>(std::max(dev::GradientBlocks(num_data_),
-                                                                dev::PackBlocks(num_data_))));
+  // (per-workgroup partials of the gradient kernel, the packing kernel or the score walk that
+  // computes the next gradients)
+  const int parts = std::max({dev::GradientBlocks(num_data_), dev::PackBlocks(num_data_),
+                              dev::AddTreeScoreGradParts(num_data_)});
+  d_root_parts_ = Alloc<double>(2 * static_cast<size_t>(parts));
+  d_max_parts_ = Alloc<float>(2 * static_cast<size_t>(parts));
   d_leaf_values_ = Alloc<double>(n_leaves);
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_mask_), std::max(1, num_features_), hipHostMallocDefault));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_rec_), sizeof(dev::SplitRecord) * std::max(1, n_leaves - 1),
@@ -900,8 +903,7 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   gh_fresh_ = false;
   // (the reduction writes the whole absmax record: no reset copy)
   if (root_from_parts_) {
-    dev::ReduceParts(d_max_parts_, d_root_parts_, dev::GradientBlocks(num_data_), num_data_, rows_cap_, d_absmax_,
-                     d_root_, stream_);
+    dev::ReduceParts(d_max_parts_, d_root_parts_, grad_parts_, num_data_, rows_cap_, d_absmax_, d_root_, stream_);
   } else {
     MaterializeSplitGradients();
     dev::PackGH(gradients, hessians, d_gh_, args_.gh_stride, num_data_, d_max_parts_, stream_);
@@ -2217,6 +2219,7 @@ void GPUTreeLearner::ValidScoreToHost(int slot, double* host) {
 // ---------------------------------------------------------------- scores & gradients
 void GPUTreeLearner::InitScores(int ntpi, const double* init_score) {
   HIPCHECK(hipSetDevice(device_id_));
+  grad_prefetched_ = false;
   num_tree_per_iteration_ = ntpi;
   const size_t n = static_cast<size_t>(num_data_) * ntpi;
   if (d_score_ == nullptr) {
@@ -2238,16 +2241,19 @@ void GPUTreeLearner::SyncScoreToHost(double* host, int k) {
 }
 
 void GPUTreeLearner::SyncScoreFromHost(const double* host, int k) {
+  grad_prefetched_ = false;
   HIPCHECK(hipMemcpyAsync(d_score_ + static_cast<size_t>(k) * num_data_, host, sizeof(double) * num_data_,
                           hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
 }
 
 void GPUTreeLearner::AddConstToScore(double v, int k) {
+  grad_prefetched_ = false;
   dev::AddConst(d_score_ + static_cast<size_t>(k) * num_data_, num_data_, v, stream_);
 }
 
 void GPUTreeLearner::MultiplyScore(double v, int k) {
+  grad_prefetched_ = false;
   dev::MulConst(d_score_ + static_cast<size_t>(k) * num_data_, num_data_, v, stream_);
 }
 
@@ -2262,6 +2268,17 @@ void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
     // the bitmap walk of every row (coalesced row reads and score updates) beats the
     // partition-ordered scatter of leaf values; it also covers out-of-bag rows.  Wider or
     // row-sparse storage scatters instead (the generic walk took 5 ms per tree on 100M rows)
+    if (last_grad_fusable_ && k == 0 && num_tree_per_iteration_ == 1 && dev::AddTreeScoreGradKind(last_grad_.kind) &&
+        FuseNextGradients()) {
+      // ... and computes the next iteration's gradients from the scores it writes
+      dev::DevTree t = StageTree(tree);
+      dev::AddTreeScoreGrad(args_, t, num_data_, score, last_grad_, stream_);
+      grad_parts_ = dev::AddTreeScoreGradParts(num_data_);
+      grad_prefetched_ = true;
+      gh_fresh_ = false;  // (d_gh_ now holds the next iteration's gradients)
+      split_stale_ = false;
+      return;
+    }
     AddTreeToScore(tree, k);
     return;
   }
@@ -2343,6 +2360,7 @@ dev::DevTree GPUTreeLearner::StageTree(const Tree* tree) {
 }
 
 void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
+  grad_prefetched_ = false;
   // NOTE: called from AddTrainedTreeToScore for out-of-bag rows only (oob_cnt_ > 0 and the
   // tree just trained), otherwise for every row
   double* score = d_score_ + static_cast<size_t>(k) * num_data_;
@@ -2359,6 +2377,19 @@ void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
   }
 }
 
+// LGBM_AMD_FUSE_GRAD=0: the score walk does not compute the next gradients
+bool GPUTreeLearner::FuseNextGradients() {
+  const char* e = std::getenv("LGBM_AMD_FUSE_GRAD");
+  return !(e != nullptr && e[0] == '0');
+}
+
+bool GPUTreeLearner::SameGradArgs(const dev::GradArgs& x, const dev::GradArgs& y) {
+  return x.kind == y.kind && x.num_class == y.num_class && x.num_data == y.num_data && x.p0 == y.p0 && x.p1 == y.p1 &&
+         x.p2 == y.p2 && x.lw0 == y.lw0 && x.lw1 == y.lw1 && x.label == y.label && x.weights == y.weights &&
+         x.label_weight == y.label_weight && x.score == y.score && x.gh == y.gh && x.gh_stride == y.gh_stride &&
+         x.max_parts == y.max_parts && x.root_parts == y.root_parts;
+}
+
 bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   if (spec.kind == DeviceGradKind::None || spec.kind == DeviceGradKind::MulticlassOVA) return false;
   if (spec.kind != DeviceGradKind::MulticlassSoftmax && ntpi != 1) return false;
@@ -2368,21 +2399,28 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     return false;  // queries larger than the LDS staging: host gradients
   }
   const size_t n = static_cast<size_t>(num_data_);
+  const bool prefetched = grad_prefetched_;
+  grad_prefetched_ = false;
+  bool uploaded = false;
   if (uploaded_label_src_ != spec.label) {
     if (d_label_ == nullptr) d_label_ = Alloc<float>(n);
     HIPCHECK(hipMemcpy(d_label_, spec.label, sizeof(float) * n, hipMemcpyHostToDevice));
     uploaded_label_src_ = spec.label;
+    uploaded = true;
   }
   if (spec.weights != nullptr && uploaded_weight_src_ != spec.weights) {
     if (d_weights_ == nullptr) d_weights_ = Alloc<float>(n);
     HIPCHECK(hipMemcpy(d_weights_, spec.weights, sizeof(float) * n, hipMemcpyHostToDevice));
     uploaded_weight_src_ = spec.weights;
+    uploaded = true;
   }
   if (spec.label_weight_arr != nullptr && uploaded_lw_src_ != spec.label_weight_arr) {
     if (d_label_weight_ == nullptr) d_label_weight_ = Alloc<float>(n);
     HIPCHECK(hipMemcpy(d_label_weight_, spec.label_weight_arr, sizeof(float) * n, hipMemcpyHostToDevice));
     uploaded_lw_src_ = spec.label_weight_arr;
+    uploaded = true;
   }
+  last_grad_fusable_ = false;
   if (listwise) {
     UploadRankTables(spec.rank, spec.kind);
     dev::RankArgs ra;
@@ -2406,6 +2444,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     dev::RankGradients(ra, stream_);
     gh_fresh_ = false;
     split_stale_ = false;
+    last_grad_fusable_ = false;
     return true;
   }
   dev::GradArgs g;
@@ -2434,10 +2473,23 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     g.max_parts = d_max_parts_;
     g.root_parts = d_root_parts_;
     g.write_split = 0;
+    // the last score walk already computed these gradients from the current scores
+    // (AddTrainedTreeToScore), unless anything changed the scores or inputs since
+    if (prefetched && !uploaded && SameGradArgs(g, last_grad_)) {
+      gh_fresh_ = true;
+      split_stale_ = true;
+      last_grad_fusable_ = true;
+      return true;
+    }
   }
   dev::Gradients(g, stream_);
   gh_fresh_ = fuse;
   split_stale_ = fuse;
+  grad_parts_ = dev::GradientBlocks(num_data_);
+  if (fuse) {
+    last_grad_ = g;
+    last_grad_fusable_ = true;
+  }
   return true;
 }
 
@@ -2531,6 +2583,8 @@ data_size_t GPUTreeLearner::DeviceSample(const DeviceSampleSpec& sp) {
 void GPUTreeLearner::UploadGradients(const score_t* g, const score_t* h, int64_t n) {
   gh_fresh_ = false;
   split_stale_ = false;
+  last_grad_fusable_ = false;
+  grad_prefetched_ = false;
   HIPCHECK(hipMemcpyAsync(d_grad_, g, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipMemcpyAsync(d_hess_, h, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));

@@ -110,6 +110,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void DestroyGraph();
   void KernelFloorProbe(const dev::KArgs& a);
   void MaterializeSplitGradients();
+  static bool FuseNextGradients();
+  static bool SameGradArgs(const dev::GradArgs& x, const dev::GradArgs& y);
   void ReportKernelTrace(int num_splits);
   void BuildRangeHistogram(int leaf, int slot);
   void DownloadPartitionToHost() const;
@@ -274,6 +276,13 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool graph_capture_failed_ = false;  // RCCL collectives could not be captured: eager trees
   bool gh_fresh_ = false;         // d_gh_ / absmax / root partials written by the gradient kernel
   bool split_stale_ = false;      // d_grad_ / d_hess_ behind d_gh_ (MaterializeSplitGradients)
+  // point-wise device gradients: the last gradient kernel's arguments; the score walk after a
+  // tree may compute the next iteration's gradients with them (grad_prefetched_), which the
+  // next ComputeGradients then takes instead of launching; any other score change drops them
+  dev::GradArgs last_grad_{};
+  bool last_grad_fusable_ = false;
+  bool grad_prefetched_ = false;
+  int grad_parts_ = 0;  // per-workgroup partials (max_parts / root_parts) of the last gradients
   bool root_from_parts_ = false;  // this tree's gradients came packed from the gradient kernel
   double* d_root_parts_ = nullptr;
   float* d_max_parts_ = nullptr;

@@ -641,3 +641,31 @@ def test_forced_splits_on_device(gpu_available, monkeypatch, tmp_path, forced):
     assert abs(_auc(y, dev.predict(X)) - _auc(y, host.predict(X))) < 5e-3
     root = dev.dump_model()["tree_info"][0]["tree_structure"]
     assert root["split_feature"] == forced["feature"]
+
+
+@pytest.mark.parametrize("params", [{"objective": "binary"}, {"objective": "regression"},
+                                    {"objective": "binary", "boosting": "goss", "learning_rate": 0.3},
+                                    {"objective": "binary", "bagging_fraction": 0.7, "bagging_freq": 1}])
+def test_score_walk_computes_next_gradients(gpu_available, monkeypatch, params):
+    """The tree's score walk computes the next iteration's gradients from the scores it writes
+    (LGBM_AMD_FUSE_GRAD, on by default) instead of a separate gradient pass: the same trees as
+    the separate pass (the root sums' per-workgroup grouping differs only in rounding)."""
+    X, y = _data(n=80000, seed=7)
+    if params["objective"] == "regression":
+        y = (X[:, 0] + 0.5 * X[:, 1] * X[:, 2]).astype(np.float32)
+    p = dict(params, verbose=-1, device_type="gpu", num_leaves=31, seed=2)
+    models, preds = {}, {}
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("LGBM_AMD_FUSE_GRAD", fuse)
+        bst = lgb.train(p, lgb.Dataset(X, y, params=p), 15)
+        models[fuse] = bst.dump_model()["tree_info"]
+        preds[fuse] = bst.predict(X)
+    for a, b in zip(models["0"], models["1"]):
+        assert a["num_leaves"] == b["num_leaves"]
+
+        def feats(node):
+            if "split_feature" not in node:
+                return []
+            return [node["split_feature"]] + feats(node["left_child"]) + feats(node["right_child"])
+        assert feats(a["tree_structure"]) == feats(b["tree_structure"])
+    np.testing.assert_allclose(preds["0"], preds["1"], rtol=1e-6, atol=1e-9)
