@@ -206,6 +206,14 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_RcclUniqueIdSize(int* out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclGetUniqueId(char* out_id);
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclInit(int num_ranks, int rank, int device_id, const char* unique_id);
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclFree();
+/* one process per GPU: capture-safe peer collectives over hipIpc-mapped windows (xGMI);
+   needs the host Network (LGBM_NetworkInit*) for the handle exchange */
+LIGHTGBM_C_EXPORT int LGBM_AMD_PeerCommInit(int device_id, double timeout_s);
+/* releases the device comm (peer or RCCL) after every rank's kernels are done */
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommFree();
+/* microseconds per device collective (kind 0 int64 reduce-scatter, 1 allgather, 2 int64
+   all-reduce) over `iters` back-to-back calls, graph-captured or eager; every rank calls it */
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommBench(int kind, int64_t bytes, int iters, int graph, double* out_us);
 /* runs every device collective on small buffers and checks the sums (1 = ok) */
 LIGHTGBM_C_EXPORT int LGBM_AMD_RcclSelfTest(int* out_ok);
 // the same all-reduces captured into a hipGraph and replayed (the device learner's tree graph)
@@ -249,6 +257,9 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_NetworkAllreduceSumF64(const double* input, int64
 // in-process device communicators (thread ranks sharing one GPU)
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, int fail_rank, int fail_at_call,
                                                          void** out);
+/* kind 0: host-rendezvous device comm (eager); 1: capture-safe one-shot peer comm */
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommCreateThreadHubEx(int num_ranks, double timeout_s, int fail_rank,
+                                                           int fail_at_call, int kind, void** out);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommJoinThreadHub(void* hub, int rank);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceCommFreeThreadHub(void* hub);
 LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceSynchronize();

@@ -80,6 +80,16 @@ class DeviceComm {
   virtual void Broadcast(void* buf, size_t bytes, int root, void* stream) = 0;
   // the collectives can be captured into a hipGraph (stream-ordered, no host rendezvous)
   virtual bool CaptureSafe() const { return true; }
+  // collectives enqueued while a guard is set are skipped when the device flag *d_flag is
+  // nonzero at run time (replicated state such as Round::done: every rank skips the same ones);
+  // communicators that cannot skip ignore it
+  virtual void SetSkipGuard(const int32_t* d_flag) { (void)d_flag; }
+  // ranks that share one device (thread ranks) and wait on each other inside kernels must
+  // not block in a device-wide synchronisation (hipFree, graph teardown) while a peer's
+  // kernel waits for a collective this rank has yet to launch: the learner calls this at the
+  // start of each tree and before re-capturing its graphs (the same points on every rank),
+  // and such comms rendezvous there.  One GPU per process: nothing to do.
+  virtual void HostBarrier() {}
   // failure detection (watchdog of the device learner): an asynchronous communicator error,
   // and aborting every pending collective so that no rank stays blocked
   virtual bool AsyncError(std::string* msg) {
@@ -183,5 +193,13 @@ std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks, 
 // (it raises before touching any peer buffer; the peers raise at their rendezvous)
 std::vector<std::shared_ptr<DeviceComm>> MakeThreadDeviceComms(int num_ranks, double timeout_s = 0, int fail_rank = -1,
                                                                int fail_at_call = 0);
+
+// capture-safe one-shot peer collectives (src/network/peer_comm.cpp): thread ranks sharing
+// the current device (timeout_s bounds every device-side wait; fail_rank's collective number
+// fail_at_call stops as a dead rank would, its peers time out) ...
+std::vector<std::shared_ptr<DeviceComm>> MakePeerThreadComms(int num_ranks, double timeout_s = 0, int fail_rank = -1,
+                                                             int fail_at_call = 0);
+// ... or one process per GPU: windows exchanged as hipIpc handles over the host Network
+std::shared_ptr<DeviceComm> MakePeerIpcComm(int device_id, double timeout_s = 0);
 
 }  // namespace lgbm_amd

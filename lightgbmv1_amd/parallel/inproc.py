@@ -10,10 +10,15 @@ one rank: the failing rank raises, its peers raise "peer rank failed" instead of
     ranks = ThreadRanks(world=2, timeout_s=30)
     results = ranks.run(lambda rank: train_my_shard(rank))
 
-With device_comm=True every rank thread also joins an in-process device communicator (the
-threads share one GPU; collectives are device kernels over the peers' buffers), so the
-data- / feature-parallel device learners run their device collective path without RCCL;
-device_fail_at_call injects a fault into rank fail_rank's device collectives instead.
+With device_comm every rank thread also joins an in-process device communicator (the
+threads share one GPU), so the data- / feature-parallel device learners run their device
+collective path without RCCL:
+  * device_comm=True / "peer": the capture-safe peer comm (src/network/peer_comm.cpp) --
+    one kernel per collective reading the peers' windows, captured in the round graphs like
+    the multi-process path; device_fail_at_call stops rank fail_rank at that collective
+    (counted on the device), its peers time out after timeout_s;
+  * device_comm="host": collectives rendezvous on the host (eager launches, no graphs);
+    device_fail_at_call makes rank fail_rank raise at that call.
 """
 import ctypes
 import threading
@@ -44,9 +49,10 @@ class ThreadRanks:
             ctypes.c_int(self.world), ctypes.c_double(timeout_s), ctypes.c_int(fail_rank),
             ctypes.c_int(fail_at_call), ctypes.byref(self._hub)))
         if device_comm:
-            _safe_call(lib.LGBM_AMD_DeviceCommCreateThreadHub(
+            kind = 0 if device_comm == "host" else 1
+            _safe_call(lib.LGBM_AMD_DeviceCommCreateThreadHubEx(
                 ctypes.c_int(self.world), ctypes.c_double(timeout_s), ctypes.c_int(fail_rank),
-                ctypes.c_int(device_fail_at_call), ctypes.byref(self._dev_hub)))
+                ctypes.c_int(device_fail_at_call), ctypes.c_int(kind), ctypes.byref(self._dev_hub)))
 
     def run(self, fn):
         """Call fn(rank) in one thread per rank (joined to the hub); returns [RankResult]."""

@@ -5,9 +5,16 @@ The native library needs two kinds of collectives:
     ``LGBM_NetworkInitWithFunctions`` as an allgather callback backed by a CPU (gloo)
     process group -- the analogue of the reference's socket/MPI linkers
     (reference src/network/linkers_socket.cpp, c_api.h LGBM_NetworkInitWithFunctions);
-  * device collectives (per-split histogram all-reduce, root statistics): an RCCL
-    communicator over xGMI created natively from an ncclUniqueId that rank 0 draws and
-    broadcasts through the same process group (src/network/rccl_comm.cpp).
+  * device collectives (per-round histogram reduce-scatter, split-record allgather, root
+    statistics), one of:
+      - "peer" (default): one-shot collectives that read the peers' HBM over xGMI, one kernel
+        each, captured in the learner's graphs; windows exported with hipIpc handles
+        exchanged through the process group (src/network/peer_comm.cpp).  A self test of every
+        collective (eager and graph-replayed) runs first; if it fails on any rank, every rank
+        falls back to RCCL;
+      - "rccl": an RCCL communicator created natively from an ncclUniqueId that rank 0 draws
+        and broadcasts through the same process group (src/network/rccl_comm.cpp).
+    Chosen by `device_comm` or LGBM_AMD_DEVICE_COMM.
 
 torch itself never touches the GPU here, so the HIP runtime is owned by the library.
 Rendezvous uses MASTER_ADDR / MASTER_PORT / RANK / WORLD_SIZE (torchrun); always use
@@ -23,7 +30,7 @@ from ..basic import _load_lib, _safe_call
 _ALLGATHER_T = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 
-_STATE = {"callbacks": None, "group": None, "rccl": False}
+_STATE = {"callbacks": None, "group": None, "rccl": False, "device_comm": None}
 
 
 def _make_allgather(dist, group):
@@ -54,10 +61,35 @@ def _make_allgather(dist, group):
     return _ALLGATHER_T(allgather)
 
 
-def init_network(use_rccl=True, backend="gloo", timeout_s=600):
-    """Initialise host (and optionally RCCL device) collectives for the current process group.
+def _all_ok(dist, group, ok):
+    """True when `ok` holds on every rank (a host all-reduce)."""
+    import torch
+    t = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(t.item())
 
-    Returns (rank, world_size, local_rank).
+
+def _init_peer(lib, dist, group, device, timeout_s):
+    """The peer comm on every rank, self-tested; False (and nothing left behind) otherwise."""
+    ok = lib.LGBM_AMD_PeerCommInit(ctypes.c_int(device), ctypes.c_double(timeout_s)) == 0
+    if not _all_ok(dist, group, ok):
+        if ok:
+            lib.LGBM_AMD_DeviceCommFree()
+        return False
+    a, b = ctypes.c_int(0), ctypes.c_int(0)
+    ok = (lib.LGBM_AMD_RcclSelfTest(ctypes.byref(a)) == 0 and a.value == 1 and
+          lib.LGBM_AMD_RcclGraphSelfTest(ctypes.byref(b)) == 0 and b.value == 1)
+    if not _all_ok(dist, group, ok):
+        lib.LGBM_AMD_DeviceCommFree()
+        return False
+    return True
+
+
+def init_network(use_rccl=True, backend="gloo", timeout_s=600, device_comm=None):
+    """Initialise host (and, with use_rccl, device) collectives for the current process group.
+
+    device_comm: "peer" or "rccl" (default: LGBM_AMD_DEVICE_COMM, else "peer" with RCCL as
+    the fallback).  Returns (rank, world_size, local_rank).
     """
     import datetime
 
@@ -81,7 +113,15 @@ def init_network(use_rccl=True, backend="gloo", timeout_s=600):
     if use_rccl:
         ndev = ctypes.c_int(0)
         _safe_call(lib.LGBM_AMD_DeviceCount(ctypes.byref(ndev)))
-        if ndev.value > 0:
+        kind = device_comm or os.environ.get("LGBM_AMD_DEVICE_COMM", "peer")
+        if ndev.value > 0 and kind == "peer":
+            if _init_peer(lib, dist, group, local_rank % ndev.value, min(120.0, float(timeout_s))):
+                _STATE["device_comm"] = "peer"
+            else:
+                kind = "rccl"
+                if rank == 0:
+                    print("[lightgbmv1_amd] peer device comm unavailable; using RCCL", flush=True)
+        if ndev.value > 0 and kind == "rccl":
             import torch
             size = ctypes.c_int(0)
             _safe_call(lib.LGBM_AMD_RcclUniqueIdSize(ctypes.byref(size)))
@@ -95,7 +135,13 @@ def init_network(use_rccl=True, backend="gloo", timeout_s=600):
                                              ctypes.c_int(local_rank % ndev.value),
                                              uid.ctypes.data_as(ctypes.c_char_p)))
             _STATE["rccl"] = True
+            _STATE["device_comm"] = "rccl"
     return rank, world, local_rank
+
+
+def device_comm_kind():
+    """"peer", "rccl" or None: the device communicator init_network set up."""
+    return _STATE["device_comm"]
 
 
 def barrier():
@@ -117,9 +163,10 @@ def allreduce_max(value):
 
 def shutdown():
     lib = _load_lib()
-    if _STATE["rccl"]:
-        lib.LGBM_AMD_RcclFree()
+    if _STATE["device_comm"] is not None:
+        lib.LGBM_AMD_DeviceCommFree()  # (after every rank's kernels are done with the windows)
         _STATE["rccl"] = False
+        _STATE["device_comm"] = None
     lib.LGBM_NetworkFree()
     try:
         import torch.distributed as dist

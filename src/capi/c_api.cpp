@@ -1546,6 +1546,19 @@ int LGBM_AMD_DeviceCommCreateThreadHub(int num_ranks, double timeout_s, int fail
   API_END();
 }
 
+// kind 0: host-rendezvous comm (eager launches); 1: capture-safe peer comm (one-shot kernels
+// over the ranks' windows, src/network/peer_comm.cpp).  fail_at_call counts collectives
+// (kind 1: executed on the device, so faults fire inside captured graphs too)
+int LGBM_AMD_DeviceCommCreateThreadHubEx(int num_ranks, double timeout_s, int fail_rank, int fail_at_call, int kind,
+                                         void** out) {
+  API_BEGIN();
+  auto* h = new DeviceRankHub();
+  h->ranks = kind == 1 ? MakePeerThreadComms(num_ranks, timeout_s, fail_rank, fail_at_call)
+                       : MakeThreadDeviceComms(num_ranks, timeout_s, fail_rank, fail_at_call);
+  *out = h;
+  API_END();
+}
+
 int LGBM_AMD_DeviceCommJoinThreadHub(void* hub, int rank) {
   API_BEGIN();
   auto* h = static_cast<DeviceRankHub*>(hub);

@@ -294,6 +294,38 @@ struct PeerBufs {
 enum PeerOp { kPeerSumF64 = 0, kPeerSumF32 = 1, kPeerSumI64 = 2, kPeerMaxU32 = 3 };
 void ReducePeers(const PeerBufs& src, int n, size_t offset, void* out, size_t count, int op, hipStream_t s);
 
+// One-shot peer collectives over symmetric windows (src/device/peer_kernels.hip, used by
+// src/network/peer_comm.cpp).  Every rank owns one window, mapped into every peer (the same
+// device for thread ranks, hipIpc handles over xGMI across processes):
+//   [kPeerFlagBytes: u64 flags[2][kMaxPeerBufs] -- arrival / departure epochs written by each
+//    peer] [stage: this rank's input of the collective in progress]
+// A collective is ONE kernel: wait until the peers left the previous collective's stage, copy
+// the input into the own stage, publish an arrival epoch to every peer, wait for every peer's
+// arrival, read the peers' stages directly (reduce / gather), publish a departure epoch.  No
+// host rendezvous: the kernels are captured into the learner's graphs.  Every wait is bounded
+// (timeout -> status code, the host raises); a collective whose guard flag is set is skipped on
+// every rank (the guard is replicated state, e.g. Round::done).
+constexpr size_t kPeerFlagBytes = 4096;
+enum PeerKind { kPeerAllreduce = 0, kPeerReduceScatter = 1, kPeerAllgather = 2, kPeerBroadcast = 3 };
+// status words (host-mapped): [0] error code, [1] abort request from the host, [2] epoch of the error
+enum PeerStatus { kPeerOk = 0, kPeerTimeout = 1, kPeerInjected = 2, kPeerAborted = 3 };
+struct PeerArgs {
+  char* win[kMaxPeerBufs];  // every rank's window (self included)
+  int32_t n, rank, kind, op, root;
+  int32_t elem;             // element bytes (reductions) or 4 / 1 (gathers, broadcast)
+  long long fail_epoch;     // fault injection: this rank stops at that collective (0: never)
+  const char* send;
+  char* recv;
+  size_t count;             // elements of this chunk (reduce-scatter: per block)
+  size_t stride;            // reduce-scatter: elements between send blocks; allgather: elements per rank
+  size_t off;               // chunk offset in elements
+  unsigned long long* ctl;  // local device words: [0] epoch, [1] copy arrivals, [2] read departures, [3] error
+  unsigned int* status;     // host-mapped PeerStatus words
+  const int32_t* guard;     // optional: nonzero -> skipped
+  long long timeout_ticks;  // 100 MHz wall-clock ticks
+};
+void PeerCollective(const PeerArgs& a, hipStream_t s);
+
 // score scaling helpers
 void AddConst(double* score, int64_t n, double v, hipStream_t s);
 void MulConst(double* score, int64_t n, double v, hipStream_t s);

@@ -128,8 +128,10 @@ int LGBM_AMD_RcclSelfTest(int* out_ok) {
     if (dc == nullptr) Log::Fatal("no device comm (call LGBM_AMD_RcclInit first)");
     const int n = dc->size(), r = dc->rank();
     const size_t cnt = 1000;
+    // (a non-blocking stream and stream-ordered copies only: ranks that share the device wait
+    // on each other inside the collective kernels, so nothing here may wait for the device)
     hipStream_t s;
-    if (hipStreamCreate(&s) != hipSuccess) Log::Fatal("hipStreamCreate failed");
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) Log::Fatal("hipStreamCreate failed");
     long long* di64;
     double* df64;
     uint32_t* du32;
@@ -145,9 +147,9 @@ int LGBM_AMD_RcclSelfTest(int* out_ok) {
       hf[i] = 0.5 * (r + 1) * i;
       hu[i] = static_cast<uint32_t>(r * 7 + i);
     }
-    (void)hipMemcpy(di64, hi.data(), cnt * sizeof(long long), hipMemcpyHostToDevice);
-    (void)hipMemcpy(df64, hf.data(), cnt * sizeof(double), hipMemcpyHostToDevice);
-    (void)hipMemcpy(du32, hu.data(), cnt * sizeof(uint32_t), hipMemcpyHostToDevice);
+    (void)hipMemcpyAsync(di64, hi.data(), cnt * sizeof(long long), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(df64, hf.data(), cnt * sizeof(double), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(du32, hu.data(), cnt * sizeof(uint32_t), hipMemcpyHostToDevice, s);
     dc->AllreduceSumI64(di64, cnt, s);
     dc->AllreduceSumF64(df64, cnt, s);
     dc->AllreduceMaxU32(du32, cnt, s);
@@ -162,20 +164,20 @@ int LGBM_AMD_RcclSelfTest(int* out_ok) {
     std::vector<long long> hrs(blk * n), hag(n, 0);
     for (size_t i = 0; i < blk * n; ++i) hrs[i] = static_cast<long long>((r + 1) * i);
     hag[r] = r + 1;
-    (void)hipMemcpy(rs_in, hrs.data(), hrs.size() * sizeof(long long), hipMemcpyHostToDevice);
-    (void)hipMemcpy(ag, hag.data(), hag.size() * sizeof(long long), hipMemcpyHostToDevice);
+    (void)hipMemcpyAsync(rs_in, hrs.data(), hrs.size() * sizeof(long long), hipMemcpyHostToDevice, s);
+    (void)hipMemcpyAsync(ag, hag.data(), hag.size() * sizeof(long long), hipMemcpyHostToDevice, s);
     dc->ReduceScatterSumI64(rs_in, rs_out, blk, s);
     dc->Allgather(ag + r, ag, sizeof(long long), s);
-    (void)hipStreamSynchronize(s);
     std::vector<long long> hro(blk);
-    (void)hipMemcpy(hro.data(), rs_out, blk * sizeof(long long), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(hag.data(), ag, n * sizeof(long long), hipMemcpyDeviceToHost);
+    (void)hipMemcpyAsync(hro.data(), rs_out, blk * sizeof(long long), hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(hag.data(), ag, n * sizeof(long long), hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(hi.data(), di64, cnt * sizeof(long long), hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(hf.data(), df64, cnt * sizeof(double), hipMemcpyDeviceToHost, s);
+    (void)hipMemcpyAsync(hu.data(), du32, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    (void)hipStreamSynchronize(s);
     (void)hipFree(rs_in);
     (void)hipFree(rs_out);
     (void)hipFree(ag);
-    (void)hipMemcpy(hi.data(), di64, cnt * sizeof(long long), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(hf.data(), df64, cnt * sizeof(double), hipMemcpyDeviceToHost);
-    (void)hipMemcpy(hu.data(), du32, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost);
     const long long tri = static_cast<long long>(n) * (n + 1) / 2;
     bool ok = true;
     for (size_t j = 0; j < blk; ++j) ok = ok && hro[j] == tri * static_cast<long long>(r * blk + j);
@@ -212,7 +214,8 @@ int LGBM_AMD_RcclGraphSelfTest(int* out_ok) {
     if (hipMalloc(&d, cnt * sizeof(long long)) != hipSuccess) Log::Fatal("hipMalloc failed");
     std::vector<long long> h(cnt);
     for (size_t i = 0; i < cnt; ++i) h[i] = static_cast<long long>(i);
-    (void)hipMemcpy(d, h.data(), cnt * sizeof(long long), hipMemcpyHostToDevice);
+    (void)hipMemcpyAsync(d, h.data(), cnt * sizeof(long long), hipMemcpyHostToDevice, s);
+    (void)hipStreamSynchronize(s);
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) Log::Fatal("begin capture failed");
@@ -223,8 +226,8 @@ int LGBM_AMD_RcclGraphSelfTest(int* out_ok) {
     for (int it = 0; it < 3; ++it) {
       if (hipGraphLaunch(ge, s) != hipSuccess) Log::Fatal("graph launch failed");
     }
+    (void)hipMemcpyAsync(h.data(), d, cnt * sizeof(long long), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
-    (void)hipMemcpy(h.data(), d, cnt * sizeof(long long), hipMemcpyDeviceToHost);
     long long f = 1;
     for (int k = 0; k < 6; ++k) f *= n;
     bool ok = true;

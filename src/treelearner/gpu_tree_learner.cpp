@@ -896,6 +896,7 @@ void GPUTreeLearner::MaterializeSplitGradients() {
 Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   common::ScopedTimer timer("GPUTreeLearner::Train");
   HIPCHECK(hipSetDevice(device_id_));
+  if (distributed_ && Network::device_comm() != nullptr) Network::device_comm()->HostBarrier();
   // fixed-point scales of this tree: max |g|, max h over all rows (and ranks)
   // the gradient kernel already interleaved (g, h) and found max|g| / max h when it wrote
   // exactly these buffers (one model per iteration, not modified on the host since)
@@ -1221,6 +1222,9 @@ void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
     return;
   }
   DeviceComm* dc = Network::device_comm();
+  // a finished tree's remaining rounds skip their collectives on every rank (Round::done is
+  // replicated state); communicators that cannot skip run them
+  dc->SetSkipGuard(&d_round_->done);
   const size_t owned = static_cast<size_t>(round_k_) * rs_block_ * 2;
   if (data_parallel_) HIPCHECK(hipMemsetAsync(d_round_send_, 0, sizeof(long long) * owned * world_, stream_));
   dev::RoundSplitReduce(a, stream_);
@@ -1234,6 +1238,7 @@ void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
     const size_t cb = per * kMaxCatWords * sizeof(uint32_t);
     dc->Allgather(fc + cb * rank_, fc, cb, stream_);
   }
+  dc->SetSkipGuard(nullptr);
   dev::RoundChildBestAndPlan(a, stream_);
 }
 
@@ -1309,6 +1314,7 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   bool graph = use_graph;
   if (graph && (round_seg_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
                 round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
+    if (dc != nullptr) dc->HostBarrier();
     DestroyGraph();
     graph = capture(&round_seg_exec_, false, kRoundSeg);
     if (!graph) DestroyGraph();
@@ -1319,6 +1325,7 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   if (graph) {
     if (static_cast<int>(round_root_execs_.size()) <= nseg) round_root_execs_.resize(nseg + 1, nullptr);
     if (round_root_execs_[nseg] == nullptr) {
+      if (dc != nullptr) dc->HostBarrier();
       graph = capture(&round_root_execs_[nseg], true, nseg * kRoundSeg);
       if (!graph) DestroyGraph();
     }
@@ -1541,6 +1548,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
       if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
           graph_root_mode_ != root_mode || graph_xt_ != (xt ? 1 : 0)) {
+        if (dcomm != nullptr) dcomm->HostBarrier();
         DestroyGraph();
         hipGraph_t g = nullptr;
         HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));

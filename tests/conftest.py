@@ -9,6 +9,14 @@ if os.environ.get("PYTEST_XDIST_WORKER_COUNT"):
     _share = max(1, (os.cpu_count() or 8) // int(os.environ["PYTEST_XDIST_WORKER_COUNT"]))
     os.environ.setdefault("OMP_NUM_THREADS", str(_share))
 
+# in-process device ranks (tests/test_gpu_distributed.py) are threads with a stream each whose
+# peer collectives wait on one another on the device: every rank's stream needs its own
+# hardware queue (HIP's default of 4 queues per process would put two ranks' kernels in one
+# queue, behind each other).  Read by the HIP runtime when it initialises.
+# (the box exports HIP's default of 4: raise it, never above what the pool allows)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

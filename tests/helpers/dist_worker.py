@@ -29,6 +29,9 @@ def main():
     # device collectives: RCCL needs one GPU per rank; with every rank on one GPU the
     # device learner falls back to the host collectives (same code path above the comm)
     rank, world, _ = torch_dist.init_network(use_rccl=os.environ.get("LGBM_TEST_RCCL", "0") == "1")
+    want = os.environ.get("LGBM_TEST_REQUIRE_COMM")
+    if want and torch_dist.device_comm_kind() != want:  # (no silent fallback in the tests)
+        raise RuntimeError("device comm %r, expected %r" % (torch_dist.device_comm_kind(), want))
     X, y = make_data()
     params = {"objective": "binary", "num_leaves": 15, "learning_rate": 0.1, "verbose": -1,
               "tree_learner": learner, "num_machines": world, "min_data_in_leaf": 20, "seed": 3,

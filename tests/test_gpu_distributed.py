@@ -1,7 +1,8 @@
 """Distributed device learners on one MI355X: ranks are threads of this process, each with
-its own stream, joined by the in-process device communicator (device kernels read the peer
-ranks' buffers; src/network/inproc_device_comm.cpp).  This runs the same collective
-sequence as RCCL on a multi-GPU node:
+its own stream, joined by the capture-safe peer communicator (one kernel per collective that
+reads the peer ranks' windows; src/network/peer_comm.cpp, src/device/peer_kernels.hip) -- the
+same kernels and the same captured round graphs as one process per GPU over xGMI, only the
+windows are mapped by pointer instead of hipIpc handles.  The collective sequence:
   * data-parallel: per split the histogrammed child's int64 histogram is reduce-scattered
     to the feature owners, owners scan their features, the per-feature split records are
     all-gathered and every rank picks the same split (reference
@@ -47,7 +48,7 @@ def _splits(model_str, tree=0):
     return rows.get("split_feature"), rows.get("threshold")
 
 
-def _run(learner, world, rounds=8, **extra):
+def _run(learner, world, rounds=8, comm=True, **extra):
     X, y = make_data(N, 10)
     full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
     serial = lgb.train(BASE, full.subset(np.arange(N)), rounds)
@@ -62,26 +63,32 @@ def _run(learner, world, rounds=8, **extra):
         bst = lgb.train(params, ds, rounds)
         return bst.model_to_string(), bst.predict(X)
 
-    with ThreadRanks(world, timeout_s=120, device_comm=True) as tr:
+    with ThreadRanks(world, timeout_s=120, device_comm=comm) as tr:
         res = tr.run(rank_fn)
     assert all(r.ok for r in res), [str(r.error) for r in res]
     return X, y, serial, [r.value for r in res]
 
 
-def test_device_comm_self_test_threads(gpu_available):
-    """Every device collective of the in-process communicator (all-reduce sum / max,
-    int64 reduce-scatter, allgather) on 3 thread ranks."""
+@pytest.mark.parametrize("comm,world", [("peer", 3), ("peer", 8), ("host", 3)])
+def test_device_comm_self_test_threads(comm, world, gpu_available):
+    """Every device collective of the in-process communicators (all-reduce sum / max,
+    int64 reduce-scatter, allgather) on thread ranks; the peer comm also replays its
+    collectives from a captured graph."""
     lib = _load_lib()
 
     def rank_fn(r):
         ok = ctypes.c_int(0)
         _safe_call(lib.LGBM_AMD_RcclSelfTest(ctypes.byref(ok)))
+        if comm == "peer":
+            ok2 = ctypes.c_int(0)
+            _safe_call(lib.LGBM_AMD_RcclGraphSelfTest(ctypes.byref(ok2)))
+            return ok.value * ok2.value
         return ok.value
 
-    with ThreadRanks(3, timeout_s=60, device_comm=True) as tr:
+    with ThreadRanks(world, timeout_s=60, device_comm=comm) as tr:
         res = tr.run(rank_fn)
     assert all(r.ok for r in res), [str(r.error) for r in res]
-    assert [r.value for r in res] == [1, 1, 1]
+    assert [r.value for r in res] == [1] * world
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -168,14 +175,18 @@ def test_distributed_round_growth_equals_one_split_per_step(learner, world, gpu_
     import json
     rows = [json.loads(line) for f in glob.glob(str(log) + "*") for line in open(f)]
     assert rows and all(row["rounds"][0] > 0 for row in rows)
+    # the peer comm is capture-safe: the rounds and their collectives ran from hipGraphs
+    assert all(row["graph"][0] for row in rows)
     assert sum(row["rounds"][0] for row in rows) < sum(row["leaves"][0] - 1 for row in rows)
 
 
-def test_device_collective_fault_mid_tree_raises_on_every_rank(gpu_available):
+@pytest.mark.parametrize("comm", ["peer", "host"])
+def test_device_collective_fault_mid_tree_raises_on_every_rank(comm, gpu_available):
     """A rank fails inside a device collective in the middle of a data-parallel tree (fault
     injected into its 30th device collective, within the second tree's rounds): the failing
-    rank raises, its peer raises at its next rendezvous instead of waiting, well within the
-    timeout -- and the GPU stays usable (a serial model trains afterwards)."""
+    rank raises; its peer raises instead of waiting forever -- at its next host rendezvous
+    (host comm), or when its device-side wait hits the timeout inside the captured round graph
+    (peer comm) -- and the GPU stays usable (a serial model trains afterwards)."""
     import time
     X, y = make_data(N, 10)
     full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
@@ -186,11 +197,62 @@ def test_device_collective_fault_mid_tree_raises_on_every_rank(gpu_available):
         return lgb.train(params, full.subset(np.arange(r, N, world)), 8).model_to_string()
 
     t0 = time.time()
-    with ThreadRanks(world, timeout_s=60, fail_rank=1, device_comm=True, device_fail_at_call=30) as tr:
+    with ThreadRanks(world, timeout_s=8 if comm == "peer" else 60, fail_rank=1, device_comm=comm,
+                     device_fail_at_call=30) as tr:
         res = tr.run(rank_fn)
     assert time.time() - t0 < 45
-    assert not res[1].ok and "injected fault in rank 1 at device collective call 30" in str(res[1].error)
-    assert not res[0].ok and "injected fault" in str(res[0].error), str(res[0].error)
+    if comm == "peer":
+        assert not res[1].ok and "injected fault (rank 1, collective 30)" in str(res[1].error), str(res[1].error)
+        assert not res[0].ok and "timed out waiting for a peer rank (rank 0, collective 30)" in str(res[0].error), \
+            str(res[0].error)
+    else:
+        assert not res[1].ok and "injected fault in rank 1 at device collective call 30" in str(res[1].error)
+        assert not res[0].ok and "injected fault" in str(res[0].error), str(res[0].error)
     # the device is left usable
     bst = lgb.train(BASE, full.subset(np.arange(N)), 2)
     assert bst.num_trees() == 2
+
+
+def test_multiprocess_peer_comm_data_parallel(gpu_available, tmp_path):
+    """One process per rank (2 processes sharing the box's one GPU): the production path of a
+    multi-GPU node -- torch.distributed (gloo) for the host collectives, the peer comm's windows
+    exported with hipIpcGetMemHandle and mapped by the other process, the round collectives
+    captured in the round graphs (ITER_LOG "graph": true).  Identical models and predictions
+    on both ranks, and a useful model."""
+    import json
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OMP_NUM_THREADS="2", LGBM_TEST_DEVICE="gpu", LGBM_TEST_RCCL="1",
+                   LGBM_AMD_DEVICE_COMM="peer", LGBM_TEST_REQUIRE_COMM="peer",
+                   LGBM_AMD_ITER_LOG=str(tmp_path / ("iters_%d.jsonl" % r)),
+                   LGBM_TEST_PARAMS=json.dumps({"max_bin": 63}))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "helpers", "dist_worker.py"), "data",
+                                       str(tmp_path)], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            out, _ = p.communicate()
+        outs.append(out.decode())
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out
+    models = [(tmp_path / ("model_%d.txt" % r)).read_text() for r in range(world)]
+    assert _trees(models[0]) == _trees(models[1])
+    import glob
+    rows = [json.loads(line) for f in glob.glob(str(tmp_path / "iters_*")) for line in open(f)]
+    assert rows and all(row["graph"][0] for row in rows), rows[:2]
+    preds = [np.load(str(tmp_path / ("pred_%d.npy" % r))) for r in range(world)]
+    np.testing.assert_array_equal(preds[0], preds[1])
+    from sklearn.metrics import roc_auc_score
+    X, y = make_data()
+    assert roc_auc_score(y, preds[0]) > 0.8
