@@ -84,6 +84,21 @@ __device__ __forceinline__ T PeerOpApply(T a, T b) {
   }
 }
 
+// grid-strided copy with four independent loads in flight per thread (uncached windows: each
+// access is a full memory round trip)
+template <typename T>
+__device__ __forceinline__ void PeerCopy(T* dst, const T* src, size_t cnt, size_t tid, size_t nth) {
+  size_t i = tid;
+  for (; i + 3 * nth < cnt; i += 4 * nth) {
+    const T v0 = src[i], v1 = src[i + nth], v2 = src[i + 2 * nth], v3 = src[i + 3 * nth];
+    dst[i] = v0;
+    dst[i + nth] = v1;
+    dst[i + 2 * nth] = v2;
+    dst[i + 3 * nth] = v3;
+  }
+  for (; i < cnt; i += nth) dst[i] = src[i];
+}
+
 // OP: 0 sum, 3 max (reductions: allreduce / reduce-scatter); -1 copy (allgather / broadcast)
 template <typename T, int OP>
 __global__ __launch_bounds__(256) void k_peer_collective(PeerArgs a) {
@@ -124,13 +139,10 @@ __global__ __launch_bounds__(256) void k_peer_collective(PeerArgs a) {
     if (kind == kPeerReduceScatter) {
       for (int p = 0; p < a.n; ++p) {
         if (p == a.rank) continue;
-        const T* src = send + static_cast<size_t>(p) * a.stride + a.off;
-        T* dst = stage + static_cast<size_t>(p) * cnt;
-        for (size_t i = tid; i < cnt; i += nth) dst[i] = src[i];
+        PeerCopy(stage + static_cast<size_t>(p) * cnt, send + static_cast<size_t>(p) * a.stride + a.off, cnt, tid, nth);
       }
     } else {
-      const T* src = send + a.off;
-      for (size_t i = tid; i < cnt; i += nth) stage[i] = src[i];
+      PeerCopy(stage, send + a.off, cnt, tid, nth);
     }
   }
   __syncthreads();
@@ -153,25 +165,29 @@ __global__ __launch_bounds__(256) void k_peer_collective(PeerArgs a) {
   if constexpr (OP >= 0) {
     const size_t own_off = kind == kPeerReduceScatter ? static_cast<size_t>(a.rank) * a.stride + a.off : a.off;
     const size_t peer_off = kind == kPeerReduceScatter ? static_cast<size_t>(a.rank) * cnt : 0;
-    for (size_t i = tid; i < cnt; i += nth) {
-      T v{};
+    // two elements per pass: 2 x n independent loads in flight
+    for (size_t i = tid; i < cnt; i += 2 * nth) {
+      const bool two = i + nth < cnt;
+      T v0{}, v1{};
       for (int p = 0; p < a.n; ++p) {
-        const T x = p == a.rank ? send[own_off + i]
-                                : reinterpret_cast<const T*>(a.win[p] + kPeerFlagBytes)[peer_off + i];
-        v = p == 0 ? x : PeerOpApply<T, OP>(v, x);
+        const T* src = p == a.rank ? send + own_off : reinterpret_cast<const T*>(a.win[p] + kPeerFlagBytes) + peer_off;
+        const T x0 = src[i];
+        const T x1 = two ? src[i + nth] : T{};
+        v0 = p == 0 ? x0 : PeerOpApply<T, OP>(v0, x0);
+        v1 = p == 0 ? x1 : PeerOpApply<T, OP>(v1, x1);
       }
-      recv[a.off + i] = v;
+      recv[a.off + i] = v0;
+      if (two) recv[a.off + i + nth] = v1;
     }
   } else if (kind == kPeerAllgather) {
     for (int p = 0; p < a.n; ++p) {
       const T* src = p == a.rank ? send + a.off : reinterpret_cast<const T*>(a.win[p] + kPeerFlagBytes);
       T* dst = recv + static_cast<size_t>(p) * a.stride + a.off;
       if (p == a.rank && src == dst) continue;  // (in place)
-      for (size_t i = tid; i < cnt; i += nth) dst[i] = src[i];
+      PeerCopy(dst, src, cnt, tid, nth);
     }
   } else if (a.rank != a.root) {
-    const T* src = reinterpret_cast<const T*>(a.win[a.root] + kPeerFlagBytes);
-    for (size_t i = tid; i < cnt; i += nth) recv[a.off + i] = src[i];
+    PeerCopy(recv + a.off, reinterpret_cast<const T*>(a.win[a.root] + kPeerFlagBytes), cnt, tid, nth);
   }
   // 5. departure: the peers may overwrite their stages once every rank has read them
   __syncthreads();
@@ -196,12 +212,12 @@ void LaunchPeer(const PeerArgs& a, int grid, hipStream_t s) {
 }  // namespace
 
 void PeerCollective(const PeerArgs& a, hipStream_t s) {
-  // bytes this rank reads: ~64 KB per workgroup, at most 64 workgroups (a few per XCD is
-  // enough for the link; more only lengthens the arrival / departure counts)
+  // bytes this rank reads: ~16 KB per workgroup (uncached accesses are latency-bound: many
+  // workgroups in flight), at most 128 (more only lengthens the arrival / departure counts)
   const size_t blocks = a.kind == kPeerAllgather ? static_cast<size_t>(a.n) : 1;
   const size_t bytes = a.count * static_cast<size_t>(a.elem) *
                        (a.kind == kPeerAllgather ? blocks : static_cast<size_t>(a.kind == kPeerBroadcast ? 1 : a.n));
-  const int grid = static_cast<int>(std::max<size_t>(1, std::min<size_t>(64, (bytes + 65535) / 65536)));
+  const int grid = static_cast<int>(std::max<size_t>(1, std::min<size_t>(128, (bytes + 16383) / 16384)));
   if (a.kind == kPeerAllreduce || a.kind == kPeerReduceScatter) {
     switch (a.op) {
       case kPeerSumF64: LaunchPeer<double, 0>(a, grid, s); break;
