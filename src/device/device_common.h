@@ -45,11 +45,18 @@ __device__ __forceinline__ int RoundIntD(double x) { return static_cast<int>(x +
 // captured graph does not depend on it)
 __device__ __forceinline__ int RootRows(const KArgs& a) { return a.num_rows_dev ? *a.num_rows_dev : a.num_rows; }
 
+// a group's bin from the row bytes at its offset, by its width (Feature::gwide: 0 8-bit,
+// 1 16-bit, 2 / 3 the low / high 4 bits)
+__device__ __forceinline__ uint32_t GroupBinAt(const uint8_t* p, int gwide) {
+  if (gwide == 1) return static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(p));
+  const uint32_t b = *p;
+  return gwide >= 2 ? (b >> ((gwide & 1) * 4)) & 15u : b;
+}
 // bin of a storage column for `row` in the row-major matrix, from the group's byte offset
 // in a row and its width (Feature::gbyte / gwide)
 __device__ __forceinline__ uint32_t RowBin(const KArgs& a, int64_t row, int gbyte, int gwide) {
   const uint8_t* p = static_cast<const uint8_t*>(a.bins) + row * (4 * static_cast<int64_t>(a.row_words)) + gbyte;
-  return gwide ? static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(p)) : static_cast<uint32_t>(*p);
+  return GroupBinAt(p, gwide);
 }
 
 // (g, h) of a row (KArgs::gh_stride)
@@ -70,7 +77,7 @@ __device__ __forceinline__ int32_t* RowBuf(const KArgs& a, int b) { return RowBu
 // else from the row-major matrix (whose line the histogram pass then reads again)
 __device__ __forceinline__ uint32_t ColBin(const KArgs& a, int64_t row, int gbyte, int gwide, int64_t col_off) {
   if (a.bins_col == nullptr) return RowBin(a, row, gbyte, gwide);
-  if (gwide) return reinterpret_cast<const uint16_t*>(a.bins_col + col_off)[row];
+  if (gwide == 1) return reinterpret_cast<const uint16_t*>(a.bins_col + col_off)[row];  // (4-bit groups: bytes)
   return a.bins_col[col_off + row];
 }
 

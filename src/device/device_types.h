@@ -35,8 +35,10 @@ struct Feature {
   int32_t sub_lo, sub_hi;  // this feature's [lo, hi) range inside the group's bin space
   int32_t real_index;
   int32_t monotone;
-  // where the group's bin sits: byte offset inside a row of the row-major matrix, 16-bit
-  // (1) or 8-bit (0), and the byte offset of its column in the column-major copy
+  // where the group's bin sits: byte offset inside a row of the row-major matrix, its width
+  // there -- 0 8-bit, 1 16-bit, 2 / 3 the low / high 4 bits of the byte (4-bit storage,
+  // GroupBinOf) -- and the byte offset of its column in the column-major copy (one byte per
+  // row for 8- and 4-bit groups)
   int32_t gbyte;
   int32_t gwide;
   int64_t col_off;

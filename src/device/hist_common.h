@@ -11,8 +11,8 @@ namespace dev {
 struct TileCtx {
   int w0, w1, lo_bin, nbins;
   int tpr, rpp, q, rs;  // threads per row, rows per pass, my word, my row slot
-  int goff[4];          // histogram offset of each group of my word inside the tile (-1: none)
-  int bits;             // bits per group of my word (8 or 16)
+  int goff[8];          // histogram offset of each group of my word inside the tile (-1: none)
+  int bits;             // bits per group of my word (4, 8 or 16)
   float sg, sh;         // fixed-point scales
 };
 
@@ -20,8 +20,9 @@ struct TileCtx {
 constexpr int kSparseGPW = 1;
 constexpr int kSparsePer = kSparsePerThread;  // (KArgs::sp_team threads per row)
 
-// GPW: groups per word (4: 8-bit layout, 2: 16-bit layout, 0: mixed layout, one more round
-// trip for the word table) or kSparseGPW; otherwise every load is independent of the others
+// GPW: groups per word (8: 4-bit layout, 4: 8-bit layout, 2: 16-bit layout, 0: mixed layout,
+// one more round trip for the word table) or kSparseGPW; otherwise every load is independent
+// of the others
 template <int GPW>
 __device__ __forceinline__ void InitTile(const KArgs& a, TileCtx* t) {
   if (GPW == kSparseGPW) {  // tile = bin range; KArgs::sp_team threads per row
@@ -36,7 +37,7 @@ __device__ __forceinline__ void InitTile(const KArgs& a, TileCtx* t) {
     t->sg = static_cast<float>(a.scales[0]);
     t->sh = static_cast<float>(a.scales[1]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) t->goff[j] = -1;
+    for (int j = 0; j < 8; ++j) t->goff[j] = -1;
     return;
   }
   t->w0 = a.tile_w0 + blockIdx.y * a.tile_words;
@@ -60,9 +61,10 @@ __device__ __forceinline__ void InitTile(const KArgs& a, TileCtx* t) {
     gcount = GPW;
     t->bits = 32 / GPW;
   }
-  int graw[4];
+  constexpr int kG = GPW == 8 ? 8 : 4;  // groups a word can hold
+  int graw[kG];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < kG; ++j) {
     const int g = gfirst + j;
     graw[j] = (j < gcount && g < a.p.num_groups) ? a.group_off[g] : -1;
   }
@@ -72,7 +74,7 @@ __device__ __forceinline__ void InitTile(const KArgs& a, TileCtx* t) {
   t->sh = static_cast<float>(a.scales[1]);
   t->nbins = hi_bin - t->lo_bin;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) t->goff[j] = graw[j] >= 0 ? graw[j] - t->lo_bin : -1;
+  for (int j = 0; j < kG; ++j) t->goff[j] = graw[j] >= 0 ? graw[j] - t->lo_bin : -1;
 }
 
 // Group bin 0 holds every row whose features all sit in their most frequent bin: it is
@@ -92,6 +94,7 @@ __device__ __forceinline__ void AddRow(unsigned long long* lds, const int* goff,
   for (int j = 0; j < (GPW == 0 ? 4 : GPW); ++j) {
     uint32_t b;
     if (GPW == 0) b = (w >> ((bits * j) & 31)) & (bits == 8 ? 0xffu : 0xffffu);
+    else if (GPW == 8) b = (w >> (4 * j)) & 0xfu;
     else b = GPW == 4 ? ((w >> (8 * j)) & 0xffu) : ((w >> (16 * j)) & 0xffffu);
     if (goff[j] >= 0 && b != 0u) {
       if (UNITS == 1) {

@@ -162,11 +162,13 @@ static void LaunchHist(const KArgs& a, hipStream_t s) {
     if (a.hist_units == 1) hipLaunchKernelGGL((k_hist<MODE, kSparseGPW, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
     else hipLaunchKernelGGL((k_hist<MODE, kSparseGPW, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
   } else if (a.hist_units == 1) {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_hist<MODE, 4, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_hist<MODE, 8, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_hist<MODE, 4, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_hist<MODE, 2, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
     else hipLaunchKernelGGL((k_hist<MODE, 0, 1>), grid, dim3(kHistThreads), lds_bytes, s, a);
   } else {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_hist<MODE, 4, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_hist<MODE, 8, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_hist<MODE, 4, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_hist<MODE, 2, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
     else hipLaunchKernelGGL((k_hist<MODE, 0, 2>), grid, dim3(kHistThreads), lds_bytes, s, a);
   }
@@ -194,6 +196,10 @@ void PrepareRoundKernels(int max_lds);
 
 // dynamic LDS above 64 KiB must be enabled per kernel (outside any graph capture)
 void PrepareKernels() {
+  AllowLds(k_hist<0, 8, 1>);
+  AllowLds(k_hist<0, 8, 2>);
+  AllowLds(k_hist<2, 8, 1>);
+  AllowLds(k_hist<2, 8, 2>);
   AllowLds(k_hist<0, 4, 1>);
   AllowLds(k_hist<0, 2, 1>);
   AllowLds(k_hist<0, 4, 2>);

@@ -44,8 +44,11 @@ struct KArgs {
   int32_t root_identity;     // root rows are 0..num_rows-1 (indices written by the root pass)
   // row layout: every group 8-bit (bin_bytes 1, 4 per word), every group 16-bit (2, 2 per
   // word), or mixed (0): each word holds 8-bit groups or 16-bit groups only, in group order
-  // (a 16-bit group starts a new word), word_g0 / word_wide describe the words
+  // (a 16-bit group starts a new word), word_g0 / word_wide describe the words.  nibbles: every
+  // group has at most 16 bins and sits in 4 bits, eight to a word (bin_bytes is then 1: the
+  // groups are byte-addressable as (byte >> 4 * high) & 15, Feature::gwide 2 / 3)
   int32_t bin_bytes;
+  int32_t nibbles;
   int32_t words_per_row;     // 32-bit words of bins per row
   // 32-bit words between consecutive rows of `bins` (>= words_per_row).  With gh_stride > 1 the
   // rows carry their (g, h) in their last two words (gh points at row 0's): a gathered row is

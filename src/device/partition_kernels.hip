@@ -291,11 +291,13 @@ static void LaunchSplit(const KArgs& a, hipStream_t s) {
     if (a.hist_units == 1) hipLaunchKernelGGL((k_split<kSparseGPW, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
     else hipLaunchKernelGGL((k_split<kSparseGPW, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
   } else if (a.hist_units == 1) {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_split<8, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
     else hipLaunchKernelGGL((k_split<0, 1, true, GR>), grid, dim3(kPartThreads), lds, s, a);
   } else {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_split<8, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_split<4, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_split<2, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
     else hipLaunchKernelGGL((k_split<0, 2, true, GR>), grid, dim3(kPartThreads), lds, s, a);
   }
@@ -309,6 +311,8 @@ void SplitStep(const KArgs& a, hipStream_t s, bool reduce) {
 
 template <int GR>
 static void AllowSplitLds(int mx) {
+  AllowLds(k_split<8, 1, true, GR>, mx);
+  AllowLds(k_split<8, 2, true, GR>, mx);
   AllowLds(k_split<4, 1, true, GR>, mx);
   AllowLds(k_split<2, 1, true, GR>, mx);
   AllowLds(k_split<4, 2, true, GR>, mx);

@@ -63,21 +63,23 @@ struct ColSrc {
   int64_t off0;          // byte offset of row 0's bin
   int64_t stride;        // bytes between rows
   uint32_t mask;
+  uint32_t shift;        // 4-bit groups in the row-major matrix: 4 for the high half of the byte
 };
 __device__ __forceinline__ ColSrc ColSource(const KArgs& a, int gbyte, int gwide, int64_t col_off) {
   ColSrc c;
   const bool col = a.bins_col != nullptr;
   c.base = col ? reinterpret_cast<const uint32_t*>(a.bins_col) : static_cast<const uint32_t*>(a.bins);
   c.off0 = col ? col_off : gbyte;
-  c.stride = col ? (gwide ? 2 : 1) : 4 * static_cast<int64_t>(a.row_words);
-  c.mask = gwide ? 0xffffu : 0xffu;
+  c.stride = col ? (gwide == 1 ? 2 : 1) : 4 * static_cast<int64_t>(a.row_words);
+  c.mask = gwide == 1 ? 0xffffu : (gwide >= 2 && !col ? 0xfu : 0xffu);
+  c.shift = gwide == 3 && !col ? 4u : 0u;
   return c;
 }
 // (row < 0: none -- row 0 is read and the result dropped, so the load is unconditional)
 __device__ __forceinline__ uint32_t ColBinNB(const ColSrc& c, int row) {
   const int64_t off = c.off0 + static_cast<int64_t>(max(row, 0)) * c.stride;
   const uint32_t wd = c.base[off >> 2];
-  const uint32_t v = (wd >> ((static_cast<uint32_t>(off) & 3u) * 8u)) & c.mask;
+  const uint32_t v = (wd >> ((static_cast<uint32_t>(off) & 3u) * 8u + c.shift)) & c.mask;
   return row < 0 ? 0u : v;
 }
 
@@ -1552,11 +1554,13 @@ void LaunchRoundSplit(const KArgs& a, hipStream_t s) {
     if (a.hist_units == 1) hipLaunchKernelGGL((k_round_split<kSparseGPW, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
     else hipLaunchKernelGGL((k_round_split<kSparseGPW, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
   } else if (a.hist_units == 1) {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_round_split<8, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
     else hipLaunchKernelGGL((k_round_split<0, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
   } else {
-    if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_round_split<8, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
     else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
     else hipLaunchKernelGGL((k_round_split<0, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
   }
@@ -1569,6 +1573,8 @@ void AllowRoundSplitLds(int mx) {
       (void)hipGetLastError();
     }
   };
+  allow(reinterpret_cast<const void*>(k_round_split<8, 1, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<8, 2, GR>));
   allow(reinterpret_cast<const void*>(k_round_split<4, 1, GR>));
   allow(reinterpret_cast<const void*>(k_round_split<2, 1, GR>));
   allow(reinterpret_cast<const void*>(k_round_split<0, 1, GR>));
@@ -1627,6 +1633,8 @@ void PrepareRoundKernels(int max_lds) {
       (void)hipGetLastError();
     }
   };
+  allow(reinterpret_cast<const void*>(k_round_hist<8, 1>));
+  allow(reinterpret_cast<const void*>(k_round_hist<8, 2>));
   allow(reinterpret_cast<const void*>(k_round_hist<4, 1>));
   allow(reinterpret_cast<const void*>(k_round_hist<2, 1>));
   allow(reinterpret_cast<const void*>(k_round_hist<0, 1>));
@@ -1674,11 +1682,13 @@ void RoundSplitReduce(const KArgs& a, hipStream_t s) {
       if (a.hist_units == 1) hipLaunchKernelGGL((k_round_hist<kSparseGPW, 1>), grid, dim3(kHistThreads), lds, s, a);
       else hipLaunchKernelGGL((k_round_hist<kSparseGPW, 2>), grid, dim3(kHistThreads), lds, s, a);
     } else if (a.hist_units == 1) {
-      if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_hist<4, 1>), grid, dim3(kHistThreads), lds, s, a);
+      if (a.nibbles) hipLaunchKernelGGL((k_round_hist<8, 1>), grid, dim3(kHistThreads), lds, s, a);
+      else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_hist<4, 1>), grid, dim3(kHistThreads), lds, s, a);
       else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_hist<2, 1>), grid, dim3(kHistThreads), lds, s, a);
       else hipLaunchKernelGGL((k_round_hist<0, 1>), grid, dim3(kHistThreads), lds, s, a);
     } else {
-      if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_hist<4, 2>), grid, dim3(kHistThreads), lds, s, a);
+      if (a.nibbles) hipLaunchKernelGGL((k_round_hist<8, 2>), grid, dim3(kHistThreads), lds, s, a);
+      else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_hist<4, 2>), grid, dim3(kHistThreads), lds, s, a);
       else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_hist<2, 2>), grid, dim3(kHistThreads), lds, s, a);
       else hipLaunchKernelGGL((k_round_hist<0, 2>), grid, dim3(kHistThreads), lds, s, a);
     }

@@ -99,8 +99,7 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
         const NodeInfo nd = STAGED ? s_node[node] : MakeNode(a, t, node);
         uint32_t gb;
         if (stage_row) {
-          const uint8_t* rb = reinterpret_cast<const uint8_t*>(my) + nd.gbyte;
-          gb = nd.gwide ? static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(rb)) : static_cast<uint32_t>(*rb);
+          gb = GroupBinAt(reinterpret_cast<const uint8_t*>(my) + nd.gbyte, nd.gwide);
         } else {
           gb = words ? RowBin(a, row, nd.gbyte, nd.gwide) : ColBin(a, row, nd.gbyte, nd.gwide, nd.col_off);
         }
@@ -135,7 +134,8 @@ __global__ __launch_bounds__(256) void k_add_tree_score(KArgs a, DevTree t, cons
 __global__ __launch_bounds__(256) void k_tree_bitmaps(KArgs a, DevTree t) {
   const int node = blockIdx.x;
   const NodeInfo nd = MakeNode(a, t, node);
-  const uint32_t gb = threadIdx.x;  // raw group bin 0..255
+  // raw byte 0..255 of the row at the group's offset: its bin (4-bit groups: one half of it)
+  const uint32_t gb = nd.gwide >= 2 ? (threadIdx.x >> ((nd.gwide & 1) * 4)) & 15u : threadIdx.x;
   const uint32_t bin = (gb < static_cast<uint32_t>(nd.sub_lo) || gb >= static_cast<uint32_t>(nd.sub_hi))
                            ? static_cast<uint32_t>(nd.mfb)
                            : gb - nd.sub_lo + nd.offset;

@@ -192,7 +192,7 @@ std::string GPUTreeLearner::DebugCheckSplits(const Tree* tree) {
   js << "{\"device_mode\": true, \"leaves\": " << L << ", \"checked\": " << checked << ", \"mismatched\": "
      << mismatched << ", \"gain_mismatch\": " << gain_mismatch << ", \"direction_ties\": " << direction_ties
      << ", \"max_rel_gain_diff\": " << Num(max_rel) << ", \"layout\": \""
-     << (sparse_rows_ ? "sparse" : (args_.bin_bytes == 1 ? "8" : (args_.bin_bytes == 2 ? "16" : "mixed")))
+     << (sparse_rows_ ? "sparse" : args_.nibbles ? "4" : (args_.bin_bytes == 1 ? "8" : (args_.bin_bytes == 2 ? "16" : "mixed")))
      << "\", \"hist_tiles\": " << args_.hist_tiles << ", \"details\": [" << details.str() << "]}";
   return js.str();
 }

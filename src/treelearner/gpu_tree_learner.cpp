@@ -130,7 +130,7 @@ void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
   UploadData();
   global_count_.assign(config_->num_leaves, 0);
   const char* layout = sparse_rows_ ? "row-sparse"
-                       : (args_.bin_bytes == 1 ? "8-bit" : (args_.bin_bytes == 2 ? "16-bit" : "8/16-bit"));
+                       : nibbles_ ? "4-bit" : (args_.bin_bytes == 1 ? "8-bit" : (args_.bin_bytes == 2 ? "16-bit" : "8/16-bit"));
   Log::Info("MI355X learner on device %d (%d CUs): %d rows, %d groups, %d histogram bins, %s rows, %d hist tiles",
             device_id_, cus, num_data_, num_groups_, total_bins_, layout, args_.hist_tiles);
 }
@@ -155,9 +155,20 @@ void GPUTreeLearner::UploadData() {
     h_gwide_[g] = (data_->group(g).num_total_bin > 256 || (uniform && max_group_bins > 256)) ? 1 : 0;
     n_wide += h_gwide_[g];
   }
+  // 4-bit storage (the reference's DenseBin<uint8_t, true>, dense_bin.hpp IS_4BIT): when every
+  // group has at most 16 bins, eight groups share a word -- half the bytes of the matrix and
+  // of each gathered row.  The histogram gather is bound by its LDS atomics (one per row and
+  // group either way), so bytes are as fast or faster (Higgs 10M x 28, max_bin 15: 2.06 vs
+  // 2.02 ms/iter, profiles/r03_v5_four_bit_ab.md): 4-bit rows are chosen when the 8-bit matrix
+  // would take more than 32 GiB of HBM, or by LGBM_AMD_NIBBLE_BINS=1 (=0: never).
+  const bool can_nib = n_wide == 0 && max_group_bins <= 16 && !uniform;
+  const size_t byte_matrix = static_cast<size_t>(num_data_) * 4 * static_cast<size_t>((num_groups_ + 3) / 4);
+  nibbles_ = can_nib && byte_matrix > (size_t(32) << 30);
+  if (const char* e = std::getenv("LGBM_AMD_NIBBLE_BINS")) nibbles_ = can_nib && e[0] == '1';
+  h_gnib_.assign(num_groups_, 0);
   int slot = 0;
   for (int g = 0; g < num_groups_; ++g) {
-    const int wide = h_gwide_[g], per = wide ? 2 : 4;
+    const int wide = h_gwide_[g], per = nibbles_ ? 8 : (wide ? 2 : 4);
     if (h_word_g0_.empty() || h_word_wide_.back() != wide || slot == per) {
       h_word_g0_.push_back(g);
       h_word_wide_.push_back(static_cast<int8_t>(wide));
@@ -165,7 +176,8 @@ void GPUTreeLearner::UploadData() {
     }
     const int w = static_cast<int>(h_word_g0_.size()) - 1;
     h_word_of_group_[g] = w;
-    h_gbyte_[g] = 4 * w + slot * (wide ? 2 : 1);
+    h_gbyte_[g] = nibbles_ ? 4 * w + slot / 2 : 4 * w + slot * (wide ? 2 : 1);
+    if (nibbles_) h_gnib_[g] = static_cast<int8_t>(2 + (slot & 1));
     ++slot;
   }
   if (h_word_g0_.empty()) {
@@ -181,6 +193,7 @@ void GPUTreeLearner::UploadData() {
   d_word_wide_ = Alloc<int8_t>(h_word_wide_.size());
   HIPCHECK(hipMemcpy(d_word_wide_, h_word_wide_.data(), h_word_wide_.size(), hipMemcpyHostToDevice));
   args_.bin_bytes = bin_bytes;
+  args_.nibbles = nibbles_ ? 1 : 0;
   args_.words_per_row = wpr;
   args_.row_words = wpr;
   args_.gh_stride = 1;
@@ -207,6 +220,12 @@ void GPUTreeLearner::UploadData() {
     if (gh_rows) {
       args_.row_words = row_words;
       args_.gh_stride = row_words / 2;
+    }
+    // LGBM_AMD_ROW_ALIGN_WORDS=n: row stride rounded up to n words (A/B: 8 -> 32-B rows that
+    // never straddle a 64-B line, at 8/7 of the matrix bytes on the headline shape)
+    if (const char* e = std::getenv("LGBM_AMD_ROW_ALIGN_WORDS")) {
+      const int al = std::max(1, std::atoi(e));
+      if (!gh_rows) args_.row_words = (wpr + al - 1) / al * al;
     }
     std::vector<uint8_t> host = RowMajorBins(data_, args_.row_words);
     d_bins_ = Alloc<uint8_t>(host.size());
@@ -262,7 +281,7 @@ void GPUTreeLearner::UploadData() {
     F.real_index = data_->RealFeatureIndex(f);
     F.monotone = meta_[f].monotone_type;
     F.gbyte = h_gbyte_[g];
-    F.gwide = h_gwide_[g];
+    F.gwide = h_gnib_[g] != 0 ? h_gnib_[g] : h_gwide_[g];
     F.col_off = col_off[g];
     F.penalty = meta_[f].penalty;
   }
@@ -471,6 +490,7 @@ void GPUTreeLearner::UploadData() {
   a.num_rows_dev = nullptr;
   a.root_identity = 1;
   a.bin_bytes = bin_bytes;
+  a.nibbles = nibbles_ ? 1 : 0;
   a.words_per_row = wpr;
   a.word_g0 = d_word_g0_;
   a.word_wide = d_word_wide_;
@@ -2067,7 +2087,8 @@ std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d, int row_word
     uint8_t* row = host.data() + static_cast<size_t>(r) * row_bytes;
     for (int g = 0; g < ng; ++g) {
       const uint32_t v = d->group(g).Get(r);
-      if (!h_gwide_[g]) row[h_gbyte_[g]] = static_cast<uint8_t>(v);
+      if (h_gnib_[g] != 0) row[h_gbyte_[g]] |= static_cast<uint8_t>((v & 15u) << ((h_gnib_[g] & 1) * 4));
+      else if (!h_gwide_[g]) row[h_gbyte_[g]] = static_cast<uint8_t>(v);
       else reinterpret_cast<uint16_t*>(row + h_gbyte_[g])[0] = static_cast<uint16_t>(v);
     }
   }

@@ -243,6 +243,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   // word holding it; per word its first group (+ sentinel) and width
   std::vector<int32_t> h_gbyte_, h_word_of_group_, h_word_g0_;
   std::vector<int8_t> h_gwide_, h_word_wide_;
+  std::vector<int8_t> h_gnib_;  // 4-bit storage: 2 / 3 the group's low / high half-byte (0: 8 / 16-bit)
+  bool nibbles_ = false;        // every group stored in 4 bits (KArgs::nibbles)
   int32_t* d_word_g0_ = nullptr;
   int8_t* d_word_wide_ = nullptr;
   // row-sparse training storage (KArgs::sp_ptr / sp_bin) instead of the word matrix

@@ -92,6 +92,15 @@ CASES = {
     "sparse_rows_dp_wide": ({"gpu_use_dp": True, "max_bin_by_feature": [511] + [63] * 9, "bagging_fraction": 0.7,
                              "bagging_freq": 1, "_env": {"LGBM_AMD_SPARSE_ROWS": "1"}}, 20000),
     "sparse_auto_tiles": ({"min_data_in_leaf": 5}, 20000),
+    # 4-bit storage: every group <= 16 bins, eight groups to a word (max_bin 15), packed and
+    # wide histograms, multi-block leaves with bagging; the row-major fallback of the split
+    # column (no column copy) reads the half-bytes
+    "nibble": ({"max_bin": 15, "_env": {"LGBM_AMD_NIBBLE_BINS": "1"}}, 20000),
+    "nibble_dp": ({"max_bin": 15, "gpu_use_dp": True, "_env": {"LGBM_AMD_NIBBLE_BINS": "1"}}, 20000),
+    "nibble_multi_block": ({"max_bin": 15, "num_leaves": 63, "bagging_fraction": 0.8, "bagging_freq": 1,
+                            "_env": {"LGBM_AMD_NIBBLE_BINS": "1"}}, 150000),
+    "nibble_no_column_copy": ({"max_bin": 15, "_env": {"LGBM_AMD_COLUMN_COPY": "0", "LGBM_AMD_NIBBLE_BINS": "1"}},
+                              20000),
 }
 
 
@@ -210,6 +219,7 @@ def test_device_tree_state(gpu_available, case, monkeypatch):
     assert rep["device_mode"] and rep["checked"] > 0, rep
     assert rep["mismatched"] == 0, json.dumps(rep)
     expect_layout = {"mixed_width": "mixed", "mixed_width_dp": "mixed", "uniform_wide": "16", "numeric": "8",
+                     "nibble": "4", "nibble_dp": "4", "nibble_multi_block": "4", "nibble_no_column_copy": "4",
                      "sparse_rows": "sparse", "sparse_rows_efb": "sparse", "sparse_rows_dp_wide": "sparse",
                      "sparse_auto_tiles": "sparse"}
     if case in expect_layout:

@@ -589,6 +589,33 @@ def test_storage_layouts_give_identical_models(gpu_available, monkeypatch, env):
     assert base == other
 
 
+def test_four_bit_storage_gives_identical_models(gpu_available, monkeypatch):
+    """4-bit storage (every group <= 16 bins, eight to a word; reference DenseBin<uint8_t,
+    true>) against 8-bit storage of the same bins: identical models (exact integer histograms),
+    with bagging, NaN missing values and a validation set scored on the device."""
+    rng = np.random.RandomState(4)
+    n = 40000
+    X = rng.randn(n, 19)
+    X[rng.rand(n) < 0.05, 3] = np.nan
+    y = (X[:, 0] + X[:, 1] * X[:, 2] - np.nan_to_num(X[:, 3]) + 0.3 * rng.randn(n) > 0).astype(np.float32)
+    params = {"objective": "binary", "num_leaves": 63, "max_bin": 15, "verbose": -1, "device_type": "gpu",
+              "seed": 2, "bagging_fraction": 0.8, "bagging_freq": 1, "metric": "auc"}
+
+    def run():
+        ds = lgb.Dataset(X[:30000], y[:30000], params=params, free_raw_data=False)
+        va = lgb.Dataset(X[30000:], y[30000:], reference=ds)
+        ev = {}
+        bst = lgb.train(params, ds, 12, valid_sets=[va], evals_result=ev, verbose_eval=False)
+        return bst.model_to_string(), ev["valid_0"]["auc"]
+
+    monkeypatch.setenv("LGBM_AMD_NIBBLE_BINS", "0")
+    m8, auc8 = run()
+    monkeypatch.setenv("LGBM_AMD_NIBBLE_BINS", "1")
+    m4, auc4 = run()
+    assert m8 == m4
+    assert auc8 == auc4
+
+
 def _forced_trees(monkeypatch, tmp_path, forced, host, cat=None, rounds=3):
     import json as _json
     rng = np.random.RandomState(31)
