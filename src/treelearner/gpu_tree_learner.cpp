@@ -872,11 +872,17 @@ void GPUTreeLearner::DecideMode() {
   // lazy penalties (per-row usage bitsets) and distributed CEGB run host-assisted
   const bool cegb = CostEffectiveGB::Enabled(*config_);
   // forced splits: applied by the pick on one process (the static BFS schedule of the JSON
-  // tree); distributed learners run them host-assisted
+  // tree); the feature-parallel learner runs them host-assisted (the data-parallel one rejects
+  // them, as the reference does).  Per-node sampling and CEGB split / coupled penalties run
+  // device-resident under the distributed learners too: every rank draws the same node samples
+  // and holds the same CEGB state, the owners' scans apply them (LGBM_AMD_DIST_HOST_ASSIST=1:
+  // the host-assisted fallback, for A/B)
+  const char* dha = std::getenv("LGBM_AMD_DIST_HOST_ASSIST");
+  const bool dist_fallback = distributed_ && dha != nullptr && dha[0] == '1';
   if (has_forced_split_ && (distributed_ || !SetupForcedSplits())) dm = false;
   if (!has_forced_split_ && args_.forced_n > 0) SetupForcedSplits();  // (cleared)
-  if ((config_->feature_fraction_bynode < 1.0 && (data_parallel_ && Network::num_machines() > 1)) ||
-      (cegb && (!config_->cegb_penalty_feature_lazy.empty() || distributed_))) {
+  if ((config_->feature_fraction_bynode < 1.0 && dist_fallback) ||
+      (cegb && (!config_->cegb_penalty_feature_lazy.empty() || dist_fallback))) {
     dm = false;
   }
   if (cegb && dm && !args_.p.cegb) SetupCegb();

@@ -256,3 +256,27 @@ def test_multiprocess_peer_comm_data_parallel(gpu_available, tmp_path):
     from sklearn.metrics import roc_auc_score
     X, y = make_data()
     assert roc_auc_score(y, preds[0]) > 0.8
+
+
+@pytest.mark.parametrize("learner,world,mode", [("data", 2, "bynode"), ("data", 3, "bynode"), ("data", 2, "cegb"),
+                                                ("feature", 2, "bynode"), ("feature", 3, "cegb")])
+def test_distributed_modes_device_resident(learner, world, mode, gpu_available, capfd, tmp_path):
+    """Per-node column sampling and CEGB split / coupled penalties under the distributed device
+    learners grow device-resident (every rank draws the same node samples and holds the same CEGB
+    state; the owners' scans apply them): identical trees on every rank, and the serial device
+    learner's first tree (exact integer histograms: the global histograms of the shards are the
+    serial ones)."""
+    if mode == "bynode":
+        extra = {"feature_fraction_bynode": 0.6}
+    else:
+        extra = {"cegb_penalty_split": 0.5, "cegb_penalty_feature_coupled": [5, 1, 3, 0, 2, 1, 4, 0, 1, 2],
+                 "cegb_tradeoff": 0.8}
+    capfd.readouterr()
+    X, y, _, dev = _run(learner, world, rounds=5, verbose=2, **extra)
+    log = capfd.readouterr().out
+    assert "device-resident growth" in log and "host-assisted growth" not in log
+    for md, _ in dev:
+        assert _trees(md) == _trees(dev[0][0])
+    full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
+    serial = lgb.train(dict(BASE, **extra), full.subset(np.arange(N)), 1)
+    assert _splits(dev[0][0], 0) == _splits(serial.model_to_string(), 0)

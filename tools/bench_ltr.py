@@ -53,6 +53,7 @@ def main():
     ap.add_argument("--max-bin", type=int, default=63)
     ap.add_argument("--device", default="gpu")
     ap.add_argument("--test-rows", type=int, default=200_000)
+    ap.add_argument("--params", default="{}", help="extra training parameters (JSON)")
     args = ap.parse_args()
     import threading
     t_start = time.time()
@@ -70,6 +71,7 @@ def main():
     params = {"objective": "lambdarank", "boosting": "goss", "num_leaves": args.leaves, "max_bin": args.max_bin,
               "learning_rate": 0.1, "min_data_in_leaf": 1, "min_sum_hessian_in_leaf": 100,
               "device_type": args.device, "verbose": -1, "num_threads": min(16, os.cpu_count() or 8)}
+    params.update(json.loads(args.params))
     train = lgb.Dataset(X, y, group=group, params=params, free_raw_data=True)
     booster = lgb.Booster(params=params, train_set=train)
     del X
