@@ -121,6 +121,17 @@ struct KArgs {
   int8_t* cegb_used;
   FeatureBest* cegb_mem;
   uint32_t* cegb_mem_cat;
+  // CEGB lazy penalties (cegb_penalty_feature_lazy; reference cost_effective_gradient_boosting.hpp
+  // CalculateOndemandCosts / UpdateLeafBestSplits): tradeoff * penalty per inner feature, or
+  // null; a row-major bitset of the (row, feature) pairs already paid for (cegb_paid_words words
+  // per row, kept over the model); every leaf's count of unpaid rows per feature; per step
+  // parity, the histogrammed child's counts and the split leaf's snapshot (k_cegb_step)
+  const double* cegb_lazy;
+  uint32_t* cegb_paid;
+  int32_t cegb_paid_words;
+  int32_t* cegb_cnt;      // [num_leaves][num_features]
+  int32_t* cegb_scratch;  // [2][num_features]
+  int32_t* cegb_snap;     // [2][num_features]
   // forced splits (reference serial_tree_learner.cpp ForceSplits), in the static BFS order of
   // the forced-split JSON tree: node k is applied as split k (while every earlier one was valid)
   // to leaf forced_leaf[k] on inner feature forced_feat[k] at bin forced_thr[k]; the children
@@ -241,6 +252,11 @@ void Partition(const KArgs& a, hipStream_t s);
 // split scans of the root / the two children of the step (per-feature results); with
 // KArgs::pick_in_find the last workgroup also records the step and picks the next split
 void FindRoot(const KArgs& a, hipStream_t s);
+// CEGB lazy penalties (KArgs::cegb_lazy): the root's unpaid counts (cegb_cnt row 0 and both
+// scratch rows pre-zeroed by the caller); per step after the partition, the split feature paid
+// on the split leaf's rows and the histogrammed child's unpaid counts
+void CegbRoot(const KArgs& a, hipStream_t s);
+void CegbStep(const KArgs& a, hipStream_t s);
 void FindStep(const KArgs& a, hipStream_t s);
 // the step's bookkeeping and the next pick as a kernel of its own (distributed learners:
 // it runs after the per-feature results were gathered from every rank)

@@ -285,6 +285,22 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     }
   }
   if (vote_empty) return;
+  // CEGB lazy penalties: this child's unpaid-row count of f -- the root's from k_cegb_root; the
+  // histogrammed child's from k_cegb_step, the other one's as the split leaf's snapshot minus
+  // it, 0 for the split feature (its rows were just paid) -- stored per leaf by the numerical
+  // kernel (every feature has a workgroup there) for the children's own steps
+  int unpaid = 0;
+  if (a.cegb_lazy != nullptr) {
+    const int nfc = a.p.num_features;
+    if (ROOT) {
+      unpaid = a.cegb_cnt[f];
+    } else {
+      const size_t po = static_cast<size_t>(s & 1) * nfc + f;
+      const int hs = a.cegb_scratch[po];
+      unpaid = f == st->cs.split.feature ? 0 : (sd.is_hist ? hs : a.cegb_snap[po] - hs);
+      if (KIND != 2 && tid == 0) a.cegb_cnt[static_cast<size_t>(sd.leaf) * nfc + f] = unpaid;
+    }
+  }
   if (KIND == 1 && F.is_cat) return;  // the categorical kernel scans it
   if (CAT && !F.is_cat) return;       // (voting global scan: an elected numerical feature)
   // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
@@ -455,6 +471,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       }
       double delta = a.p.cegb_split * L.n;
       if (a.cegb_coupled != nullptr && !a.cegb_used[f]) delta += a.cegb_coupled[f];
+      if (a.cegb_lazy != nullptr) delta += a.cegb_lazy[f] * static_cast<double>(unpaid);
       o.gain -= delta;
     }
     if (!CAT && !SIMPLE && F.monotone != 0) o.gain *= MonotonePenalty(depth, a.p.monotone_penalty);

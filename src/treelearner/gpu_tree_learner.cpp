@@ -446,6 +446,12 @@ void GPUTreeLearner::UploadData() {
   a.cegb_used = nullptr;
   a.cegb_mem = nullptr;
   a.cegb_mem_cat = nullptr;
+  a.cegb_lazy = nullptr;
+  a.cegb_paid = nullptr;
+  a.cegb_paid_words = 0;
+  a.cegb_cnt = nullptr;
+  a.cegb_scratch = nullptr;
+  a.cegb_snap = nullptr;
   a.p.world = world_;
   a.root_local = nullptr;
   a.vote_buf = nullptr;
@@ -882,7 +888,8 @@ void GPUTreeLearner::DecideMode() {
   if (has_forced_split_ && (distributed_ || !SetupForcedSplits())) dm = false;
   if (!has_forced_split_ && args_.forced_n > 0) SetupForcedSplits();  // (cleared)
   if ((config_->feature_fraction_bynode < 1.0 && dist_fallback) ||
-      (cegb && (!config_->cegb_penalty_feature_lazy.empty() || dist_fallback))) {
+      (cegb && ((!config_->cegb_penalty_feature_lazy.empty() && (distributed_ || num_features_ > 8192)) ||
+                dist_fallback))) {
     dm = false;
   }
   if (cegb && dm && !args_.p.cegb) SetupCegb();
@@ -1194,6 +1201,7 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
                               stream_));
     }
     dev::SplitStep(a, stream_, s < a.p.direct_from_split || data_parallel_);
+    if (a.cegb_lazy != nullptr) dev::CegbStep(a, stream_);
     ReduceScatterStep(s + 1);
     dev::FindStep(a, stream_);
     if (voting_) {
@@ -1231,6 +1239,11 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   HIPCHECK(hipMemsetAsync(d_scratch_, 0, zero_bytes, stream_));
   dev::HistRoot(a, stream_);
   ReduceScatterStep(0);
+  if (a.cegb_lazy != nullptr) {
+    HIPCHECK(hipMemsetAsync(a.cegb_cnt, 0, sizeof(int32_t) * num_features_, stream_));
+    HIPCHECK(hipMemsetAsync(a.cegb_scratch, 0, sizeof(int32_t) * 2 * num_features_, stream_));
+    dev::CegbRoot(a, stream_);
+  }
   dev::FindRoot(a, stream_);
   if (a.rd != nullptr) {
     if (distributed_) GatherFeatureBests();  // (the root's results, side-0 layout)
@@ -1881,6 +1894,30 @@ void GPUTreeLearner::SetupCegb() {
   }
   args_.cegb_mem = d_cegb_mem_;
   args_.cegb_mem_cat = d_cegb_mem_cat_;
+  // lazy penalties: the rows that paid for each feature, kept over the model (the reference's
+  // per-model bitset, zeroed once), and the leaves' unpaid counts (src/device/cegb_kernels.hip)
+  args_.cegb_lazy = nullptr;
+  if (!c.cegb_penalty_feature_lazy.empty()) {
+    std::vector<double> lazy(nf, 0.0);
+    for (int f = 0; f < num_features_; ++f) {
+      lazy[f] = c.cegb_tradeoff * c.cegb_penalty_feature_lazy[data_->RealFeatureIndex(f)];
+    }
+    const int pw = (nf + 31) / 32;
+    if (d_cegb_lazy_ == nullptr) {
+      d_cegb_lazy_ = Alloc<double>(nf);
+      d_cegb_paid_ = Alloc<uint32_t>(static_cast<size_t>(num_data_) * pw);
+      HIPCHECK(hipMemset(d_cegb_paid_, 0, sizeof(uint32_t) * static_cast<size_t>(num_data_) * pw));
+      d_cegb_cnt_ = Alloc<int32_t>(static_cast<size_t>(c.num_leaves) * nf);
+      d_cegb_scratch_ = Alloc<int32_t>(4 * static_cast<size_t>(nf));
+    }
+    HIPCHECK(hipMemcpy(d_cegb_lazy_, lazy.data(), sizeof(double) * nf, hipMemcpyHostToDevice));
+    args_.cegb_lazy = d_cegb_lazy_;
+    args_.cegb_paid = d_cegb_paid_;
+    args_.cegb_paid_words = pw;
+    args_.cegb_cnt = d_cegb_cnt_;
+    args_.cegb_scratch = d_cegb_scratch_;
+    args_.cegb_snap = d_cegb_scratch_ + 2 * static_cast<size_t>(nf);
+  }
   DestroyGraph();
 }
 

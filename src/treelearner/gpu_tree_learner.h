@@ -176,6 +176,11 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   double* d_cegb_coupled_ = nullptr;
   dev::FeatureBest* d_cegb_mem_ = nullptr;
   uint32_t* d_cegb_mem_cat_ = nullptr;
+  // CEGB lazy penalties (KArgs::cegb_lazy): per-feature costs, paid bitset, unpaid counts
+  double* d_cegb_lazy_ = nullptr;
+  uint32_t* d_cegb_paid_ = nullptr;
+  int32_t* d_cegb_cnt_ = nullptr;
+  int32_t* d_cegb_scratch_ = nullptr;
   std::vector<char> h_cegb_used_;
   void* d_renew_scratch_ = nullptr;  // percentile renewal (RenewTreeOutputOnDevice)
   int64_t* d_renew_off_ = nullptr;

@@ -78,16 +78,41 @@ def test_cegb_coupled_penalty_is_paid_once():
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=["coupled", "lazy", "split"])
 def test_cegb_device_learner_matches_cpu(case, gpu_available, capfd):
-    """Split and coupled penalties are applied by the device scans (the coupled refund by the
-    device pick) in device-resident growth; lazy penalties run host-assisted.  Same trees as
-    the CPU learner either way."""
+    """Split, coupled and lazy penalties are applied by the device scans in device-resident
+    growth (the coupled refund by the device pick; lazy: the paid (row, feature) bitset and
+    every leaf's unpaid counts on the device, src/device/cegb_kernels.hip).  Same trees as the
+    CPU learner."""
     cpu = _train(case, rounds=5)
     capfd.readouterr()
     gpu = _train(dict(case, verbose=2), rounds=5, device="gpu")
     log = capfd.readouterr().out
-    lazy = "cegb_penalty_feature_lazy" in case
-    assert ("host-assisted growth" in log) == lazy and ("device-resident growth" in log) != lazy
+    assert "host-assisted growth" not in log and "device-resident growth" in log
     np.testing.assert_allclose(gpu.predict(_data()[0]), cpu.predict(_data()[0]), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bagging", [False, True])
+def test_cegb_lazy_device_matches_host_assisted(bagging, gpu_available, monkeypatch):
+    """Lazy feature penalties on a larger problem (many leaves, rows paid over many splits,
+    optionally bagging): device-resident growth grows the trees of host-assisted growth (the
+    host learner's per-row bitset and counts)."""
+    rng = np.random.RandomState(3)
+    n = 20000
+    X = rng.randn(n, 12)
+    y = (X[:, 0] + X[:, 1] * X[:, 2] - X[:, 3] + 0.5 * X[:, 4] + 0.3 * rng.randn(n) > 0).astype(np.float64)
+    p = {"objective": "binary", "num_leaves": 31, "verbose": -1, "device_type": "gpu", "seed": 1, "max_bin": 63,
+         "cegb_penalty_feature_lazy": [0.02, 0.05, 0.01, 0.03, 0.0, 0.1, 0.02, 0.04, 0.01, 0.0, 0.05, 0.02],
+         "cegb_tradeoff": 0.5}
+    if bagging:
+        p.update(bagging_fraction=0.7, bagging_freq=1)
+
+    def run():
+        return _trees(lgb.train(p, lgb.Dataset(X, y, params=p), 6).model_to_string())
+
+    dev = run()
+    monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    host = run()
+    assert dev == host
 
 
 @pytest.mark.gpu
