@@ -3,7 +3,9 @@
 // instrumented, so its barriers would read as races).
 //   1. two_round loading: the pipelined block reader thread hands blocks to the parser;
 //   2. a trainer thread adds iterations (exclusive booster lock) while three threads predict
-//      dense rows (shared lock) and one reads evaluation results.
+//      dense rows (shared lock) and one reads evaluation results;
+//   3. two boosters with row-wise CPU histograms train at once on the same Dataset (its
+//      row-major copy is built once under the Dataset's lock; each learner owns its scratch).
 // usage: tsan_driver <train file> <num features>; exit status 0 = no failed call (TSan reports
 // go to stderr and make the process exit non-zero through TSAN_OPTIONS=exitcode).
 #include <atomic>
@@ -66,7 +68,25 @@ int main(int argc, char** argv) {
   int it = 0;
   CHECK_CALL(LGBM_BoosterGetCurrentIteration(bst, &it));
   CHECK_CALL(LGBM_BoosterFree(bst));
+  // 3. two row-wise boosters on one Dataset, trained concurrently
+  BoosterHandle rw[2] = {nullptr, nullptr};
+  for (auto& b : rw) {
+    CHECK_CALL(LGBM_BoosterCreate(ds, "objective=binary num_leaves=15 num_threads=1 force_row_wise=true verbose=-1", &b));
+  }
+  std::vector<std::thread> rt;
+  for (auto& b : rw) {
+    rt.emplace_back([&b] {
+      int f = 0;
+      for (int i = 0; i < 5; ++i) CHECK_CALL(LGBM_BoosterUpdateOneIter(b, &f));
+    });
+  }
+  for (auto& t : rt) t.join();
+  int it2[2] = {0, 0};
+  for (int k = 0; k < 2; ++k) {
+    CHECK_CALL(LGBM_BoosterGetCurrentIteration(rw[k], &it2[k]));
+    CHECK_CALL(LGBM_BoosterFree(rw[k]));
+  }
   CHECK_CALL(LGBM_DatasetFree(ds));
-  std::printf("tsan driver ok: %d iterations\n", it);
-  return it == 15 ? 0 : 3;
+  std::printf("tsan driver ok: %d iterations, row-wise boosters %d / %d\n", it, it2[0], it2[1]);
+  return (it == 15 && it2[0] == 5 && it2[1] == 5) ? 0 : 3;
 }
