@@ -1033,6 +1033,12 @@ __device__ __forceinline__ void WaveLdsSync() {  // lane 0's LDS stores before t
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+#ifndef LGBM_REPLAY_KEY32
+#define LGBM_REPLAY_KEY32 1
+#endif
+#ifndef LGBM_REPLAY_PREFETCH
+#define LGBM_REPLAY_PREFETCH 0  // (A/B: children loaded ahead -- 2.356 vs 2.343 ms/iter, not kept)
+#endif
 // Replay + prediction with one leaf per lane in registers (num_leaves <= 64, wave 0): a step
 // is one 64-bit DPP max over the gain keys (the tie key's max only when gains tie exactly),
 // reads of the winner's lane, and LDS reads of the node tables by the two lanes whose leaf
@@ -1041,21 +1047,86 @@ __device__ __forceinline__ void WaveLdsSync() {  // lane 0's LDS stores before t
 struct RegLeaf {
   double g;
   int rf, node, ch;
+  uint32_t k32;  // GainKey32(g): the argmax's first, 32-bit pass
+#if LGBM_REPLAY_PREFETCH
+  // the node's children (ch >= 0), loaded ahead: gain, real feature, first child of each
+  double g0, g1;
+  int rf0, rf1, ch0, ch1;
+#endif
 };
+// order-preserving 32-bit key of a gain (NaN = -inf): the gain rounded to float, whose
+// rounding is monotone -- a larger float key means a larger gain; equal float keys are
+// resolved by the exact 64-bit keys
+__device__ __forceinline__ uint32_t GainKey32(double g) {
+  if (g != g) g = -INFINITY;
+  const uint32_t b = __float_as_uint(static_cast<float>(g));
+  return (b >> 31) ? ~b : (b | 0x80000000u);
+}
 __device__ __forceinline__ int RegArgmax(const RegLeaf& x, bool live) {
   const int lane = threadIdx.x & 63;
-  const unsigned long long gk = live ? GainKey(x.g) : 0ull;
+  // one 32-bit DPP max; the exact 64-bit / tie passes only when the float keys tie
+#if LGBM_REPLAY_KEY32
+  const uint32_t k = live ? x.k32 : 0u;
+#else
+  const uint32_t k = live ? 1u : 0u;  // (A/B: every live lane into the 64-bit pass)
+#endif
+  const uint32_t km = WaveMaxDpp(k);
+  const unsigned long long t32 = __ballot(live && k == km);
+  if (__popcll(t32) == 1) return __builtin_amdgcn_readfirstlane(static_cast<int>(__builtin_ctzll(t32)));
+  const bool in = live && k == km;
+  const unsigned long long gk = in ? GainKey(x.g) : 0ull;
   const unsigned long long gm = WaveMaxDpp(gk);
-  const unsigned long long tied = __ballot(gk == gm);
+  const unsigned long long tied = __ballot(in && gk == gm);
   if (__popcll(tied) == 1) return __builtin_amdgcn_readfirstlane(static_cast<int>(__builtin_ctzll(tied)));
-  const uint32_t tm = WaveMaxDpp(gk == gm ? TieKey(x.rf, lane) : 0u);
+  const uint32_t tm = WaveMaxDpp((in && gk == gm) ? TieKey(x.rf, lane) : 0u);
   return static_cast<int>((~tm) & 1023u);
 }
+#if LGBM_REPLAY_PREFETCH
+// the children of the lane's node, loaded now and used only when the lane next wins: the
+// winner's children come from its registers (readlane) instead of an LDS round trip that the
+// next argmax would wait for
+__device__ __forceinline__ void RegPrefetch(RegLeaf* x, const double* ng, const int* nrf, const int* nch) {
+  const int c = x->ch;
+  x->g0 = c >= 0 ? ng[c] : -INFINITY;
+  x->rf0 = c >= 0 ? nrf[c] : -1;
+  x->ch0 = c >= 0 ? nch[c] : -1;
+  x->g1 = c >= 0 ? ng[c + 1] : -INFINITY;
+  x->rf1 = c >= 0 ? nrf[c + 1] : -1;
+  x->ch1 = c >= 0 ? nch[c + 1] : -1;
+}
+__device__ __forceinline__ void RegSet(RegLeaf* x, int node, double g, int rf, int ch, const double* ng, const int* nrf,
+                                       const int* nch) {
+  x->node = node;
+  x->g = g;
+  x->k32 = GainKey32(g);
+  x->rf = rf;
+  x->ch = ch;
+  RegPrefetch(x, ng, nrf, nch);
+}
+#endif
 __device__ __forceinline__ void RegLoad(RegLeaf* x, int node, const double* ng, const int* nrf, const int* nch) {
   x->node = node;
   x->g = node >= 0 ? ng[node] : -INFINITY;
+  x->k32 = GainKey32(x->g);
   x->rf = node >= 0 ? nrf[node] : -1;
   x->ch = node >= 0 ? nch[node] : -1;
+#if LGBM_REPLAY_PREFETCH
+  RegPrefetch(x, ng, nrf, nch);
+#endif
+}
+// lanes w and nl take the children of lane w's node (c, c + 1)
+__device__ __forceinline__ void RegTakeChildren(RegLeaf* x, int lane, int w, int nl, int c, const double* ng,
+                                                const int* nrf, const int* nch) {
+#if LGBM_REPLAY_PREFETCH
+  const double g0 = ReadLane(x->g0, w), g1 = ReadLane(x->g1, w);
+  const int rf0 = ReadLane(x->rf0, w), rf1 = ReadLane(x->rf1, w);
+  const int ch0 = ReadLane(x->ch0, w), ch1 = ReadLane(x->ch1, w);
+  if (lane == w) RegSet(x, c, g0, rf0, ch0, ng, nrf, nch);
+  if (lane == nl) RegSet(x, c + 1, g1, rf1, ch1, ng, nrf, nch);
+#else
+  if (lane == w) RegLoad(x, c, ng, nrf, nch);
+  if (lane == nl) RegLoad(x, c + 1, ng, nrf, nch);
+#endif
 }
 // returns s (splits after the replay); *done, *npick; acc / accn / s_pick / tnode as the LDS path
 __device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, const double* ng, const int* nrf,
@@ -1082,8 +1153,7 @@ __device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, const 
       acc[s - s0] = w;
       accn[s - s0] = ReadLane(x.node, w);
     }
-    if (lane == w) RegLoad(&x, c, ng, nrf, nch);
-    if (lane == nl) RegLoad(&x, c + 1, ng, nrf, nch);
+    RegTakeChildren(&x, lane, w, nl, c, ng, nrf, nch);
     ++s;
   }
   if (lane <= s) tnode[lane] = x.node;
@@ -1102,8 +1172,7 @@ __device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, const 
       const int c = ReadLane(x.ch, w), v = ReadLane(vd, w);
       const int nl = ss + 1;
       if (c >= 0) {
-        if (lane == w) RegLoad(&x, c, ng, nrf, nch);
-        if (lane == nl) RegLoad(&x, c + 1, ng, nrf, nch);
+        RegTakeChildren(&x, lane, w, nl, c, ng, nrf, nch);
         if (lane == w || lane == nl) vd = v + 1;
       } else {
         if (v <= vmax) {
