@@ -70,6 +70,9 @@ struct Params {
   // loses cegb_split * rows_in_leaf + KArgs::cegb_coupled[f] while f is unused by the model
   int32_t cegb;
   double cegb_split;
+  // intermediate monotone constraints (KArgs::mt_*): a split re-bounds leaves across the tree,
+  // which the next split scan re-scans
+  int32_t mono_inter;
 };
 
 // per-leaf state

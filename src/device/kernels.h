@@ -132,6 +132,15 @@ struct KArgs {
   int32_t* cegb_cnt;      // [num_leaves][num_features]
   int32_t* cegb_scratch;  // [2][num_features]
   int32_t* cegb_snap;     // [2][num_features]
+  // intermediate monotone constraints (Params::mono_inter; reference monotone_constraints.hpp
+  // IntermediateLeafConstraints, host src/treelearner/monotone_constraints.cpp): the tree's
+  // topology as the picks grow it, each leaf's membership of a monotone subtree, and the leaves
+  // the last split re-bounded (mt_upd[0] of them, then their ids), which the next split scan
+  // re-scans as sides 2.. (feat_best rows 2..) and the next pick folds into KArgs::best
+  int32_t* mt_leaf_parent;  // [num_leaves] internal node above each leaf (-1: the root leaf)
+  int32_t* mt_node;         // [num_leaves - 1][3] parent, left, right (child >= 0 node, else ~leaf)
+  int8_t* mt_in_sub;        // [num_leaves]
+  int32_t* mt_upd;          // [1 + num_leaves]
   // forced splits (reference serial_tree_learner.cpp ForceSplits), in the static BFS order of
   // the forced-split JSON tree: node k is applied as split k (while every earlier one was valid)
   // to leaf forced_leaf[k] on inner feature forced_feat[k] at bin forced_thr[k]; the children
@@ -256,6 +265,12 @@ void FindRoot(const KArgs& a, hipStream_t s);
 // scratch rows pre-zeroed by the caller); per step after the partition, the split feature paid
 // on the split leaf's rows and the histogrammed child's unpaid counts
 void CegbRoot(const KArgs& a, hipStream_t s);
+// LDS of the picking workgroup's intermediate-monotone tree walk (pick.h MonoInterUpdate); the
+// device path takes num_leaves <= kMonoInterMaxLeaves
+constexpr int kMonoInterMaxLeaves = 512;
+inline size_t MonoInterLds(int num_leaves) {
+  return static_cast<size_t>(num_leaves + 1) * (20 * sizeof(int32_t) + 2 * sizeof(double));
+}
 void CegbStep(const KArgs& a, hipStream_t s);
 void FindStep(const KArgs& a, hipStream_t s);
 // the step's bookkeeping and the next pick as a kernel of its own (distributed learners:

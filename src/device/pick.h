@@ -365,6 +365,262 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
   }
 }
 
+// ---- intermediate monotone constraints (Params::mono_inter) --------------------------------
+// The leaves the previous split re-bounded were re-scanned as sides 2.. of this step's split
+// scans: their best splits (per-feature results, SplitInfo order) replace KArgs::best before
+// the pick (SerialTreeLearner::RecomputeBestSplitForLeaf).  Every wave takes whole leaves.
+__device__ void MonoInterFold(const KArgs& a) {
+  const int n = a.mt_upd[0];
+  const int nf = a.p.num_features, lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int k = w; k < n; k += nw) {
+    const int u = a.mt_upd[1 + k];
+    ArgC c = ArgNone();
+    for (int f = lane; f < nf; f += kWave) {
+      const FeatureBest& fb = a.feat_best[FeatBestIndex(a, 2 + k, f)];
+      if (fb.feature >= 0 && (c.idx < 0 || SplitBetter(fb.gain, fb.real_feature, c.g, c.rf))) {
+        c.g = fb.gain;
+        c.rf = fb.real_feature;
+        c.idx = f;
+      }
+    }
+#pragma unroll 1
+    for (int o = 32; o > 0; o >>= 1) ArgTake(&c, ArgShflXor(c, o));
+    if (lane == 0) {
+      if (c.idx >= 0 && c.g != -INFINITY) {
+        ToDeviceSplit(a.feat_best[FeatBestIndex(a, 2 + k, c.idx)], FeatCat(a, 2 + k, c.idx), &a.best[u]);
+      } else {
+        NoSplit(&a.best[u]);
+      }
+    }
+  }
+}
+
+// After the pick of split s (leaf -> leaf, s + 1): the reference's intermediate method
+// (monotone_constraints.hpp IntermediateLeafConstraints; host LeafConstraints::BeforeSplit /
+// Update / GoUp / GoDown) on the tree so far, walked by one thread in LDS: the children bound
+// each other by their outputs (inside a monotone subtree), and at every monotone ancestor the
+// leaves of the other subtree that can touch the new leaves are re-bounded by the new outputs;
+// those whose bound changed are re-scanned by the next split scan.  Leaves that will not split
+// (best gain -inf) keep their bounds.
+__device__ void MonoInterUpdate(const KArgs& a, PickLds* pl, unsigned char* lds_raw) {
+  PickResult* pk = &pl->pk;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int L = a.p.num_leaves, s = pk->s, leaf = pk->leaf, nl = s + 1;
+  int* lpar = reinterpret_cast<int*>(lds_raw);
+  int* npar = lpar + L;
+  int* nlc = npar + L;
+  int* nrc = nlc + L;
+  int* nfeat = nrc + L;
+  int* nthv = nfeat + L;
+  int* nnum = nthv + L;
+  int* nmono = nnum + L;
+  int* insub = nmono + L;
+  int* dead = insub + L;
+  int* pf = dead + L;
+  int* pt = pf + L;
+  int* pr = pt + L;
+  int* seen = pr + L;
+  int* stale = seen + L;      // [L + 1]: count, then leaves
+  int* stk = stale + L + 1;   // [3 L]
+  double* cmn = reinterpret_cast<double*>(lds_raw + ((static_cast<size_t>(19 * L + 1) * sizeof(int) + 7) & ~size_t(7)));
+  double* cmx = cmn + L;
+  // the tree so far (nodes 0..s-1, leaves 0..s), in LDS
+  for (int i = tid; i <= s; i += nthr) {
+    lpar[i] = a.mt_leaf_parent[i];
+    insub[i] = a.mt_in_sub[i];
+    dead[i] = a.best[i].gain == -INFINITY ? 1 : 0;
+    cmn[i] = a.leaves[i].cmin;
+    cmx[i] = a.leaves[i].cmax;
+    seen[i] = 0;
+    if (i < s) {
+      npar[i] = a.mt_node[3 * i];
+      nlc[i] = a.mt_node[3 * i + 1];
+      nrc[i] = a.mt_node[3 * i + 2];
+      const DeviceSplit& r = a.rec[i].split;
+      nfeat[i] = r.feature;
+      nthv[i] = r.threshold;
+      nnum[i] = r.is_categorical ? 0 : 1;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < s; i += nthr) nmono[i] = a.feat[nfeat[i]].monotone;
+  // (the previous step's fresh children: their bests are in pl->fsplit until step 5 stores them)
+  if (tid == 0) {
+    if (pl->fresh >= 1 && pl->sm >= 0) dead[pl->sm] = pl->fsplit[0].gain == -INFINITY ? 1 : 0;
+    if (pl->fresh == 2 && pl->lg >= 0) dead[pl->lg] = pl->fsplit[1].gain == -INFINITY ? 1 : 0;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const DeviceSplit& sp = pk->split;
+    const int mono = sp.monotone_type;
+    const bool numerical = !sp.is_categorical;
+    // BeforeSplit, then Tree::Split
+    if (mono != 0 || insub[leaf]) {
+      insub[leaf] = 1;
+      insub[nl] = 1;
+    } else {
+      insub[nl] = 0;
+    }
+    const int parent = lpar[leaf];
+    npar[s] = parent;
+    if (parent >= 0) {
+      if (nlc[parent] == ~leaf) nlc[parent] = s;
+      else nrc[parent] = s;
+    }
+    nlc[s] = ~leaf;
+    nrc[s] = ~nl;
+    lpar[leaf] = s;
+    lpar[nl] = s;
+    nfeat[s] = sp.feature;
+    nthv[s] = sp.threshold;
+    nnum[s] = numerical ? 1 : 0;
+    nmono[s] = pk->F.monotone;
+    int nst = 0;
+    double lmin = cmn[leaf], lmax = cmx[leaf], rmin = -DBL_MAX, rmax = DBL_MAX;
+    if (insub[leaf]) {
+      rmin = lmin;
+      rmax = lmax;
+      if (numerical) {
+        if (mono < 0) {
+          lmin = fmax(lmin, sp.right_output);
+          rmax = fmin(rmax, sp.left_output);
+        } else if (mono > 0) {
+          lmax = fmin(lmax, sp.right_output);
+          rmin = fmax(rmin, sp.left_output);
+        }
+      }
+      const double lo_out = sp.left_output, ro_out = sp.right_output;
+      const uint32_t sthr = static_cast<uint32_t>(sp.threshold);
+      const int sinner = sp.feature;
+      // GoUp from the new node
+      int node = s, plen = 0;
+      for (;;) {
+        const int par = npar[node];
+        if (par < 0) break;
+        const int inner = nfeat[par], pmono = nmono[par];
+        const int from_right = nrc[par] == node ? 1 : 0;
+        bool relevant = true;
+        if (nnum[node]) {
+          for (int i = 0; i < plen; ++i) {
+            if (pf[i] == inner && pr[i] == from_right) {
+              relevant = false;
+              break;
+            }
+          }
+        }
+        if (relevant) {
+          if (pmono != 0) {
+            const bool node_is_left = nlc[par] == node;
+            const bool update_max = pmono < 0 ? node_is_left : !node_is_left;
+            // GoDown over the other subtree (explicit stack: node, use_left, use_right)
+            int top = 0;
+            stk[0] = node_is_left ? nrc[par] : nlc[par];
+            stk[1] = 1;
+            stk[2] = 1;
+            top = 1;
+            while (top > 0) {
+              --top;
+              const int nd = stk[3 * top], ul = stk[3 * top + 1], ur = stk[3 * top + 2];
+              if (nd < 0) {
+                const int lf = ~nd;
+                if (dead[lf]) continue;
+                double lo, hi;
+                if (ul && ur) {
+                  lo = fmin(ro_out, lo_out);
+                  hi = fmax(ro_out, lo_out);
+                } else if (ur) {
+                  lo = hi = ro_out;
+                } else {
+                  lo = hi = lo_out;
+                }
+                bool changed = false;
+                if (!update_max) {
+                  if (hi > cmn[lf]) {
+                    cmn[lf] = hi;
+                    changed = true;
+                  }
+                } else if (lo < cmx[lf]) {
+                  cmx[lf] = lo;
+                  changed = true;
+                }
+                if (changed && !seen[lf]) {
+                  seen[lf] = 1;
+                  stale[1 + nst++] = lf;
+                }
+                continue;
+              }
+              const int inn = nfeat[nd];
+              const uint32_t thr = static_cast<uint32_t>(nthv[nd]);
+              const bool num = nnum[nd] != 0;
+              bool go_left = true, go_right = true;
+              if (num) {
+                for (int i = 0; i < plen && (go_left || go_right); ++i) {
+                  if (pf[i] != inn) continue;
+                  if (thr >= static_cast<uint32_t>(pt[i]) && !pr[i]) go_right = false;
+                  if (thr <= static_cast<uint32_t>(pt[i]) && pr[i]) go_left = false;
+                }
+              }
+              bool left_for_right = true, right_for_left = true;
+              if (num && inn == sinner) {
+                if (thr >= sthr) left_for_right = false;
+                if (thr <= sthr) right_for_left = false;
+              }
+              // (the reference recurses left, then right: pushed in reverse)
+              if (go_right) {
+                stk[3 * top] = nrc[nd];
+                stk[3 * top + 1] = (left_for_right && ul) ? 1 : 0;
+                stk[3 * top + 2] = ur;
+                ++top;
+              }
+              if (go_left) {
+                stk[3 * top] = nlc[nd];
+                stk[3 * top + 1] = ul;
+                stk[3 * top + 2] = (right_for_left && ur) ? 1 : 0;
+                ++top;
+              }
+            }
+          }
+          pf[plen] = inner;
+          pt[plen] = nthv[par];
+          pr[plen] = from_right;
+          ++plen;
+        }
+        node = par;
+      }
+    }
+    pl->lc.cmin = lmin;
+    pl->lc.cmax = lmax;
+    pl->rc.cmin = rmin;
+    pl->rc.cmax = rmax;
+    stale[0] = nst;
+  }
+  __syncthreads();
+  // stores: the re-bounded leaves and their list, the grown topology
+  const int nst = stale[0];
+  for (int k = tid; k < nst; k += nthr) {
+    const int u = stale[1 + k];
+    a.leaves[u].cmin = cmn[u];
+    a.leaves[u].cmax = cmx[u];
+    a.mt_upd[1 + k] = u;
+  }
+  if (tid == 0) {
+    a.mt_upd[0] = nst;
+    a.mt_leaf_parent[leaf] = s;
+    a.mt_leaf_parent[nl] = s;
+    a.mt_in_sub[leaf] = static_cast<int8_t>(insub[leaf]);
+    a.mt_in_sub[nl] = static_cast<int8_t>(insub[nl]);
+    a.mt_node[3 * s] = npar[s];
+    a.mt_node[3 * s + 1] = nlc[s];
+    a.mt_node[3 * s + 2] = nrc[s];
+    const int parent = npar[s];
+    if (parent >= 0) {
+      a.mt_node[3 * parent + 1] = nlc[parent];
+      a.mt_node[3 * parent + 2] = nrc[parent];
+    }
+  }
+  __syncthreads();
+}
+
 // in-kernel stamp of the picking workgroup (LGBM_AMD_KTRACE)
 __device__ __forceinline__ void PickTrace(const KArgs& a, int s, int slot) {
   if (a.ktrace != nullptr && threadIdx.x == 0 && s >= 0 && s < a.p.num_leaves) {
@@ -373,7 +629,8 @@ __device__ __forceinline__ void PickTrace(const KArgs& a, int s, int slot) {
   }
 }
 
-__device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool root, PickLds* pl, int ts = -1) {
+__device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool root, PickLds* pl, int ts = -1,
+                                              unsigned char* mono_lds = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, nthr = blockDim.x;
   PickResult* pk = &pl->pk;
   // 1. bookkeeping, by a thread outside the picking wave (its stores do not hold up the
@@ -391,6 +648,11 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     StepBookkeeping(a, st, pl);
   }
   __syncthreads();
+  // intermediate monotone: the re-scanned leaves' new bests join the per-leaf table first
+  if (a.p.mono_inter && !root) {
+    MonoInterFold(a);
+    __syncthreads();
+  }
   PickTrace(a, ts, kTrPick1);
   if (a.ktrace != nullptr && tid == 0 && ts >= 0 && ts < a.p.num_leaves) a.ktrace[ts * kTraceSlots + kTrClk0] = __builtin_amdgcn_s_memtime();
   // 2. the pick
@@ -484,6 +746,7 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
       rc.frow = -1;  // the new leaf's row (below)
     }
     __syncthreads();
+    if (a.p.mono_inter && mono_lds != nullptr && !pk->forced) MonoInterUpdate(a, pl, mono_lds);
     PickTrace(a, ts, kTrPick4);
     // 5. loads that depend on the winner: the new leaf's splittable row id, the constraint
     //    mask of the split feature (the parent's splittable row is snapshot by k_split)

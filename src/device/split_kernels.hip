@@ -169,17 +169,50 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   const Feature F = a.feat[f];
   const int8_t tree_used = a.tree_mask[f];
   const Step* st = a.st;
+  // intermediate monotone constraints: sides 2.. re-scan the leaves the last split re-bounded
+  // (SerialTreeLearner::RecomputeBestSplitForLeaf: the leaf's histogram, the sums and count of
+  // its current best split, parent output 0, every feature of the tree it could split on; no
+  // node sampling, flags untouched).  An unused slot only counts its arrival.
+  const bool rescan = !ROOT && side >= 2;
+  int rleaf = -1;
+  if (rescan) {
+    if (side - 2 >= a.mt_upd[0]) return;
+    rleaf = a.mt_upd[side - 1];
+  }
   const int mi_base = ROOT ? 0 : st->bynode_next;  // this step's per-node masks (advanced by the pick)
   int8_t used = tree_used;  // evaluated at this node (feature_fraction_bynode)
-  if (a.node_mask != nullptr) used = used && a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f];
+  if (a.node_mask != nullptr && !rescan) used = used && a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f];
   // (voting: every feature is scanned -- the vote may elect one this rank could not split)
-  const int8_t parent_ok = (ROOT || a.p.vote_phase != 0) ? 1 : a.parent_flags[f];
+  const int8_t parent_ok = (ROOT || a.p.vote_phase != 0) ? 1
+                           : rescan ? a.splittable[static_cast<size_t>(a.leaves[rleaf].frow) * a.p.num_features + f]
+                                    : a.parent_flags[f];
   const double ig = a.scales[2], ih = a.scales[3];
   int s = 0, pc = 0, skip = 0;
   ChildInfo c;
   SideInfo sd;
   ChildStats cl;
-  if (!ROOT) {
+  DeviceSplit rbest;
+  if (rescan) {
+    s = st->cs.s;
+    const Leaf& lf = a.leaves[rleaf];
+    rbest = a.best[rleaf];
+    sd.lr = 0;
+    sd.leaf = rleaf;
+    sd.slot = lf.slot;
+    sd.frow = lf.frow;
+    sd.is_hist = 1;
+    sd.global_count = rbest.left_count + rbest.right_count;
+    cl.sum_g = rbest.left_sum_gradient + rbest.right_sum_gradient;
+    cl.sum_h = rbest.left_sum_hessian + rbest.right_sum_hessian;
+    cl.output = 0.0;
+    cl.cmin = lf.cmin;
+    cl.cmax = lf.cmax;
+    cl.depth = lf.depth;
+    cl.slot = lf.slot;
+    cl.leaf = rleaf;
+    cl.frow = lf.frow;
+    cl.icmask = kIcAll;
+  } else if (!ROOT) {
     s = st->cs.s;
     pc = st->cs.part_count;
     c = StepChildren(a, st);
@@ -220,7 +253,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     KTraceAt(a, s, kTrFindEntry, t_entry);
     KTrace(a, s, kTrFindHdr);
     const int nblk = StepBlocks(a, pc);
-    if (DirectPartials(a, nblk, s) && !vote_global) nblk_direct = nblk;
+    if (DirectPartials(a, nblk, s) && !vote_global && !rescan) nblk_direct = nblk;
   }
   const SplitParams& p = a.p.sp;
   LeafCtx L;
@@ -294,6 +327,8 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     const int nfc = a.p.num_features;
     if (ROOT) {
       unpaid = a.cegb_cnt[f];
+    } else if (rescan) {
+      unpaid = a.cegb_cnt[static_cast<size_t>(rleaf) * nfc + f];
     } else {
       const size_t po = static_cast<size_t>(s & 1) * nfc + f;
       const int hs = a.cegb_scratch[po];
@@ -342,7 +377,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     long long* dst = vote_global ? a.vote_hist + static_cast<size_t>(side * a.p.vote_k + blockIdx.x) * 2 *
                                                      a.p.max_feature_bins
                                  : a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
-    const long long* src = vote_global ? dst
+    const long long* src = (vote_global || rescan) ? dst
                            : a.owned_hist != nullptr ? a.owned_hist + 2 * (F.hist_offset - a.owned_bin_lo)
                                                      : StepScratch(a, parity) + 2 * F.hist_offset;
     const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
@@ -456,7 +491,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc, sh.sc2,
                                               xt_thr);
     }
-    if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (the local scan's flags stay)
+    if (tid == 0 && !vote_global && !rescan) flags[f] = splittable ? 1 : 0;  // (the local scan's flags stay)
     // SerialTreeLearner::EvalFeature order: the CEGB cost (the raw candidate remembered for the
     // coupled-penalty refund), then the monotone depth penalty
     if (a.p.cegb && tid == 0) {
@@ -477,7 +512,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     if (!CAT && !SIMPLE && F.monotone != 0) o.gain *= MonotonePenalty(depth, a.p.monotone_penalty);
     // a forced node on this child and feature: its split at the forced threshold (published
     // for the pick, which applies it as split k)
-    if (a.forced_n > 0 && tid == 0 && !vote_global) {
+    if (a.forced_n > 0 && tid == 0 && !vote_global && !rescan) {
       const int k = ROOT ? 0 : (s < a.forced_n ? a.forced_child[2 * s + sd.lr] : -1);
       if (k >= 0 && k < a.forced_n && a.forced_feat[k] == f) {
         FeatureBest fo;
@@ -554,7 +589,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   if (!ROOT && a.ktrace != nullptr && threadIdx.x == 0 && s < a.p.num_leaves) {
     a.ktrace[s * kTraceSlots + kTrPickEntry] = wall_clock64();
   }
-  PickAndRecord(a, st, ROOT, &pl, s);
+  PickAndRecord(a, st, ROOT, &pl, s, reinterpret_cast<unsigned char*>(s_bins));
   if (!ROOT && a.ktrace != nullptr && threadIdx.x == 0 && s < a.p.num_leaves) {
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     a.ktrace[s * kTraceSlots + kTrPickExit] = wall_clock64();
@@ -571,7 +606,9 @@ __global__ __launch_bounds__(kFindThreads) void k_pick(KArgs a, int root) {
 }
 
 static size_t FindLds(const KArgs& a) {
-  return a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
+  const size_t bins = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
+  // intermediate monotone: the picking workgroup walks the tree in this LDS (MonoInterLds)
+  return a.p.mono_inter ? std::max(bins, MonoInterLds(a.p.num_leaves)) : bins;
 }
 // plain gain formulas (no L1 / max_delta_step / path smoothing / monotone constraints)
 static bool SimpleGains(const KArgs& a) {
@@ -581,7 +618,9 @@ static bool SimpleGains(const KArgs& a) {
 template <bool ROOT>
 static void LaunchFind(const KArgs& a, hipStream_t s) {
   if (a.num_scan <= 0) return;  // a rank that owns no feature
-  const dim3 g(a.num_scan, ROOT ? 1 : 2);
+  // (intermediate monotone: sides 2.. re-scan up to num_leaves re-bounded leaves)
+  const int sides = ROOT ? 1 : (a.p.mono_inter ? 2 + a.p.num_leaves : 2);
+  const dim3 g(a.num_scan, sides);
   const size_t lds = FindLds(a);
   const bool simple = SimpleGains(a);
   const bool narrow = a.p.max_feature_bins <= kWave;  // (categorical scans keep kFindThreads)
@@ -595,7 +634,7 @@ static void LaunchFind(const KArgs& a, hipStream_t s) {
       else hipLaunchKernelGGL((k_find<ROOT, 1, false, kFindThreads>), g, b, lds, s, a);
     }
     const int ncat = a.p.vote_phase == 2 ? a.num_scan : a.p.has_cat;  // voting: every elected slot
-    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false, kFindThreads>), dim3(ncat, ROOT ? 1 : 2), bc, lds, s, a);
+    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false, kFindThreads>), dim3(ncat, sides), bc, lds, s, a);
   } else if (narrow) {
     if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true, kWave>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_find<ROOT, 0, false, kWave>), g, b, lds, s, a);

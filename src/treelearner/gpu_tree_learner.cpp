@@ -375,6 +375,7 @@ void GPUTreeLearner::UploadData() {
                                            2 * static_cast<size_t>(world_) * round_k_ * std::max(1, max_owned_));
   d_feat_best_ = Alloc<dev::FeatureBest>(fb_slots);
   d_feat_cat_ = Alloc<uint32_t>(fb_slots * kMaxCatWords);
+  fb_slots_ = fb_slots;
   // row blocks: the root histogram runs on two workgroups per CU, a split step on one; a
   // packed (hist_units 1) row block holds at most kHistRowsCap rows, so the fixed-point
   // scale does not depend on the number of rows; wide blocks are unbounded
@@ -446,6 +447,11 @@ void GPUTreeLearner::UploadData() {
   a.cegb_used = nullptr;
   a.cegb_mem = nullptr;
   a.cegb_mem_cat = nullptr;
+  a.p.mono_inter = 0;
+  a.mt_leaf_parent = nullptr;
+  a.mt_node = nullptr;
+  a.mt_in_sub = nullptr;
+  a.mt_upd = nullptr;
   a.cegb_lazy = nullptr;
   a.cegb_paid = nullptr;
   a.cegb_paid_words = 0;
@@ -805,6 +811,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
   DestroyGraph();  // kernel arguments are baked into the captured graph
   args_.p.sp = params_;
   args_.p.cegb = 0;  // re-derived from the new penalties by the next DecideMode
+  args_.p.mono_inter = 0;
   args_.p.max_depth = config_->max_depth;
   args_.p.monotone_penalty = config_->monotone_penalty;
   if (config_->num_leaves != old_leaves) {
@@ -865,11 +872,15 @@ void GPUTreeLearner::DecideMode() {
   // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
   const auto& ic = config_->interaction_constraints_vector;
   if (!ic.empty() && (ic.size() > static_cast<size_t>(dev::kMaxIcConstraints) || config_->feature_fraction_bynode < 1.0)) dm = false;
-  // intermediate monotone constraints re-bound (and re-scan) leaves all over the tree after a
-  // split: the host loop does that between the device histogram builds
-  if (config_->monotone_constraints_method == "intermediate" &&
-      std::any_of(config_->monotone_constraints.begin(), config_->monotone_constraints.end(),
-                  [](int8_t m) { return m != 0; })) {
+  // intermediate monotone constraints re-bound leaves all over the tree after a split: the pick
+  // walks the tree and the next split scan re-scans the re-bounded leaves (one process, one
+  // split per step; with extra_trees draws, forced splits or more than kMonoInterMaxLeaves
+  // leaves the host loop does it between the device histogram builds)
+  const bool mono_inter = config_->monotone_constraints_method == "intermediate" &&
+                          std::any_of(config_->monotone_constraints.begin(), config_->monotone_constraints.end(),
+                                      [](int8_t m) { return m != 0; });
+  if (mono_inter && (distributed_ || config_->extra_trees || has_forced_split_ ||
+                     config_->num_leaves > dev::kMonoInterMaxLeaves)) {
     dm = false;
   }
   // voting: per-node sampling and extra_trees draws stay with the host voting loop
@@ -893,6 +904,11 @@ void GPUTreeLearner::DecideMode() {
     dm = false;
   }
   if (cegb && dm && !args_.p.cegb) SetupCegb();
+  if (mono_inter && dm && !args_.p.mono_inter) SetupMonoInter();
+  if (!(mono_inter && dm) && args_.p.mono_inter) {
+    args_.p.mono_inter = 0;
+    DestroyGraph();
+  }
   if (dm != device_mode_ || !mode_decided_) {
     mode_decided_ = true;
     Log::Debug("device learner: %s growth", dm ? "device-resident" : "host-assisted");
@@ -1231,6 +1247,12 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
     HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
   }
   dev::TreeBegin(a, stream_);
+  if (a.p.mono_inter) {  // (intermediate monotone: the root leaf has no parent, nothing is re-bounded yet)
+    const int L = config_->num_leaves;
+    HIPCHECK(hipMemsetAsync(a.mt_leaf_parent, 0xff, sizeof(int32_t) * L, stream_));
+    HIPCHECK(hipMemsetAsync(a.mt_in_sub, 0, L, stream_));
+    HIPCHECK(hipMemsetAsync(a.mt_upd, 0, sizeof(int32_t), stream_));
+  }
   if (a.xt_cum != nullptr) {
     HIPCHECK(hipMemsetAsync(a.xt_cum, 0, sizeof(int32_t) * config_->num_leaves * num_features_, stream_));
   }
@@ -1295,7 +1317,7 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
   // the split order depends on more than each leaf's own rows: per-node feature samples and
   // extra_trees draws are consumed in the sequential order, CEGB's coupled penalties change
   // other leaves' gains, forced splits follow their own schedule
-  if (a.node_mask != nullptr || a.xt_base != nullptr || a.p.cegb || a.forced_n > 0) return false;
+  if (a.node_mask != nullptr || a.xt_base != nullptr || a.p.cegb || a.forced_n > 0 || a.p.mono_inter) return false;
   return true;
 }
 
@@ -1918,6 +1940,33 @@ void GPUTreeLearner::SetupCegb() {
     args_.cegb_scratch = d_cegb_scratch_;
     args_.cegb_snap = d_cegb_scratch_ + 2 * static_cast<size_t>(nf);
   }
+  DestroyGraph();
+}
+
+// intermediate monotone constraints on the device: per-feature result rows for the re-scanned
+// leaves (sides 2 .. num_leaves + 1), the tree topology and the re-bounded leaf list
+void GPUTreeLearner::SetupMonoInter() {
+  const int L = config_->num_leaves, nf = std::max(1, num_features_);
+  const size_t need = static_cast<size_t>(2 + L) * nf;
+  if (fb_slots_ < need) {
+    d_feat_best_ = Alloc<dev::FeatureBest>(need);
+    d_feat_cat_ = Alloc<uint32_t>(need * kMaxCatWords);
+    fb_slots_ = need;
+    args_.feat_best = d_feat_best_;
+    args_.feat_cat = d_feat_cat_;
+  }
+  if (mt_cap_ < L) {
+    d_mt_leaf_parent_ = Alloc<int32_t>(L);
+    d_mt_node_ = Alloc<int32_t>(3 * static_cast<size_t>(L));
+    d_mt_in_sub_ = Alloc<int8_t>(L);
+    d_mt_upd_ = Alloc<int32_t>(static_cast<size_t>(L) + 1);
+    mt_cap_ = L;
+  }
+  args_.mt_leaf_parent = d_mt_leaf_parent_;
+  args_.mt_node = d_mt_node_;
+  args_.mt_in_sub = d_mt_in_sub_;
+  args_.mt_upd = d_mt_upd_;
+  args_.p.mono_inter = 1;
   DestroyGraph();
 }
 

@@ -169,6 +169,14 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool data_parallel_ = false;  // kData on more than one rank (global counts from the split estimates)
   bool voting_ = false;         // kVoting on more than one rank
   void SetupCegb();
+  // intermediate monotone constraints on the device (KArgs::mt_*, Params::mono_inter)
+  void SetupMonoInter();
+  size_t fb_slots_ = 0;
+  int mt_cap_ = 0;
+  int32_t* d_mt_leaf_parent_ = nullptr;
+  int32_t* d_mt_node_ = nullptr;
+  int8_t* d_mt_in_sub_ = nullptr;
+  int32_t* d_mt_upd_ = nullptr;
   TreeStats last_stats_;
   double split_collective_bytes_ = 0.0;  // device collectives per split step (distributed)
   double root_collective_bytes_ = 0.0;

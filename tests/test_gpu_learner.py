@@ -437,29 +437,50 @@ def test_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
     assert abs(_auc(y, models["device"].predict(X)) - _auc(y, cpu.predict(X))) < 0.01
 
 
-def test_intermediate_monotone_on_gpu(gpu_available):
-    """monotone_constraints_method=intermediate runs host-assisted (leaves re-bounded and
-    re-scanned across the tree after each split) on device histograms: monotone predictions
-    and the CPU learner's first tree."""
+@pytest.mark.parametrize("case", ["small", "wide"])
+def test_intermediate_monotone_on_gpu(case, gpu_available, monkeypatch, capfd):
+    """monotone_constraints_method=intermediate grows device-resident: the pick walks the tree
+    to re-bound the leaves a split can touch (pick.h MonoInterUpdate) and the next split scan
+    re-scans them.  Monotone predictions, the same trees as host-assisted growth (the host
+    LeafConstraints loop on device histograms), and the CPU learner's first tree."""
     rng = np.random.RandomState(1)
-    n = 6000
-    X = rng.rand(n, 3)
-    y = (5 * X[:, 0] + np.sin(10 * np.pi * X[:, 0]) - 5 * X[:, 1] - np.cos(10 * np.pi * X[:, 1])
-         + 2 * np.sin(6 * X[:, 2]) + rng.rand(n) * 0.01)
-    params = {"verbose": -1, "monotone_constraints": [1, -1, 0], "min_data": 20, "num_leaves": 31,
+    if case == "small":
+        n = 6000
+        X = rng.rand(n, 3)
+        y = (5 * X[:, 0] + np.sin(10 * np.pi * X[:, 0]) - 5 * X[:, 1] - np.cos(10 * np.pi * X[:, 1])
+             + 2 * np.sin(6 * X[:, 2]) + rng.rand(n) * 0.01)
+        mono, leaves = [1, -1, 0], 31
+    else:
+        n = 30000
+        X = rng.rand(n, 8)
+        y = (3 * X[:, 0] + np.sin(8 * np.pi * X[:, 0]) - 2 * X[:, 1] + X[:, 2] * X[:, 3] + np.cos(6 * X[:, 4])
+             + 2 * X[:, 5] - np.sin(5 * X[:, 6]) + rng.rand(n) * 0.05)
+        mono, leaves = [1, -1, 0, 1, 0, 1, -1, 0], 63
+    params = {"verbose": 2, "monotone_constraints": mono, "min_data": 20, "num_leaves": leaves,
               "monotone_constraints_method": "intermediate", "max_bin": 63}
+    capfd.readouterr()
     gpu = lgb.train(dict(params, device_type="gpu"), lgb.Dataset(X, y), 20)
-    cpu = lgb.train(dict(params, device_type="cpu"), lgb.Dataset(X, y), 20)
+    log = capfd.readouterr().out
+    assert "device-resident growth" in log and "host-assisted growth" not in log
+    monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    host = lgb.train(dict(params, device_type="gpu", verbose=-1), lgb.Dataset(X, y), 20)
+    monkeypatch.delenv("LGBM_AMD_HOST_ASSIST")
+    cpu = lgb.train(dict(params, device_type="cpu", verbose=-1), lgb.Dataset(X, y), 20)
     grid = np.linspace(0, 1, 40)
-    for base in rng.rand(6, 3):
-        for f, sign in ((0, 1), (1, -1)):
+    for base in rng.rand(6, X.shape[1]):
+        for f, sign in [(f, m) for f, m in enumerate(mono) if m != 0]:
             pts = np.tile(base, (40, 1))
             pts[:, f] = grid
             assert np.all(np.diff(gpu.predict(pts)) * sign >= -1e-12)
+    ms = lambda b: b.model_to_string()[b.model_to_string().index("Tree=0"):b.model_to_string().index("end of trees")]
+    assert ms(gpu) == ms(host)
+    # (the re-bounding matters: the basic method grows other trees)
+    basic = lgb.train(dict(params, device_type="gpu", verbose=-1, monotone_constraints_method="basic"),
+                      lgb.Dataset(X, y), 20)
+    assert ms(basic) != ms(gpu)
     assert _splits(gpu.dump_model()["tree_info"][0]["tree_structure"]) == \
         _splits(cpu.dump_model()["tree_info"][0]["tree_structure"])
     assert np.corrcoef(gpu.predict(X), cpu.predict(X))[0, 1] > 0.999
-
 
 
 @pytest.mark.parametrize("task", ["lambdarank", "multiclass", "aucmu_weighted", "regression_family"])
