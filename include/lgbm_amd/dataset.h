@@ -10,6 +10,7 @@
 // reference's "offset" convention (bin 0 dropped when most_freq_bin == 0).
 #pragma once
 
+#include <algorithm>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -72,21 +73,53 @@ struct FeatureGroup {
   std::vector<int> inner_features;      // inner feature indices in this group
   std::vector<uint32_t> bin_offsets;    // size nf + 1, bin_offsets[0] == 1
   int num_total_bin = 1;
-  int bin_bytes = 1;                    // 1, 2 or 4 bytes per row
-  std::vector<uint8_t> data;            // num_data * bin_bytes, dense column
+  int bin_bytes = 1;                    // 1, 2 or 4 bytes per row (per stored entry when sparse)
+  // storage: dense -- data holds num_data * bin_bytes, one group bin per row -- or sparse (the
+  // reference's SparseBin, sparse_bin.hpp): only the rows whose group bin is not 0 (every member
+  // feature at its most frequent bin), ascending in sp_rows, their bins in data.  Pushes to a
+  // sparse group are buffered per thread (push_buf) and merged by Dataset::FinishLoad.
+  bool sparse = false;
+  std::vector<uint8_t> data;
+  std::vector<data_size_t> sp_rows;
+  std::vector<std::vector<std::pair<data_size_t, uint32_t>>> push_buf;  // [thread]
 
-  inline uint32_t Get(data_size_t row) const {
+  inline uint32_t ValAt(size_t k) const {
     switch (bin_bytes) {
-      case 1: return data[row];
-      case 2: return reinterpret_cast<const uint16_t*>(data.data())[row];
-      default: return reinterpret_cast<const uint32_t*>(data.data())[row];
+      case 1: return data[k];
+      case 2: return reinterpret_cast<const uint16_t*>(data.data())[k];
+      default: return reinterpret_cast<const uint32_t*>(data.data())[k];
     }
   }
+  inline uint32_t Get(data_size_t row) const {
+    if (sparse) {
+      const auto it = std::lower_bound(sp_rows.begin(), sp_rows.end(), row);
+      return (it == sp_rows.end() || *it != row) ? 0u : ValAt(static_cast<size_t>(it - sp_rows.begin()));
+    }
+    return ValAt(static_cast<size_t>(row));
+  }
   inline void Set(data_size_t row, uint32_t v) {
+    if (sparse) {
+      SetSparse(row, v);
+      return;
+    }
     switch (bin_bytes) {
       case 1: data[row] = static_cast<uint8_t>(v); break;
       case 2: reinterpret_cast<uint16_t*>(data.data())[row] = static_cast<uint16_t>(v); break;
       default: reinterpret_cast<uint32_t*>(data.data())[row] = v; break;
+    }
+  }
+  void SetSparse(data_size_t row, uint32_t v);  // (buffered: Dataset::FinishLoad merges)
+  void MergePushes();                           // sparse: sort by row, last push of a row wins, drop 0
+  // f(row, bin) for every row whose bin is not 0, ascending rows (dense: a scan of the column)
+  template <typename Fn>
+  void ForEachStored(data_size_t num_data, Fn f) const {
+    if (sparse) {
+      for (size_t k = 0; k < sp_rows.size(); ++k) f(sp_rows[k], ValAt(k));
+      return;
+    }
+    for (data_size_t r = 0; r < num_data; ++r) {
+      const uint32_t v = ValAt(static_cast<size_t>(r));
+      if (v != 0) f(r, v);
     }
   }
 };
@@ -116,7 +149,12 @@ class Dataset {
   void PushDenseRow(data_size_t row, const double* values, int ncol);
   void PushSparseRow(data_size_t row, const std::vector<std::pair<int, double>>& values);
   void PushColumnValue(data_size_t row, int real_col, double value);
-  void FinishLoad() { finished_ = true; }
+  // every push is done: sparse groups merge their per-thread push buffers
+  void FinishLoad();
+  // storage of the groups: sparse when a group's non-zero share is at most kSparseGroupRate
+  // (estimated from its features' bin mappers; LGBM_AMD_HOST_SPARSE=0 / 1 forces dense / sparse)
+  static constexpr double kSparseGroupRate = 0.2;
+  int num_sparse_groups() const;
 
   // --- queries --------------------------------------------------------------------
   data_size_t num_data() const { return num_data_; }

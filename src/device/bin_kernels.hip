@@ -134,7 +134,7 @@ std::vector<char> DeviceBinDenseMatrix(Dataset* ds, const void* data, bool is_f6
   for (int g = 0; g < ds->num_groups(); ++g) {
     const FeatureGroup& fg = ds->group(g);
     std::vector<std::pair<int, int>> members;  // (column, sub-feature)
-    bool ok = true;
+    bool ok = !fg.sparse;  // (sparse groups: pushed on the host into their stored-row lists)
     for (size_t k = 0; k < fg.inner_features.size(); ++k) {
       const int inner = fg.inner_features[k];
       const int col = ds->RealFeatureIndex(inner);

@@ -12,8 +12,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <mutex>
 #include <sstream>
 
 #include "lgbm_amd/common.h"
@@ -407,11 +409,73 @@ void Dataset::BuildGroups(const std::vector<std::vector<int>>& features_in_group
     }
     g.num_total_bin = total;
     g.bin_bytes = total <= 256 ? 1 : (total <= 65536 ? 2 : 4);
-    g.data.assign(static_cast<size_t>(num_data_) * g.bin_bytes, 0);
+    // sparse storage when at most kSparseGroupRate of the rows can hold a non-zero group bin
+    // (the members' shares outside their most frequent bins, summed: an upper bound)
+    double nonzero = 0.0;
+    for (int f : fs) nonzero += 1.0 - bin_mappers_[f]->sparse_rate();
+    g.sparse = nonzero <= kSparseGroupRate;
+    if (const char* e = std::getenv("LGBM_AMD_HOST_SPARSE")) g.sparse = e[0] == '1';
+    if (g.sparse) {
+      g.push_buf.resize(static_cast<size_t>(std::max(omp_get_max_threads(), omp_get_num_procs())));
+    } else {
+      g.data.assign(static_cast<size_t>(num_data_) * g.bin_bytes, 0);
+    }
     groups_.push_back(std::move(g));
   }
   group_bin_boundaries_.assign(1, 0);
   for (auto& g : groups_) group_bin_boundaries_.push_back(group_bin_boundaries_.back() + g.num_total_bin);
+}
+
+void FeatureGroup::SetSparse(data_size_t row, uint32_t v) {
+  static std::mutex overflow_mu;  // (a thread id beyond the buffers: shared, locked)
+  const size_t t = static_cast<size_t>(omp_get_thread_num());
+  if (t < push_buf.size()) {
+    push_buf[t].emplace_back(row, v);
+  } else {
+    std::lock_guard<std::mutex> lock(overflow_mu);
+    push_buf[0].emplace_back(row, v);
+  }
+}
+
+void FeatureGroup::MergePushes() {
+  if (!sparse) return;
+  std::vector<std::pair<data_size_t, uint32_t>> all;
+  size_t total = sp_rows.size();
+  for (const auto& b : push_buf) total += b.size();
+  all.reserve(total);
+  for (size_t k = 0; k < sp_rows.size(); ++k) all.emplace_back(sp_rows[k], ValAt(k));  // (earlier merges)
+  for (auto& b : push_buf) {
+    all.insert(all.end(), b.begin(), b.end());
+    std::vector<std::pair<data_size_t, uint32_t>>().swap(b);
+  }
+  // a row's pushes come from one thread, in push order: after a stable sort by row the last
+  // one is the value a dense column would hold
+  std::stable_sort(all.begin(), all.end(),
+                   [](const std::pair<data_size_t, uint32_t>& x, const std::pair<data_size_t, uint32_t>& y) {
+                     return x.first < y.first;
+                   });
+  sp_rows.clear();
+  data.clear();
+  sp_rows.reserve(all.size());
+  data.reserve(all.size() * bin_bytes);
+  for (size_t k = 0; k < all.size(); ++k) {
+    if (k + 1 < all.size() && all[k + 1].first == all[k].first) continue;
+    if (all[k].second == 0) continue;
+    sp_rows.push_back(all[k].first);
+    const uint32_t v = all[k].second;
+    data.insert(data.end(), reinterpret_cast<const uint8_t*>(&v), reinterpret_cast<const uint8_t*>(&v) + bin_bytes);
+  }
+}
+
+void Dataset::FinishLoad() {
+  for (auto& g : groups_) g.MergePushes();
+  finished_ = true;
+}
+
+int Dataset::num_sparse_groups() const {
+  int n = 0;
+  for (const auto& g : groups_) n += g.sparse ? 1 : 0;
+  return n;
 }
 
 void Dataset::CreateValid(const Dataset& ref, data_size_t num_data) {
@@ -435,9 +499,36 @@ void Dataset::CreateValid(const Dataset& ref, data_size_t num_data) {
 
 void Dataset::CopySubrow(const Dataset& full, const data_size_t* idx, data_size_t n) {
   CreateValid(full, n);
+  std::vector<data_size_t> new_of;  // sparse groups: full row -> subset row (-1: not taken)
+  bool ascending = true;
+  for (data_size_t i = 1; i < n && ascending; ++i) ascending = idx[i] > idx[i - 1];
   for (size_t g = 0; g < groups_.size(); ++g) {
     const auto& src = full.groups_[g];
     auto& dst = groups_[g];
+    if (dst.sparse != src.sparse) {  // (the subset keeps the full dataset's storage)
+      dst.sparse = src.sparse;
+      dst.data.clear();
+      dst.push_buf.clear();
+      if (!dst.sparse) dst.data.assign(static_cast<size_t>(n) * dst.bin_bytes, 0);
+    }
+    if (src.sparse) {
+      if (new_of.empty()) {
+        new_of.assign(static_cast<size_t>(full.num_data_), -1);
+        for (data_size_t i = 0; i < n; ++i) new_of[idx[i]] = i;
+      }
+      std::vector<std::pair<data_size_t, uint32_t>> kept;
+      src.ForEachStored(full.num_data_, [&](data_size_t r, uint32_t v) {
+        if (new_of[r] >= 0) kept.emplace_back(new_of[r], v);
+      });
+      if (!ascending) std::sort(kept.begin(), kept.end());
+      dst.sp_rows.resize(kept.size());
+      dst.data.assign(kept.size() * dst.bin_bytes, 0);
+      for (size_t k = 0; k < kept.size(); ++k) {
+        dst.sp_rows[k] = kept[k].first;
+        std::memcpy(dst.data.data() + k * dst.bin_bytes, &kept[k].second, dst.bin_bytes);  // (little endian)
+      }
+      continue;
+    }
 #pragma omp parallel for schedule(static)
     for (data_size_t i = 0; i < n; ++i) {
       std::memcpy(dst.data.data() + static_cast<size_t>(i) * dst.bin_bytes,
@@ -542,7 +633,17 @@ void Dataset::BuildRowMajor() const {
     uint8_t* dst = row_major_.data() + static_cast<size_t>(r) * row_stride_;
     for (size_t g = 0; g < groups_.size(); ++g) {
       const FeatureGroup& grp = groups_[g];
+      if (grp.sparse) continue;
       std::memcpy(dst + row_goff_[g], grp.data.data() + static_cast<size_t>(r) * grp.bin_bytes, grp.bin_bytes);
+    }
+  }
+  for (size_t g = 0; g < groups_.size(); ++g) {  // sparse groups: their stored rows only
+    const FeatureGroup& grp = groups_[g];
+    if (!grp.sparse) continue;
+#pragma omp parallel for schedule(static)
+    for (size_t k = 0; k < grp.sp_rows.size(); ++k) {
+      std::memcpy(row_major_.data() + static_cast<size_t>(grp.sp_rows[k]) * row_stride_ + row_goff_[g],
+                  grp.data.data() + k * grp.bin_bytes, grp.bin_bytes);
     }
   }
 }
@@ -635,13 +736,50 @@ void Dataset::ConstructHistograms(const std::vector<int8_t>& group_used, const d
     pg = og.data();
     ph = oh.data();
   }
+  bool leaf_ascending = true;  // (sparse groups: merge walk of the leaf's rows)
+  if (indices != nullptr && num_sparse_groups() > 0) {
+    for (data_size_t i = 1; i < n && leaf_ascending; ++i) leaf_ascending = indices[i] > indices[i - 1];
+  }
 #pragma omp parallel for schedule(dynamic, 1)
   for (int g = 0; g < ng; ++g) {
     if (!group_used[g]) continue;
     const FeatureGroup& grp = groups_[g];
     hist_t* h = hist + 2 * group_bin_boundaries_[g];
     std::fill(h, h + 2 * grp.num_total_bin, 0.0);
-    if (grp.bin_bytes == 1) {
+    if (grp.sparse) {
+      // the stored rows only (reference SparseBin::ConstructHistogram): all rows -- every entry;
+      // a leaf -- a merge walk of its ascending rows with the entries, or a search per row
+      const size_t nnz = grp.sp_rows.size();
+      if (indices == nullptr) {
+        for (size_t k = 0; k < nnz; ++k) {
+          const uint32_t b = grp.ValAt(k);
+          h[2 * b] += pg[grp.sp_rows[k]];
+          h[2 * b + 1] += ph[grp.sp_rows[k]];
+        }
+      } else if (leaf_ascending) {
+        size_t k = 0;
+        for (data_size_t i = 0; i < n && k < nnz; ++i) {
+          const data_size_t r = indices[i];
+          if (grp.sp_rows[k] < r) {
+            k = static_cast<size_t>(std::lower_bound(grp.sp_rows.begin() + k, grp.sp_rows.end(), r) - grp.sp_rows.begin());
+            if (k >= nnz) break;
+          }
+          if (grp.sp_rows[k] == r) {
+            const uint32_t b = grp.ValAt(k);
+            h[2 * b] += pg[i];
+            h[2 * b + 1] += ph[i];
+            ++k;
+          }
+        }
+      } else {
+        for (data_size_t i = 0; i < n; ++i) {
+          const uint32_t b = grp.Get(indices[i]);
+          if (b == 0) continue;
+          h[2 * b] += pg[i];
+          h[2 * b + 1] += ph[i];
+        }
+      }
+    } else if (grp.bin_bytes == 1) {
       const uint8_t* col = grp.data.data();
       if (indices) {
         for (data_size_t i = 0; i < n; ++i) {
@@ -686,7 +824,8 @@ void Dataset::FixHistogram(int inner, double sum_grad, double sum_hess, hist_t* 
 // ---------------------------------------------------------------------------------
 // binary persistence (own format; magic + versioned)
 namespace {
-const char kMagic[] = "LGBMAMD_DATASET_V1";
+const char kMagic[] = "LGBMAMD_DATASET_V2";    // V2: sparse groups (flag + stored rows)
+const char kMagicV1[] = "LGBMAMD_DATASET_V1";  // (dense groups only; still read)
 template <typename T>
 void Put(std::string* s, const T& v) { s->append(reinterpret_cast<const char*>(&v), sizeof(T)); }
 template <typename T>
@@ -743,6 +882,9 @@ void Dataset::SaveBinaryFile(const std::string& path) const {
     PutVec(&s, g.bin_offsets);
     Put(&s, g.num_total_bin);
     Put(&s, g.bin_bytes);
+    const int8_t sparse = g.sparse ? 1 : 0;
+    Put(&s, sparse);
+    if (g.sparse) PutVec(&s, g.sp_rows);
     PutVec(&s, g.data);
   }
   uint64_t nf = forced_bin_bounds_.size();
@@ -760,14 +902,16 @@ bool Dataset::IsBinaryFile(const std::string& path) {
   if (!f) return false;
   char buf[sizeof(kMagic)];
   f.read(buf, sizeof(buf));
-  return f.gcount() == static_cast<std::streamsize>(sizeof(buf)) && std::memcmp(buf, kMagic, sizeof(kMagic)) == 0;
+  return f.gcount() == static_cast<std::streamsize>(sizeof(buf)) &&
+         (std::memcmp(buf, kMagic, sizeof(kMagic)) == 0 || std::memcmp(buf, kMagicV1, sizeof(kMagicV1)) == 0);
 }
 
 std::unique_ptr<Dataset> Dataset::LoadBinaryFile(const std::string& path) {
   std::ifstream f(path, std::ios::binary);
   if (!f) Log::Fatal("Cannot open binary data file %s", path.c_str());
   std::string s((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  if (s.size() < sizeof(kMagic) || std::memcmp(s.data(), kMagic, sizeof(kMagic)) != 0) {
+  const bool v1 = s.size() >= sizeof(kMagicV1) && std::memcmp(s.data(), kMagicV1, sizeof(kMagicV1)) == 0;
+  if (s.size() < sizeof(kMagic) || (!v1 && std::memcmp(s.data(), kMagic, sizeof(kMagic)) != 0)) {
     Log::Fatal("%s is not a binary dataset file", path.c_str());
   }
   std::unique_ptr<Dataset> d(new Dataset());
@@ -799,6 +943,10 @@ std::unique_ptr<Dataset> Dataset::LoadBinaryFile(const std::string& path) {
     p = GetVec(p, &g.bin_offsets);
     p = Get(p, &g.num_total_bin);
     p = Get(p, &g.bin_bytes);
+    int8_t sparse = 0;
+    if (!v1) p = Get(p, &sparse);
+    g.sparse = sparse != 0;
+    if (g.sparse) p = GetVec(p, &g.sp_rows);
     p = GetVec(p, &g.data);
     for (int f : g.inner_features) {
       if (d->bin_mappers_[f]->GetDefaultBin() != d->bin_mappers_[f]->GetMostFreqBin()) d->need_push_zeros_.push_back(f);

@@ -249,7 +249,12 @@ void GPUTreeLearner::UploadData() {
     for (int g = 0; g < num_groups_; ++g) {
       const FeatureGroup& grp = data_->group(g);
       uint8_t* dst = col.data() + col_off[g];
-      if (!h_gwide_[g] && grp.bin_bytes == 1) {
+      if (grp.sparse) {  // (zero-filled column: the stored rows only)
+        grp.ForEachStored(num_data_, [&](data_size_t r, uint32_t v) {
+          if (!h_gwide_[g]) dst[r] = static_cast<uint8_t>(v);
+          else reinterpret_cast<uint16_t*>(dst)[r] = static_cast<uint16_t>(v);
+        });
+      } else if (!h_gwide_[g] && grp.bin_bytes == 1) {
         std::memcpy(dst, grp.data.data(), static_cast<size_t>(num_data_));
       } else {
         for (data_size_t r = 0; r < num_data_; ++r) {
@@ -2137,6 +2142,11 @@ void GPUTreeLearner::UploadSparseRows() {
     const data_size_t r0 = static_cast<data_size_t>(b) * kBlk, r1 = std::min(n, r0 + kBlk);
     for (int g = 0; g < num_groups_; ++g) {
       const FeatureGroup& grp = data_->group(g);
+      if (grp.sparse) {  // (the block's stored rows)
+        auto k = std::lower_bound(grp.sp_rows.begin(), grp.sp_rows.end(), r0);
+        for (; k != grp.sp_rows.end() && *k < r1; ++k) ptr[*k + 1] += 1;
+        continue;
+      }
       for (data_size_t r = r0; r < r1; ++r) ptr[r + 1] += grp.Get(r) != 0 ? 1 : 0;
     }
   }
@@ -2149,6 +2159,14 @@ void GPUTreeLearner::UploadSparseRows() {
     for (int g = 0; g < num_groups_; ++g) {
       const FeatureGroup& grp = data_->group(g);
       const uint32_t goff = static_cast<uint32_t>(data_->group_bin_boundary(g));
+      if (grp.sparse) {
+        size_t k = static_cast<size_t>(std::lower_bound(grp.sp_rows.begin(), grp.sp_rows.end(), r0) - grp.sp_rows.begin());
+        for (; k < grp.sp_rows.size() && grp.sp_rows[k] < r1; ++k) {
+          const data_size_t r = grp.sp_rows[k];
+          ent[cur[r - r0]++] = static_cast<uint16_t>(goff + grp.ValAt(k));
+        }
+        continue;
+      }
       for (data_size_t r = r0; r < r1; ++r) {
         const uint32_t v = grp.Get(r);
         if (v != 0) ent[cur[r - r0]++] = static_cast<uint16_t>(goff + v);
@@ -2174,14 +2192,25 @@ std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d, int row_word
   const data_size_t n = d->num_data();
   const int ng = d->num_groups();
   std::vector<uint8_t> host(static_cast<size_t>(n) * row_bytes, 0);
+  auto put = [&](uint8_t* row, int g, uint32_t v) {
+    if (h_gnib_[g] != 0) row[h_gbyte_[g]] |= static_cast<uint8_t>((v & 15u) << ((h_gnib_[g] & 1) * 4));
+    else if (!h_gwide_[g]) row[h_gbyte_[g]] = static_cast<uint8_t>(v);
+    else reinterpret_cast<uint16_t*>(row + h_gbyte_[g])[0] = static_cast<uint16_t>(v);
+  };
 #pragma omp parallel for schedule(static)
   for (data_size_t r = 0; r < n; ++r) {
     uint8_t* row = host.data() + static_cast<size_t>(r) * row_bytes;
     for (int g = 0; g < ng; ++g) {
-      const uint32_t v = d->group(g).Get(r);
-      if (h_gnib_[g] != 0) row[h_gbyte_[g]] |= static_cast<uint8_t>((v & 15u) << ((h_gnib_[g] & 1) * 4));
-      else if (!h_gwide_[g]) row[h_gbyte_[g]] = static_cast<uint8_t>(v);
-      else reinterpret_cast<uint16_t*>(row + h_gbyte_[g])[0] = static_cast<uint16_t>(v);
+      if (!d->group(g).sparse) put(row, g, d->group(g).Get(r));
+    }
+  }
+  // sparse groups: their stored rows (one group at a time: 4-bit neighbours share a byte)
+  for (int g = 0; g < ng; ++g) {
+    const FeatureGroup& grp = d->group(g);
+    if (!grp.sparse) continue;
+#pragma omp parallel for schedule(static)
+    for (size_t k = 0; k < grp.sp_rows.size(); ++k) {
+      put(host.data() + static_cast<size_t>(grp.sp_rows[k]) * row_bytes, g, grp.ValAt(k));
     }
   }
   return host;

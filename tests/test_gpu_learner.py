@@ -717,3 +717,31 @@ def test_score_walk_computes_next_gradients(gpu_available, monkeypatch, params):
             return [node["split_feature"]] + feats(node["left_child"]) + feats(node["right_child"])
         assert feats(a["tree_structure"]) == feats(b["tree_structure"])
     np.testing.assert_allclose(preds["0"], preds["1"], rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("rows_layout", ["0", "1"])
+def test_host_sparse_groups_device_learner(rows_layout, gpu_available, monkeypatch):
+    """Sparse host groups (only the rows off their most frequent bins stored) feed the device
+    learner's uploads -- word rows or row-sparse lists (LGBM_AMD_SPARSE_ROWS), the column copy,
+    device binning of the dense columns next to host-pushed sparse ones, a validation set --
+    with the same models as dense host groups."""
+    rng = np.random.RandomState(8)
+    n, f = 160000, 30
+    X = np.where(rng.rand(n, f) < 0.04, rng.randn(n, f), 0.0)
+    X[:, :3] = rng.randn(n, 3)
+    y = (X[:, 0] - X[:, 1] + 2 * X[:, 3:15].sum(1) + 0.3 * rng.randn(n) > 0).astype(np.float32)
+    monkeypatch.setenv("LGBM_AMD_SPARSE_ROWS", rows_layout)
+    params = {"objective": "binary", "num_leaves": 63, "verbose": -1, "device_type": "gpu", "seed": 2,
+              "metric": "auc", "enable_bundle": False}
+
+    def run(mode):
+        monkeypatch.setenv("LGBM_AMD_HOST_SPARSE", mode)
+        ds = lgb.Dataset(X[:140000], y[:140000], params=params)
+        va = lgb.Dataset(X[140000:], y[140000:], reference=ds)
+        ev = {}
+        bst = lgb.train(params, ds, 10, valid_sets=[va], evals_result=ev, verbose_eval=False)
+        m = bst.model_to_string()
+        return m[m.index("Tree=0"):m.index("end of trees")], ev["valid_0"]["auc"]
+
+    dense = run("0")
+    assert run("1") == dense
