@@ -9,6 +9,8 @@ all-reduce per split on top).  Synthetic data: 13 dense heavy-tailed counts + 54
 count features (97-99.5% zeros), ~3.4% positives.
 
   python tools/bench_criteo.py --rows 100000000 --steps 10 --warmup 2
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_criteo.py \
+      --rows R --learner voting      # config #5's learner: R rows per rank, one process per GPU
 """
 import argparse
 import json
@@ -37,7 +39,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--leaves", type=int, default=255)
     ap.add_argument("--device", default="gpu")
+    ap.add_argument("--learner", default="serial", choices=["serial", "data", "voting"],
+                    help="under torchrun: the distributed learner (rows are per rank)")
+    ap.add_argument("--top-k", type=int, default=20)
     args = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
     import threading
     t_start = time.time()
 
@@ -48,34 +55,47 @@ def main():
 
     threading.Thread(target=heartbeat, daemon=True).start()
     import lightgbmv1_amd as lgb
+    from lightgbmv1_amd.parallel import torch_dist
 
+    if world > 1:
+        torch_dist.init_network(use_rccl=args.device == "gpu")
     t0 = time.time()
-    X, y = make_ctr(args.rows, 5)
+    X, y = make_ctr(args.rows, 5 + rank)  # (each rank its own shard)
     t_gen = time.time() - t0
     params = {"objective": "binary", "num_leaves": args.leaves, "learning_rate": 0.1, "max_bin": 255,
               "min_data_in_leaf": 20, "device_type": args.device, "verbose": -1,
-              "num_threads": min(16, os.cpu_count() or 8)}
+              "num_threads": min(16 // max(1, world) if world > 1 else 16, os.cpu_count() or 8)}
+    if world > 1:
+        params.update(tree_learner=args.learner, num_machines=world, pre_partition=True, top_k=args.top_k)
     train = lgb.Dataset(X, y, params=params, free_raw_data=True)
     booster = lgb.Booster(params=params, train_set=train)
     del X
     setup_s = time.time() - t0
     for _ in range(args.warmup):
         booster.update()
+    torch_dist.barrier()
     lgb.device_synchronize()
     t1 = time.perf_counter()
     for _ in range(args.steps):
         booster.update()
     lgb.device_synchronize()
-    sec = (time.perf_counter() - t1) / max(1, args.steps)
+    torch_dist.barrier()
+    sec = torch_dist.allreduce_max((time.perf_counter() - t1) / max(1, args.steps))
     # the reference's single-machine time scaled to this shard's rows (linear in rows)
-    ref_scaled = REF_SEC_PER_TREE_1_MACHINE * args.rows / 1.7e9
+    ref_scaled = REF_SEC_PER_TREE_1_MACHINE * args.rows * world / 1.7e9
+    if rank != 0:
+        torch_dist.shutdown() if world > 1 else None
+        return
     print(json.dumps({
         "metric": "sec/tree, Criteo-shaped 67 sparse count features (EFB), 255 leaves, one GPU shard",
-        "value": round(sec, 6), "unit": "s/tree", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-        "higher_is_better": False, "rows": args.rows, "dtype": "fp32-grad/fx32-hist/fp64-scan", "data": "synthetic",
+        "value": round(sec, 6), "unit": "s/tree", "ranks": world, "learner": args.learner if world > 1 else "serial",
+        "steps": args.steps, "warmup": args.warmup,
+        "higher_is_better": False, "rows_per_rank": args.rows, "dtype": "fp32-grad/fx32-hist/fp64-scan", "data": "synthetic",
         "reference_1_machine_scaled_to_rows_s": round(ref_scaled, 3),
         "reference_8_machines_1p7B_s": REF_SEC_PER_TREE_8_MACHINES,
         "data_gen_s": round(t_gen, 1), "setup_s": round(setup_s, 1), "trees": booster.num_trees()}), flush=True)
+    if world > 1:
+        torch_dist.shutdown()
 
 
 if __name__ == "__main__":
