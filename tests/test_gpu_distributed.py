@@ -280,3 +280,29 @@ def test_distributed_modes_device_resident(learner, world, mode, gpu_available, 
     full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
     serial = lgb.train(dict(BASE, **extra), full.subset(np.arange(N)), 1)
     assert _splits(dev[0][0], 0) == _splits(serial.model_to_string(), 0)
+
+
+def test_bench_py_under_torchrun_two_processes(gpu_available, tmp_path):
+    """The multi-GPU benchmark entry point as the driver launches it (torch.distributed.run,
+    one process per rank, peer comm), here with 2 processes sharing the box's GPU and 1M rows:
+    rank 0 prints one JSON line with n_gpus 2 and dp2 parallelism."""
+    import json
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(HERE)
+    env = dict(os.environ, OMP_NUM_THREADS="4")
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                          "--gpus", "2", "--steps", "5", "--warmup", "2", "--rows", "1000000", "--test-rows", "50000"],
+                         cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["ms_per_step"] > 0
+    assert rec["auc_heldout"] > 0.7
+    assert "peer device comm unavailable" not in out.stdout
