@@ -765,6 +765,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     long long* nxt = RoundScratch(a, parity + 1, j);
     for (int i = tid; i < 2 * nbf; i += NT) nxt[2 * F.hist_offset + i] = 0;
   }
+  if (!CAT && dp && a.round_send != nullptr) {
+    // data-parallel: the next round's owner-major send buffer, cleared by every workgroup's
+    // share (this round's reduce-scatter has read it) -- no memset node per round
+    const size_t total = static_cast<size_t>(a.p.world) * a.round_k * a.rs_block * 2;
+    const size_t nwg = static_cast<size_t>(gridDim.x) * gridDim.y;
+    const size_t per = (total + nwg - 1) / nwg;
+    const size_t b0 = (static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * per;
+    const size_t b1 = min(total, b0 + per);
+    for (size_t i = b0 + tid; i < b1; i += NT) a.round_send[i] = 0;
+  }
   if (j >= nexp) return;
   const ExpPlan& E = rd->e[j];
   const int pc = E.part_count;

@@ -1264,6 +1264,9 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
   AllreduceRoot();
   HIPCHECK(hipMemsetAsync(d_scratch_, 0, zero_bytes, stream_));
+  if (a.rd != nullptr && data_parallel_ && d_round_send_ != nullptr) {  // (the first round's send buffer)
+    HIPCHECK(hipMemsetAsync(d_round_send_, 0, sizeof(long long) * world_ * round_k_ * rs_block_ * 2, stream_));
+  }
   dev::HistRoot(a, stream_);
   ReduceScatterStep(0);
   if (a.cegb_lazy != nullptr) {
@@ -1292,7 +1295,7 @@ void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
   // replicated state); communicators that cannot skip run them
   dc->SetSkipGuard(&d_round_->done);
   const size_t owned = static_cast<size_t>(round_k_) * rs_block_ * 2;
-  if (data_parallel_) HIPCHECK(hipMemsetAsync(d_round_send_, 0, sizeof(long long) * owned * world_, stream_));
+  // (the owner-major send buffer was cleared by the previous round's split scans, or by the root)
   dev::RoundSplitReduce(a, stream_);
   if (data_parallel_) dc->ReduceScatterSumI64(d_round_send_, d_round_owned_, owned, stream_);
   dev::RoundFind(a, stream_);
