@@ -13,7 +13,7 @@
 
 namespace lgbm_amd {
 
-constexpr int kMaxCatWords = 32;  // categorical bitset capacity: 1024 bins
+constexpr int kMaxCatWords = 128;  // categorical bitset capacity: 4096 bins
 
 struct DeviceSplit {
   double gain;

@@ -255,6 +255,30 @@ __device__ __forceinline__ void PublishI32(int32_t* dst, int32_t v) {
 struct CatWords {
   uint32_t w[kMaxCatWords];
 };
+// Category sets are copied / published write-through in 64-bit words, a few registers at a
+// time: a whole CatWords value is 128 VGPRs, and one indexed by category lives in scratch.
+// (u64 word i holds the uint32 words 2i and 2i + 1: bin b is bit b & 63 of word b >> 6)
+__device__ __forceinline__ void PublishCatCopy(uint32_t* dst, const uint32_t* src) {
+  const unsigned long long* s = reinterpret_cast<const unsigned long long*>(src);
+  GlobalU64* d = (GlobalU64*)(dst);
+#pragma unroll 1
+  for (int i0 = 0; i0 < kMaxCatWords / 2; i0 += 8) {
+    unsigned long long v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = s[i0 + k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) __hip_atomic_store(d + i0 + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// the set {bin} (bin < 0: the empty set)
+__device__ __forceinline__ void PublishCatSingle(uint32_t* dst, int bin) {
+  GlobalU64* d = (GlobalU64*)(dst);
+#pragma unroll 1
+  for (int i = 0; i < kMaxCatWords / 2; ++i) {
+    const unsigned long long v = (bin >= 0 && (bin >> 6) == i) ? (1ull << (bin & 63)) : 0ull;
+    __hip_atomic_store(d + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 // SplitInfo ordering: larger gain first, then smaller real feature index (NaN = -inf)
 __device__ __forceinline__ bool SplitBetter(double ga, int fa, double gb, int fb) {

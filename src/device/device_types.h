@@ -58,6 +58,7 @@ struct Params {
   int32_t data_parallel;  // leaf sizes/decisions from global (split-estimated) counts
   int32_t max_feature_bins;  // max stored bins of one feature (split-scan LDS staging)
   int32_t has_cat;           // number of categorical features (KArgs::cat_list; their own split-scan kernel)
+  int32_t wide_cat;          // some categorical feature has > kFindCatNarrow bins (the wide categorical kernel)
   int32_t direct_from_split; // splits >= this have no reduce kernel: the split scan sums the partials
   int32_t trace_repeat;      // diagnostics (LGBM_AMD_KTRACE_REPEAT): run the traced pick twice
   // voting-parallel split scans (reference voting_parallel_tree_learner.cpp): 0 off, 1 the

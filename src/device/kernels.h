@@ -204,7 +204,8 @@ enum TraceSlot {
   kTraceSlots = 32
 };
 
-constexpr int kFindMaxCatBins = 1024;  // categorical features scanned on device (<= 32 * kMaxCatWords)
+constexpr int kFindMaxCatBins = 4096;  // categorical features scanned on device (<= 32 * kMaxCatWords)
+constexpr int kFindCatNarrow = 1024;   // ... by the regular categorical kernel; wider ones by its wide variant
 constexpr int kHistThreads = 1024;     // histogram workgroup (16 waves)
 constexpr int kSparsePerThread = 4;    // row-sparse gathers: entries per thread and row loaded up front
 constexpr int kHistMinRows = 1024;     // rows per histogram row block, lower bound

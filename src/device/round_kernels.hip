@@ -653,7 +653,8 @@ struct RoundFindShared {
   BlockScratch<NT> sc;
   ScanScratch<NT> ssc;
   Cand sc2[NT / kWave];
-  typename std::conditional<KIND == 2, CatScratch, int>::type cat_sc;
+  typename std::conditional<KIND == 2, CatScratchT<kFindCatNarrow>,
+                            typename std::conditional<KIND == 3, CatScratchT<kFindMaxCatBins>, int>::type>::type cat_sc;
   unsigned long long s_red[2 * NT];
   ArgC arg[NT / kWave];
 };
@@ -720,8 +721,7 @@ __device__ void ChildBest(const KArgs& a, int y, int node, RoundFindShared<KIND,
       const FeatureBest w = fb0[wi];
       PublishRecord(dst, w);
       if (w.ncat > 0) {
-        const CatWords cat = *reinterpret_cast<const CatWords*>(a.feat_cat + wi * kMaxCatWords);
-        PublishRecord(reinterpret_cast<CatWords*>(a.cbest_cat + ci * kMaxCatWords), cat);
+        PublishCatCopy(a.cbest_cat + ci * kMaxCatWords, a.feat_cat + wi * kMaxCatWords);
       }
     } else {
       FeatureBest none = {};
@@ -739,7 +739,7 @@ __device__ void ChildBest(const KArgs& a, int y, int node, RoundFindShared<KIND,
 // expansion that cannot be split (max_depth, min_data_in_leaf) are not scanned.
 template <int KIND, bool SIMPLE, int NT>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave ? LGBM_FIND_WAVE_OCC : 1))) void k_round_find(KArgs a) {
-  constexpr bool CAT = KIND == 2;
+  constexpr bool CAT = KIND >= 2;  // (3: the wide categorical variant)
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
   __shared__ RoundFindShared<KIND, NT> sh;
   __shared__ int s_last;
@@ -1684,7 +1684,8 @@ void LaunchRoundFind(const KArgs& a, hipStream_t s) {
       if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads>), g, b, lds, s, a);
       else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads>), g, b, lds, s, a);
     }
-    hipLaunchKernelGGL((k_round_find<2, false, kFindThreads>), dim3(a.p.has_cat, ny), bc, lds, s, a);
+    if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads>), dim3(a.p.has_cat, ny), bc, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads>), dim3(a.p.has_cat, ny), bc, lds, s, a);
   } else if (narrow) {
     if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_round_find<0, false, kWave>), g, b, lds, s, a);

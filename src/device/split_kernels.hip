@@ -55,7 +55,7 @@ __device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, 
 // the most frequent bin is rebuilt from the leaf totals first (FixHistogram).  Invalid (gain
 // no better than the leaf's own): gain -inf, the pick then drops the forced splits.
 __device__ void ForcedGather(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int thr,
-                             FeatureBest* out, CatWords* bits) {
+                             FeatureBest* out, int* cat_bin) {
   const int nb = F.num_bin - F.offset, offset = F.offset;
   const double sum_g = L.sg, sum_h = L.sh - 2 * kEpsilon;  // the leaf's raw sums
   hv.fix_t = -1;
@@ -78,7 +78,7 @@ __device__ void ForcedGather(const Feature& F, HistView hv, const LeafCtx& L, co
   o.gain = -INFINITY;
   o.feature = -1;
   o.real_feature = -1;
-  for (int w = 0; w < kMaxCatWords; ++w) bits->w[w] = 0u;
+  *cat_bin = -1;  // (the forced category: the set published by the caller)
   double lg, lh, rg, rh;
   int lc, rc;
   if (!F.is_cat) {
@@ -111,7 +111,7 @@ __device__ void ForcedGather(const Feature& F, HistView hv, const LeafCtx& L, co
     rg = sum_g - lg;
     o.default_left = 0;
     o.ncat = 1;
-    bits->w[thr >> 5] |= 1u << (thr & 31);
+    *cat_bin = thr;
   }
   const double gain = LeafGain(lg, lh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, lc, L.parent_out, 1, 1,
                                smooth) +
@@ -143,7 +143,8 @@ struct FindShared {
   BlockScratch<NT> sc;
   ScanScratch<NT> ssc;
   Cand sc2[NT / kWave];
-  typename std::conditional<KIND == 2, CatScratch, int>::type cat_sc;
+  typename std::conditional<KIND == 2, CatScratchT<kFindCatNarrow>,
+                            typename std::conditional<KIND == 3, CatScratchT<kFindMaxCatBins>, int>::type>::type cat_sc;
   unsigned long long s_red[2 * NT];  // direct partial sums of narrow features
 };
 
@@ -151,7 +152,7 @@ struct FindShared {
 // same path (the kernel's pick tail needs all of them)
 template <bool ROOT, int KIND, bool SIMPLE, int NT>
 __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND, NT>& sh) {
-  constexpr bool CAT = KIND == 2;
+  constexpr bool CAT = KIND >= 2;  // (3: the wide categorical variant)
   constexpr int kFindThreads = NT;
   const long long t_entry = wall_clock64();
   // voting-parallel global scan: the features the vote elected for this side's leaf (an
@@ -191,11 +192,10 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   ChildInfo c;
   SideInfo sd;
   ChildStats cl;
-  DeviceSplit rbest;
   if (rescan) {
     s = st->cs.s;
     const Leaf& lf = a.leaves[rleaf];
-    rbest = a.best[rleaf];
+    const DeviceSplit& rbest = a.best[rleaf];  // (the sums and counts only: no copy of the category set)
     sd.lr = 0;
     sd.leaf = rleaf;
     sd.slot = lf.slot;
@@ -272,7 +272,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     rp.use_mc = 1;
     const double out0 = LeafOutputConstrained(sg, shh, p.lambda_l2, rp, cr, n, 0);
     const bool first = vote_global ? blockIdx.x == 0 : f == 0;
-    if (first && tid == 0 && KIND != 2) {  // (write-through: the root pick rewrites leaf 0)
+    if (first && tid == 0 && !CAT) {  // (write-through: the root pick rewrites leaf 0)
       Leaf& lf = a.leaves[0];
       if (a.p.vote_phase == 1) {
         PublishF64(&lf.lsum_g, sg);
@@ -333,7 +333,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       const size_t po = static_cast<size_t>(s & 1) * nfc + f;
       const int hs = a.cegb_scratch[po];
       unpaid = f == st->cs.split.feature ? 0 : (sd.is_hist ? hs : a.cegb_snap[po] - hs);
-      if (KIND != 2 && tid == 0) a.cegb_cnt[static_cast<size_t>(sd.leaf) * nfc + f] = unpaid;
+      if (!CAT && tid == 0) a.cegb_cnt[static_cast<size_t>(sd.leaf) * nfc + f] = unpaid;
     }
   }
   if (KIND == 1 && F.is_cat) return;  // the categorical kernel scans it
@@ -500,8 +500,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
         const size_t mi = static_cast<size_t>(leaf) * a.p.num_features + f;
         PublishRecord(&a.cegb_mem[mi], o);
         if (CAT) {
-          const CatWords bits = *reinterpret_cast<const CatWords*>(a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords);
-          PublishRecord(reinterpret_cast<CatWords*>(a.cegb_mem_cat + mi * kMaxCatWords), bits);
+          PublishCatCopy(a.cegb_mem_cat + mi * kMaxCatWords, a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords);
         }
       }
       double delta = a.p.cegb_split * L.n;
@@ -516,13 +515,13 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       const int k = ROOT ? 0 : (s < a.forced_n ? a.forced_child[2 * s + sd.lr] : -1);
       if (k >= 0 && k < a.forced_n && a.forced_feat[k] == f) {
         FeatureBest fo;
-        CatWords fbits;
-        ForcedGather(F, hv, L, p, a.forced_thr[k], &fo, &fbits);
+        int fbin;
+        ForcedGather(F, hv, L, p, a.forced_thr[k], &fo, &fbin);
         if (fo.feature == -2) {
           fo.feature = f;
           fo.real_feature = F.real_index;
         }
-        PublishRecord(reinterpret_cast<CatWords*>(a.forced_cat + static_cast<size_t>(k) * kMaxCatWords), fbits);
+        PublishCatSingle(a.forced_cat + static_cast<size_t>(k) * kMaxCatWords, fbin);
         PublishRecord(&a.forced_best[k], fo);
       }
     }
@@ -634,7 +633,8 @@ static void LaunchFind(const KArgs& a, hipStream_t s) {
       else hipLaunchKernelGGL((k_find<ROOT, 1, false, kFindThreads>), g, b, lds, s, a);
     }
     const int ncat = a.p.vote_phase == 2 ? a.num_scan : a.p.has_cat;  // voting: every elected slot
-    if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false, kFindThreads>), dim3(ncat, sides), bc, lds, s, a);
+    if (a.p.has_cat > 0 && a.p.wide_cat) hipLaunchKernelGGL((k_find<ROOT, 3, false, kFindThreads>), dim3(ncat, sides), bc, lds, s, a);
+    else if (a.p.has_cat > 0) hipLaunchKernelGGL((k_find<ROOT, 2, false, kFindThreads>), dim3(ncat, sides), bc, lds, s, a);
   } else if (narrow) {
     if (simple) hipLaunchKernelGGL((k_find<ROOT, 0, true, kWave>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_find<ROOT, 0, false, kWave>), g, b, lds, s, a);

@@ -449,13 +449,18 @@ __device__ __forceinline__ double MonotonePenalty(int depth, double mono_penalty
   return 1. - pow(2., mono_penalty - 1. - depth) + kEpsilon;
 }
 
-// LDS of the categorical scan: per-bin ctr and the stable ctr order
+// LDS of the categorical scan: per-bin ctr and the stable ctr order (CAP bins: the regular
+// kernel kFindCatNarrow, the wide one kFindMaxCatBins)
 constexpr int kCatPar = 128;  // prefix positions per direction scanned with the parallel path
 
-struct CatScratch {
-  double ctr[kFindMaxCatBins];
-  int sorted[kFindMaxCatBins];
+template <int CAP>
+struct CatScratchT {
+  static constexpr int kCap = CAP;
+  double ctr[CAP];
+  int sorted[CAP];
   int used_bin;
+  uint32_t bits[kMaxCatWords];  // the winner's category set, built here and published word-parallel
+  int ok, best_thr, best_dir;
   // parallel prefix scan: per direction and position, the bin's then the cumulative
   // (g, h, count) and the split gain there
   double pg[2][kCatPar], ph[2][kCatPar], gain[2][kCatPar];
@@ -468,9 +473,48 @@ struct CatScratch {
 // computed in parallel -- and the sequential prefix scan from both ends (<= 2 x
 // max_cat_threshold steps, thread 0) with the min_data_per_group rules.
 // returns splittable (meaningful in thread 0)
-template <int NT>
+// the candidates' stable order by ctr for wide features: a bitonic sort of (ctr, bin) pairs
+// in LDS (the ctr array holds the keys in bin order on entry; non-candidates, NaN, sort last).
+// (ctr, bin) is a total order, so the result equals std::stable_sort by ctr.
+template <int NT, typename CS>
+__device__ __forceinline__ void CatBitonicOrder(CS* cs, int bin_start, int n) {
+  int P = 1;
+  while (P < n) P <<= 1;
+  for (int i = threadIdx.x; i < P; i += NT) {
+    if (i >= n) cs->ctr[i] = INFINITY;
+    cs->sorted[i] = i < n ? bin_start + i : 0x7fffffff;
+  }
+  for (int i = threadIdx.x; i < n; i += NT) {
+    if (cs->ctr[i] != cs->ctr[i]) {  // non-candidate: after every candidate and the padding's order
+      cs->ctr[i] = INFINITY;
+      cs->sorted[i] = (1 << 30) + bin_start + i;
+    }
+  }
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += NT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const double ka = cs->ctr[i], kb = cs->ctr[ixj];
+          const int ia = cs->sorted[i], ib = cs->sorted[ixj];
+          const bool a_gt = ka > kb || (ka == kb && ia > ib);
+          if (a_gt == ((i & k) == 0)) {
+            cs->ctr[i] = kb;
+            cs->ctr[ixj] = ka;
+            cs->sorted[i] = ib;
+            cs->sorted[ixj] = ia;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <int NT, typename CS>
 __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
-                                     FeatureBest* out, uint32_t* cat_out, BlockScratch<NT>* sc, CatScratch* cs) {
+                                     FeatureBest* out, uint32_t* cat_out, BlockScratch<NT>* sc, CS* cs) {
   constexpr int kFindThreads = NT;
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
@@ -542,24 +586,30 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
   } else {
     l2 += p.cat_l2;
     // candidates and their ctr; non-candidates get NaN (never ranked)
+    const bool wide = CS::kCap > kFindCatNarrow && bin_end - bin_start > kFindCatNarrow;
+    int ncand = 0;
     for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
       const double hh = hv.H(t);
       const bool cand = static_cast<double>(RoundIntD(hh * L.cnt_factor)) >= p.cat_smooth;
-      cs->ctr[t] = cand ? hv.G(t) / (hh + p.cat_smooth) : NAN;
+      const double c = cand ? hv.G(t) / (hh + p.cat_smooth) : NAN;
+      cs->ctr[wide ? t - bin_start : t] = c;
+      ncand += c == c ? 1 : 0;
     }
     __syncthreads();
-    // stable rank among the candidates (std::stable_sort by ctr ascending)
-    int ncand = 0;
-    for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
-      const double c = cs->ctr[t];
-      if (c != c) continue;
-      ++ncand;
-      int r = 0;
-      for (int u = bin_start; u < bin_end; ++u) {
-        const double cu = cs->ctr[u];
-        r += (cu < c) | ((cu == c) & (u < t));
+    if (wide) {
+      CatBitonicOrder<NT>(cs, bin_start, bin_end - bin_start);
+    } else {
+      // stable rank among the candidates (std::stable_sort by ctr ascending)
+      for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
+        const double c = cs->ctr[t];
+        if (c != c) continue;
+        int r = 0;
+        for (int u = bin_start; u < bin_end; ++u) {
+          const double cu = cs->ctr[u];
+          r += (cu < c) | ((cu == c) & (u < t));
+        }
+        cs->sorted[r] = t;
       }
-      cs->sorted[r] = t;
     }
     double d0 = 0.0, d1 = 0.0;
     BlockSum3(d0, d1, ncand, sc);
@@ -667,6 +717,29 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
       cs->used_bin = used_bin;
     }
   }
+  // the winner's category set (thread 0's decision), in LDS, then published by every thread
+  if (tid == 0) {
+    cs->ok = splittable ? 1 : 0;
+    cs->best_thr = best.thr;
+    cs->best_dir = best_dir;
+  }
+  __syncthreads();
+  if (cs->ok) {
+    for (int w = tid; w < kMaxCatWords; w += kFindThreads) cs->bits[w] = 0u;
+    __syncthreads();
+    const int k = onehot ? 1 : cs->best_thr + 1;
+    for (int i = tid; i < k; i += kFindThreads) {
+      const int b = (onehot ? cs->best_thr : cs->best_dir == 1 ? cs->sorted[i] : cs->sorted[cs->used_bin - 1 - i]) + offset;
+      atomicOr(&cs->bits[b >> 5], 1u << (b & 31));
+    }
+    __syncthreads();
+    GlobalU64* dst = (GlobalU64*)(cat_out);
+    for (int w = tid; w < kMaxCatWords / 2; w += kFindThreads) {
+      const unsigned long long v = static_cast<unsigned long long>(cs->bits[2 * w]) |
+                                   (static_cast<unsigned long long>(cs->bits[2 * w + 1]) << 32);
+      __hip_atomic_store(dst + w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (tid != 0 || !splittable) return splittable;
   out->lo = LeafOutputConstrained(best.lg, best.lh, l2, p, L.c, best.lc, L.parent_out);
   out->lc = best.lc;
@@ -677,21 +750,7 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
   out->rg = L.sg - best.lg;
   out->rh = L.sh - best.lh - kEpsilon;
   out->gain = (best.gain - min_gain_shift) * F.penalty;
-  CatWords bits;  // (published whole: the picking workgroup reads the winner's set)
-  for (int w = 0; w < kMaxCatWords; ++w) bits.w[w] = 0u;
-  if (onehot) {
-    const int b = best.thr + offset;
-    bits.w[b >> 5] |= 1u << (b & 31);
-    out->ncat = 1;
-  } else {
-    const int k = best.thr + 1;
-    for (int i = 0; i < k; ++i) {
-      const int b = (best_dir == 1 ? cs->sorted[i] : cs->sorted[cs->used_bin - 1 - i]) + offset;
-      bits.w[b >> 5] |= 1u << (b & 31);
-    }
-    out->ncat = k;
-  }
-  PublishRecord(reinterpret_cast<CatWords*>(cat_out), bits);
+  out->ncat = onehot ? 1 : best.thr + 1;
   return true;
 }
 

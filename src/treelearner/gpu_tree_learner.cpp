@@ -550,6 +550,8 @@ void GPUTreeLearner::UploadData() {
     if (feats[f].is_cat) cats.push_back(f);
   }
   a.p.has_cat = static_cast<int32_t>(cats.size());
+  a.p.wide_cat = 0;
+  for (int f : cats) a.p.wide_cat |= feats[f].num_bin > dev::kFindCatNarrow ? 1 : 0;
   d_cat_list_ = Alloc<int32_t>(std::max<size_t>(1, cats.size()));
   if (!cats.empty()) {
     HIPCHECK(hipMemcpy(d_cat_list_, cats.data(), sizeof(int32_t) * cats.size(), hipMemcpyHostToDevice));
@@ -2432,6 +2434,12 @@ void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
       split_stale_ = false;
       return;
     }
+    AddTreeToScore(tree, k);
+    return;
+  }
+  if (!device_mode_) {
+    // host-assisted growth keeps the leaves' row ranges on the host (the device leaf records
+    // are the last device-resident tree's): walk the tree for every row instead
     AddTreeToScore(tree, k);
     return;
   }

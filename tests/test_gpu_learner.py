@@ -242,6 +242,67 @@ def test_categorical_splits_on_device(gpu_available):
     assert auc_g > 0.85 and abs(auc_c - auc_g) < 2e-3
 
 
+def _cat_splits(node):
+    if "split_feature" not in node:
+        return []
+    return ([(node["split_feature"], node["decision_type"], str(node["threshold"]), node["internal_count"])]
+            + _cat_splits(node["left_child"]) + _cat_splits(node["right_child"]))
+
+
+@pytest.mark.parametrize("extra", [{}, {"max_cat_threshold": 64, "cat_smooth": 1, "min_data_per_group": 20}],
+                         ids=["default", "wide_sets"])
+def test_wide_categorical_on_device(gpu_available, monkeypatch, capfd, extra):
+    """A categorical feature with more than 1024 bins (here ~2500 categories) is scanned on the
+    device by the wide categorical kernel (bitonic ctr order in LDS, 4096-bin category sets):
+    device-resident growth, and the trees equal host-assisted growth's (host split finder)."""
+    rng = np.random.RandomState(31)
+    n, ncat = 200000, 2500
+    X = rng.randn(n, 5).astype(np.float32)
+    X[:, 0] = rng.randint(0, ncat, size=n)
+    eff = rng.randn(ncat)
+    y = ((1.2 * eff[X[:, 0].astype(int)] + X[:, 1] + 0.5 * rng.randn(n)) > 0).astype(np.float32)
+    params = dict({"objective": "binary", "num_leaves": 31, "verbose": -1, "device_type": "gpu",
+                   "max_bin": 255}, **extra)
+    capfd.readouterr()
+    ds = lgb.Dataset(X, y, params=params, categorical_feature=[0])
+    models = {"device": lgb.train(dict(params, verbose=2), ds, 5, verbose_eval=False)}
+    log = capfd.readouterr().out
+    assert "device-resident growth" in log and "host-assisted growth" not in log
+    monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    ds = lgb.Dataset(X, y, params=params, categorical_feature=[0])
+    models["host"] = lgb.train(params, ds, 5, verbose_eval=False)
+    monkeypatch.delenv("LGBM_AMD_HOST_ASSIST", raising=False)
+    dt = models["device"].dump_model()["tree_info"]
+    ht = models["host"].dump_model()["tree_info"]
+    assert any(len(str(nd[2]).split("||")) > 1 for t in dt for nd in _cat_splits(t["tree_structure"])
+               if nd[1] == "==")
+    for i in range(len(dt)):
+        assert _cat_splits(dt[i]["tree_structure"]) == _cat_splits(ht[i]["tree_structure"]), i
+    binned = models["device"].dump_model()
+    assert binned["tree_info"][0]["num_cat"] > 0
+
+
+def test_host_assisted_scores_wide_groups(gpu_available, monkeypatch):
+    """Host-assisted growth on 16-bit storage groups (a 300-category feature): the training
+    scores follow the trees (the leaves' row ranges live on the host there, so the score
+    update walks the tree) -- the recorded training loss equals the model's own."""
+    rng = np.random.RandomState(32)
+    n = 60000
+    X = rng.randn(n, 4).astype(np.float32)
+    X[:, 0] = rng.randint(0, 300, size=n)
+    eff = rng.randn(300)
+    y = ((eff[X[:, 0].astype(int)] + X[:, 1] + 0.5 * rng.randn(n)) > 0).astype(np.float32)
+    monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    params = {"objective": "binary", "num_leaves": 15, "verbose": -1, "device_type": "gpu",
+              "metric": "binary_logloss"}
+    ds = lgb.Dataset(X, y, params=params, categorical_feature=[0])
+    ev = {}
+    bst = lgb.train(params, ds, 3, valid_sets=[ds], valid_names=["train"], evals_result=ev, verbose_eval=False)
+    p = np.clip(bst.predict(X), 1e-15, 1 - 1e-15)
+    ll = float(-np.mean(y * np.log(p) + (1 - y) * np.log(1 - p)))
+    assert abs(ev["train"]["binary_logloss"][-1] - ll) < 1e-9
+
+
 def test_validation_scores_on_device(gpu_available):
     """Validation sets are scored on the device (one traversal kernel per tree): the recorded
     metric equals the metric of the booster's own predictions, and early stopping works."""
