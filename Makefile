@@ -17,7 +17,7 @@ CXXFLAGS ?= -O3 -std=c++17 -fPIC -fopenmp -Wall -Wno-unused-function -Wno-sign-c
 # at once instead of when its result is used
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Iinclude -munsafe-fp-atomics -mllvm -amdgpu-atomic-optimizer-strategy=None -Wno-unused-result
 HIPEXTRA ?=
-LDFLAGS := -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -Wl,-rpath,$(ROCM)/lib
+LDFLAGS := -shared -fopenmp -L$(ROCM)/lib -lamdhip64 -lrccl -ldl -Wl,-rpath,$(ROCM)/lib
 
 HOST_SRCS := $(filter-out src/cli/main.cpp,$(shell find src -name '*.cpp'))
 DEV_SRCS := $(shell find src -name '*.hip')

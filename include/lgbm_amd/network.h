@@ -202,4 +202,12 @@ std::vector<std::shared_ptr<DeviceComm>> MakePeerThreadComms(int num_ranks, doub
 // ... or one process per GPU: windows exchanged as hipIpc handles over the host Network
 std::shared_ptr<DeviceComm> MakePeerIpcComm(int device_id, double timeout_s = 0);
 
+// MPI host transport (src/network/mpi_transport.cpp; reference linkers_mpi.cpp), the MPI library
+// opened at run time: Network::Init uses it instead of the TCP mesh when LGBM_AMD_NETWORK=mpi.
+// The CLI finalizes MPI at a normal exit (when this process initialised it) and aborts it after
+// an error, so that no peer stays blocked in a collective.
+bool MpiSelected();
+void MpiFinalizeIfStarted();
+void MpiAbortIfStarted();
+
 }  // namespace lgbm_amd

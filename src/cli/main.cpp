@@ -252,7 +252,9 @@ int main(int argc, char** argv) {
   }
   if (!success) {
     Network::Dispose();
+    MpiAbortIfStarted();
     return 1;
   }
+  MpiFinalizeIfStarted();
   return 0;
 }

@@ -17,6 +17,7 @@
 namespace lgbm_amd {
 
 std::shared_ptr<HostTransport> MakeTcpTransport(const Config& cfg);  // tcp_transport.cpp
+std::shared_ptr<HostTransport> MakeMpiTransport(const Config& cfg);  // mpi_transport.cpp
 
 namespace {
 
@@ -218,7 +219,7 @@ std::vector<std::shared_ptr<HostTransport>> MakeThreadTransports(int num_ranks, 
 
 void Network::Init(const Config& cfg) {
   if (cfg.num_machines <= 1) return;
-  State().transport = MakeTcpTransport(cfg);
+  State().transport = MpiSelected() ? MakeMpiTransport(cfg) : MakeTcpTransport(cfg);
   Log::Info("Local rank: %d, total number of machines: %d", rank(), num_machines());
 }
 

@@ -4,7 +4,9 @@
 MODE "collectives": runs allgather / reduce-scatter / all-reduce checks and writes
 OUT_DIR/coll_<rank>.json; "train": trains a data-parallel model and writes
 OUT_DIR/model_<rank>.txt; "die": joins the mesh and exits at once (peer failure);
-"survive": joins, then trains -- it must fail with an error, not hang or abort.
+"survive": joins, then trains -- it must fail with an error, not hang or abort;
+"train_mpi": like "train" over the MPI transport (LGBM_AMD_NETWORK=mpi in the environment,
+MACHINES only gives the world size).
 """
 import json
 import os
@@ -56,10 +58,27 @@ def train(rank, world, machines, port, out_dir):
         f.write(bst.model_to_string())
 
 
+def train_mpi(rank, world, out_dir):
+    nat.call("LGBM_NetworkInit", nat.cstr(""), nat.c_int(0), nat.c_int(1), nat.c_int(world))
+    assert host.world() == (rank, world), host.world()
+    X, y = make_data()
+    idx = np.arange(rank, X.shape[0], world)
+    params = {"objective": "binary", "num_leaves": 15, "verbose": -1, "tree_learner": "data",
+              "num_machines": world, "pre_partition": True, "min_data_in_leaf": 20, "seed": 3,
+              "deterministic": True, "num_threads": 2}
+    bst = lgb.train(params, lgb.Dataset(X[idx], y[idx], params=params), 8)
+    with open(os.path.join(out_dir, "model_mpi_%d.txt" % rank), "w") as f:
+        f.write(bst.model_to_string())
+    nat.call("LGBM_NetworkFree")
+
+
 def main():
     mode, rank, machines, out_dir = sys.argv[1], int(sys.argv[2]), sys.argv[3], sys.argv[4]
     ports = [int(m.split(":")[1]) for m in machines.split(",")]
     world = len(ports)
+    if mode == "train_mpi":
+        train_mpi(rank, world, out_dir)
+        return
     if mode == "train":
         train(rank, world, machines, ports[rank], out_dir)
         return

@@ -64,11 +64,12 @@ def _free_ports(n):
     return ports
 
 
-def _spawn(modes, tmp_path, timeout=120):
+def _spawn(modes, tmp_path, timeout=120, rank_env=None):
     ports = _free_ports(len(modes))
     machines = ",".join("127.0.0.1:%d" % p for p in ports)
     env = dict(os.environ, OMP_NUM_THREADS="2")
-    procs = [subprocess.Popen([sys.executable, WORKER, m, str(r), machines, str(tmp_path)], env=env,
+    procs = [subprocess.Popen([sys.executable, WORKER, m, str(r), machines, str(tmp_path)],
+                              env=dict(env, **(rank_env(r) if rank_env else {})),
                               stdout=subprocess.PIPE, stderr=subprocess.STDOUT) for r, m in enumerate(modes)]
     outs = []
     for p in procs:
@@ -104,3 +105,48 @@ def test_tcp_peer_failure_raises_on_survivor(tmp_path):
     assert outs[0][0] == 0, outs[0][1]
     text = open(tmp_path / "survivor_0.txt").read()
     assert text.startswith("error:") and "rank 1" in text, text
+
+
+FAKE_MPI = os.path.join(os.path.dirname(__file__), "native", "fake_mpi.c")
+
+
+def _fake_mpi(tmp_path):
+    lib = str(tmp_path / "libfakempi.so")
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-O1", "-o", lib, FAKE_MPI])
+    return lib
+
+
+def test_mpi_transport_data_parallel_training(tmp_path):
+    """The MPI transport (reference linkers_mpi.cpp) over a file-backed MPICH-ABI stand-in
+    library (tests/native/fake_mpi.c; no MPI is installed here): two processes train
+    data-parallel with LGBM_AMD_NETWORK=mpi and no machine list, and produce the same trees
+    as each other and as the same run over the TCP mesh."""
+    lib = _fake_mpi(tmp_path)
+    mpi_dir = tmp_path / "mpi"
+    mpi_dir.mkdir()
+    env = lambda r: {"LGBM_AMD_NETWORK": "mpi", "LGBM_AMD_MPI_LIB": lib, "FAKE_MPI_RANK": str(r),
+                     "FAKE_MPI_SIZE": "2", "FAKE_MPI_DIR": str(mpi_dir)}
+    outs = _spawn(["train_mpi"] * 2, tmp_path, rank_env=env)
+    assert all(rc == 0 for rc, _ in outs), outs
+    assert not list(mpi_dir.glob("m_*")), "undelivered MPI messages"
+    outs = _spawn(["train"] * 2, tmp_path)
+    assert all(rc == 0 for rc, _ in outs), outs
+    tree = lambda m: m[m.index("Tree=0"):m.index("end of trees")]
+    mpi = [tree(open(tmp_path / ("model_mpi_%d.txt" % r)).read()) for r in range(2)]
+    tcp = tree(open(tmp_path / "model_0.txt").read())
+    assert mpi[0] == mpi[1] == tcp
+
+
+def test_mpi_transport_missing_library_raises(tmp_path):
+    code = ("import lightgbmv1_amd as lgb\n"
+            "from lightgbmv1_amd import _native as nat\n"
+            "try:\n"
+            "    nat.call('LGBM_NetworkInit', nat.cstr(''), nat.c_int(0), nat.c_int(1), nat.c_int(2))\n"
+            "    print('no error')\n"
+            "except lgb.LightGBMError as e:\n"
+            "    print('error:', e)\n")
+    env = dict(os.environ, LGBM_AMD_NETWORK="mpi", LGBM_AMD_MPI_LIB=str(tmp_path / "nope.so"),
+               PYTHONPATH=os.path.join(os.path.dirname(__file__), ".."))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    assert "error:" in out.stdout and "no MPI library" in out.stdout, out.stdout
