@@ -150,8 +150,12 @@ struct FindShared {
 
 // the scan of one (feature, child) by one workgroup: every thread of the workgroup takes the
 // same path (the kernel's pick tail needs all of them)
+// side: the child (0: the smaller one); d0_in / drew: categorical extra_trees only -- the draws
+// the smaller child's scan of this feature consumed, and this scan's (see k_find)
 template <bool ROOT, int KIND, bool SIMPLE, int NT>
-__device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND, NT>& sh) {
+__device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindShared<ROOT, KIND, NT>& sh, const int side,
+                                         const int d0_in, int* drew) {
+  if (drew != nullptr) *drew = 0;
   constexpr bool CAT = KIND >= 2;  // (3: the wide categorical variant)
   constexpr int kFindThreads = NT;
   const long long t_entry = wall_clock64();
@@ -162,7 +166,6 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   if (vote_global) f = a.vote_list[blockIdx.y * a.p.vote_k + blockIdx.x];
   const bool vote_empty = vote_global && f < 0;
   if (vote_empty) f = 0;
-  const int side = blockIdx.y;
   const int tid = threadIdx.x;
   const int units = a.hist_units;
   // ---- independent loads first (one round trip): the feature, its mask, the scales and the
@@ -224,7 +227,14 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   // (SerialTreeLearner::FindBestSplitsFromHistograms); draw k of the tree is the base state
   // stepped k times.  The smaller child's workgroup appends the step's count row.
   int xt_thr = kNoRandThr;
-  if (a.xt_base != nullptr) {
+  uint32_t xt_r = 0u;
+  if (a.xt_base != nullptr && CAT) {
+    // categorical: whether a scan draws depends on its histogram (the sorted scan's
+    // max_threshold), so k_find scans both children in one workgroup, the smaller one first,
+    // and appends the step's count row itself
+    const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * a.p.num_features + f];
+    xt_r = LcgSkip(a.xt_base[f], prev + (side == 1 ? d0_in : 0) + 1) & 0x7fffffffu;
+  } else if (a.xt_base != nullptr) {
     const int nf = a.p.num_features;
     const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * nf + f];
     const bool gate = tree_used && parent_ok && !skip;
@@ -486,7 +496,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     bool splittable;
     if constexpr (CAT) {
       splittable = FindCategoricalBlock(F, hv, L, p, &o, a.feat_cat + FeatBestIndex(a, side, f) * kMaxCatWords, &sh.sc,
-                                        &sh.cat_sc);
+                                        &sh.cat_sc, a.xt_base != nullptr, xt_r, drew);
     } else {
       splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc, sh.sc2,
                                               xt_thr);
@@ -548,7 +558,27 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   __shared__ int s_last;
   Step* st = a.st;
   if (!ROOT && st->done) return;
-  FindBody<ROOT, KIND, SIMPLE, NT>(a, s_bins, sh);
+  if (KIND >= 2 && a.xt_base != nullptr) {
+    // categorical extra_trees: the larger child's draw follows the smaller child's, whose count
+    // depends on its histogram -- workgroup (f, 0) scans both children in order and appends the
+    // feature's count row (over the numerical kernel's); workgroups (f, 1) only arrive
+    if (blockIdx.y == 0) {
+      int d0 = 0, d1 = 0;
+      FindBody<ROOT, KIND, SIMPLE, NT>(a, s_bins, sh, 0, 0, &d0);
+      if (!ROOT) {
+        __syncthreads();
+        FindBody<ROOT, KIND, SIMPLE, NT>(a, s_bins, sh, 1, d0, &d1);
+      }
+      if (threadIdx.x == 0) {
+        const int nf = a.p.num_features, f = a.cat_list[blockIdx.x];
+        const int s = ROOT ? 0 : st->cs.s;
+        const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * nf + f];
+        a.xt_cum[static_cast<size_t>(ROOT ? 0 : s + 1) * nf + f] = prev + d0 + d1;
+      }
+    }
+  } else {
+    FindBody<ROOT, KIND, SIMPLE, NT>(a, s_bins, sh, blockIdx.y, 0, nullptr);
+  }
   // single process: the last workgroup of the step records it and picks the next split
   // (with categorical features the numerical kernel runs first and does not count)
   if (!a.pick_in_find || (KIND == 1)) return;

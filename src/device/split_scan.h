@@ -514,7 +514,8 @@ __device__ __forceinline__ void CatBitonicOrder(CS* cs, int bin_start, int n) {
 
 template <int NT, typename CS>
 __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p,
-                                     FeatureBest* out, uint32_t* cat_out, BlockScratch<NT>* sc, CS* cs) {
+                                     FeatureBest* out, uint32_t* cat_out, BlockScratch<NT>* sc, CS* cs,
+                                     bool xt = false, uint32_t xt_r = 0u, int* drew = nullptr) {
   constexpr int kFindThreads = NT;
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
@@ -559,7 +560,18 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
   best.lg = best.lh = 0.0;
   best.lc = 0;
   int best_dir = 1;
+  // extra_trees (xt): the feature's next draw xt_r (31 bits) picks the one threshold evaluated,
+  // NextInt(bin_start, bin_end) one-vs-rest, NextInt(0, max_threshold) sorted -- drawn only when
+  // the range is not empty (*drew: whether this scan consumed a draw); without a draw the
+  // threshold stays 0, as in the reference
+  if (drew != nullptr) *drew = 0;
   if (onehot) {
+    int rthr = -1;
+    if (xt) {
+      const bool d = bin_end - bin_start > 0;
+      rthr = d ? bin_start + static_cast<int>(xt_r % static_cast<uint32_t>(bin_end - bin_start)) : 0;
+      if (drew != nullptr) *drew = d ? 1 : 0;
+    }
     bool any = false;
     for (int t = bin_start + tid; t < bin_end; t += kFindThreads) {
       const double g = hv.G(t), hh = hv.H(t);
@@ -570,6 +582,7 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
       const double oh = L.sh - hh - kEpsilon;
       if (oh < min_h) continue;
       const double og = L.sg - g;
+      if (rthr >= 0 && t != rthr) continue;
       const double gain = SplitGain(og, oh, g, hh + kEpsilon, l2, p, L.c, 0, other, cnt, L.parent_out);
       if (gain <= min_gain_shift) continue;
       any = true;
@@ -616,6 +629,12 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
     const int used_bin = ncand;
     const int max_num_cat = min(p.max_cat_threshold, (used_bin + 1) / 2);
     const int npos = min(used_bin, max_num_cat);
+    int rthr = -1;
+    if (xt) {
+      const int mt = max(npos - 1, 0);
+      rthr = mt > 0 ? static_cast<int>(xt_r % static_cast<uint32_t>(mt)) : 0;
+      if (drew != nullptr) *drew = mt > 0 ? 1 : 0;
+    }
     if (npos <= kCatPar) {
       // (1) every thread stages one position's bin statistics, (2) one thread per direction
       // accumulates the prefix sums in the sequential order (bit-identical sums), (3) every
@@ -663,6 +682,7 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
             if (L.sh - lh < min_h) break;
             if (cnt_group < p.min_data_per_group) continue;
             cnt_group = 0;
+            if (rthr >= 0 && i != rthr) continue;
             const double gain = cs->gain[o][i];
             if (gain <= min_gain_shift) continue;
             splittable = true;
@@ -700,6 +720,7 @@ __device__ __forceinline__ bool FindCategoricalBlock(const Feature& F, HistView 
           if (rh < min_h) break;
           if (cnt_group < p.min_data_per_group) continue;
           cnt_group = 0;
+          if (rthr >= 0 && i != rthr) continue;
           const double rg = L.sg - lg;
           const double gain = SplitGain(lg, lh, rg, rh, l2, p, L.c, 0, lc, rc, L.parent_out);
           if (gain <= min_gain_shift) continue;

@@ -872,9 +872,10 @@ void GPUTreeLearner::DecideMode() {
     if (m->bin_type() == BinType::Categorical) any_cat = true;
     if (m->bin_type() == BinType::Categorical && m->num_bin() > dev::kFindMaxCatBins) dm = false;
   }
-  // extra_trees: random numerical thresholds are drawn on the device (categorical draws
-  // depend on the sorted-category scan: host-assisted then)
-  if (config_->extra_trees && any_cat) dm = false;
+  // extra_trees: random thresholds are drawn on the device (categorical ones by the workgroup
+  // that scans both children of the feature in order); the distributed learners keep
+  // categorical draws host-assisted
+  if (config_->extra_trees && any_cat && distributed_) dm = false;
   // interaction constraints: on the device up to 64 constraints without per-node sampling
   // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
   const auto& ic = config_->interaction_constraints_vector;

@@ -498,6 +498,37 @@ def test_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
     assert abs(_auc(y, models["device"].predict(X)) - _auc(y, cpu.predict(X))) < 0.01
 
 
+@pytest.mark.parametrize("extra", [{}, {"feature_fraction_bynode": 0.7, "feature_fraction_seed": 4},
+                                   {"max_cat_threshold": 3, "cat_smooth": 1, "min_data_per_group": 10}],
+                         ids=["plain", "bynode", "few_thresholds"])
+def test_categorical_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
+    """extra_trees with categorical features grows device-resident: one-vs-rest features draw
+    NextInt(bin_start, bin_end), sorted ones NextInt(0, max_threshold) only when that range is
+    not empty -- a count that depends on the child's histogram, so one workgroup scans both
+    children of a categorical feature in order (reference feature_histogram.hpp:314-401).  The
+    trees equal host-assisted growth's tree for tree (the generators stay in step)."""
+    X, y = _cat_data(30000, seed=21)
+    params = dict({"objective": "binary", "num_leaves": 31, "verbose": -1, "device_type": "gpu",
+                   "extra_trees": True, "extra_seed": 5, "max_cat_to_onehot": 4, "min_data_per_group": 50,
+                   "cat_smooth": 5, "seed": 2}, **extra)
+    capfd.readouterr()
+    small = dict(params, verbose=2)
+    lgb.train(small, lgb.Dataset(X[:4000], y[:4000], params=small, categorical_feature=[0, 1]), 1)
+    assert "device-resident growth" in capfd.readouterr().out
+    models = {}
+    for mode in ("device", "host"):
+        if mode == "host":
+            monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+        models[mode] = lgb.train(params, lgb.Dataset(X, y, params=params, categorical_feature=[0, 1]), 8)
+        monkeypatch.delenv("LGBM_AMD_HOST_ASSIST", raising=False)
+    dt = models["device"].dump_model()["tree_info"]
+    ht = models["host"].dump_model()["tree_info"]
+    assert len(dt) == len(ht)
+    for i in range(len(dt)):
+        assert _cat_splits(dt[i]["tree_structure"]) == _cat_splits(ht[i]["tree_structure"]), i
+    assert any(t["num_cat"] > 0 for t in dt)
+
+
 @pytest.mark.parametrize("case", ["small", "wide"])
 def test_intermediate_monotone_on_gpu(case, gpu_available, monkeypatch, capfd):
     """monotone_constraints_method=intermediate grows device-resident: the pick walks the tree
