@@ -21,6 +21,13 @@ struct KArgs {
   const int32_t* group_off;  // [num_groups] first histogram bin of each storage column
   const int8_t* tree_mask;   // [num_features] feature used by this tree
   const int8_t* node_mask;   // [2 * num_leaves - 1][num_features] per-node samples (feature_fraction_bynode), or null
+  // per-node sampling under interaction constraints (bynode_rng non-null; k_bynode_step draws
+  // the children's node_mask rows): the tree's node pool (inner features in the host sampler's
+  // order), the sample size before filtering, the generator state, a [num_features] scratch
+  const int32_t* bynode_pool;
+  int32_t bynode_pool_n, bynode_cnt;
+  uint32_t* bynode_rng;
+  int32_t* bynode_scratch;
   const GH* gh;              // interleaved (gradient, hessian) per row
   int32_t* idx;              // partition index buffer 0 (root rows)
   int32_t* tmp;              // partition index buffer 1 (leaves alternate: Leaf::buf), then 2.. at buf_stride
@@ -273,6 +280,8 @@ inline size_t MonoInterLds(int num_leaves) {
   return static_cast<size_t>(num_leaves + 1) * (20 * sizeof(int32_t) + 2 * sizeof(double));
 }
 void CegbStep(const KArgs& a, hipStream_t s);
+// interaction constraints + feature_fraction_bynode: the step's two node masks (bynode_kernels.hip)
+void ByNodeStep(const KArgs& a, hipStream_t s);
 void FindStep(const KArgs& a, hipStream_t s);
 // the step's bookkeeping and the next pick as a kernel of its own (distributed learners:
 // it runs after the per-feature results were gathered from every rank)

@@ -134,6 +134,24 @@ class ColSampler {
     for (int c = 0; c < calls; ++c) (void)GetByNode(nullptr, 0);
   }
 
+  // the device's by-node sampling under interaction constraints (bynode_kernels.hip): the
+  // tree's node pool as inner features in GetByNode's order, the sample size before the
+  // constraint filter, and the generator state (read before, set after a device tree)
+  std::vector<int32_t> NodePoolInner() const {
+    std::vector<int32_t> out;
+    if (need_reset_tree_) {
+      for (int fi : used_idx_) out.push_back(data_->InnerFeatureIndex(valid_[fi]));
+    } else {
+      for (int f : valid_) out.push_back(data_->InnerFeatureIndex(f));
+    }
+    return out;
+  }
+  int NodeSampleCount() const {
+    return GetCnt(need_reset_tree_ ? used_idx_.size() : valid_.size(), frac_node_);
+  }
+  uint32_t rng_state() const { return rnd_.state(); }
+  void set_rng_state(uint32_t x) { rnd_ = Random(static_cast<int>(x)); }
+
   const std::vector<int8_t>& is_feature_used_bytree() const { return used_; }
   bool has_interaction_constraints() const { return !constraints_.empty(); }
   bool need_by_node() const { return frac_node_ < 1.0f || !constraints_.empty(); }

@@ -352,6 +352,9 @@ void GPUTreeLearner::UploadData() {
   d_tree_mask_ = Alloc<int8_t>(num_features_);
   d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
   h_node_mask_.clear();
+  d_bynode_pool_ = Alloc<int32_t>(std::max(1, num_features_));
+  d_bynode_scratch_ = Alloc<int32_t>(std::max(1, num_features_));
+  d_bynode_rng_ = Alloc<uint32_t>(1);
   d_xt_base_ = Alloc<uint32_t>(std::max(1, num_features_));
   d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
   if (d_gh_ == nullptr) d_gh_ = Alloc<dev::GH>(num_data_);
@@ -474,6 +477,11 @@ void GPUTreeLearner::UploadData() {
   a.group_off = d_group_off_;
   a.tree_mask = d_tree_mask_;
   a.node_mask = nullptr;
+  a.bynode_pool = d_bynode_pool_;
+  a.bynode_pool_n = 0;
+  a.bynode_cnt = 0;
+  a.bynode_rng = nullptr;
+  a.bynode_scratch = d_bynode_scratch_;
   a.gh = d_gh_;
   a.idx = d_idx_;
   a.tmp = d_tmp_;
@@ -876,10 +884,13 @@ void GPUTreeLearner::DecideMode() {
   // that scans both children of the feature in order); the distributed learners keep
   // categorical draws host-assisted
   if (config_->extra_trees && any_cat && distributed_) dm = false;
-  // interaction constraints: on the device up to 64 constraints without per-node sampling
-  // (ColSampler::GetByNode samples from the allowed set: host-assisted then)
+  // interaction constraints: on the device up to 64 constraints; with per-node sampling the
+  // children's masks are drawn on the device after each partition (k_bynode_step; one process)
   const auto& ic = config_->interaction_constraints_vector;
-  if (!ic.empty() && (ic.size() > static_cast<size_t>(dev::kMaxIcConstraints) || config_->feature_fraction_bynode < 1.0)) dm = false;
+  if (!ic.empty() && (ic.size() > static_cast<size_t>(dev::kMaxIcConstraints) ||
+                      (config_->feature_fraction_bynode < 1.0 && distributed_))) {
+    dm = false;
+  }
   // intermediate monotone constraints re-bound leaves all over the tree after a split: the pick
   // walks the tree and the next split scan re-scans the re-bounded leaves (one process, one
   // split per step; with extra_trees draws, forced splits or more than kMonoInterMaxLeaves
@@ -1226,6 +1237,7 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
     }
     dev::SplitStep(a, stream_, s < a.p.direct_from_split || data_parallel_);
     if (a.cegb_lazy != nullptr) dev::CegbStep(a, stream_);
+    if (a.bynode_rng != nullptr) dev::ByNodeStep(a, stream_);
     ReduceScatterStep(s + 1);
     dev::FindStep(a, stream_);
     if (voting_) {
@@ -1550,7 +1562,24 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
   dev::KArgs a = args_;
   const bool bynode = config_->feature_fraction_bynode < 1.0;
-  if (bynode) {
+  const bool bynode_ic = bynode && col_sampler_.has_interaction_constraints();
+  if (bynode_ic) {
+    // the root's mask (no branch: every constraint's features) from a copy of the generator;
+    // the children's masks are drawn on the device from the state after it (k_bynode_step)
+    const Tree empty(2, true);
+    ColSampler copy(col_sampler_);
+    h_node_mask_ = copy.GetByNode(&empty, 0);
+    h_bynode_rng_ = copy.rng_state();
+    h_bynode_pool_ = col_sampler_.NodePoolInner();
+    HIPCHECK(hipMemcpyAsync(d_node_mask_, h_node_mask_.data(), h_node_mask_.size(), hipMemcpyHostToDevice, stream_));
+    HIPCHECK(hipMemcpyAsync(d_bynode_pool_, h_bynode_pool_.data(), sizeof(int32_t) * h_bynode_pool_.size(),
+                            hipMemcpyHostToDevice, stream_));
+    HIPCHECK(hipMemcpyAsync(d_bynode_rng_, &h_bynode_rng_, sizeof(uint32_t), hipMemcpyHostToDevice, stream_));
+    a.node_mask = d_node_mask_;
+    a.bynode_pool_n = static_cast<int32_t>(h_bynode_pool_.size());
+    a.bynode_cnt = col_sampler_.NodeSampleCount();
+    a.bynode_rng = d_bynode_rng_;
+  } else if (bynode) {
     // every GetByNode draw the tree can make (root + two per split), from a copy of the
     // generator; the draws actually made are replayed after the tree
     h_node_mask_ = col_sampler_.PeekByNodeMasks(2 * (config_->num_leaves - 1) + 1);
@@ -1619,7 +1648,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     if (use_graph) {
       const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
       if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
-          graph_root_mode_ != root_mode || graph_xt_ != (xt ? 1 : 0)) {
+          graph_root_mode_ != root_mode || graph_xt_ != (xt ? 1 : 0) + (bynode_ic ? 2 : 0)) {
         if (dcomm != nullptr) dcomm->HostBarrier();
         DestroyGraph();
         hipGraph_t g = nullptr;
@@ -1645,7 +1674,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
           graph_rows_ = a.num_rows;
           graph_identity_ = a.root_identity;
           graph_root_mode_ = root_mode;
-          graph_xt_ = xt ? 1 : 0;
+          graph_xt_ = (xt ? 1 : 0) + (bynode_ic ? 2 : 0);  // (the by-node kernels are part of the graph)
         }
       }
       if (graph_exec_ != nullptr) {
@@ -1675,7 +1704,15 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
     const bool root_scanned = h_step_->root_count >= 2 * config_->min_data_in_leaf;  // global count
-    col_sampler_.AdvanceByNode(root_scanned ? h_step_->bynode_next : 0);
+    if (bynode_ic) {
+      // the device generator went on from the root's draw: the host one takes its state
+      if (root_scanned) {
+        HIPCHECK(hipMemcpy(&h_bynode_rng_, d_bynode_rng_, sizeof(uint32_t), hipMemcpyDeviceToHost));
+        col_sampler_.set_rng_state(h_bynode_rng_);
+      }
+    } else {
+      col_sampler_.AdvanceByNode(root_scanned ? h_step_->bynode_next : 0);
+    }
   }
   if (xt && h_step_->root_count >= 2 * config_->min_data_in_leaf) {
     // replay the draws the split scans made: the rows are running counts, steps not run are 0

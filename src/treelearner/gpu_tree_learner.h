@@ -233,6 +233,13 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int32_t* d_cat_list_ = nullptr;       // categorical features (KArgs::cat_list)
   dev::IcMask* d_feat_icmask_ = nullptr;  // KArgs::feat_icmask
   std::vector<int8_t> h_node_mask_;     // (kept alive for the async upload)
+  // per-node sampling under interaction constraints (bynode_kernels.hip): node pool, generator
+  // state, scratch row
+  int32_t* d_bynode_pool_ = nullptr;
+  uint32_t* d_bynode_rng_ = nullptr;
+  int32_t* d_bynode_scratch_ = nullptr;
+  std::vector<int32_t> h_bynode_pool_;
+  uint32_t h_bynode_rng_ = 0;
   uint32_t* d_xt_base_ = nullptr;       // extra_trees: per-feature generator states, tree start
   int32_t* d_xt_cum_ = nullptr;         // extra_trees: draws per feature after each step
   std::vector<uint32_t> h_xt_base_;

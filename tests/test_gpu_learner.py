@@ -498,6 +498,38 @@ def test_extra_trees_device_resident(gpu_available, monkeypatch, capfd, extra):
     assert abs(_auc(y, models["device"].predict(X)) - _auc(y, cpu.predict(X))) < 0.01
 
 
+@pytest.mark.parametrize("extra", [
+    {"feature_fraction_bynode": 0.5},
+    {"feature_fraction_bynode": 0.25, "feature_fraction_seed": 3},
+    {"feature_fraction_bynode": 0.6, "feature_fraction": 0.8, "feature_fraction_seed": 8},
+], ids=["half", "quarter", "with_bytree"])
+def test_interaction_constraints_bynode_device_resident(gpu_available, monkeypatch, capfd, extra):
+    """Interaction constraints with feature_fraction_bynode grow device-resident: after each
+    partition k_bynode_step draws the two children's masks from the tree's used features that
+    the branch allows (reference col_sampler.hpp:91-162), both Random::Sample branches, from a
+    device generator whose state the host sampler takes after the tree.  Trees equal
+    host-assisted growth's (host ColSampler::GetByNode) tree for tree."""
+    X, y = _data(30000, seed=17)
+    params = dict({"objective": "binary", "num_leaves": 31, "max_bin": 63, "verbose": -1, "device_type": "gpu",
+                   "interaction_constraints": [[0, 1, 2, 3, 4, 5, 6, 7, 8, 9], [3, 5, 7, 10, 11, 12],
+                                               [1, 6, 13, 14, 15]], "seed": 4}, **extra)
+    capfd.readouterr()
+    small = dict(params, verbose=2)
+    lgb.train(small, lgb.Dataset(X[:4000], y[:4000], params=small), 1)
+    assert "device-resident growth" in capfd.readouterr().out
+    models = {}
+    for mode in ("device", "host"):
+        if mode == "host":
+            monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+        models[mode] = lgb.train(params, lgb.Dataset(X, y, params=params), 8)
+        monkeypatch.delenv("LGBM_AMD_HOST_ASSIST", raising=False)
+    dt = models["device"].dump_model()["tree_info"]
+    ht = models["host"].dump_model()["tree_info"]
+    assert len(dt) == len(ht)
+    for i in range(len(dt)):
+        assert _splits(dt[i]["tree_structure"]) == _splits(ht[i]["tree_structure"]), i
+
+
 @pytest.mark.parametrize("extra", [{}, {"feature_fraction_bynode": 0.7, "feature_fraction_seed": 4},
                                    {"max_cat_threshold": 3, "cat_smooth": 1, "min_data_per_group": 10}],
                          ids=["plain", "bynode", "few_thresholds"])
