@@ -2,6 +2,7 @@
 UndefinedBehaviorSanitizer (`make sanitize`, built by the first test that needs it, ~1 min on
 8 cores) trains the reference's example configs on the CPU learner; any ASan / UBSan report
 fails the test."""
+import fcntl
 import os
 import shutil
 import subprocess
@@ -14,9 +15,17 @@ EXAMPLES = "/root/reference/examples"
 
 
 def _build(target, path):
-    # (make is incremental: an up-to-date build returns at once, a stale one is rebuilt)
-    subprocess.run(["make", "-j" + str(min(8, os.cpu_count() or 4)), target], cwd=ROOT, check=True,
-                   capture_output=True, timeout=1500)
+    # (make is incremental: an up-to-date build returns at once, a stale one is rebuilt).  Under
+    # pytest-xdist several workers get here at once: an exclusive lock makes one build while the
+    # others wait, so none runs a binary another is still linking
+    os.makedirs(os.path.join(ROOT, "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "build", ".sanitize.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        try:
+            subprocess.run(["make", "-j" + str(min(8, os.cpu_count() or 4)), target], cwd=ROOT, check=True,
+                           capture_output=True, timeout=1500)
+        finally:
+            fcntl.flock(lock, fcntl.LOCK_UN)
     assert os.path.isfile(path), target
 
 
