@@ -354,7 +354,7 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
   // the normal pick above stands (reference ForceSplits' abort)
   if (s < a.forced_n && !a.st->forced_abort) {
     const FeatureBest& fb = a.forced_best[s];
-    if (fb.feature >= 0 && fb.gain > -INFINITY) {
+    if (fb.feature >= 0 && fb.gain > -INFINITY && fb.lc + fb.rc > 0) {  // (an all-zero record: nobody's)
       out->forced = 1;
       out->leaf = a.forced_leaf[s];
       pl->win_feature = fb.feature;

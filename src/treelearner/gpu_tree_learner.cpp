@@ -1252,6 +1252,12 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
 
 // the tree's root: row set, sums, histogram and split scan (+ the first pick / plan)
 void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
+  if (a.forced_n > 0) {
+    // every forced record starts the tree as zero words: a node whose leaf was not scanned this
+    // tree reads as invalid (no rows) instead of as the last tree's record
+    HIPCHECK(hipMemsetAsync(d_forced_best_, 0, sizeof(dev::FeatureBest) * a.forced_n, stream_));
+    HIPCHECK(hipMemsetAsync(d_forced_cat_, 0, sizeof(uint32_t) * kMaxCatWords * a.forced_n, stream_));
+  }
   if (use_bag_) {
     // the whole buffer: the copy (like the tree's graph) does not depend on the bag size
     HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * num_data_, hipMemcpyDeviceToDevice, stream_));
