@@ -150,3 +150,30 @@ def test_mpi_transport_missing_library_raises(tmp_path):
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr
     assert "error:" in out.stdout and "no MPI library" in out.stdout, out.stdout
+
+
+@pytest.mark.skipif(not os.path.isfile("/root/reference/examples/binary_classification/binary.train"),
+                    reason="reference examples not mounted")
+def test_mpi_transport_cli_finalizes(tmp_path):
+    """The CLI over the MPI transport (two processes, data-parallel, rows split by rank) trains,
+    writes the same model on both ranks and finalizes MPI at exit like the reference's main()
+    (the stand-in library records MPI_Finalize)."""
+    lib = _fake_mpi(tmp_path)
+    mpi_dir = tmp_path / "mpi"
+    mpi_dir.mkdir()
+    cli = os.path.join(os.path.dirname(lgb.__file__), "lib", "lightgbm")
+    data = "/root/reference/examples/binary_classification/binary.train"
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, OMP_NUM_THREADS="2", LGBM_AMD_NETWORK="mpi", LGBM_AMD_MPI_LIB=lib,
+                   FAKE_MPI_RANK=str(r), FAKE_MPI_SIZE="2", FAKE_MPI_DIR=str(mpi_dir))
+        args = [cli, "task=train", "data=" + data, "objective=binary", "num_trees=3", "num_leaves=15",
+                "tree_learner=data", "num_machines=2", "verbose=-1", "deterministic=true",
+                "output_model=" + str(tmp_path / ("m%d.txt" % r))]
+        procs.append(subprocess.Popen(args, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+    outs = [p.communicate(timeout=180)[0].decode("utf-8", "replace") for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs
+    models = [open(tmp_path / ("m%d.txt" % r)).read() for r in range(2)]
+    tree = lambda m: m[m.index("Tree=0"):m.index("end of trees")]
+    assert tree(models[0]) == tree(models[1])
+    assert all((mpi_dir / ("finalized_%d" % r)).exists() for r in range(2))
