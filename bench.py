@@ -67,6 +67,9 @@ def main():
                     help="fx32: 32-bit fixed-point (g, h) per row, packed in one 64-bit histogram word; "
                          "fx64 (gpu_use_dp): 2x 64-bit words, 31-bit row resolution")
     ap.add_argument("--params", default="{}", help="extra training parameters (JSON)")
+    ap.add_argument("--eval-train", action="store_true",
+                    help="evaluate the training AUC after every iteration inside the timed loop "
+                         "(valid_sets=[dtrain] cost; device-resident metric)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -107,8 +110,11 @@ def main():
     torch_dist.barrier()
     _device_sync(lgb)
     t1 = time.perf_counter()
+    train_auc = None
     for _ in range(args.steps):
         booster.update()
+        if args.eval_train:
+            train_auc = booster.eval_train()[0][2]
     _device_sync(lgb)
     torch_dist.barrier()
     elapsed = time.perf_counter() - t1
@@ -140,6 +146,7 @@ def main():
                        "parallelism": "dp{}".format(world) if world > 1 else "single"},
             "auc_heldout": auc,
             "trees": booster.num_trees(),
+            **({"train_auc": train_auc} if args.eval_train else {}),
             "setup_s": round(setup_s, 2),
         }), flush=True)
     if world > 1:

@@ -231,6 +231,7 @@ class GBDT {
   data_size_t DeviceBagging(bool goss);
   // metric j of validation set i: on the device when its scores live there, else on the host
   std::vector<double> EvalValid(int i, int j) const;
+  std::vector<double> EvalTrain(const Metric* m);  // device-resident training scores when possible
   std::vector<bool> class_need_train_;
   bool is_constant_hessian_ = false;
   bool average_output_ = false;

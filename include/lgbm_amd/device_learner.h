@@ -64,6 +64,9 @@ class DeviceTreeLearner {
   // DeviceMetricSpec::nout values (Metric::FinishDevice turns them into the metric's values);
   // false: evaluate on the host
   virtual bool ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) = 0;
+  // the same on the device-resident training scores (training metrics every metric_freq
+  // iterations without a download of the scores); false: evaluate on the host
+  virtual bool TrainEval(const DeviceMetricSpec& spec, std::vector<double>* sums) { return false; }
 
   // the last tree: grown device-resident, splits applied, bytes moved by device collectives
   struct TreeStats {

@@ -400,6 +400,16 @@ std::vector<double> GBDT::EvalValid(int i, int j) const {
   return m->Eval(valid_score_updater_[i]->score(), objective_);
 }
 
+std::vector<double> GBDT::EvalTrain(const Metric* m) {
+  const char* hm = std::getenv("LGBM_AMD_HOST_METRICS");
+  if (device_learner_ != nullptr && !(hm != nullptr && hm[0] == '1')) {
+    const DeviceMetricSpec spec = m->DeviceSpec(objective_);
+    std::vector<double> sums;
+    if (spec.kind != 0 && device_learner_->TrainEval(spec, &sums)) return m->FinishDevice(sums);
+  }
+  return m->Eval(HostTrainScore(), objective_);
+}
+
 double* GBDT::HostTrainScore() {
   if (device_learner_ != nullptr && !host_score_fresh_) {
     for (int k = 0; k < num_tree_per_iteration_; ++k) {
@@ -715,7 +725,7 @@ std::string GBDT::OutputMetric(int iter) {
   if (need_output) {
     for (auto* m : training_metrics_) {
       auto names = m->GetName();
-      auto scores = m->Eval(HostTrainScore(), objective_);
+      auto scores = EvalTrain(m);
       for (size_t k = 0; k < names.size(); ++k) {
         std::stringstream t;
         t << "Iteration:" << iter << ", training " << names[k] << " : " << scores[k];
@@ -758,7 +768,7 @@ std::vector<double> GBDT::GetEvalAt(int data_idx) {
   std::vector<double> ret;
   if (data_idx == 0) {
     for (auto* m : training_metrics_) {
-      for (double v : m->Eval(HostTrainScore(), objective_)) ret.push_back(v);
+      for (double v : EvalTrain(m)) ret.push_back(v);
     }
   } else {
     const int i = data_idx - 1;

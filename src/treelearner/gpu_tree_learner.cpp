@@ -2400,13 +2400,30 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
   m.out = vs.metric_out;
   dev::EvalMetric(m, stream_);
   if (vs.logged_kinds.insert(spec.kind).second) {
-    Log::Debug("device metric (kind %d) on validation set %d", spec.kind, slot);
+    if (slot == train_eval_slot_) Log::Debug("device metric (kind %d) on the training set", spec.kind);
+    else Log::Debug("device metric (kind %d) on validation set %d", spec.kind, slot);
   }
   sums->assign(std::max(2, spec.nout), 0.0);
   HIPCHECK(hipMemcpyAsync(sums->data(), vs.metric_out, sizeof(double) * sums->size(), hipMemcpyDeviceToHost,
                           stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
   return true;
+}
+
+// training metrics (reference gbdt.cpp:484-542 evaluates them every metric_freq iterations):
+// the device metric kernels of the validation sets over the resident training scores, so
+// valid_sets=[train] costs one reduction instead of an 8 N-byte download and a host pass
+bool GPUTreeLearner::TrainEval(const DeviceMetricSpec& spec, std::vector<double>* sums) {
+  if (d_score_ == nullptr || num_data_ <= 0) return false;
+  if (train_eval_slot_ < 0) {
+    ValidSet vs;
+    vs.num_data = num_data_;
+    vs.ntpi = num_tree_per_iteration_;
+    vs.score = d_score_;  // (not owned: valid_allocs_ holds only the metric inputs)
+    valid_.push_back(vs);
+    train_eval_slot_ = static_cast<int>(valid_.size()) - 1;
+  }
+  return ValidEval(train_eval_slot_, spec, sums);
 }
 
 void GPUTreeLearner::ValidScoreToHost(int slot, double* host) {

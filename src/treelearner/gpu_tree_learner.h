@@ -78,6 +78,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void ValidAddTree(int slot, const Tree* tree, int tree_id) override;
   void ValidScoreToHost(int slot, double* host) override;
   bool ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) override;
+  bool TrainEval(const DeviceMetricSpec& spec, std::vector<double>* sums) override;
   bool DebugLeafState(const Tree* tree, int leaf, std::vector<int32_t>* rows, std::vector<long long>* hist,
                       std::vector<int8_t>* bin_valid, double* sums) override;
   bool DebugGradients(std::vector<float>* g, std::vector<float>* h, double* scales) override;
@@ -357,6 +358,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
     std::set<int> logged_kinds;  // metric kinds evaluated here so far (debug log)
   };
   std::vector<ValidSet> valid_;
+  int train_eval_slot_ = -1;  // valid_ entry over the training scores (d_score_; no bins)
   std::vector<void*> valid_allocs_;
   // tree upload for the score traversal: one blob (node arrays, category sets, leaf values)
   // per tree, one H2D copy from a ring of pinned staging slots (each reused once its event --

@@ -660,6 +660,54 @@ def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, cap
         np.testing.assert_allclose(dev[name], host[name], rtol=1e-9, atol=1e-12, err_msg=name)
 
 
+@pytest.mark.parametrize("task", ["binary", "lambdarank", "multiclass", "regression_family"])
+def test_training_metrics_on_device(task, gpu_available, monkeypatch, capfd):
+    """Training-set metrics (valid_sets=[dtrain]: reference gbdt.cpp:484-542) are reduced on the
+    device-resident training scores, equal to the host evaluation of the downloaded scores."""
+    rng = np.random.RandomState(5)
+    n = 12000
+    X = rng.randn(n, 8)
+    group = None
+    if task == "binary":
+        y = (X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.3 * rng.randn(n) > 0).astype(float)
+        params = {"objective": "binary", "metric": ["auc", "binary_logloss", "binary_error"],
+                  "bagging_fraction": 0.7, "bagging_freq": 1}
+        kinds = (6, 4, 5)
+    elif task == "lambdarank":
+        y = np.clip(np.round(X[:, 0] + X[:, 1] + rng.randn(n)), 0, 4)
+        group = [40] * (n // 40)
+        params = {"objective": "lambdarank", "metric": ["ndcg", "map"], "eval_at": [1, 3, 5]}
+        kinds = (30, 31)
+    elif task == "multiclass":
+        y = (np.argmax(X[:, :4] + 0.5 * rng.randn(n, 4), axis=1)).astype(float)
+        params = {"objective": "multiclass", "num_class": 4, "metric": ["multi_logloss", "multi_error", "auc_mu"]}
+        kinds = (20, 21, 22)
+    else:
+        y = np.exp(0.3 * X[:, 0]) + rng.rand(n)
+        params = {"objective": "poisson", "metric": ["poisson", "l2", "huber", "mape"]}
+        kinds = (10, 1, 11)
+    params.update({"verbose": -1, "device_type": "gpu", "num_leaves": 15, "seed": 1})
+
+    def run():
+        ds = lgb.Dataset(X, y, group=group, params=params)
+        res = {}
+        lgb.train(params, ds, 5, valid_sets=[ds], valid_names=["train"], evals_result=res, verbose_eval=False)
+        return res["train"]
+
+    capfd.readouterr()
+    params["verbose"] = 2
+    dev = run()
+    logged = capfd.readouterr().out
+    for k in kinds:
+        assert "device metric (kind %d) on the training set" % k in logged, k
+    params["verbose"] = -1
+    monkeypatch.setenv("LGBM_AMD_HOST_METRICS", "1")
+    host = run()
+    assert set(dev) == set(host) and len(dev) >= 2
+    for name in dev:
+        np.testing.assert_allclose(dev[name], host[name], rtol=1e-9, atol=1e-12, err_msg=name)
+
+
 def _leaf_values(node):
     if "leaf_index" in node:
         return [node["leaf_value"]]
