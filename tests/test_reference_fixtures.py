@@ -10,7 +10,8 @@
   xendcg with ``.query``): predictions from a matrix, from the text file and from the sklearn
   estimator agree, and a Dataset built from the file (side files loaded by name) matches the one
   built from arrays.  The example data is read from the reference checkout (``LGBM_AMD_REF_EXAMPLES``
-  or /root/reference/examples); the tests skip where it is absent.
+  or /root/reference/examples), else from the binary / regression copies in tests/data/examples
+  (so the device variants run on the GPU box); the tests skip where it is absent.
 """
 import os
 
@@ -21,7 +22,19 @@ import lightgbmv1_amd as lgb
 
 LOWER = -2.9040190126976606
 UPPER = 3.3182142872462883
-EXAMPLES = os.environ.get("LGBM_AMD_REF_EXAMPLES", "/root/reference/examples")
+_VENDORED = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "examples")
+
+
+def _examples_root():
+    """LGBM_AMD_REF_EXAMPLES, else the reference checkout, else the copies of the binary and
+    regression examples vendored under tests/data/examples (the GPU box has no checkout)"""
+    env = os.environ.get("LGBM_AMD_REF_EXAMPLES")
+    if env:
+        return env
+    return "/root/reference/examples" if os.path.isdir("/root/reference/examples") else _VENDORED
+
+
+EXAMPLES = _examples_root()
 
 
 def _breast_cancer():
