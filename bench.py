@@ -79,6 +79,16 @@ def main():
 
     if world > 1:
         torch_dist.init_network(use_rccl=args.device == "gpu")
+    # per-iteration records (rounds per tree, collective bytes) for the JSON line, unless the
+    # caller already asked for them elsewhere
+    iter_log = os.environ.get("LGBM_AMD_ITER_LOG")
+    if iter_log is None and args.device == "gpu":
+        import tempfile
+        iter_log = os.path.join(tempfile.gettempdir(), "bench_iters_%d_%d.jsonl" % (os.getpid(), rank))
+        os.environ["LGBM_AMD_ITER_LOG"] = iter_log
+        own_log = True
+    else:
+        own_log = False
     n_total = args.rows
     lo = n_total * rank // world
     hi = n_total * (rank + 1) // world
@@ -120,6 +130,15 @@ def main():
     elapsed = time.perf_counter() - t1
     elapsed = torch_dist.allreduce_max(elapsed)
     sec_per_iter = elapsed / max(1, args.steps)
+    diag = {}
+    if iter_log is not None and os.path.exists(iter_log):
+        rows = [json.loads(line) for line in open(iter_log)][-args.steps:] if args.steps > 0 else []
+        trees = [r for row in rows for r in row.get("rounds", [])]
+        if rows:
+            diag = {"rounds_per_tree": round(sum(trees) / max(1, len(trees)), 2),
+                    "collective_bytes_per_iter": round(sum(r.get("collective_bytes", 0) for r in rows) / len(rows))}
+        if own_log:
+            os.remove(iter_log)
     auc = None
     if rank == 0 and args.test_rows > 0:
         Xt, yt = make_rows(n_total + 12345678, args.test_rows, args.features)
@@ -146,6 +165,8 @@ def main():
                        "parallelism": "dp{}".format(world) if world > 1 else "single"},
             "auc_heldout": auc,
             "trees": booster.num_trees(),
+            "device_comm": torch_dist.device_comm_kind() if world > 1 else None,
+            **diag,
             **({"train_auc": train_auc} if args.eval_train else {}),
             "setup_s": round(setup_s, 2),
         }), flush=True)

@@ -244,6 +244,16 @@ class Dataset {
                                   const score_t* grad, const score_t* hess, hist_t* hist, RowWiseScratch* scratch) const;
   void BuildRowMajor() const;
 
+ public:
+  // learners in row-wise mode hold the row-major copy (a use count under row_major_mu_): the
+  // last release frees it, so a Dataset whose learners chose col-wise (the auto threading
+  // test builds the copy once) keeps no second copy of its bins (reference: the row-wise
+  // multi-val bin is dropped when col-wise wins)
+  void RetainRowMajor() const;
+  void ReleaseRowMajor() const;
+
+ private:
+  mutable int row_major_users_ = 0;
   // row-wise histograms: every group's bin of a row, contiguous (bytes per group as stored);
   // built on first use under row_major_mu_ (concurrent learners on one Dataset), then read-only
   mutable std::vector<uint8_t> row_major_;

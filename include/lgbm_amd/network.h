@@ -90,6 +90,9 @@ class DeviceComm {
   // start of each tree and before re-capturing its graphs (the same points on every rank),
   // and such comms rendezvous there.  One GPU per process: nothing to do.
   virtual void HostBarrier() {}
+  // bound of every device-side wait of later collectives (communicators without device-side
+  // waits ignore it)
+  virtual void SetWaitLimit(double seconds) { (void)seconds; }
   // failure detection (watchdog of the device learner): an asynchronous communicator error,
   // and aborting every pending collective so that no rank stays blocked
   virtual bool AsyncError(std::string* msg) {

@@ -115,7 +115,8 @@ def init_network(use_rccl=True, backend="gloo", timeout_s=600, device_comm=None)
         _safe_call(lib.LGBM_AMD_DeviceCount(ctypes.byref(ndev)))
         kind = device_comm or os.environ.get("LGBM_AMD_DEVICE_COMM", "peer")
         if ndev.value > 0 and kind == "peer":
-            if _init_peer(lib, dist, group, local_rank % ndev.value, min(120.0, float(timeout_s))):
+            # (the learner raises the device-side wait bound to its time_out minutes)
+            if _init_peer(lib, dist, group, local_rank % ndev.value, float(timeout_s)):
                 _STATE["device_comm"] = "peer"
             else:
                 kind = "rccl"

@@ -7,7 +7,8 @@
 // RF: reference src/boosting/rf.hpp:33-200 (gradients computed once from the averaged
 //   init score, shrinkage 1, running average of tree outputs).
 // With a device learner the training score lives in HBM: every score mutation goes
-// through TrainScore*(), and GOSS samples on a host copy of the device gradients.
+// through TrainScore*(), and GOSS samples on the device too (DeviceSample from GBDT::Bagging,
+// src/device/sample_kernels.hip: the same per-block generators as the host draw).
 #include <algorithm>
 #include <cmath>
 

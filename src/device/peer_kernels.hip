@@ -217,7 +217,20 @@ void PeerCollective(const PeerArgs& a, hipStream_t s) {
   const size_t blocks = a.kind == kPeerAllgather ? static_cast<size_t>(a.n) : 1;
   const size_t bytes = a.count * static_cast<size_t>(a.elem) *
                        (a.kind == kPeerAllgather ? blocks : static_cast<size_t>(a.kind == kPeerBroadcast ? 1 : a.n));
-  const int grid = static_cast<int>(std::max<size_t>(1, std::min<size_t>(128, (bytes + 16383) / 16384)));
+  // Every workgroup's first thread waits for the peers' arrival, which this rank publishes only
+  // once ALL its workgroups have staged their share: the grid must be co-resident.  It is
+  // capped at half of what the device holds at once, shared by up to a.n ranks on one device
+  // (thread ranks), so other kernels in flight cannot starve the last workgroups.
+  static const int resident = [] {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_peer_collective<double, 0>, 256, 0) != hipSuccess) {
+      (void)hipGetLastError();
+      b = 4;
+    }
+    return std::max(1, b) * NumCUs();
+  }();
+  const size_t cap = std::max<size_t>(1, static_cast<size_t>(resident) / (2 * static_cast<size_t>(std::max(1, a.n))));
+  const int grid = static_cast<int>(std::max<size_t>(1, std::min<size_t>(std::min<size_t>(128, cap), (bytes + 16383) / 16384)));
   if (a.kind == kPeerAllreduce || a.kind == kPeerReduceScatter) {
     switch (a.op) {
       case kPeerSumF64: LaunchPeer<double, 0>(a, grid, s); break;

@@ -648,6 +648,19 @@ void Dataset::BuildRowMajor() const {
   }
 }
 
+void Dataset::RetainRowMajor() const {
+  std::lock_guard<std::mutex> lock(*row_major_mu_);
+  ++row_major_users_;
+}
+
+void Dataset::ReleaseRowMajor() const {
+  std::lock_guard<std::mutex> lock(*row_major_mu_);
+  if (row_major_users_ > 0 && --row_major_users_ == 0) {
+    std::vector<uint8_t>().swap(row_major_);
+    row_stride_ = 0;
+  }
+}
+
 void Dataset::ConstructHistogramsRowWise(const std::vector<int8_t>& group_used, const data_size_t* indices,
                                          data_size_t n, const score_t* grad, const score_t* hess,
                                          hist_t* hist, RowWiseScratch* scratch) const {

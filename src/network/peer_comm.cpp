@@ -102,6 +102,13 @@ class PeerComm : public DeviceComm {
     if (ctl_ != nullptr) (void)hipFree(ctl_);
     if (status_ != nullptr) (void)hipHostFree(status_);
   }
+  // one process per GPU: ranks skew between trees (evaluation, checkpoints, logging on one
+  // rank) while their peers already wait inside the next tree's first collective, so the
+  // learner's time_out bounds the waits.  Thread ranks (tests) keep the bound they were made
+  // with: their fault-injection tests rely on it.
+  void SetWaitLimit(double seconds) override {
+    if (seconds > 0 && own_win_ != nullptr) timeout_ticks_ = static_cast<long long>(seconds * 1e8);  // (100 MHz clock)
+  }
   // the windows this comm owns / mapped (multi-process)
   void Own(char* own, std::vector<char*> opened) {
     own_win_ = own;

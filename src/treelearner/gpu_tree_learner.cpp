@@ -121,6 +121,12 @@ void GPUTreeLearner::Init(const Dataset* train_data, bool is_constant_hessian) {
   distributed_ = mode_ != Mode::kSerial && world_ > 1;
   data_parallel_ = mode_ == Mode::kData && world_ > 1;
   voting_ = mode_ == Mode::kVoting && world_ > 1;
+  // device-side waits of the collectives are bounded like the reference's socket linker: by
+  // time_out minutes (rank skew between trees -- evaluation, checkpoints, logging on one rank
+  // -- is not an error)
+  if (distributed_ && Network::device_comm() != nullptr) {
+    Network::device_comm()->SetWaitLimit(60.0 * std::max(1, config_->time_out));
+  }
   HIPCHECK(hipSetDevice(device_id_));
   int cus = 0;
   HIPCHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device_id_));
@@ -1313,7 +1319,13 @@ void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
   }
   DeviceComm* dc = Network::device_comm();
   // a finished tree's remaining rounds skip their collectives on every rank (Round::done is
-  // replicated state); communicators that cannot skip run them
+  // replicated state); communicators that cannot skip run them.  The guard is cleared on every
+  // exit of this scope: a throw between here and the last collective (a failed launch caught
+  // by the graph capture) must not leave later collectives guarded by a stale flag
+  struct SkipGuardScope {
+    DeviceComm* dc;
+    ~SkipGuardScope() { dc->SetSkipGuard(nullptr); }
+  } guard_scope{dc};
   dc->SetSkipGuard(&d_round_->done);
   const size_t owned = static_cast<size_t>(round_k_) * rs_block_ * 2;
   // (the owner-major send buffer was cleared by the previous round's split scans, or by the root)
@@ -1328,7 +1340,7 @@ void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
     const size_t cb = per * kMaxCatWords * sizeof(uint32_t);
     dc->Allgather(fc + cb * rank_, fc, cb, stream_);
   }
-  dc->SetSkipGuard(nullptr);
+  dc->SetSkipGuard(nullptr);  // (the plan's kernels are not collectives)
   dev::RoundChildBestAndPlan(a, stream_);
 }
 

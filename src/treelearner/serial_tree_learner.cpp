@@ -50,7 +50,7 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool /*is_constant_hessi
   constraints_.Init(config_->num_leaves, config_);
   ResetPool();
   splittable_.assign(config_->num_leaves, std::vector<char>(num_features_, 1));
-  hist_mode_ = config_->force_row_wise ? 2 : config_->force_col_wise ? 1 : 0;
+  SetHistMode(config_->force_row_wise ? 2 : config_->force_col_wise ? 1 : 0);
   indices_.resize(num_data_);
   leaf_begin_.assign(config_->num_leaves, 0);
   leaf_count_.assign(config_->num_leaves, 0);
@@ -60,8 +60,18 @@ void SerialTreeLearner::Init(const Dataset* train_data, bool /*is_constant_hessi
   Log::Info("Number of data points in the train set: %d, number of used features: %d", num_data_, num_features_);
 }
 
+void SerialTreeLearner::SetHistMode(int m) {
+  if (m == 2 && !holds_row_major_) data_->RetainRowMajor();
+  if (m != 2 && holds_row_major_) data_->ReleaseRowMajor();
+  holds_row_major_ = m == 2;
+  hist_mode_ = m;
+}
+
 void SerialTreeLearner::ResetTrainingData(const Dataset* train_data, bool) {
+  const int mode = hist_mode_;
+  SetHistMode(0);  // (the hold moves to the new Dataset)
   data_ = train_data;
+  SetHistMode(mode);
   num_data_ = data_->num_data();
   LGBM_CHECK_EQ(num_features_, data_->num_features());
   indices_.resize(num_data_);
@@ -98,8 +108,8 @@ void SerialTreeLearner::ResetConfig(const Config* config) {
     leaf_count_.assign(config_->num_leaves, 0);
   }
   ResetPool();
-  if (config_->force_row_wise) hist_mode_ = 2;
-  else if (config_->force_col_wise) hist_mode_ = 1;
+  if (config_->force_row_wise) SetHistMode(2);
+  else if (config_->force_col_wise) SetHistMode(1);
   col_sampler_.SetConfig(config_);
   constraints_.Init(config_->num_leaves, config_);
   InitFeatureMeta();
@@ -314,9 +324,9 @@ void SerialTreeLearner::ConstructHistograms(const std::vector<int8_t>& feature_u
     // deterministic: col-wise (the two modes sum in different orders, a timing choice would
     // make models differ between runs); else the timing test, whose winning build is kept
     if (config_->deterministic) {
-      hist_mode_ = 1;
+      SetHistMode(1);
     } else {
-      hist_mode_ = ChooseHistogramThreading(groups, all_rows ? nullptr : idx, cnt);
+      SetHistMode(ChooseHistogramThreading(groups, all_rows ? nullptr : idx, cnt));
       built = true;
     }
   }
@@ -339,6 +349,12 @@ int SerialTreeLearner::ChooseHistogramThreading(const std::vector<int8_t>& group
                                                 data_size_t cnt) {
   std::vector<hist_t>& leaf = LeafHist(smaller_slot_);
   std::vector<hist_t> other(leaf.size());
+  // (held for the test; SetHistMode(2) below keeps it if row-wise wins)
+  data_->RetainRowMajor();
+  struct Hold {
+    const Dataset* d;
+    ~Hold() { d->ReleaseRowMajor(); }
+  } hold{data_};
   const double t0 = common::NowSeconds();
   data_->ConstructHistograms(groups, idx, cnt, gradients_, hessians_, leaf.data(), false);
   const double t1 = common::NowSeconds();
@@ -346,9 +362,10 @@ int SerialTreeLearner::ChooseHistogramThreading(const std::vector<int8_t>& group
   const double t2 = common::NowSeconds();
   const bool row = (t2 - t1) < (t1 - t0);
   if (row) leaf.swap(other);
-  // (the Dataset keeps its row-major copy: it may be shared by other boosters; this learner
-  // drops only its own per-thread buffers)
+  // col-wise won: this learner's per-thread buffers go, and the Dataset's row-major copy with
+  // the test's hold unless another learner holds it
   if (!row) Dataset::RowWiseScratch().bufs.swap(row_scratch_.bufs);
+  if (row) SetHistMode(2);  // (taken before the test's hold is released)
   Log::Info("Auto-choosing %s-wise multi-threading, the overhead of testing was %f seconds.\n"
             "You can set `force_%s_wise=true` to remove the overhead.",
             row ? "row" : "col", t2 - t0, row ? "row" : "col");

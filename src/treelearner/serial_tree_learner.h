@@ -61,6 +61,9 @@ class SerialTreeLearner : public TreeLearner {
   virtual void FindBestSplits(const Tree* tree);
   virtual void ConstructHistograms(const std::vector<int8_t>& feature_used, bool use_subtract);
   int ChooseHistogramThreading(const std::vector<int8_t>& groups, const data_size_t* idx, data_size_t cnt);
+  // the histogram mode (0 undecided, 1 col-wise, 2 row-wise); row-wise holds the Dataset's
+  // row-major copy while it lasts
+  void SetHistMode(int m);
   virtual void FindBestSplitsFromHistograms(const std::vector<int8_t>& feature_used, bool use_subtract,
                                             const Tree* tree);
   virtual void Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf);
@@ -112,6 +115,9 @@ class SerialTreeLearner : public TreeLearner {
   // CPU histogram threading (reference Dataset::TestMultiThreadingMethod): 0 undecided (auto),
   // 1 col-wise (threads over feature groups), 2 row-wise (threads over row blocks)
   int hist_mode_ = 0;
+  // data_->RetainRowMajor() taken (SetHistMode; not given back at destruction: the Dataset may
+  // be freed first, and it frees the copy itself)
+  bool holds_row_major_ = false;
   Dataset::RowWiseScratch row_scratch_;  // this learner's row-wise per-thread histograms
   bool has_parent_hist_ = false;
   LeafState smaller_, larger_;
