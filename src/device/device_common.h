@@ -177,6 +177,27 @@ __device__ __forceinline__ T WaveSum(T v) {
 #endif
 }
 
+// wave-wide max over DPP lane moves (every lane of the wave active; 0 is the identity)
+template <typename T>
+__device__ __forceinline__ T WaveMaxDpp(T v) {
+  v = max(v, DppMove<0x111>(v));
+  v = max(v, DppMove<0x112>(v));
+  v = max(v, DppMove<0x114>(v));
+  v = max(v, DppMove<0x118>(v));
+  v = max(v, DppMove<0x142, 0xa>(v));
+  v = max(v, DppMove<0x143, 0xc>(v));
+  return WaveLane63(v);
+}
+
+// order-preserving key of a gain: a larger gain has a larger key, NaN orders as -inf, and
+// every key of a number (-inf included) is above 0 (the identity of WaveMaxDpp)
+__device__ __forceinline__ unsigned long long GainKey(double g) {
+  if (g != g) g = -INFINITY;
+  if (g == 0.0) g = 0.0;  // (-0.0 and 0.0 compare equal: one key)
+  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(g));
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+
 template <typename T>
 __device__ __forceinline__ T WaveSuffixIncl(T v) {
   const int lane = threadIdx.x & 63;

@@ -122,10 +122,11 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
   const int nexp = rd->nexp, nblk = rd->nblk, rpb = rd->rpb;
   TileCtx t;
   InitTile<GPW>(a, &t);
-  if (done || nexp <= 0 || static_cast<int>(blockIdx.x) >= nblk) return;
-  if (threadIdx.x < static_cast<unsigned>(nexp)) {
+  // the expansions' plans are loaded in the same batch as the round record (a slot past nexp
+  // holds a stale plan that is never staged)
+  SplitExp x;
+  if (threadIdx.x < static_cast<unsigned>(kMaxRoundExp)) {
     const ExpPlan& e = rd->e[threadIdx.x];
-    SplitExp x;
     x.pb = e.part_begin;
     x.pc = e.part_count;
     x.src = e.src_buf;
@@ -147,8 +148,9 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
     x.r.missing_type = e.feat.missing_type;
     x.r.default_bin = e.feat.default_bin;
     x.r.max_bin = e.feat.num_bin - 1;
-    ex[threadIdx.x] = x;
   }
+  if (done || nexp <= 0 || static_cast<int>(blockIdx.x) >= nblk) return;
+  if (threadIdx.x < static_cast<unsigned>(nexp)) ex[threadIdx.x] = x;
   for (int i = threadIdx.x; i < nexp * kMaxCatWords; i += kPartThreads) {
     const int j = i / kMaxCatWords;
     cat_bits[j][i % kMaxCatWords] = rd->e[j].split.is_categorical ? rd->e[j].split.cat_bits[i % kMaxCatWords] : 0u;
@@ -647,6 +649,32 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
   }
 }
 
+// the plan's LDS tables (RoundPlanLds bytes): node tables (gain, -inf when the node has no
+// split; real feature; first child or -1), leaf tables (gain, real feature, node; accepted
+// leaves / nodes) and the prediction's copies of the leaf tables (+ levels below the leaf)
+struct PlanTables {
+  double *ng, *tg, *sg;
+  int *nrf, *nch, *nfi, *trf, *tnode, *acc, *accn, *srf, *snode, *svd;
+  __device__ PlanTables(unsigned char* lds, int NN, int L) {
+    ng = reinterpret_cast<double*>(lds);
+    tg = ng + NN;
+    sg = tg + L;
+    nrf = reinterpret_cast<int*>(sg + L);
+    nch = nrf + NN;
+    nfi = nch + NN;  // the node's best split feature (inner index; -1: none)
+    trf = nfi + NN;
+    tnode = trf + L;
+    acc = tnode + L;
+    accn = acc + L;
+    srf = accn + L;
+    snode = srf + L;
+    svd = snode + L;
+  }
+};
+
+template <bool ROOT, int NT>
+__device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds);
+
 // ----------------------------------------------------------------------------- k_round_find
 template <int KIND, int NT>
 struct RoundFindShared {
@@ -659,10 +687,26 @@ struct RoundFindShared {
   ArgC arg[NT / kWave];
 };
 
+// the wave's best candidate in ArgTake order (larger gain, NaN = -inf; smaller real feature;
+// lower index): two 64-bit DPP max-reductions and a read of the winning lane instead of a
+// butterfly of 4-field shuffles through the LDS crossbar
 __device__ __forceinline__ ArgC ArgWaveBest(ArgC c) {
-#pragma unroll 1
-  for (int o = 32; o > 0; o >>= 1) ArgTake(&c, ArgShflXor(c, o));
-  return c;
+  const bool live = c.idx >= 0;
+  const unsigned long long k1 = live ? GainKey(c.g) : 0ull;  // (GainKey(-inf) > 0: a live -inf still counts)
+  const unsigned long long m1 = WaveMaxDpp(k1);
+  if (m1 == 0ull) return ArgNone();
+  const bool t1 = live && k1 == m1;
+  const unsigned long long k2 = t1 ? ((static_cast<unsigned long long>(~static_cast<uint32_t>(c.rf)) << 32) |
+                                      static_cast<unsigned long long>(~static_cast<uint32_t>(c.idx)))
+                                   : 0ull;
+  const unsigned long long m2 = WaveMaxDpp(k2);
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(__builtin_ctzll(__ballot(t1 && k2 == m2))));
+  ArgC r;
+  r.g = ReadLane(c.g, w);
+  r.rf = ReadLane(c.rf, w);
+  r.idx = ReadLane(c.idx, w);
+  r.x = ReadLane(c.x, w);
+  return r;
 }
 
 // per-feature result slot of child y, inner feature f (distributed: rank-major blocks)
@@ -744,20 +788,38 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   __shared__ RoundFindShared<KIND, NT> sh;
   __shared__ int s_last;
   Round* rd = a.rd;
-  if (rd->done) return;
-  if (a.ktrace != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && rd->round < a.p.num_leaves) {
-    a.ktrace[static_cast<size_t>(rd->round) * kTraceSlots + 25] = wall_clock64();
-  }
+  const long long t_entry = a.ktrace != nullptr ? wall_clock64() : 0;
   const int y = blockIdx.y, j = y >> 1, lr = y & 1;
   const int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
   const int tid = threadIdx.x;
   const int NF = a.p.num_features;
   const int units = a.hist_units;
+  // the round record, the expansion's plan and the feature in one batch of loads, the
+  // finished-tree check included (it used to cost a round trip of its own)
+  const int done = rd->done, nexp = rd->nexp, rround = rd->round;
+  const ExpPlan& E = rd->e[j];
+  const int pc = E.part_count, tl = rd->cur[j][0];
+  const int e_gl0 = E.lr[0].global_count, e_gl1 = E.lr[1].global_count, e_hl = E.hist_left;
+  const int e_slot_new = E.slot_new, e_slot_parent = E.slot_parent, e_frow = E.frow_child[lr];
+  const int e_frow_parent = E.frow_parent, blk_off = E.blk_off, e_nblk = E.nblk;
+  const ChildStats cl = E.lr[lr];
   const Feature F = a.feat[f];
   const int8_t tree_used = a.tree_mask[f];
-  const int nexp = rd->nexp, parity = rd->round & 1;
+  if (done) return;
+  if (a.ktrace != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && rround < a.p.num_leaves) {
+    a.ktrace[static_cast<size_t>(rround) * kTraceSlots + 25] = wall_clock64();
+  }
+  const int parity = rround & 1;
   const int nbf = F.num_bin - F.offset;
   const double ig = a.scales[2], ih = a.scales[3];
+  // LGBM_AMD_KTRACE: the planning workgroup's own path through the scan (slots 26..31: entry,
+  // inputs loaded, histogram staged, scan done, child's arrival, child's fold done)
+  const bool ktw = a.ktrace != nullptr && tid == 0 && rround < a.p.num_leaves;
+  long long kt[6] = {0, 0, 0, 0, 0, 0};
+  if (ktw) {
+    kt[0] = t_entry;
+    kt[1] = wall_clock64();
+  }
   // this feature's bins of expansion j's reduce buffer for the next round (every expansion
   // slot: the next round may use any)
   const bool dp = a.p.data_parallel != 0;
@@ -776,20 +838,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     for (size_t i = b0 + tid; i < b1; i += NT) a.round_send[i] = 0;
   }
   if (j >= nexp) return;
-  const ExpPlan& E = rd->e[j];
-  const int pc = E.part_count;
-  const int tl = rd->cur[j][0];
   // data-parallel: the children's global counts from the split's estimates (reference
   // data_parallel_tree_learner.cpp: global leaf counts from the SplitInfo)
-  const int lc = dp ? E.lr[0].global_count : tl, rc = dp ? E.lr[1].global_count : pc - tl;
-  const ChildStats cl = E.lr[lr];
+  const int lc = dp ? e_gl0 : tl, rc = dp ? e_gl1 : pc - tl;
   const int md = a.p.sp.min_data_in_leaf;
   const bool skip = (a.p.max_depth > 0 && cl.depth >= a.p.max_depth) || (lc < 2 * md && rc < 2 * md);
-  const bool is_hist = (lr == 0) == (E.hist_left != 0);
-  const int slot = is_hist ? E.slot_new : E.slot_parent;
-  const int frow = E.frow_child[lr];
-  const int nblk = RoundHistBlocks(a, rd, j), blk_off = E.blk_off;
-  const int8_t parent_ok = a.splittable[static_cast<size_t>(E.frow_parent) * NF + f];
+  const bool is_hist = (lr == 0) == (e_hl != 0);
+  const int slot = is_hist ? e_slot_new : e_slot_parent;
+  const int frow = e_frow;
+  const int nblk = a.round_fused ? e_nblk : RoundHistBlocks(a, rd, j);
+  const int8_t parent_ok = a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
   FeatureBest* fb_out = &a.feat_best[RoundFbIndex(a, y, f)];
   int8_t* flags = a.splittable + static_cast<size_t>(frow) * NF;
   const SplitParams& p = a.p.sp;
@@ -908,6 +966,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
       }
     }
     __syncthreads();
+    if (ktw) kt[2] = wall_clock64();
     if (used) {
       L.cnt_factor = L.n / L.sh;
       const double gain_shift = LeafGain(L.sg, L.sh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, L.n,
@@ -934,14 +993,16 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
       if (o.gain == -INFINITY) o.feature = -1;
     }
   }
+  if (ktw) kt[3] = wall_clock64();
   if (write && tid == 0) PublishRecord(fb_out, o);
   // (distributed: the results are gathered from every rank first, k_round_childbest folds them)
   if (KIND == 1 || a.round_dist) return;  // (the categorical kernel counts the arrivals)
-  // arrival: the child's last workgroup folds the child's per-feature results
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   ArrivalRelease();
   __syncthreads();
+  // arrival: the child's last workgroup folds the child's per-feature results
   if (tid == 0) {
+    if (ktw) kt[4] = wall_clock64();
     const unsigned nwg = gridDim.x;
     uint32_t* cc = a.child_cnt + static_cast<size_t>(y) * (kFindSub + 1) * kFindSubStride;
     int last = 0;
@@ -972,6 +1033,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   __syncthreads();
   if (!s_last) return;
   ChildBest<KIND, NT>(a, y, frow, sh);
+  if (ktw) kt[5] = wall_clock64();
   if (!a.plan_in_find) return;
   // the last child of the round to finish plans the next round (its scans' results were
   // published write-through; one agent-scope acquire)
@@ -991,6 +1053,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   }
   __syncthreads();
   if (!s_last) return;
+  if (ktw) {
+    for (int k = 0; k < 6; ++k) a.ktrace[static_cast<size_t>(rround) * kTraceSlots + 26 + k] = kt[k];
+#if LGBM_FIND_PHASES
+    for (int k = 0; k < 4; ++k) a.ktrace[static_cast<size_t>(rround) * kTraceSlots + 12 + k] = g_find_phase[k];
+#endif
+  }
   RoundPlanBody<false, NT>(a, reinterpret_cast<unsigned char*>(s_bins));
 }
 
@@ -998,24 +1066,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
 // ordered keys of the replay's argmax (SplitInfo order over leaves): larger gain first (NaN =
 // -inf), then smaller real feature, then lower leaf id -- two wave max-reductions over DPP
 // lane moves instead of a shuffle butterfly carrying five values
-__device__ __forceinline__ unsigned long long GainKey(double g) {
-  if (g != g) g = -INFINITY;
-  const unsigned long long b = static_cast<unsigned long long>(__double_as_longlong(g));
-  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
 __device__ __forceinline__ uint32_t TieKey(int rf, int leaf) {
   const uint32_t r = rf < 0 ? 0x3fffffu : min(static_cast<uint32_t>(rf), 0x3ffffeu);
   return ~((r << 10) | static_cast<uint32_t>(leaf));
-}
-template <typename T>
-__device__ __forceinline__ T WaveMaxDpp(T v) {  // every lane of the wave active; 0 is the identity
-  v = max(v, DppMove<0x111>(v));
-  v = max(v, DppMove<0x112>(v));
-  v = max(v, DppMove<0x114>(v));
-  v = max(v, DppMove<0x118>(v));
-  v = max(v, DppMove<0x142, 0xa>(v));
-  v = max(v, DppMove<0x143, 0xc>(v));
-  return WaveLane63(v);
 }
 // the argmax leaf among l <= s with take(l) (one wave; -1: none)
 template <typename Take>
@@ -1214,23 +1267,20 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   __shared__ ArgC s_arg[kPlanThreads / kWave];
   __shared__ int s_pick[kMaxRoundExp];
   __shared__ int s_pc[kMaxRoundExp];
+  // the next round's expansion plans and their children's nodes, composed in LDS by one thread
+  // each and stored by every thread in 8-byte words (one thread storing a ~0.9 KB plan field by
+  // field took ~3.5 us)
+  __shared__ ExpPlan s_e[kMaxRoundExp];
+  __shared__ RNode s_c[2 * kMaxRoundExp];
   Round* rd = a.rd;
   const int L = a.p.num_leaves, NF = a.p.num_features, NN = a.round_nodes, tid = threadIdx.x, lane = tid & 63;
   // node tables (gain, -inf when the node has no split; real feature; first child or -1),
   // leaf tables (gain, real feature, node; accepted leaves / nodes) and the prediction's copies
   // of the leaf tables (+ levels below the real leaf)
-  double* ng = reinterpret_cast<double*>(plan_lds);
-  double* tg = ng + NN;
-  double* sg = tg + L;
-  int* nrf = reinterpret_cast<int*>(sg + L);
-  int* nch = nrf + NN;
-  int* trf = nch + NN;
-  int* tnode = trf + L;
-  int* acc = tnode + L;
-  int* accn = acc + L;
-  int* srf = accn + L;
-  int* snode = srf + L;
-  int* svd = snode + L;
+  const PlanTables T(plan_lds, NN, L);
+  double *ng = T.ng, *tg = T.tg, *sg = T.sg;
+  int *nrf = T.nrf, *nch = T.nch, *nfi = T.nfi, *trf = T.trf, *tnode = T.tnode, *acc = T.acc, *accn = T.accn,
+      *srf = T.srf, *snode = T.snode, *svd = T.svd;
   const int s0 = rd->nsplit;
   const int nexp_prev = rd->nexp;
   const int round0 = rd->round, rounds0 = rd->rounds, accmax0 = rd->accepted_max;
@@ -1303,6 +1353,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       ng[0] = b.idx >= 0 ? b.g : -INFINITY;
       nrf[0] = b.idx >= 0 ? b.rf : -1;
       nch[0] = -1;
+      nfi[0] = b.idx >= 0 ? fb.feature : -1;
       tnode[0] = 0;
       tg[0] = ng[0];
       trf[0] = nrf[0];
@@ -1331,6 +1382,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       ng[n] = fi >= 0 ? g : -INFINITY;
       nrf[n] = rf;
       nch[n] = ex ? ch : -1;
+      nfi[n] = fi;
     }
     for (int l = tid; l <= s0 && l < L; l += kPlanThreads) tnode[l] = a.leaves[l].frow;
     __syncthreads();
@@ -1445,44 +1497,130 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     ktr[22] = nacc;
     ktr[23] = nexp;
   }
-  // the accepted splits: split records (the node's best split, its partition counts)
-  for (int k = tid; k < nacc; k += kPlanThreads) {
-    const int n = accn[k];
-    const FeatureBest& cb = a.cbest[n];
-    const int tl = a.rnode[n].total_left, cnt = a.rnode[n].count;
-    SplitRecord& rec = a.rec[s0 + k];
-    rec.leaf = acc[k];
-    rec.left_count = dp ? cb.lc : tl;
-    rec.right_count = dp ? cb.rc : cnt - tl;
-    ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, &rec.split);
-  }
-  // the leaves the replay changed, from their final nodes (a leaf changed twice is written
-  // twice with the same record)
-  for (int i = tid; i < 2 * nacc; i += kPlanThreads) {
-    const int k = i >> 1;
-    const int l = (i & 1) == 0 ? acc[k] : s0 + k + 1;
-    const int n = tnode[l];
-    const RNode R = a.rnode[n];
-    Leaf lf;
-    lf.begin = R.begin;
-    lf.count = R.count;
-    lf.global_count = dp ? R.st.global_count : R.count;
-    lf.depth = R.st.depth;
-    lf.slot = R.st.slot;
-    lf.buf = R.buf;
-    lf.frow = n;
-    lf.pad = 0;
-    lf.icmask = R.st.icmask;
-    lf.sum_g = R.st.sum_g;
-    lf.sum_h = R.st.sum_h;
-    lf.output = R.st.output;
-    lf.lsum_g = lf.lsum_h = 0.0;
-    lf.cmin = R.st.cmin;
-    lf.cmax = R.st.cmax;
-    a.leaves[l] = lf;
-    DeviceSplit* d = &a.best[l];
-    if (ng[n] != -INFINITY) ToDeviceSplit(a.cbest[n], a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, d);
-    else NoSplit(d);
+  // the plan's records in one pass over a combined item space, so that each thread's loads are
+  // one round trip: [0, nexp) the next round's expansions (when the tree goes on), then the
+  // accepted splits' records, then the leaves the replay changed (from their final nodes; a
+  // leaf changed twice is written twice with the same record)
+  const int next_frow = nn;
+  const int nbuf = a.round_vmax + 2;
+  const int nent = s_done ? 0 : nexp;
+  for (int it = tid; it < nent + 3 * nacc; it += kPlanThreads) {
+    if (it < nent) {
+      const int j = it, node = s_pick[j];
+      // independent loads (one round trip): the node, its best split, the split feature's record
+      // (its index from the node table) and interaction mask
+      const int fi = nfi[node];
+      const RNode P = a.rnode[node];
+      const FeatureBest& cb = a.cbest[node];
+      const double lsg = cb.lg, lsh = cb.lh, lo = cb.lo;
+      const double rsg = cb.rg, rsh = cb.rh, ro = cb.ro;
+      const int lcnt = cb.lc, rcnt = cb.rc, mono = cb.mono, iscat = cb.ncat > 0 ? 1 : 0;
+      const IcMask fmask = a.feat_icmask != nullptr ? a.feat_icmask[fi] : kIcAll;
+      ExpPlan& e = s_e[j];
+      e.feat = a.feat[fi];
+      ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(node) * kMaxCatWords, &e.split);
+      s_pc[j] = P.count;
+      const int hl = lcnt <= rcnt ? 1 : 0;
+      e.node = node;
+      e.part_begin = P.begin;
+      e.part_count = P.count;
+      e.src_buf = P.buf;
+      e.dst_buf = P.buf + 1 == nbuf ? 0 : P.buf + 1;
+      e.hist_left = hl;
+      e.slot_parent = P.st.slot;
+      e.slot_new = next_slot + j;
+      e.frow_parent = node;
+      e.frow_child[0] = next_frow + 2 * j;
+      e.frow_child[1] = next_frow + 2 * j + 1;
+      // children's statistics from the split (basic monotone constraints: the mid-point bound)
+      const int depth = P.st.depth + 1;
+      double pmin = P.st.cmin, pmax = P.st.cmax, rmin = P.st.cmin, rmax = P.st.cmax;
+      if (!iscat) {
+        const double mid = (lo + ro) / 2.0f;
+        if (mono < 0) {
+          pmin = fmax(pmin, mid);
+          rmax = fmin(rmax, mid);
+        } else if (mono > 0) {
+          pmax = fmin(pmax, mid);
+          rmin = fmax(rmin, mid);
+        }
+      }
+      const IcMask icm = P.st.icmask & fmask;
+      ChildStats lc, rc;
+      lc.sum_g = lsg;
+      lc.sum_h = lsh;
+      lc.output = lo;
+      lc.cmin = pmin;
+      lc.cmax = pmax;
+      lc.global_count = lcnt;
+      lc.depth = depth;
+      lc.slot = hl ? e.slot_new : P.st.slot;
+      lc.leaf = -1;
+      lc.frow = e.frow_child[0];
+      lc.icmask = icm;
+      rc.sum_g = rsg;
+      rc.sum_h = rsh;
+      rc.output = ro;
+      rc.cmin = rmin;
+      rc.cmax = rmax;
+      rc.global_count = rcnt;
+      rc.depth = depth;
+      rc.slot = hl ? P.st.slot : e.slot_new;
+      rc.leaf = -1;
+      rc.frow = e.frow_child[1];
+      rc.icmask = icm;
+      e.lr[0] = lc;
+      e.lr[1] = rc;
+      a.rnode[node].expanded = 1;
+      a.rnode[node].child = e.frow_child[0];
+      RNode C;
+      C.begin = C.count = 0;  // (set by the next plan, from the partition counts)
+      C.buf = e.dst_buf;
+      C.expanded = 0;
+      C.child = -1;
+      C.total_left = 0;
+      C.st = lc;
+      s_c[2 * j] = C;
+      C.st = rc;
+      s_c[2 * j + 1] = C;
+    } else if (it < nent + nacc) {
+      // an accepted split: its record (the node's best split, its partition counts)
+      const int k = it - nent;
+      const int n = accn[k];
+      const FeatureBest& cb = a.cbest[n];
+      const int tl = a.rnode[n].total_left, cnt = a.rnode[n].count;
+      SplitRecord& rec = a.rec[s0 + k];
+      rec.leaf = acc[k];
+      rec.left_count = dp ? cb.lc : tl;
+      rec.right_count = dp ? cb.rc : cnt - tl;
+      ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, &rec.split);
+    } else {
+      const int i = it - nent - nacc;
+      const int k = i >> 1;
+      const int l = (i & 1) == 0 ? acc[k] : s0 + k + 1;
+      const int n = tnode[l];
+      const RNode R = a.rnode[n];
+      Leaf lf;
+      lf.begin = R.begin;
+      lf.count = R.count;
+      lf.global_count = dp ? R.st.global_count : R.count;
+      lf.depth = R.st.depth;
+      lf.slot = R.st.slot;
+      lf.buf = R.buf;
+      lf.frow = n;
+      lf.pad = 0;
+      lf.icmask = R.st.icmask;
+      lf.sum_g = R.st.sum_g;
+      lf.sum_h = R.st.sum_h;
+      lf.output = R.st.output;
+      lf.lsum_g = lf.lsum_h = 0.0;
+      lf.cmin = R.st.cmin;
+      lf.cmax = R.st.cmax;
+      a.leaves[l] = lf;
+      DeviceSplit* d = &a.best[l];
+      if (ng[n] != -INFINITY) ToDeviceSplit(a.cbest[n], a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, d);
+      else NoSplit(d);
+    }
   }
   stamp(19);
   if (s_done) {
@@ -1494,86 +1632,6 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     }
     return;
   }
-  const int next_frow = nn;
-  const int nbuf = a.round_vmax + 2;
-  if (tid < nexp) {
-    const int j = tid, node = s_pick[j];
-    // independent loads: the node, its best split and the split feature's record
-    const RNode P = a.rnode[node];
-    const FeatureBest& cb = a.cbest[node];
-    const double lsg = cb.lg, lsh = cb.lh, lo = cb.lo;
-    const double rsg = cb.rg, rsh = cb.rh, ro = cb.ro;
-    const int lcnt = cb.lc, rcnt = cb.rc, mono = cb.mono, iscat = cb.ncat > 0 ? 1 : 0;
-    const int fi = cb.feature;
-    const IcMask fmask = a.feat_icmask != nullptr ? a.feat_icmask[fi] : kIcAll;
-    ExpPlan& e = rd->e[j];
-    CopyWords(&a.feat[fi], &e.feat, 0, 1);
-    ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(node) * kMaxCatWords, &e.split);
-    s_pc[j] = P.count;
-    const int hl = lcnt <= rcnt ? 1 : 0;
-    e.node = node;
-    e.part_begin = P.begin;
-    e.part_count = P.count;
-    e.src_buf = P.buf;
-    e.dst_buf = P.buf + 1 == nbuf ? 0 : P.buf + 1;
-    e.hist_left = hl;
-    e.slot_parent = P.st.slot;
-    e.slot_new = next_slot + j;
-    e.frow_parent = node;
-    e.frow_child[0] = next_frow + 2 * j;
-    e.frow_child[1] = next_frow + 2 * j + 1;
-    // children's statistics from the split (basic monotone constraints: the mid-point bound)
-    const int depth = P.st.depth + 1;
-    double pmin = P.st.cmin, pmax = P.st.cmax, rmin = P.st.cmin, rmax = P.st.cmax;
-    if (!iscat) {
-      const double mid = (lo + ro) / 2.0f;
-      if (mono < 0) {
-        pmin = fmax(pmin, mid);
-        rmax = fmin(rmax, mid);
-      } else if (mono > 0) {
-        pmax = fmin(pmax, mid);
-        rmin = fmax(rmin, mid);
-      }
-    }
-    const IcMask icm = P.st.icmask & fmask;
-    ChildStats lc, rc;
-    lc.sum_g = lsg;
-    lc.sum_h = lsh;
-    lc.output = lo;
-    lc.cmin = pmin;
-    lc.cmax = pmax;
-    lc.global_count = lcnt;
-    lc.depth = depth;
-    lc.slot = hl ? e.slot_new : P.st.slot;
-    lc.leaf = -1;
-    lc.frow = e.frow_child[0];
-    lc.icmask = icm;
-    rc.sum_g = rsg;
-    rc.sum_h = rsh;
-    rc.output = ro;
-    rc.cmin = rmin;
-    rc.cmax = rmax;
-    rc.global_count = rcnt;
-    rc.depth = depth;
-    rc.slot = hl ? P.st.slot : e.slot_new;
-    rc.leaf = -1;
-    rc.frow = e.frow_child[1];
-    rc.icmask = icm;
-    e.lr[0] = lc;
-    e.lr[1] = rc;
-    a.rnode[node].expanded = 1;
-    a.rnode[node].child = e.frow_child[0];
-    RNode C;
-    C.begin = C.count = 0;  // (set by the next plan, from the partition counts)
-    C.buf = e.dst_buf;
-    C.expanded = 0;
-    C.child = -1;
-    C.total_left = 0;
-    C.st = lc;
-    a.rnode[e.frow_child[0]] = C;
-    C.st = rc;
-    a.rnode[e.frow_child[1]] = C;
-  }
   __syncthreads();
   stamp(20);
   if (tid == 0) {
@@ -1583,18 +1641,22 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     // balanced over the grid: the smallest m with blocks of ceil(rows / (m * grid - nexp))
     // rows under the packed headroom; every workgroup then takes m blocks at most (one
     // partial block per expansion rounds up)
-    const long long g = max(1, a.round_grid), cap = a.hist_rows_cap;
-    long long m = 1;
-    while (m * g - nexp > 0 && (rows + m * g - nexp - 1) / (m * g - nexp) > cap) ++m;
-    long long rpb = m * g - nexp > 0 ? (rows + m * g - nexp - 1) / (m * g - nexp) : cap;
+    // (the smallest m with ceil(rows / (m g - nexp)) <= cap, i.e. m g - nexp >= ceil(rows / cap);
+    // rows and cap are below 2^31, so every dividend fits 32 unsigned bits: no 64-bit divisions)
+    const unsigned g = static_cast<unsigned>(max(1, a.round_grid)), cap = static_cast<unsigned>(a.hist_rows_cap);
+    const unsigned urows = static_cast<unsigned>(rows), unexp = static_cast<unsigned>(nexp);
+    const unsigned need = (urows + cap - 1u) / cap + unexp;
+    const unsigned m = g <= unexp ? 1u : max(1u, (need + g - 1u) / g);
+    long long rpb = m * g > unexp ? (urows + m * g - unexp - 1u) / (m * g - unexp) : cap;
     rpb = max(rpb, static_cast<long long>(a.blk_min_rows));
-    rpb = min(rpb, cap);
+    rpb = min(rpb, static_cast<long long>(cap));
     rpb = max(rpb, 1ll);
     int off = 0;
+    const unsigned rpb32 = static_cast<unsigned>(rpb);  // (32-bit divisions: a 64-bit one is a long call)
     for (int j = 0; j < nexp; ++j) {
-      const int nb = static_cast<int>((s_pc[j] + rpb - 1) / rpb);
-      rd->e[j].blk_off = off;
-      rd->e[j].nblk = nb;
+      const int nb = static_cast<int>((static_cast<unsigned>(s_pc[j]) + rpb32 - 1u) / rpb32);
+      s_e[j].blk_off = off;
+      s_e[j].nblk = nb;
       off += nb;
     }
     rd->rpb = static_cast<int>(rpb);
@@ -1608,6 +1670,24 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     rd->accepted_max = max(accmax0, nacc);
   }
   if (tid < kMaxRoundExp) rd->cur[tid][0] = rd->cur[tid][1] = 0;
+  __syncthreads();
+  // the plans and the children's nodes (contiguous from next_frow) in 8-byte words; a plan's
+  // category set only when its split is categorical (the split kernel reads it only then)
+  {
+    constexpr int kEW = sizeof(ExpPlan) / 8, kCW = sizeof(RNode) / 8;
+    static_assert(sizeof(ExpPlan) % 8 == 0 && sizeof(RNode) % 8 == 0, "8-byte words");
+    // (the words lying wholly inside the category set: its offset need not be 8-aligned)
+    constexpr int kCatOff = __builtin_offsetof(ExpPlan, split) + __builtin_offsetof(DeviceSplit, cat_bits);
+    constexpr int kCat0 = (kCatOff + 7) / 8;
+    constexpr int kCat1 = (kCatOff + 4 * kMaxCatWords) / 8;
+    for (int i = tid; i < nexp * kEW; i += kPlanThreads) {
+      const int j = i / kEW, w = i - j * kEW;
+      if (w >= kCat0 && w < kCat1 && !s_e[j].split.is_categorical) continue;
+      reinterpret_cast<unsigned long long*>(&rd->e[j])[w] = reinterpret_cast<const unsigned long long*>(&s_e[j])[w];
+    }
+    unsigned long long* cdst = reinterpret_cast<unsigned long long*>(a.rnode + next_frow);
+    for (int i = tid; i < 2 * nexp * kCW; i += kPlanThreads) cdst[i] = reinterpret_cast<const unsigned long long*>(s_c)[i];
+  }
   stamp(21);
 }
 
@@ -1620,7 +1700,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
 
 size_t RoundPlanLds(int num_leaves, int nodes) {
   const size_t L = static_cast<size_t>(num_leaves), N = static_cast<size_t>(nodes);
-  return (N + 2 * L) * sizeof(double) + N * sizeof(int) * 2 + L * sizeof(int) * 7;
+  return (N + 2 * L) * sizeof(double) + N * sizeof(int) * 3 + L * sizeof(int) * 7;
 }
 
 namespace {

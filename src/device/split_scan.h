@@ -29,7 +29,32 @@ __device__ __forceinline__ bool CandBetter(const Cand& x, const Cand& y, bool re
   return reverse ? x.thr > y.thr : x.thr < y.thr;
 }
 
+#ifndef LGBM_DPP_ARGMAX
+#define LGBM_DPP_ARGMAX 1
+#endif
+// the wave's best candidate in CandBetter order: a 64-bit DPP max of the gain key (NaN below
+// every number), then among the lanes holding it the threshold order (reverse: highest,
+// forward: lowest) as a 32-bit DPP max, and reads of the winning lane -- instead of a
+// butterfly of five-field shuffles through the LDS crossbar (~2.7 us per scan workgroup)
 __device__ __forceinline__ Cand WaveBestCand(Cand c, bool reverse) {
+#if LGBM_DPP_ARGMAX
+  const unsigned long long k1 = c.gain != c.gain ? 1ull : GainKey(c.gain) + 1ull;  // (> 0: the DPP identity)
+  const unsigned long long m1 = WaveMaxDpp(k1);
+  const bool t1 = k1 == m1;
+  // (thresholds are signed, -1 included: offset by 2^31 to order them as unsigned, + 1 > 0)
+  const uint32_t tu = static_cast<uint32_t>(c.thr) ^ 0x80000000u;
+  const unsigned long long k2 = t1 ? static_cast<unsigned long long>(reverse ? tu : ~tu) + 1ull : 0ull;
+  const unsigned long long m2 = WaveMaxDpp(k2);
+  const unsigned long long win = __ballot(t1 && k2 == m2);
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(__builtin_ctzll(win)));
+  Cand r;
+  r.gain = ReadLane(c.gain, w);
+  r.thr = ReadLane(c.thr, w);
+  r.lg = ReadLane(c.lg, w);
+  r.lh = ReadLane(c.lh, w);
+  r.lc = ReadLane(c.lc, w);
+  return r;
+#else
   for (int o = 32; o > 0; o >>= 1) {
     Cand o2;
     o2.gain = __shfl_xor(c.gain, o, kWave);
@@ -40,6 +65,7 @@ __device__ __forceinline__ Cand WaveBestCand(Cand c, bool reverse) {
     if (CandBetter(o2, c, reverse)) c = o2;
   }
   return c;
+#endif
 }
 
 struct LeafCtx {
@@ -273,10 +299,21 @@ __device__ __forceinline__ double OutputOf(double sg, double sh, double l2, cons
 // Every candidate -- reverse at t (right = bins t..t_start), forward at t (left = bins
 // 0..t), and the forward "nothing stored on the left" start -- goes through one evaluation
 // site (instruction footprint: these kernels run once per split on a cold I-cache).
+#ifndef LGBM_FIND_PHASES
+#define LGBM_FIND_PHASES 0  // (A/B instrumentation: phase timestamps of the scan, g_find_phase)
+#endif
+#if LGBM_FIND_PHASES
+__shared__ long long g_find_phase[4];
+#define LGBM_FIND_STAMP(k) \
+  if (threadIdx.x == 0) g_find_phase[k] = wall_clock64()
+#else
+#define LGBM_FIND_STAMP(k)
+#endif
 template <bool SIMPLE, int NT>
 __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx& L, const SplitParams& p, int depth,
                                    double mono_penalty, FeatureBest* out, BlockScratch<NT>* sc, ScanScratch<NT>* ssc,
                                    Cand* sc2, int rthr) {
+  LGBM_FIND_STAMP(0);
   const int tid = threadIdx.x;
   const int nb = F.num_bin - F.offset;
   const int offset = F.offset;
@@ -310,6 +347,7 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
   }
   ScanAcc ex, tot;
   BlockScanNum(&v, &ex, &tot, ssc);
+  LGBM_FIND_STAMP(1);
   // FixHistogram
   if (fix_t >= 0) {
     const double fix_g = L.sg - tot.ag;
@@ -415,7 +453,9 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
       else fb = nc;
     }
   }
+  LGBM_FIND_STAMP(2);
   BlockBestPair(&rb, &fb, &any, sc, sc2);
+  LGBM_FIND_STAMP(3);
   out->gain = -INFINITY;
   out->default_left = two ? 1 : (F.missing_type == 2 ? 0 : 1);
   out->mono = F.monotone;

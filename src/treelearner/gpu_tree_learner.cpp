@@ -1464,14 +1464,24 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
     HIPCHECK(hipMemcpy(t.data(), a.ktrace, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
     static const char* names[] = {"stage", "side", "resv", "write", "gather", "tail", "store"};
-    // plans: slot 16 entry time, 17..21 phase times (loads, replay + prediction, acceptance,
-    // entries, sizing), 22 accepted, 23 planned, 25 the split scan's start
+    // plans: slot 16 entry time, 17..21 phase times (loads, replay + prediction, records of the
+    // expansions / accepted splits / changed leaves, barrier, sizing), 22 accepted, 23 planned,
+    // 25 the split scan's start
     for (int r = 0; r <= h_round_->rounds && r < L; ++r) {
       const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
       if (o[16] == 0) continue;
-      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay+predict=%.2f accept=%.2f entries=%.2f sizing=%.2f us; accepted %lld planned %lld\n",
+      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay+predict=%.2f records=%.2f sync=%.2f sizing=%.2f us; accepted %lld planned %lld\n",
                    r, o[25] != 0 ? (o[16] - o[25]) / 100.0 : 0.0, o[17] / 100.0, o[18] / 100.0, o[19] / 100.0,
                    o[20] / 100.0, o[21] / 100.0, o[22], o[23]);
+      if (o[26] != 0) {  // the planning workgroup's scan path, from the first scan workgroup's start
+        auto us = [&](int k) { return (o[k] - o[25]) / 100.0; };
+        std::fprintf(stderr, "  planner wg: entry %.2f loaded %.2f staged %.2f scanned %.2f arrived %.2f folded %.2f plan %.2f us\n",
+                     us(26), us(27), us(28), us(29), us(30), us(31), us(16));
+        if (o[12] != 0) {  // (LGBM_FIND_PHASES builds: the scan's phases)
+          std::fprintf(stderr, "  planner scan: begin %.2f prefix %.2f candidates %.2f argmax %.2f us\n", us(12), us(13),
+                       us(14), us(15));
+        }
+      }
     }
     for (int r = 1; r <= h_round_->rounds && r < L; ++r) {
       const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
