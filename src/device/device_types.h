@@ -104,6 +104,7 @@ struct ChildStats {
   int32_t global_count, depth, slot, leaf;
   int32_t frow;        // splittable row the child's scan writes
   IcMask icmask;       // Leaf::icmask
+  double lsum_g, lsum_h;  // voting-parallel round growth: this rank's sums of the node's rows
 };
 
 // the split being applied, as chosen by the partition kernel's pick
@@ -200,6 +201,7 @@ struct ExpPlan {
   Feature feat;                  // the split feature's record
   DeviceSplit split;
   ChildStats lr[2];              // left / right child as known from the split
+  double plsum_g, plsum_h;       // voting-parallel: the node's local sums (RNode::st.lsum_*)
 };
 
 // one node of a tree under round growth (index: its splittable row): the root and both
@@ -226,6 +228,9 @@ struct Round {
   uint32_t child_done;   // children of the round whose best split is folded (plan in the split scan)
   int32_t pad;
   int32_t cur[kMaxRoundExp][2];  // partition cursors of each expansion: rows placed left / right
+  // voting-parallel: the fixed-point (g, h) sums of each expansion's histogrammed child over
+  // this rank's rows (its local sums; the other child's are the parent's minus these)
+  unsigned long long loc_acc[kMaxRoundExp][2];
   ExpPlan e[kMaxRoundExp];
 };
 

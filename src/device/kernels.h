@@ -195,6 +195,12 @@ struct KArgs {
   // ([world][round_k][rs_block][2] int64, owner-major), reduce-scattered into round_owned
   // ([round_k][rs_block][2]: this rank's owned bins of every expansion)
   int32_t round_dist;
+  // voting-parallel round growth: phase 1 scans every feature of both children of every
+  // expansion on this rank's histograms and sums (Params::vote_phase 1); the round's proposals
+  // ([world][2 * round_k][vote_k] in vote_buf), elected features ([2 * round_k][vote_k] in
+  // vote_list) and their histograms ([2 * round_k][vote_k][2 * max_feature_bins] in vote_hist)
+  // feed phase 2, the global scan of the elected features (grid (vote_k, 2 * round_k))
+  int32_t round_vote;
   int32_t max_owned;
   int32_t rs_block;
   long long* round_send;
@@ -296,6 +302,12 @@ void RoundStep(const KArgs& a, hipStream_t s);  // single process: split + reduc
 void RoundSplitReduce(const KArgs& a, hipStream_t s);
 void RoundFind(const KArgs& a, hipStream_t s);
 void RoundChildBestAndPlan(const KArgs& a, hipStream_t s);
+// voting-parallel rounds: the proposals of every child of the round from the phase-1 scan, and
+// after their allgather the elections and the elected features' local histograms; then the
+// phase-2 (global) scan of the elected features
+void RoundVoteLocal(const KArgs& a, hipStream_t s);
+void RoundVoteElect(const KArgs& a, hipStream_t s);
+void RoundFindElected(const KArgs& a, hipStream_t s);
 size_t RoundPlanLds(int num_leaves, int nodes);
 // voting-parallel: this rank's top-k proposals per leaf from the local scan (into its block
 // of vote_buf); after the allgather, the election and the elected features' local histograms

@@ -183,6 +183,10 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const unsigned long long lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   const bool writer = blockIdx.y == 0;
+  // voting-parallel: the histogrammed rows' fixed-point (g, h), summed per row block by the
+  // threads of word 0 of column tile 0 (each row once) -- that child's local sums
+  const bool loc_sums = a.round_vote != 0 && writer;
+  long long loc_g = 0, loc_h = 0;
   int row[kSplitRows];
   uint32_t gb[kSplitRows];
   auto load_rows = [&](int jn, int t0n, int r1n, int* rr) {
@@ -306,6 +310,15 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
 #pragma unroll
             for (int k = 0; k < GR; ++k) v[k] = GhAt(a, rr[k] >= 0 ? rr[k] : 0);
             AddSparseRows<GR, UNITS>(a, lds, t, rr, v);
+            if (loc_sums && t.q == 0) {
+#pragma unroll
+              for (int k = 0; k < GR; ++k) {
+                if (rr[k] >= 0) {
+                  loc_g += __float2ll_rn(v[k].x * t.sg);
+                  loc_h += __float2ll_rn(v[k].y * t.sh);
+                }
+              }
+            }
           }
         } else {
           // software-pipelined: the next batch's row words and (g, h) are in flight while this
@@ -329,6 +342,15 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
             if (j0 + step < nh) fetch(j0 + step, wn, vn);
 #pragma unroll
             for (int k = 0; k < GR; ++k) AddRow<GPW, UNITS>(lds, t.goff, t.bits, wd[k], v[k], t.sg, t.sh);
+            if (loc_sums && t.q == 0) {
+#pragma unroll
+              for (int k = 0; k < GR; ++k) {
+                if (j0 + k * t.rpp < nh) {
+                  loc_g += __float2ll_rn(v[k].x * t.sg);
+                  loc_h += __float2ll_rn(v[k].y * t.sh);
+                }
+              }
+            }
 #pragma unroll
             for (int k = 0; k < GR; ++k) {
               wd[k] = wn[k];
@@ -379,6 +401,14 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
     unsigned long long* out = a.partials + static_cast<size_t>(kb) * UNITS * a.p.total_bins +
                               static_cast<size_t>(UNITS) * t.lo_bin;
     for (int i = threadIdx.x; i < UNITS * t.nbins; i += kPartThreads) out[i] = lds[i];
+    if (loc_sums) {  // (uniform: every lane of every wave takes part in the sums)
+      const long long bg = WaveSum(loc_g), bh = WaveSum(loc_h);
+      if (lane == 0 && (bg != 0 || bh != 0)) {
+        atomicAdd(&rd->loc_acc[j][0], static_cast<unsigned long long>(bg));
+        atomicAdd(&rd->loc_acc[j][1], static_cast<unsigned long long>(bh));
+      }
+      loc_g = loc_h = 0;
+    }
     stamp(6);
   }
   if (tr) {
@@ -607,7 +637,9 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
   const int j = blockIdx.z;
   if (j >= rd->nexp) return;
   const int nblk = RoundHistBlocks(a, rd, j);
-  const bool dp = a.p.data_parallel != 0;  // every expansion reduced, into the owner-major send buffer
+  // data-parallel: every expansion reduced, into the owner-major send buffer (voting keeps
+  // rank-local histograms: the single-process layout)
+  const bool dp = a.p.data_parallel != 0 && !a.round_vote;
   if (!dp && nblk <= kDirectChunk) return;  // summed by the split scan
   if (static_cast<int>(blockIdx.y) * kReduceChunk >= nblk) return;
   const int bin = blockIdx.x * blockDim.x + threadIdx.x;
@@ -711,7 +743,7 @@ __device__ __forceinline__ ArgC ArgWaveBest(ArgC c) {
 
 // per-feature result slot of child y, inner feature f (distributed: rank-major blocks)
 __device__ __forceinline__ size_t RoundFbIndex(const KArgs& a, int y, int f) {
-  if (!a.round_dist) return static_cast<size_t>(y) * a.p.num_features + f;
+  if (!a.round_dist || a.round_vote) return static_cast<size_t>(y) * a.p.num_features + f;
   const int fi = a.fb_index[f], per = 2 * a.max_owned;
   const int owner = fi / per, local = fi - owner * per;
   return (static_cast<size_t>(owner) * 2 * a.round_k + y) * a.max_owned + local;
@@ -790,7 +822,15 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   Round* rd = a.rd;
   const long long t_entry = a.ktrace != nullptr ? wall_clock64() : 0;
   const int y = blockIdx.y, j = y >> 1, lr = y & 1;
-  const int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
+  // voting-parallel rounds (KArgs::round_vote): Params::vote_phase 1 scans every feature on this
+  // rank's histograms, sums and counts; 2 scans the features the vote elected for child y
+  // (KArgs::vote_list) on their all-reduced histograms (KArgs::vote_hist)
+  const bool vote_local = a.round_vote && a.p.vote_phase == 1;
+  const bool vote_global = a.round_vote && a.p.vote_phase == 2;
+  int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
+  if (vote_global) f = a.vote_list[y * a.p.vote_k + blockIdx.x];
+  const bool vote_empty = vote_global && f < 0;
+  if (vote_empty) f = 0;
   const int tid = threadIdx.x;
   const int NF = a.p.num_features;
   const int units = a.hist_units;
@@ -803,6 +843,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const int e_slot_new = E.slot_new, e_slot_parent = E.slot_parent, e_frow = E.frow_child[lr];
   const int e_frow_parent = E.frow_parent, blk_off = E.blk_off, e_nblk = E.nblk;
   const ChildStats cl = E.lr[lr];
+  const unsigned long long loc0 = rd->loc_acc[j][0], loc1 = rd->loc_acc[j][1];
+  const double pl_g = E.plsum_g, pl_h = E.plsum_h;
   const Feature F = a.feat[f];
   const int8_t tree_used = a.tree_mask[f];
   if (done) return;
@@ -823,11 +865,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   // this feature's bins of expansion j's reduce buffer for the next round (every expansion
   // slot: the next round may use any)
   const bool dp = a.p.data_parallel != 0;
-  if (!CAT && lr == 0 && !dp) {
+  const bool owner = dp && !a.round_vote;  // (data-parallel: reduce-scattered to the feature owners)
+  if (!CAT && lr == 0 && !owner && !vote_global) {
     long long* nxt = RoundScratch(a, parity + 1, j);
     for (int i = tid; i < 2 * nbf; i += NT) nxt[2 * F.hist_offset + i] = 0;
   }
-  if (!CAT && dp && a.round_send != nullptr) {
+  if (!CAT && owner && a.round_send != nullptr) {
     // data-parallel: the next round's owner-major send buffer, cleared by every workgroup's
     // share (this round's reduce-scatter has read it) -- no memset node per round
     const size_t total = static_cast<size_t>(a.p.world) * a.round_k * a.rs_block * 2;
@@ -837,7 +880,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     const size_t b1 = min(total, b0 + per);
     for (size_t i = b0 + tid; i < b1; i += NT) a.round_send[i] = 0;
   }
-  if (j >= nexp) return;
+  if (j >= nexp || vote_empty) return;
+  if (vote_global && CAT && !F.is_cat) return;  // (an elected numerical feature)
   // data-parallel: the children's global counts from the split's estimates (reference
   // data_parallel_tree_learner.cpp: global leaf counts from the SplitInfo)
   const int lc = dp ? e_gl0 : tl, rc = dp ? e_gl1 : pc - tl;
@@ -847,7 +891,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const int slot = is_hist ? e_slot_new : e_slot_parent;
   const int frow = e_frow;
   const int nblk = a.round_fused ? e_nblk : RoundHistBlocks(a, rd, j);
-  const int8_t parent_ok = a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
+  // (voting: every feature is scanned -- the vote may elect one this rank could not split)
+  const int8_t parent_ok = a.round_vote ? 1 : a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
   FeatureBest* fb_out = &a.feat_best[RoundFbIndex(a, y, f)];
   int8_t* flags = a.splittable + static_cast<size_t>(frow) * NF;
   const SplitParams& p = a.p.sp;
@@ -881,17 +926,28 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     L.parent_out = cl.output;
     L.c.min = cl.cmin;
     L.c.max = cl.cmax;
+    if (vote_local) {
+      // this rank's rows of the child: the histogrammed child's sums from k_round_split, the
+      // other one's as the parent's minus those
+      const double hg = static_cast<double>(static_cast<long long>(loc0)) * ig;
+      const double hh = static_cast<double>(static_cast<long long>(loc1)) * ih;
+      L.sg = is_hist ? hg : pl_g - hg;
+      L.sh = (is_hist ? hh : pl_h - hh) + 2 * kEpsilon;
+      L.n = lr == 0 ? tl : pc - tl;
+    }
     const int nh = 2 * a.p.total_bins;
-    long long* dst = a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
-    const long long* src = dp ? a.round_owned + 2 * (static_cast<size_t>(j) * a.rs_block + (F.hist_offset - a.owned_bin_lo))
-                              : RoundScratch(a, parity, j) + 2 * F.hist_offset;
+    long long* dst = vote_global ? a.vote_hist + static_cast<size_t>(y * a.p.vote_k + blockIdx.x) * 2 * a.p.max_feature_bins
+                                 : a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
+    const long long* src = vote_global ? dst
+                           : owner ? a.round_owned + 2 * (static_cast<size_t>(j) * a.rs_block + (F.hist_offset - a.owned_bin_lo))
+                                   : RoundScratch(a, parity, j) + 2 * F.hist_offset;
     const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
     const unsigned long long* part = a.partials + static_cast<size_t>(blk_off) * pstride + static_cast<size_t>(units) * F.hist_offset;
     const bool stage = a.p.max_feature_bins <= kFindLdsBins;
     double* sgv = s_bins;
     double* shv = s_bins + (stage ? a.p.max_feature_bins : 0);
-    const bool subtract = !is_hist;
-    const int nblk_direct = (!dp && nblk <= kDirectChunk) ? nblk : -1;
+    const bool subtract = !is_hist && !vote_global;
+    const int nblk_direct = (!owner && !vote_global && nblk <= kDirectChunk) ? nblk : -1;
     const bool spread = nblk_direct > 1 && 2 * nbf <= NT;
     long long pg0 = 0, ph0 = 0;
     if (subtract && tid < nbf) {
@@ -958,8 +1014,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
         g = (i == tid ? pg0 : dst[2 * i]) - g;
         h = (i == tid ? ph0 : dst[2 * i + 1]) - h;
       }
-      dst[2 * i] = g;
-      dst[2 * i + 1] = h;
+      if (!vote_global) {
+        dst[2 * i] = g;
+        dst[2 * i + 1] = h;
+      }
       if (stage) {
         sgv[i] = static_cast<double>(g) * ig;
         shv[i] = static_cast<double>(h) * ih;
@@ -1349,6 +1407,8 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       r.st.leaf = 0;
       r.st.frow = 0;
       r.st.icmask = R.icmask;
+      r.st.lsum_g = R.lsum_g;  // (voting: the local root scan's sums)
+      r.st.lsum_h = R.lsum_h;
       a.rnode[0] = r;
       ng[0] = b.idx >= 0 ? b.g : -INFINITY;
       nrf[0] = b.idx >= 0 ? b.rf : -1;
@@ -1372,6 +1432,16 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       cn[1].begin = pb + tl;
       cn[1].count = pc - tl;
       cn[1].buf = db;
+      if (a.round_vote) {
+        // this rank's sums of the children (the local scan's, from k_round_split's fixed point)
+        const double hg = static_cast<double>(static_cast<long long>(rd->loc_acc[tid][0])) * a.scales[2];
+        const double hh = static_cast<double>(static_cast<long long>(rd->loc_acc[tid][1])) * a.scales[3];
+        const int h = E.hist_left ? 0 : 1;
+        cn[h].st.lsum_g = hg;
+        cn[h].st.lsum_h = hh;
+        cn[1 - h].st.lsum_g = E.plsum_g - hg;
+        cn[1 - h].st.lsum_h = E.plsum_h - hh;
+      }
     }
     // one batch of independent loads: every node's best and children, every leaf's node
     for (int n = tid; n < nn; n += kPlanThreads) {
@@ -1532,6 +1602,8 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       e.frow_parent = node;
       e.frow_child[0] = next_frow + 2 * j;
       e.frow_child[1] = next_frow + 2 * j + 1;
+      e.plsum_g = P.st.lsum_g;
+      e.plsum_h = P.st.lsum_h;
       // children's statistics from the split (basic monotone constraints: the mid-point bound)
       const int depth = P.st.depth + 1;
       double pmin = P.st.cmin, pmax = P.st.cmax, rmin = P.st.cmin, rmax = P.st.cmax;
@@ -1558,6 +1630,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       lc.leaf = -1;
       lc.frow = e.frow_child[0];
       lc.icmask = icm;
+      lc.lsum_g = lc.lsum_h = 0.0;  // (voting: set by the next plan, from the partition's local sums)
       rc.sum_g = rsg;
       rc.sum_h = rsh;
       rc.output = ro;
@@ -1569,6 +1642,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       rc.leaf = -1;
       rc.frow = e.frow_child[1];
       rc.icmask = icm;
+      rc.lsum_g = rc.lsum_h = 0.0;
       e.lr[0] = lc;
       e.lr[1] = rc;
       a.rnode[node].expanded = 1;
@@ -1613,7 +1687,8 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       lf.sum_g = R.st.sum_g;
       lf.sum_h = R.st.sum_h;
       lf.output = R.st.output;
-      lf.lsum_g = lf.lsum_h = 0.0;
+      lf.lsum_g = R.st.lsum_g;
+      lf.lsum_h = R.st.lsum_h;
       lf.cmin = R.st.cmin;
       lf.cmax = R.st.cmax;
       a.leaves[l] = lf;
@@ -1669,7 +1744,10 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     rd->rounds = rounds0 + 1;
     rd->accepted_max = max(accmax0, nacc);
   }
-  if (tid < kMaxRoundExp) rd->cur[tid][0] = rd->cur[tid][1] = 0;
+  if (tid < kMaxRoundExp) {
+    rd->cur[tid][0] = rd->cur[tid][1] = 0;
+    rd->loc_acc[tid][0] = rd->loc_acc[tid][1] = 0ull;
+  }
   __syncthreads();
   // the plans and the children's nodes (contiguous from next_frow) in 8-byte words; a plan's
   // category set only when its split is categorical (the split kernel reads it only then)
@@ -1756,6 +1834,8 @@ void LaunchRoundFind(const KArgs& a, hipStream_t s) {
   const bool simple = RoundSimpleGains(a);
   const bool narrow = a.p.max_feature_bins <= kWave;
   const dim3 g(a.num_scan, ny), b(narrow ? kWave : kFindThreads), bc(kFindThreads);
+  // (voting global scan: every elected slot, numerical or categorical, in both kernels)
+  const int ncat = (a.round_vote && a.p.vote_phase == 2) ? a.num_scan : a.p.has_cat;
   if (a.p.has_cat) {
     if (narrow) {
       if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave>), g, b, lds, s, a);
@@ -1764,8 +1844,8 @@ void LaunchRoundFind(const KArgs& a, hipStream_t s) {
       if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads>), g, b, lds, s, a);
       else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads>), g, b, lds, s, a);
     }
-    if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads>), dim3(a.p.has_cat, ny), bc, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads>), dim3(a.p.has_cat, ny), bc, lds, s, a);
+    if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads>), dim3(ncat, ny), bc, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads>), dim3(ncat, ny), bc, lds, s, a);
   } else if (narrow) {
     if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave>), g, b, lds, s, a);
     else hipLaunchKernelGGL((k_round_find<0, false, kWave>), g, b, lds, s, a);
@@ -1821,6 +1901,8 @@ void RoundStep(const KArgs& a, hipStream_t s) {
 }
 
 void RoundFind(const KArgs& a, hipStream_t s) { LaunchRoundFind(a, s); }
+
+void RoundFindElected(const KArgs& a, hipStream_t s) { LaunchRoundFind(a, s); }  // (a: vote_phase 2, num_scan vote_k)
 
 void RoundChildBestAndPlan(const KArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_round_childbest, dim3(2 * a.round_k), dim3(kFindThreads), 0, s, a);

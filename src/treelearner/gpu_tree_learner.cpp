@@ -339,14 +339,11 @@ void GPUTreeLearner::UploadData() {
   args_.tile_words = tile_words;
   SetupOwnership();
   const int n_leaves = config_->num_leaves;
-  // round growth: up to round_k_ leaves expanded per round (single process; LGBM_AMD_ROUND_K,
-  // 1 = one split per step)
-  round_k_ = 1;
-  if (!voting_) {  // (distributed data- / feature-parallel: rounds with a device communicator)
-    round_k_ = 6;  // (A/B at 300 iterations of the headline: K 3..16 = 2.40 2.27 2.20 2.20 2.21 2.30 2.48 2.50 ms)
-    if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) round_k_ = std::atoi(e);
-    round_k_ = std::max(1, std::min(dev::kMaxRoundExp, round_k_));
-  }
+  // round growth: up to round_k_ leaves expanded per round (LGBM_AMD_ROUND_K, 1 = one split per
+  // step; distributed learners run rounds with a device communicator)
+  round_k_ = 6;  // (A/B at 300 iterations of the headline: K 3..16 = 2.40 2.27 2.20 2.20 2.21 2.30 2.48 2.50 ms)
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) round_k_ = std::atoi(e);
+  round_k_ = std::max(1, std::min(dev::kMaxRoundExp, round_k_));
   // speculation below the leaves (LGBM_AMD_ROUND_VMAX levels, 0: leaves only): one index
   // buffer per level + 2 (device_types.h), bounded to 32 GiB of row indices
   round_vmax_ = dev::kMaxRoundVmax;
@@ -587,9 +584,11 @@ void GPUTreeLearner::UploadData() {
       return MakeSplitParams(local);
     }();
     d_root_local_ = Alloc<double>(3);
-    d_vote_buf_ = Alloc<dev::VoteEntry>(static_cast<size_t>(world_) * 2 * vote_k_);
-    d_vote_list_ = Alloc<int32_t>(2 * static_cast<size_t>(vote_k_));
-    d_vote_hist_ = Alloc<long long>(static_cast<size_t>(2 * vote_k_) * 2 * max_fb);
+    // (round growth: one election per child of the round's expansions, 2 * round_k_ at once)
+    const size_t sides = 2 * static_cast<size_t>(std::max(1, round_k_));
+    d_vote_buf_ = Alloc<dev::VoteEntry>(static_cast<size_t>(world_) * sides * vote_k_);
+    d_vote_list_ = Alloc<int32_t>(sides * vote_k_);
+    d_vote_hist_ = Alloc<long long>(sides * vote_k_ * 2 * max_fb);
     a.root_local = d_root_local_;
     a.vote_buf = d_vote_buf_;
     a.vote_list = d_vote_list_;
@@ -634,6 +633,7 @@ void GPUTreeLearner::UploadData() {
   a.rd = nullptr;
   a.round_k = round_k_;
   a.round_dist = distributed_ ? 1 : 0;
+  a.round_vote = (voting_ && round_k_ > 1) ? 1 : 0;
   a.max_owned = max_owned_;
   a.rs_block = rs_block_;
   a.round_send = nullptr;
@@ -652,7 +652,8 @@ void GPUTreeLearner::UploadData() {
   // the plan in the split scan's last workgroup while its tables fit the scan's LDS budget
   a.plan_in_find = (!distributed_ && dev::RoundPlanLds(n_leaves, split_rows_) <= 16384) ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_PLAN_IN_FIND")) a.plan_in_find = e[0] == '1' ? 1 : 0;
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_FUSED")) a.round_fused = e[0] == '1' ? 1 : 0;
+  // (voting: the local sums are accumulated by k_round_split)
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_FUSED")) a.round_fused = (e[0] == '1' || a.round_vote) ? 1 : 0;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) a.round_grid = std::max(1, std::atoi(e));
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GR")) a.round_gr = std::atoi(e);
   a.round_need_div = 0;
@@ -1219,12 +1220,8 @@ void GPUTreeLearner::DestroyGraph() {
 void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
   EnqueueRoot(a);
   // voting: the global scan of the elected features picks (pick_in_find); the local scan does not
-  dev::KArgs glob = a;
+  const dev::KArgs glob = voting_ ? VoteGlobalArgs(a, 1) : a;
   if (voting_) {
-    glob.p.vote_phase = 2;
-    glob.p.sp = params_;
-    glob.pick_in_find = 1;
-    glob.num_scan = vote_k_;
     VoteExchange(glob, true);
     dev::FindRoot(glob, stream_);
   } else if (distributed_) {
@@ -1302,10 +1299,25 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
     dev::CegbRoot(a, stream_);
   }
   dev::FindRoot(a, stream_);
-  if (a.rd != nullptr) {
+  if (a.rd != nullptr && voting_) {
+    // the root's vote and global scan (publish only), then the first plan from its results
+    const dev::KArgs glob = VoteGlobalArgs(a, 0);
+    VoteExchange(glob, true);
+    dev::FindRoot(glob, stream_);
+    dev::RoundRootPlan(glob, stream_);
+  } else if (a.rd != nullptr) {
     if (distributed_) GatherFeatureBests();  // (the root's results, side-0 layout)
     dev::RoundRootPlan(a, stream_);
   }
+}
+
+dev::KArgs GPUTreeLearner::VoteGlobalArgs(const dev::KArgs& a, int pick_in_find) const {
+  dev::KArgs glob = a;
+  glob.p.vote_phase = 2;
+  glob.p.sp = params_;
+  glob.pick_in_find = pick_in_find;
+  glob.num_scan = vote_k_;
+  return glob;
 }
 
 // one round: single process, every kernel back to back; distributed, the histograms
@@ -1327,6 +1339,18 @@ void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
     ~SkipGuardScope() { dc->SetSkipGuard(nullptr); }
   } guard_scope{dc};
   dc->SetSkipGuard(&d_round_->done);
+  if (voting_) {
+    // the local scan of every child of the round, one vote for all of them, the global scan of
+    // the elected features (reference voting_parallel_tree_learner.cpp:300-343, per round)
+    const dev::KArgs glob = VoteGlobalArgs(a, 0);
+    dev::RoundSplitReduce(a, stream_);
+    dev::RoundFind(a, stream_);
+    RoundVoteExchange(glob);
+    dev::RoundFindElected(glob, stream_);
+    dc->SetSkipGuard(nullptr);
+    dev::RoundChildBestAndPlan(glob, stream_);
+    return;
+  }
   const size_t owned = static_cast<size_t>(round_k_) * rs_block_ * 2;
   // (the owner-major send buffer was cleared by the previous round's split scans, or by the root)
   dev::RoundSplitReduce(a, stream_);
@@ -1344,8 +1368,22 @@ void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
   dev::RoundChildBestAndPlan(a, stream_);
 }
 
+void GPUTreeLearner::RoundVoteExchange(const dev::KArgs& glob) {
+  DeviceComm* dc = Network::device_comm();  // (round growth runs with a device communicator only)
+  dev::RoundVoteLocal(glob, stream_);
+  const size_t prop_bytes = sizeof(dev::VoteEntry) * 2 * static_cast<size_t>(round_k_) * vote_k_;
+  char* vb = reinterpret_cast<char*>(d_vote_buf_);
+  dc->Allgather(vb + prop_bytes * rank_, vb, prop_bytes, stream_);
+  dev::RoundVoteElect(glob, stream_);
+  dc->AllreduceSumI64(d_vote_hist_, 2 * static_cast<size_t>(round_k_) * vote_k_ * 2 * glob.p.max_feature_bins, stream_);
+}
+
 double GPUTreeLearner::RoundCollectiveBytes() const {
   if (!distributed_) return 0.0;
+  if (voting_) {
+    const double sides = 2.0 * round_k_ * vote_k_;
+    return sides * sizeof(dev::VoteEntry) * world_ + sides * 2.0 * args_.p.max_feature_bins * sizeof(long long);
+  }
   const double per = 2.0 * round_k_ * std::max(1, max_owned_) *
                      (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0)) * world_;
   return per + (data_parallel_ ? sizeof(long long) * 2.0 * round_k_ * rs_block_ * world_ : 0.0);
@@ -1353,7 +1391,7 @@ double GPUTreeLearner::RoundCollectiveBytes() const {
 
 // ---------------------------------------------------------------- round growth
 bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
-  if (round_k_ <= 1 || voting_ || d_round_ == nullptr) return false;
+  if (round_k_ <= 1 || d_round_ == nullptr) return false;
   if (distributed_ && Network::device_comm() == nullptr) return false;  // (host collectives: one split per step)
   // the split order depends on more than each leaf's own rows: per-node feature samples and
   // extra_trees draws are consumed in the sequential order, CEGB's coupled penalties change

@@ -202,6 +202,11 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int32_t* d_vote_list_ = nullptr;        // [2][vote_k]
   long long* d_vote_hist_ = nullptr;      // [2][vote_k][max_feature_bins][2]
   void VoteExchange(const dev::KArgs& glob, bool root);
+  // voting: the arguments of the global scan of the elected features (Params::vote_phase 2)
+  dev::KArgs VoteGlobalArgs(const dev::KArgs& a, int pick_in_find) const;
+  // voting rounds: proposals of every child of the round -> allgather -> elections + elected
+  // local histograms -> all-reduce (one of each per round)
+  void RoundVoteExchange(const dev::KArgs& glob);
   bool distributed_ = false;    // kData / kFeature on more than one rank
   int world_ = 1, rank_ = 0;
   // feature ownership (distributed): contiguous storage-group blocks balanced by bins

@@ -156,18 +156,22 @@ def test_device_distributed_with_efb_bundles(learner, gpu_available):
     assert _trees(res[0].value) == _trees(res[1].value)
 
 
-@pytest.mark.parametrize("learner,world", [("data", 2), ("data", 4), ("feature", 3)])
-def test_distributed_round_growth_equals_one_split_per_step(learner, world, gpu_available, monkeypatch, tmp_path):
-    """Distributed round growth (round_kernels.hip: up to 8 leaves expanded per round, the
+@pytest.mark.parametrize("learner,world,k", [("data", 2, 8), ("data", 4, 8), ("feature", 3, 8), ("voting", 2, 6),
+                                             ("voting", 4, 6)])
+def test_distributed_round_growth_equals_one_split_per_step(learner, world, k, gpu_available, monkeypatch, tmp_path):
+    """Distributed round growth (round_kernels.hip: up to k leaves expanded per round, the
     histograms reduce-scattered and the per-feature records gathered once per round instead of
-    once per split) grows the same trees as one split per step (LGBM_AMD_ROUND_K=1), on every
-    rank; the iteration log shows the rounds (fewer than the splits)."""
+    once per split; voting: one proposal allgather and one elected-histogram all-reduce per
+    round for all of the round's children) grows the same trees as one split per step
+    (LGBM_AMD_ROUND_K=1), on every rank; the iteration log shows the rounds (fewer than the
+    splits)."""
+    extra = {"top_k": 4} if learner == "voting" else {}
     monkeypatch.setenv("LGBM_AMD_ROUND_K", "1")
-    _, _, _, base = _run(learner, world, rounds=6)
-    monkeypatch.setenv("LGBM_AMD_ROUND_K", "8")
+    _, _, _, base = _run(learner, world, rounds=6, **extra)
+    monkeypatch.setenv("LGBM_AMD_ROUND_K", str(k))
     log = tmp_path / "iters.jsonl"
     monkeypatch.setenv("LGBM_AMD_ITER_LOG", str(log))
-    _, _, _, spec = _run(learner, world, rounds=6)
+    _, _, _, spec = _run(learner, world, rounds=6, **extra)
     monkeypatch.delenv("LGBM_AMD_ITER_LOG")
     for (mb, _), (ms, _) in zip(base, spec):
         assert _trees(mb) == _trees(ms)
