@@ -37,6 +37,9 @@ namespace {
 #ifndef LGBM_FIND_WAVE_OCC
 #define LGBM_FIND_WAVE_OCC 4
 #endif
+#ifndef LGBM_ORACLE_SEQ
+#define LGBM_ORACLE_SEQ 0  // A/B timing oracles only: 1 sequential (g, h) gathers, 2 also sequential row words
+#endif
 constexpr unsigned kRoundFlatMax = 128;  // split-scan grid rows up to this size count on one counter
 constexpr int kRPartWaves = kPartThreads / kWave;
 constexpr int kRGatherNarrow = 2, kRGatherWide = 8, kRGatherNarrowMaxWords = 8;
@@ -331,8 +334,16 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
             for (int k = 0; k < GR; ++k) {
               const int jr = j0 + k * t.rpp;
               const int x = jr < nh ? rowlist[jr] : -1;
+#if LGBM_ORACLE_SEQ
+              // timing oracle (wrong histograms): the gathers read the parent range's positions
+              // instead of the rows, i.e. leaf-ordered copies that cost nothing to maintain
+              const int xp = X.pb + t0 + jr;
+              v_[k] = GhAt(a, x >= 0 ? xp : 0);
+              w_[k] = x >= 0 ? bins32[static_cast<int64_t>(LGBM_ORACLE_SEQ >= 2 ? xp : x) * wpr + wi] : 0u;
+#else
               v_[k] = GhAt(a, x >= 0 ? x : 0);
               w_[k] = x >= 0 ? bins32[static_cast<int64_t>(x) * wpr + wi] : 0u;  // word 0: every bin skipped
+#endif
             }
           };
           if (t.rs < nh) fetch(t.rs, wd, v);
