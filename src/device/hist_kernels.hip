@@ -124,6 +124,7 @@ __global__ __launch_bounds__(256) void k_hist_reduce(KArgs a) {
     }
   }
   const int pos = a.rs_pos != nullptr ? a.rs_pos[bin] : bin;  // owner-major layout (data-parallel)
+  if (pos < 0) return;  // (a group no rank scans this tree)
   if (nblk <= kReduceChunk) {
     out[2 * pos] = g;
     out[2 * pos + 1] = h;

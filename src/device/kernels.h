@@ -83,16 +83,21 @@ struct KArgs {
   int32_t blk_min_rows;      // k_split: parent rows per row block, lower bound
   int32_t pick_in_find;      // the last split-scan workgroup of a step picks the next split (else k_pick)
   // distributed learners (reference data_parallel_tree_learner.cpp / feature_parallel_*):
-  // features are owned by ranks in contiguous storage-group blocks; a rank scans its own
-  const int32_t* feat_list;  // [num_scan] inner features this rank scans (null: all)
-  int32_t num_scan;          // features this rank scans
+  // features are owned by ranks in storage-group blocks; a rank scans its own.  Data-parallel
+  // with feature_fraction < 1 re-assigns the tree's used groups to the least-loaded rank by
+  // bins every tree (reference DataParallelTreeLearner::BeforeTrain); slots past the rank's
+  // features hold -1 (the grids keep one size for the captured graphs)
+  const int32_t* feat_list;  // [num_scan] inner features this rank scans (null: all; -1: none)
+  int32_t num_scan;          // features this rank scans (capacity)
   const int32_t* fb_index;   // feat_best slot of feature f for side 0 (null: f); side 1 adds fb_side
   int32_t fb_side;
   // data-parallel: the reduce kernel writes bin b at rs_pos[b] (owner-major blocks, padded
-  // to equal size for the reduce-scatter) and the split scan reads this rank's globally
-  // summed block from owned_hist (bin b at 2 * (b - owned_bin_lo)); null: the local scratch
+  // to equal size for the reduce-scatter; -1: a group no rank scans this tree) and the split
+  // scan reads owned feature f's globally summed bins from owned_hist at 2 * owned_off[f];
+  // null: the local scratch
   const int32_t* rs_pos;
   const long long* owned_hist;
+  const int32_t* owned_off;
   int32_t owned_bin_lo;
   // histogram column range (feature-parallel: the words of this rank's features)
   int32_t tile_w0, tile_w1;

@@ -680,6 +680,7 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
   int pos = bin;
   if (dp) {
     const int rp = a.rs_pos[bin], owner = rp / a.rs_block;
+    if (rp < 0) return;  // (a group no rank scans this tree)
     out = a.round_send;
     pos = (owner * a.round_k + j) * a.rs_block + (rp - owner * a.rs_block);
   }
@@ -840,7 +841,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const bool vote_global = a.round_vote && a.p.vote_phase == 2;
   int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
   if (vote_global) f = a.vote_list[y * a.p.vote_k + blockIdx.x];
-  const bool vote_empty = vote_global && f < 0;
+  const bool vote_empty = f < 0;  // (an empty elected slot, or a padded owner slot)
   if (vote_empty) f = 0;
   const int tid = threadIdx.x;
   const int NF = a.p.num_features;
@@ -950,7 +951,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     long long* dst = vote_global ? a.vote_hist + static_cast<size_t>(y * a.p.vote_k + blockIdx.x) * 2 * a.p.max_feature_bins
                                  : a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = vote_global ? dst
-                           : owner ? a.round_owned + 2 * (static_cast<size_t>(j) * a.rs_block + (F.hist_offset - a.owned_bin_lo))
+                           : owner ? a.round_owned + 2 * (static_cast<size_t>(j) * a.rs_block + a.owned_off[f])
                                    : RoundScratch(a, parity, j) + 2 * F.hist_offset;
     const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
     const unsigned long long* part = a.partials + static_cast<size_t>(blk_off) * pstride + static_cast<size_t>(units) * F.hist_offset;

@@ -163,6 +163,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   // empty slot still takes part in the step's workgroup count)
   const bool vote_global = a.p.vote_phase == 2;
   int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
+  if (f < 0 && !vote_global) return;  // a padded owner slot (distributed learners: no pick in this kernel)
   if (vote_global) f = a.vote_list[blockIdx.y * a.p.vote_k + blockIdx.x];
   const bool vote_empty = vote_global && f < 0;
   if (vote_empty) f = 0;
@@ -388,7 +389,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
                                                      a.p.max_feature_bins
                                  : a.hist + static_cast<size_t>(slot) * nh + 2 * F.hist_offset;
     const long long* src = (vote_global || rescan) ? dst
-                           : a.owned_hist != nullptr ? a.owned_hist + 2 * (F.hist_offset - a.owned_bin_lo)
+                           : a.owned_hist != nullptr ? a.owned_hist + 2 * a.owned_off[f]
                                                      : StepScratch(a, parity) + 2 * F.hist_offset;
     const size_t pstride = static_cast<size_t>(units) * a.p.total_bins;
     const unsigned long long* part = a.partials + static_cast<size_t>(units) * F.hist_offset;

@@ -532,6 +532,7 @@ void GPUTreeLearner::UploadData() {
   a.fb_side = num_features_;
   a.rs_pos = nullptr;
   a.owned_hist = nullptr;
+  a.owned_off = nullptr;
   a.owned_bin_lo = 0;
   a.tile_bins = tile_bins_for(tile_words);
   a.sp_ptr = d_sp_ptr_;
@@ -602,16 +603,18 @@ void GPUTreeLearner::UploadData() {
   } else if (distributed_) {
     // this rank scans its own features; the per-feature results are gathered rank-major
     a.feat_list = d_feat_list_;
-    a.num_scan = static_cast<int32_t>(owned_feats_.size());
+    // (per-tree owners: every capacity slot has a workgroup, the unused ones exit)
+    a.num_scan = dyn_owner_ ? max_owned_ : static_cast<int32_t>(owned_feats_.size());
     a.fb_index = d_fb_index_;
     a.fb_side = max_owned_;
     int owned_cats = 0;
     for (int f : owned_feats_) owned_cats += feats[f].is_cat ? 1 : 0;
-    a.p.has_cat = owned_cats;
+    a.p.has_cat = dyn_owner_ ? (cats.empty() ? 0 : cat_cap_) : owned_cats;
     a.cat_list = d_owned_cats_;
     if (mode_ == Mode::kData) {
       a.rs_pos = d_rs_pos_;
       a.owned_hist = d_owned_hist_;
+      a.owned_off = d_owned_off_;
       a.owned_bin_lo = owned_bin_lo_;
     } else {
       // feature-parallel: every rank has every row; histograms only over this rank's words
@@ -707,27 +710,89 @@ void GPUTreeLearner::AllocRoundState() {
 }
 
 // Feature ownership of the distributed learners (reference data_parallel_tree_learner.cpp
-// BeforeTrain :61-123 assigns used features to the least-loaded rank per tree; here the
-// storage groups are cut into `world` contiguous blocks balanced by histogram bins once, so
-// a rank's bins are one contiguous range of the histogram -- the reduce-scatter block it
-// receives -- and its features are gathered rank-major after each scan):
-//   owner(group g) = min(world - 1, mid(g) * world / total_bins), monotone in g.
+// BeforeTrain :61-123 assigns the tree's used features to the least-loaded rank by bins).
+// Here a rank owns whole storage groups; its groups' bins, packed in group order, are its
+// block of the owner-major reduce-scatter buffer (rs_pos), and its features are gathered
+// rank-major after each scan (fb_index).  The static layout cuts the groups into `world`
+// contiguous blocks balanced by bins,
+//   owner(group g) = min(world - 1, mid(g) * world / total_bins), monotone in g;
+// data-parallel training with feature_fraction < 1 re-assigns the tree's used groups every
+// tree, greedily to the rank with the fewest bins so far (OwnershipForTree), inside the
+// capacities the static layout sized the buffers and graphs for.
+GPUTreeLearner::OwnerLayout GPUTreeLearner::BuildOwnerLayout(const std::vector<int>& gown) const {
+  OwnerLayout L;
+  std::vector<int> load(world_, 0), gpos(num_groups_, -1);
+  for (int g = 0; g < num_groups_; ++g) {
+    if (gown[g] < 0) continue;
+    gpos[g] = load[gown[g]];
+    load[gown[g]] += group_off_[g + 1] - group_off_[g];
+  }
+  L.max_block = *std::max_element(load.begin(), load.end());
+  std::vector<int> count(world_, 0), local(num_features_, -1);
+  for (int f = 0; f < num_features_; ++f) {
+    const int o = gown[data_->Feature2Group(f)];
+    if (o < 0) continue;
+    local[f] = count[o]++;
+    if (o == rank_) L.feats.push_back(f);
+  }
+  L.max_feats = *std::max_element(count.begin(), count.end());
+  L.fb_index.assign(std::max(1, num_features_), 0);
+  L.owned_off.assign(std::max(1, num_features_), 0);
+  for (int f = 0; f < num_features_; ++f) {
+    const int g = data_->Feature2Group(f), o = gown[g];
+    if (o < 0) continue;  // (never read: the feature is not scanned this tree)
+    L.fb_index[f] = o * 2 * max_owned_ + local[f];
+    L.owned_off[f] = gpos[g] + (feat_hist_off_[f] - group_off_[g]);
+  }
+  L.rs_pos.assign(std::max(1, total_bins_), -1);
+  for (int g = 0; g < num_groups_; ++g) {
+    if (gown[g] < 0) continue;
+    for (int b = group_off_[g]; b < group_off_[g + 1]; ++b) L.rs_pos[b] = gown[g] * rs_block_ + gpos[g] + (b - group_off_[g]);
+  }
+  for (int f : L.feats) {
+    if (data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) L.cats.push_back(f);
+  }
+  return L;
+}
+
+void GPUTreeLearner::UploadOwnerLayout(const OwnerLayout& L) {
+  std::vector<int32_t> fl(std::max(1, max_owned_), -1), cl(std::max(1, cat_cap_), -1);
+  std::copy(L.feats.begin(), L.feats.end(), fl.begin());
+  std::copy(L.cats.begin(), L.cats.end(), cl.begin());
+  HIPCHECK(hipMemcpyAsync(d_feat_list_, fl.data(), sizeof(int32_t) * fl.size(), hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_owned_cats_, cl.data(), sizeof(int32_t) * cl.size(), hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_fb_index_, L.fb_index.data(), sizeof(int32_t) * L.fb_index.size(), hipMemcpyHostToDevice,
+                          stream_));
+  HIPCHECK(hipMemcpyAsync(d_owned_off_, L.owned_off.data(), sizeof(int32_t) * L.owned_off.size(),
+                          hipMemcpyHostToDevice, stream_));
+  HIPCHECK(hipMemcpyAsync(d_rs_pos_, L.rs_pos.data(), sizeof(int32_t) * L.rs_pos.size(), hipMemcpyHostToDevice,
+                          stream_));
+  HIPCHECK(hipStreamSynchronize(stream_));  // (the host vectors are temporaries)
+}
+
 void GPUTreeLearner::SetupOwnership() {
   owned_feats_.clear();
   max_owned_ = 0;
   rs_block_ = 0;
   owned_bin_lo_ = 0;
+  dyn_owner_ = false;
   if (!distributed_ || mode_ == Mode::kVoting) return;
-  std::vector<int32_t> goff(num_groups_ + 1, total_bins_);
-  for (int g = 0; g < num_groups_; ++g) goff[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
+  group_off_.assign(num_groups_ + 1, total_bins_);
+  for (int g = 0; g < num_groups_; ++g) group_off_[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
+  feat_hist_off_.assign(std::max(1, num_features_), 0);
+  for (int f = 0; f < num_features_; ++f) feat_hist_off_[f] = static_cast<int32_t>(data_->FeatureHistOffset(f));
   std::vector<int> gown(num_groups_);
   std::vector<int> lo(world_, -1), hi(world_, -1);
+  int max_group_bins = 1, max_group_feats = 1;
+  std::vector<int> gfeats(num_groups_, 0);
+  for (int f = 0; f < num_features_; ++f) max_group_feats = std::max(max_group_feats, ++gfeats[data_->Feature2Group(f)]);
   for (int g = 0; g < num_groups_; ++g) {
-    const long long mid2 = static_cast<long long>(goff[g]) + goff[g + 1];
+    const long long mid2 = static_cast<long long>(group_off_[g]) + group_off_[g + 1];
     gown[g] = static_cast<int>(std::min<long long>(world_ - 1, mid2 * world_ / (2LL * std::max(1, total_bins_))));
     const int r = gown[g];
-    if (lo[r] < 0) lo[r] = goff[g];
-    hi[r] = goff[g + 1];
+    if (lo[r] < 0) lo[r] = group_off_[g];
+    hi[r] = group_off_[g + 1];
+    max_group_bins = std::max(max_group_bins, group_off_[g + 1] - group_off_[g]);
   }
   int prev_end = 0;
   for (int r = 0; r < world_; ++r) {
@@ -735,35 +800,34 @@ void GPUTreeLearner::SetupOwnership() {
     prev_end = hi[r];
     rs_block_ = std::max(rs_block_, hi[r] - lo[r]);
   }
-  rs_block_ = std::max(rs_block_, 1);
   owned_bin_lo_ = lo[rank_];
-  std::vector<int> count(world_, 0), local(num_features_, 0), fown(num_features_, 0);
-  for (int f = 0; f < num_features_; ++f) {
-    fown[f] = gown[data_->Feature2Group(f)];
-    local[f] = count[fown[f]]++;
-    if (fown[f] == rank_) owned_feats_.push_back(f);
-  }
+  std::vector<int> count(world_, 0);
+  for (int f = 0; f < num_features_; ++f) count[gown[data_->Feature2Group(f)]]++;
   for (int r = 0; r < world_; ++r) max_owned_ = std::max(max_owned_, count[r]);
+  // per-tree ownership: blocks of the greedy assignment fit avg + one group (bins); the feature
+  // capacity leaves room for an uneven count -- a tree whose assignment exceeds either keeps
+  // the static layout
+  dyn_owner_ = mode_ == Mode::kData && config_->feature_fraction < 1.0 &&
+               !(std::getenv("LGBM_AMD_STATIC_OWNERS") != nullptr && std::getenv("LGBM_AMD_STATIC_OWNERS")[0] == '1');
+  int ncat = 0;
+  for (int f = 0; f < num_features_; ++f) ncat += data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical ? 1 : 0;
+  if (dyn_owner_) {
+    rs_block_ = std::max(rs_block_, (total_bins_ + world_ - 1) / world_ + max_group_bins);
+    max_owned_ = std::min(num_features_, std::max(max_owned_, (3 * num_features_ + 2 * world_ - 1) / (2 * world_) +
+                                                                    max_group_feats));
+  }
+  rs_block_ = std::max(rs_block_, 1);
   max_owned_ = std::max(max_owned_, 1);
-  std::vector<int32_t> fb_index(std::max(1, num_features_));
-  for (int f = 0; f < num_features_; ++f) fb_index[f] = fown[f] * 2 * max_owned_ + local[f];
-  std::vector<int32_t> rs_pos(std::max(1, total_bins_));
-  for (int g = 0; g < num_groups_; ++g) {
-    for (int b = goff[g]; b < goff[g + 1]; ++b) rs_pos[b] = gown[g] * rs_block_ + (b - lo[gown[g]]);
-  }
-  std::vector<int32_t> owned_cats;
-  for (int f : owned_feats_) {
-    if (data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) owned_cats.push_back(f);
-  }
-  auto upload = [&](const std::vector<int32_t>& v) {
-    int32_t* d = Alloc<int32_t>(std::max<size_t>(1, v.size()));
-    if (!v.empty()) HIPCHECK(hipMemcpy(d, v.data(), sizeof(int32_t) * v.size(), hipMemcpyHostToDevice));
-    return d;
-  };
-  d_feat_list_ = upload(std::vector<int32_t>(owned_feats_.begin(), owned_feats_.end()));
-  d_fb_index_ = upload(fb_index);
-  d_rs_pos_ = upload(rs_pos);
-  d_owned_cats_ = upload(owned_cats);
+  static_layout_ = BuildOwnerLayout(gown);
+  owned_feats_ = static_layout_.feats;
+  cat_cap_ = dyn_owner_ ? std::max(1, ncat) : std::max<int>(1, static_layout_.cats.size());
+  d_feat_list_ = Alloc<int32_t>(std::max(1, max_owned_));
+  d_fb_index_ = Alloc<int32_t>(std::max(1, num_features_));
+  d_rs_pos_ = Alloc<int32_t>(std::max(1, total_bins_));
+  d_owned_cats_ = Alloc<int32_t>(cat_cap_);
+  d_owned_off_ = Alloc<int32_t>(std::max(1, num_features_));
+  UploadOwnerLayout(static_layout_);
+  owner_layout_static_ = true;
   d_owned_hist_ = Alloc<long long>(2 * static_cast<size_t>(rs_block_));
   const size_t fb_bytes = 2 * static_cast<size_t>(max_owned_) *
                           (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0));
@@ -771,9 +835,10 @@ void GPUTreeLearner::SetupOwnership() {
   split_collective_bytes_ = rs_bytes + static_cast<double>(fb_bytes) * world_;
   root_collective_bytes_ = split_collective_bytes_ + 3 * sizeof(double) + 3 * sizeof(uint32_t);
   if (mode_ == Mode::kData) {
-    Log::Info("data-parallel device learner, rank %d of %d: %d features, histogram bins [%d, %d); per split "
+    Log::Info("data-parallel device learner, rank %d of %d: %d features, histogram bins [%d, %d)%s; per split "
               "reduce-scatter %zu bytes in / %zu out, split-record allgather %zu bytes per rank",
               rank_, world_, static_cast<int>(owned_feats_.size()), lo[rank_], hi[rank_],
+              dyn_owner_ ? " (re-assigned per tree over the used features)" : "",
               sizeof(long long) * 2 * static_cast<size_t>(rs_block_) * world_,
               sizeof(long long) * 2 * static_cast<size_t>(rs_block_), fb_bytes);
   } else {
@@ -781,6 +846,46 @@ void GPUTreeLearner::SetupOwnership() {
               "split-record allgather %zu bytes per rank", rank_, world_, static_cast<int>(owned_feats_.size()),
               lo[rank_], hi[rank_], fb_bytes);
   }
+}
+
+// the tree's used groups to the rank with the fewest bins so far, in group order (every rank
+// computes the same assignment from the same bytree sample)
+void GPUTreeLearner::OwnershipForTree() {
+  if (!dyn_owner_) return;
+  std::vector<int> gown(num_groups_, -1), load(world_, 0);
+  std::vector<char> used(num_groups_, 0);
+  for (int f = 0; f < num_features_; ++f) {
+    if (h_mask_[f]) used[data_->Feature2Group(f)] = 1;
+  }
+  for (int g = 0; g < num_groups_; ++g) {
+    if (!used[g]) continue;
+    const int r = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
+    gown[g] = r;
+    load[r] += group_off_[g + 1] - group_off_[g];
+  }
+  OwnerLayout L = BuildOwnerLayout(gown);
+  int ncats_max = 0;
+  {
+    std::vector<int> cc(world_, 0);
+    for (int f = 0; f < num_features_; ++f) {
+      const int o = gown[data_->Feature2Group(f)];
+      if (o >= 0 && data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) ncats_max = std::max(ncats_max, ++cc[o]);
+    }
+  }
+  const bool fits = L.max_block <= rs_block_ && L.max_feats <= max_owned_ && ncats_max <= cat_cap_;
+  if (!fits) {
+    if (!owner_layout_static_) UploadOwnerLayout(static_layout_);
+    owner_layout_static_ = true;
+    owned_feats_ = static_layout_.feats;
+    Log::Debug("per-tree ownership exceeds the layout's capacity (block %d / %d bins, %d / %d features): static owners",
+               L.max_block, rs_block_, L.max_feats, max_owned_);
+    return;
+  }
+  UploadOwnerLayout(L);
+  owner_layout_static_ = false;
+  owned_feats_ = L.feats;
+  Log::Debug("rank %d owns %zu of the tree's features (%d bins, largest block %d)", rank_, L.feats.size(),
+             load[rank_], L.max_block);
 }
 
 // interaction constraints as per-feature constraint bitmasks (device-resident growth
@@ -1626,6 +1731,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   col_sampler_.ResetByTree();
   const auto& mask = col_sampler_.is_feature_used_bytree();
   for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
+  OwnershipForTree();
   dev::KArgs a = args_;
   const bool bynode = config_->feature_fraction_bynode < 1.0;
   const bool bynode_ic = bynode && col_sampler_.has_interaction_constraints();

@@ -209,7 +209,21 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void RoundVoteExchange(const dev::KArgs& glob);
   bool distributed_ = false;    // kData / kFeature on more than one rank
   int world_ = 1, rank_ = 0;
-  // feature ownership (distributed): contiguous storage-group blocks balanced by bins
+  // feature ownership (distributed): storage-group blocks balanced by bins (SetupOwnership);
+  // data-parallel with feature_fraction < 1: re-assigned per tree over the used groups
+  struct OwnerLayout {
+    std::vector<int> feats, cats;              // this rank's features / categorical ones
+    std::vector<int32_t> fb_index, owned_off, rs_pos;
+    int max_block = 0, max_feats = 0;          // largest rank block (bins) / feature count
+  };
+  OwnerLayout BuildOwnerLayout(const std::vector<int>& group_owner) const;  // (owner -1: not scanned)
+  void UploadOwnerLayout(const OwnerLayout& layout);
+  void OwnershipForTree();
+  OwnerLayout static_layout_;
+  bool dyn_owner_ = false, owner_layout_static_ = true;
+  int cat_cap_ = 1;
+  std::vector<int32_t> group_off_, feat_hist_off_;
+  int32_t* d_owned_off_ = nullptr;
   std::vector<int> owned_feats_;
   int max_owned_ = 0;           // features of the largest owner (feat_best block of a rank per side)
   int owned_bin_lo_ = 0;

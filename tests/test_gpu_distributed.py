@@ -131,6 +131,24 @@ def test_device_voting_parallel(world, gpu_available, capfd, monkeypatch):
     assert _splits(out[0][0], 0) == _splits(host[0][0], 0)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_data_parallel_per_tree_ownership(world, gpu_available, monkeypatch, capfd):
+    """feature_fraction < 1: the tree's used feature groups are re-assigned to the least-loaded
+    rank by bins every tree (reference DataParallelTreeLearner::BeforeTrain); ownership only
+    decides which rank scans which feature, so the models equal the static-owner layout's
+    (LGBM_AMD_STATIC_OWNERS=1) on every rank."""
+    capfd.readouterr()
+    _, _, _, dyn = _run("data", world, rounds=6, feature_fraction=0.6, verbose=2)
+    log = capfd.readouterr().out
+    assert "re-assigned per tree over the used features" in log
+    monkeypatch.setenv("LGBM_AMD_STATIC_OWNERS", "1")
+    _, _, _, stat = _run("data", world, rounds=6, feature_fraction=0.6)
+    for (md, _), (ms, _) in zip(dyn, stat):
+        assert _trees(md) == _trees(ms)
+    for m, _ in dyn[1:]:
+        assert _trees(m) == _trees(dyn[0][0])
+
+
 @pytest.mark.parametrize("learner", ["data", "voting"])
 def test_device_distributed_with_efb_bundles(learner, gpu_available):
     """Sparse mutually exclusive columns bundled by EFB (rank 0's bundles shared by every rank)
