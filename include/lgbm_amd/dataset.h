@@ -197,6 +197,48 @@ class Dataset {
     return gb - g.bin_offsets[s] + (m->GetMostFreqBin() == 0 ? 1 : 0);
   }
 
+  // FeatureBin for rows read in ascending order (a leaf's rows, a score walk's chunk): a sparse
+  // group's stored rows are walked forward from the last hit by galloping search instead of a
+  // binary search over all of them per row (a row below the last one restarts the walk)
+  struct BinReader {
+    const FeatureGroup* g = nullptr;
+    size_t k = 0;
+    uint32_t lo = 0, hi = 0, mfb = 0, add = 0;
+    inline uint32_t Get(data_size_t row) {
+      uint32_t gb;
+      if (!g->sparse) {
+        gb = g->ValAt(static_cast<size_t>(row));
+      } else {
+        const std::vector<data_size_t>& r = g->sp_rows;
+        const size_t n = r.size();
+        if (k > 0 && r[k - 1] >= row) k = 0;
+        size_t lo_i = k, hi_i = k, step = 1;
+        while (hi_i < n && r[hi_i] < row) {
+          lo_i = hi_i + 1;
+          hi_i += step;
+          step <<= 1;
+        }
+        if (hi_i > n) hi_i = n;
+        k = static_cast<size_t>(std::lower_bound(r.begin() + lo_i, r.begin() + hi_i, row) - r.begin());
+        gb = (k < n && r[k] == row) ? g->ValAt(k) : 0u;
+      }
+      if (gb < lo || gb >= hi) return mfb;
+      return gb - lo + add;
+    }
+  };
+  BinReader FeatureBinReader(int inner) const {
+    BinReader b;
+    const FeatureGroup& g = groups_[feature2group_[inner]];
+    const int s = feature2subfeature_[inner];
+    const BinMapper* m = bin_mappers_[inner].get();
+    b.g = &g;
+    b.lo = g.bin_offsets[s];
+    b.hi = g.bin_offsets[s + 1];
+    b.mfb = m->GetMostFreqBin();
+    b.add = m->GetMostFreqBin() == 0 ? 1 : 0;
+    return b;
+  }
+
   double RealThreshold(int inner, uint32_t threshold) const { return bin_mappers_[inner]->BinToValue(threshold); }
   // feature value -> bin threshold for forced splits
   uint32_t BinThreshold(int inner, double threshold_double) const;

@@ -226,15 +226,21 @@ void Tree::AddPredictionToScore(const Dataset* data, const data_size_t* idx, dat
     default_bins[i] = m->GetDefaultBin();
     max_bins[i] = static_cast<uint32_t>(m->num_bin() - 1);
   }
-#pragma omp parallel for schedule(static, 512) if (n >= 1024)
-  for (data_size_t i = 0; i < n; ++i) {
-    const data_size_t r = idx ? idx[i] : i;
-    int node = 0;
-    while (node >= 0) {
-      const uint32_t b = data->FeatureBin(split_feature_inner_[node], r);
-      node = DecisionInner(b, node, default_bins[node], max_bins[node]);
+  // (one bin reader per node and thread: each thread's rows ascend within its chunks)
+#pragma omp parallel if (n >= 1024)
+  {
+    std::vector<Dataset::BinReader> rd(num_leaves_ - 1);
+    for (int i = 0; i < num_leaves_ - 1; ++i) rd[i] = data->FeatureBinReader(split_feature_inner_[i]);
+#pragma omp for schedule(static, 512)
+    for (data_size_t i = 0; i < n; ++i) {
+      const data_size_t r = idx ? idx[i] : i;
+      int node = 0;
+      while (node >= 0) {
+        const uint32_t b = rd[node].Get(r);
+        node = DecisionInner(b, node, default_bins[node], max_bins[node]);
+      }
+      score[r] += leaf_value_[~node];
     }
-    score[r] += leaf_value_[~node];
   }
 }
 

@@ -455,8 +455,8 @@ data_size_t SerialTreeLearner::PartitionLeaf(int leaf, int inner, const SplitInf
   const MissingType mt = m->missing_type();
   std::vector<uint32_t> bits;
   if (is_cat) bits = common::ConstructBitset(s.cat_threshold.data(), s.num_cat_threshold);
-  auto goes_left = [&](data_size_t row) -> bool {
-    const uint32_t b = data_->FeatureBin(inner, row);
+  auto goes_left = [&](Dataset::BinReader& rd, data_size_t row) -> bool {
+    const uint32_t b = rd.Get(row);
     if (is_cat) return common::FindInBitset(bits.data(), static_cast<int>(bits.size()), b);
     if ((mt == MissingType::Zero && b == default_bin) || (mt == MissingType::NaN && b == nan_bin)) return s.default_left;
     return b <= s.threshold;
@@ -469,8 +469,9 @@ data_size_t SerialTreeLearner::PartitionLeaf(int leaf, int inner, const SplitInf
   for (int b = 0; b < nb; ++b) {
     const data_size_t s0 = b * bs, e0 = std::min(cnt, s0 + bs);
     data_size_t l = 0, r = 0;
+    Dataset::BinReader rd = data_->FeatureBinReader(inner);  // (a leaf's rows are ascending)
     for (data_size_t i = s0; i < e0; ++i) {
-      if (goes_left(idx[i])) tmp_left_[begin + s0 + l++] = idx[i];
+      if (goes_left(rd, idx[i])) tmp_left_[begin + s0 + l++] = idx[i];
       else tmp_right_[begin + s0 + r++] = idx[i];
     }
     lc[b] = l;
