@@ -1,0 +1,358 @@
+// MI355X tree learner: round growth orchestration -- pools, the round sequence and its
+// collectives, the growth-mode choice and the host loop over round segments (round_kernels.hip).
+#include "gpu_learner_internal.h"
+
+namespace lgbm_amd {
+
+// histogram slots and splittable rows (nodes) of a tree: one slot per leaf, or -- round
+// growth -- one per expansion (the root's, then the histogrammed child's of each), two nodes
+// per expansion; 3 * num_leaves expansions leave the speculation 2 * num_leaves of waste,
+// 2 * num_leaves when the slots would pass 16 GiB
+void GPUTreeLearner::SizeRoundPools(int n_leaves) {
+  hist_slots_ = n_leaves;
+  split_rows_ = n_leaves;
+  if (round_k_ > 1) {
+    const double slot_bytes = 16.0 * static_cast<double>(total_bins_);
+    const int per = slot_bytes * 3.0 * n_leaves > 16.0 * (1ull << 30) ? 2 : 3;
+    hist_slots_ = per * n_leaves;
+    split_rows_ = 2 * per * n_leaves;
+  }
+  args_.round_nodes = split_rows_;
+  args_.round_emax = std::min(hist_slots_ - 1, (split_rows_ - 1) / 2);
+  args_.round_vmax = round_vmax_;
+}
+
+void GPUTreeLearner::AllocRoundState() {
+  dev::KArgs& a = args_;
+  a.rnode = nullptr;
+  a.cbest = nullptr;
+  a.cbest_cat = nullptr;
+  a.child_cnt = nullptr;
+  if (round_k_ <= 1) return;
+  d_round_ = Alloc<dev::Round>(1);
+  d_rnode_ = Alloc<dev::RNode>(split_rows_);
+  d_cbest_ = Alloc<dev::FeatureBest>(split_rows_);
+  d_cbest_cat_ = Alloc<uint32_t>(static_cast<size_t>(split_rows_) * kMaxCatWords);
+  const size_t cnt = 2 * static_cast<size_t>(dev::kMaxRoundExp) * (dev::kFindSub + 1) * dev::kFindSubStride;
+  d_child_cnt_ = Alloc<uint32_t>(cnt);
+  HIPCHECK(hipMemset(d_child_cnt_, 0, sizeof(uint32_t) * cnt));
+  HIPCHECK(hipMemset(d_round_, 0, sizeof(dev::Round)));
+  if (h_round_ == nullptr) {
+    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_round_), sizeof(dev::Round), hipHostMallocDefault));
+  }
+  a.rnode = d_rnode_;
+  a.cbest = d_cbest_;
+  a.cbest_cat = d_cbest_cat_;
+  a.child_cnt = d_child_cnt_;
+  round_hist_.clear();
+}
+
+// one round: single process, every kernel back to back; distributed, the histograms
+// reduce-scattered to their owners (data-parallel) and the per-feature results of every rank
+// gathered before the children's bests and the plan -- two collectives per round where one
+// split per step took two per split (reference data_parallel_tree_learner.cpp:154-247)
+void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
+  if (!distributed_) {
+    dev::RoundStep(a, stream_);
+    return;
+  }
+  DeviceComm* dc = Network::device_comm();
+  // a finished tree's remaining rounds skip their collectives on every rank (Round::done is
+  // replicated state); communicators that cannot skip run them.  The guard is cleared on every
+  // exit of this scope: a throw between here and the last collective (a failed launch caught
+  // by the graph capture) must not leave later collectives guarded by a stale flag
+  struct SkipGuardScope {
+    DeviceComm* dc;
+    ~SkipGuardScope() { dc->SetSkipGuard(nullptr); }
+  } guard_scope{dc};
+  dc->SetSkipGuard(&d_round_->done);
+  if (voting_) {
+    // the local scan of every child of the round, one vote for all of them, the global scan of
+    // the elected features (reference voting_parallel_tree_learner.cpp:300-343, per round)
+    const dev::KArgs glob = VoteGlobalArgs(a, 0);
+    dev::RoundSplitReduce(a, stream_);
+    dev::RoundFind(a, stream_);
+    RoundVoteExchange(glob);
+    dev::RoundFindElected(glob, stream_);
+    dc->SetSkipGuard(nullptr);
+    dev::RoundChildBestAndPlan(glob, stream_);
+    return;
+  }
+  const size_t owned = static_cast<size_t>(round_k_) * rs_block_ * 2;
+  // (the owner-major send buffer was cleared by the previous round's split scans, or by the root)
+  dev::RoundSplitReduce(a, stream_);
+  if (data_parallel_) dc->ReduceScatterSumI64(d_round_send_, d_round_owned_, owned, stream_);
+  dev::RoundFind(a, stream_);
+  const size_t per = 2 * static_cast<size_t>(round_k_) * std::max(1, max_owned_);
+  char* fb = reinterpret_cast<char*>(d_feat_best_);
+  dc->Allgather(fb + per * sizeof(dev::FeatureBest) * rank_, fb, per * sizeof(dev::FeatureBest), stream_);
+  if (num_cat_total_ > 0) {
+    char* fc = reinterpret_cast<char*>(d_feat_cat_);
+    const size_t cb = per * kMaxCatWords * sizeof(uint32_t);
+    dc->Allgather(fc + cb * rank_, fc, cb, stream_);
+  }
+  dc->SetSkipGuard(nullptr);  // (the plan's kernels are not collectives)
+  dev::RoundChildBestAndPlan(a, stream_);
+}
+
+void GPUTreeLearner::RoundVoteExchange(const dev::KArgs& glob) {
+  DeviceComm* dc = Network::device_comm();  // (round growth runs with a device communicator only)
+  dev::RoundVoteLocal(glob, stream_);
+  const size_t prop_bytes = sizeof(dev::VoteEntry) * 2 * static_cast<size_t>(round_k_) * vote_k_;
+  char* vb = reinterpret_cast<char*>(d_vote_buf_);
+  dc->Allgather(vb + prop_bytes * rank_, vb, prop_bytes, stream_);
+  dev::RoundVoteElect(glob, stream_);
+  dc->AllreduceSumI64(d_vote_hist_, 2 * static_cast<size_t>(round_k_) * vote_k_ * 2 * glob.p.max_feature_bins, stream_);
+}
+
+double GPUTreeLearner::RoundCollectiveBytes() const {
+  if (!distributed_) return 0.0;
+  if (voting_) {
+    const double sides = 2.0 * round_k_ * vote_k_;
+    return sides * sizeof(dev::VoteEntry) * world_ + sides * 2.0 * args_.p.max_feature_bins * sizeof(long long);
+  }
+  const double per = 2.0 * round_k_ * std::max(1, max_owned_) *
+                     (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0)) * world_;
+  return per + (data_parallel_ ? sizeof(long long) * 2.0 * round_k_ * rs_block_ * world_ : 0.0);
+}
+
+// ---------------------------------------------------------------- round growth
+// Round growth or one split per step (the trees are the same): rounds trade the per-split
+// latency chain for speculative work, which on large data (Criteo-shaped 255-leaf trees from
+// ~50M rows per GPU, profiles/r04_speculation_big_shards.md) costs more than the latency it
+// hides.  From 16M rows per rank (LGBM_AMD_ROUND_AUTO=1: always, 0: never) trees 1-2 are timed
+// with rounds and tree 4 with one split per step (3 captures its graph); the faster mode grows
+// every later tree.  Distributed ranks sum their times first, so all of them switch together.
+bool GPUTreeLearner::AutoGrowthRounds() {
+  if (auto_state_ == kAutoUnset) {
+    const char* e = std::getenv("LGBM_AMD_ROUND_AUTO");
+    double rows = static_cast<double>(num_data_);
+    if (distributed_ && Network::num_machines() > 1) {
+      std::vector<double> v{rows};
+      rows = Network::GlobalSum(v)[0] / Network::num_machines();
+    }
+    const bool on = e != nullptr ? e[0] == '1' : rows >= 16e6;
+    auto_state_ = on ? kAutoProbe : kAutoRounds;
+    auto_tree_ = 0;
+  }
+  if (auto_state_ == kAutoSteps) return false;
+  if (auto_state_ == kAutoProbe) return !(auto_tree_ == 3 || auto_tree_ == 4);
+  return true;
+}
+
+void GPUTreeLearner::AutoGrowthRecord(double ms) {
+  if (auto_state_ != kAutoProbe) return;
+  if (auto_tree_ == 1 || auto_tree_ == 2) auto_rounds_ms_ = std::min(auto_rounds_ms_, ms);
+  if (auto_tree_ == 4) {
+    std::vector<double> v{auto_rounds_ms_, ms};
+    if (distributed_ && Network::num_machines() > 1) v = Network::GlobalSum(v);
+    auto_state_ = v[1] < 0.97 * v[0] ? kAutoSteps : kAutoRounds;
+    Log::Info("device learner: growth timed at %.2f ms per tree with rounds, %.2f with one split per step: %s",
+              v[0] / std::max(1, distributed_ ? Network::num_machines() : 1),
+              v[1] / std::max(1, distributed_ ? Network::num_machines() : 1),
+              auto_state_ == kAutoSteps ? "one split per step from here on" : "rounds");
+  }
+  ++auto_tree_;
+}
+
+bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
+  if (round_k_ <= 1 || d_round_ == nullptr) return false;
+  if (distributed_ && Network::device_comm() == nullptr) return false;  // (host collectives: one split per step)
+  // the split order depends on more than each leaf's own rows: per-node feature samples and
+  // extra_trees draws are consumed in the sequential order, CEGB's coupled penalties change
+  // other leaves' gains, forced splits follow their own schedule
+  if (a.node_mask != nullptr || a.xt_base != nullptr || a.p.cegb || a.forced_n > 0 || a.p.mono_inter) return false;
+  return true;
+}
+
+// rounds of kRoundSeg expansions per graph launch: one root graph (the root + as many
+// segments as the recent trees needed, one cached graph per segment count) is launched; the
+// host then checks the Round record and adds segment graphs until the tree is done (a finished
+// tree's kernels exit at once: an over-provisioned round costs ~12 us, a missing one a host
+// round trip of ~60 us and a graph launch of ~8 us per segment)
+namespace {
+constexpr int kRoundSeg = 4;
+constexpr int kRoundFirstPred = 16;  // rounds enqueued for the first tree
+}
+
+int GPUTreeLearner::RunRounds(dev::KArgs a) {
+  a.rd = d_round_;
+  a.pick_in_find = 0;  // the root's split scan only publishes; RoundRootPlan picks
+  // (LGBM_AMD_KTRACE: k_round_split's phase times of one workgroup per round)
+  if (a.ktrace != nullptr) HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
+  const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
+  // distributed: the collectives are captured with the kernels when the communicator allows it
+  // (RCCL); the in-process communicator rendezvouses on the host, so its rounds run eagerly
+  DeviceComm* dc = distributed_ ? Network::device_comm() : nullptr;
+  const bool use_graph = !(ng != nullptr && ng[0] == '1') && (dc == nullptr || dc->CaptureSafe()) && !graph_capture_failed_;
+  const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
+  auto capture = [&](hipGraphExec_t* exec, bool root, int rounds) {
+    hipGraph_t g = nullptr;
+    HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+    std::string why;
+    try {
+      if (root) EnqueueRoot(a);
+      for (int r = 0; r < rounds; ++r) EnqueueRound(a);
+    } catch (const std::exception& e) {
+      why = e.what();
+    }
+    hipError_t ec = hipStreamEndCapture(stream_, &g);
+    if (why.empty() && ec == hipSuccess) ec = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
+    if (g != nullptr) (void)hipGraphDestroy(g);
+    if (!why.empty() || ec != hipSuccess) {
+      if (why.empty()) why = hipGetErrorString(ec);
+      (void)hipGetLastError();
+      *exec = nullptr;
+      if (!distributed_) Log::Fatal("device learner: capturing the round graphs failed: %s", why.c_str());
+      Log::Warning("device learner: capturing the round collectives failed (%s); launching rounds eagerly", why.c_str());
+      graph_capture_failed_ = true;
+      return false;
+    }
+    return true;
+  };
+  const int L = config_->num_leaves;
+  // segments of the root graph: the most rounds of the last trees (+1), rounded up
+  int want = kRoundFirstPred;
+  if (!round_hist_.empty()) want = *std::max_element(round_hist_.begin(), round_hist_.end()) + 1;
+  want = std::max(1, std::min(want, L - 1));
+  const int nseg = (want + kRoundSeg - 1) / kRoundSeg;
+  bool graph = use_graph;
+  if (graph && (round_seg_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
+                round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
+    if (dc != nullptr) dc->HostBarrier();
+    DestroyRoundGraphs();
+    graph = capture(&round_seg_exec_, false, kRoundSeg);
+    if (!graph) DestroyRoundGraphs();
+    round_graph_rows_ = a.num_rows;
+    round_graph_identity_ = a.root_identity;
+    round_graph_root_mode_ = root_mode;
+  }
+  if (graph) {
+    if (static_cast<int>(round_root_execs_.size()) <= nseg) round_root_execs_.resize(nseg + 1, nullptr);
+    if (round_root_execs_[nseg] == nullptr) {
+      if (dc != nullptr) dc->HostBarrier();
+      graph = capture(&round_root_execs_[nseg], true, nseg * kRoundSeg);
+      if (!graph) DestroyRoundGraphs();
+    }
+  }
+  last_stats_.graph = graph;
+  auto launch_seg = [&]() {
+    if (graph) {
+      HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
+    } else {
+      for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
+    }
+  };
+  if (graph) {
+    HIPCHECK(hipGraphLaunch(round_root_execs_[nseg], stream_));
+  } else {
+    EnqueueRoot(a);
+    for (int r = 0; r < nseg * kRoundSeg; ++r) EnqueueRound(a);
+  }
+  int launched = nseg * kRoundSeg;
+  const size_t rec_bytes = sizeof(dev::SplitRecord) * std::max(1, L - 1);
+  for (;;) {
+    HIPCHECK(hipMemcpyAsync(h_round_, d_round_, sizeof(dev::Round), hipMemcpyDeviceToHost, stream_));
+    HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, rec_bytes, hipMemcpyDeviceToHost, stream_));
+    WatchdogSync();
+    if (h_round_->done) break;
+    if (launched > 2 * L + kRoundSeg) {
+      Log::Fatal("device learner: round growth did not finish the tree after %d rounds (%d splits)", launched,
+                 h_round_->nsplit);
+    }
+    launch_seg();
+    launched += kRoundSeg;
+  }
+  if (a.ktrace != nullptr) {
+    std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
+    HIPCHECK(hipMemcpy(t.data(), a.ktrace, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
+    static const char* names[] = {"stage", "side", "resv", "write", "gather", "tail", "store"};
+    // plans: slot 16 entry time, 17..21 phase times (loads, replay + prediction, records of the
+    // expansions / accepted splits / changed leaves, barrier, sizing), 22 accepted, 23 planned,
+    // 25 the split scan's start
+    for (int r = 0; r <= h_round_->rounds && r < L; ++r) {
+      const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
+      if (o[16] == 0) continue;
+      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay+predict=%.2f records=%.2f sync=%.2f sizing=%.2f us; accepted %lld planned %lld\n",
+                   r, o[25] != 0 ? (o[16] - o[25]) / 100.0 : 0.0, o[17] / 100.0, o[18] / 100.0, o[19] / 100.0,
+                   o[20] / 100.0, o[21] / 100.0, o[22], o[23]);
+      if (o[26] != 0) {  // the planning workgroup's scan path, from the first scan workgroup's start
+        auto us = [&](int k) { return (o[k] - o[25]) / 100.0; };
+        std::fprintf(stderr, "  planner wg: entry %.2f loaded %.2f staged %.2f scanned %.2f arrived %.2f folded %.2f plan %.2f us\n",
+                     us(26), us(27), us(28), us(29), us(30), us(31), us(16));
+        if (o[12] != 0) {  // (LGBM_FIND_PHASES builds: the scan's phases)
+          std::fprintf(stderr, "  planner scan: begin %.2f prefix %.2f candidates %.2f argmax %.2f us\n", us(12), us(13),
+                       us(14), us(15));
+        }
+      }
+    }
+    for (int r = 1; r <= h_round_->rounds && r < L; ++r) {
+      const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
+      std::string line = "round " + std::to_string(r) + " exp " + std::to_string(o[10]) + " blocks " +
+                         std::to_string(o[11]) + " wg0: subtiles " + std::to_string(o[7]) + " rows " +
+                         std::to_string(o[8]) + " us";
+      char buf[64];
+      for (int k = 0; k < 7; ++k) {
+        std::snprintf(buf, sizeof(buf), " %s=%.2f", names[k], o[k] / 100.0);
+        line += buf;
+      }
+      std::snprintf(buf, sizeof(buf), " total=%.2f", o[9] / 100.0);
+      std::fprintf(stderr, "%s%s\n", line.c_str(), buf);
+    }
+  }
+  // the next tree enqueues the most rounds of the last kRoundHist trees (+1)
+  round_hist_.push_back(h_round_->rounds);
+  if (round_hist_.size() > kRoundHist) round_hist_.erase(round_hist_.begin());
+  last_stats_.rounds = h_round_->rounds;
+  last_stats_.expansions = (h_round_->next_frow - 1) / 2;
+  // (every enqueued round's collectives run; a finished tree's exit at once)
+  last_stats_.collective_bytes = distributed_ ? root_collective_bytes_ + RoundCollectiveBytes() * launched : 0.0;
+  return h_round_->nsplit;
+}
+
+// a leaf's raw histogram: its slot, or -- round growth, for a node whose pending expansion
+// reused its slot for the subtracted child -- per feature the sum over its children where the
+// node evaluated the feature (its children materialised it), recursively; elsewhere the
+// node's slot, which its subtracted descendants inherit without touching that feature's bins
+// (self checks only)
+void GPUTreeLearner::ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const {
+  (void)leaf;
+  const size_t nh = 2 * static_cast<size_t>(total_bins_);
+  raw->assign(nh, 0);
+  auto read_slot = [&](int slot, std::vector<long long>* out) {
+    out->resize(nh);
+    HIPCHECK(hipMemcpy(out->data(), d_hist_ + static_cast<size_t>(slot) * nh, sizeof(long long) * nh,
+                       hipMemcpyDeviceToHost));
+  };
+  if (d_rnode_ == nullptr || last_stats_.rounds == 0 || lf.frow < 0) {  // (one split per step: Leaf::frow is no node)
+    read_slot(lf.slot, raw);
+    return;
+  }
+  std::function<void(int, std::vector<long long>*)> node_hist = [&](int n, std::vector<long long>* out) {
+    dev::RNode r{};
+    HIPCHECK(hipMemcpy(&r, d_rnode_ + n, sizeof(r), hipMemcpyDeviceToHost));
+    read_slot(r.st.slot, out);
+    if (!r.expanded) return;
+    dev::RNode c{};
+    HIPCHECK(hipMemcpy(&c, d_rnode_ + r.child, sizeof(c), hipMemcpyDeviceToHost));
+    const int md = config_->min_data_in_leaf;
+    const int lc = r.total_left, rc = r.count - r.total_left;
+    // (children of an expansion that cannot be split are not histogrammed)
+    if ((config_->max_depth > 0 && c.st.depth >= config_->max_depth) || (lc < 2 * md && rc < 2 * md)) return;
+    std::vector<int8_t> flags(num_features_);
+    HIPCHECK(hipMemcpy(flags.data(), d_splittable_ + static_cast<size_t>(n) * num_features_, num_features_,
+                       hipMemcpyDeviceToHost));
+    std::vector<long long> h0, h1;
+    node_hist(r.child, &h0);
+    node_hist(r.child + 1, &h1);
+    for (int f = 0; f < num_features_; ++f) {
+      if (!flags[f]) continue;
+      const size_t off = 2 * static_cast<size_t>(data_->FeatureHistOffset(f));
+      const size_t len = 2 * static_cast<size_t>(data_->FeatureHistSize(f));
+      for (size_t i = off; i < off + len; ++i) (*out)[i] = h0[i] + h1[i];
+    }
+  };
+  node_hist(lf.frow, raw);
+}
+
+}  // namespace lgbm_amd

@@ -1,29 +1,5 @@
 // MI355X tree learner host orchestration (see gpu_tree_learner.h).
-#include "gpu_tree_learner.h"
-
-#include "parallel_tree_learner.h"
-
-#include <omp.h>
-
-#include <algorithm>
-#include <functional>
-#include <chrono>
-#include <cmath>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <thread>
-
-#include "lgbm_amd/common.h"
-#include "lgbm_amd/dcg.h"
-#include "lgbm_amd/log.h"
-#include "lgbm_amd/network.h"
-
-#define HIPCHECK(x)                                                                               \
-  do {                                                                                            \
-    hipError_t e_ = (x);                                                                          \
-    if (e_ != hipSuccess) Log::Fatal("HIP error %s at %s:%d: %s", #x, __FILE__, __LINE__, hipGetErrorString(e_)); \
-  } while (0)
+#include "gpu_learner_internal.h"
 
 namespace lgbm_amd {
 
@@ -56,14 +32,6 @@ GPUTreeLearner::GPUTreeLearner(const Config* config, Mode mode) : SerialTreeLear
 GPUTreeLearner::~GPUTreeLearner() {
   FreeAll();
   for (void* p : valid_allocs_) (void)hipFree(p);
-}
-
-template <typename T>
-T* GPUTreeLearner::Alloc(size_t n) {
-  void* p = nullptr;
-  HIPCHECK(hipMalloc(&p, std::max<size_t>(1, n) * sizeof(T)));
-  allocs_.push_back(p);
-  return static_cast<T*>(p);
 }
 
 void GPUTreeLearner::FreeBuffers() {
@@ -666,228 +634,6 @@ void GPUTreeLearner::UploadData() {
   AllocSplittable();
 }
 
-// histogram slots and splittable rows (nodes) of a tree: one slot per leaf, or -- round
-// growth -- one per expansion (the root's, then the histogrammed child's of each), two nodes
-// per expansion; 3 * num_leaves expansions leave the speculation 2 * num_leaves of waste,
-// 2 * num_leaves when the slots would pass 16 GiB
-void GPUTreeLearner::SizeRoundPools(int n_leaves) {
-  hist_slots_ = n_leaves;
-  split_rows_ = n_leaves;
-  if (round_k_ > 1) {
-    const double slot_bytes = 16.0 * static_cast<double>(total_bins_);
-    const int per = slot_bytes * 3.0 * n_leaves > 16.0 * (1ull << 30) ? 2 : 3;
-    hist_slots_ = per * n_leaves;
-    split_rows_ = 2 * per * n_leaves;
-  }
-  args_.round_nodes = split_rows_;
-  args_.round_emax = std::min(hist_slots_ - 1, (split_rows_ - 1) / 2);
-  args_.round_vmax = round_vmax_;
-}
-
-void GPUTreeLearner::AllocRoundState() {
-  dev::KArgs& a = args_;
-  a.rnode = nullptr;
-  a.cbest = nullptr;
-  a.cbest_cat = nullptr;
-  a.child_cnt = nullptr;
-  if (round_k_ <= 1) return;
-  d_round_ = Alloc<dev::Round>(1);
-  d_rnode_ = Alloc<dev::RNode>(split_rows_);
-  d_cbest_ = Alloc<dev::FeatureBest>(split_rows_);
-  d_cbest_cat_ = Alloc<uint32_t>(static_cast<size_t>(split_rows_) * kMaxCatWords);
-  const size_t cnt = 2 * static_cast<size_t>(dev::kMaxRoundExp) * (dev::kFindSub + 1) * dev::kFindSubStride;
-  d_child_cnt_ = Alloc<uint32_t>(cnt);
-  HIPCHECK(hipMemset(d_child_cnt_, 0, sizeof(uint32_t) * cnt));
-  HIPCHECK(hipMemset(d_round_, 0, sizeof(dev::Round)));
-  if (h_round_ == nullptr) {
-    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_round_), sizeof(dev::Round), hipHostMallocDefault));
-  }
-  a.rnode = d_rnode_;
-  a.cbest = d_cbest_;
-  a.cbest_cat = d_cbest_cat_;
-  a.child_cnt = d_child_cnt_;
-  round_hist_.clear();
-}
-
-// Feature ownership of the distributed learners (reference data_parallel_tree_learner.cpp
-// BeforeTrain :61-123 assigns the tree's used features to the least-loaded rank by bins).
-// Here a rank owns whole storage groups; its groups' bins, packed in group order, are its
-// block of the owner-major reduce-scatter buffer (rs_pos), and its features are gathered
-// rank-major after each scan (fb_index).  The static layout cuts the groups into `world`
-// contiguous blocks balanced by bins,
-//   owner(group g) = min(world - 1, mid(g) * world / total_bins), monotone in g;
-// data-parallel training with feature_fraction < 1 re-assigns the tree's used groups every
-// tree, greedily to the rank with the fewest bins so far (OwnershipForTree), inside the
-// capacities the static layout sized the buffers and graphs for.
-GPUTreeLearner::OwnerLayout GPUTreeLearner::BuildOwnerLayout(const std::vector<int>& gown) const {
-  OwnerLayout L;
-  std::vector<int> load(world_, 0), gpos(num_groups_, -1);
-  for (int g = 0; g < num_groups_; ++g) {
-    if (gown[g] < 0) continue;
-    gpos[g] = load[gown[g]];
-    load[gown[g]] += group_off_[g + 1] - group_off_[g];
-  }
-  L.max_block = *std::max_element(load.begin(), load.end());
-  std::vector<int> count(world_, 0), local(num_features_, -1);
-  for (int f = 0; f < num_features_; ++f) {
-    const int o = gown[data_->Feature2Group(f)];
-    if (o < 0) continue;
-    local[f] = count[o]++;
-    if (o == rank_) L.feats.push_back(f);
-  }
-  L.max_feats = *std::max_element(count.begin(), count.end());
-  L.fb_index.assign(std::max(1, num_features_), 0);
-  L.owned_off.assign(std::max(1, num_features_), 0);
-  for (int f = 0; f < num_features_; ++f) {
-    const int g = data_->Feature2Group(f), o = gown[g];
-    if (o < 0) continue;  // (never read: the feature is not scanned this tree)
-    L.fb_index[f] = o * 2 * max_owned_ + local[f];
-    L.owned_off[f] = gpos[g] + (feat_hist_off_[f] - group_off_[g]);
-  }
-  L.rs_pos.assign(std::max(1, total_bins_), -1);
-  for (int g = 0; g < num_groups_; ++g) {
-    if (gown[g] < 0) continue;
-    for (int b = group_off_[g]; b < group_off_[g + 1]; ++b) L.rs_pos[b] = gown[g] * rs_block_ + gpos[g] + (b - group_off_[g]);
-  }
-  for (int f : L.feats) {
-    if (data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) L.cats.push_back(f);
-  }
-  return L;
-}
-
-void GPUTreeLearner::UploadOwnerLayout(const OwnerLayout& L) {
-  std::vector<int32_t> fl(std::max(1, max_owned_), -1), cl(std::max(1, cat_cap_), -1);
-  std::copy(L.feats.begin(), L.feats.end(), fl.begin());
-  std::copy(L.cats.begin(), L.cats.end(), cl.begin());
-  HIPCHECK(hipMemcpyAsync(d_feat_list_, fl.data(), sizeof(int32_t) * fl.size(), hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_owned_cats_, cl.data(), sizeof(int32_t) * cl.size(), hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_fb_index_, L.fb_index.data(), sizeof(int32_t) * L.fb_index.size(), hipMemcpyHostToDevice,
-                          stream_));
-  HIPCHECK(hipMemcpyAsync(d_owned_off_, L.owned_off.data(), sizeof(int32_t) * L.owned_off.size(),
-                          hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_rs_pos_, L.rs_pos.data(), sizeof(int32_t) * L.rs_pos.size(), hipMemcpyHostToDevice,
-                          stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));  // (the host vectors are temporaries)
-}
-
-void GPUTreeLearner::SetupOwnership() {
-  owned_feats_.clear();
-  max_owned_ = 0;
-  rs_block_ = 0;
-  owned_bin_lo_ = 0;
-  dyn_owner_ = false;
-  if (!distributed_ || mode_ == Mode::kVoting) return;
-  group_off_.assign(num_groups_ + 1, total_bins_);
-  for (int g = 0; g < num_groups_; ++g) group_off_[g] = static_cast<int32_t>(data_->group_bin_boundary(g));
-  feat_hist_off_.assign(std::max(1, num_features_), 0);
-  for (int f = 0; f < num_features_; ++f) feat_hist_off_[f] = static_cast<int32_t>(data_->FeatureHistOffset(f));
-  std::vector<int> gown(num_groups_);
-  std::vector<int> lo(world_, -1), hi(world_, -1);
-  int max_group_bins = 1, max_group_feats = 1;
-  std::vector<int> gfeats(num_groups_, 0);
-  for (int f = 0; f < num_features_; ++f) max_group_feats = std::max(max_group_feats, ++gfeats[data_->Feature2Group(f)]);
-  for (int g = 0; g < num_groups_; ++g) {
-    const long long mid2 = static_cast<long long>(group_off_[g]) + group_off_[g + 1];
-    gown[g] = static_cast<int>(std::min<long long>(world_ - 1, mid2 * world_ / (2LL * std::max(1, total_bins_))));
-    const int r = gown[g];
-    if (lo[r] < 0) lo[r] = group_off_[g];
-    hi[r] = group_off_[g + 1];
-    max_group_bins = std::max(max_group_bins, group_off_[g + 1] - group_off_[g]);
-  }
-  int prev_end = 0;
-  for (int r = 0; r < world_; ++r) {
-    if (lo[r] < 0) lo[r] = hi[r] = prev_end;  // a rank without groups: empty block
-    prev_end = hi[r];
-    rs_block_ = std::max(rs_block_, hi[r] - lo[r]);
-  }
-  owned_bin_lo_ = lo[rank_];
-  std::vector<int> count(world_, 0);
-  for (int f = 0; f < num_features_; ++f) count[gown[data_->Feature2Group(f)]]++;
-  for (int r = 0; r < world_; ++r) max_owned_ = std::max(max_owned_, count[r]);
-  // per-tree ownership: blocks of the greedy assignment fit avg + one group (bins); the feature
-  // capacity leaves room for an uneven count -- a tree whose assignment exceeds either keeps
-  // the static layout
-  dyn_owner_ = mode_ == Mode::kData && config_->feature_fraction < 1.0 &&
-               !(std::getenv("LGBM_AMD_STATIC_OWNERS") != nullptr && std::getenv("LGBM_AMD_STATIC_OWNERS")[0] == '1');
-  int ncat = 0;
-  for (int f = 0; f < num_features_; ++f) ncat += data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical ? 1 : 0;
-  if (dyn_owner_) {
-    rs_block_ = std::max(rs_block_, (total_bins_ + world_ - 1) / world_ + max_group_bins);
-    max_owned_ = std::min(num_features_, std::max(max_owned_, (3 * num_features_ + 2 * world_ - 1) / (2 * world_) +
-                                                                    max_group_feats));
-  }
-  rs_block_ = std::max(rs_block_, 1);
-  max_owned_ = std::max(max_owned_, 1);
-  static_layout_ = BuildOwnerLayout(gown);
-  owned_feats_ = static_layout_.feats;
-  cat_cap_ = dyn_owner_ ? std::max(1, ncat) : std::max<int>(1, static_layout_.cats.size());
-  d_feat_list_ = Alloc<int32_t>(std::max(1, max_owned_));
-  d_fb_index_ = Alloc<int32_t>(std::max(1, num_features_));
-  d_rs_pos_ = Alloc<int32_t>(std::max(1, total_bins_));
-  d_owned_cats_ = Alloc<int32_t>(cat_cap_);
-  d_owned_off_ = Alloc<int32_t>(std::max(1, num_features_));
-  UploadOwnerLayout(static_layout_);
-  owner_layout_static_ = true;
-  d_owned_hist_ = Alloc<long long>(2 * static_cast<size_t>(rs_block_));
-  const size_t fb_bytes = 2 * static_cast<size_t>(max_owned_) *
-                          (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0));
-  const double rs_bytes = mode_ == Mode::kData ? sizeof(long long) * 2.0 * rs_block_ * world_ : 0.0;
-  split_collective_bytes_ = rs_bytes + static_cast<double>(fb_bytes) * world_;
-  root_collective_bytes_ = split_collective_bytes_ + 3 * sizeof(double) + 3 * sizeof(uint32_t);
-  if (mode_ == Mode::kData) {
-    Log::Info("data-parallel device learner, rank %d of %d: %d features, histogram bins [%d, %d)%s; per split "
-              "reduce-scatter %zu bytes in / %zu out, split-record allgather %zu bytes per rank",
-              rank_, world_, static_cast<int>(owned_feats_.size()), lo[rank_], hi[rank_],
-              dyn_owner_ ? " (re-assigned per tree over the used features)" : "",
-              sizeof(long long) * 2 * static_cast<size_t>(rs_block_) * world_,
-              sizeof(long long) * 2 * static_cast<size_t>(rs_block_), fb_bytes);
-  } else {
-    Log::Info("feature-parallel device learner, rank %d of %d: %d features, histogram bins [%d, %d); per split "
-              "split-record allgather %zu bytes per rank", rank_, world_, static_cast<int>(owned_feats_.size()),
-              lo[rank_], hi[rank_], fb_bytes);
-  }
-}
-
-// the tree's used groups to the rank with the fewest bins so far, in group order (every rank
-// computes the same assignment from the same bytree sample)
-void GPUTreeLearner::OwnershipForTree() {
-  if (!dyn_owner_) return;
-  std::vector<int> gown(num_groups_, -1), load(world_, 0);
-  std::vector<char> used(num_groups_, 0);
-  for (int f = 0; f < num_features_; ++f) {
-    if (h_mask_[f]) used[data_->Feature2Group(f)] = 1;
-  }
-  for (int g = 0; g < num_groups_; ++g) {
-    if (!used[g]) continue;
-    const int r = static_cast<int>(std::min_element(load.begin(), load.end()) - load.begin());
-    gown[g] = r;
-    load[r] += group_off_[g + 1] - group_off_[g];
-  }
-  OwnerLayout L = BuildOwnerLayout(gown);
-  int ncats_max = 0;
-  {
-    std::vector<int> cc(world_, 0);
-    for (int f = 0; f < num_features_; ++f) {
-      const int o = gown[data_->Feature2Group(f)];
-      if (o >= 0 && data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) ncats_max = std::max(ncats_max, ++cc[o]);
-    }
-  }
-  const bool fits = L.max_block <= rs_block_ && L.max_feats <= max_owned_ && ncats_max <= cat_cap_;
-  if (!fits) {
-    if (!owner_layout_static_) UploadOwnerLayout(static_layout_);
-    owner_layout_static_ = true;
-    owned_feats_ = static_layout_.feats;
-    Log::Debug("per-tree ownership exceeds the layout's capacity (block %d / %d bins, %d / %d features): static owners",
-               L.max_block, rs_block_, L.max_feats, max_owned_);
-    return;
-  }
-  UploadOwnerLayout(L);
-  owner_layout_static_ = false;
-  owned_feats_ = L.feats;
-  Log::Debug("rank %d owns %zu of the tree's features (%d bins, largest block %d)", rank_, L.feats.size(),
-             load[rank_], L.max_block);
-}
-
 // interaction constraints as per-feature constraint bitmasks (device-resident growth
 // supports up to 64 constraints, see DecideMode); rebuilt when the config changes
 void GPUTreeLearner::UploadInteractionMasks() {
@@ -1133,83 +879,6 @@ void GPUTreeLearner::WatchdogSync() {
   }
 }
 
-void GPUTreeLearner::AllreduceRoot() {
-  if (!(data_parallel_ || voting_) || Network::num_machines() <= 1) return;
-  // voting: the local scan of the root needs this rank's sums too
-  if (voting_) HIPCHECK(hipMemcpyAsync(d_root_local_, d_root_, sizeof(double) * 3, hipMemcpyDeviceToDevice, stream_));
-  DeviceComm* dc = Network::device_comm();
-  if (dc != nullptr) {
-    dc->AllreduceSumF64(d_root_, 3, stream_);
-    return;
-  }
-  HIPCHECK(hipMemcpyAsync(h_root_, d_root_, sizeof(double) * 3, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  auto v = Network::GlobalSum(std::vector<double>(h_root_, h_root_ + 3));
-  std::copy(v.begin(), v.end(), h_root_);
-  HIPCHECK(hipMemcpyAsync(d_root_, h_root_, sizeof(double) * 3, hipMemcpyHostToDevice, stream_));
-}
-
-// data-parallel: this rank's owner block of the step's histogram, summed over every rank
-// (reference data_parallel_tree_learner.cpp:154-173 ReduceScatter into feature owners)
-void GPUTreeLearner::ReduceScatterStep(int parity) {
-  if (!data_parallel_) return;
-  DeviceComm* dc = Network::device_comm();
-  long long* send = d_scratch_ + static_cast<size_t>(parity & 1) * args_.scratch_stride;
-  const size_t block = 2 * static_cast<size_t>(rs_block_);
-  if (dc != nullptr) {
-    dc->ReduceScatterSumI64(send, d_owned_hist_, block, stream_);  // exact: fixed-point integers
-    return;
-  }
-  // host collectives: the whole padded buffer, summed on the host
-  std::vector<long long> h(block * world_);
-  HIPCHECK(hipMemcpyAsync(h.data(), send, sizeof(long long) * h.size(), hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  auto v = Network::GlobalSum(h);
-  HIPCHECK(hipMemcpyAsync(d_owned_hist_, v.data() + block * rank_, sizeof(long long) * block, hipMemcpyHostToDevice,
-                          stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-}
-
-// distributed: every rank's per-feature results (and category sets), rank-major, so each
-// rank picks the same split (reference SyncUpGlobalBestSplit, parallel_tree_learner.h:190)
-void GPUTreeLearner::GatherFeatureBests() {
-  if (!distributed_ || voting_) return;
-  DeviceComm* dc = Network::device_comm();
-  const size_t fb_bytes = 2 * static_cast<size_t>(max_owned_) * sizeof(dev::FeatureBest);
-  const size_t cat_bytes = 2 * static_cast<size_t>(max_owned_) * kMaxCatWords * sizeof(uint32_t);
-  char* fb = reinterpret_cast<char*>(d_feat_best_);
-  char* fc = reinterpret_cast<char*>(d_feat_cat_);
-  if (dc != nullptr) {
-    dc->Allgather(fb + fb_bytes * rank_, fb, fb_bytes, stream_);
-    if (num_cat_total_ > 0) dc->Allgather(fc + cat_bytes * rank_, fc, cat_bytes, stream_);
-    return;
-  }
-  auto host_gather = [&](char* d, size_t bytes) {
-    std::vector<char> all(bytes * world_);
-    HIPCHECK(hipMemcpyAsync(all.data() + bytes * rank_, d + bytes * rank_, bytes, hipMemcpyDeviceToHost, stream_));
-    HIPCHECK(hipStreamSynchronize(stream_));
-    std::vector<char> mine(all.begin() + bytes * rank_, all.begin() + bytes * (rank_ + 1));
-    Network::Allgather(mine.data(), static_cast<comm_size_t>(bytes), all.data());
-    HIPCHECK(hipMemcpyAsync(d, all.data(), all.size(), hipMemcpyHostToDevice, stream_));
-    HIPCHECK(hipStreamSynchronize(stream_));
-  };
-  host_gather(fb, fb_bytes);
-  if (num_cat_total_ > 0) host_gather(fc, cat_bytes);
-}
-
-void GPUTreeLearner::AllreduceAbsMax() {
-  if (!(data_parallel_ || voting_) || Network::num_machines() <= 1) return;
-  DeviceComm* dc = Network::device_comm();
-  if (dc != nullptr) {
-    dc->AllreduceMaxU32(d_absmax_, 3, stream_);  // non-negative float bits order like the floats
-    return;
-  }
-  HIPCHECK(hipMemcpyAsync(h_absmax_, d_absmax_, sizeof(uint32_t) * 3, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  for (int k = 0; k < 3; ++k) h_absmax_[k] = Network::GlobalSyncUpByMax(h_absmax_[k]);
-  HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 3, hipMemcpyHostToDevice, stream_));
-}
-
 // diagnostics (LGBM_AMD_KERNEL_PROBE=1): the tree is finished (Step::done), so every step
 // kernel exits after reading the Step record; time N back-to-back launches of each
 void GPUTreeLearner::KernelFloorProbe(const dev::KArgs& a) {
@@ -1311,8 +980,16 @@ void GPUTreeLearner::ReportKernelTrace(int num_splits) {
 }
 
 void GPUTreeLearner::DestroyGraph() {
+  DestroyStepGraph();
+  DestroyRoundGraphs();
+}
+
+void GPUTreeLearner::DestroyStepGraph() {
   if (graph_exec_ != nullptr) (void)hipGraphExecDestroy(graph_exec_);
   graph_exec_ = nullptr;
+}
+
+void GPUTreeLearner::DestroyRoundGraphs() {
   for (hipGraphExec_t& e : round_root_execs_) {
     if (e != nullptr) (void)hipGraphExecDestroy(e);
   }
@@ -1416,317 +1093,6 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   }
 }
 
-dev::KArgs GPUTreeLearner::VoteGlobalArgs(const dev::KArgs& a, int pick_in_find) const {
-  dev::KArgs glob = a;
-  glob.p.vote_phase = 2;
-  glob.p.sp = params_;
-  glob.pick_in_find = pick_in_find;
-  glob.num_scan = vote_k_;
-  return glob;
-}
-
-// one round: single process, every kernel back to back; distributed, the histograms
-// reduce-scattered to their owners (data-parallel) and the per-feature results of every rank
-// gathered before the children's bests and the plan -- two collectives per round where one
-// split per step took two per split (reference data_parallel_tree_learner.cpp:154-247)
-void GPUTreeLearner::EnqueueRound(const dev::KArgs& a) {
-  if (!distributed_) {
-    dev::RoundStep(a, stream_);
-    return;
-  }
-  DeviceComm* dc = Network::device_comm();
-  // a finished tree's remaining rounds skip their collectives on every rank (Round::done is
-  // replicated state); communicators that cannot skip run them.  The guard is cleared on every
-  // exit of this scope: a throw between here and the last collective (a failed launch caught
-  // by the graph capture) must not leave later collectives guarded by a stale flag
-  struct SkipGuardScope {
-    DeviceComm* dc;
-    ~SkipGuardScope() { dc->SetSkipGuard(nullptr); }
-  } guard_scope{dc};
-  dc->SetSkipGuard(&d_round_->done);
-  if (voting_) {
-    // the local scan of every child of the round, one vote for all of them, the global scan of
-    // the elected features (reference voting_parallel_tree_learner.cpp:300-343, per round)
-    const dev::KArgs glob = VoteGlobalArgs(a, 0);
-    dev::RoundSplitReduce(a, stream_);
-    dev::RoundFind(a, stream_);
-    RoundVoteExchange(glob);
-    dev::RoundFindElected(glob, stream_);
-    dc->SetSkipGuard(nullptr);
-    dev::RoundChildBestAndPlan(glob, stream_);
-    return;
-  }
-  const size_t owned = static_cast<size_t>(round_k_) * rs_block_ * 2;
-  // (the owner-major send buffer was cleared by the previous round's split scans, or by the root)
-  dev::RoundSplitReduce(a, stream_);
-  if (data_parallel_) dc->ReduceScatterSumI64(d_round_send_, d_round_owned_, owned, stream_);
-  dev::RoundFind(a, stream_);
-  const size_t per = 2 * static_cast<size_t>(round_k_) * std::max(1, max_owned_);
-  char* fb = reinterpret_cast<char*>(d_feat_best_);
-  dc->Allgather(fb + per * sizeof(dev::FeatureBest) * rank_, fb, per * sizeof(dev::FeatureBest), stream_);
-  if (num_cat_total_ > 0) {
-    char* fc = reinterpret_cast<char*>(d_feat_cat_);
-    const size_t cb = per * kMaxCatWords * sizeof(uint32_t);
-    dc->Allgather(fc + cb * rank_, fc, cb, stream_);
-  }
-  dc->SetSkipGuard(nullptr);  // (the plan's kernels are not collectives)
-  dev::RoundChildBestAndPlan(a, stream_);
-}
-
-void GPUTreeLearner::RoundVoteExchange(const dev::KArgs& glob) {
-  DeviceComm* dc = Network::device_comm();  // (round growth runs with a device communicator only)
-  dev::RoundVoteLocal(glob, stream_);
-  const size_t prop_bytes = sizeof(dev::VoteEntry) * 2 * static_cast<size_t>(round_k_) * vote_k_;
-  char* vb = reinterpret_cast<char*>(d_vote_buf_);
-  dc->Allgather(vb + prop_bytes * rank_, vb, prop_bytes, stream_);
-  dev::RoundVoteElect(glob, stream_);
-  dc->AllreduceSumI64(d_vote_hist_, 2 * static_cast<size_t>(round_k_) * vote_k_ * 2 * glob.p.max_feature_bins, stream_);
-}
-
-double GPUTreeLearner::RoundCollectiveBytes() const {
-  if (!distributed_) return 0.0;
-  if (voting_) {
-    const double sides = 2.0 * round_k_ * vote_k_;
-    return sides * sizeof(dev::VoteEntry) * world_ + sides * 2.0 * args_.p.max_feature_bins * sizeof(long long);
-  }
-  const double per = 2.0 * round_k_ * std::max(1, max_owned_) *
-                     (sizeof(dev::FeatureBest) + (num_cat_total_ > 0 ? kMaxCatWords * sizeof(uint32_t) : 0)) * world_;
-  return per + (data_parallel_ ? sizeof(long long) * 2.0 * round_k_ * rs_block_ * world_ : 0.0);
-}
-
-// ---------------------------------------------------------------- round growth
-bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
-  if (round_k_ <= 1 || d_round_ == nullptr) return false;
-  if (distributed_ && Network::device_comm() == nullptr) return false;  // (host collectives: one split per step)
-  // the split order depends on more than each leaf's own rows: per-node feature samples and
-  // extra_trees draws are consumed in the sequential order, CEGB's coupled penalties change
-  // other leaves' gains, forced splits follow their own schedule
-  if (a.node_mask != nullptr || a.xt_base != nullptr || a.p.cegb || a.forced_n > 0 || a.p.mono_inter) return false;
-  return true;
-}
-
-// rounds of kRoundSeg expansions per graph launch: one root graph (the root + as many
-// segments as the recent trees needed, one cached graph per segment count) is launched; the
-// host then checks the Round record and adds segment graphs until the tree is done (a finished
-// tree's kernels exit at once: an over-provisioned round costs ~12 us, a missing one a host
-// round trip of ~60 us and a graph launch of ~8 us per segment)
-namespace {
-constexpr int kRoundSeg = 4;
-constexpr int kRoundFirstPred = 16;  // rounds enqueued for the first tree
-}
-
-int GPUTreeLearner::RunRounds(dev::KArgs a) {
-  a.rd = d_round_;
-  a.pick_in_find = 0;  // the root's split scan only publishes; RoundRootPlan picks
-  // (LGBM_AMD_KTRACE: k_round_split's phase times of one workgroup per round)
-  if (a.ktrace != nullptr) HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
-  const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
-  // distributed: the collectives are captured with the kernels when the communicator allows it
-  // (RCCL); the in-process communicator rendezvouses on the host, so its rounds run eagerly
-  DeviceComm* dc = distributed_ ? Network::device_comm() : nullptr;
-  const bool use_graph = !(ng != nullptr && ng[0] == '1') && (dc == nullptr || dc->CaptureSafe()) && !graph_capture_failed_;
-  const int root_mode = (root_from_parts_ && !use_bag_) ? 1 : 0;
-  auto capture = [&](hipGraphExec_t* exec, bool root, int rounds) {
-    hipGraph_t g = nullptr;
-    HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-    std::string why;
-    try {
-      if (root) EnqueueRoot(a);
-      for (int r = 0; r < rounds; ++r) EnqueueRound(a);
-    } catch (const std::exception& e) {
-      why = e.what();
-    }
-    hipError_t ec = hipStreamEndCapture(stream_, &g);
-    if (why.empty() && ec == hipSuccess) ec = hipGraphInstantiate(exec, g, nullptr, nullptr, 0);
-    if (g != nullptr) (void)hipGraphDestroy(g);
-    if (!why.empty() || ec != hipSuccess) {
-      if (why.empty()) why = hipGetErrorString(ec);
-      (void)hipGetLastError();
-      *exec = nullptr;
-      if (!distributed_) Log::Fatal("device learner: capturing the round graphs failed: %s", why.c_str());
-      Log::Warning("device learner: capturing the round collectives failed (%s); launching rounds eagerly", why.c_str());
-      graph_capture_failed_ = true;
-      return false;
-    }
-    return true;
-  };
-  const int L = config_->num_leaves;
-  // segments of the root graph: the most rounds of the last trees (+1), rounded up
-  int want = kRoundFirstPred;
-  if (!round_hist_.empty()) want = *std::max_element(round_hist_.begin(), round_hist_.end()) + 1;
-  want = std::max(1, std::min(want, L - 1));
-  const int nseg = (want + kRoundSeg - 1) / kRoundSeg;
-  bool graph = use_graph;
-  if (graph && (round_seg_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
-                round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
-    if (dc != nullptr) dc->HostBarrier();
-    DestroyGraph();
-    graph = capture(&round_seg_exec_, false, kRoundSeg);
-    if (!graph) DestroyGraph();
-    round_graph_rows_ = a.num_rows;
-    round_graph_identity_ = a.root_identity;
-    round_graph_root_mode_ = root_mode;
-  }
-  if (graph) {
-    if (static_cast<int>(round_root_execs_.size()) <= nseg) round_root_execs_.resize(nseg + 1, nullptr);
-    if (round_root_execs_[nseg] == nullptr) {
-      if (dc != nullptr) dc->HostBarrier();
-      graph = capture(&round_root_execs_[nseg], true, nseg * kRoundSeg);
-      if (!graph) DestroyGraph();
-    }
-  }
-  last_stats_.graph = graph;
-  auto launch_seg = [&]() {
-    if (graph) {
-      HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
-    } else {
-      for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
-    }
-  };
-  if (graph) {
-    HIPCHECK(hipGraphLaunch(round_root_execs_[nseg], stream_));
-  } else {
-    EnqueueRoot(a);
-    for (int r = 0; r < nseg * kRoundSeg; ++r) EnqueueRound(a);
-  }
-  int launched = nseg * kRoundSeg;
-  const size_t rec_bytes = sizeof(dev::SplitRecord) * std::max(1, L - 1);
-  for (;;) {
-    HIPCHECK(hipMemcpyAsync(h_round_, d_round_, sizeof(dev::Round), hipMemcpyDeviceToHost, stream_));
-    HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, rec_bytes, hipMemcpyDeviceToHost, stream_));
-    WatchdogSync();
-    if (h_round_->done) break;
-    if (launched > 2 * L + kRoundSeg) {
-      Log::Fatal("device learner: round growth did not finish the tree after %d rounds (%d splits)", launched,
-                 h_round_->nsplit);
-    }
-    launch_seg();
-    launched += kRoundSeg;
-  }
-  if (a.ktrace != nullptr) {
-    std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
-    HIPCHECK(hipMemcpy(t.data(), a.ktrace, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
-    static const char* names[] = {"stage", "side", "resv", "write", "gather", "tail", "store"};
-    // plans: slot 16 entry time, 17..21 phase times (loads, replay + prediction, records of the
-    // expansions / accepted splits / changed leaves, barrier, sizing), 22 accepted, 23 planned,
-    // 25 the split scan's start
-    for (int r = 0; r <= h_round_->rounds && r < L; ++r) {
-      const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
-      if (o[16] == 0) continue;
-      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay+predict=%.2f records=%.2f sync=%.2f sizing=%.2f us; accepted %lld planned %lld\n",
-                   r, o[25] != 0 ? (o[16] - o[25]) / 100.0 : 0.0, o[17] / 100.0, o[18] / 100.0, o[19] / 100.0,
-                   o[20] / 100.0, o[21] / 100.0, o[22], o[23]);
-      if (o[26] != 0) {  // the planning workgroup's scan path, from the first scan workgroup's start
-        auto us = [&](int k) { return (o[k] - o[25]) / 100.0; };
-        std::fprintf(stderr, "  planner wg: entry %.2f loaded %.2f staged %.2f scanned %.2f arrived %.2f folded %.2f plan %.2f us\n",
-                     us(26), us(27), us(28), us(29), us(30), us(31), us(16));
-        if (o[12] != 0) {  // (LGBM_FIND_PHASES builds: the scan's phases)
-          std::fprintf(stderr, "  planner scan: begin %.2f prefix %.2f candidates %.2f argmax %.2f us\n", us(12), us(13),
-                       us(14), us(15));
-        }
-      }
-    }
-    for (int r = 1; r <= h_round_->rounds && r < L; ++r) {
-      const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
-      std::string line = "round " + std::to_string(r) + " exp " + std::to_string(o[10]) + " blocks " +
-                         std::to_string(o[11]) + " wg0: subtiles " + std::to_string(o[7]) + " rows " +
-                         std::to_string(o[8]) + " us";
-      char buf[64];
-      for (int k = 0; k < 7; ++k) {
-        std::snprintf(buf, sizeof(buf), " %s=%.2f", names[k], o[k] / 100.0);
-        line += buf;
-      }
-      std::snprintf(buf, sizeof(buf), " total=%.2f", o[9] / 100.0);
-      std::fprintf(stderr, "%s%s\n", line.c_str(), buf);
-    }
-  }
-  // the next tree enqueues the most rounds of the last kRoundHist trees (+1)
-  round_hist_.push_back(h_round_->rounds);
-  if (round_hist_.size() > kRoundHist) round_hist_.erase(round_hist_.begin());
-  last_stats_.rounds = h_round_->rounds;
-  last_stats_.expansions = (h_round_->next_frow - 1) / 2;
-  // (every enqueued round's collectives run; a finished tree's exit at once)
-  last_stats_.collective_bytes = distributed_ ? root_collective_bytes_ + RoundCollectiveBytes() * launched : 0.0;
-  return h_round_->nsplit;
-}
-
-// a leaf's raw histogram: its slot, or -- round growth, for a node whose pending expansion
-// reused its slot for the subtracted child -- per feature the sum over its children where the
-// node evaluated the feature (its children materialised it), recursively; elsewhere the
-// node's slot, which its subtracted descendants inherit without touching that feature's bins
-// (self checks only)
-void GPUTreeLearner::ReadHist(const dev::Leaf& lf, int leaf, std::vector<long long>* raw) const {
-  (void)leaf;
-  const size_t nh = 2 * static_cast<size_t>(total_bins_);
-  raw->assign(nh, 0);
-  auto read_slot = [&](int slot, std::vector<long long>* out) {
-    out->resize(nh);
-    HIPCHECK(hipMemcpy(out->data(), d_hist_ + static_cast<size_t>(slot) * nh, sizeof(long long) * nh,
-                       hipMemcpyDeviceToHost));
-  };
-  if (d_rnode_ == nullptr || last_stats_.rounds == 0 || lf.frow < 0) {  // (one split per step: Leaf::frow is no node)
-    read_slot(lf.slot, raw);
-    return;
-  }
-  std::function<void(int, std::vector<long long>*)> node_hist = [&](int n, std::vector<long long>* out) {
-    dev::RNode r{};
-    HIPCHECK(hipMemcpy(&r, d_rnode_ + n, sizeof(r), hipMemcpyDeviceToHost));
-    read_slot(r.st.slot, out);
-    if (!r.expanded) return;
-    dev::RNode c{};
-    HIPCHECK(hipMemcpy(&c, d_rnode_ + r.child, sizeof(c), hipMemcpyDeviceToHost));
-    const int md = config_->min_data_in_leaf;
-    const int lc = r.total_left, rc = r.count - r.total_left;
-    // (children of an expansion that cannot be split are not histogrammed)
-    if ((config_->max_depth > 0 && c.st.depth >= config_->max_depth) || (lc < 2 * md && rc < 2 * md)) return;
-    std::vector<int8_t> flags(num_features_);
-    HIPCHECK(hipMemcpy(flags.data(), d_splittable_ + static_cast<size_t>(n) * num_features_, num_features_,
-                       hipMemcpyDeviceToHost));
-    std::vector<long long> h0, h1;
-    node_hist(r.child, &h0);
-    node_hist(r.child + 1, &h1);
-    for (int f = 0; f < num_features_; ++f) {
-      if (!flags[f]) continue;
-      const size_t off = 2 * static_cast<size_t>(data_->FeatureHistOffset(f));
-      const size_t len = 2 * static_cast<size_t>(data_->FeatureHistSize(f));
-      for (size_t i = off; i < off + len; ++i) (*out)[i] = h0[i] + h1[i];
-    }
-  };
-  node_hist(lf.frow, raw);
-}
-
-// voting: proposals -> allgather -> election + elected local histograms -> all-reduce
-// (reference voting_parallel_tree_learner.cpp:300-343); the global scan follows
-void GPUTreeLearner::VoteExchange(const dev::KArgs& glob, bool root) {
-  dev::VoteLocal(glob, stream_, root);
-  DeviceComm* dc = Network::device_comm();
-  const size_t prop_bytes = sizeof(dev::VoteEntry) * 2 * static_cast<size_t>(vote_k_);
-  char* vb = reinterpret_cast<char*>(d_vote_buf_);
-  if (dc != nullptr) {
-    dc->Allgather(vb + prop_bytes * rank_, vb, prop_bytes, stream_);
-  } else {
-    std::vector<char> all(prop_bytes * world_);
-    HIPCHECK(hipMemcpyAsync(all.data() + prop_bytes * rank_, vb + prop_bytes * rank_, prop_bytes,
-                            hipMemcpyDeviceToHost, stream_));
-    HIPCHECK(hipStreamSynchronize(stream_));
-    std::vector<char> mine(all.begin() + prop_bytes * rank_, all.begin() + prop_bytes * (rank_ + 1));
-    Network::Allgather(mine.data(), static_cast<comm_size_t>(prop_bytes), all.data());
-    HIPCHECK(hipMemcpyAsync(vb, all.data(), all.size(), hipMemcpyHostToDevice, stream_));
-  }
-  dev::VoteElect(glob, stream_, root);
-  const size_t n = static_cast<size_t>(2 * vote_k_) * 2 * glob.p.max_feature_bins;
-  if (dc != nullptr) {
-    dc->AllreduceSumI64(d_vote_hist_, n, stream_);  // exact: fixed-point integers
-  } else {
-    std::vector<long long> h(n);
-    HIPCHECK(hipMemcpyAsync(h.data(), d_vote_hist_, sizeof(long long) * n, hipMemcpyDeviceToHost, stream_));
-    HIPCHECK(hipStreamSynchronize(stream_));
-    h = Network::GlobalSum(h);
-    HIPCHECK(hipMemcpyAsync(d_vote_hist_, h.data(), sizeof(long long) * n, hipMemcpyHostToDevice, stream_));
-    HIPCHECK(hipStreamSynchronize(stream_));
-  }
-}
-
 Tree* GPUTreeLearner::TrainDeviceMode() {
   col_sampler_.ResetByTree();
   const auto& mask = col_sampler_.is_feature_used_bytree();
@@ -1785,7 +1151,9 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   last_stats_.rounds = 0;
   last_stats_.expansions = 0;
   last_stats_.graph = false;
-  const bool rounds = RoundGrowth(a);
+  const bool can_round = RoundGrowth(a);
+  const bool rounds = can_round && AutoGrowthRounds();
+  const auto t_grow = std::chrono::steady_clock::now();
   if (!rounds && last_tree_rounds_) {
     // one split per step after round trees: splittable rows follow the leaf ids again
     std::vector<dev::Leaf> lv(config_->num_leaves);
@@ -1822,7 +1190,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       if (graph_exec_ == nullptr || graph_rows_ != a.num_rows || graph_identity_ != a.root_identity ||
           graph_root_mode_ != root_mode || graph_xt_ != (xt ? 1 : 0) + (bynode_ic ? 2 : 0)) {
         if (dcomm != nullptr) dcomm->HostBarrier();
-        DestroyGraph();
+        DestroyStepGraph();  // (the round graphs stay: the growth mode may switch per tree)
         hipGraph_t g = nullptr;
         HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
         std::string why;
@@ -1865,6 +1233,9 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       cegb_->set_used_in_split(std::vector<char>(h_cegb_used_.begin(), h_cegb_used_.begin() + num_features_));
     }
     num_splits = h_step_->nsplit;
+  }
+  if (can_round) {
+    AutoGrowthRecord(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_grow).count());
   }
   last_stats_.device_mode = true;
   last_stats_.splits = num_splits;
@@ -1933,180 +1304,6 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   }
   Log::Debug("Trained a tree with leaves = %d and max_depth = %d", tree->num_leaves(), tree->max_depth());
   return tree.release();
-}
-
-// ---------------------------------------------------------------- host-assisted mode
-void GPUTreeLearner::BeforeTrain() {
-  col_sampler_.ResetByTree();
-  dev::KArgs a = args_;
-  if (use_bag_) {
-    HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * bag_cnt_, hipMemcpyDeviceToDevice, stream_));
-    a.num_rows = bag_cnt_;
-  } else {
-    dev::Iota(d_idx_, num_data_, stream_);
-    a.num_rows = num_data_;
-  }
-  a.root_identity = 0;
-  root_rows_ = a.num_rows;
-  dev::TreeBegin(a, stream_);
-  dev::RootSum(a, stream_);
-  HIPCHECK(hipMemcpyAsync(h_root_, d_root_, sizeof(double) * 3, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  double sg = h_root_[0], sh = h_root_[1], cnt = h_root_[2];
-  if (data_parallel_ && Network::num_machines() > 1) {
-    auto v = Network::GlobalSum(std::vector<double>{sg, sh, cnt});
-    sg = v[0];
-    sh = v[1];
-    cnt = v[2];
-  }
-  std::fill(leaf_begin_.begin(), leaf_begin_.end(), 0);
-  std::fill(leaf_count_.begin(), leaf_count_.end(), 0);
-  leaf_count_[0] = a.num_rows;
-  global_count_.assign(config_->num_leaves, 0);
-  global_count_[0] = static_cast<data_size_t>(cnt);
-  constraints_.Init(config_->num_leaves);
-  for (auto& s : best_split_per_leaf_) s.Reset();
-  smaller_ = LeafState{0, static_cast<data_size_t>(cnt), sg, sh, 0.0};
-  larger_ = LeafState{};
-  larger_.leaf = -1;
-}
-
-// host-assisted growth keeps every leaf's rows in index buffer 0 at [leaf_begin, +count)
-SerialTreeLearner::LeafState GPUTreeLearner::LocalLeafSums(int leaf) const {
-  LeafState ls;
-  ls.leaf = leaf;
-  ls.num_data = leaf_count_[leaf];
-  if (ls.num_data <= 0) return ls;
-  dev::KArgs a = args_;
-  a.idx = d_idx_ + leaf_begin_[leaf];
-  a.num_rows = ls.num_data;
-  a.num_rows_dev = nullptr;
-  a.root_identity = 0;
-  a.root = d_leaf_sums_;
-  dev::RootSum(a, stream_);
-  double h[3];
-  HIPCHECK(hipMemcpyAsync(h, d_leaf_sums_, sizeof(double) * 3, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  ls.sum_g = h[0];
-  ls.sum_h = h[1];
-  return ls;
-}
-
-data_size_t GPUTreeLearner::GetGlobalDataCountInLeaf(int leaf) const {
-  if (leaf < 0) return 0;
-  return data_parallel_ ? global_count_[leaf] : leaf_count_[leaf];
-}
-
-void GPUTreeLearner::BuildRangeHistogram(int leaf, int slot) {
-  dev::KArgs a = args_;
-  a.range_begin = leaf_begin_[leaf];
-  a.num_rows = leaf_count_[leaf];
-  const size_t n = 2 * static_cast<size_t>(total_bins_);
-  HIPCHECK(hipMemsetAsync(d_scratch_, 0, sizeof(long long) * n, stream_));
-  if (a.num_rows > 0) dev::HistRange(a, stream_);  // partials + reduction into scratch buffer 0
-  std::vector<long long> h(n);
-  HIPCHECK(hipMemcpyAsync(h.data(), d_scratch_, sizeof(long long) * n, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipMemcpyAsync(h_scales_, d_scales_, sizeof(double) * 4, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  if (data_parallel_ && Network::num_machines() > 1) h = Network::GlobalSum(h);
-  std::vector<hist_t>& dst = LeafHist(slot);
-  const double ig = h_scales_[2], ih = h_scales_[3];
-  for (size_t i = 0; i < n; i += 2) {
-    dst[i] = static_cast<double>(h[i]) * ig;
-    dst[i + 1] = static_cast<double>(h[i + 1]) * ih;
-  }
-}
-
-void GPUTreeLearner::ConstructHistograms(const std::vector<int8_t>&, bool use_subtract) {
-  common::ScopedTimer timer("GPUTreeLearner::ConstructHistograms");
-  BuildRangeHistogram(smaller_.leaf, smaller_slot_);
-  if (larger_slot_ >= 0 && !use_subtract) BuildRangeHistogram(larger_.leaf, larger_slot_);
-}
-
-data_size_t GPUTreeLearner::PartitionLeaf(int leaf, int inner, const SplitInfo& s, int new_leaf) {
-  const data_size_t begin = leaf_begin_[leaf];
-  const data_size_t cnt = leaf_count_[leaf];
-  dev::Step& st = *h_step_;
-  std::memset(&st, 0, sizeof(st));
-  st.cs.leaf = leaf;
-  st.cs.new_leaf = new_leaf;
-  st.cs.part_begin = begin;
-  st.cs.part_count = cnt;
-  st.cs.src_buf = 0;  // host mode keeps every leaf in buffer 0 (copied back below)
-  SplitInfo si = s;
-  si.inner_feature = inner;
-  si.ToDevice(&st.cs.split, data_->FeatureBinMapper(inner)->bin_type() == BinType::Categorical);
-  st.cs.feat = h_feats_[inner];
-  HIPCHECK(hipMemcpyAsync(d_step_, h_step_, sizeof(dev::Step), hipMemcpyHostToDevice, stream_));
-  dev::KArgs a = args_;
-  a.host_mode = 1;
-  dev::Partition(a, stream_);
-  if (cnt > 0) {
-    HIPCHECK(hipMemcpyAsync(d_idx_ + begin, d_tmp_ + begin, sizeof(int32_t) * cnt, hipMemcpyDeviceToDevice, stream_));
-  }
-  HIPCHECK(hipMemcpyAsync(h_step_, d_step_, sizeof(dev::Step), hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  const data_size_t left = h_step_->cur_left;
-  host_partition_fresh_ = false;
-  leaf_count_[leaf] = left;
-  leaf_begin_[new_leaf] = begin + left;
-  leaf_count_[new_leaf] = cnt - left;
-  return left;
-}
-
-void GPUTreeLearner::Split(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf) {
-  if (!data_parallel_) {
-    SplitInner(tree, best_leaf, left_leaf, right_leaf, true);
-    return;
-  }
-  SplitInner(tree, best_leaf, left_leaf, right_leaf, false);
-  const SplitInfo& s = best_split_per_leaf_[best_leaf];
-  global_count_[*left_leaf] = s.left_count;
-  global_count_[*right_leaf] = s.right_count;
-}
-
-// ---------------------------------------------------------------- partition mirror
-void GPUTreeLearner::DownloadPartitionToHost() const {
-  if (host_partition_fresh_) return;
-  auto* self = const_cast<GPUTreeLearner*>(this);
-  const int L = config_->num_leaves;
-  if (!device_mode_) {
-    // host-assisted growth keeps the partition in buffer 0 and its ranges on the host
-    HIPCHECK(hipMemcpyAsync(self->indices_.data(), d_idx_, sizeof(int32_t) * root_rows_, hipMemcpyDeviceToHost,
-                            stream_));
-    HIPCHECK(hipStreamSynchronize(stream_));
-    host_partition_fresh_ = true;
-    return;
-  }
-  std::vector<dev::Leaf> leaves(L);
-  HIPCHECK(hipMemcpyAsync(leaves.data(), d_leaves_, sizeof(dev::Leaf) * L, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  // each leaf's rows sit in the index buffer its last split wrote (Leaf::buf)
-  const int num_leaves_now = last_stats_.splits + 1;  // (either growth mode)
-  for (int l = 0; l < L; ++l) {
-    self->leaf_begin_[l] = leaves[l].begin;
-    self->leaf_count_[l] = l < num_leaves_now ? leaves[l].count : 0;
-    if (self->leaf_count_[l] <= 0) continue;
-    const int32_t* srcbuf = leaves[l].buf == 0 ? d_idx_ : d_tmp_ + static_cast<int64_t>(leaves[l].buf - 1) * num_data_;
-    HIPCHECK(hipMemcpyAsync(self->indices_.data() + leaves[l].begin, srcbuf + leaves[l].begin,
-                            sizeof(int32_t) * leaves[l].count, hipMemcpyDeviceToHost, stream_));
-  }
-  HIPCHECK(hipStreamSynchronize(stream_));
-  host_partition_fresh_ = true;
-}
-
-void GPUTreeLearner::AddPredictionToScore(const Tree* tree, double* out_score) const {
-  DownloadPartitionToHost();
-  SerialTreeLearner::AddPredictionToScore(tree, out_score);
-}
-
-void GPUTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
-                                     const std::function<double(const label_t*, int)>& residual,
-                                     data_size_t total_num_data, const data_size_t* bag_indices,
-                                     data_size_t bag_cnt) const {
-  if (obj == nullptr || !obj->IsRenewTreeOutput()) return;
-  DownloadPartitionToHost();
-  SerialTreeLearner::RenewTreeOutput(tree, obj, residual, total_num_data, bag_indices, bag_cnt);
 }
 
 // CEGB on the device (split + coupled penalties): the penalties, the model-wide used flags
@@ -2430,561 +1627,5 @@ std::vector<uint8_t> GPUTreeLearner::RowMajorBins(const Dataset* d, int row_word
   }
   return host;
 }
-
-// ---------------------------------------------------------------- validation sets
-int GPUTreeLearner::AddValidData(const Dataset* valid, int ntpi, const double* scores) {
-  if (valid->num_groups() != num_groups_ || valid->num_total_bin() != data_->num_total_bin()) return -1;
-  for (int g = 0; g < num_groups_; ++g) {
-    if (valid->group_bin_boundary(g) != data_->group_bin_boundary(g) ||
-        valid->group(g).num_total_bin != data_->group(g).num_total_bin) {
-      return -1;
-    }
-  }
-  HIPCHECK(hipSetDevice(device_id_));
-  ValidSet vs;
-  vs.num_data = valid->num_data();
-  vs.ntpi = ntpi;
-  std::vector<uint8_t> host = RowMajorBins(valid, args_.words_per_row);
-  HIPCHECK(hipMalloc(&vs.bins, std::max<size_t>(1, host.size())));
-  valid_allocs_.push_back(vs.bins);
-  HIPCHECK(hipMemcpy(vs.bins, host.data(), host.size(), hipMemcpyHostToDevice));
-  const size_t ns = static_cast<size_t>(vs.num_data) * ntpi;
-  HIPCHECK(hipMalloc(reinterpret_cast<void**>(&vs.score), std::max<size_t>(1, ns) * sizeof(double)));
-  valid_allocs_.push_back(vs.score);
-  HIPCHECK(hipMemcpy(vs.score, scores, ns * sizeof(double), hipMemcpyHostToDevice));
-  valid_.push_back(vs);
-  return static_cast<int>(valid_.size()) - 1;
-}
-
-void GPUTreeLearner::ValidAddConst(int slot, double v, int k) {
-  const ValidSet& vs = valid_[slot];
-  dev::AddConst(vs.score + static_cast<size_t>(k) * vs.num_data, vs.num_data, v, stream_);
-}
-
-void GPUTreeLearner::ValidMultiply(int slot, double v, int k) {
-  const ValidSet& vs = valid_[slot];
-  dev::MulConst(vs.score + static_cast<size_t>(k) * vs.num_data, vs.num_data, v, stream_);
-}
-
-void GPUTreeLearner::ValidAddTree(int slot, const Tree* tree, int k) {
-  const ValidSet& vs = valid_[slot];
-  double* score = vs.score + static_cast<size_t>(k) * vs.num_data;
-  if (tree->num_leaves() <= 1) {
-    dev::AddConst(score, vs.num_data, tree->LeafOutput(0), stream_);
-    return;
-  }
-  dev::DevTree t = StageTree(tree);
-  dev::KArgs a = args_;
-  a.bins = vs.bins;
-  a.row_words = a.words_per_row;  // (validation rows carry no (g, h))
-  dev::AddTreeScore(a, t, nullptr, vs.num_data, score, stream_);
-}
-
-bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vector<double>* sums) {
-  ValidSet& vs = valid_[slot];
-  if (spec.kind == 0 || spec.label == nullptr || vs.num_data <= 0) return false;
-  const bool aucmu = spec.kind == dev::kMetricAucMu;
-  const bool multi = spec.kind == dev::kMetricMultiLogloss || spec.kind == dev::kMetricMultiError || aucmu;
-  const bool query = spec.kind == dev::kMetricNDCG || spec.kind == dev::kMetricMAP;
-  if (vs.ntpi != (multi ? spec.num_class : 1)) return false;
-  if (query && (spec.qb == nullptr || spec.nq <= 0 || spec.eval_at.empty())) return false;
-  HIPCHECK(hipSetDevice(device_id_));
-  const size_t n = static_cast<size_t>(vs.num_data);
-  auto dev_alloc = [&](size_t bytes) {
-    void* p = nullptr;
-    HIPCHECK(hipMalloc(&p, std::max<size_t>(1, bytes)));
-    valid_allocs_.push_back(p);
-    return p;
-  };
-  auto upload = [&](const void* src, size_t bytes) {
-    void* d = dev_alloc(bytes);
-    if (bytes > 0) HIPCHECK(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice));
-    return d;
-  };
-  if (vs.label == nullptr) {
-    vs.label = static_cast<float*>(upload(spec.label, sizeof(float) * n));
-    if (spec.weights != nullptr) vs.weights = static_cast<float*>(upload(spec.weights, sizeof(float) * n));
-    vs.metric_out = static_cast<double*>(dev_alloc(sizeof(double) * 64));
-  }
-  if (spec.nout > 64) return false;
-  dev::MetricArgs m;
-  std::memset(&m, 0, sizeof(m));
-  if (query) {
-    // the metric's query inputs, uploaded on its first evaluation
-    auto it = vs.queries.find(spec.key);
-    if (it == vs.queries.end()) {
-      ValidSet::QueryInputs qi;
-      std::vector<int32_t> qb(spec.qb, spec.qb + spec.nq + 1);
-      qi.qb = static_cast<int32_t*>(upload(qb.data(), sizeof(int32_t) * qb.size()));
-      if (spec.qw != nullptr) qi.qw = static_cast<float*>(upload(spec.qw, sizeof(float) * spec.nq));
-      std::vector<int32_t> at(spec.eval_at.begin(), spec.eval_at.end());
-      qi.eval_at = static_cast<int32_t*>(upload(at.data(), sizeof(int32_t) * at.size()));
-      qi.qconst = static_cast<double*>(upload(spec.qconst.data(), sizeof(double) * spec.qconst.size()));
-      qi.label_gain = static_cast<double*>(upload(spec.label_gain.data(), sizeof(double) * spec.label_gain.size()));
-      qi.discount = static_cast<double*>(upload(spec.discount.data(), sizeof(double) * spec.discount.size()));
-      qi.scratch = dev_alloc(dev::MetricScratchBytes(0, static_cast<int64_t>(spec.nq) * spec.eval_at.size()));
-      it = vs.queries.emplace(spec.key, qi).first;
-    }
-    const ValidSet::QueryInputs& qi = it->second;
-    m.nq = spec.nq;
-    m.nk = static_cast<int32_t>(spec.eval_at.size());
-    m.qb = qi.qb;
-    m.qw = qi.qw;
-    m.eval_at = qi.eval_at;
-    m.qconst = qi.qconst;
-    m.label_gain = qi.label_gain;
-    m.discount = qi.discount;
-    m.scratch = qi.scratch;
-  } else {
-    if (aucmu) {  // the class weight matrix, uploaded on the metric's first evaluation
-      auto it = vs.queries.find(spec.key);
-      if (it == vs.queries.end()) {
-        ValidSet::QueryInputs qi;
-        qi.qconst = static_cast<double*>(upload(spec.qconst.data(), sizeof(double) * spec.qconst.size()));
-        it = vs.queries.emplace(spec.key, qi).first;
-      }
-      m.qconst = it->second.qconst;
-    }
-    if ((spec.kind == dev::kMetricAUC || aucmu) && vs.metric_scratch_rows < vs.num_data) {
-      vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(vs.num_data));
-      vs.metric_scratch_rows = vs.num_data;
-    } else if (vs.metric_scratch == nullptr) {
-      vs.metric_scratch = dev_alloc(dev::MetricScratchBytes(0));
-    }
-    m.scratch = vs.metric_scratch;
-  }
-  m.kind = spec.kind;
-  m.convert = spec.convert;
-  m.sigmoid = spec.sigmoid;
-  m.param = spec.param;
-  m.n = vs.num_data;
-  m.score = vs.score;
-  m.label = vs.label;
-  m.weights = vs.weights;
-  m.num_class = spec.num_class;
-  m.top_k = spec.top_k;
-  m.out = vs.metric_out;
-  dev::EvalMetric(m, stream_);
-  if (vs.logged_kinds.insert(spec.kind).second) {
-    if (slot == train_eval_slot_) Log::Debug("device metric (kind %d) on the training set", spec.kind);
-    else Log::Debug("device metric (kind %d) on validation set %d", spec.kind, slot);
-  }
-  sums->assign(std::max(2, spec.nout), 0.0);
-  HIPCHECK(hipMemcpyAsync(sums->data(), vs.metric_out, sizeof(double) * sums->size(), hipMemcpyDeviceToHost,
-                          stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  return true;
-}
-
-// training metrics (reference gbdt.cpp:484-542 evaluates them every metric_freq iterations):
-// the device metric kernels of the validation sets over the resident training scores, so
-// valid_sets=[train] costs one reduction instead of an 8 N-byte download and a host pass
-bool GPUTreeLearner::TrainEval(const DeviceMetricSpec& spec, std::vector<double>* sums) {
-  if (d_score_ == nullptr || num_data_ <= 0) return false;
-  if (train_eval_slot_ < 0) {
-    ValidSet vs;
-    vs.num_data = num_data_;
-    vs.ntpi = num_tree_per_iteration_;
-    vs.score = d_score_;  // (not owned: valid_allocs_ holds only the metric inputs)
-    valid_.push_back(vs);
-    train_eval_slot_ = static_cast<int>(valid_.size()) - 1;
-  }
-  return ValidEval(train_eval_slot_, spec, sums);
-}
-
-void GPUTreeLearner::ValidScoreToHost(int slot, double* host) {
-  const ValidSet& vs = valid_[slot];
-  HIPCHECK(hipMemcpyAsync(host, vs.score, sizeof(double) * vs.num_data * vs.ntpi, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-}
-
-// ---------------------------------------------------------------- scores & gradients
-void GPUTreeLearner::InitScores(int ntpi, const double* init_score) {
-  HIPCHECK(hipSetDevice(device_id_));
-  grad_prefetched_ = false;
-  num_tree_per_iteration_ = ntpi;
-  const size_t n = static_cast<size_t>(num_data_) * ntpi;
-  if (d_score_ == nullptr) {
-    d_score_ = Alloc<double>(n);
-    d_grad_ = Alloc<float>(n);
-    d_hess_ = Alloc<float>(n);
-  }
-  if (init_score != nullptr) {
-    HIPCHECK(hipMemcpy(d_score_, init_score, sizeof(double) * n, hipMemcpyHostToDevice));
-  } else {
-    HIPCHECK(hipMemset(d_score_, 0, sizeof(double) * n));
-  }
-}
-
-void GPUTreeLearner::SyncScoreToHost(double* host, int k) {
-  HIPCHECK(hipMemcpyAsync(host, d_score_ + static_cast<size_t>(k) * num_data_, sizeof(double) * num_data_,
-                          hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-}
-
-void GPUTreeLearner::SyncScoreFromHost(const double* host, int k) {
-  grad_prefetched_ = false;
-  HIPCHECK(hipMemcpyAsync(d_score_ + static_cast<size_t>(k) * num_data_, host, sizeof(double) * num_data_,
-                          hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-}
-
-void GPUTreeLearner::AddConstToScore(double v, int k) {
-  grad_prefetched_ = false;
-  dev::AddConst(d_score_ + static_cast<size_t>(k) * num_data_, num_data_, v, stream_);
-}
-
-void GPUTreeLearner::MultiplyScore(double v, int k) {
-  grad_prefetched_ = false;
-  dev::MulConst(d_score_ + static_cast<size_t>(k) * num_data_, num_data_, v, stream_);
-}
-
-void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
-  const int nl = tree->num_leaves();
-  double* score = d_score_ + static_cast<size_t>(k) * num_data_;
-  if (nl <= 1) {
-    AddConstToScore(tree->LeafOutput(0), k);
-    return;
-  }
-  if (dev::TreeBitmapsApply(args_, nl)) {
-    // the bitmap walk of every row (coalesced row reads and score updates) beats the
-    // partition-ordered scatter of leaf values; it also covers out-of-bag rows.  Wider or
-    // row-sparse storage scatters instead (the generic walk took 5 ms per tree on 100M rows)
-    if (last_grad_fusable_ && k == 0 && num_tree_per_iteration_ == 1 && dev::AddTreeScoreGradKind(last_grad_.kind) &&
-        FuseNextGradients()) {
-      // ... and computes the next iteration's gradients from the scores it writes
-      dev::DevTree t = StageTree(tree);
-      dev::AddTreeScoreGrad(args_, t, num_data_, score, last_grad_, stream_);
-      grad_parts_ = dev::AddTreeScoreGradParts(num_data_);
-      grad_prefetched_ = true;
-      gh_fresh_ = false;  // (d_gh_ now holds the next iteration's gradients)
-      split_stale_ = false;
-      return;
-    }
-    AddTreeToScore(tree, k);
-    return;
-  }
-  if (!device_mode_) {
-    // host-assisted growth keeps the leaves' row ranges on the host (the device leaf records
-    // are the last device-resident tree's): walk the tree for every row instead
-    AddTreeToScore(tree, k);
-    return;
-  }
-  std::vector<double> vals(nl);
-  for (int i = 0; i < nl; ++i) vals[i] = tree->LeafOutput(i);
-  HIPCHECK(hipMemcpyAsync(d_leaf_values_, vals.data(), sizeof(double) * nl, hipMemcpyHostToDevice, stream_));
-  dev::KArgs a = args_;
-  a.num_rows = root_rows_;
-  dev::AddLeafScore(a, d_leaf_values_, nl, score, stream_);
-  if (oob_cnt_ > 0) {
-    in_trained_update_ = true;  // AddTreeToScore restricts the traversal to out-of-bag rows
-    AddTreeToScore(tree, k);
-    in_trained_update_ = false;
-  }
-  HIPCHECK(hipStreamSynchronize(stream_));
-}
-
-dev::DevTree GPUTreeLearner::StageTree(const Tree* tree) {
-  const int nl = tree->num_leaves();
-  const int ni = nl - 1;
-  const auto& cb = tree->cat_boundaries_inner();
-  const auto& ct = tree->cat_threshold_inner();
-  // blob: [i32: split feature, left, right, category boundaries][u32: thresholds, category
-  // words][f64: leaf values][i8: decision types], 8-byte aligned sections
-  auto up8 = [](size_t x) { return (x + 7) & ~static_cast<size_t>(7); };
-  const size_t n_i32 = 3 * static_cast<size_t>(ni) + cb.size() + 1;
-  const size_t n_u32 = static_cast<size_t>(ni) + ct.size() + 1;
-  const size_t o_u32 = up8(4 * n_i32), o_f64 = o_u32 + up8(4 * n_u32), o_i8 = o_f64 + 8 * static_cast<size_t>(nl);
-  const size_t bytes = up8(o_i8 + std::max(1, ni));
-  if (tree_blob_cap_ < bytes) {
-    tree_blob_cap_ = std::max(bytes, 64 * static_cast<size_t>(config_->num_leaves) + 4096);
-    d_tree_blob_ = Alloc<char>(tree_blob_cap_);
-  }
-  const int nbm = std::max(ni, config_->num_leaves);
-  if (tree_bm_cap_ < nbm) {
-    tree_bm_cap_ = nbm;
-    d_tree_bm_ = Alloc<unsigned long long>(4 * static_cast<size_t>(nbm));
-    d_tree_bm_meta_ = Alloc<int32_t>(3 * static_cast<size_t>(nbm));
-  }
-  StageSlot& sl = stage_slots_[stage_next_];
-  stage_next_ = (stage_next_ + 1) % kStageSlots;
-  if (sl.done != nullptr) HIPCHECK(hipEventSynchronize(sl.done));  // (its previous copy: long done)
-  if (sl.cap < bytes) {
-    if (sl.host != nullptr) HIPCHECK(hipHostFree(sl.host));
-    sl.cap = std::max(bytes, tree_blob_cap_);
-    HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&sl.host), sl.cap, hipHostMallocDefault));
-  }
-  if (sl.done == nullptr) HIPCHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
-  int32_t* hi = reinterpret_cast<int32_t*>(sl.host);
-  uint32_t* hu = reinterpret_cast<uint32_t*>(sl.host + o_u32);
-  double* hf = reinterpret_cast<double*>(sl.host + o_f64);
-  int8_t* hb = reinterpret_cast<int8_t*>(sl.host + o_i8);
-  for (int j = 0; j < ni; ++j) {
-    hi[j] = tree->split_feature_inner(j);
-    hi[ni + j] = tree->left_child(j);
-    hi[2 * ni + j] = tree->right_child(j);
-    hu[j] = tree->threshold_in_bin(j);
-    hb[j] = tree->decision_type(j);
-  }
-  for (size_t j = 0; j < cb.size(); ++j) hi[3 * ni + j] = cb[j];
-  for (size_t j = 0; j < ct.size(); ++j) hu[ni + j] = ct[j];
-  for (int j = 0; j < nl; ++j) hf[j] = tree->LeafOutput(j);
-  HIPCHECK(hipMemcpyAsync(d_tree_blob_, sl.host, bytes, hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipEventRecord(sl.done, stream_));
-  const int32_t* di = reinterpret_cast<const int32_t*>(d_tree_blob_);
-  dev::DevTree t;
-  t.num_leaves = nl;
-  t.split_feature_inner = di;
-  t.left_child = di + ni;
-  t.right_child = di + 2 * ni;
-  t.cat_boundaries_inner = di + 3 * ni;
-  t.threshold_in_bin = reinterpret_cast<const uint32_t*>(d_tree_blob_ + o_u32);
-  t.cat_threshold_inner = t.threshold_in_bin + ni;
-  t.decision_type = reinterpret_cast<const int8_t*>(d_tree_blob_ + o_i8);
-  t.leaf_value = reinterpret_cast<const double*>(d_tree_blob_ + o_f64);
-  t.bm_work = d_tree_bm_;
-  t.bm_meta = d_tree_bm_meta_;
-  return t;
-}
-
-void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
-  grad_prefetched_ = false;
-  // NOTE: called from AddTrainedTreeToScore for out-of-bag rows only (oob_cnt_ > 0 and the
-  // tree just trained), otherwise for every row
-  double* score = d_score_ + static_cast<size_t>(k) * num_data_;
-  if (tree->num_leaves() <= 1) {
-    AddConstToScore(tree->LeafOutput(0), k);
-    return;
-  }
-  dev::DevTree t = StageTree(tree);
-  const bool oob_only = oob_cnt_ > 0 && in_trained_update_;
-  if (oob_only) {
-    dev::AddTreeScore(args_, t, d_oob_, oob_cnt_, score, stream_);
-  } else {
-    dev::AddTreeScore(args_, t, nullptr, num_data_, score, stream_);
-  }
-}
-
-// LGBM_AMD_FUSE_GRAD=0: the score walk does not compute the next gradients
-bool GPUTreeLearner::FuseNextGradients() {
-  const char* e = std::getenv("LGBM_AMD_FUSE_GRAD");
-  return !(e != nullptr && e[0] == '0');
-}
-
-bool GPUTreeLearner::SameGradArgs(const dev::GradArgs& x, const dev::GradArgs& y) {
-  return x.kind == y.kind && x.num_class == y.num_class && x.num_data == y.num_data && x.p0 == y.p0 && x.p1 == y.p1 &&
-         x.p2 == y.p2 && x.lw0 == y.lw0 && x.lw1 == y.lw1 && x.label == y.label && x.weights == y.weights &&
-         x.label_weight == y.label_weight && x.score == y.score && x.gh == y.gh && x.gh_stride == y.gh_stride &&
-         x.max_parts == y.max_parts && x.root_parts == y.root_parts;
-}
-
-bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
-  if (spec.kind == DeviceGradKind::None || spec.kind == DeviceGradKind::MulticlassOVA) return false;
-  if (spec.kind != DeviceGradKind::MulticlassSoftmax && ntpi != 1) return false;
-  if (spec.label == nullptr) return false;
-  const bool listwise = spec.kind == DeviceGradKind::Lambdarank || spec.kind == DeviceGradKind::RankXendcg;
-  if (listwise && (spec.rank.query_boundaries == nullptr || spec.rank.max_query_docs > dev::kRankMaxDocs)) {
-    return false;  // queries larger than the LDS staging: host gradients
-  }
-  const size_t n = static_cast<size_t>(num_data_);
-  const bool prefetched = grad_prefetched_;
-  grad_prefetched_ = false;
-  bool uploaded = false;
-  if (uploaded_label_src_ != spec.label) {
-    if (d_label_ == nullptr) d_label_ = Alloc<float>(n);
-    HIPCHECK(hipMemcpy(d_label_, spec.label, sizeof(float) * n, hipMemcpyHostToDevice));
-    uploaded_label_src_ = spec.label;
-    uploaded = true;
-  }
-  if (spec.weights != nullptr && uploaded_weight_src_ != spec.weights) {
-    if (d_weights_ == nullptr) d_weights_ = Alloc<float>(n);
-    HIPCHECK(hipMemcpy(d_weights_, spec.weights, sizeof(float) * n, hipMemcpyHostToDevice));
-    uploaded_weight_src_ = spec.weights;
-    uploaded = true;
-  }
-  if (spec.label_weight_arr != nullptr && uploaded_lw_src_ != spec.label_weight_arr) {
-    if (d_label_weight_ == nullptr) d_label_weight_ = Alloc<float>(n);
-    HIPCHECK(hipMemcpy(d_label_weight_, spec.label_weight_arr, sizeof(float) * n, hipMemcpyHostToDevice));
-    uploaded_lw_src_ = spec.label_weight_arr;
-    uploaded = true;
-  }
-  last_grad_fusable_ = false;
-  if (listwise) {
-    UploadRankTables(spec.rank, spec.kind);
-    dev::RankArgs ra;
-    ra.kind = spec.kind == DeviceGradKind::Lambdarank ? dev::kRankKindLambdarank : dev::kRankKindXendcg;
-    ra.num_queries = spec.rank.num_queries;
-    ra.qb = d_qb_;
-    ra.label = d_label_;
-    ra.weights = spec.weights != nullptr ? d_weights_ : nullptr;
-    ra.score = d_score_;
-    ra.grad = d_grad_;
-    ra.hess = d_hess_;
-    ra.inv_max_dcg = d_inv_max_dcg_;
-    ra.label_gain = d_label_gain_;
-    ra.discount = d_discount_;
-    ra.sigmoid = spec.rank.sigmoid;
-    ra.sig_min = spec.rank.sig_min;
-    ra.sig_max = spec.rank.sig_max;
-    ra.sig_factor = spec.rank.sig_factor;
-    ra.norm = spec.rank.norm ? 1 : 0;
-    ra.rng = d_rank_rng_;
-    dev::RankGradients(ra, stream_);
-    gh_fresh_ = false;
-    split_stale_ = false;
-    last_grad_fusable_ = false;
-    return true;
-  }
-  dev::GradArgs g;
-  g.kind = static_cast<int32_t>(spec.kind);
-  g.num_class = spec.kind == DeviceGradKind::MulticlassSoftmax ? ntpi : 1;
-  g.num_data = num_data_;
-  g.p0 = spec.p0;
-  g.p1 = spec.p1;
-  g.p2 = spec.p2;
-  g.lw0 = spec.label_weight[0];
-  g.lw1 = spec.label_weight[1];
-  g.label = d_label_;
-  g.weights = spec.weights != nullptr ? d_weights_ : nullptr;
-  g.label_weight = spec.label_weight_arr != nullptr ? d_label_weight_ : nullptr;
-  g.score = d_score_;
-  g.grad = d_grad_;
-  g.hess = d_hess_;
-  g.write_split = 1;
-  g.gh = nullptr;
-  g.gh_stride = args_.gh_stride;
-  g.max_parts = nullptr;
-  g.root_parts = nullptr;
-  const bool fuse = ntpi == 1 && spec.kind != DeviceGradKind::MulticlassSoftmax;
-  if (fuse) {
-    g.gh = d_gh_;
-    g.max_parts = d_max_parts_;
-    g.root_parts = d_root_parts_;
-    g.write_split = 0;
-    // the last score walk already computed these gradients from the current scores
-    // (AddTrainedTreeToScore), unless anything changed the scores or inputs since
-    if (prefetched && !uploaded && SameGradArgs(g, last_grad_)) {
-      gh_fresh_ = true;
-      split_stale_ = true;
-      last_grad_fusable_ = true;
-      return true;
-    }
-  }
-  dev::Gradients(g, stream_);
-  gh_fresh_ = fuse;
-  split_stale_ = fuse;
-  grad_parts_ = dev::GradientBlocks(num_data_);
-  if (fuse) {
-    last_grad_ = g;
-    last_grad_fusable_ = true;
-  }
-  return true;
-}
-
-// query boundaries, 1 / max DCG, label gains and position discounts (lambdarank) or the
-// per-query generators (xendcg; from here on they advance on the device)
-void GPUTreeLearner::UploadRankTables(const DeviceRankSpec& r, DeviceGradKind kind) {
-  if (uploaded_qb_src_ == r.query_boundaries) return;
-  const size_t nq = static_cast<size_t>(r.num_queries);
-  d_qb_ = Alloc<int32_t>(nq + 1);
-  HIPCHECK(hipMemcpy(d_qb_, r.query_boundaries, sizeof(int32_t) * (nq + 1), hipMemcpyHostToDevice));
-  if (kind == DeviceGradKind::Lambdarank) {
-    d_inv_max_dcg_ = Alloc<double>(nq);
-    HIPCHECK(hipMemcpy(d_inv_max_dcg_, r.inv_max_dcg, sizeof(double) * nq, hipMemcpyHostToDevice));
-    d_label_gain_ = Alloc<double>(r.num_label_gain);
-    HIPCHECK(hipMemcpy(d_label_gain_, r.label_gain, sizeof(double) * r.num_label_gain, hipMemcpyHostToDevice));
-    std::vector<double> disc(std::max<data_size_t>(1, r.max_query_docs));
-    for (size_t i = 0; i < disc.size(); ++i) disc[i] = DCG::Discount(static_cast<data_size_t>(i));
-    d_discount_ = Alloc<double>(disc.size());
-    HIPCHECK(hipMemcpy(d_discount_, disc.data(), sizeof(double) * disc.size(), hipMemcpyHostToDevice));
-  } else {
-    d_rank_rng_ = Alloc<uint32_t>(nq);
-    HIPCHECK(hipMemcpy(d_rank_rng_, r.rng_states, sizeof(uint32_t) * nq, hipMemcpyHostToDevice));
-  }
-  uploaded_qb_src_ = r.query_boundaries;
-}
-
-data_size_t GPUTreeLearner::DeviceSample(const DeviceSampleSpec& sp) {
-  HIPCHECK(hipSetDevice(device_id_));
-  const int64_t nb = dev::SampleBlocks(num_data_);
-  if (d_sample_rng_ == nullptr) {
-    d_sample_rng_ = Alloc<uint32_t>(nb);
-    d_sample_codes_ = Alloc<uint8_t>(num_data_);
-    d_sample_cnt_ = Alloc<int32_t>(nb);
-    d_sample_off_ = Alloc<int32_t>(nb);
-  }
-  if (sp.reset || !sample_seeded_) {
-    // generator of block b: Random(seed + b) (reference bagging_rands_)
-    std::vector<uint32_t> st(nb);
-    for (int64_t b = 0; b < nb; ++b) st[b] = static_cast<uint32_t>(sp.seed + static_cast<int>(b));
-    HIPCHECK(hipMemcpy(d_sample_rng_, st.data(), sizeof(uint32_t) * nb, hipMemcpyHostToDevice));
-    sample_seeded_ = true;
-  }
-  if (sp.balanced && uploaded_label_src_ != sp.label) {
-    if (d_label_ == nullptr) d_label_ = Alloc<float>(num_data_);
-    HIPCHECK(hipMemcpy(d_label_, sp.label, sizeof(float) * num_data_, hipMemcpyHostToDevice));
-    uploaded_label_src_ = sp.label;
-  }
-  if (sp.goss) MaterializeSplitGradients();  // (GOSS reads and rescales grad / hess)
-  dev::SampleArgs s;
-  s.num_data = num_data_;
-  s.num_blocks = nb;
-  s.goss = sp.goss ? 1 : 0;
-  s.balanced = sp.balanced ? 1 : 0;
-  s.num_class = sp.num_tree_per_iteration;
-  s.fraction = sp.fraction;
-  s.pos_fraction = sp.pos_fraction;
-  s.neg_fraction = sp.neg_fraction;
-  s.top_rate = sp.top_rate;
-  s.other_rate = sp.other_rate;
-  s.label = d_label_;
-  s.grad = d_grad_;
-  s.hess = d_hess_;
-  s.rng = d_sample_rng_;
-  s.codes = d_sample_codes_;
-  s.block_cnt = d_sample_cnt_;
-  s.block_off = d_sample_off_;
-  s.bag = d_bag_;
-  s.oob = d_oob_;
-  s.bag_count = d_bag_count_;
-  dev::SampleRows(s, stream_);
-  int32_t cnt = 0;
-  HIPCHECK(hipMemcpyAsync(&cnt, d_bag_count_, sizeof(int32_t), hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-  if (sp.goss) gh_fresh_ = false;  // the sampled rows' gradients were rescaled in place
-  // SerialTreeLearner::SetBaggingData state; the rows themselves stay on the device
-  bag_indices_ = nullptr;
-  bag_cnt_ = cnt;
-  use_bag_ = cnt < num_data_;
-  oob_cnt_ = num_data_ - cnt;
-  if (sp.host_indices != nullptr) {
-    sp.host_indices->resize(num_data_);
-    HIPCHECK(hipMemcpy(sp.host_indices->data(), d_bag_, sizeof(int32_t) * cnt, hipMemcpyDeviceToHost));
-    if (oob_cnt_ > 0) {
-      HIPCHECK(hipMemcpy(sp.host_indices->data() + cnt, d_oob_, sizeof(int32_t) * oob_cnt_, hipMemcpyDeviceToHost));
-    }
-    bag_indices_ = sp.host_indices->data();
-  }
-  return cnt;
-}
-
-void GPUTreeLearner::UploadGradients(const score_t* g, const score_t* h, int64_t n) {
-  gh_fresh_ = false;
-  split_stale_ = false;
-  last_grad_fusable_ = false;
-  grad_prefetched_ = false;
-  HIPCHECK(hipMemcpyAsync(d_grad_, g, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipMemcpyAsync(d_hess_, h, sizeof(float) * n, hipMemcpyHostToDevice, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-}
-
-void GPUTreeLearner::DownloadGradients(score_t* g, score_t* h, int64_t n) {
-  MaterializeSplitGradients();
-  HIPCHECK(hipMemcpyAsync(g, d_grad_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipMemcpyAsync(h, d_hess_, sizeof(float) * n, hipMemcpyDeviceToHost, stream_));
-  HIPCHECK(hipStreamSynchronize(stream_));
-}
-
-void GPUTreeLearner::Synchronize() { HIPCHECK(hipStreamSynchronize(stream_)); }
 
 }  // namespace lgbm_amd

@@ -162,6 +162,14 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   static constexpr size_t kRoundHist = 3;
   std::vector<int> round_hist_;  // rounds of the last kRoundHist trees (the next one enqueues their max + 1)
   bool last_tree_rounds_ = false;
+  // round growth vs one split per step, chosen by timing (AutoGrowthRounds)
+  enum { kAutoUnset, kAutoProbe, kAutoRounds, kAutoSteps };
+  int auto_state_ = kAutoUnset, auto_tree_ = 0;
+  double auto_rounds_ms_ = 1e300;
+  bool AutoGrowthRounds();
+  void AutoGrowthRecord(double ms);
+  void DestroyStepGraph();
+  void DestroyRoundGraphs();
 
   void SetupOwnership();
   void GatherFeatureBests();

@@ -165,3 +165,22 @@ def test_round_growth_self_check(monkeypatch, gpu_available):
         "LGBM_AMD_BoosterDeviceCheckSplits", bst.handle, size, need, buf), 1 << 16))
     assert res["device_mode"] and res["checked"] > 0
     assert res["mismatched"] == 0, res
+
+
+def test_timed_growth_mode_choice_keeps_the_trees(monkeypatch, tmp_path, capfd):
+    """LGBM_AMD_ROUND_AUTO=1 (by default from 16M rows per rank): trees 1-2 are timed with
+    round growth and tree 4 with one split per step, and the faster mode grows the rest.  The
+    growth mode never changes a tree: the model equals pure round growth's, and the iteration
+    log shows the probe trees without rounds."""
+    X, y = _data()
+    params = {"objective": "binary", "verbose": 1}
+    monkeypatch.setenv("LGBM_AMD_ROUND_AUTO", "0")
+    base, _ = _model(monkeypatch, tmp_path, 6, X, y, params, rounds=10, tag="fixed")
+    capfd.readouterr()
+    monkeypatch.setenv("LGBM_AMD_ROUND_AUTO", "1")
+    auto, rows = _model(monkeypatch, tmp_path, 6, X, y, params, rounds=10, tag="auto")
+    out = capfd.readouterr()
+    assert "growth timed at" in out.out + out.err
+    assert auto == base
+    per_tree = [r["rounds"][0] for r in rows]
+    assert per_tree[3] == 0 and per_tree[4] == 0 and per_tree[1] > 0
