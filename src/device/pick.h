@@ -53,20 +53,35 @@ __device__ __forceinline__ ArgC ArgShflXor(const ArgC& c, int o) {
   return r;
 }
 
-// three independent wave argmaxes, interleaved: each butterfly step issues the cross-lane
-// moves of all three chains before any comparison, so their latencies (ds_bpermute, ~100+
-// cycles each) overlap -- three back-to-back reductions cost ~5 us per pick.  Rolled: this
-// runs once per split on a cold I-cache.
+// the wave's best candidate in ArgTake order (larger gain, NaN = -inf; smaller real feature;
+// lower index): two 64-bit DPP max-reductions and a read of the winning lane instead of a
+// butterfly of 4-field shuffles through the LDS crossbar
+__device__ __forceinline__ ArgC ArgWaveBest(ArgC c) {
+  const bool live = c.idx >= 0;
+  const unsigned long long k1 = live ? GainKey(c.g) : 0ull;  // (GainKey(-inf) > 0: a live -inf still counts)
+  const unsigned long long m1 = WaveMaxDpp(k1);
+  if (m1 == 0ull) return ArgNone();
+  const bool t1 = live && k1 == m1;
+  const unsigned long long k2 = t1 ? ((static_cast<unsigned long long>(~static_cast<uint32_t>(c.rf)) << 32) |
+                                      static_cast<unsigned long long>(~static_cast<uint32_t>(c.idx)))
+                                   : 0ull;
+  const unsigned long long m2 = WaveMaxDpp(k2);
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(__builtin_ctzll(__ballot(t1 && k2 == m2))));
+  ArgC r;
+  r.g = ReadLane(c.g, w);
+  r.rf = ReadLane(c.rf, w);
+  r.idx = ReadLane(c.idx, w);
+  r.x = ReadLane(c.x, w);
+  return r;
+}
+
+// three independent wave argmaxes (the pick's two fresh children and the other leaves), each
+// over DPP max-reductions of ordered keys (the butterfly of 4-field shuffles through the LDS
+// crossbar this replaced cost ~5 us per pick even interleaved)
 __device__ __forceinline__ void WaveArgBest3(ArgC* a, ArgC* b, ArgC* c) {
-#pragma unroll 1
-  for (int o = 32; o > 0; o >>= 1) {
-    const ArgC oa = ArgShflXor(*a, o);
-    const ArgC ob = ArgShflXor(*b, o);
-    const ArgC oc = ArgShflXor(*c, o);
-    ArgTake(a, oa);
-    ArgTake(b, ob);
-    ArgTake(c, oc);
-  }
+  *a = ArgWaveBest(*a);
+  *b = ArgWaveBest(*b);
+  *c = ArgWaveBest(*c);
 }
 
 // cat: the feature's category set (KArgs::feat_cat) when b is a categorical split

@@ -731,28 +731,6 @@ struct RoundFindShared {
   ArgC arg[NT / kWave];
 };
 
-// the wave's best candidate in ArgTake order (larger gain, NaN = -inf; smaller real feature;
-// lower index): two 64-bit DPP max-reductions and a read of the winning lane instead of a
-// butterfly of 4-field shuffles through the LDS crossbar
-__device__ __forceinline__ ArgC ArgWaveBest(ArgC c) {
-  const bool live = c.idx >= 0;
-  const unsigned long long k1 = live ? GainKey(c.g) : 0ull;  // (GainKey(-inf) > 0: a live -inf still counts)
-  const unsigned long long m1 = WaveMaxDpp(k1);
-  if (m1 == 0ull) return ArgNone();
-  const bool t1 = live && k1 == m1;
-  const unsigned long long k2 = t1 ? ((static_cast<unsigned long long>(~static_cast<uint32_t>(c.rf)) << 32) |
-                                      static_cast<unsigned long long>(~static_cast<uint32_t>(c.idx)))
-                                   : 0ull;
-  const unsigned long long m2 = WaveMaxDpp(k2);
-  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(__builtin_ctzll(__ballot(t1 && k2 == m2))));
-  ArgC r;
-  r.g = ReadLane(c.g, w);
-  r.rf = ReadLane(c.rf, w);
-  r.idx = ReadLane(c.idx, w);
-  r.x = ReadLane(c.x, w);
-  return r;
-}
-
 // per-feature result slot of child y, inner feature f (distributed: rank-major blocks)
 __device__ __forceinline__ size_t RoundFbIndex(const KArgs& a, int y, int f) {
   if (!a.round_dist || a.round_vote) return static_cast<size_t>(y) * a.p.num_features + f;
