@@ -186,7 +186,11 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   }
   const int mi_base = ROOT ? 0 : st->bynode_next;  // this step's per-node masks (advanced by the pick)
   int8_t used = tree_used;  // evaluated at this node (feature_fraction_bynode)
-  if (a.node_mask != nullptr && !rescan) used = used && a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f];
+  // (voting: the local scan evaluates every feature, the global scan of the elected ones
+  // applies the node's sample -- VotingParallelTreeLearner::FindBestSplits)
+  if (a.node_mask != nullptr && !rescan && a.p.vote_phase != 1) {
+    used = used && a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f];
+  }
   // (voting: every feature is scanned -- the vote may elect one this rank could not split)
   const int8_t parent_ok = (ROOT || a.p.vote_phase != 0) ? 1
                            : rescan ? a.splittable[static_cast<size_t>(a.leaves[rleaf].frow) * a.p.num_features + f]

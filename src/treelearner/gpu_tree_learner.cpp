@@ -760,8 +760,9 @@ void GPUTreeLearner::DecideMode() {
                      config_->num_leaves > dev::kMonoInterMaxLeaves)) {
     dm = false;
   }
-  // voting: per-node sampling and extra_trees draws stay with the host voting loop
-  if (voting_ && (config_->feature_fraction_bynode < 1.0 || config_->extra_trees)) dm = false;
+  // voting: extra_trees draws stay with the host voting loop (its local and global scans draw
+  // in their own order); per-node sampling runs on the device (the global scan's masks)
+  if (voting_ && config_->extra_trees) dm = false;
   // CEGB: split and coupled feature penalties are applied by the device scans (single rank);
   // lazy penalties (per-row usage bitsets) and distributed CEGB run host-assisted
   const bool cegb = CostEffectiveGB::Enabled(*config_);

@@ -304,6 +304,24 @@ def test_distributed_modes_device_resident(learner, world, mode, gpu_available, 
     assert _splits(dev[0][0], 0) == _splits(serial.model_to_string(), 0)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_voting_bynode_device_resident(world, gpu_available, capfd, monkeypatch):
+    """Voting-parallel with per-node column sampling on the device: the local scans evaluate
+    every feature, the global scans of the elected features apply the node's sample (drawn in
+    the host voting loop's order); the trees equal the host voting loop's (host-assisted growth)
+    on every rank."""
+    extra = {"feature_fraction_bynode": 0.6, "top_k": 4}
+    capfd.readouterr()
+    _, _, _, dev = _run("voting", world, rounds=5, verbose=2, **extra)
+    log = capfd.readouterr().out
+    assert "device-resident growth" in log and "host-assisted growth" not in log
+    for md, _ in dev:
+        assert _trees(md) == _trees(dev[0][0])
+    monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    _, _, _, host = _run("voting", world, rounds=5, **extra)
+    assert _trees(host[0][0]) == _trees(dev[0][0])
+
+
 def test_bench_py_under_torchrun_two_processes(gpu_available, tmp_path):
     """The multi-GPU benchmark entry point as the driver launches it (torch.distributed.run,
     one process per rank, peer comm), here with 2 processes sharing the box's GPU and 1M rows:
