@@ -1240,7 +1240,7 @@ __device__ __forceinline__ void RegTakeChildren(RegLeaf* x, int lane, int w, int
 #endif
 }
 // returns s (splits after the replay); *done, *npick; acc / accn / s_pick / tnode as the LDS path
-__device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, const double* ng, const int* nrf,
+__device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, int kround, const double* ng, const int* nrf,
                                  const int* nch, int* tnode, int* acc, int* accn, int* s_pick, int* done_out,
                                  int* npick_out) {
   const int lane = threadIdx.x & 63;
@@ -1271,7 +1271,7 @@ __device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, const 
   int n = 0;
   if (!done) {
     const int need = L - 1 - s;
-    int kmax = min(a.round_k, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
+    int kmax = min(kround, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
     kmax = min(kmax, a.round_emax - used - (need - 1));
     kmax = max(kmax, min(1, a.round_emax - used));
     if (kmax <= 0) done = 1;
@@ -1332,6 +1332,8 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   const int s0 = rd->nsplit;
   const int nexp_prev = rd->nexp;
   const int round0 = rd->round, rounds0 = rd->rounds, accmax0 = rd->accepted_max;
+  const int kcur = rd->k_cur;
+  const int kround = (kcur > 0 && kcur < a.round_k) ? kcur : a.round_k;  // this tree's round width
   const int nn = rd->next_frow;  // nodes of the tree so far
   const int next_slot = rd->next_slot;
   const bool dp = a.p.data_parallel != 0;  // (global counts: the split's estimates)
@@ -1457,7 +1459,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   // expanded; its children nodes become leaves w and s + 1
   if (tid < kWave && L <= kWave) {
     int done = 0, n = 0;
-    const int s = ReplayPredictRegs(a, L, s0, (nn - 1) / 2, ng, nrf, nch, tnode, acc, accn, s_pick, &done, &n);
+    const int s = ReplayPredictRegs(a, L, s0, (nn - 1) / 2, kround, ng, nrf, nch, tnode, acc, accn, s_pick, &done, &n);
     if (lane == 0) {
       s_s1 = s;
       s_done = done;
@@ -1503,7 +1505,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       // budget: after this round, one expansion per split the tree may still need stays
       // available (each round then accepts at least its first pick, the blocker)
       const int need = L - 1 - s, used = (nn - 1) / 2;
-      int kmax = min(a.round_k, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
+      int kmax = min(kround, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
       kmax = min(kmax, a.round_emax - used - (need - 1));
       kmax = max(kmax, min(1, a.round_emax - used));
       if (kmax <= 0) done = 1;  // (unreachable: the budget keeps room for the blocker)

@@ -177,6 +177,11 @@ constexpr int kRoundFirstPred = 16;  // rounds enqueued for the first tree
 
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
   a.rd = d_round_;
+  if (k_adapt_) {
+    // this tree's round width (Round::k_cur: the captured graphs are sized for round_k_)
+    k_cur_host_ = (prev_splits_ <= 0 || prev_expansions_ <= prev_splits_ + 2) ? round_k_ : std::min(round_k_, 6);
+    HIPCHECK(hipMemcpyAsync(&d_round_->k_cur, &k_cur_host_, sizeof(int32_t), hipMemcpyHostToDevice, stream_));
+  }
   a.pick_in_find = 0;  // the root's split scan only publishes; RoundRootPlan picks
   // (LGBM_AMD_KTRACE: k_round_split's phase times of one workgroup per round)
   if (a.ktrace != nullptr) HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
@@ -305,6 +310,8 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   if (round_hist_.size() > kRoundHist) round_hist_.erase(round_hist_.begin());
   last_stats_.rounds = h_round_->rounds;
   last_stats_.expansions = (h_round_->next_frow - 1) / 2;
+  prev_expansions_ = last_stats_.expansions;
+  prev_splits_ = h_round_->nsplit;
   // (every enqueued round's collectives run; a finished tree's exit at once)
   last_stats_.collective_bytes = distributed_ ? root_collective_bytes_ + RoundCollectiveBytes() * launched : 0.0;
   return h_round_->nsplit;

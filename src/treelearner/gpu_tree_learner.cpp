@@ -309,8 +309,17 @@ void GPUTreeLearner::UploadData() {
   const int n_leaves = config_->num_leaves;
   // round growth: up to round_k_ leaves expanded per round (LGBM_AMD_ROUND_K, 1 = one split per
   // step; distributed learners run rounds with a device communicator)
-  round_k_ = 6;  // (A/B at 300 iterations of the headline: K 3..16 = 2.40 2.27 2.20 2.20 2.21 2.30 2.48 2.50 ms)
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) round_k_ = std::atoi(e);
+  // Without LGBM_AMD_ROUND_K the width adapts per tree (RunRounds): 8 while the last tree's
+  // speculation was accepted (expansions <= splits + 2: early trees), else 6 (A/B at 300
+  // iterations of the headline, profiles/r04_round_width.md: K=8 saves 2 rounds on the first
+  // trees for 2 more expansions, later it adds 8-10 unaccepted ones; fixed K 6 / 8 / 10 =
+  // 2.040 / 2.072 / 2.132 ms, window of 20 after 5: 2.148 / 2.075)
+  round_k_ = 8;
+  k_adapt_ = true;
+  if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) {
+    round_k_ = std::atoi(e);
+    k_adapt_ = false;
+  }
   round_k_ = std::max(1, std::min(dev::kMaxRoundExp, round_k_));
   // speculation below the leaves (LGBM_AMD_ROUND_VMAX levels, 0: leaves only): one index
   // buffer per level + 2 (device_types.h), bounded to 32 GiB of row indices

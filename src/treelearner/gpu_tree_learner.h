@@ -162,6 +162,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   static constexpr size_t kRoundHist = 3;
   std::vector<int> round_hist_;  // rounds of the last kRoundHist trees (the next one enqueues their max + 1)
   bool last_tree_rounds_ = false;
+  // per-tree round width (LGBM_AMD_ROUND_K unset): the last round tree's speculation outcome
+  bool k_adapt_ = false;
+  int32_t k_cur_host_ = 0;
+  int prev_expansions_ = 0, prev_splits_ = 0;
   // round growth vs one split per step, chosen by timing (AutoGrowthRounds)
   enum { kAutoUnset, kAutoProbe, kAutoRounds, kAutoSteps };
   int auto_state_ = kAutoUnset, auto_tree_ = 0;
