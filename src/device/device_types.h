@@ -104,7 +104,6 @@ struct ChildStats {
   int32_t global_count, depth, slot, leaf;
   int32_t frow;        // splittable row the child's scan writes
   IcMask icmask;       // Leaf::icmask
-  double lsum_g, lsum_h;  // voting-parallel round growth: this rank's sums of the node's rows
 };
 
 // the split being applied, as chosen by the partition kernel's pick
@@ -201,7 +200,6 @@ struct ExpPlan {
   Feature feat;                  // the split feature's record
   DeviceSplit split;
   ChildStats lr[2];              // left / right child as known from the split
-  double plsum_g, plsum_h;       // voting-parallel: the node's local sums (RNode::st.lsum_*)
 };
 
 // one node of a tree under round growth (index: its splittable row): the root and both

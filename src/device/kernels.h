@@ -206,6 +206,7 @@ struct KArgs {
   // vote_list) and their histograms ([2 * round_k][vote_k][2 * max_feature_bins] in vote_hist)
   // feed phase 2, the global scan of the elected features (grid (vote_k, 2 * round_k))
   int32_t round_vote;
+  double* rnode_lsum;  // voting rounds: this rank's (g, h) sums of every node's rows, [round_nodes][2]
   int32_t max_owned;
   int32_t rs_block;
   long long* round_send;

@@ -110,7 +110,7 @@ struct SplitExp {
 // range, rights from its back, in the other index buffer), the histogrammed child's rows
 // compacted into an LDS row list and gathered into the tile's LDS histogram, stored as
 // partial kb.  Only column tile 0 writes the partition.
-template <int GPW, int UNITS, int GR>
+template <int GPW, int UNITS, int GR, bool VOTE = false>
 __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
   extern __shared__ unsigned long long lds[];  // [UNITS * tile_bins] histogram, then the row list
   __shared__ SplitExp ex[kMaxRoundExp];
@@ -188,7 +188,9 @@ __global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
   const bool writer = blockIdx.y == 0;
   // voting-parallel: the histogrammed rows' fixed-point (g, h), summed per row block by the
   // threads of word 0 of column tile 0 (each row once) -- that child's local sums
-  const bool loc_sums = a.round_vote != 0 && writer;
+  // (a template flag: the accumulators cost the other variants registers -- Epsilon-shaped
+  // wide rows 10.6 vs 11.8 ms/iter with a run-time flag)
+  const bool loc_sums = VOTE && writer;
   long long loc_g = 0, loc_h = 0;
   int row[kSplitRows];
   uint32_t gb[kSplitRows];
@@ -803,7 +805,7 @@ __device__ void ChildBest(const KArgs& a, int y, int node, RoundFindShared<KIND,
 // expansion's reduced histogram (or sums its few partials itself) into its new slot; the
 // other one subtracts it from the parent's slot in place (exact int64).  Children of an
 // expansion that cannot be split (max_depth, min_data_in_leaf) are not scanned.
-template <int KIND, bool SIMPLE, int NT>
+template <int KIND, bool SIMPLE, int NT, bool VG = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave ? LGBM_FIND_WAVE_OCC : 1))) void k_round_find(KArgs a) {
   constexpr bool CAT = KIND >= 2;  // (3: the wide categorical variant)
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
@@ -815,10 +817,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   // voting-parallel rounds (KArgs::round_vote): Params::vote_phase 1 scans every feature on this
   // rank's histograms, sums and counts; 2 scans the features the vote elected for child y
   // (KArgs::vote_list) on their all-reduced histograms (KArgs::vote_hist)
+  // (VG: the global scan is an instantiation of its own -- a run-time flag put the elected
+  // feature's load in front of every scan's feature load: +10% on wide data)
   const bool vote_local = a.round_vote && a.p.vote_phase == 1;
-  const bool vote_global = a.round_vote && a.p.vote_phase == 2;
+  constexpr bool vote_global = VG;
   int f = CAT ? a.cat_list[blockIdx.x] : (a.feat_list != nullptr ? a.feat_list[blockIdx.x] : static_cast<int>(blockIdx.x));
-  if (vote_global) f = a.vote_list[y * a.p.vote_k + blockIdx.x];
+  if constexpr (VG) f = a.vote_list[y * a.p.vote_k + blockIdx.x];
   const bool vote_empty = f < 0;  // (an empty elected slot, or a padded owner slot)
   if (vote_empty) f = 0;
   const int tid = threadIdx.x;
@@ -833,8 +837,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const int e_slot_new = E.slot_new, e_slot_parent = E.slot_parent, e_frow = E.frow_child[lr];
   const int e_frow_parent = E.frow_parent, blk_off = E.blk_off, e_nblk = E.nblk;
   const ChildStats cl = E.lr[lr];
-  const unsigned long long loc0 = rd->loc_acc[j][0], loc1 = rd->loc_acc[j][1];
-  const double pl_g = E.plsum_g, pl_h = E.plsum_h;
   const Feature F = a.feat[f];
   const int8_t tree_used = a.tree_mask[f];
   if (done) return;
@@ -882,7 +884,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const int frow = e_frow;
   const int nblk = a.round_fused ? e_nblk : RoundHistBlocks(a, rd, j);
   // (voting: every feature is scanned -- the vote may elect one this rank could not split)
-  const int8_t parent_ok = a.round_vote ? 1 : a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
+  const int8_t parent_flag = a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
+  const int8_t parent_ok = a.round_vote ? 1 : parent_flag;
   FeatureBest* fb_out = &a.feat_best[RoundFbIndex(a, y, f)];
   int8_t* flags = a.splittable + static_cast<size_t>(frow) * NF;
   const SplitParams& p = a.p.sp;
@@ -918,7 +921,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     L.c.max = cl.cmax;
     if (vote_local) {
       // this rank's rows of the child: the histogrammed child's sums from k_round_split, the
-      // other one's as the parent's minus those
+      // other one's as the parent's minus those (loaded here only: the extra loads in the
+      // common batch cost the narrow one-wave scans of wide data ~20%)
+      const unsigned long long loc0 = rd->loc_acc[j][0], loc1 = rd->loc_acc[j][1];
+      const double pl_g = a.rnode_lsum[2 * E.node], pl_h = a.rnode_lsum[2 * E.node + 1];
       const double hg = static_cast<double>(static_cast<long long>(loc0)) * ig;
       const double hh = static_cast<double>(static_cast<long long>(loc1)) * ih;
       L.sg = is_hist ? hg : pl_g - hg;
@@ -1399,9 +1405,11 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       r.st.leaf = 0;
       r.st.frow = 0;
       r.st.icmask = R.icmask;
-      r.st.lsum_g = R.lsum_g;  // (voting: the local root scan's sums)
-      r.st.lsum_h = R.lsum_h;
       a.rnode[0] = r;
+      if (a.round_vote) {  // (voting: the local root scan's sums)
+        a.rnode_lsum[0] = R.lsum_g;
+        a.rnode_lsum[1] = R.lsum_h;
+      }
       ng[0] = b.idx >= 0 ? b.g : -INFINITY;
       nrf[0] = b.idx >= 0 ? b.rf : -1;
       nch[0] = -1;
@@ -1429,10 +1437,12 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         const double hg = static_cast<double>(static_cast<long long>(rd->loc_acc[tid][0])) * a.scales[2];
         const double hh = static_cast<double>(static_cast<long long>(rd->loc_acc[tid][1])) * a.scales[3];
         const int h = E.hist_left ? 0 : 1;
-        cn[h].st.lsum_g = hg;
-        cn[h].st.lsum_h = hh;
-        cn[1 - h].st.lsum_g = E.plsum_g - hg;
-        cn[1 - h].st.lsum_h = E.plsum_h - hh;
+        double* pl = a.rnode_lsum + 2 * E.node;
+        double* cl = a.rnode_lsum + 2 * c;
+        cl[2 * h] = hg;
+        cl[2 * h + 1] = hh;
+        cl[2 * (1 - h)] = pl[0] - hg;
+        cl[2 * (1 - h) + 1] = pl[1] - hh;
       }
     }
     // one batch of independent loads: every node's best and children, every leaf's node
@@ -1594,8 +1604,6 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       e.frow_parent = node;
       e.frow_child[0] = next_frow + 2 * j;
       e.frow_child[1] = next_frow + 2 * j + 1;
-      e.plsum_g = P.st.lsum_g;
-      e.plsum_h = P.st.lsum_h;
       // children's statistics from the split (basic monotone constraints: the mid-point bound)
       const int depth = P.st.depth + 1;
       double pmin = P.st.cmin, pmax = P.st.cmax, rmin = P.st.cmin, rmax = P.st.cmax;
@@ -1622,7 +1630,6 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       lc.leaf = -1;
       lc.frow = e.frow_child[0];
       lc.icmask = icm;
-      lc.lsum_g = lc.lsum_h = 0.0;  // (voting: set by the next plan, from the partition's local sums)
       rc.sum_g = rsg;
       rc.sum_h = rsh;
       rc.output = ro;
@@ -1634,7 +1641,6 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       rc.leaf = -1;
       rc.frow = e.frow_child[1];
       rc.icmask = icm;
-      rc.lsum_g = rc.lsum_h = 0.0;
       e.lr[0] = lc;
       e.lr[1] = rc;
       a.rnode[node].expanded = 1;
@@ -1679,8 +1685,8 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       lf.sum_g = R.st.sum_g;
       lf.sum_h = R.st.sum_h;
       lf.output = R.st.output;
-      lf.lsum_g = R.st.lsum_g;
-      lf.lsum_h = R.st.lsum_h;
+      lf.lsum_g = a.round_vote ? a.rnode_lsum[2 * n] : 0.0;
+      lf.lsum_h = a.round_vote ? a.rnode_lsum[2 * n + 1] : 0.0;
       lf.cmin = R.st.cmin;
       lf.cmax = R.st.cmax;
       a.leaves[l] = lf;
@@ -1775,43 +1781,43 @@ size_t RoundPlanLds(int num_leaves, int nodes) {
 
 namespace {
 
-template <int GR>
+template <int GR, bool VOTE = false>
 void LaunchRoundSplit(const KArgs& a, hipStream_t s) {
   const dim3 grid(a.round_grid, a.hist_tiles);
   const size_t lds = sizeof(unsigned long long) * a.hist_units * static_cast<size_t>(a.tile_bins) + sizeof(int) * kSplitSub;
   if (a.sp_ptr != nullptr) {
-    if (a.hist_units == 1) hipLaunchKernelGGL((k_round_split<kSparseGPW, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_round_split<kSparseGPW, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.hist_units == 1) hipLaunchKernelGGL((k_round_split<kSparseGPW, 1, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_round_split<kSparseGPW, 2, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
   } else if (a.hist_units == 1) {
-    if (a.nibbles) hipLaunchKernelGGL((k_round_split<8, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
-    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
-    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_round_split<0, 1, GR>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_round_split<8, 1, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 1, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 1, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_round_split<0, 1, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
   } else {
-    if (a.nibbles) hipLaunchKernelGGL((k_round_split<8, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
-    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
-    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
-    else hipLaunchKernelGGL((k_round_split<0, 2, GR>), grid, dim3(kPartThreads), lds, s, a);
+    if (a.nibbles) hipLaunchKernelGGL((k_round_split<8, 2, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 1) hipLaunchKernelGGL((k_round_split<4, 2, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
+    else if (a.bin_bytes == 2) hipLaunchKernelGGL((k_round_split<2, 2, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
+    else hipLaunchKernelGGL((k_round_split<0, 2, GR, VOTE>), grid, dim3(kPartThreads), lds, s, a);
   }
 }
 
-template <int GR>
+template <int GR, bool VOTE = false>
 void AllowRoundSplitLds(int mx) {
   auto allow = [mx](const void* k) {
     if (mx > 65536 && hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, mx) != hipSuccess) {
       (void)hipGetLastError();
     }
   };
-  allow(reinterpret_cast<const void*>(k_round_split<8, 1, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<8, 2, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<4, 1, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<2, 1, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<0, 1, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<4, 2, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<2, 2, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<0, 2, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<kSparseGPW, 1, GR>));
-  allow(reinterpret_cast<const void*>(k_round_split<kSparseGPW, 2, GR>));
+  allow(reinterpret_cast<const void*>(k_round_split<8, 1, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<8, 2, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<4, 1, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<2, 1, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<0, 1, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<4, 2, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<2, 2, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<0, 2, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<kSparseGPW, 1, GR, VOTE>));
+  allow(reinterpret_cast<const void*>(k_round_split<kSparseGPW, 2, GR, VOTE>));
 }
 
 bool RoundSimpleGains(const KArgs& a) {
@@ -1819,7 +1825,8 @@ bool RoundSimpleGains(const KArgs& a) {
   return !p.use_l1 && !p.use_max_output && !p.use_smoothing && !p.use_mc;
 }
 
-void LaunchRoundFind(const KArgs& a, hipStream_t s) {
+template <bool VG>
+void LaunchRoundFindT(const KArgs& a, hipStream_t s) {
   const int ny = 2 * a.round_k;
   size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
   if (a.plan_in_find) lds = std::max(lds, RoundPlanLds(a.p.num_leaves, a.round_nodes));
@@ -1830,21 +1837,26 @@ void LaunchRoundFind(const KArgs& a, hipStream_t s) {
   const int ncat = (a.round_vote && a.p.vote_phase == 2) ? a.num_scan : a.p.has_cat;
   if (a.p.has_cat) {
     if (narrow) {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave>), g, b, lds, s, a);
-      else hipLaunchKernelGGL((k_round_find<1, false, kWave>), g, b, lds, s, a);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave, VG>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kWave, VG>), g, b, lds, s, a);
     } else {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads>), g, b, lds, s, a);
-      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads>), g, b, lds, s, a);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads, VG>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads, VG>), g, b, lds, s, a);
     }
-    if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads>), dim3(ncat, ny), bc, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads>), dim3(ncat, ny), bc, lds, s, a);
+    if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads, VG>), dim3(ncat, ny), bc, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads, VG>), dim3(ncat, ny), bc, lds, s, a);
   } else if (narrow) {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<0, false, kWave>), g, b, lds, s, a);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave, VG>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kWave, VG>), g, b, lds, s, a);
   } else {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads>), g, b, lds, s, a);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads, VG>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads, VG>), g, b, lds, s, a);
   }
+}
+
+void LaunchRoundFind(const KArgs& a, hipStream_t s) {
+  if (a.round_vote && a.p.vote_phase == 2) LaunchRoundFindT<true>(a, s);
+  else LaunchRoundFindT<false>(a, s);
 }
 
 }  // namespace
@@ -1878,6 +1890,7 @@ void PrepareRoundKernels(int max_lds) {
   AllowRoundSplitLds<2>(max_lds);
   AllowRoundSplitLds<4>(max_lds);
   AllowRoundSplitLds<8>(max_lds);
+  AllowRoundSplitLds<2, true>(max_lds);
 }
 
 void RoundRootPlan(const KArgs& a, hipStream_t s) {
@@ -1905,7 +1918,8 @@ void RoundSplitReduce(const KArgs& a, hipStream_t s) {
   if (a.round_fused) {
     const int gr = a.round_gr > 0 ? a.round_gr
                    : ((a.sp_ptr != nullptr || a.tile_words <= kRGatherNarrowMaxWords) ? kRGatherNarrow : kRGatherWide);
-    if (gr >= 8) LaunchRoundSplit<8>(a, s);
+    if (a.round_vote) LaunchRoundSplit<2, true>(a, s);  // (voting: the local sums' variant)
+    else if (gr >= 8) LaunchRoundSplit<8>(a, s);
     else if (gr >= 4) LaunchRoundSplit<4>(a, s);
     else LaunchRoundSplit<2>(a, s);
   } else {

@@ -175,6 +175,10 @@ int LGBM_AMD_RcclSelfTest(int* out_ok) {
     (void)hipMemcpyAsync(hf.data(), df64, cnt * sizeof(double), hipMemcpyDeviceToHost, s);
     (void)hipMemcpyAsync(hu.data(), du32, cnt * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
+    // every rank is past its collectives before anyone frees: hipFree waits for the whole
+    // device, which would include a faster peer's next collective kernel, spinning until this
+    // rank joins it (thread ranks sharing one GPU)
+    dc->HostBarrier();
     (void)hipFree(rs_in);
     (void)hipFree(rs_out);
     (void)hipFree(ag);
@@ -216,6 +220,7 @@ int LGBM_AMD_RcclGraphSelfTest(int* out_ok) {
     for (size_t i = 0; i < cnt; ++i) h[i] = static_cast<long long>(i);
     (void)hipMemcpyAsync(d, h.data(), cnt * sizeof(long long), hipMemcpyHostToDevice, s);
     (void)hipStreamSynchronize(s);
+    dc->HostBarrier();  // (no rank's collectives spin while a peer still allocates)
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) Log::Fatal("begin capture failed");
@@ -228,6 +233,7 @@ int LGBM_AMD_RcclGraphSelfTest(int* out_ok) {
     }
     (void)hipMemcpyAsync(h.data(), d, cnt * sizeof(long long), hipMemcpyDeviceToHost, s);
     (void)hipStreamSynchronize(s);
+    dc->HostBarrier();  // (before the frees below wait for the device)
     long long f = 1;
     for (int k = 0; k < 6; ++k) f *= n;
     bool ok = true;

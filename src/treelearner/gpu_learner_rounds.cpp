@@ -32,6 +32,7 @@ void GPUTreeLearner::AllocRoundState() {
   d_round_ = Alloc<dev::Round>(1);
   d_rnode_ = Alloc<dev::RNode>(split_rows_);
   d_cbest_ = Alloc<dev::FeatureBest>(split_rows_);
+  if (a.round_vote) a.rnode_lsum = Alloc<double>(2 * static_cast<size_t>(split_rows_));  // (voting: local node sums)
   d_cbest_cat_ = Alloc<uint32_t>(static_cast<size_t>(split_rows_) * kMaxCatWords);
   const size_t cnt = 2 * static_cast<size_t>(dev::kMaxRoundExp) * (dev::kFindSub + 1) * dev::kFindSubStride;
   d_child_cnt_ = Alloc<uint32_t>(cnt);

@@ -314,8 +314,11 @@ void GPUTreeLearner::UploadData() {
   // iterations of the headline, profiles/r04_round_width.md: K=8 saves 2 rounds on the first
   // trees for 2 more expansions, later it adds 8-10 unaccepted ones; fixed K 6 / 8 / 10 =
   // 2.040 / 2.072 / 2.132 ms, window of 20 after 5: 2.148 / 2.075)
-  round_k_ = 8;
-  k_adapt_ = true;
+  // (wide data keeps 6: the graphs' split-scan grids are sized for the widest round, features x
+  // 2K workgroups, and the idle ones of a K=6 tree cost more than K=8 saves -- Epsilon, 2000
+  // features: 10.6 vs 11.3 ms/iter)
+  round_k_ = num_features_ <= 256 ? 8 : 6;
+  k_adapt_ = num_features_ <= 256;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) {
     round_k_ = std::atoi(e);
     k_adapt_ = false;
@@ -614,6 +617,7 @@ void GPUTreeLearner::UploadData() {
   a.round_k = round_k_;
   a.round_dist = distributed_ ? 1 : 0;
   a.round_vote = (voting_ && round_k_ > 1) ? 1 : 0;
+  a.rnode_lsum = nullptr;
   a.max_owned = max_owned_;
   a.rs_block = rs_block_;
   a.round_send = nullptr;
