@@ -805,7 +805,7 @@ __device__ void ChildBest(const KArgs& a, int y, int node, RoundFindShared<KIND,
 // expansion's reduced histogram (or sums its few partials itself) into its new slot; the
 // other one subtracts it from the parent's slot in place (exact int64).  Children of an
 // expansion that cannot be split (max_depth, min_data_in_leaf) are not scanned.
-template <int KIND, bool SIMPLE, int NT, bool VG = false>
+template <int KIND, bool SIMPLE, int NT, bool VG = false, bool PIF = true>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave ? LGBM_FIND_WAVE_OCC : 1))) void k_round_find(KArgs a) {
   constexpr bool CAT = KIND >= 2;  // (3: the wide categorical variant)
   extern __shared__ double s_bins[];  // [2][max_feature_bins] dequantised (g, h), if they fit
@@ -1088,7 +1088,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   if (!s_last) return;
   ChildBest<KIND, NT>(a, y, frow, sh);
   if (ktw) kt[5] = wall_clock64();
-  if (!a.plan_in_find) return;
+  // (PIF: an instantiation without the plan when the plan has its own kernel -- the replay's
+  // registers otherwise set the occupancy of every scan workgroup)
+  if (!PIF || !a.plan_in_find) return;
   // the last child of the round to finish plans the next round (its scans' results were
   // published write-through; one agent-scope acquire)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1113,7 +1115,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     for (int k = 0; k < 4; ++k) a.ktrace[static_cast<size_t>(rround) * kTraceSlots + 12 + k] = g_find_phase[k];
 #endif
   }
-  RoundPlanBody<false, NT>(a, reinterpret_cast<unsigned char*>(s_bins));
+  if constexpr (PIF) RoundPlanBody<false, NT>(a, reinterpret_cast<unsigned char*>(s_bins));
 }
 
 // ----------------------------------------------------------------------------- k_round_plan
@@ -1825,7 +1827,7 @@ bool RoundSimpleGains(const KArgs& a) {
   return !p.use_l1 && !p.use_max_output && !p.use_smoothing && !p.use_mc;
 }
 
-template <bool VG>
+template <bool VG, bool PIF>
 void LaunchRoundFindT(const KArgs& a, hipStream_t s) {
   const int ny = 2 * a.round_k;
   size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
@@ -1837,26 +1839,27 @@ void LaunchRoundFindT(const KArgs& a, hipStream_t s) {
   const int ncat = (a.round_vote && a.p.vote_phase == 2) ? a.num_scan : a.p.has_cat;
   if (a.p.has_cat) {
     if (narrow) {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave, VG>), g, b, lds, s, a);
-      else hipLaunchKernelGGL((k_round_find<1, false, kWave, VG>), g, b, lds, s, a);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave, VG, PIF>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kWave, VG, PIF>), g, b, lds, s, a);
     } else {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads, VG>), g, b, lds, s, a);
-      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads, VG>), g, b, lds, s, a);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads, VG, PIF>), g, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads, VG, PIF>), g, b, lds, s, a);
     }
-    if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads, VG>), dim3(ncat, ny), bc, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads, VG>), dim3(ncat, ny), bc, lds, s, a);
+    if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads, VG, PIF>), dim3(ncat, ny), bc, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads, VG, PIF>), dim3(ncat, ny), bc, lds, s, a);
   } else if (narrow) {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave, VG>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<0, false, kWave, VG>), g, b, lds, s, a);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave, VG, PIF>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kWave, VG, PIF>), g, b, lds, s, a);
   } else {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads, VG>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads, VG>), g, b, lds, s, a);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads, VG, PIF>), g, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads, VG, PIF>), g, b, lds, s, a);
   }
 }
 
 void LaunchRoundFind(const KArgs& a, hipStream_t s) {
-  if (a.round_vote && a.p.vote_phase == 2) LaunchRoundFindT<true>(a, s);
-  else LaunchRoundFindT<false>(a, s);
+  if (a.round_vote && a.p.vote_phase == 2) LaunchRoundFindT<true, false>(a, s);
+  else if (a.plan_in_find) LaunchRoundFindT<false, true>(a, s);
+  else LaunchRoundFindT<false, false>(a, s);
 }
 
 }  // namespace
