@@ -314,11 +314,8 @@ void GPUTreeLearner::UploadData() {
   // iterations of the headline, profiles/r04_round_width.md: K=8 saves 2 rounds on the first
   // trees for 2 more expansions, later it adds 8-10 unaccepted ones; fixed K 6 / 8 / 10 =
   // 2.040 / 2.072 / 2.132 ms, window of 20 after 5: 2.148 / 2.075)
-  // (wide data keeps 6: the graphs' split-scan grids are sized for the widest round, features x
-  // 2K workgroups, and the idle ones of a K=6 tree cost more than K=8 saves -- Epsilon, 2000
-  // features: 10.6 vs 11.3 ms/iter)
-  round_k_ = num_features_ <= 256 ? 8 : 6;
-  k_adapt_ = num_features_ <= 256;
+  round_k_ = 8;
+  k_adapt_ = true;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) {
     round_k_ = std::atoi(e);
     k_adapt_ = false;
