@@ -110,8 +110,11 @@ struct SplitExp {
 // range, rights from its back, in the other index buffer), the histogrammed child's rows
 // compacted into an LDS row list and gathered into the tile's LDS histogram, stored as
 // partial kb.  Only column tile 0 writes the partition.
+#ifndef LGBM_SPLIT_WAVES
+#define LGBM_SPLIT_WAVES 1  // waves per SIMD the register budget targets (A/B: 8 = two workgroups per CU)
+#endif
 template <int GPW, int UNITS, int GR, bool VOTE = false>
-__global__ __launch_bounds__(kPartThreads) void k_round_split(KArgs a) {
+__global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(LGBM_SPLIT_WAVES))) void k_round_split(KArgs a) {
   extern __shared__ unsigned long long lds[];  // [UNITS * tile_bins] histogram, then the row list
   __shared__ SplitExp ex[kMaxRoundExp];
   __shared__ uint32_t cat_bits[kMaxRoundExp][kMaxCatWords];
