@@ -628,8 +628,10 @@ void GPUTreeLearner::UploadData() {
   // one workgroup per CU: the split kernel's registers (101-128 VGPRs) allow one 1024-thread
   // workgroup per CU, so a second one per CU ran as a second wave with its tail (A/B at HEAD,
   // 60 iterations: 256 / 384 / 512 / 768 workgroups = 2.11 / 2.30 / 2.18 / 2.21 ms at 10M,
-  // 0.888 / 0.92 / 0.918 / 0.92 at 1.25M; round 3's 512 was chosen with fewer registers)
-  a.round_grid = split_grid_;
+  // 0.888 / 0.92 / 0.918 / 0.92 at 1.25M; round 3's 512 was chosen with fewer registers).
+  // Wide int64 histograms (gpu_use_dp: two words per bin, LDS-bound at one workgroup per CU
+  // either way) balance better over two waves of workgroups: 512 / 256 = 2.78 / 2.84 ms
+  a.round_grid = a.hist_units == 2 ? 2 * split_grid_ : split_grid_;
   a.round_gr = 0;
   a.round_fused = 1;
   // the plan in the split scan's last workgroup while its tables fit the scan's LDS budget
