@@ -131,6 +131,9 @@ def main():
     elapsed = torch_dist.allreduce_max(elapsed)
     sec_per_iter = elapsed / max(1, args.steps)
     diag = {}
+    if iter_log is not None and world > 1:
+        # the native log writer suffixes the rank in distributed runs (src/boosting/gbdt.cpp)
+        iter_log += ".rank%d" % rank
     if iter_log is not None and os.path.exists(iter_log):
         rows = [json.loads(line) for line in open(iter_log)][-args.steps:] if args.steps > 0 else []
         trees = [r for row in rows for r in row.get("rounds", [])]
