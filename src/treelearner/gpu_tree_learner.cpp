@@ -314,8 +314,11 @@ void GPUTreeLearner::UploadData() {
   // iterations of the headline, profiles/r04_round_width.md: K=8 saves 2 rounds on the first
   // trees for 2 more expansions, later it adds 8-10 unaccepted ones; fixed K 6 / 8 / 10 =
   // 2.040 / 2.072 / 2.132 ms, window of 20 after 5: 2.148 / 2.075)
+  // Below 4M rows per rank the width stays 8: a round there is latency-bound and the extra
+  // speculation is nearly free (r04_round_width.md: 1.25M / 2.5M rows 0.929 / 1.106 ms fixed
+  // vs 0.943 / 1.120 adaptive; Epsilon 8.28 vs 8.44 ms, Bosch / LTR shapes equal)
   round_k_ = 8;
-  k_adapt_ = true;
+  k_adapt_ = num_data_ >= 4000000;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) {
     round_k_ = std::atoi(e);
     k_adapt_ = false;
