@@ -166,14 +166,17 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
   return true;
 }
 
-// rounds of kRoundSeg expansions per graph launch: one root graph (the root + as many
-// segments as the recent trees needed, one cached graph per segment count) is launched; the
-// host then checks the Round record and adds segment graphs until the tree is done (a finished
-// tree's kernels exit at once: an over-provisioned round costs ~12 us, a missing one a host
-// round trip of ~60 us and a graph launch of ~8 us per segment)
+// One root graph (the root + a number of rounds, one cached graph per count) and segment graphs
+// of round_seg_ rounds are enqueued up to the provisioned count (the most rounds of the recent
+// trees + margin); the host then checks the Round record and adds segments until the tree is
+// done (a finished tree's kernels exit at once: an over-provisioned round costs ~12 us, a
+// missing one a host round trip and a graph launch per segment)
 namespace {
-constexpr int kRoundSeg = 4;
 constexpr int kRoundFirstPred = 16;  // rounds enqueued for the first tree
+int EnvInt(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e != nullptr ? std::atoi(e) : dflt;
+}
 }
 
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
@@ -217,27 +220,36 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     return true;
   };
   const int L = config_->num_leaves;
-  // segments of the root graph: the most rounds of the last trees (+1), rounded up
+  static const int env_hist = EnvInt("LGBM_AMD_ROUND_HIST", 0), env_margin = EnvInt("LGBM_AMD_ROUND_MARGIN", -99),
+                   env_seg = EnvInt("LGBM_AMD_ROUND_SEG", 0), env_root = EnvInt("LGBM_AMD_ROUND_ROOT", -1);
+  if (env_hist > 0) round_hist_n_ = static_cast<size_t>(env_hist);
+  if (env_margin > -99) round_margin_ = env_margin;
+  if (env_seg > 0) round_seg_ = env_seg;
+  if (env_root >= 0) round_root_fixed_ = env_root;
+  const int seg = round_seg_;
+  // rounds to enqueue: the most rounds of the last trees (+ margin)
   int want = kRoundFirstPred;
-  if (!round_hist_.empty()) want = *std::max_element(round_hist_.begin(), round_hist_.end()) + 1;
+  if (!round_hist_.empty()) want = *std::max_element(round_hist_.begin(), round_hist_.end()) + round_margin_;
   want = std::max(1, std::min(want, L - 1));
-  const int nseg = (want + kRoundSeg - 1) / kRoundSeg;
+  // the root graph: a fixed number of rounds, or the provisioned count rounded up to segments;
+  // segment graphs make up the rest before the host first looks at the Round record
+  const int root_rounds = round_root_fixed_ > 0 ? std::min(round_root_fixed_, want) : seg * ((want + seg - 1) / seg);
   bool graph = use_graph;
   if (graph && (round_seg_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
                 round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
     if (dc != nullptr) dc->HostBarrier();
     DestroyRoundGraphs();
-    graph = capture(&round_seg_exec_, false, kRoundSeg);
+    graph = capture(&round_seg_exec_, false, seg);
     if (!graph) DestroyRoundGraphs();
     round_graph_rows_ = a.num_rows;
     round_graph_identity_ = a.root_identity;
     round_graph_root_mode_ = root_mode;
   }
   if (graph) {
-    if (static_cast<int>(round_root_execs_.size()) <= nseg) round_root_execs_.resize(nseg + 1, nullptr);
-    if (round_root_execs_[nseg] == nullptr) {
+    if (static_cast<int>(round_root_execs_.size()) <= root_rounds) round_root_execs_.resize(root_rounds + 1, nullptr);
+    if (round_root_execs_[root_rounds] == nullptr) {
       if (dc != nullptr) dc->HostBarrier();
-      graph = capture(&round_root_execs_[nseg], true, nseg * kRoundSeg);
+      graph = capture(&round_root_execs_[root_rounds], true, root_rounds);
       if (!graph) DestroyRoundGraphs();
     }
   }
@@ -246,28 +258,32 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     if (graph) {
       HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
     } else {
-      for (int r = 0; r < kRoundSeg; ++r) EnqueueRound(a);
+      for (int r = 0; r < seg; ++r) EnqueueRound(a);
     }
   };
   if (graph) {
-    HIPCHECK(hipGraphLaunch(round_root_execs_[nseg], stream_));
+    HIPCHECK(hipGraphLaunch(round_root_execs_[root_rounds], stream_));
   } else {
     EnqueueRoot(a);
-    for (int r = 0; r < nseg * kRoundSeg; ++r) EnqueueRound(a);
+    for (int r = 0; r < root_rounds; ++r) EnqueueRound(a);
   }
-  int launched = nseg * kRoundSeg;
+  int launched = root_rounds;
+  while (launched < want) {  // (asynchronous: enqueued while the root graph runs)
+    launch_seg();
+    launched += seg;
+  }
   const size_t rec_bytes = sizeof(dev::SplitRecord) * std::max(1, L - 1);
   for (;;) {
     HIPCHECK(hipMemcpyAsync(h_round_, d_round_, sizeof(dev::Round), hipMemcpyDeviceToHost, stream_));
     HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, rec_bytes, hipMemcpyDeviceToHost, stream_));
     WatchdogSync();
     if (h_round_->done) break;
-    if (launched > 2 * L + kRoundSeg) {
+    if (launched > 2 * L + seg) {
       Log::Fatal("device learner: round growth did not finish the tree after %d rounds (%d splits)", launched,
                  h_round_->nsplit);
     }
     launch_seg();
-    launched += kRoundSeg;
+    launched += seg;
   }
   if (a.ktrace != nullptr) {
     std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
@@ -306,9 +322,9 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
       std::fprintf(stderr, "%s%s\n", line.c_str(), buf);
     }
   }
-  // the next tree enqueues the most rounds of the last kRoundHist trees (+1)
+  // the next tree enqueues the most rounds of the last round_hist_n_ trees (+ margin)
   round_hist_.push_back(h_round_->rounds);
-  if (round_hist_.size() > kRoundHist) round_hist_.erase(round_hist_.begin());
+  while (round_hist_.size() > round_hist_n_) round_hist_.erase(round_hist_.begin());
   last_stats_.rounds = h_round_->rounds;
   last_stats_.expansions = (h_round_->next_frow - 1) / 2;
   prev_expansions_ = last_stats_.expansions;

@@ -156,11 +156,14 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   dev::FeatureBest* d_cbest_ = nullptr;
   uint32_t* d_cbest_cat_ = nullptr;
   uint32_t* d_child_cnt_ = nullptr;
-  std::vector<hipGraphExec_t> round_root_execs_;  // [n]: root + n * kRoundSeg rounds (captured on first use)
-  hipGraphExec_t round_seg_exec_ = nullptr;        // kRoundSeg rounds
+  std::vector<hipGraphExec_t> round_root_execs_;  // [n]: root + n rounds (captured on first use)
+  hipGraphExec_t round_seg_exec_ = nullptr;        // round_seg_ rounds
   int round_graph_rows_ = -1, round_graph_identity_ = -1, round_graph_root_mode_ = -1;
-  static constexpr size_t kRoundHist = 3;
-  std::vector<int> round_hist_;  // rounds of the last kRoundHist trees (the next one enqueues their max + 1)
+  // provisioning of the enqueued rounds (RunRounds): history length, margin, rounds per segment
+  // graph, rounds in the root graph (0: the provisioned count rounded up to segments)
+  size_t round_hist_n_ = 3;
+  int round_margin_ = 0, round_seg_ = 4, round_root_fixed_ = 0;
+  std::vector<int> round_hist_;  // rounds of the last round_hist_n_ trees (the next one enqueues their max + margin)
   bool last_tree_rounds_ = false;
   // per-tree round width (LGBM_AMD_ROUND_K unset): the last round tree's speculation outcome
   bool k_adapt_ = false;
