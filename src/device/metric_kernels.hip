@@ -138,14 +138,6 @@ __global__ __launch_bounds__(kMetricThreads) void k_sum_partials(const double* p
   if (threadIdx.x == 0) out[slot] = acc;
 }
 
-__global__ __launch_bounds__(kMetricThreads) void k_auc_keys(MetricArgs m, double* keys, int32_t* idx) {
-  for (int64_t i = blockIdx.x * static_cast<int64_t>(kMetricThreads) + threadIdx.x; i < m.n;
-       i += static_cast<int64_t>(gridDim.x) * kMetricThreads) {
-    keys[i] = m.score[i];
-    idx[i] = static_cast<int32_t>(i);
-  }
-}
-
 struct PosNeg {
   double pos, neg;
 };
@@ -155,13 +147,22 @@ struct PosNegSum {
   }
 };
 
-__global__ __launch_bounds__(kMetricThreads) void k_auc_weights(MetricArgs m, const int32_t* idx, PosNeg* pn) {
-  for (int64_t k = blockIdx.x * static_cast<int64_t>(kMetricThreads) + threadIdx.x; k < m.n;
+// AUC: each row's weight with its class in the sign (negative rows -w; w = 0 either way adds
+// nothing), sorted along with the scores, so the (positive, negative) pairs are read in order
+// instead of gathered through a sorted row index
+__global__ __launch_bounds__(kMetricThreads) void k_auc_signed(MetricArgs m, float* v) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(kMetricThreads) + threadIdx.x; i < m.n;
+       i += static_cast<int64_t>(gridDim.x) * kMetricThreads) {
+    const float w = m.weights ? static_cast<float>(m.weights[i]) : 1.0f;
+    v[i] = m.label[i] > 0 ? w : -w;
+  }
+}
+
+__global__ __launch_bounds__(kMetricThreads) void k_auc_unsign(const float* v, int64_t n, PosNeg* pn) {
+  for (int64_t k = blockIdx.x * static_cast<int64_t>(kMetricThreads) + threadIdx.x; k < n;
        k += static_cast<int64_t>(gridDim.x) * kMetricThreads) {
-    const int32_t i = idx[k];
-    const double w = m.weights ? m.weights[i] : 1.0;
-    const bool pos = m.label[i] > 0;
-    pn[k] = PosNeg{pos ? w : 0.0, pos ? 0.0 : w};
+    const float x = v[k];
+    pn[k] = signbit(x) ? PosNeg{0.0, static_cast<double>(-x)} : PosNeg{static_cast<double>(x), 0.0};
   }
 }
 
@@ -314,7 +315,11 @@ size_t CubTempBytes(int64_t n) {
                                           static_cast<int*>(nullptr), PosNegSum(), nn);
   (void)hipcub::DeviceScan::ExclusiveSum(nullptr, c, static_cast<double*>(nullptr), static_cast<double*>(nullptr),
                                          nn);
-  return std::max(a, std::max(b, c));
+  size_t d = 0;
+  (void)hipcub::DeviceRadixSort::SortPairsDescending(nullptr, d, static_cast<const double*>(nullptr),
+                                                     static_cast<double*>(nullptr), static_cast<float*>(nullptr),
+                                                     static_cast<float*>(nullptr), nn);
+  return std::max(std::max(a, d), std::max(b, c));
 }
 
 }  // namespace
@@ -362,15 +367,18 @@ void EvalMetric(const MetricArgs& m, hipStream_t s) {
     size_t tb = temp_bytes;
     if (m.kind == kMetricAucMu) {
       hipLaunchKernelGGL(k_aucmu_keys, dim3(blocks), dim3(kMetricThreads), 0, s, m, ci, cj, keys, idx);
-    } else {
-      hipLaunchKernelGGL(k_auc_keys, dim3(blocks), dim3(kMetricThreads), 0, s, m, keys, idx);
-    }
-    (void)hipcub::DeviceRadixSort::SortPairsDescending(temp, tb, keys, keys_sorted, idx, idx_sorted, nn, 0,
-                                                       sizeof(double) * 8, s);
-    if (m.kind == kMetricAucMu) {
+      (void)hipcub::DeviceRadixSort::SortPairsDescending(temp, tb, keys, keys_sorted, idx, idx_sorted, nn, 0,
+                                                         sizeof(double) * 8, s);
       hipLaunchKernelGGL(k_aucmu_weights, dim3(blocks), dim3(kMetricThreads), 0, s, m, ci, cj, idx_sorted, pn);
     } else {
-      hipLaunchKernelGGL(k_auc_weights, dim3(blocks), dim3(kMetricThreads), 0, s, m, idx_sorted, pn);
+      // the scores sorted in place of a copy, the signed weights as the values (stable: ties
+      // keep the row order, as the row-index sort did)
+      float* sv = reinterpret_cast<float*>(idx);
+      float* sv_sorted = reinterpret_cast<float*>(idx_sorted);
+      hipLaunchKernelGGL(k_auc_signed, dim3(blocks), dim3(kMetricThreads), 0, s, m, sv);
+      (void)hipcub::DeviceRadixSort::SortPairsDescending(temp, tb, m.score, keys_sorted, sv, sv_sorted, nn, 0,
+                                                         sizeof(double) * 8, s);
+      hipLaunchKernelGGL(k_auc_unsign, dim3(blocks), dim3(kMetricThreads), 0, s, sv_sorted, m.n, pn);
     }
     tb = temp_bytes;
     (void)hipcub::DeviceReduce::ReduceByKey(temp, tb, keys_sorted, uniq, pn, agg, num_runs, PosNegSum(), nn, s);

@@ -660,7 +660,7 @@ def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, cap
         np.testing.assert_allclose(dev[name], host[name], rtol=1e-9, atol=1e-12, err_msg=name)
 
 
-@pytest.mark.parametrize("task", ["binary", "lambdarank", "multiclass", "regression_family"])
+@pytest.mark.parametrize("task", ["binary", "binary_weighted", "lambdarank", "multiclass", "regression_family"])
 def test_training_metrics_on_device(task, gpu_available, monkeypatch, capfd):
     """Training-set metrics (valid_sets=[dtrain]: reference gbdt.cpp:484-542) are reduced on the
     device-resident training scores, equal to the host evaluation of the downloaded scores."""
@@ -668,11 +668,14 @@ def test_training_metrics_on_device(task, gpu_available, monkeypatch, capfd):
     n = 12000
     X = rng.randn(n, 8)
     group = None
-    if task == "binary":
+    weight = None
+    if task.startswith("binary"):
         y = (X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.3 * rng.randn(n) > 0).astype(float)
         params = {"objective": "binary", "metric": ["auc", "binary_logloss", "binary_error"],
                   "bagging_fraction": 0.7, "bagging_freq": 1}
         kinds = (6, 4, 5)
+        if task == "binary_weighted":  # (AUC sorts signed weights: zero weights of both classes included)
+            weight = rng.choice([0.0, 0.5, 1.0, 2.5], size=n)
     elif task == "lambdarank":
         y = np.clip(np.round(X[:, 0] + X[:, 1] + rng.randn(n)), 0, 4)
         group = [40] * (n // 40)
@@ -689,7 +692,7 @@ def test_training_metrics_on_device(task, gpu_available, monkeypatch, capfd):
     params.update({"verbose": -1, "device_type": "gpu", "num_leaves": 15, "seed": 1})
 
     def run():
-        ds = lgb.Dataset(X, y, group=group, params=params)
+        ds = lgb.Dataset(X, y, group=group, weight=weight, params=params)
         res = {}
         lgb.train(params, ds, 5, valid_sets=[ds], valid_names=["train"], evals_result=res, verbose_eval=False)
         return res["train"]
