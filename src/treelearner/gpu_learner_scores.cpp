@@ -137,33 +137,7 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
   m.num_class = spec.num_class;
   m.top_k = spec.top_k;
   m.out = vs.metric_out;
-  if (spec.kind == dev::kMetricAUC && !metric_graph_failed_ && std::getenv("LGBM_AMD_NO_GRAPH") == nullptr) {
-    MetricGraph* mg = nullptr;
-    for (MetricGraph& g : metric_graphs_) {
-      if (g.score == m.score && g.n == m.n && g.scratch == m.scratch && g.out == m.out) mg = &g;
-    }
-    if (mg == nullptr) {
-      hipGraph_t g = nullptr;
-      hipGraphExec_t exec = nullptr;
-      HIPCHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-      dev::EvalMetric(m, stream_);
-      hipError_t ec = hipStreamEndCapture(stream_, &g);
-      if (ec == hipSuccess) ec = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
-      if (g != nullptr) (void)hipGraphDestroy(g);
-      if (ec == hipSuccess) {
-        metric_graphs_.push_back(MetricGraph{m.score, m.n, m.scratch, m.out, exec});
-        mg = &metric_graphs_.back();
-      } else {
-        (void)hipGetLastError();
-        metric_graph_failed_ = true;
-        Log::Debug("device metric: capturing the AUC evaluation failed (%s); launching it eagerly", hipGetErrorString(ec));
-      }
-    }
-    if (mg != nullptr) HIPCHECK(hipGraphLaunch(mg->exec, stream_));
-    else dev::EvalMetric(m, stream_);
-  } else {
-    dev::EvalMetric(m, stream_);
-  }
+  dev::EvalMetric(m, stream_);
   if (vs.logged_kinds.insert(spec.kind).second) {
     if (slot == train_eval_slot_) Log::Debug("device metric (kind %d) on the training set", spec.kind);
     else Log::Debug("device metric (kind %d) on validation set %d", spec.kind, slot);

@@ -1000,12 +1000,6 @@ void GPUTreeLearner::ReportKernelTrace(int num_splits) {
 void GPUTreeLearner::DestroyGraph() {
   DestroyStepGraph();
   DestroyRoundGraphs();
-  DestroyMetricGraphs();
-}
-
-void GPUTreeLearner::DestroyMetricGraphs() {
-  for (MetricGraph& g : metric_graphs_) (void)hipGraphExecDestroy(g.exec);
-  metric_graphs_.clear();
 }
 
 void GPUTreeLearner::DestroyStepGraph() {

@@ -392,18 +392,6 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
     std::set<int> logged_kinds;  // metric kinds evaluated here so far (debug log)
   };
   std::vector<ValidSet> valid_;
-  // AUC evaluations (a dozen sort / scan / reduce launches and their memsets) replayed as one
-  // graph per (scores, rows, scratch, output)
-  struct MetricGraph {
-    const void* score;
-    int64_t n;
-    const void* scratch;
-    const void* out;
-    hipGraphExec_t exec;
-  };
-  std::vector<MetricGraph> metric_graphs_;
-  bool metric_graph_failed_ = false;
-  void DestroyMetricGraphs();
   int train_eval_slot_ = -1;  // valid_ entry over the training scores (d_score_; no bins)
   std::vector<void*> valid_allocs_;
   // tree upload for the score traversal: one blob (node arrays, category sets, leaf values)

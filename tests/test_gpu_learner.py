@@ -920,3 +920,34 @@ def test_host_sparse_groups_device_learner(rows_layout, gpu_available, monkeypat
 
     dense = run("0")
     assert run("1") == dense
+
+
+@pytest.mark.parametrize("variants", [2, 8])
+def test_training_auc_with_float_colliding_scores(variants, gpu_available, monkeypatch):
+    """The device AUC sorts float32 keys: scores that differ as doubles but round to the same
+    float are ordered exactly by the pairwise correction (pairs: runs of 2) or, for long runs of
+    such scores, by the 64-bit sort (8 variants of each base score across a whole leaf)."""
+    rng = np.random.RandomState(11)
+    n = 20000
+    X = rng.randn(n, 6)
+    y = (X[:, 0] + 0.7 * rng.randn(n) > 0).astype(float)
+    if variants == 2:
+        base = rng.randn(n // 2).astype(np.float32).astype(np.float64)
+        init = np.concatenate([base, base * (1.0 + 2.0 ** -45)])
+        X[n // 2:] = X[:n // 2]  # (the pair's rows take the same leaves)
+        y[n // 2:] = 1.0 - y[:n // 2]
+    else:
+        init = 0.25 + rng.randint(0, variants, size=n) * 2.0 ** -44
+    params = {"objective": "binary", "metric": "auc", "device_type": "gpu", "num_leaves": 7, "seed": 1,
+              "learning_rate": 0.05, "verbose": -1}
+
+    def run():
+        ds = lgb.Dataset(X, y, init_score=init, params=params)
+        res = {}
+        lgb.train(params, ds, 2, valid_sets=[ds], valid_names=["train"], evals_result=res, verbose_eval=False)
+        return res["train"]["auc"]
+
+    dev = run()
+    monkeypatch.setenv("LGBM_AMD_HOST_METRICS", "1")
+    host = run()
+    np.testing.assert_allclose(dev, host, rtol=1e-12, atol=0)
