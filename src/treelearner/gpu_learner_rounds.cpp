@@ -181,6 +181,15 @@ int EnvInt(const char* name, int dflt) {
 
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
   a.rd = d_round_;
+  if (k_adapt_ && !k_adapt_checked_) {
+    k_adapt_checked_ = true;
+    double rows = static_cast<double>(num_data_);
+    if (distributed_ && Network::num_machines() > 1) {
+      std::vector<double> v{rows};
+      rows = Network::GlobalSum(v)[0] / Network::num_machines();
+    }
+    k_adapt_ = rows >= 4e6;
+  }
   if (k_adapt_) {
     // this tree's round width (Round::k_cur: the captured graphs are sized for round_k_)
     k_cur_host_ = (prev_splits_ <= 0 || prev_expansions_ <= prev_splits_ + 2) ? round_k_ : std::min(round_k_, 6);

@@ -317,8 +317,11 @@ void GPUTreeLearner::UploadData() {
   // Below 4M rows per rank the width stays 8: a round there is latency-bound and the extra
   // speculation is nearly free (r04_round_width.md: 1.25M / 2.5M rows 0.929 / 1.106 ms fixed
   // vs 0.943 / 1.120 adaptive; Epsilon 8.28 vs 8.44 ms, Bosch / LTR shapes equal)
+  // (the rows per rank are averaged over the ranks at the first tree, RunRounds: every rank
+  // must plan with the same width)
   round_k_ = 8;
-  k_adapt_ = num_data_ >= 4000000;
+  k_adapt_ = true;
+  k_adapt_checked_ = false;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) {
     round_k_ = std::atoi(e);
     k_adapt_ = false;

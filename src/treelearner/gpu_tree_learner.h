@@ -167,6 +167,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool last_tree_rounds_ = false;
   // per-tree round width (LGBM_AMD_ROUND_K unset): the last round tree's speculation outcome
   bool k_adapt_ = false;
+  bool k_adapt_checked_ = false;  // (the 4M rows-per-rank threshold, applied at the first tree)
   int32_t k_cur_host_ = 0;
   int prev_expansions_ = 0, prev_splits_ = 0;
   // round growth vs one split per step, chosen by timing (AutoGrowthRounds)
