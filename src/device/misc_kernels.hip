@@ -12,7 +12,13 @@ int g_num_cus = 256;
 int NumCUs() { return g_num_cus; }
 
 void SetNumCUs(int n) { g_num_cus = n > 0 ? n : 256; }
-int HistGridBlocks() { return 2 * g_num_cus; }
+int HistGridBlocks() {
+  static const int per_cu = [] {  // LGBM_AMD_ROOT_WG_PER_CU (A/B knob; default 2)
+    const char* e = std::getenv("LGBM_AMD_ROOT_WG_PER_CU");
+    return e != nullptr && std::atoi(e) > 0 ? std::atoi(e) : 2;
+  }();
+  return per_cu * g_num_cus;
+}
 
 // ---------------------------------------------------------------- gradient packing
 // (g, h) interleaved so a gathered row costs one 8-byte load; also the per-workgroup max|g|
