@@ -54,8 +54,13 @@ class Metadata {
   int64_t num_init_score() const { return static_cast<int64_t>(init_score_.size()); }
   std::vector<label_t>& mutable_label() { return label_; }
 
-  void SaveBinary(std::string* out) const;
+  void SaveBinary(std::string* out) const;  // (private V2 dataset files: still read)
   const char* LoadBinary(const char* p);
+  // the reference's metadata block (metadata.cpp:471-531): num_data, num_weights, num_queries
+  // (int32), labels, weights, query boundaries; init scores are not part of it
+  size_t ReferenceBinarySize() const;
+  void SaveReferenceBinary(std::string* out) const;
+  void LoadReferenceBinary(const char* p, size_t size);
 
  private:
   void ComputeQueryWeights();
@@ -267,8 +272,16 @@ class Dataset {
   void FixHistogram(int inner, double sum_grad, double sum_hess, hist_t* feature_hist) const;
 
   // --- persistence ----------------------------------------------------------------
+  // Dataset binary files in the reference's format (src/io/dataset.cpp:890-992, read as
+  // dataset_loader.cpp:273-525; src/io/dataset_binary.cpp): token, header, metadata, then one
+  // block per feature group.  Files written here load in the reference and vice versa.
   void SaveBinaryFile(const std::string& path) const;
-  static std::unique_ptr<Dataset> LoadBinaryFile(const std::string& path);
+  // rank / num_machines / partition: keep this rank's rows (or whole queries) as the reference
+  // does for a binary file under distributed training without pre_partition (Random(seed)
+  // NextShort(0, num_machines) == rank per row / query); *used gets the kept global rows
+  static std::unique_ptr<Dataset> LoadBinaryFile(const std::string& path, int rank = 0, int num_machines = 1,
+                                                 bool partition = false, int seed = 0,
+                                                 std::vector<data_size_t>* used = nullptr);
   static bool IsBinaryFile(const std::string& path);
   void DumpText(const std::string& path) const;
 
@@ -282,6 +295,10 @@ class Dataset {
 
  private:
   void BuildGroups(const std::vector<std::vector<int>>& features_in_group);
+  FeatureGroup NewGroup(const std::vector<int>& inner_features);  // offsets, width, storage
+  static std::unique_ptr<Dataset> LoadPrivateBinary(const std::string& path);
+  static std::unique_ptr<Dataset> LoadReferenceBinary(const std::string& path, int rank, int num_machines,
+                                                      bool partition, int seed, std::vector<data_size_t>* used);
   void ConstructHistogramsRowWise(const std::vector<int8_t>& group_used, const data_size_t* indices, data_size_t n,
                                   const score_t* grad, const score_t* hess, hist_t* hist, RowWiseScratch* scratch) const;
   void BuildRowMajor() const;
@@ -318,6 +335,17 @@ class Dataset {
   std::vector<std::string> feature_names_;
   std::vector<std::vector<double>> forced_bin_bounds_;
   int max_bin_ = 255;
+  // dataset parameters the binary file records (reference dataset.h:676-692)
+  int bin_construct_sample_cnt_ = 200000;
+  int min_data_in_bin_ = 3;
+  bool use_missing_ = true;
+  bool zero_as_missing_ = false;
+  std::vector<int32_t> max_bin_by_feature_;
+  // per group: the reference multi-value group (EFB's second-round bundle of sparse leftovers,
+  // reference feature_group.h:352-377) it was expanded from -- consecutive groups with one id
+  // -- or -1.  Multi-value groups are stored here as singleton groups; the binary file writes
+  // them back as the reference's one multi-value group.
+  std::vector<int> group_mv_;
   Metadata metadata_;
 };
 

@@ -149,6 +149,15 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpMetric(const char* params, const float* label, c
     if (obj) obj->Init(md, n);
     const DeviceMetricSpec spec = m->DeviceSpec(obj.get());
     if (spec.kind == 0) Log::Fatal("op metric: '%s' has no device kernel for this objective", c.metric[0].c_str());
+    bool negative_weight = false;
+    for (int32_t i = 0; weight != nullptr && i < n && !negative_weight; ++i) negative_weight = weight[i] < 0.0f;
+    if (spec.kind == dev::kMetricAUC && negative_weight) {
+      // the device AUC carries the class in the weight's sign: evaluate these rows on the host
+      std::vector<double> hs(static_cast<size_t>(std::max(0, n)));
+      OPCHECK(hipMemcpy(hs.data(), d_score, sizeof(double) * hs.size(), hipMemcpyDeviceToHost));
+      *out = m->Eval(hs.data(), obj.get())[0];
+      return;
+    }
     Scratch sc;
     dev::MetricArgs a;
     std::memset(&a, 0, sizeof(a));

@@ -404,17 +404,19 @@ std::string BinMapper::bin_info_string() const {
 
 // layout: num_bin i32 | missing i8 | trivial u8 | sparse f64 | type i8 | min f64 | max f64 | default u32 |
 //         most_freq u32 | bounds f64[num_bin] or cats i32[num_bin]
+// the reference's layout (bin.cpp:562-620: enums as 4-byte ints, bool as one byte, no padding),
+// shared by the distributed bin-mapper exchange and the dataset binary file
 size_t BinMapper::SizesInByte() const {
-  size_t s = 4 + 1 + 1 + 8 + 1 + 8 + 8 + 4 + 4;
+  size_t s = 4 + 4 + 1 + 8 + 4 + 8 + 8 + 4 + 4;
   s += bin_type_ == BinType::Numerical ? 8 * num_bin_ : 4 * num_bin_;
   return s;
 }
 
 void BinMapper::CopyTo(char* b) const {
   auto put = [&b](const void* p, size_t n) { std::memcpy(b, p, n); b += n; };
-  int8_t mt = static_cast<int8_t>(missing_type_), bt = static_cast<int8_t>(bin_type_);
-  uint8_t tr = is_trivial_ ? 1 : 0;
-  put(&num_bin_, 4); put(&mt, 1); put(&tr, 1); put(&sparse_rate_, 8); put(&bt, 1);
+  const int32_t mt = static_cast<int32_t>(missing_type_), bt = static_cast<int32_t>(bin_type_);
+  const uint8_t tr = is_trivial_ ? 1 : 0;
+  put(&num_bin_, 4); put(&mt, 4); put(&tr, 1); put(&sparse_rate_, 8); put(&bt, 4);
   put(&min_val_, 8); put(&max_val_, 8); put(&default_bin_, 4); put(&most_freq_bin_, 4);
   if (bin_type_ == BinType::Numerical) put(bin_upper_bound_.data(), 8 * num_bin_);
   else put(bin_2_categorical_.data(), 4 * num_bin_);
@@ -422,16 +424,18 @@ void BinMapper::CopyTo(char* b) const {
 
 void BinMapper::CopyFrom(const char* b) {
   auto get = [&b](void* p, size_t n) { std::memcpy(p, b, n); b += n; };
-  int8_t mt, bt;
+  int32_t mt, bt;
   uint8_t tr;
-  get(&num_bin_, 4); get(&mt, 1); get(&tr, 1); get(&sparse_rate_, 8); get(&bt, 1);
+  get(&num_bin_, 4); get(&mt, 4); get(&tr, 1); get(&sparse_rate_, 8); get(&bt, 4);
   get(&min_val_, 8); get(&max_val_, 8); get(&default_bin_, 4); get(&most_freq_bin_, 4);
+  if (mt < 0 || mt > 2 || bt < 0 || bt > 1 || num_bin_ < 0) Log::Fatal("Binary file error: corrupt bin mapper");
   missing_type_ = static_cast<MissingType>(mt);
   bin_type_ = static_cast<BinType>(bt);
   is_trivial_ = tr != 0;
   if (bin_type_ == BinType::Numerical) {
     bin_upper_bound_.resize(num_bin_);
     get(bin_upper_bound_.data(), 8 * num_bin_);
+    bin_2_categorical_.clear();
   } else {
     bin_2_categorical_.resize(num_bin_);
     get(bin_2_categorical_.data(), 4 * num_bin_);

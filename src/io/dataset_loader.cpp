@@ -386,14 +386,15 @@ std::unique_ptr<Dataset> DatasetLoader::LoadTwoRound(const std::string& filename
 }
 
 std::unique_ptr<Dataset> DatasetLoader::LoadFromFile(const std::string& filename) {
-  if (Dataset::IsBinaryFile(filename)) {
-    Log::Info("Load from binary file %s", filename.c_str());
-    return Dataset::LoadBinaryFile(filename);
-  }
-  std::string bin_path = filename + ".bin";
-  if (Dataset::IsBinaryFile(bin_path)) {
-    Log::Info("Load from binary file %s", bin_path.c_str());
-    return Dataset::LoadBinaryFile(bin_path);
+  // a dataset binary file -- <data>.bin first, then the file itself (reference
+  // dataset_loader.cpp:1171-1195); under distributed training without pre_partition each rank
+  // keeps its random share of the rows (:414-456)
+  for (const std::string& bin_path : {filename + ".bin", filename}) {
+    if (Dataset::IsBinaryFile(bin_path)) {
+      Log::Info("Load from binary file %s", bin_path.c_str());
+      const bool partition = num_machines_ > 1 && !cfg_.pre_partition;
+      return Dataset::LoadBinaryFile(bin_path, rank_, num_machines_, partition, cfg_.data_random_seed);
+    }
   }
   std::vector<std::string> header_names;
   if (cfg_.header) {

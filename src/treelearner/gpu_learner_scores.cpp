@@ -74,12 +74,22 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
     if (bytes > 0) HIPCHECK(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice));
     return d;
   };
-  if (vs.label == nullptr) {
+  if (vs.label == nullptr || vs.label_src != spec.label || vs.weights_src != spec.weights) {
+    if (vs.label != nullptr) ReleaseValidInputs(&vs);  // (the set's fields were replaced)
     vs.label = static_cast<float*>(upload(spec.label, sizeof(float) * n));
     if (spec.weights != nullptr) vs.weights = static_cast<float*>(upload(spec.weights, sizeof(float) * n));
+    vs.label_src = spec.label;
+    vs.weights_src = spec.weights;
+    vs.negative_weights = false;
+    if (spec.weights != nullptr) {
+      for (size_t i = 0; i < n && !vs.negative_weights; ++i) vs.negative_weights = spec.weights[i] < 0.0f;
+    }
     vs.metric_out = static_cast<double*>(dev_alloc(sizeof(double) * 64));
   }
   if (spec.nout > 64) return false;
+  // the device AUC sorts each row's weight with its class in the sign: a negative weight would
+  // flip the class (the reference binary_metric.hpp:240-241 adds it to the row's own class)
+  if (spec.kind == dev::kMetricAUC && vs.negative_weights) return false;
   dev::MetricArgs m;
   std::memset(&m, 0, sizeof(m));
   if (query) {
@@ -155,14 +165,45 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
 bool GPUTreeLearner::TrainEval(const DeviceMetricSpec& spec, std::vector<double>* sums) {
   if (d_score_ == nullptr || num_data_ <= 0) return false;
   if (train_eval_slot_ < 0) {
-    ValidSet vs;
+    valid_.emplace_back();
+    train_eval_slot_ = static_cast<int>(valid_.size()) - 1;
+  }
+  ValidSet& vs = valid_[train_eval_slot_];
+  if (vs.score != d_score_ || vs.num_data != num_data_ || vs.ntpi != num_tree_per_iteration_) {
+    // the training data was reset (ResetTrainingData re-allocates the scores): the slot's
+    // inputs describe the old rows
+    ReleaseValidInputs(&vs);
     vs.num_data = num_data_;
     vs.ntpi = num_tree_per_iteration_;
     vs.score = d_score_;  // (not owned: valid_allocs_ holds only the metric inputs)
-    valid_.push_back(vs);
-    train_eval_slot_ = static_cast<int>(valid_.size()) - 1;
   }
   return ValidEval(train_eval_slot_, spec, sums);
+}
+
+void GPUTreeLearner::ReleaseValidInputs(ValidSet* vs) {
+  std::vector<void*> dead = {vs->label, vs->weights, vs->metric_scratch, vs->metric_out};
+  for (const auto& kv : vs->queries) {
+    const ValidSet::QueryInputs& q = kv.second;
+    for (void* p : {static_cast<void*>(q.qb), static_cast<void*>(q.qw), static_cast<void*>(q.eval_at),
+                    static_cast<void*>(q.qconst), static_cast<void*>(q.label_gain), static_cast<void*>(q.discount),
+                    q.scratch}) {
+      dead.push_back(p);
+    }
+  }
+  HIPCHECK(hipStreamSynchronize(stream_));
+  for (void* p : dead) {
+    if (p == nullptr) continue;
+    auto it = std::find(valid_allocs_.begin(), valid_allocs_.end(), p);
+    if (it != valid_allocs_.end()) valid_allocs_.erase(it);
+    HIPCHECK(hipFree(p));
+  }
+  vs->label = vs->weights = nullptr;
+  vs->label_src = vs->weights_src = nullptr;
+  vs->negative_weights = false;
+  vs->metric_scratch = nullptr;
+  vs->metric_scratch_rows = 0;
+  vs->metric_out = nullptr;
+  vs->queries.clear();
 }
 
 void GPUTreeLearner::ValidScoreToHost(int slot, double* host) {

@@ -694,8 +694,14 @@ void GPUTreeLearner::ResetTrainingData(const Dataset* train_data, bool is_consta
   // rebuild the device data for the new rows (bin mappers are aligned)
   HIPCHECK(hipStreamSynchronize(stream_));
   FreeBuffers();
-  UploadData();
+  UploadData();  // (re-decides the round width for the new rows per rank)
   oob_cnt_ = 0;
+  // the growth-mode timing and the width history belong to the old rows (every rank resets
+  // here, so the distributed ranks re-decide at the same tree)
+  auto_state_ = kAutoUnset;
+  auto_tree_ = 0;
+  auto_rounds_ms_ = 1e300;
+  prev_splits_ = prev_expansions_ = 0;
 }
 
 void GPUTreeLearner::ResetConfig(const Config* config) {

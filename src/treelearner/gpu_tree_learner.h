@@ -377,6 +377,9 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
     int ntpi = 1;
     float* label = nullptr;    // metric inputs, uploaded on the first device evaluation
     float* weights = nullptr;
+    const void* label_src = nullptr;    // the host arrays they were uploaded from
+    const void* weights_src = nullptr;
+    bool negative_weights = false;      // (AUC carries the class in the weight's sign: host then)
     void* metric_scratch = nullptr;
     data_size_t metric_scratch_rows = 0;  // rows metric_scratch is sized for (AUC)
     double* metric_out = nullptr;
@@ -395,6 +398,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   std::vector<ValidSet> valid_;
   int train_eval_slot_ = -1;  // valid_ entry over the training scores (d_score_; no bins)
   std::vector<void*> valid_allocs_;
+  void ReleaseValidInputs(ValidSet* vs);  // frees a set's metric inputs (not its bins / scores)
   // tree upload for the score traversal: one blob (node arrays, category sets, leaf values)
   // per tree, one H2D copy from a ring of pinned staging slots (each reused once its event --
   // recorded after its copy -- has completed: no stream synchronisation per tree)

@@ -142,3 +142,81 @@ def test_headline_auc_matches_reference(tmp_path):
     auc_ours = roc_auc(yt, np.loadtxt(tmp_path / "our_pred.txt"))
     assert auc_ref > 0.75
     assert auc_ours == auc_ref
+
+
+def _sparse_multival_data(path, n=6000, seed=7):
+    """20 random 10%-dense features (EFB leaves them to its second round: one multi-value group
+    in the reference, reference dataset.cpp:188-231), 4 dense features and a label."""
+    rng = np.random.RandomState(seed)
+    dense = rng.randn(n, 4)
+    sparse = np.where(rng.rand(n, 20) < 0.1, rng.randint(1, 30, size=(n, 20)), 0).astype(float)
+    y = (dense[:, 0] + 0.3 * sparse[:, :5].sum(axis=1) / 10 + 0.3 * rng.randn(n) > 0.2).astype(float)
+    np.savetxt(path, np.column_stack([y, dense, sparse]), fmt="%.9g", delimiter="\t")
+
+
+BINARY_CASES = [("binary_classification", "binary.train", "binary.test"),
+                ("lambdarank", "rank.train", "rank.test"),
+                ("sparse_multival", "sparse.train", None),
+                ("sparse_multival_host_sparse", "sparse.train", None)]
+
+
+@pytest.mark.parametrize("name,train_file,test_file", BINARY_CASES, ids=[c[0] for c in BINARY_CASES])
+def test_dataset_binary_files_interchange(tmp_path, monkeypatch, name, train_file, test_file):
+    """Dataset binary files (reference dataset.cpp:890-992 / dataset_loader.cpp:273-525): the
+    reference's save_binary output and this framework's are the same bytes; each side trains
+    from the other's file the trees it trains from the text file.  With host-sparse storage
+    (LGBM_AMD_HOST_SPARSE=1) the bundles are written as sparse groups -- other bytes, which the
+    reference reads and trains the same trees from."""
+    host_sparse = name.endswith("_host_sparse")
+    if name.startswith("sparse_multival"):
+        d = tmp_path / name
+        d.mkdir()
+        _sparse_multival_data(d / train_file)
+        conf = ["task=train", "objective=binary", "data=" + train_file, "num_trees=8", "num_leaves=15",
+                "num_threads=4", "verbosity=-1"]
+    else:
+        d = _example(tmp_path, name)
+        conf = _train_args(8)
+    ref_dir, our_dir = tmp_path / "ref_bin", tmp_path / "our_bin"
+    shutil.copytree(d, ref_dir)
+    shutil.copytree(d, our_dir)
+    _run(ORACLE, ref_dir, *(conf + ["save_binary=true", "output_model=ref_model.txt"]))
+    if host_sparse:
+        monkeypatch.setenv("LGBM_AMD_HOST_SPARSE", "1")
+    _run(OUR_CLI, our_dir, *(conf + ["save_binary=true", "output_model=our_model.txt", "device_type=cpu"]))
+    monkeypatch.delenv("LGBM_AMD_HOST_SPARSE", raising=False)
+    ref_bin = (ref_dir / (train_file + ".bin")).read_bytes()
+    our_bin = (our_dir / (train_file + ".bin")).read_bytes()
+    assert ref_bin.startswith(b"______LightGBM_Binary_File_Token______\n")
+    if host_sparse:
+        assert our_bin != ref_bin and our_bin[:200] == ref_bin[:200]
+    else:
+        assert our_bin == ref_bin
+    if name.startswith("sparse_multival"):  # (the reference wrote a multi-value group: it is exercised)
+        ds = lgb.Dataset(str(ref_dir / (train_file + ".bin"))).construct()
+        assert ds.num_data() == 6000
+    ref_trees = _trees((ref_dir / "ref_model.txt").read_text())
+    # the reference's file trains the same trees here ...
+    x_dir, y_dir = tmp_path / "x", tmp_path / "y"
+    for dd in (x_dir, y_dir):
+        dd.mkdir()
+    (x_dir / "ref.bin").write_bytes(ref_bin)
+    (y_dir / "our.bin").write_bytes(our_bin)
+    conf_bin = [c for c in conf if not c.startswith("data=") and c != "config=train.conf"]
+    if "config=train.conf" in conf:
+        keep = [line for line in (d / "train.conf").read_text().splitlines()
+                if line.strip() and not line.strip().startswith("#") and not line.strip().startswith(("data", "valid"))]
+        (x_dir / "train.conf").write_text("\n".join(keep) + "\n")
+        (y_dir / "train.conf").write_text("\n".join(keep) + "\n")
+        conf_bin = ["config=train.conf"] + conf_bin
+    _run(OUR_CLI, x_dir, *(conf_bin + ["data=ref.bin", "output_model=m.txt", "device_type=cpu"]))
+    # ... and this framework's file trains the same trees in the reference
+    _run(ORACLE, y_dir, *(conf_bin + ["data=our.bin", "output_model=m.txt"]))
+    for other in (_trees((x_dir / "m.txt").read_text()), _trees((y_dir / "m.txt").read_text())):
+        assert len(other) == len(ref_trees)
+        for i, (a, b) in enumerate(zip(ref_trees, other)):
+            for k in ("num_leaves", "split_feature", "threshold", "decision_type", "left_child", "right_child",
+                      "leaf_count", "internal_count"):
+                assert a[k] == b[k], "tree %d: %s" % (i, k)
+            np.testing.assert_allclose(np.array(b["leaf_value"].split(), dtype=float),
+                                       np.array(a["leaf_value"].split(), dtype=float), rtol=1e-12, atol=0)

@@ -660,7 +660,8 @@ def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, cap
         np.testing.assert_allclose(dev[name], host[name], rtol=1e-9, atol=1e-12, err_msg=name)
 
 
-@pytest.mark.parametrize("task", ["binary", "binary_weighted", "lambdarank", "multiclass", "regression_family"])
+@pytest.mark.parametrize("task", ["binary", "binary_weighted", "binary_negative_weights", "lambdarank", "multiclass",
+                                  "regression_family"])
 def test_training_metrics_on_device(task, gpu_available, monkeypatch, capfd):
     """Training-set metrics (valid_sets=[dtrain]: reference gbdt.cpp:484-542) are reduced on the
     device-resident training scores, equal to the host evaluation of the downloaded scores."""
@@ -676,6 +677,12 @@ def test_training_metrics_on_device(task, gpu_available, monkeypatch, capfd):
         kinds = (6, 4, 5)
         if task == "binary_weighted":  # (AUC sorts signed weights: zero weights of both classes included)
             weight = rng.choice([0.0, 0.5, 1.0, 2.5], size=n)
+        if task == "binary_negative_weights":
+            # the device AUC carries the class in the weight's sign: with negative weights the
+            # AUC is evaluated on the host (reference binary_metric.hpp:240-241 adds a negative
+            # weight to the row's own class), the other metrics stay on the device
+            weight = rng.choice([-0.5, 0.5, 1.0, 2.5], size=n)
+            kinds = (4, 5)
     elif task == "lambdarank":
         y = np.clip(np.round(X[:, 0] + X[:, 1] + rng.randn(n)), 0, 4)
         group = [40] * (n // 40)
@@ -703,12 +710,51 @@ def test_training_metrics_on_device(task, gpu_available, monkeypatch, capfd):
     logged = capfd.readouterr().out
     for k in kinds:
         assert "device metric (kind %d) on the training set" % k in logged, k
+    if task == "binary_negative_weights":
+        assert "device metric (kind 6)" not in logged
     params["verbose"] = -1
     monkeypatch.setenv("LGBM_AMD_HOST_METRICS", "1")
     host = run()
     assert set(dev) == set(host) and len(dev) >= 2
     for name in dev:
         np.testing.assert_allclose(dev[name], host[name], rtol=1e-9, atol=1e-12, err_msg=name)
+
+
+def test_training_metrics_after_reset_training_data(gpu_available, monkeypatch):
+    """LGBM_BoosterResetTrainingData to a dataset with other rows re-allocates the device
+    training scores: the device training metrics then read the new scores, labels and weights
+    (not the freed buffers of the old rows), equal to the host evaluation."""
+    import ctypes
+    from lightgbmv1_amd.basic import _LIB, _safe_call
+    rng = np.random.RandomState(9)
+
+    def data(n):
+        X = rng.randn(n, 6)
+        y = (X[:, 0] + 0.4 * rng.randn(n) > 0).astype(float)
+        return X, y, rng.choice([0.5, 1.0, 2.0], size=n)
+
+    params = {"objective": "binary", "metric": ["auc", "binary_logloss"], "verbose": -1, "device_type": "gpu",
+              "num_leaves": 15, "seed": 1}
+    (X1, y1, w1), (X2, y2, w2) = data(9000), data(5000)
+
+    def run():
+        d1 = lgb.Dataset(X1, y1, weight=w1, params=params, free_raw_data=False)
+        bst = lgb.Booster(params, d1)
+        for _ in range(3):
+            bst.update()
+        before = bst.eval_train()
+        d2 = lgb.Dataset(X2, y2, weight=w2, reference=d1, params=params).construct()
+        _safe_call(_LIB.LGBM_BoosterResetTrainingData(bst.handle, d2.handle))
+        for _ in range(2):
+            bst.update()
+        return before, bst.eval_train()
+
+    dev = run()
+    monkeypatch.setenv("LGBM_AMD_HOST_METRICS", "1")
+    host = run()
+    for (a, b) in zip(dev, host):
+        assert [m[1] for m in a] == [m[1] for m in b]
+        np.testing.assert_allclose([m[2] for m in a], [m[2] for m in b], rtol=1e-9, atol=1e-12)
 
 
 def _leaf_values(node):
