@@ -12,8 +12,14 @@ held-out synthetic set is reported for parity checks.
       --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 5
 
 With N>1 ranks the 10M rows are sharded row-wise (rank r owns rows r*10M/N ...), one
-process per GPU, tree_learner=data: per-split histograms are all-reduced with RCCL
-(strong scaling: the total work is fixed).
+process per GPU, tree_learner=data: each round reduce-scatters its expansions' histograms to
+the feature owners and all-gathers the owners' results over the peer communicator (one kernel
+per collective reading the peers' HBM over xGMI; RCCL with LGBM_AMD_DEVICE_COMM=rccl).  Strong
+scaling: the total work is fixed, and the trees equal the 1-GPU trees.
+
+AUC parity: `auc_ref` is the held-out AUC of the same run (rows, generator seeds, tree count)
+trained by this framework's CPU learner, which grows the reference CLI's trees byte for byte
+(tests/test_golden.py); the values are pinned in tools/bench_auc_ref.json.
 """
 import argparse
 import json
@@ -26,6 +32,18 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_SEC_PER_ITER = 0.232  # GTX 1080, Higgs 10.5M x 28, 255 bins
+AUC_REF_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "bench_auc_ref.json")
+
+
+def auc_reference(rows, features, leaves, max_bin, test_rows, trees, params):
+    """The pinned CPU-learner AUC of this exact run, or None when the fixture has none."""
+    if params or not os.path.exists(AUC_REF_FILE):
+        return None
+    key = dict(rows=rows, features=features, leaves=leaves, max_bin=max_bin, test_rows=test_rows, trees=trees)
+    for e in json.load(open(AUC_REF_FILE))["entries"]:
+        if all(e.get(k) == v for k, v in key.items()):
+            return e
+    return None
 
 
 def make_rows(start, count, num_features=28, seed=20240601):
@@ -146,6 +164,10 @@ def main():
     if rank == 0 and args.test_rows > 0:
         Xt, yt = make_rows(n_total + 12345678, args.test_rows, args.features)
         auc = roc_auc(yt, booster.predict(Xt))
+    ref = auc_reference(n_total, args.features, args.leaves, args.max_bin, args.test_rows, booster.num_trees(),
+                        json.loads(args.params)) if args.device == "gpu" else None
+    auc_fields = {"auc_ref": ref["auc"] if ref else None,
+                  "auc_delta": float("%.3g" % (auc - ref["auc"])) if ref and auc is not None else None}
     if rank == 0:
         print(json.dumps({
             "metric": "sec/iteration (500 trees, 255 bins, 63 leaves) on Higgs-shaped 10Mx28; AUC parity",
@@ -167,8 +189,10 @@ def main():
                        "global_batch": n_total, "seq_len": args.features,
                        "parallelism": "dp{}".format(world) if world > 1 else "single"},
             "auc_heldout": auc,
+            **auc_fields,
             "trees": booster.num_trees(),
             "device_comm": torch_dist.device_comm_kind() if world > 1 else None,
+            **({"device_topology": torch_dist.device_topology()} if world > 1 else {}),
             **diag,
             **({"train_auc": train_auc} if args.eval_train else {}),
             "setup_s": round(setup_s, 2),

@@ -218,6 +218,14 @@ class GBDT {
   std::vector<std::string> feature_infos_;
   std::vector<int8_t> monotone_constraints_;
   std::vector<score_t> gradients_, hessians_;
+
+ public:
+  // the host learner's gradients of the last iteration (tests: device vs host objectives)
+  const std::vector<score_t>& host_gradients() const { return gradients_; }
+  const std::vector<score_t>& host_hessians() const { return hessians_; }
+  data_size_t train_num_data() const { return num_data_; }
+
+ protected:
   std::vector<data_size_t> bag_data_indices_;
   data_size_t bag_data_cnt_ = 0;
   std::vector<Random> bagging_rands_;

@@ -34,6 +34,8 @@ struct DeviceRankSpec {
   int num_label_gain = 0;
   bool norm = true;
   double sigmoid = 1.0, sig_min = -25.0, sig_max = 25.0, sig_factor = 1.0;
+  const double* sig_table = nullptr;  // [sig_bins] the sigmoid table (lambdarank)
+  int64_t sig_bins = 0;
   const unsigned* rng_states = nullptr;  // [num_queries] per-query LCG states (xendcg); the device owns them after upload
 };
 

@@ -30,7 +30,7 @@ from ..basic import _load_lib, _safe_call
 _ALLGATHER_T = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                                 ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_void_p, ctypes.c_int)
 
-_STATE = {"callbacks": None, "group": None, "rccl": False, "device_comm": None}
+_STATE = {"callbacks": None, "group": None, "rccl": False, "device_comm": None, "self_test": None}
 
 
 def _make_allgather(dist, group):
@@ -79,6 +79,7 @@ def _init_peer(lib, dist, group, device, timeout_s):
     a, b = ctypes.c_int(0), ctypes.c_int(0)
     ok = (lib.LGBM_AMD_RcclSelfTest(ctypes.byref(a)) == 0 and a.value == 1 and
           lib.LGBM_AMD_RcclGraphSelfTest(ctypes.byref(b)) == 0 and b.value == 1)
+    _STATE["self_test"] = {"eager": a.value == 1, "graph": b.value == 1}
     if not _all_ok(dist, group, ok):
         lib.LGBM_AMD_DeviceCommFree()
         return False
@@ -143,6 +144,26 @@ def init_network(use_rccl=True, backend="gloo", timeout_s=600, device_comm=None)
 def device_comm_kind():
     """"peer", "rccl" or None: the device communicator init_network set up."""
     return _STATE["device_comm"]
+
+
+def device_topology():
+    """This rank's view of the device topology (dict), for run records: the device comm kind,
+    the peer comm's self-test outcome and, per peer rank, its PCI bus id and either
+    ``same_device`` or the link type (``xgmi`` / ``pcie``) and hop count
+    (hipExtGetLinkTypeAndHopCount), or ``visible: false`` under per-process device isolation."""
+    import json
+    out = {"device_comm": _STATE["device_comm"], "self_test": _STATE["self_test"]}
+    if _STATE["device_comm"] == "peer" or _STATE["self_test"] is not None:
+        lib = _load_lib()
+        n = ctypes.c_int(0)
+        lib.LGBM_AMD_DeviceCommTopology(None, ctypes.c_int(0), ctypes.byref(n))
+        buf = ctypes.create_string_buffer(n.value + 1)
+        lib.LGBM_AMD_DeviceCommTopology(buf, ctypes.c_int(n.value + 1), ctypes.byref(n))
+        try:
+            out.update(json.loads(buf.value.decode() or "{}"))
+        except ValueError:
+            out["raw"] = buf.value.decode(errors="replace")
+    return out
 
 
 def barrier():

@@ -1426,6 +1426,27 @@ int LGBM_AMD_BoosterDeviceGradients(BoosterHandle handle, float* grad, float* he
   API_END();
 }
 
+// the gradients the last iteration trained on, from the device learner or the host learner
+// (n: entries available; grad / hess may be null to query it)
+int LGBM_AMD_BoosterLastGradients(BoosterHandle handle, float* grad, float* hess, int64_t* n) {
+  API_BEGIN();
+  GBDT* b = static_cast<Booster*>(handle)->boosting();
+  std::vector<float> g, h;
+  if (b->device_learner() != nullptr) {
+    const int64_t n_all = static_cast<int64_t>(b->train_num_data()) * b->NumModelPerIteration();
+    g.resize(n_all);
+    h.resize(n_all);
+    b->device_learner()->DownloadGradients(g.data(), h.data(), n_all);
+  } else {
+    g = b->host_gradients();
+    h = b->host_hessians();
+  }
+  *n = static_cast<int64_t>(g.size());
+  if (grad != nullptr) std::memcpy(grad, g.data(), sizeof(float) * g.size());
+  if (hess != nullptr) std::memcpy(hess, h.data(), sizeof(float) * h.size());
+  API_END();
+}
+
 int LGBM_AMD_BoosterDeviceCheckSplits(BoosterHandle handle, int64_t buffer_len, int64_t* out_len, char* out_str) {
   API_BEGIN();
   GBDT* b = static_cast<Booster*>(handle)->boosting();

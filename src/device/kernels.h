@@ -194,6 +194,13 @@ struct KArgs {
   int32_t round_gr;    // independent row gathers per thread in its histogram phase (2, 4, 8)
   int32_t round_fused;  // 1: partition + histograms in one kernel (k_round_split), 0: two (k_round_part, k_round_hist)
   int32_t plan_in_find;  // the round's last split-scan workgroup plans (else k_round_plan)
+  // single-process rounds: the reduce of the large expansions' partials runs as the first
+  // workgroups of the numerical split-scan launch instead of a kernel of its own (one launch and
+  // its gap less per round).  red_per_exp: reduce workgroups per expansion (0: a separate
+  // k_round_reduce); red_rows: grid rows of reduce workgroups in front of the scans (set per
+  // launch; 0: none in this launch)
+  int32_t red_per_exp;
+  int32_t red_rows;
   // distributed round growth (data- / feature-parallel): per-feature results rank-major,
   // [world][2 * round_k][max_owned] (a rank's local feature index from fb_index), all-gathered
   // before k_round_childbest; data-parallel: the round's histograms reduced into round_send
@@ -302,6 +309,8 @@ void PickStep(const KArgs& a, hipStream_t s, bool root);
 // then per round the fused partition + histogram of every expansion, the reduction of their
 // large histograms, the children's split scans (+ each child's best split), and the plan
 // (replay of the best-first order, next expansions).  A finished tree's kernels exit at once.
+// reduce workgroups per expansion when the reduce runs in the split-scan launch (KArgs::red_per_exp)
+int RoundReducePerExp(const KArgs& a);
 void RoundRootPlan(const KArgs& a, hipStream_t s);
 void RoundStep(const KArgs& a, hipStream_t s);  // single process: split + reduce + scans (+ plan)
 // distributed rounds: the collectives go between the parts
@@ -440,6 +449,7 @@ struct RankArgs {
   const double* discount;     // position -> 1 / log2(2 + i)
   double sigmoid;
   double sig_min, sig_max, sig_factor;  // sigmoid table domain and bins per unit
+  const double* sig_table;    // [kRankSigmoidBins] the host objective's sigmoid table (lambdarank)
   int32_t norm;               // lambdarank_norm
   uint32_t* rng;              // [num_queries] LCG states (xendcg), advanced in place
 };

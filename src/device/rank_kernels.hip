@@ -27,24 +27,31 @@ __device__ __forceinline__ double BlockSum(double v, double* red) {
   return t;
 }
 
-// the reference's 1M-entry sigmoid table, evaluated at the same quantised abscissa
+// the host objective's sigmoid table (reference rank_objective.hpp:230-245: 1M entries of
+// 1 / (1 + exp(x * sigmoid)) over [min, max]), uploaded: the device's exp may differ from the
+// host's in the last bit, the table's entries do not
 __device__ __forceinline__ double RankSigmoid(const RankArgs& ra, double x) {
-  double q;
-  if (x <= ra.sig_min) {
-    q = ra.sig_min;
-  } else if (x >= ra.sig_max) {
-    q = static_cast<double>(kRankSigmoidBins - 1) / ra.sig_factor + ra.sig_min;
-  } else {
-    const size_t i = static_cast<size_t>((x - ra.sig_min) * ra.sig_factor);
-    q = static_cast<double>(i) / ra.sig_factor + ra.sig_min;
-  }
-  return 1.0f / (1.0f + exp(q * ra.sigmoid));
+  if (x <= ra.sig_min) return ra.sig_table[0];
+  if (x >= ra.sig_max) return ra.sig_table[kRankSigmoidBins - 1];
+  return ra.sig_table[static_cast<size_t>((x - ra.sig_min) * ra.sig_factor)];
 }
 
+// One workgroup per query.  The gradients equal the host's bit for bit (so that device GOSS
+// keeps the host's rows): the reference accumulates a document's lambda in float as the
+// lower-labelled side of each pair, in the sorted order of the pair's higher side
+// (`lambdas[low] -= (float)p`), and adds its own pairs' double sum as the higher side when the
+// outer loop reaches its sorted position (`lambdas[high] += (float)sum`,
+// rank_objective.hpp:164-221).  Each thread replays that sequence for its documents over the
+// sorted order (s_doc), with the host's operation order and no contraction into FMAs.  (The
+// normalisation's sum of |lambdas| is a workgroup reduction in double: it differs from the host's
+// sequential sum in its last bits only, which reach a float gradient through the log2 factor with
+// probability ~2^-29.)
 __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
+#pragma clang fp contract(off)
   __shared__ double s_score[kRankMaxDocs];
   __shared__ int s_label[kRankMaxDocs];
-  __shared__ int s_pos[kRankMaxDocs];
+  __shared__ int s_pos[kRankMaxDocs];  // document -> sorted position
+  __shared__ int s_doc[kRankMaxDocs];  // sorted position -> document
   __shared__ double s_red[kRankThreads / kWave];
   __shared__ double s_edge[3];  // score at sorted positions 0, cnt-1, cnt-2
   const int q = blockIdx.x;
@@ -63,6 +70,7 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
       p += (sj > si) | ((sj == si) & (j < i));
     }
     s_pos[i] = p;
+    s_doc[p] = i;
     if (p == 0) s_edge[0] = si;
     if (p == cnt - 1) s_edge[1] = si;
     if (p == cnt - 2) s_edge[2] = si;
@@ -73,57 +81,76 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
   const double inv_max = ra.inv_max_dcg[q];
   const double sig = ra.sigmoid;
   const bool norm = ra.norm != 0 && best != worst;
+  // the pair (high, low): its lambda and hessian as rank_objective.hpp:186-209 computes them
+  auto pair = [&](double hs, int hl, double hd, double ls, int ll, double ld, double* pl_out, double* ph_out) {
+    const double ds = hs - ls;
+    const double dcg_gap = ra.label_gain[hl] - ra.label_gain[ll];
+    const double paired = fabs(hd - ld);
+    double dn = dcg_gap * paired * inv_max;
+    if (norm) dn /= (0.01f + fabs(ds));
+    double pl = RankSigmoid(ra, ds);
+    double ph = pl * (1.0f - pl);
+    pl *= -sig * dn;
+    ph *= sig * sig * dn;
+    *pl_out = pl;
+    *ph_out = ph;
+  };
   double sum_lambdas = 0.0;
   for (int d = threadIdx.x; d < cnt; d += kRankThreads) {
     const double sd = s_score[d];
-    double lam = 0.0, hes = 0.0;
-    if (sd != kMinScore) {
-      const int ld = s_label[d];
-      const double gd = ra.label_gain[ld];
-      const double discd = ra.discount[s_pos[d]];
-      for (int j = 0; j < cnt; ++j) {
+    const int ld = s_label[d], kd = s_pos[d];
+    const double disc_d = ra.discount[kd];
+    float lam = 0.0f, hes = 0.0f;
+    for (int k = 0; k < cnt; ++k) {
+      if (k == kd) {
+        if (sd == kMinScore) continue;
+        // d as the higher side: its pairs in the sorted order of the lower side, summed in double
+        double hsl = 0.0, hsh = 0.0;
+        for (int k2 = 0; k2 < cnt; ++k2) {
+          if (k2 == kd) continue;
+          const int j = s_doc[k2];
+          const int lj = s_label[j];
+          const double sj = s_score[j];
+          if (ld <= lj || sj == kMinScore) continue;
+          double pl, ph;
+          pair(sd, ld, disc_d, sj, lj, ra.discount[k2], &pl, &ph);
+          hsl += pl;
+          hsh += ph;
+          sum_lambdas -= 2 * pl;
+        }
+        lam = __fadd_rn(lam, static_cast<float>(hsl));
+        hes = __fadd_rn(hes, static_cast<float>(hsh));
+      } else {
+        // d as the lower side of the pair with the document at sorted position k
+        const int j = s_doc[k];
         const int lj = s_label[j];
         const double sj = s_score[j];
-        if (j == d || lj == ld || sj == kMinScore) continue;
-        const bool d_high = ld > lj;
-        const double hs = d_high ? sd : sj, ls = d_high ? sj : sd;
-        const double ds = hs - ls;
-        const double gap = d_high ? gd - ra.label_gain[lj] : ra.label_gain[lj] - gd;
-        const double pd = fabs(discd - ra.discount[s_pos[j]]);
-        double dn = gap * pd * inv_max;
-        if (norm) dn /= (0.01f + fabs(ds));
-        double pl = RankSigmoid(ra, ds);
-        double ph = pl * (1.0f - pl);
-        pl *= -sig * dn;
-        ph *= sig * sig * dn;
-        hes += ph;
-        if (d_high) {
-          lam += pl;
-          sum_lambdas -= 2 * pl;
-        } else {
-          lam -= pl;
-        }
+        if (sj == kMinScore || lj <= ld || sd == kMinScore) continue;
+        double pl, ph;
+        pair(sj, lj, ra.discount[k], sd, ld, disc_d, &pl, &ph);
+        lam = __fsub_rn(lam, static_cast<float>(pl));
+        hes = __fadd_rn(hes, static_cast<float>(ph));
       }
     }
-    ra.grad[b + d] = static_cast<float>(lam);
-    ra.hess[b + d] = static_cast<float>(hes);
+    ra.grad[b + d] = lam;
+    ra.hess[b + d] = hes;
   }
   const double total = BlockSum(sum_lambdas, s_red);
   const bool renorm = ra.norm != 0 && total > 0;
   const double nf = renorm ? log2(1 + total) / total : 1.0;
   if (!renorm && ra.weights == nullptr) return;
   for (int d = threadIdx.x; d < cnt; d += kRankThreads) {
-    double g = ra.grad[b + d], h = ra.hess[b + d];
+    float g = ra.grad[b + d], h = ra.hess[b + d];
     if (renorm) {
       g = static_cast<float>(g * nf);
       h = static_cast<float>(h * nf);
     }
-    if (ra.weights != nullptr) {
-      g *= ra.weights[b + d];
-      h *= ra.weights[b + d];
+    if (ra.weights != nullptr) {  // (reference RankingObjective::GetGradients: float products)
+      g = __fmul_rn(g, ra.weights[b + d]);
+      h = __fmul_rn(h, ra.weights[b + d]);
     }
-    ra.grad[b + d] = static_cast<float>(g);
-    ra.hess[b + d] = static_cast<float>(h);
+    ra.grad[b + d] = g;
+    ra.hess[b + d] = h;
   }
 }
 

@@ -155,6 +155,11 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(LG
     x.r.default_bin = e.feat.default_bin;
     x.r.max_bin = e.feat.num_bin - 1;
   }
+  // this round's reduce counters (KArgs::red_per_exp: the reduces run in the split-scan launch,
+  // which follows this one; the previous round's have all finished)
+  if (a.red_per_exp > 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < static_cast<unsigned>(kMaxRoundExp)) {
+    rd->red_cnt[threadIdx.x] = 0u;
+  }
   if (done || nexp <= 0 || static_cast<int>(blockIdx.x) >= nblk) return;
   if (threadIdx.x < static_cast<unsigned>(nexp)) ex[threadIdx.x] = x;
   for (int i = threadIdx.x; i < nexp * kMaxCatWords; i += kPartThreads) {
@@ -698,6 +703,75 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
   }
 }
 
+// The reduce of k_round_reduce as the first workgroups (grid rows [0, KArgs::red_rows)) of the
+// numerical split-scan launch (KArgs::red_per_exp > 0, single process): workgroup r reduces
+// bins [bx * NT, +NT) of partial chunk `by` of expansion j = r / red_per_exp.  Its sums are
+// stored write-through (agent-scope atomics), then the workgroup counts itself on
+// Round::red_cnt[j]; the scans of expansion j wait for red_per_exp counts.  Workgroups are
+// dispatched in order of their linear index, so every reduce workgroup is resident before any
+// scan workgroup that waits for it, and a reduce never waits: the waits end.
+template <int NT>
+__device__ void RoundReduceRole(const KArgs& a, int r) {
+  Round* rd = a.rd;
+  const int C = a.red_per_exp;
+  const int j = r / C, rem = r - j * C;
+  const int nb = a.p.total_bins;
+  const int nbx = (nb + NT - 1) / NT;
+  const int bx = rem % nbx, by = rem / nbx;
+  if (j >= kMaxRoundExp || rd->done || j >= rd->nexp) return;
+  const int nblk = rd->e[j].nblk;
+  if (nblk <= kDirectChunk) return;  // (summed by the split scan itself; nobody waits)
+  const int gy = C / nbx;
+  const int bin = bx * NT + static_cast<int>(threadIdx.x);
+  if (by * kReduceChunk < nblk && bin < nb) {
+    const int units = a.hist_units;
+    const size_t pstride = static_cast<size_t>(units) * nb;
+    const unsigned long long* part = a.partials + static_cast<size_t>(rd->e[j].blk_off) * pstride;
+    long long g = 0, h = 0;
+    for (int k0 = by * kReduceChunk; k0 < nblk; k0 += gy * kReduceChunk) {
+      const unsigned long long* p = part + k0 * pstride + static_cast<size_t>(units) * bin;
+      const int kn = min(kReduceChunk, nblk - k0);
+      unsigned long long v0[kReduceChunk], v1[kReduceChunk];
+#pragma unroll
+      for (int k = 0; k < kReduceChunk; ++k) {
+        v0[k] = k < kn ? p[k * pstride] : 0ull;
+        v1[k] = (units == 2 && k < kn) ? p[k * pstride + 1] : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < kReduceChunk; ++k) {
+        long long pg, ph;
+        UnpackPartial(v0[k], v1[k], units, &pg, &ph);
+        g += pg;
+        h += ph;
+      }
+    }
+    GlobalU64* out = (GlobalU64*)(RoundScratch(a, rd->round, j) + 2 * static_cast<size_t>(bin));
+    if (nblk <= kReduceChunk) {
+      __hip_atomic_store(out, static_cast<unsigned long long>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(out + 1, static_cast<unsigned long long>(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_fetch_add(out, static_cast<unsigned long long>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(out + 1, static_cast<unsigned long long>(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ArrivalRelease();
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&rd->red_cnt[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// a scan of expansion j waits for its reduce workgroups (RoundReduceRole)
+__device__ __forceinline__ void RoundReduceWait(const KArgs& a, int j) {
+  if (threadIdx.x == 0) {
+    const uint32_t want = static_cast<uint32_t>(a.red_per_exp);
+    while (__hip_atomic_load(&a.rd->red_cnt[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
 // the plan's LDS tables (RoundPlanLds bytes): node tables (gain, -inf when the node has no
 // split; real feature; first child or -1), leaf tables (gain, real feature, node; accepted
 // leaves / nodes) and the prediction's copies of the leaf tables (+ levels below the leaf)
@@ -816,7 +890,12 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   __shared__ int s_last;
   Round* rd = a.rd;
   const long long t_entry = a.ktrace != nullptr ? wall_clock64() : 0;
-  const int y = blockIdx.y, j = y >> 1, lr = y & 1;
+  if (static_cast<int>(blockIdx.y) < a.red_rows) {  // (the round's reduce workgroups come first)
+    RoundReduceRole<NT>(a, static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x));
+    return;
+  }
+  const int by = static_cast<int>(blockIdx.y) - a.red_rows;  // (the scan grid's row)
+  const int y = by, j = y >> 1, lr = y & 1;
   // voting-parallel rounds (KArgs::round_vote): Params::vote_phase 1 scans every feature on this
   // rank's histograms, sums and counts; 2 scans the features the vote elected for child y
   // (KArgs::vote_list) on their all-reduced histograms (KArgs::vote_hist)
@@ -843,7 +922,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const Feature F = a.feat[f];
   const int8_t tree_used = a.tree_mask[f];
   if (done) return;
-  if (a.ktrace != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && rround < a.p.num_leaves) {
+  if (a.ktrace != nullptr && blockIdx.x == 0 && by == 0 && threadIdx.x == 0 && rround < a.p.num_leaves) {
     a.ktrace[static_cast<size_t>(rround) * kTraceSlots + 25] = wall_clock64();
   }
   const int parity = rround & 1;
@@ -869,9 +948,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     // data-parallel: the next round's owner-major send buffer, cleared by every workgroup's
     // share (this round's reduce-scatter has read it) -- no memset node per round
     const size_t total = static_cast<size_t>(a.p.world) * a.round_k * a.rs_block * 2;
-    const size_t nwg = static_cast<size_t>(gridDim.x) * gridDim.y;
+    const size_t nwg = static_cast<size_t>(gridDim.x) * (gridDim.y - a.red_rows);
     const size_t per = (total + nwg - 1) / nwg;
-    const size_t b0 = (static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x) * per;
+    const size_t b0 = (static_cast<size_t>(by) * gridDim.x + blockIdx.x) * per;
     const size_t b1 = min(total, b0 + per);
     for (size_t i = b0 + tid; i < b1; i += NT) a.round_send[i] = 0;
   }
@@ -953,6 +1032,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
       pg0 = dst[2 * tid];
       ph0 = dst[2 * tid + 1];
     }
+    // (the reduce ran in this launch: its sums are read coherently once they are all counted)
+    const bool reduced_here = a.red_rows > 0 && nblk_direct < 0 && !owner && !vote_global;
+    if (reduced_here) RoundReduceWait(a, j);
     if (spread) {
       for (int i = tid; i < 2 * nbf; i += NT) sh.s_red[i] = 0ull;
       __syncthreads();
@@ -1005,6 +1087,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
             h += phv;
           }
         }
+      } else if (reduced_here) {
+        g = static_cast<long long>(__hip_atomic_load((GlobalU64*)(src + 2 * i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        h = static_cast<long long>(__hip_atomic_load((GlobalU64*)(src + 2 * i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       } else {
         g = src[2 * i];
         h = src[2 * i + 1];
@@ -1250,12 +1335,12 @@ __device__ __forceinline__ void RegTakeChildren(RegLeaf* x, int lane, int w, int
   if (lane == nl) RegLoad(x, c + 1, ng, nrf, nch);
 #endif
 }
-// returns s (splits after the replay); *done, *npick; acc / accn / s_pick / tnode as the LDS path
-__device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, int kround, const double* ng, const int* nrf,
-                                 const int* nch, int* tnode, int* acc, int* accn, int* s_pick, int* done_out,
-                                 int* npick_out) {
+// The replay (wave 0): returns s, the splits after it, and *done; acc / accn / tnode as the LDS
+// path.  x keeps the replayed leaves for the prediction.
+__device__ int ReplayRegs(int L, int s0, const double* ng, const int* nrf, const int* nch, int* tnode, int* acc,
+                          int* accn, RegLeaf* xp, int* done_out) {
   const int lane = threadIdx.x & 63;
-  RegLeaf x;
+  RegLeaf& x = *xp;
   RegLoad(&x, lane <= s0 ? tnode[lane] : -1, ng, nrf, nch);
   int s = s0, done = 0;
   for (;;) {
@@ -1279,7 +1364,17 @@ __device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, int kr
     ++s;
   }
   if (lane <= s) tnode[lane] = x.node;
-  int n = 0;
+  *done_out = done;
+  return s;
+}
+
+// the next round's expansions predicted past the blocker (wave 0, after ReplayRegs): returns
+// the picks' count (s_pick); *done when the tree cannot go on
+__device__ int PredictRegs(const KArgs& a, int L, int s, int used, int kround, const double* ng, const int* nrf,
+                           const int* nch, int* s_pick, RegLeaf* xp, int* done_io) {
+  const int lane = threadIdx.x & 63;
+  RegLeaf& x = *xp;
+  int done = *done_io, n = 0;
   if (!done) {
     const int need = L - 1 - s;
     int kmax = min(kround, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
@@ -1306,9 +1401,8 @@ __device__ int ReplayPredictRegs(const KArgs& a, int L, int s0, int used, int kr
     }
     if (n == 0) done = 1;
   }
-  *done_out = done;
-  *npick_out = n;
-  return s;
+  *done_io = done;
+  return n;
 }
 
 // One workgroup.  ROOT: the root's best split from its per-feature results (FindRoot), then
@@ -1472,35 +1566,28 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   stamp(17);
   // replay of the sequential order by wave 0: the argmax leaf is split while its node is
   // expanded; its children nodes become leaves w and s + 1
+  RegLeaf x;
+  int done_w = 0;
+  int s_w = s0;
   if (tid < kWave && L <= kWave) {
-    int done = 0, n = 0;
-    const int s = ReplayPredictRegs(a, L, s0, (nn - 1) / 2, kround, ng, nrf, nch, tnode, acc, accn, s_pick, &done, &n);
-    if (lane == 0) {
-      s_s1 = s;
-      s_done = done;
-      s_nexp = done ? 0 : n;
-    }
+    s_w = ReplayRegs(L, s0, ng, nrf, nch, tnode, acc, accn, &x, &done_w);
   } else if (tid < kWave) {
-    int s = s0, done = 0, blocker = -1;
     for (;;) {
-      if (s >= L - 1) {
-        done = 1;
+      if (s_w >= L - 1) {
+        done_w = 1;
         break;
       }
-      const int w = WaveArgmaxLeaf(tg, trf, s, [](int) { return true; });
+      const int w = WaveArgmaxLeaf(tg, trf, s_w, [](int) { return true; });
       if (!(tg[w] > 0.0)) {
-        done = 1;
+        done_w = 1;
         break;
       }
       const int n = tnode[w], c = nch[n];
-      if (c < 0) {
-        blocker = w;
-        break;
-      }
+      if (c < 0) break;
       if (lane == 0) {
-        const int nl = s + 1;
-        acc[s - s0] = w;
-        accn[s - s0] = n;
+        const int nl = s_w + 1;
+        acc[s_w - s0] = w;
+        accn[s_w - s0] = n;
         tnode[w] = c;
         tg[w] = ng[c];
         trf[w] = nrf[c];
@@ -1509,22 +1596,74 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         trf[nl] = nrf[c + 1];
       }
       WaveLdsSync();
-      ++s;
+      ++s_w;
     }
-    // the next round's expansions: the sequential order predicted past the blocker from the
-    // splits known so far (copies of the leaf tables): an expanded argmax joins its children,
-    // an unexpanded one is needed next -- picked (within round_vmax levels below its leaf)
-    // with its children unknown.  The blocker is the first pick.
+  }
+  if (tid == 0) s_s1 = s_w;
+  __syncthreads();  // the accepted splits and the leaves' final nodes are in LDS
+  const int s1 = s_s1, nacc = s1 - s0;
+  stamp(18);
+  // wave 0 predicts the next round while the other waves write the records of the accepted
+  // splits and of the leaves the replay changed (from their final nodes; a leaf changed twice is
+  // written twice with the same record) -- those do not depend on the prediction
+  auto accepted_record = [&](int i) {
+    if (i < nacc) {
+      // an accepted split: its record (the node's best split, its partition counts)
+      const int k = i;
+      const int n = accn[k];
+      const FeatureBest& cb = a.cbest[n];
+      const int tl = a.rnode[n].total_left, cnt = a.rnode[n].count;
+      SplitRecord& rec = a.rec[s0 + k];
+      rec.leaf = acc[k];
+      rec.left_count = dp ? cb.lc : tl;
+      rec.right_count = dp ? cb.rc : cnt - tl;
+      ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, &rec.split);
+    } else {
+      const int i2 = i - nacc;
+      const int k = i2 >> 1;
+      const int l = (i2 & 1) == 0 ? acc[k] : s0 + k + 1;
+      const int n = tnode[l];
+      const RNode R = a.rnode[n];
+      Leaf lf;
+      lf.begin = R.begin;
+      lf.count = R.count;
+      lf.global_count = dp ? R.st.global_count : R.count;
+      lf.depth = R.st.depth;
+      lf.slot = R.st.slot;
+      lf.buf = R.buf;
+      lf.frow = n;
+      lf.pad = 0;
+      lf.icmask = R.st.icmask;
+      lf.sum_g = R.st.sum_g;
+      lf.sum_h = R.st.sum_h;
+      lf.output = R.st.output;
+      lf.lsum_g = a.round_vote ? a.rnode_lsum[2 * n] : 0.0;
+      lf.lsum_h = a.round_vote ? a.rnode_lsum[2 * n + 1] : 0.0;
+      lf.cmin = R.st.cmin;
+      lf.cmax = R.st.cmax;
+      a.leaves[l] = lf;
+      DeviceSplit* d = &a.best[l];
+      if (ng[n] != -INFINITY) ToDeviceSplit(a.cbest[n], a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, d);
+      else NoSplit(d);
+    }
+  };
+  if (tid < kWave) {
     int n = 0;
-    if (!done) {
+    if (L <= kWave) {
+      n = PredictRegs(a, L, s1, (nn - 1) / 2, kround, ng, nrf, nch, s_pick, &x, &done_w);
+    } else if (!done_w) {
+      // the sequential order predicted past the blocker from the splits known so far (copies of
+      // the leaf tables): an expanded argmax joins its children, an unexpanded one is needed
+      // next -- picked (within round_vmax levels below its leaf) with its children unknown.  The
+      // blocker is the first pick.
       // budget: after this round, one expansion per split the tree may still need stays
       // available (each round then accepts at least its first pick, the blocker)
-      const int need = L - 1 - s, used = (nn - 1) / 2;
+      const int need = L - 1 - s1, used = (nn - 1) / 2;
       int kmax = min(kround, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
       kmax = min(kmax, a.round_emax - used - (need - 1));
       kmax = max(kmax, min(1, a.round_emax - used));
-      if (kmax <= 0) done = 1;  // (unreachable: the budget keeps room for the blocker)
-      for (int l = lane; l <= s; l += kWave) {
+      if (kmax <= 0) done_w = 1;  // (unreachable: the budget keeps room for the blocker)
+      for (int l = lane; l <= s1; l += kWave) {
         sg[l] = tg[l];
         srf[l] = trf[l];
         snode[l] = tnode[l];
@@ -1532,7 +1671,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       }
       WaveLdsSync();
       const int vmax = a.round_vmax;
-      for (int ss = s; !done && n < kmax && ss < L - 1; ++ss) {
+      for (int ss = s1; !done_w && n < kmax && ss < L - 1; ++ss) {
         const int w = WaveArgmaxLeaf(sg, srf, ss, [](int) { return true; });
         if (!(sg[w] > 0.0)) break;
         const int nd = snode[w], c = nch[nd], v = svd[w];
@@ -1559,33 +1698,32 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         if (c < 0 && v <= vmax) ++n;
         WaveLdsSync();
       }
-      if (n == 0) done = 1;  // (unreachable: the blocker is the first argmax)
+      if (n == 0) done_w = 1;  // (unreachable: the blocker is the first argmax)
     }
     if (lane == 0) {
-      s_s1 = s;
-      s_done = done;
-      s_nexp = done ? 0 : n;
+      s_done = done_w;
+      s_nexp = done_w ? 0 : n;
     }
+    if constexpr (NT == kWave) {  // (one wave: the records after the prediction)
+      for (int i = lane; i < 3 * nacc; i += kWave) accepted_record(i);
+    }
+  } else {
+    for (int i = tid - kWave; i < 3 * nacc; i += NT - kWave) accepted_record(i);
   }
   __syncthreads();
-  const int s1 = s_s1, nacc = s1 - s0, nexp = s_nexp;
-  stamp(18);
+  const int nexp = s_nexp;
   if (ktr != nullptr) {
     ktr[22] = nacc;
     ktr[23] = nexp;
   }
-  // the plan's records in one pass over a combined item space, so that each thread's loads are
-  // one round trip: [0, nexp) the next round's expansions (when the tree goes on), then the
-  // accepted splits' records, then the leaves the replay changed (from their final nodes; a
-  // leaf changed twice is written twice with the same record)
+  // the next round's expansions, one thread each: independent loads (one round trip) of the
+  // node, its best split, the split feature's record and interaction mask
   const int next_frow = nn;
   const int nbuf = a.round_vmax + 2;
   const int nent = s_done ? 0 : nexp;
-  for (int it = tid; it < nent + 3 * nacc; it += kPlanThreads) {
-    if (it < nent) {
+  for (int it = tid; it < nent; it += kPlanThreads) {
+    {
       const int j = it, node = s_pick[j];
-      // independent loads (one round trip): the node, its best split, the split feature's record
-      // (its index from the node table) and interaction mask
       const int fi = nfi[node];
       const RNode P = a.rnode[node];
       const FeatureBest& cb = a.cbest[node];
@@ -1660,44 +1798,6 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       s_c[2 * j] = C;
       C.st = rc;
       s_c[2 * j + 1] = C;
-    } else if (it < nent + nacc) {
-      // an accepted split: its record (the node's best split, its partition counts)
-      const int k = it - nent;
-      const int n = accn[k];
-      const FeatureBest& cb = a.cbest[n];
-      const int tl = a.rnode[n].total_left, cnt = a.rnode[n].count;
-      SplitRecord& rec = a.rec[s0 + k];
-      rec.leaf = acc[k];
-      rec.left_count = dp ? cb.lc : tl;
-      rec.right_count = dp ? cb.rc : cnt - tl;
-      ToDeviceSplit(cb, a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, &rec.split);
-    } else {
-      const int i = it - nent - nacc;
-      const int k = i >> 1;
-      const int l = (i & 1) == 0 ? acc[k] : s0 + k + 1;
-      const int n = tnode[l];
-      const RNode R = a.rnode[n];
-      Leaf lf;
-      lf.begin = R.begin;
-      lf.count = R.count;
-      lf.global_count = dp ? R.st.global_count : R.count;
-      lf.depth = R.st.depth;
-      lf.slot = R.st.slot;
-      lf.buf = R.buf;
-      lf.frow = n;
-      lf.pad = 0;
-      lf.icmask = R.st.icmask;
-      lf.sum_g = R.st.sum_g;
-      lf.sum_h = R.st.sum_h;
-      lf.output = R.st.output;
-      lf.lsum_g = a.round_vote ? a.rnode_lsum[2 * n] : 0.0;
-      lf.lsum_h = a.round_vote ? a.rnode_lsum[2 * n + 1] : 0.0;
-      lf.cmin = R.st.cmin;
-      lf.cmax = R.st.cmax;
-      a.leaves[l] = lf;
-      DeviceSplit* d = &a.best[l];
-      if (ng[n] != -INFINITY) ToDeviceSplit(a.cbest[n], a.cbest_cat + static_cast<size_t>(n) * kMaxCatWords, d);
-      else NoSplit(d);
     }
   }
   stamp(19);
@@ -1712,40 +1812,42 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   }
   __syncthreads();
   stamp(20);
-  if (tid == 0) {
-    // row blocks: one size for the round (at least blk_min_rows, at most the packed headroom)
-    long long rows = 0;
-    for (int j = 0; j < nexp; ++j) rows += s_pc[j];
+  if (tid < kWave) {
+    // row blocks: one size for the round (at least blk_min_rows, at most the packed headroom),
+    // one lane per expansion
+    const int pcj = lane < nexp ? s_pc[lane] : 0;
+    const unsigned urows = static_cast<unsigned>(WaveSum(pcj));
     // balanced over the grid: the smallest m with blocks of ceil(rows / (m * grid - nexp))
     // rows under the packed headroom; every workgroup then takes m blocks at most (one
     // partial block per expansion rounds up)
     // (the smallest m with ceil(rows / (m g - nexp)) <= cap, i.e. m g - nexp >= ceil(rows / cap);
     // rows and cap are below 2^31, so every dividend fits 32 unsigned bits: no 64-bit divisions)
     const unsigned g = static_cast<unsigned>(max(1, a.round_grid)), cap = static_cast<unsigned>(a.hist_rows_cap);
-    const unsigned urows = static_cast<unsigned>(rows), unexp = static_cast<unsigned>(nexp);
+    const unsigned unexp = static_cast<unsigned>(nexp);
     const unsigned need = (urows + cap - 1u) / cap + unexp;
     const unsigned m = g <= unexp ? 1u : max(1u, (need + g - 1u) / g);
     long long rpb = m * g > unexp ? (urows + m * g - unexp - 1u) / (m * g - unexp) : cap;
     rpb = max(rpb, static_cast<long long>(a.blk_min_rows));
     rpb = min(rpb, static_cast<long long>(cap));
     rpb = max(rpb, 1ll);
-    int off = 0;
     const unsigned rpb32 = static_cast<unsigned>(rpb);  // (32-bit divisions: a 64-bit one is a long call)
-    for (int j = 0; j < nexp; ++j) {
-      const int nb = static_cast<int>((static_cast<unsigned>(s_pc[j]) + rpb32 - 1u) / rpb32);
-      s_e[j].blk_off = off;
-      s_e[j].nblk = nb;
-      off += nb;
+    const int nb = lane < nexp ? static_cast<int>((static_cast<unsigned>(pcj) + rpb32 - 1u) / rpb32) : 0;
+    const int incl = WavePrefixIncl(nb);
+    if (lane < nexp) {
+      s_e[lane].blk_off = incl - nb;
+      s_e[lane].nblk = nb;
     }
-    rd->rpb = static_cast<int>(rpb);
-    rd->nblk = off;
-    rd->nexp = nexp;
-    rd->nsplit = s1;
-    rd->next_slot = next_slot + nexp;
-    rd->next_frow = next_frow + 2 * nexp;
-    rd->round = ROOT ? 1 : round0 + 1;  // (parity 0 of the first round holds the root histogram)
-    rd->rounds = rounds0 + 1;
-    rd->accepted_max = max(accmax0, nacc);
+    if (lane == kWave - 1) {
+      rd->rpb = static_cast<int>(rpb);
+      rd->nblk = incl;
+      rd->nexp = nexp;
+      rd->nsplit = s1;
+      rd->next_slot = next_slot + nexp;
+      rd->next_frow = next_frow + 2 * nexp;
+      rd->round = ROOT ? 1 : round0 + 1;  // (parity 0 of the first round holds the root histogram)
+      rd->rounds = rounds0 + 1;
+      rd->accepted_max = max(accmax0, nacc);
+    }
   }
   if (tid < kMaxRoundExp) {
     rd->cur[tid][0] = rd->cur[tid][1] = 0;
@@ -1830,32 +1932,43 @@ bool RoundSimpleGains(const KArgs& a) {
   return !p.use_l1 && !p.use_max_output && !p.use_smoothing && !p.use_mc;
 }
 
+// the reduce runs in the numerical split-scan launch (KArgs::red_per_exp)
+bool RoundReduceInFind(const KArgs& a) { return a.red_per_exp > 0 && !a.round_dist && a.num_scan > 0; }
+
 template <bool VG, bool PIF>
-void LaunchRoundFindT(const KArgs& a, hipStream_t s) {
+void LaunchRoundFindT(const KArgs& a0, hipStream_t s) {
+  KArgs a = a0;
+  a.red_rows = 0;  // (the categorical launch and voting's global scan: no reduce rows)
+  KArgs an = a;    // the numerical launch: the reduce workgroups in its first grid rows
+  if (!VG && RoundReduceInFind(a0)) {
+    an.red_per_exp = RoundReducePerExp(a0);  // (for this launch's scan workgroup size)
+    an.red_rows = (an.red_per_exp * a.round_k + a.num_scan - 1) / a.num_scan;
+  }
   const int ny = 2 * a.round_k;
   size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
   if (a.plan_in_find) lds = std::max(lds, RoundPlanLds(a.p.num_leaves, a.round_nodes));
   const bool simple = RoundSimpleGains(a);
   const bool narrow = a.p.max_feature_bins <= kWave;
-  const dim3 g(a.num_scan, ny), b(narrow ? kWave : kFindThreads), bc(kFindThreads);
+  const dim3 b(narrow ? kWave : kFindThreads), bc(kFindThreads);
   // (voting global scan: every elected slot, numerical or categorical, in both kernels)
   const int ncat = (a.round_vote && a.p.vote_phase == 2) ? a.num_scan : a.p.has_cat;
+  const dim3 gn(a.num_scan, ny + an.red_rows);
   if (a.p.has_cat) {
     if (narrow) {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave, VG, PIF>), g, b, lds, s, a);
-      else hipLaunchKernelGGL((k_round_find<1, false, kWave, VG, PIF>), g, b, lds, s, a);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave, VG, PIF>), gn, b, lds, s, an);
+      else hipLaunchKernelGGL((k_round_find<1, false, kWave, VG, PIF>), gn, b, lds, s, an);
     } else {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads, VG, PIF>), g, b, lds, s, a);
-      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads, VG, PIF>), g, b, lds, s, a);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads, VG, PIF>), gn, b, lds, s, an);
+      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads, VG, PIF>), gn, b, lds, s, an);
     }
     if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads, VG, PIF>), dim3(ncat, ny), bc, lds, s, a);
     else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads, VG, PIF>), dim3(ncat, ny), bc, lds, s, a);
   } else if (narrow) {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave, VG, PIF>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<0, false, kWave, VG, PIF>), g, b, lds, s, a);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave, VG, PIF>), gn, b, lds, s, an);
+    else hipLaunchKernelGGL((k_round_find<0, false, kWave, VG, PIF>), gn, b, lds, s, an);
   } else {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads, VG, PIF>), g, b, lds, s, a);
-    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads, VG, PIF>), g, b, lds, s, a);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads, VG, PIF>), gn, b, lds, s, an);
+    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads, VG, PIF>), gn, b, lds, s, an);
   }
 }
 
@@ -1897,6 +2010,13 @@ void PrepareRoundKernels(int max_lds) {
   AllowRoundSplitLds<4>(max_lds);
   AllowRoundSplitLds<8>(max_lds);
   AllowRoundSplitLds<2, true>(max_lds);
+}
+
+int RoundReducePerExp(const KArgs& a) {
+  const int nt = a.p.max_feature_bins <= kWave ? kWave : kFindThreads;  // (the numerical scan's workgroup)
+  const int nbx = (a.p.total_bins + nt - 1) / nt;
+  const int gy = std::min(4, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk);
+  return nbx * std::max(1, gy);
 }
 
 void RoundRootPlan(const KArgs& a, hipStream_t s) {
@@ -1947,6 +2067,7 @@ void RoundSplitReduce(const KArgs& a, hipStream_t s) {
       else hipLaunchKernelGGL((k_round_hist<0, 2>), grid, dim3(kHistThreads), lds, s, a);
     }
   }
+  if (RoundReduceInFind(a)) return;  // (in the split-scan launch)
   const dim3 rgrid((a.p.total_bins + 255) / 256,
                    std::min(4, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk), a.round_k);
   if (a.hist_units == 1) hipLaunchKernelGGL((k_round_reduce<1>), rgrid, dim3(256), 0, s, a);

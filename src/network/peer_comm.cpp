@@ -226,6 +226,21 @@ class PeerComm : public DeviceComm {
   std::shared_ptr<PeerWindows> shared_;
 };
 
+// the topology the last MakePeerIpcComm found (LGBM_AMD_DeviceCommTopology): JSON
+std::mutex g_topo_mu;
+std::string g_topo = "{}";
+
+const char* LinkName(uint32_t t) {
+  switch (t) {
+    case 4: return "xgmi";  // (HSA_AMD_LINK_INFO_TYPE_XGMI)
+    case 2: return "pcie";
+    case 3: return "infiniband";
+    case 1: return "qpi";
+    case 0: return "hypertransport";
+    default: return "unknown";
+  }
+}
+
 }  // namespace
 
 std::vector<std::shared_ptr<DeviceComm>> MakePeerThreadComms(int num_ranks, double timeout_s, int fail_rank,
@@ -251,10 +266,13 @@ std::shared_ptr<DeviceComm> MakePeerIpcComm(int device_id, double timeout_s) {
   const int n = Network::num_machines(), rank = Network::rank();
   if (n > dev::kMaxPeerBufs) Log::Fatal("peer device comm supports at most %d ranks", dev::kMaxPeerBufs);
   const size_t stage = StageBytesFromEnv(size_t(64) << 20);
+  // devices are identified by PCI bus id, not by ordinal: under per-process device isolation
+  // (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES) every rank's device is ordinal 0
   struct Entry {
     hipIpcMemHandle_t h;
     int32_t device;
     int32_t ok;
+    char bus[32];
   };
   Entry mine{};
   mine.device = device_id;
@@ -262,6 +280,7 @@ std::shared_ptr<DeviceComm> MakePeerIpcComm(int device_id, double timeout_s) {
   std::string why;
   try {
     PCHK(hipSetDevice(device_id));
+    PCHK(hipDeviceGetPCIBusId(mine.bus, static_cast<int>(sizeof(mine.bus)), device_id));
     own = AllocWindow(stage);
     PCHK(hipDeviceSynchronize());
     PCHK(hipIpcGetMemHandle(&mine.h, own));
@@ -275,21 +294,43 @@ std::shared_ptr<DeviceComm> MakePeerIpcComm(int device_id, double timeout_s) {
   std::vector<char*> wins(n, nullptr), opened;
   int32_t ok = 1;
   for (int p = 0; p < n; ++p) ok &= all[p].ok;
+  // this rank's view of the topology: per peer, the same device or the link and hops to it
+  std::string topo = std::string("{\"rank\": ") + std::to_string(rank) + ", \"world\": " + std::to_string(n) +
+                     ", \"device\": " + std::to_string(device_id) + ", \"bus_id\": \"" + mine.bus + "\", \"peers\": [";
   if (ok) {
     try {
       for (int p = 0; p < n; ++p) {
+        all[p].bus[sizeof(all[p].bus) - 1] = '\0';
         if (p == rank) {
           wins[p] = own;
           continue;
         }
-        if (all[p].device != device_id) {
-          int can = 0;
-          PCHK(hipDeviceCanAccessPeer(&can, device_id, all[p].device));
-          if (!can) Log::Fatal("device %d cannot access device %d", device_id, all[p].device);
-          const hipError_t e = hipDeviceEnablePeerAccess(all[p].device, 0);
-          if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) PCHK(e);
+        std::string rec = std::string("{\"rank\": ") + std::to_string(p) + ", \"bus_id\": \"" + all[p].bus + "\"";
+        if (std::strcmp(all[p].bus, mine.bus) == 0) {
+          rec += ", \"same_device\": true";  // (ranks sharing one GPU: tests, rehearsals)
+        } else {
+          int ord = -1;
+          if (hipDeviceGetByPCIBusId(&ord, all[p].bus) != hipSuccess) ord = -1;
           (void)hipGetLastError();
+          if (ord >= 0 && ord != device_id) {
+            int can = 0;
+            PCHK(hipDeviceCanAccessPeer(&can, device_id, ord));
+            if (!can) Log::Fatal("device %s cannot access device %s", mine.bus, all[p].bus);
+            const hipError_t e = hipDeviceEnablePeerAccess(ord, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) PCHK(e);
+            (void)hipGetLastError();
+            uint32_t lt = 0, hops = 0;
+            const bool have = hipExtGetLinkTypeAndHopCount(device_id, ord, &lt, &hops) == hipSuccess;
+            (void)hipGetLastError();
+            rec += std::string(", \"ordinal\": ") + std::to_string(ord) + ", \"peer_access\": true";
+            if (have) rec += std::string(", \"link\": \"") + LinkName(lt) + "\", \"hops\": " + std::to_string(hops);
+          } else {
+            // not visible to this process (device isolation): the mapping enables access lazily
+            rec += ", \"visible\": false";
+          }
         }
+        rec += "}";
+        topo += (topo.back() == '[' ? "" : ", ") + rec;
         void* q = nullptr;
         PCHK(hipIpcOpenMemHandle(&q, all[p].h, hipIpcMemLazyEnablePeerAccess));
         wins[p] = static_cast<char*>(q);
@@ -312,6 +353,12 @@ std::shared_ptr<DeviceComm> MakePeerIpcComm(int device_id, double timeout_s) {
     Log::Fatal("peer device comm setup failed on rank %d: %s", rank,
                why.empty() ? "a peer rank could not map the windows" : why.c_str());
   }
+  topo += "]}";
+  {
+    std::lock_guard<std::mutex> lk(g_topo_mu);
+    g_topo = topo;
+  }
+  Log::Info("peer device comm topology: %s", topo.c_str());
   auto c = std::make_shared<PeerComm>(rank, n, wins, stage, timeout_s > 0 ? timeout_s : 60.0, 0);
   c->Own(own, opened);
   return c;
@@ -330,6 +377,19 @@ int LGBM_AMD_PeerCommInit(int device_id, double timeout_s) {
   } catch (std::exception& e) {
     Log::Warning("%s", e.what());
     return -1;
+  }
+  return 0;
+}
+
+// the topology this rank's peer comm found (JSON: bus ids, same device or link type and hop
+// count per peer); *out_len gets the length, the text is truncated to `len` - 1 bytes
+int LGBM_AMD_DeviceCommTopology(char* out, int len, int* out_len) {
+  std::lock_guard<std::mutex> lk(g_topo_mu);
+  if (out_len != nullptr) *out_len = static_cast<int>(g_topo.size());
+  if (out != nullptr && len > 0) {
+    const size_t n = std::min(static_cast<size_t>(len - 1), g_topo.size());
+    std::memcpy(out, g_topo.data(), n);
+    out[n] = '\0';
   }
   return 0;
 }

@@ -976,6 +976,8 @@ class LambdarankNDCG : public RankingObjective {
     d.rank.sig_min = min_in_;
     d.rank.sig_max = max_in_;
     d.rank.sig_factor = idx_factor_;
+    d.rank.sig_table = table_.data();
+    d.rank.sig_bins = static_cast<int64_t>(table_.size());
     return d;
   }
 

@@ -298,13 +298,13 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);
     HIPCHECK(hipMemcpy(t.data(), a.ktrace, sizeof(long long) * t.size(), hipMemcpyDeviceToHost));
     static const char* names[] = {"stage", "side", "resv", "write", "gather", "tail", "store"};
-    // plans: slot 16 entry time, 17..21 phase times (loads, replay + prediction, records of the
-    // expansions / accepted splits / changed leaves, barrier, sizing), 22 accepted, 23 planned,
-    // 25 the split scan's start
+    // plans: slot 16 entry time, 17..21 phase times (loads, replay, prediction with the records
+    // of the accepted splits / changed leaves beside it and then the expansions' records,
+    // barrier, sizing + plan stores), 22 accepted, 23 planned, 25 the split scan's start
     for (int r = 0; r <= h_round_->rounds && r < L; ++r) {
       const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
       if (o[16] == 0) continue;
-      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay+predict=%.2f records=%.2f sync=%.2f sizing=%.2f us; accepted %lld planned %lld\n",
+      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay=%.2f predict+records=%.2f sync=%.2f sizing+stores=%.2f us; accepted %lld planned %lld\n",
                    r, o[25] != 0 ? (o[16] - o[25]) / 100.0 : 0.0, o[17] / 100.0, o[18] / 100.0, o[19] / 100.0,
                    o[20] / 100.0, o[21] / 100.0, o[22], o[23]);
       if (o[26] != 0) {  // the planning workgroup's scan path, from the first scan workgroup's start

@@ -441,6 +441,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     ra.sig_min = spec.rank.sig_min;
     ra.sig_max = spec.rank.sig_max;
     ra.sig_factor = spec.rank.sig_factor;
+    ra.sig_table = d_sig_table_;
     ra.norm = spec.rank.norm ? 1 : 0;
     ra.rng = d_rank_rng_;
     dev::RankGradients(ra, stream_);
@@ -511,6 +512,12 @@ void GPUTreeLearner::UploadRankTables(const DeviceRankSpec& r, DeviceGradKind ki
     for (size_t i = 0; i < disc.size(); ++i) disc[i] = DCG::Discount(static_cast<data_size_t>(i));
     d_discount_ = Alloc<double>(disc.size());
     HIPCHECK(hipMemcpy(d_discount_, disc.data(), sizeof(double) * disc.size(), hipMemcpyHostToDevice));
+    if (r.sig_table == nullptr || r.sig_bins != dev::kRankSigmoidBins) {
+      Log::Fatal("device lambdarank: the objective's sigmoid table (%lld entries) is not the device's (%d)",
+                 static_cast<long long>(r.sig_bins), dev::kRankSigmoidBins);
+    }
+    d_sig_table_ = Alloc<double>(static_cast<size_t>(r.sig_bins));
+    HIPCHECK(hipMemcpy(d_sig_table_, r.sig_table, sizeof(double) * r.sig_bins, hipMemcpyHostToDevice));
   } else {
     d_rank_rng_ = Alloc<uint32_t>(nq);
     HIPCHECK(hipMemcpy(d_rank_rng_, r.rng_states, sizeof(uint32_t) * nq, hipMemcpyHostToDevice));

@@ -27,6 +27,18 @@ TreeLearner* CreateDeviceTreeLearner(const std::string& learner_type, const Conf
   return nullptr;
 }
 
+// fx64 (two int64 words per bin, 31-bit rows) or fx32 (one packed word, ~16 bits below max |g|
+// per row): gpu_use_dp or gpu_hist_precision=fx64 force fx64; auto picks it for the listwise
+// objectives, whose gradients span orders of magnitude across queries (the fx32 quantum of one
+// query's max |g| erases another's small lambdas: config #4 NDCG@10 0.7911 fx32, 0.7927 fx64,
+// CPU learner 0.7955, profiles/r03_v6_ltr_ndcg_parity.md)
+bool GPUTreeLearner::WideHistograms(const Config& c) {
+  if (c.gpu_use_dp || c.gpu_hist_precision == "fx64") return true;
+  if (c.gpu_hist_precision == "fx32") return false;
+  if (c.gpu_hist_precision != "auto") Log::Fatal("gpu_hist_precision must be auto, fx32 or fx64, got %s", c.gpu_hist_precision.c_str());
+  return c.objective == "lambdarank" || c.objective == "rank_xendcg";
+}
+
 GPUTreeLearner::GPUTreeLearner(const Config* config, Mode mode) : SerialTreeLearner(config), mode_(mode) {}
 
 GPUTreeLearner::~GPUTreeLearner() {
@@ -50,7 +62,7 @@ void GPUTreeLearner::FreeBuffers() {
   d_label_ = d_weights_ = d_label_weight_ = nullptr;
   uploaded_label_src_ = uploaded_weight_src_ = uploaded_lw_src_ = nullptr;
   d_qb_ = nullptr;
-  d_inv_max_dcg_ = d_label_gain_ = d_discount_ = nullptr;
+  d_inv_max_dcg_ = d_label_gain_ = d_discount_ = d_sig_table_ = nullptr;
   d_rank_rng_ = nullptr;
   uploaded_qb_src_ = nullptr;
   d_sample_rng_ = nullptr;
@@ -273,7 +285,7 @@ void GPUTreeLearner::UploadData() {
   HIPCHECK(hipMemcpy(d_group_off_, goff.data(), sizeof(int32_t) * goff.size(), hipMemcpyHostToDevice));
   // histogram column tiles: the split kernel's LDS is the tile histogram (8 or 16 bytes per
   // bin) plus its 16 KiB row list; <= 80 KiB keeps two 1024-thread workgroups per CU
-  hist_units_ = config_->gpu_use_dp ? 2 : 1;
+  hist_units_ = WideHistograms(*config_) ? 2 : 1;
   auto tile_bins_for = [&](int tw) {
     int mx = 0;
     for (int w0 = 0; w0 < wpr; w0 += tw) {
@@ -649,6 +661,13 @@ void GPUTreeLearner::UploadData() {
   if (const char* e = std::getenv("LGBM_AMD_ROUND_GR")) a.round_gr = std::atoi(e);
   a.round_need_div = 0;
   if (const char* e = std::getenv("LGBM_AMD_ROUND_NEED_DIV")) a.round_need_div = std::max(0, std::atoi(e));
+  // single process: the reduce of the large expansions' partials in the split-scan launch
+  // (LGBM_AMD_RED_IN_FIND=0: a kernel of its own)
+  a.red_rows = 0;
+  a.red_per_exp = (!distributed_ && a.round_fused) ? dev::RoundReducePerExp(a) : 0;
+  if (const char* e = std::getenv("LGBM_AMD_RED_IN_FIND")) {
+    if (e[0] == '0') a.red_per_exp = 0;
+  }
   AllocRoundState();
   UploadInteractionMasks();
   AllocSplittable();
@@ -737,7 +756,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     AllocSplittable();
     global_count_.assign(n_leaves, 0);
   }
-  if (config_->gpu_use_dp != (hist_units_ == 2)) {
+  if (WideHistograms(*config_) != (hist_units_ == 2)) {
     Log::Warning("device learner: gpu_use_dp cannot change after training started; keeping %s histograms",
                  hist_units_ == 2 ? "wide" : "packed");
   }

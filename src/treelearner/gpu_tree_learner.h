@@ -319,7 +319,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   uint32_t* h_absmax_ = nullptr;
   double* h_scales_ = nullptr;
   int rows_cap_ = 4096;      // rows per histogram row block (packed fixed-point headroom)
-  int hist_units_ = 1;       // 1 packed (g | h) u64 per bin, 2 wide int64 g / h (gpu_use_dp)
+  int hist_units_ = 1;       // 1 packed (g | h) u64 per bin, 2 wide int64 g / h (WideHistograms)
+  static bool WideHistograms(const Config& c);
   int root_grid_ = 512;
   int split_grid_ = 256;
   int blk_min_rows_ = 2048;
@@ -360,6 +361,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   double* d_inv_max_dcg_ = nullptr;
   double* d_label_gain_ = nullptr;
   double* d_discount_ = nullptr;
+  double* d_sig_table_ = nullptr;  // lambdarank: the objective's sigmoid table
   uint32_t* d_rank_rng_ = nullptr;
   const data_size_t* uploaded_qb_src_ = nullptr;
   // device row sampling (bagging / GOSS)

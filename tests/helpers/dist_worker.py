@@ -50,6 +50,9 @@ def main():
     with open(os.path.join(out_dir, "model_%d.txt" % rank), "w") as f:
         f.write(bst.model_to_string())
     np.save(os.path.join(out_dir, "pred_%d.npy" % rank), bst.predict(X))
+    if torch_dist.device_comm_kind() is not None:
+        with open(os.path.join(out_dir, "topo_%d.json" % rank), "w") as f:
+            json.dump(torch_dist.device_topology(), f)
     torch_dist.shutdown()
 
 

@@ -14,7 +14,8 @@ points at it (default /tmp/refbuild/lightgbm).  The tests skip when it is absent
 * ``test_headline_auc_matches_reference``: a 63-leaf, 255-bin Higgs-shaped run (bench.py's
   generator, 200k rows, 50 trees): the reference and this framework's CPU learner write the same
   tree sections byte for byte, hence the same held-out AUC.  (The device learner's AUC is pinned
-  to the CPU learner's at the full headline size: profiles/r04_auc_parity_500trees.md.)
+  to the CPU learner's at the full headline size: profiles/r04_golden_headline.md and bench.py's
+  auc_ref, pinned in tools/bench_auc_ref.json.)
 """
 import os
 import shutil

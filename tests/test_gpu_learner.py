@@ -160,6 +160,45 @@ def test_listwise_gradients_on_device(gpu_available, objective):
     assert abs(res["gpu"] - res["cpu"]) < 0.02
 
 
+def _last_gradients(bst):
+    import ctypes
+    from lightgbmv1_amd.basic import _LIB, _safe_call
+    n = ctypes.c_int64(0)
+    _safe_call(_LIB.LGBM_AMD_BoosterLastGradients(bst.handle, None, None, ctypes.byref(n)))
+    g = np.zeros(n.value, dtype=np.float32)
+    h = np.zeros(n.value, dtype=np.float32)
+    _safe_call(_LIB.LGBM_AMD_BoosterLastGradients(bst.handle, g.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                                                  h.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(n)))
+    return g, h
+
+
+@pytest.mark.parametrize("extra", [{}, {"lambdarank_norm": False}, {"weighted": True}, {"sigmoid": 2.5}],
+                         ids=["norm", "no_norm", "weighted", "sigmoid"])
+def test_lambdarank_device_gradients_equal_host(gpu_available, extra):
+    """The device LambdaRank kernel replays the reference's accumulation (float sums of each
+    document's lower-side pairs in the sorted order of the higher side, the double sum of its
+    higher-side pairs added at its own position, the host's sigmoid table; reference
+    rank_objective.hpp:139-229): its gradients equal the host objective's bit for bit, from
+    random initial scores with ties (so device GOSS samples the host's rows)."""
+    X, y, group = _rank_data(nq=200, seed=8)
+    rng = np.random.RandomState(2)
+    init = np.round(rng.randn(len(y)) * 2, 1)  # (rounded: tied scores inside queries)
+    extra = dict(extra)
+    weight = None
+    if extra.pop("weighted", False):
+        weight = np.repeat(rng.choice([0.5, 1.0, 2.0], size=len(group)), group).astype(np.float32)
+    out = {}
+    for device in ("cpu", "gpu"):
+        params = dict({"objective": "lambdarank", "num_leaves": 7, "verbose": -1, "device_type": device}, **extra)
+        ds = lgb.Dataset(X, y, group=group, init_score=init, weight=weight, params=params)
+        bst = lgb.Booster(params, ds)
+        bst.update()
+        out[device] = _last_gradients(bst)
+    for k in range(2):
+        assert np.abs(out["cpu"][k]).sum() > 0
+        np.testing.assert_array_equal(out["gpu"][k], out["cpu"][k])
+
+
 def _bag_counts(device, boosting, rounds, fixed_gradients=False, **extra):
     X, y = _data(50000, seed=9)
     params = {"objective": "binary", "num_leaves": 15, "max_bin": 63, "verbose": -1, "device_type": device,

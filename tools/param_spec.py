@@ -210,6 +210,11 @@ p("gpu_use_dp", "bool", False, section=S, doc="accumulate device histograms in f
 # [new] MI355X-specific knobs
 p("hist_rows_per_block", "int", 0, save=False, section=S,
   doc="[new] rows per histogram workgroup (0: auto)")
+p("gpu_hist_precision", "string", "auto", save=False, section=S,
+  doc="[new] device histogram precision: fx32 (per-row 32-bit fixed point (g, h) packed in one "
+      "int64 word), fx64 (two int64 words, 31-bit rows; what gpu_use_dp selects) or auto (fx64 "
+      "for the listwise objectives lambdarank / rank_xendcg, whose per-query gradients span a "
+      "wide dynamic range, else fx32)")
 p("deterministic", "bool", False, save=False, section=S,
   doc="[new] fixed-order device reductions (bitwise reproducible histograms)")
 p("gpu_rccl", "bool", True, save=False, section=S,
