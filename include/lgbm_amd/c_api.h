@@ -237,6 +237,8 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_DatasetGetGroupBins(DatasetHandle handle, int32_t
 LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceLeafState(BoosterHandle handle, int leaf, int32_t* rows, int* count,
                                                       int64_t* hist, int8_t* bin_valid, int64_t* hist_len,
                                                       double* sums);
+/* the gradients the last iteration trained on (device or host learner); *n = entries */
+LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterLastGradients(BoosterHandle handle, float* grad, float* hess, int64_t* n);
 LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceGradients(BoosterHandle handle, float* grad, float* hess,
                                                       double* scales);
 // JSON report of the leaves' device best splits checked against the CPU split finder

@@ -27,6 +27,7 @@
 
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/meta.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 namespace common {
@@ -378,7 +379,7 @@ class PhaseTimer {
   }
   void Reset() { acc_.clear(); cnt_.clear(); }
   ~PhaseTimer() { if (enabled_ && !acc_.empty()) fprintf(stdout, "%s", Report().c_str()); }
-  PhaseTimer() { const char* e = getenv("LGBM_AMD_TIMETAG"); enabled_ = e && e[0] == '1'; }
+  PhaseTimer() { const char* e = tuning::Get(tuning::Knob::Timetag); enabled_ = e && e[0] == '1'; }
   void set_enabled(bool e) { enabled_ = e; }
   const std::map<std::string, double>& totals() const { return acc_; }
 
@@ -399,7 +400,7 @@ struct Roctx {
   static const Roctx& Get() {
     static const Roctx r = [] {
       Roctx x;
-      const char* e = getenv("LGBM_AMD_ROCTX");
+      const char* e = tuning::Get(tuning::Knob::Roctx);
       if (e == nullptr || e[0] != '1') return x;
       void* h = dlopen("libroctx64.so", RTLD_NOW | RTLD_GLOBAL);
       if (h == nullptr) h = dlopen("/opt/rocm/lib/libroctx64.so", RTLD_NOW | RTLD_GLOBAL);

@@ -36,6 +36,7 @@ struct DeviceMetricSpec {
   std::vector<int> eval_at;
   std::vector<double> qconst;
   std::vector<double> label_gain, discount;
+  data_size_t max_query_docs = 0;  // the longest query (queries past kRankMaxDocs: global scratch)
 };
 
 class Metric {

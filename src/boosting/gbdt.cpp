@@ -11,6 +11,7 @@
 #include "lgbm_amd/common.h"
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/network.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -365,7 +366,7 @@ void GBDT::Bagging(int iter) {
 // reference's draw with one sampling block per 1024 rows (see src/device/sample_kernels.hip)
 data_size_t GBDT::DeviceBagging(bool goss) {
   if (device_learner_ == nullptr) return -1;
-  const char* e = std::getenv("LGBM_AMD_HOST_BAGGING");
+  const char* e = tuning::Get(tuning::Knob::HostBagging);
   if (e != nullptr && e[0] == '1') return -1;
   DeviceSampleSpec sp;
   sp.goss = goss;
@@ -390,7 +391,7 @@ data_size_t GBDT::DeviceBagging(bool goss) {
 std::vector<double> GBDT::EvalValid(int i, int j) const {
   const Metric* m = valid_metrics_[i][j];
   const int slot = valid_score_updater_[i]->device_slot();
-  const char* hm = std::getenv("LGBM_AMD_HOST_METRICS");  // =1: every metric on the host (A/B)
+  const char* hm = tuning::Get(tuning::Knob::HostMetrics);  // =1: every metric on the host (A/B)
   const bool host_metrics = hm != nullptr && hm[0] == '1';
   if (slot >= 0 && device_learner_ != nullptr && !host_metrics) {
     const DeviceMetricSpec spec = m->DeviceSpec(objective_);
@@ -401,7 +402,7 @@ std::vector<double> GBDT::EvalValid(int i, int j) const {
 }
 
 std::vector<double> GBDT::EvalTrain(const Metric* m) {
-  const char* hm = std::getenv("LGBM_AMD_HOST_METRICS");
+  const char* hm = tuning::Get(tuning::Knob::HostMetrics);
   if (device_learner_ != nullptr && !(hm != nullptr && hm[0] == '1')) {
     const DeviceMetricSpec spec = m->DeviceSpec(objective_);
     std::vector<double> sums;
@@ -521,7 +522,7 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
   common::ScopedTimer timer("GBDT::TrainOneIter");
   if (!iter_log_checked_) {
     iter_log_checked_ = true;
-    if (const char* path = std::getenv("LGBM_AMD_ITER_LOG")) {
+    if (const char* path = tuning::Get(tuning::Knob::IterLog)) {
       std::string p(path);
       if (Network::num_machines() > 1) p += ".rank" + std::to_string(Network::rank());
       iter_log_.reset(new std::ofstream(p, std::ios::app));

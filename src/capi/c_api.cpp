@@ -31,6 +31,7 @@
 #include "lgbm_amd/objective.h"
 #include "lgbm_amd/predictor.h"
 #include "lgbm_amd/random.h"
+#include "lgbm_amd/tuning.h"
 
 using namespace lgbm_amd;
 
@@ -428,7 +429,7 @@ class Booster {
     if (cfg.pred_early_stop || nrow < 1024) return false;
     if (data_type != C_API_DTYPE_FLOAT32 && data_type != C_API_DTYPE_FLOAT64) return false;
     if (cfg.device_type != "gpu" && config_.device_type != "gpu") return false;
-    const char* e = std::getenv("LGBM_AMD_HOST_PREDICT");
+    const char* e = tuning::Get(tuning::Knob::HostPredict);
     if (e != nullptr && e[0] == '1') return false;
     if (!cfg.predict_disable_shape_check && ncol != boosting_->MaxFeatureIdx() + 1) return false;  // host path reports it
     std::unique_lock<std::shared_mutex> l(mu_);

@@ -19,6 +19,7 @@
 #include "lgbm_amd/dataset.h"
 #include "lgbm_amd/device_binning.h"
 #include "lgbm_amd/log.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -114,7 +115,7 @@ int BinningDevice(const Config& cfg) {
 }  // namespace
 
 bool UseDeviceBinning(const Config& cfg, int64_t nrow, int64_t ncol) {
-  const char* e = std::getenv("LGBM_AMD_DEVICE_BINNING");
+  const char* e = tuning::Get(tuning::Knob::DeviceBinning);
   if (e != nullptr && e[0] == '0') return false;
   const bool forced = e != nullptr && e[0] == '1';
   if (!forced && (cfg.device_type != "gpu" || nrow * ncol < (int64_t{1} << 22))) return false;

@@ -378,12 +378,24 @@ __device__ __forceinline__ bool DirectPartials(const KArgs& a, int nblk, int spl
   return !a.p.data_parallel && (nblk <= kDirectChunk || split >= a.p.direct_from_split);
 }
 
-// (g, h) of partial word(s) v: packed (g in the signed high half, h in the low half) or wide
+// max |h| with the sign bit set when any h is negative (k_scales then keeps the packed h half
+// signed): the hessian maxima of the gradient / packing kernels and their reductions
+__device__ __forceinline__ float HessMax(float a, float b) {
+  const unsigned s = (__float_as_uint(a) | __float_as_uint(b)) & 0x80000000u;
+  return __uint_as_float(__float_as_uint(fmaxf(fabsf(a), fabsf(b))) | s);
+}
+
+// (g, h) of partial word(s) v: packed (g in the signed high half, h in the low half) or wide.
+// A packed word is g * 2^32 + h.  h lies in [0, 2^31] when no hessian is negative and in
+// [-2^30, 2^30] otherwise (k_scales): the two ranges decode apart, a low half from 3 * 2^30 on
+// being a negative h (whose borrow is returned to g).
 __device__ __forceinline__ void UnpackPartial(unsigned long long v0, unsigned long long v1, int units, long long* g,
                                               long long* h) {
   if (units == 1) {
-    *g = static_cast<long long>(v0) >> 32;  // h (low half) is non-negative: no borrow
-    *h = static_cast<long long>(v0 & 0xffffffffull);
+    const unsigned lo = static_cast<unsigned>(v0);
+    const long long hv = lo >= 0xC0000000u ? static_cast<long long>(lo) - (1ll << 32) : static_cast<long long>(lo);
+    *g = static_cast<long long>(v0 - static_cast<unsigned long long>(hv)) >> 32;
+    *h = hv;
   } else {
     *g = static_cast<long long>(v0);
     *h = static_cast<long long>(v1);

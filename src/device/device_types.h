@@ -229,10 +229,6 @@ struct Round {
   // voting-parallel: the fixed-point (g, h) sums of each expansion's histogrammed child over
   // this rank's rows (its local sums; the other child's are the parent's minus these)
   unsigned long long loc_acc[kMaxRoundExp][2];
-  // reduce workgroups of each expansion finished in this round's split-scan launch
-  // (KArgs::red_per_exp; zeroed by the round's split kernel, whose launch follows every reduce
-  // of the previous round)
-  uint32_t red_cnt[kMaxRoundExp];
   ExpPlan e[kMaxRoundExp];
 };
 

@@ -46,6 +46,7 @@ struct KArgs {
   unsigned long long* partials;
   const double* scales;      // [scale_g, scale_h, 1/scale_g, 1/scale_h] of the current tree
   double* root;              // [sum_g, sum_h, count]
+  double* root_blk;          // [2 * 2 * CUs] per-workgroup partials of RootSum (summed in a fixed order)
   int32_t num_rows;          // local rows in the root (or the explicit range); upper bound if num_rows_dev
   const int32_t* num_rows_dev;  // root rows held on the device (a bag drawn on the device), or null
   int32_t root_identity;     // root rows are 0..num_rows-1 (indices written by the root pass)
@@ -194,13 +195,6 @@ struct KArgs {
   int32_t round_gr;    // independent row gathers per thread in its histogram phase (2, 4, 8)
   int32_t round_fused;  // 1: partition + histograms in one kernel (k_round_split), 0: two (k_round_part, k_round_hist)
   int32_t plan_in_find;  // the round's last split-scan workgroup plans (else k_round_plan)
-  // single-process rounds: the reduce of the large expansions' partials runs as the first
-  // workgroups of the numerical split-scan launch instead of a kernel of its own (one launch and
-  // its gap less per round).  red_per_exp: reduce workgroups per expansion (0: a separate
-  // k_round_reduce); red_rows: grid rows of reduce workgroups in front of the scans (set per
-  // launch; 0: none in this launch)
-  int32_t red_per_exp;
-  int32_t red_rows;
   // distributed round growth (data- / feature-parallel): per-feature results rank-major,
   // [world][2 * round_k][max_owned] (a rank's local feature index from fb_index), all-gathered
   // before k_round_childbest; data-parallel: the round's histograms reduced into round_send
@@ -276,6 +270,7 @@ int PackBlocks(int64_t n);
 void ComputeScales(const uint32_t* absmax, int rows_cap, int hist_units, double* scales, hipStream_t s);
 void TreeBegin(const KArgs& a, hipStream_t s);
 void RootSum(const KArgs& a, hipStream_t s);
+int RootSumBlocks();  // (KArgs::root_blk holds 2 doubles per block)
 // histograms: per-row-block partials, then an exact int64 reduction into scratch buffer 0
 void HistRoot(const KArgs& a, hipStream_t s);
 void HistRange(const KArgs& a, hipStream_t s);  // rows idx[range_begin, +num_rows)
@@ -309,8 +304,6 @@ void PickStep(const KArgs& a, hipStream_t s, bool root);
 // then per round the fused partition + histogram of every expansion, the reduction of their
 // large histograms, the children's split scans (+ each child's best split), and the plan
 // (replay of the best-first order, next expansions).  A finished tree's kernels exit at once.
-// reduce workgroups per expansion when the reduce runs in the split-scan launch (KArgs::red_per_exp)
-int RoundReducePerExp(const KArgs& a);
 void RoundRootPlan(const KArgs& a, hipStream_t s);
 void RoundStep(const KArgs& a, hipStream_t s);  // single process: split + reduce + scans (+ plan)
 // distributed rounds: the collectives go between the parts
@@ -452,6 +445,13 @@ struct RankArgs {
   const double* sig_table;    // [kRankSigmoidBins] the host objective's sigmoid table (lambdarank)
   int32_t norm;               // lambdarank_norm
   uint32_t* rng;              // [num_queries] LCG states (xendcg), advanced in place
+  // queries of more than kRankMaxDocs documents (one 1024-thread workgroup each over a global
+  // scratch of their rows instead of LDS): their indices and [num_data] scratch arrays
+  const int32_t* big_q;
+  int32_t num_big;
+  double *big_d0, *big_d1;
+  float* big_f;
+  int32_t *big_i0, *big_i1, *big_i2;
 };
 void RankGradients(const RankArgs& ra, hipStream_t s);
 
@@ -532,7 +532,8 @@ struct MetricArgs {
                            // AUC-mu: [num_class][num_class] auc_mu_weights
   const double* label_gain;
   const double* discount;  // [kRankMaxDocs]
-  void* scratch;         // MetricScratchBytes(n, nq * nk)
+  int32_t big;           // a query has more than kRankMaxDocs documents (scratch then holds n rows)
+  void* scratch;         // MetricScratchBytes(n, nq * nk) (query metrics: n = 0 unless big)
   double* out;           // [0] weighted loss sum (or AUC accumulator), [1] AUC positive weight; query: [nk];
                          // AUC-mu: per class pair (i < j) accumulator and class-j count
 };

@@ -232,6 +232,7 @@ T* Carve(char** p, size_t count) {
 // rank_kernels.hip), then the query's NDCG@k / MAP@k for every k into partials[q][nk]
 constexpr int kQueryThreads = 128;
 
+template <int NT>
 __device__ __forceinline__ double QBlockSum(double v, double* red) {
   for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   const int w = threadIdx.x / kWave;
@@ -239,25 +240,21 @@ __device__ __forceinline__ double QBlockSum(double v, double* red) {
   if ((threadIdx.x & (kWave - 1)) == 0) red[w] = v;
   __syncthreads();
   double t = 0.0;
-  for (int i = 0; i < kQueryThreads / kWave; ++i) t += red[i];
+  for (int i = 0; i < NT / kWave; ++i) t += red[i];
   return t;
 }
 
-__global__ __launch_bounds__(kQueryThreads) void k_query_metric(MetricArgs m, double* partials) {
-  __shared__ double s_score[kRankMaxDocs];
-  __shared__ int s_pos[kRankMaxDocs];
-  __shared__ char s_rel[kRankMaxDocs];
-  __shared__ int s_label[kRankMaxDocs];
-  __shared__ double red[kQueryThreads / kWave];
-  const int q = blockIdx.x;
+template <int NT>
+__device__ void QueryMetricBody(const MetricArgs& m, int q, double* partials, double* s_score, int* s_pos,
+                                char* s_rel, int* s_label, double* red) {
   const int b = m.qb[q], cnt = m.qb[q + 1] - b;
-  for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     s_score[i] = m.score[b + i];
     s_label[i] = static_cast<int>(m.label[b + i]);
     s_rel[i] = m.label[b + i] > 0.5f ? 1 : 0;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     const double si = s_score[i];
     int p = 0;
     for (int j = 0; j < cnt; ++j) p += (s_score[j] > si) || (s_score[j] == si && j < i);
@@ -273,7 +270,7 @@ __global__ __launch_bounds__(kQueryThreads) void k_query_metric(MetricArgs m, do
       if (m.qconst[static_cast<int64_t>(q) * m.nk] <= 0.0) {
         v = threadIdx.x == 0 ? 1.0 : 0.0;  // no relevant document: NDCG 1
       } else {
-        for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+        for (int i = threadIdx.x; i < cnt; i += NT) {
           if (s_pos[i] < k) v += m.label_gain[s_label[i]] * m.discount[s_pos[i]];
         }
         v *= inv;
@@ -281,7 +278,7 @@ __global__ __launch_bounds__(kQueryThreads) void k_query_metric(MetricArgs m, do
     } else {
       const int npos = static_cast<int>(m.qconst[q]);
       // precision at every relevant document ranked within k: (relevant ranked above + 1) / (rank + 1)
-      for (int i = threadIdx.x; i < cnt; i += kQueryThreads) {
+      for (int i = threadIdx.x; i < cnt; i += NT) {
         if (!s_rel[i] || s_pos[i] >= k) continue;
         int hits = 0;
         for (int j = 0; j < cnt; ++j) hits += s_rel[j] && s_pos[j] < s_pos[i];
@@ -289,9 +286,32 @@ __global__ __launch_bounds__(kQueryThreads) void k_query_metric(MetricArgs m, do
       }
       v = npos > 0 ? v / min(npos, k) : (threadIdx.x == 0 ? 1.0 : 0.0);
     }
-    const double t = QBlockSum(v, red);
+    const double t = QBlockSum<NT>(v, red);
     if (threadIdx.x == 0) partials[static_cast<int64_t>(q) * m.nk + kk] = t * w;
   }
+}
+
+__global__ __launch_bounds__(kQueryThreads) void k_query_metric(MetricArgs m, double* partials) {
+  __shared__ double s_score[kRankMaxDocs];
+  __shared__ int s_pos[kRankMaxDocs];
+  __shared__ char s_rel[kRankMaxDocs];
+  __shared__ int s_label[kRankMaxDocs];
+  __shared__ double red[kQueryThreads / kWave];
+  const int q = blockIdx.x;
+  if (m.qb[q + 1] - m.qb[q] > kRankMaxDocs) return;  // (k_query_metric_big)
+  QueryMetricBody<kQueryThreads>(m, q, partials, s_score, s_pos, s_rel, s_label, red);
+}
+
+// queries of more than kRankMaxDocs documents (MetricArgs::big): the same body over the query's
+// rows of a global scratch, one 1024-thread workgroup each
+constexpr int kQueryBigThreads = 1024;
+__global__ __launch_bounds__(kQueryBigThreads) void k_query_metric_big(MetricArgs m, double* partials, double* g_score,
+                                                                        int* g_pos, char* g_rel, int* g_label) {
+  __shared__ double red[kQueryBigThreads / kWave];
+  const int q = blockIdx.x;
+  const int b = m.qb[q];
+  if (m.qb[q + 1] - b <= kRankMaxDocs) return;
+  QueryMetricBody<kQueryBigThreads>(m, q, partials, g_score + b, g_pos + b, g_rel + b, g_label + b, red);
 }
 
 // one workgroup per k: the queries' values summed in query order (block-strided, then a
@@ -336,6 +356,14 @@ void EvalMetric(const MetricArgs& m, hipStream_t s) {
   if (m.kind == kMetricNDCG || m.kind == kMetricMAP) {
     double* qpart = Carve<double>(&p, static_cast<size_t>(std::max(1, m.nq * m.nk)));
     hipLaunchKernelGGL(k_query_metric, dim3(m.nq), dim3(kQueryThreads), 0, s, m, qpart);
+    if (m.big) {
+      const size_t n = static_cast<size_t>(std::max<int64_t>(1, m.n));
+      double* gs = Carve<double>(&p, n);
+      int* gp = Carve<int>(&p, n);
+      int* gl = Carve<int>(&p, n);
+      char* gr = Carve<char>(&p, n);
+      hipLaunchKernelGGL(k_query_metric_big, dim3(m.nq), dim3(kQueryBigThreads), 0, s, m, qpart, gs, gp, gr, gl);
+    }
     hipLaunchKernelGGL(k_query_sum, dim3(m.nk), dim3(kMetricThreads), 0, s, qpart, m.nq, m.nk, m.out);
     return;
   }

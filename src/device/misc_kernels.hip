@@ -1,6 +1,7 @@
 // Small per-tree kernels of the MI355X learner: gradient packing + fixed-point scale
 // selection, tree reset, root statistics and score arithmetic.
 #include "device_common.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 namespace dev {
@@ -14,8 +15,8 @@ int NumCUs() { return g_num_cus; }
 void SetNumCUs(int n) { g_num_cus = n > 0 ? n : 256; }
 int HistGridBlocks() {
   static const int per_cu = [] {  // LGBM_AMD_ROOT_WG_PER_CU (A/B knob; default 2)
-    const char* e = std::getenv("LGBM_AMD_ROOT_WG_PER_CU");
-    return e != nullptr && std::atoi(e) > 0 ? std::atoi(e) : 2;
+    const char* e = tuning::Get(tuning::Knob::RootWgPerCu);
+    return e != nullptr && std::atoi(e) > 0 ? std::atoi(e) : tuning::kRootWgPerCu;
   }();
   return per_cu * g_num_cus;
 }
@@ -31,11 +32,11 @@ __global__ __launch_bounds__(256) void k_pack_gh(const float* __restrict__ g, co
     const float a = g[i], b = h[i];
     gh[i * stride] = make_float2(a, b);
     mg = fmaxf(mg, fabsf(a));
-    mh = fmaxf(mh, fabsf(b));
+    mh = HessMax(mh, b);
   }
   for (int o = 32; o > 0; o >>= 1) {
     mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
-    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+    mh = HessMax(mh, __shfl_xor(mh, o, kWave));
   }
   __shared__ float smg[4], smh[4];
   const int w = threadIdx.x >> 6;
@@ -47,7 +48,7 @@ __global__ __launch_bounds__(256) void k_pack_gh(const float* __restrict__ g, co
   if (threadIdx.x == 0) {
     for (int i = 1; i < static_cast<int>(blockDim.x >> 6); ++i) {
       mg = fmaxf(mg, smg[i]);
-      mh = fmaxf(mh, smh[i]);
+      mh = HessMax(mh, smh[i]);
     }
     max_parts[2 * blockIdx.x] = mg;
     max_parts[2 * blockIdx.x + 1] = mh;
@@ -64,14 +65,15 @@ void PackGH(const float* g, const float* h, GH* gh, int64_t gh_stride, int64_t n
 }
 
 // scale = 2^k per component.  Packed (units 1): rows_cap * max * scale <= 2^30 (g: signed
-// high half of the packed word) and <= 2^31 (h: low half) -- a row block never holds more
-// than rows_cap rows.  Wide (units 2): max * scale <= 2^31, so each row keeps 31 bits of
+// high half of the packed word) and <= 2^31 (h: low half; 2^30 when absmax[3] flags a negative
+// hessian, see UnpackPartial) -- a row block never holds more than rows_cap rows.  Wide (units 2): max * scale <= 2^31, so each row keeps 31 bits of
 // max |g| (every fp32 gradient within 2^-7 of the maximum exactly) and sums over up to 2^31
 // rows stay inside int64.  absmax[2] (if set) carries the row cap of all ranks.
 __global__ void k_scales(const uint32_t* absmax, int rows_cap, int units, double* scales) {
   if (threadIdx.x != 0) return;
   if (absmax[2] != 0u) rows_cap = static_cast<int>(absmax[2]);
-  const double lim[2] = {units == 1 ? 1073741824.0 : 2147483648.0, 2147483648.0};
+  const double lim[2] = {units == 1 ? 1073741824.0 : 2147483648.0,
+                        units == 1 && absmax[3] != 0u ? 1073741824.0 : 2147483648.0};
   const double rows = units == 1 ? static_cast<double>(rows_cap) : 1.0;
   for (int k = 0; k < 2; ++k) {
     const double m = static_cast<double>(__uint_as_float(absmax[k]));
@@ -166,16 +168,35 @@ __global__ __launch_bounds__(256) void k_root_sum(KArgs a) {
   sg = BlockSum(sg, sh);
   shh = BlockSum(shh, sh);
   if (threadIdx.x == 0) {
-    atomicAdd(&a.root[0], sg);
-    atomicAdd(&a.root[1], shh);
-    if (blockIdx.x == 0) atomicAdd(&a.root[2], static_cast<double>(n));
+    a.root_blk[2 * blockIdx.x] = sg;
+    a.root_blk[2 * blockIdx.x + 1] = shh;
   }
 }
 
+// the workgroups' partials summed in a fixed order: the same sums on every run (float atomics
+// across workgroups would add in arrival order)
+__global__ __launch_bounds__(256) void k_root_finish(KArgs a, int nblk) {
+  __shared__ double sh[8];
+  double sg = 0.0, shh = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+    sg += a.root_blk[2 * b];
+    shh += a.root_blk[2 * b + 1];
+  }
+  sg = BlockSum(sg, sh);
+  shh = BlockSum(shh, sh);
+  if (threadIdx.x == 0) {
+    a.root[0] = sg;
+    a.root[1] = shh;
+    a.root[2] = static_cast<double>(RootRows(a));
+  }
+}
+
+int RootSumBlocks() { return 2 * NumCUs(); }
+
 void RootSum(const KArgs& a, hipStream_t s) {
-  (void)hipMemsetAsync(a.root, 0, sizeof(double) * 3, s);  // accumulated with atomics below
-  const int blocks = std::max(1, std::min((a.num_rows + 255) / 256, 2 * NumCUs()));
+  const int blocks = std::max(1, std::min((a.num_rows + 255) / 256, RootSumBlocks()));
   hipLaunchKernelGGL(k_root_sum, dim3(blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(k_root_finish, dim3(1), dim3(256), 0, s, a, blocks);
 }
 
 // ---------------------------------------------------------------- elementwise

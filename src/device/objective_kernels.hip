@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
       if (ga.gh != nullptr) {
         reinterpret_cast<float2*>(ga.gh)[i * ga.gh_stride] = make_float2(gf, hf);
         mg = fmaxf(mg, fabsf(gf));
-        mh = fmaxf(mh, fabsf(hf));
+        mh = HessMax(mh, hf);
         sg += gf;
         shh += hf;
       }
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
   __shared__ double ssg[4], ssh[4];
   for (int o = 32; o > 0; o >>= 1) {
     mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
-    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+    mh = HessMax(mh, __shfl_xor(mh, o, kWave));
     sg += __shfl_xor(sg, o, kWave);
     shh += __shfl_xor(shh, o, kWave);
   }
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
     double tg = 0.0, th = 0.0;
     for (int i = 0; i < static_cast<int>(blockDim.x >> 6); ++i) {
       mg = fmaxf(mg, smg[i]);
-      mh = fmaxf(mh, smh[i]);
+      mh = HessMax(mh, smh[i]);
       tg += ssg[i];
       th += ssh[i];
     }
@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kReducePartsThreads) void k_reduce_parts(const floa
   float x = 0.f, y = 0.f;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) {
     x = fmaxf(x, max_parts[2 * i]);
-    y = fmaxf(y, max_parts[2 * i + 1]);
+    y = HessMax(y, max_parts[2 * i + 1]);
     if (root_parts != nullptr) {
       a += root_parts[2 * i];
       b += root_parts[2 * i + 1];
@@ -110,15 +110,15 @@ __global__ __launch_bounds__(kReducePartsThreads) void k_reduce_parts(const floa
       sg[threadIdx.x] += sg[threadIdx.x + o];
       sh[threadIdx.x] += sh[threadIdx.x + o];
       mg[threadIdx.x] = fmaxf(mg[threadIdx.x], mg[threadIdx.x + o]);
-      mh[threadIdx.x] = fmaxf(mh[threadIdx.x], mh[threadIdx.x + o]);
+      mh[threadIdx.x] = HessMax(mh[threadIdx.x], mh[threadIdx.x + o]);
     }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     absmax[0] = __float_as_uint(mg[0]);  // non-negative floats order like their bit patterns
-    absmax[1] = __float_as_uint(mh[0]);
+    absmax[1] = __float_as_uint(fabsf(mh[0]));
     absmax[2] = static_cast<uint32_t>(rows_cap);  // (the row cap, max over ranks after the all-reduce)
-    absmax[3] = 0u;
+    absmax[3] = signbit(mh[0]) ? 1u : 0u;         // (a negative hessian: signed packed h)
     if (root != nullptr) {
       root[0] = sg[0];
       root[1] = sh[0];

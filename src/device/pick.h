@@ -652,6 +652,10 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
   //    wave's loads; one-wave workgroups: by the wave's first thread, before the pick)
   if (root) {
     if (tid == 0) {
+      // the tree's global root rows, on every rank (the scan of inner feature 0 publishes them
+      // too, but a distributed rank that does not own that feature never runs it): the host
+      // replays the tree's by-node / extra_trees draws only when the root was scanned
+      st->root_count = static_cast<int>(a.root[2]);
       pl->s = 0;
       pl->fresh = 1;
       pl->sm = 0;

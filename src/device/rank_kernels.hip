@@ -1,29 +1,31 @@
 // Listwise ranking gradients on device: LambdaRank-NDCG and XE-NDCG, one workgroup per
 // query (reference src/objective/rank_objective.hpp:98-285 lambdarank, :288-366 xendcg).
 //
-// A query's documents are staged in LDS (score, label, rank position).  The stable
-// descending sort of the reference (std::stable_sort by score) is computed as a rank:
-// pos(d) = #{j : s_j > s_d} + #{j < d : s_j == s_d}, O(cnt^2 / threads) LDS broadcasts
-// (queries are short: MS-LTR averages ~120 documents).  Every document then accumulates
-// its lambda / hessian over the pairs it takes part in -- as the higher-labelled side
-// (the reference's inner loop) and as the lower-labelled side (its `lambdas[low] -=`) --
-// in double, so no atomics are needed and the result does not depend on scheduling.
-// The sum of |lambdas| used by lambdarank_norm is a workgroup reduction in double.
+// A query's documents are staged in LDS (score, label, rank position), or -- queries of more
+// than kRankMaxDocs documents -- in a global scratch of the query's own rows, scanned by a
+// 1024-thread workgroup (the same code over other storage).  The stable descending sort of the
+// reference (std::stable_sort by score) is computed as a rank:
+// pos(d) = #{j : s_j > s_d} + #{j < d : s_j == s_d}, O(cnt^2 / threads) broadcasts
+// (queries are short: MS-LTR averages ~120 documents).  Every document then accumulates its
+// lambda / hessian over the pairs it takes part in in the reference's order (below), so no
+// atomics are needed and the result does not depend on scheduling.
 #include "device_common.h"
 
 namespace lgbm_amd {
 namespace dev {
 
-constexpr int kRankThreads = 128;  // two waves per query
+constexpr int kRankThreads = 128;      // two waves per query
+constexpr int kRankBigThreads = 1024;  // queries of more than kRankMaxDocs documents
 
-__device__ __forceinline__ double BlockSum(double v, double* red) {
+template <int NT>
+__device__ __forceinline__ double RankBlockSum(double v, double* red) {
   for (int o = kWave / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   const int w = threadIdx.x / kWave;
   __syncthreads();  // red may still be read by a previous reduction
   if ((threadIdx.x & (kWave - 1)) == 0) red[w] = v;
   __syncthreads();
   double t = 0.0;
-  for (int i = 0; i < kRankThreads / kWave; ++i) t += red[i];
+  for (int i = 0; i < NT / kWave; ++i) t += red[i];
   return t;
 }
 
@@ -46,23 +48,18 @@ __device__ __forceinline__ double RankSigmoid(const RankArgs& ra, double x) {
 // normalisation's sum of |lambdas| is a workgroup reduction in double: it differs from the host's
 // sequential sum in its last bits only, which reach a float gradient through the log2 factor with
 // probability ~2^-29.)
-__global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
+template <int NT>
+__device__ void LambdarankQuery(const RankArgs& ra, int q, double* s_score, int* s_label, int* s_pos, int* s_doc,
+                                double* s_red, double* s_edge) {
 #pragma clang fp contract(off)
-  __shared__ double s_score[kRankMaxDocs];
-  __shared__ int s_label[kRankMaxDocs];
-  __shared__ int s_pos[kRankMaxDocs];  // document -> sorted position
-  __shared__ int s_doc[kRankMaxDocs];  // sorted position -> document
-  __shared__ double s_red[kRankThreads / kWave];
-  __shared__ double s_edge[3];  // score at sorted positions 0, cnt-1, cnt-2
-  const int q = blockIdx.x;
   const int b = ra.qb[q];
   const int cnt = ra.qb[q + 1] - b;
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     s_score[i] = ra.score[b + i];
     s_label[i] = static_cast<int>(ra.label[b + i]);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     const double si = s_score[i];
     int p = 0;
     for (int j = 0; j < cnt; ++j) {
@@ -96,7 +93,7 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
     *ph_out = ph;
   };
   double sum_lambdas = 0.0;
-  for (int d = threadIdx.x; d < cnt; d += kRankThreads) {
+  for (int d = threadIdx.x; d < cnt; d += NT) {
     const double sd = s_score[d];
     const int ld = s_label[d], kd = s_pos[d];
     const double disc_d = ra.discount[kd];
@@ -135,11 +132,11 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
     ra.grad[b + d] = lam;
     ra.hess[b + d] = hes;
   }
-  const double total = BlockSum(sum_lambdas, s_red);
+  const double total = RankBlockSum<NT>(sum_lambdas, s_red);
   const bool renorm = ra.norm != 0 && total > 0;
   const double nf = renorm ? log2(1 + total) / total : 1.0;
   if (!renorm && ra.weights == nullptr) return;
-  for (int d = threadIdx.x; d < cnt; d += kRankThreads) {
+  for (int d = threadIdx.x; d < cnt; d += NT) {
     float g = ra.grad[b + d], h = ra.hess[b + d];
     if (renorm) {
       g = static_cast<float>(g * nf);
@@ -154,36 +151,54 @@ __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
   }
 }
 
+__global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
+  __shared__ double s_score[kRankMaxDocs];
+  __shared__ int s_label[kRankMaxDocs];
+  __shared__ int s_pos[kRankMaxDocs];  // document -> sorted position
+  __shared__ int s_doc[kRankMaxDocs];  // sorted position -> document
+  __shared__ double s_red[kRankThreads / kWave];
+  __shared__ double s_edge[3];  // score at sorted positions 0, cnt-1, cnt-2
+  const int q = blockIdx.x;
+  if (ra.qb[q + 1] - ra.qb[q] > kRankMaxDocs) return;  // (k_lambdarank_big)
+  LambdarankQuery<kRankThreads>(ra, q, s_score, s_label, s_pos, s_doc, s_red, s_edge);
+}
+
+// queries of more than kRankMaxDocs documents: the same body over the query's rows of a global
+// scratch (RankArgs::big_*)
+__global__ __launch_bounds__(kRankBigThreads) void k_lambdarank_big(RankArgs ra) {
+  __shared__ double s_red[kRankBigThreads / kWave];
+  __shared__ double s_edge[3];
+  const int q = ra.big_q[blockIdx.x];
+  const int b = ra.qb[q];
+  LambdarankQuery<kRankBigThreads>(ra, q, ra.big_d0 + b, ra.big_i0 + b, ra.big_i1 + b, ra.big_i2 + b, s_red, s_edge);
+}
+
 // XE-NDCG (reference rank_objective.hpp:304-366): softmax over the query, per-document
 // gamma draws from the query's own LCG (state advanced in place across iterations).
-__global__ __launch_bounds__(kRankThreads) void k_xendcg(RankArgs ra) {
-  __shared__ double s_rho[kRankMaxDocs];
-  __shared__ double s_par[kRankMaxDocs];
-  __shared__ float s_lam[kRankMaxDocs];
-  __shared__ double s_red[kRankThreads / kWave];
-  const int q = blockIdx.x;
+template <int NT>
+__device__ void XendcgQuery(const RankArgs& ra, int q, double* s_rho, double* s_par, float* s_lam, double* s_red) {
   const int b = ra.qb[q];
   const int cnt = ra.qb[q + 1] - b;
   if (cnt <= 1) {
-    for (int i = threadIdx.x; i < cnt; i += kRankThreads) ra.grad[b + i] = ra.hess[b + i] = 0.0f;
+    for (int i = threadIdx.x; i < cnt; i += NT) ra.grad[b + i] = ra.hess[b + i] = 0.0f;
     return;
   }
   // softmax (common::Softmax: max shift, exp, normalise)
   double mx = -INFINITY;
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) mx = fmax(mx, ra.score[b + i]);
+  for (int i = threadIdx.x; i < cnt; i += NT) mx = fmax(mx, ra.score[b + i]);
   for (int o = kWave / 2; o > 0; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o, kWave));
   __syncthreads();
   if ((threadIdx.x & (kWave - 1)) == 0) s_red[threadIdx.x / kWave] = mx;
   __syncthreads();
   mx = s_red[0];
-  for (int i = 1; i < kRankThreads / kWave; ++i) mx = fmax(mx, s_red[i]);
+  for (int i = 1; i < NT / kWave; ++i) mx = fmax(mx, s_red[i]);
   double den = 0.0;
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     const double e = exp(ra.score[b + i] - mx);
     s_rho[i] = e;
     den += e;
   }
-  den = BlockSum(den, s_red);
+  den = RankBlockSum<NT>(den, s_red);
   // gamma draws: the query's LCG is sequential over its documents
   if (threadIdx.x == 0) {
     unsigned st = ra.rng[q];
@@ -196,29 +211,29 @@ __global__ __launch_bounds__(kRankThreads) void k_xendcg(RankArgs ra) {
   }
   __syncthreads();
   double sp = 0.0;
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     s_rho[i] /= den;
     sp += s_par[i];
   }
-  sp = BlockSum(sp, s_red);
+  sp = RankBlockSum<NT>(sp, s_red);
   const double inv_den = 1.0 / fmax(kEpsilon, sp);
   double s1 = 0.0;
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     const double term = -s_par[i] * inv_den + s_rho[i];
     s_lam[i] = static_cast<float>(term);
     s_par[i] = term / (1. - s_rho[i]);
     s1 += s_par[i];
   }
-  s1 = BlockSum(s1, s_red);
+  s1 = RankBlockSum<NT>(s1, s_red);
   double s2 = 0.0;
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     const double term = s_rho[i] * (s1 - s_par[i]);
     s_lam[i] += static_cast<float>(term);
     s_par[i] = term / (1. - s_rho[i]);
     s2 += s_par[i];
   }
-  s2 = BlockSum(s2, s_red);
-  for (int i = threadIdx.x; i < cnt; i += kRankThreads) {
+  s2 = RankBlockSum<NT>(s2, s_red);
+  for (int i = threadIdx.x; i < cnt; i += NT) {
     float lam = s_lam[i] + static_cast<float>(s_rho[i] * (s2 - s_par[i]));
     float hes = static_cast<float>(s_rho[i] * (1.0 - s_rho[i]));
     if (ra.weights != nullptr) {
@@ -230,12 +245,31 @@ __global__ __launch_bounds__(kRankThreads) void k_xendcg(RankArgs ra) {
   }
 }
 
+__global__ __launch_bounds__(kRankThreads) void k_xendcg(RankArgs ra) {
+  __shared__ double s_rho[kRankMaxDocs];
+  __shared__ double s_par[kRankMaxDocs];
+  __shared__ float s_lam[kRankMaxDocs];
+  __shared__ double s_red[kRankThreads / kWave];
+  const int q = blockIdx.x;
+  if (ra.qb[q + 1] - ra.qb[q] > kRankMaxDocs) return;  // (k_xendcg_big)
+  XendcgQuery<kRankThreads>(ra, q, s_rho, s_par, s_lam, s_red);
+}
+
+__global__ __launch_bounds__(kRankBigThreads) void k_xendcg_big(RankArgs ra) {
+  __shared__ double s_red[kRankBigThreads / kWave];
+  const int q = ra.big_q[blockIdx.x];
+  const int b = ra.qb[q];
+  XendcgQuery<kRankBigThreads>(ra, q, ra.big_d0 + b, ra.big_d1 + b, ra.big_f + b, s_red);
+}
+
 void RankGradients(const RankArgs& ra, hipStream_t s) {
   if (ra.num_queries <= 0) return;
   if (ra.kind == kRankKindLambdarank) {
     hipLaunchKernelGGL(k_lambdarank, dim3(ra.num_queries), dim3(kRankThreads), 0, s, ra);
+    if (ra.num_big > 0) hipLaunchKernelGGL(k_lambdarank_big, dim3(ra.num_big), dim3(kRankBigThreads), 0, s, ra);
   } else {
     hipLaunchKernelGGL(k_xendcg, dim3(ra.num_queries), dim3(kRankThreads), 0, s, ra);
+    if (ra.num_big > 0) hipLaunchKernelGGL(k_xendcg_big, dim3(ra.num_big), dim3(kRankBigThreads), 0, s, ra);
   }
 }
 

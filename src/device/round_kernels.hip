@@ -155,11 +155,6 @@ __global__ __launch_bounds__(kPartThreads) __attribute__((amdgpu_waves_per_eu(LG
     x.r.default_bin = e.feat.default_bin;
     x.r.max_bin = e.feat.num_bin - 1;
   }
-  // this round's reduce counters (KArgs::red_per_exp: the reduces run in the split-scan launch,
-  // which follows this one; the previous round's have all finished)
-  if (a.red_per_exp > 0 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < static_cast<unsigned>(kMaxRoundExp)) {
-    rd->red_cnt[threadIdx.x] = 0u;
-  }
   if (done || nexp <= 0 || static_cast<int>(blockIdx.x) >= nblk) return;
   if (threadIdx.x < static_cast<unsigned>(nexp)) ex[threadIdx.x] = x;
   for (int i = threadIdx.x; i < nexp * kMaxCatWords; i += kPartThreads) {
@@ -703,75 +698,6 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
   }
 }
 
-// The reduce of k_round_reduce as the first workgroups (grid rows [0, KArgs::red_rows)) of the
-// numerical split-scan launch (KArgs::red_per_exp > 0, single process): workgroup r reduces
-// bins [bx * NT, +NT) of partial chunk `by` of expansion j = r / red_per_exp.  Its sums are
-// stored write-through (agent-scope atomics), then the workgroup counts itself on
-// Round::red_cnt[j]; the scans of expansion j wait for red_per_exp counts.  Workgroups are
-// dispatched in order of their linear index, so every reduce workgroup is resident before any
-// scan workgroup that waits for it, and a reduce never waits: the waits end.
-template <int NT>
-__device__ void RoundReduceRole(const KArgs& a, int r) {
-  Round* rd = a.rd;
-  const int C = a.red_per_exp;
-  const int j = r / C, rem = r - j * C;
-  const int nb = a.p.total_bins;
-  const int nbx = (nb + NT - 1) / NT;
-  const int bx = rem % nbx, by = rem / nbx;
-  if (j >= kMaxRoundExp || rd->done || j >= rd->nexp) return;
-  const int nblk = rd->e[j].nblk;
-  if (nblk <= kDirectChunk) return;  // (summed by the split scan itself; nobody waits)
-  const int gy = C / nbx;
-  const int bin = bx * NT + static_cast<int>(threadIdx.x);
-  if (by * kReduceChunk < nblk && bin < nb) {
-    const int units = a.hist_units;
-    const size_t pstride = static_cast<size_t>(units) * nb;
-    const unsigned long long* part = a.partials + static_cast<size_t>(rd->e[j].blk_off) * pstride;
-    long long g = 0, h = 0;
-    for (int k0 = by * kReduceChunk; k0 < nblk; k0 += gy * kReduceChunk) {
-      const unsigned long long* p = part + k0 * pstride + static_cast<size_t>(units) * bin;
-      const int kn = min(kReduceChunk, nblk - k0);
-      unsigned long long v0[kReduceChunk], v1[kReduceChunk];
-#pragma unroll
-      for (int k = 0; k < kReduceChunk; ++k) {
-        v0[k] = k < kn ? p[k * pstride] : 0ull;
-        v1[k] = (units == 2 && k < kn) ? p[k * pstride + 1] : 0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < kReduceChunk; ++k) {
-        long long pg, ph;
-        UnpackPartial(v0[k], v1[k], units, &pg, &ph);
-        g += pg;
-        h += ph;
-      }
-    }
-    GlobalU64* out = (GlobalU64*)(RoundScratch(a, rd->round, j) + 2 * static_cast<size_t>(bin));
-    if (nblk <= kReduceChunk) {
-      __hip_atomic_store(out, static_cast<unsigned long long>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(out + 1, static_cast<unsigned long long>(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_fetch_add(out, static_cast<unsigned long long>(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(out + 1, static_cast<unsigned long long>(h), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  ArrivalRelease();
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_fetch_add(&rd->red_cnt[j], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// a scan of expansion j waits for its reduce workgroups (RoundReduceRole)
-__device__ __forceinline__ void RoundReduceWait(const KArgs& a, int j) {
-  if (threadIdx.x == 0) {
-    const uint32_t want = static_cast<uint32_t>(a.red_per_exp);
-    while (__hip_atomic_load(&a.rd->red_cnt[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
-      __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  }
-  __syncthreads();
-}
-
 // the plan's LDS tables (RoundPlanLds bytes): node tables (gain, -inf when the node has no
 // split; real feature; first child or -1), leaf tables (gain, real feature, node; accepted
 // leaves / nodes) and the prediction's copies of the leaf tables (+ levels below the leaf)
@@ -890,11 +816,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   __shared__ int s_last;
   Round* rd = a.rd;
   const long long t_entry = a.ktrace != nullptr ? wall_clock64() : 0;
-  if (static_cast<int>(blockIdx.y) < a.red_rows) {  // (the round's reduce workgroups come first)
-    RoundReduceRole<NT>(a, static_cast<int>(blockIdx.y * gridDim.x + blockIdx.x));
-    return;
-  }
-  const int by = static_cast<int>(blockIdx.y) - a.red_rows;  // (the scan grid's row)
+  const int by = static_cast<int>(blockIdx.y);
   const int y = by, j = y >> 1, lr = y & 1;
   // voting-parallel rounds (KArgs::round_vote): Params::vote_phase 1 scans every feature on this
   // rank's histograms, sums and counts; 2 scans the features the vote elected for child y
@@ -948,7 +870,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     // data-parallel: the next round's owner-major send buffer, cleared by every workgroup's
     // share (this round's reduce-scatter has read it) -- no memset node per round
     const size_t total = static_cast<size_t>(a.p.world) * a.round_k * a.rs_block * 2;
-    const size_t nwg = static_cast<size_t>(gridDim.x) * (gridDim.y - a.red_rows);
+    const size_t nwg = static_cast<size_t>(gridDim.x) * gridDim.y;
     const size_t per = (total + nwg - 1) / nwg;
     const size_t b0 = (static_cast<size_t>(by) * gridDim.x + blockIdx.x) * per;
     const size_t b1 = min(total, b0 + per);
@@ -1032,9 +954,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
       pg0 = dst[2 * tid];
       ph0 = dst[2 * tid + 1];
     }
-    // (the reduce ran in this launch: its sums are read coherently once they are all counted)
-    const bool reduced_here = a.red_rows > 0 && nblk_direct < 0 && !owner && !vote_global;
-    if (reduced_here) RoundReduceWait(a, j);
     if (spread) {
       for (int i = tid; i < 2 * nbf; i += NT) sh.s_red[i] = 0ull;
       __syncthreads();
@@ -1087,9 +1006,6 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
             h += phv;
           }
         }
-      } else if (reduced_here) {
-        g = static_cast<long long>(__hip_atomic_load((GlobalU64*)(src + 2 * i), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        h = static_cast<long long>(__hip_atomic_load((GlobalU64*)(src + 2 * i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
       } else {
         g = src[2 * i];
         h = src[2 * i + 1];
@@ -1932,18 +1848,8 @@ bool RoundSimpleGains(const KArgs& a) {
   return !p.use_l1 && !p.use_max_output && !p.use_smoothing && !p.use_mc;
 }
 
-// the reduce runs in the numerical split-scan launch (KArgs::red_per_exp)
-bool RoundReduceInFind(const KArgs& a) { return a.red_per_exp > 0 && !a.round_dist && a.num_scan > 0; }
-
 template <bool VG, bool PIF>
-void LaunchRoundFindT(const KArgs& a0, hipStream_t s) {
-  KArgs a = a0;
-  a.red_rows = 0;  // (the categorical launch and voting's global scan: no reduce rows)
-  KArgs an = a;    // the numerical launch: the reduce workgroups in its first grid rows
-  if (!VG && RoundReduceInFind(a0)) {
-    an.red_per_exp = RoundReducePerExp(a0);  // (for this launch's scan workgroup size)
-    an.red_rows = (an.red_per_exp * a.round_k + a.num_scan - 1) / a.num_scan;
-  }
+void LaunchRoundFindT(const KArgs& a, hipStream_t s) {
   const int ny = 2 * a.round_k;
   size_t lds = a.p.max_feature_bins <= kFindLdsBins ? 2 * sizeof(double) * static_cast<size_t>(a.p.max_feature_bins) : 0;
   if (a.plan_in_find) lds = std::max(lds, RoundPlanLds(a.p.num_leaves, a.round_nodes));
@@ -1952,23 +1858,23 @@ void LaunchRoundFindT(const KArgs& a0, hipStream_t s) {
   const dim3 b(narrow ? kWave : kFindThreads), bc(kFindThreads);
   // (voting global scan: every elected slot, numerical or categorical, in both kernels)
   const int ncat = (a.round_vote && a.p.vote_phase == 2) ? a.num_scan : a.p.has_cat;
-  const dim3 gn(a.num_scan, ny + an.red_rows);
+  const dim3 gn(a.num_scan, ny);
   if (a.p.has_cat) {
     if (narrow) {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave, VG, PIF>), gn, b, lds, s, an);
-      else hipLaunchKernelGGL((k_round_find<1, false, kWave, VG, PIF>), gn, b, lds, s, an);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kWave, VG, PIF>), gn, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kWave, VG, PIF>), gn, b, lds, s, a);
     } else {
-      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads, VG, PIF>), gn, b, lds, s, an);
-      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads, VG, PIF>), gn, b, lds, s, an);
+      if (simple) hipLaunchKernelGGL((k_round_find<1, true, kFindThreads, VG, PIF>), gn, b, lds, s, a);
+      else hipLaunchKernelGGL((k_round_find<1, false, kFindThreads, VG, PIF>), gn, b, lds, s, a);
     }
     if (a.p.wide_cat) hipLaunchKernelGGL((k_round_find<3, false, kFindThreads, VG, PIF>), dim3(ncat, ny), bc, lds, s, a);
     else hipLaunchKernelGGL((k_round_find<2, false, kFindThreads, VG, PIF>), dim3(ncat, ny), bc, lds, s, a);
   } else if (narrow) {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave, VG, PIF>), gn, b, lds, s, an);
-    else hipLaunchKernelGGL((k_round_find<0, false, kWave, VG, PIF>), gn, b, lds, s, an);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kWave, VG, PIF>), gn, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kWave, VG, PIF>), gn, b, lds, s, a);
   } else {
-    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads, VG, PIF>), gn, b, lds, s, an);
-    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads, VG, PIF>), gn, b, lds, s, an);
+    if (simple) hipLaunchKernelGGL((k_round_find<0, true, kFindThreads, VG, PIF>), gn, b, lds, s, a);
+    else hipLaunchKernelGGL((k_round_find<0, false, kFindThreads, VG, PIF>), gn, b, lds, s, a);
   }
 }
 
@@ -2010,13 +1916,6 @@ void PrepareRoundKernels(int max_lds) {
   AllowRoundSplitLds<4>(max_lds);
   AllowRoundSplitLds<8>(max_lds);
   AllowRoundSplitLds<2, true>(max_lds);
-}
-
-int RoundReducePerExp(const KArgs& a) {
-  const int nt = a.p.max_feature_bins <= kWave ? kWave : kFindThreads;  // (the numerical scan's workgroup)
-  const int nbx = (a.p.total_bins + nt - 1) / nt;
-  const int gy = std::min(4, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk);
-  return nbx * std::max(1, gy);
 }
 
 void RoundRootPlan(const KArgs& a, hipStream_t s) {
@@ -2067,7 +1966,6 @@ void RoundSplitReduce(const KArgs& a, hipStream_t s) {
       else hipLaunchKernelGGL((k_round_hist<0, 2>), grid, dim3(kHistThreads), lds, s, a);
     }
   }
-  if (RoundReduceInFind(a)) return;  // (in the split-scan launch)
   const dim3 rgrid((a.p.total_bins + 255) / 256,
                    std::min(4, (a.hist_max_blocks + kReduceChunk - 1) / kReduceChunk), a.round_k);
   if (a.hist_units == 1) hipLaunchKernelGGL((k_round_reduce<1>), rgrid, dim3(256), 0, s, a);

@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include "objective_common.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 namespace dev {
@@ -303,14 +304,14 @@ __global__ __launch_bounds__(kBmRowsPerBlock) __attribute__((amdgpu_waves_per_eu
       const float gf = static_cast<float>(g), hf = static_cast<float>(h);
       reinterpret_cast<float2*>(ga.gh)[i * ga.gh_stride] = make_float2(gf, hf);
       mg = fmaxf(mg, fabsf(gf));
-      mh = fmaxf(mh, fabsf(hf));
+      mh = HessMax(mh, hf);
       sg += gf;
       shh += hf;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
     mg = fmaxf(mg, __shfl_xor(mg, o, kWave));
-    mh = fmaxf(mh, __shfl_xor(mh, o, kWave));
+    mh = HessMax(mh, __shfl_xor(mh, o, kWave));
     sg += __shfl_xor(sg, o, kWave);
     shh += __shfl_xor(shh, o, kWave);
   }
@@ -326,7 +327,7 @@ __global__ __launch_bounds__(kBmRowsPerBlock) __attribute__((amdgpu_waves_per_eu
     double tg = 0.0, th = 0.0;
     for (int i = 0; i < kBmRowsPerBlock / kWave; ++i) {
       mg = fmaxf(mg, smg[i]);
-      mh = fmaxf(mh, smh[i]);
+      mh = HessMax(mh, smh[i]);
       tg += ssg[i];
       th += ssh[i];
     }
@@ -347,8 +348,8 @@ int BmBlocks(int64_t num_rows) {
   // 32 workgroups per CU walk the chunks (LGBM_AMD_BM_WG_PER_CU; 0: one chunk per
   // workgroup).  Headline A/B at 0/4/8/16/32: 4.146/4.135/4.133/4.120/4.109 ms/iter
   static const int per_cu = [] {
-    const char* e = std::getenv("LGBM_AMD_BM_WG_PER_CU");
-    return e != nullptr ? std::atoi(e) : 32;
+    const char* e = tuning::Get(tuning::Knob::BmWgPerCu);
+    return e != nullptr ? std::atoi(e) : tuning::kScoreWalkWgPerCu;
   }();
   int64_t blocks64 = (num_rows + kBmRowsPerBlock - 1) / kBmRowsPerBlock;
   if (per_cu > 0) blocks64 = std::min<int64_t>(blocks64, static_cast<int64_t>(per_cu) * NumCUs());

@@ -22,6 +22,7 @@
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/network.h"
 #include "lgbm_amd/random.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -424,7 +425,7 @@ FeatureGroup Dataset::NewGroup(const std::vector<int>& fs) {
   double nonzero = 0.0;
   for (int f : fs) nonzero += 1.0 - bin_mappers_[f]->sparse_rate();
   g.sparse = nonzero <= kSparseGroupRate;
-  if (const char* e = std::getenv("LGBM_AMD_HOST_SPARSE")) g.sparse = e[0] == '1';
+  if (const char* e = tuning::Get(tuning::Knob::HostSparse)) g.sparse = e[0] == '1';
   if (g.sparse) {
     g.push_buf.resize(static_cast<size_t>(std::max(omp_get_max_threads(), omp_get_num_procs())));
   } else {

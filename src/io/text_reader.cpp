@@ -11,6 +11,7 @@
 #include <thread>
 
 #include "lgbm_amd/log.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -38,7 +39,7 @@ bool IsBlank(const char* p, size_t n) {
 }  // namespace
 
 void TextReader::ForEachLine(const std::string& path, bool skip_header, const LineFn& fn, size_t block_bytes) {
-  if (const char* e = std::getenv("LGBM_AMD_TEXT_BLOCK_BYTES")) {  // (tests: lines across block edges)
+  if (const char* e = tuning::Get(tuning::Knob::TextBlockBytes)) {  // (tests: lines across block edges)
     block_bytes = static_cast<size_t>(std::max(16L, std::atol(e)));
   }
   std::FILE* f = std::fopen(path.c_str(), "rb");

@@ -420,9 +420,7 @@ class QueryMetricBase : public Metric {
   DeviceMetricSpec QuerySpec(int kind) const {
     DeviceMetricSpec d;
     if (qb_ == nullptr || nq_ <= 0) return d;
-    for (data_size_t q = 0; q < nq_; ++q) {
-      if (qb_[q + 1] - qb_[q] > kDeviceMaxQueryDocs) return d;  // long queries: host
-    }
+    for (data_size_t q = 0; q < nq_; ++q) d.max_query_docs = std::max(d.max_query_docs, qb_[q + 1] - qb_[q]);
     d.kind = kind;
     d.nout = static_cast<int>(eval_at_.size());
     d.label = label_;
@@ -433,7 +431,9 @@ class QueryMetricBase : public Metric {
     d.eval_at.assign(eval_at_.begin(), eval_at_.end());
     return d;
   }
-  static constexpr data_size_t kDeviceMaxQueryDocs = 2048;  // src/device/kernels.h kRankMaxDocs
+  // queries of up to this many documents are staged in LDS by the device kernel (kRankMaxDocs);
+  // longer ones take its global-scratch variant
+  static constexpr data_size_t kDeviceMaxQueryDocs = 2048;
   std::vector<std::string> name_;
   std::vector<data_size_t> eval_at_;
   data_size_t num_data_ = 0, nq_ = 0;
@@ -474,8 +474,8 @@ class NDCGMetric : public QueryMetricBase {
       for (size_t j = 0; j < K; ++j) d.qconst[q * K + j] = inv_max_[q][j];
     }
     d.label_gain = DCG::label_gain();
-    d.discount.resize(kDeviceMaxQueryDocs);
-    for (data_size_t i = 0; i < kDeviceMaxQueryDocs; ++i) d.discount[i] = DCG::Discount(i);
+    d.discount.resize(std::max(kDeviceMaxQueryDocs, d.max_query_docs));
+    for (size_t i = 0; i < d.discount.size(); ++i) d.discount[i] = DCG::Discount(static_cast<data_size_t>(i));
     return d;
   }
   std::vector<double> Eval(const double* score, const ObjectiveFunction*) const override {

@@ -26,6 +26,7 @@
 
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/network.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -66,7 +67,7 @@ MpiLib* OpenMpi() {
   std::lock_guard<std::mutex> lk(g_mpi_mu);
   if (g_mpi != nullptr) return g_mpi;
   std::vector<std::string> names;
-  if (const char* e = std::getenv("LGBM_AMD_MPI_LIB")) names.push_back(e);
+  if (const char* e = tuning::Get(tuning::Knob::MpiLib)) names.push_back(e);
   for (const char* n : {"libmpi.so.40", "libmpi.so.12", "libmpi.so", "libmpich.so.12"}) names.push_back(n);
   void* dl = nullptr;
   std::string tried;
@@ -161,7 +162,7 @@ std::shared_ptr<HostTransport> MakeMpiTransport(const Config& cfg) {
 }
 
 bool MpiSelected() {
-  const char* e = std::getenv("LGBM_AMD_NETWORK");
+  const char* e = tuning::Get(tuning::Knob::Network);
   return e != nullptr && std::string(e) == "mpi";
 }
 

@@ -27,6 +27,7 @@
 #include "../device/kernels.h"
 #include "lgbm_amd/log.h"
 #include "lgbm_amd/network.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -39,7 +40,7 @@ namespace {
   } while (0)
 
 size_t StageBytesFromEnv(size_t dflt) {
-  const char* e = std::getenv("LGBM_AMD_PEER_STAGE_MB");
+  const char* e = tuning::Get(tuning::Knob::PeerStageMb);
   if (e != nullptr && std::atoi(e) > 0) return static_cast<size_t>(std::atoi(e)) << 20;
   return dflt;
 }
@@ -245,7 +246,7 @@ const char* LinkName(uint32_t t) {
 
 std::vector<std::shared_ptr<DeviceComm>> MakePeerThreadComms(int num_ranks, double timeout_s, int fail_rank,
                                                              int fail_at_call) {
-  const size_t stage = StageBytesFromEnv(size_t(16) << 20);
+  const size_t stage = StageBytesFromEnv(size_t(tuning::kPeerStageMbThreads) << 20);
   auto wins = std::make_shared<PeerWindows>();
   if (timeout_s > 0) wins->timeout_s = timeout_s;
   for (int r = 0; r < num_ranks; ++r) wins->win.push_back(AllocWindow(stage));
@@ -265,7 +266,7 @@ std::vector<std::shared_ptr<DeviceComm>> MakePeerThreadComms(int num_ranks, doub
 std::shared_ptr<DeviceComm> MakePeerIpcComm(int device_id, double timeout_s) {
   const int n = Network::num_machines(), rank = Network::rank();
   if (n > dev::kMaxPeerBufs) Log::Fatal("peer device comm supports at most %d ranks", dev::kMaxPeerBufs);
-  const size_t stage = StageBytesFromEnv(size_t(64) << 20);
+  const size_t stage = StageBytesFromEnv(size_t(tuning::kPeerStageMbProcesses) << 20);
   // devices are identified by PCI bus id, not by ordinal: under per-process device isolation
   // (HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES) every rank's device is ordinal 0
   struct Entry {

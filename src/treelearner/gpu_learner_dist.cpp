@@ -1,6 +1,7 @@
 // MI355X tree learner: distributed parts -- feature ownership, the root / histogram / record
 // collectives of the one-split-per-step sequence and the voting exchange.
 #include "gpu_learner_internal.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -103,7 +104,7 @@ void GPUTreeLearner::SetupOwnership() {
   // capacity leaves room for an uneven count -- a tree whose assignment exceeds either keeps
   // the static layout
   dyn_owner_ = mode_ == Mode::kData && config_->feature_fraction < 1.0 &&
-               !(std::getenv("LGBM_AMD_STATIC_OWNERS") != nullptr && std::getenv("LGBM_AMD_STATIC_OWNERS")[0] == '1');
+               !(tuning::Get(tuning::Knob::StaticOwners) != nullptr && tuning::Get(tuning::Knob::StaticOwners)[0] == '1');
   int ncat = 0;
   for (int f = 0; f < num_features_; ++f) ncat += data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical ? 1 : 0;
   if (dyn_owner_) {
@@ -251,13 +252,13 @@ void GPUTreeLearner::AllreduceAbsMax() {
   if (!(data_parallel_ || voting_) || Network::num_machines() <= 1) return;
   DeviceComm* dc = Network::device_comm();
   if (dc != nullptr) {
-    dc->AllreduceMaxU32(d_absmax_, 3, stream_);  // non-negative float bits order like the floats
+    dc->AllreduceMaxU32(d_absmax_, 4, stream_);  // non-negative float bits order like the floats; [3]: a flag
     return;
   }
-  HIPCHECK(hipMemcpyAsync(h_absmax_, d_absmax_, sizeof(uint32_t) * 3, hipMemcpyDeviceToHost, stream_));
+  HIPCHECK(hipMemcpyAsync(h_absmax_, d_absmax_, sizeof(uint32_t) * 4, hipMemcpyDeviceToHost, stream_));
   HIPCHECK(hipStreamSynchronize(stream_));
-  for (int k = 0; k < 3; ++k) h_absmax_[k] = Network::GlobalSyncUpByMax(h_absmax_[k]);
-  HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 3, hipMemcpyHostToDevice, stream_));
+  for (int k = 0; k < 4; ++k) h_absmax_[k] = Network::GlobalSyncUpByMax(h_absmax_[k]);
+  HIPCHECK(hipMemcpyAsync(d_absmax_, h_absmax_, sizeof(uint32_t) * 4, hipMemcpyHostToDevice, stream_));
 }
 
 dev::KArgs GPUTreeLearner::VoteGlobalArgs(const dev::KArgs& a, int pick_in_find) const {

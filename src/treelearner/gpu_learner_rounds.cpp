@@ -1,6 +1,7 @@
 // MI355X tree learner: round growth orchestration -- pools, the round sequence and its
 // collectives, the growth-mode choice and the host loop over round segments (round_kernels.hip).
 #include "gpu_learner_internal.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -126,13 +127,13 @@ double GPUTreeLearner::RoundCollectiveBytes() const {
 // every later tree.  Distributed ranks sum their times first, so all of them switch together.
 bool GPUTreeLearner::AutoGrowthRounds() {
   if (auto_state_ == kAutoUnset) {
-    const char* e = std::getenv("LGBM_AMD_ROUND_AUTO");
+    const char* e = tuning::Get(tuning::Knob::RoundAuto);
     double rows = static_cast<double>(num_data_);
     if (distributed_ && Network::num_machines() > 1) {
       std::vector<double> v{rows};
       rows = Network::GlobalSum(v)[0] / Network::num_machines();
     }
-    const bool on = e != nullptr ? e[0] == '1' : rows >= 16e6;
+    const bool on = e != nullptr ? e[0] == '1' : rows >= tuning::kRoundAutoRows;
     auto_state_ = on ? kAutoProbe : kAutoRounds;
     auto_tree_ = 0;
   }
@@ -171,13 +172,6 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
 // trees + margin); the host then checks the Round record and adds segments until the tree is
 // done (a finished tree's kernels exit at once: an over-provisioned round costs ~12 us, a
 // missing one a host round trip and a graph launch per segment)
-namespace {
-constexpr int kRoundFirstPred = 16;  // rounds enqueued for the first tree
-int EnvInt(const char* name, int dflt) {
-  const char* e = std::getenv(name);
-  return e != nullptr ? std::atoi(e) : dflt;
-}
-}
 
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
   a.rd = d_round_;
@@ -188,17 +182,17 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
       std::vector<double> v{rows};
       rows = Network::GlobalSum(v)[0] / Network::num_machines();
     }
-    k_adapt_ = rows >= 4e6;
+    k_adapt_ = rows >= tuning::kRoundAdaptRows;
   }
   if (k_adapt_) {
     // this tree's round width (Round::k_cur: the captured graphs are sized for round_k_)
-    k_cur_host_ = (prev_splits_ <= 0 || prev_expansions_ <= prev_splits_ + 2) ? round_k_ : std::min(round_k_, 6);
+    k_cur_host_ = (prev_splits_ <= 0 || prev_expansions_ <= prev_splits_ + 2) ? round_k_ : std::min(round_k_, tuning::kRoundWidthNarrow);
     HIPCHECK(hipMemcpyAsync(&d_round_->k_cur, &k_cur_host_, sizeof(int32_t), hipMemcpyHostToDevice, stream_));
   }
   a.pick_in_find = 0;  // the root's split scan only publishes; RoundRootPlan picks
   // (LGBM_AMD_KTRACE: k_round_split's phase times of one workgroup per round)
   if (a.ktrace != nullptr) HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
-  const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
+  const char* ng = tuning::Get(tuning::Knob::NoGraph);
   // distributed: the collectives are captured with the kernels when the communicator allows it
   // (RCCL); the in-process communicator rendezvouses on the host, so its rounds run eagerly
   DeviceComm* dc = distributed_ ? Network::device_comm() : nullptr;
@@ -229,15 +223,15 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     return true;
   };
   const int L = config_->num_leaves;
-  static const int env_hist = EnvInt("LGBM_AMD_ROUND_HIST", 0), env_margin = EnvInt("LGBM_AMD_ROUND_MARGIN", -99),
-                   env_seg = EnvInt("LGBM_AMD_ROUND_SEG", 0), env_root = EnvInt("LGBM_AMD_ROUND_ROOT", -1);
+  static const int env_hist = tuning::Int(tuning::Knob::RoundHist, 0), env_margin = tuning::Int(tuning::Knob::RoundMargin, -99),
+                   env_seg = tuning::Int(tuning::Knob::RoundSeg, 0), env_root = tuning::Int(tuning::Knob::RoundRoot, -1);
   if (env_hist > 0) round_hist_n_ = static_cast<size_t>(env_hist);
   if (env_margin > -99) round_margin_ = env_margin;
   if (env_seg > 0) round_seg_ = env_seg;
   if (env_root >= 0) round_root_fixed_ = env_root;
   const int seg = round_seg_;
   // rounds to enqueue: the most rounds of the last trees (+ margin)
-  int want = kRoundFirstPred;
+  int want = tuning::kRoundFirstTree;
   if (!round_hist_.empty()) want = *std::max_element(round_hist_.begin(), round_hist_.end()) + round_margin_;
   want = std::max(1, std::min(want, L - 1));
   // the root graph: a fixed number of rounds, or the provisioned count rounded up to segments;

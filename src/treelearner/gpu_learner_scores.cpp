@@ -1,6 +1,7 @@
 // MI355X tree learner: validation sets, device-resident training scores, gradients and
 // row sampling.
 #include "gpu_learner_internal.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -105,7 +106,9 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
       qi.qconst = static_cast<double*>(upload(spec.qconst.data(), sizeof(double) * spec.qconst.size()));
       qi.label_gain = static_cast<double*>(upload(spec.label_gain.data(), sizeof(double) * spec.label_gain.size()));
       qi.discount = static_cast<double*>(upload(spec.discount.data(), sizeof(double) * spec.discount.size()));
-      qi.scratch = dev_alloc(dev::MetricScratchBytes(0, static_cast<int64_t>(spec.nq) * spec.eval_at.size()));
+      qi.big = spec.max_query_docs > dev::kRankMaxDocs;
+      qi.scratch = dev_alloc(dev::MetricScratchBytes(qi.big ? vs.num_data : 0,
+                                                     static_cast<int64_t>(spec.nq) * spec.eval_at.size()));
       it = vs.queries.emplace(spec.key, qi).first;
     }
     const ValidSet::QueryInputs& qi = it->second;
@@ -118,6 +121,7 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
     m.label_gain = qi.label_gain;
     m.discount = qi.discount;
     m.scratch = qi.scratch;
+    m.big = qi.big ? 1 : 0;
   } else {
     if (aucmu) {  // the class weight matrix, uploaded on the metric's first evaluation
       auto it = vs.queries.find(spec.key);
@@ -381,7 +385,7 @@ void GPUTreeLearner::AddTreeToScore(const Tree* tree, int k) {
 
 // LGBM_AMD_FUSE_GRAD=0: the score walk does not compute the next gradients
 bool GPUTreeLearner::FuseNextGradients() {
-  const char* e = std::getenv("LGBM_AMD_FUSE_GRAD");
+  const char* e = tuning::Get(tuning::Knob::FuseGrad);
   return !(e != nullptr && e[0] == '0');
 }
 
@@ -397,9 +401,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   if (spec.kind != DeviceGradKind::MulticlassSoftmax && ntpi != 1) return false;
   if (spec.label == nullptr) return false;
   const bool listwise = spec.kind == DeviceGradKind::Lambdarank || spec.kind == DeviceGradKind::RankXendcg;
-  if (listwise && (spec.rank.query_boundaries == nullptr || spec.rank.max_query_docs > dev::kRankMaxDocs)) {
-    return false;  // queries larger than the LDS staging: host gradients
-  }
+  if (listwise && spec.rank.query_boundaries == nullptr) return false;
   const size_t n = static_cast<size_t>(num_data_);
   const bool prefetched = grad_prefetched_;
   grad_prefetched_ = false;
@@ -442,6 +444,14 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     ra.sig_max = spec.rank.sig_max;
     ra.sig_factor = spec.rank.sig_factor;
     ra.sig_table = d_sig_table_;
+    ra.big_q = d_rank_big_q_;
+    ra.num_big = rank_num_big_;
+    ra.big_d0 = d_rank_big_d0_;
+    ra.big_d1 = d_rank_big_d1_;
+    ra.big_f = d_rank_big_f_;
+    ra.big_i0 = d_rank_big_i0_;
+    ra.big_i1 = d_rank_big_i1_;
+    ra.big_i2 = d_rank_big_i2_;
     ra.norm = spec.rank.norm ? 1 : 0;
     ra.rng = d_rank_rng_;
     dev::RankGradients(ra, stream_);
@@ -521,6 +531,29 @@ void GPUTreeLearner::UploadRankTables(const DeviceRankSpec& r, DeviceGradKind ki
   } else {
     d_rank_rng_ = Alloc<uint32_t>(nq);
     HIPCHECK(hipMemcpy(d_rank_rng_, r.rng_states, sizeof(uint32_t) * nq, hipMemcpyHostToDevice));
+  }
+  // queries longer than the LDS staging: one 1024-thread workgroup each over a global scratch
+  std::vector<int32_t> big;
+  for (size_t q = 0; q < nq; ++q) {
+    if (r.query_boundaries[q + 1] - r.query_boundaries[q] > dev::kRankMaxDocs) big.push_back(static_cast<int32_t>(q));
+  }
+  rank_num_big_ = static_cast<int32_t>(big.size());
+  d_rank_big_q_ = nullptr;
+  d_rank_big_d0_ = d_rank_big_d1_ = nullptr;
+  d_rank_big_f_ = nullptr;
+  d_rank_big_i0_ = d_rank_big_i1_ = d_rank_big_i2_ = nullptr;
+  if (!big.empty()) {
+    const size_t n = static_cast<size_t>(num_data_);
+    d_rank_big_q_ = Alloc<int32_t>(big.size());
+    HIPCHECK(hipMemcpy(d_rank_big_q_, big.data(), sizeof(int32_t) * big.size(), hipMemcpyHostToDevice));
+    d_rank_big_d0_ = Alloc<double>(n);
+    d_rank_big_d1_ = Alloc<double>(n);
+    d_rank_big_f_ = Alloc<float>(n);
+    d_rank_big_i0_ = Alloc<int32_t>(n);
+    d_rank_big_i1_ = Alloc<int32_t>(n);
+    d_rank_big_i2_ = Alloc<int32_t>(n);
+    Log::Debug("device %s: %d queries of more than %d documents in global scratch",
+               kind == DeviceGradKind::Lambdarank ? "lambdarank" : "rank_xendcg", rank_num_big_, dev::kRankMaxDocs);
   }
   uploaded_qb_src_ = r.query_boundaries;
 }

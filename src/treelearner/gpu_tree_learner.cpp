@@ -1,5 +1,6 @@
 // MI355X tree learner host orchestration (see gpu_tree_learner.h).
 #include "gpu_learner_internal.h"
+#include "lgbm_amd/tuning.h"
 
 namespace lgbm_amd {
 
@@ -63,6 +64,11 @@ void GPUTreeLearner::FreeBuffers() {
   uploaded_label_src_ = uploaded_weight_src_ = uploaded_lw_src_ = nullptr;
   d_qb_ = nullptr;
   d_inv_max_dcg_ = d_label_gain_ = d_discount_ = d_sig_table_ = nullptr;
+  d_rank_big_q_ = nullptr;
+  rank_num_big_ = 0;
+  d_rank_big_d0_ = d_rank_big_d1_ = nullptr;
+  d_rank_big_f_ = nullptr;
+  d_rank_big_i0_ = d_rank_big_i1_ = d_rank_big_i2_ = nullptr;
   d_rank_rng_ = nullptr;
   uploaded_qb_src_ = nullptr;
   d_sample_rng_ = nullptr;
@@ -130,7 +136,7 @@ void GPUTreeLearner::UploadData() {
   // row layout: groups in order, 8-bit groups four to a 32-bit word, 16-bit groups (more than
   // 256 bins) two to a word; a group of the other width starts a new word.  One wide group no
   // longer widens every column (LGBM_AMD_UNIFORM_BINS=1: the uniform layout, for A/B runs)
-  const bool uniform = std::getenv("LGBM_AMD_UNIFORM_BINS") != nullptr && std::getenv("LGBM_AMD_UNIFORM_BINS")[0] == '1';
+  const bool uniform = tuning::Get(tuning::Knob::UniformBins) != nullptr && tuning::Get(tuning::Knob::UniformBins)[0] == '1';
   h_gwide_.assign(num_groups_, 0);
   h_gbyte_.assign(num_groups_, 0);
   h_word_of_group_.assign(num_groups_, 0);
@@ -150,7 +156,7 @@ void GPUTreeLearner::UploadData() {
   const bool can_nib = n_wide == 0 && max_group_bins <= 16 && !uniform;
   const size_t byte_matrix = static_cast<size_t>(num_data_) * 4 * static_cast<size_t>((num_groups_ + 3) / 4);
   nibbles_ = can_nib && byte_matrix > (size_t(32) << 30);
-  if (const char* e = std::getenv("LGBM_AMD_NIBBLE_BINS")) nibbles_ = can_nib && e[0] == '1';
+  if (const char* e = tuning::Get(tuning::Knob::NibbleBins)) nibbles_ = can_nib && e[0] == '1';
   h_gnib_.assign(num_groups_, 0);
   int slot = 0;
   for (int g = 0; g < num_groups_; ++g) {
@@ -202,14 +208,14 @@ void GPUTreeLearner::UploadData() {
     // A/B on the headline 10M x 28 (7 bin words -> 64-B rows): 2.52 ms/iter separate, 2.71
     // interleaved -- off by default
     bool gh_rows = false;
-    if (const char* e = std::getenv("LGBM_AMD_GH_IN_ROWS")) gh_rows = e[0] == '1';
+    if (const char* e = tuning::Get(tuning::Knob::GhInRows)) gh_rows = e[0] == '1';
     if (gh_rows) {
       args_.row_words = row_words;
       args_.gh_stride = row_words / 2;
     }
     // LGBM_AMD_ROW_ALIGN_WORDS=n: row stride rounded up to n words (A/B: 8 -> 32-B rows that
     // never straddle a 64-B line, at 8/7 of the matrix bytes on the headline shape)
-    if (const char* e = std::getenv("LGBM_AMD_ROW_ALIGN_WORDS")) {
+    if (const char* e = tuning::Get(tuning::Knob::RowAlignWords)) {
       const int al = std::max(1, std::atoi(e));
       if (!gh_rows) args_.row_words = (wpr + al - 1) / al * al;
     }
@@ -227,7 +233,7 @@ void GPUTreeLearner::UploadData() {
   for (int g = 0; g < num_groups_; ++g) col_off[g + 1] = col_off[g] + static_cast<int64_t>(num_data_) * (h_gwide_[g] ? 2 : 1);
   const size_t col_bytes = static_cast<size_t>(col_off[num_groups_]);
   bool col_copy = col_bytes <= (size_t(8) << 30);
-  if (const char* cc = std::getenv("LGBM_AMD_COLUMN_COPY")) col_copy = cc[0] == '1';
+  if (const char* cc = tuning::Get(tuning::Knob::ColumnCopy)) col_copy = cc[0] == '1';
   col_copy = col_copy || sparse_rows_;  // (the partition's only source of the split column)
   if (col_copy) {
     std::vector<uint8_t> col(std::max<size_t>(1, col_bytes));
@@ -300,7 +306,7 @@ void GPUTreeLearner::UploadData() {
   // and the row's (g, h) once) -- 1-word tiles re-gather (g, h) per tile and measured
   // ~40% slower on small leaves (profiles/r01_v2_*)
   int max_tw = 1 << 20;
-  if (const char* e = std::getenv("LGBM_AMD_HIST_TILE_WORDS")) max_tw = std::max(1, std::atoi(e));
+  if (const char* e = tuning::Get(tuning::Knob::HistTileWords)) max_tw = std::max(1, std::atoi(e));
   int tile_words = sparse_rows_ ? 1 : 0;  // (row-sparse tiles are bin ranges, below)
   const std::vector<int> limits = hist_units_ == 1 ? std::vector<int>{8192, 16384} : std::vector<int>{8192};
   for (int limit : limits) {
@@ -331,10 +337,10 @@ void GPUTreeLearner::UploadData() {
   // vs 0.943 / 1.120 adaptive; Epsilon 8.28 vs 8.44 ms, Bosch / LTR shapes equal)
   // (the rows per rank are averaged over the ranks at the first tree, RunRounds: every rank
   // must plan with the same width)
-  round_k_ = 8;
+  round_k_ = tuning::kRoundWidth;
   k_adapt_ = true;
   k_adapt_checked_ = false;
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_K")) {
+  if (const char* e = tuning::Get(tuning::Knob::RoundK)) {
     round_k_ = std::atoi(e);
     k_adapt_ = false;
   }
@@ -342,7 +348,7 @@ void GPUTreeLearner::UploadData() {
   // speculation below the leaves (LGBM_AMD_ROUND_VMAX levels, 0: leaves only): one index
   // buffer per level + 2 (device_types.h), bounded to 32 GiB of row indices
   round_vmax_ = dev::kMaxRoundVmax;
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_VMAX")) round_vmax_ = std::atoi(e);
+  if (const char* e = tuning::Get(tuning::Knob::RoundVmax)) round_vmax_ = std::atoi(e);
   round_vmax_ = std::max(0, std::min(dev::kMaxRoundVmax, round_vmax_));
   while (round_vmax_ > 0 && static_cast<double>(num_data_) * 4.0 * (round_vmax_ + 1) > 32.0 * (1ull << 30)) --round_vmax_;
   if (round_k_ <= 1) round_vmax_ = 0;
@@ -395,9 +401,9 @@ void GPUTreeLearner::UploadData() {
   const int col_tiles = sparse_rows_ ? (total_bins_ + sparse_tile_bins - 1) / sparse_tile_bins
                                      : (wpr + tile_words - 1) / tile_words;
   split_grid_ = std::max(std::min(8, dev::HistGridBlocks() / 2), dev::HistGridBlocks() / 2 / std::max(1, col_tiles));
-  if (const char* e = std::getenv("LGBM_AMD_SPLIT_GRID")) split_grid_ = std::max(1, std::atoi(e));
+  if (const char* e = tuning::Get(tuning::Knob::SplitGrid)) split_grid_ = std::max(1, std::atoi(e));
   rows_cap_ = hist_units_ == 1 ? dev::kHistRowsCap : (1 << 30);
-  if (const char* e = std::getenv("LGBM_AMD_HIST_ROWS_CAP")) {
+  if (const char* e = tuning::Get(tuning::Knob::HistRowsCap)) {
     if (hist_units_ == 1) rows_cap_ = std::max(dev::kHistMinRows, std::min(dev::kHistRowsCap, std::atoi(e)));
   }
   // rows per split row block, lower bound: 4096 for one column tile (headline 10M x 28), 2048
@@ -405,7 +411,7 @@ void GPUTreeLearner::UploadData() {
   // blocks keep its workgroups busy: Epsilon, 8 tiles, 4096/2048/1024 = 23.0/21.7/20.8 ms/iter;
   // profiles/r02_v11_blk_min_rows_wide.txt)
   blk_min_rows_ = col_tiles >= 6 ? 1024 : col_tiles > 1 ? 2048 : 4096;
-  if (const char* e = std::getenv("LGBM_AMD_BLK_MIN_ROWS")) blk_min_rows_ = std::max(256, std::atoi(e));
+  if (const char* e = tuning::Get(tuning::Knob::BlkMinRows)) blk_min_rows_ = std::max(256, std::atoi(e));
   int hist_blocks = std::max({1, dev::HistBlocksFor(num_data_, root_grid_, rows_cap_, dev::kHistMinRows),
                               dev::HistBlocksFor(num_data_, split_grid_, rows_cap_, blk_min_rows_)});
   if (round_k_ > 1) {
@@ -413,13 +419,14 @@ void GPUTreeLearner::UploadData() {
     // plus one partial block per expansion
     const int64_t capped = (static_cast<int64_t>(num_data_) + rows_cap_ - 1) / rows_cap_;
     int rg = 2 * split_grid_;
-    if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) rg = std::max(rg, std::atoi(e));
+    if (const char* e = tuning::Get(tuning::Knob::RoundGrid)) rg = std::max(rg, std::atoi(e));
     // (k_round_plan: blocks <= rows / rows_cap + expansions + grid)
     hist_blocks = std::max<int>(hist_blocks, static_cast<int>(capped + rg + dev::kMaxRoundExp + 1));
   }
   d_partials_ = Alloc<unsigned long long>(static_cast<size_t>(hist_blocks) * total_bins_ * hist_units_);
   d_root_ = Alloc<double>(4);
   d_leaf_sums_ = Alloc<double>(4);
+  d_root_blk_ = Alloc<double>(2 * static_cast<size_t>(dev::RootSumBlocks()));
   // (per-workgroup partials of the gradient kernel, the packing kernel or the score walk that
   // computes the next gradients)
   const int parts = std::max({dev::GradientBlocks(num_data_), dev::PackBlocks(num_data_),
@@ -502,13 +509,14 @@ void GPUTreeLearner::UploadData() {
   a.pick_in_find = distributed_ ? 0 : 1;  // distributed: k_pick after the gather
   a.host_mode = 0;
   a.ktrace = nullptr;
-  if (const char* kt = std::getenv("LGBM_AMD_KTRACE")) {  // (before the rest of the arguments)
+  if (const char* kt = tuning::Get(tuning::Knob::Ktrace)) {  // (before the rest of the arguments)
     if (kt[0] == '1') {
       d_ktrace_ = Alloc<long long>(static_cast<size_t>(n_leaves) * dev::kTraceSlots);
       a.ktrace = d_ktrace_;
     }
   }
   a.root = d_root_;
+  a.root_blk = d_root_blk_;
   a.num_rows = num_data_;
   a.num_rows_dev = nullptr;
   a.root_identity = 1;
@@ -550,8 +558,8 @@ void GPUTreeLearner::UploadData() {
   // from this split on the tree's graph has no reduce kernel: smaller children are small
   // enough for the split scan to sum their partial histograms (LGBM_AMD_DIRECT_FROM_SPLIT)
   a.p.direct_from_split = 100;  // a reduce kernel for every step with > kReduceChunk blocks (r02 sweep)
-  a.p.trace_repeat = std::getenv("LGBM_AMD_KTRACE_REPEAT") != nullptr ? 1 : 0;
-  if (const char* e = std::getenv("LGBM_AMD_DIRECT_FROM_SPLIT")) a.p.direct_from_split = std::atoi(e);
+  a.p.trace_repeat = tuning::Get(tuning::Knob::KtraceRepeat) != nullptr ? 1 : 0;
+  if (const char* e = tuning::Get(tuning::Knob::DirectFromSplit)) a.p.direct_from_split = std::atoi(e);
   std::vector<int32_t> cats;
   for (int f = 0; f < num_features_; ++f) {
     if (feats[f].is_cat) cats.push_back(f);
@@ -654,20 +662,13 @@ void GPUTreeLearner::UploadData() {
   a.round_fused = 1;
   // the plan in the split scan's last workgroup while its tables fit the scan's LDS budget
   a.plan_in_find = (!distributed_ && dev::RoundPlanLds(n_leaves, split_rows_) <= 16384) ? 1 : 0;
-  if (const char* e = std::getenv("LGBM_AMD_PLAN_IN_FIND")) a.plan_in_find = e[0] == '1' ? 1 : 0;
+  if (const char* e = tuning::Get(tuning::Knob::PlanInFind)) a.plan_in_find = e[0] == '1' ? 1 : 0;
   // (voting: the local sums are accumulated by k_round_split)
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_FUSED")) a.round_fused = (e[0] == '1' || a.round_vote) ? 1 : 0;
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_GRID")) a.round_grid = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_GR")) a.round_gr = std::atoi(e);
+  if (const char* e = tuning::Get(tuning::Knob::RoundFused)) a.round_fused = (e[0] == '1' || a.round_vote) ? 1 : 0;
+  if (const char* e = tuning::Get(tuning::Knob::RoundGrid)) a.round_grid = std::max(1, std::atoi(e));
+  if (const char* e = tuning::Get(tuning::Knob::RoundGr)) a.round_gr = std::atoi(e);
   a.round_need_div = 0;
-  if (const char* e = std::getenv("LGBM_AMD_ROUND_NEED_DIV")) a.round_need_div = std::max(0, std::atoi(e));
-  // single process: the reduce of the large expansions' partials in the split-scan launch
-  // (LGBM_AMD_RED_IN_FIND=0: a kernel of its own)
-  a.red_rows = 0;
-  a.red_per_exp = (!distributed_ && a.round_fused) ? dev::RoundReducePerExp(a) : 0;
-  if (const char* e = std::getenv("LGBM_AMD_RED_IN_FIND")) {
-    if (e[0] == '0') a.red_per_exp = 0;
-  }
+  if (const char* e = tuning::Get(tuning::Knob::RoundNeedDiv)) a.round_need_div = std::max(0, std::atoi(e));
   AllocRoundState();
   UploadInteractionMasks();
   AllocSplittable();
@@ -774,7 +775,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
 
 void GPUTreeLearner::DecideMode() {
   bool dm = true;
-  const char* force = std::getenv("LGBM_AMD_HOST_ASSIST");
+  const char* force = tuning::Get(tuning::Knob::HostAssist);
   if ((force != nullptr && force[0] == '1') || force_host_mode_) dm = false;
   bool any_cat = false;
   for (int f = 0; f < num_features_ && dm; ++f) {
@@ -817,7 +818,7 @@ void GPUTreeLearner::DecideMode() {
   // device-resident under the distributed learners too: every rank draws the same node samples
   // and holds the same CEGB state, the owners' scans apply them (LGBM_AMD_DIST_HOST_ASSIST=1:
   // the host-assisted fallback, for A/B)
-  const char* dha = std::getenv("LGBM_AMD_DIST_HOST_ASSIST");
+  const char* dha = tuning::Get(tuning::Knob::DistHostAssist);
   const bool dist_fallback = distributed_ && dha != nullptr && dha[0] == '1';
   if (has_forced_split_ && (distributed_ || !SetupForcedSplits())) dm = false;
   if (!has_forced_split_ && args_.forced_n > 0) SetupForcedSplits();  // (cleared)
@@ -1221,8 +1222,8 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     const bool distributed = distributed_;
     DeviceComm* dcomm = distributed ? Network::device_comm() : nullptr;
     const bool dev_comm = dcomm != nullptr && dcomm->CaptureSafe();
-    const char* ng = std::getenv("LGBM_AMD_NO_GRAPH");
-    const char* gc = std::getenv("LGBM_AMD_GRAPH_COLLECTIVES");
+    const char* ng = tuning::Get(tuning::Knob::NoGraph);
+    const char* gc = tuning::Get(tuning::Knob::GraphCollectives);
     const bool graph_collectives = dev_comm && !(gc != nullptr && gc[0] == '0') && !graph_capture_failed_;
     const bool use_graph = (!distributed || graph_collectives) && !(ng != nullptr && ng[0] == '1');
     bool launched = false;
@@ -1293,6 +1294,8 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
     const bool root_scanned = h_step_->root_count >= 2 * config_->min_data_in_leaf;  // global count
+    Log::Debug("device learner: %d splits, %d by-node draws, root count %d", num_splits, h_step_->bynode_next,
+               h_step_->root_count);
     if (bynode_ic) {
       // the device generator went on from the root's draw: the host one takes its state
       if (root_scanned) {
@@ -1315,7 +1318,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     }
   }
   if (a.ktrace != nullptr && !rounds) ReportKernelTrace(num_splits);
-  if (const char* kp = std::getenv("LGBM_AMD_KERNEL_PROBE")) {
+  if (const char* kp = tuning::Get(tuning::Knob::KernelProbe)) {
     if (kp[0] == '1' && !rounds) KernelFloorProbe(a);
   }
   const bool track = !config_->interaction_constraints_vector.empty();
@@ -1441,7 +1444,7 @@ bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction
   if (!device_mode_ || obj == nullptr || !obj->DeviceRenew(&spec) || spec.label == nullptr || d_score_ == nullptr) {
     return false;
   }
-  const char* hr = std::getenv("LGBM_AMD_HOST_RENEW");  // =1: the host path (A/B, tests)
+  const char* hr = tuning::Get(tuning::Knob::HostRenew);  // =1: the host path (A/B, tests)
   if (hr != nullptr && hr[0] == '1') return false;
   HIPCHECK(hipSetDevice(device_id_));
   const int L = tree->num_leaves();
@@ -1575,7 +1578,7 @@ bool GPUTreeLearner::SetupForcedSplits() {
 // forces the word matrix / the sparse lists (when allowed).
 bool GPUTreeLearner::UseSparseRows(int wpr) const {
   if (total_bins_ > 65535 || num_data_ <= 0 || (distributed_ && mode_ == Mode::kFeature)) return false;
-  if (const char* e = std::getenv("LGBM_AMD_SPARSE_ROWS")) return e[0] == '1';
+  if (const char* e = tuning::Get(tuning::Knob::SparseRows)) return e[0] == '1';
   const data_size_t step = std::max<data_size_t>(1, num_data_ / 65536);
   int64_t stored = 0, rows = 0;
   for (data_size_t r = 0; r < num_data_; r += step, ++rows) {

@@ -25,6 +25,7 @@
 
 #include "../device/kernels.h"
 #include "lgbm_amd/device_learner.h"
+#include "lgbm_amd/tuning.h"
 #include "serial_tree_learner.h"
 
 namespace lgbm_amd {
@@ -161,8 +162,8 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int round_graph_rows_ = -1, round_graph_identity_ = -1, round_graph_root_mode_ = -1;
   // provisioning of the enqueued rounds (RunRounds): history length, margin, rounds per segment
   // graph, rounds in the root graph (0: the provisioned count rounded up to segments)
-  size_t round_hist_n_ = 3;
-  int round_margin_ = 0, round_seg_ = 4, round_root_fixed_ = 0;
+  size_t round_hist_n_ = tuning::kRoundHistory;
+  int round_margin_ = 0, round_seg_ = tuning::kRoundSegment, round_root_fixed_ = 0;
   std::vector<int> round_hist_;  // rounds of the last round_hist_n_ trees (the next one enqueues their max + margin)
   bool last_tree_rounds_ = false;
   // per-tree round width (LGBM_AMD_ROUND_K unset): the last round tree's speculation outcome
@@ -254,6 +255,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool mode_decided_ = false;  // the first decision is logged too
   bool force_host_mode_ = false;
   double* d_leaf_sums_ = nullptr;
+  double* d_root_blk_ = nullptr;  // RootSum's per-workgroup partials
   int device_id_ = 0;
   hipStream_t stream_ = nullptr;
   dev::KArgs args_{};
@@ -362,6 +364,12 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   double* d_label_gain_ = nullptr;
   double* d_discount_ = nullptr;
   double* d_sig_table_ = nullptr;  // lambdarank: the objective's sigmoid table
+  // listwise queries of more than kRankMaxDocs documents and their global scratch (RankArgs::big_*)
+  int32_t* d_rank_big_q_ = nullptr;
+  int32_t rank_num_big_ = 0;
+  double *d_rank_big_d0_ = nullptr, *d_rank_big_d1_ = nullptr;
+  float* d_rank_big_f_ = nullptr;
+  int32_t *d_rank_big_i0_ = nullptr, *d_rank_big_i1_ = nullptr, *d_rank_big_i2_ = nullptr;
   uint32_t* d_rank_rng_ = nullptr;
   const data_size_t* uploaded_qb_src_ = nullptr;
   // device row sampling (bagging / GOSS)
@@ -393,6 +401,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
       double* label_gain = nullptr;
       double* discount = nullptr;
       void* scratch = nullptr;
+      bool big = false;  // a query longer than the LDS staging
     };
     std::unordered_map<const void*, QueryInputs> queries;
     std::set<int> logged_kinds;  // metric kinds evaluated here so far (debug log)

@@ -162,7 +162,8 @@ def test_listwise_gradients_on_device(gpu_available, objective):
 
 def _last_gradients(bst):
     import ctypes
-    from lightgbmv1_amd.basic import _LIB, _safe_call
+    from lightgbmv1_amd.basic import _load_lib, _safe_call
+    _LIB = _load_lib()
     n = ctypes.c_int64(0)
     _safe_call(_LIB.LGBM_AMD_BoosterLastGradients(bst.handle, None, None, ctypes.byref(n)))
     g = np.zeros(n.value, dtype=np.float32)
@@ -172,8 +173,9 @@ def _last_gradients(bst):
     return g, h
 
 
-@pytest.mark.parametrize("extra", [{}, {"lambdarank_norm": False}, {"weighted": True}, {"sigmoid": 2.5}],
-                         ids=["norm", "no_norm", "weighted", "sigmoid"])
+@pytest.mark.parametrize("extra", [{}, {"lambdarank_norm": False}, {"weighted": True}, {"sigmoid": 2.5},
+                                   {"big": True}],
+                         ids=["norm", "no_norm", "weighted", "sigmoid", "queries_over_2048_docs"])
 def test_lambdarank_device_gradients_equal_host(gpu_available, extra):
     """The device LambdaRank kernel replays the reference's accumulation (float sums of each
     document's lower-side pairs in the sorted order of the higher side, the double sum of its
@@ -181,9 +183,15 @@ def test_lambdarank_device_gradients_equal_host(gpu_available, extra):
     rank_objective.hpp:139-229): its gradients equal the host objective's bit for bit, from
     random initial scores with ties (so device GOSS samples the host's rows)."""
     X, y, group = _rank_data(nq=200, seed=8)
+    extra = dict(extra)
+    if extra.pop("big", False):
+        # queries longer than the LDS staging (kRankMaxDocs = 2048): the global-scratch kernel
+        rng0 = np.random.RandomState(4)
+        group = np.array([3000, 40, 2500, 30, 60], dtype=np.int64)
+        X = rng0.randn(int(group.sum()), 6).astype(np.float32)
+        y = np.clip(np.floor(X[:, 0] + 0.3 * rng0.randn(len(X)) + 1.5), 0, 4).astype(np.float32)
     rng = np.random.RandomState(2)
     init = np.round(rng.randn(len(y)) * 2, 1)  # (rounded: tied scores inside queries)
-    extra = dict(extra)
     weight = None
     if extra.pop("weighted", False):
         weight = np.repeat(rng.choice([0.5, 1.0, 2.0], size=len(group)), group).astype(np.float32)
@@ -197,6 +205,27 @@ def test_lambdarank_device_gradients_equal_host(gpu_available, extra):
     for k in range(2):
         assert np.abs(out["cpu"][k]).sum() > 0
         np.testing.assert_array_equal(out["gpu"][k], out["cpu"][k])
+
+
+@pytest.mark.parametrize("boosting", ["gbdt", "goss"])
+def test_lambdarank_ndcg_equals_cpu_learner(gpu_available, boosting):
+    """Config #4's parity at test size: LambdaRank (and LambdaRank + GOSS, with the CPU
+    learner's GOSS blocks laid out as the device's: one per 1024 rows) on the device -- fx64
+    histograms, chosen by gpu_hist_precision=auto for listwise objectives, and gradients equal
+    to the host's bit for bit -- gives the CPU learner's NDCG@10."""
+    X, y, group = _rank_data(nq=400, seed=11)
+    n = len(y)
+    res = {}
+    for device in ("cpu", "gpu"):
+        params = {"objective": "lambdarank", "num_leaves": 31, "min_data_in_leaf": 5, "learning_rate": 0.1,
+                  "max_bin": 63, "verbose": -1, "device_type": device, "seed": 3, "boosting": boosting}
+        if boosting == "goss" and device == "cpu":
+            params["num_threads"] = (n + 1023) // 1024
+        ds = lgb.Dataset(X, y, group=group, params=params)
+        b = lgb.train(params, ds, 40, verbose_eval=False)
+        res[device] = _ndcg_at(y, b.predict(X), group)
+    assert res["gpu"] > 0.7
+    assert abs(res["gpu"] - res["cpu"]) < 1e-6, res
 
 
 def _bag_counts(device, boosting, rounds, fixed_gradients=False, **extra):
@@ -646,7 +675,8 @@ def test_intermediate_monotone_on_gpu(case, gpu_available, monkeypatch, capfd):
     assert np.corrcoef(gpu.predict(X), cpu.predict(X))[0, 1] > 0.999
 
 
-@pytest.mark.parametrize("task", ["lambdarank", "multiclass", "aucmu_weighted", "regression_family"])
+@pytest.mark.parametrize("task", ["lambdarank", "lambdarank_long_queries", "multiclass", "aucmu_weighted",
+                                  "regression_family"])
 def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, capfd):
     """Validation metrics evaluated on device-resident scores (NDCG / MAP one workgroup per
     query, multiclass on class-major scores, point-wise regression losses) equal the host
@@ -654,10 +684,14 @@ def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, cap
     rng = np.random.RandomState(3)
     n, nv = 8000, 3000
     X, Xv = rng.randn(n, 8), rng.randn(nv, 8)
-    if task == "lambdarank":
+    if task.startswith("lambdarank"):
         y = np.clip(np.round(X[:, 0] + X[:, 1] + rng.randn(n)), 0, 4)
         yv = np.clip(np.round(Xv[:, 0] + Xv[:, 1] + rng.randn(nv)), 0, 4)
         group, gv = [40] * (n // 40), [30] * (nv // 30)
+        if task == "lambdarank_long_queries":
+            # queries longer than the LDS staging (2048 documents): the global-scratch kernels of
+            # the gradients and of the metrics
+            group, gv = [3000, 2600] + [40] * 60, [2100] + [30] * 30
         params = {"objective": "lambdarank", "metric": ["ndcg", "map"], "eval_at": [1, 3, 5, 10]}
     elif task in ("multiclass", "aucmu_weighted"):
         y = (np.argmax(X[:, :4] + 0.5 * rng.randn(n, 4), axis=1)).astype(float)
@@ -687,7 +721,7 @@ def test_device_metrics_equal_host_metrics(task, gpu_available, monkeypatch, cap
     params["verbose"] = 2
     dev = run()
     logged = capfd.readouterr().out
-    kinds = {"lambdarank": (30, 31), "multiclass": (20, 21, 22), "aucmu_weighted": (22,),
+    kinds = {"lambdarank": (30, 31), "lambdarank_long_queries": (30, 31), "multiclass": (20, 21, 22), "aucmu_weighted": (22,),
              "regression_family": (10, 13, 7, 8, 11)}[task]
     for k in kinds:  # the device path ran
         assert "device metric (kind %d)" % k in logged, k
@@ -764,7 +798,8 @@ def test_training_metrics_after_reset_training_data(gpu_available, monkeypatch):
     training scores: the device training metrics then read the new scores, labels and weights
     (not the freed buffers of the old rows), equal to the host evaluation."""
     import ctypes
-    from lightgbmv1_amd.basic import _LIB, _safe_call
+    from lightgbmv1_amd.basic import _load_lib, _safe_call
+    _LIB = _load_lib()
     rng = np.random.RandomState(9)
 
     def data(n):
@@ -837,18 +872,47 @@ def test_percentile_renewal_on_device(extra, gpu_available, monkeypatch):
 
 
 @pytest.mark.parametrize("extra", [{}, {"bagging_fraction": 0.7, "bagging_freq": 1},
-                                   {"objective": "multiclass", "num_class": 3}, {"gpu_use_dp": True}],
-                         ids=["binary", "bagging", "multiclass", "wide"])
+                                   {"objective": "multiclass", "num_class": 3}, {"gpu_use_dp": True},
+                                   {"negative_weights": True},
+                                   {"negative_weights": True, "bagging_fraction": 0.7, "bagging_freq": 1}],
+                         ids=["binary", "bagging", "multiclass", "wide", "negative_weights", "negative_weights_bagging"])
 def test_device_training_is_bitwise_deterministic(extra, gpu_available):
     """Run-to-run determinism of device training: histograms are exact integer sums and every
-    reduction has a fixed order, so two runs give the same model text, bit for bit."""
+    reduction has a fixed order (the root sums included), so two runs give the same model text,
+    bit for bit -- with negative hessians too (negative weights: the packed histogram's h half
+    is signed, UnpackPartial)."""
     X, y = _data(40000, seed=21)
+    extra = dict(extra)
+    weight = None
+    if extra.pop("negative_weights", False):
+        weight = np.random.RandomState(3).choice([-0.5, 0.5, 1.0, 2.5], size=len(y))
     if extra.get("objective") == "multiclass":
         y = (np.digitize(X[:, 0], [-0.5, 0.5])).astype(np.float32)
     params = {"objective": "binary", "verbose": -1, "device_type": "gpu", "num_leaves": 31, "seed": 5}
     params.update(extra)
-    runs = [lgb.train(params, lgb.Dataset(X, y), 10).model_to_string() for _ in range(2)]
+    runs = [lgb.train(params, lgb.Dataset(X, y, weight=weight), 10).model_to_string() for _ in range(2)]
     assert runs[0] == runs[1]
+
+
+def test_negative_hessians_packed_histograms(gpu_available):
+    """Negative hessians (negative weights) in the packed fx32 histograms: k_scales keeps the h
+    half signed (|h| <= 2^30 per row block) and UnpackPartial returns its borrow to g, so the
+    packed trees agree with the wide (int64 g, int64 h) ones up to fixed-point rounding."""
+    rng = np.random.RandomState(8)
+    n = 30000
+    X = rng.randn(n, 10)
+    y = (X[:, 0] + 0.7 * X[:, 1] * X[:, 2] + 0.3 * rng.randn(n) > 0).astype(float)
+    w = rng.choice([-0.5, 0.5, 1.0, 2.5], size=n)
+    base = {"objective": "binary", "verbose": -1, "device_type": "gpu", "num_leaves": 31, "seed": 5,
+            "min_data_in_leaf": 5, "lambda_l2": 1.0}
+    preds = {}
+    for prec in ("fx32", "fx64"):
+        params = dict(base, gpu_hist_precision=prec)
+        b = lgb.train(params, lgb.Dataset(X, y, weight=w), 5)
+        preds[prec] = b.predict(X, raw_score=True)
+    assert np.isfinite(preds["fx32"]).all() and np.isfinite(preds["fx64"]).all()
+    d = np.abs(preds["fx32"] - preds["fx64"])
+    assert np.median(d) < 1e-4 and np.mean(d < 1e-3) > 0.98, (np.median(d), np.mean(d < 1e-3), d.max())
 
 
 @pytest.mark.parametrize("env", [{"LGBM_AMD_SPARSE_ROWS": "1"}, {"LGBM_AMD_UNIFORM_BINS": "1"}, {"LGBM_AMD_GH_IN_ROWS": "1"}])
