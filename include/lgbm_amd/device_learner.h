@@ -40,6 +40,11 @@ class DeviceTreeLearner {
   virtual void MultiplyScore(double v, int tree_id) = 0;
   // after Train(): add the new tree by leaf partition (+ out-of-bag rows by traversal)
   virtual void AddTrainedTreeToScore(const Tree* tree, int tree_id) = 0;
+  // a promise for the next Train(): its tree goes into the training scores of class 0 through
+  // AddTrainedTreeToScore, after Tree::Shrinkage(shrinkage) and nothing else (GBDT::TrainOneIter
+  // without leaf renewal).  The learner may then add it on the device as soon as the splits are
+  // known, while the host builds the Tree object (0: no promise)
+  virtual void ExpectTrainingScoreUpdate(double shrinkage) { (void)shrinkage; }
   // any tree, by traversal of the binned training rows
   virtual void AddTreeToScore(const Tree* tree, int tree_id) = 0;
   // device gradients for a point-wise objective; false if the spec is unsupported

@@ -47,6 +47,9 @@ constexpr int kPeerStageMbProcesses = 64;  // peer comm stage, one process per G
   X(RoundFused, "LGBM_AMD_ROUND_FUSED", "0: separate partition and histogram kernels per round")               \
   X(PlanInFind, "LGBM_AMD_PLAN_IN_FIND", "0: the round's plan in a kernel of its own")                         \
   X(FuseGrad, "LGBM_AMD_FUSE_GRAD", "0: the score walk does not compute the next gradients")                   \
+  X(EarlyScore, "LGBM_AMD_EARLY_SCORE", "0: the training scores take the tree after the host has built it")     \
+  X(GraphCopyNodes, "LGBM_AMD_GRAPH_COPY_NODES", "1: the tree's scratch zeroing / mask upload as memset / memcpy nodes")  \
+  X(HostOut, "LGBM_AMD_HOST_OUT", "0: the host copies a round tree's records instead of its last plan writing them")  \
   /* storage layout (same models) */                                                                           \
   X(NibbleBins, "LGBM_AMD_NIBBLE_BINS", "1: 4-bit rows for groups of <= 16 bins (auto above 32 GiB)")          \
   X(ColumnCopy, "LGBM_AMD_COLUMN_COPY", "0/1: column-major copy of the bins (auto below 8 GiB)")                \

@@ -567,6 +567,12 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
     std::unique_ptr<Tree> tree(new Tree(2, false));
     t_phase = Clock::now();
     if (class_need_train_[k] && train_data_->num_features() > 0) {
+      // the tree goes into the training scores right after its shrinkage unless its leaves
+      // are renewed first: the device learner may add it while the host builds the Tree
+      if (device_learner_ != nullptr && num_tree_per_iteration_ == 1 &&
+          !(objective_ != nullptr && objective_->IsRenewTreeOutput())) {
+        device_learner_->ExpectTrainingScoreUpdate(shrinkage_rate_);
+      }
       tree.reset(tree_learner_->Train(grad + off, hess + off));
     }
     if (iter_log_) {
@@ -809,6 +815,10 @@ void GBDT::GetPredictAt(int data_idx, double* out, int64_t* out_len) {
   const double* raw;
   data_size_t n;
   if (data_idx == 0) {
+    if (train_score_updater_ == nullptr) {
+      Log::Fatal("GetPredictAt: the booster holds no training data (a booster loaded from a model, or one whose "
+                 "dataset was freed)");
+    }
     raw = HostTrainScore();
     n = num_data_;
   } else {

@@ -931,6 +931,7 @@ int LGBM_BoosterGetNumClasses(BoosterHandle handle, int* out_len) {
 
 int LGBM_BoosterUpdateOneIter(BoosterHandle handle, int* is_finished) {
   API_BEGIN();
+  common::ScopedTimer timer("LGBM_BoosterUpdateOneIter");
   *is_finished = static_cast<Booster*>(handle)->TrainOneIter() ? 1 : 0;
   API_END();
 }

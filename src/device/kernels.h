@@ -35,6 +35,11 @@ struct KArgs {
   Leaf* leaves;              // [num_leaves]
   Step* st;
   SplitRecord* rec;          // [num_leaves - 1]
+  // round growth, one process: pinned host memory (fine-grained) the last plan of a tree fills
+  // with the tree's split records (from word kHostOutHeaderWords) and then its scalars
+  // [done, splits, rounds, nodes] -- the host waits on that flag instead of the stream (null:
+  // the host copies the Round record and the records)
+  int32_t* host_out;
   DeviceSplit* best;         // [num_leaves]
   // histograms hold fixed-point sums: int64 (g * scale_g, h * scale_h) per bin, exact and
   // order-independent (LDS float atomics are slow on gfx950; integer ones are not)
@@ -268,7 +273,10 @@ int PackBlocks(int64_t n);
 // fixed-point scales of this tree from absmax: packed (hist_units 1) scales leave headroom
 // for rows_cap rows per row block; wide ones (2) quantise each row to 31 bits of max|g|
 void ComputeScales(const uint32_t* absmax, int rows_cap, int hist_units, double* scales, hipStream_t s);
-void TreeBegin(const KArgs& a, hipStream_t s);
+// the tree's device state reset; optionally zero `zero_bytes` at `zero` (8-byte words) and copy
+// the tree's feature mask from fine-grained host memory into KArgs::tree_mask
+void TreeBegin(const KArgs& a, hipStream_t s, void* zero = nullptr, size_t zero_bytes = 0,
+               const int8_t* mask_host = nullptr, int nmask = 0);
 void RootSum(const KArgs& a, hipStream_t s);
 int RootSumBlocks();  // (KArgs::root_blk holds 2 doubles per block)
 // histograms: per-row-block partials, then an exact int64 reduction into scratch buffer 0
@@ -343,6 +351,14 @@ struct DevTree {
 };
 void AddTreeScore(const KArgs& a, const DevTree& t, const int32_t* rows, int64_t num_rows, double* score,
                   hipStream_t s);
+// The tree of the first nsplit split records (KArgs::rec) in the DevTree layout, leaf values
+// times `shrinkage`, exactly as Tree::Split / SplitCategorical and Tree::Shrinkage build them on
+// the host (categorical sets kMaxCatWords words each): the training scores can take the tree
+// while the host builds its own.  `blob` holds TreeFromRecordsBytes(max_leaves) bytes; the
+// returned DevTree points into it (bm_work / bm_meta left null).
+size_t TreeFromRecordsBytes(int max_leaves);
+constexpr int kHostOutHeaderWords = 16;  // KArgs::host_out: the scalars' words before the records
+DevTree TreeFromRecords(const KArgs& a, int nsplit, int max_leaves, double shrinkage, char* blob, hipStream_t s);
 // whether AddTreeScore walks every row with the bitmap kernel (8-bit word rows of <= 64 bytes,
 // <= 255 internal nodes); otherwise a partition-ordered scatter of leaf values is cheaper
 bool TreeBitmapsApply(const KArgs& a, int num_leaves);

@@ -1,5 +1,8 @@
 // Small per-tree kernels of the MI355X learner: gradient packing + fixed-point scale
 // selection, tree reset, root statistics and score arithmetic.
+#include <algorithm>
+#include <stdexcept>
+
 #include "device_common.h"
 #include "lgbm_amd/tuning.h"
 
@@ -93,7 +96,19 @@ void ComputeScales(const uint32_t* absmax, int rows_cap, int units, double* scal
 }
 
 // ---------------------------------------------------------------- tree reset
-__global__ void k_tree_begin(KArgs a) {
+// Every workgroup zeroes its share of `zero` (the histogram scratch of the tree's first step or
+// round) and block 0 also copies the tree's feature mask from fine-grained host memory:
+// kernel work instead of memset / memcpy graph nodes, whose boundaries stalled the graph
+// (~10-30 us each, profiles/r05_round_latency_ab.md).
+__global__ void k_tree_begin(KArgs a, unsigned long long* zero, int64_t zero_words, const int8_t* mask_host, int nmask) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < zero_words;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    zero[i] = 0ull;
+  }
+  if (blockIdx.x != 0) return;
+  for (int f = threadIdx.x; mask_host != nullptr && f < nmask; f += blockDim.x) {
+    const_cast<int8_t*>(a.tree_mask)[f] = mask_host[f];
+  }
   const int L = a.p.num_leaves;
   for (int l = threadIdx.x; l < L; l += blockDim.x) {
     Leaf lf;
@@ -153,7 +168,13 @@ __global__ void k_tree_begin(KArgs a) {
   }
 }
 
-void TreeBegin(const KArgs& a, hipStream_t s) { hipLaunchKernelGGL(k_tree_begin, dim3(1), dim3(256), 0, s, a); }
+void TreeBegin(const KArgs& a, hipStream_t s, void* zero, size_t zero_bytes, const int8_t* mask_host, int nmask) {
+  const int64_t words = static_cast<int64_t>(zero_bytes / 8);
+  if (zero_bytes % 8 != 0) throw std::runtime_error("TreeBegin: the zeroed range is not in 8-byte words");
+  const int blocks = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(2 * NumCUs(), (words + 2047) / 2048)));
+  hipLaunchKernelGGL(k_tree_begin, dim3(blocks), dim3(256), 0, s, a, static_cast<unsigned long long*>(zero), words,
+                     mask_host, nmask);
+}
 
 __global__ __launch_bounds__(256) void k_root_sum(KArgs a) {
   __shared__ double sh[8];

@@ -1329,6 +1329,31 @@ __device__ int PredictRegs(const KArgs& a, int L, int s, int used, int kround, c
 // the sequential order is predicted to need next, the leaf that ended the replay first,
 // within the tree's expansion budget.
 // Global loads are issued in few independent batches: every one is a ~1-2 us round trip.
+// The finished tree to the host (KArgs::host_out): every split record in order (a numerical
+// split's category words skipped), then the scalars with a system-scope release, so the host
+// sees them only after the records.
+__device__ void HostTreeOut(const KArgs& a, int nsplit, int rounds, int nodes) {
+  constexpr int kRecWords = static_cast<int>(sizeof(SplitRecord) / 8);
+  constexpr int kCatWord0 =
+      static_cast<int>((__builtin_offsetof(SplitRecord, split) + __builtin_offsetof(DeviceSplit, cat_bits) + 7) / 8);
+  static_assert(sizeof(SplitRecord) % 8 == 0, "8-byte words");
+  unsigned long long* dst = reinterpret_cast<unsigned long long*>(a.host_out + kHostOutHeaderWords);
+  const unsigned long long* src = reinterpret_cast<const unsigned long long*>(a.rec);
+  for (int i = threadIdx.x; i < nsplit * kRecWords; i += blockDim.x) {
+    const int r = i / kRecWords, w = i - r * kRecWords;
+    if (w >= kCatWord0 && !a.rec[r].split.is_categorical) continue;
+    dst[i] = src[i];
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&a.host_out[1], nsplit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.host_out[2], rounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.host_out[3], nodes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.host_out[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <bool ROOT, int NT>
 __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   constexpr int kPlanThreads = NT;
@@ -1723,6 +1748,10 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       rd->nsplit = s1;
       rd->nexp = 0;
       rd->accepted_max = max(accmax0, nacc);
+    }
+    if (a.host_out != nullptr) {
+      __syncthreads();  // (this plan's records are written)
+      HostTreeOut(a, s1, rounds0, nn);
     }
     return;
   }

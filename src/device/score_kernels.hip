@@ -7,6 +7,7 @@
 // scores are streamed in order (coalesced), which beats scattering leaf values through
 // the partition order.
 #include <cstdlib>
+#include <stdexcept>
 #include <type_traits>
 
 #include "objective_common.h"
@@ -336,6 +337,119 @@ __global__ __launch_bounds__(kBmRowsPerBlock) __attribute__((amdgpu_waves_per_eu
     ga.root_parts[2 * blockIdx.x] = tg;
     ga.root_parts[2 * blockIdx.x + 1] = th;
   }
+}
+
+// ---------------------------------------------------------------- tree from split records
+namespace {
+struct TreeBlob {
+  int32_t* split_feature_inner;
+  int32_t* left_child;
+  int32_t* right_child;
+  int32_t* cat_boundaries_inner;
+  uint32_t* threshold_in_bin;
+  uint32_t* cat_threshold_inner;
+  double* leaf_value;
+  int8_t* decision_type;
+};
+TreeBlob BlobLayout(char* blob, int max_leaves) {
+  const size_t ni = static_cast<size_t>(std::max(1, max_leaves - 1));
+  auto up8 = [](size_t x) { return (x + 7) & ~static_cast<size_t>(7); };
+  TreeBlob b;
+  size_t o = 0;
+  b.leaf_value = reinterpret_cast<double*>(blob + o);
+  o += up8(sizeof(double) * (ni + 1));
+  b.split_feature_inner = reinterpret_cast<int32_t*>(blob + o);
+  o += up8(4 * ni);
+  b.left_child = reinterpret_cast<int32_t*>(blob + o);
+  o += up8(4 * ni);
+  b.right_child = reinterpret_cast<int32_t*>(blob + o);
+  o += up8(4 * ni);
+  b.cat_boundaries_inner = reinterpret_cast<int32_t*>(blob + o);
+  o += up8(4 * (ni + 1));
+  b.threshold_in_bin = reinterpret_cast<uint32_t*>(blob + o);
+  o += up8(4 * ni);
+  b.decision_type = reinterpret_cast<int8_t*>(blob + o);
+  o += up8(ni);
+  b.cat_threshold_inner = reinterpret_cast<uint32_t*>(blob + o);
+  return b;
+}
+}  // namespace
+
+// One workgroup.  Split s is internal node s; its left child starts as its leaf and its right
+// child as the new leaf s + 1 (Tree::SplitCommon), and the node takes the place of its leaf in
+// the parent -- the last earlier split that split that leaf or created it.  A leaf's value is
+// the output the last split touching it gave it (NaN -> 0), times the shrinkage, rounded to
+// zero below kZeroThreshold (Tree::Shrinkage).
+__global__ __launch_bounds__(256) void k_tree_from_records(KArgs a, int ns, double shrink, TreeBlob o) {
+  __shared__ int s_leaf[kMaxNodes];
+  __shared__ int s_cat[kMaxNodes];
+  for (int s = threadIdx.x; s < ns; s += blockDim.x) {
+    s_leaf[s] = a.rec[s].leaf;
+    s_cat[s] = a.rec[s].split.is_categorical ? 1 : 0;
+  }
+  __syncthreads();
+  for (int s = threadIdx.x; s < ns; s += blockDim.x) {
+    const DeviceSplit& d = a.rec[s].split;
+    const int f = d.feature;
+    const int missing = a.feat[f].missing_type;
+    o.split_feature_inner[s] = f;
+    o.left_child[s] = ~s_leaf[s];
+    o.right_child[s] = ~(s + 1);
+    if (s_cat[s]) {
+      int ci = 0;
+      for (int k = 0; k < s; ++k) ci += s_cat[k];
+      o.threshold_in_bin[s] = static_cast<uint32_t>(ci);
+      o.decision_type[s] = static_cast<int8_t>(1 | (missing << 2));
+      for (int w = 0; w < kMaxCatWords; ++w) o.cat_threshold_inner[static_cast<size_t>(ci) * kMaxCatWords + w] = d.cat_bits[w];
+    } else {
+      o.threshold_in_bin[s] = static_cast<uint32_t>(d.threshold);
+      o.decision_type[s] = static_cast<int8_t>((d.default_left ? 2 : 0) | (missing << 2));
+    }
+  }
+  for (int k = threadIdx.x; k <= ns; k += blockDim.x) o.cat_boundaries_inner[k] = k * kMaxCatWords;
+  __syncthreads();  // (the default children are written: the parents' slots are replaced below)
+  for (int s = 1 + static_cast<int>(threadIdx.x); s < ns; s += blockDim.x) {
+    const int l = s_leaf[s];
+    int p = s - 1;
+    while (s_leaf[p] != l && p != l - 1) --p;  // (split 0 split leaf 0: every leaf has one)
+    if (s_leaf[p] == l) o.left_child[p] = s;
+    else o.right_child[p] = s;
+  }
+  for (int l = threadIdx.x; l <= ns; l += blockDim.x) {
+    int p = ns - 1;
+    while (s_leaf[p] != l && p != l - 1) --p;
+    const DeviceSplit& d = a.rec[p].split;
+    double v = s_leaf[p] == l ? d.left_output : d.right_output;
+    if (isnan(v)) v = 0.0;
+    v *= shrink;
+    o.leaf_value[l] = (v >= -kZeroThreshold && v <= kZeroThreshold) ? 0.0 : v;
+  }
+}
+
+size_t TreeFromRecordsBytes(int max_leaves) {
+  const size_t ni = static_cast<size_t>(std::max(1, max_leaves - 1));
+  char* base = nullptr;
+  const TreeBlob b = BlobLayout(base, max_leaves);
+  return static_cast<size_t>(reinterpret_cast<char*>(b.cat_threshold_inner) - base) + 4 * ni * kMaxCatWords;
+}
+
+DevTree TreeFromRecords(const KArgs& a, int nsplit, int max_leaves, double shrinkage, char* blob, hipStream_t s) {
+  if (nsplit < 1 || nsplit > kMaxNodes || nsplit > max_leaves - 1) {
+    throw std::runtime_error("TreeFromRecords: split count out of range");
+  }
+  const TreeBlob b = BlobLayout(blob, max_leaves);
+  hipLaunchKernelGGL(k_tree_from_records, dim3(1), dim3(256), 0, s, a, nsplit, shrinkage, b);
+  DevTree t{};
+  t.num_leaves = nsplit + 1;
+  t.split_feature_inner = b.split_feature_inner;
+  t.threshold_in_bin = b.threshold_in_bin;
+  t.decision_type = b.decision_type;
+  t.left_child = b.left_child;
+  t.right_child = b.right_child;
+  t.leaf_value = b.leaf_value;
+  t.cat_boundaries_inner = b.cat_boundaries_inner;
+  t.cat_threshold_inner = b.cat_threshold_inner;
+  return t;
 }
 
 bool TreeBitmapsApply(const KArgs& a, int num_leaves) {

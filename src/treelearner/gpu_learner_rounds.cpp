@@ -1,5 +1,8 @@
 // MI355X tree learner: round growth orchestration -- pools, the round sequence and its
 // collectives, the growth-mode choice and the host loop over round segments (round_kernels.hip).
+#include <atomic>
+#include <chrono>
+
 #include "gpu_learner_internal.h"
 #include "lgbm_amd/tuning.h"
 
@@ -42,6 +45,11 @@ void GPUTreeLearner::AllocRoundState() {
   if (h_round_ == nullptr) {
     HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_round_), sizeof(dev::Round), hipHostMallocDefault));
   }
+  if (h_tree_out_ != nullptr) (void)hipHostFree(h_tree_out_);
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_tree_out_),
+                         sizeof(int32_t) * dev::kHostOutHeaderWords +
+                             sizeof(dev::SplitRecord) * std::max(1, config_->num_leaves - 1),
+                         hipHostMallocCoherent));
   a.rnode = d_rnode_;
   a.cbest = d_cbest_;
   a.cbest_cat = d_cbest_cat_;
@@ -174,7 +182,15 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
 // missing one a host round trip and a graph launch per segment)
 
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
+  common::ScopedTimer timer("GPUTreeLearner::RunRounds");
   a.rd = d_round_;
+  // one process: the tree's last plan hands its records and scalars to the host directly
+  a.host_out = (!distributed_ && !tuning::Off(tuning::Knob::HostOut)) ? h_tree_out_ : nullptr;
+  volatile int32_t* flag = a.host_out;
+  if (flag != nullptr) {
+    flag[0] = 0;  // (the previous tree's writer is long done: the host waited for it)
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+  }
   if (k_adapt_ && !k_adapt_checked_) {
     k_adapt_checked_ = true;
     double rows = static_cast<double>(num_data_);
@@ -275,18 +291,46 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     launch_seg();
     launched += seg;
   }
-  const size_t rec_bytes = sizeof(dev::SplitRecord) * std::max(1, L - 1);
-  for (;;) {
-    HIPCHECK(hipMemcpyAsync(h_round_, d_round_, sizeof(dev::Round), hipMemcpyDeviceToHost, stream_));
-    HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, rec_bytes, hipMemcpyDeviceToHost, stream_));
-    WatchdogSync();
-    if (h_round_->done) break;
-    if (launched > 2 * L + seg) {
-      Log::Fatal("device learner: round growth did not finish the tree after %d rounds (%d splits)", launched,
-                 h_round_->nsplit);
+  // the host reads the Round record's scalars only (done, splits, rounds, nodes); the split
+  // records follow once the tree is done (TrainDeviceMode)
+  constexpr size_t kRoundHeader = offsetof(dev::Round, cur);
+  tree_out_used_ = flag != nullptr;
+  if (flag != nullptr) {
+    // spin on the flag (it is set while the stream may still run the tree's surplus rounds);
+    // every ~20 us look whether the stream ran dry without it: then the tree needs more rounds
+    auto last = std::chrono::steady_clock::now();
+    for (;;) {
+      if (flag[0] != 0) break;
+      const auto now = std::chrono::steady_clock::now();
+      if (now - last < std::chrono::microseconds(20)) continue;
+      last = now;
+      const hipError_t q = hipStreamQuery(stream_);
+      if (q == hipErrorNotReady) continue;
+      HIPCHECK(q);
+      if (flag[0] != 0) break;
+      if (launched > 2 * L + seg) {
+        Log::Fatal("device learner: round growth did not finish the tree after %d rounds", launched);
+      }
+      launch_seg();
+      launched += seg;
     }
-    launch_seg();
-    launched += seg;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    h_round_->done = 1;
+    h_round_->nsplit = flag[1];
+    h_round_->rounds = flag[2];
+    h_round_->next_frow = flag[3];
+  } else {
+    for (;;) {
+      HIPCHECK(hipMemcpyAsync(h_round_, d_round_, kRoundHeader, hipMemcpyDeviceToHost, stream_));
+      WatchdogSync();
+      if (h_round_->done) break;
+      if (launched > 2 * L + seg) {
+        Log::Fatal("device learner: round growth did not finish the tree after %d rounds (%d splits)", launched,
+                   h_round_->nsplit);
+      }
+      launch_seg();
+      launched += seg;
+    }
   }
   if (a.ktrace != nullptr) {
     std::vector<long long> t(static_cast<size_t>(L) * dev::kTraceSlots);

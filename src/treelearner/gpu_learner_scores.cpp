@@ -257,9 +257,46 @@ void GPUTreeLearner::MultiplyScore(double v, int k) {
   dev::MulConst(d_score_ + static_cast<size_t>(k) * num_data_, num_data_, v, stream_);
 }
 
+bool GPUTreeLearner::FusedScoreWalk(int num_leaves, int k) const {
+  return dev::TreeBitmapsApply(args_, num_leaves) && last_grad_fusable_ && k == 0 && num_tree_per_iteration_ == 1 &&
+         dev::AddTreeScoreGradKind(last_grad_.kind) && FuseNextGradients();
+}
+
+// The tree the device just grew goes into the training scores (with the next gradients) from
+// its split records, before the host has built the Tree object: the score walk overlaps the
+// host's tree building and its return through GBDT::TrainOneIter.  AddTrainedTreeToScore then
+// only takes note.  The same DevTree and kernels as that call's fused path: the same scores.
+void GPUTreeLearner::EarlyScoreUpdate(int nsplit, double shrinkage) {
+  const int L = config_->num_leaves;
+  if (d_early_blob_ == nullptr) d_early_blob_ = Alloc<char>(dev::TreeFromRecordsBytes(L));
+  const int nbm = std::max(1, L - 1);
+  if (tree_bm_cap_ < nbm) {
+    tree_bm_cap_ = nbm;
+    d_tree_bm_ = Alloc<unsigned long long>(4 * static_cast<size_t>(nbm));
+    d_tree_bm_meta_ = Alloc<int32_t>(3 * static_cast<size_t>(nbm));
+  }
+  dev::DevTree t = dev::TreeFromRecords(args_, nsplit, L, shrinkage, d_early_blob_, stream_);
+  t.bm_work = d_tree_bm_;
+  t.bm_meta = d_tree_bm_meta_;
+  dev::AddTreeScoreGrad(args_, t, num_data_, d_score_, last_grad_, stream_);
+  early_scored_leaves_ = nsplit + 1;
+}
+
 void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
   const int nl = tree->num_leaves();
   double* score = d_score_ + static_cast<size_t>(k) * num_data_;
+  if (early_scored_leaves_ > 0) {  // (added by EarlyScoreUpdate during Train)
+    if (nl != early_scored_leaves_ || k != 0) {
+      Log::Fatal("device learner: the tree added to the training scores early has %d leaves, this one %d (class %d)",
+                 early_scored_leaves_, nl, k);
+    }
+    early_scored_leaves_ = 0;
+    grad_parts_ = dev::AddTreeScoreGradParts(num_data_);
+    grad_prefetched_ = true;
+    gh_fresh_ = false;    // (d_gh_ now holds the next iteration's gradients ...
+    split_stale_ = true;  //  ... and d_grad_ / d_hess_ are behind it until unpacked)
+    return;
+  }
   if (nl <= 1) {
     AddConstToScore(tree->LeafOutput(0), k);
     return;
@@ -268,15 +305,14 @@ void GPUTreeLearner::AddTrainedTreeToScore(const Tree* tree, int k) {
     // the bitmap walk of every row (coalesced row reads and score updates) beats the
     // partition-ordered scatter of leaf values; it also covers out-of-bag rows.  Wider or
     // row-sparse storage scatters instead (the generic walk took 5 ms per tree on 100M rows)
-    if (last_grad_fusable_ && k == 0 && num_tree_per_iteration_ == 1 && dev::AddTreeScoreGradKind(last_grad_.kind) &&
-        FuseNextGradients()) {
+    if (FusedScoreWalk(nl, k)) {
       // ... and computes the next iteration's gradients from the scores it writes
       dev::DevTree t = StageTree(tree);
       dev::AddTreeScoreGrad(args_, t, num_data_, score, last_grad_, stream_);
       grad_parts_ = dev::AddTreeScoreGradParts(num_data_);
       grad_prefetched_ = true;
-      gh_fresh_ = false;  // (d_gh_ now holds the next iteration's gradients)
-      split_stale_ = false;
+      gh_fresh_ = false;    // (d_gh_ now holds the next iteration's gradients ...
+      split_stale_ = true;  //  ... and d_grad_ / d_hess_ are behind it until unpacked)
       return;
     }
     AddTreeToScore(tree, k);

@@ -54,7 +54,7 @@ void GPUTreeLearner::FreeBuffers() {
   for (void** hp : {reinterpret_cast<void**>(&h_mask_), reinterpret_cast<void**>(&h_rec_),
                     reinterpret_cast<void**>(&h_step_), reinterpret_cast<void**>(&h_root_),
                     reinterpret_cast<void**>(&h_absmax_), reinterpret_cast<void**>(&h_scales_),
-                    reinterpret_cast<void**>(&h_round_)}) {
+                    reinterpret_cast<void**>(&h_round_), reinterpret_cast<void**>(&h_tree_out_)}) {
     if (*hp) (void)hipHostFree(*hp);
     *hp = nullptr;
   }
@@ -77,6 +77,8 @@ void GPUTreeLearner::FreeBuffers() {
   sample_seeded_ = false;
   d_tree_blob_ = nullptr;
   tree_blob_cap_ = 0;
+  d_early_blob_ = nullptr;
+  early_scored_leaves_ = 0;
   d_tree_bm_ = nullptr;
   d_tree_bm_meta_ = nullptr;
   tree_bm_cap_ = 0;
@@ -92,6 +94,8 @@ void GPUTreeLearner::FreeBuffers() {
 
 void GPUTreeLearner::FreeAll() {
   FreeBuffers();
+  if (rec_event_ != nullptr) (void)hipEventDestroy(rec_event_);
+  rec_event_ = nullptr;
   if (stream_) (void)hipStreamDestroy(stream_);
   stream_ = nullptr;
 }
@@ -434,7 +438,8 @@ void GPUTreeLearner::UploadData() {
   d_root_parts_ = Alloc<double>(2 * static_cast<size_t>(parts));
   d_max_parts_ = Alloc<float>(2 * static_cast<size_t>(parts));
   d_leaf_values_ = Alloc<double>(n_leaves);
-  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_mask_), std::max(1, num_features_), hipHostMallocDefault));
+  // (fine-grained: k_tree_begin reads the mask the host wrote before each tree's launch)
+  HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_mask_), std::max(1, num_features_), hipHostMallocCoherent));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_rec_), sizeof(dev::SplitRecord) * std::max(1, n_leaves - 1),
                          hipHostMallocDefault));
   HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h_step_), sizeof(dev::Step), hipHostMallocDefault));
@@ -495,6 +500,7 @@ void GPUTreeLearner::UploadData() {
   a.st = d_step_;
   a.find_sub = d_find_sub_;
   a.rec = d_rec_;
+  a.host_out = nullptr;
   a.best = d_best_;
   a.hist = d_hist_;
   a.scratch = d_scratch_;
@@ -869,6 +875,9 @@ void GPUTreeLearner::MaterializeSplitGradients() {
 Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   common::ScopedTimer timer("GPUTreeLearner::Train");
   HIPCHECK(hipSetDevice(device_id_));
+  train_shrink_ = expect_shrinkage_;  // (the promise covers this tree only)
+  expect_shrinkage_ = 0.0;
+  early_scored_leaves_ = 0;
   if (distributed_ && Network::device_comm() != nullptr) Network::device_comm()->HostBarrier();
   // fixed-point scales of this tree: max |g|, max h over all rows (and ranks)
   // the gradient kernel already interleaved (g, h) and found max|g| / max h when it wrote
@@ -1094,7 +1103,6 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
     // the whole buffer: the copy (like the tree's graph) does not depend on the bag size
     HIPCHECK(hipMemcpyAsync(d_idx_, d_bag_, sizeof(int32_t) * num_data_, hipMemcpyDeviceToDevice, stream_));
   }
-  HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
   // both step buffers start at zero; afterwards each split-scan zeroes the next one
   // (data-parallel: the owner-major buffer is cleared before every reduction)
   // both step buffers start at zero (round growth: every expansion buffer of both parities)
@@ -1104,7 +1112,15 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   if (a.ktrace != nullptr) {
     HIPCHECK(hipMemsetAsync(a.ktrace, 0, sizeof(long long) * dev::kTraceSlots * config_->num_leaves, stream_));
   }
-  dev::TreeBegin(a, stream_);
+  // (the scratch zeroing and the feature mask's upload happen in the tree's first kernel)
+  const bool copy_nodes = tuning::On(tuning::Knob::GraphCopyNodes);
+  if (copy_nodes) {
+    HIPCHECK(hipMemcpyAsync(d_tree_mask_, h_mask_, num_features_, hipMemcpyHostToDevice, stream_));
+    HIPCHECK(hipMemsetAsync(d_scratch_, 0, zero_bytes, stream_));
+    dev::TreeBegin(a, stream_);
+  } else {
+    dev::TreeBegin(a, stream_, d_scratch_, zero_bytes, h_mask_, num_features_);
+  }
   if (a.p.mono_inter) {  // (intermediate monotone: the root leaf has no parent, nothing is re-bounded yet)
     const int L = config_->num_leaves;
     HIPCHECK(hipMemsetAsync(a.mt_leaf_parent, 0xff, sizeof(int32_t) * L, stream_));
@@ -1116,7 +1132,6 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   }
   if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
   AllreduceRoot();
-  HIPCHECK(hipMemsetAsync(d_scratch_, 0, zero_bytes, stream_));
   if (a.rd != nullptr && data_parallel_ && d_round_send_ != nullptr) {  // (the first round's send buffer)
     HIPCHECK(hipMemsetAsync(d_round_send_, 0, sizeof(long long) * world_ * round_k_ * rs_block_ * 2, stream_));
   }
@@ -1321,10 +1336,28 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   if (const char* kp = tuning::Get(tuning::Knob::KernelProbe)) {
     if (kp[0] == '1' && !rounds) KernelFloorProbe(a);
   }
+  // the promised training-score update (ExpectTrainingScoreUpdate), on the device before the
+  // host builds the tree
+  // round growth: the tree's last plan wrote the split records to the host (KArgs::host_out),
+  // or they are copied now (one record per split) and the host waits for that copy only
+  const double shrink = train_shrink_;
+  const dev::SplitRecord* recs = h_rec_;
+  const bool copy_recs = rounds && num_splits > 0 && !tree_out_used_;
+  if (rounds && tree_out_used_) recs = reinterpret_cast<const dev::SplitRecord*>(h_tree_out_ + dev::kHostOutHeaderWords);
+  if (copy_recs) {
+    HIPCHECK(hipMemcpyAsync(h_rec_, d_rec_, sizeof(dev::SplitRecord) * num_splits, hipMemcpyDeviceToHost, stream_));
+    if (rec_event_ == nullptr) HIPCHECK(hipEventCreateWithFlags(&rec_event_, hipEventDisableTiming));
+    HIPCHECK(hipEventRecord(rec_event_, stream_));
+  }
+  if (shrink != 0.0 && num_splits >= 1 && FusedScoreWalk(num_splits + 1, 0) && !tuning::Off(tuning::Knob::EarlyScore)) {
+    EarlyScoreUpdate(num_splits, shrink);
+  }
+  if (copy_recs) HIPCHECK(hipEventSynchronize(rec_event_));
+  common::ScopedTimer build_timer("GPUTreeLearner::BuildTree");
   const bool track = !config_->interaction_constraints_vector.empty();
   std::unique_ptr<Tree> tree(new Tree(config_->num_leaves, track));
   for (int s = 0; s < num_splits; ++s) {
-    const dev::SplitRecord& r = h_rec_[s];
+    const dev::SplitRecord& r = recs[s];
     SplitInfo si;
     si.FromDevice(r.split);
     const int inner = si.inner_feature;

@@ -65,6 +65,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void AddConstToScore(double v, int tree_id) override;
   void MultiplyScore(double v, int tree_id) override;
   void AddTrainedTreeToScore(const Tree* tree, int tree_id) override;
+  void ExpectTrainingScoreUpdate(double shrinkage) override { expect_shrinkage_ = shrinkage; }
   void AddTreeToScore(const Tree* tree, int tree_id) override;
   bool ComputeGradients(const DeviceGradSpec& spec, int num_tree_per_iteration) override;
   void UploadGradients(const score_t* g, const score_t* h, int64_t n) override;
@@ -113,6 +114,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void KernelFloorProbe(const dev::KArgs& a);
   void MaterializeSplitGradients();
   static bool FuseNextGradients();
+  // the fused score walk (+ next gradients) applies to a tree of this many leaves
+  bool FusedScoreWalk(int num_leaves, int tree_id) const;
+  // the promised score update of the tree of the first nsplit device records (TreeFromRecords)
+  void EarlyScoreUpdate(int nsplit, double shrinkage);
   static bool SameGradArgs(const dev::GradArgs& x, const dev::GradArgs& y);
   void ReportKernelTrace(int num_splits);
   void BuildRangeHistogram(int leaf, int slot);
@@ -153,6 +158,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int split_rows_ = 0;      // rows of the splittable flags (round growth: the tree's nodes)
   dev::Round* d_round_ = nullptr;
   dev::Round* h_round_ = nullptr;
+  // KArgs::host_out (fine-grained pinned): the finished tree's scalars and split records, written
+  // by its last plan; the host waits on its flag (one process)
+  int32_t* h_tree_out_ = nullptr;
+  bool tree_out_used_ = false;  // the last round tree's records are in h_tree_out_
   dev::RNode* d_rnode_ = nullptr;
   dev::FeatureBest* d_cbest_ = nullptr;
   uint32_t* d_cbest_cat_ = nullptr;
@@ -422,6 +431,12 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   StageSlot stage_slots_[kStageSlots];
   int stage_next_ = 0;
   char* d_tree_blob_ = nullptr;
+  // ExpectTrainingScoreUpdate: the promised shrinkage of the next tree; the tree the device
+  // added to the training scores early (its leaves; 0: none) and its DevTree blob
+  double expect_shrinkage_ = 0.0, train_shrink_ = 0.0;
+  int early_scored_leaves_ = 0;
+  char* d_early_blob_ = nullptr;
+  hipEvent_t rec_event_ = nullptr;  // the split records' copy (round growth)
   size_t tree_blob_cap_ = 0;
   unsigned long long* d_tree_bm_ = nullptr;  // per-node decision bitmaps (score traversal)
   int32_t* d_tree_bm_meta_ = nullptr;

@@ -173,6 +173,18 @@ def _last_gradients(bst):
     return g, h
 
 
+def _train_scores(bst, n):
+    """the booster's training scores (LGBM_BoosterGetPredict, data 0)"""
+    import ctypes
+    from lightgbmv1_amd.basic import _load_lib, _safe_call
+    buf = np.zeros(n, dtype=np.float64)
+    got = ctypes.c_int64(0)
+    _safe_call(_load_lib().LGBM_BoosterGetPredict(bst.handle, ctypes.c_int(0), ctypes.byref(got),
+                                                  buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double))))
+    assert got.value == n
+    return buf
+
+
 @pytest.mark.parametrize("extra", [{}, {"lambdarank_norm": False}, {"weighted": True}, {"sigmoid": 2.5},
                                    {"big": True}],
                          ids=["norm", "no_norm", "weighted", "sigmoid", "queries_over_2048_docs"])
@@ -892,6 +904,34 @@ def test_device_training_is_bitwise_deterministic(extra, gpu_available):
     params.update(extra)
     runs = [lgb.train(params, lgb.Dataset(X, y, weight=weight), 10).model_to_string() for _ in range(2)]
     assert runs[0] == runs[1]
+
+
+@pytest.mark.parametrize("params", [{"objective": "binary"}, {"objective": "regression", "num_leaves": 63},
+                                    {"objective": "binary", "bagging_fraction": 0.7, "bagging_freq": 1},
+                                    {"objective": "binary", "categorical_feature": [3], "max_cat_to_onehot": 2}],
+                         ids=["binary", "regression", "bagging", "categorical"])
+def test_early_score_update_equals_host_tree_update(params, gpu_available, monkeypatch):
+    """The training scores take each tree from its device split records (TreeFromRecords) while
+    the host builds the Tree object: the same models and training scores, bit for bit, as
+    adding the host-built tree (LGBM_AMD_EARLY_SCORE=0)."""
+    rng = np.random.RandomState(12)
+    n = 30000
+    X = rng.randn(n, 8)
+    X[:, 3] = rng.randint(0, 12, n)
+    y = X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.2 * (X[:, 3] % 3) + 0.3 * rng.randn(n)
+    if params["objective"] == "binary":
+        y = (y > 0).astype(float)
+    out = {}
+    for early in ("1", "0"):
+        monkeypatch.setenv("LGBM_AMD_EARLY_SCORE", early)
+        p = dict({"verbose": -1, "device_type": "gpu", "num_leaves": 31, "seed": 4, "learning_rate": 0.2}, **params)
+        cat = p.pop("categorical_feature", "auto")
+        b = lgb.train(p, lgb.Dataset(X, y, categorical_feature=cat), 12, keep_training_booster=True)
+        out[early] = (b.model_to_string(), _train_scores(b, n), _last_gradients(b))
+    assert out["1"][0] == out["0"][0]
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+    for a, c in zip(out["1"][2], out["0"][2]):  # (the next iteration's gradients, from the fused walk)
+        np.testing.assert_array_equal(a, c)
 
 
 def test_negative_hessians_packed_histograms(gpu_available):

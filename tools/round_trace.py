@@ -5,7 +5,9 @@ launches per iteration, and the idle gaps between kernels (launch latency, graph
 host round trips).
 
   rocprofv3 --kernel-trace -d gpurun_out/rt -o run -- python3 bench.py --rows 1250000 --steps 20
-  python tools/round_trace.py gpurun_out/rt/<host>/<pid>/run_kernel_trace.csv [--skip 5]
+  python tools/round_trace.py gpurun_out/rt/run_results.db [--skip 5]
+
+The trace is rocprofv3's SQLite output (its `kernels` view) or a `*_kernel_trace.csv`.
 
 Prints a markdown table (mean us per iteration) and, with --last, the kernel sequence of the
 last iteration (gap-before / duration per launch).
@@ -13,6 +15,7 @@ last iteration (gap-before / duration per launch).
 import argparse
 import collections
 import csv
+import sqlite3
 
 
 def short(name):
@@ -35,8 +38,12 @@ def main():
     ap.add_argument("--skip", type=int, default=3, help="iterations skipped at the start (warm-up)")
     ap.add_argument("--last", action="store_true", help="print the last iteration's launches")
     args = ap.parse_args()
-    rows = list(csv.DictReader(open(args.trace)))
-    ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
+    if args.trace.endswith(".db"):
+        con = sqlite3.connect(args.trace)
+        ev = sorted((int(s), int(e), short(n)) for s, e, n in con.execute("select start, end, name from kernels"))
+    else:
+        rows = list(csv.DictReader(open(args.trace)))
+        ev = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])) for r in rows)
     starts = [i for i, e in enumerate(ev) if "k_tree_begin" in e[2]]
     if len(starts) < args.skip + 2:
         print("too few iterations: %d tree starts" % len(starts))
