@@ -61,6 +61,16 @@ def roc_auc(y, p):
     return float((ranks[pos].sum() - npos * (npos + 1) / 2.0) / max(1, npos * nneg))
 
 
+def growth_stats(booster):
+    """[trees, device-resident, rounds, expansions, splits, collective bytes] so far
+    (LGBM_AMD_BoosterGrowthStats: counters, no device synchronisation)"""
+    import ctypes
+    from lightgbmv1_amd import _native as nat
+    out = (ctypes.c_double * 6)()
+    nat.call("LGBM_AMD_BoosterGrowthStats", booster.handle, out, ctypes.c_int(6))
+    return list(out)
+
+
 def _device_sync(lgb):
     """Drain the device queue around the timed region (the learner's own HIP runtime;
     torch.cuda.synchronize() as well when torch already drives a GPU in this process)."""
@@ -97,16 +107,6 @@ def main():
 
     if world > 1:
         torch_dist.init_network(use_rccl=args.device == "gpu")
-    # per-iteration records (rounds per tree, collective bytes) for the JSON line, unless the
-    # caller already asked for them elsewhere
-    iter_log = os.environ.get("LGBM_AMD_ITER_LOG")
-    if iter_log is None and args.device == "gpu":
-        import tempfile
-        iter_log = os.path.join(tempfile.gettempdir(), "bench_iters_%d_%d.jsonl" % (os.getpid(), rank))
-        os.environ["LGBM_AMD_ITER_LOG"] = iter_log
-        own_log = True
-    else:
-        own_log = False
     n_total = args.rows
     lo = n_total * rank // world
     hi = n_total * (rank + 1) // world
@@ -137,6 +137,7 @@ def main():
         booster.update()
     torch_dist.barrier()
     _device_sync(lgb)
+    stats0 = growth_stats(booster) if args.device == "gpu" else None
     t1 = time.perf_counter()
     train_auc = None
     for _ in range(args.steps):
@@ -149,17 +150,11 @@ def main():
     elapsed = torch_dist.allreduce_max(elapsed)
     sec_per_iter = elapsed / max(1, args.steps)
     diag = {}
-    if iter_log is not None and world > 1:
-        # the native log writer suffixes the rank in distributed runs (src/boosting/gbdt.cpp)
-        iter_log += ".rank%d" % rank
-    if iter_log is not None and os.path.exists(iter_log):
-        rows = [json.loads(line) for line in open(iter_log)][-args.steps:] if args.steps > 0 else []
-        trees = [r for row in rows for r in row.get("rounds", [])]
-        if rows:
-            diag = {"rounds_per_tree": round(sum(trees) / max(1, len(trees)), 2),
-                    "collective_bytes_per_iter": round(sum(r.get("collective_bytes", 0) for r in rows) / len(rows))}
-        if own_log:
-            os.remove(iter_log)
+    if stats0 is not None and args.steps > 0:
+        # the timed trees' growth counters (no synchronisation inside the timed loop)
+        d = [b - a for a, b in zip(stats0, growth_stats(booster))]
+        diag = {"rounds_per_tree": round(d[2] / max(1.0, d[0]), 2),
+                "collective_bytes_per_iter": round(d[5] / args.steps)}
     auc = None
     if rank == 0 and args.test_rows > 0:
         Xt, yt = make_rows(n_total + 12345678, args.test_rows, args.features)

@@ -186,6 +186,7 @@ class GBDT {
   // LGBM_AMD_ITER_LOG=<path>: one JSON line per boosting iteration (phase times, trees, device
   // collectives); distributed ranks write <path>.rank<r>
   std::unique_ptr<std::ofstream> iter_log_;
+  double growth_stats_[6] = {0, 0, 0, 0, 0, 0};
   bool iter_log_checked_ = false;
   void LogIteration(double grad_ms, double bag_ms, const std::vector<double>& tree_ms, double renew_ms,
                     double score_ms, double total_ms, const std::vector<int>& leaves, const std::vector<int>& device,
@@ -222,6 +223,8 @@ class GBDT {
  public:
   // the host learner's gradients of the last iteration (tests: device vs host objectives)
   const std::vector<score_t>& host_gradients() const { return gradients_; }
+  // LGBM_AMD_BoosterGrowthStats: [trees, device-resident, rounds, expansions, splits, collective bytes]
+  const double* growth_stats() const { return growth_stats_; }
   const std::vector<score_t>& host_hessians() const { return hessians_; }
   data_size_t train_num_data() const { return num_data_; }
 

@@ -239,6 +239,10 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceLeafState(BoosterHandle handle, int 
                                                       double* sums);
 /* the gradients the last iteration trained on (device or host learner); *n = entries */
 LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterLastGradients(BoosterHandle handle, float* grad, float* hess, int64_t* n);
+// growth counters of the device learner summed over the trees trained so far: out[0] trees,
+// [1] of them grown device-resident, [2] rounds, [3] expansions, [4] splits, [5] bytes moved by
+// device collectives (no synchronisation: cheap inside a timed loop)
+LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterGrowthStats(BoosterHandle handle, double* out, int n);
 LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceGradients(BoosterHandle handle, float* grad, float* hess,
                                                       double* scales);
 // JSON report of the leaves' device best splits checked against the CPU split finder

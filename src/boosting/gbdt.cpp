@@ -574,6 +574,15 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
         device_learner_->ExpectTrainingScoreUpdate(shrinkage_rate_);
       }
       tree.reset(tree_learner_->Train(grad + off, hess + off));
+      if (device_learner_ != nullptr) {
+        const auto st = device_learner_->LastTreeStats();
+        growth_stats_[0] += 1;
+        growth_stats_[1] += st.device_mode ? 1 : 0;
+        growth_stats_[2] += st.rounds;
+        growth_stats_[3] += st.expansions;
+        growth_stats_[4] += st.splits;
+        growth_stats_[5] += st.collective_bytes;
+      }
     }
     if (iter_log_) {
       tree_ms.push_back(ms_since(t_phase));

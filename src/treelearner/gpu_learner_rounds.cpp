@@ -275,12 +275,14 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   last_stats_.graph = graph;
   auto launch_seg = [&]() {
     if (graph) {
+      common::ScopedTimer launch_timer("GPUTreeLearner::SegmentGraphLaunch");
       HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
     } else {
       for (int r = 0; r < seg; ++r) EnqueueRound(a);
     }
   };
   if (graph) {
+    common::ScopedTimer launch_timer("GPUTreeLearner::RootGraphLaunch");
     HIPCHECK(hipGraphLaunch(round_root_execs_[root_rounds], stream_));
   } else {
     EnqueueRoot(a);
