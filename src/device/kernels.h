@@ -465,9 +465,15 @@ struct RankArgs {
   // scratch of their rows instead of LDS): their indices and [num_data] scratch arrays
   const int32_t* big_q;
   int32_t num_big;
-  double *big_d0, *big_d1;
+  double *big_d0, *big_d1, *big_dh;
   float* big_f;
   int32_t *big_i0, *big_i1, *big_i2;
+  // queries of at most kRankMaxDocs documents: the most documents of one (the LDS staging is
+  // sized to it), and lambdarank's pair scratch -- query q's (high sorted position, low
+  // document) float pairs at pair_off[q] -- so that each pair is evaluated once (null: twice)
+  int32_t max_docs;
+  float2* pair_buf;
+  const int64_t* pair_off;
 };
 void RankGradients(const RankArgs& ra, hipStream_t s);
 

@@ -50,14 +50,17 @@ __device__ __forceinline__ double RankSigmoid(const RankArgs& ra, double x) {
 // probability ~2^-29.)
 template <int NT>
 __device__ void LambdarankQuery(const RankArgs& ra, int q, double* s_score, int* s_label, int* s_pos, int* s_doc,
-                                double* s_red, double* s_edge) {
+                                double* s_red, double* s_edge, double* s_disc, float2* pairs, double* hs_lam,
+                                double* hs_hes) {
 #pragma clang fp contract(off)
   const int b = ra.qb[q];
   const int cnt = ra.qb[q + 1] - b;
   for (int i = threadIdx.x; i < cnt; i += NT) {
     s_score[i] = ra.score[b + i];
     s_label[i] = static_cast<int>(ra.label[b + i]);
+    if (s_disc != nullptr) s_disc[i] = ra.discount[i];
   }
+  const double* disc = s_disc != nullptr ? s_disc : ra.discount;
   __syncthreads();
   for (int i = threadIdx.x; i < cnt; i += NT) {
     const double si = s_score[i];
@@ -96,25 +99,40 @@ __device__ void LambdarankQuery(const RankArgs& ra, int q, double* s_score, int*
   for (int d = threadIdx.x; d < cnt; d += NT) {
     const double sd = s_score[d];
     const int ld = s_label[d], kd = s_pos[d];
-    const double disc_d = ra.discount[kd];
+    const double disc_d = disc[kd];
+    // d as the higher side: its pairs in the sorted order of the lower side, summed in double
+    // (a loop of its own, run by every lane together: nested inside the sorted-order loop below
+    // at k == kd it ran once per lane, serialised over the wave -- 30x slower)
+    double hsl = 0.0, hsh = 0.0;
+    if (sd != kMinScore) {
+      for (int k2 = 0; k2 < cnt; ++k2) {
+        if (k2 == kd) continue;
+        const int j = s_doc[k2];
+        const int lj = s_label[j];
+        const double sj = s_score[j];
+        if (ld <= lj || sj == kMinScore) continue;
+        double pl, ph;
+        pair(sd, ld, disc_d, sj, lj, disc[k2], &pl, &ph);
+        hsl += pl;
+        hsh += ph;
+        sum_lambdas -= 2 * pl;
+        // (the lower side's float terms, read back below in its own order)
+        if (pairs != nullptr) pairs[static_cast<size_t>(kd) * cnt + j] = make_float2(static_cast<float>(pl), static_cast<float>(ph));
+      }
+    }
+    hs_lam[d] = hsl;  // (d's double sums: the second loop runs after the block's pair writes)
+    hs_hes[d] = hsh;
+  }
+  if (pairs != nullptr) __syncthreads();  // (block scope: the pair scratch is complete)
+  for (int d = threadIdx.x; d < cnt; d += NT) {
+    const double sd = s_score[d];
+    const int ld = s_label[d], kd = s_pos[d];
+    const double disc_d = disc[kd];
+    const double hsl = hs_lam[d], hsh = hs_hes[d];
     float lam = 0.0f, hes = 0.0f;
     for (int k = 0; k < cnt; ++k) {
       if (k == kd) {
         if (sd == kMinScore) continue;
-        // d as the higher side: its pairs in the sorted order of the lower side, summed in double
-        double hsl = 0.0, hsh = 0.0;
-        for (int k2 = 0; k2 < cnt; ++k2) {
-          if (k2 == kd) continue;
-          const int j = s_doc[k2];
-          const int lj = s_label[j];
-          const double sj = s_score[j];
-          if (ld <= lj || sj == kMinScore) continue;
-          double pl, ph;
-          pair(sd, ld, disc_d, sj, lj, ra.discount[k2], &pl, &ph);
-          hsl += pl;
-          hsh += ph;
-          sum_lambdas -= 2 * pl;
-        }
         lam = __fadd_rn(lam, static_cast<float>(hsl));
         hes = __fadd_rn(hes, static_cast<float>(hsh));
       } else {
@@ -123,10 +141,16 @@ __device__ void LambdarankQuery(const RankArgs& ra, int q, double* s_score, int*
         const int lj = s_label[j];
         const double sj = s_score[j];
         if (sj == kMinScore || lj <= ld || sd == kMinScore) continue;
-        double pl, ph;
-        pair(sj, lj, ra.discount[k], sd, ld, disc_d, &pl, &ph);
-        lam = __fsub_rn(lam, static_cast<float>(pl));
-        hes = __fadd_rn(hes, static_cast<float>(ph));
+        if (pairs != nullptr) {
+          const float2 v = pairs[static_cast<size_t>(k) * cnt + d];
+          lam = __fsub_rn(lam, v.x);
+          hes = __fadd_rn(hes, v.y);
+        } else {
+          double pl, ph;
+          pair(sj, lj, disc[k], sd, ld, disc_d, &pl, &ph);
+          lam = __fsub_rn(lam, static_cast<float>(pl));
+          hes = __fadd_rn(hes, static_cast<float>(ph));
+        }
       }
     }
     ra.grad[b + d] = lam;
@@ -151,16 +175,27 @@ __device__ void LambdarankQuery(const RankArgs& ra, int q, double* s_score, int*
   }
 }
 
+// LDS per query document: score, discount, the two double sums (8 B each); label, sorted
+// position, document at position (4 B each)
+constexpr int kRankLdsPerDoc = 4 * 8 + 3 * 4;
+size_t RankLds(int max_docs) { return static_cast<size_t>(std::max(1, max_docs)) * kRankLdsPerDoc; }
+
 __global__ __launch_bounds__(kRankThreads) void k_lambdarank(RankArgs ra) {
-  __shared__ double s_score[kRankMaxDocs];
-  __shared__ int s_label[kRankMaxDocs];
-  __shared__ int s_pos[kRankMaxDocs];  // document -> sorted position
-  __shared__ int s_doc[kRankMaxDocs];  // sorted position -> document
+  extern __shared__ double rank_lds[];  // RankLds(ra.max_docs) bytes
+  const int M = ra.max_docs;
+  double* s_score = rank_lds;
+  double* s_disc = s_score + M;
+  double* s_hl = s_disc + M;
+  double* s_hh = s_hl + M;
+  int* s_label = reinterpret_cast<int*>(s_hh + M);
+  int* s_pos = s_label + M;  // document -> sorted position
+  int* s_doc = s_pos + M;    // sorted position -> document
   __shared__ double s_red[kRankThreads / kWave];
   __shared__ double s_edge[3];  // score at sorted positions 0, cnt-1, cnt-2
   const int q = blockIdx.x;
   if (ra.qb[q + 1] - ra.qb[q] > kRankMaxDocs) return;  // (k_lambdarank_big)
-  LambdarankQuery<kRankThreads>(ra, q, s_score, s_label, s_pos, s_doc, s_red, s_edge);
+  float2* pairs = ra.pair_buf != nullptr ? ra.pair_buf + ra.pair_off[q] : nullptr;
+  LambdarankQuery<kRankThreads>(ra, q, s_score, s_label, s_pos, s_doc, s_red, s_edge, s_disc, pairs, s_hl, s_hh);
 }
 
 // queries of more than kRankMaxDocs documents: the same body over the query's rows of a global
@@ -170,7 +205,8 @@ __global__ __launch_bounds__(kRankBigThreads) void k_lambdarank_big(RankArgs ra)
   __shared__ double s_edge[3];
   const int q = ra.big_q[blockIdx.x];
   const int b = ra.qb[q];
-  LambdarankQuery<kRankBigThreads>(ra, q, ra.big_d0 + b, ra.big_i0 + b, ra.big_i1 + b, ra.big_i2 + b, s_red, s_edge);
+  LambdarankQuery<kRankBigThreads>(ra, q, ra.big_d0 + b, ra.big_i0 + b, ra.big_i1 + b, ra.big_i2 + b, s_red, s_edge,
+                                   nullptr, nullptr, ra.big_d1 + b, ra.big_dh + b);
 }
 
 // XE-NDCG (reference rank_objective.hpp:304-366): softmax over the query, per-document
@@ -265,7 +301,7 @@ __global__ __launch_bounds__(kRankBigThreads) void k_xendcg_big(RankArgs ra) {
 void RankGradients(const RankArgs& ra, hipStream_t s) {
   if (ra.num_queries <= 0) return;
   if (ra.kind == kRankKindLambdarank) {
-    hipLaunchKernelGGL(k_lambdarank, dim3(ra.num_queries), dim3(kRankThreads), 0, s, ra);
+    hipLaunchKernelGGL(k_lambdarank, dim3(ra.num_queries), dim3(kRankThreads), RankLds(ra.max_docs), s, ra);
     if (ra.num_big > 0) hipLaunchKernelGGL(k_lambdarank_big, dim3(ra.num_big), dim3(kRankBigThreads), 0, s, ra);
   } else {
     hipLaunchKernelGGL(k_xendcg, dim3(ra.num_queries), dim3(kRankThreads), 0, s, ra);

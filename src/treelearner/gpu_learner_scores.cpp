@@ -484,6 +484,10 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     ra.num_big = rank_num_big_;
     ra.big_d0 = d_rank_big_d0_;
     ra.big_d1 = d_rank_big_d1_;
+    ra.big_dh = d_rank_big_dh_;
+    ra.max_docs = rank_max_docs_;
+    ra.pair_buf = d_rank_pairs_;
+    ra.pair_off = d_rank_pair_off_;
     ra.big_f = d_rank_big_f_;
     ra.big_i0 = d_rank_big_i0_;
     ra.big_i1 = d_rank_big_i1_;
@@ -568,14 +572,35 @@ void GPUTreeLearner::UploadRankTables(const DeviceRankSpec& r, DeviceGradKind ki
     d_rank_rng_ = Alloc<uint32_t>(nq);
     HIPCHECK(hipMemcpy(d_rank_rng_, r.rng_states, sizeof(uint32_t) * nq, hipMemcpyHostToDevice));
   }
-  // queries longer than the LDS staging: one 1024-thread workgroup each over a global scratch
+  // queries longer than the LDS staging: one 1024-thread workgroup each over a global scratch;
+  // the others' LDS is sized to the longest of them.  Lambdarank: the pair scratch of every
+  // LDS-staged query (cnt^2 float pairs each), within a memory budget
   std::vector<int32_t> big;
+  std::vector<int64_t> pair_off(nq, 0);
+  int64_t pair_total = 0;
+  rank_max_docs_ = 1;
   for (size_t q = 0; q < nq; ++q) {
-    if (r.query_boundaries[q + 1] - r.query_boundaries[q] > dev::kRankMaxDocs) big.push_back(static_cast<int32_t>(q));
+    const int64_t cnt = r.query_boundaries[q + 1] - r.query_boundaries[q];
+    if (cnt > dev::kRankMaxDocs) {
+      big.push_back(static_cast<int32_t>(q));
+      continue;
+    }
+    rank_max_docs_ = std::max<int32_t>(rank_max_docs_, static_cast<int32_t>(cnt));
+    pair_off[q] = pair_total;
+    pair_total += cnt * cnt;
+  }
+  d_rank_pairs_ = nullptr;
+  d_rank_pair_off_ = nullptr;
+  constexpr int64_t kPairBudgetBytes = int64_t{6} << 30;
+  if (kind == DeviceGradKind::Lambdarank && pair_total > 0 &&
+      pair_total * static_cast<int64_t>(sizeof(float2)) <= kPairBudgetBytes) {
+    d_rank_pairs_ = Alloc<float2>(static_cast<size_t>(pair_total));
+    d_rank_pair_off_ = Alloc<int64_t>(nq);
+    HIPCHECK(hipMemcpy(d_rank_pair_off_, pair_off.data(), sizeof(int64_t) * nq, hipMemcpyHostToDevice));
   }
   rank_num_big_ = static_cast<int32_t>(big.size());
   d_rank_big_q_ = nullptr;
-  d_rank_big_d0_ = d_rank_big_d1_ = nullptr;
+  d_rank_big_d0_ = d_rank_big_d1_ = d_rank_big_dh_ = nullptr;
   d_rank_big_f_ = nullptr;
   d_rank_big_i0_ = d_rank_big_i1_ = d_rank_big_i2_ = nullptr;
   if (!big.empty()) {
@@ -584,6 +609,7 @@ void GPUTreeLearner::UploadRankTables(const DeviceRankSpec& r, DeviceGradKind ki
     HIPCHECK(hipMemcpy(d_rank_big_q_, big.data(), sizeof(int32_t) * big.size(), hipMemcpyHostToDevice));
     d_rank_big_d0_ = Alloc<double>(n);
     d_rank_big_d1_ = Alloc<double>(n);
+    d_rank_big_dh_ = Alloc<double>(n);
     d_rank_big_f_ = Alloc<float>(n);
     d_rank_big_i0_ = Alloc<int32_t>(n);
     d_rank_big_i1_ = Alloc<int32_t>(n);

@@ -66,7 +66,10 @@ void GPUTreeLearner::FreeBuffers() {
   d_inv_max_dcg_ = d_label_gain_ = d_discount_ = d_sig_table_ = nullptr;
   d_rank_big_q_ = nullptr;
   rank_num_big_ = 0;
-  d_rank_big_d0_ = d_rank_big_d1_ = nullptr;
+  d_rank_big_d0_ = d_rank_big_d1_ = d_rank_big_dh_ = nullptr;
+  d_rank_pairs_ = nullptr;
+  d_rank_pair_off_ = nullptr;
+  rank_max_docs_ = 0;
   d_rank_big_f_ = nullptr;
   d_rank_big_i0_ = d_rank_big_i1_ = d_rank_big_i2_ = nullptr;
   d_rank_rng_ = nullptr;

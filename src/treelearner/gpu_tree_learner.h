@@ -376,7 +376,10 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   // listwise queries of more than kRankMaxDocs documents and their global scratch (RankArgs::big_*)
   int32_t* d_rank_big_q_ = nullptr;
   int32_t rank_num_big_ = 0;
-  double *d_rank_big_d0_ = nullptr, *d_rank_big_d1_ = nullptr;
+  double *d_rank_big_d0_ = nullptr, *d_rank_big_d1_ = nullptr, *d_rank_big_dh_ = nullptr;
+  int32_t rank_max_docs_ = 0;             // most documents of a query staged in LDS
+  float2* d_rank_pairs_ = nullptr;        // lambdarank pair scratch (RankArgs::pair_buf), or null
+  int64_t* d_rank_pair_off_ = nullptr;
   float* d_rank_big_f_ = nullptr;
   int32_t *d_rank_big_i0_ = nullptr, *d_rank_big_i1_ = nullptr, *d_rank_big_i2_ = nullptr;
   uint32_t* d_rank_rng_ = nullptr;
