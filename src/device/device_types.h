@@ -225,6 +225,7 @@ struct Round {
   int32_t accepted_max;  // most splits accepted by one round (diagnostics)
   uint32_t child_done;   // children of the round whose best split is folded (plan in the split scan)
   int32_t k_cur;         // expansions per round for this tree (set by the host; 0: KArgs::round_k)
+  int32_t bynode_next;   // per-node sampling on round growth: the next draw (row of KArgs::node_mask)
   int32_t cur[kMaxRoundExp][2];  // partition cursors of each expansion: rows placed left / right
   // voting-parallel: the fixed-point (g, h) sums of each expansion's histogrammed child over
   // this rank's rows (its local sums; the other child's are the parent's minus these)

@@ -217,6 +217,16 @@ struct KArgs {
   int32_t rs_block;
   long long* round_send;
   long long* round_owned;
+  // per-node feature sampling on round growth (one process, numerical features): the scans
+  // evaluate every feature of a node (KArgs::node_mask is not applied) and keep the per-feature
+  // results per node (node_fb [round_nodes][num_features]); the replay folds a node's results
+  // with its sample once it knows the split that created the node (draw 1 + 2 s, smaller child
+  // first) and keeps the reference's splittable flags per leaf id (leaf_rows [num_leaves]
+  // [num_features], persisting across trees; the children scan with their parent's leaf row).
+  // Speculation stays at the current leaves (the draws of deeper nodes are not known yet)
+  int32_t round_bynode;
+  FeatureBest* node_fb;
+  int8_t* leaf_rows;
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

@@ -160,6 +160,7 @@ __global__ void k_tree_begin(KArgs a, unsigned long long* zero, int64_t zero_wor
       rd->rounds = 0;
       rd->accepted_max = 0;
       rd->child_done = 0u;
+      rd->bynode_next = 1;  // (per-node sampling on round growth: draw 0 is the root's)
     }
   }
   for (int k = threadIdx.x; k < a.forced_n; k += blockDim.x) {  // no stale forced results

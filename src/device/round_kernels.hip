@@ -888,7 +888,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const int frow = e_frow;
   const int nblk = a.round_fused ? e_nblk : RoundHistBlocks(a, rd, j);
   // (voting: every feature is scanned -- the vote may elect one this rank could not split)
-  const int8_t parent_flag = a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
+  // (per-node sampling: the parent leaf's row of the reference's flags, KArgs::leaf_rows)
+  const int8_t parent_flag = a.leaf_rows != nullptr ? a.leaf_rows[static_cast<size_t>(e_frow_parent) * NF + f]
+                                                    : a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
   const int8_t parent_ok = a.round_vote ? 1 : parent_flag;
   FeatureBest* fb_out = &a.feat_best[RoundFbIndex(a, y, f)];
   int8_t* flags = a.splittable + static_cast<size_t>(frow) * NF;
@@ -1052,7 +1054,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     }
   }
   if (ktw) kt[3] = wall_clock64();
-  if (write && tid == 0) PublishRecord(fb_out, o);
+  if (write && tid == 0) {
+    PublishRecord(fb_out, o);
+    if (a.node_fb != nullptr) PublishRecord(&a.node_fb[static_cast<size_t>(frow) * NF + f], o);
+  }
   // (distributed: the results are gathered from every rank first, k_round_childbest folds them)
   if (KIND == 1 || a.round_dist) return;  // (the categorical kernel counts the arrivals)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1251,10 +1256,102 @@ __device__ __forceinline__ void RegTakeChildren(RegLeaf* x, int lane, int w, int
   if (lane == nl) RegLoad(x, c + 1, ng, nrf, nch);
 #endif
 }
+// Per-node sampling (KArgs::round_bynode), wave 0, when the replay accepts split s of leaf w
+// (node n, children c = left and c + 1 = right; the left keeps leaf id w, the right is leaf
+// s + 1).  SerialTreeLearner::BeforeFindBestSplit / FindBestSplits / FindBestSplitsFromHistograms
+// in the sequential order: unless the children are not scanned (depth, min_data, the tree's last
+// split), the smaller child (fewer rows; a tie: the right one) takes draw d, the larger d + 1;
+// the parent's flag row moves to the larger child's leaf id (the smaller one keeps the stale row
+// of its id), a feature the parent could not split is 0 for the smaller child and skipped, and a
+// feature a child's sample evaluates takes the child's scan flag and competes for its best split
+// (its per-node result, KArgs::node_fb).  The children's bests go to cbest and the node tables.
+__device__ void ByNodeAccept(const KArgs& a, int s, int w, int n, int c, int* draw, double* ng, int* nrf, int* nfi) {
+  const int lane = threadIdx.x & 63;
+  const int L = a.p.num_leaves, NF = a.p.num_features, md = a.p.sp.min_data_in_leaf;
+  const RNode& P = a.rnode[n];
+  const int nl = P.total_left, nr = P.count - P.total_left;
+  const int depth = a.rnode[c].st.depth;
+  const bool scanned = s + 1 < L - 1 && !(a.p.max_depth > 0 && depth >= a.p.max_depth) && !(nl < 2 * md && nr < 2 * md);
+  if (!scanned) {
+    if (lane < 2) {
+      FeatureBest none = {};
+      none.gain = -INFINITY;
+      none.feature = none.real_feature = -1;
+      a.cbest[c + lane] = none;
+      ng[c + lane] = -INFINITY;
+      nrf[c + lane] = -1;
+      nfi[c + lane] = -1;
+    }
+    WaveLdsSync();
+    return;
+  }
+  const int d0 = *draw;
+  *draw = d0 + 2;
+  const bool small_left = nl < nr;
+  const int small_leaf = small_left ? w : s + 1, large_leaf = small_left ? s + 1 : w;
+  const int small_node = small_left ? c : c + 1, large_node = small_left ? c + 1 : c;
+  int8_t* rw = a.leaf_rows + static_cast<size_t>(w) * NF;
+  int8_t* rn = a.leaf_rows + static_cast<size_t>(s + 1) * NF;
+  int8_t* rs = a.leaf_rows + static_cast<size_t>(small_leaf) * NF;
+  int8_t* rl = a.leaf_rows + static_cast<size_t>(large_leaf) * NF;
+  const int8_t* ms = a.node_mask + static_cast<size_t>(d0) * NF;
+  const int8_t* ml = ms + NF;
+  const int8_t* fs = a.splittable + static_cast<size_t>(small_node) * NF;
+  const int8_t* fl = a.splittable + static_cast<size_t>(large_node) * NF;
+  const FeatureBest* bs = a.node_fb + static_cast<size_t>(small_node) * NF;
+  const FeatureBest* bl = a.node_fb + static_cast<size_t>(large_node) * NF;
+  ArgC cs = ArgNone(), cl = ArgNone();
+  for (int f = lane; f < NF; f += kWave) {
+    const int8_t parent = rw[f], stale = rn[f];
+    int8_t vs = stale, vl = parent;  // (the rows after the move: the larger child holds the parent's)
+    if (a.tree_mask[f]) {
+      if (!parent) {
+        vs = 0;
+      } else {
+        if (ms[f]) {
+          vs = fs[f];
+          const FeatureBest& o = bs[f];
+          if (o.feature >= 0 && (cs.idx < 0 || SplitBetter(o.gain, o.real_feature, cs.g, cs.rf))) {
+            cs.g = o.gain;
+            cs.rf = o.real_feature;
+            cs.idx = f;
+          }
+        }
+        if (ml[f]) {
+          vl = fl[f];
+          const FeatureBest& o = bl[f];
+          if (o.feature >= 0 && (cl.idx < 0 || SplitBetter(o.gain, o.real_feature, cl.g, cl.rf))) {
+            cl.g = o.gain;
+            cl.rf = o.real_feature;
+            cl.idx = f;
+          }
+        }
+      }
+    }
+    rs[f] = vs;
+    rl[f] = vl;
+  }
+  cs = ArgWaveBest(cs);
+  cl = ArgWaveBest(cl);
+  if (lane < 2) {
+    const ArgC& b = lane == 0 ? cs : cl;
+    const int node = lane == 0 ? small_node : large_node;
+    FeatureBest o = {};
+    o.gain = -INFINITY;
+    o.feature = o.real_feature = -1;
+    if (b.idx >= 0 && b.g != -INFINITY) o = (lane == 0 ? bs : bl)[b.idx];
+    a.cbest[node] = o;
+    ng[node] = o.feature >= 0 ? o.gain : -INFINITY;
+    nrf[node] = o.real_feature;
+    nfi[node] = o.feature;
+  }
+  WaveLdsSync();
+}
+
 // The replay (wave 0): returns s, the splits after it, and *done; acc / accn / tnode as the LDS
 // path.  x keeps the replayed leaves for the prediction.
-__device__ int ReplayRegs(int L, int s0, const double* ng, const int* nrf, const int* nch, int* tnode, int* acc,
-                          int* accn, RegLeaf* xp, int* done_out) {
+__device__ int ReplayRegs(const KArgs& a, int L, int s0, double* ng, int* nrf, const int* nch, int* nfi, int* tnode,
+                          int* acc, int* accn, RegLeaf* xp, int* done_out, int* draw) {
   const int lane = threadIdx.x & 63;
   RegLeaf& x = *xp;
   RegLoad(&x, lane <= s0 ? tnode[lane] : -1, ng, nrf, nch);
@@ -1276,6 +1373,7 @@ __device__ int ReplayRegs(int L, int s0, const double* ng, const int* nrf, const
       acc[s - s0] = w;
       accn[s - s0] = ReadLane(x.node, w);
     }
+    if (a.round_bynode) ByNodeAccept(a, s, w, ReadLane(x.node, w), c, draw, ng, nrf, nfi);
     RegTakeChildren(&x, lane, w, nl, c, ng, nrf, nch);
     ++s;
   }
@@ -1297,7 +1395,7 @@ __device__ int PredictRegs(const KArgs& a, int L, int s, int used, int kround, c
     kmax = min(kmax, a.round_emax - used - (need - 1));
     kmax = max(kmax, min(1, a.round_emax - used));
     if (kmax <= 0) done = 1;
-    const int vmax = a.round_vmax;
+    const int vmax = a.round_bynode ? 0 : a.round_vmax;  // (per-node sampling: the current leaves only)
     int vd = 0;
     for (int ss = s; !done && n < kmax && ss < L - 1; ++ss) {
       const int w = RegArgmax(x, lane <= ss);
@@ -1332,7 +1430,7 @@ __device__ int PredictRegs(const KArgs& a, int L, int s, int used, int kround, c
 // The finished tree to the host (KArgs::host_out): every split record in order (a numerical
 // split's category words skipped), then the scalars with a system-scope release, so the host
 // sees them only after the records.
-__device__ void HostTreeOut(const KArgs& a, int nsplit, int rounds, int nodes) {
+__device__ void HostTreeOut(const KArgs& a, int nsplit, int rounds, int nodes, int draws) {
   constexpr int kRecWords = static_cast<int>(sizeof(SplitRecord) / 8);
   constexpr int kCatWord0 =
       static_cast<int>((__builtin_offsetof(SplitRecord, split) + __builtin_offsetof(DeviceSplit, cat_bits) + 7) / 8);
@@ -1350,6 +1448,7 @@ __device__ void HostTreeOut(const KArgs& a, int nsplit, int rounds, int nodes) {
     __hip_atomic_store(&a.host_out[1], nsplit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&a.host_out[2], rounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&a.host_out[3], nodes, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&a.host_out[4], draws, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&a.host_out[0], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -1357,7 +1456,7 @@ __device__ void HostTreeOut(const KArgs& a, int nsplit, int rounds, int nodes) {
 template <bool ROOT, int NT>
 __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   constexpr int kPlanThreads = NT;
-  __shared__ int s_done, s_s1, s_nexp;
+  __shared__ int s_done, s_s1, s_nexp, s_draw;
   __shared__ ArgC s_arg[kPlanThreads / kWave];
   __shared__ int s_pick[kMaxRoundExp];
   __shared__ int s_pc[kMaxRoundExp];
@@ -1406,6 +1505,14 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     }
     c = ArgWaveBest(c);
     if (lane == 0) s_arg[tid >> 6] = c;
+    // per-node sampling: the root leaf's row of the reference's flags takes the root scan's flags
+    // of the features its sample (draw 0) evaluated; the others keep their (stale) values
+    if (a.round_bynode && static_cast<int>(a.root[2]) >= 2 * a.p.sp.min_data_in_leaf) {
+      const int8_t* rf0 = a.splittable + static_cast<size_t>(a.leaves[0].frow) * NF;
+      for (int f = tid; f < NF; f += kPlanThreads) {
+        if (a.tree_mask[f] && a.node_mask[f]) a.leaf_rows[f] = rf0[f];
+      }
+    }
     __syncthreads();
     ArgC b = s_arg[0];
     for (int k = 1; k < kPlanThreads / kWave; ++k) ArgTake(&b, s_arg[k]);
@@ -1510,8 +1617,9 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   RegLeaf x;
   int done_w = 0;
   int s_w = s0;
+  int draw = rd->bynode_next;  // (per-node sampling: the next draw; wave 0 advances it)
   if (tid < kWave && L <= kWave) {
-    s_w = ReplayRegs(L, s0, ng, nrf, nch, tnode, acc, accn, &x, &done_w);
+    s_w = ReplayRegs(a, L, s0, ng, nrf, nch, nfi, tnode, acc, accn, &x, &done_w, &draw);
   } else if (tid < kWave) {
     for (;;) {
       if (s_w >= L - 1) {
@@ -1525,6 +1633,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       }
       const int n = tnode[w], c = nch[n];
       if (c < 0) break;
+      if (a.round_bynode) ByNodeAccept(a, s_w, w, n, c, &draw, ng, nrf, nfi);
       if (lane == 0) {
         const int nl = s_w + 1;
         acc[s_w - s0] = w;
@@ -1540,7 +1649,11 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       ++s_w;
     }
   }
-  if (tid == 0) s_s1 = s_w;
+  if (tid == 0) {
+    s_s1 = s_w;
+    s_draw = draw;
+    if (a.round_bynode) rd->bynode_next = draw;
+  }
   __syncthreads();  // the accepted splits and the leaves' final nodes are in LDS
   const int s1 = s_s1, nacc = s1 - s0;
   stamp(18);
@@ -1611,7 +1724,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         svd[l] = 0;
       }
       WaveLdsSync();
-      const int vmax = a.round_vmax;
+      const int vmax = a.round_bynode ? 0 : a.round_vmax;  // (per-node sampling: the current leaves only)
       for (int ss = s1; !done_w && n < kmax && ss < L - 1; ++ss) {
         const int w = WaveArgmaxLeaf(sg, srf, ss, [](int) { return true; });
         if (!(sg[w] > 0.0)) break;
@@ -1685,7 +1798,14 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       e.hist_left = hl;
       e.slot_parent = P.st.slot;
       e.slot_new = next_slot + j;
-      e.frow_parent = node;
+      // (per-node sampling: the picked leaf's id -- its row of the reference's flags)
+      int fp = node;
+      if (a.round_bynode) {
+        for (int l = 0; l <= s1 && l < L; ++l) {
+          if (tnode[l] == node) fp = l;
+        }
+      }
+      e.frow_parent = fp;
       e.frow_child[0] = next_frow + 2 * j;
       e.frow_child[1] = next_frow + 2 * j + 1;
       // children's statistics from the split (basic monotone constraints: the mid-point bound)
@@ -1751,7 +1871,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     }
     if (a.host_out != nullptr) {
       __syncthreads();  // (this plan's records are written)
-      HostTreeOut(a, s1, rounds0, nn);
+      HostTreeOut(a, s1, rounds0, nn, s_draw);
     }
     return;
   }

@@ -55,6 +55,21 @@ void GPUTreeLearner::AllocRoundState() {
   a.cbest_cat = d_cbest_cat_;
   a.child_cnt = d_child_cnt_;
   round_hist_.clear();
+  // per-node sampling on round growth (KArgs::round_bynode): one process, no interaction
+  // constraints, numerical features (a categorical winner's category set is not kept per node)
+  a.round_bynode = 0;
+  a.node_fb = nullptr;
+  a.leaf_rows = nullptr;
+  bool any_cat = false;
+  for (int f = 0; f < num_features_; ++f) any_cat = any_cat || data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical;
+  if (config_->feature_fraction_bynode < 1.0 && config_->interaction_constraints_vector.empty() && !distributed_ &&
+      !any_cat && !tuning::Off(tuning::Knob::ByNodeRounds)) {
+    const size_t nf = static_cast<size_t>(std::max(1, num_features_));
+    a.node_fb = Alloc<dev::FeatureBest>(static_cast<size_t>(split_rows_) * nf);
+    a.leaf_rows = Alloc<int8_t>(static_cast<size_t>(config_->num_leaves) * nf);
+    HIPCHECK(hipMemset(a.leaf_rows, 1, static_cast<size_t>(config_->num_leaves) * nf));  // (SerialTreeLearner::Init)
+    a.round_bynode = 1;
+  }
 }
 
 // one round: single process, every kernel back to back; distributed, the histograms
@@ -171,7 +186,10 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
   // the split order depends on more than each leaf's own rows: per-node feature samples and
   // extra_trees draws are consumed in the sequential order, CEGB's coupled penalties change
   // other leaves' gains, forced splits follow their own schedule
-  if (a.node_mask != nullptr || a.xt_base != nullptr || a.p.cegb || a.forced_n > 0 || a.p.mono_inter) return false;
+  // (per-node sampling without interaction constraints folds each node's sample at the replay:
+  // KArgs::round_bynode)
+  if (a.node_mask != nullptr && !(a.round_bynode && a.bynode_rng == nullptr)) return false;
+  if (a.xt_base != nullptr || a.p.cegb || a.forced_n > 0 || a.p.mono_inter) return false;
   return true;
 }
 
@@ -321,6 +339,7 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     h_round_->nsplit = flag[1];
     h_round_->rounds = flag[2];
     h_round_->next_frow = flag[3];
+    h_round_->bynode_next = flag[4];
   } else {
     for (;;) {
       HIPCHECK(hipMemcpyAsync(h_round_, d_round_, kRoundHeader, hipMemcpyDeviceToHost, stream_));

@@ -1309,7 +1309,13 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     last_stats_.collective_bytes =
         distributed_ ? root_collective_bytes_ + split_collective_bytes_ * (config_->num_leaves - 1) : 0.0;
   }
-  if (bynode) {
+  if (bynode && rounds) {
+    // round growth: the draws the replay counted (Round::bynode_next), the root's included
+    // when the root was scanned (one process: the root's rows are this rank's)
+    const bool root_scanned = root_rows_ >= 2 * config_->min_data_in_leaf;
+    Log::Debug("device learner: %d splits in rounds, %d by-node draws", num_splits, h_round_->bynode_next);
+    col_sampler_.AdvanceByNode(root_scanned ? h_round_->bynode_next : 0);
+  } else if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
     const bool root_scanned = h_step_->root_count >= 2 * config_->min_data_in_leaf;  // global count
     Log::Debug("device learner: %d splits, %d by-node draws, root count %d", num_splits, h_step_->bynode_next,

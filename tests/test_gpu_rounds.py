@@ -184,3 +184,29 @@ def test_timed_growth_mode_choice_keeps_the_trees(monkeypatch, tmp_path, capfd):
     assert auto == base
     per_tree = [r["rounds"][0] for r in rows]
     assert per_tree[3] == 0 and per_tree[4] == 0 and per_tree[1] > 0
+
+
+@pytest.mark.parametrize("params", [
+    {"objective": "binary", "feature_fraction_bynode": 0.6},
+    {"objective": "binary", "feature_fraction_bynode": 0.5, "feature_fraction": 0.8, "num_leaves": 63},
+    {"objective": "binary", "feature_fraction_bynode": 0.4, "min_data_in_leaf": 1500},
+    {"objective": "binary", "feature_fraction_bynode": 0.6, "max_depth": 5, "num_leaves": 63},
+    {"objective": "regression", "feature_fraction_bynode": 0.7, "bagging_fraction": 0.7, "bagging_freq": 1},
+    {"objective": "binary", "feature_fraction_bynode": 0.6, "num_leaves": 127},
+], ids=["bynode", "bytree_bynode_63", "min_data", "max_depth", "regression_bagging", "leaves_127"])
+def test_bynode_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu_available):
+    """Per-node feature sampling on round growth (KArgs::round_bynode): the scans evaluate every
+    feature of a node, the replay folds each node's results with its draw once it knows the
+    split that created it, and keeps the reference's splittable flags per leaf id (persisting
+    across trees).  The models -- several trees, so the sampler's state and the flag rows carry
+    over -- equal one split per step's, and round growth was used."""
+    X, y = _data()
+    X = X[:, [0, 1, 2, 3, 4, 5, 6, 7, 8, 10, 11]]  # (numerical features: the round path's scope)
+    if params["objective"] == "regression":
+        y = X[:, 0] + X[:, 1] * X[:, 2] + 0.1 * np.nan_to_num(X[:, 5])
+    p = dict(params, feature_fraction_seed=7)
+    rounds, rows = _model(monkeypatch, tmp_path, 8, X, y, p, rounds=15, tag="bynode")
+    assert sum(sum(r["rounds"]) for r in rows) > 0  # (the trees grew in rounds)
+    monkeypatch.setenv("LGBM_AMD_BYNODE_ROUNDS", "0")
+    steps, _ = _model(monkeypatch, tmp_path, 8, X, y, p, rounds=15, tag="bynode_steps")
+    assert rounds == steps
