@@ -19,7 +19,10 @@
 //                   children become leaves 'leaf' and s + 1 with the expansion's statistics);
 //                   the first argmax leaf that is not expanded ends the replay.  Then the next
 //                   round's expansions are planned: the current unexpanded leaves of highest
-//                   gain (the one that ended the replay first).
+//                   gain (the one that ended the replay first).  The plan runs in the last
+//                   workgroup of k_round_find on one process; in distributed rounds the
+//                   per-feature results are gathered first, and the last workgroup of
+//                   k_round_childbest (the fold of the gathered results) runs it.
 //
 // The accepted sequence is the sequential one: a leaf's best split and its children's results
 // depend only on its own rows, and the replay uses the host loop's argmax order (gain, real
@@ -2035,14 +2038,34 @@ void LaunchRoundFind(const KArgs& a, hipStream_t s) {
 
 }  // namespace
 
-// distributed rounds: each child's best split from the gathered per-feature results
+// distributed rounds: each child's best split from the gathered per-feature results; the last
+// child to finish plans the next round (as k_round_find's last workgroup does on one process),
+// so the gather is followed by one launch instead of a fold and a plan kernel
 __global__ __launch_bounds__(kFindThreads) void k_round_childbest(KArgs a) {
   __shared__ RoundFindShared<0, kFindThreads> sh;
-  const Round* rd = a.rd;
+  __shared__ int s_last;
+  extern __shared__ unsigned char plan_lds[];
+  Round* rd = a.rd;
   if (rd->done) return;
-  const int y = blockIdx.x;
-  if (y >= 2 * rd->nexp) return;
+  const int y = blockIdx.x, nexp = rd->nexp;
+  if (y >= 2 * nexp) return;
   ChildBest<0, kFindThreads>(a, y, rd->e[y >> 1].frow_child[y & 1], sh);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ArrivalRelease();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int last = 0;
+    if (atomicAdd(&rd->child_done, 1u) == 2u * static_cast<unsigned>(nexp) - 1u) {
+      last = 1;
+      rd->child_done = 0u;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  RoundPlanBody<false, kFindThreads>(a, plan_lds);
 }
 
 void PrepareRoundKernels(int max_lds) {
@@ -2084,8 +2107,9 @@ void RoundFind(const KArgs& a, hipStream_t s) { LaunchRoundFind(a, s); }
 void RoundFindElected(const KArgs& a, hipStream_t s) { LaunchRoundFind(a, s); }  // (a: vote_phase 2, num_scan vote_k)
 
 void RoundChildBestAndPlan(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_round_childbest, dim3(2 * a.round_k), dim3(kFindThreads), 0, s, a);
-  hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves, a.round_nodes), s, a);
+  static_assert(kPlanThreads == kFindThreads, "the fold's workgroup runs the plan");
+  hipLaunchKernelGGL(k_round_childbest, dim3(2 * a.round_k), dim3(kFindThreads), RoundPlanLds(a.p.num_leaves, a.round_nodes),
+                     s, a);
 }
 
 void RoundSplitReduce(const KArgs& a, hipStream_t s) {
