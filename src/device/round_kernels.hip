@@ -890,8 +890,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   const int slot = is_hist ? e_slot_new : e_slot_parent;
   const int frow = e_frow;
   const int nblk = a.round_fused ? e_nblk : RoundHistBlocks(a, rd, j);
-  // (voting: every feature is scanned -- the vote may elect one this rank could not split)
   // (per-node sampling: the parent leaf's row of the reference's flags, KArgs::leaf_rows)
+  // (voting: every feature is scanned and its local histogram built -- the vote may elect a
+  // feature the parent's local scan could not split, whose local histogram the reference's
+  // learner would not have built (VotingParallelTreeLearner::FindBestSplits builds the tree's
+  // sample minus those, then copies the elected ones' histograms))
   const int8_t parent_flag = a.leaf_rows != nullptr ? a.leaf_rows[static_cast<size_t>(e_frow_parent) * NF + f]
                                                     : a.splittable[static_cast<size_t>(e_frow_parent) * NF + f];
   const int8_t parent_ok = a.round_vote ? 1 : parent_flag;
@@ -918,9 +921,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     if (tid == 0) flags[f] = 0;
   } else if (tree_used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
     // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
-    // but keeps its histogram (descendants subtract it)
+    // but keeps its histogram (descendants subtract it); voting's local scan evaluates it (its
+    // features are the tree's sample and the parent's flags only)
     bool used = true;
-    if (a.feat_icmask != nullptr && (cl.icmask & a.feat_icmask[f]) == 0) used = false;
+    if (a.feat_icmask != nullptr && !vote_local && (cl.icmask & a.feat_icmask[f]) == 0) used = false;
     LeafCtx L;
     L.sg = cl.sum_g;
     L.sh = cl.sum_h + 2 * kEpsilon;
@@ -1051,7 +1055,14 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
         splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, cl.depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc,
                                                     sh.sc2, kNoRandThr);
       }
-      if (tid == 0) flags[f] = splittable ? 1 : 0;
+      if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (voting: the local scan's flags)
+      // CEGB (GPUTreeLearner::CegbRounds: no refunds in a round tree), before the monotone
+      // penalty as SerialTreeLearner::ComputeBestSplitForFeature
+      if (a.p.cegb) {
+        double delta = a.p.cegb_split * L.n;
+        if (a.cegb_coupled != nullptr && !a.cegb_used[f]) delta += a.cegb_coupled[f];
+        o.gain -= delta;
+      }
       if (!CAT && !SIMPLE && F.monotone != 0) o.gain *= MonotonePenalty(cl.depth, a.p.monotone_penalty);
       if (o.gain == -INFINITY) o.feature = -1;
     }
@@ -2045,17 +2056,19 @@ __global__ __launch_bounds__(kFindThreads) void k_round_childbest(KArgs a) {
   __shared__ RoundFindShared<0, kFindThreads> sh;
   __shared__ int s_last;
   extern __shared__ unsigned char plan_lds[];
+  // every workgroup counts, an idle one too: the plan rewrites Round::nexp / done, so it may run
+  // only once no workgroup of this launch can still read them (a workgroup dispatched late --
+  // the GPU shared with other ranks' kernels -- would otherwise take the next round's nexp)
   Round* rd = a.rd;
-  if (rd->done) return;
-  const int y = blockIdx.x, nexp = rd->nexp;
-  if (y >= 2 * nexp) return;
-  ChildBest<0, kFindThreads>(a, y, rd->e[y >> 1].frow_child[y & 1], sh);
+  const int done = rd->done, nexp = rd->nexp;
+  const int y = blockIdx.x;
+  if (!done && y < 2 * nexp) ChildBest<0, kFindThreads>(a, y, rd->e[y >> 1].frow_child[y & 1], sh);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   ArrivalRelease();
   __syncthreads();
   if (threadIdx.x == 0) {
     int last = 0;
-    if (atomicAdd(&rd->child_done, 1u) == 2u * static_cast<unsigned>(nexp) - 1u) {
+    if (atomicAdd(&rd->child_done, 1u) == gridDim.x - 1u) {
       last = 1;
       rd->child_done = 0u;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -2064,7 +2077,7 @@ __global__ __launch_bounds__(kFindThreads) void k_round_childbest(KArgs a) {
     s_last = last;
   }
   __syncthreads();
-  if (!s_last) return;
+  if (!s_last || done) return;
   RoundPlanBody<false, kFindThreads>(a, plan_lds);
 }
 

@@ -191,7 +191,8 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   if (a.node_mask != nullptr && !rescan && a.p.vote_phase != 1) {
     used = used && a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f];
   }
-  // (voting: every feature is scanned -- the vote may elect one this rank could not split)
+  // (voting: every feature is scanned -- the vote may elect one this rank could not split, and
+  // its local histogram must exist; see k_round_find)
   const int8_t parent_ok = (ROOT || a.p.vote_phase != 0) ? 1
                            : rescan ? a.splittable[static_cast<size_t>(a.leaves[rleaf].frow) * a.p.num_features + f]
                                     : a.parent_flags[f];
@@ -355,7 +356,8 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   if (CAT && !F.is_cat) return;       // (voting global scan: an elected numerical feature)
   // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
   // here but keeps its histogram and its splittable flag
-  if (a.feat_icmask != nullptr && ((ROOT ? kIcAll : cl.icmask) & a.feat_icmask[f]) == 0) used = 0;
+  // (voting's local scan evaluates it: its features are the tree's sample and the parent's flags)
+  if (a.feat_icmask != nullptr && a.p.vote_phase != 1 && ((ROOT ? kIcAll : cl.icmask) & a.feat_icmask[f]) == 0) used = 0;
   int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : sd.frow) * a.p.num_features;
   FeatureBest* fb_out = &a.feat_best[FeatBestIndex(a, side, f)];
   if (tree_used && !parent_ok) {

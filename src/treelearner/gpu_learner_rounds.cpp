@@ -189,7 +189,27 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
   // (per-node sampling without interaction constraints folds each node's sample at the replay:
   // KArgs::round_bynode)
   if (a.node_mask != nullptr && !(a.round_bynode && a.bynode_rng == nullptr)) return false;
-  if (a.xt_base != nullptr || a.p.cegb || a.forced_n > 0 || a.p.mono_inter) return false;
+  if (a.xt_base != nullptr || a.forced_n > 0 || a.p.mono_inter) return false;
+  if (a.p.cegb && !CegbRounds(a)) return false;
+  return true;
+}
+
+// CEGB on round growth (one process, no lazy penalties).  A scan subtracts the split penalty,
+// tradeoff * penalty_split * rows, which depends on the node's own rows only.  A coupled
+// penalty depends on whether the model has used the feature, and a feature's first use refunds
+// the other leaves' remembered candidates (CostEfficientGradientBoosting::UpdateLeafBestSplits):
+// both change within a tree only while some feature of the tree's sample is still unused.  So a
+// tree grows in rounds once every feature of its sample is used -- its splits cannot use a new
+// feature, the coupled terms are 0 and no refund happens; the candidates a refund would read
+// later are of features outside this tree's sample (not scanned here).  Earlier trees grow one
+// split per step, as do all trees with lazy penalties.
+bool GPUTreeLearner::CegbRounds(const dev::KArgs& a) const {
+  if (distributed_ || a.cegb_lazy != nullptr || cegb_ == nullptr) return false;
+  if (a.cegb_coupled == nullptr) return true;
+  const std::vector<char>& used = cegb_->used_in_split();
+  for (int f = 0; f < num_features_; ++f) {
+    if (h_mask_[f] && (f >= static_cast<int>(used.size()) || !used[f])) return false;
+  }
   return true;
 }
 

@@ -1230,6 +1230,11 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   last_tree_rounds_ = rounds;
   int num_splits = 0;
   if (rounds) {
+    if (a.p.cegb && a.cegb_coupled != nullptr) {  // (the model-wide used flags: all of the tree's sample)
+      h_cegb_used_ = cegb_->used_in_split();
+      h_cegb_used_.resize(std::max(1, num_features_), 0);
+      HIPCHECK(hipMemcpyAsync(d_cegb_used_, h_cegb_used_.data(), h_cegb_used_.size(), hipMemcpyHostToDevice, stream_));
+    }
     num_splits = RunRounds(a);
   } else {
     // the tree's fixed kernel sequence (~4 launches per split) is replayed from a hipGraph:

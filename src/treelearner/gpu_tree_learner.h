@@ -143,6 +143,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   // leaf's own rows (per-node sampling, extra_trees draws, CEGB, forced splits) and the
   // distributed learners grow one split per step
   bool RoundGrowth(const dev::KArgs& a) const;
+  bool CegbRounds(const dev::KArgs& a) const;  // CEGB penalties on round growth (this tree)
   int RunRounds(dev::KArgs a);  // the tree's splits; h_rec_ holds their records
   void EnqueueRoot(const dev::KArgs& a);
   void EnqueueRound(const dev::KArgs& a);

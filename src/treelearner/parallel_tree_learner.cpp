@@ -468,8 +468,11 @@ void VotingParallelTreeLearner<Base>::FindBestSplits(const Tree* tree) {
     if (lb[t] > bl) bl = lb[t];
   }
   SyncUpGlobalBestSplit(&bs, &bl, this->config_->max_cat_threshold);
+  // (the reference stores this rank's bests before the sync and copies back a larger leaf's
+  // synced best only when it found a split; the sync is a max over the ranks, so a larger leaf
+  // without one keeps "no split" -- never its parent's stale best, which it would split again)
   this->best_split_per_leaf_[global_smaller_.leaf] = bs;
-  if (bl.feature >= 0 && global_larger_.leaf >= 0) this->best_split_per_leaf_[global_larger_.leaf] = bl;
+  if (global_larger_.leaf >= 0) this->best_split_per_leaf_[global_larger_.leaf] = bl;
 }
 
 template <typename Base>

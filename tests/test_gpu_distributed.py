@@ -365,6 +365,39 @@ def test_voting_bynode_device_resident(world, gpu_available, capfd, monkeypatch)
     assert _trees(host[0][0]) == _trees(dev[0][0])
 
 
+@pytest.mark.parametrize("growth", ["rounds", "steps"])
+@pytest.mark.parametrize("world", [2, 3])
+def test_voting_local_scan_interaction_constraints(world, growth, gpu_available, capfd, monkeypatch):
+    """Voting's local scans evaluate the tree's sample: interaction constraints do not apply
+    there, only to the global scans of the elected features through the node's feature set
+    (VotingParallelTreeLearner::FindBestSplits / FindBestSplitsFromHistograms), so a feature a
+    branch may not use can still be proposed and elected.  The models equal the host voting
+    loop's on every rank, with round growth and with one split per step."""
+    extra = {"top_k": 3, "min_data_in_leaf": 40,
+             "interaction_constraints": [[0, 1, 2], [2, 3, 4, 5], [6, 7, 8, 9]]}
+    if growth == "steps":
+        monkeypatch.setenv("LGBM_AMD_ROUND_K", "1")
+    capfd.readouterr()
+    _, _, _, dev = _run("voting", world, rounds=6, verbose=2, **extra)
+    log = capfd.readouterr().out
+    assert "device-resident growth" in log and "host-assisted growth" not in log
+    for md, _ in dev:
+        assert _trees(md) == _trees(dev[0][0])
+    monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+    _, _, _, host = _run("voting", world, rounds=6, **extra)
+    # the same splits; a leaf's value and weight may differ in the last bit (the host scan sums
+    # the scaled bins as doubles, the device scan the integer bins first)
+    td, th = _tree_fields(dev[0][0]), _tree_fields(host[0][0])
+    assert len(td) == len(th)
+    for i, (a, b) in enumerate(zip(td, th)):
+        for k in a:
+            if k in ("leaf_value", "leaf_weight"):
+                np.testing.assert_allclose(np.array(a[k].split(), float), np.array(b[k].split(), float), rtol=1e-12,
+                                           err_msg="tree %d: %s" % (i, k))
+            else:
+                assert a[k] == b.get(k), "tree %d: %s" % (i, k)
+
+
 def test_bench_py_under_torchrun_two_processes(gpu_available, tmp_path):
     """The multi-GPU benchmark entry point as the driver launches it (torch.distributed.run,
     one process per rank, peer comm), here with 2 processes sharing the box's GPU and 1M rows:
