@@ -144,6 +144,15 @@ struct Step {
 };
 
 // best threshold of one feature for one leaf (output of one split-scan wave)
+// one bin's inclusive prefix over a feature's bins of a node (extra_trees rounds, KArgs::
+// node_pre): (g, h) sums and the rows estimated per bin, the default bin left out as the scan
+// leaves it out
+struct XtPre {
+  double g, h;
+  int32_t c;
+  int32_t pad;
+};
+
 struct FeatureBest {
   double gain;
   double lg, lh, rg, rh, lo, ro;

@@ -227,6 +227,15 @@ struct KArgs {
   int32_t round_bynode;
   FeatureBest* node_fb;
   int8_t* leaf_rows;
+  // extra_trees on round growth (one process, numerical features without a rebuilt most
+  // frequent bin): each random threshold is the next draw of its feature's generator in the
+  // sequential order, so a scan cannot know it.  The scans store every node's per-bin inclusive
+  // prefix sums (node_pre [round_nodes][total_bins]; exact: the bins are integers on the
+  // fixed-point grid) and the replay draws each child's thresholds in the host loop's order
+  // (smaller child first, per feature) and evaluates them from the prefixes; the draws counted
+  // so far are xt_cum row 1.  Flags per leaf id as with per-node sampling (leaf_rows)
+  int32_t round_xt;
+  XtPre* node_pre;
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

@@ -724,7 +724,7 @@ struct PlanTables {
   }
 };
 
-template <bool ROOT, int NT>
+template <bool ROOT, int NT, bool XT = false>
 __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds);
 
 // ----------------------------------------------------------------------------- k_round_find
@@ -1048,6 +1048,11 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
       hv.inv_g = ig;
       hv.inv_h = ih;
       bool splittable;
+      if constexpr (!CAT) {
+        if (a.round_xt) {  // (extra_trees: the prefixes the replay evaluates its drawn thresholds from)
+          XtStorePrefix<NT>(F, hv, L, a.node_pre + static_cast<size_t>(frow) * a.p.total_bins + F.hist_offset, &sh.ssc);
+        }
+      }
       if constexpr (CAT) {
         splittable = FindCategoricalBlock(F, hv, L, p, &o, a.feat_cat + RoundFbIndex(a, y, f) * kMaxCatWords,
                                           &sh.sc, &sh.cat_sc);
@@ -1270,16 +1275,206 @@ __device__ __forceinline__ void RegTakeChildren(RegLeaf* x, int lane, int w, int
   if (lane == nl) RegLoad(x, c + 1, ng, nrf, nch);
 #endif
 }
-// Per-node sampling (KArgs::round_bynode), wave 0, when the replay accepts split s of leaf w
-// (node n, children c = left and c + 1 = right; the left keeps leaf id w, the right is leaf
-// s + 1).  SerialTreeLearner::BeforeFindBestSplit / FindBestSplits / FindBestSplitsFromHistograms
-// in the sequential order: unless the children are not scanned (depth, min_data, the tree's last
-// split), the smaller child (fewer rows; a tie: the right one) takes draw d, the larger d + 1;
-// the parent's flag row moves to the larger child's leaf id (the smaller one keeps the stale row
-// of its id), a feature the parent could not split is 0 for the smaller child and skipped, and a
-// feature a child's sample evaluates takes the child's scan flag and competes for its best split
-// (its per-node result, KArgs::node_fb).  The children's bests go to cbest and the node tables.
-__device__ void ByNodeAccept(const KArgs& a, int s, int w, int n, int c, int* draw, double* ng, int* nrf, int* nfi) {
+// extra_trees on round growth (KArgs::round_xt), one lane: feature f's split of node `node` at
+// the drawn threshold rthr, from the node's prefix table -- FindNumericalBlock's candidates at
+// that threshold (the reverse one at bin rthr + 1 - offset, the forward one at rthr - offset,
+// the forward start for a NaN bin without bin 0), the same sums (exact) and selection, then the
+// scan's feature and depth penalties.  Returns the splittable flag.
+__device__ bool XtEvalNum(const KArgs& a, const Feature& F, int f, int node, const ChildStats& cs, int n, int rthr,
+                          FeatureBest* out) {
+  const SplitParams& p = a.p.sp;
+  const bool simple = !p.use_l1 && !p.use_max_output && !p.use_smoothing && !p.use_mc;
+  const XtPre* pre = a.node_pre + static_cast<size_t>(node) * a.p.total_bins + F.hist_offset;
+  const int nb = F.num_bin - F.offset, offset = F.offset;
+  const bool two = F.num_bin > 2 && F.missing_type != 0;
+  const bool skip_def = two && F.missing_type == 1;
+  const bool na = two && F.missing_type == 2;
+  const int def_t = skip_def ? F.default_bin - offset : -1;
+  LeafCtx L;
+  L.sg = cs.sum_g;
+  L.sh = cs.sum_h + 2 * kEpsilon;
+  L.n = n;
+  L.parent_out = cs.output;
+  L.c.min = cs.cmin;
+  L.c.max = cs.cmax;
+  L.cnt_factor = L.n / L.sh;
+  L.min_gain_shift = LeafGain(L.sg, L.sh, p.lambda_l1, p.lambda_l2, p.max_delta_step, p.path_smooth, L.n, L.parent_out,
+                              p.use_l1, p.use_max_output, p.use_smoothing) +
+                     p.min_gain_to_split;
+  // the entries (one batch of loads): the last (every stored bin), the one before it (the NaN
+  // bin), the default bin and the one before it (the default bin's own sums, taken out of every
+  // prefix past it as the scan leaves it out), the reverse candidate's exclusive prefix and the
+  // forward candidate's inclusive one.  P[t]: stored bins <= t, the rebuilt one left out
+  const int fix_t = F.mfb > 0 ? F.mfb : -1;
+  const int t_r = rthr + 1 - offset, t_f = rthr - offset;
+  const XtPre zero = {0.0, 0.0, 0, 0};
+  const XtPre T = pre[nb - 1];
+  const XtPre T2 = nb >= 2 ? pre[nb - 2] : zero;
+  const XtPre D = def_t >= 0 ? pre[def_t] : zero;
+  const XtPre D2 = def_t >= 1 ? pre[def_t - 1] : zero;
+  const XtPre R = (t_r >= 1 && t_r - 1 < nb) ? pre[t_r - 1] : zero;
+  const XtPre W = (t_f >= 0 && t_f < nb) ? pre[t_f] : zero;
+  const double dg = D.g - D2.g, dh = D.h - D2.h;  // (exact: grid values)
+  const int dc = D.c - D2.c;
+  // prefix without the default bin (exact) of the bins <= t
+  auto wo_def = [&](const XtPre& e, int t, double* g, double* h, int* c) {
+    const bool sub = def_t >= 0 && def_t <= t;
+    *g = sub ? e.g - dg : e.g;
+    *h = sub ? e.h - dh : e.h;
+    *c = sub ? e.c - dc : e.c;
+  };
+  // FixHistogram: the most frequent bin from the leaf totals (every stored bin: T), added last
+  const bool fix_in = fix_t >= 0 && fix_t != def_t;
+  double fix_g = 0.0, fix_h = 0.0;
+  int fix_c = 0;
+  if (fix_t >= 0) {
+    fix_g = L.sg - T.g;
+    fix_h = (L.sh - 2 * kEpsilon) - T.h;
+    fix_c = RoundIntD(fix_h * L.cnt_factor);
+  }
+  double tot_g, tot_h;
+  int tot_c;
+  wo_def(T, nb - 1, &tot_g, &tot_h, &tot_c);
+  if (fix_in) {
+    tot_g += fix_g;
+    tot_h += fix_h;
+    tot_c += fix_c;
+  }
+  // (na: no default bin; the NaN bin is the last one -- rebuilt, or the last entry's step)
+  const bool nan_fix = fix_t == nb - 1;
+  const double ng = !na ? 0.0 : nan_fix ? fix_g : T.g - T2.g;
+  const double nh = !na ? 0.0 : nan_fix ? fix_h : T.h - T2.h;
+  const int nc = !na ? 0 : nan_fix ? fix_c : T.c - T2.c;
+  const int t_start_r = nb - 1 - (na ? 1 : 0), t_end_r = 1 - offset, t_end_f = nb - 2;
+  const double pr_g = na ? tot_g - ng : tot_g, pr_h = na ? tot_h - nh : tot_h;
+  const int pr_c = na ? tot_c - nc : tot_c;
+  const bool minus_one = na && offset == 1;
+  const double lg0 = minus_one ? L.sg - T.g : 0.0;
+  const double lh0 = minus_one ? L.sh - kEpsilon - T.h : kEpsilon;
+  const int lc0 = minus_one ? L.n - tot_c : 0;
+  const double min_h = p.min_sum_hessian_in_leaf;
+  const int min_n = p.min_data_in_leaf;
+  const int8_t mono = static_cast<int8_t>(F.monotone);
+  double rb_gain = -INFINITY, fb_gain = -INFINITY, rb_lg = 0.0, rb_lh = 0.0, fb_lg = 0.0, fb_lh = 0.0;
+  int rb_thr = -1, fb_thr = 0x7fffffff, rb_lc = 0, fb_lc = 0;
+  bool any = false;
+  for (int c = 0; c < 3; ++c) {  // 0: the forward start, 1: reverse, 2: forward
+    bool ok;
+    double xg, xh;
+    int xc, thr;
+    if (c == 0) {
+      ok = minus_one && rthr == offset - 1;
+      xg = lg0;
+      xh = lh0;
+      xc = lc0;
+      thr = offset - 1;
+    } else if (c == 1) {
+      ok = t_r != def_t && t_r >= t_end_r && t_r <= t_start_r;
+      double pg, ph;
+      int pc;
+      wo_def(R, t_r - 1, &pg, &ph, &pc);
+      const bool fx = fix_in && fix_t < t_r;
+      const double eg = fx ? pg + fix_g : pg, eh = fx ? ph + fix_h : ph;
+      const int ec = fx ? pc + fix_c : pc;
+      xg = L.sg - (pr_g - eg);
+      xh = L.sh - (pr_h - eh + kEpsilon);
+      xc = L.n - (pr_c - ec);
+      thr = t_r - 1 + offset;
+    } else {
+      ok = two && t_f >= 0 && t_f != def_t && t_f <= t_end_f;
+      double pg, ph;
+      int pc;
+      wo_def(W, t_f, &pg, &ph, &pc);
+      const bool fx = fix_in && fix_t <= t_f;
+      xg = lg0 + (fx ? pg + fix_g : pg);
+      xh = lh0 + (fx ? ph + fix_h : ph);
+      xc = lc0 + (fx ? pc + fix_c : pc);
+      thr = t_f + offset;
+    }
+    if (!ok || xc < min_n || xh < min_h) continue;
+    const int rc = L.n - xc;
+    const double rh = L.sh - xh;
+    if (rc < min_n || rh < min_h) continue;
+    const double gain = simple ? GainOf<true>(xg, xh, L.sg - xg, rh, p.lambda_l2, p, L.c, mono, xc, rc, L.parent_out)
+                               : GainOf<false>(xg, xh, L.sg - xg, rh, p.lambda_l2, p, L.c, mono, xc, rc, L.parent_out);
+    if (!(gain > L.min_gain_shift)) continue;
+    any = true;
+    if (c == 1) {
+      rb_gain = gain;
+      rb_thr = thr;
+      rb_lg = xg;
+      rb_lh = xh;
+      rb_lc = xc;
+    } else {
+      fb_gain = gain;
+      fb_thr = thr;
+      fb_lg = xg;
+      fb_lh = xh;
+      fb_lc = xc;
+    }
+  }
+  FeatureBest o;
+  o.gain = -INFINITY;
+  o.feature = f;
+  o.real_feature = F.real_index;
+  o.thr = 0;
+  o.default_left = two ? 1 : (F.missing_type == 2 ? 0 : 1);
+  o.lc = o.rc = 0;
+  o.mono = F.monotone;
+  o.ncat = 0;
+  o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
+  for (int d = 0; d < (two ? 2 : 1); ++d) {
+    const double bg = d == 0 ? rb_gain : fb_gain;
+    if (any && bg > o.gain + L.min_gain_shift) {
+      const double blg = d == 0 ? rb_lg : fb_lg, blh = d == 0 ? rb_lh : fb_lh;
+      const int blc = d == 0 ? rb_lc : fb_lc;
+      o.thr = d == 0 ? rb_thr : fb_thr;
+      o.lo = simple ? OutputOf<true>(blg, blh, p.lambda_l2, p, L.c, blc, L.parent_out)
+                    : OutputOf<false>(blg, blh, p.lambda_l2, p, L.c, blc, L.parent_out);
+      o.lc = blc;
+      o.lg = blg;
+      o.lh = blh - kEpsilon;
+      o.ro = simple ? OutputOf<true>(L.sg - blg, L.sh - blh, p.lambda_l2, p, L.c, L.n - blc, L.parent_out)
+                    : OutputOf<false>(L.sg - blg, L.sh - blh, p.lambda_l2, p, L.c, L.n - blc, L.parent_out);
+      o.rc = L.n - blc;
+      o.rg = L.sg - blg;
+      o.rh = L.sh - blh - kEpsilon;
+      o.gain = bg - L.min_gain_shift;
+      o.default_left = d == 1 ? 0 : (!two && F.missing_type == 2 ? 0 : 1);
+    }
+  }
+  o.gain *= F.penalty;
+  if (!simple && F.monotone != 0) o.gain *= MonotonePenalty(cs.depth, a.p.monotone_penalty);
+  if (o.gain == -INFINITY) o.feature = -1;
+  *out = o;
+  return any;
+}
+
+// (extra_trees: draw k of a feature's generator, k >= 1, as the step scans draw)
+__device__ __forceinline__ int XtThreshold(const KArgs& a, const Feature& F, int f, int k) {
+  const uint32_t x = LcgSkip(a.xt_base[f], k);
+  return static_cast<int>(x & 0x7fffffffu) % (F.num_bin - 2);
+}
+
+// Deferred fold (per-node sampling, KArgs::round_bynode; extra_trees, KArgs::round_xt), wave 0,
+// when the replay accepts split s of leaf w (node n, children c = left and c + 1 = right; the
+// left keeps leaf id w, the right is leaf s + 1).  SerialTreeLearner::BeforeFindBestSplit /
+// FindBestSplits / FindBestSplitsFromHistograms in the sequential order: unless the children
+// are not scanned (depth, min_data, the tree's last split), the smaller child (fewer rows; a
+// tie: the right one) is evaluated first -- per-node sampling: it takes draw d, the larger
+// d + 1; extra_trees: per feature, its threshold draw comes first.  The parent's flag row moves
+// to the larger child's leaf id (the smaller one keeps the stale row of its id), a feature the
+// parent could not split is 0 for the smaller child and skipped, and a feature a child
+// evaluates takes the child's flag and competes for its best split (per-node sampling: the
+// scan's result, KArgs::node_fb; extra_trees: the drawn threshold's, XtEvalNum).  The
+// children's bests go to cbest and the node tables.  xcnt: extra_trees draw counts of the
+// features lane, lane + 64, ... (kXtLaneFeatures per lane).
+// (XT: compiled in only where the extra_trees replay runs -- k_round_plan; the replay's
+// registers would otherwise set the occupancy of every scan workgroup of k_round_find)
+constexpr int kXtLaneFeatures = 4;
+template <bool XT>
+__device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* draw, double* ng, int* nrf, int* nfi,
+                            int* xcnt) {
   const int lane = threadIdx.x & 63;
   const int L = a.p.num_leaves, NF = a.p.num_features, md = a.p.sp.min_data_in_leaf;
   const RNode& P = a.rnode[n];
@@ -1299,8 +1494,12 @@ __device__ void ByNodeAccept(const KArgs& a, int s, int w, int n, int c, int* dr
     WaveLdsSync();
     return;
   }
-  const int d0 = *draw;
-  *draw = d0 + 2;
+  const bool bn = a.round_bynode != 0, xt = XT && a.round_xt != 0;
+  int d0 = 0;
+  if (bn) {
+    d0 = *draw;
+    *draw = d0 + 2;
+  }
   const bool small_left = nl < nr;
   const int small_leaf = small_left ? w : s + 1, large_leaf = small_left ? s + 1 : w;
   const int small_node = small_left ? c : c + 1, large_node = small_left ? c + 1 : c;
@@ -1308,36 +1507,72 @@ __device__ void ByNodeAccept(const KArgs& a, int s, int w, int n, int c, int* dr
   int8_t* rn = a.leaf_rows + static_cast<size_t>(s + 1) * NF;
   int8_t* rs = a.leaf_rows + static_cast<size_t>(small_leaf) * NF;
   int8_t* rl = a.leaf_rows + static_cast<size_t>(large_leaf) * NF;
-  const int8_t* ms = a.node_mask + static_cast<size_t>(d0) * NF;
-  const int8_t* ml = ms + NF;
+  const int8_t* ms = bn ? a.node_mask + static_cast<size_t>(d0) * NF : nullptr;
+  const int8_t* ml = bn ? ms + NF : nullptr;
   const int8_t* fs = a.splittable + static_cast<size_t>(small_node) * NF;
   const int8_t* fl = a.splittable + static_cast<size_t>(large_node) * NF;
-  const FeatureBest* bs = a.node_fb + static_cast<size_t>(small_node) * NF;
-  const FeatureBest* bl = a.node_fb + static_cast<size_t>(large_node) * NF;
+  const FeatureBest* bs = bn ? a.node_fb + static_cast<size_t>(small_node) * NF : nullptr;
+  const FeatureBest* bl = bn ? a.node_fb + static_cast<size_t>(large_node) * NF : nullptr;
+  ChildStats css, csl;
+  int ns = 0, nlg = 0;
+  if (xt) {
+    css = a.rnode[small_node].st;
+    csl = a.rnode[large_node].st;
+    ns = small_left ? nl : nr;
+    nlg = small_left ? nr : nl;
+  }
   ArgC cs = ArgNone(), cl = ArgNone();
-  for (int f = lane; f < NF; f += kWave) {
+  FeatureBest rec_s, rec_l;  // (extra_trees: this lane's best records of the two children)
+  int k = 0;
+  for (int f = lane; f < NF; f += kWave, ++k) {
     const int8_t parent = rw[f], stale = rn[f];
     int8_t vs = stale, vl = parent;  // (the rows after the move: the larger child holds the parent's)
     if (a.tree_mask[f]) {
       if (!parent) {
         vs = 0;
       } else {
-        if (ms[f]) {
-          vs = fs[f];
-          const FeatureBest& o = bs[f];
-          if (o.feature >= 0 && (cs.idx < 0 || SplitBetter(o.gain, o.real_feature, cs.g, cs.rf))) {
-            cs.g = o.gain;
-            cs.rf = o.real_feature;
-            cs.idx = f;
+        const bool es = !bn || ms[f], el = !bn || ml[f];
+        FeatureBest os, ol;
+        int8_t gs = 0, gl = 0;
+        if constexpr (XT) {
+          if (xt) {
+            const Feature F = a.feat[f];
+            int cnt = k < kXtLaneFeatures ? xcnt[k] : 0;
+            const bool drawn = F.num_bin - 2 > 0;
+            int ts = 0, tl = 0;
+            if (es && drawn) ts = XtThreshold(a, F, f, ++cnt);
+            if (el && drawn) tl = XtThreshold(a, F, f, ++cnt);
+            if (k < kXtLaneFeatures) xcnt[k] = cnt;
+            if (es) gs = XtEvalNum(a, F, f, small_node, css, ns, ts, &os) ? 1 : 0;
+            if (el) gl = XtEvalNum(a, F, f, large_node, csl, nlg, tl, &ol) ? 1 : 0;
           }
         }
-        if (ml[f]) {
-          vl = fl[f];
-          const FeatureBest& o = bl[f];
-          if (o.feature >= 0 && (cl.idx < 0 || SplitBetter(o.gain, o.real_feature, cl.g, cl.rf))) {
-            cl.g = o.gain;
-            cl.rf = o.real_feature;
+        if (!xt) {
+          if (es) {
+            os = bs[f];
+            gs = fs[f];
+          }
+          if (el) {
+            ol = bl[f];
+            gl = fl[f];
+          }
+        }
+        if (es) {
+          vs = gs;
+          if (os.feature >= 0 && (cs.idx < 0 || SplitBetter(os.gain, os.real_feature, cs.g, cs.rf))) {
+            cs.g = os.gain;
+            cs.rf = os.real_feature;
+            cs.idx = f;
+            if (xt) rec_s = os;
+          }
+        }
+        if (el) {
+          vl = gl;
+          if (ol.feature >= 0 && (cl.idx < 0 || SplitBetter(ol.gain, ol.real_feature, cl.g, cl.rf))) {
+            cl.g = ol.gain;
+            cl.rf = ol.real_feature;
             cl.idx = f;
+            if (xt) rec_l = ol;
           }
         }
       }
@@ -1345,14 +1580,31 @@ __device__ void ByNodeAccept(const KArgs& a, int s, int w, int n, int c, int* dr
     rs[f] = vs;
     rl[f] = vl;
   }
-  cs = ArgWaveBest(cs);
-  cl = ArgWaveBest(cl);
-  if (lane < 2) {
-    const ArgC& b = lane == 0 ? cs : cl;
+  const ArgC bcs = ArgWaveBest(cs), bcl = ArgWaveBest(cl);
+  FeatureBest none = {};
+  none.gain = -INFINITY;
+  none.feature = none.real_feature = -1;
+  if (xt) {
+    // the lane holding a child's winner hands its record over through LDS; lanes 0 / 1 store
+    // the children's bests (a uniform-address store from a lane picked at run time lost its
+    // value to the other lanes' masked copies)
+    __shared__ FeatureBest s_rec[2];
+    if (bcs.idx >= 0 && (bcs.idx & (kWave - 1)) == lane) s_rec[0] = rec_s;
+    if (bcl.idx >= 0 && (bcl.idx & (kWave - 1)) == lane) s_rec[1] = rec_l;
+    WaveLdsSync();
+    if (lane < 2) {
+      const ArgC& b = lane == 0 ? bcs : bcl;
+      const int node = lane == 0 ? small_node : large_node;
+      const bool ok = b.idx >= 0 && b.g != -INFINITY;
+      a.cbest[node] = ok ? s_rec[lane] : none;
+      ng[node] = ok ? b.g : -INFINITY;
+      nrf[node] = ok ? b.rf : -1;
+      nfi[node] = ok ? b.idx : -1;
+    }
+  } else if (lane < 2) {
+    const ArgC& b = lane == 0 ? bcs : bcl;
     const int node = lane == 0 ? small_node : large_node;
-    FeatureBest o = {};
-    o.gain = -INFINITY;
-    o.feature = o.real_feature = -1;
+    FeatureBest o = none;
     if (b.idx >= 0 && b.g != -INFINITY) o = (lane == 0 ? bs : bl)[b.idx];
     a.cbest[node] = o;
     ng[node] = o.feature >= 0 ? o.gain : -INFINITY;
@@ -1364,8 +1616,9 @@ __device__ void ByNodeAccept(const KArgs& a, int s, int w, int n, int c, int* dr
 
 // The replay (wave 0): returns s, the splits after it, and *done; acc / accn / tnode as the LDS
 // path.  x keeps the replayed leaves for the prediction.
+template <bool XT>
 __device__ int ReplayRegs(const KArgs& a, int L, int s0, double* ng, int* nrf, const int* nch, int* nfi, int* tnode,
-                          int* acc, int* accn, RegLeaf* xp, int* done_out, int* draw) {
+                          int* acc, int* accn, RegLeaf* xp, int* done_out, int* draw, int* xcnt) {
   const int lane = threadIdx.x & 63;
   RegLeaf& x = *xp;
   RegLoad(&x, lane <= s0 ? tnode[lane] : -1, ng, nrf, nch);
@@ -1387,7 +1640,7 @@ __device__ int ReplayRegs(const KArgs& a, int L, int s0, double* ng, int* nrf, c
       acc[s - s0] = w;
       accn[s - s0] = ReadLane(x.node, w);
     }
-    if (a.round_bynode) ByNodeAccept(a, s, w, ReadLane(x.node, w), c, draw, ng, nrf, nfi);
+    if (a.round_bynode || (XT && a.round_xt)) DeferAccept<XT>(a, s, w, ReadLane(x.node, w), c, draw, ng, nrf, nfi, xcnt);
     RegTakeChildren(&x, lane, w, nl, c, ng, nrf, nch);
     ++s;
   }
@@ -1409,7 +1662,7 @@ __device__ int PredictRegs(const KArgs& a, int L, int s, int used, int kround, c
     kmax = min(kmax, a.round_emax - used - (need - 1));
     kmax = max(kmax, min(1, a.round_emax - used));
     if (kmax <= 0) done = 1;
-    const int vmax = a.round_bynode ? 0 : a.round_vmax;  // (per-node sampling: the current leaves only)
+    const int vmax = (a.round_bynode || a.round_xt) ? 0 : a.round_vmax;  // (deferred folds: the current leaves only)
     int vd = 0;
     for (int ss = s; !done && n < kmax && ss < L - 1; ++ss) {
       const int w = RegArgmax(x, lane <= ss);
@@ -1467,7 +1720,7 @@ __device__ void HostTreeOut(const KArgs& a, int nsplit, int rounds, int nodes, i
   }
 }
 
-template <bool ROOT, int NT>
+template <bool ROOT, int NT, bool XT>
 __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   constexpr int kPlanThreads = NT;
   __shared__ int s_done, s_s1, s_nexp, s_draw;
@@ -1521,10 +1774,10 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     if (lane == 0) s_arg[tid >> 6] = c;
     // per-node sampling: the root leaf's row of the reference's flags takes the root scan's flags
     // of the features its sample (draw 0) evaluated; the others keep their (stale) values
-    if (a.round_bynode && static_cast<int>(a.root[2]) >= 2 * a.p.sp.min_data_in_leaf) {
+    if (a.leaf_rows != nullptr && static_cast<int>(a.root[2]) >= 2 * a.p.sp.min_data_in_leaf) {
       const int8_t* rf0 = a.splittable + static_cast<size_t>(a.leaves[0].frow) * NF;
       for (int f = tid; f < NF; f += kPlanThreads) {
-        if (a.tree_mask[f] && a.node_mask[f]) a.leaf_rows[f] = rf0[f];
+        if (a.tree_mask[f] && (a.node_mask == nullptr || a.node_mask[f])) a.leaf_rows[f] = rf0[f];
       }
     }
     __syncthreads();
@@ -1632,8 +1885,18 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   int done_w = 0;
   int s_w = s0;
   int draw = rd->bynode_next;  // (per-node sampling: the next draw; wave 0 advances it)
+  // (extra_trees: the draws counted so far -- the root scan's row 0 for the first plan, then
+  // row 1 -- of the features lane, lane + 64, ...; wave 0 advances and stores them)
+  int xcnt[kXtLaneFeatures] = {0, 0, 0, 0};
+  if (XT && a.round_xt && tid < kWave) {
+#pragma unroll
+    for (int k = 0; k < kXtLaneFeatures; ++k) {
+      const int f = lane + k * kWave;
+      if (f < NF) xcnt[k] = a.xt_cum[(ROOT ? 0 : NF) + f];
+    }
+  }
   if (tid < kWave && L <= kWave) {
-    s_w = ReplayRegs(a, L, s0, ng, nrf, nch, nfi, tnode, acc, accn, &x, &done_w, &draw);
+    s_w = ReplayRegs<XT>(a, L, s0, ng, nrf, nch, nfi, tnode, acc, accn, &x, &done_w, &draw, xcnt);
   } else if (tid < kWave) {
     for (;;) {
       if (s_w >= L - 1) {
@@ -1647,7 +1910,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       }
       const int n = tnode[w], c = nch[n];
       if (c < 0) break;
-      if (a.round_bynode) ByNodeAccept(a, s_w, w, n, c, &draw, ng, nrf, nfi);
+      if (a.round_bynode || (XT && a.round_xt)) DeferAccept<XT>(a, s_w, w, n, c, &draw, ng, nrf, nfi, xcnt);
       if (lane == 0) {
         const int nl = s_w + 1;
         acc[s_w - s0] = w;
@@ -1667,6 +1930,13 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     s_s1 = s_w;
     s_draw = draw;
     if (a.round_bynode) rd->bynode_next = draw;
+  }
+  if (XT && a.round_xt && tid < kWave) {
+#pragma unroll
+    for (int k = 0; k < kXtLaneFeatures; ++k) {
+      const int f = lane + k * kWave;
+      if (f < NF) a.xt_cum[NF + f] = xcnt[k];
+    }
   }
   __syncthreads();  // the accepted splits and the leaves' final nodes are in LDS
   const int s1 = s_s1, nacc = s1 - s0;
@@ -1738,7 +2008,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         svd[l] = 0;
       }
       WaveLdsSync();
-      const int vmax = a.round_bynode ? 0 : a.round_vmax;  // (per-node sampling: the current leaves only)
+      const int vmax = (a.round_bynode || a.round_xt) ? 0 : a.round_vmax;  // (deferred folds: the current leaves only)
       for (int ss = s1; !done_w && n < kmax && ss < L - 1; ++ss) {
         const int w = WaveArgmaxLeaf(sg, srf, ss, [](int) { return true; });
         if (!(sg[w] > 0.0)) break;
@@ -1814,7 +2084,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       e.slot_new = next_slot + j;
       // (per-node sampling: the picked leaf's id -- its row of the reference's flags)
       int fp = node;
-      if (a.round_bynode) {
+      if (a.leaf_rows != nullptr) {
         for (int l = 0; l <= s1 && l < L; ++l) {
           if (tnode[l] == node) fp = l;
         }
@@ -1957,7 +2227,7 @@ template <bool ROOT>
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
   extern __shared__ unsigned char plan_lds[];
   if (a.rd->done) return;
-  RoundPlanBody<ROOT, kPlanThreads>(a, plan_lds);
+  RoundPlanBody<ROOT, kPlanThreads, true>(a, plan_lds);  // (the extra_trees replay runs here only)
 }
 
 size_t RoundPlanLds(int num_leaves, int nodes) {

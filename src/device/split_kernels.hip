@@ -25,20 +25,6 @@ namespace dev {
 // 2: the categorical features (grid over KArgs::cat_list).  The categorical scan has its
 // own register / LDS footprint, so it runs in a kernel of its own (inlined: a called
 // function costs ~700 B/lane of stack and ran ~10x slower).
-// extra_trees: Random::Step31 applied k times (x -> 214013 x + 2531011), by squaring the map
-__device__ __forceinline__ uint32_t LcgSkip(uint32_t x, int k) {
-  uint32_t am = 214013u, cm = 2531011u, ar = 1u, cr = 0u;
-  while (k > 0) {
-    if (k & 1) {
-      ar = am * ar;
-      cr = am * cr + cm;
-    }
-    cm = am * cm + cm;
-    am = am * am;
-    k >>= 1;
-  }
-  return ar * x + cr;
-}
 
 // extra_trees: whether the host learner scans f at node mi (the feature is used by the tree,
 // its parent could split on it, the node samples it and its constraints allow it) and so

@@ -348,23 +348,24 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
   ScanAcc ex, tot;
   BlockScanNum(&v, &ex, &tot, ssc);
   LGBM_FIND_STAMP(1);
-  // FixHistogram
+  // FixHistogram.  The stored bins are integers on the fixed-point grid, so every prefix of them
+  // is exact in any order; the rebuilt bin is not, and it is added to a candidate's prefix last
+  // (fix_in) -- the canonical sums the extra_trees replay of round growth reproduces from stored
+  // prefixes (XtStorePrefix / XtEvalNum)
+  double fix_g = 0.0, fix_h = 0.0;
+  int fix_c = 0;
+  const bool fix_in = fix_t >= 0 && fix_t != def_t;
   if (fix_t >= 0) {
-    const double fix_g = L.sg - tot.ag;
-    const double fix_h = (L.sh - 2 * kEpsilon) - tot.ah;
-    const int fix_c = RoundIntD(fix_h * L.cnt_factor);
+    fix_g = L.sg - tot.ag;
+    fix_h = (L.sh - 2 * kEpsilon) - tot.ah;
+    fix_c = RoundIntD(fix_h * L.cnt_factor);
     hv.fix_t = fix_t;
     hv.fix_g = fix_g;
     hv.fix_h = fix_h;
-    if (fix_t != def_t) {
+    if (fix_in) {
       tot.g += fix_g;
       tot.h += fix_h;
       tot.c += fix_c;
-      if (fix_t < b0) {
-        ex.g += fix_g;
-        ex.h += fix_h;
-        ex.c += fix_c;
-      }
     }
     if (fix_t == nb - 1) {
       tot.ng = fix_g;
@@ -416,21 +417,25 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
     } else if (rev) {
       ok = t != def_t && t >= t_end_r && t <= t_start_r;
       // left = total - right, right = bins t..t_start (the reference adds kEpsilon to it)
-      xg = L.sg - (pr_g - pg);
-      xh = L.sh - (pr_h - ph + kEpsilon);
-      xc = L.n - (pr_c - pc);
+      const bool fx = fix_in && fix_t < t;
+      const double eg = fx ? pg + fix_g : pg, eh = fx ? ph + fix_h : ph;
+      const int ec = fx ? pc + fix_c : pc;
+      xg = L.sg - (pr_g - eg);
+      xh = L.sh - (pr_h - eh + kEpsilon);
+      xc = L.n - (pr_c - ec);
       thr = t - 1 + offset;
     } else {
-      if (t != def_t) {
-        const double h = hv.H(t);
-        pg += hv.G(t);
+      if (t != def_t && t != fix_t) {
+        const double h = hv.RawH(t);
+        pg += hv.RawG(t);
         ph += h;
         pc += RoundIntD(h * L.cnt_factor);
       }
       ok = two && t != def_t && t <= t_end_f;
-      xg = lg0 + pg;
-      xh = lh0 + ph;
-      xc = lc0 + pc;
+      const bool fx = fix_in && fix_t <= t;
+      xg = lg0 + (fx ? pg + fix_g : pg);
+      xh = lh0 + (fx ? ph + fix_h : ph);
+      xc = lc0 + (fx ? pc + fix_c : pc);
       thr = t + offset;
     }
     if (!ok || xc < min_n || xh < min_h) continue;
@@ -480,6 +485,65 @@ __device__ bool FindNumericalBlock(const Feature& F, HistView hv, const LeafCtx&
   (void)depth;
   (void)mono_penalty;
   return any;
+}
+
+// extra_trees on round growth (KArgs::node_pre): the inclusive prefix over a feature's stored
+// bins of (g, h, estimated rows) -- the rebuilt most frequent bin left out, the default bin in
+// (the replay takes it out again).  Every stored bin is an integer on the fixed-point grid, so
+// these are exactly the sums FindNumericalBlock accumulates, whatever the order, and a
+// threshold drawn later is evaluated from a few entries.  Ends with a barrier (ssc is reused)
+template <int NT>
+__device__ void XtStorePrefix(const Feature& F, HistView hv, const LeafCtx& L, XtPre* out, ScanScratch<NT>* ssc) {
+  const int tid = threadIdx.x;
+  const int nb = F.num_bin - F.offset;
+  const int fix_t = F.mfb > 0 ? F.mfb : -1;
+  const int K = (nb + NT - 1) / NT;
+  const int b0 = tid * K, b1 = min(nb, b0 + K);
+  hv.fix_t = -1;
+  ScanAcc v = {0.0, 0.0, 0, 0.0, 0.0, 0.0, 0.0, 0};
+#pragma unroll 1
+  for (int t = b0; t < b1; ++t) {
+    if (t == fix_t) continue;
+    const double h = hv.RawH(t);
+    v.g += hv.RawG(t);
+    v.h += h;
+    v.c += RoundIntD(h * L.cnt_factor);
+  }
+  ScanAcc ex, tot;
+  BlockScanNum(&v, &ex, &tot, ssc);
+  double pg = ex.g, ph = ex.h;
+  int pc = ex.c;
+#pragma unroll 1
+  for (int t = b0; t < b1; ++t) {
+    if (t != fix_t) {
+      const double h = hv.RawH(t);
+      pg += hv.RawG(t);
+      ph += h;
+      pc += RoundIntD(h * L.cnt_factor);
+    }
+    XtPre o;
+    o.g = pg;
+    o.h = ph;
+    o.c = pc;
+    o.pad = 0;
+    out[t] = o;
+  }
+  __syncthreads();
+}
+
+// extra_trees: Random::Step31 applied k times (x -> 214013 x + 2531011), by squaring the map
+__device__ __forceinline__ uint32_t LcgSkip(uint32_t x, int k) {
+  uint32_t am = 214013u, cm = 2531011u, ar = 1u, cr = 0u;
+  while (k > 0) {
+    if (k & 1) {
+      ar = am * ar;
+      cr = am * cr + cm;
+    }
+    cm = am * cm + cm;
+    am = am * am;
+    k >>= 1;
+  }
+  return ar * x + cr;
 }
 
 // MonotoneSplitPenalty(depth, penalization)

@@ -32,6 +32,11 @@ void GPUTreeLearner::AllocRoundState() {
   a.cbest = nullptr;
   a.cbest_cat = nullptr;
   a.child_cnt = nullptr;
+  a.round_bynode = 0;
+  a.node_fb = nullptr;
+  a.leaf_rows = nullptr;
+  a.round_xt = 0;
+  a.node_pre = nullptr;
   if (round_k_ <= 1) return;
   d_round_ = Alloc<dev::Round>(1);
   d_rnode_ = Alloc<dev::RNode>(split_rows_);
@@ -57,18 +62,29 @@ void GPUTreeLearner::AllocRoundState() {
   round_hist_.clear();
   // per-node sampling on round growth (KArgs::round_bynode): one process, no interaction
   // constraints, numerical features (a categorical winner's category set is not kept per node)
-  a.round_bynode = 0;
-  a.node_fb = nullptr;
-  a.leaf_rows = nullptr;
   bool any_cat = false;
   for (int f = 0; f < num_features_; ++f) any_cat = any_cat || data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical;
-  if (config_->feature_fraction_bynode < 1.0 && config_->interaction_constraints_vector.empty() && !distributed_ &&
-      !any_cat && !tuning::Off(tuning::Knob::ByNodeRounds)) {
-    const size_t nf = static_cast<size_t>(std::max(1, num_features_));
-    a.node_fb = Alloc<dev::FeatureBest>(static_cast<size_t>(split_rows_) * nf);
+  const bool simple_rounds = config_->interaction_constraints_vector.empty() && !distributed_ && !any_cat;
+  const bool bynode = config_->feature_fraction_bynode < 1.0 && simple_rounds && !tuning::Off(tuning::Knob::ByNodeRounds);
+  // extra_trees on round growth (KArgs::round_xt): also no CEGB or forced splits, at most
+  // kXtLaneFeatures * 64 features (the replay's draw counters), prefix tables under 8 GiB
+  const double pre_bytes = static_cast<double>(split_rows_) * total_bins_ * sizeof(dev::XtPre);
+  const bool xt = config_->extra_trees && simple_rounds && !CostEffectiveGB::Enabled(*config_) &&
+                  config_->forcedsplits_filename.empty() && num_features_ <= 4 * 64 &&
+                  pre_bytes <= 8.0 * (1ull << 30) && !tuning::Off(tuning::Knob::XtRounds);
+  const size_t nf = static_cast<size_t>(std::max(1, num_features_));
+  if (bynode || xt) {
     a.leaf_rows = Alloc<int8_t>(static_cast<size_t>(config_->num_leaves) * nf);
     HIPCHECK(hipMemset(a.leaf_rows, 1, static_cast<size_t>(config_->num_leaves) * nf));  // (SerialTreeLearner::Init)
+  }
+  if (bynode) {
+    a.node_fb = Alloc<dev::FeatureBest>(static_cast<size_t>(split_rows_) * nf);
     a.round_bynode = 1;
+  }
+  if (xt) {
+    a.node_pre = Alloc<dev::XtPre>(static_cast<size_t>(split_rows_) * total_bins_);
+    a.round_xt = 1;
+    a.plan_in_find = 0;  // (the extra_trees replay is compiled into k_round_plan only)
   }
 }
 
@@ -189,7 +205,7 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
   // (per-node sampling without interaction constraints folds each node's sample at the replay:
   // KArgs::round_bynode)
   if (a.node_mask != nullptr && !(a.round_bynode && a.bynode_rng == nullptr)) return false;
-  if (a.xt_base != nullptr || a.forced_n > 0 || a.p.mono_inter) return false;
+  if ((a.xt_base != nullptr && !a.round_xt) || a.forced_n > 0 || a.p.mono_inter) return false;
   if (a.p.cegb && !CegbRounds(a)) return false;
   return true;
 }

@@ -1335,7 +1335,10 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       col_sampler_.AdvanceByNode(root_scanned ? h_step_->bynode_next : 0);
     }
   }
-  if (xt && h_step_->root_count >= 2 * config_->min_data_in_leaf) {
+  // (round growth: one process, the root's rows are this rank's; the plans keep the replay's
+  // counts in row 1)
+  const int xt_root_count = rounds ? static_cast<int>(root_rows_) : h_step_->root_count;
+  if (xt && xt_root_count >= 2 * config_->min_data_in_leaf) {
     // replay the draws the split scans made: the rows are running counts, steps not run are 0
     const int rows = config_->num_leaves;
     h_xt_cum_.resize(static_cast<size_t>(rows) * num_features_);

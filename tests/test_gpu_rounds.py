@@ -234,3 +234,27 @@ def test_cegb_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu
     steps, _ = _model(monkeypatch, tmp_path, 1, X, y, dict(p), rounds=15, tag="cegb_steps")
     assert rounds == steps
 
+
+@pytest.mark.parametrize("params", [
+    {"objective": "binary", "extra_trees": True},
+    {"objective": "binary", "extra_trees": True, "num_leaves": 63, "max_bin": 255},
+    {"objective": "regression", "extra_trees": True, "bagging_fraction": 0.7, "bagging_freq": 1},
+    {"objective": "binary", "extra_trees": True, "min_data_in_leaf": 1500, "max_depth": 6},
+    {"objective": "binary", "extra_trees": True, "monotone_constraints": [1, 0, 0, -1, 0, 0, 0, 1, 0, 0, 0, 0]},
+    {"objective": "binary", "extra_trees": True, "zero_as_missing": True, "lambda_l1": 0.3},
+    {"objective": "binary", "extra_trees": True, "feature_fraction_bynode": 0.6, "feature_fraction": 0.8},
+], ids=["binary", "leaves_63", "regression_bagging", "min_data_depth", "monotone", "zero_missing_l1", "bynode"])
+def test_extra_trees_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu_available):
+    """extra_trees on round growth (KArgs::round_xt): the scans store every node's per-bin
+    prefixes, the replay draws each child's thresholds in the sequential order and evaluates
+    them exactly; the models -- several trees, so the generators' states carry over -- equal
+    one split per step's (the step scans' draws), and round growth was used."""
+    X, y = _data()
+    p = dict(params, extra_seed=9, feature_fraction_seed=5)
+    if p["objective"] == "regression":
+        y = (X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.2 * np.random.RandomState(4).randn(len(y))).astype(np.float32)
+    rounds, rows = _model(monkeypatch, tmp_path, 8, X, y, dict(p), rounds=12, tag="xt")
+    assert sum(sum(r["rounds"]) for r in rows) > 0  # (the trees grew in rounds)
+    steps, _ = _model(monkeypatch, tmp_path, 1, X, y, dict(p), rounds=12, tag="xt_steps")
+    assert rounds == steps
+
