@@ -1467,8 +1467,8 @@ __device__ __forceinline__ int XtThreshold(const KArgs& a, const Feature& F, int
 // parent could not split is 0 for the smaller child and skipped, and a feature a child
 // evaluates takes the child's flag and competes for its best split (per-node sampling: the
 // scan's result, KArgs::node_fb; extra_trees: the drawn threshold's, XtEvalNum).  The
-// children's bests go to cbest and the node tables.  xcnt: extra_trees draw counts of the
-// features lane, lane + 64, ... (kXtLaneFeatures per lane).
+// children's bests go to cbest and the node tables.  xcnt: extra_trees draw counts per feature
+// (LDS, at most kXtLaneFeatures * 64 features).
 // (XT: compiled in only where the extra_trees replay runs -- k_round_plan; the replay's
 // registers would otherwise set the occupancy of every scan workgroup of k_round_find)
 constexpr int kXtLaneFeatures = 4;
@@ -1537,12 +1537,12 @@ __device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
         if constexpr (XT) {
           if (xt) {
             const Feature F = a.feat[f];
-            int cnt = k < kXtLaneFeatures ? xcnt[k] : 0;
+            int cnt = xcnt[f];
             const bool drawn = F.num_bin - 2 > 0;
             int ts = 0, tl = 0;
             if (es && drawn) ts = XtThreshold(a, F, f, ++cnt);
             if (el && drawn) tl = XtThreshold(a, F, f, ++cnt);
-            if (k < kXtLaneFeatures) xcnt[k] = cnt;
+            xcnt[f] = cnt;
             if (es) gs = XtEvalNum(a, F, f, small_node, css, ns, ts, &os) ? 1 : 0;
             if (el) gl = XtEvalNum(a, F, f, large_node, csl, nlg, tl, &ol) ? 1 : 0;
           }
@@ -1886,14 +1886,11 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   int s_w = s0;
   int draw = rd->bynode_next;  // (per-node sampling: the next draw; wave 0 advances it)
   // (extra_trees: the draws counted so far -- the root scan's row 0 for the first plan, then
-  // row 1 -- of the features lane, lane + 64, ...; wave 0 advances and stores them)
-  int xcnt[kXtLaneFeatures] = {0, 0, 0, 0};
+  // row 1 -- per feature, in LDS; wave 0 advances and stores them)
+  __shared__ int s_xcnt[XT ? kXtLaneFeatures * kWave : 1];
+  int* xcnt = s_xcnt;
   if (XT && a.round_xt && tid < kWave) {
-#pragma unroll
-    for (int k = 0; k < kXtLaneFeatures; ++k) {
-      const int f = lane + k * kWave;
-      if (f < NF) xcnt[k] = a.xt_cum[(ROOT ? 0 : NF) + f];
-    }
+    for (int f = lane; f < NF; f += kWave) xcnt[f] = a.xt_cum[(ROOT ? 0 : NF) + f];
   }
   if (tid < kWave && L <= kWave) {
     s_w = ReplayRegs<XT>(a, L, s0, ng, nrf, nch, nfi, tnode, acc, accn, &x, &done_w, &draw, xcnt);
@@ -1932,11 +1929,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     if (a.round_bynode) rd->bynode_next = draw;
   }
   if (XT && a.round_xt && tid < kWave) {
-#pragma unroll
-    for (int k = 0; k < kXtLaneFeatures; ++k) {
-      const int f = lane + k * kWave;
-      if (f < NF) a.xt_cum[NF + f] = xcnt[k];
-    }
+    for (int f = lane; f < NF; f += kWave) a.xt_cum[NF + f] = xcnt[f];
   }
   __syncthreads();  // the accepted splits and the leaves' final nodes are in LDS
   const int s1 = s_s1, nacc = s1 - s0;
@@ -2223,12 +2216,23 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   stamp(21);
 }
 
-template <bool ROOT>
+// (XT: the extra_trees replay's instantiation, launched only with KArgs::round_xt -- its
+// registers and stack would slow every other plan)
+template <bool ROOT, bool XT>
 __global__ __launch_bounds__(kPlanThreads) void k_round_plan(KArgs a) {
   extern __shared__ unsigned char plan_lds[];
   if (a.rd->done) return;
-  RoundPlanBody<ROOT, kPlanThreads, true>(a, plan_lds);  // (the extra_trees replay runs here only)
+  RoundPlanBody<ROOT, kPlanThreads, XT>(a, plan_lds);
 }
+
+namespace {
+template <bool ROOT>
+void LaunchRoundPlan(const KArgs& a, hipStream_t s) {
+  const size_t lds = RoundPlanLds(a.p.num_leaves, a.round_nodes);
+  if (a.round_xt) hipLaunchKernelGGL((k_round_plan<ROOT, true>), dim3(1), dim3(kPlanThreads), lds, s, a);
+  else hipLaunchKernelGGL((k_round_plan<ROOT, false>), dim3(1), dim3(kPlanThreads), lds, s, a);
+}
+}  // namespace
 
 size_t RoundPlanLds(int num_leaves, int nodes) {
   const size_t L = static_cast<size_t>(num_leaves), N = static_cast<size_t>(nodes);
@@ -2374,14 +2378,14 @@ void PrepareRoundKernels(int max_lds) {
 }
 
 void RoundRootPlan(const KArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL((k_round_plan<true>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves, a.round_nodes), s, a);
+  LaunchRoundPlan<true>(a, s);
 }
 
 void RoundStep(const KArgs& a, hipStream_t s) {
   RoundSplitReduce(a, s);
   RoundFind(a, s);
   if (!a.plan_in_find) {
-    hipLaunchKernelGGL((k_round_plan<false>), dim3(1), dim3(kPlanThreads), RoundPlanLds(a.p.num_leaves, a.round_nodes), s, a);
+    LaunchRoundPlan<false>(a, s);
   }
 }
 
