@@ -1307,13 +1307,16 @@ __device__ bool XtEvalNum(const KArgs& a, const Feature& F, int f, int node, con
   // forward candidate's inclusive one.  P[t]: stored bins <= t, the rebuilt one left out
   const int fix_t = F.mfb > 0 ? F.mfb : -1;
   const int t_r = rthr + 1 - offset, t_f = rthr - offset;
+  // (unconditional loads at clamped indices, the unused ones zeroed after: one round trip)
   const XtPre zero = {0.0, 0.0, 0, 0};
+  auto at = [&](int t) { return pre[min(max(t, 0), nb - 1)]; };
   const XtPre T = pre[nb - 1];
-  const XtPre T2 = nb >= 2 ? pre[nb - 2] : zero;
-  const XtPre D = def_t >= 0 ? pre[def_t] : zero;
-  const XtPre D2 = def_t >= 1 ? pre[def_t - 1] : zero;
-  const XtPre R = (t_r >= 1 && t_r - 1 < nb) ? pre[t_r - 1] : zero;
-  const XtPre W = (t_f >= 0 && t_f < nb) ? pre[t_f] : zero;
+  XtPre T2 = at(nb - 2), D = at(def_t), D2 = at(def_t - 1), R = at(t_r - 1), W = at(t_f);
+  if (nb < 2) T2 = zero;
+  if (def_t < 0) D = zero;
+  if (def_t < 1) D2 = zero;
+  if (!(t_r >= 1 && t_r - 1 < nb)) R = zero;
+  if (!(t_f >= 0 && t_f < nb)) W = zero;
   const double dg = D.g - D2.g, dh = D.h - D2.h;  // (exact: grid values)
   const int dc = D.c - D2.c;
   // prefix without the default bin (exact) of the bins <= t
@@ -1523,62 +1526,89 @@ __device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
   }
   ArgC cs = ArgNone(), cl = ArgNone();
   FeatureBest rec_s, rec_l;  // (extra_trees: this lane's best records of the two children)
-  int k = 0;
-  for (int f = lane; f < NF; f += kWave, ++k) {
-    const int8_t parent = rw[f], stale = rn[f];
-    int8_t vs = stale, vl = parent;  // (the rows after the move: the larger child holds the parent's)
-    if (a.tree_mask[f]) {
-      if (!parent) {
-        vs = 0;
-      } else {
-        const bool es = !bn || ms[f], el = !bn || ml[f];
-        FeatureBest os, ol;
-        int8_t gs = 0, gl = 0;
-        if constexpr (XT) {
-          if (xt) {
-            const Feature F = a.feat[f];
-            int cnt = xcnt[f];
-            const bool drawn = F.num_bin - 2 > 0;
-            int ts = 0, tl = 0;
-            if (es && drawn) ts = XtThreshold(a, F, f, ++cnt);
-            if (el && drawn) tl = XtThreshold(a, F, f, ++cnt);
-            xcnt[f] = cnt;
-            if (es) gs = XtEvalNum(a, F, f, small_node, css, ns, ts, &os) ? 1 : 0;
-            if (el) gl = XtEvalNum(a, F, f, large_node, csl, nlg, tl, &ol) ? 1 : 0;
+  // (the flag rows are read before any is written: the children's rows are the parent's and the
+  // new leaf's)
+  if constexpr (XT) {
+    if (xt) {
+      // extra_trees, one child's evaluation live at a time: pass 0 the smaller child (its flags
+      // kept in LDS), pass 1 the larger one and the rows
+      __shared__ int8_t s_gs[kXtLaneFeatures * kWave];
+      for (int pass = 0; pass < 2; ++pass) {
+        const bool small = pass == 0;
+        for (int f = lane; f < NF; f += kWave) {
+          const int8_t parent = rw[f], stale = rn[f];
+          const bool live = a.tree_mask[f] && parent;
+          const bool es = !bn || ms[f], el = !bn || ml[f];
+          const Feature F = a.feat[f];
+          const bool drawn = F.num_bin - 2 > 0;
+          const int cnt = xcnt[f];  // (the smaller child draws first)
+          int8_t g = -1;
+          if (live && (small ? es : el)) {
+            const int k = cnt + 1 + (!small && es && drawn ? 1 : 0);
+            const int thr = drawn ? XtThreshold(a, F, f, k) : 0;
+            FeatureBest o;
+            g = XtEvalNum(a, F, f, small ? small_node : large_node, small ? css : csl, small ? ns : nlg, thr, &o) ? 1 : 0;
+            ArgC& cc = small ? cs : cl;
+            if (o.feature >= 0 && (cc.idx < 0 || SplitBetter(o.gain, o.real_feature, cc.g, cc.rf))) {
+              cc.g = o.gain;
+              cc.rf = o.real_feature;
+              cc.idx = f;
+              if (small) rec_s = o;
+              else rec_l = o;
+            }
           }
+          if (small) {
+            s_gs[f] = g;
+            continue;
+          }
+          int8_t vs = stale, vl = parent;
+          if (a.tree_mask[f]) {
+            if (!parent) {
+              vs = 0;
+            } else {
+              if (s_gs[f] >= 0) vs = s_gs[f];
+              if (g >= 0) vl = g;
+            }
+          }
+          if (live) xcnt[f] = cnt + ((es && drawn) ? 1 : 0) + ((el && drawn) ? 1 : 0);
+          rs[f] = vs;
+          rl[f] = vl;
         }
-        if (!xt) {
-          if (es) {
-            os = bs[f];
-            gs = fs[f];
+        WaveLdsSync();
+      }
+    }
+  }
+  if (!xt) {
+    for (int f = lane; f < NF; f += kWave) {
+      const int8_t parent = rw[f], stale = rn[f];
+      int8_t vs = stale, vl = parent;  // (the rows after the move: the larger child holds the parent's)
+      if (a.tree_mask[f]) {
+        if (!parent) {
+          vs = 0;
+        } else {
+          if (!bn || ms[f]) {
+            vs = fs[f];
+            const FeatureBest& o = bs[f];
+            if (o.feature >= 0 && (cs.idx < 0 || SplitBetter(o.gain, o.real_feature, cs.g, cs.rf))) {
+              cs.g = o.gain;
+              cs.rf = o.real_feature;
+              cs.idx = f;
+            }
           }
-          if (el) {
-            ol = bl[f];
-            gl = fl[f];
-          }
-        }
-        if (es) {
-          vs = gs;
-          if (os.feature >= 0 && (cs.idx < 0 || SplitBetter(os.gain, os.real_feature, cs.g, cs.rf))) {
-            cs.g = os.gain;
-            cs.rf = os.real_feature;
-            cs.idx = f;
-            if (xt) rec_s = os;
-          }
-        }
-        if (el) {
-          vl = gl;
-          if (ol.feature >= 0 && (cl.idx < 0 || SplitBetter(ol.gain, ol.real_feature, cl.g, cl.rf))) {
-            cl.g = ol.gain;
-            cl.rf = ol.real_feature;
-            cl.idx = f;
-            if (xt) rec_l = ol;
+          if (!bn || ml[f]) {
+            vl = fl[f];
+            const FeatureBest& o = bl[f];
+            if (o.feature >= 0 && (cl.idx < 0 || SplitBetter(o.gain, o.real_feature, cl.g, cl.rf))) {
+              cl.g = o.gain;
+              cl.rf = o.real_feature;
+              cl.idx = f;
+            }
           }
         }
       }
+      rs[f] = vs;
+      rl[f] = vl;
     }
-    rs[f] = vs;
-    rl[f] = vl;
   }
   const ArgC bcs = ArgWaveBest(cs), bcl = ArgWaveBest(cl);
   FeatureBest none = {};
