@@ -51,6 +51,7 @@ constexpr int kPeerStageMbProcesses = 64;  // peer comm stage, one process per G
   X(GraphCopyNodes, "LGBM_AMD_GRAPH_COPY_NODES", "1: the tree's scratch zeroing / mask upload as memset / memcpy nodes")  \
   X(ByNodeRounds, "LGBM_AMD_BYNODE_ROUNDS", "0: per-node feature sampling grows one split per step instead of rounds")  \
   X(XtRounds, "LGBM_AMD_XT_ROUNDS", "0: extra_trees grows one split per step instead of rounds")                \
+  X(CegbRounds, "LGBM_AMD_CEGB_ROUNDS", "0: CEGB coupled penalties refunded on one split per step until every feature is used")  \
   X(HostOut, "LGBM_AMD_HOST_OUT", "0: the host copies a round tree's records instead of its last plan writing them")  \
   /* storage layout (same models) */                                                                           \
   X(NibbleBins, "LGBM_AMD_NIBBLE_BINS", "1: 4-bit rows for groups of <= 16 bins (auto above 32 GiB)")          \

@@ -236,6 +236,12 @@ struct KArgs {
   // so far are xt_cum row 1.  Flags per leaf id as with per-node sampling (leaf_rows)
   int32_t round_xt;
   XtPre* node_pre;
+  // CEGB coupled penalties on round growth (one process, no lazy penalties or monotone
+  // constraints): the scans publish raw candidates (node_fb); the replay refunds a feature's
+  // first use to the other leaves, remembers each child's candidates (cegb_mem, per leaf id)
+  // and subtracts the penalties of the used set it has reached; the plan expands only leaves
+  // no refund can change (and the blocker, which is accepted before any other split)
+  int32_t round_cegb;
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
       if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (voting: the local scan's flags)
       // CEGB (GPUTreeLearner::CegbRounds: no refunds in a round tree), before the monotone
       // penalty as SerialTreeLearner::ComputeBestSplitForFeature
-      if (a.p.cegb) {
+      if (a.p.cegb && !a.round_cegb) {  // (KArgs::round_cegb: the replay subtracts them)
         double delta = a.p.cegb_split * L.n;
         if (a.cegb_coupled != nullptr && !a.cegb_used[f]) delta += a.cegb_coupled[f];
         o.gain -= delta;
@@ -1476,10 +1476,41 @@ __device__ __forceinline__ int XtThreshold(const KArgs& a, const Feature& F, int
 // registers would otherwise set the occupancy of every scan workgroup of k_round_find)
 constexpr int kXtLaneFeatures = 4;
 template <bool XT>
-__device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* draw, double* ng, int* nrf, int* nfi,
-                            int* xcnt) {
+__device__ bool DeferAccept(const KArgs& a, int s, int w, int n, int c, int* draw, double* ng, int* nrf, int* nfi,
+                            int* xcnt, int my_node, const int* tnode) {
   const int lane = threadIdx.x & 63;
   const int L = a.p.num_leaves, NF = a.p.num_features, md = a.p.sp.min_data_in_leaf;
+  // CEGB coupled penalties (KArgs::round_cegb): the split's feature, if the model had not used
+  // it, refunds its coupled penalty to the other leaves' remembered candidates first
+  // (CostEfficientGradientBoosting::UpdateLeafBestSplits, at SplitInner's start).  A refunded
+  // leaf is never an expanded one: the plan expands only leaves no refund can change (below).
+  // Leaf l's node: this lane's my_node (register replay, leaf = lane) or tnode[l].
+  bool refunded = false;
+  if (a.round_cegb && a.cegb_coupled != nullptr) {
+    const int fsplit = nfi[n];
+    if (fsplit >= 0 && !a.cegb_used[fsplit]) {
+      refunded = true;
+      const double refund = a.cegb_coupled[fsplit];
+      for (int l = lane; l <= s; l += kWave) {
+        if (l == w) continue;
+        const int nd = tnode != nullptr ? tnode[l] : my_node;
+        FeatureBest cand = a.cegb_mem[static_cast<size_t>(l) * NF + fsplit];
+        cand.gain += refund;
+        const double cg = ng[nd];
+        const int crf = nrf[nd] < 0 ? 0x7fffffff : nrf[nd];
+        const int nrf_c = cand.feature < 0 ? 0x7fffffff : cand.real_feature;
+        if (cg > -INFINITY && (cand.gain > cg || (cand.gain == cg && nrf_c < crf))) {
+          a.cbest[nd] = cand;
+          ng[nd] = cand.gain;
+          nrf[nd] = cand.real_feature;
+          nfi[nd] = cand.feature;
+        }
+      }
+      if (lane == 0) a.cegb_used[fsplit] = 1;
+      __threadfence_block();  // (the children's folds below and later splits read the flag)
+      WaveLdsSync();
+    }
+  }
   const RNode& P = a.rnode[n];
   const int nl = P.total_left, nr = P.count - P.total_left;
   const int depth = a.rnode[c].st.depth;
@@ -1495,7 +1526,7 @@ __device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
       nfi[c + lane] = -1;
     }
     WaveLdsSync();
-    return;
+    return refunded;
   }
   const bool bn = a.round_bynode != 0, xt = XT && a.round_xt != 0;
   int d0 = 0;
@@ -1514,16 +1545,23 @@ __device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
   const int8_t* ml = bn ? ms + NF : nullptr;
   const int8_t* fs = a.splittable + static_cast<size_t>(small_node) * NF;
   const int8_t* fl = a.splittable + static_cast<size_t>(large_node) * NF;
-  const FeatureBest* bs = bn ? a.node_fb + static_cast<size_t>(small_node) * NF : nullptr;
-  const FeatureBest* bl = bn ? a.node_fb + static_cast<size_t>(large_node) * NF : nullptr;
+  const bool cg = a.round_cegb != 0;
+  const FeatureBest* bs = (bn || cg) ? a.node_fb + static_cast<size_t>(small_node) * NF : nullptr;
+  const FeatureBest* bl = (bn || cg) ? a.node_fb + static_cast<size_t>(large_node) * NF : nullptr;
+  const int ns = small_left ? nl : nr, nlg = small_left ? nr : nl;
   ChildStats css, csl;
-  int ns = 0, nlg = 0;
   if (xt) {
     css = a.rnode[small_node].st;
     csl = a.rnode[large_node].st;
-    ns = small_left ? nl : nr;
-    nlg = small_left ? nr : nl;
   }
+  // (CEGB: the scans published the raw candidates -- remembered per leaf id for later refunds
+  // -- and the penalties of the model's used set now are subtracted here)
+  auto cegb_take = [&](FeatureBest* o, int leaf, int f, int rows) {
+    a.cegb_mem[static_cast<size_t>(leaf) * NF + f] = *o;
+    double delta = a.p.cegb_split * rows;
+    if (a.cegb_coupled != nullptr && !a.cegb_used[f]) delta += a.cegb_coupled[f];
+    o->gain -= delta;
+  };
   ArgC cs = ArgNone(), cl = ArgNone();
   FeatureBest rec_s, rec_l;  // (extra_trees: this lane's best records of the two children)
   // (the flag rows are read before any is written: the children's rows are the parent's and the
@@ -1588,7 +1626,8 @@ __device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
         } else {
           if (!bn || ms[f]) {
             vs = fs[f];
-            const FeatureBest& o = bs[f];
+            FeatureBest o = bs[f];
+            if (cg) cegb_take(&o, small_leaf, f, ns);
             if (o.feature >= 0 && (cs.idx < 0 || SplitBetter(o.gain, o.real_feature, cs.g, cs.rf))) {
               cs.g = o.gain;
               cs.rf = o.real_feature;
@@ -1597,7 +1636,8 @@ __device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
           }
           if (!bn || ml[f]) {
             vl = fl[f];
-            const FeatureBest& o = bl[f];
+            FeatureBest o = bl[f];
+            if (cg) cegb_take(&o, large_leaf, f, nlg);
             if (o.feature >= 0 && (cl.idx < 0 || SplitBetter(o.gain, o.real_feature, cl.g, cl.rf))) {
               cl.g = o.gain;
               cl.rf = o.real_feature;
@@ -1635,13 +1675,17 @@ __device__ void DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
     const ArgC& b = lane == 0 ? bcs : bcl;
     const int node = lane == 0 ? small_node : large_node;
     FeatureBest o = none;
-    if (b.idx >= 0 && b.g != -INFINITY) o = (lane == 0 ? bs : bl)[b.idx];
+    if (b.idx >= 0 && b.g != -INFINITY) {
+      o = (lane == 0 ? bs : bl)[b.idx];
+      if (cg) o.gain = b.g;  // (the penalised gain)
+    }
     a.cbest[node] = o;
     ng[node] = o.feature >= 0 ? o.gain : -INFINITY;
     nrf[node] = o.real_feature;
     nfi[node] = o.feature;
   }
   WaveLdsSync();
+  return refunded;
 }
 
 // The replay (wave 0): returns s, the splits after it, and *done; acc / accn / tnode as the LDS
@@ -1670,8 +1714,12 @@ __device__ int ReplayRegs(const KArgs& a, int L, int s0, double* ng, int* nrf, c
       acc[s - s0] = w;
       accn[s - s0] = ReadLane(x.node, w);
     }
-    if (a.round_bynode || (XT && a.round_xt)) DeferAccept<XT>(a, s, w, ReadLane(x.node, w), c, draw, ng, nrf, nfi, xcnt);
+    bool refunded = false;
+    if (a.round_bynode || a.round_cegb || (XT && a.round_xt)) {
+      refunded = DeferAccept<XT>(a, s, w, ReadLane(x.node, w), c, draw, ng, nrf, nfi, xcnt, x.node, nullptr);
+    }
     RegTakeChildren(&x, lane, w, nl, c, ng, nrf, nch);
+    if (refunded) RegLoad(&x, lane <= nl ? x.node : -1, ng, nrf, nch);  // (refunded leaves' new bests)
     ++s;
   }
   if (lane <= s) tnode[lane] = x.node;
@@ -1692,7 +1740,7 @@ __device__ int PredictRegs(const KArgs& a, int L, int s, int used, int kround, c
     kmax = min(kmax, a.round_emax - used - (need - 1));
     kmax = max(kmax, min(1, a.round_emax - used));
     if (kmax <= 0) done = 1;
-    const int vmax = (a.round_bynode || a.round_xt) ? 0 : a.round_vmax;  // (deferred folds: the current leaves only)
+    const int vmax = (a.round_bynode || a.round_xt || a.round_cegb) ? 0 : a.round_vmax;  // (deferred folds: the current leaves only)
     int vd = 0;
     for (int ss = s; !done && n < kmax && ss < L - 1; ++ss) {
       const int w = RegArgmax(x, lane <= ss);
@@ -1937,7 +1985,10 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
       }
       const int n = tnode[w], c = nch[n];
       if (c < 0) break;
-      if (a.round_bynode || (XT && a.round_xt)) DeferAccept<XT>(a, s_w, w, n, c, &draw, ng, nrf, nfi, xcnt);
+      bool refunded = false;
+      if (a.round_bynode || a.round_cegb || (XT && a.round_xt)) {
+        refunded = DeferAccept<XT>(a, s_w, w, n, c, &draw, ng, nrf, nfi, xcnt, -1, tnode);
+      }
       if (lane == 0) {
         const int nl = s_w + 1;
         acc[s_w - s0] = w;
@@ -1950,6 +2001,13 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         trf[nl] = nrf[c + 1];
       }
       WaveLdsSync();
+      if (refunded) {  // (refunded leaves' new bests)
+        for (int l = lane; l <= s_w + 1; l += kWave) {
+          tg[l] = ng[tnode[l]];
+          trf[l] = nrf[tnode[l]];
+        }
+        WaveLdsSync();
+      }
       ++s_w;
     }
   }
@@ -2031,7 +2089,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         svd[l] = 0;
       }
       WaveLdsSync();
-      const int vmax = (a.round_bynode || a.round_xt) ? 0 : a.round_vmax;  // (deferred folds: the current leaves only)
+      const int vmax = (a.round_bynode || a.round_xt || a.round_cegb) ? 0 : a.round_vmax;  // (deferred folds: the current leaves only)
       for (int ss = s1; !done_w && n < kmax && ss < L - 1; ++ss) {
         const int w = WaveArgmaxLeaf(sg, srf, ss, [](int) { return true; });
         if (!(sg[w] > 0.0)) break;
@@ -2072,6 +2130,40 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     for (int i = tid - kWave; i < 3 * nacc; i += NT - kWave) accepted_record(i);
   }
   __syncthreads();
+  if (a.round_cegb && a.cegb_coupled != nullptr && !s_done && s_nexp > 1) {
+    // CEGB coupled penalties: a pick past the blocker is expanded only if no refund can change
+    // its best split, i.e. no feature of the tree the model has not used yet has a remembered
+    // candidate that would beat it with its coupled penalty back (the blocker is accepted first
+    // in the next replay, before any refund)
+    __shared__ int s_unsafe[kMaxRoundExp];
+    const int ne = s_nexp;
+    if (tid < ne) s_unsafe[tid] = 0;
+    __syncthreads();
+    for (int i = tid; i < (ne - 1) * NF; i += kPlanThreads) {
+      const int j = 1 + i / NF, f = i - (j - 1) * NF;
+      if (!a.tree_mask[f] || a.cegb_used[f]) continue;
+      const int node = s_pick[j];
+      int leaf = -1;
+      for (int l = 0; l <= s1 && l < L; ++l) {
+        if (tnode[l] == node) leaf = l;
+      }
+      if (leaf < 0) continue;
+      const FeatureBest& m = a.cegb_mem[static_cast<size_t>(leaf) * NF + f];
+      const double g = m.gain + a.cegb_coupled[f];
+      const int rf = m.feature < 0 ? 0x7fffffff : m.real_feature;
+      const int crf = nrf[node] < 0 ? 0x7fffffff : nrf[node];
+      if (g > ng[node] || (g == ng[node] && rf < crf)) s_unsafe[j] = 1;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int m = 1;
+      for (int j = 1; j < ne; ++j) {
+        if (!s_unsafe[j]) s_pick[m++] = s_pick[j];
+      }
+      s_nexp = m;
+    }
+    __syncthreads();
+  }
   const int nexp = s_nexp;
   if (ktr != nullptr) {
     ktr[22] = nacc;

@@ -37,6 +37,7 @@ void GPUTreeLearner::AllocRoundState() {
   a.leaf_rows = nullptr;
   a.round_xt = 0;
   a.node_pre = nullptr;
+  a.round_cegb = 0;
   if (round_k_ <= 1) return;
   d_round_ = Alloc<dev::Round>(1);
   d_rnode_ = Alloc<dev::RNode>(split_rows_);
@@ -72,15 +73,21 @@ void GPUTreeLearner::AllocRoundState() {
   const bool xt = config_->extra_trees && simple_rounds && !CostEffectiveGB::Enabled(*config_) &&
                   config_->forcedsplits_filename.empty() && num_features_ <= 4 * 64 &&
                   pre_bytes <= 8.0 * (1ull << 30) && !tuning::Off(tuning::Knob::XtRounds);
+  // CEGB coupled penalties on round growth (KArgs::round_cegb): also no lazy penalties or
+  // monotone constraints (the replay subtracts the penalties from raw candidates)
+  const bool mono = std::any_of(config_->monotone_constraints.begin(), config_->monotone_constraints.end(),
+                                [](int8_t m) { return m != 0; });
+  const bool cegb = CostEffectiveGB::Enabled(*config_) && !config_->cegb_penalty_feature_coupled.empty() &&
+                    config_->cegb_penalty_feature_lazy.empty() && simple_rounds && !mono &&
+                    !tuning::Off(tuning::Knob::CegbRounds);
   const size_t nf = static_cast<size_t>(std::max(1, num_features_));
-  if (bynode || xt) {
+  if (bynode || xt || cegb) {
     a.leaf_rows = Alloc<int8_t>(static_cast<size_t>(config_->num_leaves) * nf);
     HIPCHECK(hipMemset(a.leaf_rows, 1, static_cast<size_t>(config_->num_leaves) * nf));  // (SerialTreeLearner::Init)
   }
-  if (bynode) {
-    a.node_fb = Alloc<dev::FeatureBest>(static_cast<size_t>(split_rows_) * nf);
-    a.round_bynode = 1;
-  }
+  if (bynode || cegb) a.node_fb = Alloc<dev::FeatureBest>(static_cast<size_t>(split_rows_) * nf);
+  if (bynode) a.round_bynode = 1;
+  if (cegb) a.round_cegb = 1;
   if (xt) {
     a.node_pre = Alloc<dev::XtPre>(static_cast<size_t>(split_rows_) * total_bins_);
     a.round_xt = 1;
@@ -221,7 +228,7 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
 // split per step, as do all trees with lazy penalties.
 bool GPUTreeLearner::CegbRounds(const dev::KArgs& a) const {
   if (distributed_ || a.cegb_lazy != nullptr || cegb_ == nullptr) return false;
-  if (a.cegb_coupled == nullptr) return true;
+  if (a.cegb_coupled == nullptr || a.round_cegb) return true;  // (round_cegb: refunds in the replay)
   const std::vector<char>& used = cegb_->used_in_split();
   for (int f = 0; f < num_features_; ++f) {
     if (h_mask_[f] && (f >= static_cast<int>(used.size()) || !used[f])) return false;

@@ -1236,6 +1236,11 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       HIPCHECK(hipMemcpyAsync(d_cegb_used_, h_cegb_used_.data(), h_cegb_used_.size(), hipMemcpyHostToDevice, stream_));
     }
     num_splits = RunRounds(a);
+    if (a.round_cegb && a.cegb_coupled != nullptr && cegb_) {  // (the features the tree used first)
+      HIPCHECK(hipStreamSynchronize(stream_));
+      HIPCHECK(hipMemcpy(h_cegb_used_.data(), d_cegb_used_, h_cegb_used_.size(), hipMemcpyDeviceToHost));
+      cegb_->set_used_in_split(std::vector<char>(h_cegb_used_.begin(), h_cegb_used_.begin() + num_features_));
+    }
   } else {
     // the tree's fixed kernel sequence (~4 launches per split) is replayed from a hipGraph:
     // eager launches are host-bound at ~4 us each, longer than most of these kernels.  With

@@ -218,7 +218,12 @@ def test_bynode_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, g
     {"objective": "binary", "cegb_penalty_split": 1e-5, "cegb_penalty_feature_coupled": [0.3] * 6},
     {"objective": "regression", "cegb_penalty_feature_coupled": [0.2, 0.0] * 3, "feature_fraction": 0.7},
     {"objective": "binary", "cegb_penalty_split": 2e-5, "feature_fraction_bynode": 0.6, "_cat": []},
-], ids=["split", "split_tradeoff_63", "coupled", "coupled_bytree", "split_bynode"])
+    {"objective": "binary", "cegb_penalty_split": 1e-5, "cegb_penalty_feature_coupled": [5.0] * 6, "_first": True},
+    {"objective": "binary", "cegb_tradeoff": 0.5, "cegb_penalty_feature_coupled": [40.0, 2.0, 0.0] * 2,
+     "feature_fraction": 0.7, "num_leaves": 63, "_first": True},
+    {"objective": "binary", "cegb_penalty_feature_coupled": [20.0] * 6, "feature_fraction_bynode": 0.6, "_first": True},
+], ids=["split", "split_tradeoff_63", "coupled", "coupled_bytree", "split_bynode", "coupled_first_trees",
+        "coupled_large_63", "coupled_bynode"])
 def test_cegb_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu_available):
     """CEGB penalties on round growth (GPUTreeLearner::CegbRounds): the scans subtract the split
     penalty of the node's rows; with coupled penalties a tree grows in rounds once every feature
@@ -227,10 +232,13 @@ def test_cegb_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu
     X, y = _data()
     X = X[:, [0, 1, 2, 3, 5, 7]]  # (informative features: every one is used within a few trees)
     p = dict(params, feature_fraction_seed=5)
+    first = p.pop("_first", False)  # (coupled penalties from the first tree: refunds inside round trees)
     if p["objective"] == "regression":
         y = (X[:, 0] + 0.5 * X[:, 1] * X[:, 2] + 0.2 * np.random.RandomState(4).randn(len(y))).astype(np.float32)
     rounds, rows = _model(monkeypatch, tmp_path, 8, X, y, dict(p), rounds=15, tag="cegb")
     assert sum(sum(r["rounds"]) for r in rows) > 0  # (some trees grew in rounds)
+    if first:
+        assert sum(rows[0]["rounds"]) > 0  # (the first tree, with every feature unused, too)
     steps, _ = _model(monkeypatch, tmp_path, 1, X, y, dict(p), rounds=15, tag="cegb_steps")
     assert rounds == steps
 
