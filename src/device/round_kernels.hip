@@ -1624,23 +1624,36 @@ __device__ bool DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
         if (!parent) {
           vs = 0;
         } else {
+          // (the fold reads three fields of a record; CEGB copies it into the leaf's memory)
           if (!bn || ms[f]) {
             vs = fs[f];
-            FeatureBest o = bs[f];
-            if (cg) cegb_take(&o, small_leaf, f, ns);
-            if (o.feature >= 0 && (cs.idx < 0 || SplitBetter(o.gain, o.real_feature, cs.g, cs.rf))) {
-              cs.g = o.gain;
-              cs.rf = o.real_feature;
+            const FeatureBest& r = bs[f];
+            double og = r.gain;
+            const int orf = r.real_feature, ofe = r.feature;
+            if (cg) {
+              FeatureBest o = r;
+              cegb_take(&o, small_leaf, f, ns);
+              og = o.gain;
+            }
+            if (ofe >= 0 && (cs.idx < 0 || SplitBetter(og, orf, cs.g, cs.rf))) {
+              cs.g = og;
+              cs.rf = orf;
               cs.idx = f;
             }
           }
           if (!bn || ml[f]) {
             vl = fl[f];
-            FeatureBest o = bl[f];
-            if (cg) cegb_take(&o, large_leaf, f, nlg);
-            if (o.feature >= 0 && (cl.idx < 0 || SplitBetter(o.gain, o.real_feature, cl.g, cl.rf))) {
-              cl.g = o.gain;
-              cl.rf = o.real_feature;
+            const FeatureBest& r = bl[f];
+            double og = r.gain;
+            const int orf = r.real_feature, ofe = r.feature;
+            if (cg) {
+              FeatureBest o = r;
+              cegb_take(&o, large_leaf, f, nlg);
+              og = o.gain;
+            }
+            if (ofe >= 0 && (cl.idx < 0 || SplitBetter(og, orf, cl.g, cl.rf))) {
+              cl.g = og;
+              cl.rf = orf;
               cl.idx = f;
             }
           }
