@@ -222,8 +222,10 @@ def test_bynode_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, g
     {"objective": "binary", "cegb_tradeoff": 0.5, "cegb_penalty_feature_coupled": [40.0, 2.0, 0.0] * 2,
      "feature_fraction": 0.7, "num_leaves": 63, "_first": True},
     {"objective": "binary", "cegb_penalty_feature_coupled": [20.0] * 6, "feature_fraction_bynode": 0.6, "_first": True},
+    {"objective": "binary", "cegb_penalty_feature_coupled": [10.0] * 6, "num_leaves": 127, "min_data_in_leaf": 40,
+     "_first": True},
 ], ids=["split", "split_tradeoff_63", "coupled", "coupled_bytree", "split_bynode", "coupled_first_trees",
-        "coupled_large_63", "coupled_bynode"])
+        "coupled_large_63", "coupled_bynode", "coupled_127"])
 def test_cegb_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu_available):
     """CEGB penalties on round growth (GPUTreeLearner::CegbRounds): the scans subtract the split
     penalty of the node's rows; with coupled penalties a tree grows in rounds once every feature
@@ -251,7 +253,9 @@ def test_cegb_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu
     {"objective": "binary", "extra_trees": True, "monotone_constraints": [1, 0, 0, -1, 0, 0, 0, 1, 0, 0, 0, 0]},
     {"objective": "binary", "extra_trees": True, "zero_as_missing": True, "lambda_l1": 0.3},
     {"objective": "binary", "extra_trees": True, "feature_fraction_bynode": 0.6, "feature_fraction": 0.8},
-], ids=["binary", "leaves_63", "regression_bagging", "min_data_depth", "monotone", "zero_missing_l1", "bynode"])
+    {"objective": "binary", "extra_trees": True, "num_leaves": 127, "min_data_in_leaf": 40},
+], ids=["binary", "leaves_63", "regression_bagging", "min_data_depth", "monotone", "zero_missing_l1", "bynode",
+        "leaves_127"])
 def test_extra_trees_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu_available):
     """extra_trees on round growth (KArgs::round_xt): the scans store every node's per-bin
     prefixes, the replay draws each child's thresholds in the sequential order and evaluates
