@@ -2510,6 +2510,12 @@ void PrepareRoundKernels(int max_lds) {
   AllowRoundSplitLds<4>(max_lds);
   AllowRoundSplitLds<8>(max_lds);
   AllowRoundSplitLds<2, true>(max_lds);
+  // the plans' node tables (RoundPlanLds) pass 64 KiB from ~400 leaves
+  allow(reinterpret_cast<const void*>(k_round_plan<true, false>));
+  allow(reinterpret_cast<const void*>(k_round_plan<false, false>));
+  allow(reinterpret_cast<const void*>(k_round_plan<true, true>));
+  allow(reinterpret_cast<const void*>(k_round_plan<false, true>));
+  allow(reinterpret_cast<const void*>(k_round_childbest));
 }
 
 void RoundRootPlan(const KArgs& a, hipStream_t s) {
