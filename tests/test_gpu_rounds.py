@@ -61,6 +61,7 @@ CASES = {
     "multiclass": {"objective": "multiclass", "num_class": 3},
     "quantile": {"objective": "quantile", "alpha": 0.3},
     "ff_bytree": {"objective": "binary", "feature_fraction": 0.6},
+    "leaves_511": {"objective": "binary", "num_leaves": 511, "min_data_in_leaf": 10},  # (plan LDS past 64 KiB)
 }
 
 
