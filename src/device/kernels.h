@@ -217,7 +217,7 @@ struct KArgs {
   int32_t rs_block;
   long long* round_send;
   long long* round_owned;
-  // per-node feature sampling on round growth (one process, numerical features): the scans
+  // per-node feature sampling on round growth (one process, no interaction constraints): the scans
   // evaluate every feature of a node (KArgs::node_mask is not applied) and keep the per-feature
   // results per node (node_fb [round_nodes][num_features]); the replay folds a node's results
   // with its sample once it knows the split that created the node (draw 1 + 2 s, smaller child
@@ -242,6 +242,12 @@ struct KArgs {
   // and subtracts the penalties of the used set it has reached; the plan expands only leaves
   // no refund can change (and the blocker, which is accepted before any other split)
   int32_t round_cegb;
+  // per-node sampling with categorical features: each categorical feature's category set per
+  // node ([round_nodes][node_cat_slots][kMaxCatWords]; node_cat_slot: the feature's slot, -1
+  // for a numerical one), copied to the node's best when the replay picks it
+  uint32_t* node_fb_cat;
+  const int32_t* node_cat_slot;
+  int32_t node_cat_slots;
 };
 
 // in-kernel timestamp slots (first workgroup, first thread; constant 100 MHz clock)

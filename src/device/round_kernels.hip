@@ -1077,6 +1077,17 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     PublishRecord(fb_out, o);
     if (a.node_fb != nullptr) PublishRecord(&a.node_fb[static_cast<size_t>(frow) * NF + f], o);
   }
+  if constexpr (CAT) {
+    // (per-node sampling: the category set kept per node, from this scan's slot)
+    if (write && a.node_fb_cat != nullptr && a.node_cat_slot[f] >= 0) {
+      __syncthreads();
+      if (tid == 0 && o.ncat > 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        PublishCatCopy(a.node_fb_cat + (static_cast<size_t>(frow) * a.node_cat_slots + a.node_cat_slot[f]) * kMaxCatWords,
+                       a.feat_cat + RoundFbIndex(a, y, f) * kMaxCatWords);
+      }
+    }
+  }
   // (distributed: the results are gathered from every rank first, k_round_childbest folds them)
   if (KIND == 1 || a.round_dist) return;  // (the categorical kernel counts the arrivals)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1696,6 +1707,17 @@ __device__ bool DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
     ng[node] = o.feature >= 0 ? o.gain : -INFINITY;
     nrf[node] = o.real_feature;
     nfi[node] = o.feature;
+  }
+  if (!xt && a.node_fb_cat != nullptr) {
+    // a categorical winner's category set, from the node's copy (the whole wave)
+    for (int side = 0; side < 2; ++side) {
+      const ArgC& b = side == 0 ? bcs : bcl;
+      if (b.idx < 0 || b.g == -INFINITY || a.node_cat_slot[b.idx] < 0) continue;
+      const int node = side == 0 ? small_node : large_node;
+      const uint32_t* src = a.node_fb_cat + (static_cast<size_t>(node) * a.node_cat_slots + a.node_cat_slot[b.idx]) * kMaxCatWords;
+      uint32_t* dst = a.cbest_cat + static_cast<size_t>(node) * kMaxCatWords;
+      for (int i = lane; i < kMaxCatWords; i += kWave) dst[i] = src[i];
+    }
   }
   WaveLdsSync();
   return refunded;

@@ -38,6 +38,9 @@ void GPUTreeLearner::AllocRoundState() {
   a.round_xt = 0;
   a.node_pre = nullptr;
   a.round_cegb = 0;
+  a.node_fb_cat = nullptr;
+  a.node_cat_slot = nullptr;
+  a.node_cat_slots = 0;
   if (round_k_ <= 1) return;
   d_round_ = Alloc<dev::Round>(1);
   d_rnode_ = Alloc<dev::RNode>(split_rows_);
@@ -62,11 +65,20 @@ void GPUTreeLearner::AllocRoundState() {
   a.child_cnt = d_child_cnt_;
   round_hist_.clear();
   // per-node sampling on round growth (KArgs::round_bynode): one process, no interaction
-  // constraints, numerical features (a categorical winner's category set is not kept per node)
+  // constraints (categorical features: their category sets are kept per node)
   bool any_cat = false;
   for (int f = 0; f < num_features_; ++f) any_cat = any_cat || data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical;
-  const bool simple_rounds = config_->interaction_constraints_vector.empty() && !distributed_ && !any_cat;
-  const bool bynode = config_->feature_fraction_bynode < 1.0 && simple_rounds && !tuning::Off(tuning::Knob::ByNodeRounds);
+  const bool base_rounds = config_->interaction_constraints_vector.empty() && !distributed_;
+  const bool simple_rounds = base_rounds && !any_cat;
+  // (categorical features: each node keeps its categorical features' category sets)
+  std::vector<int32_t> cat_slot(std::max(1, num_features_), -1);
+  int ncs = 0;
+  for (int f = 0; f < num_features_; ++f) {
+    if (data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical) cat_slot[f] = ncs++;
+  }
+  const double cat_bytes = static_cast<double>(split_rows_) * ncs * kMaxCatWords * sizeof(uint32_t);
+  const bool bynode = config_->feature_fraction_bynode < 1.0 && base_rounds && cat_bytes <= 2.0 * (1ull << 30) &&
+                      !tuning::Off(tuning::Knob::ByNodeRounds);
   // extra_trees on round growth (KArgs::round_xt): also no CEGB or forced splits, at most
   // kXtLaneFeatures * 64 features (the replay's draw counters), prefix tables under 8 GiB
   const double pre_bytes = static_cast<double>(split_rows_) * total_bins_ * sizeof(dev::XtPre);
@@ -87,6 +99,13 @@ void GPUTreeLearner::AllocRoundState() {
   }
   if (bynode || cegb) a.node_fb = Alloc<dev::FeatureBest>(static_cast<size_t>(split_rows_) * nf);
   if (bynode) a.round_bynode = 1;
+  if (bynode && ncs > 0) {
+    a.node_fb_cat = Alloc<uint32_t>(static_cast<size_t>(split_rows_) * ncs * kMaxCatWords);
+    int32_t* slots = Alloc<int32_t>(cat_slot.size());
+    HIPCHECK(hipMemcpy(slots, cat_slot.data(), sizeof(int32_t) * cat_slot.size(), hipMemcpyHostToDevice));
+    a.node_cat_slot = slots;
+    a.node_cat_slots = ncs;
+  }
   if (cegb) a.round_cegb = 1;
   if (xt) {
     a.node_pre = Alloc<dev::XtPre>(static_cast<size_t>(split_rows_) * total_bins_);

@@ -214,6 +214,25 @@ def test_bynode_rounds_equal_one_split_per_step(params, monkeypatch, tmp_path, g
 
 
 @pytest.mark.parametrize("params", [
+    {"objective": "binary", "feature_fraction_bynode": 0.6, "_cat": [9]},
+    {"objective": "binary", "feature_fraction_bynode": 0.5, "_cat": [9, 7], "num_leaves": 63, "max_cat_to_onehot": 8},
+], ids=["cat", "two_cats_63"])
+def test_bynode_rounds_categorical_equal_one_split_per_step(params, monkeypatch, tmp_path, gpu_available):
+    """Per-node sampling on round growth with categorical features: each node keeps its
+    categorical features' category sets (KArgs::node_fb_cat), and the replay copies the
+    winner's set to the node's best.  The models equal one split per step's."""
+    X, y = _data()
+    if 7 in params["_cat"]:
+        X = X.copy()
+        X[:, 7] = np.random.RandomState(5).randint(0, 40, size=len(y))
+    p = dict(params, feature_fraction_seed=7)
+    rounds, rows = _model(monkeypatch, tmp_path, 8, X, y, dict(p), rounds=12, tag="bynode_cat")
+    assert sum(sum(r["rounds"]) for r in rows) > 0  # (the trees grew in rounds)
+    steps, _ = _model(monkeypatch, tmp_path, 1, X, y, dict(p), rounds=12, tag="bynode_cat_steps")
+    assert rounds == steps
+
+
+@pytest.mark.parametrize("params", [
     {"objective": "binary", "cegb_penalty_split": 1e-4},
     {"objective": "binary", "cegb_tradeoff": 0.5, "cegb_penalty_split": 4e-5, "num_leaves": 63, "max_bin": 255},
     {"objective": "binary", "cegb_penalty_split": 1e-5, "cegb_penalty_feature_coupled": [0.3] * 6},
