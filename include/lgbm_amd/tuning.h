@@ -22,6 +22,14 @@ constexpr int kScoreWalkWgPerCu = 32;      // score walk workgroups per CU (r02_
 constexpr int kRootWgPerCu = 2;            // root histogram workgroups per CU (r04_final_remeasure.md)
 constexpr int kPeerStageMbThreads = 16;    // peer comm stage, thread ranks (MiB)
 constexpr int kPeerStageMbProcesses = 64;  // peer comm stage, one process per GPU (MiB)
+// lambdarank pair scratch (cnt^2 float pairs per LDS-staged query, each pair evaluated once):
+// at most this share of the free device memory when the tables are uploaded, and at most
+// kRankPairCapMb; above it the kernel evaluates each pair from both ends (same gradients)
+constexpr double kRankPairFreeShare = 0.125;
+constexpr int kRankPairCapMb = 6144;
+// NDCG / MAP on the device rank each document against every other of its query (one workgroup
+// per query): validation sets with a longer query are evaluated on the host
+constexpr int kQueryMetricDeviceMaxDocs = 16384;
 
 // ---- the variables: X(id, name, what it does)
 #define LGBM_AMD_KNOBS(X)                                                                                        \
@@ -70,7 +78,7 @@ constexpr int kPeerStageMbProcesses = 64;  // peer comm stage, one process per G
   X(RoundHist, "LGBM_AMD_ROUND_HIST", "n: rounds enqueued = the most of the last n trees")                     \
   X(RoundMargin, "LGBM_AMD_ROUND_MARGIN", "n: extra rounds enqueued per tree")                                 \
   X(RoundSeg, "LGBM_AMD_ROUND_SEG", "n: rounds per segment graph")                                             \
-  X(RoundRoot, "LGBM_AMD_ROUND_ROOT", "n: rounds in the root graph (0: enqueued count rounded to segments)")    \
+  X(RoundRoot, "LGBM_AMD_ROUND_ROOT", "n: rounds in the root graph (0: the enqueued count)")                   \
   X(RoundGrid, "LGBM_AMD_ROUND_GRID", "n: round split workgroups")                                             \
   X(RoundGr, "LGBM_AMD_ROUND_GR", "n: rows gathered per pass in the round split kernel")                      \
   X(RoundNeedDiv, "LGBM_AMD_ROUND_NEED_DIV", "n: picks per round capped by remaining splits / n")              \
@@ -79,6 +87,7 @@ constexpr int kPeerStageMbProcesses = 64;  // peer comm stage, one process per G
   X(DirectFromSplit, "LGBM_AMD_DIRECT_FROM_SPLIT", "n: split steps whose partials the split scan sums itself")  \
   X(BmWgPerCu, "LGBM_AMD_BM_WG_PER_CU", "n: score walk workgroups per CU")                                     \
   X(RootWgPerCu, "LGBM_AMD_ROOT_WG_PER_CU", "n: root histogram workgroups per CU")                             \
+  X(RankPairMb, "LGBM_AMD_RANK_PAIR_MB", "n: lambdarank pair scratch budget (MiB; 0: no scratch)")            \
   /* distributed */                                                                                            \
   X(PeerStageMb, "LGBM_AMD_PEER_STAGE_MB", "n: peer comm stage size (MiB)")                                    \
   X(Network, "LGBM_AMD_NETWORK", "host network transport (tcp / mpi)")                                         \

@@ -86,7 +86,7 @@ bool GBDT::PredictDenseOnDevice(const void* data, bool is_double, int64_t nrow, 
   std::vector<double> raw_out(static_cast<size_t>(nrow) * ntpi);
   {
     DeviceBuffers b;
-    dev::ForestArgs f;
+    dev::ForestArgs f{};
     f.num_trees = nt;
     f.num_class = ntpi;
     f.num_cols = ncol;

@@ -105,7 +105,7 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpGradients(const char* params, const float* label
       Log::Fatal("op gradients: objective '%s' has no point-wise device kernel", c.objective.c_str());
     }
     Scratch sc;
-    dev::GradArgs g;
+    dev::GradArgs g{};
     g.kind = static_cast<int32_t>(spec.kind);
     g.num_class = spec.kind == DeviceGradKind::MulticlassSoftmax ? obj->NumModelPerIteration() : 1;
     g.num_data = n;
@@ -120,6 +120,7 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpGradients(const char* params, const float* label
     g.score = d_score;
     g.grad = d_grad;
     g.hess = d_hess;
+    g.write_split = 1;
     g.gh = nullptr;
     g.gh_stride = 1;
     g.max_parts = nullptr;
@@ -159,8 +160,7 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpMetric(const char* params, const float* label, c
       return;
     }
     Scratch sc;
-    dev::MetricArgs a;
-    std::memset(&a, 0, sizeof(a));
+    dev::MetricArgs a{};
     a.kind = spec.kind;
     a.convert = spec.convert;
     a.sigmoid = spec.sigmoid;
@@ -193,7 +193,7 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpSampleRows(int64_t n, int32_t seed, int32_t goss
     const int64_t nb = dev::SampleBlocks(n);
     std::vector<uint32_t> st(nb);
     for (int64_t b = 0; b < nb; ++b) st[b] = static_cast<uint32_t>(seed + static_cast<int>(b));
-    dev::SampleArgs s;
+    dev::SampleArgs s{};
     s.num_data = n;
     s.num_blocks = nb;
     s.goss = goss;

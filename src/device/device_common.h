@@ -402,5 +402,26 @@ __device__ __forceinline__ void UnpackPartial(unsigned long long v0, unsigned lo
   }
 }
 
+// the fixed-point scales of a tree from absmax = (max |g| bits, max |h| bits, rows cap or 0,
+// negative-hessian flag): scales[0..1] = 2^k per component, scales[2..3] their inverses (see
+// k_scales in misc_kernels.hip for the headroom rules).  One thread.
+__device__ inline void ScalesFromAbsmax(const uint32_t absmax[4], int rows_cap, int units, double* scales) {
+  if (absmax[2] != 0u) rows_cap = static_cast<int>(absmax[2]);
+  const double lim[2] = {units == 1 ? 1073741824.0 : 2147483648.0,
+                        units == 1 && absmax[3] != 0u ? 1073741824.0 : 2147483648.0};
+  const double rows = units == 1 ? static_cast<double>(rows_cap) : 1.0;
+  for (int k = 0; k < 2; ++k) {
+    const double m = static_cast<double>(__uint_as_float(absmax[k]));
+    double sc = 1.0;
+    if (m > 0.0 && isfinite(m)) {
+      int e = static_cast<int>(floor(log2(lim[k] / (rows * m))));
+      e = max(-120, min(120, e));
+      sc = ldexp(1.0, e);
+    }
+    scales[k] = sc;
+    scales[2 + k] = 1.0 / sc;
+  }
+}
+
 }  // namespace dev
 }  // namespace lgbm_amd

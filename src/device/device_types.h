@@ -47,33 +47,33 @@ struct Feature {
 
 // tree-growth parameters (uniform for the launch)
 struct Params {
-  SplitParams sp;
-  int32_t num_leaves;
-  int32_t max_depth;
-  int32_t num_features;
-  int32_t num_groups;
-  int32_t row_stride;  // bytes (or uint16 elements) per row in the bin matrix
-  int32_t total_bins;  // histogram length in bins
-  double monotone_penalty;
-  int32_t data_parallel;  // leaf sizes/decisions from global (split-estimated) counts
-  int32_t max_feature_bins;  // max stored bins of one feature (split-scan LDS staging)
-  int32_t has_cat;           // number of categorical features (KArgs::cat_list; their own split-scan kernel)
-  int32_t wide_cat;          // some categorical feature has > kFindCatNarrow bins (the wide categorical kernel)
-  int32_t direct_from_split; // splits >= this have no reduce kernel: the split scan sums the partials
-  int32_t trace_repeat;      // diagnostics (LGBM_AMD_KTRACE_REPEAT): run the traced pick twice
+  SplitParams sp{};
+  int32_t num_leaves{};
+  int32_t max_depth{};
+  int32_t num_features{};
+  int32_t num_groups{};
+  int32_t row_stride{};  // bytes (or uint16 elements) per row in the bin matrix
+  int32_t total_bins{};  // histogram length in bins
+  double monotone_penalty{};
+  int32_t data_parallel{};  // leaf sizes/decisions from global (split-estimated) counts
+  int32_t max_feature_bins{};  // max stored bins of one feature (split-scan LDS staging)
+  int32_t has_cat{};           // number of categorical features (KArgs::cat_list; their own split-scan kernel)
+  int32_t wide_cat{};          // some categorical feature has > kFindCatNarrow bins (the wide categorical kernel)
+  int32_t direct_from_split{}; // splits >= this have no reduce kernel: the split scan sums the partials
+  int32_t trace_repeat{};      // diagnostics (LGBM_AMD_KTRACE_REPEAT): run the traced pick twice
   // voting-parallel split scans (reference voting_parallel_tree_learner.cpp): 0 off, 1 the
   // local scan (rank-local sums / counts / parameters, every feature), 2 the global scan of the
   // elected features (KArgs::vote_list, histograms in KArgs::vote_hist)
-  int32_t vote_phase;
-  int32_t vote_k;  // top_k: features each rank proposes and the vote elects, per leaf
-  int32_t world;   // ranks
+  int32_t vote_phase{};
+  int32_t vote_k{};  // top_k: features each rank proposes and the vote elects, per leaf
+  int32_t world{};   // ranks
   // cost-effective gradient boosting (split and coupled feature penalties): a candidate's gain
   // loses cegb_split * rows_in_leaf + KArgs::cegb_coupled[f] while f is unused by the model
-  int32_t cegb;
-  double cegb_split;
+  int32_t cegb{};
+  double cegb_split{};
   // intermediate monotone constraints (KArgs::mt_*): a split re-bounds leaves across the tree,
   // which the next split scan re-scans
-  int32_t mono_inter;
+  int32_t mono_inter{};
 };
 
 // per-leaf state

@@ -194,6 +194,7 @@ template void LaunchReduce<1>(const KArgs&, hipStream_t);
 
 void PrepareSplitKernels(int max_lds);
 void PrepareRoundKernels(int max_lds);
+void PrepareRankKernels(int max_lds);
 
 // dynamic LDS above 64 KiB must be enabled per kernel (outside any graph capture)
 void PrepareKernels() {
@@ -219,6 +220,7 @@ void PrepareKernels() {
   AllowLds(k_hist<2, kSparseGPW, 2>);
   PrepareSplitKernels(MaxDynLds());
   PrepareRoundKernels(MaxDynLds());
+  PrepareRankKernels(MaxDynLds());
 }
 
 void HistRoot(const KArgs& a, hipStream_t s) { LaunchHist<0>(a, s); }

@@ -74,21 +74,8 @@ void PackGH(const float* g, const float* h, GH* gh, int64_t gh_stride, int64_t n
 // rows stay inside int64.  absmax[2] (if set) carries the row cap of all ranks.
 __global__ void k_scales(const uint32_t* absmax, int rows_cap, int units, double* scales) {
   if (threadIdx.x != 0) return;
-  if (absmax[2] != 0u) rows_cap = static_cast<int>(absmax[2]);
-  const double lim[2] = {units == 1 ? 1073741824.0 : 2147483648.0,
-                        units == 1 && absmax[3] != 0u ? 1073741824.0 : 2147483648.0};
-  const double rows = units == 1 ? static_cast<double>(rows_cap) : 1.0;
-  for (int k = 0; k < 2; ++k) {
-    const double m = static_cast<double>(__uint_as_float(absmax[k]));
-    double sc = 1.0;
-    if (m > 0.0 && isfinite(m)) {
-      int e = static_cast<int>(floor(log2(lim[k] / (rows * m))));
-      e = max(-120, min(120, e));
-      sc = ldexp(1.0, e);
-    }
-    scales[k] = sc;
-    scales[2 + k] = 1.0 / sc;
-  }
+  const uint32_t am[4] = {absmax[0], absmax[1], absmax[2], absmax[3]};
+  ScalesFromAbsmax(am, rows_cap, units, scales);
 }
 
 void ComputeScales(const uint32_t* absmax, int rows_cap, int units, double* scales, hipStream_t s) {

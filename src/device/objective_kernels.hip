@@ -37,7 +37,7 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
       double g, h;
       if (!RowGrad(ga, i, n, yv[k], sv[k], wv[k], g, h)) continue;
       const float gf = static_cast<float>(g), hf = static_cast<float>(h);
-      if (ga.write_split) {
+      if (ga.write_split || ga.gh == nullptr) {  // (without gh, grad / hess are the only output)
         ga.grad[i] = gf;
         ga.hess[i] = hf;
       }
@@ -87,7 +87,8 @@ __global__ __launch_bounds__(256) void k_gradients(GradArgs ga) {
 constexpr int kReducePartsThreads = 1024;
 __global__ __launch_bounds__(kReducePartsThreads) void k_reduce_parts(const float* max_parts, const double* root_parts,
                                                                       int nparts, int64_t n, int rows_cap,
-                                                                      uint32_t* absmax, double* root) {
+                                                                      uint32_t* absmax, double* root, int units,
+                                                                      double* scales) {
   __shared__ double sg[kReducePartsThreads], sh[kReducePartsThreads];
   __shared__ float mg[kReducePartsThreads], mh[kReducePartsThreads];
   double a = 0.0, b = 0.0;
@@ -115,10 +116,13 @@ __global__ __launch_bounds__(kReducePartsThreads) void k_reduce_parts(const floa
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    absmax[0] = __float_as_uint(mg[0]);  // non-negative floats order like their bit patterns
-    absmax[1] = __float_as_uint(fabsf(mh[0]));
-    absmax[2] = static_cast<uint32_t>(rows_cap);  // (the row cap, max over ranks after the all-reduce)
-    absmax[3] = signbit(mh[0]) ? 1u : 0u;         // (a negative hessian: signed packed h)
+    const uint32_t am[4] = {__float_as_uint(mg[0]),  // non-negative floats order like their bit patterns
+                            __float_as_uint(fabsf(mh[0])),
+                            static_cast<uint32_t>(rows_cap),  // (the row cap, max over ranks after the all-reduce)
+                            signbit(mh[0]) ? 1u : 0u};        // (a negative hessian: signed packed h)
+    for (int k = 0; k < 4; ++k) absmax[k] = am[k];
+    // one process: the tree's scales at once (no all-reduce between: k_scales' work, one launch less)
+    if (scales != nullptr) ScalesFromAbsmax(am, rows_cap, units, scales);
     if (root != nullptr) {
       root[0] = sg[0];
       root[1] = sh[0];
@@ -130,9 +134,9 @@ __global__ __launch_bounds__(kReducePartsThreads) void k_reduce_parts(const floa
 int GradientBlocks(int64_t n) { return GridFor(n); }
 
 void ReduceParts(const float* max_parts, const double* root_parts, int nparts, int64_t n, int rows_cap,
-                 uint32_t* absmax, double* root, hipStream_t s) {
+                 uint32_t* absmax, double* root, hipStream_t s, int units, double* scales) {
   hipLaunchKernelGGL(k_reduce_parts, dim3(1), dim3(kReducePartsThreads), 0, s, max_parts, root_parts, nparts, n, rows_cap,
-                     absmax, root);
+                     absmax, root, units, scales);
 }
 
 void Gradients(const GradArgs& g, hipStream_t s) {

@@ -298,6 +298,17 @@ __global__ __launch_bounds__(kRankBigThreads) void k_xendcg_big(RankArgs ra) {
   XendcgQuery<kRankBigThreads>(ra, q, ra.big_d0 + b, ra.big_d1 + b, ra.big_f + b, s_red);
 }
 
+// k_lambdarank stages up to kRankMaxDocs documents in dynamic LDS (RankLds(kRankMaxDocs) is 88 KiB):
+// above 64 KiB the kernel must be enabled once per process, outside any graph capture
+void PrepareRankKernels(int max_lds) {
+  if (max_lds > 65536 && hipFuncSetAttribute(reinterpret_cast<const void*>(k_lambdarank),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, max_lds) != hipSuccess) {
+    (void)hipGetLastError();  // a launch above 64 KiB then fails, and RankGradients reports it
+  }
+}
+
+size_t RankLdsBytes(int max_docs) { return RankLds(max_docs); }
+
 void RankGradients(const RankArgs& ra, hipStream_t s) {
   if (ra.num_queries <= 0) return;
   if (ra.kind == kRankKindLambdarank) {

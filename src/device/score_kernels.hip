@@ -426,6 +426,100 @@ __global__ __launch_bounds__(256) void k_tree_from_records(KArgs a, int ns, doub
   }
 }
 
+// k_tree_from_records and k_tree_bitmaps in one launch (one workgroup per internal node; the
+// score walk's two single-purpose launches were ~4.5 us each on the tree's critical path).
+// Node s's children: the first later split of its leaf (left) or of its new leaf s + 1 (right),
+// else those leaves -- the same links as k_tree_from_records' parent search (a split's parent is
+// the last earlier split of its leaf, and no split between s and that first one touches it).
+// Workgroup 0 also writes the leaf values and the category boundaries.
+__global__ __launch_bounds__(256) void k_tree_from_records_bm(KArgs a, int ns, double shrink, TreeBlob o,
+                                                              unsigned long long* bm_work, int32_t* bm_meta) {
+  __shared__ int s_leaf[kMaxNodes];
+  __shared__ int s_cat[kMaxNodes];
+  __shared__ int s_lr[2];
+  const int s = blockIdx.x;
+  for (int k = threadIdx.x; k < ns; k += blockDim.x) {
+    s_leaf[k] = a.rec[k].leaf;
+    s_cat[k] = a.rec[k].split.is_categorical ? 1 : 0;
+  }
+  if (threadIdx.x == 0) s_lr[0] = s_lr[1] = 0x7fffffff;
+  __syncthreads();
+  const int l = s_leaf[s];
+  for (int k = s + 1 + static_cast<int>(threadIdx.x); k < ns; k += blockDim.x) {
+    if (s_leaf[k] == l) atomicMin(&s_lr[0], k);
+    if (s_leaf[k] == s + 1) atomicMin(&s_lr[1], k);
+  }
+  if (s == 0) {
+    for (int k = threadIdx.x; k <= ns; k += blockDim.x) o.cat_boundaries_inner[k] = k * kMaxCatWords;
+    for (int lf = threadIdx.x; lf <= ns; lf += blockDim.x) {
+      int p = ns - 1;
+      while (s_leaf[p] != lf && p != lf - 1) --p;
+      const DeviceSplit& d = a.rec[p].split;
+      double v = s_leaf[p] == lf ? d.left_output : d.right_output;
+      if (isnan(v)) v = 0.0;
+      v *= shrink;
+      o.leaf_value[lf] = (v >= -kZeroThreshold && v <= kZeroThreshold) ? 0.0 : v;
+    }
+  }
+  __syncthreads();
+  const DeviceSplit& d = a.rec[s].split;
+  const int f = d.feature;
+  const Feature F = a.feat[f];
+  const bool cat = s_cat[s] != 0;
+  int ci = 0;
+  if (cat) {
+    for (int k = 0; k < s; ++k) ci += s_cat[k];
+  }
+  NodeInfo nd;
+  nd.gbyte = F.gbyte;
+  nd.gwide = static_cast<int16_t>(F.gwide);
+  nd.col_off = F.col_off;
+  nd.left_is_default = (!cat && d.default_left) ? 1 : 0;
+  nd.missing_type = static_cast<int16_t>(F.missing_type);
+  nd.is_cat = cat ? 1 : 0;
+  nd.sub_lo = F.sub_lo;
+  nd.sub_hi = F.sub_hi;
+  nd.offset = F.offset;
+  nd.mfb = F.mfb;
+  nd.default_bin = F.default_bin;
+  nd.max_bin = F.num_bin - 1;
+  nd.threshold = cat ? static_cast<uint32_t>(ci) : static_cast<uint32_t>(d.threshold);
+  nd.left = s_lr[0] != 0x7fffffff ? s_lr[0] : ~l;
+  nd.right = s_lr[1] != 0x7fffffff ? s_lr[1] : ~(s + 1);
+  if (threadIdx.x == 0) {
+    o.split_feature_inner[s] = f;
+    o.left_child[s] = nd.left;
+    o.right_child[s] = nd.right;
+    o.threshold_in_bin[s] = nd.threshold;
+    o.decision_type[s] = static_cast<int8_t>((cat ? 1 : (d.default_left ? 2 : 0)) | (F.missing_type << 2));
+    bm_meta[s * 3 + 0] = nd.gbyte;
+    bm_meta[s * 3 + 1] = nd.left;
+    bm_meta[s * 3 + 2] = nd.right;
+  }
+  if (cat) {
+    for (int w = threadIdx.x; w < kMaxCatWords; w += blockDim.x) {
+      o.cat_threshold_inner[static_cast<size_t>(ci) * kMaxCatWords + w] = d.cat_bits[w];
+    }
+  }
+  // the node's "goes left" set over the raw group byte (k_tree_bitmaps)
+  const uint32_t gb = nd.gwide >= 2 ? (threadIdx.x >> ((nd.gwide & 1) * 4)) & 15u : threadIdx.x;
+  const uint32_t bin = (gb < static_cast<uint32_t>(nd.sub_lo) || gb >= static_cast<uint32_t>(nd.sub_hi))
+                           ? static_cast<uint32_t>(nd.mfb)
+                           : gb - nd.sub_lo + nd.offset;
+  bool left;
+  if (cat) {
+    const int word = static_cast<int>(bin >> 5);
+    left = word < kMaxCatWords && ((d.cat_bits[word] >> (bin & 31u)) & 1u);
+  } else if ((nd.missing_type == 1 && bin == static_cast<uint32_t>(nd.default_bin)) ||
+             (nd.missing_type == 2 && bin == static_cast<uint32_t>(nd.max_bin))) {
+    left = nd.left_is_default != 0;
+  } else {
+    left = bin <= nd.threshold;
+  }
+  const unsigned long long m = __ballot(left);
+  if ((threadIdx.x & 63) == 0) bm_work[s * 4 + (threadIdx.x >> 6)] = m;
+}
+
 size_t TreeFromRecordsBytes(int max_leaves) {
   const size_t ni = static_cast<size_t>(std::max(1, max_leaves - 1));
   char* base = nullptr;
@@ -433,13 +527,21 @@ size_t TreeFromRecordsBytes(int max_leaves) {
   return static_cast<size_t>(reinterpret_cast<char*>(b.cat_threshold_inner) - base) + 4 * ni * kMaxCatWords;
 }
 
-DevTree TreeFromRecords(const KArgs& a, int nsplit, int max_leaves, double shrinkage, char* blob, hipStream_t s) {
+DevTree TreeFromRecords(const KArgs& a, int nsplit, int max_leaves, double shrinkage, char* blob, hipStream_t s,
+                        unsigned long long* bm_work, int32_t* bm_meta) {
   if (nsplit < 1 || nsplit > kMaxNodes || nsplit > max_leaves - 1) {
     throw std::runtime_error("TreeFromRecords: split count out of range");
   }
   const TreeBlob b = BlobLayout(blob, max_leaves);
-  hipLaunchKernelGGL(k_tree_from_records, dim3(1), dim3(256), 0, s, a, nsplit, shrinkage, b);
   DevTree t{};
+  if (bm_work != nullptr && bm_meta != nullptr && TreeBitmapsApply(a, nsplit + 1)) {
+    hipLaunchKernelGGL(k_tree_from_records_bm, dim3(nsplit), dim3(256), 0, s, a, nsplit, shrinkage, b, bm_work, bm_meta);
+    t.bm_work = bm_work;
+    t.bm_meta = bm_meta;
+    t.bm_ready = 1;
+  } else {
+    hipLaunchKernelGGL(k_tree_from_records, dim3(1), dim3(256), 0, s, a, nsplit, shrinkage, b);
+  }
   t.num_leaves = nsplit + 1;
   t.split_feature_inner = b.split_feature_inner;
   t.threshold_in_bin = b.threshold_in_bin;
@@ -482,7 +584,7 @@ bool AddTreeScoreGradKind(int kind) {
 void AddTreeScoreGrad(const KArgs& a, const DevTree& t, int64_t num_rows, double* score, const GradArgs& ga,
                       hipStream_t s) {
   const int ni = t.num_leaves - 1;
-  hipLaunchKernelGGL(k_tree_bitmaps, dim3(ni), dim3(256), 0, s, a, t);
+  if (!t.bm_ready) hipLaunchKernelGGL(k_tree_bitmaps, dim3(ni), dim3(256), 0, s, a, t);
   const size_t lds = sizeof(uint32_t) * kBmRowsPerBlock * a.row_words;
   const dim3 grid(BmBlocks(num_rows)), block(kBmRowsPerBlock);
   auto go = [&](auto kind) {

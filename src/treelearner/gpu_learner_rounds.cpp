@@ -2,6 +2,7 @@
 // collectives, the growth-mode choice and the host loop over round segments (round_kernels.hip).
 #include <atomic>
 #include <chrono>
+#include <thread>
 
 #include "gpu_learner_internal.h"
 #include "lgbm_amd/tuning.h"
@@ -330,9 +331,10 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   int want = tuning::kRoundFirstTree;
   if (!round_hist_.empty()) want = *std::max_element(round_hist_.begin(), round_hist_.end()) + round_margin_;
   want = std::max(1, std::min(want, L - 1));
-  // the root graph: a fixed number of rounds, or the provisioned count rounded up to segments;
+  // the root graph: a fixed number of rounds, or exactly the provisioned count (one cached graph
+  // per count; rounding up to whole segments ran ~1.5 no-op rounds of three launches per tree);
   // segment graphs make up the rest before the host first looks at the Round record
-  const int root_rounds = round_root_fixed_ > 0 ? std::min(round_root_fixed_, want) : seg * ((want + seg - 1) / seg);
+  const int root_rounds = round_root_fixed_ > 0 ? std::min(round_root_fixed_, want) : want;
   bool graph = use_graph;
   if (graph && (round_seg_exec_ == nullptr || round_graph_rows_ != a.num_rows ||
                 round_graph_identity_ != a.root_identity || round_graph_root_mode_ != root_mode)) {
@@ -380,14 +382,27 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
   if (flag != nullptr) {
     // spin on the flag (it is set while the stream may still run the tree's surplus rounds);
     // every ~20 us look whether the stream ran dry without it: then the tree needs more rounds
-    auto last = std::chrono::steady_clock::now();
+    // (a pause per read; past the first millisecond the thread yields between reads, so a long
+    // tree does not hold a host core the OpenMP host work could use; time_out bounds the wait)
+    const auto t0 = std::chrono::steady_clock::now();
+    auto last = t0;
+    const double limit_s = 60.0 * std::max(1, config_->time_out);
     for (;;) {
       if (flag[0] != 0) break;
+      __builtin_ia32_pause();
       const auto now = std::chrono::steady_clock::now();
-      if (now - last < std::chrono::microseconds(20)) continue;
+      if (now - last < std::chrono::microseconds(20)) {
+        if (now - t0 > std::chrono::milliseconds(1)) std::this_thread::yield();
+        continue;
+      }
       last = now;
       const hipError_t q = hipStreamQuery(stream_);
-      if (q == hipErrorNotReady) continue;
+      if (q == hipErrorNotReady) {
+        if (std::chrono::duration<double>(now - t0).count() > limit_s) {
+          Log::Fatal("device learner: the tree's rounds did not finish within time_out=%d min", config_->time_out);
+        }
+        continue;
+      }
       HIPCHECK(q);
       if (flag[0] != 0) break;
       if (launched > 2 * L + seg) {

@@ -62,6 +62,9 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
   const bool query = spec.kind == dev::kMetricNDCG || spec.kind == dev::kMetricMAP;
   if (vs.ntpi != (multi ? spec.num_class : 1)) return false;
   if (query && (spec.qb == nullptr || spec.nq <= 0 || spec.eval_at.empty())) return false;
+  // a query's device ranking is O(cnt^2) on one workgroup; very long queries are sorted on the
+  // host in O(cnt log cnt) instead (reference rank_metric.hpp)
+  if (query && spec.max_query_docs > tuning::kQueryMetricDeviceMaxDocs) return false;
   HIPCHECK(hipSetDevice(device_id_));
   const size_t n = static_cast<size_t>(vs.num_data);
   auto dev_alloc = [&](size_t bytes) {
@@ -91,8 +94,7 @@ bool GPUTreeLearner::ValidEval(int slot, const DeviceMetricSpec& spec, std::vect
   // the device AUC sorts each row's weight with its class in the sign: a negative weight would
   // flip the class (the reference binary_metric.hpp:240-241 adds it to the row's own class)
   if (spec.kind == dev::kMetricAUC && vs.negative_weights) return false;
-  dev::MetricArgs m;
-  std::memset(&m, 0, sizeof(m));
+  dev::MetricArgs m{};
   if (query) {
     // the metric's query inputs, uploaded on its first evaluation
     auto it = vs.queries.find(spec.key);
@@ -275,7 +277,7 @@ void GPUTreeLearner::EarlyScoreUpdate(int nsplit, double shrinkage) {
     d_tree_bm_ = Alloc<unsigned long long>(4 * static_cast<size_t>(nbm));
     d_tree_bm_meta_ = Alloc<int32_t>(3 * static_cast<size_t>(nbm));
   }
-  dev::DevTree t = dev::TreeFromRecords(args_, nsplit, L, shrinkage, d_early_blob_, stream_);
+  dev::DevTree t = dev::TreeFromRecords(args_, nsplit, L, shrinkage, d_early_blob_, stream_, d_tree_bm_, d_tree_bm_meta_);
   t.bm_work = d_tree_bm_;
   t.bm_meta = d_tree_bm_meta_;
   dev::AddTreeScoreGrad(args_, t, num_data_, d_score_, last_grad_, stream_);
@@ -386,7 +388,7 @@ dev::DevTree GPUTreeLearner::StageTree(const Tree* tree) {
   HIPCHECK(hipMemcpyAsync(d_tree_blob_, sl.host, bytes, hipMemcpyHostToDevice, stream_));
   HIPCHECK(hipEventRecord(sl.done, stream_));
   const int32_t* di = reinterpret_cast<const int32_t*>(d_tree_blob_);
-  dev::DevTree t;
+  dev::DevTree t{};
   t.num_leaves = nl;
   t.split_feature_inner = di;
   t.left_child = di + ni;
@@ -463,7 +465,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   last_grad_fusable_ = false;
   if (listwise) {
     UploadRankTables(spec.rank, spec.kind);
-    dev::RankArgs ra;
+    dev::RankArgs ra{};
     ra.kind = spec.kind == DeviceGradKind::Lambdarank ? dev::kRankKindLambdarank : dev::kRankKindXendcg;
     ra.num_queries = spec.rank.num_queries;
     ra.qb = d_qb_;
@@ -495,12 +497,13 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     ra.norm = spec.rank.norm ? 1 : 0;
     ra.rng = d_rank_rng_;
     dev::RankGradients(ra, stream_);
+    HIPCHECK(hipGetLastError());  // (a failed launch would leave last iteration's gradients)
     gh_fresh_ = false;
     split_stale_ = false;
     last_grad_fusable_ = false;
     return true;
   }
-  dev::GradArgs g;
+  dev::GradArgs g{};
   g.kind = static_cast<int32_t>(spec.kind);
   g.num_class = spec.kind == DeviceGradKind::MulticlassSoftmax ? ntpi : 1;
   g.num_data = num_data_;
@@ -591,9 +594,22 @@ void GPUTreeLearner::UploadRankTables(const DeviceRankSpec& r, DeviceGradKind ki
   }
   d_rank_pairs_ = nullptr;
   d_rank_pair_off_ = nullptr;
-  constexpr int64_t kPairBudgetBytes = int64_t{6} << 30;
-  if (kind == DeviceGradKind::Lambdarank && pair_total > 0 &&
-      pair_total * static_cast<int64_t>(sizeof(float2)) <= kPairBudgetBytes) {
+  // budget: a share of the free memory (the histograms and round buffers are already resident),
+  // capped; LGBM_AMD_RANK_PAIR_MB overrides it
+  int64_t pair_budget = int64_t{tuning::kRankPairCapMb} << 20;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+    pair_budget = std::min<int64_t>(pair_budget, static_cast<int64_t>(tuning::kRankPairFreeShare * free_b));
+  } else {
+    (void)hipGetLastError();
+  }
+  pair_budget = static_cast<int64_t>(tuning::Int(tuning::Knob::RankPairMb, static_cast<int>(pair_budget >> 20))) << 20;
+  const int64_t pair_bytes = pair_total * static_cast<int64_t>(sizeof(float2));
+  if (kind == DeviceGradKind::Lambdarank && pair_total > 0 && pair_bytes > pair_budget) {
+    Log::Info("device lambdarank: pair scratch of %.1f MiB is over its %.1f MiB budget; each pair is evaluated "
+              "from both of its documents", pair_bytes / 1048576.0, pair_budget / 1048576.0);
+  }
+  if (kind == DeviceGradKind::Lambdarank && pair_total > 0 && pair_bytes <= pair_budget) {
     d_rank_pairs_ = Alloc<float2>(static_cast<size_t>(pair_total));
     d_rank_pair_off_ = Alloc<int64_t>(nq);
     HIPCHECK(hipMemcpy(d_rank_pair_off_, pair_off.data(), sizeof(int64_t) * nq, hipMemcpyHostToDevice));
@@ -642,7 +658,7 @@ data_size_t GPUTreeLearner::DeviceSample(const DeviceSampleSpec& sp) {
     uploaded_label_src_ = sp.label;
   }
   if (sp.goss) MaterializeSplitGradients();  // (GOSS reads and rescales grad / hess)
-  dev::SampleArgs s;
+  dev::SampleArgs s{};
   s.num_data = num_data_;
   s.num_blocks = nb;
   s.goss = sp.goss ? 1 : 0;

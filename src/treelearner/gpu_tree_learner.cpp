@@ -887,17 +887,23 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   // exactly these buffers (one model per iteration, not modified on the host since)
   root_from_parts_ = gh_fresh_ && gradients == d_grad_ && hessians == d_hess_;
   gh_fresh_ = false;
-  // (the reduction writes the whole absmax record: no reset copy)
+  // (the reduction writes the whole absmax record: no reset copy; without an all-reduce of it
+  // the same launch computes the scales)
+  const bool absmax_global = (data_parallel_ || voting_) && Network::num_machines() > 1;
+  double* fused_scales = absmax_global ? nullptr : d_scales_;
   if (root_from_parts_) {
-    dev::ReduceParts(d_max_parts_, d_root_parts_, grad_parts_, num_data_, rows_cap_, d_absmax_, d_root_, stream_);
+    dev::ReduceParts(d_max_parts_, d_root_parts_, grad_parts_, num_data_, rows_cap_, d_absmax_, d_root_, stream_,
+                     hist_units_, fused_scales);
   } else {
     MaterializeSplitGradients();
     dev::PackGH(gradients, hessians, d_gh_, args_.gh_stride, num_data_, d_max_parts_, stream_);
     dev::ReduceParts(d_max_parts_, nullptr, dev::PackBlocks(num_data_), num_data_, rows_cap_, d_absmax_, nullptr,
-                     stream_);
+                     stream_, hist_units_, fused_scales);
   }
-  AllreduceAbsMax();
-  dev::ComputeScales(d_absmax_, rows_cap_, hist_units_, d_scales_, stream_);
+  if (absmax_global) {
+    AllreduceAbsMax();
+    dev::ComputeScales(d_absmax_, rows_cap_, hist_units_, d_scales_, stream_);
+  }
   host_partition_fresh_ = false;
   DecideMode();
   if (device_mode_) return TrainDeviceMode();
@@ -1526,7 +1532,7 @@ bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction
   std::vector<int64_t> off(L + 1, 0);
   for (int l = 0; l < L; ++l) off[l + 1] = off[l] + leaves[l].count;
   HIPCHECK(hipMemcpyAsync(d_renew_off_, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, stream_));
-  dev::RenewArgs r;
+  dev::RenewArgs r{};
   r.leaves = d_leaves_;
   r.idx = d_idx_;
   r.tmp = d_tmp_;

@@ -186,9 +186,10 @@ def _train_scores(bst, n):
 
 
 @pytest.mark.parametrize("extra", [{}, {"lambdarank_norm": False}, {"weighted": True}, {"sigmoid": 2.5},
-                                   {"big": True}],
-                         ids=["norm", "no_norm", "weighted", "sigmoid", "queries_over_2048_docs"])
-def test_lambdarank_device_gradients_equal_host(gpu_available, extra):
+                                   {"big": True}, {"mid": True}, {"no_pairs": True}],
+                         ids=["norm", "no_norm", "weighted", "sigmoid", "queries_over_2048_docs",
+                              "queries_1600_to_2048_docs", "pair_scratch_over_budget"])
+def test_lambdarank_device_gradients_equal_host(gpu_available, extra, monkeypatch):
     """The device LambdaRank kernel replays the reference's accumulation (float sums of each
     document's lower-side pairs in the sorted order of the higher side, the double sum of its
     higher-side pairs added at its own position, the host's sigmoid table; reference
@@ -202,6 +203,15 @@ def test_lambdarank_device_gradients_equal_host(gpu_available, extra):
         group = np.array([3000, 40, 2500, 30, 60], dtype=np.int64)
         X = rng0.randn(int(group.sum()), 6).astype(np.float32)
         y = np.clip(np.floor(X[:, 0] + 0.3 * rng0.randn(len(X)) + 1.5), 0, 4).astype(np.float32)
+    if extra.pop("mid", False):
+        # queries staged in LDS whose staging passes 64 KiB (44 B per document: 1490+ documents)
+        rng0 = np.random.RandomState(5)
+        group = np.array([1600, 50, 2048, 1900, 20], dtype=np.int64)
+        X = rng0.randn(int(group.sum()), 6).astype(np.float32)
+        y = np.clip(np.floor(X[:, 0] + 0.3 * rng0.randn(len(X)) + 1.5), 0, 4).astype(np.float32)
+    if extra.pop("no_pairs", False):
+        # a pair scratch budget of 0: each pair evaluated from both of its documents
+        monkeypatch.setenv("LGBM_AMD_RANK_PAIR_MB", "0")
     rng = np.random.RandomState(2)
     init = np.round(rng.randn(len(y)) * 2, 1)  # (rounded: tied scores inside queries)
     weight = None
