@@ -62,12 +62,12 @@ def roc_auc(y, p):
 
 
 def growth_stats(booster):
-    """[trees, device-resident, rounds, expansions, splits, collective bytes] so far
-    (LGBM_AMD_BoosterGrowthStats: counters, no device synchronisation)"""
+    """[trees, device-resident, rounds, expansions, splits, collective bytes, trees launched
+    speculatively] so far (LGBM_AMD_BoosterGrowthStats: counters, no device synchronisation)"""
     import ctypes
     from lightgbmv1_amd import _native as nat
-    out = (ctypes.c_double * 6)()
-    nat.call("LGBM_AMD_BoosterGrowthStats", booster.handle, out, ctypes.c_int(6))
+    out = (ctypes.c_double * 7)()
+    nat.call("LGBM_AMD_BoosterGrowthStats", booster.handle, out, ctypes.c_int(7))
     return list(out)
 
 
@@ -136,6 +136,10 @@ def main():
     for _ in range(args.warmup):
         booster.update()
     torch_dist.barrier()
+    # (with speculation -- LGBM_AMD_SPECULATE=1, one process -- the last warm-up update launched
+    # the first timed tree, and this synchronisation lets it finish before the clock starts; the
+    # last timed update launches one more tree, which the closing synchronisation waits for: the
+    # timed region runs exactly `steps` trees' device work)
     _device_sync(lgb)
     stats0 = growth_stats(booster) if args.device == "gpu" else None
     t1 = time.perf_counter()
@@ -154,7 +158,8 @@ def main():
         # the timed trees' growth counters (no synchronisation inside the timed loop)
         d = [b - a for a, b in zip(stats0, growth_stats(booster))]
         diag = {"rounds_per_tree": round(d[2] / max(1.0, d[0]), 2),
-                "collective_bytes_per_iter": round(d[5] / args.steps)}
+                "collective_bytes_per_iter": round(d[5] / args.steps),
+                "speculated_trees": int(d[6])}
     auc = None
     if rank == 0 and args.test_rows > 0:
         Xt, yt = make_rows(n_total + 12345678, args.test_rows, args.features)

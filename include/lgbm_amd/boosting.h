@@ -186,13 +186,17 @@ class GBDT {
   // LGBM_AMD_ITER_LOG=<path>: one JSON line per boosting iteration (phase times, trees, device
   // collectives); distributed ranks write <path>.rank<r>
   std::unique_ptr<std::ofstream> iter_log_;
-  double growth_stats_[6] = {0, 0, 0, 0, 0, 0};
+  double growth_stats_[7] = {0, 0, 0, 0, 0, 0, 0};
   bool iter_log_checked_ = false;
   void LogIteration(double grad_ms, double bag_ms, const std::vector<double>& tree_ms, double renew_ms,
                     double score_ms, double total_ms, const std::vector<int>& leaves, const std::vector<int>& device,
                     const std::vector<int>& rounds, const std::vector<int>& expansions, const std::vector<int>& graphs,
                     double coll_bytes);
   DeviceTreeLearner* device_learner_ = nullptr;
+  // whether the device learner may launch the next iteration's tree before it is asked for:
+  // plain boosting whose next tree depends on nothing but this tree's score update -- no
+  // bagging, leaf renewal, custom gradients or dropped trees (DART / GOSS / RF: false)
+  virtual bool SpeculationSafe(bool own_gradients) const;
   const ObjectiveFunction* objective_ = nullptr;
   std::unique_ptr<ObjectiveFunction> loaded_objective_;
   std::vector<const Metric*> training_metrics_;
@@ -223,7 +227,8 @@ class GBDT {
  public:
   // the host learner's gradients of the last iteration (tests: device vs host objectives)
   const std::vector<score_t>& host_gradients() const { return gradients_; }
-  // LGBM_AMD_BoosterGrowthStats: [trees, device-resident, rounds, expansions, splits, collective bytes]
+  // LGBM_AMD_BoosterGrowthStats: [trees, device-resident, rounds, expansions, splits, collective bytes,
+  // trees launched speculatively]
   const double* growth_stats() const { return growth_stats_; }
   const std::vector<score_t>& host_hessians() const { return hessians_; }
   data_size_t train_num_data() const { return num_data_; }
@@ -253,6 +258,7 @@ class GBDT {
 class DART : public GBDT {
  public:
   DART() { name_ = "dart"; }
+  bool SpeculationSafe(bool) const override { return false; }
   void Init(const Config* config, const Dataset* train_data, const ObjectiveFunction* objective,
             const std::vector<const Metric*>& training_metrics) override;
   void ResetConfig(const Config* config) override;
@@ -276,6 +282,7 @@ class DART : public GBDT {
 class GOSS : public GBDT {
  public:
   GOSS() { name_ = "goss"; }
+  bool SpeculationSafe(bool) const override { return false; }
   void Init(const Config* config, const Dataset* train_data, const ObjectiveFunction* objective,
             const std::vector<const Metric*>& training_metrics) override;
   void ResetTrainingData(const Dataset* train_data, const ObjectiveFunction* objective,
@@ -294,6 +301,7 @@ class GOSS : public GBDT {
 
 class RF : public GBDT {
  public:
+  bool SpeculationSafe(bool) const override { return false; }
   RF() {
     name_ = "rf";
     average_output_ = true;

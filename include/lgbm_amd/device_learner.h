@@ -45,6 +45,10 @@ class DeviceTreeLearner {
   // without leaf renewal).  The learner may then add it on the device as soon as the splits are
   // known, while the host builds the Tree object (0: no promise)
   virtual void ExpectTrainingScoreUpdate(double shrinkage) { (void)shrinkage; }
+  // GBDT's permission, per iteration, to launch the next tree on the device before this
+  // Train() returns (plain boosting: no bagging, renewal, custom gradients or dropped trees);
+  // the learner checks the next Train()'s inputs against the launch and regrows if they differ
+  virtual void AllowSpeculation(bool allowed) { (void)allowed; }
   // any tree, by traversal of the binned training rows
   virtual void AddTreeToScore(const Tree* tree, int tree_id) = 0;
   // device gradients for a point-wise objective; false if the spec is unsupported
@@ -81,6 +85,7 @@ class DeviceTreeLearner {
     int expansions = 0;  // round growth: nodes expanded (accepted splits + speculation never accepted)
     bool graph = false;  // the tree's kernels (and collectives) were replayed from hipGraphs
     double collective_bytes = 0.0;
+    bool speculated = false;  // grown by a launch made when the previous tree ended (AllowSpeculation)
   };
   virtual TreeStats LastTreeStats() const { return TreeStats(); }
   // percentile leaf renewal (L1 / quantile / MAPE) of the tree just grown, on the device from

@@ -61,6 +61,7 @@ constexpr int kQueryMetricDeviceMaxDocs = 16384;
   X(XtRounds, "LGBM_AMD_XT_ROUNDS", "0: extra_trees grows one split per step instead of rounds")                \
   X(CegbRounds, "LGBM_AMD_CEGB_ROUNDS", "0: CEGB coupled penalties refunded on one split per step until every feature is used")  \
   X(HostOut, "LGBM_AMD_HOST_OUT", "0: the host copies a round tree's records instead of its last plan writing them")  \
+  X(Speculate, "LGBM_AMD_SPECULATE", "1: the next tree is launched when this one ends, before GBDT asks for it")  \
   /* storage layout (same models) */                                                                           \
   X(NibbleBins, "LGBM_AMD_NIBBLE_BINS", "1: 4-bit rows for groups of <= 16 bins (auto above 32 GiB)")          \
   X(ColumnCopy, "LGBM_AMD_COLUMN_COPY", "0/1: column-major copy of the bins (auto below 8 GiB)")                \

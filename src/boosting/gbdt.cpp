@@ -518,6 +518,14 @@ void GBDT::LogIteration(double grad_ms, double bag_ms, const std::vector<double>
   iter_log_->flush();
 }
 
+bool GBDT::SpeculationSafe(bool own_gradients) const {
+  const Config& c = *config_;
+  const bool bagging = c.bagging_freq > 0 && (c.bagging_fraction < 1.0 || c.pos_bagging_fraction < 1.0 ||
+                                              c.neg_bagging_fraction < 1.0);
+  return own_gradients && num_tree_per_iteration_ == 1 && !bagging && !need_re_bagging_ && bag_data_cnt_ == num_data_ &&
+         !(objective_ != nullptr && objective_->IsRenewTreeOutput());
+}
+
 bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
   common::ScopedTimer timer("GBDT::TrainOneIter");
   if (!iter_log_checked_) {
@@ -573,6 +581,7 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
           !(objective_ != nullptr && objective_->IsRenewTreeOutput())) {
         device_learner_->ExpectTrainingScoreUpdate(shrinkage_rate_);
       }
+      if (device_learner_ != nullptr) device_learner_->AllowSpeculation(SpeculationSafe(gradients == nullptr));
       tree.reset(tree_learner_->Train(grad + off, hess + off));
       if (device_learner_ != nullptr) {
         const auto st = device_learner_->LastTreeStats();
@@ -582,6 +591,7 @@ bool GBDT::TrainOneIter(const score_t* gradients, const score_t* hessians) {
         growth_stats_[3] += st.expansions;
         growth_stats_[4] += st.splits;
         growth_stats_[5] += st.collective_bytes;
+        growth_stats_[6] += st.speculated ? 1 : 0;
       }
     }
     if (iter_log_) {

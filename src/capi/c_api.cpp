@@ -1452,7 +1452,7 @@ int LGBM_AMD_BoosterLastGradients(BoosterHandle handle, float* grad, float* hess
 int LGBM_AMD_BoosterGrowthStats(BoosterHandle handle, double* out, int n) {
   API_BEGIN();
   const double* s = static_cast<Booster*>(handle)->boosting()->growth_stats();
-  for (int i = 0; i < n && i < 6; ++i) out[i] = s[i];
+  for (int i = 0; i < n && i < 7; ++i) out[i] = s[i];
   API_END();
 }
 

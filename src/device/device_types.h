@@ -158,6 +158,10 @@ struct FeatureBest {
   double lg, lh, rg, rh, lo, ro;
   int32_t feature, real_feature, thr, default_left, lc, rc, mono;
   int32_t ncat;  // categorical: categories in the left set (KArgs::feat_cat); 0: numerical
+  // the scan's "feature had a valid split" flag it wrote into KArgs::splittable (-1: none
+  // written) -- gathered with the record, so distributed rounds complete every rank's rows
+  int32_t flag;
+  int32_t pad;
 };
 
 // voting-parallel: one rank's proposal for a leaf (reference LightSplitInfo: the local best

@@ -910,6 +910,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   o.lc = o.rc = 0;
   o.mono = 0;
   o.ncat = 0;
+  o.flag = -1;
+  o.pad = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
   bool write = true;
   if (KIND == 1 && F.is_cat) {
@@ -919,6 +921,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   } else if (tree_used && !parent_ok) {
     // the parent could not split on f: neither child evaluates it (SerialTreeLearner::FindBestSplits)
     if (tid == 0) flags[f] = 0;
+    o.flag = 0;
   } else if (tree_used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
     // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
     // but keeps its histogram (descendants subtract it); voting's local scan evaluates it (its
@@ -1061,6 +1064,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
                                                     sh.sc2, kNoRandThr);
       }
       if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (voting: the local scan's flags)
+      if (!vote_global) o.flag = splittable ? 1 : 0;
       // CEGB (GPUTreeLearner::CegbRounds: no refunds in a round tree), before the monotone
       // penalty as SerialTreeLearner::ComputeBestSplitForFeature
       if (a.p.cegb && !a.round_cegb) {  // (KArgs::round_cegb: the replay subtracts them)
@@ -1436,6 +1440,8 @@ __device__ bool XtEvalNum(const KArgs& a, const Feature& F, int f, int node, con
   o.lc = o.rc = 0;
   o.mono = F.monotone;
   o.ncat = 0;
+  o.flag = -1;
+  o.pad = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
   for (int d = 0; d < (two ? 2 : 1); ++d) {
     const double bg = d == 0 ? rb_gain : fb_gain;
@@ -1523,7 +1529,11 @@ __device__ bool DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
     }
   }
   const RNode& P = a.rnode[n];
-  const int nl = P.total_left, nr = P.count - P.total_left;
+  // (data-parallel: the children's global counts -- the split's estimates -- as the reference's
+  // GetGlobalDataCountInLeaf; this rank's rows otherwise)
+  const bool dpc = a.p.data_parallel != 0;
+  const int nl = dpc ? a.rnode[c].st.global_count : P.total_left;
+  const int nr = dpc ? a.rnode[c + 1].st.global_count : P.count - P.total_left;
   const int depth = a.rnode[c].st.depth;
   const bool scanned = s + 1 < L - 1 && !(a.p.max_depth > 0 && depth >= a.p.max_depth) && !(nl < 2 * md && nr < 2 * md);
   if (!scanned) {
@@ -1890,7 +1900,13 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     if (a.leaf_rows != nullptr && static_cast<int>(a.root[2]) >= 2 * a.p.sp.min_data_in_leaf) {
       const int8_t* rf0 = a.splittable + static_cast<size_t>(a.leaves[0].frow) * NF;
       for (int f = tid; f < NF; f += kPlanThreads) {
-        if (a.tree_mask[f] && (a.node_mask == nullptr || a.node_mask[f])) a.leaf_rows[f] = rf0[f];
+        if (!(a.tree_mask[f] && (a.node_mask == nullptr || a.node_mask[f]))) continue;
+        if (a.round_dist) {  // (each rank wrote its own features' flags: the gathered records carry them all)
+          const int fl = a.feat_best[FeatBestIndex(a, 0, f)].flag;
+          if (fl >= 0) a.leaf_rows[f] = static_cast<int8_t>(fl);
+        } else {
+          a.leaf_rows[f] = rf0[f];
+        }
       }
     }
     __syncthreads();
@@ -1913,6 +1929,9 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         NoSplit(&a.best[0]);
       }
       a.cbest[0] = fb;
+      // (per-node sampling: a root the reference learner does not scan makes no draw -- the
+      // host advances its sampler by Round::bynode_next draws)
+      if (a.round_bynode && static_cast<int>(a.root[2]) < 2 * a.p.sp.min_data_in_leaf) rd->bynode_next = 0;
       const Leaf R = a.leaves[0];
       RNode r;
       r.begin = R.begin;
@@ -2493,7 +2512,30 @@ __global__ __launch_bounds__(kFindThreads) void k_round_childbest(KArgs a) {
   Round* rd = a.rd;
   const int done = rd->done, nexp = rd->nexp;
   const int y = blockIdx.x;
-  if (!done && y < 2 * nexp) ChildBest<0, kFindThreads>(a, y, rd->e[y >> 1].frow_child[y & 1], sh);
+  if (!done && y < 2 * nexp) {
+    const int node = rd->e[y >> 1].frow_child[y & 1];
+    ChildBest<0, kFindThreads>(a, y, node, sh);
+    // deferred folds (per-node sampling, CEGB): every rank's copy of the child's per-feature
+    // results and flags, from the gathered records (each rank scanned only its own features)
+    if (a.round_dist && !a.round_vote && (a.node_fb != nullptr || a.leaf_rows != nullptr)) {
+      const int NF = a.p.num_features;
+      typedef __attribute__((address_space(1))) int8_t GlobalI8;
+      for (int f = threadIdx.x; f < NF; f += blockDim.x) {
+        if (!a.tree_mask[f]) continue;  // (no owner this tree)
+        const size_t wi = RoundFbIndex(a, y, f);
+        const FeatureBest r = a.feat_best[wi];
+        if (a.node_fb != nullptr) PublishRecord(&a.node_fb[static_cast<size_t>(node) * NF + f], r);
+        if (r.flag >= 0) {
+          __hip_atomic_store((GlobalI8*)(a.splittable + static_cast<size_t>(node) * NF + f), static_cast<int8_t>(r.flag),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (a.node_fb_cat != nullptr && a.node_cat_slot[f] >= 0 && r.ncat > 0) {
+          PublishCatCopy(a.node_fb_cat + (static_cast<size_t>(node) * a.node_cat_slots + a.node_cat_slot[f]) * kMaxCatWords,
+                         a.feat_cat + wi * kMaxCatWords);
+        }
+      }
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   ArrivalRelease();
   __syncthreads();

@@ -372,6 +372,8 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   o.lc = o.rc = 0;
   o.mono = 0;
   o.ncat = 0;
+  o.flag = -1;
+  o.pad = 0;
   o.lg = o.lh = o.rg = o.rh = o.lo = o.ro = 0.0;
   // a sampled-out feature (bynode) still materialises its histogram: descendants subtract it
   if (tree_used && (!F.is_cat || F.num_bin <= kFindMaxCatBins)) {
@@ -495,6 +497,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
                                               xt_thr);
     }
     if (tid == 0 && !vote_global && !rescan) flags[f] = splittable ? 1 : 0;  // (the local scan's flags stay)
+    if (!vote_global && !rescan) o.flag = splittable ? 1 : 0;
     // SerialTreeLearner::EvalFeature order: the CEGB cost (the raw candidate remembered for the
     // coupled-penalty refund), then the monotone depth penalty
     if (a.p.cegb && tid == 0) {
@@ -517,7 +520,8 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     if (a.forced_n > 0 && tid == 0 && !vote_global && !rescan) {
       const int k = ROOT ? 0 : (s < a.forced_n ? a.forced_child[2 * s + sd.lr] : -1);
       if (k >= 0 && k < a.forced_n && a.forced_feat[k] == f) {
-        FeatureBest fo;
+        FeatureBest fo = {};
+        fo.flag = -1;
         int fbin;
         ForcedGather(F, hv, L, p, a.forced_thr[k], &fo, &fbin);
         if (fo.feature == -2) {

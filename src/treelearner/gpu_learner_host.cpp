@@ -174,6 +174,7 @@ void GPUTreeLearner::RenewTreeOutput(Tree* tree, const ObjectiveFunction* obj,
                                      data_size_t total_num_data, const data_size_t* bag_indices,
                                      data_size_t bag_cnt) const {
   if (obj == nullptr || !obj->IsRenewTreeOutput()) return;
+  if (spec_live_) Log::Fatal("device learner: leaf renewal after the next tree was launched (speculation not allowed)");
   DownloadPartitionToHost();
   SerialTreeLearner::RenewTreeOutput(tree, obj, residual, total_num_data, bag_indices, bag_cnt);
 }

@@ -65,11 +65,13 @@ void GPUTreeLearner::AllocRoundState() {
   a.cbest_cat = d_cbest_cat_;
   a.child_cnt = d_child_cnt_;
   round_hist_.clear();
-  // per-node sampling on round growth (KArgs::round_bynode): one process, no interaction
+  // per-node sampling on round growth (KArgs::round_bynode): one process or the data- /
+  // feature-parallel learners (every rank draws the same samples; k_round_childbest completes
+  // each rank's per-node results and flags from the gathered records), no interaction
   // constraints (categorical features: their category sets are kept per node)
   bool any_cat = false;
   for (int f = 0; f < num_features_; ++f) any_cat = any_cat || data_->FeatureBinMapper(f)->bin_type() == BinType::Categorical;
-  const bool base_rounds = config_->interaction_constraints_vector.empty() && !distributed_;
+  const bool base_rounds = config_->interaction_constraints_vector.empty() && !voting_;
   const bool simple_rounds = base_rounds && !any_cat;
   // (categorical features: each node keeps its categorical features' category sets)
   std::vector<int32_t> cat_slot(std::max(1, num_features_), -1);
@@ -83,7 +85,7 @@ void GPUTreeLearner::AllocRoundState() {
   // extra_trees on round growth (KArgs::round_xt): also no CEGB or forced splits, at most
   // kXtLaneFeatures * 64 features (the replay's draw counters), prefix tables under 8 GiB
   const double pre_bytes = static_cast<double>(split_rows_) * total_bins_ * sizeof(dev::XtPre);
-  const bool xt = config_->extra_trees && simple_rounds && !CostEffectiveGB::Enabled(*config_) &&
+  const bool xt = config_->extra_trees && simple_rounds && !distributed_ && !CostEffectiveGB::Enabled(*config_) &&
                   config_->forcedsplits_filename.empty() && num_features_ <= 4 * 64 &&
                   pre_bytes <= 8.0 * (1ull << 30) && !tuning::Off(tuning::Knob::XtRounds);
   // CEGB coupled penalties on round growth (KArgs::round_cegb): also no lazy penalties or
@@ -237,7 +239,7 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
   return true;
 }
 
-// CEGB on round growth (one process, no lazy penalties).  A scan subtracts the split penalty,
+// CEGB on round growth (one process or data- / feature-parallel, no lazy penalties).  A scan subtracts the split penalty,
 // tradeoff * penalty_split * rows, which depends on the node's own rows only.  A coupled
 // penalty depends on whether the model has used the feature, and a feature's first use refunds
 // the other leaves' remembered candidates (CostEfficientGradientBoosting::UpdateLeafBestSplits):
@@ -247,7 +249,7 @@ bool GPUTreeLearner::RoundGrowth(const dev::KArgs& a) const {
 // later are of features outside this tree's sample (not scanned here).  Earlier trees grow one
 // split per step, as do all trees with lazy penalties.
 bool GPUTreeLearner::CegbRounds(const dev::KArgs& a) const {
-  if (distributed_ || a.cegb_lazy != nullptr || cegb_ == nullptr) return false;
+  if (voting_ || a.cegb_lazy != nullptr || cegb_ == nullptr) return false;
   if (a.cegb_coupled == nullptr || a.round_cegb) return true;  // (round_cegb: refunds in the replay)
   const std::vector<char>& used = cegb_->used_in_split();
   for (int f = 0; f < num_features_; ++f) {
@@ -263,7 +265,14 @@ bool GPUTreeLearner::CegbRounds(const dev::KArgs& a) const {
 // missing one a host round trip and a graph launch per segment)
 
 int GPUTreeLearner::RunRounds(dev::KArgs a) {
-  common::ScopedTimer timer("GPUTreeLearner::RunRounds");
+  RoundLaunch rl = LaunchRounds(a);
+  return WaitRounds(&rl);
+}
+
+// the tree's root graph and its provisioned rounds, enqueued without waiting (also the
+// speculative launch of the next tree, LaunchSpeculative)
+GPUTreeLearner::RoundLaunch GPUTreeLearner::LaunchRounds(dev::KArgs a) {
+  common::ScopedTimer timer("GPUTreeLearner::LaunchRounds");
   a.rd = d_round_;
   // one process: the tree's last plan hands its records and scalars to the host directly
   a.host_out = (!distributed_ && !tuning::Off(tuning::Knob::HostOut)) ? h_tree_out_ : nullptr;
@@ -354,15 +363,10 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
       if (!graph) DestroyRoundGraphs();
     }
   }
-  last_stats_.graph = graph;
-  auto launch_seg = [&]() {
-    if (graph) {
-      common::ScopedTimer launch_timer("GPUTreeLearner::SegmentGraphLaunch");
-      HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
-    } else {
-      for (int r = 0; r < seg; ++r) EnqueueRound(a);
-    }
-  };
+  RoundLaunch rl;
+  rl.a = a;
+  rl.graph = graph;
+  rl.seg = seg;
   if (graph) {
     common::ScopedTimer launch_timer("GPUTreeLearner::RootGraphLaunch");
     HIPCHECK(hipGraphLaunch(round_root_execs_[root_rounds], stream_));
@@ -370,11 +374,34 @@ int GPUTreeLearner::RunRounds(dev::KArgs a) {
     EnqueueRoot(a);
     for (int r = 0; r < root_rounds; ++r) EnqueueRound(a);
   }
-  int launched = root_rounds;
-  while (launched < want) {  // (asynchronous: enqueued while the root graph runs)
-    launch_seg();
-    launched += seg;
+  rl.launched = root_rounds;
+  while (rl.launched < want) {  // (asynchronous: enqueued while the root graph runs)
+    LaunchSegment(rl);
+    rl.launched += seg;
   }
+  return rl;
+}
+
+void GPUTreeLearner::LaunchSegment(const RoundLaunch& rl) {
+  if (rl.graph) {
+    common::ScopedTimer launch_timer("GPUTreeLearner::SegmentGraphLaunch");
+    HIPCHECK(hipGraphLaunch(round_seg_exec_, stream_));
+  } else {
+    for (int r = 0; r < rl.seg; ++r) EnqueueRound(rl.a);
+  }
+}
+
+// the host side of a launched tree: wait for its last plan (more segments if the provisioned
+// rounds did not finish it), then its counters
+int GPUTreeLearner::WaitRounds(RoundLaunch* rlp) {
+  common::ScopedTimer timer("GPUTreeLearner::RunRounds");
+  RoundLaunch& rl = *rlp;
+  const dev::KArgs& a = rl.a;
+  volatile int32_t* flag = a.host_out;
+  const int L = config_->num_leaves, seg = rl.seg;
+  int& launched = rl.launched;
+  auto launch_seg = [&]() { LaunchSegment(rl); };
+  last_stats_.graph = rl.graph;
   // the host reads the Round record's scalars only (done, splits, rounds, nodes); the split
   // records follow once the tree is done (TrainDeviceMode)
   constexpr size_t kRoundHeader = offsetof(dev::Round, cur);

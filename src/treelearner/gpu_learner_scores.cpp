@@ -443,6 +443,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
   const size_t n = static_cast<size_t>(num_data_);
   const bool prefetched = grad_prefetched_;
   grad_prefetched_ = false;
+  grad_from_prefetch_ = false;
   bool uploaded = false;
   if (uploaded_label_src_ != spec.label) {
     if (d_label_ == nullptr) d_label_ = Alloc<float>(n);
@@ -535,9 +536,11 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
       gh_fresh_ = true;
       split_stale_ = true;
       last_grad_fusable_ = true;
+      grad_from_prefetch_ = true;
       return true;
     }
   }
+  grad_from_prefetch_ = false;
   dev::Gradients(g, stream_);
   gh_fresh_ = fuse;
   split_stale_ = fuse;

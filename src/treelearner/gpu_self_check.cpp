@@ -46,6 +46,10 @@ bool LeafScanned(const Tree* tree, int leaf, const Config& cfg) {
 
 bool GPUTreeLearner::DebugLeafState(const Tree* tree, int leaf, std::vector<int32_t>* rows,
                                     std::vector<long long>* hist, std::vector<int8_t>* bin_valid, double* sums) {
+  if (spec_live_) {
+    Log::Fatal("device learner: the device holds the next tree (launched speculatively); set "
+               "LGBM_AMD_SPECULATE=0 to inspect the last tree's device state");
+  }
   if (!device_mode_ || d_leaves_ == nullptr || tree == nullptr || leaf < 0 || leaf >= tree->num_leaves()) {
     return false;
   }
@@ -94,6 +98,10 @@ bool GPUTreeLearner::DebugGradients(std::vector<float>* g, std::vector<float>* h
 }
 
 std::string GPUTreeLearner::DebugCheckSplits(const Tree* tree) {
+  if (spec_live_) {
+    Log::Fatal("device learner: the device holds the next tree (launched speculatively); set "
+               "LGBM_AMD_SPECULATE=0 to inspect the last tree's device state");
+  }
   std::ostringstream js;
   if (!device_mode_ || tree == nullptr) return "{\"device_mode\": false}";
   double scales[4];

@@ -43,6 +43,8 @@ bool GPUTreeLearner::WideHistograms(const Config& c) {
 GPUTreeLearner::GPUTreeLearner(const Config* config, Mode mode) : SerialTreeLearner(config), mode_(mode) {}
 
 GPUTreeLearner::~GPUTreeLearner() {
+  if (spec_live_ && stream_ != nullptr) (void)hipStreamSynchronize(stream_);  // (a launched next tree)
+  spec_live_ = false;
   FreeAll();
   for (void* p : valid_allocs_) (void)hipFree(p);
 }
@@ -718,6 +720,8 @@ void GPUTreeLearner::AllocSplittable() {
 }
 
 void GPUTreeLearner::ResetTrainingData(const Dataset* train_data, bool is_constant_hessian) {
+  DropSpeculation();
+  ++state_epoch_;
   SerialTreeLearner::ResetTrainingData(train_data, is_constant_hessian);
   HIPCHECK(hipSetDevice(device_id_));
   // rebuild the device data for the new rows (bin mappers are aligned)
@@ -734,6 +738,8 @@ void GPUTreeLearner::ResetTrainingData(const Dataset* train_data, bool is_consta
 }
 
 void GPUTreeLearner::ResetConfig(const Config* config) {
+  DropSpeculation();
+  ++state_epoch_;
   const int old_leaves = config_->num_leaves;
   SerialTreeLearner::ResetConfig(config);
   DestroyGraph();  // kernel arguments are baked into the captured graph
@@ -850,6 +856,7 @@ void GPUTreeLearner::DecideMode() {
 }
 
 void GPUTreeLearner::SetBaggingData(const Dataset* subset, const data_size_t* used_indices, data_size_t n) {
+  DropSpeculation();
   SerialTreeLearner::SetBaggingData(subset, used_indices, n);
   HIPCHECK(hipSetDevice(device_id_));
   oob_cnt_ = 0;
@@ -887,6 +894,23 @@ Tree* GPUTreeLearner::Train(const score_t* gradients, const score_t* hessians) {
   // exactly these buffers (one model per iteration, not modified on the host since)
   root_from_parts_ = gh_fresh_ && gradients == d_grad_ && hessians == d_hess_;
   gh_fresh_ = false;
+  if (spec_live_) {
+    // the tree launched when the last one ended: its scales came from the score walk's
+    // partials, so it is this tree when these are the walk's gradients and nothing was reset
+    if (root_from_parts_ && grad_from_prefetch_ && spec_epoch_ == state_epoch_ && !use_bag_) {
+      spec_live_ = false;
+      spec_sampler_.reset();
+      host_partition_fresh_ = false;
+      DecideMode();
+      if (device_mode_) return TrainDeviceMode(true);
+      DropSpeculation();  // (unreachable: the mode depends on the configuration only)
+    } else {
+      Log::Debug("device learner: the launched tree is regrown (walk parts %d, prefetched gradients %d, epoch %d, bag %d)",
+                 root_from_parts_ ? 1 : 0, grad_from_prefetch_ ? 1 : 0, spec_epoch_ == state_epoch_ ? 1 : 0,
+                 use_bag_ ? 1 : 0);
+      DropSpeculation();
+    }
+  }
   // (the reduction writes the whole absmax record: no reset copy; without an all-reduce of it
   // the same launch computes the scales)
   const bool absmax_global = (data_parallel_ || voting_) && Network::num_machines() > 1;
@@ -1164,10 +1188,12 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   }
 }
 
-Tree* GPUTreeLearner::TrainDeviceMode() {
-  col_sampler_.ResetByTree();
-  const auto& mask = col_sampler_.is_feature_used_bytree();
-  for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
+Tree* GPUTreeLearner::TrainDeviceMode(bool speculated) {
+  if (!speculated) {  // (a speculated tree drew its sample when it was launched)
+    col_sampler_.ResetByTree();
+    const auto& mask = col_sampler_.is_feature_used_bytree();
+    for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
+  }
   OwnershipForTree();
   dev::KArgs a = args_;
   const bool bynode = config_->feature_fraction_bynode < 1.0;
@@ -1222,6 +1248,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   last_stats_.rounds = 0;
   last_stats_.expansions = 0;
   last_stats_.graph = false;
+  last_stats_.speculated = speculated;
   const bool can_round = RoundGrowth(a);
   const bool rounds = can_round && AutoGrowthRounds();
   const auto t_grow = std::chrono::steady_clock::now();
@@ -1233,6 +1260,7 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     for (int l = 0; l < config_->num_leaves; ++l) lv[l].frow = l;
     HIPCHECK(hipMemcpy(d_leaves_, lv.data(), sizeof(dev::Leaf) * lv.size(), hipMemcpyHostToDevice));
   }
+  if (speculated && !rounds) Log::Fatal("device learner: the launched next tree is not a round tree");
   last_tree_rounds_ = rounds;
   int num_splits = 0;
   if (rounds) {
@@ -1241,7 +1269,13 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
       h_cegb_used_.resize(std::max(1, num_features_), 0);
       HIPCHECK(hipMemcpyAsync(d_cegb_used_, h_cegb_used_.data(), h_cegb_used_.size(), hipMemcpyHostToDevice, stream_));
     }
-    num_splits = RunRounds(a);
+    if (speculated) {
+      num_splits = WaitRounds(&spec_);
+    } else if (spec_live_) {
+      Log::Fatal("device learner: a launched next tree was not consumed");
+    } else {
+      num_splits = RunRounds(a);
+    }
     if (a.round_cegb && a.cegb_coupled != nullptr && cegb_) {  // (the features the tree used first)
       HIPCHECK(hipStreamSynchronize(stream_));
       HIPCHECK(hipMemcpy(h_cegb_used_.data(), d_cegb_used_, h_cegb_used_.size(), hipMemcpyDeviceToHost));
@@ -1327,10 +1361,9 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
   }
   if (bynode && rounds) {
     // round growth: the draws the replay counted (Round::bynode_next), the root's included
-    // when the root was scanned (one process: the root's rows are this rank's)
-    const bool root_scanned = root_rows_ >= 2 * config_->min_data_in_leaf;
+    // when the root was scanned (0 otherwise: the root plan decides from the global count)
     Log::Debug("device learner: %d splits in rounds, %d by-node draws", num_splits, h_round_->bynode_next);
-    col_sampler_.AdvanceByNode(root_scanned ? h_round_->bynode_next : 0);
+    col_sampler_.AdvanceByNode(h_round_->bynode_next);
   } else if (bynode) {
     // the root's draw happens only if the host learner would have scanned the root
     const bool root_scanned = h_step_->root_count >= 2 * config_->min_data_in_leaf;  // global count
@@ -1413,7 +1446,60 @@ Tree* GPUTreeLearner::TrainDeviceMode() {
     Log::Warning("No further splits with positive gain, best gain: %f", -std::numeric_limits<double>::infinity());
   }
   Log::Debug("Trained a tree with leaves = %d and max_depth = %d", tree->num_leaves(), tree->max_depth());
+  // the records are consumed: the next tree may be launched now (its last plan rewrites them)
+  const bool spec_ok = SpeculationEligible(a, rounds) && early_scored_leaves_ == num_splits + 1 && num_splits >= 1;
+  Log::Debug("device learner: next tree %s (allowed %d, rounds %d, scored early %d/%d)", spec_ok ? "launched" : "not launched",
+             spec_allowed_ ? 1 : 0, rounds ? 1 : 0, early_scored_leaves_, num_splits + 1);
+  if (spec_ok) LaunchSpeculative();
   return tree.release();
+}
+
+// The next tree may be launched before GBDT asks for it when nothing between the two Train()
+// calls can change its inputs: GBDT allowed it (plain boosting, no bagging / renewal / custom
+// gradients, one model per iteration), this tree's score walk computes the next gradients, and
+// the tree grows in rounds of a single process without per-tree host state (per-node samples,
+// extra_trees draws, CEGB, forced splits, intermediate monotone, the timing probe).
+bool GPUTreeLearner::SpeculationEligible(const dev::KArgs& a, bool rounds) const {
+  if (!spec_allowed_ || !rounds || distributed_ || use_bag_ || !device_mode_) return false;
+  if (!tuning::On(tuning::Knob::Speculate)) return false;  // (opt-in: profiles/r06_speculation_ab.md)
+  if (a.host_out == nullptr && !tree_out_used_) return false;
+  if (config_->feature_fraction_bynode < 1.0 || config_->extra_trees || CostEffectiveGB::Enabled(*config_)) return false;
+  if (a.forced_n > 0 || a.p.mono_inter || a.ktrace != nullptr) return false;
+  if (auto_state_ != kAutoRounds || num_tree_per_iteration_ != 1) return false;
+  return true;
+}
+
+void GPUTreeLearner::LaunchSpeculative() {
+  common::ScopedTimer timer("GPUTreeLearner::LaunchSpeculative");
+  // Train()'s prologue: the scales and root sums from the walk's partials (as a prefetched
+  // gradient computation leaves them), the tree's feature sample
+  const int parts = dev::AddTreeScoreGradParts(num_data_);
+  dev::ReduceParts(d_max_parts_, d_root_parts_, parts, num_data_, rows_cap_, d_absmax_, d_root_, stream_, hist_units_,
+                   d_scales_);
+  spec_sampler_.reset(new ColSampler(col_sampler_));
+  col_sampler_.ResetByTree();
+  const auto& mask = col_sampler_.is_feature_used_bytree();
+  for (int f = 0; f < num_features_; ++f) h_mask_[f] = mask[f];
+  // TrainDeviceMode's arguments of a plain round tree over every row
+  dev::KArgs a = args_;
+  a.num_rows = num_data_;
+  a.root_identity = 1;
+  root_rows_ = num_data_;
+  const bool keep_parts = root_from_parts_;
+  root_from_parts_ = true;  // (the root graph of this mode: root sums from the partials)
+  spec_ = LaunchRounds(a);
+  root_from_parts_ = keep_parts;
+  spec_live_ = true;
+  spec_epoch_ = state_epoch_;
+}
+
+void GPUTreeLearner::DropSpeculation() {
+  if (!spec_live_) return;
+  spec_live_ = false;
+  HIPCHECK(hipStreamSynchronize(stream_));  // (the launched tree finishes: its rounds were provisioned or exit)
+  if (spec_sampler_) col_sampler_ = *spec_sampler_;
+  spec_sampler_.reset();
+  ++state_epoch_;
 }
 
 // CEGB on the device (split + coupled penalties): the penalties, the model-wide used flags
@@ -1501,6 +1587,7 @@ void GPUTreeLearner::SetupMonoInter() {
 // leaves' rows straight from the partition, residuals from the device scores; leaf outputs
 // averaged over the ranks like the host path
 bool GPUTreeLearner::RenewTreeOutputOnDevice(Tree* tree, const ObjectiveFunction* obj, int tree_id) {
+  if (spec_live_) Log::Fatal("device learner: leaf renewal after the next tree was launched (speculation not allowed)");
   DeviceRenewSpec spec;
   if (!device_mode_ || obj == nullptr || !obj->DeviceRenew(&spec) || spec.label == nullptr || d_score_ == nullptr) {
     return false;

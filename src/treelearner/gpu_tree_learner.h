@@ -66,6 +66,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void MultiplyScore(double v, int tree_id) override;
   void AddTrainedTreeToScore(const Tree* tree, int tree_id) override;
   void ExpectTrainingScoreUpdate(double shrinkage) override { expect_shrinkage_ = shrinkage; }
+  void AllowSpeculation(bool allowed) override { spec_allowed_ = allowed; }
   void AddTreeToScore(const Tree* tree, int tree_id) override;
   bool ComputeGradients(const DeviceGradSpec& spec, int num_tree_per_iteration) override;
   void UploadGradients(const score_t* g, const score_t* h, int64_t n) override;
@@ -108,7 +109,7 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   void FreeAll();
   void FreeBuffers();
   void DecideMode();
-  Tree* TrainDeviceMode();
+  Tree* TrainDeviceMode(bool speculated = false);
   void EnqueueTree(const dev::KArgs& a);
   void DestroyGraph();
   void KernelFloorProbe(const dev::KArgs& a);
@@ -145,6 +146,31 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   bool RoundGrowth(const dev::KArgs& a) const;
   bool CegbRounds(const dev::KArgs& a) const;  // CEGB penalties on round growth (this tree)
   int RunRounds(dev::KArgs a);  // the tree's splits; h_rec_ holds their records
+  struct RoundLaunch {  // a launched round tree (LaunchRounds), as its wait needs it
+    dev::KArgs a{};
+    int launched = 0;  // rounds enqueued
+    int seg = 1;
+    bool graph = false;
+  };
+  RoundLaunch LaunchRounds(dev::KArgs a);
+  void LaunchSegment(const RoundLaunch& rl);
+  int WaitRounds(RoundLaunch* rl);
+  // Speculative next tree (one process, plain round growth, GBDT's permission): when a tree's
+  // last plan is seen, its score walk (+ the next gradients) is already enqueued, and so is
+  // the next tree -- its scales, root and provisioned rounds -- before the host returns
+  // through GBDT.  The next Train() only waits for it if its inputs are the ones the launch
+  // assumed (the walk's gradients, nothing reset); otherwise the launched tree is drained and
+  // the tree grown again with the same feature sample.
+  bool SpeculationEligible(const dev::KArgs& a, bool rounds) const;
+  void LaunchSpeculative();
+  void DropSpeculation();  // drain a launched next tree, restore the column sampler
+  bool spec_allowed_ = false;
+  bool spec_live_ = false;
+  RoundLaunch spec_;
+  std::unique_ptr<ColSampler> spec_sampler_;  // the sampler before the launched tree's draw
+  uint64_t state_epoch_ = 0;     // bumped by every reset of the learner's inputs
+  uint64_t spec_epoch_ = 0;
+  bool grad_from_prefetch_ = false;  // the last ComputeGradients took the score walk's gradients
   void EnqueueRoot(const dev::KArgs& a);
   void EnqueueRound(const dev::KArgs& a);
   double RoundCollectiveBytes() const;  // device collectives of one distributed round

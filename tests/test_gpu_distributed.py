@@ -207,16 +207,26 @@ def test_device_distributed_with_efb_bundles(learner, gpu_available):
     assert _trees(res[0].value) == _trees(res[1].value)
 
 
-@pytest.mark.parametrize("learner,world,k", [("data", 2, 8), ("data", 4, 8), ("feature", 3, 8), ("voting", 2, 6),
-                                             ("voting", 4, 6)])
-def test_distributed_round_growth_equals_one_split_per_step(learner, world, k, gpu_available, monkeypatch, tmp_path):
+@pytest.mark.parametrize("learner,world,k,mode", [("data", 2, 8, ""), ("data", 4, 8, ""), ("feature", 3, 8, ""),
+                                                  ("voting", 2, 6, ""), ("voting", 4, 6, ""),
+                                                  ("data", 2, 8, "bynode"), ("data", 3, 8, "bynode"),
+                                                  ("feature", 2, 8, "bynode"), ("data", 2, 8, "cegb"),
+                                                  ("data", 3, 8, "cegb"), ("feature", 3, 8, "cegb")])
+def test_distributed_round_growth_equals_one_split_per_step(learner, world, k, mode, gpu_available, monkeypatch,
+                                                            tmp_path):
     """Distributed round growth (round_kernels.hip: up to k leaves expanded per round, the
     histograms reduce-scattered and the per-feature records gathered once per round instead of
     once per split; voting: one proposal allgather and one elected-histogram all-reduce per
     round for all of the round's children) grows the same trees as one split per step
     (LGBM_AMD_ROUND_K=1), on every rank; the iteration log shows the rounds (fewer than the
-    splits)."""
+    splits).  Per-node sampling and CEGB coupled penalties too: their folds are deferred to the
+    plan's replay, which every rank runs on the gathered per-feature results and flags."""
     extra = {"top_k": 4} if learner == "voting" else {}
+    if mode == "bynode":
+        extra["feature_fraction_bynode"] = 0.6
+    elif mode == "cegb":
+        extra.update(cegb_penalty_split=0.5, cegb_penalty_feature_coupled=[5, 1, 3, 0, 2, 1, 4, 0, 1, 2],
+                     cegb_tradeoff=0.8)
     monkeypatch.setenv("LGBM_AMD_ROUND_K", "1")
     _, _, _, base = _run(learner, world, rounds=6, **extra)
     monkeypatch.setenv("LGBM_AMD_ROUND_K", str(k))

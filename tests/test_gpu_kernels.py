@@ -25,6 +25,12 @@ from lightgbmv1_amd import _native as nat
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _last_tree_on_device(monkeypatch):
+    """the device-state hooks read the last tree: no next tree launched early (LGBM_AMD_SPECULATE)"""
+    monkeypatch.setenv("LGBM_AMD_SPECULATE", "0")
+
+
 def _data(n, seed=5, f=10):
     rng = np.random.RandomState(seed)
     X = rng.randn(n, f)

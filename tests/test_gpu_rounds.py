@@ -159,6 +159,7 @@ def test_round_growth_self_check(monkeypatch, gpu_available):
     (pending expansions: the leaf's histogram is the sum of its children's slots)."""
     from lightgbmv1_amd import _native as nat
     monkeypatch.setenv("LGBM_AMD_ROUND_K", "8")
+    monkeypatch.setenv("LGBM_AMD_SPECULATE", "0")  # (the device must hold the last tree, not the next)
     X, y = _data(seed=5)
     p = {"objective": "binary", "verbose": -1, "device_type": "gpu", "num_leaves": 63, "max_bin": 63, "seed": 3}
     bst = lgb.train(p, lgb.Dataset(X, y, params=p), 3, keep_training_booster=True)
@@ -290,3 +291,65 @@ def test_extra_trees_rounds_equal_one_split_per_step(params, monkeypatch, tmp_pa
     steps, _ = _model(monkeypatch, tmp_path, 1, X, y, dict(p), rounds=12, tag="xt_steps")
     assert rounds == steps
 
+
+
+def _growth_stats(bst):
+    import ctypes
+    from lightgbmv1_amd import _native as nat
+    out = (ctypes.c_double * 7)()
+    nat.call("LGBM_AMD_BoosterGrowthStats", bst.handle, out, ctypes.c_int(7))
+    return list(out)
+
+
+@pytest.mark.parametrize("case", ["plain", "feature_fraction", "valid_early_stop", "rollback", "reset_lr",
+                                  "regression_l1", "bagging"])
+def test_speculative_next_tree_equals_sequential(case, monkeypatch, gpu_available):
+    """The next tree launched when a tree's last plan is seen (before the host returns through
+    GBDT; LGBM_AMD_SPECULATE=1, opt-in) grows the model of launching it when GBDT asks for it,
+    bit for bit: with a per-tree feature sample drawn at launch, with validation and early
+    stopping between iterations, after a rollback or a learning-rate reset (the launched tree is
+    drained and regrown from the same sample), and where GBDT forbids it (leaf renewal,
+    bagging).  The growth counters show which trees were launched early."""
+    X, y = _data(n=60000, seed=21)
+    Xv, yv = _data(n=8000, seed=22)
+    params = {"objective": "binary", "verbose": -1, "device_type": "gpu", "seed": 5, "num_leaves": 31,
+              "max_bin": 63, "learning_rate": 0.1}
+    if case == "feature_fraction":
+        params["feature_fraction"] = 0.7
+    if case == "regression_l1":
+        params["objective"] = "regression_l1"
+    if case == "bagging":
+        params.update(bagging_fraction=0.7, bagging_freq=1)
+
+    def run(spec):
+        monkeypatch.setenv("LGBM_AMD_SPECULATE", "1" if spec else "0")
+        ds = lgb.Dataset(X, y, params=params, free_raw_data=False)
+        if case == "valid_early_stop":
+            dv = lgb.Dataset(Xv, yv, reference=ds)
+            bst = lgb.train(dict(params, metric="auc"), ds, 40, valid_sets=[dv], early_stopping_rounds=3,
+                            verbose_eval=False, keep_training_booster=True)
+        elif case in ("rollback", "reset_lr"):
+            bst = lgb.Booster(params, ds)
+            for _ in range(4):
+                bst.update()
+            if case == "rollback":
+                bst.rollback_one_iter()
+            else:
+                bst.reset_parameter({"learning_rate": 0.05})
+            for _ in range(4):
+                bst.update()
+        else:
+            bst = lgb.train(params, ds, 12, keep_training_booster=True)
+        stats = _growth_stats(bst)
+        text = bst.model_to_string()
+        del bst
+        return text, stats
+
+    seq, st0 = run(False)
+    spec, st1 = run(True)
+    assert spec == seq
+    assert st0[6] == 0
+    if case in ("regression_l1", "bagging"):
+        assert st1[6] == 0  # (GBDT does not allow it)
+    else:
+        assert st1[6] >= 3, st1
