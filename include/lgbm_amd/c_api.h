@@ -243,6 +243,8 @@ LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterLastGradients(BoosterHandle handle, float*
 // [1] of them grown device-resident, [2] rounds, [3] expansions, [4] splits, [5] bytes moved by
 // device collectives (no synchronisation: cheap inside a timed loop)
 LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterGrowthStats(BoosterHandle handle, double* out, int n);
+// free / total bytes of the current HIP device (hipMemGetInfo)
+LIGHTGBM_C_EXPORT int LGBM_AMD_DeviceMemInfo(int64_t* free_bytes, int64_t* total_bytes);
 LIGHTGBM_C_EXPORT int LGBM_AMD_BoosterDeviceGradients(BoosterHandle handle, float* grad, float* hess,
                                                       double* scales);
 // JSON report of the leaves' device best splits checked against the CPU split finder

@@ -4,6 +4,7 @@
 // Errors are reported as return code -1 with the message in LGBM_GetLastError().
 #include "lgbm_amd/c_api.h"
 
+#include <hip/hip_runtime_api.h>
 #include <omp.h>
 
 #include <cmath>
@@ -1446,6 +1447,19 @@ int LGBM_AMD_BoosterLastGradients(BoosterHandle handle, float* grad, float* hess
   *n = static_cast<int64_t>(g.size());
   if (grad != nullptr) std::memcpy(grad, g.data(), sizeof(float) * g.size());
   if (hess != nullptr) std::memcpy(hess, h.data(), sizeof(float) * h.size());
+  API_END();
+}
+
+// free / total bytes of the calling thread's current HIP device
+int LGBM_AMD_DeviceMemInfo(int64_t* free_bytes, int64_t* total_bytes) {
+  API_BEGIN();
+  size_t f = 0, t = 0;
+  if (hipMemGetInfo(&f, &t) != hipSuccess) {
+    (void)hipGetLastError();
+    Log::Fatal("hipMemGetInfo failed");
+  }
+  *free_bytes = static_cast<int64_t>(f);
+  *total_bytes = static_cast<int64_t>(t);
   API_END();
 }
 

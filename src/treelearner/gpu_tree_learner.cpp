@@ -1109,7 +1109,9 @@ void GPUTreeLearner::EnqueueTree(const dev::KArgs& a) {
       HIPCHECK(hipMemsetAsync(d_scratch_ + static_cast<size_t>((s + 1) & 1) * a.scratch_stride, 0, stride_bytes,
                               stream_));
     }
-    dev::SplitStep(a, stream_, s < a.p.direct_from_split || data_parallel_);
+    // (a reduce kernel for every step of the learners with global counts -- data- and
+    // voting-parallel: DirectPartials never lets their split scans sum the partials)
+    dev::SplitStep(a, stream_, s < a.p.direct_from_split || a.p.data_parallel != 0);
     if (a.cegb_lazy != nullptr) dev::CegbStep(a, stream_);
     if (a.bynode_rng != nullptr) dev::ByNodeStep(a, stream_);
     ReduceScatterStep(s + 1);

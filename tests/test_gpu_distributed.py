@@ -245,6 +245,26 @@ def test_distributed_round_growth_equals_one_split_per_step(learner, world, k, m
     assert sum(row["rounds"][0] for row in rows) < sum(row["leaves"][0] - 1 for row in rows)
 
 
+@pytest.mark.parametrize("learner", ["voting", "data"])
+def test_one_split_per_step_past_direct_partials(learner, gpu_available, monkeypatch):
+    """Trees of more than 100 splits grown one split per step: from split direct_from_split
+    (100) the serial learner's split scans sum the row blocks' partial histograms themselves and
+    no reduce kernel is launched; the learners with global counts (data- and voting-parallel)
+    never do, so their steps keep the reduce kernel.  Round 6 found voting's steps without it
+    past split 100 (stale histograms: held-out AUC 0.68 instead of 0.81 on Criteo-shaped data,
+    tools/diag_voting.py).  The one-split-per-step model equals round growth's, on every rank."""
+    extra = {"num_leaves": 160, "min_data_in_leaf": 5}
+    if learner == "voting":
+        extra["top_k"] = 4
+    monkeypatch.setenv("LGBM_AMD_ROUND_K", "1")
+    _, _, _, steps = _run(learner, 2, rounds=3, **extra)
+    monkeypatch.delenv("LGBM_AMD_ROUND_K")
+    _, _, _, rounds = _run(learner, 2, rounds=3, **extra)
+    for (ms, _), (mr, _) in zip(steps, rounds):
+        assert _trees(ms) == _trees(mr)
+    assert max(int(x["num_leaves"]) for x in _tree_fields(steps[0][0])) > 101
+
+
 @pytest.mark.parametrize("comm", ["peer", "host"])
 def test_device_collective_fault_mid_tree_raises_on_every_rank(comm, gpu_available):
     """A rank fails inside a device collective in the middle of a data-parallel tree (fault
