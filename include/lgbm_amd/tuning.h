@@ -83,6 +83,7 @@ constexpr int kQueryMetricDeviceMaxDocs = 16384;
   X(RoundGrid, "LGBM_AMD_ROUND_GRID", "n: round split workgroups")                                             \
   X(RoundGr, "LGBM_AMD_ROUND_GR", "n: rows gathered per pass in the round split kernel")                      \
   X(RoundNeedDiv, "LGBM_AMD_ROUND_NEED_DIV", "n: picks per round capped by remaining splits / n")              \
+  X(RoundPredict, "LGBM_AMD_ROUND_PREDICT", "0/1: next round's picks by the step walk / bottleneck keys")     \
   X(SplitGrid, "LGBM_AMD_SPLIT_GRID", "n: one-split-per-step split workgroups")                                \
   X(BlkMinRows, "LGBM_AMD_BLK_MIN_ROWS", "n: smallest row block")                                              \
   X(DirectFromSplit, "LGBM_AMD_DIRECT_FROM_SPLIT", "n: split steps whose partials the split scan sums itself")  \

@@ -157,12 +157,13 @@ struct FeatureBest {
   double gain;
   double lg, lh, rg, rh, lo, ro;
   int32_t feature, real_feature, thr, default_left, lc, rc, mono;
-  int32_t ncat;  // categorical: categories in the left set (KArgs::feat_cat); 0: numerical
+  int16_t ncat;  // categorical: categories in the left set (KArgs::feat_cat, <= kFindMaxCatBins); 0: numerical
   // the scan's "feature had a valid split" flag it wrote into KArgs::splittable (-1: none
   // written) -- gathered with the record, so distributed rounds complete every rank's rows
-  int32_t flag;
-  int32_t pad;
+  int8_t flag;
+  int8_t pad;
 };
+static_assert(sizeof(FeatureBest) == 88, "FeatureBest: eleven 8-byte words");
 
 // voting-parallel: one rank's proposal for a leaf (reference LightSplitInfo: the local best
 // split's gain and its local row count)

@@ -196,6 +196,7 @@ struct KArgs {
   int32_t round_nodes{};  // node capacity (splittable rows of a tree)
   int32_t round_emax{};   // expansions of a tree, upper bound (histogram slots - 1, (round_nodes - 1) / 2)
   int32_t round_need_div{};  // > 0: at most max(1, splits still possible / round_need_div) picks per round (A/B: off)
+  int32_t round_predict{};   // the next round's picks: 1 bottleneck order keys (PredictBottleneck), 0 the step-by-step walk
   int32_t round_grid{};  // workgroups of a round's split kernel (row blocks: the round's rows / round_grid)
   int32_t round_gr{};    // independent row gathers per thread in its histogram phase (2, 4, 8)
   int32_t round_fused{};  // 1: partition + histograms in one kernel (k_round_split), 0: two (k_round_part, k_round_hist)

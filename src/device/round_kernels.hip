@@ -706,12 +706,14 @@ __global__ __launch_bounds__(256) void k_round_reduce(KArgs a) {
 // leaves / nodes) and the prediction's copies of the leaf tables (+ levels below the leaf)
 struct PlanTables {
   double *ng, *tg, *sg;
-  int *nrf, *nch, *nfi, *trf, *tnode, *acc, *accn, *srf, *snode, *svd;
+  unsigned long long* qkey;  // the bottleneck prediction's region: order keys and nodes (PredictBottleneck)
+  int *nrf, *nch, *nfi, *trf, *tnode, *acc, *accn, *srf, *snode, *svd, *qn;
   __device__ PlanTables(unsigned char* lds, int NN, int L) {
     ng = reinterpret_cast<double*>(lds);
     tg = ng + NN;
     sg = tg + L;
-    nrf = reinterpret_cast<int*>(sg + L);
+    qkey = reinterpret_cast<unsigned long long*>(sg + L);
+    nrf = reinterpret_cast<int*>(qkey + NN);
     nch = nrf + NN;
     nfi = nch + NN;  // the node's best split feature (inner index; -1: none)
     trf = nfi + NN;
@@ -721,6 +723,7 @@ struct PlanTables {
     srf = accn + L;
     snode = srf + L;
     svd = snode + L;
+    qn = svd + L;
   }
 };
 
@@ -1063,8 +1066,10 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
         splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, cl.depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc,
                                                     sh.sc2, kNoRandThr);
       }
-      if (tid == 0 && !vote_global) flags[f] = splittable ? 1 : 0;  // (voting: the local scan's flags)
-      if (!vote_global) o.flag = splittable ? 1 : 0;
+      if (tid == 0 && !vote_global) {  // (voting: the local scan's flags; categorical: thread 0 decides)
+        flags[f] = splittable ? 1 : 0;
+        o.flag = splittable ? 1 : 0;
+      }
       // CEGB (GPUTreeLearner::CegbRounds: no refunds in a round tree), before the monotone
       // penalty as SerialTreeLearner::ComputeBestSplitForFeature
       if (a.p.cegb && !a.round_cegb) {  // (KArgs::round_cegb: the replay subtracts them)
@@ -1737,11 +1742,12 @@ __device__ bool DeferAccept(const KArgs& a, int s, int w, int n, int c, int* dra
 // path.  x keeps the replayed leaves for the prediction.
 template <bool XT>
 __device__ int ReplayRegs(const KArgs& a, int L, int s0, double* ng, int* nrf, const int* nch, int* nfi, int* tnode,
-                          int* acc, int* accn, RegLeaf* xp, int* done_out, int* draw, int* xcnt) {
+                          int* acc, int* accn, RegLeaf* xp, int* done_out, int* draw, int* xcnt, int* blocker) {
   const int lane = threadIdx.x & 63;
   RegLeaf& x = *xp;
   RegLoad(&x, lane <= s0 ? tnode[lane] : -1, ng, nrf, nch);
   int s = s0, done = 0;
+  *blocker = -1;
   for (;;) {
     if (s >= L - 1) {
       done = 1;
@@ -1753,7 +1759,10 @@ __device__ int ReplayRegs(const KArgs& a, int L, int s0, double* ng, int* nrf, c
       break;
     }
     const int c = ReadLane(x.ch, w);
-    if (c < 0) break;
+    if (c < 0) {
+      *blocker = ReadLane(x.node, w);
+      break;
+    }
     const int nl = s + 1;
     if (lane == 0) {
       acc[s - s0] = w;
@@ -1807,6 +1816,109 @@ __device__ int PredictRegs(const KArgs& a, int L, int s, int used, int kround, c
   }
   *done_io = done;
   return n;
+}
+
+// The next round's picks from order keys instead of the step walk (KArgs::round_predict; wave
+// 0 after the replay, any num_leaves; the blocker is the first pick).  Best-first order pops a
+// node only after its ancestors below the current leaf, so the known nodes come out by
+// decreasing bottleneck m(v) -- the least gain on the path from the leaf to v: the frontier
+// falls below m(v) only after v is reached -- and, within one bottleneck, by the least gain
+// below it (m2), ancestors first.  Keys (m, m2, -depth) of float-rounded gains: ties and deeper
+// bottleneck levels order approximately, which only changes the nodes expanded ahead, never
+// the tree (the replay is exact).  A pick's pops before it are the region's nodes with gain > 0
+// on the path and a larger key; picks stop at kmax or when the tree's remaining splits are used
+// up, as the walk's.  Cost: one pass per level of the known region and two wave passes per pick
+// instead of one argmax step per pop (the walk's 3 -> 18 us per plan late in a 63-leaf tree).
+__device__ int PredictBottleneck(const KArgs& a, int L, int s, int used, int kround, const double* ng, const int* nch,
+                                 const int* tnode, int blocker, unsigned long long* qkey, int* qn, int* s_pick,
+                                 int* done_io) {
+  const int lane = threadIdx.x & 63;
+  int done = *done_io, n = 0;
+  const int need = L - 1 - s;
+  int kmax = 0;
+  if (!done) {
+    kmax = min(kround, a.round_need_div > 0 ? max(1, need / a.round_need_div) : need);
+    kmax = min(kmax, a.round_emax - used - (need - 1));
+    kmax = max(kmax, min(1, a.round_emax - used));
+    if (kmax <= 0 || blocker < 0) done = 1;  // (unreachable: the budget keeps room for the blocker)
+  }
+  if (!done) {
+    const int vmax = (a.round_bynode || a.round_xt || a.round_cegb) ? 0 : min(a.round_vmax, 14);
+    constexpr uint32_t kPos = 0x80000000u;   // GainKey32(0.0): keys above are gains > 0
+    constexpr uint32_t kNone = 0xfffffff0u;  // m2 before a gain below the bottleneck (low 4 bits: 15 - depth)
+    for (int l = lane; l <= s; l += kWave) {  // the region's first level: the leaves' nodes
+      const int nd = tnode[l];
+      qn[l] = nd;
+      qkey[l] = (static_cast<unsigned long long>(GainKey32(ng[nd])) << 32) | kNone | 15u;
+    }
+    WaveLdsSync();
+    // the region level by level: an expanded node with m > 0 appends its children
+    int head = 0, tail = s + 1;
+    while (head < tail) {
+      const int i = head + lane, t0 = tail;
+      unsigned long long k = 0;
+      int c = -1;
+      if (i < t0) {
+        k = qkey[i];
+        c = nch[qn[i]];
+      }
+      const uint32_t km = static_cast<uint32_t>(k >> 32);
+      const bool grow = i < t0 && c >= 0 && km > kPos;
+      const unsigned long long bm = __ballot(grow);
+      if (grow) {
+        const int q = t0 + 2 * __popcll(bm & ((1ull << lane) - 1));
+        const uint32_t km2 = static_cast<uint32_t>(k) & kNone;
+        const uint32_t d = min(16u - (static_cast<uint32_t>(k) & 15u), 15u);  // the children's depth
+        for (int j = 0; j < 2; ++j) {
+          const uint32_t kc = GainKey32(ng[c + j]);
+          const uint32_t m1 = kc <= km ? kc : km;
+          const uint32_t m2 = kc <= km ? kNone : min(km2, kc & kNone);
+          qn[q + j] = c + j;
+          qkey[q + j] = (static_cast<unsigned long long>(m1) << 32) | m2 | (15u - d);
+        }
+      }
+      tail = t0 + 2 * __popcll(bm);
+      head = min(head + kWave, t0);
+      WaveLdsSync();
+    }
+    const int R = tail;
+    if (lane == 0) s_pick[0] = blocker;
+    n = 1;
+    for (; n < kmax; ++n) {
+      // the best candidate left: unexpanded, within vmax levels, m > 0, not picked
+      unsigned long long bk = 0;
+      int bi = -1;
+      for (int i = lane; i < R; i += kWave) {
+        const int nd = qn[i];
+        const unsigned long long k = qkey[i];
+        if (nd < 0 || nd == blocker || static_cast<uint32_t>(k >> 32) <= kPos) continue;
+        if (15 - static_cast<int>(k & 15u) > vmax || nch[nd] >= 0) continue;
+        if (k > bk) {
+          bk = k;
+          bi = i;
+        }
+      }
+      const unsigned long long gm = WaveMaxDpp(bk);
+      if (gm == 0) break;
+      // its pops before it: the region's nodes with m > 0 and a larger key
+      int cnt = 0;
+      for (int i = lane; i < R; i += kWave) {
+        const unsigned long long k = qkey[i];
+        cnt += (static_cast<uint32_t>(k >> 32) > kPos && k > gm) ? 1 : 0;
+      }
+      if (WaveSum(cnt) >= need) break;
+      const unsigned long long own = __ballot(bi >= 0 && bk == gm);
+      const int idx = ReadLane(bi, static_cast<int>(__builtin_ctzll(own)));
+      if (lane == 0) {
+        const int nd = qn[idx];
+        s_pick[n] = nd;
+        qn[idx] = -1 - nd;
+      }
+      WaveLdsSync();
+    }
+  }
+  *done_io = done;
+  return done ? 0 : n;
 }
 
 // One workgroup.  ROOT: the root's best split from its per-feature results (FindRoot), then
@@ -2014,7 +2126,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   // replay of the sequential order by wave 0: the argmax leaf is split while its node is
   // expanded; its children nodes become leaves w and s + 1
   RegLeaf x;
-  int done_w = 0;
+  int done_w = 0, blocker_w = -1;
   int s_w = s0;
   int draw = rd->bynode_next;  // (per-node sampling: the next draw; wave 0 advances it)
   // (extra_trees: the draws counted so far -- the root scan's row 0 for the first plan, then
@@ -2025,7 +2137,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     for (int f = lane; f < NF; f += kWave) xcnt[f] = a.xt_cum[(ROOT ? 0 : NF) + f];
   }
   if (tid < kWave && L <= kWave) {
-    s_w = ReplayRegs<XT>(a, L, s0, ng, nrf, nch, nfi, tnode, acc, accn, &x, &done_w, &draw, xcnt);
+    s_w = ReplayRegs<XT>(a, L, s0, ng, nrf, nch, nfi, tnode, acc, accn, &x, &done_w, &draw, xcnt, &blocker_w);
   } else if (tid < kWave) {
     for (;;) {
       if (s_w >= L - 1) {
@@ -2038,7 +2150,10 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
         break;
       }
       const int n = tnode[w], c = nch[n];
-      if (c < 0) break;
+      if (c < 0) {
+        blocker_w = n;
+        break;
+      }
       bool refunded = false;
       if (a.round_bynode || a.round_cegb || (XT && a.round_xt)) {
         refunded = DeferAccept<XT>(a, s_w, w, n, c, &draw, ng, nrf, nfi, xcnt, -1, tnode);
@@ -2122,7 +2237,9 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
   };
   if (tid < kWave) {
     int n = 0;
-    if (L <= kWave) {
+    if (a.round_predict) {
+      n = PredictBottleneck(a, L, s1, (nn - 1) / 2, kround, ng, nch, tnode, blocker_w, T.qkey, T.qn, s_pick, &done_w);
+    } else if (L <= kWave) {
       n = PredictRegs(a, L, s1, (nn - 1) / 2, kround, ng, nrf, nch, s_pick, &x, &done_w);
     } else if (!done_w) {
       // the sequential order predicted past the blocker from the splits known so far (copies of
@@ -2412,7 +2529,7 @@ void LaunchRoundPlan(const KArgs& a, hipStream_t s) {
 
 size_t RoundPlanLds(int num_leaves, int nodes) {
   const size_t L = static_cast<size_t>(num_leaves), N = static_cast<size_t>(nodes);
-  return (N + 2 * L) * sizeof(double) + N * sizeof(int) * 3 + L * sizeof(int) * 7;
+  return (2 * N + 2 * L) * sizeof(double) + N * sizeof(int) * 4 + L * sizeof(int) * 7;
 }
 
 namespace {

@@ -496,8 +496,11 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
       splittable = FindNumericalBlock<SIMPLE, NT>(F, hv, L, p, depth, a.p.monotone_penalty, &o, &sh.sc, &sh.ssc, sh.sc2,
                                               xt_thr);
     }
-    if (tid == 0 && !vote_global && !rescan) flags[f] = splittable ? 1 : 0;  // (the local scan's flags stay)
-    if (!vote_global && !rescan) o.flag = splittable ? 1 : 0;
+    // (the local scan's flags stay; thread 0's: the categorical scan decides on thread 0 only)
+    if (tid == 0 && !vote_global && !rescan) {
+      flags[f] = splittable ? 1 : 0;
+      o.flag = splittable ? 1 : 0;
+    }
     // SerialTreeLearner::EvalFeature order: the CEGB cost (the raw candidate remembered for the
     // coupled-penalty refund), then the monotone depth penalty
     if (a.p.cegb && tid == 0) {

@@ -680,6 +680,8 @@ void GPUTreeLearner::UploadData() {
   if (const char* e = tuning::Get(tuning::Knob::RoundGr)) a.round_gr = std::atoi(e);
   a.round_need_div = 0;
   if (const char* e = tuning::Get(tuning::Knob::RoundNeedDiv)) a.round_need_div = std::max(0, std::atoi(e));
+  a.round_predict = 1;
+  if (const char* e = tuning::Get(tuning::Knob::RoundPredict)) a.round_predict = e[0] == '0' ? 0 : 1;
   AllocRoundState();
   UploadInteractionMasks();
   AllocSplittable();
