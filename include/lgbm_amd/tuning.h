@@ -6,6 +6,8 @@
 #pragma once
 
 #include <cstdlib>
+#include <cstring>
+#include <type_traits>
 
 namespace lgbm_amd {
 namespace tuning {
@@ -40,6 +42,7 @@ constexpr int kQueryMetricDeviceMaxDocs = 16384;
   X(KernelProbe, "LGBM_AMD_KERNEL_PROBE", "1: time back-to-back launches of every step kernel after a tree")     \
   X(Timetag, "LGBM_AMD_TIMETAG", "1: host phase timers (common::PhaseTimer)")                                  \
   X(Roctx, "LGBM_AMD_ROCTX", "1: roctx ranges around the host phases")                                         \
+  X(PoisonArgs, "LGBM_AMD_POISON_ARGS", "1: argument structs filled with 0xA5 before their call sites set them")  \
   /* reference paths: parity tests and A/Bs */                                                                 \
   X(HostAssist, "LGBM_AMD_HOST_ASSIST", "1: host-assisted growth over device histograms")                      \
   X(DistHostAssist, "LGBM_AMD_DIST_HOST_ASSIST", "1: host-assisted per-node sampling / CEGB when distributed")  \
@@ -126,6 +129,16 @@ inline bool Off(Knob k) {
 inline int Int(Knob k, int dflt) {
   const char* e = Get(k);
   return e != nullptr ? std::atoi(e) : dflt;
+}
+
+// LGBM_AMD_POISON_ARGS=1 (tests): a device argument struct whose call site sets every field the
+// kernel reads is filled with 0xA5 bytes first, so a forgotten field reads garbage on every run
+// instead of whatever the stack held (round 5: an unset GradArgs::write_split passed on one box
+// and zeroed the gradients on another)
+template <typename T>
+inline void PoisonArgs(T* a) {
+  static_assert(std::is_trivially_copyable<T>::value, "plain argument struct");
+  if (On(Knob::PoisonArgs)) std::memset(static_cast<void*>(a), 0xA5, sizeof(T));
 }
 
 }  // namespace tuning

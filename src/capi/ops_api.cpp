@@ -21,6 +21,7 @@
 #include "lgbm_amd/config.h"
 #include "lgbm_amd/dataset.h"
 #include "lgbm_amd/log.h"
+#include "lgbm_amd/tuning.h"
 #include "lgbm_amd/metric.h"
 #include "lgbm_amd/objective.h"
 
@@ -106,6 +107,7 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpGradients(const char* params, const float* label
     }
     Scratch sc;
     dev::GradArgs g{};
+    tuning::PoisonArgs(&g);  // (every field set below)
     g.kind = static_cast<int32_t>(spec.kind);
     g.num_class = spec.kind == DeviceGradKind::MulticlassSoftmax ? obj->NumModelPerIteration() : 1;
     g.num_data = n;
@@ -194,6 +196,7 @@ LIGHTGBM_C_EXPORT int LGBMAMD_OpSampleRows(int64_t n, int32_t seed, int32_t goss
     std::vector<uint32_t> st(nb);
     for (int64_t b = 0; b < nb; ++b) st[b] = static_cast<uint32_t>(seed + static_cast<int>(b));
     dev::SampleArgs s{};
+    tuning::PoisonArgs(&s);
     s.num_data = n;
     s.num_blocks = nb;
     s.goss = goss;

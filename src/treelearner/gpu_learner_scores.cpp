@@ -505,6 +505,7 @@ bool GPUTreeLearner::ComputeGradients(const DeviceGradSpec& spec, int ntpi) {
     return true;
   }
   dev::GradArgs g{};
+  tuning::PoisonArgs(&g);  // (every field set below)
   g.kind = static_cast<int32_t>(spec.kind);
   g.num_class = spec.kind == DeviceGradKind::MulticlassSoftmax ? ntpi : 1;
   g.num_data = num_data_;
@@ -662,6 +663,7 @@ data_size_t GPUTreeLearner::DeviceSample(const DeviceSampleSpec& sp) {
   }
   if (sp.goss) MaterializeSplitGradients();  // (GOSS reads and rescales grad / hess)
   dev::SampleArgs s{};
+  tuning::PoisonArgs(&s);
   s.num_data = num_data_;
   s.num_blocks = nb;
   s.goss = sp.goss ? 1 : 0;

@@ -279,6 +279,14 @@ def test_device_bagging_matches_host_draw(gpu_available):
     assert _bag_counts("gpu", "gbdt", 6, **kw) == _bag_counts("cpu", "gbdt", 6, **kw)
 
 
+def test_device_bagging_with_poisoned_args(monkeypatch, gpu_available):
+    """The learner's gradient and bagging launches set every argument field: with the structs
+    poisoned first (LGBM_AMD_POISON_ARGS=1) the bags still equal the host draw."""
+    monkeypatch.setenv("LGBM_AMD_POISON_ARGS", "1")
+    kw = dict(bagging_fraction=0.6, bagging_freq=2, bagging_seed=5)
+    assert _bag_counts("gpu", "gbdt", 6, **kw) == _bag_counts("cpu", "gbdt", 6, **kw)
+
+
 def test_device_balanced_bagging_matches_host_draw(gpu_available):
     kw = dict(pos_bagging_fraction=0.5, neg_bagging_fraction=0.8, bagging_freq=1)
     assert _bag_counts("gpu", "gbdt", 4, **kw) == _bag_counts("cpu", "gbdt", 4, **kw)

@@ -92,6 +92,28 @@ def test_gradients_match_torch(obj, kind, params, weighted, gpu_available):
     np.testing.assert_allclose(h.cpu().double().numpy(), rh.float().double().numpy(), rtol=2e-6, atol=1e-6)
 
 
+def test_gradients_and_bagging_with_poisoned_args(monkeypatch, gpu_available):
+    """LGBM_AMD_POISON_ARGS=1 fills the argument structs with 0xA5 bytes before their call sites
+    set them: a field the call site forgets reads garbage on every run (round 5's unset
+    GradArgs::write_split zeroed the gradients on one box only)."""
+    from lightgbmv1_amd import ops
+    monkeypatch.setenv("LGBM_AMD_POISON_ARGS", "1")
+    for obj, kind, params in GRAD_CASES:
+        for weighted in (False, True):
+            s, y, w = _data(kind=kind)
+            w = w if weighted else None
+            g, h = ops.gradients(dict(params, objective=obj, verbose=-1), torch.tensor(s, device="cuda"), y, w)
+            rg, rh = _ref_grad(obj, s, y, w, params)
+            np.testing.assert_allclose(g.cpu().double().numpy(), rg.float().double().numpy(), rtol=2e-6, atol=1e-6,
+                                       err_msg=obj)
+            np.testing.assert_allclose(h.cpu().double().numpy(), rh.float().double().numpy(), rtol=2e-6, atol=1e-6,
+                                       err_msg=obj)
+    bag, oob = ops.sample_rows(10 * 1024 + 77, fraction=0.5, seed=3)
+    rb, ro = _ref_bag(10 * 1024 + 77, 0.5, 3)
+    np.testing.assert_array_equal(bag.cpu().numpy(), rb)
+    np.testing.assert_array_equal(oob.cpu().numpy(), ro)
+
+
 def test_multiclass_softmax_gradients_match_torch(gpu_available):
     from lightgbmv1_amd import ops
     K = 4
