@@ -31,7 +31,7 @@ __device__ void ByNodeRow(const KArgs& a, IcMask icm, int8_t* row, Random* rng) 
     int n = 0;
     for (int i = 0; i < a.bynode_pool_n; ++i) {
       const int f = a.bynode_pool[i];
-      if ((a.feat_icmask[f] & icm) != 0) pool[n++] = f;
+      if (IcAny(a.feat_icmask[f] & icm)) pool[n++] = f;
     }
     const int k = min(a.bynode_cnt, n);
     if (k > 0 && k <= n) {

@@ -77,10 +77,27 @@ struct Params {
 };
 
 // per-leaf state
-// interaction-constraint sets of a leaf / feature (bit k: constraint k; up to 64 constraints)
-using IcMask = uint64_t;
-constexpr IcMask kIcAll = ~IcMask{0};
-constexpr int kMaxIcConstraints = 64;
+// interaction-constraint sets of a leaf / feature: bit k of the words is constraint k (up to
+// kMaxIcConstraints; more run host-assisted).  constexpr helpers (host and device)
+constexpr int kIcWords = 4;
+constexpr int kMaxIcConstraints = 64 * kIcWords;
+struct IcMask {
+  uint64_t w[kIcWords];
+  constexpr IcMask operator&(const IcMask& o) const {
+    IcMask r{};
+    for (int i = 0; i < kIcWords; ++i) r.w[i] = w[i] & o.w[i];
+    return r;
+  }
+  constexpr void Set(int k) { w[k >> 6] |= uint64_t{1} << (k & 63); }
+};
+// any constraint in common (a leaf may split on a feature iff IcAny(leaf & feature))
+constexpr bool IcAny(const IcMask& m) {
+  uint64_t x = 0;
+  for (int i = 0; i < kIcWords; ++i) x |= m.w[i];
+  return x != 0;
+}
+static_assert(kIcWords == 4, "kIcAll lists kIcWords words");
+constexpr IcMask kIcAll = {{~uint64_t{0}, ~uint64_t{0}, ~uint64_t{0}, ~uint64_t{0}}};
 
 struct Leaf {
   int32_t begin;         // local index range in the partition array

@@ -121,7 +121,7 @@ struct KArgs {
   int8_t* parent_flags{};      // [num_features]
   const int32_t* cat_list{};   // [Params::has_cat] the categorical features
   // interaction constraints (<= 32): bit k set iff constraint k holds the feature, or null.
-  // A leaf may split on f iff (Leaf::icmask & feat_icmask[f]) != 0 (ColSampler::GetByNode)
+  // A leaf may split on f iff IcAny(Leaf::icmask & feat_icmask[f]) (ColSampler::GetByNode)
   const IcMask* feat_icmask{};  // [num_features]
   // extra_trees: each feature's generator state at the tree's start (FeatureMeta::rand) and the
   // running count of its draws, one row per split step (row 0: the root scan, row s + 1: after

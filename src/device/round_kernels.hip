@@ -930,7 +930,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
     // but keeps its histogram (descendants subtract it); voting's local scan evaluates it (its
     // features are the tree's sample and the parent's flags only)
     bool used = true;
-    if (a.feat_icmask != nullptr && !vote_local && (cl.icmask & a.feat_icmask[f]) == 0) used = false;
+    if (a.feat_icmask != nullptr && !vote_local && !IcAny(cl.icmask & a.feat_icmask[f])) used = false;
     LeafCtx L;
     L.sg = cl.sum_g;
     L.sh = cl.sum_h + 2 * kEpsilon;

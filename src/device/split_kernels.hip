@@ -32,7 +32,7 @@ namespace dev {
 __device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, int mi, IcMask icmask, bool gate) {
   if (!gate || F.num_bin - 2 <= 0) return 0;
   if (a.node_mask != nullptr && !a.node_mask[static_cast<size_t>(mi) * a.p.num_features + f]) return 0;
-  if (a.feat_icmask != nullptr && (icmask & a.feat_icmask[f]) == 0) return 0;
+  if (a.feat_icmask != nullptr && !IcAny(icmask & a.feat_icmask[f])) return 0;
   return 1;
 }
 
@@ -343,7 +343,7 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
   // interaction constraints: like a sampled-out feature, a disallowed one is not evaluated
   // here but keeps its histogram and its splittable flag
   // (voting's local scan evaluates it: its features are the tree's sample and the parent's flags)
-  if (a.feat_icmask != nullptr && a.p.vote_phase != 1 && ((ROOT ? kIcAll : cl.icmask) & a.feat_icmask[f]) == 0) used = 0;
+  if (a.feat_icmask != nullptr && a.p.vote_phase != 1 && !IcAny((ROOT ? kIcAll : cl.icmask) & a.feat_icmask[f])) used = 0;
   int8_t* flags = a.splittable + static_cast<size_t>(ROOT ? a.leaves[0].frow : sd.frow) * a.p.num_features;
   FeatureBest* fb_out = &a.feat_best[FeatBestIndex(a, side, f)];
   if (tree_used && !parent_ok) {

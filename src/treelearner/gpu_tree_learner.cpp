@@ -688,16 +688,16 @@ void GPUTreeLearner::UploadData() {
 }
 
 // interaction constraints as per-feature constraint bitmasks (device-resident growth
-// supports up to 64 constraints, see DecideMode); rebuilt when the config changes
+// supports up to dev::kMaxIcConstraints = 256 constraints, see DecideMode); rebuilt when the config changes
 void GPUTreeLearner::UploadInteractionMasks() {
   const auto& ic = config_->interaction_constraints_vector;
   args_.feat_icmask = nullptr;
   if (ic.empty() || ic.size() > static_cast<size_t>(dev::kMaxIcConstraints)) return;
-  std::vector<dev::IcMask> icm(std::max(1, num_features_), 0);
+  std::vector<dev::IcMask> icm(std::max(1, num_features_), dev::IcMask{});
   for (int f = 0; f < num_features_; ++f) {
     const int real = data_->RealFeatureIndex(f);
     for (size_t k = 0; k < ic.size(); ++k) {
-      if (std::find(ic[k].begin(), ic[k].end(), real) != ic[k].end()) icm[f] |= dev::IcMask{1} << k;
+      if (std::find(ic[k].begin(), ic[k].end(), real) != ic[k].end()) icm[f].Set(static_cast<int>(k));
     }
   }
   if (d_feat_icmask_ == nullptr) d_feat_icmask_ = Alloc<dev::IcMask>(icm.size());
@@ -805,7 +805,7 @@ void GPUTreeLearner::DecideMode() {
   // that scans both children of the feature in order); the distributed learners keep
   // categorical draws host-assisted
   if (config_->extra_trees && any_cat && distributed_) dm = false;
-  // interaction constraints: on the device up to 64 constraints; with per-node sampling the
+  // interaction constraints: on the device up to 256 constraints; with per-node sampling the
   // children's masks are drawn on the device after each partition (k_bynode_step; one process)
   const auto& ic = config_->interaction_constraints_vector;
   if (!ic.empty() && (ic.size() > static_cast<size_t>(dev::kMaxIcConstraints) ||

@@ -5,6 +5,8 @@ scales), the host's are fp64 sums, and the device scans evaluate thresholds with
 prefix sums, so trees are compared structurally (split features / thresholds of the
 first tree) and by metric, not bit for bit.
 """
+import json
+
 import numpy as np
 import pytest
 
@@ -523,22 +525,26 @@ def _branches(node, path=()):
     yield from _branches(node["right_child"], p)
 
 
-@pytest.mark.parametrize("wide", [False, True], ids=["3_constraints", "40_constraints"])
-def test_interaction_constraints_device_resident(gpu_available, monkeypatch, wide):
-    """Interaction constraints run in device-resident growth (per-leaf 64-bit constraint
-    bitmasks, reference col_sampler.hpp:92-126): every root-to-leaf branch uses features of one
-    constraint, and the trees equal the host-assisted learner's (same device histograms,
-    host split loop).  The wide case puts the useful constraints at bits 37-39."""
+@pytest.mark.parametrize("wide", [0, 37, 197], ids=["3_constraints", "40_constraints", "200_constraints"])
+def test_interaction_constraints_device_resident(gpu_available, monkeypatch, tmp_path, wide):
+    """Interaction constraints run in device-resident growth (per-leaf constraint bitmasks of
+    four 64-bit words, reference col_sampler.hpp:92-126): every root-to-leaf branch uses
+    features of one constraint, and the trees equal the host-assisted learner's (same device
+    histograms, host split loop).  The wide cases put the useful constraints at bits 37-39 and
+    197-199 (the fourth word) after single-feature constraints."""
     X, y = _data(30000, seed=5)
-    ic = [[0, 1, 2], [3, 5, 7], [1, 6]]
-    if wide:
-        ic = [[k % 8] for k in range(37)] + ic
+    ic = [[k % 8] for k in range(wide)] + [[0, 1, 2], [3, 5, 7], [1, 6]]
     models = {}
     for mode in ("device", "host"):
         if mode == "host":
             monkeypatch.setenv("LGBM_AMD_HOST_ASSIST", "1")
+        log = tmp_path / ("iters_%s.jsonl" % mode)
+        monkeypatch.setenv("LGBM_AMD_ITER_LOG", str(log))
         b = _train(X, y, "gpu", rounds=8, interaction_constraints=ic)
+        monkeypatch.delenv("LGBM_AMD_ITER_LOG")
         monkeypatch.delenv("LGBM_AMD_HOST_ASSIST", raising=False)
+        rows = [json.loads(line) for line in log.read_text().splitlines()]
+        assert all(r["device_resident"][0] == (mode == "device") for r in rows), (mode, rows[0])
         models[mode] = b
         for t in b.dump_model()["tree_info"]:
             for br in _branches(t["tree_structure"]):
