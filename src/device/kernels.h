@@ -172,6 +172,11 @@ struct KArgs {
   const int32_t* forced_child{};
   FeatureBest* forced_best{};
   uint32_t* forced_cat{};
+  // feature-parallel: forced_best / forced_cat are this rank's block of forced_world blocks of
+  // forced_n records, gathered after each scan; the pick takes the owner's (the only valid one)
+  int32_t forced_world{};
+  const FeatureBest* forced_all{};
+  const uint32_t* forced_cat_all{};
   // arrival sub-counters of large split-scan grids, [kFindSub] at kFindSubStride words: each on
   // a cache line of its own (atomics to one line serialise like atomics to one word)
   uint32_t* find_sub{};

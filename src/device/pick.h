@@ -151,7 +151,16 @@ struct PickLds {
   IcMask icm;
   FeatureBest ffb;  // the forced split's record and category set
   uint32_t ffcat[kMaxCatWords];
+  int forced_rank;  // feature-parallel: the rank whose forced record is valid (the feature's owner)
 };
+// the forced record of node s as rank r wrote it (KArgs::forced_world ranks, or this process)
+__device__ __forceinline__ const FeatureBest& ForcedRecord(const KArgs& a, int r, int s) {
+  return a.forced_world > 1 ? a.forced_all[static_cast<size_t>(r) * a.forced_n + s] : a.forced_best[s];
+}
+__device__ __forceinline__ const uint32_t* ForcedCat(const KArgs& a, int r, int s) {
+  return a.forced_world > 1 ? a.forced_cat_all + (static_cast<size_t>(r) * a.forced_n + s) * kMaxCatWords
+                            : a.forced_cat + static_cast<size_t>(s) * kMaxCatWords;
+}
 
 template <typename T>
 __device__ __forceinline__ void CopyWords(const T* src, T* dst, int lane, int lanes) {
@@ -368,11 +377,18 @@ __device__ __forceinline__ void PickWave(const KArgs& a, PickLds* pl) {
   // forced splits: node s, while every earlier one was valid; an invalid one ends them and
   // the normal pick above stands (reference ForceSplits' abort)
   if (s < a.forced_n && !a.st->forced_abort) {
-    const FeatureBest& fb = a.forced_best[s];
-    if (fb.feature >= 0 && fb.gain > -INFINITY && fb.lc + fb.rc > 0) {  // (an all-zero record: nobody's)
+    // (feature-parallel: only the owner of the node's feature scanned it -- the other ranks'
+    // records are the tree's reset ones)
+    int fr = -1;
+    for (int r = 0; r < max(1, a.forced_world) && fr < 0; ++r) {
+      const FeatureBest& fb = ForcedRecord(a, r, s);
+      if (fb.feature >= 0 && fb.gain > -INFINITY && fb.lc + fb.rc > 0) fr = r;  // (an all-zero record: nobody's)
+    }
+    if (fr >= 0) {
       out->forced = 1;
       out->leaf = a.forced_leaf[s];
-      pl->win_feature = fb.feature;
+      pl->win_feature = ForcedRecord(a, fr, s).feature;
+      pl->forced_rank = fr;
       out->done = 0;
     } else {
       a.st->forced_abort = 1;
@@ -702,9 +718,9 @@ __device__ __forceinline__ void PickAndRecord(const KArgs& a, Step* st, bool roo
     }
     if (pk->forced) {
       if (w == (2 % nw)) {
-        CopyWords(&a.forced_best[pk->s], &pl->ffb, lane, kWave);
-        CopyWords(reinterpret_cast<const uint32_t(*)[kMaxCatWords]>(a.forced_cat + static_cast<size_t>(pk->s) * kMaxCatWords),
-                  &pl->ffcat, lane, kWave);
+        CopyWords(&ForcedRecord(a, pl->forced_rank, pk->s), &pl->ffb, lane, kWave);
+        CopyWords(reinterpret_cast<const uint32_t(*)[kMaxCatWords]>(ForcedCat(a, pl->forced_rank, pk->s)), &pl->ffcat,
+                  lane, kWave);
       }
     } else if (!win_fresh && w == (2 % nw)) {
       CopyWords(&a.best[leaf], &pk->split, lane, kWave);

@@ -230,9 +230,19 @@ void GPUTreeLearner::GatherFeatureBests() {
   const size_t cat_bytes = 2 * static_cast<size_t>(max_owned_) * kMaxCatWords * sizeof(uint32_t);
   char* fb = reinterpret_cast<char*>(d_feat_best_);
   char* fc = reinterpret_cast<char*>(d_feat_cat_);
+  // feature-parallel forced splits: the owners' records of every forced node (KArgs::forced_all)
+  const dev::KArgs& fa = args_;
+  const size_t ff_bytes = fa.forced_world > 1 ? sizeof(dev::FeatureBest) * fa.forced_n : 0;
+  const size_t fcat_bytes = fa.forced_world > 1 ? sizeof(uint32_t) * kMaxCatWords * fa.forced_n : 0;
+  char* ff = reinterpret_cast<char*>(d_forced_best_);
+  char* ffc = reinterpret_cast<char*>(d_forced_cat_);
   if (dc != nullptr) {
     dc->Allgather(fb + fb_bytes * rank_, fb, fb_bytes, stream_);
     if (num_cat_total_ > 0) dc->Allgather(fc + cat_bytes * rank_, fc, cat_bytes, stream_);
+    if (ff_bytes > 0) {
+      dc->Allgather(ff + ff_bytes * rank_, ff, ff_bytes, stream_);
+      if (num_cat_total_ > 0) dc->Allgather(ffc + fcat_bytes * rank_, ffc, fcat_bytes, stream_);
+    }
     return;
   }
   auto host_gather = [&](char* d, size_t bytes) {
@@ -246,6 +256,10 @@ void GPUTreeLearner::GatherFeatureBests() {
   };
   host_gather(fb, fb_bytes);
   if (num_cat_total_ > 0) host_gather(fc, cat_bytes);
+  if (ff_bytes > 0) {
+    host_gather(ff, ff_bytes);
+    if (num_cat_total_ > 0) host_gather(ffc, fcat_bytes);
+  }
 }
 
 void GPUTreeLearner::AllreduceAbsMax() {

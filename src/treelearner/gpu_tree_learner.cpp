@@ -829,15 +829,16 @@ void GPUTreeLearner::DecideMode() {
   // CEGB: split and coupled feature penalties are applied by the device scans (single rank);
   // lazy penalties (per-row usage bitsets) and distributed CEGB run host-assisted
   const bool cegb = CostEffectiveGB::Enabled(*config_);
-  // forced splits: applied by the pick on one process (the static BFS schedule of the JSON
-  // tree); the feature-parallel learner runs them host-assisted (the data-parallel one rejects
-  // them, as the reference does).  Per-node sampling and CEGB split / coupled penalties run
+  // forced splits: applied by the pick (the static BFS schedule of the JSON tree); under the
+  // feature-parallel learner the owner of a forced node's feature computes its record and every
+  // rank picks it from the gathered records (the data-parallel learner rejects forced splits, as
+  // the reference does; voting keeps them host-assisted).  Per-node sampling and CEGB split / coupled penalties run
   // device-resident under the distributed learners too: every rank draws the same node samples
   // and holds the same CEGB state, the owners' scans apply them (LGBM_AMD_DIST_HOST_ASSIST=1:
   // the host-assisted fallback, for A/B)
   const char* dha = tuning::Get(tuning::Knob::DistHostAssist);
   const bool dist_fallback = distributed_ && dha != nullptr && dha[0] == '1';
-  if (has_forced_split_ && (distributed_ || !SetupForcedSplits())) dm = false;
+  if (has_forced_split_ && ((distributed_ && !ForcedGathered()) || !SetupForcedSplits())) dm = false;
   if (!has_forced_split_ && args_.forced_n > 0) SetupForcedSplits();  // (cleared)
   if ((config_->feature_fraction_bynode < 1.0 && dist_fallback) ||
       (cegb && ((!config_->cegb_penalty_feature_lazy.empty() && (distributed_ || num_features_ > 8192)) ||
@@ -1133,8 +1134,9 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   if (a.forced_n > 0) {
     // every forced record starts the tree as zero words: a node whose leaf was not scanned this
     // tree reads as invalid (no rows) instead of as the last tree's record
-    HIPCHECK(hipMemsetAsync(d_forced_best_, 0, sizeof(dev::FeatureBest) * a.forced_n, stream_));
-    HIPCHECK(hipMemsetAsync(d_forced_cat_, 0, sizeof(uint32_t) * kMaxCatWords * a.forced_n, stream_));
+    const size_t blocks = a.forced_world > 1 ? a.forced_world : 1;
+    HIPCHECK(hipMemsetAsync(d_forced_best_, 0, sizeof(dev::FeatureBest) * a.forced_n * blocks, stream_));
+    HIPCHECK(hipMemsetAsync(d_forced_cat_, 0, sizeof(uint32_t) * kMaxCatWords * a.forced_n * blocks, stream_));
   }
   if (use_bag_) {
     // the whole buffer: the copy (like the tree's graph) does not depend on the bag size
@@ -1707,14 +1709,21 @@ bool GPUTreeLearner::SetupForcedSplits() {
   blk.insert(blk.end(), child.begin(), child.end());
   d_forced_i32_ = Alloc<int32_t>(blk.size());
   HIPCHECK(hipMemcpy(d_forced_i32_, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
-  d_forced_best_ = Alloc<dev::FeatureBest>(n);
-  d_forced_cat_ = Alloc<uint32_t>(static_cast<size_t>(n) * kMaxCatWords);
+  // feature-parallel: one block of records per rank (the owner of a node's feature fills its
+  // own block; GatherFeatureBests gathers them)
+  const int blocks = ForcedGathered() ? world_ : 1;
+  d_forced_best_ = Alloc<dev::FeatureBest>(static_cast<size_t>(blocks) * n);
+  d_forced_cat_ = Alloc<uint32_t>(static_cast<size_t>(blocks) * n * kMaxCatWords);
+  const int mine = blocks > 1 ? rank_ : 0;
   args_.forced_feat = d_forced_i32_;
   args_.forced_thr = d_forced_i32_ + n;
   args_.forced_leaf = d_forced_i32_ + 2 * n;
   args_.forced_child = d_forced_i32_ + 3 * n;
-  args_.forced_best = d_forced_best_;
-  args_.forced_cat = d_forced_cat_;
+  args_.forced_best = d_forced_best_ + static_cast<size_t>(mine) * n;
+  args_.forced_cat = d_forced_cat_ + static_cast<size_t>(mine) * n * kMaxCatWords;
+  args_.forced_world = blocks > 1 ? blocks : 0;
+  args_.forced_all = d_forced_best_;
+  args_.forced_cat_all = d_forced_cat_;
   args_.forced_n = n;
   forced_ok_ = true;
   DestroyGraph();  // (the captured tree holds the kernel arguments)

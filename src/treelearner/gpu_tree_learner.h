@@ -134,6 +134,9 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   dev::DevTree StageTree(const Tree* tree);
   bool UseSparseRows(int wpr) const;
   bool SetupForcedSplits();  // KArgs::forced_*; false: the forced splits need host-assisted growth
+  // feature-parallel forced splits: each rank's records gathered after the scans (data-parallel
+  // rejects forced splits as the reference does; voting keeps them host-assisted)
+  bool ForcedGathered() const { return distributed_ && !data_parallel_ && !voting_ && world_ > 1; }
   void UploadSparseRows();
   std::vector<uint8_t> RowMajorBins(const Dataset* d, int row_words) const;
   template <typename T>

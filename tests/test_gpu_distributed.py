@@ -378,6 +378,37 @@ def test_distributed_modes_device_resident(learner, world, mode, gpu_available, 
 
 
 @pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("forced", [
+    {"feature": 0, "threshold": 0.1, "left": {"feature": 7, "threshold": -0.2, "left": {"feature": 3, "threshold": 0.5}},
+     "right": {"feature": 5, "threshold": 0.3}},
+    # an invalid node (an unknown feature) ends the forced splits early
+    {"feature": 6, "threshold": 0.0, "left": {"feature": 99, "threshold": 1.0}, "right": {"feature": 2, "threshold": 0.0}},
+], ids=["valid", "invalid_node"])
+def test_feature_parallel_forced_splits_device_resident(world, forced, gpu_available, capfd, tmp_path):
+    """Forced splits under the feature-parallel learner grow device-resident: the owner of a
+    forced node's feature computes its record in its split scan, the records are gathered with
+    the per-feature results and every rank's pick applies the owner's.  Every rank has every
+    row, so the trees equal the serial device learner's (itself equal to host-assisted growth,
+    tests/test_gpu_learner.py::test_forced_splits_on_device) and the forced root is applied."""
+    import json as _json
+    path = tmp_path / "forced.json"
+    path.write_text(_json.dumps(forced))
+    extra = {"forcedsplits_filename": str(path)}
+    capfd.readouterr()
+    X, y, _, dev = _run("feature", world, rounds=5, verbose=2, **extra)
+    log = capfd.readouterr().out
+    assert "device-resident growth" in log and "host-assisted growth" not in log
+    for md, _ in dev:
+        assert _trees(md) == _trees(dev[0][0])
+    full = lgb.Dataset(X, y, params=BASE, free_raw_data=False).construct()
+    serial = lgb.train(dict(BASE, **extra), full.subset(np.arange(N)), 5)
+    assert _trees(dev[0][0]) == _trees(serial.model_to_string())
+    if forced["feature"] == 0:  # (the valid schedule: its root is applied)
+        root = serial.dump_model()["tree_info"][0]["tree_structure"]
+        assert root["split_feature"] == forced["feature"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
 def test_voting_bynode_device_resident(world, gpu_available, capfd, monkeypatch):
     """Voting-parallel with per-node column sampling on the device: the local scans evaluate
     every feature, the global scans of the elected features apply the node's sample (drawn in
