@@ -328,6 +328,11 @@ struct ChildInfo {
   int skip;                     // neither child can be split (depth / min_data / last split)
 };
 
+// min_data_in_leaf of the rule that skips a step's scans when both children are too small
+// (Params::skip_min_data: voting's local scans hold local parameters)
+__device__ __forceinline__ int SkipMinData(const KArgs& a) {
+  return a.p.skip_min_data > 0 ? a.p.skip_min_data - 1 : a.p.sp.min_data_in_leaf;
+}
 __device__ __forceinline__ ChildInfo StepChildren(const KArgs& a, const Step* st) {
   ChildInfo c;
   const CurSplit& cs = st->cs;
@@ -335,7 +340,7 @@ __device__ __forceinline__ ChildInfo StepChildren(const KArgs& a, const Step* st
   c.total_left = st->cur_left;
   c.left_count = a.p.data_parallel ? cs.split.left_count : c.total_left;
   c.right_count = a.p.data_parallel ? cs.split.right_count : pc - c.total_left;
-  const int md = a.p.sp.min_data_in_leaf;
+  const int md = SkipMinData(a);
   c.skip = (a.p.max_depth > 0 && cs.child_depth >= a.p.max_depth) ||
            (c.right_count < 2 * md && c.left_count < 2 * md) || (cs.s + 1 >= a.p.num_leaves - 1);
   c.small_is_left = c.left_count < c.right_count;

@@ -67,6 +67,10 @@ struct Params {
   int32_t vote_phase{};
   int32_t vote_k{};  // top_k: features each rank proposes and the vote elects, per leaf
   int32_t world{};   // ranks
+  // > 0: 1 + min_data_in_leaf of the children-skip rule (StepChildren) when sp holds other
+  // parameters -- voting's local scans run with min_data_in_leaf / world, but the reference
+  // skips a step's scans by the global parameter (SerialTreeLearner::BeforeFindBestSplit)
+  int32_t skip_min_data{};
   // cost-effective gradient boosting (split and coupled feature penalties): a candidate's gain
   // loses cegb_split * rows_in_leaf + KArgs::cegb_coupled[f] while f is unused by the model
   int32_t cegb{};

@@ -38,7 +38,7 @@ namespace dev {
 namespace {
 
 #ifndef LGBM_FIND_WAVE_OCC
-#define LGBM_FIND_WAVE_OCC 4
+#define LGBM_FIND_WAVE_OCC 2  // (one-wave scans without register spills: see split_kernels.hip)
 #endif
 #ifndef LGBM_ORACLE_SEQ
 #define LGBM_ORACLE_SEQ 0  // A/B timing oracles only: 1 sequential (g, h) gathers, 2 also sequential row words
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == kWave 
   // data-parallel: the children's global counts from the split's estimates (reference
   // data_parallel_tree_learner.cpp: global leaf counts from the SplitInfo)
   const int lc = dp ? e_gl0 : tl, rc = dp ? e_gl1 : pc - tl;
-  const int md = a.p.sp.min_data_in_leaf;
+  const int md = SkipMinData(a);
   const bool skip = (a.p.max_depth > 0 && cl.depth >= a.p.max_depth) || (lc < 2 * md && rc < 2 * md);
   const bool is_hist = (lr == 0) == (e_hl != 0);
   const int slot = is_hist ? e_slot_new : e_slot_parent;

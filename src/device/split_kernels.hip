@@ -543,7 +543,11 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
 }
 
 #ifndef LGBM_FIND_WAVE_OCC
-#define LGBM_FIND_WAVE_OCC 4  // one-wave split scans: waves per SIMD the register budget allows
+// one-wave split scans: waves per SIMD the register budget allows.  2 (256 VGPRs): at 4 the
+// non-root kernels spilled 72-76 bytes per lane, and trees grown with them changed with
+// unrelated code edits (one-split-per-step categorical trees, voting ranks that disagreed)
+// while the spill-free build stayed exact -- tests/test_gpu_distributed.py voting cases
+#define LGBM_FIND_WAVE_OCC 2
 #endif
 constexpr unsigned kFindFlatMax = 128;  // split-scan grids up to this size count arrivals on one counter
 

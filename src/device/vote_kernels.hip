@@ -218,7 +218,7 @@ __device__ __forceinline__ RoundChild RoundVoteChild(const KArgs& a, const Round
   if (rd->done || j >= rd->nexp) return c;
   const ExpPlan& E = rd->e[j];
   const int lc = E.lr[0].global_count, rc = E.lr[1].global_count, depth = E.lr[lr].depth;
-  const int md = a.p.sp.min_data_in_leaf;
+  const int md = SkipMinData(a);
   c.active = !((a.p.max_depth > 0 && depth >= a.p.max_depth) || (lc < 2 * md && rc < 2 * md));
   c.global_rows = lr == 0 ? lc : rc;
   const bool is_hist = (lr == 0) == (E.hist_left != 0);

@@ -592,6 +592,7 @@ void GPUTreeLearner::UploadData() {
     }
     a.p.vote_phase = 1;
     a.p.vote_k = vote_k_;
+    a.p.skip_min_data = config_->min_data_in_leaf + 1;  // (encoded + 1: 0 is unset)
     a.p.sp = [&] {
       Config local = *config_;
       local.min_data_in_leaf /= world_;
@@ -823,8 +824,11 @@ void GPUTreeLearner::DecideMode() {
                      config_->num_leaves > dev::kMonoInterMaxLeaves)) {
     dm = false;
   }
-  // voting: extra_trees draws stay with the host voting loop (its local and global scans draw
-  // in their own order); per-node sampling runs on the device (the global scan's masks)
+  // voting: extra_trees draws stay with the host voting loop -- its local scans skip the
+  // features their parent's local scan could not split and draw from the feature generators,
+  // its global scans draw from a second generator set on the rank that owns each elected
+  // histogram (reference feature_metas_); per-node sampling runs on the device (the global
+  // scan's masks)
   if (voting_ && config_->extra_trees) dm = false;
   // CEGB: split and coupled feature penalties are applied by the device scans (single rank);
   // lazy penalties (per-row usage bitsets) and distributed CEGB run host-assisted

@@ -268,6 +268,7 @@ void VotingParallelTreeLearner<Base>::Init(const Dataset* train_data, bool is_co
   num_machines_ = Network::num_machines();
   top_k_ = std::min(this->config_->top_k, this->num_features_);
   InitLocalParams();
+  global_meta_ = this->meta_;  // (freshly seeded: Random(extra_seed + feature))
   global_count_.assign(this->config_->num_leaves, 0);
   global_small_hist_.assign(2 * this->data_->num_total_bin(), 0.0);
   global_large_hist_.assign(2 * this->data_->num_total_bin(), 0.0);
@@ -281,6 +282,7 @@ void VotingParallelTreeLearner<Base>::ResetConfig(const Config* config) {
   Base::ResetConfig(config);
   top_k_ = std::min(this->config_->top_k, this->num_features_);
   InitLocalParams();
+  global_meta_ = this->meta_;  // (both generator sets reseeded, as the reference's ResetConfig)
   global_count_.assign(this->config_->num_leaves, 0);
 }
 
@@ -453,13 +455,13 @@ void VotingParallelTreeLearner<Base>::FindBestSplits(const Tree* tree) {
       hist_t* h = global_small_hist_.data() + off;
       std::memcpy(h, out_buf_.data() + s_read[f], bytes);
       this->data_->FixHistogram(f, global_smaller_.sum_g, global_smaller_.sum_h, h);
-      this->EvalFeature(h, f, this->params_, global_smaller_, sdepth, &sb[tid]);
+      this->EvalFeature(h, f, this->params_, global_smaller_, sdepth, &sb[tid], &global_meta_[f]);
     }
     if (l_agg[f] && global_larger_.leaf >= 0 && l_node[f]) {
       hist_t* h = global_large_hist_.data() + off;
       std::memcpy(h, out_buf_.data() + l_read[f], bytes);
       this->data_->FixHistogram(f, global_larger_.sum_g, global_larger_.sum_h, h);
-      this->EvalFeature(h, f, this->params_, global_larger_, ldepth, &lb[tid]);
+      this->EvalFeature(h, f, this->params_, global_larger_, ldepth, &lb[tid], &global_meta_[f]);
     }
   }
   SplitInfo bs, bl;

@@ -86,6 +86,10 @@ class VotingParallelTreeLearner : public Base {
 
   int rank_ = 0, num_machines_ = 1, top_k_ = 20;
   SplitParams local_params_;
+  // the global scans' feature metadata: a second extra_trees generator set, seeded like meta_
+  // (reference voting_parallel_tree_learner.cpp:61-90 feature_metas_), drawn only by the rank
+  // that owns an elected histogram
+  std::vector<FeatureMeta> global_meta_;
   LeafState global_smaller_, global_larger_;
   std::vector<data_size_t> global_count_;
   std::vector<hist_t> global_small_hist_, global_large_hist_;

@@ -379,7 +379,7 @@ void SerialTreeLearner::ComputeBestSplitForFeature(int slot, int inner, const st
 }
 
 bool SerialTreeLearner::EvalFeature(hist_t* hist, int inner, const SplitParams& p, const LeafState& ls, int depth,
-                                    SplitInfo* best) {
+                                    SplitInfo* best, const FeatureMeta* meta) {
   const ConstraintRange& c = constraints_.entries[ls.leaf];
   double parent_output;
   if (ls.leaf == 0) {
@@ -394,8 +394,8 @@ bool SerialTreeLearner::EvalFeature(hist_t* hist, int inner, const SplitParams& 
   }
   SplitInfo ns;
   bool splittable = false;
-  FindBestThreshold(meta_[inner], p, config_->extra_trees, hist, ls.sum_g, ls.sum_h, ls.num_data, c, parent_output,
-                    &ns, &splittable);
+  FindBestThreshold(meta != nullptr ? *meta : meta_[inner], p, config_->extra_trees, hist, ls.sum_g, ls.sum_h,
+                    ls.num_data, c, parent_output, &ns, &splittable);
   ns.feature = data_->RealFeatureIndex(inner);
   ns.inner_feature = inner;
   if (cegb_) ns.gain -= cegb_->DeltaGain(inner, ns.feature, ls.leaf, ls.num_data, ns);

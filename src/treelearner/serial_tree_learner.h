@@ -74,7 +74,10 @@ class SerialTreeLearner : public TreeLearner {
   void ComputeBestSplitForFeature(int slot, int inner, const std::vector<int8_t>& node_used, const LeafState& ls,
                                   int depth, SplitInfo* best);
   // evaluate one feature histogram with explicit params; returns splittability
-  bool EvalFeature(hist_t* hist, int inner, const SplitParams& p, const LeafState& ls, int depth, SplitInfo* best);
+  // meta: the feature's metadata and extra_trees generator (default meta_[inner]; the voting
+  // learner's global scans pass their own generator set)
+  bool EvalFeature(hist_t* hist, int inner, const SplitParams& p, const LeafState& ls, int depth, SplitInfo* best,
+                   const FeatureMeta* meta = nullptr);
   void SplitInner(Tree* tree, int best_leaf, int* left_leaf, int* right_leaf, bool update_cnt);
   // a leaf's histogram (the leaf must hold a pool slot: BeforeFindBestSplit assigns them)
   std::vector<hist_t>& LeafHist(int leaf) { return hist_pool_[leaf_slot_[leaf]]; }
