@@ -2239,6 +2239,7 @@ __device__ void RoundPlanBody(const KArgs& a, unsigned char* plan_lds) {
     int n = 0;
     if (a.round_predict) {
       n = PredictBottleneck(a, L, s1, (nn - 1) / 2, kround, ng, nch, tnode, blocker_w, T.qkey, T.qn, s_pick, &done_w);
+      if (ktr != nullptr) ktr[24] = wall_clock64() - tprev;  // (the prediction alone)
     } else if (L <= kWave) {
       n = PredictRegs(a, L, s1, (nn - 1) / 2, kround, ng, nrf, nch, s_pick, &x, &done_w);
     } else if (!done_w) {

@@ -467,8 +467,8 @@ int GPUTreeLearner::WaitRounds(RoundLaunch* rlp) {
     for (int r = 0; r <= h_round_->rounds && r < L; ++r) {
       const long long* o = &t[static_cast<size_t>(r) * dev::kTraceSlots];
       if (o[16] == 0) continue;
-      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay=%.2f predict+records=%.2f sync=%.2f sizing+stores=%.2f us; accepted %lld planned %lld\n",
-                   r, o[25] != 0 ? (o[16] - o[25]) / 100.0 : 0.0, o[17] / 100.0, o[18] / 100.0, o[19] / 100.0,
+      std::fprintf(stderr, "plan %d: scan->plan %.2f loads=%.2f replay=%.2f predict+records=%.2f (predict %.2f) sync=%.2f sizing+stores=%.2f us; accepted %lld planned %lld\n",
+                   r, o[25] != 0 ? (o[16] - o[25]) / 100.0 : 0.0, o[17] / 100.0, o[18] / 100.0, o[19] / 100.0, o[24] / 100.0,
                    o[20] / 100.0, o[21] / 100.0, o[22], o[23]);
       if (o[26] != 0) {  // the planning workgroup's scan path, from the first scan workgroup's start
         auto us = [&](int k) { return (o[k] - o[25]) / 100.0; };
