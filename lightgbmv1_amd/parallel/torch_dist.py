@@ -128,16 +128,28 @@ def init_network(use_rccl=True, backend="gloo", timeout_s=600, device_comm=None)
             size = ctypes.c_int(0)
             _safe_call(lib.LGBM_AMD_RcclUniqueIdSize(ctypes.byref(size)))
             uid = np.zeros(size.value, dtype=np.uint8)
+            ok = True
             if rank == 0:
-                _safe_call(lib.LGBM_AMD_RcclGetUniqueId(uid.ctypes.data_as(ctypes.c_char_p)))
+                ok = lib.LGBM_AMD_RcclGetUniqueId(uid.ctypes.data_as(ctypes.c_char_p)) == 0
             t = torch.from_numpy(uid)
             dist.broadcast(t, src=0, group=group)
             uid = t.numpy()
-            _safe_call(lib.LGBM_AMD_RcclInit(ctypes.c_int(world), ctypes.c_int(rank),
-                                             ctypes.c_int(local_rank % ndev.value),
-                                             uid.ctypes.data_as(ctypes.c_char_p)))
-            _STATE["rccl"] = True
-            _STATE["device_comm"] = "rccl"
+            ok = _all_ok(dist, group, ok)
+            if ok:
+                ok = lib.LGBM_AMD_RcclInit(ctypes.c_int(world), ctypes.c_int(rank),
+                                           ctypes.c_int(local_rank % ndev.value),
+                                           uid.ctypes.data_as(ctypes.c_char_p)) == 0
+            if _all_ok(dist, group, ok):
+                _STATE["rccl"] = True
+                _STATE["device_comm"] = "rccl"
+            else:
+                # neither device communicator: the learners' collectives go through the host
+                # process group (slower, same trees)
+                if ok:
+                    lib.LGBM_AMD_DeviceCommFree()
+                if rank == 0:
+                    print("[lightgbmv1_amd] RCCL unavailable; device collectives over the host process group",
+                          flush=True)
     return rank, world, local_rank
 
 
