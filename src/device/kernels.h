@@ -128,6 +128,13 @@ struct KArgs {
   // step s; rows of steps not run stay 0), or null
   const uint32_t* xt_base{};   // [num_features]
   int32_t* xt_cum{};           // [num_leaves][num_features]
+  // voting-parallel extra_trees: the global scans draw from a second generator set, only on the
+  // rank that owns the elected histogram (reference voting_parallel_tree_learner.cpp:61-90,
+  // CopyLocalHistogram); every rank replays every owner's draws: the states of every rank's set
+  // at the tree's start ([world][num_features]) and their running counts ([num_leaves][world]
+  // [num_features], rows as xt_cum), or null.  The local scans draw from xt_base / xt_cum.
+  const uint32_t* xt_base_glob{};
+  int32_t* xt_cum_glob{};
   // voting-parallel (Params::vote_phase): this rank's root sums before the all-reduce, the
   // proposals of every rank ([world][2][vote_k], this rank's block at rank), the elected
   // features per leaf ([2][vote_k], -1 padded) and their histograms ([2][vote_k][max_feature_bins]

@@ -36,6 +36,88 @@ __device__ __forceinline__ int XtDraws(const KArgs& a, const Feature& F, int f, 
   return 1;
 }
 
+// ---- voting-parallel extra_trees (KArgs::xt_base_glob)
+// the owner of elected slot i of side (0: the smaller leaf) -- the reference's CopyLocalHistogram:
+// each rank in turn takes ceil(elected / world) histograms, alternating smaller-leaf and
+// larger-leaf slots and starting each rank with a smaller-leaf one
+__device__ int VoteOwner(const KArgs& a, bool root, int side, int i) {
+  const int k = a.p.vote_k, W = a.p.world;
+  int n0 = 0, n1 = 0;
+  for (int j = 0; j < k; ++j) {
+    n0 += a.vote_list[j] >= 0 ? 1 : 0;
+    n1 += (!root && a.vote_list[k + j] >= 0) ? 1 : 0;
+  }
+  const int total = n0 + n1, avg = (total + W - 1) / W;
+  int used = 0, si = 0, li = 0;
+  for (int m = 0; m < W; ++m) {
+    const int want = min(avg, total - used);
+    int cnt = 0;
+    while (cnt < want) {
+      if (si < n0) {
+        if (side == 0 && si == i) return m;
+        ++si;
+        ++cnt;
+      }
+      if (cnt >= want) break;
+      if (li < n1) {
+        if (side == 1 && li == i) return m;
+        ++li;
+        ++cnt;
+      }
+    }
+    used += cnt;
+  }
+  return -1;
+}
+// whether the global scan of side evaluates f (ComputeBestSplitForFeature's is_feature_used:
+// the tree's and the node's samples, the interaction constraints) -- and so draws
+__device__ bool VoteXtUsed(const KArgs& a, int f, int side, int mi_base, IcMask icm) {
+  if (!a.tree_mask[f]) return false;
+  if (a.node_mask != nullptr && !a.node_mask[static_cast<size_t>(mi_base + side) * a.p.num_features + f]) return false;
+  if (a.feat_icmask != nullptr && !IcAny(icm & a.feat_icmask[f])) return false;
+  return true;
+}
+// the draws rank r's global scans make of f this step (smaller leaf first)
+__device__ int VoteXtDraws(const KArgs& a, bool root, int r, int f, int mi_base, IcMask icm, int sides_upto) {
+  const int k = a.p.vote_k;
+  int d = 0;
+  for (int side = 0; side < sides_upto; ++side) {
+    for (int j = 0; j < k; ++j) {
+      if (a.vote_list[side * k + j] != f) continue;
+      if (VoteOwner(a, root, side, j) == r && VoteXtUsed(a, f, side, mi_base, icm)) ++d;
+      break;
+    }
+  }
+  return d;
+}
+// the step's row of global draw counts, every (rank, feature), strided over the scan's grid
+__device__ void VoteXtCountRow(const KArgs& a, bool root, int s, int mi_base, bool skip, IcMask icm) {
+  const int nf = a.p.num_features, W = a.p.world;
+  const size_t n = static_cast<size_t>(W) * nf;
+  const int32_t* prev = root ? nullptr : a.xt_cum_glob + static_cast<size_t>(s) * n;
+  int32_t* row = a.xt_cum_glob + static_cast<size_t>(root ? 0 : s + 1) * n;
+  const size_t wg = static_cast<size_t>(blockIdx.y) * gridDim.x + blockIdx.x;
+  const size_t nwg = static_cast<size_t>(gridDim.x) * gridDim.y;
+  for (size_t e = wg * blockDim.x + threadIdx.x; e < n; e += nwg * blockDim.x) {
+    const int r = static_cast<int>(e / nf), f = static_cast<int>(e % nf);
+    const int d = (!skip && a.feat[f].num_bin - 2 > 0) ? VoteXtDraws(a, root, r, f, mi_base, icm, root ? 1 : 2) : 0;
+    row[e] = (prev != nullptr ? prev[e] : 0) + d;
+  }
+}
+// the random threshold of elected slot i (side) of f: the owner's next draw, after its draw for
+// the smaller leaf's slot of f this step
+__device__ int VoteXtThreshold(const KArgs& a, const Feature& F, int f, int side, int i, bool root, int s, int mi_base,
+                               IcMask icm) {
+  const int nf = a.p.num_features, W = a.p.world;
+  if (F.num_bin - 2 <= 0 || !VoteXtUsed(a, f, side, mi_base, icm)) return 0;
+  const int r = VoteOwner(a, root, side, i);
+  if (r < 0) return 0;
+  const int before = side == 1 ? VoteXtDraws(a, root, r, f, mi_base, icm, 1) : 0;
+  const int prev = root ? 0 : a.xt_cum_glob[(static_cast<size_t>(s) * W + r) * nf + f];
+  const uint32_t x = LcgSkip(a.xt_base_glob[static_cast<size_t>(r) * nf + f], prev + before + 1);
+  return static_cast<int>((x & 0x7fffffffu) % static_cast<uint32_t>(F.num_bin - 2));
+}
+
 // GatherInfoForThreshold (reference feature_histogram.hpp; host split_finder.cpp): the split of
 // a forced node at bin `thr` from the leaf's histogram, one thread.  hv holds the raw bins;
 // the most frequent bin is rebuilt from the leaf totals first (FixHistogram).  Invalid (gain
@@ -226,13 +308,22 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     // and appends the step's count row itself
     const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * a.p.num_features + f];
     xt_r = LcgSkip(a.xt_base[f], prev + (side == 1 ? d0_in : 0) + 1) & 0x7fffffffu;
+  } else if (a.xt_base != nullptr && vote_global) {
+    // voting: the owner's draw from the global generator set (KArgs::xt_base_glob)
+    const IcMask icm = ROOT ? kIcAll : cl.icmask;
+    xt_thr = 0;
+    if (!vote_empty && !skip) xt_thr = VoteXtThreshold(a, F, f, side, blockIdx.x, ROOT, s, mi_base, icm);
+    VoteXtCountRow(a, ROOT, s, mi_base, skip != 0, icm);
   } else if (a.xt_base != nullptr) {
     const int nf = a.p.num_features;
     const int prev = ROOT ? 0 : a.xt_cum[static_cast<size_t>(s) * nf + f];
-    const bool gate = tree_used && parent_ok && !skip;
+    // (voting's local scans: the features whose parent's local scan could split, no node
+    // sample and no interaction constraints -- VotingParallelTreeLearner::FindBestSplits)
+    const bool vote_local = a.p.vote_phase == 1;
+    const bool gate = tree_used && (vote_local ? (ROOT || a.parent_flags[f] != 0) : parent_ok) && !skip;
     const IcMask icm = ROOT ? kIcAll : cl.icmask;  // both children carry the same constraints
-    const int d0 = XtDraws(a, F, f, mi_base, icm, gate);
-    const int d1 = ROOT ? 0 : XtDraws(a, F, f, mi_base + 1, icm, gate);
+    const int d0 = vote_local ? (gate && F.num_bin - 2 > 0 ? 1 : 0) : XtDraws(a, F, f, mi_base, icm, gate);
+    const int d1 = ROOT ? 0 : vote_local ? d0 : XtDraws(a, F, f, mi_base + 1, icm, gate);
     if (side == 0 && tid == 0) a.xt_cum[static_cast<size_t>(ROOT ? 0 : s + 1) * nf + f] = prev + d0 + d1;
     xt_thr = 0;  // num_bin <= 2: no draw, threshold 0 only
     if (side == 0 ? d0 : d1) {
@@ -473,8 +564,13 @@ __device__ __forceinline__ void FindBody(const KArgs& a, double* s_bins, FindSha
     }
     __syncthreads();  // the workgroup's stores become visible to all its threads
     if (!ROOT) KTrace(a, s, kTrFindLoaded);
-    if (!used) {
+    // voting extra_trees: the reference's local scans skip the features the parent's local scan
+    // could not split (at its random threshold) -- their histograms exist for the vote, they
+    // propose nothing and draw nothing (VotingParallelTreeLearner::FindBestSplits)
+    const bool vote_skip = a.p.vote_phase == 1 && a.xt_base != nullptr && !ROOT && !rescan && !a.parent_flags[f];
+    if (!used || vote_skip) {
       if (tid == 0) {
+        if (vote_skip) flags[f] = 0;
         FeatureBest none = {};
         none.gain = -INFINITY;
         none.feature = none.real_feature = -1;

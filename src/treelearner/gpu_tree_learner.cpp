@@ -370,6 +370,7 @@ void GPUTreeLearner::UploadData() {
   d_bynode_rng_ = Alloc<uint32_t>(1);
   d_xt_base_ = Alloc<uint32_t>(std::max(1, num_features_));
   d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
+  AllocVoteXt(n_leaves);
   if (d_gh_ == nullptr) d_gh_ = Alloc<dev::GH>(num_data_);
   d_idx_ = Alloc<int32_t>(num_data_);
   d_tmp_ = Alloc<int32_t>(static_cast<size_t>(num_data_) * (round_vmax_ + 1));
@@ -745,6 +746,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
   ++state_epoch_;
   const int old_leaves = config_->num_leaves;
   SerialTreeLearner::ResetConfig(config);
+  ResetVoteXt();  // (both generator sets reseeded, as the reference's ResetConfig)
   DestroyGraph();  // kernel arguments are baked into the captured graph
   args_.p.sp = params_;
   args_.p.cegb = 0;  // re-derived from the new penalties by the next DecideMode
@@ -758,6 +760,7 @@ void GPUTreeLearner::ResetConfig(const Config* config) {
     d_leaves_ = Alloc<dev::Leaf>(n_leaves);
     d_node_mask_ = Alloc<int8_t>(static_cast<size_t>(2 * n_leaves) * std::max(1, num_features_));
     d_xt_cum_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * std::max(1, num_features_));
+    AllocVoteXt(n_leaves);
     d_rec_ = Alloc<dev::SplitRecord>(std::max(1, n_leaves - 1));
     d_best_ = Alloc<DeviceSplit>(n_leaves);
     SizeRoundPools(n_leaves);
@@ -829,7 +832,7 @@ void GPUTreeLearner::DecideMode() {
   // its global scans draw from a second generator set on the rank that owns each elected
   // histogram (reference feature_metas_); per-node sampling runs on the device (the global
   // scan's masks)
-  if (voting_ && config_->extra_trees) dm = false;
+  if (voting_ && config_->extra_trees && any_cat) dm = false;
   // CEGB: split and coupled feature penalties are applied by the device scans (single rank);
   // lazy penalties (per-row usage bitsets) and distributed CEGB run host-assisted
   const bool cegb = CostEffectiveGB::Enabled(*config_);
@@ -1173,6 +1176,9 @@ void GPUTreeLearner::EnqueueRoot(const dev::KArgs& a) {
   if (a.xt_cum != nullptr) {
     HIPCHECK(hipMemsetAsync(a.xt_cum, 0, sizeof(int32_t) * config_->num_leaves * num_features_, stream_));
   }
+  if (a.xt_cum_glob != nullptr) {
+    HIPCHECK(hipMemsetAsync(a.xt_cum_glob, 0, sizeof(int32_t) * config_->num_leaves * world_ * num_features_, stream_));
+  }
   if (!(root_from_parts_ && !use_bag_)) dev::RootSum(a, stream_);  // else: set by ReduceParts
   AllreduceRoot();
   if (a.rd != nullptr && data_parallel_ && d_round_send_ != nullptr) {  // (the first round's send buffer)
@@ -1234,6 +1240,19 @@ Tree* GPUTreeLearner::TrainDeviceMode(bool speculated) {
   const bool xt = config_->extra_trees;
   a.xt_base = nullptr;
   a.xt_cum = nullptr;
+  a.xt_base_glob = nullptr;
+  a.xt_cum_glob = nullptr;
+  if (xt && voting_) {
+    // voting: every rank's global generator set at the tree's start (every rank replays every
+    // owner's draws; VoteXtAdvance catches the host states up after the tree)
+    if (xt_glob_rand_.size() != static_cast<size_t>(world_) * num_features_) ResetVoteXt();
+    h_xt_base_glob_.resize(xt_glob_rand_.size());
+    for (size_t i = 0; i < xt_glob_rand_.size(); ++i) h_xt_base_glob_[i] = xt_glob_rand_[i].state();
+    HIPCHECK(hipMemcpyAsync(d_xt_base_glob_, h_xt_base_glob_.data(), sizeof(uint32_t) * h_xt_base_glob_.size(),
+                            hipMemcpyHostToDevice, stream_));
+    a.xt_base_glob = d_xt_base_glob_;
+    a.xt_cum_glob = d_xt_cum_glob_;
+  }
   if (xt) {
     // each feature's generator state at the tree's start: the split scans derive their draws
     // from it and the step rows of xt_cum; the host generators catch up after the tree
@@ -1403,6 +1422,7 @@ Tree* GPUTreeLearner::TrainDeviceMode(bool speculated) {
       for (int k = 0; k < n; ++k) meta_[f].rand.NextInt(0, 2);
     }
   }
+  if (xt && a.xt_cum_glob != nullptr) VoteXtAdvance();
   if (a.ktrace != nullptr && !rounds) ReportKernelTrace(num_splits);
   if (const char* kp = tuning::Get(tuning::Knob::KernelProbe)) {
     if (kp[0] == '1' && !rounds) KernelFloorProbe(a);
@@ -1501,6 +1521,37 @@ void GPUTreeLearner::LaunchSpeculative() {
   root_from_parts_ = keep_parts;
   spec_live_ = true;
   spec_epoch_ = state_epoch_;
+}
+
+// voting extra_trees: the global scans' generator sets of every rank (each seeded like the
+// feature generators, Random(extra_seed + feature): reference feature_metas_), and their
+// device tables
+void GPUTreeLearner::ResetVoteXt() {
+  xt_glob_rand_.clear();
+  if (!voting_) return;
+  xt_glob_rand_.reserve(static_cast<size_t>(world_) * num_features_);
+  for (int r = 0; r < world_; ++r) {
+    for (int f = 0; f < num_features_; ++f) xt_glob_rand_.emplace_back(config_->extra_seed + f);
+  }
+}
+void GPUTreeLearner::AllocVoteXt(int n_leaves) {
+  if (!voting_) return;
+  const size_t wf = static_cast<size_t>(world_) * std::max(1, num_features_);
+  d_xt_base_glob_ = Alloc<uint32_t>(wf);
+  d_xt_cum_glob_ = Alloc<int32_t>(static_cast<size_t>(n_leaves) * wf);
+}
+// after a voting tree: every rank's global generators advance by the draws its global scans
+// made (the rows are running counts, steps not run are 0)
+void GPUTreeLearner::VoteXtAdvance() {
+  const size_t wf = static_cast<size_t>(world_) * num_features_;
+  const int rows = config_->num_leaves;
+  std::vector<int32_t> cum(static_cast<size_t>(rows) * wf);
+  HIPCHECK(hipMemcpy(cum.data(), d_xt_cum_glob_, sizeof(int32_t) * cum.size(), hipMemcpyDeviceToHost));
+  for (size_t e = 0; e < wf; ++e) {
+    int n = 0;
+    for (int r = 0; r < rows; ++r) n = std::max(n, cum[static_cast<size_t>(r) * wf + e]);
+    for (int k = 0; k < n; ++k) xt_glob_rand_[e].NextInt(0, 2);
+  }
 }
 
 void GPUTreeLearner::DropSpeculation() {

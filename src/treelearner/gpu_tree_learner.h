@@ -321,6 +321,15 @@ class GPUTreeLearner : public SerialTreeLearner, public DeviceTreeLearner {
   int32_t* d_xt_cum_ = nullptr;         // extra_trees: draws per feature after each step
   std::vector<uint32_t> h_xt_base_;
   std::vector<int32_t> h_xt_cum_;
+  // voting extra_trees: every rank's global-scan generator set (ResetVoteXt), its device states
+  // per tree and running draw counts (KArgs::xt_base_glob / xt_cum_glob)
+  std::vector<Random> xt_glob_rand_;
+  std::vector<uint32_t> h_xt_base_glob_;
+  uint32_t* d_xt_base_glob_ = nullptr;
+  int32_t* d_xt_cum_glob_ = nullptr;
+  void ResetVoteXt();
+  void AllocVoteXt(int n_leaves);
+  void VoteXtAdvance();
   dev::GH* d_gh_ = nullptr;
   int32_t* d_idx_ = nullptr;
   int32_t* d_tmp_ = nullptr;
