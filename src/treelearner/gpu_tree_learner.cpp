@@ -810,12 +810,11 @@ void GPUTreeLearner::DecideMode() {
   // categorical draws host-assisted
   if (config_->extra_trees && any_cat && distributed_) dm = false;
   // interaction constraints: on the device up to 256 constraints; with per-node sampling the
-  // children's masks are drawn on the device after each partition (k_bynode_step; one process)
+  // children's masks are drawn on the device after each partition (k_bynode_step) -- under the
+  // distributed learners too: every rank picks the same split, so every rank's generator draws
+  // the same masks
   const auto& ic = config_->interaction_constraints_vector;
-  if (!ic.empty() && (ic.size() > static_cast<size_t>(dev::kMaxIcConstraints) ||
-                      (config_->feature_fraction_bynode < 1.0 && distributed_))) {
-    dm = false;
-  }
+  if (!ic.empty() && ic.size() > static_cast<size_t>(dev::kMaxIcConstraints)) dm = false;
   // intermediate monotone constraints re-bound leaves all over the tree after a split: the pick
   // walks the tree and the next split scan re-scans the re-bounded leaves (one process, one
   // split per step; with extra_trees draws, forced splits or more than kMonoInterMaxLeaves

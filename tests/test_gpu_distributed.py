@@ -352,7 +352,8 @@ def test_multiprocess_peer_comm(learner, gpu_available, tmp_path):
 
 
 @pytest.mark.parametrize("learner,world,mode", [("data", 2, "bynode"), ("data", 3, "bynode"), ("data", 2, "cegb"),
-                                                ("feature", 2, "bynode"), ("feature", 3, "cegb")])
+                                                ("feature", 2, "bynode"), ("feature", 3, "cegb"),
+                                                ("data", 2, "bynode_ic"), ("feature", 3, "bynode_ic")])
 def test_distributed_modes_device_resident(learner, world, mode, gpu_available, capfd, tmp_path):
     """Per-node column sampling and CEGB split / coupled penalties under the distributed device
     learners grow device-resident (every rank draws the same node samples and holds the same CEGB
@@ -361,6 +362,8 @@ def test_distributed_modes_device_resident(learner, world, mode, gpu_available, 
     serial ones)."""
     if mode == "bynode":
         extra = {"feature_fraction_bynode": 0.6}
+    elif mode == "bynode_ic":  # (per-node masks drawn on the device from the branch-allowed pool)
+        extra = {"feature_fraction_bynode": 0.6, "interaction_constraints": [[0, 1, 2], [3, 4, 5, 6], [1, 7, 8, 9]]}
     else:
         extra = {"cegb_penalty_split": 0.5, "cegb_penalty_feature_coupled": [5, 1, 3, 0, 2, 1, 4, 0, 1, 2],
                  "cegb_tradeoff": 0.8}
