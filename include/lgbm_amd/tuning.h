@@ -16,6 +16,7 @@ namespace tuning {
 constexpr int kRoundWidth = 8;             // expansions per round (r04_round_width.md)
 constexpr int kRoundWidthNarrow = 6;       // ... for trees whose last tree's speculation was not accepted
 constexpr double kRoundAdaptRows = 4e6;    // rows per rank from which the width adapts per tree
+constexpr int kRoundLeavesPerWidth = 10;    // wide trees: the width is num_leaves / 10, 8 to 16 (r06_round_width_255.md)
 constexpr double kRoundAutoRows = 16e6;    // rows per rank from which round growth is timed against one split per step
 constexpr int kRoundHistory = 3;           // rounds enqueued per tree: the most of the last N trees
 constexpr int kRoundSegment = 4;           // rounds per segment graph
