@@ -2,7 +2,7 @@
 GPU, device communicator) at 255 leaves under the leaf-scaled round width (16) and width 8:
 the models must be equal.
 
-  python tools/diag_width_dist.py [rows_per_rank]
+  python tools/diag_width_dist.py [rows_per_rank] [num_leaves]
 """
 import os
 import sys
@@ -21,7 +21,7 @@ def main():
     rng = np.random.default_rng(5)
     X = rng.standard_normal((world * n, 28)).astype(np.float32)
     y = (X[:, :6].sum(axis=1) + 0.5 * rng.standard_normal(world * n) > 0).astype(np.float64)
-    base = {"objective": "binary", "num_leaves": 255, "learning_rate": 0.1, "min_data_in_leaf": 20, "verbose": -1,
+    base = {"objective": "binary", "num_leaves": int(sys.argv[2]) if len(sys.argv) > 2 else 255, "learning_rate": 0.1, "min_data_in_leaf": 20, "verbose": -1,
             "device_type": "gpu", "seed": 3, "max_bin": 255}
     full = lgb.Dataset(X, y, params=base, free_raw_data=False).construct()
     ok = True
